@@ -1,0 +1,144 @@
+/*
+ * rgpu.h — C ABI of librgpu.so, the MI355X-native windowed temporal-analysis library.
+ *
+ * This is the drop-in boundary that replaces the per-partition analysis hot path of
+ * Raphtory (Haaroon/raphtory @ v0).  Citations use
+ *   S/ = mainproject/cluster/src/main/scala/com/raphtory/
+ * A JNI shim binds these entry points from a GpuReaderWorker that
+ * takes the place of S/core/components/PartitionManager/Workers/ReaderWorker.scala.
+ *
+ * Conventions
+ *   - return 0 on success, a negative RGPU_E* code on failure; rgpu_last_error() says why.
+ *     Nothing throws or aborts across this boundary.
+ *   - caller-owned host arrays are copied during the call and never retained.
+ *   - device memory (and, later, communicators) are owned by the rgpu_ctx.
+ *   - result buffers are caller-allocated with (cap, *n); if *n > cap, call again.
+ *   - calls on one ctx are serialised by an internal mutex (10 ReaderWorker actors run
+ *     concurrently on reader-dispatcher, application.conf:246-264).
+ *   - times are int64 milliseconds >= 0; vertex ids are int64 in [0, 2^31)
+ *     (message targets are truncated with .toInt, VertexVisitor.scala:117-122).
+ */
+#ifndef RGPU_H
+#define RGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RGPU_ABI_VERSION 1
+
+/* error codes */
+#define RGPU_OK 0
+#define RGPU_EINVAL (-1)   /* bad argument (ids out of range, windows, hop index ...) */
+#define RGPU_ESTATE (-2)   /* call not valid in this state (e.g. run before seal) */
+#define RGPU_EHIP (-3)     /* HIP runtime failure */
+#define RGPU_ENOMEM (-4)   /* host or device allocation failed */
+#define RGPU_ENOTSUP (-5)  /* feature not available in this build */
+
+/* GraphUpdate kinds, S/core/model/communication/raphtoryMessages.scala:38-55 */
+#define RGPU_VADD 0        /* VertexAdd        -> EntityStorage.vertexAdd      :73-87  */
+#define RGPU_VDEL 1        /* VertexDelete     -> EntityStorage.vertexRemoval  :148-232 */
+#define RGPU_EADD 2        /* EdgeAdd          -> EntityStorage.edgeAdd        :237-290 */
+#define RGPU_EDEL 3        /* EdgeDelete       -> EntityStorage.edgeRemoval    :327-383 */
+
+/* analysers recognised on the GPU (AnalyserPresentCheck by class name, Reader.scala:68-85) */
+#define RGPU_ALGO_CC 0     /* S/core/analysis/Algorithms/ConnectedComponents.scala */
+#define RGPU_ALGO_DEGREE 1 /* S/core/analysis/Algorithms/DegreeBasic.scala (and DegreeRanking) */
+#define RGPU_ALGO_PR 2     /* PageRank per SURVEY.md App. A.5 (reference PageRank.scala is broken) */
+
+/* rgpu_run_view_batch flags */
+#define RGPU_RUN_RETAIN 1   /* keep per-vertex results of every view (for *_vertex_* queries) */
+#define RGPU_RUN_PROFILE 2  /* time every kernel launch with HIP events (rgpu_stats) */
+
+typedef struct rgpu_ctx rgpu_ctx;
+
+/* ConnectedComponents.processBatchWindowResults summary of one view,
+ * ConnectedComponents.scala:137-145 (computed over the label->count map). */
+typedef struct {
+  int64_t biggest;               /* max component size ("biggest")                 */
+  int64_t total;                 /* number of labels ("total")                     */
+  int64_t total_without_islands; /* labels with count > 1                          */
+  int64_t total_islands;         /* total - total_without_islands                  */
+  int64_t clusters_gt2;          /* labels with count > 2 ("clustersGT2")          */
+  int64_t sum_all;               /* sum of counts = |view vertices| (proportion)   */
+  int64_t sum_without_islands;   /* sum of counts > 1 (proportionWithoutIslands)   */
+  int64_t supersteps;            /* supersteps executed for the batch holding it   */
+} rgpu_cc_summary_t;
+
+typedef struct {
+  int64_t vertices, edges;       /* packed entity counts of this partition */
+  int64_t vertex_events, edge_events, deaths;
+  int64_t views, batches, supersteps, launches;
+  double ms_total;               /* wall ms inside the last rgpu_run_view_batch */
+  /* per-kernel event timing (RGPU_RUN_PROFILE): 0=window_mask 1=slots 2=cc_step 3=cc_hist
+   * 4=cc_summary 5=pr_step 6=degree */
+  int64_t kernel_launches[8];
+  double kernel_ms[8];
+  double kernel_bytes[8];        /* algorithmic bytes summed over launches */
+} rgpu_stats_t;
+
+int rgpu_abi_version(void);
+
+/* One context per Partition Manager / GPU (Reader.scala:42-53 spawns one reader per PM). */
+int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out);
+
+/* Append updates (any order).  Replaces the Router -> IngestionWorker -> EntityStorage
+ * path for the analysis hot path; the final histories follow EntityStorage.scala:73-453. */
+int rgpu_ingest(rgpu_ctx* ctx, const int64_t* t, const uint8_t* kind, const int64_t* src,
+                const int64_t* dst, size_t n);
+
+/* Sort + merge + pack the ingested stream into SoA histories and copy them to HBM. */
+int rgpu_seal(rgpu_ctx* ctx);
+
+/* Newest ingested time: the watermark ReaderWorker.processTimeCheckRequest compares
+ * against (ReaderWorker.scala:259-274). */
+int rgpu_newest_time(rgpu_ctx* ctx, int64_t* out);
+
+/* Multi-GPU vertex-partitioned exchange (RCCL).  Not in this build: RGPU_ENOTSUP. */
+int rgpu_exchange_init(rgpu_ctx* ctx, const void* rccl_unique_id);
+
+/* Run one analyser over every (hop, window) view: hops[n_hops] are the Range hop
+ * timestamps (RangeAnalysisTask.restart, RangeAnalysisTask.scala:18-35), windows[n_w]
+ * the user's batched window list in the user's order (n_w == 0 => ViewLens, no
+ * window).  Replaces the Setup / NextStep* / Finish rounds that AnalysisTask drives
+ * through ReaderWorker (AnalysisTask.scala:162-283, ReaderWorker.scala:159-257).
+ * max_steps: Analyser.defineMaxSteps (CC = 100).  pr_iters: PageRank iterations. */
+int rgpu_run_view_batch(rgpu_ctx* ctx, int algo, const int64_t* hops, size_t n_hops,
+                        const int64_t* windows, size_t n_w, int max_steps, int pr_iters,
+                        int flags);
+
+/* CC summary of view (hop, win) of the last run (ConnectedComponents.scala:137-145). */
+int rgpu_cc_summary(rgpu_ctx* ctx, size_t hop, size_t win, rgpu_cc_summary_t* out);
+
+/* CC label -> count map of view (hop, win): ConnectedComponents.returnResults
+ * (ConnectedComponents.scala:37-42) merged over the partition.  Needs RGPU_RUN_RETAIN. */
+int rgpu_cc_result(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* labels, int32_t* counts,
+                   size_t cap, size_t* n);
+
+/* Per-vertex CC labels of view (hop, win), ascending id.  Needs RGPU_RUN_RETAIN. */
+int rgpu_cc_vertex_labels(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, int64_t* labels,
+                          size_t cap, size_t* n);
+
+/* DegreeBasic.returnResults (DegreeBasic.scala:16-28): tot = {totalV, totalOut, totalIn};
+ * top-20 by in-degree (ties by ascending id) when RGPU_RUN_RETAIN was set, else zeros. */
+int rgpu_degree_result(rgpu_ctx* ctx, size_t hop, size_t win, int64_t tot[3], int64_t* top_id,
+                       int32_t* top_out, int32_t* top_in);
+
+/* Per-vertex degrees of view (hop, win), ascending id.  Needs RGPU_RUN_RETAIN. */
+int rgpu_degree_vertex(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, int32_t* outdeg,
+                       int32_t* indeg, size_t cap, size_t* n);
+
+/* PageRank of view (hop, win), ascending id.  Needs RGPU_RUN_RETAIN. */
+int rgpu_pr_result(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, double* pr, size_t cap,
+                   size_t* n);
+
+int rgpu_stats(rgpu_ctx* ctx, rgpu_stats_t* out);
+const char* rgpu_last_error(rgpu_ctx* ctx);
+void rgpu_close(rgpu_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,601 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY (see oracle.h for the rules and parity status).
+ *
+ * A plain-C restatement of the reference's hot path, organised like the Scala it
+ * follows so each step can be checked line by line:
+ *
+ *   S/ = /root/reference/mainproject/cluster/src/main/scala/com/raphtory/
+ *
+ *   history map ........ S/core/model/graphentities/Entity.scala:25-57 (TreeMap put-overwrite,
+ *                        revive/kill, checkOldestNewest), Edge.scala:36-44 (killList)
+ *   ingest ............. S/core/storage/EntityStorage.scala:73-97 (vertexAdd, placeholder),
+ *                        :148-232 (vertexRemoval), :237-290 (edgeAdd), :327-383 (edgeRemoval)
+ *   liveness ........... Entity.scala:173-201 (closestTime linear scan, aliveAt, aliveAtWithWindow)
+ *   view filter ........ GraphLenses/WindowLens.scala:23-68, ViewLens.scala:20-54,
+ *                        Vertex.scala:64-74 (viewAt / viewAtWithWindow)
+ *   BSP driver ......... PartitionManager/Workers/ReaderWorker.scala:159-257 (setup/nextStep/
+ *                        returnResults with shrinkWindow), Tasks/AnalysisTask.scala:162-283
+ *   messaging .......... entityVisitors/VertexVisitor.scala:81-120, VertexMutliQueue.scala:11-38
+ *   CC ................. Algorithms/ConnectedComponents.scala:10-42,160
+ *   degree ............. Algorithms/DegreeBasic.scala:16-28
+ *   PageRank ........... SURVEY.md App. A.5 (constants from examples/random/depricated/PageRank.scala:11-45)
+ *
+ * The whole stream is applied to ONE storage (a single Partition Manager whose 10
+ * workers share Edge objects through local actor messages), in stream order, with
+ * remote/other-worker messages delivered immediately (the quiescent state).
+ */
+#include "oracle.h"
+
+#include <limits.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ TreeMap */
+/* mutable.TreeMap[Long,Boolean] with put-overwrite (Entity.scala:25).  Kept
+ * ascending; HistoryOrdering's descending order never changes a lookup result. */
+typedef struct {
+  int64_t* k;
+  uint8_t* v;
+  int n, cap;
+} TMap;
+
+static int tm_put(TMap* m, int64_t k, uint8_t v) {
+  int lo = 0, hi = m->n;
+  if (m->n > 0 && m->k[m->n - 1] < k) {
+    lo = hi = m->n; /* append fast path: streams are mostly time ordered */
+  } else {
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      if (m->k[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    if (lo < m->n && m->k[lo] == k) { m->v[lo] = v; return 0; } /* last put wins */
+  }
+  if (m->n == m->cap) {
+    int nc = m->cap ? m->cap * 2 : 4;
+    int64_t* nk = (int64_t*)realloc(m->k, sizeof(int64_t) * nc);
+    uint8_t* nv = (uint8_t*)realloc(m->v, nc);
+    if (!nk || !nv) return -1;
+    m->k = nk; m->v = nv; m->cap = nc;
+  }
+  memmove(m->k + lo + 1, m->k + lo, sizeof(int64_t) * (m->n - lo));
+  memmove(m->v + lo + 1, m->v + lo, (size_t)(m->n - lo));
+  m->k[lo] = k; m->v[lo] = v; m->n++;
+  return 0;
+}
+static void tm_free(TMap* m) { free(m->k); free(m->v); m->k = NULL; m->v = NULL; m->n = m->cap = 0; }
+
+/* ----------------------------------------------------------------- entities */
+typedef struct {
+  TMap hist;   /* previousState */
+  TMap rem;    /* removeList */
+  int64_t oldest, newest;
+} Entity;
+
+typedef struct { int* a; int n, cap; } IVec;
+static int iv_push(IVec* v, int x) {
+  if (v->n == v->cap) {
+    int nc = v->cap ? v->cap * 2 : 4;
+    int* na = (int*)realloc(v->a, sizeof(int) * nc);
+    if (!na) return -1;
+    v->a = na; v->cap = nc;
+  }
+  v->a[v->n++] = x;
+  return 0;
+}
+
+typedef struct { Entity e; int64_t src, dst; } Edge;
+typedef struct { Entity e; int64_t id; IVec out, in; } Vertex;
+
+/* Entity constructor (Entity.scala:18-36): previousState = {creationTime -> isInitialValue},
+ * removeList = {creationTime -> false} iff !isInitialValue. */
+static void ent_init(Entity* e, int64_t t, int initial) {
+  memset(e, 0, sizeof(*e));
+  tm_put(&e->hist, t, (uint8_t)(initial ? 1 : 0));
+  if (!initial) tm_put(&e->rem, t, 0);
+  e->oldest = e->newest = t;
+}
+static void ent_check(Entity* e, int64_t t) { /* checkOldestNewest, Entity.scala:52-57 */
+  if (t > e->newest) e->newest = t;
+  if (e->oldest > t) e->oldest = t;
+}
+static void ent_revive(Entity* e, int64_t t) { ent_check(e, t); tm_put(&e->hist, t, 1); }       /* :41-44 */
+static void ent_kill(Entity* e, int64_t t) { ent_check(e, t); tm_put(&e->rem, t, 0); tm_put(&e->hist, t, 0); } /* :46-50 */
+static void edge_killlist(Entity* e, const TMap* vk) { /* Edge.killList, Edge.scala:36-44 (no checkOldestNewest) */
+  for (int i = 0; i < vk->n; i++) { tm_put(&e->rem, vk->k[i], 0); tm_put(&e->hist, vk->k[i], 0); }
+}
+
+/* closestTime, Entity.scala:173-183: full linear scan, closest starts at -1. */
+static void closest_time(const Entity* e, int64_t time, int64_t* ct, int* val) {
+  int64_t c = -1; int v = 0;
+  for (int i = 0; i < e->hist.n; i++) {
+    int64_t k = e->hist.k[i];
+    if (k <= time && (time - k) < (time - c)) { c = k; v = e->hist.v[i]; }
+  }
+  *ct = c; *val = v;
+}
+/* aliveAt (:185-191) for window < 0, aliveAtWithWindow (:193-201) otherwise. */
+static int ent_alive(const Entity* e, int64_t time, int64_t window) {
+  if (time < e->oldest) return 0;
+  int64_t c; int v;
+  closest_time(e, time, &c, &v);
+  if (window < 0) return v;
+  return (time - c <= window) ? v : 0;
+}
+
+/* ---------------------------------------------------------------- hash map */
+typedef struct { uint64_t* keys; int32_t* vals; size_t cap, n; } HMap;
+static uint64_t mix64(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+  return x;
+}
+static int hm_init(HMap* h, size_t cap) {
+  h->cap = 16; while (h->cap < cap * 2) h->cap <<= 1;
+  h->keys = (uint64_t*)malloc(sizeof(uint64_t) * h->cap);
+  h->vals = (int32_t*)malloc(sizeof(int32_t) * h->cap);
+  if (!h->keys || !h->vals) return -1;
+  for (size_t i = 0; i < h->cap; i++) h->vals[i] = -1;
+  h->n = 0;
+  return 0;
+}
+static int32_t hm_get(const HMap* h, uint64_t k) {
+  size_t i = mix64(k) & (h->cap - 1);
+  while (h->vals[i] >= 0) { if (h->keys[i] == k) return h->vals[i]; i = (i + 1) & (h->cap - 1); }
+  return -1;
+}
+static int hm_put(HMap* h, uint64_t k, int32_t v);
+static int hm_grow(HMap* h) {
+  HMap n2;
+  if (hm_init(&n2, h->cap) != 0) return -1; /* doubles */
+  for (size_t i = 0; i < h->cap; i++) if (h->vals[i] >= 0) hm_put(&n2, h->keys[i], h->vals[i]);
+  free(h->keys); free(h->vals); *h = n2;
+  return 0;
+}
+static int hm_put(HMap* h, uint64_t k, int32_t v) {
+  if ((h->n + 1) * 2 > h->cap && hm_grow(h) != 0) return -1;
+  size_t i = mix64(k) & (h->cap - 1);
+  while (h->vals[i] >= 0) { if (h->keys[i] == k) { h->vals[i] = v; return 0; } i = (i + 1) & (h->cap - 1); }
+  h->keys[i] = k; h->vals[i] = v; h->n++;
+  return 0;
+}
+
+/* ----------------------------------------------------------------- storage */
+struct orc_graph {
+  Vertex* vs; size_t nv, capv;
+  Edge* es; size_t ne, cape;
+  HMap vmap, emap;
+  int32_t* order; /* vertex indices sorted by id (ParTrieMap iteration order is irrelevant) */
+};
+
+static uint64_t ekey(int64_t s, int64_t d) { return ((uint64_t)s << 32) | (uint64_t)d; }
+
+static int new_vertex(orc_graph* g, int64_t t, int64_t id, int initial) {
+  if (g->nv == g->capv) {
+    size_t nc = g->capv ? g->capv * 2 : 1024;
+    Vertex* nvs = (Vertex*)realloc(g->vs, sizeof(Vertex) * nc);
+    if (!nvs) return -1;
+    g->vs = nvs; g->capv = nc;
+  }
+  Vertex* v = &g->vs[g->nv];
+  memset(v, 0, sizeof(*v));
+  ent_init(&v->e, t, initial);
+  v->id = id;
+  if (hm_put(&g->vmap, (uint64_t)id, (int32_t)g->nv) != 0) return -1;
+  return (int)g->nv++;
+}
+static int new_edge(orc_graph* g, int64_t t, int64_t s, int64_t d, int initial) {
+  if (g->ne == g->cape) {
+    size_t nc = g->cape ? g->cape * 2 : 1024;
+    Edge* nes = (Edge*)realloc(g->es, sizeof(Edge) * nc);
+    if (!nes) return -1;
+    g->es = nes; g->cape = nc;
+  }
+  Edge* e = &g->es[g->ne];
+  memset(e, 0, sizeof(*e));
+  ent_init(&e->e, t, initial);
+  e->src = s; e->dst = d;
+  if (hm_put(&g->emap, ekey(s, d), (int32_t)g->ne) != 0) return -1;
+  return (int)g->ne++;
+}
+
+/* EntityStorage.vertexAdd, :73-87 */
+static int vertex_add(orc_graph* g, int64_t t, int64_t id) {
+  int32_t vi = hm_get(&g->vmap, (uint64_t)id);
+  if (vi >= 0) { ent_revive(&g->vs[vi].e, t); return vi; }
+  return new_vertex(g, t, id, 1);
+}
+/* EntityStorage.getVertexOrPlaceholder, :89-97 (new vertex, then wipe()) */
+static int vertex_or_placeholder(orc_graph* g, int64_t t, int64_t id) {
+  int32_t vi = hm_get(&g->vmap, (uint64_t)id);
+  if (vi >= 0) return vi;
+  vi = new_vertex(g, t, id, 1);
+  if (vi >= 0) g->vs[vi].e.hist.n = 0; /* Entity.wipe, Entity.scala:158 (oldestPoint untouched) */
+  return vi;
+}
+/* EntityStorage.vertexRemoval, :148-232 */
+static int vertex_removal(orc_graph* g, int64_t t, int64_t id) {
+  int32_t vi = hm_get(&g->vmap, (uint64_t)id);
+  if (vi >= 0) ent_kill(&g->vs[vi].e, t);
+  else if ((vi = new_vertex(g, t, id, 0)) < 0) return -1; /* placeholder created dead, :153-156 */
+  Vertex* v = &g->vs[vi];
+  for (int i = 0; i < v->in.n; i++) ent_kill(&g->es[v->in.a[i]].e, t);   /* :189-213 */
+  for (int i = 0; i < v->out.n; i++) ent_kill(&g->es[v->out.a[i]].e, t); /* :214-228 */
+  return 0;
+}
+/* EntityStorage.edgeAdd, :237-290 (local && sameWorker order; other-worker and remote
+ * paths deliver the same puts, :99-116, :292-314, :447-453). */
+static int edge_add(orc_graph* g, int64_t t, int64_t s, int64_t d) {
+  int si = vertex_add(g, t, s);
+  if (si < 0) return -1;
+  int32_t ei = hm_get(&g->emap, ekey(s, d));
+  int present = ei >= 0;
+  if (!present) {
+    if ((ei = new_edge(g, t, s, d, 1)) < 0) return -1;
+    if (iv_push(&g->vs[si].out, ei) != 0) return -1; /* srcVertex.addOutgoingEdge, :255 */
+  }
+  if (s != d) { /* :257-263 */
+    int di = vertex_add(g, t, d);
+    if (di < 0) return -1;
+    if (!present) {
+      if (iv_push(&g->vs[di].in, ei) != 0) return -1;
+      edge_killlist(&g->es[ei].e, &g->vs[di].e.rem);
+    }
+  }
+  if (present) ent_revive(&g->es[ei].e, t);                 /* :268-269 */
+  else edge_killlist(&g->es[ei].e, &g->vs[si].e.rem);       /* :276-278 */
+  return 0;
+}
+/* EntityStorage.edgeRemoval, :327-383 */
+static int edge_removal(orc_graph* g, int64_t t, int64_t s, int64_t d) {
+  int si = vertex_or_placeholder(g, t, s);
+  if (si < 0) return -1;
+  int32_t ei = hm_get(&g->emap, ekey(s, d));
+  int present = ei >= 0;
+  if (!present) {
+    if ((ei = new_edge(g, t, s, d, 0)) < 0) return -1;      /* initialValue = false, :341 */
+    if (iv_push(&g->vs[si].out, ei) != 0) return -1;
+  }
+  if (s != d) {
+    int di = vertex_or_placeholder(g, t, d);
+    if (di < 0) return -1;
+    if (!present) {
+      if (iv_push(&g->vs[di].in, ei) != 0) return -1;
+      edge_killlist(&g->es[ei].e, &g->vs[di].e.rem);
+    }
+  }
+  if (present) ent_kill(&g->es[ei].e, t);                   /* :365-366 */
+  else edge_killlist(&g->es[ei].e, &g->vs[si].e.rem);       /* :373-375 */
+  return 0;
+}
+
+static const orc_graph* g_sort_ctx;
+static int cmp_vid(const void* a, const void* b) {
+  int64_t x = g_sort_ctx->vs[*(const int32_t*)a].id, y = g_sort_ctx->vs[*(const int32_t*)b].id;
+  return (x > y) - (x < y);
+}
+
+orc_graph* orc_build(const int64_t* t, const uint8_t* kind, const int64_t* src,
+                     const int64_t* dst, size_t n) {
+  orc_graph* g = (orc_graph*)calloc(1, sizeof(orc_graph));
+  if (!g) return NULL;
+  if (hm_init(&g->vmap, 1024) || hm_init(&g->emap, 1024)) { orc_free(g); return NULL; }
+  for (size_t i = 0; i < n; i++) {
+    /* keys >= 0, ids in [0, 2^31) (message targets are .toInt, VertexVisitor.scala:117) */
+    if (t[i] < 0 || src[i] < 0 || src[i] > INT32_MAX) { orc_free(g); return NULL; }
+    if ((kind[i] == ORC_EADD || kind[i] == ORC_EDEL) && (dst[i] < 0 || dst[i] > INT32_MAX)) { orc_free(g); return NULL; }
+    int rc;
+    switch (kind[i]) {
+      case ORC_VADD: rc = vertex_add(g, t[i], src[i]) < 0 ? -1 : 0; break;
+      case ORC_VDEL: rc = vertex_removal(g, t[i], src[i]); break;
+      case ORC_EADD: rc = edge_add(g, t[i], src[i], dst[i]); break;
+      case ORC_EDEL: rc = edge_removal(g, t[i], src[i], dst[i]); break;
+      default: rc = -1;
+    }
+    if (rc != 0) { orc_free(g); return NULL; }
+  }
+  g->order = (int32_t*)malloc(sizeof(int32_t) * (g->nv ? g->nv : 1));
+  if (!g->order) { orc_free(g); return NULL; }
+  for (size_t i = 0; i < g->nv; i++) g->order[i] = (int32_t)i;
+  g_sort_ctx = g;
+  qsort(g->order, g->nv, sizeof(int32_t), cmp_vid);
+  return g;
+}
+
+void orc_free(orc_graph* g) {
+  if (!g) return;
+  for (size_t i = 0; i < g->nv; i++) {
+    tm_free(&g->vs[i].e.hist); tm_free(&g->vs[i].e.rem);
+    free(g->vs[i].out.a); free(g->vs[i].in.a);
+  }
+  for (size_t i = 0; i < g->ne; i++) { tm_free(&g->es[i].e.hist); tm_free(&g->es[i].e.rem); }
+  free(g->vs); free(g->es); free(g->order);
+  free(g->vmap.keys); free(g->vmap.vals); free(g->emap.keys); free(g->emap.vals);
+  free(g);
+}
+
+size_t orc_num_vertices(const orc_graph* g) { return g->nv; }
+size_t orc_num_edges(const orc_graph* g) { return g->ne; }
+
+static const Entity* find_entity(const orc_graph* g, int is_edge, int64_t s, int64_t d) {
+  if (s < 0 || s > INT32_MAX) return NULL;
+  if (is_edge) {
+    if (d < 0 || d > INT32_MAX) return NULL;
+    int32_t ei = hm_get(&g->emap, ekey(s, d));
+    return ei >= 0 ? &g->es[ei].e : NULL;
+  }
+  int32_t vi = hm_get(&g->vmap, (uint64_t)s);
+  return vi >= 0 ? &g->vs[vi].e : NULL;
+}
+
+long orc_history(const orc_graph* g, int is_edge, int64_t src, int64_t dst,
+                 int64_t* times, uint8_t* flags, size_t cap) {
+  const Entity* e = find_entity(g, is_edge, src, dst);
+  if (!e) return -1;
+  for (int i = 0; i < e->hist.n && (size_t)i < cap; i++) { times[i] = e->hist.k[i]; flags[i] = e->hist.v[i]; }
+  return e->hist.n;
+}
+
+int orc_alive(const orc_graph* g, int is_edge, int64_t src, int64_t dst, int64_t t, int64_t window) {
+  const Entity* e = find_entity(g, is_edge, src, dst);
+  return e ? ent_alive(e, t, window) : 0;
+}
+
+/* ------------------------------------------------------------ lens helpers */
+/* Window list of the job: nw == 0 => ViewLens (aliveAt, window -1), ReaderWorker.scala:324-352. */
+typedef struct {
+  int nwin;
+  int64_t w[64];
+  int canon[64]; /* comp keys / job ids are name+t+w (VertexVisitor.scala:81-96, WindowLens.scala:160):
+                    equal window values share state */
+} WinSet;
+
+static int winset_init(WinSet* ws, const int64_t* windows, int nw) {
+  if (nw < 0 || nw > 64) return -1;
+  ws->nwin = nw ? nw : 1;
+  for (int i = 0; i < ws->nwin; i++) {
+    ws->w[i] = nw ? windows[i] : -1;
+    if (nw && windows[i] < 0) return -1;
+    ws->canon[i] = i;
+    for (int j = 0; j < i; j++) if (ws->w[j] == ws->w[i]) { ws->canon[i] = ws->canon[j]; break; }
+  }
+  return 0;
+}
+
+/* Lens key sets: new WindowLens(t, w0) filters every vertex (WindowLens.scala:131-132), then
+ * shrinkWindow(w_i) filters the running key set (:167-173).  mem[i*nv + v]. */
+static void build_keysets(const orc_graph* g, int64_t t, const WinSet* ws, uint8_t* mem) {
+  size_t nv = g->nv;
+  for (size_t v = 0; v < nv; v++) mem[v] = (uint8_t)ent_alive(&g->vs[v].e, t, ws->w[0]);
+  for (int i = 1; i < ws->nwin; i++)
+    for (size_t v = 0; v < nv; v++)
+      mem[(size_t)i * nv + v] = mem[(size_t)(i - 1) * nv + v] && ent_alive(&g->vs[v].e, t, ws->w[i]);
+}
+
+/* messageAllNeighbours: keys(outgoingProcessing) ∪ keys(incomingProcessing) after
+ * viewAtWithWindow(t, setWindow) (VertexVisitor.scala:119-120, Vertex.scala:70-74).
+ * Writes distinct neighbour vertex indices into nb; uses mark[] (all zero on entry/exit). */
+static int neighbours(const orc_graph* g, int vi, int64_t t, int64_t w, int* nb, uint8_t* mark) {
+  const Vertex* v = &g->vs[vi];
+  int n = 0;
+  for (int i = 0; i < v->out.n; i++) {
+    const Edge* e = &g->es[v->out.a[i]];
+    if (!ent_alive(&e->e, t, w)) continue;
+    int x = hm_get(&g->vmap, (uint64_t)e->dst);
+    if (!mark[x]) { mark[x] = 1; nb[n++] = x; }
+  }
+  for (int i = 0; i < v->in.n; i++) {
+    const Edge* e = &g->es[v->in.a[i]];
+    if (!ent_alive(&e->e, t, w)) continue;
+    int x = hm_get(&g->vmap, (uint64_t)e->src);
+    if (!mark[x]) { mark[x] = 1; nb[n++] = x; }
+  }
+  for (int i = 0; i < n; i++) mark[nb[i]] = 0;
+  return n;
+}
+
+/* ------------------------------------------------------------------- CC */
+int orc_cc(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int max_steps,
+           int mode, int64_t* ids, int64_t* labels, size_t cap, size_t* n_out, int* steps) {
+  WinSet ws;
+  if (winset_init(&ws, windows, nw) != 0) return -1;
+  size_t nv = g->nv;
+  int nwin = ws.nwin;
+  size_t nvs = nv ? nv : 1;
+  uint8_t* mem = (uint8_t*)calloc((size_t)nwin * nvs, 1);
+  uint8_t* lset = (uint8_t*)calloc((size_t)nwin * nvs, 1);      /* computationValues contains */
+  int64_t* lbl = (int64_t*)malloc(sizeof(int64_t) * nwin * nvs);
+  int64_t* qmin = (int64_t*)malloc(sizeof(int64_t) * 2 * nwin * nvs); /* VertexMutliQueue even/odd */
+  uint32_t* qcnt = (uint32_t*)calloc((size_t)2 * nwin * nvs, sizeof(uint32_t));
+  int* nb = (int*)malloc(sizeof(int) * nvs);
+  int* list = (int*)malloc(sizeof(int) * nvs);
+  uint8_t* mark = (uint8_t*)calloc(nvs, 1);
+  /* mode 1 cache: filtered neighbour lists per (window, vertex) */
+  int** nbc = NULL; int* nbn = NULL;
+  int rc = -1;
+  if (!mem || !lset || !lbl || !qmin || !qcnt || !nb || !list || !mark) goto done;
+  *steps = 0;
+
+  build_keysets(g, t, &ws, mem);
+  if (mode == 1) {
+    nbc = (int**)calloc((size_t)nwin * nvs, sizeof(int*));
+    nbn = (int*)calloc((size_t)nwin * nvs, sizeof(int));
+    if (!nbc || !nbn) goto done;
+    for (int i = 0; i < nwin; i++)
+      for (size_t v = 0; v < nv; v++) {
+        if (!mem[(size_t)i * nv + v]) continue;
+        int k = neighbours(g, (int)v, t, ws.w[i], nb, mark);
+        nbn[(size_t)i * nv + v] = k;
+        nbc[(size_t)i * nv + v] = (int*)malloc(sizeof(int) * (k ? k : 1));
+        if (!nbc[(size_t)i * nv + v]) goto done;
+        memcpy(nbc[(size_t)i * nv + v], nb, sizeof(int) * k);
+      }
+  }
+
+#define NEIGH(i, v, outp, outn)                                                  \
+  do {                                                                           \
+    if (mode == 1) { outp = nbc[(size_t)(i) * nv + (v)]; outn = nbn[(size_t)(i) * nv + (v)]; } \
+    else { outn = neighbours(g, (v), t, ws.w[i], nb, mark); outp = nb; }         \
+  } while (0)
+#define SEND(i, step, lab, v)                                                   \
+  do {                                                                           \
+    const int* np_; int nn_;                                                     \
+    NEIGH(i, v, np_, nn_);                                                       \
+    size_t qb_ = ((size_t)((step) + 1) % 2 * nwin + ws.canon[i]) * nv;           \
+    for (int q_ = 0; q_ < nn_; q_++) {                                           \
+      size_t x_ = qb_ + np_[q_];                                                 \
+      if (qcnt[x_] == 0 || (lab) < qmin[x_]) qmin[x_] = (lab);                   \
+      qcnt[x_]++;                                                                \
+    }                                                                            \
+  } while (0)
+
+  if (max_steps > 1) { /* AnalysisTask.timeResponse :169 — Setup only when maxSteps > 1 */
+    /* ReaderWorker.setup :173-186 — ConnectedComponents.setup :10-17 per window */
+    for (int i = 0; i < nwin; i++) {
+      int c = ws.canon[i];
+      for (size_t v = 0; v < nv; v++) {
+        if (!mem[(size_t)i * nv + v]) continue;
+        size_t li = (size_t)c * nv + v;
+        if (!lset[li]) { lset[li] = 1; lbl[li] = g->vs[v].id; } /* getOrSetCompValue("cclabel", id) */
+        int64_t toSend = lbl[li];
+        SEND(i, 0, toSend, (int)v);
+      }
+    }
+    for (int s = 1;; s++) {
+      /* ReaderWorker.nextStep :190-219 — a NEW WindowLens per superstep */
+      if (mode == 0) build_keysets(g, t, &ws, mem);
+      long totalKeys = 0, votes = 0;
+      for (int i = 0; i < nwin; i++) {
+        int c = ws.canon[i];
+        size_t qb = ((size_t)(s % 2) * nwin + c) * nv;
+        /* getVerticesWithMessages, WindowLens.scala:149-158 */
+        int nl = 0;
+        for (size_t v = 0; v < nv; v++)
+          if (mem[(size_t)i * nv + v] && qcnt[qb + v] > 0) list[nl++] = (int)v;
+        totalKeys += nl;
+        /* ConnectedComponents.analyse :19-35 */
+        for (int a = 0; a < nl; a++) {
+          int v = list[a];
+          int64_t label = qmin[qb + v];
+          qcnt[qb + v] = 0; /* clearQueue */
+          size_t li = (size_t)c * nv + v;
+          if (!lset[li]) { lset[li] = 1; lbl[li] = label; }
+          int64_t cur = lbl[li];
+          if (label < cur) { lbl[li] = label; SEND(i, s, label, v); }
+          else votes++;
+        }
+      }
+      *steps = s;
+      /* AnalysisTask.endStep :208-225, WindowLens.checkVotes :175-176 */
+      if (s == max_steps || totalKeys == votes) break;
+    }
+  }
+  /* ReaderWorker.returnResults :232-257 — ConnectedComponents.returnResults :37-42 */
+  if (mode == 0) build_keysets(g, t, &ws, mem);
+  for (int i = 0; i < nwin; i++) {
+    int c = ws.canon[i];
+    size_t k = 0;
+    for (size_t r = 0; r < nv; r++) {
+      int v = g->order[r];
+      if (!mem[(size_t)i * nv + v]) continue;
+      if (k >= cap) goto done;
+      size_t li = (size_t)c * nv + v;
+      ids[(size_t)i * cap + k] = g->vs[v].id;
+      labels[(size_t)i * cap + k] = lset[li] ? lbl[li] : g->vs[v].id;
+      k++;
+    }
+    n_out[i] = k;
+  }
+  rc = 0;
+#undef SEND
+#undef NEIGH
+done:
+  if (nbc) { for (size_t i = 0; i < (size_t)nwin * nvs; i++) free(nbc[i]); free(nbc); }
+  free(nbn);
+  free(mem); free(lset); free(lbl); free(qmin); free(qcnt); free(nb); free(list); free(mark);
+  return rc;
+}
+
+/* ---------------------------------------------------------------- degree */
+static void vertex_degree(const orc_graph* g, int v, int64_t t, int64_t w, int32_t* od, int32_t* id) {
+  const Vertex* x = &g->vs[v];
+  int32_t o = 0, in = 0;
+  for (int i = 0; i < x->out.n; i++) o += ent_alive(&g->es[x->out.a[i]].e, t, w);
+  for (int i = 0; i < x->in.n; i++) in += ent_alive(&g->es[x->in.a[i]].e, t, w);
+  *od = o; *id = in;
+}
+
+int orc_degree(const orc_graph* g, int64_t t, const int64_t* windows, int nw,
+               int64_t* ids, int32_t* outdeg, int32_t* indeg, size_t cap, size_t* n_out) {
+  WinSet ws;
+  if (winset_init(&ws, windows, nw) != 0) return -1;
+  size_t nv = g->nv;
+  uint8_t* mem = (uint8_t*)calloc((size_t)ws.nwin * (nv ? nv : 1), 1);
+  if (!mem) return -1;
+  build_keysets(g, t, &ws, mem);
+  for (int i = 0; i < ws.nwin; i++) {
+    size_t k = 0;
+    for (size_t r = 0; r < nv; r++) {
+      int v = g->order[r];
+      if (!mem[(size_t)i * nv + v]) continue;
+      if (k >= cap) { free(mem); return -1; }
+      size_t o = (size_t)i * cap + k;
+      ids[o] = g->vs[v].id;
+      vertex_degree(g, v, t, ws.w[i], &outdeg[o], &indeg[o]);
+      k++;
+    }
+    n_out[i] = k;
+  }
+  free(mem);
+  return 0;
+}
+
+/* -------------------------------------------------------------- pagerank */
+int orc_pagerank(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int iters,
+                 int64_t* ids, double* pr, size_t cap, size_t* n_out) {
+  WinSet ws;
+  if (winset_init(&ws, windows, nw) != 0) return -1;
+  size_t nv = g->nv, nvs = nv ? nv : 1;
+  uint8_t* mem = (uint8_t*)calloc((size_t)ws.nwin * nvs, 1);
+  double* cur = (double*)malloc(sizeof(double) * nvs);
+  double* nxt = (double*)malloc(sizeof(double) * nvs);
+  int32_t* od = (int32_t*)malloc(sizeof(int32_t) * nvs);
+  int rc = -1;
+  if (!mem || !cur || !nxt || !od) goto done;
+  build_keysets(g, t, &ws, mem);
+  for (int i = 0; i < ws.nwin; i++) {
+    const uint8_t* m = mem + (size_t)i * nv;
+    for (size_t v = 0; v < nv; v++) {
+      cur[v] = 1.0; /* defaultPR, PageRank.scala:14 */
+      int32_t dummy;
+      vertex_degree(g, (int)v, t, ws.w[i], &od[v], &dummy);
+    }
+    for (int it = 0; it < iters; it++) {
+      for (size_t v = 0; v < nv; v++) nxt[v] = 0.0;
+      for (size_t u = 0; u < nv; u++) {
+        if (!m[u]) continue;
+        double c = cur[u] / (double)(od[u] > 1 ? od[u] : 1); /* max(outdeg,1), PageRank.scala:35 */
+        const Vertex* x = &g->vs[u];
+        for (int k = 0; k < x->out.n; k++) {
+          const Edge* e = &g->es[x->out.a[k]];
+          if (!ent_alive(&e->e, t, ws.w[i])) continue;
+          int d = hm_get(&g->vmap, (uint64_t)e->dst);
+          if (m[d]) nxt[d] += c;
+        }
+      }
+      for (size_t v = 0; v < nv; v++) cur[v] = m[v] ? 0.15 + 0.85 * nxt[v] : 1.0; /* d = 0.85, :11 */
+    }
+    size_t k = 0;
+    for (size_t r = 0; r < nv; r++) {
+      int v = g->order[r];
+      if (!m[v]) continue;
+      if (k >= cap) goto done;
+      ids[(size_t)i * cap + k] = g->vs[v].id;
+      pr[(size_t)i * cap + k] = cur[v];
+      k++;
+    }
+    n_out[i] = k;
+  }
+  rc = 0;
+done:
+  free(mem); free(cur); free(nxt); free(od);
+  return rc;
+}

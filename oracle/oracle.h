@@ -1,0 +1,71 @@
+/*
+ * oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of Raphtory's windowed temporal-analysis path, written from the
+ * reference Scala source (Haaroon/raphtory @ v0).  It is the *checker* for the HIP
+ * path: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load it.  The product library (raphtory_amd/) never links or calls it.
+ *
+ * Parity status: the reference is Scala/Akka and cannot be built or run in this
+ * image (no JDK / scalac / sbt, no dependency cache) and it ships no tests, golden
+ * vectors or reproducible sample outputs.  This oracle is therefore pinned only by
+ * hand-derived known-answer tests that cite the Scala lines they follow
+ * (tests/test_oracle_kat.py, tests/golden/kat_*.json) — "parity unpinned" against
+ * reference-run outputs.
+ *
+ * Event kinds follow GraphUpdate (raphtoryMessages.scala:38-55).
+ */
+#ifndef RAPHTORY_ORACLE_H
+#define RAPHTORY_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_VADD = 0, ORC_VDEL = 1, ORC_EADD = 2, ORC_EDEL = 3 };
+
+typedef struct orc_graph orc_graph;
+
+/* Replays the stream, in order, through a restatement of EntityStorage
+ * (EntityStorage.scala:73-453) for one Partition Manager.  Returns NULL on bad input. */
+orc_graph* orc_build(const int64_t* t, const uint8_t* kind, const int64_t* src,
+                     const int64_t* dst, size_t n);
+void orc_free(orc_graph* g);
+
+size_t orc_num_vertices(const orc_graph* g);
+size_t orc_num_edges(const orc_graph* g);
+
+/* History of one entity as the reference leaves it (Entity.previousState,
+ * Entity.scala:25), ascending by time.  Returns number of points (may exceed cap),
+ * or -1 if the entity does not exist.  Edge = (src,dst); vertex: dst ignored. */
+long orc_history(const orc_graph* g, int is_edge, int64_t src, int64_t dst,
+                 int64_t* times, uint8_t* flags, size_t cap);
+
+/* Entity.aliveAtWithWindow (Entity.scala:193-201); window < 0 => Entity.aliveAt (:185-191). */
+int orc_alive(const orc_graph* g, int is_edge, int64_t src, int64_t dst, int64_t t, int64_t window);
+
+/* ConnectedComponents over one view at time t with the batched window list
+ * `windows[nw]` (nw == 0 => ViewLens).  mode 0 = reference structure (lens rebuilt
+ * every superstep by linear closestTime scans, adjacency re-filtered on every
+ * getVertex); mode 1 = same semantics with per-view caching.
+ * Outputs, per window i: n_out[i] vertices written to ids/labels at offset
+ * i*cap (ascending id).  *steps = supersteps executed (AnalysisTask.endStep).
+ * Returns 0 or -1 (cap too small / bad args). */
+int orc_cc(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int max_steps,
+           int mode, int64_t* ids, int64_t* labels, size_t cap, size_t* n_out, int* steps);
+
+/* DegreeBasic.returnResults (DegreeBasic.scala:16-28) per window, per vertex. */
+int orc_degree(const orc_graph* g, int64_t t, const int64_t* windows, int nw,
+               int64_t* ids, int32_t* outdeg, int32_t* indeg, size_t cap, size_t* n_out);
+
+/* PageRank, SURVEY.md App. A.5 spec (the reference PageRank.scala is broken):
+ * PR0 = 1, PR' = 0.15 + 0.85 * sum_{u->v} PR(u)/max(outdeg(u),1), fp64, iters rounds. */
+int orc_pagerank(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int iters,
+                 int64_t* ids, double* pr, size_t cap, size_t* n_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,133 @@
+"""ctypes bindings of the in-tree native libraries.
+
+``librgpu.so`` is the product: HIP kernels + host packer behind the C ABI declared in
+``include/rgpu.h``.  There is no CPU fallback: if the library is missing or does not load,
+every call raises :class:`NativeUnavailable`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD_DIR = os.path.join(_HERE, "_build")
+
+# error codes / constants mirrored from include/rgpu.h
+RGPU_OK = 0
+RGPU_EINVAL, RGPU_ESTATE, RGPU_EHIP, RGPU_ENOMEM, RGPU_ENOTSUP = -1, -2, -3, -4, -5
+RGPU_VADD, RGPU_VDEL, RGPU_EADD, RGPU_EDEL = 0, 1, 2, 3
+RGPU_ALGO_CC, RGPU_ALGO_DEGREE, RGPU_ALGO_PR = 0, 1, 2
+RGPU_RUN_RETAIN, RGPU_RUN_PROFILE = 1, 2
+ERROR_NAMES = {
+    RGPU_EINVAL: "RGPU_EINVAL",
+    RGPU_ESTATE: "RGPU_ESTATE",
+    RGPU_EHIP: "RGPU_EHIP",
+    RGPU_ENOMEM: "RGPU_ENOMEM",
+    RGPU_ENOTSUP: "RGPU_ENOTSUP",
+}
+KERNEL_NAMES = ["window_mask", "cc_slots", "cc_step", "cc_hist", "cc_summary", "pr_step", "degree", "-"]
+
+# exported symbols of librgpu.so, exactly the declarations of include/rgpu.h
+EXPORTS = [
+    "rgpu_abi_version", "rgpu_open", "rgpu_ingest", "rgpu_seal", "rgpu_newest_time",
+    "rgpu_exchange_init", "rgpu_run_view_batch", "rgpu_cc_summary", "rgpu_cc_result",
+    "rgpu_cc_vertex_labels", "rgpu_degree_result", "rgpu_degree_vertex", "rgpu_pr_result",
+    "rgpu_stats", "rgpu_last_error", "rgpu_close",
+]
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class CCSummary(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in (
+        "biggest", "total", "total_without_islands", "total_islands", "clusters_gt2",
+        "sum_all", "sum_without_islands", "supersteps")]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("vertices", C.c_int64), ("edges", C.c_int64),
+        ("vertex_events", C.c_int64), ("edge_events", C.c_int64), ("deaths", C.c_int64),
+        ("views", C.c_int64), ("batches", C.c_int64), ("supersteps", C.c_int64), ("launches", C.c_int64),
+        ("ms_total", C.c_double),
+        ("kernel_launches", C.c_int64 * 8), ("kernel_ms", C.c_double * 8), ("kernel_bytes", C.c_double * 8),
+    ]
+
+
+_P64 = C.POINTER(C.c_int64)
+_P32 = C.POINTER(C.c_int32)
+_PU8 = C.POINTER(C.c_uint8)
+_PD = C.POINTER(C.c_double)
+_SZ = C.c_size_t
+_CTX = C.c_void_p
+
+_SIGS = {
+    "rgpu_abi_version": (C.c_int, []),
+    "rgpu_open": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(_CTX)]),
+    "rgpu_ingest": (C.c_int, [_CTX, _P64, _PU8, _P64, _P64, _SZ]),
+    "rgpu_seal": (C.c_int, [_CTX]),
+    "rgpu_newest_time": (C.c_int, [_CTX, _P64]),
+    "rgpu_exchange_init": (C.c_int, [_CTX, C.c_void_p]),
+    "rgpu_run_view_batch": (C.c_int, [_CTX, C.c_int, _P64, _SZ, _P64, _SZ, C.c_int, C.c_int, C.c_int]),
+    "rgpu_cc_summary": (C.c_int, [_CTX, _SZ, _SZ, C.POINTER(CCSummary)]),
+    "rgpu_cc_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P32, _SZ, C.POINTER(_SZ)]),
+    "rgpu_cc_vertex_labels": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P64, _SZ, C.POINTER(_SZ)]),
+    "rgpu_degree_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P64, _P32, _P32]),
+    "rgpu_degree_vertex": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P32, _P32, _SZ, C.POINTER(_SZ)]),
+    "rgpu_pr_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _PD, _SZ, C.POINTER(_SZ)]),
+    "rgpu_stats": (C.c_int, [_CTX, C.POINTER(Stats)]),
+    "rgpu_last_error": (C.c_char_p, [_CTX]),
+    "rgpu_close": (None, [_CTX]),
+}
+
+_lib = None
+_synth = None
+
+
+def lib_path(name: str = "librgpu.so") -> str:
+    return os.path.join(BUILD_DIR, name)
+
+
+def rgpu() -> C.CDLL:
+    """The loaded librgpu.so (raises NativeUnavailable — never falls back)."""
+    global _lib
+    if _lib is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise NativeUnavailable(
+                f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        try:
+            lib = C.CDLL(path)
+        except OSError as e:  # pragma: no cover - depends on the box
+            raise NativeUnavailable(f"cannot load {path}: {e}") from e
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def synth() -> C.CDLL:
+    global _synth
+    if _synth is None:
+        path = lib_path("libsynth.so")
+        if not os.path.exists(path):
+            raise NativeUnavailable(f"{path} is missing")
+        s = C.CDLL(path)
+        s.rg_gen_uniform.restype = _SZ
+        s.rg_gen_uniform.argtypes = [C.c_uint64, C.c_int64, _SZ, C.c_int64, C.c_int64,
+                                     C.c_double, C.c_double, C.c_double, _P64, _PU8, _P64, _P64]
+        s.rg_gen_powerlaw.restype = _SZ
+        s.rg_gen_powerlaw.argtypes = [C.c_uint64, C.c_int64, _SZ, C.c_double, C.c_int64, C.c_int64,
+                                      _P64, _PU8, _P64, _P64]
+        s.rg_gen_gab.restype = _SZ
+        s.rg_gen_gab.argtypes = [C.c_uint64, C.c_int64, _SZ, C.c_int64, C.c_int64, _P64, _PU8, _P64, _P64]
+        _synth = s
+    return _synth
+
+
+def ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))

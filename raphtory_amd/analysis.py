@@ -1,0 +1,334 @@
+"""Host-side mirror of Raphtory's analysis plugin surface for the GPU path.
+
+S/ = mainproject/cluster/src/main/scala/com/raphtory/ in the reference.
+
+* ``Analyser`` subclasses keep the reference names and result shapes:
+  ``ConnectedComponents`` (S/core/analysis/Algorithms/ConnectedComponents.scala),
+  ``DegreeBasic`` (Algorithms/DegreeBasic.scala), ``PageRank`` (SURVEY.md App. A.5 spec; the
+  reference examples/random/depricated/PageRank.scala is broken).  ``returnResults`` gives the
+  merged per-partition result (label->count map / degree tuple) and the ``process*Results``
+  methods format the reference's output lines.
+* ``*AnalysisTask`` classes mirror S/core/analysis/Tasks/** : the job kinds spawned by
+  AnalysisManager (AnalysisManager.scala:133-167) for windowType "false"/"true"/"batched".
+  Where the reference runs Setup/NextStep*/Finish per hop through ten ReaderWorkers, one
+  ``TemporalGraph.run`` call evaluates every hop x window on the GPU.
+"""
+from __future__ import annotations
+
+import json
+import math
+import time
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .graph import TemporalGraph
+from .synth import range_hops
+
+
+# ---------------------------------------------------------------- JVM number printing
+def java_float_str(x, double: bool = False) -> str:
+    """Float.toString / Double.toString shape (plain decimal in [1e-3, 1e7), else
+    d.dddE±n; shortest round-trip digits).  JDK-12 digit strings are parity-unpinned."""
+    v = float(np.float64(x) if double else np.float32(x))
+    if math.isnan(v):
+        return "NaN"
+    if math.isinf(v):
+        return "Infinity" if v > 0 else "-Infinity"
+    r = repr(v) if double else np.format_float_positional(np.float32(x), unique=True, trim="-")
+    if v != 0 and not (1e-3 <= abs(v) < 1e7):
+        s = np.format_float_scientific(np.float64(v) if double else np.float32(v), unique=True, trim="-")
+        mant, exp = s.split("e")
+        if "." not in mant:
+            mant += ".0"
+        return f"{mant}E{int(exp)}"
+    if "e" in r or "E" in r:
+        r = np.format_float_positional(np.float64(v), unique=True, trim="-")
+    if "." not in r:
+        r += ".0"
+    if r.endswith("."):
+        r += "0"
+    return r
+
+
+# ---------------------------------------------------------------- analysers
+class Analyser:
+    """S/core/analysis/API/Analyser.scala:30-63"""
+    algo = ""
+
+    def __init__(self, args: Sequence[str] = ()):
+        self.args = list(args)
+        self.lines: List[str] = []
+
+    def defineMaxSteps(self) -> int:  # noqa: N802 (reference names)
+        raise NotImplementedError
+
+    def returnResults(self, graph: TemporalGraph, hop: int, win: int):  # noqa: N802
+        raise NotImplementedError
+
+    def processResults(self, results, timestamp, viewCompleteTime):  # noqa: N802
+        raise NotImplementedError
+
+    def processViewResults(self, results, timestamp, viewCompleteTime):  # noqa: N802
+        self.processResults(results, timestamp, viewCompleteTime)
+
+    def processWindowResults(self, results, timestamp, windowSize, viewCompleteTime):  # noqa: N802
+        self.processResults(results, timestamp, viewCompleteTime)
+
+    def processBatchWindowResults(self, results, timestamp, windowSet, viewCompleteTime):  # noqa: N802
+        self.processResults(results, timestamp, viewCompleteTime)
+
+
+def cc_fields(grouped: Dict[int, int]) -> Optional[dict]:
+    """ConnectedComponents.processBatchWindowResults summary (ConnectedComponents.scala:137-145);
+    None for an empty view (maxBy throws UnsupportedOperationException -> "No activity")."""
+    if not grouped:
+        return None
+    counts = np.fromiter(grouped.values(), np.int64)
+    non_isl = counts[counts > 1]
+    biggest = int(counts.max())
+    return {
+        "biggest": biggest,
+        "total": int(counts.size),
+        "totalWithoutIslands": int(non_isl.size),
+        "totalIslands": int(counts.size - non_isl.size),
+        "proportion": np.float32(biggest) / np.float32(int(counts.sum())),
+        "proportionWithoutIslands": (np.float32(biggest) / np.float32(int(non_isl.sum()))
+                                     if non_isl.size else np.float32(np.inf)),
+        "clustersGT2": int((counts > 2).sum()),
+    }
+
+
+def cc_fields_from_summary(s) -> Optional[dict]:
+    """Same fields from the GPU-side summary (rgpu_cc_summary_t), no label map needed."""
+    if s.total == 0:
+        return None
+    return {
+        "biggest": int(s.biggest),
+        "total": int(s.total),
+        "totalWithoutIslands": int(s.total_without_islands),
+        "totalIslands": int(s.total_islands),
+        "proportion": np.float32(s.biggest) / np.float32(s.sum_all),
+        "proportionWithoutIslands": (np.float32(s.biggest) / np.float32(s.sum_without_islands)
+                                     if s.sum_without_islands else np.float32(np.inf)),
+        "clustersGT2": int(s.clusters_gt2),
+    }
+
+
+class ConnectedComponents(Analyser):
+    """S/core/analysis/Algorithms/ConnectedComponents.scala:8-162"""
+    algo = "cc"
+
+    def defineMaxSteps(self) -> int:  # :160
+        return 100
+
+    def returnResults(self, graph, hop, win):  # :37-42 (merged over the partition)
+        return graph.cc_result(hop, win)
+
+    @staticmethod
+    def _line(timestamp, window, f, view_ms) -> str:
+        head = f'{{"time":{timestamp},' + (f'"windowsize":{window},' if window is not None else "")
+        return (head + f'"biggest":{f["biggest"]},"total":{f["total"]},'
+                f'"totalWithoutIslands":{f["totalWithoutIslands"]},"totalIslands":{f["totalIslands"]},'
+                f'"proportion":{java_float_str(f["proportion"])},'
+                f'"proportionWithoutIslands":{java_float_str(f["proportionWithoutIslands"])},'
+                f'"clustersGT2":{f["clustersGT2"]},"viewTime":{view_ms},"concatTime":0}},')
+
+    def _emit(self, fields, timestamp, window, view_ms):
+        if fields is None:
+            where = f"view at {timestamp}" + (f" with window {window}" if window is not None else "")
+            self.lines.append(f"No activity for  {where}")  # :65/:89/:119/:154
+        else:
+            self.lines.append(self._line(timestamp, window, fields, view_ms))
+
+    def processResults(self, results, timestamp, viewCompleteTime):  # :44-67
+        merged: Dict[int, int] = {}
+        for part in results:
+            for k, v in part.items():
+                merged[k] = merged.get(k, 0) + v
+        self._emit(cc_fields(merged), timestamp, None, viewCompleteTime)
+
+    def processWindowResults(self, results, timestamp, windowSize, viewCompleteTime):  # :93-122
+        merged: Dict[int, int] = {}
+        for part in results:
+            for k, v in part.items():
+                merged[k] = merged.get(k, 0) + v
+        self._emit(cc_fields(merged), timestamp, windowSize, viewCompleteTime)
+
+    def processBatchWindowResults(self, results, timestamp, windowSet, viewCompleteTime):  # :124-158
+        for i, window in enumerate(results):
+            merged: Dict[int, int] = {}
+            for part in window:
+                for k, v in part.items():
+                    merged[k] = merged.get(k, 0) + v
+            self._emit(cc_fields(merged), timestamp, windowSet[i], viewCompleteTime)
+
+
+class DegreeBasic(Analyser):
+    """S/core/analysis/Algorithms/DegreeBasic.scala:8-79"""
+    algo = "degree"
+
+    def defineMaxSteps(self) -> int:  # :30
+        return 1
+
+    def returnResults(self, graph, hop, win):  # :16-28 -> (totalV, totalOut, totalIn, top20)
+        return graph.degree_result(hop, win)
+
+    @staticmethod
+    def _degree(results):
+        tv = sum(r[0] for r in results)
+        te = sum(r[2] for r in results)
+        deg = (te / tv) if tv else float("nan")  # Int/Int as Double: 0.0/0.0 = NaN
+        return tv, te, deg
+
+    def processResults(self, results, timestamp, viewCompleteTime):  # :32-46
+        tv, te, deg = self._degree(results)
+        self.lines.append(f"{timestamp},{tv},{te},{java_float_str(deg, double=True)}")
+
+    def processWindowResults(self, results, timestamp, windowSize, viewCompleteTime):  # :48-66
+        tv, te, deg = self._degree(results)
+        self.lines.append(f"{timestamp},{windowSize},{tv},{te},{java_float_str(deg, double=True)}")
+
+    def processBatchWindowResults(self, results, timestamp, windowSet, viewCompleteTime):  # :68-78
+        for i, window in enumerate(results):
+            self.processWindowResults(window, timestamp, windowSet[i], viewCompleteTime)
+
+
+class PageRank(Analyser):
+    """PageRank as specified in SURVEY.md App. A.5 (constants of
+    examples/random/depricated/PageRank.scala:11-45; 20 iterations per BASELINE config C3)."""
+    algo = "pagerank"
+
+    def __init__(self, args: Sequence[str] = (), iterations: int = 20):
+        super().__init__(args)
+        self.iterations = iterations
+
+    def defineMaxSteps(self) -> int:
+        return self.iterations
+
+    def returnResults(self, graph, hop, win):
+        ids, pr = graph.pr_result(hop, win)
+        return dict(zip(ids.tolist(), pr.tolist()))
+
+    def processResults(self, results, timestamp, viewCompleteTime):
+        merged: Dict[int, float] = {}
+        for part in results:
+            merged.update(part)
+        top = sorted(merged.items(), key=lambda kv: (-kv[1], kv[0]))[:5]
+        self.lines.append(json.dumps({"time": timestamp, "top5": top, "vertices": len(merged)}))
+
+
+# ---------------------------------------------------------------- tasks
+class TimeNotIngested(RuntimeError):
+    """TimeCheck failed (ReaderWorker.processTimeCheckRequest :259-274); the reference retries in 10 s."""
+
+
+class AnalysisTask:
+    """S/core/analysis/Tasks/AnalysisTask.scala — here one GPU call per job."""
+
+    def __init__(self, graphs: Sequence[TemporalGraph], analyser: Analyser, retain_results: bool = True):
+        self.graphs = list(graphs)
+        self.analyser = analyser
+        self.retain = retain_results
+        self.view_ms = 0.0
+
+    # overridden by the subclasses
+    def hops(self) -> np.ndarray:
+        raise NotImplementedError
+
+    def windowSet(self) -> List[int]:  # noqa: N802
+        return []
+
+    def windowSize(self) -> int:  # noqa: N802
+        return -1
+
+    def _windows(self) -> List[int]:
+        ws = self.windowSet()
+        if ws:
+            return list(ws)
+        return [self.windowSize()] if self.windowSize() != -1 else []
+
+    def time_check(self, hops: np.ndarray) -> None:
+        newest = min(g.newest_time() for g in self.graphs)
+        if hops.size and int(hops.max()) > newest:
+            raise TimeNotIngested(f"{int(hops.max())} is yet to be ingested, currently at {newest}")
+
+    def run(self) -> List[str]:
+        hops = self.hops()
+        self.time_check(hops)
+        windows = self._windows()
+        a = self.analyser
+        max_steps = a.defineMaxSteps()
+        t0 = time.perf_counter()
+        for g in self.graphs:
+            g.run(a.algo, hops, windows, max_steps=max_steps if a.algo == "cc" else 100,
+                  pr_iters=max_steps if a.algo == "pagerank" else 0, retain=self.retain)
+        self.view_ms = (time.perf_counter() - t0) * 1e3 / max(1, len(hops))
+        vt = int(round(self.view_ms))
+        for h, t in enumerate(hops.tolist()):
+            if self.windowSet():
+                # BWindowed*AnalysisTask.result: [worker][window] -> [window][worker]
+                results = [[g_res for g_res in (a.returnResults(g, h, w) for g in self.graphs)]
+                           for w in range(len(windows))]
+                a.processBatchWindowResults(results, t, windows, vt)
+            elif windows:
+                a.processWindowResults([a.returnResults(g, h, 0) for g in self.graphs], t, windows[0], vt)
+            else:
+                a.processViewResults([a.returnResults(g, h, 0) for g in self.graphs], t, vt)
+        return a.lines
+
+
+class ViewAnalysisTask(AnalysisTask):
+    def __init__(self, graphs, analyser, timestamp: int, **kw):
+        super().__init__(graphs, analyser, **kw)
+        self.timestamp = timestamp
+
+    def hops(self):
+        return np.asarray([self.timestamp], np.int64)
+
+
+class WindowedViewAnalysisTask(ViewAnalysisTask):
+    def __init__(self, graphs, analyser, timestamp: int, window: int, **kw):
+        super().__init__(graphs, analyser, timestamp, **kw)
+        self.window = window
+
+    def windowSize(self):  # noqa: N802
+        return self.window
+
+
+class BWindowedViewAnalysisTask(ViewAnalysisTask):
+    def __init__(self, graphs, analyser, timestamp: int, windows: Sequence[int], **kw):
+        super().__init__(graphs, analyser, timestamp, **kw)
+        self.windows = list(windows)
+
+    def windowSet(self):  # noqa: N802
+        return self.windows
+
+
+class RangeAnalysisTask(AnalysisTask):
+    """RangeTasks/RangeAnalysisTask.scala:51-78"""
+
+    def __init__(self, graphs, analyser, start: int, end: int, jump: int, **kw):
+        super().__init__(graphs, analyser, **kw)
+        self.start, self.end, self.jump = start, end, jump
+
+    def hops(self):
+        return range_hops(self.start, self.end, self.jump)
+
+
+class WindowedRangeAnalysisTask(RangeAnalysisTask):
+    def __init__(self, graphs, analyser, start, end, jump, window: int, **kw):
+        super().__init__(graphs, analyser, start, end, jump, **kw)
+        self.window = window
+
+    def windowSize(self):  # noqa: N802
+        return self.window
+
+
+class BWindowedRangeAnalysisTask(RangeAnalysisTask):
+    def __init__(self, graphs, analyser, start, end, jump, windows: Sequence[int], **kw):
+        super().__init__(graphs, analyser, start, end, jump, **kw)
+        self.windows = list(windows)
+
+    def windowSet(self):  # noqa: N802
+        return self.windows

@@ -1,0 +1,515 @@
+// kernels.hip — gfx950 kernels of the windowed temporal-analysis path.
+//
+// Layout: a *batch* holds up to 64 views (hop k, window w) -> bit / lane j = k*W + w.
+// Every per-vertex quantity of a batch is a 64-lane row (one wavefront lane per view), so
+// one pass over the adjacency serves every view of every hop in the batch.
+//
+//   k_vertex_mask  K1  Entity.aliveAtWithWindow for every vertex x hop x window, with the
+//                      batched running-min window (WindowLens.shrinkWindow, WindowLens.scala:167-173)
+//   k_edge_mask    K1  the same for edges: own history + endpoint death lists (killList)
+//   k_cc_slots     K2  per-view adjacency filter (Vertex.viewAtWithWindow, Vertex.scala:70-74)
+//                      compacted into a batch CSR with a 64-bit view mask per slot
+//   k_cc_step      K3  one CC superstep for all views (ConnectedComponents.analyse :19-35)
+//   k_cc_hist/summary K5 label->count histogram + processBatchWindowResults summary (:137-145)
+//   k_degree       DegreeBasic.returnResults (DegreeBasic.scala:16-28)
+//   k_pr_slots/k_pr_step  PageRank spec
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.hpp"
+
+namespace rgpu {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+  uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l);
+  uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  int l = lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// floor(t) of a sorted key list (key = time*2 + alive): index of the last key <= 2t+1, or -1.
+__device__ __forceinline__ int64_t floor_idx(const int64_t* key, int64_t lo, int64_t hi, int64_t t) {
+  const int64_t probe = 2 * t + 1;
+  int64_t a = lo, b = hi;
+  while (a < b) {
+    int64_t m = (a + b) >> 1;
+    if (key[m] <= probe) a = m + 1; else b = m;
+  }
+  return a - 1 >= lo ? a - 1 : -1;
+}
+// last death time <= t in a sorted list, or -1
+__device__ __forceinline__ int64_t last_death(const int64_t* dt, int64_t lo, int64_t hi, int64_t t) {
+  int64_t a = lo, b = hi;
+  while (a < b) {
+    int64_t m = (a + b) >> 1;
+    if (dt[m] <= t) a = m + 1; else b = m;
+  }
+  return a > lo ? dt[a - 1] : -1;
+}
+
+// ---------------------------------------------------------------- K1: window masks
+__global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* __restrict__ voff,
+                                                     const int64_t* __restrict__ vkey, BatchParams bp,
+                                                     uint64_t* __restrict__ vm) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t lo = voff[v], hi = voff[v + 1];
+    uint64_t m = 0;
+    for (int k = 0; k < bp.K; k++) {
+      const int64_t t = bp.hop[k];
+      const int64_t f = floor_idx(vkey, lo, hi, t);
+      if (f < 0) continue;
+      const int64_t key = vkey[f];
+      if (!(key & 1)) continue;  // floor is a deletion
+      const int64_t age = t - (key >> 1);
+      for (int w = 0; w < bp.W; w++)
+        if (age <= bp.thr_v[w]) m |= 1ull << (k * bp.W + w);
+    }
+    vm[v] = m;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __restrict__ esrc,
+                                                   const int32_t* __restrict__ edst,
+                                                   const int64_t* __restrict__ eoff,
+                                                   const int64_t* __restrict__ ekey,
+                                                   const int64_t* __restrict__ doff,
+                                                   const int64_t* __restrict__ dtime, BatchParams bp,
+                                                   uint64_t* __restrict__ em) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t lo = eoff[e], hi = eoff[e + 1];
+    const int32_t s = esrc[e], d = edst[e];
+    const int64_t s0 = doff[s], s1 = doff[s + 1], d0 = doff[d], d1 = doff[d + 1];
+    uint64_t m = 0;
+    for (int k = 0; k < bp.K; k++) {
+      const int64_t t = bp.hop[k];
+      const int64_t f = floor_idx(ekey, lo, hi, t);
+      if (f < 0) continue;
+      const int64_t key = ekey[f];
+      if (!(key & 1)) continue;
+      const int64_t ft = key >> 1;
+      // an endpoint death in (ft, t] is a later kill point (killList / vertexRemoval)
+      if (s1 > s0 && last_death(dtime, s0, s1, t) > ft) continue;
+      if (d1 > d0 && last_death(dtime, d0, d1, t) > ft) continue;
+      const int64_t age = t - ft;
+      for (int w = 0; w < bp.W; w++)
+        if (age <= bp.thr_e[w]) m |= 1ull << (k * bp.W + w);
+    }
+    em[e] = m;
+  }
+}
+
+// ---------------------------------------------------------------- K2: batch CSR
+// One wave per vertex.  Static slots of rank v = its out-edges then its in-edges
+// (adjacency offset out_off[v] + in_off[v]).  Slot kept iff its view mask
+//   em[e] & vm[nbr] & vm[v]  != 0
+// i.e. the edge is alive in the view's own window AND both endpoints are in the view's
+// (running-min) vertex set — messages to vertices outside the lens are never read
+// (WindowLens.getVerticesWithMessages, WindowLens.scala:149-158).  Self-loops only
+// message the vertex itself and never change a label: dropped.
+// Also writes the initial label row (label = own rank, ConnectedComponents.setup :10-17).
+__global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __restrict__ out_off,
+                                                  const int64_t* __restrict__ in_off,
+                                                  const int32_t* __restrict__ in_eid,
+                                                  const int32_t* __restrict__ esrc,
+                                                  const int32_t* __restrict__ edst,
+                                                  const uint64_t* __restrict__ vm,
+                                                  const uint64_t* __restrict__ em,
+                                                  int32_t* __restrict__ cnt, int32_t* __restrict__ snbr,
+                                                  uint64_t* __restrict__ smask,
+                                                  int32_t* __restrict__ lab0,
+                                                  unsigned long long* __restrict__ counters) {
+  __shared__ unsigned long long red[2];
+  if (threadIdx.x < 2) red[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned long long members = 0, alive = 0;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    lab0[v * 64 + lane] = (int32_t)v;
+    const uint64_t mv = vm[v];
+    if (mv == 0) {
+      if (lane == 0) cnt[v] = 0;
+      continue;
+    }
+    const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
+    const int64_t nout = o1 - o0, ntot = nout + (i1 - i0), base = o0 + i0;
+    int32_t count = 0;
+    for (int64_t c = 0; c < ntot; c += 64) {
+      const int64_t j = c + lane;
+      uint64_t m = 0;
+      int32_t nb = 0;
+      if (j < ntot) {
+        int64_t e;
+        if (j < nout) { e = o0 + j; nb = edst[e]; }
+        else { e = in_eid[i0 + (j - nout)]; nb = esrc[e]; }
+        if (nb != (int32_t)v) m = em[e] & vm[nb] & mv;
+      }
+      const uint64_t bal = __ballot(m != 0);
+      if (m) {
+        const int64_t pos = base + count + __popcll(bal & lanemask_lt());
+        snbr[pos] = nb;
+        smask[pos] = m;
+      }
+      count += __popcll(bal);
+    }
+    if (lane == 0) cnt[v] = count;
+    members += 1;
+    alive += (unsigned long long)count;
+  }
+  if (lane == 0) {
+    atomicAdd(&red[0], members);
+    atomicAdd(&red[1], alive);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&counters[0], red[0]);
+    atomicAdd(&counters[1], red[1]);
+  }
+}
+
+// ---------------------------------------------------------------- K3: CC superstep
+// Jacobi min-label step for every view of the batch at once: a vertex takes the min of
+// its own label and the labels of neighbours whose label improved in the previous step
+// (only those sent messages: ConnectedComponents.analyse :19-35, VertexMutliQueue parity
+// queues).  step 1 consumes the setup messages (every member "changed").  A step with no
+// improvement anywhere ends the job (AnalysisTask.endStep :208-225): later launches exit.
+__global__ __launch_bounds__(256) void k_cc_step(int step, int64_t nv, const int64_t* __restrict__ out_off,
+                                                 const int64_t* __restrict__ in_off,
+                                                 const uint64_t* __restrict__ vm,
+                                                 const int32_t* __restrict__ cnt,
+                                                 const int32_t* __restrict__ snbr,
+                                                 const uint64_t* __restrict__ smask,
+                                                 const int32_t* __restrict__ lab_cur,
+                                                 int32_t* __restrict__ lab_next,
+                                                 const uint64_t* __restrict__ chg_prev,
+                                                 uint64_t* __restrict__ chg_next,
+                                                 int32_t* __restrict__ stepcnt) {
+  if (step > 1 && stepcnt[step - 1] == 0) return;
+  __shared__ int32_t red;
+  if (threadIdx.x == 0) red = 0;
+  __syncthreads();
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  int32_t changed = 0;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    const uint64_t mv = vm[v];
+    if (mv == 0) continue;
+    const int32_t cur = lab_cur[v * 64 + lane];
+    int32_t best = cur;
+    const int32_t n = cnt[v];
+    const int64_t base = out_off[v] + in_off[v];
+    for (int32_t c = 0; c < n; c += 64) {
+      const int32_t j = c + lane;
+      uint64_t act = 0;
+      int32_t nb = 0;
+      if (j < n) {
+        nb = snbr[base + j];
+        act = smask[base + j] & chg_prev[nb];
+      }
+      uint64_t bal = __ballot(act != 0);
+      while (bal) {
+        const int L = __builtin_ctzll(bal);
+        bal &= bal - 1;
+        const int32_t nbL = __builtin_amdgcn_readlane(nb, L);
+        const uint64_t aL = readlane64(act, L);
+        if ((aL >> lane) & 1) {
+          const int32_t x = lab_cur[(int64_t)nbL * 64 + lane];
+          best = x < best ? x : best;
+        }
+      }
+    }
+    lab_next[v * 64 + lane] = best;
+    const uint64_t ch = __ballot(best < cur);
+    if (lane == 0) chg_next[v] = ch;
+    changed += ch != 0;
+  }
+  if (lane == 0 && changed) atomicAdd(&red, changed);
+  __syncthreads();
+  if (threadIdx.x == 0 && red) atomicAdd(&stepcnt[step], red);
+}
+
+// ---------------------------------------------------------------- K5: CC reductions
+// label -> count histogram (ConnectedComponents.returnResults :37-42, groupBy over labels)
+__global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, const uint64_t* __restrict__ vm,
+                                                 const int32_t* __restrict__ lab,
+                                                 int32_t* __restrict__ hist) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    const uint64_t mv = vm[v];
+    if ((mv >> lane) & 1) atomicAdd(&hist[(int64_t)lab[v * 64 + lane] * 64 + lane], 1);
+  }
+}
+
+// processBatchWindowResults summary per view (ConnectedComponents.scala:137-145); clears
+// the histogram for the next batch.  stats[f*64 + view]: 0 biggest 1 total 2 total>1
+// 3 total>2 4 sum 5 sum(count>1)
+__global__ __launch_bounds__(256) void k_cc_summary(int64_t nv, int32_t* __restrict__ hist,
+                                                    unsigned long long* __restrict__ stats) {
+  __shared__ unsigned long long red[6][64];
+  for (int i = threadIdx.x; i < 6 * 64; i += blockDim.x) (&red[0][0])[i] = 0;
+  __syncthreads();
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned long long big = 0, tot = 0, nis = 0, gt2 = 0, sum = 0, snis = 0;
+  for (int64_t r = wave; r < nv; r += nwaves) {
+    const int32_t c = hist[r * 64 + lane];
+    if (c) {
+      hist[r * 64 + lane] = 0;
+      const unsigned long long uc = (unsigned long long)c;
+      big = uc > big ? uc : big;
+      tot += 1;
+      nis += c > 1;
+      gt2 += c > 2;
+      sum += uc;
+      snis += c > 1 ? uc : 0;
+    }
+  }
+  atomicMax(&red[0][lane], big);
+  atomicAdd(&red[1][lane], tot);
+  atomicAdd(&red[2][lane], nis);
+  atomicAdd(&red[3][lane], gt2);
+  atomicAdd(&red[4][lane], sum);
+  atomicAdd(&red[5][lane], snis);
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int j = threadIdx.x;
+    if (red[0][j]) atomicMax(&stats[0 * 64 + j], red[0][j]);
+    for (int f = 1; f < 6; f++)
+      if (red[f][j]) atomicAdd(&stats[f * 64 + j], red[f][j]);
+  }
+}
+
+// ---------------------------------------------------------------- degree
+// DegreeBasic.returnResults (DegreeBasic.scala:16-28) for every view: out = alive
+// out-edges incl. a self-loop, in = alive in-edges (a self-loop never enters
+// incomingEdges, EntityStorage.scala:257), edges filtered by their own history only
+// (Vertex.viewAtWithWindow).  Per-vertex rows are written to outdeg/indeg; per-view
+// totals (V, sum out, sum in) into stats[f*64 + view].
+__global__ __launch_bounds__(256) void k_degree(int64_t nv, const int64_t* __restrict__ out_off,
+                                                const int64_t* __restrict__ in_off,
+                                                const int32_t* __restrict__ in_eid,
+                                                const uint64_t* __restrict__ vm,
+                                                const uint64_t* __restrict__ em,
+                                                int32_t* __restrict__ outdeg,
+                                                int32_t* __restrict__ indeg,
+                                                unsigned long long* __restrict__ stats) {
+  __shared__ uint64_t tile[4][64];
+  __shared__ unsigned long long red[3][64];
+  for (int i = threadIdx.x; i < 3 * 64; i += blockDim.x) (&red[0][0])[i] = 0;
+  __syncthreads();
+  const int lane = lane_id(), wib = threadIdx.x >> 6;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned long long tv = 0, to = 0, ti = 0;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    const uint64_t mv = vm[v];
+    int32_t od = 0, id = 0;
+    if (mv) {
+      const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
+      for (int dir = 0; dir < 2; dir++) {
+        const int64_t n = dir ? i1 - i0 : o1 - o0;
+        int32_t acc = 0;
+        for (int64_t c = 0; c < n; c += 64) {
+          const int64_t j = c + lane;
+          uint64_t m = 0;
+          if (j < n) m = em[dir ? in_eid[i0 + j] : o0 + j];
+          tile[wib][lane] = m;  // transpose through LDS: lane = view
+          __builtin_amdgcn_wave_barrier();
+          const int lim = (int)(n - c < 64 ? n - c : 64);
+          for (int q = 0; q < lim; q++) acc += (int32_t)((tile[wib][q] >> lane) & 1);
+          __builtin_amdgcn_wave_barrier();
+        }
+        if (dir) id = acc; else od = acc;
+      }
+      const int in_view = (int)((mv >> lane) & 1);
+      od = in_view ? od : 0;
+      id = in_view ? id : 0;
+      tv += in_view;
+      to += od;
+      ti += id;
+    }
+    outdeg[v * 64 + lane] = od;
+    indeg[v * 64 + lane] = id;
+  }
+  atomicAdd(&red[0][lane], tv);
+  atomicAdd(&red[1][lane], to);
+  atomicAdd(&red[2][lane], ti);
+  __syncthreads();
+  if (threadIdx.x < 64)
+    for (int f = 0; f < 3; f++)
+      if (red[f][threadIdx.x]) atomicAdd(&stats[f * 64 + threadIdx.x], red[f][threadIdx.x]);
+}
+
+// ---------------------------------------------------------------- PageRank (App. A.5)
+// Pull slots of rank v = its in-edges plus its self-loop (messageAllOutgoingNeighbors
+// reaches the vertex itself); kept iff em[e] & vm[src] & vm[v] != 0.  Static capacity
+// in-degree + 1 at offset in_off[v] + v.  Initialises PR0 = 1 and contrib = 1/max(od,1).
+__global__ __launch_bounds__(256) void k_pr_slots(int64_t nv, const int64_t* __restrict__ out_off,
+                                                  const int64_t* __restrict__ in_off,
+                                                  const int32_t* __restrict__ in_eid,
+                                                  const int32_t* __restrict__ esrc,
+                                                  const int32_t* __restrict__ edst,
+                                                  const uint64_t* __restrict__ vm,
+                                                  const uint64_t* __restrict__ em,
+                                                  const int32_t* __restrict__ outdeg,
+                                                  int32_t* __restrict__ cnt, int32_t* __restrict__ snbr,
+                                                  uint64_t* __restrict__ smask,
+                                                  double* __restrict__ pr,
+                                                  double* __restrict__ contrib) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    const int32_t od = outdeg[v * 64 + lane];
+    pr[v * 64 + lane] = 1.0;  // defaultPR, PageRank.scala:14
+    contrib[v * 64 + lane] = 1.0 / (double)(od > 1 ? od : 1);
+    const uint64_t mv = vm[v];
+    if (mv == 0) {
+      if (lane == 0) cnt[v] = 0;
+      continue;
+    }
+    const int64_t i0 = in_off[v], i1 = in_off[v + 1], nin = i1 - i0, base = i0 + v;
+    int32_t count = 0;
+    for (int64_t c = 0; c < nin; c += 64) {
+      const int64_t j = c + lane;
+      uint64_t m = 0;
+      int32_t nb = 0;
+      if (j < nin) {
+        const int32_t e = in_eid[i0 + j];
+        nb = esrc[e];
+        m = em[e] & vm[nb] & mv;
+      }
+      const uint64_t bal = __ballot(m != 0);
+      if (m) {
+        const int64_t pos = base + count + __popcll(bal & lanemask_lt());
+        snbr[pos] = nb;
+        smask[pos] = m;
+      }
+      count += __popcll(bal);
+    }
+    // self-loop: out-edges of v are sorted by dst
+    int64_t a = out_off[v], b = out_off[v + 1];
+    while (a < b) {
+      const int64_t mid = (a + b) >> 1;
+      if (edst[mid] < (int32_t)v) a = mid + 1; else b = mid;
+    }
+    if (lane == 0) {
+      if (a < out_off[v + 1] && edst[a] == (int32_t)v) {
+        const uint64_t m = em[a] & mv;
+        if (m) {
+          snbr[base + count] = (int32_t)v;
+          smask[base + count] = m;
+          count++;
+        }
+      }
+      cnt[v] = count;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pr_step(int64_t nv, const int64_t* __restrict__ in_off,
+                                                 const uint64_t* __restrict__ vm,
+                                                 const int32_t* __restrict__ outdeg,
+                                                 const int32_t* __restrict__ cnt,
+                                                 const int32_t* __restrict__ snbr,
+                                                 const uint64_t* __restrict__ smask,
+                                                 const double* __restrict__ contrib_cur,
+                                                 double* __restrict__ contrib_next,
+                                                 double* __restrict__ pr) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    const uint64_t mv = vm[v];
+    if (mv == 0) continue;
+    const int32_t n = cnt[v];
+    const int64_t base = in_off[v] + v;
+    double acc = 0.0;
+    for (int32_t c = 0; c < n; c += 64) {
+      const int32_t j = c + lane;
+      uint64_t m = 0;
+      int32_t nb = 0;
+      if (j < n) { nb = snbr[base + j]; m = smask[base + j]; }
+      uint64_t bal = __ballot(m != 0);
+      while (bal) {
+        const int L = __builtin_ctzll(bal);
+        bal &= bal - 1;
+        const int32_t nbL = __builtin_amdgcn_readlane(nb, L);
+        const uint64_t mL = readlane64(m, L);
+        if ((mL >> lane) & 1) acc += contrib_cur[(int64_t)nbL * 64 + lane];
+      }
+    }
+    if ((mv >> lane) & 1) {
+      const double p = 0.15 + 0.85 * acc;  // dumplingFactor 0.85, PageRank.scala:11
+      const int32_t od = outdeg[v * 64 + lane];
+      pr[v * 64 + lane] = p;
+      contrib_next[v * 64 + lane] = p / (double)(od > 1 ? od : 1);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
+  int64_t g = (items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (unsigned)(g > cap ? cap : g);
+}
+
+void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm) {
+  k_vertex_mask<<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm);
+}
+void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em) {
+  k_edge_mask<<<grid_for(g.ne, 256), 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff,
+                                                   g.dtime, bp, em);
+}
+void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+                     int32_t* cnt, int32_t* snbr, uint64_t* smask, int32_t* lab0,
+                     unsigned long long* counters) {
+  k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
+                                                vm, em, cnt, snbr, smask, lab0, counters);
+}
+void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
+                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
+                    const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
+                    uint64_t* chg_next, int32_t* stepcnt) {
+  k_cc_step<<<grid_for(g.nv, 4), 256, 0, s>>>(step, g.nv, g.out_off, g.in_off, vm, cnt, snbr, smask,
+                                               lab_cur, lab_next, chg_prev, chg_next, stepcnt);
+}
+void launch_cc_hist(hipStream_t s, const DevGraph& g, const uint64_t* vm, const int32_t* lab,
+                    int32_t* hist) {
+  k_cc_hist<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, vm, lab, hist);
+}
+void launch_cc_summary(hipStream_t s, const DevGraph& g, int32_t* hist, unsigned long long* stats) {
+  k_cc_summary<<<grid_for(g.nv, 4, 2048), 256, 0, s>>>(g.nv, hist, stats);
+}
+void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+                   int32_t* outdeg, int32_t* indeg, unsigned long long* stats) {
+  k_degree<<<grid_for(g.nv, 4, 2048), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, vm, em,
+                                                    outdeg, indeg, stats);
+}
+void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+                     const int32_t* outdeg, int32_t* cnt, int32_t* snbr, uint64_t* smask,
+                     double* pr, double* contrib) {
+  k_pr_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
+                                                vm, em, outdeg, cnt, snbr, smask, pr, contrib);
+}
+void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const int32_t* outdeg,
+                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
+                    const double* contrib_cur, double* contrib_next, double* pr) {
+  k_pr_step<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.in_off, vm, outdeg, cnt, snbr, smask,
+                                               contrib_cur, contrib_next, pr);
+}
+
+}  // namespace rgpu

@@ -1,0 +1,51 @@
+// kernels.hpp — device-side graph view, batch parameters and kernel launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rgpu {
+
+constexpr int kViews = 64;  // views per batch = wavefront width (lane j <-> view j)
+
+// One batch of views: hops[K] x windows[W], view bit j = k*W + w, K*W <= 64.
+struct BatchParams {
+  int K, W;
+  int64_t hop[kViews];    // view timestamps (RangeAnalysisTask hop times)
+  int64_t thr_v[kViews];  // vertex-set window of window index w: min(w_0..w_w)  (shrinkWindow)
+  int64_t thr_e[kViews];  // edge window of window index w: w_w (viewAtWithWindow(t, setWindow))
+};
+
+// Sealed partition resident in HBM.
+struct DevGraph {
+  int64_t nv = 0, ne = 0, n_in = 0;
+  const int64_t *voff = nullptr, *vkey = nullptr;    // vertex histories
+  const int64_t *doff = nullptr, *dtime = nullptr;   // vertex death lists
+  const int32_t *esrc = nullptr, *edst = nullptr;    // edges sorted by (src, dst)
+  const int64_t *eoff = nullptr, *ekey = nullptr;    // edge own histories
+  const int64_t *out_off = nullptr, *in_off = nullptr;
+  const int32_t* in_eid = nullptr;
+};
+
+void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm);
+void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em);
+void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+                     int32_t* cnt, int32_t* snbr, uint64_t* smask, int32_t* lab0,
+                     unsigned long long* counters);
+void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
+                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
+                    const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
+                    uint64_t* chg_next, int32_t* stepcnt);
+void launch_cc_hist(hipStream_t s, const DevGraph& g, const uint64_t* vm, const int32_t* lab,
+                    int32_t* hist);
+void launch_cc_summary(hipStream_t s, const DevGraph& g, int32_t* hist, unsigned long long* stats);
+void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+                   int32_t* outdeg, int32_t* indeg, unsigned long long* stats);
+void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+                     const int32_t* outdeg, int32_t* cnt, int32_t* snbr, uint64_t* smask,
+                     double* pr, double* contrib);
+void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const int32_t* outdeg,
+                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
+                    const double* contrib_cur, double* contrib_next, double* pr);
+
+}  // namespace rgpu

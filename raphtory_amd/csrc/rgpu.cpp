@@ -1,0 +1,763 @@
+// rgpu.cpp — C ABI (include/rgpu.h) and the batch scheduler that drives the kernels.
+//
+// One rgpu_ctx = one Partition Manager's reader (S/core/components/PartitionManager/
+// Reader.scala:42-53) bound to one GPU.  rgpu_run_view_batch replaces the whole
+// Setup -> NextStep* -> Finish conversation that AnalysisTask (S/core/analysis/Tasks/
+// AnalysisTask.scala:162-283) drives through ten ReaderWorkers, for every hop of a Range
+// job (RangeAnalysisTask.scala:18-35) and every window of the batch at once.
+//
+// Scheduling: hops are grouped into batches of K = floor(64/W) hops (64 views).  Two
+// batch slots, each with its own HIP stream and buffers, are kept in flight: while the
+// host inspects one slot's superstep counters (the halting vote), the other slot's
+// kernels keep the GPU busy.  Supersteps are enqueued in chunks; a step whose
+// predecessor changed nothing exits at once (device-side halting), so over-enqueueing
+// costs only an empty launch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+#include "rgpu_internal.hpp"
+
+using namespace rgpu;
+
+namespace {
+
+struct HipFail {
+  std::string msg;
+};
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) throw HipFail{std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUMMARY = 4,
+                KID_PR = 5, KID_DEGREE = 6, KID_N = 8 };
+
+constexpr int kMaxSteps = 128;
+constexpr int kStatWords = 7 * kViews;  // 6 per-view fields + counters row
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev = nullptr;
+  uint64_t *vm = nullptr, *em = nullptr;
+  int32_t *cnt = nullptr, *snbr = nullptr;
+  uint64_t* smask = nullptr;
+  int32_t* lab[2] = {nullptr, nullptr};
+  uint64_t* chg[2] = {nullptr, nullptr};
+  int32_t *stepcnt = nullptr, *hist = nullptr;
+  unsigned long long* stats = nullptr;
+  int32_t *outdeg = nullptr, *indeg = nullptr;
+  double *pr = nullptr, *contrib[2] = {nullptr, nullptr};
+  int32_t *pcnt = nullptr, *psnbr = nullptr;
+  uint64_t* psmask = nullptr;
+  int32_t* h_stepcnt = nullptr;
+  unsigned long long* h_stats = nullptr;
+  // state of the batch in flight
+  int batch = -1, phase = 0, r_launched = 0, r_final = 0, kb = 0;
+};
+
+struct Retained {  // per batch, RGPU_RUN_RETAIN
+  std::vector<uint64_t> vm;
+  std::vector<int32_t> a, b;  // CC: labels | degree: out, in
+  std::vector<double> pr;
+};
+
+struct Timed {
+  int kid;
+  int slot;
+  hipEvent_t a, b;
+  double bytes;
+};
+
+}  // namespace
+
+struct rgpu_ctx {
+  std::mutex mu;
+  int part = 0, nparts = 1, device = 0;
+  std::string err;
+  std::vector<Event> events;
+  int64_t newest = -1;
+  bool sealed = false;
+  Packed pk;
+  DevGraph g;
+  std::vector<void*> graph_allocs;
+  Slot slot[2];
+  int nslots = 2;
+  bool slot_cc = false, slot_deg = false, slot_pr = false;
+  // last run
+  int algo = -1, K = 0, W = 0;
+  size_t n_hops = 0;
+  std::vector<rgpu_cc_summary_t> cc;
+  std::vector<int64_t> deg;  // [view][3]
+  std::vector<Retained> kept;
+  bool retained = false;
+  rgpu_stats_t st{};
+  // profiling
+  bool profile = false;
+  std::vector<hipEvent_t> evpool;
+  size_t evused = 0;
+  std::vector<Timed> timed;
+};
+
+namespace {
+
+template <class T>
+T* dalloc(std::vector<void*>& list, size_t n) {
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, sizeof(T) * (n ? n : 1)));
+  list.push_back(p);
+  return (T*)p;
+}
+template <class T>
+T* dupload(std::vector<void*>& list, const std::vector<T>& h) {
+  T* d = dalloc<T>(list, h.size());
+  if (!h.empty()) HIPCHK(hipMemcpy(d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+  return d;
+}
+
+void free_graph(rgpu_ctx* c) {
+  for (void* p : c->graph_allocs) (void)hipFree(p);
+  c->graph_allocs.clear();
+  for (Slot& s : c->slot) {
+    if (s.h_stepcnt) (void)hipHostFree(s.h_stepcnt);
+    if (s.h_stats) (void)hipHostFree(s.h_stats);
+    if (s.ev) (void)hipEventDestroy(s.ev);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = Slot();
+  }
+  c->slot_cc = c->slot_deg = c->slot_pr = false;
+  c->g = DevGraph();
+}
+
+hipEvent_t take_event(rgpu_ctx* c) {
+  if (c->evused == c->evpool.size()) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    c->evpool.push_back(e);
+  }
+  return c->evpool[c->evused++];
+}
+
+// Run `fn` (one kernel launch) on slot stream, bracketed by events in profile mode.
+template <class F>
+void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn) {
+  Slot& s = c->slot[si];
+  if (c->profile) {
+    hipEvent_t a = take_event(c), b = take_event(c);
+    HIPCHK(hipEventRecord(a, s.stream));
+    fn();
+    HIPCHK(hipEventRecord(b, s.stream));
+    c->timed.push_back({kid, si, a, b, bytes});
+  } else {
+    fn();
+  }
+  HIPCHK(hipGetLastError());
+  c->st.kernel_launches[kid]++;
+  c->st.kernel_bytes[kid] += bytes;
+}
+
+void ensure_slots(rgpu_ctx* c, int algo) {
+  auto& L = c->graph_allocs;
+  const int64_t nv = c->g.nv, ne = c->g.ne, nin = c->g.n_in;
+  const size_t rows = (size_t)nv * kViews;
+  for (int i = 0; i < 2; i++) {
+    Slot& s = c->slot[i];
+    if (!s.stream) {
+      HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+      HIPCHK(hipHostMalloc((void**)&s.h_stepcnt, sizeof(int32_t) * kMaxSteps));
+      HIPCHK(hipHostMalloc((void**)&s.h_stats, sizeof(unsigned long long) * kStatWords));
+      s.vm = dalloc<uint64_t>(L, nv);
+      s.em = dalloc<uint64_t>(L, ne);
+      s.stepcnt = dalloc<int32_t>(L, kMaxSteps);
+      s.stats = dalloc<unsigned long long>(L, kStatWords);
+    }
+    if (algo == RGPU_ALGO_CC && !c->slot_cc) {
+      s.cnt = dalloc<int32_t>(L, nv);
+      s.snbr = dalloc<int32_t>(L, ne + nin);
+      s.smask = dalloc<uint64_t>(L, ne + nin);
+      s.lab[0] = dalloc<int32_t>(L, rows);
+      s.lab[1] = dalloc<int32_t>(L, rows);
+      s.chg[0] = dalloc<uint64_t>(L, nv);
+      s.chg[1] = dalloc<uint64_t>(L, nv);
+      s.hist = dalloc<int32_t>(L, rows);
+      HIPCHK(hipMemset(s.hist, 0, sizeof(int32_t) * (rows ? rows : 1)));
+    }
+    if ((algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) && !c->slot_deg) {
+      s.outdeg = dalloc<int32_t>(L, rows);
+      s.indeg = dalloc<int32_t>(L, rows);
+    }
+    if (algo == RGPU_ALGO_PR && !c->slot_pr) {
+      s.pr = dalloc<double>(L, rows);
+      s.contrib[0] = dalloc<double>(L, rows);
+      s.contrib[1] = dalloc<double>(L, rows);
+      s.pcnt = dalloc<int32_t>(L, nv);
+      s.psnbr = dalloc<int32_t>(L, nin + nv);
+      s.psmask = dalloc<uint64_t>(L, nin + nv);
+    }
+  }
+  if (algo == RGPU_ALGO_CC) c->slot_cc = true;
+  if (algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) c->slot_deg = true;
+  if (algo == RGPU_ALGO_PR) c->slot_pr = true;
+}
+
+struct RunCfg {
+  int algo, max_steps, pr_iters, flags;
+  int K, W;
+  const int64_t* hops;
+  size_t n_hops;
+  int64_t thr_v[kViews], thr_e[kViews];
+  int chunk0, chunk;
+};
+
+// algorithmic bytes: see rgpu_stats_t.kernel_bytes
+double bytes_mask(const DevGraph& g) {
+  return 8.0 * (g.nv + 1) + 8.0 * g.nv + 8.0 * (g.ne + 1) + 16.0 * g.ne + 8.0 * g.ne;
+}
+
+void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
+  Slot& s = c->slot[si];
+  const DevGraph& g = c->g;
+  int last = std::min(rc.max_steps, s.r_launched + n);
+  for (int r = s.r_launched + 1; r <= last; r++) {
+    const uint64_t* chg_prev = r == 1 ? s.vm : s.chg[(r - 1) & 1];
+    timed_launch(c, si, KID_STEP, 0.0, [&] {
+      launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
+                     chg_prev, s.chg[r & 1], s.stepcnt);
+    });
+  }
+  s.r_launched = last;
+  HIPCHK(hipMemcpyAsync(s.h_stepcnt, s.stepcnt, sizeof(int32_t) * kMaxSteps, hipMemcpyDeviceToHost,
+                        s.stream));
+  HIPCHK(hipEventRecord(s.ev, s.stream));
+  s.phase = 1;
+}
+
+void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
+  Slot& s = c->slot[si];
+  const DevGraph& g = c->g;
+  if (rc.algo == RGPU_ALGO_CC) {
+    const int32_t* lab = s.lab[s.r_final & 1];
+    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g, s.vm, lab, s.hist); });
+    timed_launch(c, si, KID_SUMMARY, 512.0 * g.nv,
+                 [&] { launch_cc_summary(s.stream, g, s.hist, s.stats); });
+  }
+  HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatWords,
+                        hipMemcpyDeviceToHost, s.stream));
+  if (rc.flags & RGPU_RUN_RETAIN) {
+    Retained& R = c->kept[s.batch];
+    const size_t rows = (size_t)g.nv * kViews;
+    R.vm.resize(g.nv);
+    HIPCHK(hipMemcpyAsync(R.vm.data(), s.vm, sizeof(uint64_t) * g.nv, hipMemcpyDeviceToHost, s.stream));
+    if (rc.algo == RGPU_ALGO_CC) {
+      R.a.resize(rows);
+      HIPCHK(hipMemcpyAsync(R.a.data(), s.lab[s.r_final & 1], sizeof(int32_t) * rows,
+                            hipMemcpyDeviceToHost, s.stream));
+    } else if (rc.algo == RGPU_ALGO_DEGREE) {
+      R.a.resize(rows);
+      R.b.resize(rows);
+      HIPCHK(hipMemcpyAsync(R.a.data(), s.outdeg, sizeof(int32_t) * rows, hipMemcpyDeviceToHost, s.stream));
+      HIPCHK(hipMemcpyAsync(R.b.data(), s.indeg, sizeof(int32_t) * rows, hipMemcpyDeviceToHost, s.stream));
+    } else {
+      R.pr.resize(rows);
+      HIPCHK(hipMemcpyAsync(R.pr.data(), s.pr, sizeof(double) * rows, hipMemcpyDeviceToHost, s.stream));
+    }
+  }
+  HIPCHK(hipEventRecord(s.ev, s.stream));
+  s.phase = 2;
+}
+
+void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
+  Slot& s = c->slot[si];
+  const DevGraph& g = c->g;
+  BatchParams bp;
+  std::memset(&bp, 0, sizeof(bp));
+  const size_t h0 = (size_t)b * rc.K;
+  bp.K = (int)std::min<size_t>(rc.K, rc.n_hops - h0);
+  bp.W = rc.W;
+  for (int k = 0; k < bp.K; k++) bp.hop[k] = rc.hops[h0 + k];
+  for (int w = 0; w < rc.W; w++) { bp.thr_v[w] = rc.thr_v[w]; bp.thr_e[w] = rc.thr_e[w]; }
+  s.batch = b;
+  s.kb = bp.K;
+  s.r_launched = 0;
+  s.r_final = 0;
+  HIPCHK(hipMemsetAsync(s.stats, 0, sizeof(unsigned long long) * kStatWords, s.stream));
+  HIPCHK(hipMemsetAsync(s.stepcnt, 0, sizeof(int32_t) * kMaxSteps, s.stream));
+  const double bm = bytes_mask(g);
+  timed_launch(c, si, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.vkey.size() + 8.0 * g.nv,
+               [&] { launch_vertex_mask(s.stream, g, bp, s.vm); });
+  timed_launch(c, si, KID_MASK, bm - (16.0 * g.nv + 8.0) + 8.0 * c->pk.ekey.size(),
+               [&] { launch_edge_mask(s.stream, g, bp, s.em); });
+  if (rc.algo == RGPU_ALGO_CC) {
+    // bytes: per vertex vm + 4 offsets + label row + cnt; per static slot index, em, vm[nb];
+    // alive slots written (the kernel reports members/alive; static part counted here)
+    const double b2 = g.nv * (8.0 + 32.0 + 256.0 + 4.0) + (double)(g.ne + g.n_in) * 24.0;
+    timed_launch(c, si, KID_SLOTS, b2, [&] {
+      launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.lab[0], s.stats + 6 * kViews);
+    });
+    if (rc.max_steps <= 1) {  // AnalysisTask.timeResponse :169: no Setup when maxSteps <= 1
+      s.r_final = 0;
+      finish_batch(c, si, rc);
+    } else {
+      launch_chunk(c, si, rc, rc.chunk0);
+    }
+  } else {
+    timed_launch(c, si, KID_DEGREE, g.nv * (8.0 + 32.0 + 512.0) + (double)(g.ne + g.n_in) * 12.0, [&] {
+      launch_degree(s.stream, g, s.vm, s.em, s.outdeg, s.indeg, s.stats);
+    });
+    if (rc.algo == RGPU_ALGO_PR) {
+      timed_launch(c, si, KID_SLOTS, g.nv * (8.0 + 24.0 + 256.0 + 1024.0) + (double)(g.n_in) * 24.0, [&] {
+        launch_pr_slots(s.stream, g, s.vm, s.em, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.pr, s.contrib[0]);
+      });
+      for (int it = 0; it < rc.pr_iters; it++) {
+        const double bp_bytes = g.nv * (8.0 + 16.0 + 4.0 + 256.0 + 1024.0) + (double)(g.n_in + g.nv) * 12.0;
+        timed_launch(c, si, KID_PR, bp_bytes, [&] {
+          launch_pr_step(s.stream, g, s.vm, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.contrib[it & 1],
+                         s.contrib[(it + 1) & 1], s.pr);
+        });
+      }
+    }
+    finish_batch(c, si, rc);
+  }
+}
+
+void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
+  Slot& s = c->slot[si];
+  const unsigned long long* h = s.h_stats;
+  for (int k = 0; k < s.kb; k++)
+    for (int w = 0; w < rc.W; w++) {
+      const int j = k * rc.W + w;
+      const size_t view = ((size_t)s.batch * rc.K + k) * rc.W + w;
+      if (rc.algo == RGPU_ALGO_CC) {
+        rgpu_cc_summary_t& o = c->cc[view];
+        o.biggest = (int64_t)h[0 * kViews + j];
+        o.total = (int64_t)h[1 * kViews + j];
+        o.total_without_islands = (int64_t)h[2 * kViews + j];
+        o.total_islands = o.total - o.total_without_islands;
+        o.clusters_gt2 = (int64_t)h[3 * kViews + j];
+        o.sum_all = (int64_t)h[4 * kViews + j];
+        o.sum_without_islands = (int64_t)h[5 * kViews + j];
+        o.supersteps = s.r_final;
+      } else if (rc.algo == RGPU_ALGO_DEGREE) {
+        for (int f = 0; f < 3; f++) c->deg[view * 3 + f] = (int64_t)h[f * kViews + j];
+      }
+    }
+  if (rc.algo == RGPU_ALGO_CC) {
+    // superstep bytes: every step reads vm of all vertices, and per member
+    // vertex 2 offsets + cnt + label row in/out + change word; per alive slot nbr + mask +
+    // the neighbour's change word.  Executed steps = r_final (later launches exit at once).
+    const double members = (double)h[6 * kViews + 0], alive = (double)h[6 * kViews + 1];
+    const double per_step = 8.0 * c->g.nv + members * (16.0 + 4.0 + 512.0 + 8.0) + alive * 20.0;
+    c->st.kernel_bytes[KID_STEP] += per_step * s.r_final;
+    c->st.supersteps += s.r_final;
+  }
+  s.phase = 0;
+  s.batch = -1;
+}
+
+int run_impl(rgpu_ctx* c, RunCfg& rc) {
+  const size_t nb = (rc.n_hops + rc.K - 1) / rc.K;
+  c->st.views += (int64_t)(rc.n_hops * rc.W);
+  c->st.batches += (int64_t)nb;
+  size_t next = 0;
+  int nslots = c->nslots;
+  for (;;) {
+    bool busy = false, progressed = false;
+    for (int si = 0; si < nslots; si++) {
+      Slot& s = c->slot[si];
+      if (s.phase == 0) {
+        if (next < nb) {
+          start_batch(c, si, (int)next++, rc);
+          progressed = true;
+          busy = true;
+        }
+        continue;
+      }
+      busy = true;
+      hipError_t q = hipEventQuery(s.ev);
+      if (q == hipErrorNotReady) continue;
+      HIPCHK(q);
+      progressed = true;
+      if (s.phase == 1) {
+        int r0 = 0;
+        for (int r = 1; r <= s.r_launched; r++)
+          if (s.h_stepcnt[r] == 0) { r0 = r; break; }
+        if (r0) { s.r_final = r0; finish_batch(c, si, rc); }
+        else if (s.r_launched >= rc.max_steps) { s.r_final = rc.max_steps; finish_batch(c, si, rc); }
+        else launch_chunk(c, si, rc, rc.chunk);
+      } else {
+        harvest(c, si, rc);
+        if (next < nb) start_batch(c, si, (int)next++, rc);
+      }
+    }
+    if (!busy) break;
+    if (!progressed) {
+      // nothing ready: block on the slot whose pending event is oldest (slot order is fine)
+      for (int si = 0; si < nslots; si++)
+        if (c->slot[si].phase != 0) { HIPCHK(hipEventSynchronize(c->slot[si].ev)); break; }
+    }
+  }
+  return 0;
+}
+
+int fail(rgpu_ctx* c, int code, const std::string& m) {
+  if (c) c->err = m;
+  return code;
+}
+
+int env_int(const char* k, int d) {
+  const char* v = std::getenv(k);
+  return v && *v ? std::atoi(v) : d;
+}
+
+}  // namespace
+
+// ======================================================================== C ABI
+extern "C" {
+
+int rgpu_abi_version(void) { return RGPU_ABI_VERSION; }
+
+int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) {
+  if (!out) return RGPU_EINVAL;
+  *out = nullptr;
+  if (num_partitions < 1 || partition_id < 0 || partition_id >= num_partitions || device < 0)
+    return RGPU_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return RGPU_EHIP;
+  rgpu_ctx* c = new (std::nothrow) rgpu_ctx();
+  if (!c) return RGPU_ENOMEM;
+  c->part = partition_id;
+  c->nparts = num_partitions;
+  c->device = device;
+  c->nslots = std::max(1, std::min(2, env_int("RGPU_SLOTS", 2)));
+  if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
+  *out = c;
+  return RGPU_OK;
+}
+
+int rgpu_ingest(rgpu_ctx* c, const int64_t* t, const uint8_t* kind, const int64_t* src,
+                const int64_t* dst, size_t n) {
+  if (!c) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (n && (!t || !kind || !src)) return fail(c, RGPU_EINVAL, "null input array");
+  try {
+    c->events.reserve(c->events.size() + n);
+    for (size_t i = 0; i < n; i++) {
+      if (kind[i] > RGPU_EDEL) return fail(c, RGPU_EINVAL, "unknown update kind");
+      if (kind[i] >= RGPU_EADD && !dst) return fail(c, RGPU_EINVAL, "edge update without dst array");
+      c->events.push_back({t[i], src[i], kind[i] >= RGPU_EADD ? dst[i] : -1, kind[i]});
+      c->newest = std::max(c->newest, t[i]);
+    }
+  } catch (const std::bad_alloc&) {
+    return fail(c, RGPU_ENOMEM, "host allocation failed");
+  }
+  c->sealed = false;
+  return RGPU_OK;
+}
+
+int rgpu_seal(rgpu_ctx* c) {
+  if (!c) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    std::string e = pack_events(c->events, c->part, c->nparts, &c->pk);
+    if (!e.empty()) return fail(c, c->nparts > 1 ? RGPU_ENOTSUP : RGPU_EINVAL, e);
+    free_graph(c);
+    const Packed& P = c->pk;
+    auto& L = c->graph_allocs;
+    DevGraph g;
+    g.nv = P.nv;
+    g.ne = P.ne;
+    g.n_in = P.in_off.empty() ? 0 : P.in_off.back();
+    g.voff = dupload(L, P.voff);
+    g.vkey = dupload(L, P.vkey);
+    g.doff = dupload(L, P.doff);
+    g.dtime = dupload(L, P.dtime);
+    g.esrc = dupload(L, P.esrc);
+    g.edst = dupload(L, P.edst);
+    g.eoff = dupload(L, P.eoff);
+    g.ekey = dupload(L, P.ekey);
+    g.out_off = dupload(L, P.out_off);
+    g.in_off = dupload(L, P.in_off);
+    g.in_eid = dupload(L, P.in_eid);
+    c->g = g;
+    HIPCHK(hipDeviceSynchronize());
+    c->st.vertices = P.nv;
+    c->st.edges = P.ne;
+    c->st.vertex_events = (int64_t)P.vkey.size();
+    c->st.edge_events = (int64_t)P.ekey.size();
+    c->st.deaths = (int64_t)P.dtime.size();
+    c->sealed = true;
+  } catch (const HipFail& f) {
+    return fail(c, RGPU_EHIP, f.msg);
+  } catch (const std::bad_alloc&) {
+    return fail(c, RGPU_ENOMEM, "host allocation failed");
+  }
+  return RGPU_OK;
+}
+
+int rgpu_newest_time(rgpu_ctx* c, int64_t* out) {
+  if (!c || !out) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  *out = c->newest;
+  return RGPU_OK;
+}
+
+int rgpu_exchange_init(rgpu_ctx* c, const void* id) {
+  (void)id;
+  if (!c) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return fail(c, RGPU_ENOTSUP, "vertex-partitioned RCCL exchange is not in this build");
+}
+
+int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hops,
+                        const int64_t* windows, size_t n_w, int max_steps, int pr_iters,
+                        int flags) {
+  if (!c) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->sealed) return fail(c, RGPU_ESTATE, "rgpu_run_view_batch before rgpu_seal");
+  if (algo < RGPU_ALGO_CC || algo > RGPU_ALGO_PR) return fail(c, RGPU_EINVAL, "unknown algo");
+  if (!hops || n_hops == 0) return fail(c, RGPU_EINVAL, "no hops");
+  if (n_w > (size_t)kViews) return fail(c, RGPU_EINVAL, "more than 64 windows in one batch");
+  if (n_w && !windows) return fail(c, RGPU_EINVAL, "null window array");
+  if (algo == RGPU_ALGO_CC && max_steps > kMaxSteps - 1)
+    return fail(c, RGPU_EINVAL, "max_steps above 127");
+  if (algo == RGPU_ALGO_PR && (pr_iters < 0 || pr_iters > 100000))
+    return fail(c, RGPU_EINVAL, "bad pr_iters");
+  for (size_t i = 0; i < n_hops; i++)
+    if (hops[i] < 0 || hops[i] >= ((int64_t)1 << 61)) return fail(c, RGPU_EINVAL, "hop time out of range");
+  RunCfg rc;
+  rc.algo = algo;
+  rc.max_steps = max_steps;
+  rc.pr_iters = pr_iters;
+  rc.flags = flags;
+  rc.W = n_w ? (int)n_w : 1;
+  rc.K = kViews / rc.W;
+  rc.hops = hops;
+  rc.n_hops = n_hops;
+  int64_t run_min = INT64_MAX;
+  for (int w = 0; w < rc.W; w++) {
+    int64_t wv = n_w ? windows[w] : INT64_MAX;  // ViewLens = no window (aliveAt)
+    if (wv < 0) return fail(c, RGPU_EINVAL, "negative window");
+    for (int u = 0; u < w; u++)
+      if (n_w && windows[u] == wv)
+        return fail(c, RGPU_EINVAL,
+                    "duplicate window in batch (the reference shares state between them, "
+                    "VertexVisitor.scala:81-96; not supported)");
+    run_min = std::min(run_min, wv);
+    rc.thr_e[w] = wv;
+    rc.thr_v[w] = run_min;  // WindowLens.shrinkWindow keeps the running intersection
+  }
+  rc.chunk0 = std::max(1, env_int("RGPU_CHUNK0", 12));
+  rc.chunk = std::max(1, env_int("RGPU_CHUNK", 8));
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    ensure_slots(c, algo);
+    const size_t nb = (n_hops + rc.K - 1) / rc.K;
+    c->algo = algo;
+    c->K = rc.K;
+    c->W = rc.W;
+    c->n_hops = n_hops;
+    c->cc.assign(algo == RGPU_ALGO_CC ? n_hops * rc.W : 0, rgpu_cc_summary_t{});
+    c->deg.assign(algo == RGPU_ALGO_DEGREE ? n_hops * rc.W * 3 : 0, 0);
+    c->kept.clear();
+    c->retained = (flags & RGPU_RUN_RETAIN) != 0;
+    if (c->retained) c->kept.resize(nb);
+    c->profile = (flags & RGPU_RUN_PROFILE) != 0;
+    c->evused = 0;
+    c->timed.clear();
+    for (int k = 0; k < KID_N; k++) { c->st.kernel_launches[k] = 0; c->st.kernel_ms[k] = 0; c->st.kernel_bytes[k] = 0; }
+    c->st.views = c->st.batches = c->st.supersteps = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    run_impl(c, rc);
+    for (int si = 0; si < 2; si++)
+      if (c->slot[si].stream) HIPCHK(hipStreamSynchronize(c->slot[si].stream));
+    auto t1 = std::chrono::steady_clock::now();
+    c->st.ms_total = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    c->st.launches = 0;
+    for (int k = 0; k < KID_N; k++) c->st.launches += c->st.kernel_launches[k];
+    for (const Timed& tm : c->timed) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, tm.a, tm.b));
+      c->st.kernel_ms[tm.kid] += ms;
+    }
+  } catch (const HipFail& f) {
+    return fail(c, RGPU_EHIP, f.msg);
+  } catch (const std::bad_alloc&) {
+    return fail(c, RGPU_ENOMEM, "host allocation failed");
+  }
+  return RGPU_OK;
+}
+
+static int view_index(rgpu_ctx* c, size_t hop, size_t win, size_t* batch, int* lane) {
+  if (hop >= c->n_hops || win >= (size_t)c->W) return fail(c, RGPU_EINVAL, "view index out of range");
+  *batch = hop / c->K;
+  *lane = (int)((hop % c->K) * c->W + win);
+  return RGPU_OK;
+}
+
+int rgpu_cc_summary(rgpu_ctx* c, size_t hop, size_t win, rgpu_cc_summary_t* out) {
+  if (!c || !out) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_CC) return fail(c, RGPU_ESTATE, "last run was not CC");
+  size_t b;
+  int j;
+  if (int e = view_index(c, hop, win, &b, &j)) return e;
+  *out = c->cc[hop * c->W + win];
+  return RGPU_OK;
+}
+
+int rgpu_cc_vertex_labels(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int64_t* labels,
+                          size_t cap, size_t* n) {
+  if (!c || !n) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_CC || !c->retained) return fail(c, RGPU_ESTATE, "needs a CC run with RGPU_RUN_RETAIN");
+  size_t b;
+  int j;
+  if (int e = view_index(c, hop, win, &b, &j)) return e;
+  const Retained& R = c->kept[b];
+  size_t k = 0;
+  for (int64_t v = 0; v < c->pk.nv; v++) {
+    if (!((R.vm[v] >> j) & 1)) continue;
+    if (k < cap) {
+      ids[k] = c->pk.vid[v];
+      labels[k] = c->pk.vid[R.a[(size_t)v * kViews + j]];
+    }
+    k++;
+  }
+  *n = k;
+  return RGPU_OK;
+}
+
+int rgpu_cc_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* labels, int32_t* counts,
+                   size_t cap, size_t* n) {
+  if (!c || !n) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_CC || !c->retained) return fail(c, RGPU_ESTATE, "needs a CC run with RGPU_RUN_RETAIN");
+  size_t b;
+  int j;
+  if (int e = view_index(c, hop, win, &b, &j)) return e;
+  const Retained& R = c->kept[b];
+  std::vector<int32_t> lab;
+  for (int64_t v = 0; v < c->pk.nv; v++)
+    if ((R.vm[v] >> j) & 1) lab.push_back(R.a[(size_t)v * kViews + j]);
+  std::sort(lab.begin(), lab.end());
+  size_t k = 0;
+  for (size_t i = 0; i < lab.size();) {
+    size_t h = i;
+    while (h < lab.size() && lab[h] == lab[i]) h++;
+    if (k < cap) { labels[k] = c->pk.vid[lab[i]]; counts[k] = (int32_t)(h - i); }
+    k++;
+    i = h;
+  }
+  *n = k;
+  return RGPU_OK;
+}
+
+int rgpu_degree_vertex(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int32_t* outdeg,
+                       int32_t* indeg, size_t cap, size_t* n) {
+  if (!c || !n) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_DEGREE || !c->retained) return fail(c, RGPU_ESTATE, "needs a degree run with RGPU_RUN_RETAIN");
+  size_t b;
+  int j;
+  if (int e = view_index(c, hop, win, &b, &j)) return e;
+  const Retained& R = c->kept[b];
+  size_t k = 0;
+  for (int64_t v = 0; v < c->pk.nv; v++) {
+    if (!((R.vm[v] >> j) & 1)) continue;
+    if (k < cap) {
+      ids[k] = c->pk.vid[v];
+      outdeg[k] = R.a[(size_t)v * kViews + j];
+      indeg[k] = R.b[(size_t)v * kViews + j];
+    }
+    k++;
+  }
+  *n = k;
+  return RGPU_OK;
+}
+
+int rgpu_degree_result(rgpu_ctx* c, size_t hop, size_t win, int64_t tot[3], int64_t* top_id,
+                       int32_t* top_out, int32_t* top_in) {
+  if (!c || !tot) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_DEGREE) return fail(c, RGPU_ESTATE, "last run was not degree");
+  size_t b;
+  int j;
+  if (int e = view_index(c, hop, win, &b, &j)) return e;
+  for (int f = 0; f < 3; f++) tot[f] = c->deg[(hop * c->W + win) * 3 + f];
+  if (top_id && top_out && top_in) {
+    for (int i = 0; i < 20; i++) { top_id[i] = -1; top_out[i] = 0; top_in[i] = 0; }
+    if (c->retained) {
+      const Retained& R = c->kept[b];
+      std::vector<int64_t> vs;
+      for (int64_t v = 0; v < c->pk.nv; v++)
+        if ((R.vm[v] >> j) & 1) vs.push_back(v);
+      // DegreeBasic sorts by in-degree descending (:26); ParTrieMap tie order is not
+      // deterministic, ties here go by ascending id
+      auto key = [&](int64_t v) { return R.b[(size_t)v * kViews + j]; };
+      size_t m = std::min<size_t>(20, vs.size());
+      std::partial_sort(vs.begin(), vs.begin() + m, vs.end(), [&](int64_t x, int64_t y) {
+        return key(x) != key(y) ? key(x) > key(y) : x < y;
+      });
+      for (size_t i = 0; i < m; i++) {
+        top_id[i] = c->pk.vid[vs[i]];
+        top_out[i] = R.a[(size_t)vs[i] * kViews + j];
+        top_in[i] = R.b[(size_t)vs[i] * kViews + j];
+      }
+    }
+  }
+  return RGPU_OK;
+}
+
+int rgpu_pr_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, double* pr, size_t cap,
+                   size_t* n) {
+  if (!c || !n) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_PR || !c->retained) return fail(c, RGPU_ESTATE, "needs a PR run with RGPU_RUN_RETAIN");
+  size_t b;
+  int j;
+  if (int e = view_index(c, hop, win, &b, &j)) return e;
+  const Retained& R = c->kept[b];
+  size_t k = 0;
+  for (int64_t v = 0; v < c->pk.nv; v++) {
+    if (!((R.vm[v] >> j) & 1)) continue;
+    if (k < cap) { ids[k] = c->pk.vid[v]; pr[k] = R.pr[(size_t)v * kViews + j]; }
+    k++;
+  }
+  *n = k;
+  return RGPU_OK;
+}
+
+int rgpu_stats(rgpu_ctx* c, rgpu_stats_t* out) {
+  if (!c || !out) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  *out = c->st;
+  return RGPU_OK;
+}
+
+const char* rgpu_last_error(rgpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void rgpu_close(rgpu_ctx* c) {
+  if (!c) return;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    (void)hipSetDevice(c->device);
+    for (Slot& s : c->slot)
+      if (s.stream) (void)hipStreamSynchronize(s.stream);
+    free_graph(c);
+    for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
+  }
+  delete c;
+}
+
+}  // extern "C"

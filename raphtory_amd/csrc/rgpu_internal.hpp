@@ -1,0 +1,38 @@
+// rgpu_internal.hpp — shared declarations of librgpu (host packer + HIP kernels + C ABI).
+#pragma once
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rgpu.h"
+
+namespace rgpu {
+
+// Packed, sealed graph of one partition.  All arrays are SoA.
+// History keys are  key = t*2 + alive  so that one int64 compare orders (time, flag)
+// and `key <= 2*t+1` finds floor(t) (Entity.closestTime, Entity.scala:173-183).
+struct Packed {
+  int64_t nv = 0, ne = 0;
+  std::vector<int64_t> vid;          // [nv] vertex ids, ascending; rank = index
+  std::vector<int64_t> voff, vkey;   // vertex histories: [nv+1], [voff[nv]]
+  std::vector<int64_t> doff, dtime;  // vertex death times (VertexDelete), ascending, distinct
+  std::vector<int32_t> esrc, edst;   // [ne] edge endpoints (ranks), sorted by (src, dst)
+  std::vector<int64_t> eoff, ekey;   // edge own histories, ties vs endpoint deaths pre-resolved
+  std::vector<int64_t> out_off;      // [nv+1] out-edges of rank v are edges [out_off[v], out_off[v+1])
+  std::vector<int64_t> in_off;       // [nv+1] in-edges (no self-loops), ordered by (dst, src)
+  std::vector<int32_t> in_eid;       // [in_off[nv]] edge ids of in-edges
+  int64_t newest = -1;
+};
+
+struct Event {
+  int64_t t;
+  int64_t src, dst;
+  uint8_t kind;
+};
+
+// Host packer (packer.cpp).  Returns empty string or an error message.
+std::string pack_events(const std::vector<Event>& ev, int partition, int num_partitions,
+                        Packed* out);
+
+}  // namespace rgpu

@@ -1,0 +1,159 @@
+"""TemporalGraph — one partition's GPU-resident temporal graph behind the C ABI (include/rgpu.h).
+
+This is the host object a GpuReaderWorker would hold (one per Partition Manager / GPU):
+ingest the update stream, seal it into HBM, then answer whole Range jobs per call.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+
+
+class RGPUError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{N.ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+ALGOS = {"cc": N.RGPU_ALGO_CC, "degree": N.RGPU_ALGO_DEGREE, "pagerank": N.RGPU_ALGO_PR}
+
+
+def _i64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int64))
+
+
+class TemporalGraph:
+    def __init__(self, partition: int = 0, num_partitions: int = 1, device: int = 0):
+        self._lib = N.rgpu()
+        ctx = C.c_void_p()
+        rc = self._lib.rgpu_open(partition, num_partitions, device, C.byref(ctx))
+        if rc != 0:
+            raise RGPUError(rc, f"rgpu_open(partition={partition}, num_partitions={num_partitions}, "
+                                f"device={device}) failed")
+        self._ctx = ctx
+        self._hops: Optional[np.ndarray] = None
+        self._windows: List[int] = []
+
+    # ------------------------------------------------------------------ plumbing
+    def _check(self, rc: int) -> None:
+        if rc != 0:
+            raise RGPUError(rc, (self._lib.rgpu_last_error(self._ctx) or b"").decode())
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.rgpu_close(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ ingest
+    def ingest(self, t, kind, src, dst) -> None:
+        t, src, dst = _i64(t), _i64(src), _i64(dst)
+        kind = np.ascontiguousarray(np.asarray(kind, dtype=np.uint8))
+        n = t.shape[0]
+        if not (kind.shape[0] == src.shape[0] == dst.shape[0] == n):
+            raise ValueError("ingest arrays must have equal length")
+        self._check(self._lib.rgpu_ingest(self._ctx, N.ptr(t, C.c_int64), N.ptr(kind, C.c_uint8),
+                                          N.ptr(src, C.c_int64), N.ptr(dst, C.c_int64), n))
+
+    def ingest_stream(self, s) -> None:
+        self.ingest(s.t, s.kind, s.src, s.dst)
+
+    def seal(self) -> None:
+        self._check(self._lib.rgpu_seal(self._ctx))
+
+    def newest_time(self) -> int:
+        out = C.c_int64()
+        self._check(self._lib.rgpu_newest_time(self._ctx, C.byref(out)))
+        return out.value
+
+    # ------------------------------------------------------------------ run
+    def run(self, algo: str, hops: Sequence[int], windows: Sequence[int] = (), max_steps: int = 100,
+            pr_iters: int = 20, retain: bool = False, profile: bool = False) -> None:
+        hops = _i64(hops)
+        w = _i64(list(windows))
+        flags = (N.RGPU_RUN_RETAIN if retain else 0) | (N.RGPU_RUN_PROFILE if profile else 0)
+        wptr = N.ptr(w, C.c_int64) if w.shape[0] else None
+        self._check(self._lib.rgpu_run_view_batch(self._ctx, ALGOS[algo], N.ptr(hops, C.c_int64), hops.shape[0],
+                                                  wptr, w.shape[0], max_steps, pr_iters, flags))
+        self._hops = hops
+        self._windows = list(w)
+
+    @property
+    def n_windows(self) -> int:
+        return max(1, len(self._windows))
+
+    def cc_summary(self, hop: int, win: int) -> N.CCSummary:
+        out = N.CCSummary()
+        self._check(self._lib.rgpu_cc_summary(self._ctx, hop, win, C.byref(out)))
+        return out
+
+    def cc_summaries(self) -> np.ndarray:
+        """[n_hops, n_windows, 8] int64: the CCSummary fields of every view."""
+        nh, nw = len(self._hops), self.n_windows
+        out = np.zeros((nh, nw, 8), np.int64)
+        s = N.CCSummary()
+        for h in range(nh):
+            for w in range(nw):
+                self._check(self._lib.rgpu_cc_summary(self._ctx, h, w, C.byref(s)))
+                out[h, w] = [getattr(s, f) for f, _ in N.CCSummary._fields_]
+        return out
+
+    def _sized(self, fn, hop, win, arrays_factory):
+        n = C.c_size_t()
+        self._check(fn(self._ctx, hop, win, *[None for _ in range(arrays_factory(0)[1])], 0, C.byref(n)))
+        arrs, _ = arrays_factory(n.value)
+        ptrs = [N.ptr(a, t) for a, t in arrs]
+        self._check(fn(self._ctx, hop, win, *ptrs, n.value, C.byref(n)))
+        return [a for a, _ in arrs]
+
+    def cc_vertex_labels(self, hop: int, win: int) -> Tuple[np.ndarray, np.ndarray]:
+        ids, labels = self._sized(self._lib.rgpu_cc_vertex_labels, hop, win,
+                                  lambda n: ([(np.empty(n, np.int64), C.c_int64), (np.empty(n, np.int64), C.c_int64)], 2))
+        return ids, labels
+
+    def cc_result(self, hop: int, win: int) -> Dict[int, int]:
+        labels, counts = self._sized(self._lib.rgpu_cc_result, hop, win,
+                                     lambda n: ([(np.empty(n, np.int64), C.c_int64), (np.empty(n, np.int32), C.c_int32)], 2))
+        return {int(l): int(c) for l, c in zip(labels, counts)}
+
+    def degree_vertex(self, hop: int, win: int):
+        return self._sized(self._lib.rgpu_degree_vertex, hop, win,
+                           lambda n: ([(np.empty(n, np.int64), C.c_int64), (np.empty(n, np.int32), C.c_int32),
+                                       (np.empty(n, np.int32), C.c_int32)], 3))
+
+    def degree_result(self, hop: int, win: int):
+        tot = np.zeros(3, np.int64)
+        ids = np.zeros(20, np.int64)
+        od = np.zeros(20, np.int32)
+        idg = np.zeros(20, np.int32)
+        self._check(self._lib.rgpu_degree_result(self._ctx, hop, win, N.ptr(tot, C.c_int64), N.ptr(ids, C.c_int64),
+                                                 N.ptr(od, C.c_int32), N.ptr(idg, C.c_int32)))
+        top = [(int(i), int(o), int(d)) for i, o, d in zip(ids, od, idg) if i >= 0]
+        return (int(tot[0]), int(tot[1]), int(tot[2]), top)
+
+    def pr_result(self, hop: int, win: int):
+        return self._sized(self._lib.rgpu_pr_result, hop, win,
+                           lambda n: ([(np.empty(n, np.int64), C.c_int64), (np.empty(n, np.float64), C.c_double)], 2))
+
+    def stats(self) -> dict:
+        s = N.Stats()
+        self._check(self._lib.rgpu_stats(self._ctx, C.byref(s)))
+        d = {f: getattr(s, f) for f, _ in N.Stats._fields_ if f not in ("kernel_launches", "kernel_ms", "kernel_bytes")}
+        d["kernels"] = {N.KERNEL_NAMES[i]: {"launches": s.kernel_launches[i], "ms": s.kernel_ms[i],
+                                            "bytes": s.kernel_bytes[i]} for i in range(7)}
+        return d
