@@ -15,6 +15,7 @@
 //   k_pr_slots/k_pr_step  PageRank spec
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdint>
 
 #include "kernels.hpp"
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
   }
 }
 
-// ---------------------------------------------------------------- K2: batch CSR
+// ---------------------------------------------------------------- K2: batch CSR (+ superstep 1)
 // One wave per vertex.  Static slots of rank v = its out-edges then its in-edges
 // (adjacency offset out_off[v] + in_off[v]).  Slot kept iff its view mask
 //   em[e] & vm[nbr] & vm[v]  != 0
@@ -113,7 +114,16 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
 // (running-min) vertex set — messages to vertices outside the lens are never read
 // (WindowLens.getVerticesWithMessages, WindowLens.scala:149-158).  Self-loops only
 // message the vertex itself and never change a label: dropped.
-// Also writes the initial label row (label = own rank, ConnectedComponents.setup :10-17).
+//
+// Setup (ConnectedComponents.setup :10-17) sends every member's own id, so superstep 1 needs
+// no gather: label_1(v) = min(own rank, ranks of kept neighbours) per view.  This kernel
+// writes label_0 (= rank) and label_1 rows, the step-1 change words, the step-2 frontier
+// bitmap and stepcnt[1]; vadj[v] = OR of v's kept slot masks (v isolated in view j iff bit j
+// is clear).
+__device__ __forceinline__ void mark(uint32_t* act, int32_t x) {
+  atomicOr(&act[x >> 5], 1u << (x & 31));
+}
+
 __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __restrict__ out_off,
                                                   const int64_t* __restrict__ in_off,
                                                   const int32_t* __restrict__ in_eid,
@@ -123,25 +133,30 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
                                                   const uint64_t* __restrict__ em,
                                                   int32_t* __restrict__ cnt, int32_t* __restrict__ snbr,
                                                   uint64_t* __restrict__ smask,
-                                                  int32_t* __restrict__ lab0,
+                                                  uint64_t* __restrict__ vadj,
+                                                  int32_t* __restrict__ lab0, int32_t* __restrict__ lab1,
+                                                  uint64_t* __restrict__ chg1, uint32_t* __restrict__ act2,
+                                                  int32_t* __restrict__ stepcnt,
                                                   unsigned long long* __restrict__ counters) {
-  __shared__ unsigned long long red[2];
-  if (threadIdx.x < 2) red[threadIdx.x] = 0;
+  __shared__ unsigned long long red[3];
+  if (threadIdx.x < 3) red[threadIdx.x] = 0;
   __syncthreads();
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  unsigned long long members = 0, alive = 0;
+  unsigned long long members = 0, alive = 0, changed = 0;
   for (int64_t v = wave; v < nv; v += nwaves) {
-    lab0[v * 64 + lane] = (int32_t)v;
     const uint64_t mv = vm[v];
+    const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
+    lab0[v * 64 + lane] = (int32_t)v;
     if (mv == 0) {
-      if (lane == 0) cnt[v] = 0;
+      lab1[v * 64 + lane] = (int32_t)v;
+      if (lane == 0) { cnt[v] = 0; vadj[v] = 0; }
       continue;
     }
-    const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
     const int64_t nout = o1 - o0, ntot = nout + (i1 - i0), base = o0 + i0;
-    int32_t count = 0;
+    int32_t count = 0, best = (int32_t)v;
+    uint64_t any = 0;
     for (int64_t c = 0; c < ntot; c += 64) {
       const int64_t j = c + lane;
       uint64_t m = 0;
@@ -152,26 +167,46 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
         else { e = in_eid[i0 + (j - nout)]; nb = esrc[e]; }
         if (nb != (int32_t)v) m = em[e] & vm[nb] & mv;
       }
-      const uint64_t bal = __ballot(m != 0);
+      uint64_t bal = __ballot(m != 0);
       if (m) {
         const int64_t pos = base + count + __popcll(bal & lanemask_lt());
         snbr[pos] = nb;
         smask[pos] = m;
       }
       count += __popcll(bal);
+      while (bal) {  // superstep 1: neighbours' labels are their ranks
+        const int L = __builtin_ctzll(bal);
+        bal &= bal - 1;
+        const int32_t q = __builtin_amdgcn_readlane(nb, L);
+        const uint64_t mL = readlane64(m, L);
+        any |= mL;
+        if (((mL >> lane) & 1) && q < best) best = q;
+      }
     }
-    if (lane == 0) cnt[v] = count;
+    lab1[v * 64 + lane] = best;
+    const uint64_t ch = __ballot(best < (int32_t)v);
+    if (lane == 0) { cnt[v] = count; vadj[v] = any; chg1[v] = ch; }
+    if (ch) {
+      changed++;
+      if (lane == 0) mark(act2, (int32_t)v);
+      for (int32_t c = 0; c < count; c += 64) {
+        const int32_t j = c + lane;
+        if (j < count && (smask[base + j] & ch)) mark(act2, snbr[base + j]);
+      }
+    }
     members += 1;
     alive += (unsigned long long)count;
   }
   if (lane == 0) {
     atomicAdd(&red[0], members);
     atomicAdd(&red[1], alive);
+    atomicAdd(&red[2], changed);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     atomicAdd(&counters[0], red[0]);
     atomicAdd(&counters[1], red[1]);
+    if (red[2]) atomicAdd(&stepcnt[1], (int32_t)red[2]);
   }
 }
 
@@ -181,8 +216,52 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
 // (only those sent messages: ConnectedComponents.analyse :19-35, VertexMutliQueue parity
 // queues).  step 1 consumes the setup messages (every member "changed").  A step with no
 // improvement anywhere ends the job (AnalysisTask.endStep :208-225): later launches exit.
-__global__ __launch_bounds__(256) void k_cc_step(int step, int64_t nv, const int64_t* __restrict__ out_off,
-                                                 const int64_t* __restrict__ in_off,
+//
+// Frontier: step r only visits vertices set in the bitmap act_cur, which step r-1 filled
+// with every vertex that changed (so both label buffers catch up) and every neighbour that
+// shares a view with the change.  Bitmaps rotate over three buffers; each step zeroes the
+// one it will not touch (read two steps ago, written next step).
+constexpr int kChunk = 8;  // vertices per wave visit (8-aligned -> inside one bitmap word)
+
+// Gather the label rows of the neighbours flagged in `act` (lane = slot) and fold them into
+// `best` (lane = view); four independent loads in flight per round.
+__device__ __forceinline__ int32_t gather_min(uint64_t act, int32_t nb, int32_t best,
+                                              const int32_t* __restrict__ lab_cur, int lane) {
+  uint64_t bal = __ballot(act != 0);
+  while (bal) {
+    int32_t x0 = INT32_MAX, x1 = INT32_MAX, x2 = INT32_MAX, x3 = INT32_MAX;
+    int L = __builtin_ctzll(bal);
+    bal &= bal - 1;
+    int32_t q = __builtin_amdgcn_readlane(nb, L);
+    if ((readlane64(act, L) >> lane) & 1) x0 = lab_cur[(int64_t)q * 64 + lane];
+    if (bal) {
+      L = __builtin_ctzll(bal);
+      bal &= bal - 1;
+      q = __builtin_amdgcn_readlane(nb, L);
+      if ((readlane64(act, L) >> lane) & 1) x1 = lab_cur[(int64_t)q * 64 + lane];
+    }
+    if (bal) {
+      L = __builtin_ctzll(bal);
+      bal &= bal - 1;
+      q = __builtin_amdgcn_readlane(nb, L);
+      if ((readlane64(act, L) >> lane) & 1) x2 = lab_cur[(int64_t)q * 64 + lane];
+    }
+    if (bal) {
+      L = __builtin_ctzll(bal);
+      bal &= bal - 1;
+      q = __builtin_amdgcn_readlane(nb, L);
+      if ((readlane64(act, L) >> lane) & 1) x3 = lab_cur[(int64_t)q * 64 + lane];
+    }
+    best = min(best, min(min(x0, x1), min(x2, x3)));
+  }
+  return best;
+}
+
+// A wave visits the frontier vertices of one 8-vertex chunk.  Loads are issued per stage
+// for all of the chunk's vertices before anything waits on them (metadata and own label
+// rows, then the first 64 kept slots of each, then the neighbours' change words), so a
+// chunk costs ~4 dependent memory round trips plus the label gathers, not ~5 per vertex.
+__global__ __launch_bounds__(256) void k_cc_step(int step, int64_t nv, const int64_t* __restrict__ adj_off,
                                                  const uint64_t* __restrict__ vm,
                                                  const int32_t* __restrict__ cnt,
                                                  const int32_t* __restrict__ snbr,
@@ -191,63 +270,151 @@ __global__ __launch_bounds__(256) void k_cc_step(int step, int64_t nv, const int
                                                  int32_t* __restrict__ lab_next,
                                                  const uint64_t* __restrict__ chg_prev,
                                                  uint64_t* __restrict__ chg_next,
-                                                 int32_t* __restrict__ stepcnt) {
-  if (step > 1 && stepcnt[step - 1] == 0) return;
+                                                 const uint32_t* __restrict__ act_cur,
+                                                 uint32_t* __restrict__ act_next,
+                                                 uint32_t* __restrict__ act_clear,
+                                                 int32_t* __restrict__ stepcnt,
+                                                 unsigned long long* __restrict__ work) {
+  if (stepcnt[step - 1] == 0) return;
   __shared__ int32_t red;
-  if (threadIdx.x == 0) red = 0;
+  __shared__ unsigned long long wred[2];
+  if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; }
+  const int64_t nwords = (nv + 31) >> 5;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
+       i += (int64_t)gridDim.x * blockDim.x)
+    act_clear[i] = 0;
   __syncthreads();
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int32_t changed = 0;
-  for (int64_t v = wave; v < nv; v += nwaves) {
-    const uint64_t mv = vm[v];
-    if (mv == 0) continue;
-    const int32_t cur = lab_cur[v * 64 + lane];
-    int32_t best = cur;
-    const int32_t n = cnt[v];
-    const int64_t base = out_off[v] + in_off[v];
-    for (int32_t c = 0; c < n; c += 64) {
-      const int32_t j = c + lane;
-      uint64_t act = 0;
-      int32_t nb = 0;
-      if (j < n) {
-        nb = snbr[base + j];
-        act = smask[base + j] & chg_prev[nb];
+  unsigned long long pv = 0, ps = 0;
+  for (int64_t c = wave; c * kChunk < nv; c += nwaves) {
+    const int64_t v0 = c * kChunk;
+    uint32_t bits = (act_cur[v0 >> 5] >> (v0 & 31)) & 0xffu;
+    if (v0 + kChunk > nv) bits &= (1u << (nv - v0)) - 1;
+    if (!bits) continue;
+    // stage 1: metadata (lane i < 8 -> vertex v0+i) and own label rows
+    const bool okl = lane < kChunk && ((bits >> lane) & 1);
+    const uint64_t mv_l = okl ? vm[v0 + lane] : 0;
+    const int32_t n_l = okl ? cnt[v0 + lane] : 0;
+    const int64_t b_l = okl ? adj_off[v0 + lane] : 0;
+    int32_t cur[kChunk];
+#pragma unroll
+    for (int i = 0; i < kChunk; i++) cur[i] = ((bits >> i) & 1) ? lab_cur[(v0 + i) * 64 + lane] : 0;
+    // stage 2: first 64 kept slots of every vertex
+    int32_t nb[kChunk];
+    uint64_t sm[kChunk];
+#pragma unroll
+    for (int i = 0; i < kChunk; i++) {
+      const int32_t n = __builtin_amdgcn_readlane(n_l, i);
+      const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
+      nb[i] = 0;
+      sm[i] = 0;
+      if (lane < n) { nb[i] = snbr[base + lane]; sm[i] = smask[base + lane]; }
+    }
+    // stage 3: which of those neighbours changed in the previous step, in which views
+    uint64_t act[kChunk];
+#pragma unroll
+    for (int i = 0; i < kChunk; i++) act[i] = sm[i] ? (sm[i] & chg_prev[nb[i]]) : 0;
+    // stage 4: per vertex, gather + min + publish
+#pragma unroll
+    for (int i = 0; i < kChunk; i++) {
+      if (!((bits >> i) & 1)) continue;
+      const uint64_t mv = readlane64(mv_l, i);
+      if (mv == 0) continue;
+      const int64_t v = v0 + i;
+      const int32_t n = __builtin_amdgcn_readlane(n_l, i);
+      const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
+      pv += 1;
+      ps += (unsigned long long)n;
+      int32_t best = gather_min(act[i], nb[i], cur[i], lab_cur, lane);
+      for (int32_t c2 = 64; c2 < n; c2 += 64) {  // vertices with more than 64 kept slots
+        const int32_t j = c2 + lane;
+        uint64_t a2 = 0;
+        int32_t q = 0;
+        if (j < n) {
+          q = snbr[base + j];
+          a2 = smask[base + j] & chg_prev[q];
+        }
+        best = gather_min(a2, q, best, lab_cur, lane);
       }
-      uint64_t bal = __ballot(act != 0);
-      while (bal) {
-        const int L = __builtin_ctzll(bal);
-        bal &= bal - 1;
-        const int32_t nbL = __builtin_amdgcn_readlane(nb, L);
-        const uint64_t aL = readlane64(act, L);
-        if ((aL >> lane) & 1) {
-          const int32_t x = lab_cur[(int64_t)nbL * 64 + lane];
-          best = x < best ? x : best;
+      lab_next[v * 64 + lane] = best;
+      const uint64_t ch = __ballot(best < cur[i]);
+      if (lane == 0) chg_next[v] = ch;
+      if (ch) {
+        changed++;
+        if (lane == 0) mark(act_next, (int32_t)v);
+        if (sm[i] & ch) mark(act_next, nb[i]);
+        for (int32_t c2 = 64; c2 < n; c2 += 64) {
+          const int32_t j = c2 + lane;
+          if (j < n && (smask[base + j] & ch)) mark(act_next, snbr[base + j]);
         }
       }
     }
-    lab_next[v * 64 + lane] = best;
-    const uint64_t ch = __ballot(best < cur);
-    if (lane == 0) chg_next[v] = ch;
-    changed += ch != 0;
   }
-  if (lane == 0 && changed) atomicAdd(&red, changed);
+  if (lane == 0) {
+    if (changed) atomicAdd(&red, changed);
+    atomicAdd(&wred[0], pv);
+    atomicAdd(&wred[1], ps);
+  }
   __syncthreads();
-  if (threadIdx.x == 0 && red) atomicAdd(&stepcnt[step], red);
+  if (threadIdx.x == 0) {
+    if (red) atomicAdd(&stepcnt[step], red);
+    atomicAdd(&work[2 * step], wred[0]);
+    atomicAdd(&work[2 * step + 1], wred[1]);
+  }
 }
 
 // ---------------------------------------------------------------- K5: CC reductions
-// label -> count histogram (ConnectedComponents.returnResults :37-42, groupBy over labels)
-__global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, const uint64_t* __restrict__ vm,
+// label -> count histogram (ConnectedComponents.returnResults :37-42, groupBy over labels).
+// A wave stages the label rows of 64 consecutive vertices in LDS, then per view puts the 64
+// vertices on the lanes and adds each distinct label once per wave (popcount of the lanes
+// that carry it): the giant component costs one atomic per 64 vertices, not one per vertex.
+// Members with no kept slot in a view are isolated there: islands (count 1) that need no
+// histogram entry; they are added to total / sum / biggest directly.
+__global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int nviews, const uint64_t* __restrict__ vm,
+                                                 const uint64_t* __restrict__ vadj,
                                                  const int32_t* __restrict__ lab,
-                                                 int32_t* __restrict__ hist) {
-  const int lane = lane_id();
+                                                 int32_t* __restrict__ hist,
+                                                 unsigned long long* __restrict__ stats) {
+  __shared__ int32_t tile[4][64][65];
+  __shared__ unsigned int iso[64];
+  if (threadIdx.x < 64) iso[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = lane_id(), wib = threadIdx.x >> 6;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t v = wave; v < nv; v += nwaves) {
-    const uint64_t mv = vm[v];
-    if ((mv >> lane) & 1) atomicAdd(&hist[(int64_t)lab[v * 64 + lane] * 64 + lane], 1);
+  for (int64_t c = wave; c * 64 < nv; c += nwaves) {
+    const int64_t v0 = c * 64;
+    const int nvc = (int)(nv - v0 < 64 ? nv - v0 : 64);
+    for (int i = 0; i < nvc; i++) tile[wib][i][lane] = lab[(v0 + i) * 64 + lane];
+    const uint64_t mvl = lane < nvc ? vm[v0 + lane] : 0;
+    const uint64_t adl = lane < nvc ? vadj[v0 + lane] : 0;
+    __builtin_amdgcn_wave_barrier();
+    for (int j = 0; j < nviews; j++) {
+      const bool in_view = (mvl >> j) & 1;
+      const bool member = in_view && ((adl >> j) & 1);
+      const uint64_t isolated = __ballot(in_view && !member);
+      if (lane == 0 && isolated) atomicAdd(&iso[j], (unsigned)__popcll(isolated));
+      const int32_t l = tile[wib][lane][j];
+      uint64_t todo = __ballot(member);
+      while (todo) {
+        const int leader = __builtin_ctzll(todo);
+        const int32_t L = __builtin_amdgcn_readlane(l, leader);
+        const uint64_t same = __ballot(member && l == L);
+        if (lane == leader) atomicAdd(&hist[(int64_t)L * 64 + j], __popcll(same));
+        todo &= ~same;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if (threadIdx.x < 64 && iso[threadIdx.x]) {
+    const unsigned long long k = iso[threadIdx.x];
+    atomicMax(&stats[0 * 64 + threadIdx.x], 1ull);
+    atomicAdd(&stats[1 * 64 + threadIdx.x], k);
+    atomicAdd(&stats[4 * 64 + threadIdx.x], k);
   }
 }
 
@@ -475,21 +642,26 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
                                                    g.dtime, bp, em);
 }
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
-                     int32_t* cnt, int32_t* snbr, uint64_t* smask, int32_t* lab0,
+                     int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
+                     int32_t* lab1, uint64_t* chg1, uint32_t* act2, int32_t* stepcnt,
                      unsigned long long* counters) {
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
-                                                vm, em, cnt, snbr, smask, lab0, counters);
+                                                vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
+                                                stepcnt, counters);
 }
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
-                    uint64_t* chg_next, int32_t* stepcnt) {
-  k_cc_step<<<grid_for(g.nv, 4), 256, 0, s>>>(step, g.nv, g.out_off, g.in_off, vm, cnt, snbr, smask,
-                                               lab_cur, lab_next, chg_prev, chg_next, stepcnt);
+                    uint64_t* chg_next, const uint32_t* act_cur, uint32_t* act_next,
+                    uint32_t* act_clear, int32_t* stepcnt, unsigned long long* work) {
+  k_cc_step<<<grid_for(g.nv, 4 * kChunk), 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask,
+                                                        lab_cur, lab_next, chg_prev, chg_next,
+                                                        act_cur, act_next, act_clear, stepcnt, work);
 }
-void launch_cc_hist(hipStream_t s, const DevGraph& g, const uint64_t* vm, const int32_t* lab,
-                    int32_t* hist) {
-  k_cc_hist<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, vm, lab, hist);
+void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t* vm,
+                    const uint64_t* vadj, const int32_t* lab, int32_t* hist,
+                    unsigned long long* stats) {
+  k_cc_hist<<<grid_for(g.nv, 4 * 64, 2048), 256, 0, s>>>(g.nv, nviews, vm, vadj, lab, hist, stats);
 }
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int32_t* hist, unsigned long long* stats) {
   k_cc_summary<<<grid_for(g.nv, 4, 2048), 256, 0, s>>>(g.nv, hist, stats);

@@ -24,20 +24,24 @@ struct DevGraph {
   const int32_t *esrc = nullptr, *edst = nullptr;    // edges sorted by (src, dst)
   const int64_t *eoff = nullptr, *ekey = nullptr;    // edge own histories
   const int64_t *out_off = nullptr, *in_off = nullptr;
+  const int64_t* adj_off = nullptr;                  // out_off + in_off: static slot offset
   const int32_t* in_eid = nullptr;
 };
 
 void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm);
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em);
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
-                     int32_t* cnt, int32_t* snbr, uint64_t* smask, int32_t* lab0,
+                     int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
+                     int32_t* lab1, uint64_t* chg1, uint32_t* act2, int32_t* stepcnt,
                      unsigned long long* counters);
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
-                    uint64_t* chg_next, int32_t* stepcnt);
-void launch_cc_hist(hipStream_t s, const DevGraph& g, const uint64_t* vm, const int32_t* lab,
-                    int32_t* hist);
+                    uint64_t* chg_next, const uint32_t* act_cur, uint32_t* act_next,
+                    uint32_t* act_clear, int32_t* stepcnt, unsigned long long* work);
+void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t* vm,
+                    const uint64_t* vadj, const int32_t* lab, int32_t* hist,
+                    unsigned long long* stats);
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int32_t* hist, unsigned long long* stats);
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                    int32_t* outdeg, int32_t* indeg, unsigned long long* stats);

@@ -54,6 +54,10 @@ struct Slot {
   int32_t* lab[2] = {nullptr, nullptr};
   uint64_t* chg[2] = {nullptr, nullptr};
   int32_t *stepcnt = nullptr, *hist = nullptr;
+  uint32_t* act[3] = {nullptr, nullptr, nullptr};  // CC frontier bitmaps
+  uint64_t* vadj = nullptr;                         // OR of kept slot masks per vertex
+  unsigned long long* work = nullptr;               // [step][processed vertices, slots]
+  unsigned long long* h_work = nullptr;
   unsigned long long* stats = nullptr;
   int32_t *outdeg = nullptr, *indeg = nullptr;
   double *pr = nullptr, *contrib[2] = {nullptr, nullptr};
@@ -130,6 +134,7 @@ void free_graph(rgpu_ctx* c) {
   for (Slot& s : c->slot) {
     if (s.h_stepcnt) (void)hipHostFree(s.h_stepcnt);
     if (s.h_stats) (void)hipHostFree(s.h_stats);
+    if (s.h_work) (void)hipHostFree(s.h_work);
     if (s.ev) (void)hipEventDestroy(s.ev);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot();
@@ -176,6 +181,7 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
       HIPCHK(hipHostMalloc((void**)&s.h_stepcnt, sizeof(int32_t) * kMaxSteps));
       HIPCHK(hipHostMalloc((void**)&s.h_stats, sizeof(unsigned long long) * kStatWords));
+      HIPCHK(hipHostMalloc((void**)&s.h_work, sizeof(unsigned long long) * 2 * kMaxSteps));
       s.vm = dalloc<uint64_t>(L, nv);
       s.em = dalloc<uint64_t>(L, ne);
       s.stepcnt = dalloc<int32_t>(L, kMaxSteps);
@@ -190,6 +196,9 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       s.chg[0] = dalloc<uint64_t>(L, nv);
       s.chg[1] = dalloc<uint64_t>(L, nv);
       s.hist = dalloc<int32_t>(L, rows);
+      for (int b = 0; b < 3; b++) s.act[b] = dalloc<uint32_t>(L, (nv + 31) / 32 + 1);
+      s.vadj = dalloc<uint64_t>(L, nv);
+      s.work = dalloc<unsigned long long>(L, 2 * kMaxSteps);
       HIPCHK(hipMemset(s.hist, 0, sizeof(int32_t) * (rows ? rows : 1)));
     }
     if ((algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) && !c->slot_deg) {
@@ -229,15 +238,17 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
   const DevGraph& g = c->g;
   int last = std::min(rc.max_steps, s.r_launched + n);
   for (int r = s.r_launched + 1; r <= last; r++) {
-    const uint64_t* chg_prev = r == 1 ? s.vm : s.chg[(r - 1) & 1];
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
-                     chg_prev, s.chg[r & 1], s.stepcnt);
+                     s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
+                     s.act[(r + 2) % 3], s.stepcnt, s.work);
     });
   }
   s.r_launched = last;
   HIPCHK(hipMemcpyAsync(s.h_stepcnt, s.stepcnt, sizeof(int32_t) * kMaxSteps, hipMemcpyDeviceToHost,
                         s.stream));
+  HIPCHK(hipMemcpyAsync(s.h_work, s.work, sizeof(unsigned long long) * 2 * kMaxSteps,
+                        hipMemcpyDeviceToHost, s.stream));
   HIPCHK(hipEventRecord(s.ev, s.stream));
   s.phase = 1;
 }
@@ -247,7 +258,7 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
   const DevGraph& g = c->g;
   if (rc.algo == RGPU_ALGO_CC) {
     const int32_t* lab = s.lab[s.r_final & 1];
-    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g, s.vm, lab, s.hist); });
+    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g, s.kb * rc.W, s.vm, s.vadj, lab, s.hist, s.stats); });
     timed_launch(c, si, KID_SUMMARY, 512.0 * g.nv,
                  [&] { launch_cc_summary(s.stream, g, s.hist, s.stats); });
   }
@@ -292,18 +303,23 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   s.r_final = 0;
   HIPCHK(hipMemsetAsync(s.stats, 0, sizeof(unsigned long long) * kStatWords, s.stream));
   HIPCHK(hipMemsetAsync(s.stepcnt, 0, sizeof(int32_t) * kMaxSteps, s.stream));
+  if (s.work) HIPCHK(hipMemsetAsync(s.work, 0, sizeof(unsigned long long) * 2 * kMaxSteps, s.stream));
   const double bm = bytes_mask(g);
   timed_launch(c, si, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.vkey.size() + 8.0 * g.nv,
                [&] { launch_vertex_mask(s.stream, g, bp, s.vm); });
   timed_launch(c, si, KID_MASK, bm - (16.0 * g.nv + 8.0) + 8.0 * c->pk.ekey.size(),
                [&] { launch_edge_mask(s.stream, g, bp, s.em); });
   if (rc.algo == RGPU_ALGO_CC) {
-    // bytes: per vertex vm + 4 offsets + label row + cnt; per static slot index, em, vm[nb];
-    // alive slots written (the kernel reports members/alive; static part counted here)
-    const double b2 = g.nv * (8.0 + 32.0 + 256.0 + 4.0) + (double)(g.ne + g.n_in) * 24.0;
+    for (int b = 0; b < 3; b++)
+      HIPCHK(hipMemsetAsync(s.act[b], 0, sizeof(uint32_t) * ((g.nv + 31) / 32 + 1), s.stream));
+    // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
+    // em, vm[nb]; kept slots written (12 B each, counted in harvest)
+    const double b2 = g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0;
     timed_launch(c, si, KID_SLOTS, b2, [&] {
-      launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.lab[0], s.stats + 6 * kViews);
+      launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
+                      s.chg[1], s.act[2], s.stepcnt, s.stats + 6 * kViews);
     });
+    s.r_launched = 1;  // superstep 1 ran inside the slot kernel
     if (rc.max_steps <= 1) {  // AnalysisTask.timeResponse :169: no Setup when maxSteps <= 1
       s.r_final = 0;
       finish_batch(c, si, rc);
@@ -352,12 +368,15 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
       }
     }
   if (rc.algo == RGPU_ALGO_CC) {
-    // superstep bytes: every step reads vm of all vertices, and per member
-    // vertex 2 offsets + cnt + label row in/out + change word; per alive slot nbr + mask +
-    // the neighbour's change word.  Executed steps = r_final (later launches exit at once).
-    const double members = (double)h[6 * kViews + 0], alive = (double)h[6 * kViews + 1];
-    const double per_step = 8.0 * c->g.nv + members * (16.0 + 4.0 + 512.0 + 8.0) + alive * 20.0;
-    c->st.kernel_bytes[KID_STEP] += per_step * s.r_final;
+    // superstep bytes, per executed step r >= 2: frontier bitmap read + the
+    // bitmap two steps ahead cleared (8 B per 32 vertices); per visited vertex vm, cnt,
+    // adj_off, label row in and out, change word (540 B); per slot of a visited vertex nbr,
+    // mask and the neighbour's change word (20 B).  Label gathers are not counted.
+    const double alive = (double)h[6 * kViews + 1];
+    c->st.kernel_bytes[KID_SLOTS] += 12.0 * alive;
+    const double words = (double)((c->g.nv + 31) / 32);
+    for (int r = 2; r <= s.r_final; r++)
+      c->st.kernel_bytes[KID_STEP] += 8.0 * words + 540.0 * (double)s.h_work[2 * r] + 20.0 * (double)s.h_work[2 * r + 1];
     c->st.supersteps += s.r_final;
   }
   s.phase = 0;
@@ -488,6 +507,11 @@ int rgpu_seal(rgpu_ctx* c) {
     g.ekey = dupload(L, P.ekey);
     g.out_off = dupload(L, P.out_off);
     g.in_off = dupload(L, P.in_off);
+    {
+      std::vector<int64_t> adj(P.nv + 1);
+      for (int64_t v = 0; v <= P.nv; v++) adj[v] = P.out_off[v] + P.in_off[v];
+      g.adj_off = dupload(L, adj);
+    }
     g.in_eid = dupload(L, P.in_eid);
     c->g = g;
     HIPCHK(hipDeviceSynchronize());
