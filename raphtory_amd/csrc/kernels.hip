@@ -106,6 +106,20 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
   }
 }
 
+// Per-step work counters, sharded 64 ways so that blocks never pile up on one address (a
+// same-address atomic is serialised at the memory side, ~10 ns each: 3k blocks x 3 counters
+// on one word cost more than a sparse superstep).  Layout work[(step*64 + shard)*3 + f],
+// f = visited vertices, visited slots, changed vertices.  Only written when work != nullptr
+// (profile / trace runs).  The halting vote is a plain flag store instead (idempotent).
+__device__ __forceinline__ void add_work(unsigned long long* work, int step, unsigned long long a,
+                                         unsigned long long b, unsigned long long c) {
+  if (!work) return;
+  unsigned long long* w = work + ((size_t)step * 64 + (blockIdx.x & 63)) * 3;
+  if (a) atomicAdd(&w[0], a);
+  if (b) atomicAdd(&w[1], b);
+  if (c) atomicAdd(&w[2], c);
+}
+
 // ---------------------------------------------------------------- K2: batch CSR (+ superstep 1)
 // One wave per vertex.  Static slots of rank v = its out-edges then its in-edges
 // (adjacency offset out_off[v] + in_off[v]).  Slot kept iff its view mask
@@ -136,8 +150,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
                                                   uint64_t* __restrict__ vadj,
                                                   int32_t* __restrict__ lab0, int32_t* __restrict__ lab1,
                                                   uint64_t* __restrict__ chg1, uint32_t* __restrict__ act2,
-                                                  int32_t* __restrict__ stepcnt,
-                                                  unsigned long long* __restrict__ counters) {
+                                                  int32_t* __restrict__ stepflag,
+                                                  unsigned long long* __restrict__ work) {
   __shared__ unsigned long long red[3];
   if (threadIdx.x < 3) red[threadIdx.x] = 0;
   __syncthreads();
@@ -198,15 +212,14 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
     alive += (unsigned long long)count;
   }
   if (lane == 0) {
-    atomicAdd(&red[0], members);
-    atomicAdd(&red[1], alive);
-    atomicAdd(&red[2], changed);
+    if (members) atomicAdd(&red[0], members);
+    if (alive) atomicAdd(&red[1], alive);
+    if (changed) atomicAdd(&red[2], changed);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicAdd(&counters[0], red[0]);
-    atomicAdd(&counters[1], red[1]);
-    if (red[2]) atomicAdd(&stepcnt[1], (int32_t)red[2]);
+    if (red[2]) stepflag[1] = 1;
+    add_work(work, 1, red[0], red[1], red[2]);
   }
 }
 
@@ -223,6 +236,21 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
 // one it will not touch (read two steps ago, written next step).
 constexpr int kChunk = 8;  // vertices per wave visit (8-aligned -> inside one bitmap word)
 
+// Variant 0: one frontier vertex at a time per wave (simple dependent chain per vertex).
+__global__ __launch_bounds__(256) void k_cc_step_v0(int step, int64_t nv, const int64_t* __restrict__ adj_off,
+                                                    const uint64_t* __restrict__ vm,
+                                                    const int32_t* __restrict__ cnt,
+                                                    const int32_t* __restrict__ snbr,
+                                                    const uint64_t* __restrict__ smask,
+                                                    const int32_t* __restrict__ lab_cur,
+                                                    int32_t* __restrict__ lab_next,
+                                                    const uint64_t* __restrict__ chg_prev,
+                                                    uint64_t* __restrict__ chg_next,
+                                                    const uint32_t* __restrict__ act_cur,
+                                                    uint32_t* __restrict__ act_next,
+                                                    uint32_t* __restrict__ act_clear,
+                                                    int32_t* __restrict__ stepflag,
+                                                    unsigned long long* __restrict__ work);
 // Gather the label rows of the neighbours flagged in `act` (lane = slot) and fold them into
 // `best` (lane = view); four independent loads in flight per round.
 __device__ __forceinline__ int32_t gather_min(uint64_t act, int32_t nb, int32_t best,
@@ -273,9 +301,9 @@ __global__ __launch_bounds__(256) void k_cc_step(int step, int64_t nv, const int
                                                  const uint32_t* __restrict__ act_cur,
                                                  uint32_t* __restrict__ act_next,
                                                  uint32_t* __restrict__ act_clear,
-                                                 int32_t* __restrict__ stepcnt,
+                                                 int32_t* __restrict__ stepflag,
                                                  unsigned long long* __restrict__ work) {
-  if (stepcnt[step - 1] == 0) return;
+  if (stepflag[step - 1] == 0) return;
   __shared__ int32_t red;
   __shared__ unsigned long long wred[2];
   if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; }
@@ -355,14 +383,91 @@ __global__ __launch_bounds__(256) void k_cc_step(int step, int64_t nv, const int
   }
   if (lane == 0) {
     if (changed) atomicAdd(&red, changed);
-    atomicAdd(&wred[0], pv);
-    atomicAdd(&wred[1], ps);
+    if (pv) atomicAdd(&wred[0], pv);
+    if (ps) atomicAdd(&wred[1], ps);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (red) atomicAdd(&stepcnt[step], red);
-    atomicAdd(&work[2 * step], wred[0]);
-    atomicAdd(&work[2 * step + 1], wred[1]);
+    if (red) stepflag[step] = 1;
+    add_work(work, step, wred[0], wred[1], (unsigned long long)red);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cc_step_v0(int step, int64_t nv, const int64_t* __restrict__ adj_off,
+                                                    const uint64_t* __restrict__ vm,
+                                                    const int32_t* __restrict__ cnt,
+                                                    const int32_t* __restrict__ snbr,
+                                                    const uint64_t* __restrict__ smask,
+                                                    const int32_t* __restrict__ lab_cur,
+                                                    int32_t* __restrict__ lab_next,
+                                                    const uint64_t* __restrict__ chg_prev,
+                                                    uint64_t* __restrict__ chg_next,
+                                                    const uint32_t* __restrict__ act_cur,
+                                                    uint32_t* __restrict__ act_next,
+                                                    uint32_t* __restrict__ act_clear,
+                                                    int32_t* __restrict__ stepflag,
+                                                    unsigned long long* __restrict__ work) {
+  if (stepflag[step - 1] == 0) return;
+  __shared__ int32_t red;
+  __shared__ unsigned long long wred[2];
+  if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; }
+  const int64_t nwords = (nv + 31) >> 5;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
+       i += (int64_t)gridDim.x * blockDim.x)
+    act_clear[i] = 0;
+  __syncthreads();
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  int32_t changed = 0;
+  unsigned long long pv = 0, ps = 0;
+  for (int64_t c = wave; c * kChunk < nv; c += nwaves) {
+    const int64_t v0 = c * kChunk;
+    uint32_t bits = (act_cur[v0 >> 5] >> (v0 & 31)) & 0xffu;
+    while (bits) {
+      const int64_t v = v0 + __builtin_ctz(bits);
+      bits &= bits - 1;
+      if (v >= nv) break;
+      const uint64_t mv = vm[v];
+      const int32_t n = cnt[v];
+      const int64_t base = adj_off[v];
+      const int32_t cur = lab_cur[v * 64 + lane];
+      if (mv == 0) continue;
+      pv += 1;
+      ps += (unsigned long long)n;
+      int32_t best = cur;
+      for (int32_t c2 = 0; c2 < n; c2 += 64) {
+        const int32_t j = c2 + lane;
+        uint64_t a2 = 0;
+        int32_t q = 0;
+        if (j < n) {
+          q = snbr[base + j];
+          a2 = smask[base + j] & chg_prev[q];
+        }
+        best = gather_min(a2, q, best, lab_cur, lane);
+      }
+      lab_next[v * 64 + lane] = best;
+      const uint64_t ch = __ballot(best < cur);
+      if (lane == 0) chg_next[v] = ch;
+      if (ch) {
+        changed++;
+        if (lane == 0) mark(act_next, (int32_t)v);
+        for (int32_t c2 = 0; c2 < n; c2 += 64) {
+          const int32_t j = c2 + lane;
+          if (j < n && (smask[base + j] & ch)) mark(act_next, snbr[base + j]);
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    if (changed) atomicAdd(&red, changed);
+    if (pv) atomicAdd(&wred[0], pv);
+    if (ps) atomicAdd(&wred[1], ps);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (red) stepflag[step] = 1;
+    add_work(work, step, wred[0], wred[1], (unsigned long long)red);
   }
 }
 
@@ -388,7 +493,13 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int nviews, const u
   for (int64_t c = wave; c * 64 < nv; c += nwaves) {
     const int64_t v0 = c * 64;
     const int nvc = (int)(nv - v0 < 64 ? nv - v0 : 64);
-    for (int i = 0; i < nvc; i++) tile[wib][i][lane] = lab[(v0 + i) * 64 + lane];
+    for (int i0 = 0; i0 < 64; i0 += 16) {  // 16 independent row loads in flight, then LDS
+      int32_t r[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) r[k] = i0 + k < nvc ? lab[(v0 + i0 + k) * 64 + lane] : 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) tile[wib][i0 + k][lane] = r[k];
+    }
     const uint64_t mvl = lane < nvc ? vm[v0 + lane] : 0;
     const uint64_t adl = lane < nvc ? vadj[v0 + lane] : 0;
     __builtin_amdgcn_wave_barrier();
@@ -643,32 +754,37 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
 }
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
-                     int32_t* lab1, uint64_t* chg1, uint32_t* act2, int32_t* stepcnt,
-                     unsigned long long* counters) {
+                     int32_t* lab1, uint64_t* chg1, uint32_t* act2, int32_t* stepflag,
+                     unsigned long long* work) {
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
                                                 vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
-                                                stepcnt, counters);
+                                                stepflag, work);
 }
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint32_t* act_cur, uint32_t* act_next,
-                    uint32_t* act_clear, int32_t* stepcnt, unsigned long long* work) {
-  k_cc_step<<<grid_for(g.nv, 4 * kChunk), 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask,
-                                                        lab_cur, lab_next, chg_prev, chg_next,
-                                                        act_cur, act_next, act_clear, stepcnt, work);
+                    uint32_t* act_clear, int32_t* stepcnt, unsigned long long* work, int variant) {
+  if (variant == 1)
+    k_cc_step<<<grid_for(g.nv, 4 * kChunk), 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask,
+                                                          lab_cur, lab_next, chg_prev, chg_next,
+                                                          act_cur, act_next, act_clear, stepcnt, work);
+  else
+    k_cc_step_v0<<<grid_for(g.nv, 4 * kChunk), 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask,
+                                                             lab_cur, lab_next, chg_prev, chg_next,
+                                                             act_cur, act_next, act_clear, stepcnt, work);
 }
 void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist,
                     unsigned long long* stats) {
-  k_cc_hist<<<grid_for(g.nv, 4 * 64, 2048), 256, 0, s>>>(g.nv, nviews, vm, vadj, lab, hist, stats);
+  k_cc_hist<<<grid_for(g.nv, 4 * 64, 512), 256, 0, s>>>(g.nv, nviews, vm, vadj, lab, hist, stats);
 }
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int32_t* hist, unsigned long long* stats) {
-  k_cc_summary<<<grid_for(g.nv, 4, 2048), 256, 0, s>>>(g.nv, hist, stats);
+  k_cc_summary<<<grid_for(g.nv, 4, 256), 256, 0, s>>>(g.nv, hist, stats);
 }
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                    int32_t* outdeg, int32_t* indeg, unsigned long long* stats) {
-  k_degree<<<grid_for(g.nv, 4, 2048), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, vm, em,
+  k_degree<<<grid_for(g.nv, 4, 256), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, vm, em,
                                                     outdeg, indeg, stats);
 }
 void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -44,6 +45,7 @@ enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUM
 
 constexpr int kMaxSteps = 128;
 constexpr int kStatWords = 7 * kViews;  // 6 per-view fields + counters row
+constexpr int kWorkWords = kMaxSteps * 64 * 3;
 
 struct Slot {
   hipStream_t stream = nullptr;
@@ -53,10 +55,10 @@ struct Slot {
   uint64_t* smask = nullptr;
   int32_t* lab[2] = {nullptr, nullptr};
   uint64_t* chg[2] = {nullptr, nullptr};
-  int32_t *stepcnt = nullptr, *hist = nullptr;
+  int32_t *stepcnt = nullptr, *hist = nullptr;   // stepcnt[r] = 1 iff superstep r changed a label
   uint32_t* act[3] = {nullptr, nullptr, nullptr};  // CC frontier bitmaps
   uint64_t* vadj = nullptr;                         // OR of kept slot masks per vertex
-  unsigned long long* work = nullptr;               // [step][processed vertices, slots]
+  unsigned long long* work = nullptr;               // [step][64 shards][visited, slots, changed]
   unsigned long long* h_work = nullptr;
   unsigned long long* stats = nullptr;
   int32_t *outdeg = nullptr, *indeg = nullptr;
@@ -78,6 +80,7 @@ struct Retained {  // per batch, RGPU_RUN_RETAIN
 struct Timed {
   int kid;
   int slot;
+  int batch, step;
   hipEvent_t a, b;
   double bytes;
 };
@@ -96,6 +99,10 @@ struct rgpu_ctx {
   std::vector<void*> graph_allocs;
   Slot slot[2];
   int nslots = 2;
+  int step_variant = 0;                 // RGPU_STEP_VARIANT: 0 per-vertex chain, 1 chunk-pipelined
+  std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
+  struct StepRec { int batch, step; unsigned long long pv, ps; int changed; };
+  std::vector<StepRec> steprec;
   bool slot_cc = false, slot_deg = false, slot_pr = false;
   // last run
   int algo = -1, K = 0, W = 0;
@@ -154,14 +161,14 @@ hipEvent_t take_event(rgpu_ctx* c) {
 
 // Run `fn` (one kernel launch) on slot stream, bracketed by events in profile mode.
 template <class F>
-void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn) {
+void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn, int step = 0) {
   Slot& s = c->slot[si];
   if (c->profile) {
     hipEvent_t a = take_event(c), b = take_event(c);
     HIPCHK(hipEventRecord(a, s.stream));
     fn();
     HIPCHK(hipEventRecord(b, s.stream));
-    c->timed.push_back({kid, si, a, b, bytes});
+    c->timed.push_back({kid, si, s.batch, step, a, b, bytes});
   } else {
     fn();
   }
@@ -181,7 +188,7 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
       HIPCHK(hipHostMalloc((void**)&s.h_stepcnt, sizeof(int32_t) * kMaxSteps));
       HIPCHK(hipHostMalloc((void**)&s.h_stats, sizeof(unsigned long long) * kStatWords));
-      HIPCHK(hipHostMalloc((void**)&s.h_work, sizeof(unsigned long long) * 2 * kMaxSteps));
+      HIPCHK(hipHostMalloc((void**)&s.h_work, sizeof(unsigned long long) * kWorkWords));
       s.vm = dalloc<uint64_t>(L, nv);
       s.em = dalloc<uint64_t>(L, ne);
       s.stepcnt = dalloc<int32_t>(L, kMaxSteps);
@@ -198,7 +205,7 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       s.hist = dalloc<int32_t>(L, rows);
       for (int b = 0; b < 3; b++) s.act[b] = dalloc<uint32_t>(L, (nv + 31) / 32 + 1);
       s.vadj = dalloc<uint64_t>(L, nv);
-      s.work = dalloc<unsigned long long>(L, 2 * kMaxSteps);
+      s.work = dalloc<unsigned long long>(L, kWorkWords);
       HIPCHK(hipMemset(s.hist, 0, sizeof(int32_t) * (rows ? rows : 1)));
     }
     if ((algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) && !c->slot_deg) {
@@ -241,14 +248,15 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                      s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
-                     s.act[(r + 2) % 3], s.stepcnt, s.work);
-    });
+                     s.act[(r + 2) % 3], s.stepcnt, c->profile ? s.work : nullptr, c->step_variant);
+    }, r);
   }
   s.r_launched = last;
   HIPCHK(hipMemcpyAsync(s.h_stepcnt, s.stepcnt, sizeof(int32_t) * kMaxSteps, hipMemcpyDeviceToHost,
                         s.stream));
-  HIPCHK(hipMemcpyAsync(s.h_work, s.work, sizeof(unsigned long long) * 2 * kMaxSteps,
-                        hipMemcpyDeviceToHost, s.stream));
+  if (c->profile)
+    HIPCHK(hipMemcpyAsync(s.h_work, s.work, sizeof(unsigned long long) * kWorkWords,
+                          hipMemcpyDeviceToHost, s.stream));
   HIPCHK(hipEventRecord(s.ev, s.stream));
   s.phase = 1;
 }
@@ -303,7 +311,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   s.r_final = 0;
   HIPCHK(hipMemsetAsync(s.stats, 0, sizeof(unsigned long long) * kStatWords, s.stream));
   HIPCHK(hipMemsetAsync(s.stepcnt, 0, sizeof(int32_t) * kMaxSteps, s.stream));
-  if (s.work) HIPCHK(hipMemsetAsync(s.work, 0, sizeof(unsigned long long) * 2 * kMaxSteps, s.stream));
+  if (s.work && c->profile)
+    HIPCHK(hipMemsetAsync(s.work, 0, sizeof(unsigned long long) * kWorkWords, s.stream));
   const double bm = bytes_mask(g);
   timed_launch(c, si, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.vkey.size() + 8.0 * g.nv,
                [&] { launch_vertex_mask(s.stream, g, bp, s.vm); });
@@ -317,7 +326,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     const double b2 = g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0;
     timed_launch(c, si, KID_SLOTS, b2, [&] {
       launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
-                      s.chg[1], s.act[2], s.stepcnt, s.stats + 6 * kViews);
+                      s.chg[1], s.act[2], s.stepcnt, c->profile ? s.work : nullptr);
     });
     s.r_launched = 1;  // superstep 1 ran inside the slot kernel
     if (rc.max_steps <= 1) {  // AnalysisTask.timeResponse :169: no Setup when maxSteps <= 1
@@ -372,11 +381,20 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
     // bitmap two steps ahead cleared (8 B per 32 vertices); per visited vertex vm, cnt,
     // adj_off, label row in and out, change word (540 B); per slot of a visited vertex nbr,
     // mask and the neighbour's change word (20 B).  Label gathers are not counted.
-    const double alive = (double)h[6 * kViews + 1];
-    c->st.kernel_bytes[KID_SLOTS] += 12.0 * alive;
-    const double words = (double)((c->g.nv + 31) / 32);
-    for (int r = 2; r <= s.r_final; r++)
-      c->st.kernel_bytes[KID_STEP] += 8.0 * words + 540.0 * (double)s.h_work[2 * r] + 20.0 * (double)s.h_work[2 * r + 1];
+    if (c->profile) {
+      auto wsum = [&](int r, int f) {
+        unsigned long long t = 0;
+        for (int k = 0; k < 64; k++) t += s.h_work[((size_t)r * 64 + k) * 3 + f];
+        return t;
+      };
+      c->st.kernel_bytes[KID_SLOTS] += 12.0 * (double)wsum(1, 1);
+      const double words = (double)((c->g.nv + 31) / 32);
+      for (int r = 2; r <= s.r_final; r++)
+        c->st.kernel_bytes[KID_STEP] += 8.0 * words + 540.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1);
+      if (!c->trace_path.empty())
+        for (int r = 1; r <= s.r_final; r++)
+          c->steprec.push_back({s.batch, r, wsum(r, 0), wsum(r, 1), (int)wsum(r, 2)});
+    }
     c->st.supersteps += s.r_final;
   }
   s.phase = 0;
@@ -458,6 +476,8 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->nparts = num_partitions;
   c->device = device;
   c->nslots = std::max(1, std::min(2, env_int("RGPU_SLOTS", 2)));
+  c->step_variant = env_int("RGPU_STEP_VARIANT", 0);
+  if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
   *out = c;
   return RGPU_OK;
@@ -609,11 +629,21 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->st.ms_total = std::chrono::duration<double, std::milli>(t1 - t0).count();
     c->st.launches = 0;
     for (int k = 0; k < KID_N; k++) c->st.launches += c->st.kernel_launches[k];
+    FILE* tf = nullptr;
+    if (!c->trace_path.empty() && (tf = std::fopen(c->trace_path.c_str(), "w")))
+      std::fprintf(tf, "kind,batch,step,kernel,ms,pv,ps,changed\n");
     for (const Timed& tm : c->timed) {
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, tm.a, tm.b));
       c->st.kernel_ms[tm.kid] += ms;
+      if (tf) std::fprintf(tf, "L,%d,%d,%d,%.4f,,,\n", tm.batch, tm.step, tm.kid, ms);
     }
+    if (tf) {
+      for (const auto& r : c->steprec)
+        std::fprintf(tf, "S,%d,%d,,,%llu,%llu,%d\n", r.batch, r.step, r.pv, r.ps, r.changed);
+      std::fclose(tf);
+    }
+    c->steprec.clear();
   } catch (const HipFail& f) {
     return fail(c, RGPU_EHIP, f.msg);
   } catch (const std::bad_alloc&) {
