@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* 
       if (!(key & 1)) continue;  // floor is a deletion
       const int64_t age = t - (key >> 1);
       for (int w = 0; w < bp.W; w++)
-        if (age <= bp.thr_v[w]) m |= 1ull << (k * bp.W + w);
+        if (age <= bp.thr_v[w]) m |= 1ull << (w * bp.KS + k);
     }
     vm[v] = m;
   }
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
       if (d1 > d0 && last_death(dtime, d0, d1, t) > ft) continue;
       const int64_t age = t - ft;
       for (int w = 0; w < bp.W; w++)
-        if (age <= bp.thr_e[w]) m |= 1ull << (k * bp.W + w);
+        if (age <= bp.thr_e[w]) m |= 1ull << (w * bp.KS + k);
     }
     em[e] = m;
   }
@@ -162,12 +162,11 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
   for (int64_t v = wave; v < nv; v += nwaves) {
     const uint64_t mv = vm[v];
     const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
-    lab0[v * 64 + lane] = (int32_t)v;
     if (mv == 0) {
-      lab1[v * 64 + lane] = (int32_t)v;
       if (lane == 0) { cnt[v] = 0; vadj[v] = 0; }
       continue;
     }
+    lab0[v * 64 + lane] = (int32_t)v;  // whole rows: partial-line stores cost a fill
     const int64_t nout = o1 - o0, ntot = nout + (i1 - i0), base = o0 + i0;
     int32_t count = 0, best = (int32_t)v;
     uint64_t any = 0;
@@ -329,7 +328,9 @@ __global__ __launch_bounds__(256) void k_cc_step(int step, int64_t nv, const int
     const int64_t b_l = okl ? adj_off[v0 + lane] : 0;
     int32_t cur[kChunk];
 #pragma unroll
-    for (int i = 0; i < kChunk; i++) cur[i] = ((bits >> i) & 1) ? lab_cur[(v0 + i) * 64 + lane] : 0;
+    for (int i = 0; i < kChunk; i++)
+      cur[i] = (((bits >> i) & 1) && ((readlane64(mv_l, i) >> lane) & 1)) ? lab_cur[(v0 + i) * 64 + lane]
+                                                                        : INT32_MAX;
     // stage 2: first 64 kept slots of every vertex
     int32_t nb[kChunk];
     uint64_t sm[kChunk];
@@ -431,8 +432,9 @@ __global__ __launch_bounds__(256) void k_cc_step_v0(int step, int64_t nv, const 
       const uint64_t mv = vm[v];
       const int32_t n = cnt[v];
       const int64_t base = adj_off[v];
-      const int32_t cur = lab_cur[v * 64 + lane];
       if (mv == 0) continue;
+      const bool mine = (mv >> lane) & 1;
+      const int32_t cur = mine ? lab_cur[v * 64 + lane] : INT32_MAX;
       pv += 1;
       ps += (unsigned long long)n;
       int32_t best = cur;
@@ -514,7 +516,7 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int nviews, const u
         const int leader = __builtin_ctzll(todo);
         const int32_t L = __builtin_amdgcn_readlane(l, leader);
         const uint64_t same = __ballot(member && l == L);
-        if (lane == leader) atomicAdd(&hist[(int64_t)L * 64 + j], __popcll(same));
+        if (lane == leader) atomicAdd(&hist[(int64_t)j * nv + L], __popcll(same));
         todo &= ~same;
       }
     }
@@ -529,22 +531,21 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int nviews, const u
   }
 }
 
-// processBatchWindowResults summary per view (ConnectedComponents.scala:137-145); clears
-// the histogram for the next batch.  stats[f*64 + view]: 0 biggest 1 total 2 total>1
-// 3 total>2 4 sum 5 sum(count>1)
+// processBatchWindowResults summary per view (ConnectedComponents.scala:137-145) from the
+// view-major histogram hist[view][rank]; clears it for the next batch.  blockIdx.y = view,
+// blockIdx.x strides over ranks; one atomic per (block, field).  stats[f*64 + view]:
+// 0 biggest 1 total 2 total>1 3 total>2 4 sum 5 sum(count>1)
 __global__ __launch_bounds__(256) void k_cc_summary(int64_t nv, int32_t* __restrict__ hist,
                                                     unsigned long long* __restrict__ stats) {
-  __shared__ unsigned long long red[6][64];
-  for (int i = threadIdx.x; i < 6 * 64; i += blockDim.x) (&red[0][0])[i] = 0;
-  __syncthreads();
-  const int lane = lane_id();
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  __shared__ unsigned long long red[6][4];
+  const int j = blockIdx.y;
+  int32_t* h = hist + (int64_t)j * nv;
   unsigned long long big = 0, tot = 0, nis = 0, gt2 = 0, sum = 0, snis = 0;
-  for (int64_t r = wave; r < nv; r += nwaves) {
-    const int32_t c = hist[r * 64 + lane];
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nv;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t c = h[r];
     if (c) {
-      hist[r * 64 + lane] = 0;
+      h[r] = 0;
       const unsigned long long uc = (unsigned long long)c;
       big = uc > big ? uc : big;
       tot += 1;
@@ -554,18 +555,26 @@ __global__ __launch_bounds__(256) void k_cc_summary(int64_t nv, int32_t* __restr
       snis += c > 1 ? uc : 0;
     }
   }
-  atomicMax(&red[0][lane], big);
-  atomicAdd(&red[1][lane], tot);
-  atomicAdd(&red[2][lane], nis);
-  atomicAdd(&red[3][lane], gt2);
-  atomicAdd(&red[4][lane], sum);
-  atomicAdd(&red[5][lane], snis);
+  unsigned long long v[6] = {big, tot, nis, gt2, sum, snis};
+#pragma unroll
+  for (int f = 0; f < 6; f++) {
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long x = __shfl_xor(v[f], o);
+      v[f] = f == 0 ? (x > v[f] ? x : v[f]) : v[f] + x;
+    }
+  }
+  const int lane = lane_id(), wib = threadIdx.x >> 6;
+  if (lane == 0)
+    for (int f = 0; f < 6; f++) red[f][wib] = v[f];
   __syncthreads();
-  if (threadIdx.x < 64) {
-    const int j = threadIdx.x;
-    if (red[0][j]) atomicMax(&stats[0 * 64 + j], red[0][j]);
-    for (int f = 1; f < 6; f++)
-      if (red[f][j]) atomicAdd(&stats[f * 64 + j], red[f][j]);
+  if (threadIdx.x < 6) {
+    const int f = threadIdx.x;
+    unsigned long long a = red[f][0];
+    for (int w = 1; w < 4; w++) a = f == 0 ? (red[f][w] > a ? red[f][w] : a) : a + red[f][w];
+    if (a) {
+      if (f == 0) atomicMax(&stats[j], a);
+      else atomicAdd(&stats[f * 64 + j], a);
+    }
   }
 }
 
@@ -739,6 +748,8 @@ __global__ __launch_bounds__(256) void k_pr_step(int64_t nv, const int64_t* __re
 }
 
 // ---------------------------------------------------------------- launchers
+int g_step_grid = 2048;
+
 static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
   int64_t g = (items + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -765,12 +776,13 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint32_t* act_cur, uint32_t* act_next,
                     uint32_t* act_clear, int32_t* stepcnt, unsigned long long* work, int variant) {
+  const unsigned grid = grid_for(g.nv, 4 * kChunk, (unsigned)g_step_grid);
   if (variant == 1)
-    k_cc_step<<<grid_for(g.nv, 4 * kChunk), 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask,
+    k_cc_step<<<grid, 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask,
                                                           lab_cur, lab_next, chg_prev, chg_next,
                                                           act_cur, act_next, act_clear, stepcnt, work);
   else
-    k_cc_step_v0<<<grid_for(g.nv, 4 * kChunk), 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask,
+    k_cc_step_v0<<<grid, 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask,
                                                              lab_cur, lab_next, chg_prev, chg_next,
                                                              act_cur, act_next, act_clear, stepcnt, work);
 }
@@ -779,8 +791,10 @@ void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t
                     unsigned long long* stats) {
   k_cc_hist<<<grid_for(g.nv, 4 * 64, 512), 256, 0, s>>>(g.nv, nviews, vm, vadj, lab, hist, stats);
 }
-void launch_cc_summary(hipStream_t s, const DevGraph& g, int32_t* hist, unsigned long long* stats) {
-  k_cc_summary<<<grid_for(g.nv, 4, 256), 256, 0, s>>>(g.nv, hist, stats);
+void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
+                       unsigned long long* stats) {
+  dim3 grid(grid_for(g.nv, 256, 32), (unsigned)nviews);
+  k_cc_summary<<<grid, 256, 0, s>>>(g.nv, hist, stats);
 }
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                    int32_t* outdeg, int32_t* indeg, unsigned long long* stats) {

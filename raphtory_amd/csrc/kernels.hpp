@@ -8,9 +8,11 @@ namespace rgpu {
 
 constexpr int kViews = 64;  // views per batch = wavefront width (lane j <-> view j)
 
-// One batch of views: hops[K] x windows[W], view bit j = k*W + w, K*W <= 64.
+// One batch of views: hops[K] x windows[W], view bit j = w*KS + k (window-major, KS = hop
+// stride of the run, K <= KS hops in this batch, KS*W <= 64).  Window-major order keeps the
+// views a vertex belongs to (the long windows) in the low lanes of its label row.
 struct BatchParams {
-  int K, W;
+  int K, W, KS;
   int64_t hop[kViews];    // view timestamps (RangeAnalysisTask hop times)
   int64_t thr_v[kViews];  // vertex-set window of window index w: min(w_0..w_w)  (shrinkWindow)
   int64_t thr_e[kViews];  // edge window of window index w: w_w (viewAtWithWindow(t, setWindow))
@@ -34,6 +36,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint32_t* act2, int32_t* stepflag,
                      unsigned long long* work);
+extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID)
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
@@ -42,7 +45,8 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
 void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist,
                     unsigned long long* stats);
-void launch_cc_summary(hipStream_t s, const DevGraph& g, int32_t* hist, unsigned long long* stats);
+void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
+                       unsigned long long* stats);
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                    int32_t* outdeg, int32_t* indeg, unsigned long long* stats);
 void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,

@@ -266,9 +266,9 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
   const DevGraph& g = c->g;
   if (rc.algo == RGPU_ALGO_CC) {
     const int32_t* lab = s.lab[s.r_final & 1];
-    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g, s.kb * rc.W, s.vm, s.vadj, lab, s.hist, s.stats); });
-    timed_launch(c, si, KID_SUMMARY, 512.0 * g.nv,
-                 [&] { launch_cc_summary(s.stream, g, s.hist, s.stats); });
+    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g, rc.K * rc.W, s.vm, s.vadj, lab, s.hist, s.stats); });
+    timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * rc.K * rc.W,
+                 [&] { launch_cc_summary(s.stream, g, rc.K * rc.W, s.hist, s.stats); });
   }
   HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatWords,
                         hipMemcpyDeviceToHost, s.stream));
@@ -303,6 +303,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   const size_t h0 = (size_t)b * rc.K;
   bp.K = (int)std::min<size_t>(rc.K, rc.n_hops - h0);
   bp.W = rc.W;
+  bp.KS = rc.K;
   for (int k = 0; k < bp.K; k++) bp.hop[k] = rc.hops[h0 + k];
   for (int w = 0; w < rc.W; w++) { bp.thr_v[w] = rc.thr_v[w]; bp.thr_e[w] = rc.thr_e[w]; }
   s.batch = b;
@@ -360,7 +361,7 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
   const unsigned long long* h = s.h_stats;
   for (int k = 0; k < s.kb; k++)
     for (int w = 0; w < rc.W; w++) {
-      const int j = k * rc.W + w;
+      const int j = w * rc.K + k;  // window-major view bit
       const size_t view = ((size_t)s.batch * rc.K + k) * rc.W + w;
       if (rc.algo == RGPU_ALGO_CC) {
         rgpu_cc_summary_t& o = c->cc[view];
@@ -477,6 +478,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->device = device;
   c->nslots = std::max(1, std::min(2, env_int("RGPU_SLOTS", 2)));
   c->step_variant = env_int("RGPU_STEP_VARIANT", 0);
+  if (env_int("RGPU_STEP_GRID", 0) > 0) g_step_grid = env_int("RGPU_STEP_GRID", 0);
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
   *out = c;
@@ -655,7 +657,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
 static int view_index(rgpu_ctx* c, size_t hop, size_t win, size_t* batch, int* lane) {
   if (hop >= c->n_hops || win >= (size_t)c->W) return fail(c, RGPU_EINVAL, "view index out of range");
   *batch = hop / c->K;
-  *lane = (int)((hop % c->K) * c->W + win);
+  *lane = (int)(win * c->K + hop % c->K);
   return RGPU_OK;
 }
 
