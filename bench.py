@@ -126,7 +126,7 @@ def main():
     roofline = None
     kstats = {}
     if not a.no_profile_pass:
-        g.run("cc", hops, windows, profile=True)
+        g.run("cc", hops, windows, profile=True, serial=True)
         ks = g.stats()["kernels"]
         kstats = {k: v for k, v in ks.items() if v["launches"]}
         dom = max(kstats, key=lambda k: kstats[k]["ms"])

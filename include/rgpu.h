@@ -51,6 +51,7 @@ extern "C" {
 /* rgpu_run_view_batch flags */
 #define RGPU_RUN_RETAIN 1   /* keep per-vertex results of every view (for *_vertex_* queries) */
 #define RGPU_RUN_PROFILE 2  /* time every kernel launch with HIP events (rgpu_stats) */
+#define RGPU_RUN_SERIAL 4   /* one batch in flight (clean per-kernel event times) */
 
 typedef struct rgpu_ctx rgpu_ctx;
 

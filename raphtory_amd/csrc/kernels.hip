@@ -134,9 +134,6 @@ __device__ __forceinline__ void add_work(unsigned long long* work, int step, uns
 // writes label_0 (= rank) and label_1 rows, the step-1 change words, the step-2 frontier
 // bitmap and stepcnt[1]; vadj[v] = OR of v's kept slot masks (v isolated in view j iff bit j
 // is clear).
-__device__ __forceinline__ void mark(uint32_t* act, int32_t x) {
-  atomicOr(&act[x >> 5], 1u << (x & 31));
-}
 
 __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __restrict__ out_off,
                                                   const int64_t* __restrict__ in_off,
@@ -149,7 +146,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
                                                   uint64_t* __restrict__ smask,
                                                   uint64_t* __restrict__ vadj,
                                                   int32_t* __restrict__ lab0, int32_t* __restrict__ lab1,
-                                                  uint64_t* __restrict__ chg1, uint32_t* __restrict__ act2,
+                                                  uint64_t* __restrict__ chg1, uint8_t* __restrict__ act2,
                                                   int32_t* __restrict__ stepflag,
                                                   unsigned long long* __restrict__ work) {
   __shared__ unsigned long long red[3];
@@ -201,10 +198,10 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
     if (lane == 0) { cnt[v] = count; vadj[v] = any; chg1[v] = ch; }
     if (ch) {
       changed++;
-      if (lane == 0) mark(act2, (int32_t)v);
+      if (lane == 0) act2[v] = 1;
       for (int32_t c = 0; c < count; c += 64) {
         const int32_t j = c + lane;
-        if (j < count && (smask[base + j] & ch)) mark(act2, snbr[base + j]);
+        if (j < count && (smask[base + j] & ch)) act2[snbr[base + j]] = 1;
       }
     }
     members += 1;
@@ -233,23 +230,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
 // with every vertex that changed (so both label buffers catch up) and every neighbour that
 // shares a view with the change.  Bitmaps rotate over three buffers; each step zeroes the
 // one it will not touch (read two steps ago, written next step).
-constexpr int kChunk = 8;  // vertices per wave visit (8-aligned -> inside one bitmap word)
 
-// Variant 0: one frontier vertex at a time per wave (simple dependent chain per vertex).
-__global__ __launch_bounds__(256) void k_cc_step_v0(int step, int64_t nv, const int64_t* __restrict__ adj_off,
-                                                    const uint64_t* __restrict__ vm,
-                                                    const int32_t* __restrict__ cnt,
-                                                    const int32_t* __restrict__ snbr,
-                                                    const uint64_t* __restrict__ smask,
-                                                    const int32_t* __restrict__ lab_cur,
-                                                    int32_t* __restrict__ lab_next,
-                                                    const uint64_t* __restrict__ chg_prev,
-                                                    uint64_t* __restrict__ chg_next,
-                                                    const uint32_t* __restrict__ act_cur,
-                                                    uint32_t* __restrict__ act_next,
-                                                    uint32_t* __restrict__ act_clear,
-                                                    int32_t* __restrict__ stepflag,
-                                                    unsigned long long* __restrict__ work);
 // Gather the label rows of the neighbours flagged in `act` (lane = slot) and fold them into
 // `best` (lane = view); four independent loads in flight per round.
 __device__ __forceinline__ int32_t gather_min(uint64_t act, int32_t nb, int32_t best,
@@ -284,80 +265,88 @@ __device__ __forceinline__ int32_t gather_min(uint64_t act, int32_t nb, int32_t 
   return best;
 }
 
-// A wave visits the frontier vertices of one 8-vertex chunk.  Loads are issued per stage
-// for all of the chunk's vertices before anything waits on them (metadata and own label
-// rows, then the first 64 kept slots of each, then the neighbours' change words), so a
-// chunk costs ~4 dependent memory round trips plus the label gathers, not ~5 per vertex.
-__global__ __launch_bounds__(256) void k_cc_step(int step, int64_t nv, const int64_t* __restrict__ adj_off,
-                                                 const uint64_t* __restrict__ vm,
-                                                 const int32_t* __restrict__ cnt,
-                                                 const int32_t* __restrict__ snbr,
-                                                 const uint64_t* __restrict__ smask,
-                                                 const int32_t* __restrict__ lab_cur,
-                                                 int32_t* __restrict__ lab_next,
-                                                 const uint64_t* __restrict__ chg_prev,
-                                                 uint64_t* __restrict__ chg_next,
-                                                 const uint32_t* __restrict__ act_cur,
-                                                 uint32_t* __restrict__ act_next,
-                                                 uint32_t* __restrict__ act_clear,
-                                                 int32_t* __restrict__ stepflag,
-                                                 unsigned long long* __restrict__ work) {
+// Variant 2 (default): frontier flags are bytes (plain idempotent stores, no RMW), and a
+// wave's CH-vertex chunk runs loads-first: metadata + own change words + own label rows,
+// slot rows, neighbour change words, then every label gather of the chunk, and only then
+// the stores (rows, change words, next-frontier flags).  On CDNA stores and atomics count in
+// vmcnt, so interleaving them with the next vertex's loads would serialise the chunk.
+// A visited vertex rewrites its row only if it changed now or in the previous step (the
+// only cases where the two label buffers differ).
+template <int CH>
+__global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const int64_t* __restrict__ adj_off,
+                                                  const uint64_t* __restrict__ vm,
+                                                  const int32_t* __restrict__ cnt,
+                                                  const int32_t* __restrict__ snbr,
+                                                  const uint64_t* __restrict__ smask,
+                                                  const int32_t* __restrict__ lab_cur,
+                                                  int32_t* __restrict__ lab_next,
+                                                  const uint64_t* __restrict__ chg_prev,
+                                                  uint64_t* __restrict__ chg_next,
+                                                  const uint8_t* __restrict__ act_cur,
+                                                  uint8_t* __restrict__ act_next,
+                                                  uint8_t* __restrict__ act_clear,
+                                                  int32_t* __restrict__ stepflag,
+                                                  unsigned long long* __restrict__ work) {
   if (stepflag[step - 1] == 0) return;
   __shared__ int32_t red;
   __shared__ unsigned long long wred[2];
   if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; }
-  const int64_t nwords = (nv + 31) >> 5;
+  const int64_t nwords = (nv + 7) >> 3;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
        i += (int64_t)gridDim.x * blockDim.x)
-    act_clear[i] = 0;
+    reinterpret_cast<uint64_t*>(act_clear)[i] = 0;
   __syncthreads();
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int32_t changed = 0;
   unsigned long long pv = 0, ps = 0;
-  for (int64_t c = wave; c * kChunk < nv; c += nwaves) {
-    const int64_t v0 = c * kChunk;
-    uint32_t bits = (act_cur[v0 >> 5] >> (v0 & 31)) & 0xffu;
-    if (v0 + kChunk > nv) bits &= (1u << (nv - v0)) - 1;
+  for (int64_t c = wave; c * CH < nv; c += nwaves) {
+    const int64_t v0 = c * CH;
+    uint32_t bits = 0;
+    {
+      const uint64_t f = CH == 8 ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
+                                 : *reinterpret_cast<const uint32_t*>(act_cur + v0);
+#pragma unroll
+      for (int i = 0; i < CH; i++) bits |= ((f >> (8 * i)) & 0xffu) ? (1u << i) : 0u;
+    }
+    if (v0 + CH > nv) bits &= (1u << (nv - v0)) - 1;
     if (!bits) continue;
-    // stage 1: metadata (lane i < 8 -> vertex v0+i) and own label rows
-    const bool okl = lane < kChunk && ((bits >> lane) & 1);
+    // stage 1: metadata, own change word of the previous step, own label rows
+    const bool okl = lane < CH && ((bits >> lane) & 1);
     const uint64_t mv_l = okl ? vm[v0 + lane] : 0;
     const int32_t n_l = okl ? cnt[v0 + lane] : 0;
     const int64_t b_l = okl ? adj_off[v0 + lane] : 0;
-    int32_t cur[kChunk];
+    const uint64_t cp_l = okl ? chg_prev[v0 + lane] : 0;
+    int32_t cur[CH];
 #pragma unroll
-    for (int i = 0; i < kChunk; i++)
+    for (int i = 0; i < CH; i++)
       cur[i] = (((bits >> i) & 1) && ((readlane64(mv_l, i) >> lane) & 1)) ? lab_cur[(v0 + i) * 64 + lane]
                                                                         : INT32_MAX;
-    // stage 2: first 64 kept slots of every vertex
-    int32_t nb[kChunk];
-    uint64_t sm[kChunk];
+    // stage 2: first 64 kept slots of each vertex
+    int32_t nb[CH];
+    uint64_t sm[CH];
 #pragma unroll
-    for (int i = 0; i < kChunk; i++) {
+    for (int i = 0; i < CH; i++) {
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
       const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
       nb[i] = 0;
       sm[i] = 0;
       if (lane < n) { nb[i] = snbr[base + lane]; sm[i] = smask[base + lane]; }
     }
-    // stage 3: which of those neighbours changed in the previous step, in which views
-    uint64_t act[kChunk];
+    // stage 3: neighbours' change words
+    uint64_t act[CH];
 #pragma unroll
-    for (int i = 0; i < kChunk; i++) act[i] = sm[i] ? (sm[i] & chg_prev[nb[i]]) : 0;
-    // stage 4: per vertex, gather + min + publish
+    for (int i = 0; i < CH; i++) act[i] = sm[i] ? (sm[i] & chg_prev[nb[i]]) : 0;
+    // stage 4a: all gathers of the chunk (loads only)
+    int32_t best[CH];
 #pragma unroll
-    for (int i = 0; i < kChunk; i++) {
+    for (int i = 0; i < CH; i++) {
+      best[i] = cur[i];
       if (!((bits >> i) & 1)) continue;
-      const uint64_t mv = readlane64(mv_l, i);
-      if (mv == 0) continue;
-      const int64_t v = v0 + i;
+      best[i] = gather_min(act[i], nb[i], cur[i], lab_cur, lane);
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
       const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
-      pv += 1;
-      ps += (unsigned long long)n;
-      int32_t best = gather_min(act[i], nb[i], cur[i], lab_cur, lane);
       for (int32_t c2 = 64; c2 < n; c2 += 64) {  // vertices with more than 64 kept slots
         const int32_t j = c2 + lane;
         uint64_t a2 = 0;
@@ -366,97 +355,30 @@ __global__ __launch_bounds__(256) void k_cc_step(int step, int64_t nv, const int
           q = snbr[base + j];
           a2 = smask[base + j] & chg_prev[q];
         }
-        best = gather_min(a2, q, best, lab_cur, lane);
-      }
-      lab_next[v * 64 + lane] = best;
-      const uint64_t ch = __ballot(best < cur[i]);
-      if (lane == 0) chg_next[v] = ch;
-      if (ch) {
-        changed++;
-        if (lane == 0) mark(act_next, (int32_t)v);
-        if (sm[i] & ch) mark(act_next, nb[i]);
-        for (int32_t c2 = 64; c2 < n; c2 += 64) {
-          const int32_t j = c2 + lane;
-          if (j < n && (smask[base + j] & ch)) mark(act_next, snbr[base + j]);
-        }
+        best[i] = gather_min(a2, q, best[i], lab_cur, lane);
       }
     }
-  }
-  if (lane == 0) {
-    if (changed) atomicAdd(&red, changed);
-    if (pv) atomicAdd(&wred[0], pv);
-    if (ps) atomicAdd(&wred[1], ps);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (red) stepflag[step] = 1;
-    add_work(work, step, wred[0], wred[1], (unsigned long long)red);
-  }
-}
-
-__global__ __launch_bounds__(256) void k_cc_step_v0(int step, int64_t nv, const int64_t* __restrict__ adj_off,
-                                                    const uint64_t* __restrict__ vm,
-                                                    const int32_t* __restrict__ cnt,
-                                                    const int32_t* __restrict__ snbr,
-                                                    const uint64_t* __restrict__ smask,
-                                                    const int32_t* __restrict__ lab_cur,
-                                                    int32_t* __restrict__ lab_next,
-                                                    const uint64_t* __restrict__ chg_prev,
-                                                    uint64_t* __restrict__ chg_next,
-                                                    const uint32_t* __restrict__ act_cur,
-                                                    uint32_t* __restrict__ act_next,
-                                                    uint32_t* __restrict__ act_clear,
-                                                    int32_t* __restrict__ stepflag,
-                                                    unsigned long long* __restrict__ work) {
-  if (stepflag[step - 1] == 0) return;
-  __shared__ int32_t red;
-  __shared__ unsigned long long wred[2];
-  if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; }
-  const int64_t nwords = (nv + 31) >> 5;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
-       i += (int64_t)gridDim.x * blockDim.x)
-    act_clear[i] = 0;
-  __syncthreads();
-  const int lane = lane_id();
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  int32_t changed = 0;
-  unsigned long long pv = 0, ps = 0;
-  for (int64_t c = wave; c * kChunk < nv; c += nwaves) {
-    const int64_t v0 = c * kChunk;
-    uint32_t bits = (act_cur[v0 >> 5] >> (v0 & 31)) & 0xffu;
-    while (bits) {
-      const int64_t v = v0 + __builtin_ctz(bits);
-      bits &= bits - 1;
-      if (v >= nv) break;
-      const uint64_t mv = vm[v];
-      const int32_t n = cnt[v];
-      const int64_t base = adj_off[v];
+    // stage 4b: publish
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+      if (!((bits >> i) & 1)) continue;
+      const uint64_t mv = readlane64(mv_l, i);
       if (mv == 0) continue;
-      const bool mine = (mv >> lane) & 1;
-      const int32_t cur = mine ? lab_cur[v * 64 + lane] : INT32_MAX;
+      const int64_t v = v0 + i;
+      const int32_t n = __builtin_amdgcn_readlane(n_l, i);
       pv += 1;
       ps += (unsigned long long)n;
-      int32_t best = cur;
-      for (int32_t c2 = 0; c2 < n; c2 += 64) {
-        const int32_t j = c2 + lane;
-        uint64_t a2 = 0;
-        int32_t q = 0;
-        if (j < n) {
-          q = snbr[base + j];
-          a2 = smask[base + j] & chg_prev[q];
-        }
-        best = gather_min(a2, q, best, lab_cur, lane);
-      }
-      lab_next[v * 64 + lane] = best;
-      const uint64_t ch = __ballot(best < cur);
+      const uint64_t ch = __ballot(best[i] < cur[i]);
+      if (ch || readlane64(cp_l, i)) lab_next[v * 64 + lane] = best[i];
       if (lane == 0) chg_next[v] = ch;
       if (ch) {
         changed++;
-        if (lane == 0) mark(act_next, (int32_t)v);
-        for (int32_t c2 = 0; c2 < n; c2 += 64) {
+        if (lane == 0) act_next[v] = 1;
+        if (sm[i] & ch) act_next[nb[i]] = 1;
+        const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
+        for (int32_t c2 = 64; c2 < n; c2 += 64) {
           const int32_t j = c2 + lane;
-          if (j < n && (smask[base + j] & ch)) mark(act_next, snbr[base + j]);
+          if (j < n && (smask[base + j] & ch)) act_next[snbr[base + j]] = 1;
         }
       }
     }
@@ -748,7 +670,7 @@ __global__ __launch_bounds__(256) void k_pr_step(int64_t nv, const int64_t* __re
 }
 
 // ---------------------------------------------------------------- launchers
-int g_step_grid = 2048;
+int g_step_grid = 4096;
 
 static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
   int64_t g = (items + per_block - 1) / per_block;
@@ -765,7 +687,7 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
 }
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
-                     int32_t* lab1, uint64_t* chg1, uint32_t* act2, int32_t* stepflag,
+                     int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      unsigned long long* work) {
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
                                                 vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
@@ -774,17 +696,17 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
-                    uint64_t* chg_next, const uint32_t* act_cur, uint32_t* act_next,
-                    uint32_t* act_clear, int32_t* stepcnt, unsigned long long* work, int variant) {
-  const unsigned grid = grid_for(g.nv, 4 * kChunk, (unsigned)g_step_grid);
-  if (variant == 1)
-    k_cc_step<<<grid, 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask,
-                                                          lab_cur, lab_next, chg_prev, chg_next,
-                                                          act_cur, act_next, act_clear, stepcnt, work);
-  else
-    k_cc_step_v0<<<grid, 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask,
-                                                             lab_cur, lab_next, chg_prev, chg_next,
-                                                             act_cur, act_next, act_clear, stepcnt, work);
+                    uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
+                    uint8_t* act_clear, int32_t* stepflag, unsigned long long* work, int variant) {
+  if (variant == 4) {
+    const unsigned grid = grid_for(g.nv, 4 * 4, (unsigned)g_step_grid);
+    k_cc_step2<4><<<grid, 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
+                                       chg_prev, chg_next, act_cur, act_next, act_clear, stepflag, work);
+  } else {
+    const unsigned grid = grid_for(g.nv, 4 * 8, (unsigned)g_step_grid);
+    k_cc_step2<8><<<grid, 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
+                                       chg_prev, chg_next, act_cur, act_next, act_clear, stepflag, work);
+  }
 }
 void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist,

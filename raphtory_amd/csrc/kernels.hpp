@@ -34,14 +34,14 @@ void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp,
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em);
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
-                     int32_t* lab1, uint64_t* chg1, uint32_t* act2, int32_t* stepflag,
+                     int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      unsigned long long* work);
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID)
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
-                    uint64_t* chg_next, const uint32_t* act_cur, uint32_t* act_next,
-                    uint32_t* act_clear, int32_t* stepcnt, unsigned long long* work, int variant);
+                    uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
+                    uint8_t* act_clear, int32_t* stepflag, unsigned long long* work, int variant);
 void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist,
                     unsigned long long* stats);

@@ -56,7 +56,7 @@ struct Slot {
   int32_t* lab[2] = {nullptr, nullptr};
   uint64_t* chg[2] = {nullptr, nullptr};
   int32_t *stepcnt = nullptr, *hist = nullptr;   // stepcnt[r] = 1 iff superstep r changed a label
-  uint32_t* act[3] = {nullptr, nullptr, nullptr};  // CC frontier bitmaps
+  uint8_t* act[3] = {nullptr, nullptr, nullptr};   // CC frontier flags (byte per vertex)
   uint64_t* vadj = nullptr;                         // OR of kept slot masks per vertex
   unsigned long long* work = nullptr;               // [step][64 shards][visited, slots, changed]
   unsigned long long* h_work = nullptr;
@@ -203,7 +203,7 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       s.chg[0] = dalloc<uint64_t>(L, nv);
       s.chg[1] = dalloc<uint64_t>(L, nv);
       s.hist = dalloc<int32_t>(L, rows);
-      for (int b = 0; b < 3; b++) s.act[b] = dalloc<uint32_t>(L, (nv + 31) / 32 + 1);
+      for (int b = 0; b < 3; b++) s.act[b] = dalloc<uint8_t>(L, (size_t)((nv + 7) / 8 + 1) * 8);
       s.vadj = dalloc<uint64_t>(L, nv);
       s.work = dalloc<unsigned long long>(L, kWorkWords);
       HIPCHK(hipMemset(s.hist, 0, sizeof(int32_t) * (rows ? rows : 1)));
@@ -321,7 +321,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
                [&] { launch_edge_mask(s.stream, g, bp, s.em); });
   if (rc.algo == RGPU_ALGO_CC) {
     for (int b = 0; b < 3; b++)
-      HIPCHK(hipMemsetAsync(s.act[b], 0, sizeof(uint32_t) * ((g.nv + 31) / 32 + 1), s.stream));
+      HIPCHK(hipMemsetAsync(s.act[b], 0, (size_t)((g.nv + 7) / 8 + 1) * 8, s.stream));
     // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
     const double b2 = g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0;
@@ -389,9 +389,12 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
         return t;
       };
       c->st.kernel_bytes[KID_SLOTS] += 12.0 * (double)wsum(1, 1);
-      const double words = (double)((c->g.nv + 31) / 32);
+      // per executed step: frontier flags read + flags two steps ahead cleared (2 B per
+      // vertex); per visited vertex vm, cnt, adj_off, own change word, label row in and out,
+      // change word out (548 B); per slot of a visited vertex nbr + mask + neighbour's change
+      // word (20 B).  Label gathers and flag stores are not counted.
       for (int r = 2; r <= s.r_final; r++)
-        c->st.kernel_bytes[KID_STEP] += 8.0 * words + 540.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1);
+        c->st.kernel_bytes[KID_STEP] += 2.0 * c->g.nv + 548.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1);
       if (!c->trace_path.empty())
         for (int r = 1; r <= s.r_final; r++)
           c->steprec.push_back({s.batch, r, wsum(r, 0), wsum(r, 1), (int)wsum(r, 2)});
@@ -407,7 +410,7 @@ int run_impl(rgpu_ctx* c, RunCfg& rc) {
   c->st.views += (int64_t)(rc.n_hops * rc.W);
   c->st.batches += (int64_t)nb;
   size_t next = 0;
-  int nslots = c->nslots;
+  int nslots = (rc.flags & RGPU_RUN_SERIAL) ? 1 : c->nslots;
   for (;;) {
     bool busy = false, progressed = false;
     for (int si = 0; si < nslots; si++) {
@@ -477,7 +480,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->nparts = num_partitions;
   c->device = device;
   c->nslots = std::max(1, std::min(2, env_int("RGPU_SLOTS", 2)));
-  c->step_variant = env_int("RGPU_STEP_VARIANT", 0);
+  c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   if (env_int("RGPU_STEP_GRID", 0) > 0) g_step_grid = env_int("RGPU_STEP_GRID", 0);
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
