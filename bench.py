@@ -51,6 +51,20 @@ def dist_env():
     return rank, world, local
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (tools/gpu_profile.sh -> profiles/latest_pmc.json), or None."""
+    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if kernel not in d.get("FETCH_SIZE", {}).get("kernel", ""):
+        return None, None
+    return round(d["traffic_bytes_per_launch"]["value"]), "profiles/latest_pmc.json: " + d["traffic_bytes_per_launch"]["formula"]
+
+
 def cpu_baseline(stream, hops, windows, budget_s, n_edges):
     """The oracle in reference structure (mode 0: lens rebuilt by linear closestTime scans every
     superstep, adjacency re-filtered on every visit), single thread, on a bounded prefix of
@@ -85,12 +99,13 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from raphtory_amd import TemporalGraph
+    from raphtory_amd.replicas import max_over_ranks, replica_hops
     from raphtory_amd.synth import BATCH_WINDOWS, DAY, HOUR, T0_README, gen_uniform, range_hops
 
     stream = gen_uniform(1, 100_000, 1_000_000)
     jump = HOUR
     base = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, jump)
-    hops = base + (rank * jump) // world  # replica r runs the grid offset by r*jump/N
+    hops = replica_hops(base, jump, rank, world)  # replica r runs the grid offset by r*jump/N
     windows = BATCH_WINDOWS
 
     g = TemporalGraph(device=local)
@@ -114,10 +129,7 @@ def main():
         g.run("cc", hops, windows)
     barrier()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(elapsed, dist, device="cuda")
     ms_per_step = elapsed * 1e3 / a.steps
     units = n_edges * len(windows) * len(hops) * world
     value = units / (ms_per_step / 1e3)
@@ -132,8 +144,10 @@ def main():
         dom = max(kstats, key=lambda k: kstats[k]["ms"])
         d = kstats[dom]
         gbs = d["bytes"] / (d["ms"] / 1e3) / 1e9
+        traffic, tsrc = pmc_traffic(dom)
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_source": tsrc,
                     "avg_launch_us": round(d["ms"] * 1e3 / d["launches"], 2),
                     "algorithmic_bytes_per_launch": d["bytes"] / d["launches"]}
 
