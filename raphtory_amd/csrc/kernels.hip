@@ -232,46 +232,43 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
 // one it will not touch (read two steps ago, written next step).
 
 // Gather the label rows of the neighbours flagged in `act` (lane = slot) and fold them into
-// `best` (lane = view); four independent loads in flight per round.
+// `best` (lane = view); four loads in flight per round.  Loads are unconditional (whole
+// rows of valid vertices) and masked afterwards with a select: a predicated load in an
+// exec-masked branch makes hipcc wait (vmcnt(0)) before the else-path writes the same
+// register, which serialises the loads.
 __device__ __forceinline__ int32_t gather_min(uint64_t act, int32_t nb, int32_t best,
                                               const int32_t* __restrict__ lab_cur, int lane) {
   uint64_t bal = __ballot(act != 0);
   while (bal) {
-    int32_t x0 = INT32_MAX, x1 = INT32_MAX, x2 = INT32_MAX, x3 = INT32_MAX;
-    int L = __builtin_ctzll(bal);
+    const int L0 = __builtin_ctzll(bal);
     bal &= bal - 1;
-    int32_t q = __builtin_amdgcn_readlane(nb, L);
-    if ((readlane64(act, L) >> lane) & 1) x0 = lab_cur[(int64_t)q * 64 + lane];
-    if (bal) {
-      L = __builtin_ctzll(bal);
-      bal &= bal - 1;
-      q = __builtin_amdgcn_readlane(nb, L);
-      if ((readlane64(act, L) >> lane) & 1) x1 = lab_cur[(int64_t)q * 64 + lane];
-    }
-    if (bal) {
-      L = __builtin_ctzll(bal);
-      bal &= bal - 1;
-      q = __builtin_amdgcn_readlane(nb, L);
-      if ((readlane64(act, L) >> lane) & 1) x2 = lab_cur[(int64_t)q * 64 + lane];
-    }
-    if (bal) {
-      L = __builtin_ctzll(bal);
-      bal &= bal - 1;
-      q = __builtin_amdgcn_readlane(nb, L);
-      if ((readlane64(act, L) >> lane) & 1) x3 = lab_cur[(int64_t)q * 64 + lane];
-    }
-    best = min(best, min(min(x0, x1), min(x2, x3)));
+    const int L1 = bal ? __builtin_ctzll(bal) : L0;
+    bal &= bal - 1;
+    const int L2 = bal ? __builtin_ctzll(bal) : L0;
+    bal &= bal - 1;
+    const int L3 = bal ? __builtin_ctzll(bal) : L0;
+    bal &= bal - 1;
+    const int32_t q0 = __builtin_amdgcn_readlane(nb, L0), q1 = __builtin_amdgcn_readlane(nb, L1);
+    const int32_t q2 = __builtin_amdgcn_readlane(nb, L2), q3 = __builtin_amdgcn_readlane(nb, L3);
+    const int32_t x0 = lab_cur[(int64_t)q0 * 64 + lane], x1 = lab_cur[(int64_t)q1 * 64 + lane];
+    const int32_t x2 = lab_cur[(int64_t)q2 * 64 + lane], x3 = lab_cur[(int64_t)q3 * 64 + lane];
+    const int32_t y0 = ((readlane64(act, L0) >> lane) & 1) ? x0 : INT32_MAX;
+    const int32_t y1 = ((readlane64(act, L1) >> lane) & 1) ? x1 : INT32_MAX;
+    const int32_t y2 = ((readlane64(act, L2) >> lane) & 1) ? x2 : INT32_MAX;
+    const int32_t y3 = ((readlane64(act, L3) >> lane) & 1) ? x3 : INT32_MAX;
+    best = min(best, min(min(y0, y1), min(y2, y3)));
   }
   return best;
 }
 
-// Variant 2 (default): frontier flags are bytes (plain idempotent stores, no RMW), and a
+// Superstep kernel.  Frontier flags are bytes (plain idempotent stores, no RMW), and a
 // wave's CH-vertex chunk runs loads-first: metadata + own change words + own label rows,
 // slot rows, neighbour change words, then every label gather of the chunk, and only then
 // the stores (rows, change words, next-frontier flags).  On CDNA stores and atomics count in
-// vmcnt, so interleaving them with the next vertex's loads would serialise the chunk.
-// A visited vertex rewrites its row only if it changed now or in the previous step (the
-// only cases where the two label buffers differ).
+// vmcnt, so interleaving them with the next vertex's loads would serialise the chunk.  All
+// loads are unconditional from padded buffers (see gather_min).  A visited vertex rewrites
+// its row only if it changed now or in the previous step (the only cases where the two
+// label buffers differ).
 template <int CH>
 __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const int64_t* __restrict__ adj_off,
                                                   const uint64_t* __restrict__ vm,
@@ -312,56 +309,56 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     }
     if (v0 + CH > nv) bits &= (1u << (nv - v0)) - 1;
     if (!bits) continue;
-    // stage 1: metadata, own change word of the previous step, own label rows
+    // stage 1: metadata (lane i -> vertex v0+i), own change words, own label rows
+    const int64_t vl = v0 + (lane & (CH - 1));
     const bool okl = lane < CH && ((bits >> lane) & 1);
-    const uint64_t mv_l = okl ? vm[v0 + lane] : 0;
-    const int32_t n_l = okl ? cnt[v0 + lane] : 0;
-    const int64_t b_l = okl ? adj_off[v0 + lane] : 0;
-    const uint64_t cp_l = okl ? chg_prev[v0 + lane] : 0;
+    const uint64_t mv_l = okl ? vm[vl] : 0;
+    const int32_t n_l = okl ? cnt[vl] : 0;
+    const int64_t b_l = adj_off[vl];
+    const uint64_t cp_l = chg_prev[vl];
     int32_t cur[CH];
 #pragma unroll
-    for (int i = 0; i < CH; i++)
-      cur[i] = (((bits >> i) & 1) && ((readlane64(mv_l, i) >> lane) & 1)) ? lab_cur[(v0 + i) * 64 + lane]
-                                                                        : INT32_MAX;
-    // stage 2: first 64 kept slots of each vertex
+    for (int i = 0; i < CH; i++) cur[i] = lab_cur[(v0 + i) * 64 + lane];
+    // stage 2: first 64 kept slots of each vertex (clamped loads, masked by select)
     int32_t nb[CH];
     uint64_t sm[CH];
 #pragma unroll
     for (int i = 0; i < CH; i++) {
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
       const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
-      nb[i] = 0;
-      sm[i] = 0;
-      if (lane < n) { nb[i] = snbr[base + lane]; sm[i] = smask[base + lane]; }
+      const int64_t idx = base + (lane < n ? lane : 0);
+      const int32_t q = snbr[idx];
+      const uint64_t m = smask[idx];
+      nb[i] = lane < n ? q : 0;
+      sm[i] = lane < n ? m : 0;
     }
-    // stage 3: neighbours' change words
+    // stage 3: neighbours' change words (vertex 0's word for idle lanes, masked by sm = 0)
     uint64_t act[CH];
 #pragma unroll
-    for (int i = 0; i < CH; i++) act[i] = sm[i] ? (sm[i] & chg_prev[nb[i]]) : 0;
+    for (int i = 0; i < CH; i++) act[i] = sm[i] & chg_prev[nb[i]];
+    // own rows are only meaningful on member lanes
+#pragma unroll
+    for (int i = 0; i < CH; i++) cur[i] = ((readlane64(mv_l, i) >> lane) & 1) ? cur[i] : INT32_MAX;
     // stage 4a: all gathers of the chunk (loads only)
     int32_t best[CH];
 #pragma unroll
     for (int i = 0; i < CH; i++) {
-      best[i] = cur[i];
-      if (!((bits >> i) & 1)) continue;
       best[i] = gather_min(act[i], nb[i], cur[i], lab_cur, lane);
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
-      const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
-      for (int32_t c2 = 64; c2 < n; c2 += 64) {  // vertices with more than 64 kept slots
-        const int32_t j = c2 + lane;
-        uint64_t a2 = 0;
-        int32_t q = 0;
-        if (j < n) {
-          q = snbr[base + j];
-          a2 = smask[base + j] & chg_prev[q];
+      if (n > 64) {  // vertices with more than 64 kept slots
+        const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
+        for (int32_t c2 = 64; c2 < n; c2 += 64) {
+          const int32_t j = c2 + lane;
+          const int64_t idx = base + (j < n ? j : c2);
+          const int32_t q = snbr[idx];
+          const uint64_t a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
+          best[i] = gather_min(a2, q, best[i], lab_cur, lane);
         }
-        best[i] = gather_min(a2, q, best[i], lab_cur, lane);
       }
     }
     // stage 4b: publish
 #pragma unroll
     for (int i = 0; i < CH; i++) {
-      if (!((bits >> i) & 1)) continue;
       const uint64_t mv = readlane64(mv_l, i);
       if (mv == 0) continue;
       const int64_t v = v0 + i;
@@ -375,10 +372,12 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
         changed++;
         if (lane == 0) act_next[v] = 1;
         if (sm[i] & ch) act_next[nb[i]] = 1;
-        const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
-        for (int32_t c2 = 64; c2 < n; c2 += 64) {
-          const int32_t j = c2 + lane;
-          if (j < n && (smask[base + j] & ch)) act_next[snbr[base + j]] = 1;
+        if (n > 64) {
+          const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
+          for (int32_t c2 = 64; c2 < n; c2 += 64) {
+            const int32_t j = c2 + lane;
+            if (j < n && (smask[base + j] & ch)) act_next[snbr[base + j]] = 1;
+          }
         }
       }
     }

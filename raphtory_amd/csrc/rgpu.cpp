@@ -46,6 +46,8 @@ enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUM
 constexpr int kMaxSteps = 128;
 constexpr int kStatWords = 7 * kViews;  // 6 per-view fields + counters row
 constexpr int kWorkWords = kMaxSteps * 64 * 3;
+constexpr int64_t kPad = 64;  // tail padding of per-vertex / per-slot batch arrays
+constexpr int kMaxSlots = 4;  // batches in flight (one HIP stream each; GPU_MAX_HW_QUEUES = 4)
 
 struct Slot {
   hipStream_t stream = nullptr;
@@ -69,6 +71,7 @@ struct Slot {
   unsigned long long* h_stats = nullptr;
   // state of the batch in flight
   int batch = -1, phase = 0, r_launched = 0, r_final = 0, kb = 0;
+  uint64_t evseq = 0;  // order in which slot events were recorded (wait on the oldest)
 };
 
 struct Retained {  // per batch, RGPU_RUN_RETAIN
@@ -97,7 +100,7 @@ struct rgpu_ctx {
   Packed pk;
   DevGraph g;
   std::vector<void*> graph_allocs;
-  Slot slot[2];
+  Slot slot[kMaxSlots];
   int nslots = 2;
   int step_variant = 0;                 // RGPU_STEP_VARIANT: 0 per-vertex chain, 1 chunk-pipelined
   std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
@@ -116,6 +119,7 @@ struct rgpu_ctx {
   bool profile = false;
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
+  uint64_t evcounter = 0;
   std::vector<Timed> timed;
 };
 
@@ -181,7 +185,7 @@ void ensure_slots(rgpu_ctx* c, int algo) {
   auto& L = c->graph_allocs;
   const int64_t nv = c->g.nv, ne = c->g.ne, nin = c->g.n_in;
   const size_t rows = (size_t)nv * kViews;
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < c->nslots; i++) {
     Slot& s = c->slot[i];
     if (!s.stream) {
       HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
@@ -189,19 +193,23 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       HIPCHK(hipHostMalloc((void**)&s.h_stepcnt, sizeof(int32_t) * kMaxSteps));
       HIPCHK(hipHostMalloc((void**)&s.h_stats, sizeof(unsigned long long) * kStatWords));
       HIPCHK(hipHostMalloc((void**)&s.h_work, sizeof(unsigned long long) * kWorkWords));
-      s.vm = dalloc<uint64_t>(L, nv);
+      s.vm = dalloc<uint64_t>(L, nv + kPad);
       s.em = dalloc<uint64_t>(L, ne);
       s.stepcnt = dalloc<int32_t>(L, kMaxSteps);
       s.stats = dalloc<unsigned long long>(L, kStatWords);
     }
     if (algo == RGPU_ALGO_CC && !c->slot_cc) {
-      s.cnt = dalloc<int32_t>(L, nv);
-      s.snbr = dalloc<int32_t>(L, ne + nin);
-      s.smask = dalloc<uint64_t>(L, ne + nin);
-      s.lab[0] = dalloc<int32_t>(L, rows);
-      s.lab[1] = dalloc<int32_t>(L, rows);
-      s.chg[0] = dalloc<uint64_t>(L, nv);
-      s.chg[1] = dalloc<uint64_t>(L, nv);
+      // padded so that the superstep kernel's clamped, unconditional loads stay in bounds
+      s.cnt = dalloc<int32_t>(L, nv + kPad);
+      s.snbr = dalloc<int32_t>(L, ne + nin + kPad);
+      s.smask = dalloc<uint64_t>(L, ne + nin + kPad);
+      s.lab[0] = dalloc<int32_t>(L, rows + kPad * kViews);
+      s.lab[1] = dalloc<int32_t>(L, rows + kPad * kViews);
+      s.chg[0] = dalloc<uint64_t>(L, nv + kPad);
+      s.chg[1] = dalloc<uint64_t>(L, nv + kPad);
+      HIPCHK(hipMemset(s.chg[0], 0, sizeof(uint64_t) * (nv + kPad)));
+      HIPCHK(hipMemset(s.chg[1], 0, sizeof(uint64_t) * (nv + kPad)));
+      HIPCHK(hipMemset(s.snbr, 0, sizeof(int32_t) * (ne + nin + kPad)));
       s.hist = dalloc<int32_t>(L, rows);
       for (int b = 0; b < 3; b++) s.act[b] = dalloc<uint8_t>(L, (size_t)((nv + 7) / 8 + 1) * 8);
       s.vadj = dalloc<uint64_t>(L, nv);
@@ -258,6 +266,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     HIPCHK(hipMemcpyAsync(s.h_work, s.work, sizeof(unsigned long long) * kWorkWords,
                           hipMemcpyDeviceToHost, s.stream));
   HIPCHK(hipEventRecord(s.ev, s.stream));
+  s.evseq = ++c->evcounter;
   s.phase = 1;
 }
 
@@ -292,6 +301,7 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
     }
   }
   HIPCHK(hipEventRecord(s.ev, s.stream));
+  s.evseq = ++c->evcounter;
   s.phase = 2;
 }
 
@@ -443,8 +453,10 @@ int run_impl(rgpu_ctx* c, RunCfg& rc) {
     if (!busy) break;
     if (!progressed) {
       // nothing ready: block on the slot whose pending event is oldest (slot order is fine)
+      int oldest = -1;
       for (int si = 0; si < nslots; si++)
-        if (c->slot[si].phase != 0) { HIPCHK(hipEventSynchronize(c->slot[si].ev)); break; }
+        if (c->slot[si].phase != 0 && (oldest < 0 || c->slot[si].evseq < c->slot[oldest].evseq)) oldest = si;
+      if (oldest >= 0) HIPCHK(hipEventSynchronize(c->slot[oldest].ev));
     }
   }
   return 0;
@@ -479,7 +491,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->part = partition_id;
   c->nparts = num_partitions;
   c->device = device;
-  c->nslots = std::max(1, std::min(2, env_int("RGPU_SLOTS", 2)));
+  c->nslots = std::max(1, std::min(kMaxSlots, env_int("RGPU_SLOTS", 3)));
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   if (env_int("RGPU_STEP_GRID", 0) > 0) g_step_grid = env_int("RGPU_STEP_GRID", 0);
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
@@ -533,8 +545,9 @@ int rgpu_seal(rgpu_ctx* c) {
     g.out_off = dupload(L, P.out_off);
     g.in_off = dupload(L, P.in_off);
     {
-      std::vector<int64_t> adj(P.nv + 1);
+      std::vector<int64_t> adj(P.nv + 1 + 64);  // padded: read unconditionally by the step kernel
       for (int64_t v = 0; v <= P.nv; v++) adj[v] = P.out_off[v] + P.in_off[v];
+      for (int64_t v = P.nv + 1; v < (int64_t)adj.size(); v++) adj[v] = adj[P.nv];
       g.adj_off = dupload(L, adj);
     }
     g.in_eid = dupload(L, P.in_eid);
@@ -628,7 +641,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->st.views = c->st.batches = c->st.supersteps = 0;
     auto t0 = std::chrono::steady_clock::now();
     run_impl(c, rc);
-    for (int si = 0; si < 2; si++)
+    for (int si = 0; si < kMaxSlots; si++)
       if (c->slot[si].stream) HIPCHK(hipStreamSynchronize(c->slot[si].stream));
     auto t1 = std::chrono::steady_clock::now();
     c->st.ms_total = std::chrono::duration<double, std::milli>(t1 - t0).count();
