@@ -33,6 +33,25 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// ---------------------------------------------------------------- label-row access
+// A label row is 64 lanes x 4 B = 256 B (four 64-B lines).  Rows are read and written
+// through a per-row buffer descriptor (the row base is wave-uniform): a lane that must not
+// touch memory gets an out-of-range offset, so it reads 0 / writes nothing with no memory
+// traffic and no exec-masked branch (a branchy predicated load makes hipcc wait vmcnt(0)
+// before the other path writes the same register).  Stores cover whole 64-B lines of the
+// lanes that matter, never partial lines (a partial-line store costs a fill).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const int32_t* row) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)row, (short)0, 256, 0x00020000);
+}
+__device__ __forceinline__ int32_t row_load(const int32_t* row, bool on, int lane) {
+  return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(row_rsrc(row), on ? lane * 4 : 0x7fffffff, 0, 0);
+}
+__device__ __forceinline__ void row_store(int32_t* row, int32_t x, bool on, int lane) {
+  __builtin_amdgcn_raw_buffer_store_b32(x, row_rsrc(row), on ? lane * 4 : 0x7fffffff, 0, 0);
+}
+// lanes of the 64-B lines (16 lanes each) that hold at least one view of mask m
+__device__ __forceinline__ bool line_has(uint64_t m, int lane) { return ((m >> (lane & 48)) & 0xffffull) != 0; }
+
 // floor(t) of a sorted key list (key = time*2 + alive): index of the last key <= 2t+1, or -1.
 __device__ __forceinline__ int64_t floor_idx(const int64_t* key, int64_t lo, int64_t hi, int64_t t) {
   const int64_t probe = 2 * t + 1;
@@ -54,16 +73,46 @@ __device__ __forceinline__ int64_t last_death(const int64_t* dt, int64_t lo, int
 }
 
 // ---------------------------------------------------------------- K1: window masks
+// Advance a floor index to hop time t (hops of a batch ascend when bp.sorted): step forward
+// while the next key is <= 2t+1; after 8 steps fall back to a binary search of the rest.
+__device__ __forceinline__ int64_t floor_advance(const int64_t* key, int64_t f, int64_t lo, int64_t hi,
+                                                 int64_t t) {
+  const int64_t probe = 2 * t + 1;
+  int64_t g = f < lo ? lo : f + 1;  // first candidate after the current floor
+  for (int s = 0; s < 8; s++) {
+    if (g >= hi || key[g] > probe) return g - 1 >= lo ? g - 1 : -1;
+    g++;
+  }
+  return floor_idx(key, g, hi, t) >= 0 ? floor_idx(key, g, hi, t) : g - 1;
+}
+__device__ __forceinline__ int64_t death_advance(const int64_t* dt, int64_t p, int64_t hi, int64_t t) {
+  // p = index of the first death time > previous hop; returns first index with time > t
+  while (p < hi && dt[p] <= t) p++;
+  return p;
+}
+
+// The first kernel of every batch also clears the batch's small state (stats words, superstep
+// flags, frontier flags), so a batch needs no memset launches.
 __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* __restrict__ voff,
                                                      const int64_t* __restrict__ vkey, BatchParams bp,
-                                                     uint64_t* __restrict__ vm) {
+                                                     uint64_t* __restrict__ vm, BatchClear clr) {
+  {
+    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = tid; i < clr.n_stats; i += nth) clr.stats[i] = 0;
+    for (int64_t i = tid; i < clr.n_flags; i += nth) clr.flags[i] = 0;
+    for (int b = 0; b < 3; b++)
+      if (clr.act[b])
+        for (int64_t i = tid; i < clr.n_act_words; i += nth) reinterpret_cast<uint64_t*>(clr.act[b])[i] = 0;
+  }
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv;
        v += (int64_t)gridDim.x * blockDim.x) {
     const int64_t lo = voff[v], hi = voff[v + 1];
     uint64_t m = 0;
+    int64_t f = -1;
     for (int k = 0; k < bp.K; k++) {
       const int64_t t = bp.hop[k];
-      const int64_t f = floor_idx(vkey, lo, hi, t);
+      f = (bp.sorted && k > 0) ? floor_advance(vkey, f, lo, hi, t) : floor_idx(vkey, lo, hi, t);
       if (f < 0) continue;
       const int64_t key = vkey[f];
       if (!(key & 1)) continue;  // floor is a deletion
@@ -88,16 +137,31 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
     const int32_t s = esrc[e], d = edst[e];
     const int64_t s0 = doff[s], s1 = doff[s + 1], d0 = doff[d], d1 = doff[d + 1];
     uint64_t m = 0;
+    int64_t f = -1, ps = s0, pd = d0;
     for (int k = 0; k < bp.K; k++) {
       const int64_t t = bp.hop[k];
-      const int64_t f = floor_idx(ekey, lo, hi, t);
+      int64_t lds, ldd;  // last death time <= t of src / dst (-1: none)
+      if (bp.sorted && k > 0) {
+        f = floor_advance(ekey, f, lo, hi, t);
+        ps = death_advance(dtime, ps, s1, t);
+        pd = death_advance(dtime, pd, d1, t);
+        lds = ps > s0 ? dtime[ps - 1] : -1;
+        ldd = pd > d0 ? dtime[pd - 1] : -1;
+      } else {
+        f = floor_idx(ekey, lo, hi, t);
+        lds = s1 > s0 ? last_death(dtime, s0, s1, t) : -1;
+        ldd = d1 > d0 ? last_death(dtime, d0, d1, t) : -1;
+        if (bp.sorted) {  // k == 0: position the death cursors
+          ps = death_advance(dtime, s0, s1, t);
+          pd = death_advance(dtime, d0, d1, t);
+        }
+      }
       if (f < 0) continue;
       const int64_t key = ekey[f];
       if (!(key & 1)) continue;
       const int64_t ft = key >> 1;
       // an endpoint death in (ft, t] is a later kill point (killList / vertexRemoval)
-      if (s1 > s0 && last_death(dtime, s0, s1, t) > ft) continue;
-      if (d1 > d0 && last_death(dtime, d0, d1, t) > ft) continue;
+      if (lds > ft || ldd > ft) continue;
       const int64_t age = t - ft;
       for (int w = 0; w < bp.W; w++)
         if (age <= bp.thr_e[w]) m |= 1ull << (w * bp.KS + k);
@@ -148,6 +212,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
                                                   int32_t* __restrict__ lab0, int32_t* __restrict__ lab1,
                                                   uint64_t* __restrict__ chg1, uint8_t* __restrict__ act2,
                                                   int32_t* __restrict__ stepflag,
+                                                  int32_t* __restrict__ hostflag,
                                                   unsigned long long* __restrict__ work) {
   __shared__ unsigned long long red[3];
   if (threadIdx.x < 3) red[threadIdx.x] = 0;
@@ -163,7 +228,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
       if (lane == 0) { cnt[v] = 0; vadj[v] = 0; }
       continue;
     }
-    lab0[v * 64 + lane] = (int32_t)v;  // whole rows: partial-line stores cost a fill
+    row_store(lab0 + v * 64, (int32_t)v, line_has(mv, lane), lane);
     const int64_t nout = o1 - o0, ntot = nout + (i1 - i0), base = o0 + i0;
     int32_t count = 0, best = (int32_t)v;
     uint64_t any = 0;
@@ -193,7 +258,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
         if (((mL >> lane) & 1) && q < best) best = q;
       }
     }
-    lab1[v * 64 + lane] = best;
+    row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
     const uint64_t ch = __ballot(best < (int32_t)v);
     if (lane == 0) { cnt[v] = count; vadj[v] = any; chg1[v] = ch; }
     if (ch) {
@@ -214,7 +279,10 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (red[2]) stepflag[1] = 1;
+    if (red[2] && stepflag[1] == 0) {
+      stepflag[1] = 1;
+      if (hostflag) hostflag[1] = 1;
+    }
     add_work(work, 1, red[0], red[1], red[2]);
   }
 }
@@ -232,10 +300,15 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
 // one it will not touch (read two steps ago, written next step).
 
 // Gather the label rows of the neighbours flagged in `act` (lane = slot) and fold them into
-// `best` (lane = view); four loads in flight per round.  Loads are unconditional (whole
-// rows of valid vertices) and masked afterwards with a select: a predicated load in an
-// exec-masked branch makes hipcc wait (vmcnt(0)) before the else-path writes the same
-// register, which serialises the loads.
+// `best` (lane = view); four row loads in flight per round, each touching only the lanes
+// (views) in which that neighbour changed (row_load).
+template <bool BUF>
+__device__ __forceinline__ int32_t row_get(const int32_t* row, bool on, int lane) {
+  if (BUF) return row_load(row, on, lane);
+  return row[lane];  // whole-row load, masked by the caller's select
+}
+
+template <bool BUF>
 __device__ __forceinline__ int32_t gather_min(uint64_t act, int32_t nb, int32_t best,
                                               const int32_t* __restrict__ lab_cur, int lane) {
   uint64_t bal = __ballot(act != 0);
@@ -250,12 +323,14 @@ __device__ __forceinline__ int32_t gather_min(uint64_t act, int32_t nb, int32_t 
     bal &= bal - 1;
     const int32_t q0 = __builtin_amdgcn_readlane(nb, L0), q1 = __builtin_amdgcn_readlane(nb, L1);
     const int32_t q2 = __builtin_amdgcn_readlane(nb, L2), q3 = __builtin_amdgcn_readlane(nb, L3);
-    const int32_t x0 = lab_cur[(int64_t)q0 * 64 + lane], x1 = lab_cur[(int64_t)q1 * 64 + lane];
-    const int32_t x2 = lab_cur[(int64_t)q2 * 64 + lane], x3 = lab_cur[(int64_t)q3 * 64 + lane];
-    const int32_t y0 = ((readlane64(act, L0) >> lane) & 1) ? x0 : INT32_MAX;
-    const int32_t y1 = ((readlane64(act, L1) >> lane) & 1) ? x1 : INT32_MAX;
-    const int32_t y2 = ((readlane64(act, L2) >> lane) & 1) ? x2 : INT32_MAX;
-    const int32_t y3 = ((readlane64(act, L3) >> lane) & 1) ? x3 : INT32_MAX;
+    const bool o0 = (readlane64(act, L0) >> lane) & 1, o1 = (readlane64(act, L1) >> lane) & 1;
+    const bool o2 = (readlane64(act, L2) >> lane) & 1, o3 = (readlane64(act, L3) >> lane) & 1;
+    const int32_t x0 = row_get<BUF>(lab_cur + (int64_t)q0 * 64, o0, lane);
+    const int32_t x1 = row_get<BUF>(lab_cur + (int64_t)q1 * 64, o1, lane);
+    const int32_t x2 = row_get<BUF>(lab_cur + (int64_t)q2 * 64, o2, lane);
+    const int32_t x3 = row_get<BUF>(lab_cur + (int64_t)q3 * 64, o3, lane);
+    const int32_t y0 = o0 ? x0 : INT32_MAX, y1 = o1 ? x1 : INT32_MAX;
+    const int32_t y2 = o2 ? x2 : INT32_MAX, y3 = o3 ? x3 : INT32_MAX;
     best = min(best, min(min(y0, y1), min(y2, y3)));
   }
   return best;
@@ -269,7 +344,7 @@ __device__ __forceinline__ int32_t gather_min(uint64_t act, int32_t nb, int32_t 
 // loads are unconditional from padded buffers (see gather_min).  A visited vertex rewrites
 // its row only if it changed now or in the previous step (the only cases where the two
 // label buffers differ).
-template <int CH>
+template <int CH, bool BUF>
 __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const int64_t* __restrict__ adj_off,
                                                   const uint64_t* __restrict__ vm,
                                                   const int32_t* __restrict__ cnt,
@@ -283,6 +358,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
                                                   uint8_t* __restrict__ act_next,
                                                   uint8_t* __restrict__ act_clear,
                                                   int32_t* __restrict__ stepflag,
+                                                  int32_t* __restrict__ hostflag,
                                                   unsigned long long* __restrict__ work) {
   if (stepflag[step - 1] == 0) return;
   __shared__ int32_t red;
@@ -318,7 +394,8 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     const uint64_t cp_l = chg_prev[vl];
     int32_t cur[CH];
 #pragma unroll
-    for (int i = 0; i < CH; i++) cur[i] = lab_cur[(v0 + i) * 64 + lane];
+    for (int i = 0; i < CH; i++)
+      cur[i] = row_get<BUF>(lab_cur + (v0 + i) * 64, (readlane64(mv_l, i) >> lane) & 1, lane);
     // stage 2: first 64 kept slots of each vertex (clamped loads, masked by select)
     int32_t nb[CH];
     uint64_t sm[CH];
@@ -343,7 +420,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     int32_t best[CH];
 #pragma unroll
     for (int i = 0; i < CH; i++) {
-      best[i] = gather_min(act[i], nb[i], cur[i], lab_cur, lane);
+      best[i] = gather_min<BUF>(act[i], nb[i], cur[i], lab_cur, lane);
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
       if (n > 64) {  // vertices with more than 64 kept slots
         const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
@@ -352,7 +429,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
           const int64_t idx = base + (j < n ? j : c2);
           const int32_t q = snbr[idx];
           const uint64_t a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
-          best[i] = gather_min(a2, q, best[i], lab_cur, lane);
+          best[i] = gather_min<BUF>(a2, q, best[i], lab_cur, lane);
         }
       }
     }
@@ -366,7 +443,10 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
       pv += 1;
       ps += (unsigned long long)n;
       const uint64_t ch = __ballot(best[i] < cur[i]);
-      if (ch || readlane64(cp_l, i)) lab_next[v * 64 + lane] = best[i];
+      if (ch || readlane64(cp_l, i)) {
+        if (BUF) row_store(lab_next + v * 64, best[i], line_has(mv, lane), lane);
+        else lab_next[v * 64 + lane] = best[i];
+      }
       if (lane == 0) chg_next[v] = ch;
       if (ch) {
         changed++;
@@ -389,7 +469,10 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (red) stepflag[step] = 1;
+    if (red && stepflag[step] == 0) {  // first writers also tell the host (mapped pinned memory)
+      stepflag[step] = 1;
+      if (hostflag) hostflag[step] = 1;
+    }
     add_work(work, step, wred[0], wred[1], (unsigned long long)red);
   }
 }
@@ -401,6 +484,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
 // that carry it): the giant component costs one atomic per 64 vertices, not one per vertex.
 // Members with no kept slot in a view are isolated there: islands (count 1) that need no
 // histogram entry; they are added to total / sum / biggest directly.
+template <bool BUF>
 __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int nviews, const uint64_t* __restrict__ vm,
                                                  const uint64_t* __restrict__ vadj,
                                                  const int32_t* __restrict__ lab,
@@ -419,7 +503,14 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int nviews, const u
     for (int i0 = 0; i0 < 64; i0 += 16) {  // 16 independent row loads in flight, then LDS
       int32_t r[16];
 #pragma unroll
-      for (int k = 0; k < 16; k++) r[k] = i0 + k < nvc ? lab[(v0 + i0 + k) * 64 + lane] : 0;
+      for (int k = 0; k < 16; k++) {
+        if (BUF) {
+          const uint64_t mk = i0 + k < nvc ? vm[v0 + i0 + k] : 0;  // scalar: wave-uniform vertex
+          r[k] = row_load(lab + (v0 + i0 + k) * 64, (mk >> lane) & 1, lane);
+        } else {
+          r[k] = i0 + k < nvc ? lab[(v0 + i0 + k) * 64 + lane] : 0;
+        }
+      }
 #pragma unroll
       for (int k = 0; k < 16; k++) tile[wib][i0 + k][lane] = r[k];
     }
@@ -670,6 +761,7 @@ __global__ __launch_bounds__(256) void k_pr_step(int64_t nv, const int64_t* __re
 
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 4096;
+int g_rowbuf = 0;
 
 static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
   int64_t g = (items + per_block - 1) / per_block;
@@ -677,8 +769,9 @@ static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
   return (unsigned)(g > cap ? cap : g);
 }
 
-void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm) {
-  k_vertex_mask<<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm);
+void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm,
+                        const BatchClear& clr) {
+  k_vertex_mask<<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm, clr);
 }
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em) {
   k_edge_mask<<<grid_for(g.ne, 256), 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff,
@@ -687,30 +780,33 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
-                     unsigned long long* work) {
+                     int32_t* hostflag, unsigned long long* work) {
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
                                                 vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
-                                                stepflag, work);
+                                                stepflag, hostflag, work);
 }
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
-                    uint8_t* act_clear, int32_t* stepflag, unsigned long long* work, int variant) {
-  if (variant == 4) {
-    const unsigned grid = grid_for(g.nv, 4 * 4, (unsigned)g_step_grid);
-    k_cc_step2<4><<<grid, 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
-                                       chg_prev, chg_next, act_cur, act_next, act_clear, stepflag, work);
-  } else {
-    const unsigned grid = grid_for(g.nv, 4 * 8, (unsigned)g_step_grid);
-    k_cc_step2<8><<<grid, 256, 0, s>>>(step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
-                                       chg_prev, chg_next, act_cur, act_next, act_clear, stepflag, work);
-  }
+                    uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
+                    unsigned long long* work, int variant) {
+  const int ch = (variant & 15) == 8 ? 8 : 4;
+  const bool buf = (variant & 16) != 0;
+  const unsigned grid = grid_for(g.nv, 4 * ch, (unsigned)g_step_grid);
+#define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
+    act_cur, act_next, act_clear, stepflag, hostflag, work
+  if (ch == 8 && buf) k_cc_step2<8, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else if (ch == 8) k_cc_step2<8, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else if (buf) k_cc_step2<4, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else k_cc_step2<4, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+#undef RGPU_STEP_ARGS
 }
 void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist,
                     unsigned long long* stats) {
-  k_cc_hist<<<grid_for(g.nv, 4 * 64, 512), 256, 0, s>>>(g.nv, nviews, vm, vadj, lab, hist, stats);
+  if (g_rowbuf) k_cc_hist<true><<<grid_for(g.nv, 4 * 64, 512), 256, 0, s>>>(g.nv, nviews, vm, vadj, lab, hist, stats);
+  else k_cc_hist<false><<<grid_for(g.nv, 4 * 64, 512), 256, 0, s>>>(g.nv, nviews, vm, vadj, lab, hist, stats);
 }
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
                        unsigned long long* stats) {

@@ -13,6 +13,7 @@ constexpr int kViews = 64;  // views per batch = wavefront width (lane j <-> vie
 // views a vertex belongs to (the long windows) in the low lanes of its label row.
 struct BatchParams {
   int K, W, KS;
+  int sorted;             // hop[] ascending: K1 advances floors instead of searching per hop
   int64_t hop[kViews];    // view timestamps (RangeAnalysisTask hop times)
   int64_t thr_v[kViews];  // vertex-set window of window index w: min(w_0..w_w)  (shrinkWindow)
   int64_t thr_e[kViews];  // edge window of window index w: w_w (viewAtWithWindow(t, setWindow))
@@ -30,18 +31,31 @@ struct DevGraph {
   const int32_t* in_eid = nullptr;
 };
 
-void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm);
+// Small per-batch state cleared by the first kernel of the batch (no memset launches).
+struct BatchClear {
+  unsigned long long* stats = nullptr;
+  int64_t n_stats = 0;
+  int32_t* flags = nullptr;
+  int64_t n_flags = 0;
+  uint8_t* act[3] = {nullptr, nullptr, nullptr};
+  int64_t n_act_words = 0;  // uint64 words per act buffer
+};
+
+void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm,
+                        const BatchClear& clr);
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em);
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
-                     unsigned long long* work);
+                     int32_t* hostflag, unsigned long long* work);
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID)
+extern int g_rowbuf;     // label rows via buffer descriptors (RGPU_ROWBUF)
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
-                    uint8_t* act_clear, int32_t* stepflag, unsigned long long* work, int variant);
+                    uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
+                    unsigned long long* work, int variant);
 void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist,
                     unsigned long long* stats);

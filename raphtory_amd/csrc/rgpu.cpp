@@ -67,7 +67,8 @@ struct Slot {
   double *pr = nullptr, *contrib[2] = {nullptr, nullptr};
   int32_t *pcnt = nullptr, *psnbr = nullptr;
   uint64_t* psmask = nullptr;
-  int32_t* h_stepcnt = nullptr;
+  int32_t* h_stepcnt = nullptr;   // host-mapped superstep flags, written by the kernels
+  int32_t* d_hostflag = nullptr;  // device address of h_stepcnt
   unsigned long long* h_stats = nullptr;
   // state of the batch in flight
   int batch = -1, phase = 0, r_launched = 0, r_final = 0, kb = 0;
@@ -102,6 +103,7 @@ struct rgpu_ctx {
   std::vector<void*> graph_allocs;
   Slot slot[kMaxSlots];
   int nslots = 2;
+  bool hostflags = true;                // superstep flags via host-mapped memory (else copies)
   int step_variant = 0;                 // RGPU_STEP_VARIANT: 0 per-vertex chain, 1 chunk-pipelined
   std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
   struct StepRec { int batch, step; unsigned long long pv, ps; int changed; };
@@ -190,7 +192,8 @@ void ensure_slots(rgpu_ctx* c, int algo) {
     if (!s.stream) {
       HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
       HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
-      HIPCHK(hipHostMalloc((void**)&s.h_stepcnt, sizeof(int32_t) * kMaxSteps));
+      HIPCHK(hipHostMalloc((void**)&s.h_stepcnt, sizeof(int32_t) * kMaxSteps, hipHostMallocMapped));
+      HIPCHK(hipHostGetDevicePointer((void**)&s.d_hostflag, s.h_stepcnt, 0));
       HIPCHK(hipHostMalloc((void**)&s.h_stats, sizeof(unsigned long long) * kStatWords));
       HIPCHK(hipHostMalloc((void**)&s.h_work, sizeof(unsigned long long) * kWorkWords));
       s.vm = dalloc<uint64_t>(L, nv + kPad);
@@ -256,12 +259,14 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                      s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
-                     s.act[(r + 2) % 3], s.stepcnt, c->profile ? s.work : nullptr, c->step_variant);
+                     s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
+                     c->profile ? s.work : nullptr, c->step_variant | (g_rowbuf ? 16 : 0));
     }, r);
   }
   s.r_launched = last;
-  HIPCHK(hipMemcpyAsync(s.h_stepcnt, s.stepcnt, sizeof(int32_t) * kMaxSteps, hipMemcpyDeviceToHost,
-                        s.stream));
+  if (!c->hostflags)
+    HIPCHK(hipMemcpyAsync(s.h_stepcnt, s.stepcnt, sizeof(int32_t) * kMaxSteps, hipMemcpyDeviceToHost,
+                          s.stream));
   if (c->profile)
     HIPCHK(hipMemcpyAsync(s.h_work, s.work, sizeof(unsigned long long) * kWorkWords,
                           hipMemcpyDeviceToHost, s.stream));
@@ -314,30 +319,41 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   bp.K = (int)std::min<size_t>(rc.K, rc.n_hops - h0);
   bp.W = rc.W;
   bp.KS = rc.K;
-  for (int k = 0; k < bp.K; k++) bp.hop[k] = rc.hops[h0 + k];
+  bp.sorted = 1;
+  for (int k = 0; k < bp.K; k++) {
+    bp.hop[k] = rc.hops[h0 + k];
+    if (k > 0 && bp.hop[k] < bp.hop[k - 1]) bp.sorted = 0;
+  }
   for (int w = 0; w < rc.W; w++) { bp.thr_v[w] = rc.thr_v[w]; bp.thr_e[w] = rc.thr_e[w]; }
   s.batch = b;
   s.kb = bp.K;
   s.r_launched = 0;
   s.r_final = 0;
-  HIPCHK(hipMemsetAsync(s.stats, 0, sizeof(unsigned long long) * kStatWords, s.stream));
-  HIPCHK(hipMemsetAsync(s.stepcnt, 0, sizeof(int32_t) * kMaxSteps, s.stream));
+  std::memset(s.h_stepcnt, 0, sizeof(int32_t) * kMaxSteps);  // slot idle: no kernel writes it
+  BatchClear clr;
+  clr.stats = s.stats;
+  clr.n_stats = kStatWords;
+  clr.flags = s.stepcnt;
+  clr.n_flags = kMaxSteps;
+  if (rc.algo == RGPU_ALGO_CC) {
+    for (int b = 0; b < 3; b++) clr.act[b] = s.act[b];
+    clr.n_act_words = (g.nv + 7) / 8 + 1;
+  }
   if (s.work && c->profile)
     HIPCHK(hipMemsetAsync(s.work, 0, sizeof(unsigned long long) * kWorkWords, s.stream));
   const double bm = bytes_mask(g);
   timed_launch(c, si, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.vkey.size() + 8.0 * g.nv,
-               [&] { launch_vertex_mask(s.stream, g, bp, s.vm); });
+               [&] { launch_vertex_mask(s.stream, g, bp, s.vm, clr); });
   timed_launch(c, si, KID_MASK, bm - (16.0 * g.nv + 8.0) + 8.0 * c->pk.ekey.size(),
                [&] { launch_edge_mask(s.stream, g, bp, s.em); });
   if (rc.algo == RGPU_ALGO_CC) {
-    for (int b = 0; b < 3; b++)
-      HIPCHK(hipMemsetAsync(s.act[b], 0, (size_t)((g.nv + 7) / 8 + 1) * 8, s.stream));
     // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
     const double b2 = g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0;
     timed_launch(c, si, KID_SLOTS, b2, [&] {
       launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
-                      s.chg[1], s.act[2], s.stepcnt, c->profile ? s.work : nullptr);
+                      s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
+                      c->profile ? s.work : nullptr);
     });
     s.r_launched = 1;  // superstep 1 ran inside the slot kernel
     if (rc.max_steps <= 1) {  // AnalysisTask.timeResponse :169: no Setup when maxSteps <= 1
@@ -494,6 +510,8 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->nslots = std::max(1, std::min(kMaxSlots, env_int("RGPU_SLOTS", 3)));
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   if (env_int("RGPU_STEP_GRID", 0) > 0) g_step_grid = env_int("RGPU_STEP_GRID", 0);
+  g_rowbuf = env_int("RGPU_ROWBUF", 0);
+  c->hostflags = env_int("RGPU_HOSTFLAG", 1) != 0;
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
   *out = c;
