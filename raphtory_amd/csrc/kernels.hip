@@ -336,6 +336,41 @@ __device__ __forceinline__ int32_t gather_min(uint64_t act, int32_t nb, int32_t 
   return best;
 }
 
+// Gathers of a whole 4-vertex chunk, interleaved: each round takes up to two changed
+// neighbours of every vertex (8 row loads in flight), then folds them.  Vertex positions
+// are static (unrolled), so no register is dynamically indexed.
+template <bool BUF>
+__device__ __forceinline__ void gather_min_x4(const uint64_t (&act)[4], const int32_t (&nb)[4],
+                                              int32_t (&best)[4], const int32_t* __restrict__ lab_cur,
+                                              int lane) {
+  uint64_t bal[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) bal[i] = __ballot(act[i] != 0);
+  while (bal[0] | bal[1] | bal[2] | bal[3]) {
+    int32_t x[4][2];
+    bool on[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        on[i][h] = false;
+        x[i][h] = INT32_MAX;
+        if (bal[i]) {  // wave-uniform
+          const int L = __builtin_ctzll(bal[i]);
+          bal[i] &= bal[i] - 1;
+          const int32_t q = __builtin_amdgcn_readlane(nb[i], L);
+          on[i][h] = (readlane64(act[i], L) >> lane) & 1;
+          x[i][h] = row_get<BUF>(lab_cur + (int64_t)q * 64, on[i][h], lane);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) best[i] = min(best[i], on[i][h] ? x[i][h] : INT32_MAX);
+  }
+}
+
 // Superstep kernel.  Frontier flags are bytes (plain idempotent stores, no RMW), and a
 // wave's CH-vertex chunk runs loads-first: metadata + own change words + own label rows,
 // slot rows, neighbour change words, then every label gather of the chunk, and only then
@@ -419,8 +454,15 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     // stage 4a: all gathers of the chunk (loads only)
     int32_t best[CH];
 #pragma unroll
+    for (int i = 0; i < CH; i++) best[i] = cur[i];
+    if constexpr (CH == 4) {
+      gather_min_x4<BUF>(act, nb, best, lab_cur, lane);
+    } else {
+#pragma unroll
+      for (int i = 0; i < CH; i++) best[i] = gather_min<BUF>(act[i], nb[i], cur[i], lab_cur, lane);
+    }
+#pragma unroll
     for (int i = 0; i < CH; i++) {
-      best[i] = gather_min<BUF>(act[i], nb[i], cur[i], lab_cur, lane);
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
       if (n > 64) {  // vertices with more than 64 kept slots
         const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
@@ -516,8 +558,13 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int nviews, const u
     }
     const uint64_t mvl = lane < nvc ? vm[v0 + lane] : 0;
     const uint64_t adl = lane < nvc ? vadj[v0 + lane] : 0;
+    uint64_t any = mvl;  // views with at least one member in this chunk (OR over lanes)
+    for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
+    any = readlane64(any, 0) & (nviews >= 64 ? ~0ull : ((1ull << nviews) - 1));
     __builtin_amdgcn_wave_barrier();
-    for (int j = 0; j < nviews; j++) {
+    while (any) {
+      const int j = __builtin_ctzll(any);
+      any &= any - 1;
       const bool in_view = (mvl >> j) & 1;
       const bool member = in_view && ((adl >> j) & 1);
       const uint64_t isolated = __ballot(in_view && !member);
@@ -762,6 +809,8 @@ __global__ __launch_bounds__(256) void k_pr_step(int64_t nv, const int64_t* __re
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 4096;
 int g_rowbuf = 0;
+int g_tail_step = 14;
+int g_tail_grid = 1024;
 
 static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
   int64_t g = (items + per_block - 1) / per_block;
@@ -793,7 +842,9 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     unsigned long long* work, int variant) {
   const int ch = (variant & 15) == 8 ? 8 : 4;
   const bool buf = (variant & 16) != 0;
-  const unsigned grid = grid_for(g.nv, 4 * ch, (unsigned)g_step_grid);
+  // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches
+  const unsigned cap = step >= g_tail_step ? (unsigned)g_tail_grid : (unsigned)g_step_grid;
+  const unsigned grid = grid_for(g.nv, 4 * ch, cap);
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work
   if (ch == 8 && buf) k_cc_step2<8, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);

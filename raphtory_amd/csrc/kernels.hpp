@@ -50,6 +50,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const
                      int32_t* hostflag, unsigned long long* work);
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID)
 extern int g_rowbuf;     // label rows via buffer descriptors (RGPU_ROWBUF)
+extern int g_tail_step, g_tail_grid;  // supersteps >= tail_step use at most tail_grid blocks
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,

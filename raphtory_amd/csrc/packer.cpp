@@ -16,13 +16,20 @@
 //
 // Endpoint deaths are NOT copied into every edge (a hub with many deaths would multiply
 // its degree by its death count).  They stay in per-vertex death lists, and the window
-// kernel applies them (DESIGN.md §3).  The one place that needs stream order — an own
+// kernel applies them (DESIGN.md §2).  The one place that needs stream order — an own
 // edge point and an endpoint death at the same time — is resolved here, per point, as the
 // reference's put order resolves it: a death that happened before the edge existed is
 // applied right after the edge's creation (killList at creation), later deaths at their
 // own stream position.
+//
+// Parallel layout (std::thread, RGPU_THREADS, default min(16, cores)): ids are sorted by
+// chunk sort + pairwise merges; every record is then scattered by entity rank (counting
+// sort, one atomic cursor per rank) and each entity's small segment is sorted on its own.
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "rgpu_internal.hpp"
 
@@ -30,19 +37,119 @@ namespace rgpu {
 namespace {
 
 struct VPoint {
-  int32_t r;
-  uint8_t flag;
   int64_t t, idx;
+  uint8_t flag;
 };
 struct EPoint {
-  int32_t s, d;
+  int32_t d;
   uint8_t flag;
   int64_t t, idx;
 };
 struct Death {
-  int32_t r;
   int64_t t, idx;
 };
+
+int num_threads() {
+  const char* e = std::getenv("RGPU_THREADS");
+  int t = e && *e ? std::atoi(e) : 0;
+  if (t <= 0) {
+    t = (int)std::thread::hardware_concurrency();
+    if (t > 16) t = 16;  // a GPU box's CPU share
+  }
+  return t < 1 ? 1 : t;
+}
+
+// run f(lo, hi, tid) over [0, n) in T contiguous chunks
+template <class F>
+void parallel_for(size_t n, int T, F f) {
+  if (T <= 1 || n < 4096) {
+    f((size_t)0, n, 0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int k = 0; k < T; k++) {
+    const size_t lo = n * k / T, hi = n * (k + 1) / T;
+    th.emplace_back([=, &f] { f(lo, hi, k); });
+  }
+  for (auto& x : th) x.join();
+}
+
+template <class T, class C>
+void parallel_sort(std::vector<T>& v, int nt, C cmp) {
+  const size_t n = v.size();
+  if (nt <= 1 || n < (1u << 16)) {
+    std::sort(v.begin(), v.end(), cmp);
+    return;
+  }
+  int parts = 1;
+  while (parts * 2 <= nt) parts *= 2;
+  std::vector<size_t> cut(parts + 1);
+  for (int k = 0; k <= parts; k++) cut[k] = n * k / parts;
+  {
+    std::vector<std::thread> th;
+    for (int k = 0; k < parts; k++)
+      th.emplace_back([&, k] { std::sort(v.begin() + cut[k], v.begin() + cut[k + 1], cmp); });
+    for (auto& x : th) x.join();
+  }
+  std::vector<T> buf(n);
+  std::vector<T>* src = &v;
+  std::vector<T>* dst = &buf;
+  for (int w = 1; w < parts; w *= 2) {
+    std::vector<std::thread> th;
+    for (int k = 0; k < parts; k += 2 * w)
+      th.emplace_back([&, k] {
+        const size_t a = cut[k], m = cut[k + w], b = cut[std::min(k + 2 * w, parts)];
+        std::merge(src->begin() + a, src->begin() + m, src->begin() + m, src->begin() + b,
+                   dst->begin() + a, cmp);
+      });
+    for (auto& x : th) x.join();
+    std::swap(src, dst);
+  }
+  if (src != &v) v.swap(*src);
+}
+
+// counting-sort scatter: key(i) in [0, nkeys) -> records grouped by key, offsets in off[nkeys+1]
+template <class R, class KeyF, class MakeF>
+void group_by_key(size_t n, int64_t nkeys, int nt, KeyF key, MakeF make, std::vector<int64_t>& off,
+                  std::vector<R>& out) {
+  off.assign(nkeys + 1, 0);
+  std::vector<std::atomic<int64_t>> cnt(nkeys + 1);
+  for (auto& c : cnt) c.store(0, std::memory_order_relaxed);
+  parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; i++) {
+      const int64_t k = key(i);
+      if (k >= 0) cnt[k + 1].fetch_add(1, std::memory_order_relaxed);
+    }
+  });
+  for (int64_t k = 0; k < nkeys; k++) off[k + 1] = off[k] + cnt[k + 1].load(std::memory_order_relaxed);
+  for (int64_t k = 0; k <= nkeys; k++) cnt[k].store(off[k], std::memory_order_relaxed);
+  out.resize(off[nkeys]);
+  parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; i++) {
+      const int64_t k = key(i);
+      if (k >= 0) out[cnt[k].fetch_add(1, std::memory_order_relaxed)] = make(i);
+    }
+  });
+}
+
+// per-segment sorts, load-balanced by segment start (segments are small; hubs get a thread)
+template <class R, class C>
+void sort_segments(std::vector<R>& recs, const std::vector<int64_t>& off, int nt, C cmp) {
+  const int64_t nseg = (int64_t)off.size() - 1;
+  std::atomic<int64_t> next(0);
+  auto work = [&] {
+    for (;;) {
+      const int64_t s0 = next.fetch_add(1024);
+      if (s0 >= nseg) return;
+      const int64_t s1 = std::min(nseg, s0 + 1024);
+      for (int64_t s = s0; s < s1; s++)
+        if (off[s + 1] - off[s] > 1) std::sort(recs.begin() + off[s], recs.begin() + off[s + 1], cmp);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int k = 0; k < nt; k++) th.emplace_back(work);
+  for (auto& x : th) x.join();
+}
 
 }  // namespace
 
@@ -51,128 +158,172 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
   if (num_partitions != 1 || partition != 0)
     return "vertex-partitioned contexts (num_partitions > 1) are not in this build; "
            "run one replica context per GPU";
+  const int nt = num_threads();
+  const size_t n = ev.size();
   const int64_t kMaxT = (int64_t)1 << 61;
-  std::vector<int64_t> ids;
-  ids.reserve(ev.size() * 2);
-  int64_t newest = -1;
   for (const Event& e : ev) {
     if (e.kind > RGPU_EDEL) return "unknown update kind";
     if (e.t < 0 || e.t >= kMaxT) return "time out of range [0, 2^61)";
     if (e.src < 0 || e.src > INT32_MAX) return "vertex id out of range [0, 2^31)";
-    ids.push_back(e.src);
-    if (e.kind >= RGPU_EADD) {
-      if (e.dst < 0 || e.dst > INT32_MAX) return "vertex id out of range [0, 2^31)";
-      ids.push_back(e.dst);
-    }
-    newest = std::max(newest, e.t);
+    if (e.kind >= RGPU_EADD && (e.dst < 0 || e.dst > INT32_MAX)) return "vertex id out of range [0, 2^31)";
   }
-  std::sort(ids.begin(), ids.end());
-  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
   Packed& P = *out;
   P = Packed();
+  // ---- vertex ids: sorted, distinct; rank = position
+  std::vector<int64_t> ids;
+  ids.reserve(n * 2);
+  int64_t newest = -1;
+  for (const Event& e : ev) {
+    ids.push_back(e.src);
+    if (e.kind >= RGPU_EADD) ids.push_back(e.dst);
+    newest = std::max(newest, e.t);
+  }
+  parallel_sort(ids, nt, std::less<int64_t>());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
   P.newest = newest;
   P.nv = (int64_t)ids.size();
   P.vid = ids;
-  auto rank = [&](int64_t id) {
-    return (int32_t)(std::lower_bound(ids.begin(), ids.end(), id) - ids.begin());
-  };
+  std::vector<int32_t> rs(n), rd(n, -1);
+  parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; i++) {
+      rs[i] = (int32_t)(std::lower_bound(ids.begin(), ids.end(), ev[i].src) - ids.begin());
+      if (ev[i].kind >= RGPU_EADD)
+        rd[i] = (int32_t)(std::lower_bound(ids.begin(), ids.end(), ev[i].dst) - ids.begin());
+    }
+  });
 
-  std::vector<VPoint> vp;
-  std::vector<EPoint> ep;
-  std::vector<Death> dd;
-  vp.reserve(ev.size() * 2);
-  ep.reserve(ev.size());
-  for (size_t i = 0; i < ev.size(); i++) {
-    const Event& e = ev[i];
-    int64_t idx = (int64_t)i;
-    int32_t rs = rank(e.src);
-    switch (e.kind) {
-      case RGPU_VADD: vp.push_back({rs, 1, e.t, idx}); break;
-      case RGPU_VDEL:
-        vp.push_back({rs, 0, e.t, idx});
-        dd.push_back({rs, e.t, idx});
-        break;
-      case RGPU_EADD: {
-        int32_t rd = rank(e.dst);
-        vp.push_back({rs, 1, e.t, idx});
-        if (rd != rs) vp.push_back({rd, 1, e.t, idx});
-        ep.push_back({rs, rd, 1, e.t, idx});
-        break;
+  // ---- vertex histories: records grouped by rank (src of every update; dst of EdgeAdd unless
+  // a self-loop), each segment sorted by (t, idx), equal t collapsed (last put wins)
+  {
+    // a record slot per (event, end): 2i = src side, 2i+1 = dst side
+    auto vkey_of = [&](size_t j) -> int64_t {
+      const size_t i = j >> 1;
+      const Event& e = ev[i];
+      if (!(j & 1)) return e.kind == RGPU_EDEL ? -1 : rs[i];
+      return (e.kind == RGPU_EADD && rd[i] != rs[i]) ? rd[i] : -1;
+    };
+    auto vmake = [&](size_t j) {
+      const size_t i = j >> 1;
+      return VPoint{ev[i].t, (int64_t)i, (uint8_t)(ev[i].kind == RGPU_VDEL ? 0 : 1)};
+    };
+    std::vector<int64_t> off;
+    std::vector<VPoint> vp;
+    group_by_key<VPoint>(2 * n, P.nv, nt, vkey_of, vmake, off, vp);
+    sort_segments(vp, off, nt, [](const VPoint& a, const VPoint& b) {
+      return a.t != b.t ? a.t < b.t : a.idx < b.idx;
+    });
+    // collapse: count distinct times per rank, then fill
+    P.voff.assign(P.nv + 1, 0);
+    parallel_for((size_t)P.nv, nt, [&](size_t lo, size_t hi, int) {
+      for (size_t r = lo; r < hi; r++) {
+        int64_t c = 0;
+        for (int64_t k = off[r]; k < off[r + 1]; k++)
+          if (k + 1 == off[r + 1] || vp[k + 1].t != vp[k].t) c++;
+        P.voff[r + 1] = c;
       }
-      case RGPU_EDEL: ep.push_back({rs, rank(e.dst), 0, e.t, idx}); break;
+    });
+    for (int64_t v = 0; v < P.nv; v++) P.voff[v + 1] += P.voff[v];
+    P.vkey.resize(P.voff[P.nv]);
+    parallel_for((size_t)P.nv, nt, [&](size_t lo, size_t hi, int) {
+      for (size_t r = lo; r < hi; r++) {
+        int64_t o = P.voff[r];
+        for (int64_t k = off[r]; k < off[r + 1]; k++)
+          if (k + 1 == off[r + 1] || vp[k + 1].t != vp[k].t) P.vkey[o++] = vp[k].t * 2 + vp[k].flag;
+      }
+    });
+  }
+
+  // ---- death lists: distinct VDEL times per rank, with the last stream index at each time
+  std::vector<int64_t> dlast;
+  {
+    auto dkey = [&](size_t i) -> int64_t { return ev[i].kind == RGPU_VDEL ? rs[i] : -1; };
+    auto dmake = [&](size_t i) { return Death{ev[i].t, (int64_t)i}; };
+    std::vector<int64_t> off;
+    std::vector<Death> dd;
+    group_by_key<Death>(n, P.nv, nt, dkey, dmake, off, dd);
+    sort_segments(dd, off, nt, [](const Death& a, const Death& b) {
+      return a.t != b.t ? a.t < b.t : a.idx < b.idx;
+    });
+    P.doff.assign(P.nv + 1, 0);
+    for (int64_t r = 0; r < P.nv; r++) {
+      int64_t c = 0;
+      for (int64_t k = off[r]; k < off[r + 1]; k++)
+        if (k + 1 == off[r + 1] || dd[k + 1].t != dd[k].t) {
+          P.dtime.push_back(dd[k].t);
+          dlast.push_back(dd[k].idx);
+          c++;
+        }
+      P.doff[r + 1] = P.doff[r] + c;
     }
   }
-
-  // ---- vertex histories: sort (rank, t, idx), collapse equal t (last put wins)
-  std::sort(vp.begin(), vp.end(), [](const VPoint& a, const VPoint& b) {
-    if (a.r != b.r) return a.r < b.r;
-    if (a.t != b.t) return a.t < b.t;
-    return a.idx < b.idx;
-  });
-  P.voff.assign(P.nv + 1, 0);
-  P.vkey.reserve(vp.size());
-  for (size_t i = 0; i < vp.size(); i++) {
-    if (i + 1 < vp.size() && vp[i + 1].r == vp[i].r && vp[i + 1].t == vp[i].t) continue;
-    P.vkey.push_back(vp[i].t * 2 + vp[i].flag);
-    P.voff[vp[i].r + 1]++;
-  }
-  for (int64_t v = 0; v < P.nv; v++) P.voff[v + 1] += P.voff[v];
-
-  // ---- death lists: distinct times, with the last stream index at each time
-  std::sort(dd.begin(), dd.end(), [](const Death& a, const Death& b) {
-    if (a.r != b.r) return a.r < b.r;
-    if (a.t != b.t) return a.t < b.t;
-    return a.idx < b.idx;
-  });
-  P.doff.assign(P.nv + 1, 0);
-  std::vector<int64_t> dlast;  // max stream index of a death at dtime[i]
-  for (size_t i = 0; i < dd.size(); i++) {
-    if (i + 1 < dd.size() && dd[i + 1].r == dd[i].r && dd[i + 1].t == dd[i].t) continue;
-    P.dtime.push_back(dd[i].t);
-    dlast.push_back(dd[i].idx);
-    P.doff[dd[i].r + 1]++;
-  }
-  for (int64_t v = 0; v < P.nv; v++) P.doff[v + 1] += P.doff[v];
   auto death_at = [&](int32_t r, int64_t t) -> int64_t {  // -1 if no death at exactly t
     auto b = P.dtime.begin() + P.doff[r], e = P.dtime.begin() + P.doff[r + 1];
     auto it = std::lower_bound(b, e, t);
     return (it != e && *it == t) ? dlast[it - P.dtime.begin()] : -1;
   };
 
-  // ---- edge own histories
-  std::sort(ep.begin(), ep.end(), [](const EPoint& a, const EPoint& b) {
-    if (a.s != b.s) return a.s < b.s;
-    if (a.d != b.d) return a.d < b.d;
-    if (a.t != b.t) return a.t < b.t;
-    return a.idx < b.idx;
-  });
-  P.eoff.push_back(0);
-  for (size_t g = 0; g < ep.size();) {
-    size_t h = g;
-    int64_t created = ep[g].idx;  // stream index of the edge's first update
-    while (h < ep.size() && ep[h].s == ep[g].s && ep[h].d == ep[g].d) {
-      created = std::min(created, ep[h].idx);
-      h++;
-    }
-    for (size_t i = g; i < h; i++) {
-      if (i + 1 < h && ep[i + 1].t == ep[i].t) continue;  // collapse: last put wins
-      uint8_t flag = ep[i].flag;
-      // tie with an endpoint death at the same time: compare put positions (x2 so that
-      // "right after creation" = 2*created+1 sits between two stream indices)
-      int64_t pd = death_at(ep[i].s, ep[i].t);
-      if (ep[i].d != ep[i].s) pd = std::max(pd, death_at(ep[i].d, ep[i].t));
-      if (pd >= 0) {
-        int64_t pd2 = pd < created ? 2 * created + 1 : 2 * pd;
-        if (pd2 > 2 * ep[i].idx) flag = 0;
+  // ---- edge own histories: grouped by src rank, each src segment sorted by (dst, t, idx)
+  {
+    auto ekey = [&](size_t i) -> int64_t { return ev[i].kind >= RGPU_EADD ? rs[i] : -1; };
+    auto emake = [&](size_t i) {
+      return EPoint{rd[i], (uint8_t)(ev[i].kind == RGPU_EADD ? 1 : 0), ev[i].t, (int64_t)i};
+    };
+    std::vector<int64_t> off;
+    std::vector<EPoint> ep;
+    group_by_key<EPoint>(n, P.nv, nt, ekey, emake, off, ep);
+    sort_segments(ep, off, nt, [](const EPoint& a, const EPoint& b) {
+      if (a.d != b.d) return a.d < b.d;
+      if (a.t != b.t) return a.t < b.t;
+      return a.idx < b.idx;
+    });
+    // per src: number of edges and of collapsed points (parallel), then fill
+    std::vector<int64_t> ne_of(P.nv + 1, 0), np_of(P.nv + 1, 0);
+    parallel_for((size_t)P.nv, nt, [&](size_t lo, size_t hi, int) {
+      for (size_t r = lo; r < hi; r++) {
+        int64_t ce = 0, cp = 0;
+        for (int64_t k = off[r]; k < off[r + 1]; k++) {
+          const bool last_of_edge = k + 1 == off[r + 1] || ep[k + 1].d != ep[k].d;
+          if (last_of_edge) ce++;
+          if (last_of_edge || ep[k + 1].t != ep[k].t) cp++;
+        }
+        ne_of[r + 1] = ce;
+        np_of[r + 1] = cp;
       }
-      P.ekey.push_back(ep[i].t * 2 + flag);
-    }
-    P.esrc.push_back(ep[g].s);
-    P.edst.push_back(ep[g].d);
-    P.eoff.push_back((int64_t)P.ekey.size());
-    g = h;
+    });
+    for (int64_t r = 0; r < P.nv; r++) { ne_of[r + 1] += ne_of[r]; np_of[r + 1] += np_of[r]; }
+    P.ne = ne_of[P.nv];
+    P.esrc.resize(P.ne);
+    P.edst.resize(P.ne);
+    P.eoff.assign(P.ne + 1, 0);
+    P.ekey.resize(np_of[P.nv]);
+    parallel_for((size_t)P.nv, nt, [&](size_t lo, size_t hi, int) {
+      for (size_t r = lo; r < hi; r++) {
+        int64_t e = ne_of[r], p = np_of[r];
+        for (int64_t g = off[r]; g < off[r + 1];) {
+          int64_t h = g, created = ep[g].idx;  // stream index of the edge's first update
+          while (h < off[r + 1] && ep[h].d == ep[g].d) { created = std::min(created, ep[h].idx); h++; }
+          for (int64_t k = g; k < h; k++) {
+            if (k + 1 < h && ep[k + 1].t == ep[k].t) continue;  // collapse: last put wins
+            uint8_t flag = ep[k].flag;
+            // tie with an endpoint death at the same time: compare put positions (x2 so that
+            // "right after creation" = 2*created+1 sits between two stream indices)
+            int64_t pd = death_at((int32_t)r, ep[k].t);
+            if (ep[k].d != (int32_t)r) pd = std::max(pd, death_at(ep[k].d, ep[k].t));
+            if (pd >= 0) {
+              const int64_t pd2 = pd < created ? 2 * created + 1 : 2 * pd;
+              if (pd2 > 2 * ep[k].idx) flag = 0;
+            }
+            P.ekey[p++] = ep[k].t * 2 + flag;
+          }
+          P.esrc[e] = (int32_t)r;
+          P.edst[e] = ep[g].d;
+          P.eoff[e + 1] = p;
+          e++;
+          g = h;
+        }
+      }
+    });
   }
-  P.ne = (int64_t)P.esrc.size();
 
   // ---- adjacency: out-edges by src (edge order), in-edges by (dst, src), self-loops
   // never enter incomingEdges (EntityStorage.scala:257)

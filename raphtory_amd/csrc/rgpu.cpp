@@ -511,6 +511,8 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   if (env_int("RGPU_STEP_GRID", 0) > 0) g_step_grid = env_int("RGPU_STEP_GRID", 0);
   g_rowbuf = env_int("RGPU_ROWBUF", 0);
+  if (env_int("RGPU_TAIL_STEP", 0) > 0) g_tail_step = env_int("RGPU_TAIL_STEP", 0);
+  if (env_int("RGPU_TAIL_GRID", 0) > 0) g_tail_grid = env_int("RGPU_TAIL_GRID", 0);
   c->hostflags = env_int("RGPU_HOSTFLAG", 1) != 0;
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }

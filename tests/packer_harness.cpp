@@ -1,0 +1,62 @@
+// TEST INFRASTRUCTURE: CPU harness around the product's host packer (raphtory_amd/csrc/
+// packer.cpp, compiled here with g++).  ph_alive restates the window-mask kernels' liveness
+// rule (kernels.hip: k_vertex_mask / k_edge_mask) on the packed arrays so that the packer
+// can be checked against the oracle's literal EntityStorage replay without a GPU.
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
+#include "rgpu_internal.hpp"
+
+using rgpu::Event;
+using rgpu::Packed;
+
+extern "C" void* ph_pack(const int64_t* t, const uint8_t* kind, const int64_t* src, const int64_t* dst,
+                         size_t n) {
+  std::vector<Event> ev(n);
+  for (size_t i = 0; i < n; i++) ev[i] = {t[i], src[i], kind[i] >= 2 ? dst[i] : -1, kind[i]};
+  Packed* p = new Packed();
+  if (!rgpu::pack_events(ev, 0, 1, p).empty()) { delete p; return nullptr; }
+  return p;
+}
+extern "C" void ph_free(void* h) { delete (Packed*)h; }
+extern "C" int64_t ph_num(void* h, int what) {
+  const Packed* p = (const Packed*)h;
+  return what == 0 ? p->nv : what == 1 ? p->ne : what == 2 ? (int64_t)p->vkey.size() : (int64_t)p->ekey.size();
+}
+
+static int64_t floor_key(const std::vector<int64_t>& key, int64_t lo, int64_t hi, int64_t t) {
+  auto it = std::upper_bound(key.begin() + lo, key.begin() + hi, 2 * t + 1);
+  return it == key.begin() + lo ? -1 : *(it - 1);
+}
+static int64_t last_death(const Packed* p, int32_t r, int64_t t) {
+  auto b = p->dtime.begin() + p->doff[r], e = p->dtime.begin() + p->doff[r + 1];
+  auto it = std::upper_bound(b, e, t);
+  return it == b ? -1 : *(it - 1);
+}
+// window < 0 => ViewLens (no window)
+extern "C" int ph_alive(void* h, int is_edge, int64_t src, int64_t dst, int64_t t, int64_t window) {
+  const Packed* p = (const Packed*)h;
+  auto rank = [&](int64_t id) -> int64_t {
+    auto it = std::lower_bound(p->vid.begin(), p->vid.end(), id);
+    return (it == p->vid.end() || *it != id) ? -1 : it - p->vid.begin();
+  };
+  const int64_t rs = rank(src);
+  if (rs < 0) return 0;
+  const int64_t w = window < 0 ? INT64_MAX : window;
+  if (!is_edge) {
+    const int64_t k = floor_key(p->vkey, p->voff[rs], p->voff[rs + 1], t);
+    return k >= 0 && (k & 1) && t - (k >> 1) <= w;
+  }
+  const int64_t rd = rank(dst);
+  if (rd < 0) return 0;
+  int64_t e = -1;
+  for (int64_t x = p->out_off[rs]; x < p->out_off[rs + 1]; x++)
+    if (p->edst[x] == rd) e = x;
+  if (e < 0) return 0;
+  const int64_t k = floor_key(p->ekey, p->eoff[e], p->eoff[e + 1], t);
+  if (k < 0 || !(k & 1)) return 0;
+  const int64_t ft = k >> 1;
+  if (last_death(p, (int32_t)rs, t) > ft || last_death(p, (int32_t)rd, t) > ft) return 0;
+  return t - ft <= w;
+}
