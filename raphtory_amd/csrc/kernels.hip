@@ -302,10 +302,15 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
 // Gather the label rows of the neighbours flagged in `act` (lane = slot) and fold them into
 // `best` (lane = view); four row loads in flight per round, each touching only the lanes
 // (views) in which that neighbour changed (row_load).
+// One always-cached 64-B line: lanes whose value will be discarded read it instead of their
+// (cold) line of a label row, so a gather only pulls the lines of the views it needs — no
+// branch, no descriptor.  Only read, never written.
+__device__ int32_t g_dummy_line[16];
+
 template <bool BUF>
 __device__ __forceinline__ int32_t row_get(const int32_t* row, bool on, int lane) {
   if (BUF) return row_load(row, on, lane);
-  return row[lane];  // whole-row load, masked by the caller's select
+  return *(on ? row + lane : g_dummy_line + (lane & 15));  // off lanes: caller's select discards
 }
 
 template <bool BUF>

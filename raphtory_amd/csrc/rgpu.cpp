@@ -213,11 +213,9 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       HIPCHK(hipMemset(s.chg[0], 0, sizeof(uint64_t) * (nv + kPad)));
       HIPCHK(hipMemset(s.chg[1], 0, sizeof(uint64_t) * (nv + kPad)));
       HIPCHK(hipMemset(s.snbr, 0, sizeof(int32_t) * (ne + nin + kPad)));
-      s.hist = dalloc<int32_t>(L, rows);
       for (int b = 0; b < 3; b++) s.act[b] = dalloc<uint8_t>(L, (size_t)((nv + 7) / 8 + 1) * 8);
       s.vadj = dalloc<uint64_t>(L, nv);
       s.work = dalloc<unsigned long long>(L, kWorkWords);
-      HIPCHK(hipMemset(s.hist, 0, sizeof(int32_t) * (rows ? rows : 1)));
     }
     if ((algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) && !c->slot_deg) {
       s.outdeg = dalloc<int32_t>(L, rows);
@@ -280,9 +278,13 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
   const DevGraph& g = c->g;
   if (rc.algo == RGPU_ALGO_CC) {
     const int32_t* lab = s.lab[s.r_final & 1];
-    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g, rc.K * rc.W, s.vm, s.vadj, lab, s.hist, s.stats); });
+    // the other label buffer is free now: it becomes the view-major histogram (keeps the
+    // batch's working set inside the Infinity Cache with several batches in flight)
+    int32_t* hist = s.lab[(s.r_final + 1) & 1];
+    HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)g.nv * kViews, s.stream));
+    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g, rc.K * rc.W, s.vm, s.vadj, lab, hist, s.stats); });
     timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * rc.K * rc.W,
-                 [&] { launch_cc_summary(s.stream, g, rc.K * rc.W, s.hist, s.stats); });
+                 [&] { launch_cc_summary(s.stream, g, rc.K * rc.W, hist, s.stats); });
   }
   HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatWords,
                         hipMemcpyDeviceToHost, s.stream));
