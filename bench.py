@@ -41,6 +41,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-profile-pass", action="store_true")
+    p.add_argument("--config", default="c2", choices=["c2", "c3"], help="c2 = the headline metric")
+    p.add_argument("--c3-vertices", type=int, default=10_000_000)
+    p.add_argument("--c3-events", type=int, default=100_000_000)
     return p.parse_args()
 
 
@@ -88,8 +91,55 @@ def cpu_baseline(stream, hops, windows, budget_s, n_edges):
     }
 
 
+def run_c3(a, rank, world, local):
+    """BASELINE configs[2] (C3): power-law stream, 10M vertices / 100M updates over two years;
+    Range over the last 60 days, daily hops, windows [month, week, day]; PageRank (20
+    iterations) + DegreeBasic.  A secondary line, not the headline metric."""
+    import torch
+    from raphtory_amd import TemporalGraph
+    from raphtory_amd.synth import DAY, MONTH, T0_README, WEEK, YEAR, gen_powerlaw, range_hops
+    t0 = time.perf_counter()
+    nv, ne = (a.c3_vertices, a.c3_events)
+    s = gen_powerlaw(3, nv, ne, t0=T0_README, t1=T0_README + 2 * YEAR)
+    gen_s = time.perf_counter() - t0
+    g = TemporalGraph(device=local)
+    g.ingest_stream(s)
+    t0 = time.perf_counter()
+    g.seal()
+    seal_s = time.perf_counter() - t0
+    end = T0_README + 2 * YEAR
+    hops = range_hops(end - 60 * DAY, end, DAY)
+    windows = [MONTH, WEEK, DAY]
+    st = g.stats()
+    out = {"config": "C3", "vertices": st["vertices"], "edge_entities": st["edges"],
+           "vertex_events": st["vertex_events"], "edge_events": st["edge_events"], "deaths": st["deaths"],
+           "gen_s": round(gen_s, 2), "seal_s": round(seal_s, 2), "hops": len(hops), "windows": len(windows)}
+    for algo in ("pagerank", "degree"):
+        g.run(algo, hops, windows, pr_iters=20)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            g.run(algo, hops, windows, pr_iters=20)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3 / a.steps
+        out[algo] = {"ms": round(ms, 2), "edge_windows_per_s": st["edges"] * len(windows) * len(hops) / (ms / 1e3)}
+        g.run(algo, hops, windows, pr_iters=20, profile=True, serial=True)
+        out[algo]["kernels"] = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                                    "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
+                                for k, v in g.stats()["kernels"].items() if v["launches"]}
+    tot = [g.degree_result(h, w)[:3] for h in (0, len(hops) - 1) for w in range(3)]
+    out["degree_totals_first_last_hop"] = tot
+    g.close()
+    print(json.dumps(out))
+
+
 def main():
     a = parse()
+    if a.config == "c3":
+        rank, world, local = dist_env()
+        import torch
+        torch.cuda.set_device(local)
+        return run_c3(a, rank, world, local)
     rank, world, local = dist_env()
     import torch
     torch.cuda.set_device(local)

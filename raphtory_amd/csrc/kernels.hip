@@ -85,10 +85,23 @@ __device__ __forceinline__ int64_t floor_advance(const int64_t* key, int64_t f, 
   }
   return floor_idx(key, g, hi, t) >= 0 ? floor_idx(key, g, hi, t) : g - 1;
 }
+// first index in [p, hi) whose death time is > t (binary search)
+__device__ __forceinline__ int64_t first_after(const int64_t* dt, int64_t p, int64_t hi, int64_t t) {
+  int64_t a = p, b = hi;
+  while (a < b) {
+    const int64_t m = (a + b) >> 1;
+    if (dt[m] <= t) a = m + 1; else b = m;
+  }
+  return a;
+}
+// cursor p = first death after the previous hop; advance to the first death after t (a few
+// linear steps, then a binary search: a power-law hub can die thousands of times per day)
 __device__ __forceinline__ int64_t death_advance(const int64_t* dt, int64_t p, int64_t hi, int64_t t) {
-  // p = index of the first death time > previous hop; returns first index with time > t
-  while (p < hi && dt[p] <= t) p++;
-  return p;
+  for (int s = 0; s < 4; s++) {
+    if (p >= hi || dt[p] > t) return p;
+    p++;
+  }
+  return first_after(dt, p, hi, t);
 }
 
 // The first kernel of every batch also clears the batch's small state (stats words, superstep
@@ -152,8 +165,8 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
         lds = s1 > s0 ? last_death(dtime, s0, s1, t) : -1;
         ldd = d1 > d0 ? last_death(dtime, d0, d1, t) : -1;
         if (bp.sorted) {  // k == 0: position the death cursors
-          ps = death_advance(dtime, s0, s1, t);
-          pd = death_advance(dtime, d0, d1, t);
+          ps = first_after(dtime, s0, s1, t);
+          pd = first_after(dtime, d0, d1, t);
         }
       }
       if (f < 0) continue;
