@@ -97,8 +97,26 @@ int rgpu_seal(rgpu_ctx* ctx);
  * against (ReaderWorker.scala:259-274). */
 int rgpu_newest_time(rgpu_ctx* ctx, int64_t* out);
 
-/* Multi-GPU vertex-partitioned exchange (RCCL).  Not in this build: RGPU_ENOTSUP. */
-int rgpu_exchange_init(rgpu_ctx* ctx, const void* rccl_unique_id);
+/* Multi-GPU vertex-partitioned mode.  A context opened with
+ * num_partitions = P > 1 owns the vertices with Utils.getPartition(id, P) == partition_id
+ * (S/core/utils/Utils.scala:32-33) plus ghost copies of their remote neighbours, as a
+ * Partition Manager keeps SplitEdge copies (EntityStorage.scala:303-305).  Every partition
+ * must be handed the WHOLE update stream (rgpu_ingest); each keeps what it needs.
+ *
+ * rgpu_exchange_id: make the id blob (RGPU_XCHG_ID_BYTES) once, on one rank, and hand it to
+ *   every partition (RGPU_XCHG_RCCL: an ncclUniqueId — one process per GPU;
+ *   RGPU_XCHG_LOOPBACK: partitions living in one process, e.g. to test on one GPU).
+ * rgpu_exchange_init: join the group (collective over the P partitions; before the first
+ *   run).  A no-op when num_partitions == 1.
+ * A partitioned run is collective too: every partition calls rgpu_run_view_batch with the
+ * same arguments.  Results: rgpu_cc_summary is the merged (all-partition) summary on every
+ * partition; rgpu_cc_result / *_vertex_* / rgpu_pr_result / rgpu_degree_result cover this
+ * partition's own vertices (the per-shard returnResults the caller merges). */
+#define RGPU_XCHG_ID_BYTES 128
+#define RGPU_XCHG_RCCL 0
+#define RGPU_XCHG_LOOPBACK 1
+int rgpu_exchange_id(int kind, uint8_t* out /* RGPU_XCHG_ID_BYTES */);
+int rgpu_exchange_init(rgpu_ctx* ctx, const void* id /* RGPU_XCHG_ID_BYTES */);
 
 /* Run one analyser over every (hop, window) view: hops[n_hops] are the Range hop
  * timestamps (RangeAnalysisTask.restart, RangeAnalysisTask.scala:18-35), windows[n_w]

@@ -18,6 +18,7 @@ RGPU_EINVAL, RGPU_ESTATE, RGPU_EHIP, RGPU_ENOMEM, RGPU_ENOTSUP = -1, -2, -3, -4,
 RGPU_VADD, RGPU_VDEL, RGPU_EADD, RGPU_EDEL = 0, 1, 2, 3
 RGPU_ALGO_CC, RGPU_ALGO_DEGREE, RGPU_ALGO_PR = 0, 1, 2
 RGPU_RUN_RETAIN, RGPU_RUN_PROFILE, RGPU_RUN_SERIAL = 1, 2, 4
+RGPU_XCHG_ID_BYTES, RGPU_XCHG_RCCL, RGPU_XCHG_LOOPBACK = 128, 0, 1
 ERROR_NAMES = {
     RGPU_EINVAL: "RGPU_EINVAL",
     RGPU_ESTATE: "RGPU_ESTATE",
@@ -30,7 +31,7 @@ KERNEL_NAMES = ["window_mask", "cc_slots", "cc_step", "cc_hist", "cc_summary", "
 # exported symbols of librgpu.so, exactly the declarations of include/rgpu.h
 EXPORTS = [
     "rgpu_abi_version", "rgpu_open", "rgpu_ingest", "rgpu_seal", "rgpu_newest_time",
-    "rgpu_exchange_init", "rgpu_run_view_batch", "rgpu_cc_summary", "rgpu_cc_result",
+    "rgpu_exchange_id", "rgpu_exchange_init", "rgpu_run_view_batch", "rgpu_cc_summary", "rgpu_cc_result",
     "rgpu_cc_vertex_labels", "rgpu_degree_result", "rgpu_degree_vertex", "rgpu_pr_result",
     "rgpu_stats", "rgpu_last_error", "rgpu_close",
 ]
@@ -69,7 +70,8 @@ _SIGS = {
     "rgpu_ingest": (C.c_int, [_CTX, _P64, _PU8, _P64, _P64, _SZ]),
     "rgpu_seal": (C.c_int, [_CTX]),
     "rgpu_newest_time": (C.c_int, [_CTX, _P64]),
-    "rgpu_exchange_init": (C.c_int, [_CTX, C.c_void_p]),
+    "rgpu_exchange_id": (C.c_int, [C.c_int, C.c_char_p]),
+    "rgpu_exchange_init": (C.c_int, [_CTX, C.c_char_p]),
     "rgpu_run_view_batch": (C.c_int, [_CTX, C.c_int, _P64, _SZ, _P64, _SZ, C.c_int, C.c_int, C.c_int]),
     "rgpu_cc_summary": (C.c_int, [_CTX, _SZ, _SZ, C.POINTER(CCSummary)]),
     "rgpu_cc_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P32, _SZ, C.POINTER(_SZ)]),

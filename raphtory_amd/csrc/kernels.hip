@@ -212,11 +212,13 @@ __device__ __forceinline__ void add_work(unsigned long long* work, int step, uns
 // bitmap and stepcnt[1]; vadj[v] = OR of v's kept slot masks (v isolated in view j iff bit j
 // is clear).
 
-__global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __restrict__ out_off,
+__global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
+                                                  const int64_t* __restrict__ out_off,
                                                   const int64_t* __restrict__ in_off,
                                                   const int32_t* __restrict__ in_eid,
                                                   const int32_t* __restrict__ esrc,
                                                   const int32_t* __restrict__ edst,
+                                                  const int32_t* __restrict__ grank,
                                                   const uint64_t* __restrict__ vm,
                                                   const uint64_t* __restrict__ em,
                                                   int32_t* __restrict__ cnt, int32_t* __restrict__ snbr,
@@ -241,19 +243,25 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
       if (lane == 0) { cnt[v] = 0; vadj[v] = 0; }
       continue;
     }
-    row_store(lab0 + v * 64, (int32_t)v, line_has(mv, lane), lane);
+    // label = global rank (== local rank with one partition).  A ghost (v >= n_own) only
+    // gets its slots (to its owned neighbours) and label_0 rows here: its label_1 row comes
+    // from its owner in the step-1 exchange.
+    const bool own = v < n_own;
+    const int32_t me = grank ? grank[v] : (int32_t)v;
+    row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
     const int64_t nout = o1 - o0, ntot = nout + (i1 - i0), base = o0 + i0;
-    int32_t count = 0, best = (int32_t)v;
+    int32_t count = 0, best = me;
     uint64_t any = 0;
     for (int64_t c = 0; c < ntot; c += 64) {
       const int64_t j = c + lane;
       uint64_t m = 0;
-      int32_t nb = 0;
+      int32_t nb = 0, lb = 0;
       if (j < ntot) {
         int64_t e;
         if (j < nout) { e = o0 + j; nb = edst[e]; }
         else { e = in_eid[i0 + (j - nout)]; nb = esrc[e]; }
         if (nb != (int32_t)v) m = em[e] & vm[nb] & mv;
+        lb = grank ? grank[nb] : nb;
       }
       uint64_t bal = __ballot(m != 0);
       if (m) {
@@ -262,18 +270,20 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, const int64_t* __r
         smask[pos] = m;
       }
       count += __popcll(bal);
-      while (bal) {  // superstep 1: neighbours' labels are their ranks
+      if (!own) continue;
+      while (bal) {  // superstep 1: neighbours' labels are their own ranks
         const int L = __builtin_ctzll(bal);
         bal &= bal - 1;
-        const int32_t q = __builtin_amdgcn_readlane(nb, L);
+        const int32_t q = __builtin_amdgcn_readlane(lb, L);
         const uint64_t mL = readlane64(m, L);
         any |= mL;
         if (((mL >> lane) & 1) && q < best) best = q;
       }
     }
     row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
-    const uint64_t ch = __ballot(best < (int32_t)v);
+    const uint64_t ch = __ballot(best < me);
     if (lane == 0) { cnt[v] = count; vadj[v] = any; chg1[v] = ch; }
+    if (!own) continue;
     if (ch) {
       changed++;
       if (lane == 0) act2[v] = 1;
@@ -545,7 +555,8 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
 // Members with no kept slot in a view are isolated there: islands (count 1) that need no
 // histogram entry; they are added to total / sum / biggest directly.
 template <bool BUF>
-__global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int nviews, const uint64_t* __restrict__ vm,
+__global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int64_t hstride, int nviews,
+                                                 const uint64_t* __restrict__ vm,
                                                  const uint64_t* __restrict__ vadj,
                                                  const int32_t* __restrict__ lab,
                                                  int32_t* __restrict__ hist,
@@ -593,7 +604,7 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int nviews, const u
         const int leader = __builtin_ctzll(todo);
         const int32_t L = __builtin_amdgcn_readlane(l, leader);
         const uint64_t same = __ballot(member && l == L);
-        if (lane == leader) atomicAdd(&hist[(int64_t)j * nv + L], __popcll(same));
+        if (lane == leader) atomicAdd(&hist[(int64_t)j * hstride + L], __popcll(same));
         todo &= ~same;
       }
     }
@@ -824,6 +835,170 @@ __global__ __launch_bounds__(256) void k_pr_step(int64_t nv, const int64_t* __re
   }
 }
 
+// ---------------------------------------------------------------- partition exchange
+// (host side in rgpu.cpp run_partitioned).  Send list entries are owned
+// ranks grouped by peer (xs_off); a record is 68 words: [0] entry index in the peer's list,
+// [2..3] the step's change word, [4..67] the label row.  A boundary vertex is sent when it
+// was visited in the step and changed now or in the previous step — exactly when its own
+// superstep kernel rewrote its row — so the peer's ghost rows track both label buffers.
+
+__global__ __launch_bounds__(256) void k_xpack_cc(int64_t nx, const int32_t* __restrict__ xv,
+                                                  const int32_t* __restrict__ xq,
+                                                  const int64_t* __restrict__ xoff,
+                                                  const uint8_t* __restrict__ act,
+                                                  const uint64_t* __restrict__ vm,
+                                                  const uint64_t* __restrict__ chg_now,
+                                                  const uint64_t* __restrict__ chg_prev,
+                                                  const int32_t* __restrict__ lab,
+                                                  int32_t* __restrict__ sbuf,
+                                                  int32_t* __restrict__ scnt) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t c = wave; c * 64 < nx; c += nwaves) {
+    const int64_t e = c * 64 + lane;
+    const bool ok = e < nx;
+    const int32_t v = ok ? xv[e] : 0;
+    const int32_t q = ok ? xq[e] : -1;
+    bool want = ok && vm[v] != 0 && (act == nullptr || act[v] != 0);
+    const uint64_t ch = ok ? chg_now[v] : 0;
+    if (want) want = (ch | (chg_prev ? chg_prev[v] : 0ull)) != 0;
+    const uint64_t todo = __ballot(want);
+    if (!todo) continue;
+    int64_t rec = 0;
+    uint64_t rem = todo;
+    while (rem) {  // reserve record slots, one atomic per (wave, peer)
+      const int leader = __builtin_ctzll(rem);
+      const int32_t Q = __builtin_amdgcn_readlane(q, leader);
+      const uint64_t same = __ballot(want && q == Q);
+      int32_t base = 0;
+      if (lane == leader) base = atomicAdd(&scnt[Q], __popcll(same));
+      base = __builtin_amdgcn_readlane(base, leader);
+      if (want && q == Q) rec = xoff[Q] + base + __popcll(same & lanemask_lt());
+      rem &= ~same;
+    }
+    uint64_t b = todo;
+    while (b) {
+      const int L = __builtin_ctzll(b);
+      b &= b - 1;
+      const int32_t vL = __builtin_amdgcn_readlane(v, L);
+      const int32_t qL = __builtin_amdgcn_readlane(q, L);
+      const int64_t rL = (int64_t)readlane64((uint64_t)rec, L);
+      const uint64_t chL = readlane64(ch, L);
+      int32_t* r = sbuf + rL * kXRecWords;
+      r[4 + lane] = lab[(int64_t)vL * 64 + lane];
+      if (lane == 0) {
+        r[0] = (int32_t)(c * 64 + L - xoff[qL]);
+        r[1] = 0;
+        r[2] = (int32_t)(uint32_t)chL;
+        r[3] = (int32_t)(uint32_t)(chL >> 32);
+      }
+    }
+  }
+}
+
+// Records from one peer: ghost row + change word, and the ghost's owned neighbours that
+// share a view with the change join the next frontier (as a local change would do).
+__global__ __launch_bounds__(256) void k_xunpack_cc(int64_t nrec, const int32_t* __restrict__ rbuf,
+                                                    const int32_t* __restrict__ xrl,
+                                                    const int64_t* __restrict__ adj_off,
+                                                    const int32_t* __restrict__ cnt,
+                                                    const int32_t* __restrict__ snbr,
+                                                    const uint64_t* __restrict__ smask,
+                                                    int32_t* __restrict__ lab,
+                                                    uint64_t* __restrict__ chg,
+                                                    uint8_t* __restrict__ act_next) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t k = wave; k < nrec; k += nwaves) {
+    const int32_t* r = rbuf + k * kXRecWords;
+    const int32_t g = xrl[r[0]];
+    const uint64_t ch = (uint64_t)(uint32_t)r[2] | ((uint64_t)(uint32_t)r[3] << 32);
+    lab[(int64_t)g * 64 + lane] = r[4 + lane];
+    if (lane == 0) chg[g] = ch;
+    if (ch) {
+      const int32_t n = cnt[g];
+      const int64_t base = adj_off[g];
+      for (int32_t c = 0; c < n; c += 64) {
+        const int32_t j = c + lane;
+        if (j < n && (smask[base + j] & ch)) act_next[snbr[base + j]] = 1;
+      }
+    }
+  }
+}
+
+// fp64 rows (PageRank contributions) of a whole list: gather into / scatter out of a
+// contiguous buffer, one wave per entry
+__global__ __launch_bounds__(256) void k_xgather_f64(int64_t n, const int32_t* __restrict__ xv,
+                                                     const double* __restrict__ rows,
+                                                     double* __restrict__ buf) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t k = wave; k < n; k += nwaves) buf[k * 64 + lane] = rows[(int64_t)xv[k] * 64 + lane];
+}
+__global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* __restrict__ xv,
+                                                      const double* __restrict__ buf,
+                                                      double* __restrict__ rows) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t k = wave; k < n; k += nwaves) rows[(int64_t)xv[k] * 64 + lane] = buf[k * 64 + lane];
+}
+
+__global__ __launch_bounds__(256) void k_add_i32(int32_t* __restrict__ dst, const int32_t* __restrict__ src,
+                                                 int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] += src[i];
+}
+
+// Summary over this partition's slice [x0, x0+len) of the reduce-scattered view-major
+// histogram (stride ng per view): blockIdx.y = view.
+__global__ __launch_bounds__(256) void k_cc_summary_rs(const int32_t* __restrict__ chunk, int64_t x0,
+                                                       int64_t len, int64_t ng,
+                                                       unsigned long long* __restrict__ stats) {
+  __shared__ unsigned long long red[6][4];
+  const int j = blockIdx.y;
+  const int64_t lo = x0 > (int64_t)j * ng ? x0 : (int64_t)j * ng;
+  const int64_t hi = (x0 + len) < (int64_t)(j + 1) * ng ? (x0 + len) : (int64_t)(j + 1) * ng;
+  unsigned long long big = 0, tot = 0, nis = 0, gt2 = 0, sum = 0, snis = 0;
+  for (int64_t r = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < hi;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t c = chunk[r - x0];
+    if (c) {
+      const unsigned long long uc = (unsigned long long)c;
+      big = uc > big ? uc : big;
+      tot += 1;
+      nis += c > 1;
+      gt2 += c > 2;
+      sum += uc;
+      snis += c > 1 ? uc : 0;
+    }
+  }
+  unsigned long long v[6] = {big, tot, nis, gt2, sum, snis};
+#pragma unroll
+  for (int f = 0; f < 6; f++) {
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long x = __shfl_xor(v[f], o);
+      v[f] = f == 0 ? (x > v[f] ? x : v[f]) : v[f] + x;
+    }
+  }
+  const int lane = lane_id(), wib = threadIdx.x >> 6;
+  if (lane == 0)
+    for (int f = 0; f < 6; f++) red[f][wib] = v[f];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int f = threadIdx.x;
+    unsigned long long a = red[f][0];
+    for (int w = 1; w < 4; w++) a = f == 0 ? (red[f][w] > a ? red[f][w] : a) : a + red[f][w];
+    if (a) {
+      if (f == 0) atomicMax(&stats[j], a);
+      else atomicAdd(&stats[f * 64 + j], a);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 4096;
 int g_rowbuf = 0;
@@ -848,8 +1023,8 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work) {
-  k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
-                                                vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
+  k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
+                                                g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work);
 }
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
@@ -871,11 +1046,11 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   else k_cc_step2<4, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
 #undef RGPU_STEP_ARGS
 }
-void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t* vm,
+void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist,
                     unsigned long long* stats) {
-  if (g_rowbuf) k_cc_hist<true><<<grid_for(g.nv, 4 * 64, 512), 256, 0, s>>>(g.nv, nviews, vm, vadj, lab, hist, stats);
-  else k_cc_hist<false><<<grid_for(g.nv, 4 * 64, 512), 256, 0, s>>>(g.nv, nviews, vm, vadj, lab, hist, stats);
+  if (g_rowbuf) k_cc_hist<true><<<grid_for(nv, 4 * 64, 512), 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, stats);
+  else k_cc_hist<false><<<grid_for(nv, 4 * 64, 512), 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, stats);
 }
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
                        unsigned long long* stats) {
@@ -898,6 +1073,35 @@ void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const 
                     const double* contrib_cur, double* contrib_next, double* pr) {
   k_pr_step<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.in_off, vm, outdeg, cnt, snbr, smask,
                                                contrib_cur, contrib_next, pr);
+}
+
+void launch_xpack_cc(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
+                     const uint8_t* act, const uint64_t* vm, const uint64_t* chg_now,
+                     const uint64_t* chg_prev, const int32_t* lab, int32_t* sbuf, int32_t* scnt) {
+  if (nx <= 0) return;
+  k_xpack_cc<<<grid_for(nx, 4 * 64, 2048), 256, 0, s>>>(nx, xv, xq, xoff, act, vm, chg_now, chg_prev, lab,
+                                                         sbuf, scnt);
+}
+void launch_xunpack_cc(hipStream_t s, int64_t nrec, const int32_t* rbuf, const int32_t* xrl,
+                       const DevGraph& g, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
+                       int32_t* lab, uint64_t* chg, uint8_t* act_next) {
+  if (nrec <= 0) return;
+  k_xunpack_cc<<<grid_for(nrec, 4, 4096), 256, 0, s>>>(nrec, rbuf, xrl, g.adj_off, cnt, snbr, smask, lab, chg,
+                                                        act_next);
+}
+void launch_xgather_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* rows, double* buf) {
+  if (n > 0) k_xgather_f64<<<grid_for(n, 4, 4096), 256, 0, s>>>(n, xv, rows, buf);
+}
+void launch_xscatter_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* buf, double* rows) {
+  if (n > 0) k_xscatter_f64<<<grid_for(n, 4, 4096), 256, 0, s>>>(n, xv, buf, rows);
+}
+void launch_add_i32(hipStream_t s, int32_t* dst, const int32_t* src, int64_t n) {
+  if (n > 0) k_add_i32<<<grid_for(n, 256, 4096), 256, 0, s>>>(dst, src, n);
+}
+void launch_cc_summary_rs(hipStream_t s, int nviews, const int32_t* chunk, int64_t x0, int64_t len,
+                          int64_t ng, unsigned long long* stats) {
+  dim3 grid(grid_for(ng, 256, 32), (unsigned)nviews);
+  k_cc_summary_rs<<<grid, 256, 0, s>>>(chunk, x0, len, ng, stats);
 }
 
 }  // namespace rgpu

@@ -29,6 +29,8 @@ struct DevGraph {
   const int64_t *out_off = nullptr, *in_off = nullptr;
   const int64_t* adj_off = nullptr;                  // out_off + in_off: static slot offset
   const int32_t* in_eid = nullptr;
+  int64_t n_own = 0;                                 // ranks [0, n_own) owned (== nv, one partition)
+  const int32_t* grank = nullptr;                    // global rank per local rank (null: identity)
 };
 
 // Small per-batch state cleared by the first kernel of the batch (no memset launches).
@@ -57,7 +59,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, int variant);
-void launch_cc_hist(hipStream_t s, const DevGraph& g, int nviews, const uint64_t* vm,
+void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist,
                     unsigned long long* stats);
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
@@ -70,5 +72,19 @@ void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const
 void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const int32_t* outdeg,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const double* contrib_cur, double* contrib_next, double* pr);
+
+// partition exchange (vertex-partitioned mode)
+constexpr int kXRecWords = 68;  // ints per boundary-row record
+void launch_xpack_cc(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
+                     const uint8_t* act, const uint64_t* vm, const uint64_t* chg_now,
+                     const uint64_t* chg_prev, const int32_t* lab, int32_t* sbuf, int32_t* scnt);
+void launch_xunpack_cc(hipStream_t s, int64_t nrec, const int32_t* rbuf, const int32_t* xrl,
+                       const DevGraph& g, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
+                       int32_t* lab, uint64_t* chg, uint8_t* act_next);
+void launch_xgather_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* rows, double* buf);
+void launch_xscatter_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* buf, double* rows);
+void launch_add_i32(hipStream_t s, int32_t* dst, const int32_t* src, int64_t n);
+void launch_cc_summary_rs(hipStream_t s, int nviews, const int32_t* chunk, int64_t x0, int64_t len,
+                          int64_t ng, unsigned long long* stats);
 
 }  // namespace rgpu

@@ -155,9 +155,7 @@ void sort_segments(std::vector<R>& recs, const std::vector<int64_t>& off, int nt
 
 std::string pack_events(const std::vector<Event>& ev, int partition, int num_partitions,
                         Packed* out) {
-  if (num_partitions != 1 || partition != 0)
-    return "vertex-partitioned contexts (num_partitions > 1) are not in this build; "
-           "run one replica context per GPU";
+  if (num_partitions < 1 || partition < 0 || partition >= num_partitions) return "bad partition";
   const int nt = num_threads();
   const size_t n = ev.size();
   const int64_t kMaxT = (int64_t)1 << 61;
@@ -169,7 +167,9 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
   }
   Packed& P = *out;
   P = Packed();
-  // ---- vertex ids: sorted, distinct; rank = position
+  P.part = partition;
+  P.nparts = num_partitions;
+  // ---- vertex ids: sorted, distinct; global rank = position
   std::vector<int64_t> ids;
   ids.reserve(n * 2);
   int64_t newest = -1;
@@ -181,8 +181,6 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
   parallel_sort(ids, nt, std::less<int64_t>());
   ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
   P.newest = newest;
-  P.nv = (int64_t)ids.size();
-  P.vid = ids;
   std::vector<int32_t> rs(n), rd(n, -1);
   parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
     for (size_t i = lo; i < hi; i++) {
@@ -191,6 +189,53 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
         rd[i] = (int32_t)(std::lower_bound(ids.begin(), ids.end(), ev[i].dst) - ids.begin());
     }
   });
+  if (num_partitions == 1) {
+    P.nv = P.n_own = (int64_t)ids.size();
+    P.vid = std::move(ids);
+  } else {
+    // Partition view (the reference's PM keeps its own vertices plus SplitEdge copies,
+    // EntityStorage.scala:303-305): owned vertices, ghosts = other endpoints of edges that
+    // touch an owned vertex.  Every partition is handed the whole stream, so a ghost's
+    // history (all its events) and every edge's endpoint deaths are complete here.
+    // Local rank order: owned by id, then ghosts by id; labels stay global ranks.
+    const int64_t ng = (int64_t)ids.size();
+    std::vector<std::atomic<uint8_t>> role(ng);  // 0 owned, 1 ghost, 2 not kept
+    parallel_for((size_t)ng, nt, [&](size_t lo, size_t hi, int) {
+      for (size_t g = lo; g < hi; g++)
+        role[g].store(partition_of(ids[g], num_partitions) == partition ? 0 : 2, std::memory_order_relaxed);
+    });
+    parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
+      for (size_t i = lo; i < hi; i++) {
+        if (ev[i].kind < RGPU_EADD || rs[i] == rd[i]) continue;
+        const bool so = role[rs[i]].load(std::memory_order_relaxed) == 0;
+        const bool dn = role[rd[i]].load(std::memory_order_relaxed) == 0;
+        if (so && !dn) role[rd[i]].store(1, std::memory_order_relaxed);
+        if (dn && !so) role[rs[i]].store(1, std::memory_order_relaxed);
+      }
+    });
+    std::vector<int32_t> g2l(ng, -1);
+    for (int r = 0; r < 2; r++)
+      for (int64_t g = 0; g < ng; g++)
+        if (role[g].load(std::memory_order_relaxed) == r) {
+          g2l[g] = (int32_t)P.vid.size();
+          P.vid.push_back(ids[g]);
+          P.grank.push_back((int32_t)g);
+          if (r == 0) P.n_own++;
+        }
+    P.nv = (int64_t)P.vid.size();
+    parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
+      for (size_t i = lo; i < hi; i++) {
+        rs[i] = g2l[rs[i]];
+        if (rd[i] >= 0) rd[i] = g2l[rd[i]];
+      }
+    });
+    P.gvid = std::move(ids);
+  }
+  const int64_t n_own = P.n_own;
+  // an edge is kept iff both endpoints are kept and one of them is owned
+  auto edge_kept = [&](size_t i) {
+    return rs[i] >= 0 && rd[i] >= 0 && (rs[i] < n_own || rd[i] < n_own);
+  };
 
   // ---- vertex histories: records grouped by rank (src of every update; dst of EdgeAdd unless
   // a self-loop), each segment sorted by (t, idx), equal t collapsed (last put wins)
@@ -199,8 +244,8 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
     auto vkey_of = [&](size_t j) -> int64_t {
       const size_t i = j >> 1;
       const Event& e = ev[i];
-      if (!(j & 1)) return e.kind == RGPU_EDEL ? -1 : rs[i];
-      return (e.kind == RGPU_EADD && rd[i] != rs[i]) ? rd[i] : -1;
+      if (!(j & 1)) return e.kind == RGPU_EDEL || rs[i] < 0 ? -1 : rs[i];
+      return (e.kind == RGPU_EADD && rd[i] != rs[i] && rd[i] >= 0) ? rd[i] : -1;
     };
     auto vmake = [&](size_t j) {
       const size_t i = j >> 1;
@@ -236,7 +281,7 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
   // ---- death lists: distinct VDEL times per rank, with the last stream index at each time
   std::vector<int64_t> dlast;
   {
-    auto dkey = [&](size_t i) -> int64_t { return ev[i].kind == RGPU_VDEL ? rs[i] : -1; };
+    auto dkey = [&](size_t i) -> int64_t { return ev[i].kind == RGPU_VDEL && rs[i] >= 0 ? rs[i] : -1; };
     auto dmake = [&](size_t i) { return Death{ev[i].t, (int64_t)i}; };
     std::vector<int64_t> off;
     std::vector<Death> dd;
@@ -264,7 +309,7 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
 
   // ---- edge own histories: grouped by src rank, each src segment sorted by (dst, t, idx)
   {
-    auto ekey = [&](size_t i) -> int64_t { return ev[i].kind >= RGPU_EADD ? rs[i] : -1; };
+    auto ekey = [&](size_t i) -> int64_t { return ev[i].kind >= RGPU_EADD && edge_kept(i) ? rs[i] : -1; };
     auto emake = [&](size_t i) {
       return EPoint{rd[i], (uint8_t)(ev[i].kind == RGPU_EADD ? 1 : 0), ev[i].t, (int64_t)i};
     };
@@ -341,6 +386,35 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
   std::vector<int64_t> fill(P.in_off.begin(), P.in_off.end() - 1);
   for (int64_t e = 0; e < P.ne; e++)
     if (P.esrc[e] != P.edst[e]) P.in_eid[fill[P.edst[e]]++] = (int32_t)e;
+
+  // ---- exchange plan (P > 1): an edge between owned v and ghost g (owner q) puts v on the
+  // send list to q and g on the receive list from q; q derives the same pair from the same
+  // edge, and both sides order by id, so entry i of our list for q is entry i of q's list
+  const int np = num_partitions;
+  std::vector<std::vector<int32_t>> S(np), R(np);
+  if (np > 1)
+    for (int64_t e = 0; e < P.ne; e++) {
+      const int32_t a = P.esrc[e], b = P.edst[e];
+      if ((a < n_own) == (b < n_own)) continue;
+      const int32_t own = a < n_own ? a : b, gh = a < n_own ? b : a;
+      const int q = partition_of(P.vid[gh], np);
+      S[q].push_back(own);
+      R[q].push_back(gh);
+    }
+  P.xs_off.assign(np + 1, 0);
+  P.xr_off.assign(np + 1, 0);
+  for (int q = 0; q < np; q++) {
+    for (auto* L : {&S[q], &R[q]}) {
+      std::sort(L->begin(), L->end());
+      L->erase(std::unique(L->begin(), L->end()), L->end());
+    }
+    P.xs_v.insert(P.xs_v.end(), S[q].begin(), S[q].end());
+    P.xs_q.insert(P.xs_q.end(), S[q].size(), q);
+    P.xr_v.insert(P.xr_v.end(), R[q].begin(), R[q].end());
+    P.xr_q.insert(P.xr_q.end(), R[q].size(), q);
+    P.xs_off[q + 1] = (int64_t)P.xs_v.size();
+    P.xr_off[q + 1] = (int64_t)P.xr_v.size();
+  }
   return "";
 }
 

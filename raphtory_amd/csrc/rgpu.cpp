@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "exchange.hpp"
 #include "kernels.hpp"
 #include "rgpu_internal.hpp"
 
@@ -81,6 +82,23 @@ struct Retained {  // per batch, RGPU_RUN_RETAIN
   std::vector<double> pr;
 };
 
+// device state of the vertex-partitioned mode (one partition per GPU)
+struct Part {
+  Exchange* xchg = nullptr;
+  int64_t nxs = 0, nxr = 0, ng = 0, hist_total = 0;
+  std::vector<int64_t> xs_off, xr_off;        // host copies of the plan offsets
+  int32_t *xs_v = nullptr, *xs_q = nullptr, *xr_v = nullptr;
+  int64_t* xs_off_d = nullptr;
+  int32_t *sbuf = nullptr, *rbuf = nullptr;   // CC boundary-row records
+  double *sbuf_f = nullptr, *rbuf_f = nullptr;  // PR contribution rows
+  int32_t *scnt = nullptr, *hist = nullptr, *chunk = nullptr;
+  int64_t *xa = nullptr, *xb = nullptr;       // [P][2] counts exchange (device)
+  int64_t* h_x = nullptr;                     // pinned host staging [2P]
+  int32_t* h_scnt = nullptr;                  // pinned [P + 1]
+  bool cc_ready = false, pr_ready = false;
+  double bytes_sent = 0;
+};
+
 struct Timed {
   int kid;
   int slot;
@@ -94,6 +112,7 @@ struct Timed {
 struct rgpu_ctx {
   std::mutex mu;
   int part = 0, nparts = 1, device = 0;
+  bool partitioned = false;  // nparts > 1, or RGPU_PARTITIONED=1 (the partitioned path with P = 1)
   std::string err;
   std::vector<Event> events;
   int64_t newest = -1;
@@ -123,6 +142,7 @@ struct rgpu_ctx {
   size_t evused = 0;
   uint64_t evcounter = 0;
   std::vector<Timed> timed;
+  Part pt;
 };
 
 namespace {
@@ -144,6 +164,13 @@ T* dupload(std::vector<void*>& list, const std::vector<T>& h) {
 void free_graph(rgpu_ctx* c) {
   for (void* p : c->graph_allocs) (void)hipFree(p);
   c->graph_allocs.clear();
+  if (c->pt.h_x) (void)hipHostFree(c->pt.h_x);
+  if (c->pt.h_scnt) (void)hipHostFree(c->pt.h_scnt);
+  {
+    Exchange* x = c->pt.xchg;
+    c->pt = Part();
+    c->pt.xchg = x;  // the communicator outlives a re-seal
+  }
   for (Slot& s : c->slot) {
     if (s.h_stepcnt) (void)hipHostFree(s.h_stepcnt);
     if (s.h_stats) (void)hipHostFree(s.h_stats);
@@ -230,6 +257,30 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       s.psmask = dalloc<uint64_t>(L, nin + nv);
     }
   }
+  if (c->partitioned) {
+    Part& X = c->pt;
+    const int P = c->nparts;
+    if (!X.h_x) {
+      HIPCHK(hipHostMalloc((void**)&X.h_x, sizeof(int64_t) * 2 * P));
+      HIPCHK(hipHostMalloc((void**)&X.h_scnt, sizeof(int32_t) * (P + 1)));
+      X.scnt = dalloc<int32_t>(L, P);
+      X.xa = dalloc<int64_t>(L, 2 * P);
+      X.xb = dalloc<int64_t>(L, 2 * P);
+    }
+    if (algo == RGPU_ALGO_CC && !X.cc_ready) {
+      X.sbuf = dalloc<int32_t>(L, (size_t)X.nxs * kXRecWords);
+      X.rbuf = dalloc<int32_t>(L, (size_t)X.nxr * kXRecWords);
+      X.hist_total = ((int64_t)kViews * X.ng + P - 1) / P * P;
+      X.hist = dalloc<int32_t>(L, X.hist_total);
+      X.chunk = dalloc<int32_t>(L, X.hist_total / P);
+      X.cc_ready = true;
+    }
+    if (algo == RGPU_ALGO_PR && !X.pr_ready) {
+      X.sbuf_f = dalloc<double>(L, (size_t)X.nxs * kViews);
+      X.rbuf_f = dalloc<double>(L, (size_t)X.nxr * kViews);
+      X.pr_ready = true;
+    }
+  }
   if (algo == RGPU_ALGO_CC) c->slot_cc = true;
   if (algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) c->slot_deg = true;
   if (algo == RGPU_ALGO_PR) c->slot_pr = true;
@@ -282,7 +333,7 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
     // batch's working set inside the Infinity Cache with several batches in flight)
     int32_t* hist = s.lab[(s.r_final + 1) & 1];
     HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)g.nv * kViews, s.stream));
-    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g, rc.K * rc.W, s.vm, s.vadj, lab, hist, s.stats); });
+    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g.nv, g.nv, rc.K * rc.W, s.vm, s.vadj, lab, hist, s.stats); });
     timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * rc.K * rc.W,
                  [&] { launch_cc_summary(s.stream, g, rc.K * rc.W, hist, s.stats); });
   }
@@ -480,6 +531,209 @@ int run_impl(rgpu_ctx* c, RunCfg& rc) {
   return 0;
 }
 
+
+// ------------------------------------------------------------------ vertex-partitioned runs
+// One batch at a time on slot 0, the host driving every superstep: the halting vote is
+// global (a ghost that changed on another GPU wakes local vertices), so each step ends in
+// the counts exchange.  Per superstep r (AnalysisTask.syncMessages/endStep,
+// AnalysisTask.scala:190-225, with the ReaderWorker message traffic replaced by rows):
+//   pack changed boundary rows -> all-to-all [rows for q, my changed flag] -> if anyone
+//   changed: grouped send/recv of the rows -> unpack into ghost rows + next frontier.
+DevGraph owned_view(const rgpu_ctx* c) {
+  DevGraph g = c->g;
+  g.nv = c->pk.n_own;  // kernels that compute per-vertex results visit owned ranks only
+  return g;
+}
+
+// returns the number of partitions' vertices that changed in step r (0 = global halt)
+int64_t cc_exchange(rgpu_ctx* c, int r) {
+  Slot& s = c->slot[0];
+  Part& X = c->pt;
+  const int P = c->nparts, me = c->part;
+  HIPCHK(hipMemsetAsync(X.scnt, 0, sizeof(int32_t) * P, s.stream));
+  launch_xpack_cc(s.stream, X.nxs, X.xs_v, X.xs_q, X.xs_off_d, r == 1 ? nullptr : s.act[r % 3], s.vm,
+                  s.chg[r & 1], r == 1 ? nullptr : s.chg[(r - 1) & 1], s.lab[r & 1], X.sbuf, X.scnt);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(X.h_scnt, X.scnt, sizeof(int32_t) * P, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipMemcpyAsync(X.h_scnt + P, s.stepcnt + r, sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipStreamSynchronize(s.stream));
+  for (int q = 0; q < P; q++) {
+    X.h_x[2 * q] = q == me ? 0 : X.h_scnt[q];
+    X.h_x[2 * q + 1] = X.h_scnt[P] != 0;
+  }
+  HIPCHK(hipMemcpyAsync(X.xa, X.h_x, sizeof(int64_t) * 2 * P, hipMemcpyHostToDevice, s.stream));
+  X.xchg->alltoall_i64(X.xa, X.xb, 2, s.stream);
+  std::vector<int64_t> sent(X.h_x, X.h_x + 2 * P);
+  HIPCHK(hipMemcpyAsync(X.h_x, X.xb, sizeof(int64_t) * 2 * P, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipStreamSynchronize(s.stream));
+  int64_t changed = 0;
+  for (int q = 0; q < P; q++) changed += X.h_x[2 * q + 1];
+  if (!changed) return 0;
+  std::vector<void*> sp(P), rp(P);
+  std::vector<size_t> sb(P), rb(P);
+  for (int q = 0; q < P; q++) {
+    sp[q] = X.sbuf + X.xs_off[q] * kXRecWords;
+    rp[q] = X.rbuf + X.xr_off[q] * kXRecWords;
+    sb[q] = (size_t)sent[2 * q] * kXRecWords * 4;
+    rb[q] = q == me ? 0 : (size_t)X.h_x[2 * q] * kXRecWords * 4;
+    X.bytes_sent += (double)sb[q];
+  }
+  X.xchg->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
+  for (int q = 0; q < P; q++)
+    if (q != me && rb[q])
+      launch_xunpack_cc(s.stream, X.h_x[2 * q], (const int32_t*)rp[q], X.xr_v + X.xr_off[q], c->g, s.cnt,
+                        s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[(r + 1) % 3]);
+  HIPCHK(hipGetLastError());
+  // the vote is global: the next superstep must run even if nothing changed here
+  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(s.stepcnt + r), 1, 1, s.stream));
+  return changed;
+}
+
+void pr_exchange(rgpu_ctx* c, double* contrib) {
+  Slot& s = c->slot[0];
+  Part& X = c->pt;
+  const int P = c->nparts, me = c->part;
+  launch_xgather_f64(s.stream, X.nxs, X.xs_v, contrib, X.sbuf_f);
+  HIPCHK(hipGetLastError());
+  std::vector<void*> sp(P), rp(P);
+  std::vector<size_t> sb(P), rb(P);
+  for (int q = 0; q < P; q++) {
+    sp[q] = X.sbuf_f + X.xs_off[q] * kViews;
+    rp[q] = X.rbuf_f + X.xr_off[q] * kViews;
+    sb[q] = q == me ? 0 : (size_t)(X.xs_off[q + 1] - X.xs_off[q]) * kViews * 8;
+    rb[q] = q == me ? 0 : (size_t)(X.xr_off[q + 1] - X.xr_off[q]) * kViews * 8;
+    X.bytes_sent += (double)sb[q];
+  }
+  X.xchg->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
+  launch_xscatter_f64(s.stream, X.nxr, X.xr_v, X.rbuf_f, contrib);
+  HIPCHK(hipGetLastError());
+}
+
+void finish_partitioned_cc(rgpu_ctx* c, const RunCfg& rc) {
+  Slot& s = c->slot[0];
+  Part& X = c->pt;
+  const int P = c->nparts, nviews = rc.K * rc.W;
+  const int32_t* lab = s.lab[s.r_final & 1];
+  // per-partition label -> count of owned members (ConnectedComponents.returnResults :37-42),
+  // summed over partitions by reduce-scatter (the cross-shard merge of
+  // processBatchWindowResults :137), each partition summarising its slice, then the summary
+  // fields all-reduced (max for biggest)
+  HIPCHK(hipMemsetAsync(X.hist, 0, sizeof(int32_t) * X.hist_total, s.stream));
+  timed_launch(c, 0, KID_HIST, 12.0 * c->pk.n_own, [&] {
+    launch_cc_hist(s.stream, c->pk.n_own, X.ng, nviews, s.vm, s.vadj, lab, X.hist, s.stats);
+  });
+  const int64_t cnt = X.hist_total / P;
+  X.xchg->reduce_scatter_i32(X.hist, X.chunk, (size_t)cnt, s.stream);
+  timed_launch(c, 0, KID_SUMMARY, 4.0 * cnt, [&] {
+    launch_cc_summary_rs(s.stream, nviews, X.chunk, cnt * c->part, cnt, X.ng, s.stats);
+  });
+  X.xchg->allreduce_u64(s.stats, kViews, true, s.stream);
+  X.xchg->allreduce_u64(s.stats + kViews, 5 * kViews, false, s.stream);
+}
+
+int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
+  const size_t nb = (rc.n_hops + rc.K - 1) / rc.K;
+  c->st.views += (int64_t)(rc.n_hops * rc.W);
+  c->st.batches += (int64_t)nb;
+  Slot& s = c->slot[0];
+  const DevGraph go = owned_view(c);
+  for (size_t b = 0; b < nb; b++) {
+    BatchParams bp;
+    std::memset(&bp, 0, sizeof(bp));
+    const size_t h0 = b * rc.K;
+    bp.K = (int)std::min<size_t>(rc.K, rc.n_hops - h0);
+    bp.W = rc.W;
+    bp.KS = rc.K;
+    bp.sorted = 1;
+    for (int k = 0; k < bp.K; k++) {
+      bp.hop[k] = rc.hops[h0 + k];
+      if (k > 0 && bp.hop[k] < bp.hop[k - 1]) bp.sorted = 0;
+    }
+    for (int w = 0; w < rc.W; w++) { bp.thr_v[w] = rc.thr_v[w]; bp.thr_e[w] = rc.thr_e[w]; }
+    s.batch = (int)b;
+    s.kb = bp.K;
+    BatchClear clr;
+    clr.stats = s.stats;
+    clr.n_stats = kStatWords;
+    clr.flags = s.stepcnt;
+    clr.n_flags = kMaxSteps;
+    if (rc.algo == RGPU_ALGO_CC) {
+      for (int k = 0; k < 3; k++) clr.act[k] = s.act[k];
+      clr.n_act_words = (c->g.nv + 7) / 8 + 1;
+    }
+    const DevGraph& g = c->g;
+    timed_launch(c, 0, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.vkey.size() + 8.0 * g.nv,
+                 [&] { launch_vertex_mask(s.stream, g, bp, s.vm, clr); });
+    timed_launch(c, 0, KID_MASK, bytes_mask(g) - (16.0 * g.nv + 8.0) + 8.0 * c->pk.ekey.size(),
+                 [&] { launch_edge_mask(s.stream, g, bp, s.em); });
+    if (rc.algo == RGPU_ALGO_CC) {
+      timed_launch(c, 0, KID_SLOTS, g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0, [&] {
+        launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
+                        s.chg[1], s.act[2], s.stepcnt, nullptr, nullptr);
+      });
+      s.r_final = 0;
+      if (rc.max_steps > 1) {
+        s.r_final = rc.max_steps;
+        if (cc_exchange(c, 1) == 0) {
+          s.r_final = 1;
+        } else {
+          for (int r = 2; r <= rc.max_steps; r++) {
+            timed_launch(c, 0, KID_STEP, 0.0, [&] {
+              launch_cc_step(s.stream, r, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
+                             s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
+                             s.act[(r + 2) % 3], s.stepcnt, nullptr, nullptr, c->step_variant);
+            }, r);
+            if (cc_exchange(c, r) == 0) { s.r_final = r; break; }
+          }
+        }
+      }
+      finish_partitioned_cc(c, rc);
+    } else {
+      timed_launch(c, 0, KID_DEGREE, go.nv * (8.0 + 32.0 + 512.0) + (double)(g.ne + g.n_in) * 12.0, [&] {
+        launch_degree(s.stream, go, s.vm, s.em, s.outdeg, s.indeg, s.stats);
+      });
+      if (rc.algo == RGPU_ALGO_PR) {
+        timed_launch(c, 0, KID_SLOTS, go.nv * (8.0 + 24.0 + 256.0 + 1024.0) + (double)(g.n_in) * 24.0, [&] {
+          launch_pr_slots(s.stream, go, s.vm, s.em, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.pr, s.contrib[0]);
+        });
+        pr_exchange(c, s.contrib[0]);
+        for (int it = 0; it < rc.pr_iters; it++) {
+          timed_launch(c, 0, KID_PR, go.nv * (8.0 + 16.0 + 4.0 + 256.0 + 1024.0) + (double)(g.n_in + go.nv) * 12.0, [&] {
+            launch_pr_step(s.stream, go, s.vm, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.contrib[it & 1],
+                           s.contrib[(it + 1) & 1], s.pr);
+          });
+          if (it + 1 < rc.pr_iters) pr_exchange(c, s.contrib[(it + 1) & 1]);
+        }
+      }
+    }
+    // stats, retained rows (finish_batch without the single-GPU CC reductions)
+    HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatWords,
+                          hipMemcpyDeviceToHost, s.stream));
+    if (rc.flags & RGPU_RUN_RETAIN) {
+      Retained& R = c->kept[b];
+      const size_t rows = (size_t)g.nv * kViews;
+      R.vm.resize(g.nv);
+      HIPCHK(hipMemcpyAsync(R.vm.data(), s.vm, sizeof(uint64_t) * g.nv, hipMemcpyDeviceToHost, s.stream));
+      if (rc.algo == RGPU_ALGO_CC) {
+        R.a.resize(rows);
+        HIPCHK(hipMemcpyAsync(R.a.data(), s.lab[s.r_final & 1], sizeof(int32_t) * rows,
+                              hipMemcpyDeviceToHost, s.stream));
+      } else if (rc.algo == RGPU_ALGO_DEGREE) {
+        R.a.resize(rows);
+        R.b.resize(rows);
+        HIPCHK(hipMemcpyAsync(R.a.data(), s.outdeg, sizeof(int32_t) * rows, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(hipMemcpyAsync(R.b.data(), s.indeg, sizeof(int32_t) * rows, hipMemcpyDeviceToHost, s.stream));
+      } else {
+        R.pr.resize(rows);
+        HIPCHK(hipMemcpyAsync(R.pr.data(), s.pr, sizeof(double) * rows, hipMemcpyDeviceToHost, s.stream));
+      }
+    }
+    HIPCHK(hipStreamSynchronize(s.stream));
+    harvest(c, 0, rc);
+  }
+  return 0;
+}
+
 int fail(rgpu_ctx* c, int code, const std::string& m) {
   if (c) c->err = m;
   return code;
@@ -509,6 +763,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->part = partition_id;
   c->nparts = num_partitions;
   c->device = device;
+  c->partitioned = num_partitions > 1 || env_int("RGPU_PARTITIONED", 0) != 0;
   c->nslots = std::max(1, std::min(kMaxSlots, env_int("RGPU_SLOTS", 3)));
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   if (env_int("RGPU_STEP_GRID", 0) > 0) g_step_grid = env_int("RGPU_STEP_GRID", 0);
@@ -548,7 +803,7 @@ int rgpu_seal(rgpu_ctx* c) {
   try {
     HIPCHK(hipSetDevice(c->device));
     std::string e = pack_events(c->events, c->part, c->nparts, &c->pk);
-    if (!e.empty()) return fail(c, c->nparts > 1 ? RGPU_ENOTSUP : RGPU_EINVAL, e);
+    if (!e.empty()) return fail(c, RGPU_EINVAL, e);
     free_graph(c);
     const Packed& P = c->pk;
     auto& L = c->graph_allocs;
@@ -573,9 +828,23 @@ int rgpu_seal(rgpu_ctx* c) {
       g.adj_off = dupload(L, adj);
     }
     g.in_eid = dupload(L, P.in_eid);
+    g.n_own = P.n_own;
+    if (c->partitioned) {
+      if (c->nparts > 1) g.grank = dupload(L, P.grank);
+      Part& X = c->pt;
+      X.ng = c->nparts > 1 ? (int64_t)P.gvid.size() : P.nv;
+      X.nxs = (int64_t)P.xs_v.size();
+      X.nxr = (int64_t)P.xr_v.size();
+      X.xs_off = P.xs_off;
+      X.xr_off = P.xr_off;
+      X.xs_v = dupload(L, P.xs_v);
+      X.xs_q = dupload(L, P.xs_q);
+      X.xr_v = dupload(L, P.xr_v);
+      X.xs_off_d = dupload(L, P.xs_off);
+    }
     c->g = g;
     HIPCHK(hipDeviceSynchronize());
-    c->st.vertices = P.nv;
+    c->st.vertices = P.n_own;
     c->st.edges = P.ne;
     c->st.vertex_events = (int64_t)P.vkey.size();
     c->st.edge_events = (int64_t)P.ekey.size();
@@ -596,11 +865,21 @@ int rgpu_newest_time(rgpu_ctx* c, int64_t* out) {
   return RGPU_OK;
 }
 
+int rgpu_exchange_id(int kind, uint8_t* out) {
+  if (!out || (kind != RGPU_XCHG_RCCL && kind != RGPU_XCHG_LOOPBACK)) return RGPU_EINVAL;
+  return make_exchange_id(kind, out).empty() ? RGPU_OK : RGPU_EHIP;
+}
+
 int rgpu_exchange_init(rgpu_ctx* c, const void* id) {
-  (void)id;
-  if (!c) return RGPU_EINVAL;
+  if (!c || !id) return RGPU_EINVAL;
   std::lock_guard<std::mutex> lk(c->mu);
-  return fail(c, RGPU_ENOTSUP, "vertex-partitioned RCCL exchange is not in this build");
+  if (!c->partitioned) return RGPU_OK;  // one partition: nothing to exchange
+  if (c->pt.xchg) return fail(c, RGPU_ESTATE, "exchange already initialised");
+  Exchange* x = nullptr;
+  std::string e = open_exchange((const uint8_t*)id, c->part, c->nparts, c->device, &x);
+  if (!e.empty()) return fail(c, RGPU_EHIP, e);
+  c->pt.xchg = x;
+  return RGPU_OK;
 }
 
 int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hops,
@@ -609,6 +888,8 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   if (!c) return RGPU_EINVAL;
   std::lock_guard<std::mutex> lk(c->mu);
   if (!c->sealed) return fail(c, RGPU_ESTATE, "rgpu_run_view_batch before rgpu_seal");
+  if (c->partitioned && !c->pt.xchg)
+    return fail(c, RGPU_ESTATE, "partitioned context: call rgpu_exchange_init before running");
   if (algo < RGPU_ALGO_CC || algo > RGPU_ALGO_PR) return fail(c, RGPU_EINVAL, "unknown algo");
   if (!hops || n_hops == 0) return fail(c, RGPU_EINVAL, "no hops");
   if (n_w > (size_t)kViews) return fail(c, RGPU_EINVAL, "more than 64 windows in one batch");
@@ -662,7 +943,9 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     for (int k = 0; k < KID_N; k++) { c->st.kernel_launches[k] = 0; c->st.kernel_ms[k] = 0; c->st.kernel_bytes[k] = 0; }
     c->st.views = c->st.batches = c->st.supersteps = 0;
     auto t0 = std::chrono::steady_clock::now();
-    run_impl(c, rc);
+    c->pt.bytes_sent = 0;
+    if (c->partitioned) run_partitioned(c, rc);
+    else run_impl(c, rc);
     for (int si = 0; si < kMaxSlots; si++)
       if (c->slot[si].stream) HIPCHK(hipStreamSynchronize(c->slot[si].stream));
     auto t1 = std::chrono::steady_clock::now();
@@ -688,8 +971,15 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     return fail(c, RGPU_EHIP, f.msg);
   } catch (const std::bad_alloc&) {
     return fail(c, RGPU_ENOMEM, "host allocation failed");
+  } catch (const std::exception& x) {  // exchange (RCCL / loopback) failures
+    return fail(c, RGPU_EHIP, x.what());
   }
   return RGPU_OK;
+}
+
+// id of the vertex whose global rank is l (CC labels are global ranks)
+static int64_t label_id(const rgpu_ctx* c, int32_t l) {
+  return c->nparts > 1 ? c->pk.gvid[l] : c->pk.vid[l];
 }
 
 static int view_index(rgpu_ctx* c, size_t hop, size_t win, size_t* batch, int* lane) {
@@ -720,11 +1010,11 @@ int rgpu_cc_vertex_labels(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
   size_t k = 0;
-  for (int64_t v = 0; v < c->pk.nv; v++) {
+  for (int64_t v = 0; v < c->pk.n_own; v++) {
     if (!((R.vm[v] >> j) & 1)) continue;
     if (k < cap) {
       ids[k] = c->pk.vid[v];
-      labels[k] = c->pk.vid[R.a[(size_t)v * kViews + j]];
+      labels[k] = label_id(c, R.a[(size_t)v * kViews + j]);
     }
     k++;
   }
@@ -742,14 +1032,14 @@ int rgpu_cc_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* labels, int32_t
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
   std::vector<int32_t> lab;
-  for (int64_t v = 0; v < c->pk.nv; v++)
+  for (int64_t v = 0; v < c->pk.n_own; v++)
     if ((R.vm[v] >> j) & 1) lab.push_back(R.a[(size_t)v * kViews + j]);
   std::sort(lab.begin(), lab.end());
   size_t k = 0;
   for (size_t i = 0; i < lab.size();) {
     size_t h = i;
     while (h < lab.size() && lab[h] == lab[i]) h++;
-    if (k < cap) { labels[k] = c->pk.vid[lab[i]]; counts[k] = (int32_t)(h - i); }
+    if (k < cap) { labels[k] = label_id(c, lab[i]); counts[k] = (int32_t)(h - i); }
     k++;
     i = h;
   }
@@ -767,7 +1057,7 @@ int rgpu_degree_vertex(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int32_
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
   size_t k = 0;
-  for (int64_t v = 0; v < c->pk.nv; v++) {
+  for (int64_t v = 0; v < c->pk.n_own; v++) {
     if (!((R.vm[v] >> j) & 1)) continue;
     if (k < cap) {
       ids[k] = c->pk.vid[v];
@@ -794,7 +1084,7 @@ int rgpu_degree_result(rgpu_ctx* c, size_t hop, size_t win, int64_t tot[3], int6
     if (c->retained) {
       const Retained& R = c->kept[b];
       std::vector<int64_t> vs;
-      for (int64_t v = 0; v < c->pk.nv; v++)
+      for (int64_t v = 0; v < c->pk.n_own; v++)
         if ((R.vm[v] >> j) & 1) vs.push_back(v);
       // DegreeBasic sorts by in-degree descending (:26); ParTrieMap tie order is not
       // deterministic, ties here go by ascending id
@@ -823,7 +1113,7 @@ int rgpu_pr_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, double* pr
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
   size_t k = 0;
-  for (int64_t v = 0; v < c->pk.nv; v++) {
+  for (int64_t v = 0; v < c->pk.n_own; v++) {
     if (!((R.vm[v] >> j) & 1)) continue;
     if (k < cap) { ids[k] = c->pk.vid[v]; pr[k] = R.pr[(size_t)v * kViews + j]; }
     k++;
@@ -849,6 +1139,8 @@ void rgpu_close(rgpu_ctx* c) {
     for (Slot& s : c->slot)
       if (s.stream) (void)hipStreamSynchronize(s.stream);
     free_graph(c);
+    delete c->pt.xchg;
+    c->pt.xchg = nullptr;
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
   }
   delete c;

@@ -23,7 +23,22 @@ struct Packed {
   std::vector<int64_t> in_off;       // [nv+1] in-edges (no self-loops), ordered by (dst, src)
   std::vector<int32_t> in_eid;       // [in_off[nv]] edge ids of in-edges
   int64_t newest = -1;
+  // ---- vertex partitioning (num_partitions > 1); identity when P = 1
+  int part = 0, nparts = 1;
+  int64_t n_own = 0;                 // ranks [0, n_own) are owned here, [n_own, nv) are ghosts
+  std::vector<int32_t> grank;        // [nv] global rank = CC label of each local rank (P > 1)
+  std::vector<int64_t> gvid;         // global vertex ids ascending (P > 1): label -> id
+  // exchange plan: per peer q, owned ranks that are ghosts on q (xs) and ghosts owned by q
+  // (xr), both ascending by id, so q's xr list for this partition equals this xs list for q
+  std::vector<int64_t> xs_off, xr_off;  // [P+1]
+  std::vector<int32_t> xs_v, xr_v, xs_q, xr_q;
 };
+
+// Utils.getPartition (S/core/utils/Utils.scala:32-33): (|id| mod 10P) div 10
+inline int partition_of(int64_t id, int nparts) {
+  const int64_t a = id < 0 ? -id : id;
+  return (int)((a % (10 * (int64_t)nparts)) / 10);
+}
 
 struct Event {
   int64_t t;

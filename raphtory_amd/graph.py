@@ -76,6 +76,22 @@ class TemporalGraph:
     def seal(self) -> None:
         self._check(self._lib.rgpu_seal(self._ctx))
 
+    # ------------------------------------------------------------------ partitions
+    @staticmethod
+    def exchange_id(loopback: bool = False) -> bytes:
+        """Id blob for rgpu_exchange_init: an RCCL unique id (one process per GPU; make it on
+        one rank and broadcast it) or a loopback group key (partitions in one process)."""
+        buf = C.create_string_buffer(N.RGPU_XCHG_ID_BYTES)
+        rc = N.rgpu().rgpu_exchange_id(N.RGPU_XCHG_LOOPBACK if loopback else N.RGPU_XCHG_RCCL, buf)
+        if rc != 0:
+            raise RGPUError(rc, "rgpu_exchange_id failed")
+        return buf.raw
+
+    def exchange_init(self, xid: bytes) -> None:
+        if len(xid) != N.RGPU_XCHG_ID_BYTES:
+            raise ValueError("exchange id must be RGPU_XCHG_ID_BYTES long")
+        self._check(self._lib.rgpu_exchange_init(self._ctx, xid))
+
     def newest_time(self) -> int:
         out = C.c_int64()
         self._check(self._lib.rgpu_newest_time(self._ctx, C.byref(out)))

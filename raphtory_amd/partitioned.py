@@ -1,0 +1,109 @@
+"""Vertex-partitioned runs: one partition per GPU, boundary label rows
+exchanged every superstep (RCCL), component sizes merged across partitions.
+
+Two ways to hold the partitions:
+  * one process per GPU (torch.distributed): :func:`open_rccl_partition` gives this rank's
+    TemporalGraph, joined to an RCCL communicator whose id rank 0 broadcasts;
+  * :class:`LoopbackPartitions`: all P partitions in one process (one host thread each, same
+    or different devices) over the library's loopback exchange — the same protocol, used to
+    test the partitioned path on one GPU.
+
+Each partition must be handed the whole update stream (include/rgpu.h); runs are
+collective (every partition calls run with the same arguments).
+"""
+from __future__ import annotations
+
+import threading
+from typing import Callable, List, Sequence
+
+import numpy as np
+
+from .graph import TemporalGraph
+
+
+def open_rccl_partition(device: int, dist=None) -> TemporalGraph:
+    """This rank's partition (partition = rank, P = world size), joined to the RCCL group."""
+    if dist is None:
+        import torch.distributed as dist
+    rank, world = dist.get_rank(), dist.get_world_size()
+    g = TemporalGraph(rank, world, device)
+    box = [TemporalGraph.exchange_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    g.exchange_init(box[0])  # collective: every rank joins the communicator here
+    return g
+
+
+class LoopbackPartitions:
+    def __init__(self, nparts: int, device: int | Sequence[int] = 0):
+        devs = [device] * nparts if isinstance(device, int) else list(device)
+        self.parts: List[TemporalGraph] = [TemporalGraph(p, nparts, devs[p]) for p in range(nparts)]
+        xid = TemporalGraph.exchange_id(loopback=True)
+        for g in self.parts:
+            g.exchange_init(xid)
+
+    def _all(self, fn: Callable[[TemporalGraph], object]) -> list:
+        out, errs = [None] * len(self.parts), []
+
+        def body(i):
+            try:
+                out[i] = fn(self.parts[i])
+            except BaseException as e:  # noqa: BLE001 - re-raised below
+                errs.append(e)
+
+        th = [threading.Thread(target=body, args=(i,)) for i in range(len(self.parts))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
+        return out
+
+    def ingest_stream(self, s) -> None:
+        for g in self.parts:
+            g.ingest_stream(s)
+
+    def seal(self) -> None:
+        self._all(lambda g: g.seal())
+
+    def run(self, *a, **kw) -> None:
+        self._all(lambda g: g.run(*a, **kw))
+
+    # merged results ------------------------------------------------------------
+    def cc_summary(self, hop: int, win: int):
+        return self.parts[0].cc_summary(hop, win)
+
+    def cc_vertex_labels(self, hop: int, win: int):
+        ids, lab = zip(*[g.cc_vertex_labels(hop, win) for g in self.parts])
+        ids, lab = np.concatenate(ids), np.concatenate(lab)
+        o = np.argsort(ids, kind="stable")
+        return ids[o], lab[o]
+
+    def cc_result(self, hop: int, win: int) -> dict:
+        out: dict = {}
+        for g in self.parts:  # processBatchWindowResults merge (ConnectedComponents.scala:49)
+            for k, v in g.cc_result(hop, win).items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def degree_vertex(self, hop: int, win: int):
+        cols = list(zip(*[g.degree_vertex(hop, win) for g in self.parts]))
+        ids, od, idg = (np.concatenate(c) for c in cols)
+        o = np.argsort(ids, kind="stable")
+        return ids[o], od[o], idg[o]
+
+    def degree_totals(self, hop: int, win: int):
+        tot = np.zeros(3, np.int64)
+        for g in self.parts:  # DegreeBasic.processWindowResults sums shard tuples (:35-36)
+            tot += np.asarray(g.degree_result(hop, win)[:3])
+        return tuple(int(x) for x in tot)
+
+    def pr_result(self, hop: int, win: int):
+        ids, pr = zip(*[g.pr_result(hop, win) for g in self.parts])
+        ids, pr = np.concatenate(ids), np.concatenate(pr)
+        o = np.argsort(ids, kind="stable")
+        return ids[o], pr[o]
+
+    def close(self) -> None:
+        for g in self.parts:
+            g.close()

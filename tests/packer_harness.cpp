@@ -19,10 +19,34 @@ extern "C" void* ph_pack(const int64_t* t, const uint8_t* kind, const int64_t* s
   if (!rgpu::pack_events(ev, 0, 1, p).empty()) { delete p; return nullptr; }
   return p;
 }
+// partition view (num_partitions > 1): same stream, one partition's pack
+extern "C" void* ph_pack_part(const int64_t* t, const uint8_t* kind, const int64_t* src, const int64_t* dst,
+                              size_t n, int part, int nparts) {
+  std::vector<Event> ev(n);
+  for (size_t i = 0; i < n; i++) ev[i] = {t[i], src[i], kind[i] >= 2 ? dst[i] : -1, kind[i]};
+  Packed* p = new Packed();
+  if (!rgpu::pack_events(ev, part, nparts, p).empty()) { delete p; return nullptr; }
+  return p;
+}
+// what: 0 local vertex ids [nv], 1 global rank per local rank [nv] (P > 1), 2 send list ids of
+// peer q, 3 receive list ids of peer q, 4 edge src ids, 5 edge dst ids; returns the count
+extern "C" int64_t ph_list(void* h, int what, int q, int64_t* out) {
+  const Packed* p = (const Packed*)h;
+  std::vector<int64_t> v;
+  if (what == 0) v.assign(p->vid.begin(), p->vid.end());
+  if (what == 1) v.assign(p->grank.begin(), p->grank.end());
+  if (what == 2) for (int64_t i = p->xs_off[q]; i < p->xs_off[q + 1]; i++) v.push_back(p->vid[p->xs_v[i]]);
+  if (what == 3) for (int64_t i = p->xr_off[q]; i < p->xr_off[q + 1]; i++) v.push_back(p->vid[p->xr_v[i]]);
+  if (what == 4) for (int64_t e = 0; e < p->ne; e++) v.push_back(p->vid[p->esrc[e]]);
+  if (what == 5) for (int64_t e = 0; e < p->ne; e++) v.push_back(p->vid[p->edst[e]]);
+  if (out) std::copy(v.begin(), v.end(), out);
+  return (int64_t)v.size();
+}
 extern "C" void ph_free(void* h) { delete (Packed*)h; }
 extern "C" int64_t ph_num(void* h, int what) {
   const Packed* p = (const Packed*)h;
-  return what == 0 ? p->nv : what == 1 ? p->ne : what == 2 ? (int64_t)p->vkey.size() : (int64_t)p->ekey.size();
+  return what == 0 ? p->nv : what == 1 ? p->ne : what == 2 ? (int64_t)p->vkey.size()
+       : what == 3 ? (int64_t)p->ekey.size() : p->n_own;
 }
 
 static int64_t floor_key(const std::vector<int64_t>& key, int64_t lo, int64_t hi, int64_t t) {
@@ -37,9 +61,12 @@ static int64_t last_death(const Packed* p, int32_t r, int64_t t) {
 // window < 0 => ViewLens (no window)
 extern "C" int ph_alive(void* h, int is_edge, int64_t src, int64_t dst, int64_t t, int64_t window) {
   const Packed* p = (const Packed*)h;
-  auto rank = [&](int64_t id) -> int64_t {
-    auto it = std::lower_bound(p->vid.begin(), p->vid.end(), id);
-    return (it == p->vid.end() || *it != id) ? -1 : it - p->vid.begin();
+  auto rank = [&](int64_t id) -> int64_t {  // local order is (owned, ghost) by id: search both runs
+    for (auto [lo, hi] : {std::pair<int64_t, int64_t>{0, p->n_own}, {p->n_own, p->nv}}) {
+      auto it = std::lower_bound(p->vid.begin() + lo, p->vid.begin() + hi, id);
+      if (it != p->vid.begin() + hi && *it == id) return it - p->vid.begin();
+    }
+    return -1;
   };
   const int64_t rs = rank(src);
   if (rs < 0) return 0;

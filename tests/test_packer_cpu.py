@@ -2,43 +2,21 @@
 test harness, against the oracle's literal EntityStorage replay: every vertex and edge
 liveness decision (aliveAt / aliveAtWithWindow) at many times and windows, on tie-heavy and
 out-of-order streams, single- and multi-threaded packing."""
-import ctypes as C
-import os
-import subprocess
-
 import numpy as np
 import pytest
 
 from oracle import Oracle
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO = os.path.join(ROOT, "tests", "_build", "libpacker_harness.so")
+from harness import load_packer_harness, pack
 
 
 @pytest.fixture(scope="module")
 def ph():
-    os.makedirs(os.path.dirname(SO), exist_ok=True)
-    src = [os.path.join(ROOT, "tests", "packer_harness.cpp"), os.path.join(ROOT, "raphtory_amd", "csrc", "packer.cpp")]
-    if not os.path.exists(SO) or any(os.path.getmtime(s) > os.path.getmtime(SO) for s in src):
-        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread",
-                        "-I", os.path.join(ROOT, "raphtory_amd", "csrc"), "-o", SO] + src, check=True)
-    L = C.CDLL(SO)
-    P64, PU8 = C.POINTER(C.c_int64), C.POINTER(C.c_uint8)
-    L.ph_pack.restype = C.c_void_p
-    L.ph_pack.argtypes = [P64, PU8, P64, P64, C.c_size_t]
-    L.ph_alive.restype = C.c_int
-    L.ph_alive.argtypes = [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_int64]
-    L.ph_free.argtypes = [C.c_void_p]
-    L.ph_num.restype = C.c_int64
-    L.ph_num.argtypes = [C.c_void_p, C.c_int]
-    return L
+    return load_packer_harness()
 
 
 def _pack(L, t, k, s, d):
-    p = lambda a, ty: a.ctypes.data_as(C.POINTER(ty))
-    h = L.ph_pack(p(t, C.c_int64), p(k, C.c_uint8), p(s, C.c_int64), p(d, C.c_int64), len(t))
-    assert h
-    return h
+    return pack(L, t, k, s, d)
 
 
 def _stream(seed, n, nv, tie, shuffle=False):

@@ -1,0 +1,134 @@
+"""Vertex-partitioned packing on the CPU: the product's host packer built
+with g++ (tests/harness.py).  Checks, per partition of P:
+  * owned vertices are exactly Utils.getPartition(id, P) == p (Utils.scala:32-33) and ghosts
+    exactly their non-owned neighbours; edges exactly those touching an owned vertex;
+  * every owned / ghost vertex and every kept edge is alive at exactly the same (t, w) as in
+    the one-partition pack (so ghost histories and endpoint deaths are complete);
+  * the exchange plan is symmetric: partition p's send list for q equals q's receive list
+    from p, entry by entry (this is what lets boundary rows travel as (index, row) records);
+  * the same plan agreement across two real processes (gloo, world size 2)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from harness import load_packer_harness, pack, plist
+from raphtory_amd.partition import get_partition
+
+
+@pytest.fixture(scope="module")
+def ph():
+    return load_packer_harness()
+
+
+def _stream(seed, n, nv, tie=2):
+    rng = np.random.default_rng(seed)
+    t = (np.arange(n) // tie).astype(np.int64) * 5
+    k = rng.choice(4, size=n, p=[0.25, 0.45, 0.12, 0.18]).astype(np.uint8)
+    ids = rng.choice(np.arange(10 * nv), size=nv, replace=False).astype(np.int64)  # spread over partitions
+    s = ids[rng.integers(0, nv, n)]
+    d = np.where(k >= 2, ids[rng.integers(0, nv, n)], -1).astype(np.int64)
+    return t, k, s, d
+
+
+@pytest.mark.parametrize("P", [2, 3, 5])
+def test_roles_edges_and_plan(ph, P):
+    t, k, s, d = _stream(P, 6000, 300)
+    all_ids = np.unique(np.concatenate([s, d[k >= 2]]))
+    e = k >= 2
+    pairs = {(int(a), int(b)) for a, b in zip(s[e], d[e])}
+    handles = [pack(ph, t, k, s, d, p, P) for p in range(P)]
+    owned_union = []
+    for p, h in enumerate(handles):
+        vid = plist(ph, h, 0)
+        n_own = ph.ph_num(h, 4)
+        own, ghost = vid[:n_own], vid[n_own:]
+        assert np.all(np.diff(own) > 0) and np.all(np.diff(ghost) > 0)
+        assert np.array_equal(own, all_ids[get_partition(all_ids, P) == p])
+        owned_union.append(own)
+        own_set = set(own.tolist())
+        nbrs = {b for a, b in pairs if a in own_set and a != b} | {a for a, b in pairs if b in own_set and a != b}
+        assert set(ghost.tolist()) == nbrs - own_set
+        # global ranks index the global id list
+        gr = plist(ph, h, 1)
+        assert np.array_equal(all_ids[gr], vid)
+        kept = set(zip(plist(ph, h, 4).tolist(), plist(ph, h, 5).tolist()))
+        assert kept == {(a, b) for a, b in pairs if a in own_set or b in own_set}
+    assert np.array_equal(np.sort(np.concatenate(owned_union)), all_ids)
+    for p in range(P):
+        assert len(plist(ph, handles[p], 2, p)) == 0 and len(plist(ph, handles[p], 3, p)) == 0
+        for q in range(P):
+            if q != p:
+                assert np.array_equal(plist(ph, handles[p], 2, q), plist(ph, handles[q], 3, p))
+    for h in handles:
+        ph.ph_free(h)
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_partition_liveness_matches_single(ph, P):
+    t, k, s, d = _stream(10 + P, 5000, 120, tie=3)
+    h1 = pack(ph, t, k, s, d)
+    e = k >= 2
+    pairs = sorted({(int(a), int(b)) for a, b in zip(s[e], d[e])})
+    times = np.unique(np.concatenate([t[::37], t[::53] + 1]))[::3]
+    bad = 0
+    for p in range(P):
+        hp = pack(ph, t, k, s, d, p, P)
+        vid = plist(ph, hp, 0)
+        kept = list(zip(plist(ph, hp, 4).tolist(), plist(ph, hp, 5).tolist()))
+        for tt in times.tolist():
+            for w in (-1, 0, 40, 2000):
+                for v in vid.tolist():
+                    bad += ph.ph_alive(hp, 0, v, -1, tt, w) != ph.ph_alive(h1, 0, v, -1, tt, w)
+                for a, b in kept[:: max(1, len(kept) // 60)]:
+                    bad += ph.ph_alive(hp, 1, a, b, tt, w) != ph.ph_alive(h1, 1, a, b, tt, w)
+        ph.ph_free(hp)
+    ph.ph_free(h1)
+    assert len(pairs) > 100 and bad == 0
+
+
+# ---------------------------------------------------------------- two processes (gloo)
+def _free_port():
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    p = so.getsockname()[1]
+    so.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    L = load_packer_harness()
+    t, k, s, d = _stream(77, 8000, 400)  # every rank is handed the whole stream
+    h = pack(L, t, k, s, d, rank, world)
+    mine = {"own": plist(L, h, 0)[:L.ph_num(h, 4)].tolist(),
+            "send": {p: plist(L, h, 2, p).tolist() for p in range(world)},
+            "recv": {p: plist(L, h, 3, p).tolist() for p in range(world)}}
+    allp = [None] * world
+    dist.all_gather_object(allp, mine)
+    ok = all(allp[a]["send"][b] == allp[b]["recv"][a] for a in range(world) for b in range(world) if a != b)
+    owned = sorted(sum((x["own"] for x in allp), []))
+    ids = np.unique(np.concatenate([s, d[k >= 2]])).tolist()
+    if rank == 0:
+        q.put((ok, owned == ids, sum(len(x["send"][1 - i]) for i, x in enumerate(allp))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_partition_plan_world2_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok, cover, nsend = q.get(timeout=180)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert ok and cover and nsend > 0
