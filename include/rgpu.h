@@ -74,7 +74,7 @@ typedef struct {
   int64_t views, batches, supersteps, launches;
   double ms_total;               /* wall ms inside the last rgpu_run_view_batch */
   /* per-kernel event timing (RGPU_RUN_PROFILE): 0=window_mask 1=slots 2=cc_step 3=cc_hist
-   * 4=cc_summary 5=pr_step 6=degree */
+   * 4=cc_summary 5=pr_step 6=degree 7=cc_tail (late supersteps, one workgroup) */
   int64_t kernel_launches[8];
   double kernel_ms[8];
   double kernel_bytes[8];        /* algorithmic bytes summed over launches */

@@ -26,7 +26,7 @@ ERROR_NAMES = {
     RGPU_ENOMEM: "RGPU_ENOMEM",
     RGPU_ENOTSUP: "RGPU_ENOTSUP",
 }
-KERNEL_NAMES = ["window_mask", "cc_slots", "cc_step", "cc_hist", "cc_summary", "pr_step", "degree", "-"]
+KERNEL_NAMES = ["window_mask", "cc_slots", "cc_step", "cc_hist", "cc_summary", "pr_step", "degree", "cc_tail"]
 
 # exported symbols of librgpu.so, exactly the declarations of include/rgpu.h
 EXPORTS = [

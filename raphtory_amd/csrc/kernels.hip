@@ -104,24 +104,57 @@ __device__ __forceinline__ int64_t death_advance(const int64_t* dt, int64_t p, i
   return first_after(dt, p, hi, t);
 }
 
-// The first kernel of every batch also clears the batch's small state (stats words, superstep
-// flags, frontier flags), so a batch needs no memset launches.
+// A batch's small state (stats words, superstep flags, frontier flags) is cleared by its
+// first kernel: the vertex-mask kernel when the batch has its own masks, else k_batch_clear.
+__device__ __forceinline__ void batch_clear(const BatchClear& clr) {
+  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = tid; i < clr.n_stats; i += nth) clr.stats[i] = 0;
+  for (int64_t i = tid; i < clr.n_flags; i += nth) clr.flags[i] = 0;
+  for (int b = 0; b < 3; b++)
+    if (clr.act[b])
+      for (int64_t i = tid; i < clr.n_act_words; i += nth) reinterpret_cast<uint64_t*>(clr.act[b])[i] = 0;
+}
+__global__ __launch_bounds__(256) void k_batch_clear(BatchClear clr) { batch_clear(clr); }
+
+// Window test of one entity at hop k (age = t - floor time): view bits of every window.
+// PLANAR = false: one word, bit w*KS + k (all windows of the batch in one label row).
+// PLANAR = true : one word per window (plane w, bit k), W <= kMaxPlanes — the masks of one
+// hop block for every window-major batch that will use it.
+template <bool PLANAR>
+__device__ __forceinline__ void window_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const BatchParams& bp,
+                                            const int64_t* thr, int64_t age, int k) {
+  if constexpr (PLANAR) {
+#pragma unroll
+    for (int w = 0; w < kMaxPlanes; w++)
+      if (w < bp.W && age <= thr[w]) m[w] |= 1ull << k;
+  } else {
+    for (int w = 0; w < bp.W; w++)
+      if (age <= thr[w]) m[0] |= 1ull << (w * bp.KS + k);
+  }
+}
+template <bool PLANAR>
+__device__ __forceinline__ void store_bits(const uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const BatchParams& bp,
+                                           uint64_t* out, int64_t stride, int64_t i) {
+  if constexpr (PLANAR) {
+#pragma unroll
+    for (int w = 0; w < kMaxPlanes; w++)
+      if (w < bp.W) out[w * stride + i] = m[w];
+  } else {
+    out[i] = m[0];
+  }
+}
+
+template <bool PLANAR>
 __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* __restrict__ voff,
                                                      const int64_t* __restrict__ vkey, BatchParams bp,
-                                                     uint64_t* __restrict__ vm, BatchClear clr) {
-  {
-    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t nth = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = tid; i < clr.n_stats; i += nth) clr.stats[i] = 0;
-    for (int64_t i = tid; i < clr.n_flags; i += nth) clr.flags[i] = 0;
-    for (int b = 0; b < 3; b++)
-      if (clr.act[b])
-        for (int64_t i = tid; i < clr.n_act_words; i += nth) reinterpret_cast<uint64_t*>(clr.act[b])[i] = 0;
-  }
+                                                     uint64_t* __restrict__ vm, int64_t vstride,
+                                                     BatchClear clr) {
+  batch_clear(clr);
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv;
        v += (int64_t)gridDim.x * blockDim.x) {
     const int64_t lo = voff[v], hi = voff[v + 1];
-    uint64_t m = 0;
+    uint64_t m[PLANAR ? kMaxPlanes : 1] = {};
     int64_t f = -1;
     for (int k = 0; k < bp.K; k++) {
       const int64_t t = bp.hop[k];
@@ -130,26 +163,26 @@ __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* 
       const int64_t key = vkey[f];
       if (!(key & 1)) continue;  // floor is a deletion
       const int64_t age = t - (key >> 1);
-      for (int w = 0; w < bp.W; w++)
-        if (age <= bp.thr_v[w]) m |= 1ull << (w * bp.KS + k);
+      window_bits<PLANAR>(m, bp, bp.thr_v, age, k);
     }
-    vm[v] = m;
+    store_bits<PLANAR>(m, bp, vm, vstride, v);
   }
 }
 
+template <bool PLANAR>
 __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __restrict__ esrc,
                                                    const int32_t* __restrict__ edst,
                                                    const int64_t* __restrict__ eoff,
                                                    const int64_t* __restrict__ ekey,
                                                    const int64_t* __restrict__ doff,
                                                    const int64_t* __restrict__ dtime, BatchParams bp,
-                                                   uint64_t* __restrict__ em) {
+                                                   uint64_t* __restrict__ em, int64_t estride) {
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t lo = eoff[e], hi = eoff[e + 1];
     const int32_t s = esrc[e], d = edst[e];
     const int64_t s0 = doff[s], s1 = doff[s + 1], d0 = doff[d], d1 = doff[d + 1];
-    uint64_t m = 0;
+    uint64_t m[PLANAR ? kMaxPlanes : 1] = {};
     int64_t f = -1, ps = s0, pd = d0;
     for (int k = 0; k < bp.K; k++) {
       const int64_t t = bp.hop[k];
@@ -176,10 +209,9 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
       // an endpoint death in (ft, t] is a later kill point (killList / vertexRemoval)
       if (lds > ft || ldd > ft) continue;
       const int64_t age = t - ft;
-      for (int w = 0; w < bp.W; w++)
-        if (age <= bp.thr_e[w]) m |= 1ull << (w * bp.KS + k);
+      window_bits<PLANAR>(m, bp, bp.thr_e, age, k);
     }
-    em[e] = m;
+    store_bits<PLANAR>(m, bp, em, estride, e);
   }
 }
 
@@ -399,66 +431,74 @@ __device__ __forceinline__ void gather_min_x4(const uint64_t (&act)[4], const in
   }
 }
 
-// Superstep kernel.  Frontier flags are bytes (plain idempotent stores, no RMW), and a
-// wave's CH-vertex chunk runs loads-first: metadata + own change words + own label rows,
-// slot rows, neighbour change words, then every label gather of the chunk, and only then
-// the stores (rows, change words, next-frontier flags).  On CDNA stores and atomics count in
-// vmcnt, so interleaving them with the next vertex's loads would serialise the chunk.  All
-// loads are unconditional from padded buffers (see gather_min).  A visited vertex rewrites
-// its row only if it changed now or in the previous step (the only cases where the two
-// label buffers differ).
-template <int CH, bool BUF>
-__global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const int64_t* __restrict__ adj_off,
-                                                  const uint64_t* __restrict__ vm,
-                                                  const int32_t* __restrict__ cnt,
-                                                  const int32_t* __restrict__ snbr,
-                                                  const uint64_t* __restrict__ smask,
-                                                  const int32_t* __restrict__ lab_cur,
-                                                  int32_t* __restrict__ lab_next,
-                                                  const uint64_t* __restrict__ chg_prev,
-                                                  uint64_t* __restrict__ chg_next,
-                                                  const uint8_t* __restrict__ act_cur,
-                                                  uint8_t* __restrict__ act_next,
-                                                  uint8_t* __restrict__ act_clear,
-                                                  int32_t* __restrict__ stepflag,
-                                                  int32_t* __restrict__ hostflag,
-                                                  unsigned long long* __restrict__ work) {
-  if (stepflag[step - 1] == 0) return;
-  __shared__ int32_t red;
-  __shared__ unsigned long long wred[2];
-  if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; }
-  const int64_t nwords = (nv + 7) >> 3;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
-       i += (int64_t)gridDim.x * blockDim.x)
-    reinterpret_cast<uint64_t*>(act_clear)[i] = 0;
-  __syncthreads();
-  const int lane = lane_id();
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  int32_t changed = 0;
-  unsigned long long pv = 0, ps = 0;
-  for (int64_t c = wave; c * CH < nv; c += nwaves) {
-    const int64_t v0 = c * CH;
-    uint32_t bits = 0;
-    {
-      const uint64_t f = CH == 8 ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
-                                 : *reinterpret_cast<const uint32_t*>(act_cur + v0);
-#pragma unroll
-      for (int i = 0; i < CH; i++) bits |= ((f >> (8 * i)) & 0xffu) ? (1u << i) : 0u;
-    }
-    if (v0 + CH > nv) bits &= (1u << (nv - v0)) - 1;
-    if (!bits) continue;
-    // stage 1: metadata (lane i -> vertex v0+i), own change words, own label rows
-    const int64_t vl = v0 + (lane & (CH - 1));
+// Frontier list of the single-workgroup tail kernel (k_cc_tail), in LDS.
+constexpr int kTailListCap = 2048;
+struct TailList {
+  int32_t* list;  // next frontier
+  int* n;         // its length; may run past kTailListCap (the entries past it are dropped)
+};
+
+// Set the frontier flag of v (byte per vertex) and report whether it was clear before.
+__device__ __forceinline__ bool flag_fresh(uint8_t* act, int64_t v) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(act + (v & ~(int64_t)3));
+  const int sh = 8 * (int)(v & 3);
+  return (atomicOr(w, 1u << sh) & (0xffu << sh)) == 0;
+}
+// Wave-uniform call: append the lanes with `fresh` to the list.
+__device__ __forceinline__ void list_append(bool fresh, int32_t v, const TailList& tl, int lane) {
+  const uint64_t b = __ballot(fresh);
+  if (!b) return;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(tl.n, __popcll(b));
+  base = __builtin_amdgcn_readlane(base, 0);
+  const int idx = base + __popcll(b & lanemask_lt());
+  if (fresh && idx < kTailListCap) tl.list[idx] = v;
+}
+// Next-frontier flag of v on the lanes with `want`: a plain byte store (full-grid kernel:
+// idempotent, no RMW) or flag + list append (tail kernel).  Wave-uniform call.
+template <bool TAIL>
+__device__ __forceinline__ void mark(bool want, int32_t v, uint8_t* act_next, const TailList& tl, int lane) {
+  if (!TAIL) {
+    if (want) act_next[v] = 1;
+  } else {
+    const bool fresh = want && flag_fresh(act_next, v);
+    list_append(fresh, v, tl, lane);
+  }
+}
+
+// One CH-vertex chunk of a superstep.  Vertex i (< CH) of the chunk is readlane(vl, i) and
+// is taken iff bit i of `bits` is set; every lane holds a valid (padded) vertex for the
+// unconditional loads.  The chunk runs loads-first: metadata + own change words + own label
+// rows, slot rows, neighbour change words, then every label gather of the chunk, and only
+// then the stores (rows, change words, next-frontier flags).  On CDNA stores and atomics
+// count in vmcnt, so interleaving them with the next vertex's loads would serialise the
+// chunk.  All loads are unconditional from padded buffers (see gather_min).  A visited
+// vertex rewrites its row only if it changed now or in the previous step (the only cases
+// where the two label buffers differ).
+template <int CH, bool BUF, bool TAIL>
+__device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_t* __restrict__ adj_off,
+                                         const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
+                                         const int32_t* __restrict__ snbr,
+                                         const uint64_t* __restrict__ smask,
+                                         const int32_t* __restrict__ lab_cur, int32_t* __restrict__ lab_next,
+                                         const uint64_t* __restrict__ chg_prev,
+                                         uint64_t* __restrict__ chg_next, uint8_t* __restrict__ act_next,
+                                         const TailList& tl, int lane, int32_t& changed,
+                                         unsigned long long& pv, unsigned long long& ps) {
+  {
+    // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
     const uint64_t mv_l = okl ? vm[vl] : 0;
     const int32_t n_l = okl ? cnt[vl] : 0;
     const int64_t b_l = adj_off[vl];
     const uint64_t cp_l = chg_prev[vl];
+    int64_t vv[CH];
     int32_t cur[CH];
 #pragma unroll
-    for (int i = 0; i < CH; i++)
-      cur[i] = row_get<BUF>(lab_cur + (v0 + i) * 64, (readlane64(mv_l, i) >> lane) & 1, lane);
+    for (int i = 0; i < CH; i++) {
+      vv[i] = (int64_t)readlane64((uint64_t)vl, i);
+      cur[i] = row_get<BUF>(lab_cur + vv[i] * 64, (readlane64(mv_l, i) >> lane) & 1, lane);
+    }
     // stage 2: first 64 kept slots of each vertex (clamped loads, masked by select)
     int32_t nb[CH];
     uint64_t sm[CH];
@@ -508,7 +548,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     for (int i = 0; i < CH; i++) {
       const uint64_t mv = readlane64(mv_l, i);
       if (mv == 0) continue;
-      const int64_t v = v0 + i;
+      const int64_t v = vv[i];
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
       pv += 1;
       ps += (unsigned long long)n;
@@ -520,17 +560,69 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
       if (lane == 0) chg_next[v] = ch;
       if (ch) {
         changed++;
-        if (lane == 0) act_next[v] = 1;
-        if (sm[i] & ch) act_next[nb[i]] = 1;
+        mark<TAIL>(lane == 0, (int32_t)v, act_next, tl, lane);
+        mark<TAIL>((sm[i] & ch) != 0, nb[i], act_next, tl, lane);
         if (n > 64) {
           const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
           for (int32_t c2 = 64; c2 < n; c2 += 64) {
             const int32_t j = c2 + lane;
-            if (j < n && (smask[base + j] & ch)) act_next[snbr[base + j]] = 1;
+            const int64_t idx = base + (j < n ? j : c2);
+            const int32_t q = snbr[idx];
+            mark<TAIL>(j < n && (smask[idx] & ch) != 0, q, act_next, tl, lane);
           }
         }
       }
     }
+  }
+}
+
+// Superstep kernel (full grid).  Step r visits the vertices flagged in act_cur (bytes, plain
+// idempotent stores by step r-1), CH consecutive ranks per wave-chunk, and clears act_clear
+// (read two steps ago, written next step).
+template <int CH, bool BUF>
+__global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const int64_t* __restrict__ adj_off,
+                                                  const uint64_t* __restrict__ vm,
+                                                  const int32_t* __restrict__ cnt,
+                                                  const int32_t* __restrict__ snbr,
+                                                  const uint64_t* __restrict__ smask,
+                                                  const int32_t* __restrict__ lab_cur,
+                                                  int32_t* __restrict__ lab_next,
+                                                  const uint64_t* __restrict__ chg_prev,
+                                                  uint64_t* __restrict__ chg_next,
+                                                  const uint8_t* __restrict__ act_cur,
+                                                  uint8_t* __restrict__ act_next,
+                                                  uint8_t* __restrict__ act_clear,
+                                                  int32_t* __restrict__ stepflag,
+                                                  int32_t* __restrict__ hostflag,
+                                                  unsigned long long* __restrict__ work) {
+  if (stepflag[step - 1] == 0) return;
+  __shared__ int32_t red;
+  __shared__ unsigned long long wred[2];
+  if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; }
+  const int64_t nwords = (nv + 7) >> 3;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
+       i += (int64_t)gridDim.x * blockDim.x)
+    reinterpret_cast<uint64_t*>(act_clear)[i] = 0;
+  __syncthreads();
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  int32_t changed = 0;
+  unsigned long long pv = 0, ps = 0;
+  const TailList none{nullptr, nullptr};
+  for (int64_t c = wave; c * CH < nv; c += nwaves) {
+    const int64_t v0 = c * CH;
+    uint32_t bits = 0;
+    {
+      const uint64_t f = CH == 8 ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
+                                 : *reinterpret_cast<const uint32_t*>(act_cur + v0);
+#pragma unroll
+      for (int i = 0; i < CH; i++) bits |= ((f >> (8 * i)) & 0xffu) ? (1u << i) : 0u;
+    }
+    if (v0 + CH > nv) bits &= (1u << (nv - v0)) - 1;
+    if (!bits) continue;
+    cc_chunk<CH, BUF, false>(v0 + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
+                             lab_next, chg_prev, chg_next, act_next, none, lane, changed, pv, ps);
   }
   if (lane == 0) {
     if (changed) atomicAdd(&red, changed);
@@ -547,58 +639,166 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   }
 }
 
+// Late supersteps touch tens to hundreds of vertices (long chains converging), yet as
+// separate full-grid launches each pays ~8-10 us of launch + dependent-load latency.
+// k_cc_tail runs them back to back inside ONE workgroup (16 waves on one CU) with a barrier
+// between supersteps: one workgroup's global stores are visible to its own waves after
+// __syncthreads (same CU, same L1), so no grid-wide synchronisation is needed.  The frontier
+// is a list in LDS, deduplicated through the same byte flags (atomicOr) the full-grid kernel
+// uses, and the superstep body is cc_chunk itself, on the same label / change-word / flag
+// buffers with the same rotation — so the two kernels hand over at any superstep: when the
+// next frontier holds more than `cap` vertices the tail stops, its flags complete in
+// act[(r+1)%3], and the full-grid kernel takes superstep r+1.  info[0] = the last superstep
+// executed (r0-1 if none).
+constexpr int kTailThreads = 1024;
+
+template <bool BUF>
+__global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int cap, int64_t nv,
+                                                          const int64_t* __restrict__ adj_off,
+                                                          const uint64_t* __restrict__ vm,
+                                                          const int32_t* __restrict__ cnt,
+                                                          const int32_t* __restrict__ snbr,
+                                                          const uint64_t* __restrict__ smask,
+                                                          int32_t* lab0, int32_t* lab1, uint64_t* chg0,
+                                                          uint64_t* chg1, uint8_t* act0, uint8_t* act1,
+                                                          uint8_t* act2, int32_t* __restrict__ stepflag,
+                                                          int32_t* __restrict__ hostflag,
+                                                          int32_t* __restrict__ info,
+                                                          unsigned long long* __restrict__ work) {
+  __shared__ int32_t list[2][kTailListCap];
+  __shared__ int nlist[2];
+  __shared__ int nchanged;
+  __shared__ unsigned long long wsum[2];
+  auto ACT = [&](int k) { return k == 0 ? act0 : (k == 1 ? act1 : act2); };
+  const int lane = lane_id(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (stepflag[r0 - 1] == 0) {  // the batch has halted already
+    if (threadIdx.x == 0) info[0] = r0 - 1;
+    return;
+  }
+  if (threadIdx.x == 0) { nlist[0] = 0; nlist[1] = 0; }
+  __syncthreads();
+  {  // frontier of step r0 (flags act[r0%3]) -> list 0; clear act[(r0+2)%3] (frontier of r0-1)
+    const uint64_t* a = reinterpret_cast<const uint64_t*>(ACT(r0 % 3));
+    uint64_t* z = reinterpret_cast<uint64_t*>(ACT((r0 + 2) % 3));
+    const int64_t nwords = (nv + 7) >> 3;
+    for (int64_t i = threadIdx.x; i < nwords; i += blockDim.x) {
+      const uint64_t f = a[i];
+      z[i] = 0;
+      if (f) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) bits |= ((f >> (8 * k)) & 0xffu) ? (1u << k) : 0u;
+        int idx = atomicAdd(&nlist[0], __popc(bits));
+        while (bits) {
+          const int k = __builtin_ctz(bits);
+          bits &= bits - 1;
+          if (idx < kTailListCap) list[0][idx] = (int32_t)(i * 8 + k);
+          idx++;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  int p = 0, r = r0 - 1;  // r: last superstep executed
+  for (;;) {
+    const int ncur = nlist[p];
+    if (ncur > cap) break;  // too wide for one workgroup: the full-grid kernel takes step r+1
+    const int s = r + 1;
+    __syncthreads();  // everyone has read nlist[p] and left the previous clear loop
+    if (threadIdx.x == 0) { nlist[p ^ 1] = 0; nchanged = 0; wsum[0] = 0; wsum[1] = 0; }
+    __syncthreads();
+    uint8_t* a_cur = ACT(s % 3);
+    uint8_t* a_next = ACT((s + 1) % 3);
+    const int32_t* lab_cur = ((s - 1) & 1) ? lab1 : lab0;
+    int32_t* lab_next = (s & 1) ? lab1 : lab0;
+    const uint64_t* chg_prev = ((s - 1) & 1) ? chg1 : chg0;
+    uint64_t* chg_next = (s & 1) ? chg1 : chg0;
+    const TailList tl{list[p ^ 1], &nlist[p ^ 1]};
+    int32_t changed = 0;
+    unsigned long long pv = 0, ps = 0;
+    for (int c = wid * 4; c < ncur; c += nw * 4) {
+      const int k = c + (lane & 3) < ncur ? c + (lane & 3) : c;
+      const uint32_t bits = ncur - c >= 4 ? 0xfu : ((1u << (ncur - c)) - 1);
+      cc_chunk<4, BUF, true>((int64_t)list[p][k], bits, adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
+                             chg_prev, chg_next, a_next, tl, lane, changed, pv, ps);
+    }
+    if (lane == 0) {
+      if (changed) atomicAdd(&nchanged, changed);
+      if (pv) atomicAdd(&wsum[0], pv);
+      if (ps) atomicAdd(&wsum[1], ps);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < ncur; k += blockDim.x) a_cur[list[p][k]] = 0;  // step s consumed them
+    const int nch = nchanged;
+    if (threadIdx.x == 0) {
+      if (nch) {
+        stepflag[s] = 1;
+        if (hostflag) hostflag[s] = 1;
+      }
+      add_work(work, s, wsum[0], wsum[1], (unsigned long long)nch);
+    }
+    r = s;
+    p ^= 1;
+    if (nch == 0 || s >= rmax) break;
+  }
+  if (threadIdx.x == 0) info[0] = r;
+}
+
 // ---------------------------------------------------------------- K5: CC reductions
 // label -> count histogram (ConnectedComponents.returnResults :37-42, groupBy over labels).
-// A wave stages the label rows of 64 consecutive vertices in LDS, then per view puts the 64
-// vertices on the lanes and adds each distinct label once per wave (popcount of the lanes
-// that carry it): the giant component costs one atomic per 64 vertices, not one per vertex.
+// A block stages the label rows of 64 consecutive vertices in LDS (16 rows per wave), then
+// its four waves split the views (wave w takes views j = w mod 4): per view the 64 vertices
+// sit on the lanes and each distinct label is added once per chunk (popcount of the lanes
+// that carry it), so the giant component costs one atomic per 64 vertices, not one per
+// vertex.  The per-view loop is serial, latency-bound work: one chunk per block keeps ~24
+// waves per CU on it (one chunk per wave kept ~6).
 // Members with no kept slot in a view are isolated there: islands (count 1) that need no
-// histogram entry; they are added to total / sum / biggest directly.
+// histogram entry.  Their counts go to iso[shard][view] (64 shards: a few dozen blocks per
+// address, not thousands); the summary kernel folds them into total / sum / biggest.
 template <bool BUF>
 __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int64_t hstride, int nviews,
                                                  const uint64_t* __restrict__ vm,
                                                  const uint64_t* __restrict__ vadj,
                                                  const int32_t* __restrict__ lab,
                                                  int32_t* __restrict__ hist,
-                                                 unsigned long long* __restrict__ stats) {
-  __shared__ int32_t tile[4][64][65];
+                                                 unsigned int* __restrict__ iso_g) {
+  __shared__ int32_t tile[64][65];
   __shared__ unsigned int iso[64];
   if (threadIdx.x < 64) iso[threadIdx.x] = 0;
-  __syncthreads();
   const int lane = lane_id(), wib = threadIdx.x >> 6;
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t c = wave; c * 64 < nv; c += nwaves) {
+  const uint64_t vmask = (nviews >= 64 ? ~0ull : ((1ull << nviews) - 1)) & (0x1111111111111111ull << wib);
+  for (int64_t c = blockIdx.x; c * 64 < nv; c += gridDim.x) {
     const int64_t v0 = c * 64;
     const int nvc = (int)(nv - v0 < 64 ? nv - v0 : 64);
-    for (int i0 = 0; i0 < 64; i0 += 16) {  // 16 independent row loads in flight, then LDS
-      int32_t r[16];
+    {
+      int32_t r[16];  // 16 independent row loads in flight, then LDS
 #pragma unroll
       for (int k = 0; k < 16; k++) {
+        const int i = wib * 16 + k;
         if (BUF) {
-          const uint64_t mk = i0 + k < nvc ? vm[v0 + i0 + k] : 0;  // scalar: wave-uniform vertex
-          r[k] = row_load(lab + (v0 + i0 + k) * 64, (mk >> lane) & 1, lane);
+          const uint64_t mk = i < nvc ? vm[v0 + i] : 0;  // scalar: wave-uniform vertex
+          r[k] = row_load(lab + (v0 + i) * 64, (mk >> lane) & 1, lane);
         } else {
-          r[k] = i0 + k < nvc ? lab[(v0 + i0 + k) * 64 + lane] : 0;
+          r[k] = i < nvc ? lab[(v0 + i) * 64 + lane] : 0;
         }
       }
 #pragma unroll
-      for (int k = 0; k < 16; k++) tile[wib][i0 + k][lane] = r[k];
+      for (int k = 0; k < 16; k++) tile[wib * 16 + k][lane] = r[k];
     }
     const uint64_t mvl = lane < nvc ? vm[v0 + lane] : 0;
     const uint64_t adl = lane < nvc ? vadj[v0 + lane] : 0;
     uint64_t any = mvl;  // views with at least one member in this chunk (OR over lanes)
     for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
-    any = readlane64(any, 0) & (nviews >= 64 ? ~0ull : ((1ull << nviews) - 1));
-    __builtin_amdgcn_wave_barrier();
+    any = readlane64(any, 0) & vmask;
+    __syncthreads();
     while (any) {
       const int j = __builtin_ctzll(any);
       any &= any - 1;
       const bool in_view = (mvl >> j) & 1;
       const bool member = in_view && ((adl >> j) & 1);
       const uint64_t isolated = __ballot(in_view && !member);
-      if (lane == 0 && isolated) atomicAdd(&iso[j], (unsigned)__popcll(isolated));
-      const int32_t l = tile[wib][lane][j];
+      if (lane == 0 && isolated) iso[j] += (unsigned)__popcll(isolated);  // view j: this wave only
+      const int32_t l = tile[lane][j];
       uint64_t todo = __ballot(member);
       while (todo) {
         const int leader = __builtin_ctzll(todo);
@@ -608,14 +808,24 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int64_t hstride, in
         todo &= ~same;
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads();  // the tile is rewritten by the next chunk
   }
-  __syncthreads();
-  if (threadIdx.x < 64 && iso[threadIdx.x]) {
-    const unsigned long long k = iso[threadIdx.x];
-    atomicMax(&stats[0 * 64 + threadIdx.x], 1ull);
-    atomicAdd(&stats[1 * 64 + threadIdx.x], k);
-    atomicAdd(&stats[4 * 64 + threadIdx.x], k);
+  if (threadIdx.x < 64 && iso[threadIdx.x])
+    atomicAdd(&iso_g[(blockIdx.x & 63) * 64 + threadIdx.x], iso[threadIdx.x]);
+}
+
+// Fold the isolated-member shards of view j into the summary (islands: count 1 each) and
+// clear them for the next batch.  Called by block (0, j) of a summary kernel.
+__device__ __forceinline__ void fold_iso(unsigned int* __restrict__ iso_g, int j,
+                                         unsigned long long* __restrict__ stats) {
+  if (threadIdx.x >= 64) return;
+  unsigned long long k = iso_g[threadIdx.x * 64 + j];
+  if (k) iso_g[threadIdx.x * 64 + j] = 0;
+  for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o);
+  if (threadIdx.x == 0 && k) {
+    atomicMax(&stats[0 * 64 + j], 1ull);
+    atomicAdd(&stats[1 * 64 + j], k);
+    atomicAdd(&stats[4 * 64 + j], k);
   }
 }
 
@@ -624,9 +834,11 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int64_t hstride, in
 // blockIdx.x strides over ranks; one atomic per (block, field).  stats[f*64 + view]:
 // 0 biggest 1 total 2 total>1 3 total>2 4 sum 5 sum(count>1)
 __global__ __launch_bounds__(256) void k_cc_summary(int64_t nv, int32_t* __restrict__ hist,
-                                                    unsigned long long* __restrict__ stats) {
+                                                    unsigned long long* __restrict__ stats,
+                                                    unsigned int* __restrict__ iso) {
   __shared__ unsigned long long red[6][4];
   const int j = blockIdx.y;
+  if (blockIdx.x == 0) fold_iso(iso, j, stats);
   int32_t* h = hist + (int64_t)j * nv;
   unsigned long long big = 0, tot = 0, nis = 0, gt2 = 0, sum = 0, snis = 0;
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nv;
@@ -957,9 +1169,11 @@ __global__ __launch_bounds__(256) void k_add_i32(int32_t* __restrict__ dst, cons
 // histogram (stride ng per view): blockIdx.y = view.
 __global__ __launch_bounds__(256) void k_cc_summary_rs(const int32_t* __restrict__ chunk, int64_t x0,
                                                        int64_t len, int64_t ng,
-                                                       unsigned long long* __restrict__ stats) {
+                                                       unsigned long long* __restrict__ stats,
+                                                       unsigned int* __restrict__ iso) {
   __shared__ unsigned long long red[6][4];
   const int j = blockIdx.y;
+  if (blockIdx.x == 0) fold_iso(iso, j, stats);
   const int64_t lo = x0 > (int64_t)j * ng ? x0 : (int64_t)j * ng;
   const int64_t hi = (x0 + len) < (int64_t)(j + 1) * ng ? (x0 + len) : (int64_t)(j + 1) * ng;
   unsigned long long big = 0, tot = 0, nis = 0, gt2 = 0, sum = 0, snis = 0;
@@ -1011,13 +1225,21 @@ static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
   return (unsigned)(g > cap ? cap : g);
 }
 
-void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm,
-                        const BatchClear& clr) {
-  k_vertex_mask<<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm, clr);
+void launch_batch_clear(hipStream_t s, const BatchClear& clr) {
+  k_batch_clear<<<16, 256, 0, s>>>(clr);
 }
-void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em) {
-  k_edge_mask<<<grid_for(g.ne, 256), 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff,
-                                                   g.dtime, bp, em);
+void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm,
+                        int64_t vstride, bool planar, const BatchClear& clr) {
+  if (planar) k_vertex_mask<true><<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm, vstride, clr);
+  else k_vertex_mask<false><<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm, vstride, clr);
+}
+void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar) {
+  if (planar)
+    k_edge_mask<true><<<grid_for(g.ne, 256), 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime,
+                                                           bp, em, g.ne);
+  else
+    k_edge_mask<false><<<grid_for(g.ne, 256), 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime,
+                                                            bp, em, g.ne);
 }
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
@@ -1046,16 +1268,28 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   else k_cc_step2<4, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
 #undef RGPU_STEP_ARGS
 }
+void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
+                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,
+                    int32_t* lab1, uint64_t* chg0, uint64_t* chg1, uint8_t* act0, uint8_t* act1,
+                    uint8_t* act2, int32_t* stepflag, int32_t* hostflag, int32_t* info,
+                    unsigned long long* work) {
+  cap = cap < kTailListCap ? cap : kTailListCap;
+#define RGPU_TAIL_ARGS r0, rmax, cap, g.nv, g.adj_off, vm, cnt, snbr, smask, lab0, lab1, chg0, chg1, act0, act1, \
+    act2, stepflag, hostflag, info, work
+  if (g_rowbuf) k_cc_tail<true><<<1, kTailThreads, 0, s>>>(RGPU_TAIL_ARGS);
+  else k_cc_tail<false><<<1, kTailThreads, 0, s>>>(RGPU_TAIL_ARGS);
+#undef RGPU_TAIL_ARGS
+}
 void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, const uint64_t* vm,
-                    const uint64_t* vadj, const int32_t* lab, int32_t* hist,
-                    unsigned long long* stats) {
-  if (g_rowbuf) k_cc_hist<true><<<grid_for(nv, 4 * 64, 512), 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, stats);
-  else k_cc_hist<false><<<grid_for(nv, 4 * 64, 512), 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, stats);
+                    const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso) {
+  const unsigned grid = grid_for(nv, 64, 8192);
+  if (g_rowbuf) k_cc_hist<true><<<grid, 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso);
+  else k_cc_hist<false><<<grid, 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso);
 }
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
-                       unsigned long long* stats) {
+                       unsigned long long* stats, unsigned int* iso) {
   dim3 grid(grid_for(g.nv, 256, 32), (unsigned)nviews);
-  k_cc_summary<<<grid, 256, 0, s>>>(g.nv, hist, stats);
+  k_cc_summary<<<grid, 256, 0, s>>>(g.nv, hist, stats, iso);
 }
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                    int32_t* outdeg, int32_t* indeg, unsigned long long* stats) {
@@ -1099,9 +1333,9 @@ void launch_add_i32(hipStream_t s, int32_t* dst, const int32_t* src, int64_t n) 
   if (n > 0) k_add_i32<<<grid_for(n, 256, 4096), 256, 0, s>>>(dst, src, n);
 }
 void launch_cc_summary_rs(hipStream_t s, int nviews, const int32_t* chunk, int64_t x0, int64_t len,
-                          int64_t ng, unsigned long long* stats) {
+                          int64_t ng, unsigned long long* stats, unsigned int* iso) {
   dim3 grid(grid_for(ng, 256, 32), (unsigned)nviews);
-  k_cc_summary_rs<<<grid, 256, 0, s>>>(chunk, x0, len, ng, stats);
+  k_cc_summary_rs<<<grid, 256, 0, s>>>(chunk, x0, len, ng, stats, iso);
 }
 
 }  // namespace rgpu

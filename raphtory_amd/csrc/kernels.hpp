@@ -43,9 +43,13 @@ struct BatchClear {
   int64_t n_act_words = 0;  // uint64 words per act buffer
 };
 
+// K1.  planar = false: one mask word per entity, view bit w*KS + k.  planar = true (W <=
+// kMaxPlanes): one word per window w at out[w*stride + i], bit k = hop of the block.
+constexpr int kMaxPlanes = 8;
+void launch_batch_clear(hipStream_t s, const BatchClear& clr);
 void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm,
-                        const BatchClear& clr);
-void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em);
+                        int64_t vstride, bool planar, const BatchClear& clr);
+void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar);
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
@@ -59,11 +63,18 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, int variant);
+// Many late supersteps in one single-workgroup launch while the frontier stays below `cap`
+// vertices; info[0] <- last superstep executed (host-mapped).
+void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
+                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,
+                    int32_t* lab1, uint64_t* chg0, uint64_t* chg1, uint8_t* act0, uint8_t* act1,
+                    uint8_t* act2, int32_t* stepflag, int32_t* hostflag, int32_t* info,
+                    unsigned long long* work);
+constexpr int kIsoWords = 64 * 64;  // isolated-member counts [64 shards][64 views]
 void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, const uint64_t* vm,
-                    const uint64_t* vadj, const int32_t* lab, int32_t* hist,
-                    unsigned long long* stats);
+                    const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso);
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
-                       unsigned long long* stats);
+                       unsigned long long* stats, unsigned int* iso);
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                    int32_t* outdeg, int32_t* indeg, unsigned long long* stats);
 void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
@@ -85,6 +96,6 @@ void launch_xgather_f64(hipStream_t s, int64_t n, const int32_t* xv, const doubl
 void launch_xscatter_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* buf, double* rows);
 void launch_add_i32(hipStream_t s, int32_t* dst, const int32_t* src, int64_t n);
 void launch_cc_summary_rs(hipStream_t s, int nviews, const int32_t* chunk, int64_t x0, int64_t len,
-                          int64_t ng, unsigned long long* stats);
+                          int64_t ng, unsigned long long* stats, unsigned int* iso);
 
 }  // namespace rgpu

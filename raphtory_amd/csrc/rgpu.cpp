@@ -42,7 +42,7 @@ struct HipFail {
   } while (0)
 
 enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUMMARY = 4,
-                KID_PR = 5, KID_DEGREE = 6, KID_N = 8 };
+                KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_N = 8 };
 
 constexpr int kMaxSteps = 128;
 constexpr int kStatWords = 7 * kViews;  // 6 per-view fields + counters row
@@ -53,7 +53,8 @@ constexpr int kMaxSlots = 4;  // batches in flight (one HIP stream each; GPU_MAX
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
-  uint64_t *vm = nullptr, *em = nullptr;
+  uint64_t *vm = nullptr, *em = nullptr;          // masks of the batch in flight
+  uint64_t *vm_own = nullptr, *em_own = nullptr;  // this slot's own (hop-major batches)
   int32_t *cnt = nullptr, *snbr = nullptr;
   uint64_t* smask = nullptr;
   int32_t* lab[2] = {nullptr, nullptr};
@@ -70,9 +71,14 @@ struct Slot {
   uint64_t* psmask = nullptr;
   int32_t* h_stepcnt = nullptr;   // host-mapped superstep flags, written by the kernels
   int32_t* d_hostflag = nullptr;  // device address of h_stepcnt
+  int32_t* h_tail = nullptr;      // host-mapped: [0] last superstep a k_cc_tail launch executed
+  int32_t* d_tail = nullptr;
+  unsigned int* iso = nullptr;    // isolated-member counts [64 shards][64 views] (k_cc_hist)
   unsigned long long* h_stats = nullptr;
   // state of the batch in flight
   int batch = -1, phase = 0, r_launched = 0, r_final = 0, kb = 0;
+  bool tail_pending = false;       // a k_cc_tail launch is in the last enqueued chunk
+  uint8_t by_tail[kMaxSteps] = {}; // superstep r ran inside k_cc_tail (bytes accounting)
   uint64_t evseq = 0;  // order in which slot events were recorded (wait on the oldest)
 };
 
@@ -97,6 +103,17 @@ struct Part {
   int32_t* h_scnt = nullptr;                  // pinned [P + 1]
   bool cc_ready = false, pr_ready = false;
   double bytes_sent = 0;
+};
+
+// Window-major batches (one window per batch, 64 hops): K1 runs once per 64-hop block for
+// every window, into a mask set shared by the block's W batches (on whichever slots run them).
+constexpr int kMaskSets = 2;
+struct MaskSet {
+  uint64_t *vm = nullptr, *em = nullptr;  // plane w: vm[w*(nv+kPad) + v], em[w*ne + e]
+  int planes = 0;
+  hipEvent_t k1 = nullptr;                // K1 of the current block done
+  hipEvent_t done[kMaxPlanes] = {};       // batch (block, w) has stopped reading the set
+  int pending = 0;                        // batches of the current block not yet finished
 };
 
 struct Timed {
@@ -124,12 +141,18 @@ struct rgpu_ctx {
   int nslots = 2;
   bool hostflags = true;                // superstep flags via host-mapped memory (else copies)
   int step_variant = 0;                 // RGPU_STEP_VARIANT: 0 per-vertex chain, 1 chunk-pipelined
+  bool tail_on = true;                  // RGPU_TAIL: late supersteps in one-workgroup k_cc_tail launches
+  int tail_cap = 256;                   // RGPU_TAIL_CAP: widest frontier the tail kernel takes
+  int64_t tail_maxv = 4 << 20;          // RGPU_TAIL_MAXV: no tail kernel above this many vertices
   std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
   struct StepRec { int batch, step; unsigned long long pv, ps; int changed; };
   std::vector<StepRec> steprec;
   bool slot_cc = false, slot_deg = false, slot_pr = false;
-  // last run
-  int algo = -1, K = 0, W = 0;
+  bool wmajor = true;                   // RGPU_WMAJOR: window-major batches when 2 <= W <= kMaxPlanes
+  MaskSet mset[kMaskSets];
+  int grp_last[kMaxPlanes] = {};        // supersteps of the last batch of each window group
+  // last run: views (hop, win) -> batch (hop/K)*G + win/gsize, lane (win%gsize)*K + hop%K
+  int algo = -1, K = 0, W = 0, G = 1, gsize = 1;
   size_t n_hops = 0;
   std::vector<rgpu_cc_summary_t> cc;
   std::vector<int64_t> deg;  // [view][3]
@@ -173,6 +196,7 @@ void free_graph(rgpu_ctx* c) {
   }
   for (Slot& s : c->slot) {
     if (s.h_stepcnt) (void)hipHostFree(s.h_stepcnt);
+    if (s.h_tail) (void)hipHostFree(s.h_tail);
     if (s.h_stats) (void)hipHostFree(s.h_stats);
     if (s.h_work) (void)hipHostFree(s.h_work);
     if (s.ev) (void)hipEventDestroy(s.ev);
@@ -180,6 +204,12 @@ void free_graph(rgpu_ctx* c) {
     s = Slot();
   }
   c->slot_cc = c->slot_deg = c->slot_pr = false;
+  for (MaskSet& m : c->mset) {
+    if (m.k1) (void)hipEventDestroy(m.k1);
+    for (hipEvent_t e : m.done)
+      if (e) (void)hipEventDestroy(e);
+    m = MaskSet();
+  }
   c->g = DevGraph();
 }
 
@@ -210,6 +240,33 @@ void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn, int step = 0
   c->st.kernel_bytes[kid] += bytes;
 }
 
+void ensure_masks(rgpu_ctx* c, int G) {
+  auto& L = c->graph_allocs;
+  const int64_t nv = c->g.nv, ne = c->g.ne;
+  if (G == 1) {
+    for (int i = 0; i < c->nslots; i++) {
+      Slot& s = c->slot[i];
+      if (!s.vm_own) {
+        s.vm_own = dalloc<uint64_t>(L, nv + kPad);
+        s.em_own = dalloc<uint64_t>(L, ne);
+      }
+    }
+    return;
+  }
+  for (MaskSet& m : c->mset) {
+    if (m.planes < G) {  // (a smaller earlier allocation stays in graph_allocs until re-seal)
+      m.vm = dalloc<uint64_t>(L, (size_t)G * (nv + kPad));
+      m.em = dalloc<uint64_t>(L, (size_t)G * ne);
+      m.planes = G;
+    }
+    if (!m.k1) {
+      HIPCHK(hipEventCreateWithFlags(&m.k1, hipEventDisableTiming));
+      for (hipEvent_t& e : m.done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    m.pending = 0;
+  }
+}
+
 void ensure_slots(rgpu_ctx* c, int algo) {
   auto& L = c->graph_allocs;
   const int64_t nv = c->g.nv, ne = c->g.ne, nin = c->g.n_in;
@@ -221,10 +278,10 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
       HIPCHK(hipHostMalloc((void**)&s.h_stepcnt, sizeof(int32_t) * kMaxSteps, hipHostMallocMapped));
       HIPCHK(hipHostGetDevicePointer((void**)&s.d_hostflag, s.h_stepcnt, 0));
+      HIPCHK(hipHostMalloc((void**)&s.h_tail, sizeof(int32_t) * 4, hipHostMallocMapped));
+      HIPCHK(hipHostGetDevicePointer((void**)&s.d_tail, s.h_tail, 0));
       HIPCHK(hipHostMalloc((void**)&s.h_stats, sizeof(unsigned long long) * kStatWords));
       HIPCHK(hipHostMalloc((void**)&s.h_work, sizeof(unsigned long long) * kWorkWords));
-      s.vm = dalloc<uint64_t>(L, nv + kPad);
-      s.em = dalloc<uint64_t>(L, ne);
       s.stepcnt = dalloc<int32_t>(L, kMaxSteps);
       s.stats = dalloc<unsigned long long>(L, kStatWords);
     }
@@ -243,6 +300,8 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       for (int b = 0; b < 3; b++) s.act[b] = dalloc<uint8_t>(L, (size_t)((nv + 7) / 8 + 1) * 8);
       s.vadj = dalloc<uint64_t>(L, nv);
       s.work = dalloc<unsigned long long>(L, kWorkWords);
+      s.iso = dalloc<unsigned int>(L, kIsoWords);  // zero between batches: the summary kernel clears it
+      HIPCHK(hipMemset(s.iso, 0, sizeof(unsigned int) * kIsoWords));
     }
     if ((algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) && !c->slot_deg) {
       s.outdeg = dalloc<int32_t>(L, rows);
@@ -288,7 +347,9 @@ void ensure_slots(rgpu_ctx* c, int algo) {
 
 struct RunCfg {
   int algo, max_steps, pr_iters, flags;
-  int K, W;
+  int K, W;         // hops per batch (64 / gsize), windows of the run
+  int G, gsize;     // window groups (batches per hop block), windows per group
+  size_t nblk, nb;  // hop blocks, batches
   const int64_t* hops;
   size_t n_hops;
   int64_t thr_v[kViews], thr_e[kViews];
@@ -313,6 +374,18 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     }, r);
   }
   s.r_launched = last;
+  if (c->tail_on && g.nv <= c->tail_maxv && s.r_launched < rc.max_steps) {
+    // the rest of the supersteps in one workgroup while the frontier stays narrow; it stops
+    // (and the host continues with full-grid launches) at the first wide frontier
+    const int r0 = s.r_launched + 1;
+    s.h_tail[0] = -1;
+    timed_launch(c, si, KID_TAIL, 0.0, [&] {
+      launch_cc_tail(s.stream, r0, rc.max_steps, c->tail_cap, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[0],
+                     s.lab[1], s.chg[0], s.chg[1], s.act[0], s.act[1], s.act[2], s.stepcnt,
+                     c->hostflags ? s.d_hostflag : nullptr, s.d_tail, c->profile ? s.work : nullptr);
+    }, r0);
+    s.tail_pending = true;
+  }
   if (!c->hostflags)
     HIPCHK(hipMemcpyAsync(s.h_stepcnt, s.stepcnt, sizeof(int32_t) * kMaxSteps, hipMemcpyDeviceToHost,
                           s.stream));
@@ -333,9 +406,10 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
     // batch's working set inside the Infinity Cache with several batches in flight)
     int32_t* hist = s.lab[(s.r_final + 1) & 1];
     HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)g.nv * kViews, s.stream));
-    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g.nv, g.nv, rc.K * rc.W, s.vm, s.vadj, lab, hist, s.stats); });
-    timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * rc.K * rc.W,
-                 [&] { launch_cc_summary(s.stream, g, rc.K * rc.W, hist, s.stats); });
+    const int nviews = rc.K * rc.gsize;
+    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g.nv, g.nv, nviews, s.vm, s.vadj, lab, hist, s.iso); });
+    timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * nviews,
+                 [&] { launch_cc_summary(s.stream, g, nviews, hist, s.stats, s.iso); });
   }
   HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatWords,
                         hipMemcpyDeviceToHost, s.stream));
@@ -358,17 +432,33 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
       HIPCHK(hipMemcpyAsync(R.pr.data(), s.pr, sizeof(double) * rows, hipMemcpyDeviceToHost, s.stream));
     }
   }
+  if (rc.G > 1) {  // the batch no longer reads its mask set
+    MaskSet& M = c->mset[(s.batch / rc.G) % kMaskSets];
+    HIPCHK(hipEventRecord(M.done[s.batch % rc.G], s.stream));
+    M.pending--;
+  }
   HIPCHK(hipEventRecord(s.ev, s.stream));
   s.evseq = ++c->evcounter;
   s.phase = 2;
 }
 
+// Batch b = hop block b / G (hops [hb*K, hb*K + K)) x window group b % G.  Hop-major runs
+// (G = 1): the batch is the block, all windows in one label row, K1 per batch into the slot's
+// own masks.  Window-major runs (G = W): one window per batch; K1 runs once per block, for
+// every window, on the stream of the block's first batch, into a shared mask set.
+bool can_start(const rgpu_ctx* c, size_t b, const RunCfg& rc) {
+  if (rc.G == 1 || b % rc.G != 0) return true;
+  return c->mset[(b / rc.G) % kMaskSets].pending == 0;  // set still read by an older block
+}
+
 void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   Slot& s = c->slot[si];
   const DevGraph& g = c->g;
+  const size_t hb = (size_t)b / rc.G;
+  const int grp = b % rc.G;
   BatchParams bp;
   std::memset(&bp, 0, sizeof(bp));
-  const size_t h0 = (size_t)b * rc.K;
+  const size_t h0 = hb * rc.K;
   bp.K = (int)std::min<size_t>(rc.K, rc.n_hops - h0);
   bp.W = rc.W;
   bp.KS = rc.K;
@@ -382,6 +472,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   s.kb = bp.K;
   s.r_launched = 0;
   s.r_final = 0;
+  s.tail_pending = false;
+  std::memset(s.by_tail, 0, sizeof(s.by_tail));
   std::memset(s.h_stepcnt, 0, sizeof(int32_t) * kMaxSteps);  // slot idle: no kernel writes it
   BatchClear clr;
   clr.stats = s.stats;
@@ -395,10 +487,31 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   if (s.work && c->profile)
     HIPCHK(hipMemsetAsync(s.work, 0, sizeof(unsigned long long) * kWorkWords, s.stream));
   const double bm = bytes_mask(g);
-  timed_launch(c, si, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.vkey.size() + 8.0 * g.nv,
-               [&] { launch_vertex_mask(s.stream, g, bp, s.vm, clr); });
-  timed_launch(c, si, KID_MASK, bm - (16.0 * g.nv + 8.0) + 8.0 * c->pk.ekey.size(),
-               [&] { launch_edge_mask(s.stream, g, bp, s.em); });
+  const double bv = 8.0 * (g.nv + 1) + 8.0 * c->pk.vkey.size(), be = bm - (16.0 * g.nv + 8.0) - 8.0 * g.ne + 8.0 * c->pk.ekey.size();
+  if (rc.G == 1) {
+    s.vm = s.vm_own;
+    s.em = s.em_own;
+    timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv, [&] { launch_vertex_mask(s.stream, g, bp, s.vm, 0, false, clr); });
+    timed_launch(c, si, KID_MASK, be + 8.0 * g.ne, [&] { launch_edge_mask(s.stream, g, bp, s.em, false); });
+  } else {
+    MaskSet& M = c->mset[hb % kMaskSets];
+    if (grp == 0) {
+      // the set's previous block is finished-enqueued (can_start); wait for it on the device
+      for (int w = 0; w < rc.G; w++) HIPCHK(hipStreamWaitEvent(s.stream, M.done[w], 0));
+      const BatchClear none;
+      timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv * rc.W,
+                   [&] { launch_vertex_mask(s.stream, g, bp, M.vm, g.nv + kPad, true, none); });
+      timed_launch(c, si, KID_MASK, be + 8.0 * g.ne * rc.W, [&] { launch_edge_mask(s.stream, g, bp, M.em, true); });
+      HIPCHK(hipEventRecord(M.k1, s.stream));
+      M.pending = rc.G;
+    } else {
+      HIPCHK(hipStreamWaitEvent(s.stream, M.k1, 0));
+    }
+    s.vm = M.vm + (size_t)grp * (g.nv + kPad);
+    s.em = M.em + (size_t)grp * g.ne;
+    launch_batch_clear(s.stream, clr);
+    HIPCHK(hipGetLastError());
+  }
   if (rc.algo == RGPU_ALGO_CC) {
     // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
@@ -413,7 +526,9 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       s.r_final = 0;
       finish_batch(c, si, rc);
     } else {
-      launch_chunk(c, si, rc, rc.chunk0);
+      // first chunk: up to the step the group's previous batch halted at (then the tail kernel)
+      const int last = c->grp_last[grp];
+      launch_chunk(c, si, rc, last > 0 ? std::max(1, std::min(rc.chunk0, last)) : rc.chunk0);
     }
   } else {
     timed_launch(c, si, KID_DEGREE, g.nv * (8.0 + 32.0 + 512.0) + (double)(g.ne + g.n_in) * 12.0, [&] {
@@ -438,10 +553,12 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
 void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
   Slot& s = c->slot[si];
   const unsigned long long* h = s.h_stats;
+  const size_t hb = (size_t)s.batch / rc.G;
+  const int grp = s.batch % rc.G;
   for (int k = 0; k < s.kb; k++)
-    for (int w = 0; w < rc.W; w++) {
-      const int j = w * rc.K + k;  // window-major view bit
-      const size_t view = ((size_t)s.batch * rc.K + k) * rc.W + w;
+    for (int wl = 0; wl < rc.gsize; wl++) {
+      const int j = wl * rc.K + k;  // view bit: window-major within the batch
+      const size_t view = (hb * rc.K + k) * rc.W + (size_t)grp * rc.gsize + wl;
       if (rc.algo == RGPU_ALGO_CC) {
         rgpu_cc_summary_t& o = c->cc[view];
         o.biggest = (int64_t)h[0 * kViews + j];
@@ -472,20 +589,23 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
       // vertex); per visited vertex vm, cnt, adj_off, own change word, label row in and out,
       // change word out (548 B); per slot of a visited vertex nbr + mask + neighbour's change
       // word (20 B).  Label gathers and flag stores are not counted.
+      // (a tail-kernel superstep reads no bitmap: its frontier is a list in LDS)
       for (int r = 2; r <= s.r_final; r++)
-        c->st.kernel_bytes[KID_STEP] += 2.0 * c->g.nv + 548.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1);
+        c->st.kernel_bytes[s.by_tail[r] ? KID_TAIL : KID_STEP] +=
+            (s.by_tail[r] ? 0.0 : 2.0 * c->g.nv) + 548.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1);
       if (!c->trace_path.empty())
         for (int r = 1; r <= s.r_final; r++)
           c->steprec.push_back({s.batch, r, wsum(r, 0), wsum(r, 1), (int)wsum(r, 2)});
     }
     c->st.supersteps += s.r_final;
+    c->grp_last[grp] = s.r_final;
   }
   s.phase = 0;
   s.batch = -1;
 }
 
 int run_impl(rgpu_ctx* c, RunCfg& rc) {
-  const size_t nb = (rc.n_hops + rc.K - 1) / rc.K;
+  const size_t nb = rc.nb;
   c->st.views += (int64_t)(rc.n_hops * rc.W);
   c->st.batches += (int64_t)nb;
   size_t next = 0;
@@ -495,7 +615,7 @@ int run_impl(rgpu_ctx* c, RunCfg& rc) {
     for (int si = 0; si < nslots; si++) {
       Slot& s = c->slot[si];
       if (s.phase == 0) {
-        if (next < nb) {
+        if (next < nb && can_start(c, next, rc)) {
           start_batch(c, si, (int)next++, rc);
           progressed = true;
           busy = true;
@@ -508,6 +628,14 @@ int run_impl(rgpu_ctx* c, RunCfg& rc) {
       HIPCHK(q);
       progressed = true;
       if (s.phase == 1) {
+        if (s.tail_pending) {
+          const int rd = s.h_tail[0];
+          if (rd < s.r_launched || rd > rc.max_steps)
+            throw HipFail{"k_cc_tail reported superstep " + std::to_string(rd)};
+          for (int r = s.r_launched + 1; r <= rd; r++) s.by_tail[r] = 1;
+          s.r_launched = rd;
+          s.tail_pending = false;
+        }
         int r0 = 0;
         for (int r = 1; r <= s.r_launched; r++)
           if (s.h_stepcnt[r] == 0) { r0 = r; break; }
@@ -516,7 +644,7 @@ int run_impl(rgpu_ctx* c, RunCfg& rc) {
         else launch_chunk(c, si, rc, rc.chunk);
       } else {
         harvest(c, si, rc);
-        if (next < nb) start_batch(c, si, (int)next++, rc);
+        if (next < nb && can_start(c, next, rc)) start_batch(c, si, (int)next++, rc);
       }
     }
     if (!busy) break;
@@ -620,19 +748,19 @@ void finish_partitioned_cc(rgpu_ctx* c, const RunCfg& rc) {
   // fields all-reduced (max for biggest)
   HIPCHK(hipMemsetAsync(X.hist, 0, sizeof(int32_t) * X.hist_total, s.stream));
   timed_launch(c, 0, KID_HIST, 12.0 * c->pk.n_own, [&] {
-    launch_cc_hist(s.stream, c->pk.n_own, X.ng, nviews, s.vm, s.vadj, lab, X.hist, s.stats);
+    launch_cc_hist(s.stream, c->pk.n_own, X.ng, nviews, s.vm, s.vadj, lab, X.hist, s.iso);
   });
   const int64_t cnt = X.hist_total / P;
   X.xchg->reduce_scatter_i32(X.hist, X.chunk, (size_t)cnt, s.stream);
   timed_launch(c, 0, KID_SUMMARY, 4.0 * cnt, [&] {
-    launch_cc_summary_rs(s.stream, nviews, X.chunk, cnt * c->part, cnt, X.ng, s.stats);
+    launch_cc_summary_rs(s.stream, nviews, X.chunk, cnt * c->part, cnt, X.ng, s.stats, s.iso);
   });
   X.xchg->allreduce_u64(s.stats, kViews, true, s.stream);
   X.xchg->allreduce_u64(s.stats + kViews, 5 * kViews, false, s.stream);
 }
 
 int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
-  const size_t nb = (rc.n_hops + rc.K - 1) / rc.K;
+  const size_t nb = rc.nb;  // hop-major (G = 1)
   c->st.views += (int64_t)(rc.n_hops * rc.W);
   c->st.batches += (int64_t)nb;
   Slot& s = c->slot[0];
@@ -662,10 +790,12 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
       clr.n_act_words = (c->g.nv + 7) / 8 + 1;
     }
     const DevGraph& g = c->g;
+    s.vm = s.vm_own;
+    s.em = s.em_own;
     timed_launch(c, 0, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.vkey.size() + 8.0 * g.nv,
-                 [&] { launch_vertex_mask(s.stream, g, bp, s.vm, clr); });
+                 [&] { launch_vertex_mask(s.stream, g, bp, s.vm, 0, false, clr); });
     timed_launch(c, 0, KID_MASK, bytes_mask(g) - (16.0 * g.nv + 8.0) + 8.0 * c->pk.ekey.size(),
-                 [&] { launch_edge_mask(s.stream, g, bp, s.em); });
+                 [&] { launch_edge_mask(s.stream, g, bp, s.em, false); });
     if (rc.algo == RGPU_ALGO_CC) {
       timed_launch(c, 0, KID_SLOTS, g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0, [&] {
         launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
@@ -771,6 +901,10 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   if (env_int("RGPU_TAIL_STEP", 0) > 0) g_tail_step = env_int("RGPU_TAIL_STEP", 0);
   if (env_int("RGPU_TAIL_GRID", 0) > 0) g_tail_grid = env_int("RGPU_TAIL_GRID", 0);
   c->hostflags = env_int("RGPU_HOSTFLAG", 1) != 0;
+  c->tail_on = env_int("RGPU_TAIL", 1) != 0;
+  c->wmajor = env_int("RGPU_WMAJOR", 1) != 0;
+  c->tail_cap = std::max(1, env_int("RGPU_TAIL_CAP", 256));
+  c->tail_maxv = std::max(0, env_int("RGPU_TAIL_MAXV", 4 << 20));
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
   *out = c;
@@ -906,7 +1040,14 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   rc.pr_iters = pr_iters;
   rc.flags = flags;
   rc.W = n_w ? (int)n_w : 1;
-  rc.K = kViews / rc.W;
+  // window-major batches when they pay: each window's views in their own batches (64 hops),
+  // so the cheap short windows no longer ride along the long windows' supersteps
+  const bool wm = c->wmajor && !c->partitioned && rc.W >= 2 && rc.W <= kMaxPlanes;
+  rc.G = wm ? rc.W : 1;
+  rc.gsize = wm ? 1 : rc.W;
+  rc.K = kViews / rc.gsize;
+  rc.nblk = (n_hops + rc.K - 1) / rc.K;
+  rc.nb = rc.nblk * rc.G;
   rc.hops = hops;
   rc.n_hops = n_hops;
   int64_t run_min = INT64_MAX;
@@ -927,10 +1068,14 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   try {
     HIPCHK(hipSetDevice(c->device));
     ensure_slots(c, algo);
-    const size_t nb = (n_hops + rc.K - 1) / rc.K;
+    ensure_masks(c, rc.G);
+    const size_t nb = rc.nb;
     c->algo = algo;
     c->K = rc.K;
     c->W = rc.W;
+    c->G = rc.G;
+    c->gsize = rc.gsize;
+    for (int& x : c->grp_last) x = 0;
     c->n_hops = n_hops;
     c->cc.assign(algo == RGPU_ALGO_CC ? n_hops * rc.W : 0, rgpu_cc_summary_t{});
     c->deg.assign(algo == RGPU_ALGO_DEGREE ? n_hops * rc.W * 3 : 0, 0);
@@ -984,8 +1129,8 @@ static int64_t label_id(const rgpu_ctx* c, int32_t l) {
 
 static int view_index(rgpu_ctx* c, size_t hop, size_t win, size_t* batch, int* lane) {
   if (hop >= c->n_hops || win >= (size_t)c->W) return fail(c, RGPU_EINVAL, "view index out of range");
-  *batch = hop / c->K;
-  *lane = (int)(win * c->K + hop % c->K);
+  *batch = (hop / c->K) * c->G + win / c->gsize;
+  *lane = (int)((win % c->gsize) * c->K + hop % c->K);
   return RGPU_OK;
 }
 

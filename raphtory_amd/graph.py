@@ -172,5 +172,5 @@ class TemporalGraph:
         self._check(self._lib.rgpu_stats(self._ctx, C.byref(s)))
         d = {f: getattr(s, f) for f, _ in N.Stats._fields_ if f not in ("kernel_launches", "kernel_ms", "kernel_bytes")}
         d["kernels"] = {N.KERNEL_NAMES[i]: {"launches": s.kernel_launches[i], "ms": s.kernel_ms[i],
-                                            "bytes": s.kernel_bytes[i]} for i in range(7)}
+                                            "bytes": s.kernel_bytes[i]} for i in range(len(N.KERNEL_NAMES))}
         return d

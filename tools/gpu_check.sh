@@ -21,6 +21,7 @@ for s in ${STEPS:-pytest smoke bench}; do
     pytest) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} ;;
     smoke)  step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
     bench)  step bench 900 python bench.py ${BENCH_ARGS:-} ;;
+    probe)  step probe 900 python tools/probe.py ${PROBE_CFGS:-} ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
