@@ -16,14 +16,14 @@ from raphtory_amd.synth import BATCH_WINDOWS, DAY, HOUR, MONTH, T0_README, WEEK,
 pytestmark = pytest.mark.gpu
 
 MODES = [
-    {"RGPU_TAIL": "0"},                                    # full-grid kernel only
-    {},                                                    # defaults (window-major batches)
-    {"RGPU_CHUNK0": "1", "RGPU_TAIL_CAP": "3"},            # tail from step 3, hands back often
-    {"RGPU_CHUNK0": "2", "RGPU_CHUNK": "1", "RGPU_TAIL_CAP": "40"},
-    {"RGPU_WMAJOR": "0"},                                  # hop-major batches (all windows per row)
-    {"RGPU_WMAJOR": "0", "RGPU_TAIL": "0", "RGPU_SLOTS": "1"},
+    {},                                                    # defaults (window-major, full-grid steps)
+    {"RGPU_TAIL": "1"},                                    # tail kernel after the first chunk
+    {"RGPU_TAIL": "1", "RGPU_CHUNK0": "1", "RGPU_TAIL_CAP": "3"},  # tail from step 3, hands back often
+    {"RGPU_TAIL": "1", "RGPU_CHUNK0": "2", "RGPU_CHUNK": "1", "RGPU_TAIL_CAP": "40", "RGPU_POLL": "0"},
+    {"RGPU_WMAJOR": "0", "RGPU_TAIL": "1"},                # hop-major batches (all windows per row)
+    {"RGPU_WMAJOR": "0", "RGPU_SLOTS": "1"},
 ]
-MODE_IDS = ["notail", "default", "cap3", "cap40", "hopmajor", "hopmajor-serial"]
+MODE_IDS = ["default", "tail", "tail-cap3", "tail-cap40-blocking", "hopmajor-tail", "hopmajor-serial"]
 
 
 def graph_env(stream, env):
