@@ -117,22 +117,9 @@ __device__ __forceinline__ void batch_clear(const BatchClear& clr) {
 }
 __global__ __launch_bounds__(256) void k_batch_clear(BatchClear clr) { batch_clear(clr); }
 
-// Window test of one entity at hop k (age = t - floor time): view bits of every window.
-// PLANAR = false: one word, bit w*KS + k (all windows of the batch in one label row).
-// PLANAR = true : one word per window (plane w, bit k), W <= kMaxPlanes — the masks of one
-// hop block for every window-major batch that will use it.
-template <bool PLANAR>
-__device__ __forceinline__ void window_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const BatchParams& bp,
-                                            const int64_t* thr, int64_t age, int k) {
-  if constexpr (PLANAR) {
-#pragma unroll
-    for (int w = 0; w < kMaxPlanes; w++)
-      if (w < bp.W && age <= thr[w]) m[w] |= 1ull << k;
-  } else {
-    for (int w = 0; w < bp.W; w++)
-      if (age <= thr[w]) m[0] |= 1ull << (w * bp.KS + k);
-  }
-}
+// Window bits of an entity.  PLANAR = false: one word, bit w*KS + k (all windows of the batch
+// in one label row).  PLANAR = true: one word per window (plane w, bit k), W <= kMaxPlanes —
+// the masks of one hop block for every window-major batch that will use it.
 template <bool PLANAR>
 __device__ __forceinline__ void store_bits(const uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const BatchParams& bp,
                                            uint64_t* out, int64_t stride, int64_t i) {
@@ -145,25 +132,111 @@ __device__ __forceinline__ void store_bits(const uint64_t (&m)[PLANAR ? kMaxPlan
   }
 }
 
+// ---- interval form (hops ascending).  floor(t) = the last point with time <= t (key >> 1),
+// so point i is the floor exactly for the hops with time(i) <= t_k < time(i+1): one interval
+// of hop indices per point.  Walking the few points between the block's first and last hop
+// (one floor search, then a linear walk) replaces a floor search per hop; per alive point the
+// window test is another interval, t_k <= time(i) + w.  Edges also end an interval at the
+// first endpoint death after time(i) (a death in (time(i), t] kills: killList /
+// vertexRemoval).  Entities with more than bp.iv_max points in the block's range (power-law
+// hubs) keep the per-hop form.
+struct HopLDS {
+  int64_t hop[kViews];
+  int64_t thr[kViews];
+  int K, W, KS;
+};
+__device__ __forceinline__ void hop_lds_init(HopLDS& L, const BatchParams& bp, const int64_t* thr) {
+  if (threadIdx.x < kViews) {
+    L.hop[threadIdx.x] = bp.hop[threadIdx.x];
+    L.thr[threadIdx.x] = thr[threadIdx.x];
+  }
+  if (threadIdx.x == 0) { L.K = bp.K; L.W = bp.W; L.KS = bp.KS; }
+  __syncthreads();
+}
+// first hop index with hop >= x (K if none)
+__device__ __forceinline__ int hop_lb(const HopLDS& L, int64_t x) {
+  int a = 0, b = L.K;
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    if (L.hop[m] < x) a = m + 1; else b = m;
+  }
+  return a;
+}
+__device__ __forceinline__ uint64_t range_bits(int a, int b) {  // bits [a, b)
+  if (b <= a) return 0;
+  return (b - a >= 64 ? ~0ull : ((1ull << (b - a)) - 1)) << a;
+}
+// bits of alive point time tf whose floor interval is hop indices [a, b)
+template <bool PLANAR>
+__device__ __forceinline__ void interval_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const HopLDS& L,
+                                              int64_t tf, int a, int b) {
+  if (a >= b) return;
+  const int64_t tlast = L.hop[b - 1];
+  if constexpr (PLANAR) {
+#pragma unroll
+    for (int w = 0; w < kMaxPlanes; w++)
+      if (w < L.W) {
+        const int u = L.thr[w] >= tlast - tf ? b : min(b, hop_lb(L, tf + L.thr[w] + 1));
+        m[w] |= range_bits(a, u);
+      }
+  } else {
+    for (int w = 0; w < L.W; w++) {
+      const int u = L.thr[w] >= tlast - tf ? b : min(b, hop_lb(L, tf + L.thr[w] + 1));
+      m[0] |= range_bits(a, u) << (w * L.KS);
+    }
+  }
+}
+// the per-hop form's window bits from the LDS copy
+template <bool PLANAR>
+__device__ __forceinline__ void hop_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const HopLDS& L,
+                                         int64_t age, int k) {
+  if constexpr (PLANAR) {
+#pragma unroll
+    for (int w = 0; w < kMaxPlanes; w++)
+      if (w < L.W && age <= L.thr[w]) m[w] |= 1ull << k;
+  } else {
+    for (int w = 0; w < L.W; w++)
+      if (age <= L.thr[w]) m[0] |= 1ull << (w * L.KS + k);
+  }
+}
+
 template <bool PLANAR>
 __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* __restrict__ voff,
                                                      const int64_t* __restrict__ vkey, BatchParams bp,
                                                      uint64_t* __restrict__ vm, int64_t vstride,
                                                      BatchClear clr) {
+  __shared__ HopLDS L;
+  hop_lds_init(L, bp, bp.thr_v);
   batch_clear(clr);
+  const int K = L.K;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv;
        v += (int64_t)gridDim.x * blockDim.x) {
     const int64_t lo = voff[v], hi = voff[v + 1];
     uint64_t m[PLANAR ? kMaxPlanes : 1] = {};
+    if (bp.sorted && bp.iv_max >= 0) {
+      const int64_t f0 = floor_idx(vkey, lo, hi, L.hop[0]);
+      const int64_t f1 = floor_idx(vkey, lo, hi, L.hop[K - 1]);
+      if (f1 - f0 <= bp.iv_max) {  // f1 < 0: dead at every hop
+        for (int64_t i = f0 < 0 ? lo : f0; i <= f1; i++) {
+          const int64_t key = vkey[i];
+          if (!(key & 1)) continue;  // a deletion: dead over its interval
+          const int64_t tf = key >> 1;
+          const int b = i + 1 < hi ? hop_lb(L, vkey[i + 1] >> 1) : K;
+          interval_bits<PLANAR>(m, L, tf, hop_lb(L, tf), b);
+        }
+        store_bits<PLANAR>(m, bp, vm, vstride, v);
+        continue;
+      }
+    }
     int64_t f = -1;
-    for (int k = 0; k < bp.K; k++) {
-      const int64_t t = bp.hop[k];
+    for (int k = 0; k < K; k++) {
+      const int64_t t = L.hop[k];
       f = (bp.sorted && k > 0) ? floor_advance(vkey, f, lo, hi, t) : floor_idx(vkey, lo, hi, t);
       if (f < 0) continue;
       const int64_t key = vkey[f];
       if (!(key & 1)) continue;  // floor is a deletion
       const int64_t age = t - (key >> 1);
-      window_bits<PLANAR>(m, bp, bp.thr_v, age, k);
+      hop_bits<PLANAR>(m, L, age, k);
     }
     store_bits<PLANAR>(m, bp, vm, vstride, v);
   }
@@ -177,15 +250,37 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
                                                    const int64_t* __restrict__ doff,
                                                    const int64_t* __restrict__ dtime, BatchParams bp,
                                                    uint64_t* __restrict__ em, int64_t estride) {
+  __shared__ HopLDS L;
+  hop_lds_init(L, bp, bp.thr_e);
+  const int K = L.K;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t lo = eoff[e], hi = eoff[e + 1];
     const int32_t s = esrc[e], d = edst[e];
     const int64_t s0 = doff[s], s1 = doff[s + 1], d0 = doff[d], d1 = doff[d + 1];
     uint64_t m[PLANAR ? kMaxPlanes : 1] = {};
+    if (bp.sorted && bp.iv_max >= 0) {
+      const int64_t f0 = floor_idx(ekey, lo, hi, L.hop[0]);
+      const int64_t f1 = floor_idx(ekey, lo, hi, L.hop[K - 1]);
+      if (f1 - f0 <= bp.iv_max) {
+        for (int64_t i = f0 < 0 ? lo : f0; i <= f1; i++) {
+          const int64_t key = ekey[i];
+          if (!(key & 1)) continue;
+          const int64_t tf = key >> 1;
+          int b = i + 1 < hi ? hop_lb(L, ekey[i + 1] >> 1) : K;
+          // first endpoint death after tf ends the interval
+          const int64_t ps = first_after(dtime, s0, s1, tf), pd = first_after(dtime, d0, d1, tf);
+          const int64_t dn = min(ps < s1 ? dtime[ps] : INT64_MAX, pd < d1 ? dtime[pd] : INT64_MAX);
+          if (dn != INT64_MAX) b = min(b, hop_lb(L, dn));
+          interval_bits<PLANAR>(m, L, tf, hop_lb(L, tf), b);
+        }
+        store_bits<PLANAR>(m, bp, em, estride, e);
+        continue;
+      }
+    }
     int64_t f = -1, ps = s0, pd = d0;
-    for (int k = 0; k < bp.K; k++) {
-      const int64_t t = bp.hop[k];
+    for (int k = 0; k < K; k++) {
+      const int64_t t = L.hop[k];
       int64_t lds, ldd;  // last death time <= t of src / dst (-1: none)
       if (bp.sorted && k > 0) {
         f = floor_advance(ekey, f, lo, hi, t);
@@ -209,7 +304,7 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
       // an endpoint death in (ft, t] is a later kill point (killList / vertexRemoval)
       if (lds > ft || ldd > ft) continue;
       const int64_t age = t - ft;
-      window_bits<PLANAR>(m, bp, bp.thr_e, age, k);
+      hop_bits<PLANAR>(m, L, age, k);
     }
     store_bits<PLANAR>(m, bp, em, estride, e);
   }

@@ -14,6 +14,7 @@ constexpr int kViews = 64;  // views per batch = wavefront width (lane j <-> vie
 struct BatchParams {
   int K, W, KS;
   int sorted;             // hop[] ascending: K1 advances floors instead of searching per hop
+  int iv_max;             // K1 interval form for entities with <= iv_max points in range (< 0: off)
   int64_t hop[kViews];    // view timestamps (RangeAnalysisTask hop times)
   int64_t thr_v[kViews];  // vertex-set window of window index w: min(w_0..w_w)  (shrinkWindow)
   int64_t thr_e[kViews];  // edge window of window index w: w_w (viewAtWithWindow(t, setWindow))

@@ -151,6 +151,7 @@ struct rgpu_ctx {
   bool wmajor = true;                   // RGPU_WMAJOR: window-major batches when 2 <= W <= kMaxPlanes
   bool poll = true;                     // RGPU_POLL: spin on event queries instead of blocking
   bool hostprof = false;                // RGPU_HOSTPROF: print host-side scheduling times
+  int iv_max = 32;                      // RGPU_IVMAX: K1 interval form up to this many points (< 0 off)
   MaskSet mset[kMaskSets];
   int grp_last[kMaxPlanes] = {};        // supersteps of the last batch of each window group
   // last run: views (hop, win) -> batch (hop/K)*G + win/gsize, lane (win%gsize)*K + hop%K
@@ -465,6 +466,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   bp.W = rc.W;
   bp.KS = rc.K;
   bp.sorted = 1;
+  bp.iv_max = c->iv_max;
   for (int k = 0; k < bp.K; k++) {
     bp.hop[k] = rc.hops[h0 + k];
     if (k > 0 && bp.hop[k] < bp.hop[k - 1]) bp.sorted = 0;
@@ -789,6 +791,7 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
     bp.W = rc.W;
     bp.KS = rc.K;
     bp.sorted = 1;
+    bp.iv_max = c->iv_max;
     for (int k = 0; k < bp.K; k++) {
       bp.hop[k] = rc.hops[h0 + k];
       if (k > 0 && bp.hop[k] < bp.hop[k - 1]) bp.sorted = 0;
@@ -921,6 +924,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->wmajor = env_int("RGPU_WMAJOR", 1) != 0;
   c->poll = env_int("RGPU_POLL", 1) != 0;
   c->hostprof = env_int("RGPU_HOSTPROF", 0) != 0;
+  c->iv_max = env_int("RGPU_IVMAX", 32);
   c->tail_cap = std::max(1, env_int("RGPU_TAIL_CAP", 256));
   c->tail_maxv = std::max(0, env_int("RGPU_TAIL_MAXV", 4 << 20));
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;

@@ -105,3 +105,32 @@ def test_tail_modes_agree_on_c2_slice():
             continue
         assert np.array_equal(summ[..., :7], ref_summ), mode
         assert all(np.array_equal(a, b) for a, b in zip(labs, ref_lab)), mode
+
+
+@pytest.mark.parametrize("ivmax", ["-1", "0", "3", "96"])
+def test_window_mask_forms_vs_oracle(ivmax):
+    """K1 computes a hop block's masks per history point (interval form) for entities with at
+    most RGPU_IVMAX points in the block's range, per hop otherwise; both forms, and every mix
+    of them, give the oracle's per-vertex degrees (DegreeBasic.scala:16-28: vertex set and edge
+    liveness straight from the masks) and CC labels.  Power-law stream: hubs with long
+    histories and many deaths; out-of-order hops take the per-hop form."""
+    from raphtory_amd.synth import gen_powerlaw
+    st = gen_powerlaw(5, 3000, 40_000, t0=0, t1=YEAR)
+    o = Oracle.from_stream(st)
+    g = graph_env(st, {"RGPU_IVMAX": ivmax})
+    hops = range_hops(YEAR - 70 * DAY, YEAR + DAY, DAY)
+    wins = [MONTH, WEEK, DAY]
+    for hs in (hops, hops[::-1][:20]):
+        g.run("degree", hs, wins, retain=True)
+        for h, t in enumerate(np.asarray(hs).tolist()):
+            res = o.degree(t, wins)
+            for w in range(3):
+                ids, od, idg = res[w]
+                gids, god, gid = g.degree_vertex(h, w)
+                assert np.array_equal(gids, ids) and np.array_equal(god, od) and np.array_equal(gid, idg), (ivmax, t, w)
+    g.run("cc", hops[:40], wins, retain=True)
+    for h, t in enumerate(hops[:40].tolist()):
+        res, _ = o.cc(t, wins, mode=1)
+        for w in range(3):
+            assert np.array_equal(g.cc_vertex_labels(h, w)[1], res[w][1]), (ivmax, t, w)
+    g.close()
