@@ -312,16 +312,18 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
 
 // Per-step work counters, sharded 64 ways so that blocks never pile up on one address (a
 // same-address atomic is serialised at the memory side, ~10 ns each: 3k blocks x 3 counters
-// on one word cost more than a sparse superstep).  Layout work[(step*64 + shard)*3 + f],
-// f = visited vertices, visited slots, changed vertices.  Only written when work != nullptr
-// (profile / trace runs).  The halting vote is a plain flag store instead (idempotent).
+// on one word cost more than a sparse superstep).  Layout work[(step*64 + shard)*4 + f],
+// f = visited vertices, visited slots, changed vertices, gathered labels.  Only written when
+// work != nullptr (profile / trace runs).  The halting vote is a plain flag store instead.
 __device__ __forceinline__ void add_work(unsigned long long* work, int step, unsigned long long a,
-                                         unsigned long long b, unsigned long long c) {
+                                         unsigned long long b, unsigned long long c,
+                                         unsigned long long d = 0) {
   if (!work) return;
-  unsigned long long* w = work + ((size_t)step * 64 + (blockIdx.x & 63)) * 3;
+  unsigned long long* w = work + ((size_t)step * 64 + (blockIdx.x & 63)) * 4;
   if (a) atomicAdd(&w[0], a);
   if (b) atomicAdd(&w[1], b);
   if (c) atomicAdd(&w[2], c);
+  if (d) atomicAdd(&w[3], d);
 }
 
 // ---------------------------------------------------------------- K2: batch CSR (+ superstep 1)
@@ -579,7 +581,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          const uint64_t* __restrict__ chg_prev,
                                          uint64_t* __restrict__ chg_next, uint8_t* __restrict__ act_next,
                                          const TailList& tl, int lane, int32_t& changed,
-                                         unsigned long long& pv, unsigned long long& ps) {
+                                         unsigned long long& pv, unsigned long long& ps,
+                                         unsigned long long& pg) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
@@ -610,7 +613,10 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     // stage 3: neighbours' change words (vertex 0's word for idle lanes, masked by sm = 0)
     uint64_t act[CH];
 #pragma unroll
-    for (int i = 0; i < CH; i++) act[i] = sm[i] & chg_prev[nb[i]];
+    for (int i = 0; i < CH; i++) {
+      act[i] = sm[i] & chg_prev[nb[i]];
+      pg += __popcll(act[i]);  // labels this lane's slot gathers (per lane; summed at the end)
+    }
     // own rows are only meaningful on member lanes
 #pragma unroll
     for (int i = 0; i < CH; i++) cur[i] = ((readlane64(mv_l, i) >> lane) & 1) ? cur[i] : INT32_MAX;
@@ -634,6 +640,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
           const int64_t idx = base + (j < n ? j : c2);
           const int32_t q = snbr[idx];
           const uint64_t a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
+          pg += __popcll(a2);
           best[i] = gather_min<BUF>(a2, q, best[i], lab_cur, lane);
         }
       }
@@ -692,8 +699,8 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
                                                   unsigned long long* __restrict__ work) {
   if (stepflag[step - 1] == 0) return;
   __shared__ int32_t red;
-  __shared__ unsigned long long wred[2];
-  if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; }
+  __shared__ unsigned long long wred[3];
+  if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; wred[2] = 0; }
   const int64_t nwords = (nv + 7) >> 3;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -703,7 +710,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int32_t changed = 0;
-  unsigned long long pv = 0, ps = 0;
+  unsigned long long pv = 0, ps = 0, pg = 0;
   const TailList none{nullptr, nullptr};
   for (int64_t c = wave; c * CH < nv; c += nwaves) {
     const int64_t v0 = c * CH;
@@ -717,12 +724,15 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     if (v0 + CH > nv) bits &= (1u << (nv - v0)) - 1;
     if (!bits) continue;
     cc_chunk<CH, BUF, false>(v0 + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
-                             lab_next, chg_prev, chg_next, act_next, none, lane, changed, pv, ps);
+                             lab_next, chg_prev, chg_next, act_next, none, lane, changed, pv, ps, pg);
   }
+  if (work)
+    for (int o = 32; o > 0; o >>= 1) pg += __shfl_xor(pg, o);
   if (lane == 0) {
     if (changed) atomicAdd(&red, changed);
     if (pv) atomicAdd(&wred[0], pv);
     if (ps) atomicAdd(&wred[1], ps);
+    if (pg) atomicAdd(&wred[2], pg);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -730,7 +740,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
       stepflag[step] = 1;
       if (hostflag) hostflag[step] = 1;
     }
-    add_work(work, step, wred[0], wred[1], (unsigned long long)red);
+    add_work(work, step, wred[0], wred[1], (unsigned long long)red, wred[2]);
   }
 }
 
@@ -763,7 +773,7 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
   __shared__ int32_t list[2][kTailListCap];
   __shared__ int nlist[2];
   __shared__ int nchanged;
-  __shared__ unsigned long long wsum[2];
+  __shared__ unsigned long long wsum[3];
   auto ACT = [&](int k) { return k == 0 ? act0 : (k == 1 ? act1 : act2); };
   const int lane = lane_id(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if (stepflag[r0 - 1] == 0) {  // the batch has halted already
@@ -800,7 +810,7 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
     if (ncur > cap) break;  // too wide for one workgroup: the full-grid kernel takes step r+1
     const int s = r + 1;
     __syncthreads();  // everyone has read nlist[p] and left the previous clear loop
-    if (threadIdx.x == 0) { nlist[p ^ 1] = 0; nchanged = 0; wsum[0] = 0; wsum[1] = 0; }
+    if (threadIdx.x == 0) { nlist[p ^ 1] = 0; nchanged = 0; wsum[0] = 0; wsum[1] = 0; wsum[2] = 0; }
     __syncthreads();
     uint8_t* a_cur = ACT(s % 3);
     uint8_t* a_next = ACT((s + 1) % 3);
@@ -810,17 +820,19 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
     uint64_t* chg_next = (s & 1) ? chg1 : chg0;
     const TailList tl{list[p ^ 1], &nlist[p ^ 1]};
     int32_t changed = 0;
-    unsigned long long pv = 0, ps = 0;
+    unsigned long long pv = 0, ps = 0, pg = 0;
     for (int c = wid * 4; c < ncur; c += nw * 4) {
       const int k = c + (lane & 3) < ncur ? c + (lane & 3) : c;
       const uint32_t bits = ncur - c >= 4 ? 0xfu : ((1u << (ncur - c)) - 1);
       cc_chunk<4, BUF, true>((int64_t)list[p][k], bits, adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
-                             chg_prev, chg_next, a_next, tl, lane, changed, pv, ps);
+                             chg_prev, chg_next, a_next, tl, lane, changed, pv, ps, pg);
     }
+    for (int o = 32; o > 0; o >>= 1) pg += __shfl_xor(pg, o);
     if (lane == 0) {
       if (changed) atomicAdd(&nchanged, changed);
       if (pv) atomicAdd(&wsum[0], pv);
       if (ps) atomicAdd(&wsum[1], ps);
+      if (pg) atomicAdd(&wsum[2], pg);
     }
     __syncthreads();
     for (int k = threadIdx.x; k < ncur; k += blockDim.x) a_cur[list[p][k]] = 0;  // step s consumed them
@@ -830,7 +842,7 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
         stepflag[s] = 1;
         if (hostflag) hostflag[s] = 1;
       }
-      add_work(work, s, wsum[0], wsum[1], (unsigned long long)nch);
+      add_work(work, s, wsum[0], wsum[1], (unsigned long long)nch, wsum[2]);
     }
     r = s;
     p ^= 1;

@@ -46,7 +46,7 @@ enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUM
 
 constexpr int kMaxSteps = 128;
 constexpr int kStatWords = 7 * kViews;  // 6 per-view fields + counters row
-constexpr int kWorkWords = kMaxSteps * 64 * 3;
+constexpr int kWorkWords = kMaxSteps * 64 * 4;
 constexpr int64_t kPad = 64;  // tail padding of per-vertex / per-slot batch arrays
 constexpr int kMaxSlots = 4;  // batches in flight (one HIP stream each; GPU_MAX_HW_QUEUES = 4)
 
@@ -226,10 +226,11 @@ hipEvent_t take_event(rgpu_ctx* c) {
 }
 
 // Run `fn` (one kernel launch) on slot stream, bracketed by events in profile mode.
+// evented = false: the caller brackets a group of launches itself (see launch_chunk).
 template <class F>
-void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn, int step = 0) {
+void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn, int step = 0, bool evented = true) {
   Slot& s = c->slot[si];
-  if (c->profile) {
+  if (c->profile && evented) {
     hipEvent_t a = take_event(c), b = take_event(c);
     HIPCHK(hipEventRecord(a, s.stream));
     fn();
@@ -368,13 +369,26 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
   Slot& s = c->slot[si];
   const DevGraph& g = c->g;
   int last = std::min(rc.max_steps, s.r_launched + n);
+  // profile: ONE event pair around the chunk's back-to-back superstep launches (per-launch
+  // pairs add ~3 us of marker latency to a ~12 us kernel; rocprofv3's per-dispatch times
+  // agree with the chunk average)
+  hipEvent_t ea = nullptr, eb = nullptr;
+  if (c->profile && last > s.r_launched) {
+    ea = take_event(c);
+    eb = take_event(c);
+    HIPCHK(hipEventRecord(ea, s.stream));
+  }
   for (int r = s.r_launched + 1; r <= last; r++) {
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                      s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
                      s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                      c->profile ? s.work : nullptr, c->step_variant | (g_rowbuf ? 16 : 0));
-    }, r);
+    }, r, false);
+  }
+  if (ea) {
+    HIPCHK(hipEventRecord(eb, s.stream));
+    c->timed.push_back({KID_STEP, si, s.batch, s.r_launched + 1, ea, eb, 0.0});
   }
   s.r_launched = last;
   if (c->tail_on && g.nv <= c->tail_maxv && s.r_launched < rc.max_steps) {
@@ -585,18 +599,19 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
     if (c->profile) {
       auto wsum = [&](int r, int f) {
         unsigned long long t = 0;
-        for (int k = 0; k < 64; k++) t += s.h_work[((size_t)r * 64 + k) * 3 + f];
+        for (int k = 0; k < 64; k++) t += s.h_work[((size_t)r * 64 + k) * 4 + f];
         return t;
       };
       c->st.kernel_bytes[KID_SLOTS] += 12.0 * (double)wsum(1, 1);
       // per executed step: frontier flags read + flags two steps ahead cleared (2 B per
       // vertex); per visited vertex vm, cnt, adj_off, own change word, label row in and out,
       // change word out (548 B); per slot of a visited vertex nbr + mask + neighbour's change
-      // word (20 B).  Label gathers and flag stores are not counted.
-      // (a tail-kernel superstep reads no bitmap: its frontier is a list in LDS)
+      // word (20 B); per gathered label (a neighbour's label in a view where it changed) 4 B.
+      // Flag stores are not counted.  (A tail-kernel step reads no bitmap: its frontier is a
+      // list in LDS.)
       for (int r = 2; r <= s.r_final; r++)
-        c->st.kernel_bytes[s.by_tail[r] ? KID_TAIL : KID_STEP] +=
-            (s.by_tail[r] ? 0.0 : 2.0 * c->g.nv) + 548.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1);
+        c->st.kernel_bytes[s.by_tail[r] ? KID_TAIL : KID_STEP] += (s.by_tail[r] ? 0.0 : 2.0 * c->g.nv) +
+            548.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1) + 4.0 * (double)wsum(r, 3);
       if (!c->trace_path.empty())
         for (int r = 1; r <= s.r_final; r++)
           c->steprec.push_back({s.batch, r, wsum(r, 0), wsum(r, 1), (int)wsum(r, 2)});

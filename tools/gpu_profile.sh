@@ -1,15 +1,45 @@
 #!/bin/bash
-# Bench + rocprofv3 evidence for profiles/: kernel-trace/stats pass, then one PMC pass per
-# counter (FETCH_SIZE, WRITE_SIZE) on the dominant kernel — never combined with tracing.
+# Bench + rocprofv3 evidence for profiles/: the bench line, then a kernel-trace/stats pass and
+# one PMC pass per counter (FETCH_SIZE, WRITE_SIZE) on the dominant kernel, all on
+# `bench.py --profile-only` (the serial HIP-event pass the roofline figures come from), never
+# combining counters with tracing.  Summary -> gpurun_out/prof/pmc_summary.json.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/prof
 mkdir -p $O
+K=${KREGEX:-k_cc_step2}
 run() { local name=$1 secs=$2; shift 2; echo "=== $name"; timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "=== $name rc=$rc"; tail -3 "$O/$name.log"; [ $rc -eq 0 ] || exit $rc; }
 run bench 600 python bench.py ${BENCH_ARGS:-}
 grep '^{' $O/bench.log > $O/bench.json || true
-run kt 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
-run fetch 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_cc_step -d $O/fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-profile-pass
-run write 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_cc_step -d $O/write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-profile-pass
-find $O -name '*.csv' | head -20
+run prof_only 300 python bench.py --profile-only ${BENCH_ARGS:-}
+grep '^{' $O/prof_only.log > $O/prof_only.json || true
+run kt 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
+run fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $O/fetch -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
+run write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O/write -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
+python3 - "$K" <<'PY'
+import csv, glob, json, sys
+k = sys.argv[1]
+out = {}
+for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+    vals, durs = [], []
+    for f in glob.glob(f"gpurun_out/prof/{ctr.split('_')[0].lower()}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") == ctr and k in r.get("Kernel_Name", ""):
+                vals.append(float(r["Counter_Value"]))
+                try:
+                    durs.append((float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) / 1e3)
+                except (KeyError, ValueError):
+                    pass
+    if vals:
+        out[ctr] = {"kernel": k, "dispatches": len(vals), "mean_kb_per_dispatch": sum(vals) / len(vals),
+                    "total_kb": sum(vals), "mean_dispatch_us_under_pmc": sum(durs) / len(durs) if durs else None}
+if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
+    out["traffic_bytes_per_launch"] = {
+        "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM section: gfx950 FETCH_SIZE counts "
+                   "half of a wide read; narrow 4/8-B gathers are uncalibrated; Infinity-Cache hits are counted)",
+        "value": 2 * out["FETCH_SIZE"]["mean_kb_per_dispatch"] * 1024 + out["WRITE_SIZE"]["mean_kb_per_dispatch"] * 1024}
+json.dump(out, open("gpurun_out/prof/pmc_summary.json", "w"), indent=1)
+print(json.dumps(out)[:600])
+PY
+find $O -name '*stats.csv' | head
