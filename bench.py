@@ -44,9 +44,12 @@ def parse():
     p.add_argument("--profile-only", action="store_true",
                    help="only the serial HIP-event profile pass (the command rocprofv3 is run on, so "
                         "that its per-kernel averages match the roofline figures)")
-    p.add_argument("--config", default="c2", choices=["c2", "c3"], help="c2 = the headline metric")
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4"], help="c2 = the headline metric")
     p.add_argument("--c3-vertices", type=int, default=10_000_000)
     p.add_argument("--c3-events", type=int, default=100_000_000)
+    p.add_argument("--c4-users", type=int, default=20_000_000)
+    p.add_argument("--c4-interactions", type=int, default=333_333_334, help="x3 updates (1B at the default)")
+    p.add_argument("--c4-hops", type=int, default=168)
     return p.parse_args()
 
 
@@ -136,8 +139,85 @@ def run_c3(a, rank, world, local):
     print(json.dumps(out))
 
 
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def run_c4(a, rank, world, local):
+    """BASELINE configs[3] (C4): GAB-shaped add-only stream — (VADD s, VADD d, EADD s->d) triples
+    at one t (GabUserGraphRouter.scala:31-33) — 20M users, 333M interactions = 1B updates,
+    2016-08-10 -> 2018-05-31; batched windows {y,m,w,d,h}, hourly hops, the last 168 hops; CC.
+    N = 1: one graph.  N > 1: vertex-partitioned (Utils.getPartition), one partition per GPU,
+    boundary label rows exchanged over RCCL every superstep; every rank
+    generates the same seeded stream and keeps what its partition needs.  Secondary line."""
+    import torch
+    from raphtory_amd import TemporalGraph
+    from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab, range_hops
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")  # control plane; the data path is the library's RCCL
+    t0 = time.perf_counter()
+    s = gen_gab(4, a.c4_users, a.c4_interactions)
+    gen_s = time.perf_counter() - t0
+    log(f"C4 stream: {len(s)} updates generated in {gen_s:.1f} s")
+    if dist is not None:
+        from raphtory_amd.partitioned import open_rccl_partition
+        g = open_rccl_partition(local, dist)
+    else:
+        g = TemporalGraph(device=local)
+    g.ingest_stream(s)
+    end = int(s.t[-1])
+    n_up = len(s)
+    del s
+    t0 = time.perf_counter()
+    g.seal()
+    seal_s = time.perf_counter() - t0
+    st = g.stats()
+    log(f"sealed in {seal_s:.1f} s: {st['vertices']} vertices, {st['edges']} edge entities")
+    hops = range_hops(end - (a.c4_hops - 1) * HOUR, end, HOUR)
+    windows = BATCH_WINDOWS
+    g.run("cc", hops, windows)  # warm-up
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        g.run("cc", hops, windows)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    ms = (time.perf_counter() - t0) * 1e3 / a.steps
+    if dist is not None:
+        from raphtory_amd.replicas import max_over_ranks
+        ms = max_over_ranks(ms, dist)
+    log(f"query {ms:.1f} ms")
+    g.run("cc", hops, windows, profile=True, serial=True)
+    ks = {k: v for k, v in g.stats()["kernels"].items() if v["launches"]}
+    summ = g.cc_summaries()
+    out = {"config": "C4", "n_gpus": world, "updates": n_up, "vertices": st["vertices"], "edge_entities": st["edges"],
+           "vertex_events": st["vertex_events"], "edge_events": st["edge_events"], "gen_s": round(gen_s, 1),
+           "seal_s": round(seal_s, 1), "hops": len(hops), "windows": len(windows), "ms_per_query": round(ms, 2),
+           "edge_windows_per_s": st["edges"] * len(windows) * len(hops) / (ms / 1e3) if world == 1 else None,
+           "supersteps_per_batch_mean": round(g.stats()["supersteps"] / max(1, g.stats()["batches"]), 2),
+           "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3), "avg_us": round(v["ms"] * 1e3 / v["launches"], 2),
+                           "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)} for k, v in ks.items()},
+           "check": {"sum_biggest": int(summ[..., 0].sum()), "sum_total": int(summ[..., 1].sum()),
+                     "sum_members": int(summ[..., 5].sum())}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    g.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.config == "c4":
+        rank, world, local = dist_env()
+        import torch
+        torch.cuda.set_device(local)
+        return run_c4(a, rank, world, local)
     if a.config == "c3":
         rank, world, local = dist_env()
         import torch

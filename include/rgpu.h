@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RGPU_ABI_VERSION 1
+#define RGPU_ABI_VERSION 2
 
 /* error codes */
 #define RGPU_OK 0
@@ -74,10 +74,11 @@ typedef struct {
   int64_t views, batches, supersteps, launches;
   double ms_total;               /* wall ms inside the last rgpu_run_view_batch */
   /* per-kernel event timing (RGPU_RUN_PROFILE): 0=window_mask 1=slots 2=cc_step 3=cc_hist
-   * 4=cc_summary 5=pr_step 6=degree 7=cc_tail (late supersteps, one workgroup) */
-  int64_t kernel_launches[8];
-  double kernel_ms[8];
-  double kernel_bytes[8];        /* algorithmic bytes summed over launches */
+   * 4=cc_summary 5=pr_step 6=degree 7=cc_tail (late supersteps, one workgroup)
+   * 8=heavy (hub segment kernels) 9-11 reserved */
+  int64_t kernel_launches[12];
+  double kernel_ms[12];
+  double kernel_bytes[12];       /* algorithmic bytes summed over launches */
 } rgpu_stats_t;
 
 int rgpu_abi_version(void);

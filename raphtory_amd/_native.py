@@ -26,7 +26,8 @@ ERROR_NAMES = {
     RGPU_ENOMEM: "RGPU_ENOMEM",
     RGPU_ENOTSUP: "RGPU_ENOTSUP",
 }
-KERNEL_NAMES = ["window_mask", "cc_slots", "cc_step", "cc_hist", "cc_summary", "pr_step", "degree", "cc_tail"]
+KERNEL_NAMES = ["window_mask", "cc_slots", "cc_step", "cc_hist", "cc_summary", "pr_step", "degree", "cc_tail",
+                "heavy", "-", "-", "-"]
 
 # exported symbols of librgpu.so, exactly the declarations of include/rgpu.h
 EXPORTS = [
@@ -53,7 +54,7 @@ class Stats(C.Structure):
         ("vertex_events", C.c_int64), ("edge_events", C.c_int64), ("deaths", C.c_int64),
         ("views", C.c_int64), ("batches", C.c_int64), ("supersteps", C.c_int64), ("launches", C.c_int64),
         ("ms_total", C.c_double),
-        ("kernel_launches", C.c_int64 * 8), ("kernel_ms", C.c_double * 8), ("kernel_bytes", C.c_double * 8),
+        ("kernel_launches", C.c_int64 * 12), ("kernel_ms", C.c_double * 12), ("kernel_bytes", C.c_double * 12),
     ]
 
 

@@ -357,7 +357,12 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   uint64_t* __restrict__ chg1, uint8_t* __restrict__ act2,
                                                   int32_t* __restrict__ stepflag,
                                                   int32_t* __restrict__ hostflag,
-                                                  unsigned long long* __restrict__ work) {
+                                                  unsigned long long* __restrict__ work,
+                                                  const int32_t* __restrict__ hv_of,
+                                                  const int32_t* __restrict__ hv_seg,
+                                                  const int32_t* __restrict__ segcnt,
+                                                  const uint64_t* __restrict__ segor,
+                                                  int32_t* __restrict__ hbest) {
   __shared__ unsigned long long red[3];
   if (threadIdx.x < 3) red[threadIdx.x] = 0;
   __syncthreads();
@@ -370,6 +375,38 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
     if (mv == 0) {
       if (lane == 0) { cnt[v] = 0; vadj[v] = 0; }
+      continue;
+    }
+    if (hv_of && hv_of[v] >= 0) {
+      // heavy vertex: its segments were compacted by k_heavy_slots, which also left the
+      // superstep-1 minima of its neighbours' ranks in hbest; neighbours of a change are
+      // marked by k_heavy_mark.  (Heavy vertices exist only with one partition.)
+      const int32_t h = hv_of[v], me = (int32_t)v;
+      const int32_t x = hbest[(int64_t)h * 64 + lane];
+      hbest[(int64_t)h * 64 + lane] = INT32_MAX;
+      row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
+      const int32_t best = min(me, x);
+      row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+      uint64_t any = 0;
+      unsigned long long kept = 0;
+      for (int32_t k = hv_seg[h] + lane; k < hv_seg[h + 1]; k += 64) {
+        any |= segor[k];
+        kept += (unsigned long long)segcnt[k];
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        any |= __shfl_xor(any, o);
+        kept += __shfl_xor(kept, o);
+      }
+      const uint64_t ch = __ballot(best < me);
+      if (lane == 0) {
+        cnt[v] = 0;
+        vadj[v] = any;
+        chg1[v] = ch;
+        if (ch) act2[v] = 1;
+      }
+      changed += ch != 0;
+      members += 1;
+      alive += kept;
       continue;
     }
     // label = global rank (== local rank with one partition).  A ghost (v >= n_own) only
@@ -582,12 +619,14 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          uint64_t* __restrict__ chg_next, uint8_t* __restrict__ act_next,
                                          const TailList& tl, int lane, int32_t& changed,
                                          unsigned long long& pv, unsigned long long& ps,
-                                         unsigned long long& pg) {
+                                         unsigned long long& pg, const int32_t* __restrict__ hv_of = nullptr,
+                                         int32_t* __restrict__ hbest = nullptr) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
     const uint64_t mv_l = okl ? vm[vl] : 0;
-    const int32_t n_l = okl ? cnt[vl] : 0;
+    const int32_t n_l = okl ? cnt[vl] : 0;  // 0 for a heavy vertex (its slots are in segments)
+    const int32_t hh_l = (okl && hv_of) ? hv_of[vl] : -1;
     const int64_t b_l = adj_off[vl];
     const uint64_t cp_l = chg_prev[vl];
     int64_t vv[CH];
@@ -645,6 +684,19 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
         }
       }
     }
+    // heavy vertices: the step's minima over their segments (k_heavy_gather); reset for the
+    // next step.  Their neighbours are marked by k_heavy_mark.
+    if (hv_of) {
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        const int32_t h = __builtin_amdgcn_readlane(hh_l, i);
+        if (h >= 0) {
+          const int32_t x = hbest[(int64_t)h * 64 + lane];
+          hbest[(int64_t)h * 64 + lane] = INT32_MAX;
+          best[i] = min(best[i], ((readlane64(mv_l, i) >> lane) & 1) ? x : INT32_MAX);
+        }
+      }
+    }
     // stage 4b: publish
 #pragma unroll
     for (int i = 0; i < CH; i++) {
@@ -696,7 +748,9 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
                                                   uint8_t* __restrict__ act_clear,
                                                   int32_t* __restrict__ stepflag,
                                                   int32_t* __restrict__ hostflag,
-                                                  unsigned long long* __restrict__ work) {
+                                                  unsigned long long* __restrict__ work,
+                                                  const int32_t* __restrict__ hv_of,
+                                                  int32_t* __restrict__ hbest) {
   if (stepflag[step - 1] == 0) return;
   __shared__ int32_t red;
   __shared__ unsigned long long wred[3];
@@ -724,7 +778,8 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     if (v0 + CH > nv) bits &= (1u << (nv - v0)) - 1;
     if (!bits) continue;
     cc_chunk<CH, BUF, false>(v0 + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
-                             lab_next, chg_prev, chg_next, act_next, none, lane, changed, pv, ps, pg);
+                             lab_next, chg_prev, chg_next, act_next, none, lane, changed, pv, ps, pg, hv_of,
+                             hbest);
   }
   if (work)
     for (int o = 32; o > 0; o >>= 1) pg += __shfl_xor(pg, o);
@@ -849,6 +904,186 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
     if (nch == 0 || s >= rmax) break;
   }
   if (threadIdx.x == 0) info[0] = r;
+}
+
+// ---------------------------------------------------------------- heavy vertices
+// A power-law hub has 1e5-1e6 slots: as one wave's serial loop it would be the whole
+// superstep.  Its static slots are cut into segments of <= kSegSlots, one wave each, and the
+// per-view minimum over a segment is formed with lane = slot: every lane loads the whole
+// label row of its neighbour (or an always-cached row of INT32_MAX when that neighbour has
+// nothing new), folds it into acc[64], and a butterfly reduce-scatter leaves the minimum of
+// view j in lane j, added to the hub's row with one coalesced atomicMin.
+
+__device__ int4 g_max_row[16] = {
+    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
+    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
+    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
+    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
+    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
+    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
+    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
+    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}};
+
+// acc[j] per lane -> returns the minimum over the wave of view `lane` (each butterfly step
+// keeps the half of the views that the lane's bit selects and takes the partner's copy).
+__device__ __forceinline__ int32_t wave_min_scatter(int32_t (&acc)[64], int lane) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const bool up = (lane & d) != 0;
+#pragma unroll
+    for (int i = 0; i < d; i++) {
+      const int32_t send = up ? acc[i] : acc[i + d];
+      const int32_t recv = __shfl_xor(send, d);
+      acc[i] = min(up ? acc[i + d] : acc[i], recv);
+    }
+  }
+  return acc[0];
+}
+
+// K2 for heavy vertices: compact each segment's kept slots (kept iff em[e] & vm[nb] & vm[v])
+// at its static position, record its count and mask OR, and fold the superstep-1 minima
+// (neighbours' ranks, ConnectedComponents.setup sends own ids) into hbest.
+__global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t* __restrict__ seg_v,
+                                                     const int32_t* __restrict__ seg_h,
+                                                     const int64_t* __restrict__ seg_lo,
+                                                     const int32_t* __restrict__ seg_n,
+                                                     const int64_t* __restrict__ out_off,
+                                                     const int64_t* __restrict__ in_off,
+                                                     const int64_t* __restrict__ adj_off,
+                                                     const int32_t* __restrict__ in_eid,
+                                                     const int32_t* __restrict__ esrc,
+                                                     const int32_t* __restrict__ edst,
+                                                     const uint64_t* __restrict__ vm,
+                                                     const uint64_t* __restrict__ em,
+                                                     int32_t* __restrict__ snbr, uint64_t* __restrict__ smask,
+                                                     int32_t* __restrict__ segcnt, uint64_t* __restrict__ segor,
+                                                     int32_t* __restrict__ hbest) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t sg = wave; sg < nseg; sg += nwaves) {
+    const int32_t v = seg_v[sg];
+    const uint64_t mv = vm[v];
+    if (mv == 0) {
+      if (lane == 0) { segcnt[sg] = 0; segor[sg] = 0; }
+      continue;
+    }
+    const int64_t lo = seg_lo[sg], rel0 = lo - adj_off[v], o0 = out_off[v], i0 = in_off[v];
+    const int64_t nout = out_off[v + 1] - o0;
+    const int32_t ns = seg_n[sg];
+    int32_t acc[64];
+#pragma unroll
+    for (int j = 0; j < 64; j++) acc[j] = INT32_MAX;
+    int32_t count = 0;
+    uint64_t any = 0;
+    for (int32_t c = 0; c < ns; c += 64) {
+      const int32_t jj = c + lane;
+      uint64_t m = 0;
+      int32_t nb = 0;
+      if (jj < ns) {
+        const int64_t rel = rel0 + jj;
+        int64_t e;
+        if (rel < nout) { e = o0 + rel; nb = edst[e]; }
+        else { e = in_eid[i0 + (rel - nout)]; nb = esrc[e]; }
+        if (nb != v) m = em[e] & vm[nb] & mv;
+      }
+      const uint64_t bal = __ballot(m != 0);
+      if (m) {
+        const int64_t pos = lo + count + __popcll(bal & lanemask_lt());
+        snbr[pos] = nb;
+        smask[pos] = m;
+      }
+      count += __popcll(bal);
+      any |= m;
+#pragma unroll
+      for (int j = 0; j < 64; j++) acc[j] = ((m >> j) & 1) ? min(acc[j], nb) : acc[j];
+    }
+    for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
+    if (lane == 0) { segcnt[sg] = count; segor[sg] = any; }
+    if (any) {
+      const int32_t mn = wave_min_scatter(acc, lane);
+      if (mn != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], mn);
+    }
+  }
+}
+
+// Superstep r, before the full-grid kernel: minimum over each segment of a flagged heavy
+// vertex of the labels of its neighbours that changed in r-1 (views where they did).
+__global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, const int32_t* __restrict__ seg_v,
+                                                      const int32_t* __restrict__ seg_h,
+                                                      const int64_t* __restrict__ seg_lo,
+                                                      const int32_t* __restrict__ segcnt,
+                                                      const int32_t* __restrict__ snbr,
+                                                      const uint64_t* __restrict__ smask,
+                                                      const int32_t* __restrict__ lab_cur,
+                                                      const uint64_t* __restrict__ chg_prev,
+                                                      const uint8_t* __restrict__ act_cur,
+                                                      const int32_t* __restrict__ stepflag,
+                                                      int32_t* __restrict__ hbest) {
+  if (stepflag[step - 1] == 0) return;
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t sg = wave; sg < nseg; sg += nwaves) {
+    const int32_t v = seg_v[sg];
+    if (!act_cur[v]) continue;
+    const int32_t n = segcnt[sg];
+    if (n == 0) continue;
+    const int64_t base = seg_lo[sg];
+    int32_t acc[64];
+#pragma unroll
+    for (int j = 0; j < 64; j++) acc[j] = INT32_MAX;
+    uint64_t anyw = 0;
+    for (int32_t c = 0; c < n; c += 64) {
+      const int32_t jj = c + lane;
+      const int64_t idx = base + (jj < n ? jj : c);
+      const int32_t q = snbr[idx];
+      const uint64_t a = jj < n ? (smask[idx] & chg_prev[q]) : 0;
+      anyw |= a;
+      const int4* row = a ? reinterpret_cast<const int4*>(lab_cur + (int64_t)q * 64) : g_max_row;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int4 x = row[k];
+        acc[4 * k + 0] = ((a >> (4 * k + 0)) & 1) ? min(acc[4 * k + 0], x.x) : acc[4 * k + 0];
+        acc[4 * k + 1] = ((a >> (4 * k + 1)) & 1) ? min(acc[4 * k + 1], x.y) : acc[4 * k + 1];
+        acc[4 * k + 2] = ((a >> (4 * k + 2)) & 1) ? min(acc[4 * k + 2], x.z) : acc[4 * k + 2];
+        acc[4 * k + 3] = ((a >> (4 * k + 3)) & 1) ? min(acc[4 * k + 3], x.w) : acc[4 * k + 3];
+      }
+    }
+    if (__ballot(anyw != 0) == 0) continue;
+    const int32_t mn = wave_min_scatter(acc, lane);
+    if (mn != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], mn);
+  }
+}
+
+// Superstep r, after the full-grid kernel: the neighbours of every heavy vertex that changed
+// in r (and was visited: its change word is current) sharing a changed view join the next
+// frontier.  act_cur = nullptr: every member was visited (superstep 1).
+__global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, const int32_t* __restrict__ seg_v,
+                                                    const int64_t* __restrict__ seg_lo,
+                                                    const int32_t* __restrict__ segcnt,
+                                                    const int32_t* __restrict__ snbr,
+                                                    const uint64_t* __restrict__ smask,
+                                                    const uint64_t* __restrict__ chg_now,
+                                                    const uint8_t* __restrict__ act_cur,
+                                                    uint8_t* __restrict__ act_next,
+                                                    const int32_t* __restrict__ stepflag) {
+  if (stepflag[step] == 0) return;
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t sg = wave; sg < nseg; sg += nwaves) {
+    const int32_t v = seg_v[sg];
+    if (act_cur && !act_cur[v]) continue;
+    const uint64_t ch = chg_now[v];
+    if (!ch) continue;
+    const int32_t n = segcnt[sg];
+    const int64_t base = seg_lo[sg];
+    for (int32_t c = 0; c < n; c += 64) {
+      const int32_t jj = c + lane;
+      if (jj < n && (smask[base + jj] & ch)) act_next[snbr[base + jj]] = 1;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- K5: CC reductions
@@ -1351,29 +1586,54 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
-                     int32_t* hostflag, unsigned long long* work) {
+                     int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb) {
+  const bool hv = g.n_seg > 0;
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
-                                                stepflag, hostflag, work);
+                                                stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
+                                                hb.segcnt, hb.segor, hb.best);
 }
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
-                    unsigned long long* work, int variant) {
+                    unsigned long long* work, int variant, int32_t* hbest) {
   const int ch = (variant & 15) == 8 ? 8 : 4;
   const bool buf = (variant & 16) != 0;
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches
   const unsigned cap = step >= g_tail_step ? (unsigned)g_tail_grid : (unsigned)g_step_grid;
   const unsigned grid = grid_for(g.nv, 4 * ch, cap);
+  const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
-    act_cur, act_next, act_clear, stepflag, hostflag, work
+    act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest
   if (ch == 8 && buf) k_cc_step2<8, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (ch == 8) k_cc_step2<8, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (buf) k_cc_step2<4, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else k_cc_step2<4, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
 #undef RGPU_STEP_ARGS
+}
+void launch_heavy_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb) {
+  if (g.n_seg <= 0) return;
+  k_heavy_slots<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off,
+                                                            g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
+                                                            snbr, smask, hb.segcnt, hb.segor, hb.best);
+}
+void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
+                         const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
+                         const int32_t* stepflag, int step, const HeavyBuf& hb) {
+  if (g.n_seg <= 0) return;
+  k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
+                                                             snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
+                                                             hb.best);
+}
+void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
+                       const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
+                       const HeavyBuf& hb, const uint8_t* act_cur) {
+  if (g.n_seg <= 0) return;
+  k_heavy_mark<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
+                                                           chg_now, act_cur, act_next, stepflag);
 }
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,

@@ -32,6 +32,23 @@ struct DevGraph {
   const int32_t* in_eid = nullptr;
   int64_t n_own = 0;                                 // ranks [0, n_own) owned (== nv, one partition)
   const int32_t* grank = nullptr;                    // global rank per local rank (null: identity)
+  // heavy vertices (static slots > RGPU_HEAVY, power-law hubs): their slots are split into
+  // segments of <= kSegSlots static slots, each compacted / gathered / marked by its own wave
+  int64_t n_heavy = 0, n_seg = 0;
+  const int32_t* hv_of = nullptr;   // [nv] heavy index or -1
+  const int32_t* hv_seg = nullptr;  // [n_heavy+1] first segment of each heavy vertex
+  const int32_t* seg_v = nullptr;   // [n_seg] vertex rank of the segment
+  const int32_t* seg_h = nullptr;   // [n_seg] heavy index of the segment
+  const int64_t* seg_lo = nullptr;  // [n_seg] first static slot (absolute, = adj_off[v] + offset)
+  const int32_t* seg_n = nullptr;   // [n_seg] static slots in the segment
+};
+constexpr int kSegSlots = 512;
+
+// Per-batch state of the heavy-vertex path (one per batch slot).
+struct HeavyBuf {
+  int32_t* segcnt = nullptr;   // [n_seg] kept slots of the segment (compacted at seg_lo)
+  uint64_t* segor = nullptr;   // [n_seg] OR of the segment's kept slot masks
+  int32_t* best = nullptr;     // [n_heavy][64] partial minima of the step (INT32_MAX when idle)
 };
 
 // Small per-batch state cleared by the first kernel of the batch (no memset launches).
@@ -54,7 +71,18 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
-                     int32_t* hostflag, unsigned long long* work);
+                     int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb);
+// heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
+// (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
+// next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
+void launch_heavy_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb);
+void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
+                         const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
+                         const int32_t* stepflag, int step, const HeavyBuf& hb);
+void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
+                       const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
+                       const HeavyBuf& hb, const uint8_t* act_cur);
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID)
 extern int g_rowbuf;     // label rows via buffer descriptors (RGPU_ROWBUF)
 extern int g_tail_step, g_tail_grid;  // supersteps >= tail_step use at most tail_grid blocks
@@ -63,7 +91,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
-                    unsigned long long* work, int variant);
+                    unsigned long long* work, int variant, int32_t* hbest = nullptr);
 // Many late supersteps in one single-workgroup launch while the frontier stays below `cap`
 // vertices; info[0] <- last superstep executed (host-mapped).
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,

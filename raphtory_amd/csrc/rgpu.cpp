@@ -42,7 +42,7 @@ struct HipFail {
   } while (0)
 
 enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUMMARY = 4,
-                KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_N = 8 };
+                KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_HEAVY = 8, KID_N = 12 };
 
 constexpr int kMaxSteps = 128;
 constexpr int kStatWords = 7 * kViews;  // 6 per-view fields + counters row
@@ -74,6 +74,7 @@ struct Slot {
   int32_t* h_tail = nullptr;      // host-mapped: [0] last superstep a k_cc_tail launch executed
   int32_t* d_tail = nullptr;
   unsigned int* iso = nullptr;    // isolated-member counts [64 shards][64 views] (k_cc_hist)
+  HeavyBuf hv;                    // heavy-vertex segment state (graphs with hubs)
   unsigned long long* h_stats = nullptr;
   // state of the batch in flight
   int batch = -1, phase = 0, r_launched = 0, r_final = 0, kb = 0;
@@ -152,6 +153,7 @@ struct rgpu_ctx {
   bool poll = true;                     // RGPU_POLL: spin on event queries instead of blocking
   bool hostprof = false;                // RGPU_HOSTPROF: print host-side scheduling times
   int iv_max = 32;                      // RGPU_IVMAX: K1 interval form up to this many points (< 0 off)
+  int heavy_t = 2048;                   // RGPU_HEAVY: static slots above which a vertex is split (0 off)
   MaskSet mset[kMaskSets];
   int grp_last[kMaxPlanes] = {};        // supersteps of the last batch of each window group
   // last run: views (hop, win) -> batch (hop/K)*G + win/gsize, lane (win%gsize)*K + hop%K
@@ -306,6 +308,12 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       s.work = dalloc<unsigned long long>(L, kWorkWords);
       s.iso = dalloc<unsigned int>(L, kIsoWords);  // zero between batches: the summary kernel clears it
       HIPCHK(hipMemset(s.iso, 0, sizeof(unsigned int) * kIsoWords));
+      if (c->g.n_seg > 0) {
+        s.hv.segcnt = dalloc<int32_t>(L, c->g.n_seg);
+        s.hv.segor = dalloc<uint64_t>(L, c->g.n_seg);
+        s.hv.best = dalloc<int32_t>(L, (size_t)c->g.n_heavy * kViews);  // INT32_MAX between uses
+        HIPCHK(hipMemsetD32((hipDeviceptr_t)s.hv.best, INT32_MAX, (size_t)c->g.n_heavy * kViews));
+      }
     }
     if ((algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) && !c->slot_deg) {
       s.outdeg = dalloc<int32_t>(L, rows);
@@ -378,20 +386,32 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     eb = take_event(c);
     HIPCHK(hipEventRecord(ea, s.stream));
   }
+  const bool hv = g.n_seg > 0;
   for (int r = s.r_launched + 1; r <= last; r++) {
+    if (hv)  // heavy vertices: segment minima before the step, neighbour marking after it
+      timed_launch(c, si, KID_HEAVY, 0.0, [&] {
+        launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[(r - 1) & 1], s.chg[(r - 1) & 1], s.act[r % 3],
+                            s.stepcnt, r, s.hv);
+      }, r, false);
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                      s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
                      s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
-                     c->profile ? s.work : nullptr, c->step_variant | (g_rowbuf ? 16 : 0));
+                     c->profile ? s.work : nullptr, c->step_variant | (g_rowbuf ? 16 : 0),
+                     hv ? s.hv.best : nullptr);
     }, r, false);
+    if (hv)
+      timed_launch(c, si, KID_HEAVY, 0.0, [&] {
+        launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[r & 1], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
+                          s.act[r % 3]);
+      }, r, false);
   }
   if (ea) {
     HIPCHK(hipEventRecord(eb, s.stream));
     c->timed.push_back({KID_STEP, si, s.batch, s.r_launched + 1, ea, eb, 0.0});
   }
   s.r_launched = last;
-  if (c->tail_on && g.nv <= c->tail_maxv && s.r_launched < rc.max_steps) {
+  if (c->tail_on && g.n_seg == 0 && g.nv <= c->tail_maxv && s.r_launched < rc.max_steps) {
     // the rest of the supersteps in one workgroup while the frontier stays narrow; it stops
     // (and the host continues with full-grid launches) at the first wide frontier
     const int r0 = s.r_launched + 1;
@@ -534,11 +554,17 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
     const double b2 = g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0;
+    if (g.n_seg > 0)
+      timed_launch(c, si, KID_HEAVY, 0.0, [&] { launch_heavy_slots(s.stream, g, s.vm, s.em, s.snbr, s.smask, s.hv); });
     timed_launch(c, si, KID_SLOTS, b2, [&] {
       launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
-                      c->profile ? s.work : nullptr);
+                      c->profile ? s.work : nullptr, s.hv);
     });
+    if (g.n_seg > 0)
+      timed_launch(c, si, KID_HEAVY, 0.0, [&] {
+        launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[1], s.act[2], s.stepcnt, 1, s.hv, nullptr);
+      });
     s.r_launched = 1;  // superstep 1 ran inside the slot kernel
     if (rc.max_steps <= 1) {  // AnalysisTask.timeResponse :169: no Setup when maxSteps <= 1
       s.r_final = 0;
@@ -833,7 +859,7 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
     if (rc.algo == RGPU_ALGO_CC) {
       timed_launch(c, 0, KID_SLOTS, g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0, [&] {
         launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
-                        s.chg[1], s.act[2], s.stepcnt, nullptr, nullptr);
+                        s.chg[1], s.act[2], s.stepcnt, nullptr, nullptr, HeavyBuf());
       });
       s.r_final = 0;
       if (rc.max_steps > 1) {
@@ -940,6 +966,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->poll = env_int("RGPU_POLL", 1) != 0;
   c->hostprof = env_int("RGPU_HOSTPROF", 0) != 0;
   c->iv_max = env_int("RGPU_IVMAX", 32);
+  c->heavy_t = env_int("RGPU_HEAVY", 2048);
   c->tail_cap = std::max(1, env_int("RGPU_TAIL_CAP", 256));
   c->tail_maxv = std::max(0, env_int("RGPU_TAIL_MAXV", 4 << 20));
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
@@ -1000,6 +1027,35 @@ int rgpu_seal(rgpu_ctx* c) {
     }
     g.in_eid = dupload(L, P.in_eid);
     g.n_own = P.n_own;
+    if (!c->partitioned && c->heavy_t > 0) {
+      // heavy vertices (power-law hubs): static slot lists cut into kSegSlots segments
+      std::vector<int32_t> hv_of(P.nv, -1), hv_seg(1, 0), seg_v, seg_h, seg_n;
+      std::vector<int64_t> seg_lo;
+      for (int64_t v = 0; v < P.nv; v++) {
+        const int64_t deg = (P.out_off[v + 1] - P.out_off[v]) + (P.in_off[v + 1] - P.in_off[v]);
+        if (deg <= c->heavy_t) continue;
+        const int32_t h = (int32_t)(hv_seg.size() - 1);
+        hv_of[v] = h;
+        const int64_t a0 = P.out_off[v] + P.in_off[v];
+        for (int64_t o = 0; o < deg; o += kSegSlots) {
+          seg_v.push_back((int32_t)v);
+          seg_h.push_back(h);
+          seg_lo.push_back(a0 + o);
+          seg_n.push_back((int32_t)std::min<int64_t>(kSegSlots, deg - o));
+        }
+        hv_seg.push_back((int32_t)seg_v.size());
+      }
+      if (!seg_v.empty()) {
+        g.n_heavy = (int64_t)hv_seg.size() - 1;
+        g.n_seg = (int64_t)seg_v.size();
+        g.hv_of = dupload(L, hv_of);
+        g.hv_seg = dupload(L, hv_seg);
+        g.seg_v = dupload(L, seg_v);
+        g.seg_h = dupload(L, seg_h);
+        g.seg_lo = dupload(L, seg_lo);
+        g.seg_n = dupload(L, seg_n);
+      }
+    }
     if (c->partitioned) {
       if (c->nparts > 1) g.grank = dupload(L, P.grank);
       Part& X = c->pt;
