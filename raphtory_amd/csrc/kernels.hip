@@ -1226,6 +1226,24 @@ __global__ __launch_bounds__(256) void k_cc_summary(int64_t nv, int32_t* __restr
 // incomingEdges, EntityStorage.scala:257), edges filtered by their own history only
 // (Vertex.viewAtWithWindow).  Per-vertex rows are written to outdeg/indeg; per-view
 // totals (V, sum out, sum in) into stats[f*64 + view].
+// 64x64 bit-matrix transpose across the wave: lane r holds row r (bit c = column c) and gets
+// column r back (bit s = row s).  Six butterfly levels of 64-bit shuffles.
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int d) {
+  const uint32_t lo = __shfl_xor((uint32_t)x, d), hi = __shfl_xor((uint32_t)(x >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane) {
+  const uint64_t M[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                         0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const int d = 32 >> k;
+    const uint64_t y = shfl_xor64(x, d);
+    x = (lane & d) ? ((x & ~M[k]) | ((y & ~M[k]) >> d)) : ((x & M[k]) | ((y & M[k]) << d));
+  }
+  return x;
+}
+
 __global__ __launch_bounds__(256) void k_degree(int64_t nv, const int64_t* __restrict__ out_off,
                                                 const int64_t* __restrict__ in_off,
                                                 const int32_t* __restrict__ in_eid,
@@ -1233,12 +1251,12 @@ __global__ __launch_bounds__(256) void k_degree(int64_t nv, const int64_t* __res
                                                 const uint64_t* __restrict__ em,
                                                 int32_t* __restrict__ outdeg,
                                                 int32_t* __restrict__ indeg,
-                                                unsigned long long* __restrict__ stats) {
-  __shared__ uint64_t tile[4][64];
+                                                unsigned long long* __restrict__ stats,
+                                                const int32_t* __restrict__ hv_of) {
   __shared__ unsigned long long red[3][64];
   for (int i = threadIdx.x; i < 3 * 64; i += blockDim.x) (&red[0][0])[i] = 0;
   __syncthreads();
-  const int lane = lane_id(), wib = threadIdx.x >> 6;
+  const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   unsigned long long tv = 0, to = 0, ti = 0;
@@ -1247,18 +1265,15 @@ __global__ __launch_bounds__(256) void k_degree(int64_t nv, const int64_t* __res
     int32_t od = 0, id = 0;
     if (mv) {
       const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
-      for (int dir = 0; dir < 2; dir++) {
+      const bool heavy = hv_of && hv_of[v] >= 0;  // counted by k_heavy_degree (rows start at 0)
+      for (int dir = 0; dir < 2 && !heavy; dir++) {
         const int64_t n = dir ? i1 - i0 : o1 - o0;
         int32_t acc = 0;
-        for (int64_t c = 0; c < n; c += 64) {
+        for (int64_t c = 0; c < n; c += 64) {  // lane = edge -> transpose -> lane = view
           const int64_t j = c + lane;
           uint64_t m = 0;
           if (j < n) m = em[dir ? in_eid[i0 + j] : o0 + j];
-          tile[wib][lane] = m;  // transpose through LDS: lane = view
-          __builtin_amdgcn_wave_barrier();
-          const int lim = (int)(n - c < 64 ? n - c : 64);
-          for (int q = 0; q < lim; q++) acc += (int32_t)((tile[wib][q] >> lane) & 1);
-          __builtin_amdgcn_wave_barrier();
+          acc += __popcll(transpose64(m, lane));
         }
         if (dir) id = acc; else od = acc;
       }
@@ -1281,6 +1296,114 @@ __global__ __launch_bounds__(256) void k_degree(int64_t nv, const int64_t* __res
       if (red[f][threadIdx.x]) atomicAdd(&stats[f * 64 + threadIdx.x], red[f][threadIdx.x]);
 }
 
+// Degree of heavy vertices: per segment, alive out- / in-slots counted per view (lane = slot ->
+// bit transpose -> lane = view), added to the hub's rows and the view totals.
+__global__ __launch_bounds__(256) void k_heavy_degree(int64_t nseg, const int32_t* __restrict__ seg_v,
+                                                      const int64_t* __restrict__ seg_lo,
+                                                      const int32_t* __restrict__ seg_n,
+                                                      const int64_t* __restrict__ out_off,
+                                                      const int64_t* __restrict__ in_off,
+                                                      const int64_t* __restrict__ adj_off,
+                                                      const int32_t* __restrict__ in_eid,
+                                                      const uint64_t* __restrict__ vm,
+                                                      const uint64_t* __restrict__ em,
+                                                      int32_t* __restrict__ outdeg, int32_t* __restrict__ indeg,
+                                                      unsigned long long* __restrict__ stats) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t sg = wave; sg < nseg; sg += nwaves) {
+    const int32_t v = seg_v[sg];
+    const uint64_t mv = vm[v];
+    if (mv == 0) continue;
+    const int64_t rel0 = seg_lo[sg] - adj_off[v], o0 = out_off[v], i0 = in_off[v];
+    const int64_t nout = out_off[v + 1] - o0;
+    const int32_t ns = seg_n[sg];
+    int32_t co = 0, ci = 0;
+    for (int32_t c = 0; c < ns; c += 64) {
+      const int32_t jj = c + lane;
+      uint64_t mo = 0, mi = 0;
+      if (jj < ns) {
+        const int64_t rel = rel0 + jj;
+        if (rel < nout) mo = em[o0 + rel];
+        else mi = em[in_eid[i0 + (rel - nout)]];
+      }
+      co += __popcll(transpose64(mo, lane));
+      ci += __popcll(transpose64(mi, lane));
+    }
+    const bool in_view = (mv >> lane) & 1;
+    if (in_view && co) {
+      atomicAdd(&outdeg[(int64_t)v * 64 + lane], co);
+      atomicAdd(&stats[1 * 64 + lane], (unsigned long long)co);
+    }
+    if (in_view && ci) {
+      atomicAdd(&indeg[(int64_t)v * 64 + lane], ci);
+      atomicAdd(&stats[2 * 64 + lane], (unsigned long long)ci);
+    }
+  }
+}
+
+// PageRank pull for heavy vertices: per segment, the alive in-slots' contributions (views in
+// em[e] & vm[src] & vm[v]) summed per view, four neighbour rows in flight, then added to the
+// hub's fp64 accumulator row (k_pr_step adds it and resets it).  fp64 atomics make the sum
+// order vary between runs: within the spec's L1 <= 1e-6 (App. A.5), not bit-stable.
+__global__ __launch_bounds__(256) void k_heavy_pr(int64_t nseg, const int32_t* __restrict__ seg_v,
+                                                  const int32_t* __restrict__ seg_h,
+                                                  const int64_t* __restrict__ seg_lo,
+                                                  const int32_t* __restrict__ seg_n,
+                                                  const int64_t* __restrict__ out_off,
+                                                  const int64_t* __restrict__ in_off,
+                                                  const int64_t* __restrict__ adj_off,
+                                                  const int32_t* __restrict__ in_eid,
+                                                  const int32_t* __restrict__ esrc,
+                                                  const uint64_t* __restrict__ vm,
+                                                  const uint64_t* __restrict__ em,
+                                                  const double* __restrict__ contrib_cur,
+                                                  double* __restrict__ hacc) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t sg = wave; sg < nseg; sg += nwaves) {
+    const int32_t v = seg_v[sg];
+    const uint64_t mv = vm[v];
+    if (mv == 0) continue;
+    const int64_t rel0 = seg_lo[sg] - adj_off[v], i0 = in_off[v];
+    const int64_t nout = out_off[v + 1] - out_off[v];
+    const int32_t ns = seg_n[sg];
+    if (rel0 + ns <= nout) continue;  // out-slots only
+    double acc = 0.0;
+    for (int32_t c = 0; c < ns; c += 64) {
+      const int64_t rel = rel0 + c + lane;
+      uint64_t m = 0;
+      int32_t nb = 0;
+      if (c + lane < ns && rel >= nout) {
+        const int32_t e = in_eid[i0 + (rel - nout)];
+        nb = esrc[e];
+        m = em[e] & vm[nb] & mv;
+      }
+      uint64_t bal = __ballot(m != 0);
+      while (bal) {
+        int L[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          L[u] = bal ? __builtin_ctzll(bal) : -1;
+          if (bal) bal &= bal - 1;
+        }
+        double x[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int Lu = L[u] < 0 ? L[0] : L[u];
+          const int32_t q = __builtin_amdgcn_readlane(nb, Lu);
+          const bool on = L[u] >= 0 && ((readlane64(m, Lu) >> lane) & 1);
+          x[u] = on ? contrib_cur[(int64_t)q * 64 + lane] : 0.0;
+        }
+        acc += (x[0] + x[1]) + (x[2] + x[3]);
+      }
+    }
+    if (acc != 0.0) atomicAdd(&hacc[(int64_t)seg_h[sg] * 64 + lane], acc);
+  }
+}
+
 // ---------------------------------------------------------------- PageRank (App. A.5)
 // Pull slots of rank v = its in-edges plus its self-loop (messageAllOutgoingNeighbors
 // reaches the vertex itself); kept iff em[e] & vm[src] & vm[v] != 0.  Static capacity
@@ -1296,7 +1419,8 @@ __global__ __launch_bounds__(256) void k_pr_slots(int64_t nv, const int64_t* __r
                                                   int32_t* __restrict__ cnt, int32_t* __restrict__ snbr,
                                                   uint64_t* __restrict__ smask,
                                                   double* __restrict__ pr,
-                                                  double* __restrict__ contrib) {
+                                                  double* __restrict__ contrib,
+                                                  const int32_t* __restrict__ hv_of) {
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -1309,7 +1433,9 @@ __global__ __launch_bounds__(256) void k_pr_slots(int64_t nv, const int64_t* __r
       if (lane == 0) cnt[v] = 0;
       continue;
     }
-    const int64_t i0 = in_off[v], i1 = in_off[v + 1], nin = i1 - i0, base = i0 + v;
+    const int64_t i0 = in_off[v], i1 = in_off[v + 1], base = i0 + v;
+    // a heavy vertex's in-slots are pulled per segment by k_heavy_pr: only its self-loop here
+    const int64_t nin = (hv_of && hv_of[v] >= 0) ? 0 : i1 - i0;
     int32_t count = 0;
     for (int64_t c = 0; c < nin; c += 64) {
       const int64_t j = c + lane;
@@ -1356,7 +1482,9 @@ __global__ __launch_bounds__(256) void k_pr_step(int64_t nv, const int64_t* __re
                                                  const uint64_t* __restrict__ smask,
                                                  const double* __restrict__ contrib_cur,
                                                  double* __restrict__ contrib_next,
-                                                 double* __restrict__ pr) {
+                                                 double* __restrict__ pr,
+                                                 const int32_t* __restrict__ hv_of,
+                                                 double* __restrict__ hacc) {
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -1372,12 +1500,29 @@ __global__ __launch_bounds__(256) void k_pr_step(int64_t nv, const int64_t* __re
       int32_t nb = 0;
       if (j < n) { nb = snbr[base + j]; m = smask[base + j]; }
       uint64_t bal = __ballot(m != 0);
-      while (bal) {
-        const int L = __builtin_ctzll(bal);
-        bal &= bal - 1;
-        const int32_t nbL = __builtin_amdgcn_readlane(nb, L);
-        const uint64_t mL = readlane64(m, L);
-        if ((mL >> lane) & 1) acc += contrib_cur[(int64_t)nbL * 64 + lane];
+      while (bal) {  // four neighbour rows in flight
+        int L[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          L[u] = bal ? __builtin_ctzll(bal) : -1;
+          if (bal) bal &= bal - 1;
+        }
+        double x[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int Lu = L[u] < 0 ? L[0] : L[u];
+          const int32_t q = __builtin_amdgcn_readlane(nb, Lu);
+          const bool on = L[u] >= 0 && ((readlane64(m, Lu) >> lane) & 1);
+          x[u] = on ? contrib_cur[(int64_t)q * 64 + lane] : 0.0;
+        }
+        acc += (x[0] + x[1]) + (x[2] + x[3]);
+      }
+    }
+    if (hv_of) {
+      const int32_t h = hv_of[v];
+      if (h >= 0) {
+        acc += hacc[(int64_t)h * 64 + lane];
+        hacc[(int64_t)h * 64 + lane] = 0.0;
       }
     }
     if ((mv >> lane) & 1) {
@@ -1660,20 +1805,30 @@ void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hi
 }
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                    int32_t* outdeg, int32_t* indeg, unsigned long long* stats) {
-  k_degree<<<grid_for(g.nv, 4, 256), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, vm, em,
-                                                    outdeg, indeg, stats);
+  k_degree<<<grid_for(g.nv, 4, 2048), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, vm, em,
+                                                     outdeg, indeg, stats, g.n_seg > 0 ? g.hv_of : nullptr);
+  if (g.n_seg > 0)
+    k_heavy_degree<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_lo, g.seg_n, g.out_off,
+                                                               g.in_off, g.adj_off, g.in_eid, vm, em, outdeg, indeg,
+                                                               stats);
 }
 void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      const int32_t* outdeg, int32_t* cnt, int32_t* snbr, uint64_t* smask,
                      double* pr, double* contrib) {
   k_pr_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
-                                                vm, em, outdeg, cnt, snbr, smask, pr, contrib);
+                                                vm, em, outdeg, cnt, snbr, smask, pr, contrib,
+                                                g.n_seg > 0 ? g.hv_of : nullptr);
 }
-void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const int32_t* outdeg,
-                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
-                    const double* contrib_cur, double* contrib_next, double* pr) {
+void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+                    const int32_t* outdeg, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
+                    const double* contrib_cur, double* contrib_next, double* pr, double* hacc) {
+  if (g.n_seg > 0 && hacc)
+    k_heavy_pr<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off,
+                                                           g.in_off, g.adj_off, g.in_eid, g.esrc, vm, em, contrib_cur,
+                                                           hacc);
   k_pr_step<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.in_off, vm, outdeg, cnt, snbr, smask,
-                                               contrib_cur, contrib_next, pr);
+                                               contrib_cur, contrib_next, pr,
+                                               g.n_seg > 0 && hacc ? g.hv_of : nullptr, hacc);
 }
 
 void launch_xpack_cc(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,

@@ -49,6 +49,7 @@ struct HeavyBuf {
   int32_t* segcnt = nullptr;   // [n_seg] kept slots of the segment (compacted at seg_lo)
   uint64_t* segor = nullptr;   // [n_seg] OR of the segment's kept slot masks
   int32_t* best = nullptr;     // [n_heavy][64] partial minima of the step (INT32_MAX when idle)
+  double* pacc = nullptr;      // [n_heavy][64] PageRank pull accumulators (0 when idle)
 };
 
 // Small per-batch state cleared by the first kernel of the batch (no memset launches).
@@ -109,9 +110,10 @@ void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const u
 void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      const int32_t* outdeg, int32_t* cnt, int32_t* snbr, uint64_t* smask,
                      double* pr, double* contrib);
-void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const int32_t* outdeg,
-                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
-                    const double* contrib_cur, double* contrib_next, double* pr);
+// hacc: [n_heavy][64] fp64 accumulators of the heavy vertices (zero between uses), or null
+void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+                    const int32_t* outdeg, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
+                    const double* contrib_cur, double* contrib_next, double* pr, double* hacc);
 
 // partition exchange (vertex-partitioned mode)
 constexpr int kXRecWords = 68;  // ints per boundary-row record

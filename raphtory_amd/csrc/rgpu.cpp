@@ -320,6 +320,10 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       s.indeg = dalloc<int32_t>(L, rows);
     }
     if (algo == RGPU_ALGO_PR && !c->slot_pr) {
+      if (c->g.n_seg > 0) {
+        s.hv.pacc = dalloc<double>(L, (size_t)c->g.n_heavy * kViews);  // zero between uses
+        HIPCHK(hipMemset(s.hv.pacc, 0, sizeof(double) * (size_t)c->g.n_heavy * kViews));
+      }
       s.pr = dalloc<double>(L, rows);
       s.contrib[0] = dalloc<double>(L, rows);
       s.contrib[1] = dalloc<double>(L, rows);
@@ -585,8 +589,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       for (int it = 0; it < rc.pr_iters; it++) {
         const double bp_bytes = g.nv * (8.0 + 16.0 + 4.0 + 256.0 + 1024.0) + (double)(g.n_in + g.nv) * 12.0;
         timed_launch(c, si, KID_PR, bp_bytes, [&] {
-          launch_pr_step(s.stream, g, s.vm, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.contrib[it & 1],
-                         s.contrib[(it + 1) & 1], s.pr);
+          launch_pr_step(s.stream, g, s.vm, s.em, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.contrib[it & 1],
+                         s.contrib[(it + 1) & 1], s.pr, s.hv.pacc);
         });
       }
     }
@@ -889,8 +893,8 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
         pr_exchange(c, s.contrib[0]);
         for (int it = 0; it < rc.pr_iters; it++) {
           timed_launch(c, 0, KID_PR, go.nv * (8.0 + 16.0 + 4.0 + 256.0 + 1024.0) + (double)(g.n_in + go.nv) * 12.0, [&] {
-            launch_pr_step(s.stream, go, s.vm, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.contrib[it & 1],
-                           s.contrib[(it + 1) & 1], s.pr);
+            launch_pr_step(s.stream, go, s.vm, s.em, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.contrib[it & 1],
+                           s.contrib[(it + 1) & 1], s.pr, nullptr);
           });
           if (it + 1 < rc.pr_iters) pr_exchange(c, s.contrib[(it + 1) & 1]);
         }

@@ -95,3 +95,34 @@ def test_heavy_split_matches_undivided_on_gab_range():
     for summ, labs in out[1:]:
         assert np.array_equal(summ, out[0][0])
         assert all(np.array_equal(a, b) for a, b in zip(labs, out[0][1]))
+
+
+PR_L1_TOL = 1e-6
+
+
+@pytest.mark.parametrize("heavy", ["0", "8", "300"])
+def test_hubs_degree_and_pagerank_vs_oracle(heavy):
+    """DegreeBasic per-vertex degrees (DegreeBasic.scala:16-28) exact, PageRank (App. A.5) within
+    L1 <= 1e-6, with the hubs' slots counted / pulled per segment (k_heavy_degree, k_heavy_pr)."""
+    st = hubs_stream(seed=5)
+    o = Oracle.from_stream(st)
+    g = graph_env(st, {"RGPU_HEAVY": heavy})
+    hops = range_hops(T0_README + 5 * DAY, T0_README + 70 * DAY, 5 * DAY)
+    wins = [MONTH, WEEK, DAY]
+    g.run("degree", hops, wins, retain=True)
+    for h, t in enumerate(hops.tolist()):
+        res = o.degree(t, wins)
+        for w in range(3):
+            ids, od, idg = res[w]
+            gids, god, gid = g.degree_vertex(h, w)
+            assert np.array_equal(gids, ids) and np.array_equal(god, od) and np.array_equal(gid, idg), (heavy, t, w)
+            assert g.degree_result(h, w)[:3] == (len(ids), int(od.sum()), int(idg.sum()))
+    g.run("pagerank", hops[::3], wins, pr_iters=20, retain=True)
+    for h, t in enumerate(hops[::3].tolist()):
+        res = o.pagerank(t, wins, iters=20)
+        for w in range(3):
+            ids, pr = res[w]
+            gids, gpr = g.pr_result(h, w)
+            assert np.array_equal(gids, ids)
+            assert np.abs(gpr - pr).sum() <= PR_L1_TOL, (heavy, t, w, np.abs(gpr - pr).sum())
+    g.close()
