@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RGPU_ABI_VERSION 2
+#define RGPU_ABI_VERSION 3
 
 /* error codes */
 #define RGPU_OK 0
@@ -79,6 +79,10 @@ typedef struct {
   int64_t kernel_launches[12];
   double kernel_ms[12];
   double kernel_bytes[12];       /* algorithmic bytes summed over launches */
+  /* last rgpu_seal: wall ms, 1 if it merged a delta into the resident graph (live ingest),
+   * and the number of updates that delta held (ABI 3) */
+  double seal_ms;
+  int64_t seal_incremental, seal_delta_updates;
 } rgpu_stats_t;
 
 int rgpu_abi_version(void);
@@ -91,7 +95,11 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out);
 int rgpu_ingest(rgpu_ctx* ctx, const int64_t* t, const uint8_t* kind, const int64_t* src,
                 const int64_t* dst, size_t n);
 
-/* Sort + merge + pack the ingested stream into SoA histories and copy them to HBM. */
+/* Sort + merge + pack the ingested stream into SoA histories and copy them to HBM.
+ * Live ingest (IngestionWorker.scala:31-256 keeps appending while LiveAnalysisTask.scala:13-107
+ * re-runs): after the first seal, rgpu_ingest + rgpu_seal again merges only the new updates
+ * into the HBM-resident graph (merge.hip; one partition, RGPU_DELTA=0 forces a full re-pack).
+ * The new updates count as later in stream order than every sealed one. */
 int rgpu_seal(rgpu_ctx* ctx);
 
 /* Newest ingested time: the watermark ReaderWorker.processTimeCheckRequest compares

@@ -129,4 +129,36 @@ void launch_add_i32(hipStream_t s, int32_t* dst, const int32_t* src, int64_t n);
 void launch_cc_summary_rs(hipStream_t s, int nviews, const int32_t* chunk, int64_t x0, int64_t len,
                           int64_t ng, unsigned long long* stats, unsigned int* iso);
 
+// incremental seal (merge.hip): a sealed base graph and a host-packed delta (rgpu_internal.hpp
+// Delta), all device pointers
+struct MergeIn {
+  int64_t nv_old = 0, nv2 = 0, ne_old = 0, nin_old = 0;
+  const int32_t *esrc = nullptr, *edst = nullptr, *in_eid = nullptr;  // base
+  const int64_t *eoff = nullptr, *ekey = nullptr, *voff = nullptr, *vkey = nullptr, *in_off = nullptr;
+  const int32_t *old2new = nullptr, *new2old = nullptr;
+  int64_t n_new = 0, nde = 0, ndd = 0, ndv = 0, nni = 0;
+  const int64_t* nn_key = nullptr;
+  const int32_t *nn_didx = nullptr, *de_base = nullptr;
+  const int64_t *dkoff = nullptr, *dkey = nullptr;
+  const int32_t* dd_rank = nullptr;
+  const int64_t *dd_off = nullptr, *dd_t = nullptr;
+  const int32_t* dv_rank = nullptr;
+  const int64_t *dv_off = nullptr, *dv_key = nullptr;
+  const int64_t* ni_key = nullptr;
+  const int32_t* ni_idx = nullptr;
+};
+void launch_edge_find(hipStream_t s, int64_t nq, const int32_t* qs, const int32_t* qd, const int64_t* out_off,
+                      const int32_t* edst, int32_t* res);
+void launch_merge_edges(hipStream_t s, const MergeIn& m, int32_t* esrc2, int32_t* edst2, int32_t* eo2n,
+                        int32_t* mbase, int32_t* mdlt, int32_t* npos);
+// off[0, n) counts -> off[0, n] exclusive offsets; tmp: scan_tmp_words(n) int64 words
+void launch_scan_counts(hipStream_t s, int64_t n, int64_t* off, int64_t* tmp);
+int64_t scan_tmp_words(int64_t n);
+void launch_edge_hist(hipStream_t s, bool write, const MergeIn& m, int64_t ne2, const int32_t* mbase,
+                      const int32_t* mdlt, const int32_t* esrc2, const int32_t* edst2, int64_t* cnt_off,
+                      int64_t* ekey2);
+void launch_vertex_hist(hipStream_t s, bool write, const MergeIn& m, int64_t* cnt_off, int64_t* vkey2);
+void launch_merge_in(hipStream_t s, const MergeIn& m, const int32_t* eo2n, const int32_t* npos,
+                     const int64_t* in_off2, int32_t* in_eid2);
+
 }  // namespace rgpu

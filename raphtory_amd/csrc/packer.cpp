@@ -415,7 +415,246 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
     P.xs_off[q + 1] = (int64_t)P.xs_v.size();
     P.xr_off[q + 1] = (int64_t)P.xr_v.size();
   }
+  P.n_vkey = (int64_t)P.vkey.size();
+  P.n_ekey = (int64_t)P.ekey.size();
+  P.n_in = P.in_off[P.nv];
   return "";
+}
+
+// ---------------------------------------------------------------------------------------
+// Incremental seal, host half (rgpu_internal.hpp: Delta).  Delta indices are 1-based so
+// that 0 can stand for "somewhere in the base": every base put precedes every delta put.
+std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed& B, Delta* out) {
+  const int nt = num_threads();
+  const size_t n = ev.size() - first;
+  const int64_t kMaxT = (int64_t)1 << 61;
+  for (size_t i = first; i < ev.size(); i++) {
+    const Event& e = ev[i];
+    if (e.kind > RGPU_EDEL) return "unknown update kind";
+    if (e.t < 0 || e.t >= kMaxT) return "time out of range [0, 2^61)";
+    if (e.src < 0 || e.src > INT32_MAX) return "vertex id out of range [0, 2^31)";
+    if (e.kind >= RGPU_EADD && (e.dst < 0 || e.dst > INT32_MAX)) return "vertex id out of range [0, 2^31)";
+  }
+  Delta& D = *out;
+  D = Delta();
+  D.nd = (int64_t)n;
+  D.nv_old = B.nv;
+  // ---- ids: new ids merged into the base order; both rank maps are monotone
+  std::vector<int64_t> ids;
+  ids.reserve(2 * n);
+  for (size_t i = first; i < ev.size(); i++) {
+    ids.push_back(ev[i].src);
+    if (ev[i].kind >= RGPU_EADD) ids.push_back(ev[i].dst);
+  }
+  parallel_sort(ids, nt, std::less<int64_t>());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  std::vector<int64_t> nid;
+  for (int64_t x : ids)
+    if (!std::binary_search(B.vid.begin(), B.vid.end(), x)) nid.push_back(x);
+  D.nv = B.nv + (int64_t)nid.size();
+  D.vid.resize(D.nv);
+  D.old2new.resize(B.nv);
+  D.new2old.assign(D.nv, -1);
+  {
+    int64_t a = 0, b = 0, r = 0;
+    while (a < B.nv || b < (int64_t)nid.size()) {
+      if (b == (int64_t)nid.size() || (a < B.nv && B.vid[a] < nid[b])) {
+        D.vid[r] = B.vid[a];
+        D.old2new[a] = (int32_t)r;
+        D.new2old[r] = (int32_t)a;
+        a++;
+      } else {
+        D.vid[r] = nid[b++];
+      }
+      r++;
+    }
+  }
+  std::vector<int32_t> rs(n), rd(n, -1);
+  parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; i++) {
+      const Event& e = ev[first + i];
+      rs[i] = (int32_t)(std::lower_bound(D.vid.begin(), D.vid.end(), e.src) - D.vid.begin());
+      if (e.kind >= RGPU_EADD) rd[i] = (int32_t)(std::lower_bound(D.vid.begin(), D.vid.end(), e.dst) - D.vid.begin());
+    }
+  });
+  // ---- vertex points (same records as pack_events), collapsed per (rank, t): last put wins
+  {
+    struct R { int32_t v; uint8_t f; int64_t t, idx; };
+    std::vector<R> r;
+    r.reserve(2 * n);
+    for (size_t i = 0; i < n; i++) {
+      const Event& e = ev[first + i];
+      if (e.kind != RGPU_EDEL) r.push_back({rs[i], (uint8_t)(e.kind == RGPU_VDEL ? 0 : 1), e.t, (int64_t)i + 1});
+      if (e.kind == RGPU_EADD && rd[i] != rs[i]) r.push_back({rd[i], 1, e.t, (int64_t)i + 1});
+    }
+    parallel_sort(r, nt, [](const R& a, const R& b) {
+      if (a.v != b.v) return a.v < b.v;
+      return a.t != b.t ? a.t < b.t : a.idx < b.idx;
+    });
+    D.dv_off.push_back(0);
+    for (size_t k = 0; k < r.size(); k++) {
+      if (k + 1 < r.size() && r[k + 1].v == r[k].v && r[k + 1].t == r[k].t) continue;
+      if (D.dv_rank.empty() || D.dv_rank.back() != r[k].v) {
+        if (!D.dv_rank.empty()) D.dv_off.push_back((int64_t)D.dv_key.size());
+        D.dv_rank.push_back(r[k].v);
+      }
+      D.dv_key.push_back(r[k].t * 2 + r[k].f);
+    }
+    if (!D.dv_rank.empty()) D.dv_off.push_back((int64_t)D.dv_key.size());
+  }
+  // ---- delta deaths: distinct times per rank with the last delta index at each time
+  {
+    struct R { int32_t v; int64_t t, idx; };
+    std::vector<R> r;
+    for (size_t i = 0; i < n; i++)
+      if (ev[first + i].kind == RGPU_VDEL) r.push_back({rs[i], ev[first + i].t, (int64_t)i + 1});
+    std::sort(r.begin(), r.end(), [](const R& a, const R& b) {
+      if (a.v != b.v) return a.v < b.v;
+      return a.t != b.t ? a.t < b.t : a.idx < b.idx;
+    });
+    D.dd_off.push_back(0);
+    for (size_t k = 0; k < r.size(); k++) {
+      if (k + 1 < r.size() && r[k + 1].v == r[k].v && r[k + 1].t == r[k].t) continue;
+      if (D.dd_rank.empty() || D.dd_rank.back() != r[k].v) {
+        if (!D.dd_rank.empty()) D.dd_off.push_back((int64_t)D.dd_t.size());
+        D.dd_rank.push_back(r[k].v);
+      }
+      D.dd_t.push_back(r[k].t);
+      D.dd_last.push_back(r[k].idx);
+    }
+    if (!D.dd_rank.empty()) D.dd_off.push_back((int64_t)D.dd_t.size());
+  }
+  // ---- delta edge points grouped by (s, d), each edge's points by (t, idx)
+  {
+    struct R { int32_t s, d; uint8_t f; int64_t t, idx; };
+    std::vector<R> r;
+    for (size_t i = 0; i < n; i++) {
+      const Event& e = ev[first + i];
+      if (e.kind >= RGPU_EADD) r.push_back({rs[i], rd[i], (uint8_t)(e.kind == RGPU_EADD ? 1 : 0), e.t, (int64_t)i + 1});
+    }
+    parallel_sort(r, nt, [](const R& a, const R& b) {
+      if (a.s != b.s) return a.s < b.s;
+      if (a.d != b.d) return a.d < b.d;
+      return a.t != b.t ? a.t < b.t : a.idx < b.idx;
+    });
+    D.de_poff.push_back(0);
+    for (size_t k = 0; k < r.size(); k++) {
+      if (k == 0 || r[k].s != r[k - 1].s || r[k].d != r[k - 1].d) {
+        if (k) D.de_poff.push_back((int64_t)k);
+        D.de_s.push_back(r[k].s);
+        D.de_d.push_back(r[k].d);
+        D.de_qs.push_back(D.new2old[r[k].s]);
+        D.de_qd.push_back(D.new2old[r[k].d]);
+      }
+      D.de_pt.push_back(r[k].t);
+      D.de_pidx.push_back(r[k].idx);
+      D.de_pflag.push_back(r[k].f);
+    }
+    if (!r.empty()) D.de_poff.push_back((int64_t)r.size());
+  }
+  return "";
+}
+
+void finish_delta(const Packed& B, const std::vector<int32_t>& base_eid, Delta* out) {
+  Delta& D = *out;
+  const int64_t nde = (int64_t)D.de_s.size();
+  D.de_base = base_eid;
+  // death at exactly t: the last delta index, 0 for a base death, -1 for none
+  auto death_at = [&](int32_t v, int64_t t) -> int64_t {
+    auto it = std::lower_bound(D.dd_rank.begin(), D.dd_rank.end(), v);
+    if (it != D.dd_rank.end() && *it == v) {
+      const size_t j = it - D.dd_rank.begin();
+      auto b = D.dd_t.begin() + D.dd_off[j], e = D.dd_t.begin() + D.dd_off[j + 1];
+      auto f = std::lower_bound(b, e, t);
+      if (f != e && *f == t) return D.dd_last[f - D.dd_t.begin()];
+    }
+    const int32_t u = D.new2old[v];
+    if (u >= 0) {
+      auto b = B.dtime.begin() + B.doff[u], e = B.dtime.begin() + B.doff[u + 1];
+      if (std::binary_search(b, e, t)) return 0;
+    }
+    return -1;
+  };
+  // own points: collapse equal t (last put wins), then the tie with an endpoint death at the
+  // same t exactly as pack_events resolves it (x2 positions; a base edge was created at 0)
+  D.de_koff.assign(nde + 1, 0);
+  for (int64_t i = 0; i < nde; i++) {
+    const int64_t p0 = D.de_poff[i], p1 = D.de_poff[i + 1];
+    int64_t cr = 0;  // creation put: the edge's first delta update (points are in time order)
+    if (base_eid[i] < 0) {
+      cr = D.de_pidx[p0];
+      for (int64_t k = p0; k < p1; k++) cr = std::min(cr, D.de_pidx[k]);
+    }
+    for (int64_t k = p0; k < p1; k++) {
+      if (k + 1 < p1 && D.de_pt[k + 1] == D.de_pt[k]) continue;
+      uint8_t flag = D.de_pflag[k];
+      int64_t pd = death_at(D.de_s[i], D.de_pt[k]);
+      if (D.de_d[i] != D.de_s[i]) pd = std::max(pd, death_at(D.de_d[i], D.de_pt[k]));
+      if (pd >= 0) {
+        const int64_t pd2 = pd < cr ? 2 * cr + 1 : 2 * pd;
+        if (pd2 > 2 * D.de_pidx[k]) flag = 0;
+      }
+      D.de_key.push_back(D.de_pt[k] * 2 + flag);
+    }
+    D.de_koff[i + 1] = (int64_t)D.de_key.size();
+  }
+  // new edges, and their in-edge records (self-loops never enter incomingEdges)
+  std::vector<int64_t> outc(D.nv + 1, 0), inc(D.nv + 1, 0);
+  for (int64_t i = 0; i < nde; i++) {
+    if (base_eid[i] >= 0) continue;
+    const int32_t s = D.de_s[i], d = D.de_d[i];
+    D.nn_key.push_back(((int64_t)s << 32) | d);
+    D.nn_didx.push_back((int32_t)i);
+    outc[s + 1]++;
+    if (s != d) {
+      D.ni_key.push_back(((int64_t)d << 32) | s);
+      D.ni_idx.push_back((int32_t)D.nn_key.size() - 1);
+      inc[d + 1]++;
+    }
+  }
+  {
+    std::vector<size_t> o(D.ni_key.size());
+    for (size_t k = 0; k < o.size(); k++) o[k] = k;
+    std::sort(o.begin(), o.end(), [&](size_t a, size_t b) { return D.ni_key[a] < D.ni_key[b]; });
+    std::vector<int64_t> k2(o.size());
+    std::vector<int32_t> i2(o.size());
+    for (size_t k = 0; k < o.size(); k++) { k2[k] = D.ni_key[o[k]]; i2[k] = D.ni_idx[o[k]]; }
+    D.ni_key.swap(k2);
+    D.ni_idx.swap(i2);
+  }
+  // merged offsets and death lists (O(V) host work)
+  D.out_off.assign(D.nv + 1, 0);
+  D.in_off.assign(D.nv + 1, 0);
+  D.doff.assign(D.nv + 1, 0);
+  D.dtime.clear();
+  D.dtime.reserve(B.dtime.size() + D.dd_t.size());
+  size_t jd = 0;
+  for (int64_t v = 0; v < D.nv; v++) {
+    const int32_t u = D.new2old[v];
+    int64_t oc = outc[v + 1], ic = inc[v + 1];
+    if (u >= 0) {
+      oc += B.out_off[u + 1] - B.out_off[u];
+      ic += B.in_off[u + 1] - B.in_off[u];
+    }
+    D.out_off[v + 1] = D.out_off[v] + oc;
+    D.in_off[v + 1] = D.in_off[v] + ic;
+    const int64_t* b0 = u >= 0 ? B.dtime.data() + B.doff[u] : nullptr;
+    const int64_t* b1 = u >= 0 ? B.dtime.data() + B.doff[u + 1] : nullptr;
+    const int64_t *c0 = nullptr, *c1 = nullptr;
+    if (jd < D.dd_rank.size() && D.dd_rank[jd] == v) {
+      c0 = D.dd_t.data() + D.dd_off[jd];
+      c1 = D.dd_t.data() + D.dd_off[jd + 1];
+      jd++;
+    }
+    while (b0 != b1 || c0 != c1) {  // sorted union of distinct times
+      int64_t t;
+      if (c0 == c1 || (b0 != b1 && *b0 < *c0)) t = *b0++;
+      else if (b0 == b1 || *c0 < *b0) t = *c0++;
+      else { t = *b0++; c0++; }
+      D.dtime.push_back(t);
+    }
+    D.doff[v + 1] = (int64_t)D.dtime.size();
+  }
 }
 
 }  // namespace rgpu

@@ -34,6 +34,7 @@ namespace {
 
 struct HipFail {
   std::string msg;
+  int code = 0;  // 0: RGPU_EHIP
 };
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
@@ -135,6 +136,8 @@ struct rgpu_ctx {
   std::vector<Event> events;
   int64_t newest = -1;
   bool sealed = false;
+  size_t n_sealed = 0;                  // events[0, n_sealed) are in the resident graph
+  bool delta_on = true;                 // RGPU_DELTA: merge later updates into it (else re-pack)
   Packed pk;
   DevGraph g;
   std::vector<void*> graph_allocs;
@@ -529,7 +532,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   if (s.work && c->profile)
     HIPCHK(hipMemsetAsync(s.work, 0, sizeof(unsigned long long) * kWorkWords, s.stream));
   const double bm = bytes_mask(g);
-  const double bv = 8.0 * (g.nv + 1) + 8.0 * c->pk.vkey.size(), be = bm - (16.0 * g.nv + 8.0) - 8.0 * g.ne + 8.0 * c->pk.ekey.size();
+  const double bv = 8.0 * (g.nv + 1) + 8.0 * c->pk.n_vkey, be = bm - (16.0 * g.nv + 8.0) - 8.0 * g.ne + 8.0 * c->pk.n_ekey;
   if (rc.G == 1) {
     s.vm = s.vm_own;
     s.em = s.em_own;
@@ -856,9 +859,9 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
     const DevGraph& g = c->g;
     s.vm = s.vm_own;
     s.em = s.em_own;
-    timed_launch(c, 0, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.vkey.size() + 8.0 * g.nv,
+    timed_launch(c, 0, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.n_vkey + 8.0 * g.nv,
                  [&] { launch_vertex_mask(s.stream, g, bp, s.vm, 0, false, clr); });
-    timed_launch(c, 0, KID_MASK, bytes_mask(g) - (16.0 * g.nv + 8.0) + 8.0 * c->pk.ekey.size(),
+    timed_launch(c, 0, KID_MASK, bytes_mask(g) - (16.0 * g.nv + 8.0) + 8.0 * c->pk.n_ekey,
                  [&] { launch_edge_mask(s.stream, g, bp, s.em, false); });
     if (rc.algo == RGPU_ALGO_CC) {
       timed_launch(c, 0, KID_SLOTS, g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0, [&] {
@@ -973,6 +976,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->heavy_t = env_int("RGPU_HEAVY", 2048);
   c->tail_cap = std::max(1, env_int("RGPU_TAIL_CAP", 256));
   c->tail_maxv = std::max(0, env_int("RGPU_TAIL_MAXV", 4 << 20));
+  c->delta_on = env_int("RGPU_DELTA", 1) != 0;
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
   *out = c;
@@ -999,11 +1003,219 @@ int rgpu_ingest(rgpu_ctx* c, const int64_t* t, const uint8_t* kind, const int64_
   return RGPU_OK;
 }
 
+namespace {
+
+// Heavy vertices (power-law hubs): static slot lists cut into kSegSlots segments.
+void build_heavy(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L, const std::vector<int64_t>& out_off,
+                 const std::vector<int64_t>& in_off) {
+  if (c->partitioned || c->heavy_t <= 0) return;
+  std::vector<int32_t> hv_of(g.nv, -1), hv_seg(1, 0), seg_v, seg_h, seg_n;
+  std::vector<int64_t> seg_lo;
+  for (int64_t v = 0; v < g.nv; v++) {
+    const int64_t deg = (out_off[v + 1] - out_off[v]) + (in_off[v + 1] - in_off[v]);
+    if (deg <= c->heavy_t) continue;
+    const int32_t h = (int32_t)(hv_seg.size() - 1);
+    hv_of[v] = h;
+    const int64_t a0 = out_off[v] + in_off[v];
+    for (int64_t o = 0; o < deg; o += kSegSlots) {
+      seg_v.push_back((int32_t)v);
+      seg_h.push_back(h);
+      seg_lo.push_back(a0 + o);
+      seg_n.push_back((int32_t)std::min<int64_t>(kSegSlots, deg - o));
+    }
+    hv_seg.push_back((int32_t)seg_v.size());
+  }
+  if (seg_v.empty()) return;
+  g.n_heavy = (int64_t)hv_seg.size() - 1;
+  g.n_seg = (int64_t)seg_v.size();
+  g.hv_of = dupload(L, hv_of);
+  g.hv_seg = dupload(L, hv_seg);
+  g.seg_v = dupload(L, seg_v);
+  g.seg_h = dupload(L, seg_h);
+  g.seg_lo = dupload(L, seg_lo);
+  g.seg_n = dupload(L, seg_n);
+}
+
+const int64_t* upload_adj(std::vector<void*>& L, const std::vector<int64_t>& out_off,
+                          const std::vector<int64_t>& in_off) {
+  const int64_t nv = (int64_t)out_off.size() - 1;
+  std::vector<int64_t> adj(nv + 1 + 64);  // padded: read unconditionally by the step kernel
+  for (int64_t v = 0; v <= nv; v++) adj[v] = out_off[v] + in_off[v];
+  for (int64_t v = nv + 1; v < (int64_t)adj.size(); v++) adj[v] = adj[nv];
+  return dupload(L, adj);
+}
+
+void finish_seal(rgpu_ctx* c) {
+  Packed& P = c->pk;
+  c->st.vertices = P.n_own;
+  c->st.edges = P.ne;
+  c->st.vertex_events = P.n_vkey;
+  c->st.edge_events = P.n_ekey;
+  c->st.deaths = (int64_t)P.dtime.size();
+  c->n_sealed = c->events.size();
+  c->sealed = true;
+  if (!c->partitioned) {  // the big arrays live in HBM only (the delta merge keeps them there)
+    for (auto* v : {&P.voff, &P.vkey, &P.eoff, &P.ekey}) std::vector<int64_t>().swap(*v);
+    for (auto* v : {&P.esrc, &P.edst, &P.in_eid}) std::vector<int32_t>().swap(*v);
+  }
+}
+
+// Incremental seal: merge the updates ingested since the last seal into the resident graph
+// (merge.hip).  Host: delta-sized sorts + O(V) offsets; device: every big array.
+void seal_delta(rgpu_ctx* c) {
+  Packed& B = c->pk;
+  Delta D;
+  std::string e = pack_delta(c->events, c->n_sealed, B, &D);
+  if (!e.empty()) throw HipFail{e, RGPU_EINVAL};
+  std::vector<void*> T;  // temporaries
+  std::vector<void*> L;  // the merged graph
+  hipStream_t s = nullptr;
+  try {
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const DevGraph& g0 = c->g;
+    const int64_t nde = (int64_t)D.de_s.size();
+    std::vector<int32_t> base_eid(nde, -1);
+    if (nde) {
+      int32_t* qs = dupload(T, D.de_qs);
+      int32_t* qd = dupload(T, D.de_qd);
+      int32_t* res = dalloc<int32_t>(T, nde);
+      launch_edge_find(s, nde, qs, qd, g0.out_off, g0.edst, res);
+      HIPCHK(hipMemcpyAsync(base_eid.data(), res, sizeof(int32_t) * nde, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    finish_delta(B, base_eid, &D);
+    MergeIn m;
+    m.nv_old = g0.nv;
+    m.nv2 = D.nv;
+    m.ne_old = g0.ne;
+    m.nin_old = g0.n_in;
+    m.esrc = g0.esrc;
+    m.edst = g0.edst;
+    m.in_eid = g0.in_eid;
+    m.eoff = g0.eoff;
+    m.ekey = g0.ekey;
+    m.voff = g0.voff;
+    m.vkey = g0.vkey;
+    m.in_off = g0.in_off;
+    m.old2new = dupload(T, D.old2new);
+    m.new2old = dupload(T, D.new2old);
+    m.n_new = (int64_t)D.nn_key.size();
+    m.nde = nde;
+    m.nn_key = dupload(T, D.nn_key);
+    m.nn_didx = dupload(T, D.nn_didx);
+    m.de_base = dupload(T, D.de_base);
+    m.dkoff = dupload(T, D.de_koff);
+    m.dkey = dupload(T, D.de_key);
+    m.ndd = (int64_t)D.dd_rank.size();
+    m.dd_rank = dupload(T, D.dd_rank);
+    m.dd_off = dupload(T, D.dd_off);
+    m.dd_t = dupload(T, D.dd_t);
+    m.ndv = (int64_t)D.dv_rank.size();
+    m.dv_rank = dupload(T, D.dv_rank);
+    m.dv_off = dupload(T, D.dv_off);
+    m.dv_key = dupload(T, D.dv_key);
+    m.nni = (int64_t)D.ni_key.size();
+    m.ni_key = dupload(T, D.ni_key);
+    m.ni_idx = dupload(T, D.ni_idx);
+
+    DevGraph g;
+    g.nv = g.n_own = D.nv;
+    g.ne = g0.ne + m.n_new;
+    g.n_in = D.in_off[D.nv];
+    int32_t* esrc2 = dalloc<int32_t>(L, g.ne);
+    int32_t* edst2 = dalloc<int32_t>(L, g.ne);
+    int32_t* eo2n = dalloc<int32_t>(T, g0.ne);
+    int32_t* mbase = dalloc<int32_t>(T, g.ne);
+    int32_t* mdlt = dalloc<int32_t>(T, g.ne);
+    int32_t* npos = dalloc<int32_t>(T, m.n_new);
+    launch_merge_edges(s, m, esrc2, edst2, eo2n, mbase, mdlt, npos);
+    int64_t* stmp = dalloc<int64_t>(T, scan_tmp_words(std::max(g.ne, g.nv)));
+    // edge histories: count, scan, write
+    int64_t* eoff2 = dalloc<int64_t>(L, g.ne + 1);
+    launch_edge_hist(s, false, m, g.ne, mbase, mdlt, esrc2, edst2, eoff2, nullptr);
+    launch_scan_counts(s, g.ne, eoff2, stmp);
+    int64_t nek = 0, nvk = 0;
+    HIPCHK(hipMemcpyAsync(&nek, eoff2 + g.ne, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int64_t* ekey2 = dalloc<int64_t>(L, nek);
+    launch_edge_hist(s, true, m, g.ne, mbase, mdlt, esrc2, edst2, eoff2, ekey2);
+    // vertex histories
+    int64_t* voff2 = dalloc<int64_t>(L, g.nv + 1);
+    launch_vertex_hist(s, false, m, voff2, nullptr);
+    launch_scan_counts(s, g.nv, voff2, stmp);
+    HIPCHK(hipMemcpyAsync(&nvk, voff2 + g.nv, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int64_t* vkey2 = dalloc<int64_t>(L, nvk);
+    launch_vertex_hist(s, true, m, voff2, vkey2);
+    // adjacency offsets (host-merged), in-edges
+    int64_t* in_off2 = dupload(L, D.in_off);
+    int32_t* in_eid2 = dalloc<int32_t>(L, g.n_in);
+    launch_merge_in(s, m, eo2n, npos, in_off2, in_eid2);
+    HIPCHK(hipGetLastError());
+    g.esrc = esrc2;
+    g.edst = edst2;
+    g.eoff = eoff2;
+    g.ekey = ekey2;
+    g.voff = voff2;
+    g.vkey = vkey2;
+    g.in_off = in_off2;
+    g.in_eid = in_eid2;
+    g.out_off = dupload(L, D.out_off);
+    g.adj_off = upload_adj(L, D.out_off, D.in_off);
+    g.doff = dupload(L, D.doff);
+    g.dtime = dupload(L, D.dtime);
+    build_heavy(c, g, L, D.out_off, D.in_off);
+    HIPCHK(hipStreamSynchronize(s));
+    for (void* p : T) (void)hipFree(p);
+    T.clear();
+    (void)hipStreamDestroy(s);
+    s = nullptr;
+    free_graph(c);  // old graph arrays, batch slots and mask sets (sizes changed)
+    c->graph_allocs.swap(L);
+    c->g = g;
+    B.nv = B.n_own = D.nv;
+    B.ne = g.ne;
+    B.vid.swap(D.vid);
+    B.doff.swap(D.doff);
+    B.dtime.swap(D.dtime);
+    B.out_off.swap(D.out_off);
+    B.in_off.swap(D.in_off);
+    B.n_vkey = nvk;
+    B.n_ekey = nek;
+    B.n_in = g.n_in;
+    B.newest = c->newest;
+    c->st.seal_delta_updates = D.nd;
+  } catch (...) {
+    for (void* p : T) (void)hipFree(p);
+    for (void* p : L) (void)hipFree(p);
+    if (s) (void)hipStreamDestroy(s);
+    throw;
+  }
+}
+
+}  // namespace
+
 int rgpu_seal(rgpu_ctx* c) {
   if (!c) return RGPU_EINVAL;
   std::lock_guard<std::mutex> lk(c->mu);
+  const auto t0 = std::chrono::steady_clock::now();
   try {
     HIPCHK(hipSetDevice(c->device));
+    if (c->n_sealed > 0 && c->n_sealed == c->events.size()) {  // nothing new since the last seal
+      c->sealed = true;
+      return RGPU_OK;
+    }
+    c->sealed = false;
+    c->st.seal_incremental = 0;
+    c->st.seal_delta_updates = 0;
+    if (c->delta_on && !c->partitioned && c->n_sealed > 0 && c->g.nv > 0) {
+      // live ingest: merge the delta into the resident graph
+      seal_delta(c);
+      c->st.seal_incremental = 1;
+      finish_seal(c);
+      c->st.seal_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      return RGPU_OK;
+    }
     std::string e = pack_events(c->events, c->part, c->nparts, &c->pk);
     if (!e.empty()) return fail(c, RGPU_EINVAL, e);
     free_graph(c);
@@ -1012,7 +1224,7 @@ int rgpu_seal(rgpu_ctx* c) {
     DevGraph g;
     g.nv = P.nv;
     g.ne = P.ne;
-    g.n_in = P.in_off.empty() ? 0 : P.in_off.back();
+    g.n_in = P.n_in;
     g.voff = dupload(L, P.voff);
     g.vkey = dupload(L, P.vkey);
     g.doff = dupload(L, P.doff);
@@ -1023,43 +1235,10 @@ int rgpu_seal(rgpu_ctx* c) {
     g.ekey = dupload(L, P.ekey);
     g.out_off = dupload(L, P.out_off);
     g.in_off = dupload(L, P.in_off);
-    {
-      std::vector<int64_t> adj(P.nv + 1 + 64);  // padded: read unconditionally by the step kernel
-      for (int64_t v = 0; v <= P.nv; v++) adj[v] = P.out_off[v] + P.in_off[v];
-      for (int64_t v = P.nv + 1; v < (int64_t)adj.size(); v++) adj[v] = adj[P.nv];
-      g.adj_off = dupload(L, adj);
-    }
+    g.adj_off = upload_adj(L, P.out_off, P.in_off);
     g.in_eid = dupload(L, P.in_eid);
     g.n_own = P.n_own;
-    if (!c->partitioned && c->heavy_t > 0) {
-      // heavy vertices (power-law hubs): static slot lists cut into kSegSlots segments
-      std::vector<int32_t> hv_of(P.nv, -1), hv_seg(1, 0), seg_v, seg_h, seg_n;
-      std::vector<int64_t> seg_lo;
-      for (int64_t v = 0; v < P.nv; v++) {
-        const int64_t deg = (P.out_off[v + 1] - P.out_off[v]) + (P.in_off[v + 1] - P.in_off[v]);
-        if (deg <= c->heavy_t) continue;
-        const int32_t h = (int32_t)(hv_seg.size() - 1);
-        hv_of[v] = h;
-        const int64_t a0 = P.out_off[v] + P.in_off[v];
-        for (int64_t o = 0; o < deg; o += kSegSlots) {
-          seg_v.push_back((int32_t)v);
-          seg_h.push_back(h);
-          seg_lo.push_back(a0 + o);
-          seg_n.push_back((int32_t)std::min<int64_t>(kSegSlots, deg - o));
-        }
-        hv_seg.push_back((int32_t)seg_v.size());
-      }
-      if (!seg_v.empty()) {
-        g.n_heavy = (int64_t)hv_seg.size() - 1;
-        g.n_seg = (int64_t)seg_v.size();
-        g.hv_of = dupload(L, hv_of);
-        g.hv_seg = dupload(L, hv_seg);
-        g.seg_v = dupload(L, seg_v);
-        g.seg_h = dupload(L, seg_h);
-        g.seg_lo = dupload(L, seg_lo);
-        g.seg_n = dupload(L, seg_n);
-      }
-    }
+    build_heavy(c, g, L, P.out_off, P.in_off);
     if (c->partitioned) {
       if (c->nparts > 1) g.grank = dupload(L, P.grank);
       Part& X = c->pt;
@@ -1075,17 +1254,13 @@ int rgpu_seal(rgpu_ctx* c) {
     }
     c->g = g;
     HIPCHK(hipDeviceSynchronize());
-    c->st.vertices = P.n_own;
-    c->st.edges = P.ne;
-    c->st.vertex_events = (int64_t)P.vkey.size();
-    c->st.edge_events = (int64_t)P.ekey.size();
-    c->st.deaths = (int64_t)P.dtime.size();
-    c->sealed = true;
+    finish_seal(c);
   } catch (const HipFail& f) {
-    return fail(c, RGPU_EHIP, f.msg);
+    return fail(c, f.code ? f.code : RGPU_EHIP, f.msg);
   } catch (const std::bad_alloc&) {
     return fail(c, RGPU_ENOMEM, "host allocation failed");
   }
+  c->st.seal_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return RGPU_OK;
 }
 

@@ -23,6 +23,7 @@ struct Packed {
   std::vector<int64_t> in_off;       // [nv+1] in-edges (no self-loops), ordered by (dst, src)
   std::vector<int32_t> in_eid;       // [in_off[nv]] edge ids of in-edges
   int64_t newest = -1;
+  int64_t n_vkey = 0, n_ekey = 0, n_in = 0;  // sizes (the big arrays are dropped after upload)
   // ---- vertex partitioning (num_partitions > 1); identity when P = 1
   int part = 0, nparts = 1;
   int64_t n_own = 0;                 // ranks [0, n_own) are owned here, [n_own, nv) are ghosts
@@ -49,5 +50,37 @@ struct Event {
 // Host packer (packer.cpp).  Returns empty string or an error message.
 std::string pack_events(const std::vector<Event>& ev, int partition, int num_partitions,
                         Packed* out);
+
+// Incremental seal (live ingest), host half.  Updates ev[first, n)
+// arrive after a sealed one-partition base; every one of them comes later in stream order
+// than every base update, so at equal times a delta put wins (TreeMap put-overwrite,
+// Entity.scala:25).  Only delta-sized work and O(V) offset arrays stay on the host; the big
+// history / edge / in-edge arrays are merged in HBM (merge.hip).  Ranks below are in the
+// merged rank space unless named old.
+struct Delta {
+  int64_t nv_old = 0, nv = 0, nd = 0;  // nd = delta updates
+  std::vector<int64_t> vid;             // merged ids (rank = index)
+  std::vector<int32_t> old2new, new2old;
+  // delta vertex points per rank, collapsed (last put wins), ranks ascending
+  std::vector<int32_t> dv_rank;
+  std::vector<int64_t> dv_off, dv_key;
+  // delta deaths (VertexDelete): distinct times per rank, with the last delta index (1-based)
+  std::vector<int32_t> dd_rank;
+  std::vector<int64_t> dd_off, dd_t, dd_last;
+  // delta edges: distinct (s, d), ascending; old ranks (-1: endpoint is new) for the base lookup
+  std::vector<int32_t> de_s, de_d, de_qs, de_qd;
+  std::vector<int64_t> de_poff, de_pt, de_pidx;  // raw points per edge, by (t, idx); idx 1-based
+  std::vector<uint8_t> de_pflag;
+  // after the base lookup (finish_delta)
+  std::vector<int32_t> de_base;          // base edge id or -1 (new edge)
+  std::vector<int64_t> de_koff, de_key;  // collapsed, tie-resolved own points
+  std::vector<int64_t> nn_key;           // new edges: (s << 32) | d ascending
+  std::vector<int32_t> nn_didx;          // their delta edge index
+  std::vector<int64_t> ni_key;           // new non-loop edges by (d << 32) | s ascending
+  std::vector<int32_t> ni_idx;           // their index in nn_*
+  std::vector<int64_t> out_off, in_off, doff, dtime;  // merged
+};
+std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed& base, Delta* out);
+void finish_delta(const Packed& base, const std::vector<int32_t>& base_eid, Delta* d);
 
 }  // namespace rgpu

@@ -1,0 +1,170 @@
+"""Live ingest: updates appended after a seal are merged into the
+HBM-resident graph by the incremental seal (merge.hip) instead of a full re-pack.
+
+Parity: after every seal the HIP path must answer exactly as the CPU oracle replaying the
+whole stream so far (labels, component maps, degrees bit-exact; PageRank L1 <= 1e-6), and
+exactly as a graph sealed once from the same full stream.  The later chunk counts as later
+in stream order (the reference applies updates in arrival order, EntityStorage.scala:73-453),
+so ties between a sealed point and a new one resolve to the new one — the cut points below
+split groups of equal timestamps on purpose.
+"""
+import numpy as np
+import pytest
+
+from oracle import Oracle
+from raphtory_amd import RGPUError, TemporalGraph
+from raphtory_amd.synth import BATCH_WINDOWS, DAY, HOUR, MONTH, WEEK, YEAR, gen_gab, gen_powerlaw, gen_uniform
+from tests.test_gpu_parity import check_cc, check_degree, check_pr
+
+pytestmark = pytest.mark.gpu
+
+
+def _growing_tie_stream(seed, n, nv_max=200):
+    """Equal timestamps in groups of 4 and ids that keep appearing (new vertices per chunk)."""
+    rng = np.random.default_rng(seed)
+    t = (np.arange(n) // 4).astype(np.int64) * 10
+    kind = rng.choice(4, size=n, p=[0.25, 0.45, 0.12, 0.18]).astype(np.uint8)
+    hi = np.minimum(nv_max, 8 + np.arange(n) // 12)
+    src = (rng.random(n) * hi).astype(np.int64)
+    dst = np.where(kind >= 2, (rng.random(n) * hi).astype(np.int64), -1).astype(np.int64)
+    return t, kind, src, dst
+
+
+def _cut(arrs, lo, hi):
+    return [a[lo:hi] for a in arrs]
+
+
+def _live(arrs, cuts, check):
+    """Ingest arrs in the chunks given by `cuts`, sealing after each; check(g, prefix) each time."""
+    g = TemporalGraph()
+    bounds = [0] + list(cuts) + [len(arrs[0])]
+    for k in range(len(bounds) - 1):
+        g.ingest(*_cut(arrs, bounds[k], bounds[k + 1]))
+        g.seal()
+        st = g.stats()
+        assert st["seal_incremental"] == (1 if k else 0)
+        assert st["seal_delta_updates"] == (bounds[k + 1] - bounds[k] if k else 0)
+        check(g, _cut(arrs, 0, bounds[k + 1]))
+    return g
+
+
+def _same_as_full(g, arrs, algo, hops, windows):
+    f = TemporalGraph()
+    f.ingest(*arrs)
+    f.seal()
+    a, b = g.stats(), f.stats()
+    for k in ("vertices", "edges", "vertex_events", "edge_events", "deaths"):
+        assert a[k] == b[k], (k, a[k], b[k])
+    f.run(algo, hops, windows)
+    g.run(algo, hops, windows)
+    if algo == "cc":
+        assert np.array_equal(g.cc_summaries(), f.cc_summaries())
+    f.close()
+
+
+def test_live_ties_new_vertices_each_seal():
+    arrs = _growing_tie_stream(7, 8000)
+    wins = [5000, 1000, 200, 40]
+
+    def check(g, pre):
+        o = Oracle(*pre)
+        end = int(pre[0][-1])
+        hops = np.arange(0, end + 20, max(37, end // 12), dtype=np.int64)
+        check_cc(g, o, hops, wins)
+        check_degree(g, o, hops[::2], wins)
+
+    # cut points inside groups of equal timestamps (t = i // 4)
+    g = _live(arrs, [1001, 2002, 2003, 4507, 6001], check)
+    hops = np.arange(0, int(arrs[0][-1]) + 20, 97, dtype=np.int64)
+    _same_as_full(g, arrs, "cc", hops, wins)
+    g.close()
+
+
+def test_live_out_of_order_deltas():
+    # later chunks carry times all over the sealed range (late events and endpoint deaths
+    # landing on sealed edge points)
+    s = gen_uniform(3, 90, 4000, t0=0, dt=1000)
+    rng = np.random.default_rng(2)
+    p = rng.permutation(len(s))
+    arrs = [s.t[p], s.kind[p], s.src[p], s.dst[p]]
+    wins = [2_000_000, 500_000, 100_000]
+    hops = np.arange(100_000, 4_000_000, 190_000, dtype=np.int64)
+
+    def check(g, pre):
+        o = Oracle(*pre)
+        check_cc(g, o, hops, wins)
+        check_pr(g, o, hops[::4], wins)
+
+    g = _live(arrs, [1500, 2600, 3900], check)
+    _same_as_full(g, arrs, "cc", hops, wins)
+    g.close()
+
+
+def test_live_deaths_tie_sealed_edge_points():
+    # hand-made: a sealed edge point and a later VertexDelete of an endpoint at the same t
+    # (the kill is the later put: EntityStorage.vertexRemoval :189-228), a re-add after it,
+    # and a new edge created at the time of an earlier (sealed) death (killList, :262,277)
+    base = ([10, 20, 30, 40], [2, 2, 2, 1], [1, 2, 3, 5], [2, 3, 4, -1])
+    d1 = ([20, 30, 40], [1, 3, 2], [3, 3, 5], [-1, 4, 6])
+    d2 = ([30, 50, 20], [2, 0, 2], [3, 2, 2], [4, -1, 3])
+    arrs = [np.asarray(np.concatenate([b, x, y]), dt)
+            for b, x, y, dt in zip(base, d1, d2, (np.int64, np.uint8, np.int64, np.int64))]
+    hops = np.arange(0, 80, 5, dtype=np.int64)
+    wins = [100, 25, 10, 0]
+
+    def check(g, pre):
+        o = Oracle(*pre)
+        check_cc(g, o, hops, wins)
+        check_degree(g, o, hops, wins)
+
+    g = _live(arrs, [4, 7], check)
+    g.close()
+
+
+def test_live_powerlaw_heavy_vertices_and_gab():
+    # hubs above the heavy-vertex threshold change their segment lists between seals
+    s = gen_powerlaw(3, 2000, 24_000, t0=0, t1=2 * YEAR)
+    arrs = [s.t, s.kind, s.src, s.dst]
+    hops = np.linspace(2 * YEAR - 60 * DAY, 2 * YEAR, 5).astype(np.int64)
+    wins = [MONTH, WEEK, DAY]
+
+    def check(g, pre):
+        o = Oracle(*pre)
+        check_cc(g, o, hops, wins)
+        check_degree(g, o, hops, wins)
+        check_pr(g, o, hops[-2:], wins)
+
+    import os
+    old = os.environ.get("RGPU_HEAVY")
+    os.environ["RGPU_HEAVY"] = "64"  # small graph: make hubs heavy
+    try:
+        g = _live(arrs, [16_000, 20_000], check)
+        _same_as_full(g, arrs, "cc", hops, wins)
+    finally:
+        if old is None:
+            os.environ.pop("RGPU_HEAVY", None)
+        else:
+            os.environ["RGPU_HEAVY"] = old
+    g.close()
+    s = gen_gab(4, 3000, 6000)
+    arrs = [s.t, s.kind, s.src, s.dst]
+    end = int(s.t[-1])
+    hops = np.arange(end - 48 * HOUR, end + 1, 8 * HOUR, dtype=np.int64)
+
+    def check2(g, pre):
+        check_cc(g, Oracle(*pre), hops, BATCH_WINDOWS)
+
+    g = _live(arrs, [9000, 15000], check2)
+    g.close()
+
+
+def test_live_seal_errors_and_noop():
+    g = TemporalGraph()
+    g.ingest([1, 2], [2, 2], [1, 2], [2, 3])
+    g.seal()
+    g.seal()  # nothing new: no-op
+    assert g.stats()["seal_incremental"] == 0
+    g.ingest([3], [2], [1], [1 << 40])  # id out of range in the delta
+    with pytest.raises(RGPUError):
+        g.seal()
+    g.close()
