@@ -129,6 +129,9 @@ def synth() -> C.CDLL:
                                       _P64, _PU8, _P64, _P64]
         s.rg_gen_gab.restype = _SZ
         s.rg_gen_gab.argtypes = [C.c_uint64, C.c_int64, _SZ, C.c_int64, C.c_int64, _P64, _PU8, _P64, _P64]
+        s.rg_gen_gab_keyed.restype = _SZ
+        s.rg_gen_gab_keyed.argtypes = [C.c_uint64, C.c_uint64, C.c_int64, _SZ, C.c_int64, C.c_int64, _P64, _PU8,
+                                       _P64, _P64]
         _synth = s
     return _synth
 

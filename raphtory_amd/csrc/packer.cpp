@@ -448,9 +448,14 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
   }
   parallel_sort(ids, nt, std::less<int64_t>());
   ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-  std::vector<int64_t> nid;
-  for (int64_t x : ids)
-    if (!std::binary_search(B.vid.begin(), B.vid.end(), x)) nid.push_back(x);
+  std::vector<int64_t> nid;  // ids not in the base: one sorted walk over both
+  {
+    size_t a = 0;
+    for (int64_t x : ids) {
+      while (a < B.vid.size() && B.vid[a] < x) a++;
+      if (a == B.vid.size() || B.vid[a] != x) nid.push_back(x);
+    }
+  }
   D.nv = B.nv + (int64_t)nid.size();
   D.vid.resize(D.nv);
   D.old2new.resize(B.nv);
@@ -469,12 +474,22 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
       r++;
     }
   }
+  // merged rank of every delta id (ids ascending, so one walk), then each update's ranks by
+  // a search in the delta's own id list (much smaller than the graph's)
+  std::vector<int32_t> idrank(ids.size());
+  {
+    size_t r = 0;
+    for (size_t k = 0; k < ids.size(); k++) {
+      while (D.vid[r] < ids[k]) r++;
+      idrank[k] = (int32_t)r;
+    }
+  }
   std::vector<int32_t> rs(n), rd(n, -1);
   parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
     for (size_t i = lo; i < hi; i++) {
       const Event& e = ev[first + i];
-      rs[i] = (int32_t)(std::lower_bound(D.vid.begin(), D.vid.end(), e.src) - D.vid.begin());
-      if (e.kind >= RGPU_EADD) rd[i] = (int32_t)(std::lower_bound(D.vid.begin(), D.vid.end(), e.dst) - D.vid.begin());
+      rs[i] = idrank[std::lower_bound(ids.begin(), ids.end(), e.src) - ids.begin()];
+      if (e.kind >= RGPU_EADD) rd[i] = idrank[std::lower_bound(ids.begin(), ids.end(), e.dst) - ids.begin()];
     }
   });
   // ---- vertex points (same records as pack_events), collapsed per (rank, t): last put wins
@@ -612,32 +627,40 @@ void finish_delta(const Packed& B, const std::vector<int32_t>& base_eid, Delta* 
       inc[d + 1]++;
     }
   }
+  const int nt = num_threads();
   {
-    std::vector<size_t> o(D.ni_key.size());
-    for (size_t k = 0; k < o.size(); k++) o[k] = k;
-    std::sort(o.begin(), o.end(), [&](size_t a, size_t b) { return D.ni_key[a] < D.ni_key[b]; });
-    std::vector<int64_t> k2(o.size());
-    std::vector<int32_t> i2(o.size());
-    for (size_t k = 0; k < o.size(); k++) { k2[k] = D.ni_key[o[k]]; i2[k] = D.ni_idx[o[k]]; }
-    D.ni_key.swap(k2);
-    D.ni_idx.swap(i2);
+    std::vector<std::pair<int64_t, int32_t>> o(D.ni_key.size());
+    for (size_t k = 0; k < o.size(); k++) o[k] = {D.ni_key[k], D.ni_idx[k]};
+    parallel_sort(o, nt, [](const std::pair<int64_t, int32_t>& a, const std::pair<int64_t, int32_t>& b) {
+      return a.first < b.first;
+    });
+    for (size_t k = 0; k < o.size(); k++) { D.ni_key[k] = o[k].first; D.ni_idx[k] = o[k].second; }
   }
   // merged offsets and death lists (O(V) host work)
   D.out_off.assign(D.nv + 1, 0);
   D.in_off.assign(D.nv + 1, 0);
+  parallel_for((size_t)D.nv, nt, [&](size_t lo, size_t hi, int) {  // counts, then one prefix pass
+    for (size_t v = lo; v < hi; v++) {
+      const int32_t u = D.new2old[v];
+      int64_t oc = outc[v + 1], ic = inc[v + 1];
+      if (u >= 0) {
+        oc += B.out_off[u + 1] - B.out_off[u];
+        ic += B.in_off[u + 1] - B.in_off[u];
+      }
+      D.out_off[v + 1] = oc;
+      D.in_off[v + 1] = ic;
+    }
+  });
+  for (int64_t v = 0; v < D.nv; v++) {
+    D.out_off[v + 1] += D.out_off[v];
+    D.in_off[v + 1] += D.in_off[v];
+  }
   D.doff.assign(D.nv + 1, 0);
   D.dtime.clear();
   D.dtime.reserve(B.dtime.size() + D.dd_t.size());
   size_t jd = 0;
-  for (int64_t v = 0; v < D.nv; v++) {
+  for (int64_t v = 0; v < D.nv && !(B.dtime.empty() && D.dd_t.empty()); v++) {
     const int32_t u = D.new2old[v];
-    int64_t oc = outc[v + 1], ic = inc[v + 1];
-    if (u >= 0) {
-      oc += B.out_off[u + 1] - B.out_off[u];
-      ic += B.in_off[u + 1] - B.in_off[u];
-    }
-    D.out_off[v + 1] = D.out_off[v] + oc;
-    D.in_off[v + 1] = D.in_off[v] + ic;
     const int64_t* b0 = u >= 0 ? B.dtime.data() + B.doff[u] : nullptr;
     const int64_t* b1 = u >= 0 ? B.dtime.data() + B.doff[u + 1] : nullptr;
     const int64_t *c0 = nullptr, *c1 = nullptr;

@@ -141,6 +141,11 @@ struct rgpu_ctx {
   Packed pk;
   DevGraph g;
   std::vector<void*> graph_allocs;
+  // batch-slot and mask-set buffers, sized for cap_* >= the graph (a live-ingest merge that
+  // still fits keeps them: reallocating tens of GB per merge would dominate the tick)
+  std::vector<void*> slot_allocs;
+  int64_t cap_nv = 0, cap_ne = 0, cap_nin = 0;
+  bool hv_cc = false, hv_pr = false;    // heavy-vertex slot buffers (graph_allocs) ready
   Slot slot[kMaxSlots];
   int nslots = 2;
   bool hostflags = true;                // superstep flags via host-mapped memory (else copies)
@@ -192,9 +197,12 @@ T* dupload(std::vector<void*>& list, const std::vector<T>& h) {
   return d;
 }
 
+void release_slots(rgpu_ctx* c);
 void free_graph(rgpu_ctx* c) {
   for (void* p : c->graph_allocs) (void)hipFree(p);
   c->graph_allocs.clear();
+  release_slots(c);
+  c->g = DevGraph();
   if (c->pt.h_x) (void)hipHostFree(c->pt.h_x);
   if (c->pt.h_scnt) (void)hipHostFree(c->pt.h_scnt);
   {
@@ -202,6 +210,13 @@ void free_graph(rgpu_ctx* c) {
     c->pt = Part();
     c->pt.xchg = x;  // the communicator outlives a re-seal
   }
+}
+
+void release_slots(rgpu_ctx* c) {
+  for (void* p : c->slot_allocs) (void)hipFree(p);
+  c->slot_allocs.clear();
+  c->cap_nv = c->cap_ne = c->cap_nin = 0;
+  c->hv_cc = c->hv_pr = false;  // (their buffers are in graph_allocs)
   for (Slot& s : c->slot) {
     if (s.h_stepcnt) (void)hipHostFree(s.h_stepcnt);
     if (s.h_tail) (void)hipHostFree(s.h_tail);
@@ -218,7 +233,6 @@ void free_graph(rgpu_ctx* c) {
       if (e) (void)hipEventDestroy(e);
     m = MaskSet();
   }
-  c->g = DevGraph();
 }
 
 hipEvent_t take_event(rgpu_ctx* c) {
@@ -250,8 +264,8 @@ void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn, int step = 0
 }
 
 void ensure_masks(rgpu_ctx* c, int G) {
-  auto& L = c->graph_allocs;
-  const int64_t nv = c->g.nv, ne = c->g.ne;
+  auto& L = c->slot_allocs;
+  const int64_t nv = c->cap_nv, ne = c->cap_ne;
   if (G == 1) {
     for (int i = 0; i < c->nslots; i++) {
       Slot& s = c->slot[i];
@@ -263,7 +277,7 @@ void ensure_masks(rgpu_ctx* c, int G) {
     return;
   }
   for (MaskSet& m : c->mset) {
-    if (m.planes < G) {  // (a smaller earlier allocation stays in graph_allocs until re-seal)
+    if (m.planes < G) {  // (a smaller earlier allocation stays in slot_allocs until re-seal)
       m.vm = dalloc<uint64_t>(L, (size_t)G * (nv + kPad));
       m.em = dalloc<uint64_t>(L, (size_t)G * ne);
       m.planes = G;
@@ -277,8 +291,15 @@ void ensure_masks(rgpu_ctx* c, int G) {
 }
 
 void ensure_slots(rgpu_ctx* c, int algo) {
-  auto& L = c->graph_allocs;
-  const int64_t nv = c->g.nv, ne = c->g.ne, nin = c->g.n_in;
+  if (c->cap_nv < c->g.nv || c->cap_ne < c->g.ne || c->cap_nin < c->g.n_in) {
+    release_slots(c);
+    c->cap_nv = c->g.nv;
+    c->cap_ne = c->g.ne;
+    c->cap_nin = c->g.n_in;
+  }
+  auto& L = c->slot_allocs;
+  auto& LG = c->graph_allocs;  // heavy-vertex buffers: sized by the graph's segments
+  const int64_t nv = c->cap_nv, ne = c->cap_ne, nin = c->cap_nin;
   const size_t rows = (size_t)nv * kViews;
   for (int i = 0; i < c->nslots; i++) {
     Slot& s = c->slot[i];
@@ -311,22 +332,22 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       s.work = dalloc<unsigned long long>(L, kWorkWords);
       s.iso = dalloc<unsigned int>(L, kIsoWords);  // zero between batches: the summary kernel clears it
       HIPCHK(hipMemset(s.iso, 0, sizeof(unsigned int) * kIsoWords));
-      if (c->g.n_seg > 0) {
-        s.hv.segcnt = dalloc<int32_t>(L, c->g.n_seg);
-        s.hv.segor = dalloc<uint64_t>(L, c->g.n_seg);
-        s.hv.best = dalloc<int32_t>(L, (size_t)c->g.n_heavy * kViews);  // INT32_MAX between uses
-        HIPCHK(hipMemsetD32((hipDeviceptr_t)s.hv.best, INT32_MAX, (size_t)c->g.n_heavy * kViews));
-      }
+    }
+    if (algo == RGPU_ALGO_CC && !c->hv_cc && c->g.n_seg > 0) {
+      s.hv.segcnt = dalloc<int32_t>(LG, c->g.n_seg);
+      s.hv.segor = dalloc<uint64_t>(LG, c->g.n_seg);
+      s.hv.best = dalloc<int32_t>(LG, (size_t)c->g.n_heavy * kViews);  // INT32_MAX between uses
+      HIPCHK(hipMemsetD32((hipDeviceptr_t)s.hv.best, INT32_MAX, (size_t)c->g.n_heavy * kViews));
     }
     if ((algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) && !c->slot_deg) {
       s.outdeg = dalloc<int32_t>(L, rows);
       s.indeg = dalloc<int32_t>(L, rows);
     }
+    if (algo == RGPU_ALGO_PR && !c->hv_pr && c->g.n_seg > 0) {
+      s.hv.pacc = dalloc<double>(LG, (size_t)c->g.n_heavy * kViews);  // zero between uses
+      HIPCHK(hipMemset(s.hv.pacc, 0, sizeof(double) * (size_t)c->g.n_heavy * kViews));
+    }
     if (algo == RGPU_ALGO_PR && !c->slot_pr) {
-      if (c->g.n_seg > 0) {
-        s.hv.pacc = dalloc<double>(L, (size_t)c->g.n_heavy * kViews);  // zero between uses
-        HIPCHK(hipMemset(s.hv.pacc, 0, sizeof(double) * (size_t)c->g.n_heavy * kViews));
-      }
       s.pr = dalloc<double>(L, rows);
       s.contrib[0] = dalloc<double>(L, rows);
       s.contrib[1] = dalloc<double>(L, rows);
@@ -341,25 +362,26 @@ void ensure_slots(rgpu_ctx* c, int algo) {
     if (!X.h_x) {
       HIPCHK(hipHostMalloc((void**)&X.h_x, sizeof(int64_t) * 2 * P));
       HIPCHK(hipHostMalloc((void**)&X.h_scnt, sizeof(int32_t) * (P + 1)));
-      X.scnt = dalloc<int32_t>(L, P);
-      X.xa = dalloc<int64_t>(L, 2 * P);
-      X.xb = dalloc<int64_t>(L, 2 * P);
+      X.scnt = dalloc<int32_t>(LG, P);
+      X.xa = dalloc<int64_t>(LG, 2 * P);
+      X.xb = dalloc<int64_t>(LG, 2 * P);
     }
     if (algo == RGPU_ALGO_CC && !X.cc_ready) {
-      X.sbuf = dalloc<int32_t>(L, (size_t)X.nxs * kXRecWords);
-      X.rbuf = dalloc<int32_t>(L, (size_t)X.nxr * kXRecWords);
+      X.sbuf = dalloc<int32_t>(LG, (size_t)X.nxs * kXRecWords);
+      X.rbuf = dalloc<int32_t>(LG, (size_t)X.nxr * kXRecWords);
       X.hist_total = ((int64_t)kViews * X.ng + P - 1) / P * P;
-      X.hist = dalloc<int32_t>(L, X.hist_total);
-      X.chunk = dalloc<int32_t>(L, X.hist_total / P);
+      X.hist = dalloc<int32_t>(LG, X.hist_total);
+      X.chunk = dalloc<int32_t>(LG, X.hist_total / P);
       X.cc_ready = true;
     }
     if (algo == RGPU_ALGO_PR && !X.pr_ready) {
-      X.sbuf_f = dalloc<double>(L, (size_t)X.nxs * kViews);
-      X.rbuf_f = dalloc<double>(L, (size_t)X.nxr * kViews);
+      X.sbuf_f = dalloc<double>(LG, (size_t)X.nxs * kViews);
+      X.rbuf_f = dalloc<double>(LG, (size_t)X.nxr * kViews);
       X.pr_ready = true;
     }
   }
-  if (algo == RGPU_ALGO_CC) c->slot_cc = true;
+  if (algo == RGPU_ALGO_CC) c->slot_cc = c->hv_cc = true;
+  if (algo == RGPU_ALGO_PR) c->hv_pr = true;
   if (algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) c->slot_deg = true;
   if (algo == RGPU_ALGO_PR) c->slot_pr = true;
 }
@@ -989,7 +1011,8 @@ int rgpu_ingest(rgpu_ctx* c, const int64_t* t, const uint8_t* kind, const int64_
   std::lock_guard<std::mutex> lk(c->mu);
   if (n && (!t || !kind || !src)) return fail(c, RGPU_EINVAL, "null input array");
   try {
-    c->events.reserve(c->events.size() + n);
+    const size_t need = c->events.size() + n;  // geometric growth: live ingest appends often
+    if (c->events.capacity() < need) c->events.reserve(std::max(need, c->events.capacity() * 3 / 2));
     for (size_t i = 0; i < n; i++) {
       if (kind[i] > RGPU_EDEL) return fail(c, RGPU_EINVAL, "unknown update kind");
       if (kind[i] >= RGPU_EADD && !dst) return fail(c, RGPU_EINVAL, "edge update without dst array");
@@ -1065,7 +1088,16 @@ void finish_seal(rgpu_ctx* c) {
 void seal_delta(rgpu_ctx* c) {
   Packed& B = c->pk;
   Delta D;
+  auto tp = std::chrono::steady_clock::now();
+  auto phase = [&](const char* what) {  // RGPU_HOSTPROF: host-side phase times
+    if (!c->hostprof) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[rgpu seal_delta] %-10s %8.2f ms\n", what,
+                 std::chrono::duration<double, std::milli>(now - tp).count());
+    tp = now;
+  };
   std::string e = pack_delta(c->events, c->n_sealed, B, &D);
+  phase("pack");
   if (!e.empty()) throw HipFail{e, RGPU_EINVAL};
   std::vector<void*> T;  // temporaries
   std::vector<void*> L;  // the merged graph
@@ -1083,7 +1115,9 @@ void seal_delta(rgpu_ctx* c) {
       HIPCHK(hipMemcpyAsync(base_eid.data(), res, sizeof(int32_t) * nde, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
     }
+    phase("lookup");
     finish_delta(B, base_eid, &D);
+    phase("finish");
     MergeIn m;
     m.nv_old = g0.nv;
     m.nv2 = D.nv;
@@ -1166,13 +1200,34 @@ void seal_delta(rgpu_ctx* c) {
     g.dtime = dupload(L, D.dtime);
     build_heavy(c, g, L, D.out_off, D.in_off);
     HIPCHK(hipStreamSynchronize(s));
+    phase("merge");
     for (void* p : T) (void)hipFree(p);
     T.clear();
     (void)hipStreamDestroy(s);
     s = nullptr;
-    free_graph(c);  // old graph arrays, batch slots and mask sets (sizes changed)
+    // swap in the merged graph; batch slots and mask sets stay if they fit (else they are
+    // reallocated on the next run with 25 % headroom for the ticks to come)
+    for (void* p : c->graph_allocs) (void)hipFree(p);
     c->graph_allocs.swap(L);
+    L.clear();
     c->g = g;
+    c->hv_cc = c->hv_pr = false;
+    for (Slot& sl : c->slot) sl.hv = HeavyBuf();
+    if (g.nv > c->cap_nv || g.ne > c->cap_ne || g.n_in > c->cap_nin) {
+      release_slots(c);
+      c->cap_nv = g.nv + g.nv / 4;
+      c->cap_ne = g.ne + g.ne / 4;
+      c->cap_nin = g.n_in + g.n_in / 4;
+    } else {
+      for (int i = 0; i < c->nslots; i++) {  // per-rank state that K2 does not rewrite
+        Slot& sl = c->slot[i];
+        if (sl.chg[0]) {
+          HIPCHK(hipMemset(sl.chg[0], 0, sizeof(uint64_t) * (c->cap_nv + kPad)));
+          HIPCHK(hipMemset(sl.chg[1], 0, sizeof(uint64_t) * (c->cap_nv + kPad)));
+          HIPCHK(hipMemset(sl.snbr, 0, sizeof(int32_t) * (c->cap_ne + c->cap_nin + kPad)));
+        }
+      }
+    }
     B.nv = B.n_own = D.nv;
     B.ne = g.ne;
     B.vid.swap(D.vid);
@@ -1185,6 +1240,7 @@ void seal_delta(rgpu_ctx* c) {
     B.n_in = g.n_in;
     B.newest = c->newest;
     c->st.seal_delta_updates = D.nd;
+    phase("swap");
   } catch (...) {
     for (void* p : T) (void)hipFree(p);
     for (void* p : L) (void)hipFree(p);

@@ -111,8 +111,16 @@ size_t rg_gen_powerlaw(uint64_t seed, int64_t nverts, size_t n, double gamma, in
 /* C4: `inter` GAB-like interactions -> 3*inter add-only events.  Power-law activity on both
  * ends; timestamps at 1 s granularity x1000 over [t0, t1) with a monotone diurnal warp
  * g(f) = f + A sin(2 pi D f)/(2 pi D), A = 0.6, D = days in span. */
+/* id_key: the user-id scattering key (the same key = the same users, e.g. later ticks of a
+ * live stream drawn with another seed) */
+size_t rg_gen_gab_keyed(uint64_t seed, uint64_t id_key, int64_t users, size_t inter, int64_t t0, int64_t t1,
+                        int64_t* t, uint8_t* kind, int64_t* src, int64_t* dst);
 size_t rg_gen_gab(uint64_t seed, int64_t users, size_t inter, int64_t t0, int64_t t1,
                   int64_t* t, uint8_t* kind, int64_t* src, int64_t* dst) {
+  return rg_gen_gab_keyed(seed, seed, users, inter, t0, t1, t, kind, src, dst);
+}
+size_t rg_gen_gab_keyed(uint64_t seed, uint64_t id_key, int64_t users, size_t inter, int64_t t0, int64_t t1,
+                        int64_t* t, uint8_t* kind, int64_t* src, int64_t* dst) {
   uint64_t s = seed;
   PL p = pl_make(users, 2.1);
   double span_s = (double)((t1 - t0) / 1000);
@@ -122,7 +130,7 @@ size_t rg_gen_gab(uint64_t seed, int64_t users, size_t inter, int64_t t0, int64_
     double f = (double)i / (double)inter;
     double g = f + A * sin(twopi * days * f) / (twopi * days);
     int64_t ts = t0 + (int64_t)floor(g * span_s) * 1000;
-    int64_t a = perm31(pl_draw(&p, &s), seed), b = perm31(pl_draw(&p, &s), seed);
+    int64_t a = perm31(pl_draw(&p, &s), id_key), b = perm31(pl_draw(&p, &s), id_key);
     size_t o = 3 * i;
     t[o] = t[o + 1] = t[o + 2] = ts;
     kind[o] = 0; src[o] = a; dst[o] = -1;

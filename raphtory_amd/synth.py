@@ -61,13 +61,16 @@ def gen_powerlaw(seed: int, nverts: int, n: int, gamma: float = 2.1,
     return Stream(t, k, s, d)
 
 
-def gen_gab(seed: int, users: int, interactions: int, t0: int = GAB_T0, t1: int = GAB_T1) -> Stream:
-    """C4 shape: add-only (VADD s, VADD d, EADD s->d) triples at one t (GabUserGraphRouter)."""
+def gen_gab(seed: int, users: int, interactions: int, t0: int = GAB_T0, t1: int = GAB_T1,
+            id_key: int = None) -> Stream:
+    """C4 shape: add-only (VADD s, VADD d, EADD s->d) triples at one t (GabUserGraphRouter).
+    id_key (default: seed) scatters user ranks over ids; keep it fixed to draw later ticks of
+    one live stream (same users) with other seeds."""
     n = 3 * interactions
     t, k, s, d = _alloc(n)
-    N.synth().rg_gen_gab(seed, users, interactions, t0, t1,
-                         N.ptr(t, N.C.c_int64), N.ptr(k, N.C.c_uint8),
-                         N.ptr(s, N.C.c_int64), N.ptr(d, N.C.c_int64))
+    N.synth().rg_gen_gab_keyed(seed, seed if id_key is None else id_key, users, interactions, t0, t1,
+                               N.ptr(t, N.C.c_int64), N.ptr(k, N.C.c_uint8),
+                               N.ptr(s, N.C.c_int64), N.ptr(d, N.C.c_int64))
     return Stream(t, k, s, d)
 
 
