@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RGPU_ABI_VERSION 3
+#define RGPU_ABI_VERSION 4
 
 /* error codes */
 #define RGPU_OK 0
@@ -94,6 +94,32 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out);
  * path for the analysis hot path; the final histories follow EntityStorage.scala:73-453. */
 int rgpu_ingest(rgpu_ctx* ctx, const int64_t* t, const uint8_t* kind, const int64_t* src,
                 const int64_t* dst, size_t n);
+
+/* Binary GraphUpdate log ("RGEV") — the Router-side packer and the
+ * partition-side decoder, replacing one Tracked*GraphUpdate actor message per update
+ * (RouterWorker.sendGraphUpdate, S/core/components/Router/RouterWorker.scala:88-116; update
+ * case classes raphtoryMessages.scala:38-55).  A log is a sequence of self-checking blocks
+ * (little-endian):
+ *    0 u32 magic 0x56454752 ("RGEV")   4 u16 version = 1   6 u16 flags = 0
+ *    8 u32 n, 1..RGPU_RGEV_MAX_BLOCK  12 u32 checksum      16 i64 t_base (min time in block)
+ *   24 u32 dt[n] (t - t_base) | u8 kind[n] zero-padded to a multiple of 4 | i32 src[n] | i32 dst[n]
+ * checksum = lo32(a) ^ hi32(a) ^ lo32(b) ^ hi32(b) of a Fletcher-64 over the payload's u32
+ * words (a += w; b += a, both mod 2^64).  Stream order is kept (ties resolve by it); vertex
+ * updates carry dst = -1; 13 bytes per update + 24 per block.
+ * rgpu_rgev_encode: pass out = NULL for the size (*written); blocks hold at most `block`
+ *   updates (0 = RGPU_RGEV_MAX_BLOCK) and end early where the time span would pass 2^32 - 1.
+ * rgpu_rgev_decode: expands every WHOLE block in buf (a trailing partial block is left:
+ *   *consumed says how far it read, so a socket reader keeps the rest for the next call);
+ *   pass t = NULL for the count (*n).  Any malformed block fails the call, nothing written.
+ * rgpu_ingest_rgev: decode + rgpu_ingest in one call (same validation, same order).
+ * The codec calls need no GPU and no ctx; their errors are in rgpu_rgev_last_error(). */
+#define RGPU_RGEV_MAX_BLOCK (1u << 20)
+int rgpu_rgev_encode(const int64_t* t, const uint8_t* kind, const int64_t* src, const int64_t* dst,
+                     size_t n, size_t block, uint8_t* out, size_t cap, size_t* written);
+int rgpu_rgev_decode(const uint8_t* buf, size_t bytes, int64_t* t, uint8_t* kind, int64_t* src,
+                     int64_t* dst, size_t cap, size_t* n, size_t* consumed);
+const char* rgpu_rgev_last_error(void);
+int rgpu_ingest_rgev(rgpu_ctx* ctx, const uint8_t* buf, size_t bytes, size_t* consumed);
 
 /* Sort + merge + pack the ingested stream into SoA histories and copy them to HBM.
  * Live ingest (IngestionWorker.scala:31-256 keeps appending while LiveAnalysisTask.scala:13-107

@@ -8,5 +8,6 @@ partition function (``partition``) and the synthetic spouts (``synth``).
 from ._native import NativeUnavailable  # noqa: F401
 from .graph import RGPUError, TemporalGraph  # noqa: F401
 from .partition import get_partition, get_worker  # noqa: F401
+from . import rgev  # noqa: F401
 
 __all__ = ["TemporalGraph", "RGPUError", "NativeUnavailable", "get_partition", "get_worker"]

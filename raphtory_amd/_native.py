@@ -35,6 +35,7 @@ EXPORTS = [
     "rgpu_exchange_id", "rgpu_exchange_init", "rgpu_run_view_batch", "rgpu_cc_summary", "rgpu_cc_result",
     "rgpu_cc_vertex_labels", "rgpu_degree_result", "rgpu_degree_vertex", "rgpu_pr_result",
     "rgpu_stats", "rgpu_last_error", "rgpu_close",
+    "rgpu_rgev_encode", "rgpu_rgev_decode", "rgpu_rgev_last_error", "rgpu_ingest_rgev",
 ]
 
 
@@ -84,6 +85,10 @@ _SIGS = {
     "rgpu_stats": (C.c_int, [_CTX, C.POINTER(Stats)]),
     "rgpu_last_error": (C.c_char_p, [_CTX]),
     "rgpu_close": (None, [_CTX]),
+    "rgpu_rgev_encode": (C.c_int, [_P64, _PU8, _P64, _P64, _SZ, _SZ, _PU8, _SZ, C.POINTER(_SZ)]),
+    "rgpu_rgev_decode": (C.c_int, [_PU8, _SZ, _P64, _PU8, _P64, _P64, _SZ, C.POINTER(_SZ), C.POINTER(_SZ)]),
+    "rgpu_rgev_last_error": (C.c_char_p, []),
+    "rgpu_ingest_rgev": (C.c_int, [_CTX, _PU8, _SZ, C.POINTER(_SZ)]),
 }
 
 _lib = None

@@ -1026,6 +1026,27 @@ int rgpu_ingest(rgpu_ctx* c, const int64_t* t, const uint8_t* kind, const int64_
   return RGPU_OK;
 }
 
+int rgpu_ingest_rgev(rgpu_ctx* c, const uint8_t* buf, size_t bytes, size_t* consumed) {
+  if (!c) return RGPU_EINVAL;
+  if (!consumed) return fail(c, RGPU_EINVAL, "null argument");
+  size_t n = 0, used = 0;
+  if (rgpu_rgev_decode(buf, bytes, nullptr, nullptr, nullptr, nullptr, 0, &n, &used) != RGPU_OK)
+    return fail(c, RGPU_EINVAL, rgpu_rgev_last_error());
+  *consumed = 0;
+  if (n == 0) return RGPU_OK;
+  try {
+    std::vector<int64_t> t(n), src(n), dst(n);
+    std::vector<uint8_t> kind(n);
+    if (rgpu_rgev_decode(buf, used, t.data(), kind.data(), src.data(), dst.data(), n, &n, &used) != RGPU_OK)
+      return fail(c, RGPU_EINVAL, rgpu_rgev_last_error());
+    const int rc = rgpu_ingest(c, t.data(), kind.data(), src.data(), dst.data(), n);
+    if (rc == RGPU_OK) *consumed = used;
+    return rc;
+  } catch (const std::bad_alloc&) {
+    return fail(c, RGPU_ENOMEM, "host allocation failed");
+  }
+}
+
 namespace {
 
 // Heavy vertices (power-law hubs): static slot lists cut into kSegSlots segments.

@@ -70,6 +70,15 @@ class TemporalGraph:
         self._check(self._lib.rgpu_ingest(self._ctx, N.ptr(t, C.c_int64), N.ptr(kind, C.c_uint8),
                                           N.ptr(src, C.c_int64), N.ptr(dst, C.c_int64), n))
 
+    def ingest_rgev(self, buf) -> int:
+        """Ingest the whole RGEV blocks in ``buf`` (rgev.py); returns the bytes consumed (a
+        trailing partial block is left for the caller's next call)."""
+        b = np.frombuffer(buf, dtype=np.uint8)
+        used = C.c_size_t()
+        self._check(self._lib.rgpu_ingest_rgev(self._ctx, N.ptr(b, C.c_uint8) if b.shape[0] else None,
+                                               b.shape[0], C.byref(used)))
+        return used.value
+
     def ingest_stream(self, s) -> None:
         self.ingest(s.t, s.kind, s.src, s.dst)
 
