@@ -144,6 +144,9 @@ struct MergeIn {
   const int64_t *dd_off = nullptr, *dd_t = nullptr;
   const int32_t* dv_rank = nullptr;
   const int64_t *dv_off = nullptr, *dv_key = nullptr;
+  int64_t nvk_old = 0, ndvk = 0;      // base vertex keys, delta vertex keys
+  int64_t* coll = nullptr;             // [ndvk + 1] collision flags -> prefix (scratch)
+  int64_t* coll_tmp = nullptr;         // scan_tmp_words(ndvk) (scratch)
   const int64_t* ni_key = nullptr;
   const int32_t* ni_idx = nullptr;
 };

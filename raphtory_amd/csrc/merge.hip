@@ -11,7 +11,8 @@
 //    (src, dst) order; a base edge e lands at e + #(new edges with a smaller key), a new edge
 //    i at i + #(base edges with a smaller key) (binary searches);
 //  * histories: per entity, base points and delta points are merged by time; at equal time
-//    the delta point wins (later put).  A base edge point at the time of a DELTA endpoint
+//    the delta point wins (later put).  Edge histories (short) merge one entity per thread;
+//    vertex histories (power-law: hubs hold millions of points) place every point by itself.  A base edge point at the time of a DELTA endpoint
 //    death becomes a removal (the kill is the later put, EntityStorage.scala:189-228);
 //  * in-edges: per destination, base in-edges and new in-edges interleave by source rank.
 // Irregular integer work; HBM-bound.  Bytes per merged entity are its old + new arrays.
@@ -178,26 +179,97 @@ __global__ __launch_bounds__(kB) void k_edge_hist(int64_t ne2, const int32_t* __
   }
 }
 
-template <bool WRITE>
-__global__ __launch_bounds__(kB) void k_vertex_hist(int64_t nv2, const int32_t* __restrict__ new2old,
-                                                    const int64_t* __restrict__ voff, const int64_t* __restrict__ vkey,
-                                                    int64_t ndv, const int32_t* __restrict__ dv_rank,
-                                                    const int64_t* __restrict__ dv_off, const int64_t* __restrict__ dv_key,
-                                                    int64_t* __restrict__ cnt_off, int64_t* __restrict__ vkey2) {
+// ---- vertex histories by position formula (power-law safe: no per-entity serial merge, whose
+// cost per wave is the longest history among its 64 lanes — a hub's millions of points).
+// Base and delta lists of one vertex are both time-sorted with distinct times; a delta point
+// replaces a base point at the same time.  coll[j] = 1 iff delta key j has such a twin; after
+// an exclusive scan, coll[j] counts the colliding delta keys before j.
+//   count(v)          = na + nb - collisions(v)
+//   pos(base a_i)     = voff2[v] + i + #(delta times < t_i) - #(colliding delta keys among those)
+//   pos(delta b_j)    = voff2[v] + j + #(base times < t_j) - #(colliding delta keys before j)
+// (the base keys dropped before a point are exactly the colliding delta keys before it).
+__device__ __forceinline__ int64_t seg_of(const int64_t* __restrict__ off, int64_t nseg, int64_t j) {
+  int64_t lo = 0, hi = nseg + 1;  // first index with off > j, minus one
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (off[m] <= j) lo = m + 1;
+    else hi = m;
+  }
+  return lo - 1;
+}
+__device__ __forceinline__ int64_t find_rank(const int32_t* __restrict__ a, int64_t n, int32_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (a[m] < v) lo = m + 1;
+    else hi = m;
+  }
+  return lo < n && a[lo] == v ? lo : -1;
+}
+
+__global__ __launch_bounds__(kB) void k_dv_collide(int64_t ndvk, int64_t ndv, const int32_t* __restrict__ dv_rank,
+                                                   const int64_t* __restrict__ dv_off, const int64_t* __restrict__ dv_key,
+                                                   const int32_t* __restrict__ new2old, const int64_t* __restrict__ voff,
+                                                   const int64_t* __restrict__ vkey, int64_t* __restrict__ coll) {
+  for (int64_t j = blockIdx.x * (int64_t)kB + threadIdx.x; j < ndvk; j += (int64_t)gridDim.x * kB) {
+    const int32_t u = new2old[dv_rank[seg_of(dv_off, ndv, j)]];
+    int64_t c = 0;
+    if (u >= 0) {
+      const int64_t a0 = voff[u], na = voff[u + 1] - a0, T = dv_key[j] >> 1;
+      const int64_t i = lower64(vkey + a0, na, 2 * T);
+      c = i < na && (vkey[a0 + i] >> 1) == T;
+    }
+    coll[j] = c;
+  }
+}
+
+__global__ __launch_bounds__(kB) void k_vertex_count(int64_t nv2, const int32_t* __restrict__ new2old,
+                                                     const int64_t* __restrict__ voff, int64_t ndv,
+                                                     const int32_t* __restrict__ dv_rank, const int64_t* __restrict__ dv_off,
+                                                     const int64_t* __restrict__ coll, int64_t* __restrict__ cnt) {
   for (int64_t v = blockIdx.x * (int64_t)kB + threadIdx.x; v < nv2; v += (int64_t)gridDim.x * kB) {
     const int32_t u = new2old[v];
-    const int64_t a0 = u >= 0 ? voff[u] : 0, na = u >= 0 ? voff[u + 1] - a0 : 0;
-    int64_t lo = 0, hi = ndv;
-    while (lo < hi) {
-      const int64_t m = (lo + hi) >> 1;
-      if (dv_rank[m] < v) lo = m + 1;
-      else hi = m;
+    int64_t c = u >= 0 ? voff[u + 1] - voff[u] : 0;
+    const int64_t sg = find_rank(dv_rank, ndv, (int32_t)v);
+    if (sg >= 0) c += (dv_off[sg + 1] - dv_off[sg]) - (coll[dv_off[sg + 1]] - coll[dv_off[sg]]);
+    cnt[v] = c;
+  }
+}
+
+__global__ __launch_bounds__(kB) void k_vertex_write_base(int64_t nvk_old, int64_t nv_old, const int64_t* __restrict__ voff,
+                                                          const int64_t* __restrict__ vkey, const int32_t* __restrict__ old2new,
+                                                          int64_t ndv, const int32_t* __restrict__ dv_rank,
+                                                          const int64_t* __restrict__ dv_off, const int64_t* __restrict__ dv_key,
+                                                          const int64_t* __restrict__ coll, const int64_t* __restrict__ voff2,
+                                                          int64_t* __restrict__ vkey2) {
+  for (int64_t i = blockIdx.x * (int64_t)kB + threadIdx.x; i < nvk_old; i += (int64_t)gridDim.x * kB) {
+    const int64_t u = seg_of(voff, nv_old, i);
+    const int32_t v = old2new[u];
+    const int64_t key = vkey[i], T = key >> 1;
+    int64_t blt = 0, clt = 0;
+    const int64_t sg = find_rank(dv_rank, ndv, v);
+    if (sg >= 0) {
+      const int64_t b0 = dv_off[sg], nb = dv_off[sg + 1] - b0;
+      blt = lower64(dv_key + b0, nb, 2 * T);
+      if (blt < nb && (dv_key[b0 + blt] >> 1) == T) continue;  // replaced by the delta point
+      clt = coll[b0 + blt] - coll[b0];
     }
-    const bool hit = lo < ndv && dv_rank[lo] == v;
-    const int64_t b0 = hit ? dv_off[lo] : 0, nb = hit ? dv_off[lo + 1] - b0 : 0;
-    auto keep = [](int64_t k) { return k; };
-    if (WRITE) merge_keys<true>(vkey + a0, na, dv_key + b0, nb, vkey2 + cnt_off[v], keep);
-    else cnt_off[v] = merge_keys<false>(vkey + a0, na, dv_key + b0, nb, nullptr, keep);
+    vkey2[voff2[v] + (i - voff[u]) + blt - clt] = key;
+  }
+}
+
+__global__ __launch_bounds__(kB) void k_vertex_write_delta(int64_t ndvk, int64_t ndv, const int32_t* __restrict__ dv_rank,
+                                                           const int64_t* __restrict__ dv_off, const int64_t* __restrict__ dv_key,
+                                                           const int32_t* __restrict__ new2old, const int64_t* __restrict__ voff,
+                                                           const int64_t* __restrict__ vkey, const int64_t* __restrict__ coll,
+                                                           const int64_t* __restrict__ voff2, int64_t* __restrict__ vkey2) {
+  for (int64_t j = blockIdx.x * (int64_t)kB + threadIdx.x; j < ndvk; j += (int64_t)gridDim.x * kB) {
+    const int64_t sg = seg_of(dv_off, ndv, j);
+    const int32_t v = dv_rank[sg];
+    const int32_t u = new2old[v];
+    const int64_t b0 = dv_off[sg], key = dv_key[j];
+    const int64_t alt = u >= 0 ? lower64(vkey + voff[u], voff[u + 1] - voff[u], 2 * (key >> 1)) : 0;
+    vkey2[voff2[v] + (j - b0) + alt - (coll[j] - coll[b0])] = key;
   }
 }
 
@@ -343,12 +415,22 @@ void launch_edge_hist(hipStream_t s, bool write, const MergeIn& m, int64_t ne2, 
 
 void launch_vertex_hist(hipStream_t s, bool write, const MergeIn& m, int64_t* cnt_off, int64_t* vkey2) {
   if (!m.nv2) return;
-  if (write)
-    k_vertex_hist<true><<<grid_for(m.nv2), kB, 0, s>>>(m.nv2, m.new2old, m.voff, m.vkey, m.ndv, m.dv_rank, m.dv_off,
-                                                       m.dv_key, cnt_off, vkey2);
-  else
-    k_vertex_hist<false><<<grid_for(m.nv2), kB, 0, s>>>(m.nv2, m.new2old, m.voff, m.vkey, m.ndv, m.dv_rank, m.dv_off,
-                                                        m.dv_key, cnt_off, vkey2);
+  if (!write) {  // collision flags -> exclusive prefix (m.coll[0, ndvk]), then per-vertex counts
+    if (m.ndvk) {
+      k_dv_collide<<<grid_for(m.ndvk), kB, 0, s>>>(m.ndvk, m.ndv, m.dv_rank, m.dv_off, m.dv_key, m.new2old, m.voff,
+                                                  m.vkey, m.coll);
+      launch_scan_counts(s, m.ndvk, m.coll, m.coll_tmp);
+    }
+    k_vertex_count<<<grid_for(m.nv2), kB, 0, s>>>(m.nv2, m.new2old, m.voff, m.ndv, m.dv_rank, m.dv_off, m.coll,
+                                                 cnt_off);
+    return;
+  }
+  if (m.nvk_old)
+    k_vertex_write_base<<<grid_for(m.nvk_old), kB, 0, s>>>(m.nvk_old, m.nv_old, m.voff, m.vkey, m.old2new, m.ndv,
+                                                           m.dv_rank, m.dv_off, m.dv_key, m.coll, cnt_off, vkey2);
+  if (m.ndvk)
+    k_vertex_write_delta<<<grid_for(m.ndvk), kB, 0, s>>>(m.ndvk, m.ndv, m.dv_rank, m.dv_off, m.dv_key, m.new2old,
+                                                         m.voff, m.vkey, m.coll, cnt_off, vkey2);
 }
 
 void launch_merge_in(hipStream_t s, const MergeIn& m, const int32_t* eo2n, const int32_t* npos,

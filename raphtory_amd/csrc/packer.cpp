@@ -26,6 +26,8 @@
 // chunk sort + pairwise merges; every record is then scattered by entity rank (counting
 // sort, one atomic cursor per rank) and each entity's small segment is sorted on its own.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -149,6 +151,88 @@ void sort_segments(std::vector<R>& recs, const std::vector<int64_t>& off, int nt
   std::vector<std::thread> th;
   for (int k = 0; k < nt; k++) th.emplace_back(work);
   for (auto& x : th) x.join();
+}
+
+// Stable parallel LSD radix sort of (key, val) pairs on key bits [0, bits): 11-bit digits,
+// per-thread digit histograms, each thread scattering its own contiguous input range in order.
+template <class V>
+void radix_sort_pairs(std::vector<uint64_t>& key, std::vector<V>& val, int bits, int nt) {
+  const size_t n = key.size();
+  if (n < 2 || bits <= 0) return;
+  constexpr int kD = 11;
+  constexpr size_t kNB = (size_t)1 << kD;
+  const int T = n < (1u << 16) ? 1 : nt;
+  std::vector<uint64_t> k2(n);
+  std::vector<V> v2(n);
+  std::vector<size_t> hist((size_t)T * kNB);
+  auto run = [&](auto f) {
+    if (T == 1) {
+      f(0);
+      return;
+    }
+    std::vector<std::thread> th;
+    for (int q = 0; q < T; q++) th.emplace_back([&, q] { f(q); });
+    for (auto& x : th) x.join();
+  };
+  for (int sh = 0; sh < bits; sh += kD) {
+    std::fill(hist.begin(), hist.end(), 0);
+    run([&](int q) {
+      size_t* h = hist.data() + (size_t)q * kNB;
+      for (size_t i = n * q / T, e = n * (q + 1) / T; i < e; i++) h[(key[i] >> sh) & (kNB - 1)]++;
+    });
+    size_t run_off = 0;
+    for (size_t d = 0; d < kNB; d++)
+      for (int q = 0; q < T; q++) {
+        const size_t c = hist[(size_t)q * kNB + d];
+        hist[(size_t)q * kNB + d] = run_off;
+        run_off += c;
+      }
+    run([&](int q) {
+      size_t* h = hist.data() + (size_t)q * kNB;
+      for (size_t i = n * q / T, e = n * (q + 1) / T; i < e; i++) {
+        const size_t o = h[(key[i] >> sh) & (kNB - 1)]++;
+        k2[o] = key[i];
+        v2[o] = val[i];
+      }
+    });
+    key.swap(k2);
+    val.swap(v2);
+  }
+}
+
+// Parallel build of (key, val) pairs in stream order: emit(i, out) writes the 0..M pairs of
+// item i (M = max_per) into out and returns how many; chunks are concatenated in order.
+template <class Emit>
+void build_pairs(size_t n, int nt, int max_per, std::vector<uint64_t>& key, std::vector<uint64_t>& val, Emit emit) {
+  const int T = n < 4096 ? 1 : nt;
+  std::vector<size_t> cnt(T + 1, 0);
+  parallel_for(n, nt, [&](size_t lo, size_t hi, int q) {
+    uint64_t k[4], v[4];
+    size_t c = 0;
+    for (size_t i = lo; i < hi; i++) c += emit(i, k, v);
+    cnt[q + 1] = c;
+  });
+  for (int q = 0; q < T; q++) cnt[q + 1] += cnt[q];
+  key.resize(cnt[T]);
+  val.resize(cnt[T]);
+  parallel_for(n, nt, [&](size_t lo, size_t hi, int q) {
+    uint64_t k[4], v[4];
+    size_t o = cnt[q];
+    for (size_t i = lo; i < hi; i++) {
+      const int m = emit(i, k, v);
+      for (int j = 0; j < m; j++) {
+        key[o] = k[j];
+        val[o++] = v[j];
+      }
+    }
+  });
+  (void)max_per;
+}
+
+inline int bits_for(uint64_t maxv) {
+  int b = 1;
+  while (b < 64 && (maxv >> b)) b++;
+  return b;
 }
 
 }  // namespace
@@ -424,8 +508,22 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
 // ---------------------------------------------------------------------------------------
 // Incremental seal, host half (rgpu_internal.hpp: Delta).  Delta indices are 1-based so
 // that 0 can stand for "somewhere in the base": every base put precedes every delta put.
+// RGPU_HOSTPROF=1: host phase times of the delta packer on stderr
+struct PhaseTimer {
+  const char* tag;
+  bool on = std::getenv("RGPU_HOSTPROF") && std::atoi(std::getenv("RGPU_HOSTPROF")) != 0;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void operator()(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[rgpu %s] %-12s %8.2f ms\n", tag, what, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
+
 std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed& B, Delta* out) {
   const int nt = num_threads();
+  PhaseTimer ph{"pack_delta"};
   const size_t n = ev.size() - first;
   const int64_t kMaxT = (int64_t)1 << 61;
   for (size_t i = first; i < ev.size(); i++) {
@@ -435,19 +533,48 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
     if (e.src < 0 || e.src > INT32_MAX) return "vertex id out of range [0, 2^31)";
     if (e.kind >= RGPU_EADD && (e.dst < 0 || e.dst > INT32_MAX)) return "vertex id out of range [0, 2^31)";
   }
+  ph("validate");
   Delta& D = *out;
   D = Delta();
   D.nd = (int64_t)n;
   D.nv_old = B.nv;
-  // ---- ids: new ids merged into the base order; both rank maps are monotone
-  std::vector<int64_t> ids;
-  ids.reserve(2 * n);
-  for (size_t i = first; i < ev.size(); i++) {
-    ids.push_back(ev[i].src);
-    if (ev[i].kind >= RGPU_EADD) ids.push_back(ev[i].dst);
+  // ---- ids: new ids merged into the base order; both rank maps are monotone.  Every id slot
+  // (2i = src of update i, 2i+1 = its dst) is radix-sorted by id, so the ranks are scattered
+  // back from the sorted order with no per-update search.
+  std::vector<uint64_t> sk;
+  std::vector<uint64_t> sv;
+  {
+    std::vector<size_t> cnt(nt + 1, 0);
+    parallel_for(n, nt, [&](size_t lo, size_t hi, int q) {
+      size_t c = 0;
+      for (size_t i = lo; i < hi; i++) c += ev[first + i].kind >= RGPU_EADD ? 2 : 1;
+      cnt[q + 1] = c;
+    });
+    const int used = n < 4096 ? 1 : nt;
+    for (int q = 0; q < used; q++) cnt[q + 1] += cnt[q];
+    sk.resize(cnt[used]);
+    sv.resize(cnt[used]);
+    parallel_for(n, nt, [&](size_t lo, size_t hi, int q) {
+      size_t o = cnt[q];
+      for (size_t i = lo; i < hi; i++) {
+        const Event& e = ev[first + i];
+        sk[o] = (uint64_t)e.src;
+        sv[o++] = 2 * (uint64_t)i;
+        if (e.kind >= RGPU_EADD) {
+          sk[o] = (uint64_t)e.dst;
+          sv[o++] = 2 * (uint64_t)i + 1;
+        }
+      }
+    });
   }
-  parallel_sort(ids, nt, std::less<int64_t>());
-  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+  radix_sort_pairs(sk, sv, 31, nt);
+  std::vector<int64_t> ids;  // distinct delta ids, ascending
+  std::vector<uint32_t> uidx(sk.size());  // sorted slot -> index in ids
+  for (size_t p = 0; p < sk.size(); p++) {
+    if (p == 0 || sk[p] != sk[p - 1]) ids.push_back((int64_t)sk[p]);
+    uidx[p] = (uint32_t)(ids.size() - 1);
+  }
+  ph("ids sort");
   std::vector<int64_t> nid;  // ids not in the base: one sorted walk over both
   {
     size_t a = 0;
@@ -474,6 +601,7 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
       r++;
     }
   }
+  ph("id merge");
   // merged rank of every delta id (ids ascending, so one walk), then each update's ranks by
   // a search in the delta's own id list (much smaller than the graph's)
   std::vector<int32_t> idrank(ids.size());
@@ -485,27 +613,55 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
     }
   }
   std::vector<int32_t> rs(n), rd(n, -1);
-  parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
-    for (size_t i = lo; i < hi; i++) {
-      const Event& e = ev[first + i];
-      rs[i] = idrank[std::lower_bound(ids.begin(), ids.end(), e.src) - ids.begin()];
-      if (e.kind >= RGPU_EADD) rd[i] = idrank[std::lower_bound(ids.begin(), ids.end(), e.dst) - ids.begin()];
+  parallel_for(sk.size(), nt, [&](size_t lo, size_t hi, int) {
+    for (size_t p = lo; p < hi; p++) {
+      const uint64_t slot = sv[p];
+      (slot & 1 ? rd : rs)[slot >> 1] = idrank[uidx[p]];
     }
   });
+  std::vector<uint64_t>().swap(sk);
+  std::vector<uint64_t>().swap(sv);
+  std::vector<uint32_t>().swap(uidx);
+  // times non-decreasing in stream order (the usual live case): a stable sort by entity then
+  // already leaves each entity's points in (t, idx) order
+  bool mono = true;
+  for (size_t i = 1; i < n && mono; i++) mono = ev[first + i].t >= ev[first + i - 1].t;
+  ph("ranks");
   // ---- vertex points (same records as pack_events), collapsed per (rank, t): last put wins
   {
     struct R { int32_t v; uint8_t f; int64_t t, idx; };
     std::vector<R> r;
-    r.reserve(2 * n);
-    for (size_t i = 0; i < n; i++) {
-      const Event& e = ev[first + i];
-      if (e.kind != RGPU_EDEL) r.push_back({rs[i], (uint8_t)(e.kind == RGPU_VDEL ? 0 : 1), e.t, (int64_t)i + 1});
-      if (e.kind == RGPU_EADD && rd[i] != rs[i]) r.push_back({rd[i], 1, e.t, (int64_t)i + 1});
+    if (mono) {  // radix by rank over (update, endpoint) records built in stream order
+      std::vector<uint64_t> key, val;
+      build_pairs(n, nt, 2, key, val, [&](size_t i, uint64_t* k, uint64_t* v) {
+        const uint8_t kd = ev[first + i].kind;
+        int m = 0;
+        if (kd != RGPU_EDEL) { k[m] = (uint64_t)rs[i]; v[m++] = 2 * (uint64_t)i; }
+        if (kd == RGPU_EADD && rd[i] != rs[i]) { k[m] = (uint64_t)rd[i]; v[m++] = 2 * (uint64_t)i + 1; }
+        return m;
+      });
+      radix_sort_pairs(key, val, bits_for((uint64_t)D.nv), nt);
+      r.resize(key.size());
+      parallel_for(key.size(), nt, [&](size_t lo, size_t hi, int) {
+        for (size_t p = lo; p < hi; p++) {
+          const size_t i = val[p] >> 1;
+          const Event& e = ev[first + i];
+          const uint8_t f = (val[p] & 1) ? 1 : (uint8_t)(e.kind == RGPU_VDEL ? 0 : 1);
+          r[p] = {(int32_t)key[p], f, e.t, (int64_t)i + 1};
+        }
+      });
+    } else {
+      r.reserve(2 * n);
+      for (size_t i = 0; i < n; i++) {
+        const Event& e = ev[first + i];
+        if (e.kind != RGPU_EDEL) r.push_back({rs[i], (uint8_t)(e.kind == RGPU_VDEL ? 0 : 1), e.t, (int64_t)i + 1});
+        if (e.kind == RGPU_EADD && rd[i] != rs[i]) r.push_back({rd[i], 1, e.t, (int64_t)i + 1});
+      }
+      parallel_sort(r, nt, [](const R& a, const R& b) {
+        if (a.v != b.v) return a.v < b.v;
+        return a.t != b.t ? a.t < b.t : a.idx < b.idx;
+      });
     }
-    parallel_sort(r, nt, [](const R& a, const R& b) {
-      if (a.v != b.v) return a.v < b.v;
-      return a.t != b.t ? a.t < b.t : a.idx < b.idx;
-    });
     D.dv_off.push_back(0);
     for (size_t k = 0; k < r.size(); k++) {
       if (k + 1 < r.size() && r[k + 1].v == r[k].v && r[k + 1].t == r[k].t) continue;
@@ -517,6 +673,7 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
     }
     if (!D.dv_rank.empty()) D.dv_off.push_back((int64_t)D.dv_key.size());
   }
+  ph("vpoints");
   // ---- delta deaths: distinct times per rank with the last delta index at each time
   {
     struct R { int32_t v; int64_t t, idx; };
@@ -539,19 +696,39 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
     }
     if (!D.dd_rank.empty()) D.dd_off.push_back((int64_t)D.dd_t.size());
   }
+  ph("deaths");
   // ---- delta edge points grouped by (s, d), each edge's points by (t, idx)
   {
     struct R { int32_t s, d; uint8_t f; int64_t t, idx; };
     std::vector<R> r;
-    for (size_t i = 0; i < n; i++) {
-      const Event& e = ev[first + i];
-      if (e.kind >= RGPU_EADD) r.push_back({rs[i], rd[i], (uint8_t)(e.kind == RGPU_EADD ? 1 : 0), e.t, (int64_t)i + 1});
+    if (mono) {  // radix by (s, d) = s * nv + d over the edge updates in stream order
+      std::vector<uint64_t> key, val;
+      build_pairs(n, nt, 1, key, val, [&](size_t i, uint64_t* k, uint64_t* v) {
+        if (ev[first + i].kind < RGPU_EADD) return 0;
+        k[0] = (uint64_t)rs[i] * (uint64_t)D.nv + (uint64_t)rd[i];
+        v[0] = i;
+        return 1;
+      });
+      radix_sort_pairs(key, val, bits_for((uint64_t)D.nv * (uint64_t)D.nv), nt);
+      r.resize(key.size());
+      parallel_for(key.size(), nt, [&](size_t lo, size_t hi, int) {
+        for (size_t p = lo; p < hi; p++) {
+          const size_t i = val[p];
+          const Event& e = ev[first + i];
+          r[p] = {rs[i], rd[i], (uint8_t)(e.kind == RGPU_EADD ? 1 : 0), e.t, (int64_t)i + 1};
+        }
+      });
+    } else {
+      for (size_t i = 0; i < n; i++) {
+        const Event& e = ev[first + i];
+        if (e.kind >= RGPU_EADD) r.push_back({rs[i], rd[i], (uint8_t)(e.kind == RGPU_EADD ? 1 : 0), e.t, (int64_t)i + 1});
+      }
+      parallel_sort(r, nt, [](const R& a, const R& b) {
+        if (a.s != b.s) return a.s < b.s;
+        if (a.d != b.d) return a.d < b.d;
+        return a.t != b.t ? a.t < b.t : a.idx < b.idx;
+      });
     }
-    parallel_sort(r, nt, [](const R& a, const R& b) {
-      if (a.s != b.s) return a.s < b.s;
-      if (a.d != b.d) return a.d < b.d;
-      return a.t != b.t ? a.t < b.t : a.idx < b.idx;
-    });
     D.de_poff.push_back(0);
     for (size_t k = 0; k < r.size(); k++) {
       if (k == 0 || r[k].s != r[k - 1].s || r[k].d != r[k - 1].d) {
@@ -567,11 +744,13 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
     }
     if (!r.empty()) D.de_poff.push_back((int64_t)r.size());
   }
+  ph("epoints");
   return "";
 }
 
 void finish_delta(const Packed& B, const std::vector<int32_t>& base_eid, Delta* out) {
   Delta& D = *out;
+  PhaseTimer ph{"finish_delta"};
   const int64_t nde = (int64_t)D.de_s.size();
   D.de_base = base_eid;
   // death at exactly t: the last delta index, 0 for a base death, -1 for none
@@ -592,27 +771,42 @@ void finish_delta(const Packed& B, const std::vector<int32_t>& base_eid, Delta* 
   };
   // own points: collapse equal t (last put wins), then the tie with an endpoint death at the
   // same t exactly as pack_events resolves it (x2 positions; a base edge was created at 0)
-  D.de_koff.assign(nde + 1, 0);
-  for (int64_t i = 0; i < nde; i++) {
+  // per edge: emit(i, out) writes its keys (out = nullptr: count only); counts, scan, fill
+  auto emit = [&](int64_t i, int64_t* out) -> int64_t {
     const int64_t p0 = D.de_poff[i], p1 = D.de_poff[i + 1];
     int64_t cr = 0;  // creation put: the edge's first delta update (points are in time order)
     if (base_eid[i] < 0) {
       cr = D.de_pidx[p0];
       for (int64_t k = p0; k < p1; k++) cr = std::min(cr, D.de_pidx[k]);
     }
+    int64_t m = 0;
     for (int64_t k = p0; k < p1; k++) {
       if (k + 1 < p1 && D.de_pt[k + 1] == D.de_pt[k]) continue;
-      uint8_t flag = D.de_pflag[k];
-      int64_t pd = death_at(D.de_s[i], D.de_pt[k]);
-      if (D.de_d[i] != D.de_s[i]) pd = std::max(pd, death_at(D.de_d[i], D.de_pt[k]));
-      if (pd >= 0) {
-        const int64_t pd2 = pd < cr ? 2 * cr + 1 : 2 * pd;
-        if (pd2 > 2 * D.de_pidx[k]) flag = 0;
+      if (out) {
+        uint8_t flag = D.de_pflag[k];
+        int64_t pd = death_at(D.de_s[i], D.de_pt[k]);
+        if (D.de_d[i] != D.de_s[i]) pd = std::max(pd, death_at(D.de_d[i], D.de_pt[k]));
+        if (pd >= 0) {
+          const int64_t pd2 = pd < cr ? 2 * cr + 1 : 2 * pd;
+          if (pd2 > 2 * D.de_pidx[k]) flag = 0;
+        }
+        out[m] = D.de_pt[k] * 2 + flag;
       }
-      D.de_key.push_back(D.de_pt[k] * 2 + flag);
+      m++;
     }
-    D.de_koff[i + 1] = (int64_t)D.de_key.size();
-  }
+    return m;
+  };
+  const int nt0 = num_threads();
+  D.de_koff.assign(nde + 1, 0);
+  parallel_for((size_t)nde, nt0, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; i++) D.de_koff[i + 1] = emit((int64_t)i, nullptr);
+  });
+  for (int64_t i = 0; i < nde; i++) D.de_koff[i + 1] += D.de_koff[i];
+  D.de_key.resize(D.de_koff[nde]);
+  parallel_for((size_t)nde, nt0, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; i++) emit((int64_t)i, D.de_key.data() + D.de_koff[i]);
+  });
+  ph("own keys");
   // new edges, and their in-edge records (self-loops never enter incomingEdges)
   std::vector<int64_t> outc(D.nv + 1, 0), inc(D.nv + 1, 0);
   for (int64_t i = 0; i < nde; i++) {
@@ -628,14 +822,24 @@ void finish_delta(const Packed& B, const std::vector<int32_t>& base_eid, Delta* 
     }
   }
   const int nt = num_threads();
-  {
-    std::vector<std::pair<int64_t, int32_t>> o(D.ni_key.size());
-    for (size_t k = 0; k < o.size(); k++) o[k] = {D.ni_key[k], D.ni_idx[k]};
-    parallel_sort(o, nt, [](const std::pair<int64_t, int32_t>& a, const std::pair<int64_t, int32_t>& b) {
-      return a.first < b.first;
+  {  // by (d, s) = d * nv + s (keys are distinct, so stability does not matter here)
+    const uint64_t nv = (uint64_t)D.nv;
+    std::vector<uint64_t> key(D.ni_key.size()), val(D.ni_key.size());
+    parallel_for(key.size(), nt, [&](size_t lo, size_t hi, int) {
+      for (size_t k = lo; k < hi; k++) {
+        key[k] = (uint64_t)(D.ni_key[k] >> 32) * nv + (uint64_t)(D.ni_key[k] & 0xffffffff);
+        val[k] = (uint64_t)D.ni_idx[k];
+      }
     });
-    for (size_t k = 0; k < o.size(); k++) { D.ni_key[k] = o[k].first; D.ni_idx[k] = o[k].second; }
+    radix_sort_pairs(key, val, bits_for(nv * nv), nt);
+    parallel_for(key.size(), nt, [&](size_t lo, size_t hi, int) {
+      for (size_t k = lo; k < hi; k++) {
+        D.ni_key[k] = ((int64_t)(key[k] / nv) << 32) | (int64_t)(key[k] % nv);
+        D.ni_idx[k] = (int32_t)val[k];
+      }
+    });
   }
+  ph("new edges");
   // merged offsets and death lists (O(V) host work)
   D.out_off.assign(D.nv + 1, 0);
   D.in_off.assign(D.nv + 1, 0);
@@ -655,6 +859,7 @@ void finish_delta(const Packed& B, const std::vector<int32_t>& base_eid, Delta* 
     D.out_off[v + 1] += D.out_off[v];
     D.in_off[v + 1] += D.in_off[v];
   }
+  ph("offsets");
   D.doff.assign(D.nv + 1, 0);
   D.dtime.clear();
   D.dtime.reserve(B.dtime.size() + D.dd_t.size());
@@ -678,6 +883,7 @@ void finish_delta(const Packed& B, const std::vector<int32_t>& base_eid, Delta* 
     }
     D.doff[v + 1] = (int64_t)D.dtime.size();
   }
+  ph("deaths");
 }
 
 }  // namespace rgpu

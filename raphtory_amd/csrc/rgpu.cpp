@@ -52,6 +52,8 @@ constexpr int64_t kPad = 64;  // tail padding of per-vertex / per-slot batch arr
 constexpr int kMaxSlots = 4;  // batches in flight (one HIP stream each; GPU_MAX_HW_QUEUES = 4)
 
 struct Slot {
+  // buffers allocated for this slot (slots are allocated lazily: a run uses min(slots, batches))
+  bool a_cc = false, a_deg = false, a_pr = false, h_cc = false, h_pr = false;
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   uint64_t *vm = nullptr, *em = nullptr;          // masks of the batch in flight
@@ -145,7 +147,6 @@ struct rgpu_ctx {
   // still fits keeps them: reallocating tens of GB per merge would dominate the tick)
   std::vector<void*> slot_allocs;
   int64_t cap_nv = 0, cap_ne = 0, cap_nin = 0;
-  bool hv_cc = false, hv_pr = false;    // heavy-vertex slot buffers (graph_allocs) ready
   Slot slot[kMaxSlots];
   int nslots = 2;
   bool hostflags = true;                // superstep flags via host-mapped memory (else copies)
@@ -156,7 +157,6 @@ struct rgpu_ctx {
   std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
   struct StepRec { int batch, step; unsigned long long pv, ps; int changed; };
   std::vector<StepRec> steprec;
-  bool slot_cc = false, slot_deg = false, slot_pr = false;
   bool wmajor = true;                   // RGPU_WMAJOR: window-major batches when 2 <= W <= kMaxPlanes
   bool poll = true;                     // RGPU_POLL: spin on event queries instead of blocking
   bool hostprof = false;                // RGPU_HOSTPROF: print host-side scheduling times
@@ -216,7 +216,6 @@ void release_slots(rgpu_ctx* c) {
   for (void* p : c->slot_allocs) (void)hipFree(p);
   c->slot_allocs.clear();
   c->cap_nv = c->cap_ne = c->cap_nin = 0;
-  c->hv_cc = c->hv_pr = false;  // (their buffers are in graph_allocs)
   for (Slot& s : c->slot) {
     if (s.h_stepcnt) (void)hipHostFree(s.h_stepcnt);
     if (s.h_tail) (void)hipHostFree(s.h_tail);
@@ -226,7 +225,6 @@ void release_slots(rgpu_ctx* c) {
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot();
   }
-  c->slot_cc = c->slot_deg = c->slot_pr = false;
   for (MaskSet& m : c->mset) {
     if (m.k1) (void)hipEventDestroy(m.k1);
     for (hipEvent_t e : m.done)
@@ -263,11 +261,11 @@ void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn, int step = 0
   c->st.kernel_bytes[kid] += bytes;
 }
 
-void ensure_masks(rgpu_ctx* c, int G) {
+void ensure_masks(rgpu_ctx* c, int G, int nuse) {
   auto& L = c->slot_allocs;
   const int64_t nv = c->cap_nv, ne = c->cap_ne;
   if (G == 1) {
-    for (int i = 0; i < c->nslots; i++) {
+    for (int i = 0; i < nuse; i++) {
       Slot& s = c->slot[i];
       if (!s.vm_own) {
         s.vm_own = dalloc<uint64_t>(L, nv + kPad);
@@ -290,7 +288,7 @@ void ensure_masks(rgpu_ctx* c, int G) {
   }
 }
 
-void ensure_slots(rgpu_ctx* c, int algo) {
+void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
   if (c->cap_nv < c->g.nv || c->cap_ne < c->g.ne || c->cap_nin < c->g.n_in) {
     release_slots(c);
     c->cap_nv = c->g.nv;
@@ -301,7 +299,7 @@ void ensure_slots(rgpu_ctx* c, int algo) {
   auto& LG = c->graph_allocs;  // heavy-vertex buffers: sized by the graph's segments
   const int64_t nv = c->cap_nv, ne = c->cap_ne, nin = c->cap_nin;
   const size_t rows = (size_t)nv * kViews;
-  for (int i = 0; i < c->nslots; i++) {
+  for (int i = 0; i < nuse; i++) {
     Slot& s = c->slot[i];
     if (!s.stream) {
       HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
@@ -315,7 +313,7 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       s.stepcnt = dalloc<int32_t>(L, kMaxSteps);
       s.stats = dalloc<unsigned long long>(L, kStatWords);
     }
-    if (algo == RGPU_ALGO_CC && !c->slot_cc) {
+    if (algo == RGPU_ALGO_CC && !s.a_cc) {
       // padded so that the superstep kernel's clamped, unconditional loads stay in bounds
       s.cnt = dalloc<int32_t>(L, nv + kPad);
       s.snbr = dalloc<int32_t>(L, ne + nin + kPad);
@@ -333,21 +331,21 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       s.iso = dalloc<unsigned int>(L, kIsoWords);  // zero between batches: the summary kernel clears it
       HIPCHK(hipMemset(s.iso, 0, sizeof(unsigned int) * kIsoWords));
     }
-    if (algo == RGPU_ALGO_CC && !c->hv_cc && c->g.n_seg > 0) {
+    if (algo == RGPU_ALGO_CC && !s.h_cc && c->g.n_seg > 0) {
       s.hv.segcnt = dalloc<int32_t>(LG, c->g.n_seg);
       s.hv.segor = dalloc<uint64_t>(LG, c->g.n_seg);
       s.hv.best = dalloc<int32_t>(LG, (size_t)c->g.n_heavy * kViews);  // INT32_MAX between uses
       HIPCHK(hipMemsetD32((hipDeviceptr_t)s.hv.best, INT32_MAX, (size_t)c->g.n_heavy * kViews));
     }
-    if ((algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) && !c->slot_deg) {
+    if ((algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) && !s.a_deg) {
       s.outdeg = dalloc<int32_t>(L, rows);
       s.indeg = dalloc<int32_t>(L, rows);
     }
-    if (algo == RGPU_ALGO_PR && !c->hv_pr && c->g.n_seg > 0) {
+    if (algo == RGPU_ALGO_PR && !s.h_pr && c->g.n_seg > 0) {
       s.hv.pacc = dalloc<double>(LG, (size_t)c->g.n_heavy * kViews);  // zero between uses
       HIPCHK(hipMemset(s.hv.pacc, 0, sizeof(double) * (size_t)c->g.n_heavy * kViews));
     }
-    if (algo == RGPU_ALGO_PR && !c->slot_pr) {
+    if (algo == RGPU_ALGO_PR && !s.a_pr) {
       s.pr = dalloc<double>(L, rows);
       s.contrib[0] = dalloc<double>(L, rows);
       s.contrib[1] = dalloc<double>(L, rows);
@@ -380,10 +378,13 @@ void ensure_slots(rgpu_ctx* c, int algo) {
       X.pr_ready = true;
     }
   }
-  if (algo == RGPU_ALGO_CC) c->slot_cc = c->hv_cc = true;
-  if (algo == RGPU_ALGO_PR) c->hv_pr = true;
-  if (algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) c->slot_deg = true;
-  if (algo == RGPU_ALGO_PR) c->slot_pr = true;
+  for (int i = 0; i < nuse; i++) {
+    Slot& s = c->slot[i];
+    if (algo == RGPU_ALGO_CC) s.a_cc = s.h_cc = true;
+    if (algo == RGPU_ALGO_PR) s.h_pr = true;
+    if (algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) s.a_deg = true;
+    if (algo == RGPU_ALGO_PR) s.a_pr = true;
+  }
 }
 
 struct RunCfg {
@@ -396,6 +397,12 @@ struct RunCfg {
   int64_t thr_v[kViews], thr_e[kViews];
   int chunk0, chunk;
 };
+
+// batch slots a run uses: one per batch in flight, never more than the batches it has
+int run_slots(const rgpu_ctx* c, const RunCfg& rc) {
+  const int n = (rc.flags & RGPU_RUN_SERIAL) ? 1 : c->nslots;
+  return (int)std::max<size_t>(1, std::min<size_t>((size_t)n, rc.nb));
+}
 
 // algorithmic bytes: see rgpu_stats_t.kernel_bytes
 double bytes_mask(const DevGraph& g) {
@@ -683,7 +690,7 @@ int run_impl(rgpu_ctx* c, RunCfg& rc) {
   c->st.views += (int64_t)(rc.n_hops * rc.W);
   c->st.batches += (int64_t)nb;
   size_t next = 0;
-  int nslots = (rc.flags & RGPU_RUN_SERIAL) ? 1 : c->nslots;
+  const int nslots = run_slots(c, rc);
   using clk = std::chrono::steady_clock;
   double t_block = 0;  // host time blocked on events (RGPU_HOSTPROF)
   const auto t_run = clk::now();
@@ -1012,7 +1019,7 @@ int rgpu_ingest(rgpu_ctx* c, const int64_t* t, const uint8_t* kind, const int64_
   if (n && (!t || !kind || !src)) return fail(c, RGPU_EINVAL, "null input array");
   try {
     const size_t need = c->events.size() + n;  // geometric growth: live ingest appends often
-    if (c->events.capacity() < need) c->events.reserve(std::max(need, c->events.capacity() * 3 / 2));
+    if (c->events.capacity() < need) c->events.reserve(std::max(need, c->events.capacity() * 2));
     for (size_t i = 0; i < n; i++) {
       if (kind[i] > RGPU_EDEL) return fail(c, RGPU_EINVAL, "unknown update kind");
       if (kind[i] >= RGPU_EADD && !dst) return fail(c, RGPU_EINVAL, "edge update without dst array");
@@ -1169,10 +1176,16 @@ void seal_delta(rgpu_ctx* c) {
     m.dv_rank = dupload(T, D.dv_rank);
     m.dv_off = dupload(T, D.dv_off);
     m.dv_key = dupload(T, D.dv_key);
+    m.nvk_old = B.n_vkey;
+    m.ndvk = (int64_t)D.dv_key.size();
+    m.coll = dalloc<int64_t>(T, m.ndvk + 1);
+    m.coll_tmp = dalloc<int64_t>(T, scan_tmp_words(std::max<int64_t>(m.ndvk, 1)));
     m.nni = (int64_t)D.ni_key.size();
     m.ni_key = dupload(T, D.ni_key);
     m.ni_idx = dupload(T, D.ni_idx);
 
+    HIPCHK(hipStreamSynchronize(s));
+    phase("upload");
     DevGraph g;
     g.nv = g.n_own = D.nv;
     g.ne = g0.ne + m.n_new;
@@ -1183,7 +1196,10 @@ void seal_delta(rgpu_ctx* c) {
     int32_t* mbase = dalloc<int32_t>(T, g.ne);
     int32_t* mdlt = dalloc<int32_t>(T, g.ne);
     int32_t* npos = dalloc<int32_t>(T, m.n_new);
+    phase("alloc e");
     launch_merge_edges(s, m, esrc2, edst2, eo2n, mbase, mdlt, npos);
+    HIPCHK(hipStreamSynchronize(s));
+    phase("place");
     int64_t* stmp = dalloc<int64_t>(T, scan_tmp_words(std::max(g.ne, g.nv)));
     // edge histories: count, scan, write
     int64_t* eoff2 = dalloc<int64_t>(L, g.ne + 1);
@@ -1192,16 +1208,24 @@ void seal_delta(rgpu_ctx* c) {
     int64_t nek = 0, nvk = 0;
     HIPCHK(hipMemcpyAsync(&nek, eoff2 + g.ne, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    phase("e count");
     int64_t* ekey2 = dalloc<int64_t>(L, nek);
+    phase("alloc ekey");
     launch_edge_hist(s, true, m, g.ne, mbase, mdlt, esrc2, edst2, eoff2, ekey2);
     // vertex histories
+    HIPCHK(hipStreamSynchronize(s));
+    phase("e write");
     int64_t* voff2 = dalloc<int64_t>(L, g.nv + 1);
     launch_vertex_hist(s, false, m, voff2, nullptr);
     launch_scan_counts(s, g.nv, voff2, stmp);
     HIPCHK(hipMemcpyAsync(&nvk, voff2 + g.nv, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    phase("v count");
     int64_t* vkey2 = dalloc<int64_t>(L, nvk);
+    phase("alloc vkey");
     launch_vertex_hist(s, true, m, voff2, vkey2);
+    HIPCHK(hipStreamSynchronize(s));
+    phase("hist kernels");
     // adjacency offsets (host-merged), in-edges
     int64_t* in_off2 = dupload(L, D.in_off);
     int32_t* in_eid2 = dalloc<int32_t>(L, g.n_in);
@@ -1219,26 +1243,31 @@ void seal_delta(rgpu_ctx* c) {
     g.adj_off = upload_adj(L, D.out_off, D.in_off);
     g.doff = dupload(L, D.doff);
     g.dtime = dupload(L, D.dtime);
+    HIPCHK(hipStreamSynchronize(s));
+    phase("adjacency");
     build_heavy(c, g, L, D.out_off, D.in_off);
     HIPCHK(hipStreamSynchronize(s));
-    phase("merge");
+    phase("heavy");
     for (void* p : T) (void)hipFree(p);
     T.clear();
     (void)hipStreamDestroy(s);
     s = nullptr;
     // swap in the merged graph; batch slots and mask sets stay if they fit (else they are
-    // reallocated on the next run with 25 % headroom for the ticks to come)
+    // reallocated on the next run with 2x headroom for the ticks to come)
+    phase("free temps");
     for (void* p : c->graph_allocs) (void)hipFree(p);
     c->graph_allocs.swap(L);
     L.clear();
     c->g = g;
-    c->hv_cc = c->hv_pr = false;
-    for (Slot& sl : c->slot) sl.hv = HeavyBuf();
+    for (Slot& sl : c->slot) {
+      sl.hv = HeavyBuf();
+      sl.h_cc = sl.h_pr = false;
+    }
     if (g.nv > c->cap_nv || g.ne > c->cap_ne || g.n_in > c->cap_nin) {
       release_slots(c);
-      c->cap_nv = g.nv + g.nv / 4;
-      c->cap_ne = g.ne + g.ne / 4;
-      c->cap_nin = g.n_in + g.n_in / 4;
+      c->cap_nv = 2 * g.nv;  // doubling: a growing live graph re-allocates O(log) times
+      c->cap_ne = 2 * g.ne;
+      c->cap_nin = 2 * g.n_in;
     } else {
       for (int i = 0; i < c->nslots; i++) {  // per-rank state that K2 does not rewrite
         Slot& sl = c->slot[i];
@@ -1390,8 +1419,10 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   rc.flags = flags;
   rc.W = n_w ? (int)n_w : 1;
   // window-major batches when they pay: each window's views in their own batches (64 hops),
-  // so the cheap short windows no longer ride along the long windows' supersteps
-  const bool wm = c->wmajor && !c->partitioned && rc.W >= 2 && rc.W <= kMaxPlanes;
+  // so the cheap short windows no longer ride along the long windows' supersteps (not when all
+  // views fit one hop-major batch, e.g. a live query of the newest hop)
+  const bool wm = c->wmajor && !c->partitioned && rc.W >= 2 && rc.W <= kMaxPlanes &&
+                  n_hops * (size_t)rc.W > (size_t)kViews;  // else one hop-major batch holds every view
   rc.G = wm ? rc.W : 1;
   rc.gsize = wm ? 1 : rc.W;
   rc.K = kViews / rc.gsize;
@@ -1416,8 +1447,16 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   rc.chunk = std::max(1, env_int("RGPU_CHUNK", 8));
   try {
     HIPCHK(hipSetDevice(c->device));
-    ensure_slots(c, algo);
-    ensure_masks(c, rc.G);
+    {
+      const auto ta = std::chrono::steady_clock::now();
+      ensure_slots(c, algo, run_slots(c, rc));
+      ensure_masks(c, rc.G, run_slots(c, rc));
+      if (c->hostprof) {
+        HIPCHK(hipDeviceSynchronize());
+        std::fprintf(stderr, "rgpu hostprof: ensure buffers %.2f ms\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count());
+      }
+    }
     const size_t nb = rc.nb;
     c->algo = algo;
     c->K = rc.K;
