@@ -567,7 +567,9 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
       }
     });
   }
+  ph("ids build");
   radix_sort_pairs(sk, sv, 31, nt);
+  ph("i radix");
   std::vector<int64_t> ids;  // distinct delta ids, ascending
   std::vector<uint32_t> uidx(sk.size());  // sorted slot -> index in ids
   for (size_t p = 0; p < sk.size(); p++) {
@@ -575,43 +577,46 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
     uidx[p] = (uint32_t)(ids.size() - 1);
   }
   ph("ids sort");
-  std::vector<int64_t> nid;  // ids not in the base: one sorted walk over both
-  {
-    size_t a = 0;
-    for (int64_t x : ids) {
-      while (a < B.vid.size() && B.vid[a] < x) a++;
-      if (a == B.vid.size() || B.vid[a] != x) nid.push_back(x);
-    }
-  }
+  // ids not in the base (parallel searches), then both rank maps by position formulas: base
+  // id a lands at a + #(new ids below it), new id j at j + #(base ids below it)
+  std::vector<uint8_t> isnew(ids.size());
+  parallel_for(ids.size(), nt, [&](size_t lo, size_t hi, int) {
+    for (size_t k = lo; k < hi; k++) isnew[k] = !std::binary_search(B.vid.begin(), B.vid.end(), ids[k]);
+  });
+  std::vector<int64_t> nid;
+  for (size_t k = 0; k < ids.size(); k++)
+    if (isnew[k]) nid.push_back(ids[k]);
   D.nv = B.nv + (int64_t)nid.size();
   D.vid.resize(D.nv);
   D.old2new.resize(B.nv);
   D.new2old.assign(D.nv, -1);
-  {
-    int64_t a = 0, b = 0, r = 0;
-    while (a < B.nv || b < (int64_t)nid.size()) {
-      if (b == (int64_t)nid.size() || (a < B.nv && B.vid[a] < nid[b])) {
-        D.vid[r] = B.vid[a];
-        D.old2new[a] = (int32_t)r;
-        D.new2old[r] = (int32_t)a;
-        a++;
-      } else {
-        D.vid[r] = nid[b++];
-      }
-      r++;
+  parallel_for((size_t)B.nv, nt, [&](size_t lo, size_t hi, int) {
+    if (lo >= hi) return;
+    size_t b = std::lower_bound(nid.begin(), nid.end(), B.vid[lo]) - nid.begin();
+    for (size_t a = lo; a < hi; a++) {
+      while (b < nid.size() && nid[b] < B.vid[a]) b++;
+      const size_t r = a + b;
+      D.vid[r] = B.vid[a];
+      D.old2new[a] = (int32_t)r;
+      D.new2old[r] = (int32_t)a;
     }
-  }
+  });
+  parallel_for(nid.size(), nt, [&](size_t lo, size_t hi, int) {
+    for (size_t j = lo; j < hi; j++)
+      D.vid[j + (std::lower_bound(B.vid.begin(), B.vid.end(), nid[j]) - B.vid.begin())] = nid[j];
+  });
   ph("id merge");
   // merged rank of every delta id (ids ascending, so one walk), then each update's ranks by
   // a search in the delta's own id list (much smaller than the graph's)
   std::vector<int32_t> idrank(ids.size());
-  {
-    size_t r = 0;
-    for (size_t k = 0; k < ids.size(); k++) {
+  parallel_for(ids.size(), nt, [&](size_t lo, size_t hi, int) {
+    if (lo >= hi) return;
+    size_t r = std::lower_bound(D.vid.begin(), D.vid.end(), ids[lo]) - D.vid.begin();
+    for (size_t k = lo; k < hi; k++) {
       while (D.vid[r] < ids[k]) r++;
       idrank[k] = (int32_t)r;
     }
-  }
+  });
   std::vector<int32_t> rs(n), rd(n, -1);
   parallel_for(sk.size(), nt, [&](size_t lo, size_t hi, int) {
     for (size_t p = lo; p < hi; p++) {
@@ -640,7 +645,9 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
         if (kd == RGPU_EADD && rd[i] != rs[i]) { k[m] = (uint64_t)rd[i]; v[m++] = 2 * (uint64_t)i + 1; }
         return m;
       });
+  ph("v build");
       radix_sort_pairs(key, val, bits_for((uint64_t)D.nv), nt);
+  ph("v radix");
       r.resize(key.size());
       parallel_for(key.size(), nt, [&](size_t lo, size_t hi, int) {
         for (size_t p = lo; p < hi; p++) {
@@ -662,16 +669,42 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
         return a.t != b.t ? a.t < b.t : a.idx < b.idx;
       });
     }
-    D.dv_off.push_back(0);
-    for (size_t k = 0; k < r.size(); k++) {
-      if (k + 1 < r.size() && r[k + 1].v == r[k].v && r[k + 1].t == r[k].t) continue;
-      if (D.dv_rank.empty() || D.dv_rank.back() != r[k].v) {
-        if (!D.dv_rank.empty()) D.dv_off.push_back((int64_t)D.dv_key.size());
-        D.dv_rank.push_back(r[k].v);
+    ph("v fill");
+    // collapse equal (rank, t) to the last put; one group per rank run (the last record of a
+    // run is always kept).  Parallel: per-chunk counts of kept records and run starts, then fill.
+    const size_t nr = r.size();
+    auto kept = [&](size_t k) { return !(k + 1 < nr && r[k + 1].v == r[k].v && r[k + 1].t == r[k].t); };
+    auto start = [&](size_t k) { return k == 0 || r[k - 1].v != r[k].v; };
+    const int T = nr < 4096 ? 1 : nt;
+    std::vector<size_t> ck(T + 1, 0), cg(T + 1, 0);
+    parallel_for(nr, nt, [&](size_t lo, size_t hi, int q) {  // (local sums: no false sharing)
+      size_t a = 0, g = 0;
+      for (size_t k = lo; k < hi; k++) {
+        a += kept(k);
+        g += start(k);
       }
-      D.dv_key.push_back(r[k].t * 2 + r[k].f);
+      ck[q + 1] = a;
+      cg[q + 1] = g;
+    });
+    for (int q = 0; q < T; q++) {
+      ck[q + 1] += ck[q];
+      cg[q + 1] += cg[q];
     }
-    if (!D.dv_rank.empty()) D.dv_off.push_back((int64_t)D.dv_key.size());
+    D.dv_key.resize(ck[T]);
+    D.dv_rank.resize(cg[T]);
+    D.dv_off.resize(cg[T] + 1);
+    parallel_for(nr, nt, [&](size_t lo, size_t hi, int q) {
+      size_t a = ck[q], g = cg[q];
+      for (size_t k = lo; k < hi; k++) {
+        if (start(k)) {
+          D.dv_rank[g] = r[k].v;
+          D.dv_off[g++] = (int64_t)a;
+        }
+        if (kept(k)) D.dv_key[a++] = r[k].t * 2 + r[k].f;
+      }
+    });
+    D.dv_off[cg[T]] = (int64_t)ck[T];
+    if (nr == 0) D.dv_off.assign(1, 0);
   }
   ph("vpoints");
   // ---- delta deaths: distinct times per rank with the last delta index at each time
@@ -709,7 +742,9 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
         v[0] = i;
         return 1;
       });
+  ph("e build");
       radix_sort_pairs(key, val, bits_for((uint64_t)D.nv * (uint64_t)D.nv), nt);
+  ph("e radix");
       r.resize(key.size());
       parallel_for(key.size(), nt, [&](size_t lo, size_t hi, int) {
         for (size_t p = lo; p < hi; p++) {
@@ -729,20 +764,44 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
         return a.t != b.t ? a.t < b.t : a.idx < b.idx;
       });
     }
-    D.de_poff.push_back(0);
-    for (size_t k = 0; k < r.size(); k++) {
-      if (k == 0 || r[k].s != r[k - 1].s || r[k].d != r[k - 1].d) {
-        if (k) D.de_poff.push_back((int64_t)k);
-        D.de_s.push_back(r[k].s);
-        D.de_d.push_back(r[k].d);
-        D.de_qs.push_back(D.new2old[r[k].s]);
-        D.de_qd.push_back(D.new2old[r[k].d]);
+    ph("e fill");
+    // one group per distinct (s, d); every point is kept.  Parallel counts of group starts, fill.
+    const size_t nr = r.size();
+    auto start = [&](size_t k) { return k == 0 || r[k].s != r[k - 1].s || r[k].d != r[k - 1].d; };
+    const int T = nr < 4096 ? 1 : nt;
+    std::vector<size_t> cg(T + 1, 0);
+    parallel_for(nr, nt, [&](size_t lo, size_t hi, int q) {
+      size_t g = 0;
+      for (size_t k = lo; k < hi; k++) g += start(k);
+      cg[q + 1] = g;
+    });
+    for (int q = 0; q < T; q++) cg[q + 1] += cg[q];
+    const size_t ng = cg[T];
+    D.de_s.resize(ng);
+    D.de_d.resize(ng);
+    D.de_qs.resize(ng);
+    D.de_qd.resize(ng);
+    D.de_poff.resize(ng + 1);
+    D.de_pt.resize(nr);
+    D.de_pidx.resize(nr);
+    D.de_pflag.resize(nr);
+    parallel_for(nr, nt, [&](size_t lo, size_t hi, int q) {
+      size_t g = cg[q];
+      for (size_t k = lo; k < hi; k++) {
+        if (start(k)) {
+          D.de_s[g] = r[k].s;
+          D.de_d[g] = r[k].d;
+          D.de_qs[g] = D.new2old[r[k].s];
+          D.de_qd[g] = D.new2old[r[k].d];
+          D.de_poff[g++] = (int64_t)k;
+        }
+        D.de_pt[k] = r[k].t;
+        D.de_pidx[k] = r[k].idx;
+        D.de_pflag[k] = r[k].f;
       }
-      D.de_pt.push_back(r[k].t);
-      D.de_pidx.push_back(r[k].idx);
-      D.de_pflag.push_back(r[k].f);
-    }
-    if (!r.empty()) D.de_poff.push_back((int64_t)r.size());
+    });
+    D.de_poff[ng] = (int64_t)nr;
+    if (nr == 0) D.de_poff.assign(1, 0);
   }
   ph("epoints");
   return "";
@@ -808,18 +867,41 @@ void finish_delta(const Packed& B, const std::vector<int32_t>& base_eid, Delta* 
   });
   ph("own keys");
   // new edges, and their in-edge records (self-loops never enter incomingEdges)
-  std::vector<int64_t> outc(D.nv + 1, 0), inc(D.nv + 1, 0);
-  for (int64_t i = 0; i < nde; i++) {
-    if (base_eid[i] >= 0) continue;
-    const int32_t s = D.de_s[i], d = D.de_d[i];
-    D.nn_key.push_back(((int64_t)s << 32) | d);
-    D.nn_didx.push_back((int32_t)i);
-    outc[s + 1]++;
-    if (s != d) {
-      D.ni_key.push_back(((int64_t)d << 32) | s);
-      D.ni_idx.push_back((int32_t)D.nn_key.size() - 1);
-      inc[d + 1]++;
+  {  // in delta-edge order, i.e. (s, d) ascending: per-chunk counts, then a parallel fill
+    const int T = nde < 4096 ? 1 : nt0;
+    std::vector<size_t> cn(T + 1, 0), ci(T + 1, 0);
+    parallel_for((size_t)nde, nt0, [&](size_t lo, size_t hi, int q) {  // (local sums)
+      size_t a = 0, b = 0;
+      for (size_t i = lo; i < hi; i++)
+        if (base_eid[i] < 0) {
+          a++;
+          b += D.de_s[i] != D.de_d[i];
+        }
+      cn[q + 1] = a;
+      ci[q + 1] = b;
+    });
+    for (int q = 0; q < T; q++) {
+      cn[q + 1] += cn[q];
+      ci[q + 1] += ci[q];
     }
+    D.nn_key.resize(cn[T]);
+    D.nn_didx.resize(cn[T]);
+    D.ni_key.resize(ci[T]);
+    D.ni_idx.resize(ci[T]);
+    parallel_for((size_t)nde, nt0, [&](size_t lo, size_t hi, int q) {
+      size_t a = cn[q], b = ci[q];
+      for (size_t i = lo; i < hi; i++) {
+        if (base_eid[i] >= 0) continue;
+        const int32_t s = D.de_s[i], d = D.de_d[i];
+        D.nn_key[a] = ((int64_t)s << 32) | d;
+        D.nn_didx[a] = (int32_t)i;
+        if (s != d) {
+          D.ni_key[b] = ((int64_t)d << 32) | s;
+          D.ni_idx[b++] = (int32_t)a;
+        }
+        a++;
+      }
+    });
   }
   const int nt = num_threads();
   {  // by (d, s) = d * nv + s (keys are distinct, so stability does not matter here)
@@ -844,9 +926,15 @@ void finish_delta(const Packed& B, const std::vector<int32_t>& base_eid, Delta* 
   D.out_off.assign(D.nv + 1, 0);
   D.in_off.assign(D.nv + 1, 0);
   parallel_for((size_t)D.nv, nt, [&](size_t lo, size_t hi, int) {  // counts, then one prefix pass
+    if (lo >= hi) return;
+    // new out-edges of v: its run in nn_key ((s, d) ascending); new in-edges: its run in ni_key
+    size_t po = std::lower_bound(D.nn_key.begin(), D.nn_key.end(), (int64_t)lo << 32) - D.nn_key.begin();
+    size_t pi = std::lower_bound(D.ni_key.begin(), D.ni_key.end(), (int64_t)lo << 32) - D.ni_key.begin();
     for (size_t v = lo; v < hi; v++) {
       const int32_t u = D.new2old[v];
-      int64_t oc = outc[v + 1], ic = inc[v + 1];
+      int64_t oc = 0, ic = 0;
+      for (; po < D.nn_key.size() && (size_t)(D.nn_key[po] >> 32) == v; po++) oc++;
+      for (; pi < D.ni_key.size() && (size_t)(D.ni_key[pi] >> 32) == v; pi++) ic++;
       if (u >= 0) {
         oc += B.out_off[u + 1] - B.out_off[u];
         ic += B.in_off[u + 1] - B.in_off[u];
