@@ -153,14 +153,15 @@ void sort_segments(std::vector<R>& recs, const std::vector<int64_t>& off, int nt
   for (auto& x : th) x.join();
 }
 
-// Stable parallel LSD radix sort of (key, val) pairs on key bits [0, bits): 11-bit digits,
+// Stable parallel LSD radix sort of (key, val) pairs on key bits [0, bits): <= 12-bit digits,
 // per-thread digit histograms, each thread scattering its own contiguous input range in order.
 template <class V>
 void radix_sort_pairs(std::vector<uint64_t>& key, std::vector<V>& val, int bits, int nt) {
   const size_t n = key.size();
   if (n < 2 || bits <= 0) return;
-  constexpr int kD = 11;
-  constexpr size_t kNB = (size_t)1 << kD;
+  const int passes = (bits + 11) / 12;                // digits of at most 12 bits, as few passes as
+  const int kD = (bits + passes - 1) / passes;         // possible (24-bit ranks: 2 x 12, 31-bit ids: 3 x 11)
+  const size_t kNB = (size_t)1 << kD;
   const int T = n < (1u << 16) ? 1 : nt;
   std::vector<uint64_t> k2(n);
   std::vector<V> v2(n);
@@ -943,9 +944,30 @@ void finish_delta(const Packed& B, const std::vector<int32_t>& base_eid, Delta* 
       D.in_off[v + 1] = ic;
     }
   });
-  for (int64_t v = 0; v < D.nv; v++) {
-    D.out_off[v + 1] += D.out_off[v];
-    D.in_off[v + 1] += D.in_off[v];
+  {  // two-level parallel prefix: chunk totals, then each chunk adds its offset
+    const int T = D.nv < 4096 ? 1 : nt;
+    std::vector<int64_t> to(T + 1, 0), ti(T + 1, 0);
+    parallel_for((size_t)D.nv, nt, [&](size_t lo, size_t hi, int q) {
+      int64_t a = 0, b = 0;
+      for (size_t v = lo; v < hi; v++) {
+        a += D.out_off[v + 1];
+        b += D.in_off[v + 1];
+        D.out_off[v + 1] = a;
+        D.in_off[v + 1] = b;
+      }
+      to[q + 1] = a;
+      ti[q + 1] = b;
+    });
+    for (int q = 0; q < T; q++) {
+      to[q + 1] += to[q];
+      ti[q + 1] += ti[q];
+    }
+    parallel_for((size_t)D.nv, nt, [&](size_t lo, size_t hi, int q) {
+      for (size_t v = lo; v < hi; v++) {
+        D.out_off[v + 1] += to[q];
+        D.in_off[v + 1] += ti[q];
+      }
+    });
   }
   ph("offsets");
   D.doff.assign(D.nv + 1, 0);
