@@ -1092,7 +1092,8 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
 // its four waves split the views (wave w takes views j = w mod 4): per view the 64 vertices
 // sit on the lanes and each distinct label is added once per chunk (popcount of the lanes
 // that carry it), so the giant component costs one atomic per 64 vertices, not one per
-// vertex.  The per-view loop is serial, latency-bound work: one chunk per block keeps ~24
+// vertex.  The dedup loop is serial (a ballot per distinct label), so after `rounds` labels
+// the remaining lanes (small components) issue their own atomics in one instruction.  The per-view loop is serial, latency-bound work: one chunk per block keeps ~24
 // waves per CU on it (one chunk per wave kept ~6).
 // Members with no kept slot in a view are isolated there: islands (count 1) that need no
 // histogram entry.  Their counts go to iso[shard][view] (64 shards: a few dozen blocks per
@@ -1103,7 +1104,7 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int64_t hstride, in
                                                  const uint64_t* __restrict__ vadj,
                                                  const int32_t* __restrict__ lab,
                                                  int32_t* __restrict__ hist,
-                                                 unsigned int* __restrict__ iso_g) {
+                                                 unsigned int* __restrict__ iso_g, int rounds) {
   __shared__ int32_t tile[64][65];
   __shared__ unsigned int iso[64];
   if (threadIdx.x < 64) iso[threadIdx.x] = 0;
@@ -1142,7 +1143,11 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int64_t hstride, in
       if (lane == 0 && isolated) iso[j] += (unsigned)__popcll(isolated);  // view j: this wave only
       const int32_t l = tile[lane][j];
       uint64_t todo = __ballot(member);
-      while (todo) {
+      for (int it = 0; todo; it++) {
+        if (it == rounds) {  // the rest: one atomic per lane, all issued at once
+          if ((todo >> lane) & 1) atomicAdd(&hist[(int64_t)j * hstride + l], 1);
+          break;
+        }
         const int leader = __builtin_ctzll(todo);
         const int32_t L = __builtin_amdgcn_readlane(l, leader);
         const uint64_t same = __ballot(member && l == L);
@@ -1703,6 +1708,7 @@ __global__ __launch_bounds__(256) void k_cc_summary_rs(const int32_t* __restrict
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
 int g_rowbuf = 0;
+int g_hist_rounds = 4;  // (C2: 64 rounds 145 ms, 4 rounds 138 ms; 1 round 147 ms)
 int g_tail_step = 14;
 int g_tail_grid = 1024;
 
@@ -1799,8 +1805,8 @@ void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g,
 void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso) {
   const unsigned grid = grid_for(nv, 64, 8192);
-  if (g_rowbuf) k_cc_hist<true><<<grid, 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso);
-  else k_cc_hist<false><<<grid, 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso);
+  if (g_rowbuf) k_cc_hist<true><<<grid, 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso, g_hist_rounds);
+  else k_cc_hist<false><<<grid, 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso, g_hist_rounds);
 }
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
                        unsigned long long* stats, unsigned int* iso) {
