@@ -1708,6 +1708,7 @@ __global__ __launch_bounds__(256) void k_cc_summary_rs(const int32_t* __restrict
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
 int g_rowbuf = 0;
+int g_sum_blocks = 32;  // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 int g_hist_rounds = 4;  // (C2: 64 rounds 145 ms, 4 rounds 138 ms; 1 round 147 ms)
 int g_tail_step = 14;
 int g_tail_grid = 1024;
@@ -1810,7 +1811,7 @@ void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, cons
 }
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
                        unsigned long long* stats, unsigned int* iso) {
-  dim3 grid(grid_for(g.nv, 256, 32), (unsigned)nviews);
+  dim3 grid(grid_for(g.nv, 256, (unsigned)g_sum_blocks), (unsigned)nviews);
   k_cc_summary<<<grid, 256, 0, s>>>(g.nv, hist, stats, iso);
 }
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,

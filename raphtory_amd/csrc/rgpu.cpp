@@ -994,6 +994,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   if (env_int("RGPU_STEP_GRID", 0) > 0) g_step_grid = env_int("RGPU_STEP_GRID", 0);
   if (env_int("RGPU_HIST_ROUNDS", 0) > 0) g_hist_rounds = env_int("RGPU_HIST_ROUNDS", 0);
+  if (env_int("RGPU_SUMMARY_BLOCKS", 0) > 0) g_sum_blocks = env_int("RGPU_SUMMARY_BLOCKS", 0);
   g_rowbuf = env_int("RGPU_ROWBUF", 0);
   if (env_int("RGPU_TAIL_STEP", 0) > 0) g_tail_step = env_int("RGPU_TAIL_STEP", 0);
   if (env_int("RGPU_TAIL_GRID", 0) > 0) g_tail_grid = env_int("RGPU_TAIL_GRID", 0);
