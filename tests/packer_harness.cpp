@@ -87,3 +87,65 @@ extern "C" int ph_alive(void* h, int is_edge, int64_t src, int64_t dst, int64_t 
   if (last_death(p, (int32_t)rs, t) > ft || last_death(p, (int32_t)rd, t) > ft) return 0;
   return t - ft <= w;
 }
+
+// Live-ingest host half (packer.cpp pack_delta / finish_delta) against a one-shot pack of the
+// same stream: base = updates [0, cut), delta = [cut, n).  The base-edge lookup that the device
+// does (k_edge_find) is done here by binary search.  Checks the merged ids, rank maps, adjacency
+// offsets, death lists, the merged edge set, and every vertex history merged as merge.hip's
+// position formulas define it (base and delta by time, the delta point winning a tie).
+// Returns 0, or the number of the first failed check.
+extern "C" int ph_delta_check(const int64_t* t, const uint8_t* kind, const int64_t* src, const int64_t* dst,
+                              size_t n, size_t cut) {
+  std::vector<Event> ev(n);
+  for (size_t i = 0; i < n; i++) ev[i] = {t[i], src[i], kind[i] >= 2 ? dst[i] : -1, kind[i]};
+  std::vector<Event> head(ev.begin(), ev.begin() + cut);
+  Packed B, F;
+  if (!rgpu::pack_events(head, 0, 1, &B).empty() || !rgpu::pack_events(ev, 0, 1, &F).empty()) return 1;
+  rgpu::Delta D;
+  if (!rgpu::pack_delta(ev, cut, B, &D).empty()) return 2;
+  std::vector<int32_t> base_eid(D.de_s.size(), -1);
+  for (size_t i = 0; i < D.de_s.size(); i++) {
+    const int32_t qs = D.de_qs[i], qd = D.de_qd[i];
+    if (qs < 0 || qd < 0) continue;
+    auto lo = B.edst.begin() + B.out_off[qs], hi = B.edst.begin() + B.out_off[qs + 1];
+    auto it = std::lower_bound(lo, hi, qd);
+    if (it != hi && *it == qd) base_eid[i] = (int32_t)(it - B.edst.begin());
+  }
+  rgpu::finish_delta(B, base_eid, &D);
+  if (D.nv != F.nv || D.vid != F.vid) return 3;
+  for (int64_t a = 0; a < B.nv; a++)
+    if (D.vid[D.old2new[a]] != B.vid[a] || D.new2old[D.old2new[a]] != a) return 4;
+  if (D.out_off != F.out_off || D.in_off != F.in_off) return 5;
+  if (D.doff != F.doff || D.dtime != F.dtime) return 6;
+  // merged edge set: base edges (remapped) + new edges == the one-shot pack's edges
+  std::vector<int64_t> keys;
+  for (int64_t e = 0; e < B.ne; e++)
+    keys.push_back(((int64_t)D.old2new[B.esrc[e]] << 32) | D.old2new[B.edst[e]]);
+  for (int64_t k : D.nn_key) keys.push_back(k);
+  std::sort(keys.begin(), keys.end());
+  if ((int64_t)keys.size() != F.ne) return 7;
+  for (int64_t e = 0; e < F.ne; e++)
+    if (keys[e] != (((int64_t)F.esrc[e] << 32) | F.edst[e])) return 8;
+  // vertex histories
+  for (int64_t v = 0; v < D.nv; v++) {
+    std::vector<int64_t> a, b, m;
+    const int32_t u = D.new2old[v];
+    if (u >= 0) a.assign(B.vkey.begin() + B.voff[u], B.vkey.begin() + B.voff[u + 1]);
+    auto it = std::lower_bound(D.dv_rank.begin(), D.dv_rank.end(), (int32_t)v);
+    if (it != D.dv_rank.end() && *it == v) {
+      const size_t g = it - D.dv_rank.begin();
+      b.assign(D.dv_key.begin() + D.dv_off[g], D.dv_key.begin() + D.dv_off[g + 1]);
+    }
+    size_t i = 0, j = 0;
+    while (i < a.size() || j < b.size()) {
+      if (j == b.size() || (i < a.size() && (a[i] >> 1) < (b[j] >> 1))) m.push_back(a[i++]);
+      else {
+        if (i < a.size() && (a[i] >> 1) == (b[j] >> 1)) i++;
+        m.push_back(b[j++]);
+      }
+    }
+    if (!std::equal(m.begin(), m.end(), F.vkey.begin() + F.voff[v]) || (int64_t)m.size() != F.voff[v + 1] - F.voff[v])
+      return 9;
+  }
+  return 0;
+}

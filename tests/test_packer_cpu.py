@@ -7,7 +7,7 @@ import pytest
 
 from oracle import Oracle
 
-from harness import load_packer_harness, pack
+from harness import P64, PU8, load_packer_harness, pack
 
 
 @pytest.fixture(scope="module")
@@ -67,3 +67,21 @@ def test_parallel_pack_is_deterministic(ph, monkeypatch):
             assert ph.ph_alive(h1, 0, v, -1, tt, 3000) == ph.ph_alive(h8, 0, v, -1, tt, 3000)
     ph.ph_free(h1)
     ph.ph_free(h8)
+
+
+@pytest.mark.parametrize("seed,tie,shuffle,threads,frac,n", [(11, 1, False, "1", 0.5, 40_000),
+                                                             (12, 4, False, "8", 0.7, 40_000),
+                                                             (13, 3, True, "8", 0.4, 40_000),
+                                                             (14, 2, True, "1", 0.9, 40_000),
+                                                             (15, 2, False, "8", 0.3, 200_000)])
+def test_live_delta_host_half_matches_one_shot_pack(ph, seed, tie, shuffle, threads, frac, n, monkeypatch):
+    """pack_delta + finish_delta (live ingest) vs pack_events of the whole stream:
+    ids, rank maps, offsets, death lists, edge set and merged vertex histories.  Cuts fall
+    inside groups of equal times; the shuffled streams exercise the non-monotone fallback,
+    the ordered ones the radix path (8 threads: multi-chunk parallel code; 200k updates: the
+    multi-threaded radix passes)."""
+    monkeypatch.setenv("RGPU_THREADS", threads)
+    t, k, s, d = _stream(seed, n, 3_000 if n < 100_000 else 20_000, tie, shuffle)
+    rc = ph.ph_delta_check(t.ctypes.data_as(P64), k.ctypes.data_as(PU8), s.ctypes.data_as(P64),
+                           d.ctypes.data_as(P64), len(t), int(len(t) * frac))
+    assert rc == 0, f"check {rc} failed"
