@@ -418,6 +418,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     const int64_t nout = o1 - o0, ntot = nout + (i1 - i0), base = o0 + i0;
     int32_t count = 0, best = me;
     uint64_t any = 0;
+    uint64_t m_keep = 0;  // ntot <= 64: this lane's slot stays in registers for the marking below
+    int32_t nb_keep = 0;
     for (int64_t c = 0; c < ntot; c += 64) {
       const int64_t j = c + lane;
       uint64_t m = 0;
@@ -436,6 +438,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         smask[pos] = m;
       }
       count += __popcll(bal);
+      m_keep = m;
+      nb_keep = nb;
       if (!own) continue;
       while (bal) {  // superstep 1: neighbours' labels are their own ranks
         const int L = __builtin_ctzll(bal);
@@ -453,9 +457,13 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     if (ch) {
       changed++;
       if (lane == 0) act2[v] = 1;
-      for (int32_t c = 0; c < count; c += 64) {
-        const int32_t j = c + lane;
-        if (j < count && (smask[base + j] & ch)) act2[snbr[base + j]] = 1;
+      if (ntot <= 64) {  // one slot chunk: mark from registers, no re-read of the stored slots
+        if (m_keep & ch) act2[nb_keep] = 1;
+      } else {
+        for (int32_t c = 0; c < count; c += 64) {
+          const int32_t j = c + lane;
+          if (j < count && (smask[base + j] & ch)) act2[snbr[base + j]] = 1;
+        }
       }
     }
     members += 1;
