@@ -621,6 +621,7 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
   std::vector<int32_t> rs(n), rd(n, -1);
   parallel_for(sk.size(), nt, [&](size_t lo, size_t hi, int) {
     for (size_t p = lo; p < hi; p++) {
+      if (p + 16 < hi) __builtin_prefetch(&(sv[p + 16] & 1 ? rd : rs)[sv[p + 16] >> 1], 1);
       const uint64_t slot = sv[p];
       (slot & 1 ? rd : rs)[slot >> 1] = idrank[uidx[p]];
     }
@@ -652,6 +653,7 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
       r.resize(key.size());
       parallel_for(key.size(), nt, [&](size_t lo, size_t hi, int) {
         for (size_t p = lo; p < hi; p++) {
+          if (p + 16 < hi) __builtin_prefetch(&ev[first + (val[p + 16] >> 1)]);  // random gathers: keep 16 in flight
           const size_t i = val[p] >> 1;
           const Event& e = ev[first + i];
           const uint8_t f = (val[p] & 1) ? 1 : (uint8_t)(e.kind == RGPU_VDEL ? 0 : 1);
@@ -749,6 +751,7 @@ std::string pack_delta(const std::vector<Event>& ev, size_t first, const Packed&
       r.resize(key.size());
       parallel_for(key.size(), nt, [&](size_t lo, size_t hi, int) {
         for (size_t p = lo; p < hi; p++) {
+          if (p + 16 < hi) __builtin_prefetch(&ev[first + val[p + 16]]);
           const size_t i = val[p];
           const Event& e = ev[first + i];
           r[p] = {rs[i], rd[i], (uint8_t)(e.kind == RGPU_EADD ? 1 : 0), e.t, (int64_t)i + 1};
