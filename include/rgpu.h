@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RGPU_ABI_VERSION 4
+#define RGPU_ABI_VERSION 5
 
 /* error codes */
 #define RGPU_OK 0
@@ -47,6 +47,7 @@ extern "C" {
 #define RGPU_ALGO_CC 0     /* S/core/analysis/Algorithms/ConnectedComponents.scala */
 #define RGPU_ALGO_DEGREE 1 /* S/core/analysis/Algorithms/DegreeBasic.scala (and DegreeRanking) */
 #define RGPU_ALGO_PR 2     /* PageRank per SURVEY.md App. A.5 (reference PageRank.scala is broken) */
+#define RGPU_ALGO_DIFFUSION 3 /* S/core/analysis/Algorithms/BinaryDefusion.scala (ABI 5) */
 
 /* rgpu_run_view_batch flags */
 #define RGPU_RUN_RETAIN 1   /* keep per-vertex results of every view (for *_vertex_* queries) */
@@ -75,7 +76,7 @@ typedef struct {
   double ms_total;               /* wall ms inside the last rgpu_run_view_batch */
   /* per-kernel event timing (RGPU_RUN_PROFILE): 0=window_mask 1=slots 2=cc_step 3=cc_hist
    * 4=cc_summary 5=pr_step 6=degree 7=cc_tail (late supersteps, one workgroup)
-   * 8=heavy (hub segment kernels) 9-11 reserved */
+   * 8=heavy (hub segment kernels) 9=diffusion step 10-11 reserved */
   int64_t kernel_launches[12];
   double kernel_ms[12];
   double kernel_bytes[12];       /* algorithmic bytes summed over launches */
@@ -187,6 +188,27 @@ int rgpu_degree_vertex(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, int3
 /* PageRank of view (hop, win), ascending id.  Needs RGPU_RUN_RETAIN. */
 int rgpu_pr_result(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, double* pr, size_t cap,
                    size_t* n);
+
+/* BinaryDefusion (BinaryDefusion.scala:9-51; VertexVisitor messaging, VertexVisitor.scala:99-135)
+ * parameters for later RGPU_ALGO_DIFFUSION runs: seed_id = infectedNode (:10, default 31).
+ * The reference flips Random.nextBoolean() per message (:17,:32), unseeded and so not
+ * reproducible; here the flip is a fixed hash (coin = 1, the default; coin = 0 sends every
+ * message, the deterministic taint/reachability form).  With mix = the splitmix64 finaliser
+ * (x ^= x>>30; x *= 0xbf58476d1ce4e5b9; x ^= x>>27; x *= 0x94d049bb133111eb; x ^= x>>31), u64
+ * wrap-around arithmetic and w = the view's window (-1 for a ViewLens):
+ *   salt(t, w)         = mix(coin_seed ^ mix((u64)t ^ mix((u64)w)))
+ *   heads(u, v, r, t, w) = top bit of mix(salt(t, w) ^ mix((u64)u * 0x9E3779B97F4A7C15 ^ mix((u64)v + r)))
+ * for a message from vertex id u to vertex id v sent at superstep r (setup = 0).
+ * Diffusion runs need one partition (num_partitions == 1) and max_steps <= 127. */
+int rgpu_set_diffusion(rgpu_ctx* ctx, int64_t seed_id, uint64_t coin_seed, int coin);
+
+/* Diffusion result of view (hop, win): infected vertices and the supersteps its batch ran. */
+int rgpu_diffusion_result(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* infected, int64_t* supersteps);
+
+/* BinaryDefusion.returnResults (:38-49): (id, infected superstep) of every infected vertex of
+ * the view, ascending id.  Needs RGPU_RUN_RETAIN. */
+int rgpu_diffusion_vertex(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, int32_t* steps,
+                          size_t cap, size_t* n);
 
 int rgpu_stats(rgpu_ctx* ctx, rgpu_stats_t* out);
 const char* rgpu_last_error(rgpu_ctx* ctx);

@@ -53,6 +53,9 @@ def lib() -> C.CDLL:
         L.orc_degree.argtypes = [C.c_void_p, C.c_int64, _P64, C.c_int, _P64, _P32, _P32, _SZ, C.POINTER(_SZ)]
         L.orc_pagerank.restype = C.c_int
         L.orc_pagerank.argtypes = [C.c_void_p, C.c_int64, _P64, C.c_int, C.c_int, _P64, _PD, _SZ, C.POINTER(_SZ)]
+        L.orc_diffusion.restype = C.c_int
+        L.orc_diffusion.argtypes = [C.c_void_p, C.c_int64, _P64, C.c_int, C.c_int, C.c_int64, C.c_uint64,
+                                    C.c_int, _P64, _P32, _SZ, C.POINTER(_SZ), C.POINTER(C.c_int)]
         _lib = L
     return _lib
 
@@ -148,6 +151,23 @@ class Oracle:
         if rc != 0:
             raise RuntimeError("orc_pagerank failed")
         return [(ids[i * cap:i * cap + n[i]].copy(), pr[i * cap:i * cap + n[i]].copy()) for i in range(nw)]
+
+    def diffusion(self, t: int, windows: Sequence[int] = (), max_steps: int = 100, seed_id: int = 31,
+                  coin_seed: int = 0, coin: bool = True):
+        """BinaryDefusion -> ([(ids, infected_step)] per window, supersteps)"""
+        w, nw = self._win(windows)
+        cap = max(1, self.nv)
+        ids = np.empty(nw * cap, np.int64)
+        st = np.empty(nw * cap, np.int32)
+        n = (C.c_size_t * nw)()
+        steps = C.c_int()
+        rc = lib().orc_diffusion(self._g, t, _p(w, C.c_int64) if len(w) else None, len(w), max_steps, seed_id,
+                                 coin_seed & (2**64 - 1), int(coin), _p(ids, C.c_int64), _p(st, C.c_int32), cap,
+                                 n, C.byref(steps))
+        if rc != 0:
+            raise RuntimeError("orc_diffusion failed")
+        out = [(ids[i * cap:i * cap + n[i]].copy(), st[i * cap:i * cap + n[i]].copy()) for i in range(nw)]
+        return out, steps.value
 
 
 def label_counts(labels: np.ndarray) -> dict:

@@ -599,3 +599,103 @@ done:
   free(mem); free(cur); free(nxt); free(od);
   return rc;
 }
+
+/* ------------------------------------------------------------ diffusion */
+/* BinaryDefusion.scala:9-51 run through the reference's BSP: Setup (superstep 0, only when
+ * maxSteps > 1, AnalysisTask.scala:169), then per superstep s the vertices with messages
+ * (getVerticesWithMessages, WindowLens.scala:149-158) clear their queue; an infected one
+ * votes to halt (:27-28), a new one records infected = s and messages every out-neighbour
+ * (outgoingProcessing after viewAtWithWindow, VertexVisitor.scala:32) on a coin flip (:31-33);
+ * halt at s == maxSteps or when every message holder voted (AnalysisTask.endStep :208-225).
+ * The coin replaces the unseeded Random.nextBoolean() by the hash specified in
+ * include/rgpu.h (rgpu_set_diffusion); coin == 0 sends every message. */
+static uint64_t dmix(uint64_t x) {
+  x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull; x ^= x >> 27; x *= 0x94d049bb133111ebull; x ^= x >> 31;
+  return x;
+}
+static int dcoin(uint64_t salt, int64_t u, int64_t v, int r) {
+  uint64_t a = dmix((uint64_t)v + (uint64_t)(int64_t)r);
+  uint64_t b = dmix(((uint64_t)u * 0x9E3779B97F4A7C15ull) ^ a);
+  return (int)(dmix(salt ^ b) >> 63);
+}
+
+int orc_diffusion(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int max_steps,
+                  int64_t seed_id, uint64_t coin_seed, int coin, int64_t* ids, int32_t* step_out,
+                  size_t cap, size_t* n_out, int* steps) {
+  WinSet ws;
+  if (winset_init(&ws, windows, nw) != 0) return -1;
+  size_t nv = g->nv, nvs = nv ? nv : 1;
+  int nwin = ws.nwin;
+  uint8_t* mem = (uint8_t*)calloc((size_t)nwin * nvs, 1);
+  int32_t* inf = (int32_t*)malloc(sizeof(int32_t) * nwin * nvs);  /* compValue "infected", -1 = none */
+  uint32_t* q = (uint32_t*)calloc((size_t)2 * nwin * nvs, sizeof(uint32_t)); /* queue sizes, parity */
+  int* list = (int*)malloc(sizeof(int) * nvs);
+  uint64_t salt[64];
+  int rc = -1;
+  if (!mem || !inf || !q || !list) goto done;
+  for (size_t i = 0; i < (size_t)nwin * nvs; i++) inf[i] = -1;
+  for (int i = 0; i < nwin; i++) salt[i] = dmix(coin_seed ^ dmix((uint64_t)t ^ dmix((uint64_t)ws.w[i])));
+  build_keysets(g, t, &ws, mem);
+  *steps = 0;
+  /* messageNeighbour to every out-neighbour of v whose edge is alive in the view */
+#define DSEND(i, s, v)                                                                   \
+  do {                                                                                   \
+    const Vertex* x_ = &g->vs[(v)];                                                      \
+    size_t qb_ = ((size_t)(((s) + 1) % 2) * nwin + ws.canon[i]) * nv;                    \
+    for (int k_ = 0; k_ < x_->out.n; k_++) {                                             \
+      const Edge* e_ = &g->es[x_->out.a[k_]];                                            \
+      if (!ent_alive(&e_->e, t, ws.w[i])) continue;                                      \
+      int d_ = hm_get(&g->vmap, (uint64_t)e_->dst);                                      \
+      if (!coin || dcoin(salt[i], x_->id, e_->dst, (s))) q[qb_ + d_]++;                  \
+    }                                                                                    \
+  } while (0)
+  if (max_steps > 1) {
+    int32_t sv = hm_get(&g->vmap, (uint64_t)seed_id);
+    for (int i = 0; i < nwin; i++) { /* setup :11-21 */
+      if (seed_id < 0 || seed_id >= ((int64_t)1 << 31) || sv < 0 || !mem[(size_t)i * nv + sv]) continue;
+      size_t li = (size_t)ws.canon[i] * nv + sv;
+      if (inf[li] < 0) inf[li] = 0;  /* getOrSetCompValue("infected", superStep = 0) */
+      DSEND(i, 0, sv);
+    }
+    for (int s = 1;; s++) {
+      long totalKeys = 0, votes = 0;
+      for (int i = 0; i < nwin; i++) {
+        int c = ws.canon[i];
+        size_t qb = ((size_t)(s % 2) * nwin + c) * nv;
+        int nl = 0;
+        for (size_t v = 0; v < nv; v++)
+          if (mem[(size_t)i * nv + v] && q[qb + v] > 0) list[nl++] = (int)v;
+        totalKeys += nl;
+        for (int a = 0; a < nl; a++) { /* analyse :23-36 */
+          int v = list[a];
+          q[qb + v] = 0; /* clearQueue */
+          size_t li = (size_t)c * nv + v;
+          if (inf[li] >= 0) { votes++; continue; }
+          inf[li] = s;
+          DSEND(i, s, v);
+        }
+      }
+      *steps = s;
+      if (s == max_steps || totalKeys == votes) break;
+    }
+  }
+#undef DSEND
+  for (int i = 0; i < nwin; i++) { /* returnResults :38-49, ascending id */
+    size_t k = 0;
+    for (size_t r = 0; r < nv; r++) {
+      int v = g->order[r];
+      if (!mem[(size_t)i * nv + v]) continue;
+      int32_t x = inf[(size_t)ws.canon[i] * nv + v];
+      if (x < 0) continue;
+      if (k >= cap) goto done;
+      ids[(size_t)i * cap + k] = g->vs[v].id;
+      step_out[(size_t)i * cap + k] = x;
+      k++;
+    }
+    n_out[i] = k;
+  }
+  rc = 0;
+done:
+  free(mem); free(inf); free(q); free(list);
+  return rc;
+}

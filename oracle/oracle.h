@@ -62,6 +62,11 @@ int orc_degree(const orc_graph* g, int64_t t, const int64_t* windows, int nw,
 
 /* PageRank, SURVEY.md App. A.5 spec (the reference PageRank.scala is broken):
  * PR0 = 1, PR' = 0.15 + 0.85 * sum_{u->v} PR(u)/max(outdeg(u),1), fp64, iters rounds. */
+/* BinaryDefusion (reference BSP structure, hash coin of include/rgpu.h): per window the
+ * infected vertices (ascending id) with their infection superstep. */
+int orc_diffusion(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int max_steps,
+                  int64_t seed_id, uint64_t coin_seed, int coin, int64_t* ids, int32_t* step_out,
+                  size_t cap, size_t* n_out, int* steps);
 int orc_pagerank(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int iters,
                  int64_t* ids, double* pr, size_t cap, size_t* n_out);
 

@@ -16,7 +16,7 @@ BUILD_DIR = os.path.join(_HERE, "_build")
 RGPU_OK = 0
 RGPU_EINVAL, RGPU_ESTATE, RGPU_EHIP, RGPU_ENOMEM, RGPU_ENOTSUP = -1, -2, -3, -4, -5
 RGPU_VADD, RGPU_VDEL, RGPU_EADD, RGPU_EDEL = 0, 1, 2, 3
-RGPU_ALGO_CC, RGPU_ALGO_DEGREE, RGPU_ALGO_PR = 0, 1, 2
+RGPU_ALGO_CC, RGPU_ALGO_DEGREE, RGPU_ALGO_PR, RGPU_ALGO_DIFFUSION = 0, 1, 2, 3
 RGPU_RUN_RETAIN, RGPU_RUN_PROFILE, RGPU_RUN_SERIAL = 1, 2, 4
 RGPU_XCHG_ID_BYTES, RGPU_XCHG_RCCL, RGPU_XCHG_LOOPBACK = 128, 0, 1
 ERROR_NAMES = {
@@ -27,7 +27,7 @@ ERROR_NAMES = {
     RGPU_ENOTSUP: "RGPU_ENOTSUP",
 }
 KERNEL_NAMES = ["window_mask", "cc_slots", "cc_step", "cc_hist", "cc_summary", "pr_step", "degree", "cc_tail",
-                "heavy", "-", "-", "-"]
+                "heavy", "diffusion", "-", "-"]
 
 # exported symbols of librgpu.so, exactly the declarations of include/rgpu.h
 EXPORTS = [
@@ -36,6 +36,7 @@ EXPORTS = [
     "rgpu_cc_vertex_labels", "rgpu_degree_result", "rgpu_degree_vertex", "rgpu_pr_result",
     "rgpu_stats", "rgpu_last_error", "rgpu_close",
     "rgpu_rgev_encode", "rgpu_rgev_decode", "rgpu_rgev_last_error", "rgpu_ingest_rgev",
+    "rgpu_set_diffusion", "rgpu_diffusion_result", "rgpu_diffusion_vertex",
 ]
 
 
@@ -82,6 +83,9 @@ _SIGS = {
     "rgpu_degree_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P64, _P32, _P32]),
     "rgpu_degree_vertex": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P32, _P32, _SZ, C.POINTER(_SZ)]),
     "rgpu_pr_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _PD, _SZ, C.POINTER(_SZ)]),
+    "rgpu_set_diffusion": (C.c_int, [_CTX, C.c_int64, C.c_uint64, C.c_int]),
+    "rgpu_diffusion_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P64]),
+    "rgpu_diffusion_vertex": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P32, _SZ, C.POINTER(_SZ)]),
     "rgpu_stats": (C.c_int, [_CTX, C.POINTER(Stats)]),
     "rgpu_last_error": (C.c_char_p, [_CTX]),
     "rgpu_close": (None, [_CTX]),

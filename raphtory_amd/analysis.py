@@ -218,6 +218,44 @@ class PageRank(Analyser):
         self.lines.append(json.dumps({"time": timestamp, "top5": top, "vertices": len(merged)}))
 
 
+class BinaryDefusion(Analyser):
+    """S/core/analysis/Algorithms/BinaryDefusion.scala:9-60 on the GPU (raphtory_amd/csrc/diffusion.hip).
+
+    The reference's per-message ``Random.nextBoolean()`` (:17, :32) is unseeded; here it is the
+    hash coin of ``include/rgpu.h`` (``coin_seed``), or no coin at all (``coin=False``: every
+    message is sent, the taint/reachability form).  ``processResults`` is ``???`` in the
+    reference (:53); views print the infected (id, superstep) list and its size (:55-59)."""
+    algo = "diffusion"
+
+    def __init__(self, args: Sequence[str] = (), infected_node: int = 31, coin_seed: int = 0, coin: bool = True):
+        super().__init__(args)
+        self.infectedNode = infected_node  # :10
+        self.coin_seed = coin_seed
+        self.coin = coin
+
+    def defineMaxSteps(self) -> int:  # :51
+        return 100
+
+    def prepare(self, graph) -> None:
+        graph.set_diffusion(self.infectedNode, self.coin_seed, self.coin)
+
+    def returnResults(self, graph, hop, win):  # :38-49
+        ids, steps = graph.diffusion_vertex(hop, win)
+        return list(zip(ids.tolist(), steps.tolist()))
+
+    def processViewResults(self, results, timestamp, viewCompleteTime):  # :55-59
+        end = sorted(x for part in results for x in part)
+        self.lines.append(json.dumps({"time": timestamp, "infected": end, "size": len(end)}))
+
+    def processResults(self, results, timestamp, viewCompleteTime):
+        self.processViewResults(results, timestamp, viewCompleteTime)
+
+    def processBatchWindowResults(self, results, timestamp, windowSet, viewCompleteTime):
+        for w, per_window in zip(windowSet, results):
+            end = sorted(x for part in per_window for x in part)
+            self.lines.append(json.dumps({"time": timestamp, "windowsize": w, "infected": end, "size": len(end)}))
+
+
 # ---------------------------------------------------------------- tasks
 class TimeNotIngested(RuntimeError):
     """TimeCheck failed (ReaderWorker.processTimeCheckRequest :259-274); the reference retries in 10 s."""
@@ -261,7 +299,9 @@ class AnalysisTask:
         max_steps = a.defineMaxSteps()
         t0 = time.perf_counter()
         for g in self.graphs:
-            g.run(a.algo, hops, windows, max_steps=max_steps if a.algo == "cc" else 100,
+            if hasattr(a, "prepare"):
+                a.prepare(g)
+            g.run(a.algo, hops, windows, max_steps=max_steps if a.algo in ("cc", "diffusion") else 100,
                   pr_iters=max_steps if a.algo == "pagerank" else 0, retain=self.retain)
         self.view_ms = (time.perf_counter() - t0) * 1e3 / max(1, len(hops))
         vt = int(round(self.view_ms))

@@ -117,6 +117,18 @@ void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const 
                     const int32_t* outdeg, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const double* contrib_cur, double* contrib_next, double* pr, double* hacc);
 
+// BinaryDefusion (diffusion.hip): per-lane coin salts of a batch (view j -> (hop, window))
+struct DiffSalts {
+  uint64_t s[64];
+};
+void launch_diff_setup(hipStream_t s, int64_t nv, const uint64_t* vm, int64_t seed, uint64_t* inf,
+                       uint64_t* front0, uint8_t* steprow);
+void launch_diff_step(hipStream_t s, int step, const DevGraph& g, const int64_t* vid, const uint64_t* vm,
+                      const uint64_t* em, uint64_t* inf, const uint64_t* front_in, uint64_t* front_out,
+                      uint8_t* steprow, const DiffSalts& salts, int coin, int32_t* stepflag,
+                      int32_t* hostflag);
+void launch_diff_count(hipStream_t s, int64_t nv, const uint64_t* inf, unsigned long long* stats);
+
 // partition exchange (vertex-partitioned mode)
 constexpr int kXRecWords = 68;  // ints per boundary-row record
 void launch_xpack_cc(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,

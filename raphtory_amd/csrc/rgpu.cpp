@@ -43,7 +43,7 @@ struct HipFail {
   } while (0)
 
 enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUMMARY = 4,
-                KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_HEAVY = 8, KID_N = 12 };
+                KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_HEAVY = 8, KID_DIFF = 9, KID_N = 12 };
 
 constexpr int kMaxSteps = 128;
 constexpr int kStatWords = 7 * kViews;  // 6 per-view fields + counters row
@@ -53,7 +53,7 @@ constexpr int kMaxSlots = 4;  // batches in flight (one HIP stream each; GPU_MAX
 
 struct Slot {
   // buffers allocated for this slot (slots are allocated lazily: a run uses min(slots, batches))
-  bool a_cc = false, a_deg = false, a_pr = false, h_cc = false, h_pr = false;
+  bool a_cc = false, a_deg = false, a_pr = false, h_cc = false, h_pr = false, a_diff = false;
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   uint64_t *vm = nullptr, *em = nullptr;          // masks of the batch in flight
@@ -78,6 +78,10 @@ struct Slot {
   int32_t* d_tail = nullptr;
   unsigned int* iso = nullptr;    // isolated-member counts [64 shards][64 views] (k_cc_hist)
   HeavyBuf hv;                    // heavy-vertex segment state (graphs with hubs)
+  // BinaryDefusion (diffusion.hip): infected views, views infected last / this step, step rows
+  uint64_t *dinf = nullptr, *dfront[2] = {nullptr, nullptr};
+  uint8_t* dstep = nullptr;
+  DiffSalts salts;                // coin salt per lane of the batch in flight
   unsigned long long* h_stats = nullptr;
   // state of the batch in flight
   int batch = -1, phase = 0, r_launched = 0, r_final = 0, kb = 0;
@@ -90,6 +94,7 @@ struct Retained {  // per batch, RGPU_RUN_RETAIN
   std::vector<uint64_t> vm;
   std::vector<int32_t> a, b;  // CC: labels | degree: out, in
   std::vector<double> pr;
+  std::vector<uint8_t> st;    // diffusion: infection superstep per (vertex, lane), 0xFF = none
 };
 
 // device state of the vertex-partitioned mode (one partition per GPU)
@@ -169,6 +174,12 @@ struct rgpu_ctx {
   size_t n_hops = 0;
   std::vector<rgpu_cc_summary_t> cc;
   std::vector<int64_t> deg;  // [view][3]
+  std::vector<int64_t> dcount, dsteps;  // diffusion: infected vertices, supersteps per view
+  int64_t diff_seed = 31;               // BinaryDefusion.infectedNode (BinaryDefusion.scala:10)
+  uint64_t diff_coin_seed = 0;
+  int diff_coin = 1;
+  int64_t diff_seed_rank = -1;          // of the run in progress
+  int64_t* d_vid = nullptr;             // vertex ids on the device (diffusion coins hash ids)
   std::vector<Retained> kept;
   bool retained = false;
   rgpu_stats_t st{};
@@ -216,6 +227,7 @@ void release_slots(rgpu_ctx* c) {
   for (void* p : c->slot_allocs) (void)hipFree(p);
   c->slot_allocs.clear();
   c->cap_nv = c->cap_ne = c->cap_nin = 0;
+  c->d_vid = nullptr;
   for (Slot& s : c->slot) {
     if (s.h_stepcnt) (void)hipHostFree(s.h_stepcnt);
     if (s.h_tail) (void)hipHostFree(s.h_tail);
@@ -345,6 +357,12 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       s.hv.pacc = dalloc<double>(LG, (size_t)c->g.n_heavy * kViews);  // zero between uses
       HIPCHK(hipMemset(s.hv.pacc, 0, sizeof(double) * (size_t)c->g.n_heavy * kViews));
     }
+    if (algo == RGPU_ALGO_DIFFUSION && !s.a_diff) {
+      s.dinf = dalloc<uint64_t>(L, nv + kPad);
+      s.dfront[0] = dalloc<uint64_t>(L, nv + kPad);
+      s.dfront[1] = dalloc<uint64_t>(L, nv + kPad);
+      s.dstep = dalloc<uint8_t>(L, rows);
+    }
     if (algo == RGPU_ALGO_PR && !s.a_pr) {
       s.pr = dalloc<double>(L, rows);
       s.contrib[0] = dalloc<double>(L, rows);
@@ -384,7 +402,9 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
     if (algo == RGPU_ALGO_PR) s.h_pr = true;
     if (algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) s.a_deg = true;
     if (algo == RGPU_ALGO_PR) s.a_pr = true;
+    if (algo == RGPU_ALGO_DIFFUSION) s.a_diff = true;
   }
+  if (algo == RGPU_ALGO_DIFFUSION && !c->d_vid) c->d_vid = dalloc<int64_t>(L, nv);
 }
 
 struct RunCfg {
@@ -395,6 +415,7 @@ struct RunCfg {
   const int64_t* hops;
   size_t n_hops;
   int64_t thr_v[kViews], thr_e[kViews];
+  int64_t wval[kViews];  // the user's window values (-1 = ViewLens): diffusion coin salts
   int chunk0, chunk;
 };
 
@@ -402,6 +423,19 @@ struct RunCfg {
 int run_slots(const rgpu_ctx* c, const RunCfg& rc) {
   const int n = (rc.flags & RGPU_RUN_SERIAL) ? 1 : c->nslots;
   return (int)std::max<size_t>(1, std::min<size_t>((size_t)n, rc.nb));
+}
+
+// diffusion coin salt of a view (include/rgpu.h, rgpu_set_diffusion)
+uint64_t hmix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x;
+}
+uint64_t diff_salt(uint64_t coin_seed, int64_t t, int64_t w) {
+  return hmix64(coin_seed ^ hmix64((uint64_t)t ^ hmix64((uint64_t)w)));
 }
 
 // algorithmic bytes: see rgpu_stats_t.kernel_bytes
@@ -422,8 +456,15 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     eb = take_event(c);
     HIPCHK(hipEventRecord(ea, s.stream));
   }
-  const bool hv = g.n_seg > 0;
+  const bool hv = g.n_seg > 0 && rc.algo == RGPU_ALGO_CC;
   for (int r = s.r_launched + 1; r <= last; r++) {
+    if (rc.algo == RGPU_ALGO_DIFFUSION) {
+      timed_launch(c, si, KID_DIFF, 0.0, [&] {
+        launch_diff_step(s.stream, r, g, c->d_vid, s.vm, s.em, s.dinf, s.dfront[(r - 1) & 1], s.dfront[r & 1],
+                         s.dstep, s.salts, c->diff_coin, s.stepcnt, c->hostflags ? s.d_hostflag : nullptr);
+      }, r, false);
+      continue;
+    }
     if (hv)  // heavy vertices: segment minima before the step, neighbour marking after it
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[(r - 1) & 1], s.chg[(r - 1) & 1], s.act[r % 3],
@@ -444,10 +485,11 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
   }
   if (ea) {
     HIPCHK(hipEventRecord(eb, s.stream));
-    c->timed.push_back({KID_STEP, si, s.batch, s.r_launched + 1, ea, eb, 0.0});
+    c->timed.push_back({rc.algo == RGPU_ALGO_DIFFUSION ? KID_DIFF : KID_STEP, si, s.batch, s.r_launched + 1, ea, eb, 0.0});
   }
   s.r_launched = last;
-  if (c->tail_on && g.n_seg == 0 && g.nv <= c->tail_maxv && s.r_launched < rc.max_steps) {
+  if (rc.algo == RGPU_ALGO_CC && c->tail_on && g.n_seg == 0 && g.nv <= c->tail_maxv &&
+      s.r_launched < rc.max_steps) {
     // the rest of the supersteps in one workgroup while the frontier stays narrow; it stops
     // (and the host continues with full-grid launches) at the first wide frontier
     const int r0 = s.r_launched + 1;
@@ -483,6 +525,9 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
     timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g.nv, g.nv, nviews, s.vm, s.vadj, lab, hist, s.iso); });
     timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * nviews,
                  [&] { launch_cc_summary(s.stream, g, nviews, hist, s.stats, s.iso); });
+  } else if (rc.algo == RGPU_ALGO_DIFFUSION) {
+    launch_diff_count(s.stream, g.nv, s.dinf, s.stats);
+    HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatWords,
                         hipMemcpyDeviceToHost, s.stream));
@@ -495,6 +540,9 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
       R.a.resize(rows);
       HIPCHK(hipMemcpyAsync(R.a.data(), s.lab[s.r_final & 1], sizeof(int32_t) * rows,
                             hipMemcpyDeviceToHost, s.stream));
+    } else if (rc.algo == RGPU_ALGO_DIFFUSION) {
+      R.st.resize(rows);
+      HIPCHK(hipMemcpyAsync(R.st.data(), s.dstep, rows, hipMemcpyDeviceToHost, s.stream));
     } else if (rc.algo == RGPU_ALGO_DEGREE) {
       R.a.resize(rows);
       R.b.resize(rows);
@@ -586,6 +634,27 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     launch_batch_clear(s.stream, clr);
     HIPCHK(hipGetLastError());
   }
+  if (rc.algo == RGPU_ALGO_DIFFUSION) {
+    // coin salts: lane j = wl*K + k is hop h0 + k, window grp*gsize + wl (include/rgpu.h)
+    for (int j = 0; j < kViews; j++) {
+      const int k = j % rc.K, wl = j / rc.K;
+      const int64_t t = k < bp.K ? bp.hop[k] : 0;
+      const int64_t w = wl < rc.gsize ? rc.wval[grp * rc.gsize + wl] : -1;
+      s.salts.s[j] = diff_salt(c->diff_coin_seed, t, w);
+    }
+    // Setup (superstep 0) only when defineMaxSteps > 1 (AnalysisTask.timeResponse :169)
+    launch_diff_setup(s.stream, g.nv, s.vm, rc.max_steps > 1 ? c->diff_seed_rank : -1, s.dinf, s.dfront[0],
+                      s.dstep);
+    HIPCHK(hipGetLastError());
+    s.r_launched = 0;
+    if (rc.max_steps <= 1) {
+      s.r_final = 0;
+      finish_batch(c, si, rc);
+    } else {
+      launch_chunk(c, si, rc, rc.chunk0);
+    }
+    return;
+  }
   if (rc.algo == RGPU_ALGO_CC) {
     // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
@@ -651,6 +720,9 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
         o.supersteps = s.r_final;
       } else if (rc.algo == RGPU_ALGO_DEGREE) {
         for (int f = 0; f < 3; f++) c->deg[view * 3 + f] = (int64_t)h[f * kViews + j];
+      } else if (rc.algo == RGPU_ALGO_DIFFUSION) {
+        c->dcount[view] = (int64_t)h[j];
+        c->dsteps[view] = s.r_final;
       }
     }
   if (rc.algo == RGPU_ALGO_CC) {
@@ -681,6 +753,7 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
     c->st.supersteps += s.r_final;
     c->grp_last[grp] = s.r_final;
   }
+  if (rc.algo == RGPU_ALGO_DIFFUSION) c->st.supersteps += s.r_final;
   s.phase = 0;
   s.batch = -1;
 }
@@ -1404,11 +1477,13 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   if (!c->sealed) return fail(c, RGPU_ESTATE, "rgpu_run_view_batch before rgpu_seal");
   if (c->partitioned && !c->pt.xchg)
     return fail(c, RGPU_ESTATE, "partitioned context: call rgpu_exchange_init before running");
-  if (algo < RGPU_ALGO_CC || algo > RGPU_ALGO_PR) return fail(c, RGPU_EINVAL, "unknown algo");
+  if (algo < RGPU_ALGO_CC || algo > RGPU_ALGO_DIFFUSION) return fail(c, RGPU_EINVAL, "unknown algo");
+  if (algo == RGPU_ALGO_DIFFUSION && c->partitioned)
+    return fail(c, RGPU_EINVAL, "diffusion runs need one partition");
   if (!hops || n_hops == 0) return fail(c, RGPU_EINVAL, "no hops");
   if (n_w > (size_t)kViews) return fail(c, RGPU_EINVAL, "more than 64 windows in one batch");
   if (n_w && !windows) return fail(c, RGPU_EINVAL, "null window array");
-  if (algo == RGPU_ALGO_CC && max_steps > kMaxSteps - 1)
+  if ((algo == RGPU_ALGO_CC || algo == RGPU_ALGO_DIFFUSION) && max_steps > kMaxSteps - 1)
     return fail(c, RGPU_EINVAL, "max_steps above 127");
   if (algo == RGPU_ALGO_PR && (pr_iters < 0 || pr_iters > 100000))
     return fail(c, RGPU_EINVAL, "bad pr_iters");
@@ -1443,6 +1518,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
                     "VertexVisitor.scala:81-96; not supported)");
     run_min = std::min(run_min, wv);
     rc.thr_e[w] = wv;
+    rc.wval[w] = n_w ? windows[w] : -1;
     rc.thr_v[w] = run_min;  // WindowLens.shrinkWindow keeps the running intersection
   }
   rc.chunk0 = std::max(1, env_int("RGPU_CHUNK0", 12));
@@ -1469,6 +1545,15 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->n_hops = n_hops;
     c->cc.assign(algo == RGPU_ALGO_CC ? n_hops * rc.W : 0, rgpu_cc_summary_t{});
     c->deg.assign(algo == RGPU_ALGO_DEGREE ? n_hops * rc.W * 3 : 0, 0);
+    c->dcount.assign(algo == RGPU_ALGO_DIFFUSION ? n_hops * rc.W : 0, 0);
+    c->dsteps.assign(algo == RGPU_ALGO_DIFFUSION ? n_hops * rc.W : 0, 0);
+    if (algo == RGPU_ALGO_DIFFUSION) {
+      // ids ascend with rank: the seed's rank by binary search (-1: not in the graph)
+      const auto& vid = c->pk.vid;
+      auto it = std::lower_bound(vid.begin(), vid.begin() + c->g.nv, c->diff_seed);
+      c->diff_seed_rank = (it != vid.begin() + c->g.nv && *it == c->diff_seed) ? (int64_t)(it - vid.begin()) : -1;
+      if (c->g.nv) HIPCHK(hipMemcpy(c->d_vid, vid.data(), sizeof(int64_t) * c->g.nv, hipMemcpyHostToDevice));
+    }
     c->kept.clear();
     c->retained = (flags & RGPU_RUN_RETAIN) != 0;
     if (c->retained) c->kept.resize(nb);
@@ -1651,6 +1736,48 @@ int rgpu_pr_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, double* pr
   for (int64_t v = 0; v < c->pk.n_own; v++) {
     if (!((R.vm[v] >> j) & 1)) continue;
     if (k < cap) { ids[k] = c->pk.vid[v]; pr[k] = R.pr[(size_t)v * kViews + j]; }
+    k++;
+  }
+  *n = k;
+  return RGPU_OK;
+}
+
+int rgpu_set_diffusion(rgpu_ctx* c, int64_t seed_id, uint64_t coin_seed, int coin) {
+  if (!c) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->diff_seed = seed_id;
+  c->diff_coin_seed = coin_seed;
+  c->diff_coin = coin ? 1 : 0;
+  return RGPU_OK;
+}
+
+int rgpu_diffusion_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* infected, int64_t* supersteps) {
+  if (!c) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_DIFFUSION) return fail(c, RGPU_ESTATE, "last run was not diffusion");
+  size_t b;
+  int j;
+  if (int e = view_index(c, hop, win, &b, &j)) return e;
+  if (infected) *infected = c->dcount[hop * c->W + win];
+  if (supersteps) *supersteps = c->dsteps[hop * c->W + win];
+  return RGPU_OK;
+}
+
+int rgpu_diffusion_vertex(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int32_t* steps, size_t cap,
+                          size_t* n) {
+  if (!c || !n) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_DIFFUSION || !c->retained)
+    return fail(c, RGPU_ESTATE, "needs a diffusion run with RGPU_RUN_RETAIN");
+  size_t b;
+  int j;
+  if (int e = view_index(c, hop, win, &b, &j)) return e;
+  const Retained& R = c->kept[b];
+  size_t k = 0;
+  for (int64_t v = 0; v < c->pk.n_own; v++) {
+    const uint8_t r = R.st[(size_t)v * kViews + j];
+    if (r == 0xFF) continue;  // returnResults keeps infected vertices only (:43-49)
+    if (k < cap) { ids[k] = c->pk.vid[v]; steps[k] = r; }
     k++;
   }
   *n = k;

@@ -19,7 +19,8 @@ class RGPUError(RuntimeError):
         self.code = code
 
 
-ALGOS = {"cc": N.RGPU_ALGO_CC, "degree": N.RGPU_ALGO_DEGREE, "pagerank": N.RGPU_ALGO_PR}
+ALGOS = {"cc": N.RGPU_ALGO_CC, "degree": N.RGPU_ALGO_DEGREE, "pagerank": N.RGPU_ALGO_PR,
+         "diffusion": N.RGPU_ALGO_DIFFUSION}
 
 
 def _i64(a) -> np.ndarray:
@@ -175,6 +176,22 @@ class TemporalGraph:
     def pr_result(self, hop: int, win: int):
         return self._sized(self._lib.rgpu_pr_result, hop, win,
                            lambda n: ([(np.empty(n, np.int64), C.c_int64), (np.empty(n, np.float64), C.c_double)], 2))
+
+    def set_diffusion(self, seed_id: int = 31, coin_seed: int = 0, coin: bool = True) -> None:
+        """BinaryDefusion parameters (infectedNode, hash-coin seed; coin=False sends every message)."""
+        self._check(self._lib.rgpu_set_diffusion(self._ctx, seed_id, coin_seed & (2**64 - 1), int(coin)))
+
+    def diffusion_result(self, hop: int, win: int) -> Tuple[int, int]:
+        """-> (infected vertices, supersteps of the batch) of view (hop, win)"""
+        n, st = C.c_int64(), C.c_int64()
+        self._check(self._lib.rgpu_diffusion_result(self._ctx, hop, win, C.byref(n), C.byref(st)))
+        return n.value, st.value
+
+    def diffusion_vertex(self, hop: int, win: int) -> Tuple[np.ndarray, np.ndarray]:
+        """BinaryDefusion.returnResults: (ids, infected superstep) ascending id (needs retain)."""
+        ids, steps = self._sized(self._lib.rgpu_diffusion_vertex, hop, win,
+                                 lambda n: ([(np.empty(n, np.int64), C.c_int64), (np.empty(n, np.int32), C.c_int32)], 2))
+        return ids, steps
 
     def stats(self) -> dict:
         s = N.Stats()
