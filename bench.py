@@ -44,7 +44,8 @@ def parse():
     p.add_argument("--profile-only", action="store_true",
                    help="only the serial HIP-event profile pass (the command rocprofv3 is run on, so "
                         "that its per-kernel averages match the roofline figures)")
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"], help="c2 = the headline metric")
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "diffusion"],
+                   help="c2 = the headline metric; diffusion = BinaryDefusion over the C2 query (secondary)")
     p.add_argument("--c5-users", type=int, default=20_000_000)
     p.add_argument("--c5-base", type=int, default=33_333_334, help="sealed base interactions (x3 updates)")
     p.add_argument("--c5-tick", type=int, default=3_333_334, help="interactions streamed per hour tick (x3 updates)")
@@ -139,6 +140,42 @@ def run_c3(a, rank, world, local):
                                 for k, v in g.stats()["kernels"].items() if v["launches"]}
     tot = [g.degree_result(h, w)[:3] for h in (0, len(hops) - 1) for w in range(3)]
     out["degree_totals_first_last_hop"] = tot
+    g.close()
+    print(json.dumps(out))
+
+
+def run_diffusion(a, rank, world, local):
+    """Secondary line: BinaryDefusion (BinaryDefusion.scala) over the C2
+    query (8,041 hourly hops x {y,m,w,d,h}, infectedNode 31), hash coin and taint (no coin)."""
+    import torch
+    from raphtory_amd import TemporalGraph
+    from raphtory_amd.synth import BATCH_WINDOWS, DAY, HOUR, T0_README, gen_uniform, range_hops
+    stream = gen_uniform(1, 100_000, 1_000_000)
+    hops = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, HOUR)
+    g = TemporalGraph(device=local)
+    g.ingest_stream(stream)
+    g.seal()
+    st = g.stats()
+    out = {"config": "C2 query, BinaryDefusion", "vertices": st["vertices"], "edge_entities": st["edges"],
+           "hops": len(hops), "windows": len(BATCH_WINDOWS)}
+    for name, coin in (("coin", True), ("taint", False)):
+        g.set_diffusion(31, 0, coin)
+        g.run("diffusion", hops, BATCH_WINDOWS)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            g.run("diffusion", hops, BATCH_WINDOWS)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3 / a.steps
+        r = {"ms": round(ms, 2), "edge_windows_per_s": st["edges"] * len(BATCH_WINDOWS) * len(hops) / (ms / 1e3)}
+        sizes = [g.diffusion_result(h, w)[0] for h in (0, len(hops) // 2, len(hops) - 1) for w in range(5)]
+        r["infected_first_mid_last_hop"] = sizes
+        g.run("diffusion", hops, BATCH_WINDOWS, profile=True, serial=True)
+        r["supersteps"] = g.stats()["supersteps"]
+        r["kernels"] = {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                            "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
+                        for k, v in g.stats()["kernels"].items() if v["launches"]}
+        out[name] = r
     g.close()
     print(json.dumps(out))
 
@@ -287,6 +324,11 @@ def main():
         import torch
         torch.cuda.set_device(local)
         return run_c5(a, rank, world, local)
+    if a.config == "diffusion":
+        rank, world, local = dist_env()
+        import torch
+        torch.cuda.set_device(local)
+        return run_diffusion(a, rank, world, local)
     if a.config == "c3":
         rank, world, local = dist_env()
         import torch

@@ -504,7 +504,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
   if (!c->hostflags)
     HIPCHK(hipMemcpyAsync(s.h_stepcnt, s.stepcnt, sizeof(int32_t) * kMaxSteps, hipMemcpyDeviceToHost,
                           s.stream));
-  if (c->profile)
+  if (c->profile && rc.algo == RGPU_ALGO_CC)
     HIPCHK(hipMemcpyAsync(s.h_work, s.work, sizeof(unsigned long long) * kWorkWords,
                           hipMemcpyDeviceToHost, s.stream));
   HIPCHK(hipEventRecord(s.ev, s.stream));
@@ -651,7 +651,9 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       s.r_final = 0;
       finish_batch(c, si, rc);
     } else {
-      launch_chunk(c, si, rc, rc.chunk0);
+      // first chunk sized by the step the group's previous batch halted at (+1 for its halt step)
+      const int last = c->grp_last[grp];
+      launch_chunk(c, si, rc, last > 0 ? std::max(2, std::min(rc.chunk0, last + 1)) : rc.chunk0);
     }
     return;
   }
@@ -753,7 +755,14 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
     c->st.supersteps += s.r_final;
     c->grp_last[grp] = s.r_final;
   }
-  if (rc.algo == RGPU_ALGO_DIFFUSION) c->st.supersteps += s.r_final;
+  if (rc.algo == RGPU_ALGO_DIFFUSION) {
+    // per executed superstep: vm, inf, in_off pair, front out (40 B per vertex)
+    // and per in-edge in_eid, esrc, em, the source's front word (24 B); a vertex with no
+    // candidate view skips its in-edges, so this is the full-pass (upper) figure
+    c->st.kernel_bytes[KID_DIFF] += s.r_final * (40.0 * c->g.nv + 24.0 * c->g.n_in);
+    c->st.supersteps += s.r_final;
+    c->grp_last[grp] = s.r_final;
+  }
   s.phase = 0;
   s.batch = -1;
 }

@@ -63,6 +63,9 @@ def test_coin_uniform_window_major(uniform):
     for cs in (0, 99):
         assert check_diff(g, o, hops, [MONTH, WEEK, DAY], coin_seed=cs) > 0
     check_diff(g, o, hops[:3], [], coin_seed=7)  # ViewLens
+    g.run("diffusion", hops, [MONTH, WEEK, DAY], profile=True, serial=True)  # event-timed pass
+    k = g.stats()["kernels"]["diffusion"]
+    assert k["launches"] > 0 and k["ms"] > 0 and k["bytes"] > 0
 
 
 def test_caps_and_absent_seed(uniform):
