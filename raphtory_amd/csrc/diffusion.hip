@@ -18,7 +18,7 @@
 // Layout: lane = view (64 per batch), as in CC.  Per vertex: inf (u64, infected views),
 // front[2] (u64, views infected in the previous / this step), and a u8 row of 64 infection
 // steps (0xFF = not infected).  One wave per vertex pulls over its in-edges (in_off /
-// in_eid): a message from u reaches v in view j iff u was infected in j at step r-1, the
+// in_eid), 64 in-edges per load round: a message from u reaches v in view j iff u was infected in j at step r-1, the
 // edge is alive in j (K1 edge mask: own history + endpoint deaths) and the coin is heads;
 // v takes it iff v is a member of j and not yet infected there.  Bound: one pass over the
 // in-CSR per superstep (HBM / Infinity-Cache gathers), no MFMA.
@@ -93,12 +93,25 @@ __global__ __launch_bounds__(256) void k_diff_step(int step, int64_t nv, const i
       const int64_t k0 = in_off[v], k1 = in_off[v + 1];
       const int64_t myid = vid[v];
       bool hit = false;
-      for (int64_t k = k0; k < k1; k++) {
-        const int32_t e = in_eid[k];
-        const int32_t u = esrc[e];
-        const uint64_t f = front_in[u] & em[e] & cand;
-        if (!f) continue;
-        if (!hit && ((f >> lane) & 1)) hit = coin ? diff_coin(salt, vid[u], myid, step - 1) : true;
+      // lane = in-edge for the loads (one dependent chain in_eid -> esrc -> front per 64
+      // in-edges), lane = view for the coins of the few edges that carry a message
+      for (int64_t base = k0; base < k1; base += 64) {
+        const int64_t k = base + lane;
+        uint64_t f = 0;
+        int32_t u = 0;
+        if (k < k1) {
+          const int32_t e = in_eid[k];
+          u = esrc[e];
+          f = front_in[u] & em[e] & cand;
+        }
+        uint64_t msg = __ballot(f != 0);
+        while (msg) {
+          const int l = __builtin_ctzll(msg);
+          msg &= msg - 1;
+          const uint64_t fl = __shfl(f, l);
+          const int32_t ul = __shfl(u, l);
+          if (!hit && ((fl >> lane) & 1)) hit = coin ? diff_coin(salt, vid[ul], myid, step - 1) : true;
+        }
         if ((__ballot(hit) & cand) == cand) break;  // every candidate view already infected
       }
       newly = __ballot(hit) & cand;
