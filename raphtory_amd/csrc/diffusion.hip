@@ -46,14 +46,17 @@ __device__ __forceinline__ bool diff_coin(uint64_t salt, int64_t u, int64_t v, i
 // every view it belongs to, at step 0.  Rows are written as u64 words (8 views each).
 __global__ __launch_bounds__(256) void k_diff_setup(int64_t nv, const uint64_t* __restrict__ vm, int64_t seed,
                                                     uint64_t* __restrict__ inf, uint64_t* __restrict__ front0,
-                                                    uint64_t* __restrict__ steprow) {
+                                                    uint64_t* __restrict__ steprow,
+                                                    unsigned long long* __restrict__ stats) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   for (int64_t v = i0; v < nv; v += stride) {
     const uint64_t m = v == seed ? vm[v] : 0;
     inf[v] = m;
     front0[v] = m;
+    for (uint64_t b = m; b; b &= b - 1) atomicAdd(&stats[__builtin_ctzll(b)], 1ull);  // infected counts
   }
+  if (!steprow) return;  // rows only when the run retains per-vertex results
   for (int64_t i = i0; i < nv * 8; i += stride) {
     uint64_t w = ~0ull;
     if (i / 8 == seed) {
@@ -76,11 +79,15 @@ __global__ __launch_bounds__(256) void k_diff_step(int step, int64_t nv, const i
                                                    uint64_t* __restrict__ front_out,
                                                    uint8_t* __restrict__ steprow, DiffSalts salts, int coin,
                                                    int32_t* __restrict__ stepflag,
-                                                   int32_t* __restrict__ hostflag) {
+                                                   int32_t* __restrict__ hostflag,
+                                                   unsigned long long* __restrict__ stats) {
   if (step >= 2 && stepflag[step - 1] == 0) return;  // halted: nobody was infected at step-1
   __shared__ int32_t red;
+  __shared__ unsigned int acc[64];  // newly infected per view, this block
   if (threadIdx.x == 0) red = 0;
+  if (threadIdx.x < 64) acc[threadIdx.x] = 0;
   __syncthreads();
+  unsigned int mycnt = 0;  // lane j: vertices this wave infected in view j
   const int lane = threadIdx.x & 63;
   const uint64_t salt = salts.s[lane];
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -115,7 +122,8 @@ __global__ __launch_bounds__(256) void k_diff_step(int step, int64_t nv, const i
         if ((__ballot(hit) & cand) == cand) break;  // every candidate view already infected
       }
       newly = __ballot(hit) & cand;
-      if ((newly >> lane) & 1) steprow[v * 64 + lane] = (uint8_t)step;
+      if (steprow && ((newly >> lane) & 1)) steprow[v * 64 + lane] = (uint8_t)step;
+      mycnt += (unsigned int)((newly >> lane) & 1);
     }
     if (lane == 0) {
       front_out[v] = newly;
@@ -124,35 +132,14 @@ __global__ __launch_bounds__(256) void k_diff_step(int step, int64_t nv, const i
     changed |= newly != 0;
   }
   if (lane == 0 && changed) red = 1;
+  if (mycnt) atomicAdd(&acc[lane], mycnt);
   __syncthreads();
   if (threadIdx.x == 0 && red && stepflag[step] == 0) {
     stepflag[step] = 1;
     if (hostflag) hostflag[step] = 1;
   }
-}
-
-// infected vertices per view -> stats[view]; one LDS reduction per block, one atomic per
-// (block, view).
-__global__ __launch_bounds__(256) void k_diff_count(int64_t nv, const uint64_t* __restrict__ inf,
-                                                    unsigned long long* __restrict__ stats) {
-  __shared__ unsigned int acc[64];
-  if (threadIdx.x < 64) acc[threadIdx.x] = 0;
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  unsigned int mine = 0;  // lane j: infected count of view j over this wave's chunks
-  for (int64_t c = wave; c * 64 < nv; c += nwaves) {
-    const int64_t v = c * 64 + lane;
-    const uint64_t x = v < nv ? inf[v] : 0;
-    for (int j = 0; j < 64; j++) {
-      const unsigned int n = (unsigned int)__popcll(__ballot((x >> j) & 1));
-      if (lane == j) mine += n;
-    }
-  }
-  if (mine) atomicAdd(&acc[lane], mine);
-  __syncthreads();
-  if (threadIdx.x < 64 && acc[threadIdx.x]) atomicAdd(&stats[threadIdx.x], (unsigned long long)acc[threadIdx.x]);
+  if (red && threadIdx.x < 64 && acc[threadIdx.x])
+    atomicAdd(&stats[threadIdx.x], (unsigned long long)acc[threadIdx.x]);
 }
 
 static unsigned dgrid(int64_t items, int per_block, unsigned cap) {
@@ -162,22 +149,19 @@ static unsigned dgrid(int64_t items, int per_block, unsigned cap) {
 }
 
 void launch_diff_setup(hipStream_t s, int64_t nv, const uint64_t* vm, int64_t seed, uint64_t* inf,
-                       uint64_t* front0, uint8_t* steprow) {
-  k_diff_setup<<<dgrid(nv * 8, 256, 4096), 256, 0, s>>>(nv, vm, seed, inf, front0,
-                                                         reinterpret_cast<uint64_t*>(steprow));
+                       uint64_t* front0, uint8_t* steprow, unsigned long long* stats) {
+  k_diff_setup<<<dgrid(steprow ? nv * 8 : nv, 256, 4096), 256, 0, s>>>(nv, vm, seed, inf, front0,
+                                                                        reinterpret_cast<uint64_t*>(steprow), stats);
 }
 
 void launch_diff_step(hipStream_t s, int step, const DevGraph& g, const int64_t* vid, const uint64_t* vm,
                       const uint64_t* em, uint64_t* inf, const uint64_t* front_in, uint64_t* front_out,
                       uint8_t* steprow, const DiffSalts& salts, int coin, int32_t* stepflag,
-                      int32_t* hostflag) {
+                      int32_t* hostflag, unsigned long long* stats) {
   k_diff_step<<<dgrid(g.nv, 4, 4096), 256, 0, s>>>(step, g.nv, g.in_off, g.in_eid, g.esrc, vid, vm, em, inf,
                                                     front_in, front_out, steprow, salts, coin, stepflag,
-                                                    hostflag);
+                                                    hostflag, stats);
 }
 
-void launch_diff_count(hipStream_t s, int64_t nv, const uint64_t* inf, unsigned long long* stats) {
-  k_diff_count<<<dgrid(nv, 256, 1024), 256, 0, s>>>(nv, inf, stats);
-}
 
 }  // namespace rgpu

@@ -461,7 +461,8 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     if (rc.algo == RGPU_ALGO_DIFFUSION) {
       timed_launch(c, si, KID_DIFF, 0.0, [&] {
         launch_diff_step(s.stream, r, g, c->d_vid, s.vm, s.em, s.dinf, s.dfront[(r - 1) & 1], s.dfront[r & 1],
-                         s.dstep, s.salts, c->diff_coin, s.stepcnt, c->hostflags ? s.d_hostflag : nullptr);
+                         (rc.flags & RGPU_RUN_RETAIN) ? s.dstep : nullptr, s.salts, c->diff_coin, s.stepcnt,
+                         c->hostflags ? s.d_hostflag : nullptr, s.stats);
       }, r, false);
       continue;
     }
@@ -525,9 +526,6 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
     timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g.nv, g.nv, nviews, s.vm, s.vadj, lab, hist, s.iso); });
     timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * nviews,
                  [&] { launch_cc_summary(s.stream, g, nviews, hist, s.stats, s.iso); });
-  } else if (rc.algo == RGPU_ALGO_DIFFUSION) {
-    launch_diff_count(s.stream, g.nv, s.dinf, s.stats);
-    HIPCHK(hipGetLastError());
   }
   HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatWords,
                         hipMemcpyDeviceToHost, s.stream));
@@ -644,7 +642,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     }
     // Setup (superstep 0) only when defineMaxSteps > 1 (AnalysisTask.timeResponse :169)
     launch_diff_setup(s.stream, g.nv, s.vm, rc.max_steps > 1 ? c->diff_seed_rank : -1, s.dinf, s.dfront[0],
-                      s.dstep);
+                      (rc.flags & RGPU_RUN_RETAIN) ? s.dstep : nullptr, s.stats);
     HIPCHK(hipGetLastError());
     s.r_launched = 0;
     if (rc.max_steps <= 1) {

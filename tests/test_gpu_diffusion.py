@@ -63,6 +63,12 @@ def test_coin_uniform_window_major(uniform):
     for cs in (0, 99):
         assert check_diff(g, o, hops, [MONTH, WEEK, DAY], coin_seed=cs) > 0
     check_diff(g, o, hops[:3], [], coin_seed=7)  # ViewLens
+    # without retain: no per-vertex rows, the infected counts come from the step kernels alone
+    g.set_diffusion(31, 99, True)
+    g.run("diffusion", hops, [MONTH, WEEK, DAY], retain=True)
+    kept = [g.diffusion_result(h, w) for h in range(len(hops)) for w in range(3)]
+    g.run("diffusion", hops, [MONTH, WEEK, DAY], retain=False)
+    assert [g.diffusion_result(h, w) for h in range(len(hops)) for w in range(3)] == kept
     g.run("diffusion", hops, [MONTH, WEEK, DAY], profile=True, serial=True)  # event-timed pass
     k = g.stats()["kernels"]["diffusion"]
     assert k["launches"] > 0 and k["ms"] > 0 and k["bytes"] > 0
