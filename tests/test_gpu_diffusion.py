@@ -118,3 +118,22 @@ def test_analysis_task_lines(uniform):
     import json
     first = json.loads(lines[0])
     assert first["size"] == len(res[0][0])
+
+
+def test_diffusion_after_live_delta_seals():
+    # ids first seen in later chunks shift every rank: the coins hash ids, so the device id
+    # array must follow the merged graph (rgpu_seal's delta path)
+    s = gen_uniform(5, 1500, 30000, dt=31_536 * 33)
+    n = len(s.t)
+    g = TemporalGraph()
+    cuts = [0, n // 3, 2 * n // 3, n]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        g.ingest(s.t[a:b], s.kind[a:b], s.src[a:b], s.dst[a:b])
+        g.seal()
+        o = Oracle(s.t[:b], s.kind[:b], s.src[:b], s.dst[:b])
+        t_end = int(s.t[b - 1])
+        hops = np.array([t_end - 20 * DAY, t_end - 5 * DAY, t_end], np.int64)
+        check_diff(g, o, hops, [MONTH, WEEK], coin_seed=4)
+        check_diff(g, o, hops, [MONTH], coin=False)
+    assert g.stats()["seal_incremental"] == 1
+    g.close()
