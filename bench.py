@@ -46,6 +46,8 @@ def parse():
                         "that its per-kernel averages match the roofline figures)")
     p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "diffusion"],
                    help="c2 = the headline metric; diffusion = BinaryDefusion over the C2 query (secondary)")
+    p.add_argument("--diff-seed", type=int, default=31,
+                   help="diffusion infectedNode (BinaryDefusion.scala:10); -1 = the vertex with most EADDs as source")
     p.add_argument("--c5-users", type=int, default=20_000_000)
     p.add_argument("--c5-base", type=int, default=33_333_334, help="sealed base interactions (x3 updates)")
     p.add_argument("--c5-tick", type=int, default=3_333_334, help="interactions streamed per hour tick (x3 updates)")
@@ -152,14 +154,19 @@ def run_diffusion(a, rank, world, local):
     from raphtory_amd.synth import BATCH_WINDOWS, DAY, HOUR, T0_README, gen_uniform, range_hops
     stream = gen_uniform(1, 100_000, 1_000_000)
     hops = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, HOUR)
+    seed = a.diff_seed
+    if seed < 0:
+        import numpy as np
+        ids, cnt = np.unique(stream.src[stream.kind == 2], return_counts=True)
+        seed = int(ids[np.argmax(cnt)])
     g = TemporalGraph(device=local)
     g.ingest_stream(stream)
     g.seal()
     st = g.stats()
-    out = {"config": "C2 query, BinaryDefusion", "vertices": st["vertices"], "edge_entities": st["edges"],
-           "hops": len(hops), "windows": len(BATCH_WINDOWS)}
+    out = {"config": "C2 query, BinaryDefusion", "infectedNode": seed, "vertices": st["vertices"],
+           "edge_entities": st["edges"], "hops": len(hops), "windows": len(BATCH_WINDOWS)}
     for name, coin in (("coin", True), ("taint", False)):
-        g.set_diffusion(31, 0, coin)
+        g.set_diffusion(seed, 0, coin)
         g.run("diffusion", hops, BATCH_WINDOWS)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
