@@ -43,9 +43,13 @@ __device__ __forceinline__ bool diff_coin(uint64_t salt, int64_t u, int64_t v, i
 }
 
 // superstep 0: clear the batch state; the seed (rank `seed`, < 0 if absent) is infected in
-// every view it belongs to, at step 0.  Rows are written as u64 words (8 views each).
+// every view it belongs to, at step 0, and its out-neighbours are flagged active for step 1
+// (act1 was cleared by the batch's first kernel).  Rows are written as u64 words (8 views).
 __global__ __launch_bounds__(256) void k_diff_setup(int64_t nv, const uint64_t* __restrict__ vm, int64_t seed,
+                                                    const int64_t* __restrict__ out_off,
+                                                    const int32_t* __restrict__ edst,
                                                     uint64_t* __restrict__ inf, uint64_t* __restrict__ front0,
+                                                    uint8_t* __restrict__ act1,
                                                     uint64_t* __restrict__ steprow,
                                                     unsigned long long* __restrict__ stats) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -54,7 +58,10 @@ __global__ __launch_bounds__(256) void k_diff_setup(int64_t nv, const uint64_t* 
     const uint64_t m = v == seed ? vm[v] : 0;
     inf[v] = m;
     front0[v] = m;
-    for (uint64_t b = m; b; b &= b - 1) atomicAdd(&stats[__builtin_ctzll(b)], 1ull);  // infected counts
+    if (m) {
+      for (uint64_t b = m; b; b &= b - 1) atomicAdd(&stats[__builtin_ctzll(b)], 1ull);  // infected counts
+      for (int64_t k = out_off[v]; k < out_off[v + 1]; k++) act1[edst[k]] = 1;
+    }
   }
   if (!steprow) return;  // rows only when the run retains per-vertex results
   for (int64_t i = i0; i < nv * 8; i += stride) {
@@ -68,15 +75,26 @@ __global__ __launch_bounds__(256) void k_diff_setup(int64_t nv, const uint64_t* 
   }
 }
 
+// Superstep `step`.  Only vertices flagged active (an in-neighbour was newly infected at
+// step-1, flagged by that step) can receive a message.  A wave takes 64 vertices (lane =
+// vertex: flags, masks, front stores coalesced), then for each active candidate pulls its
+// in-edges 64 at a time (lane = in-edge) and flips the coins of the edges carrying a
+// message (lane = view).  A newly infected vertex flags its out-neighbours for step+1.
+// Flag buffers rotate over three steps: read act_cur, write act_next, clear act_clear.
 __global__ __launch_bounds__(256) void k_diff_step(int step, int64_t nv, const int64_t* __restrict__ in_off,
                                                    const int32_t* __restrict__ in_eid,
                                                    const int32_t* __restrict__ esrc,
+                                                   const int64_t* __restrict__ out_off,
+                                                   const int32_t* __restrict__ edst,
                                                    const int64_t* __restrict__ vid,
                                                    const uint64_t* __restrict__ vm,
                                                    const uint64_t* __restrict__ em,
                                                    uint64_t* __restrict__ inf,
                                                    const uint64_t* __restrict__ front_in,
                                                    uint64_t* __restrict__ front_out,
+                                                   const uint8_t* __restrict__ act_cur,
+                                                   uint8_t* __restrict__ act_next,
+                                                   uint8_t* __restrict__ act_clear,
                                                    uint8_t* __restrict__ steprow, DiffSalts salts, int coin,
                                                    int32_t* __restrict__ stepflag,
                                                    int32_t* __restrict__ hostflag,
@@ -86,6 +104,10 @@ __global__ __launch_bounds__(256) void k_diff_step(int step, int64_t nv, const i
   __shared__ unsigned int acc[64];  // newly infected per view, this block
   if (threadIdx.x == 0) red = 0;
   if (threadIdx.x < 64) acc[threadIdx.x] = 0;
+  const int64_t nwords = (nv + 7) >> 3;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
+       i += (int64_t)gridDim.x * blockDim.x)
+    reinterpret_cast<uint64_t*>(act_clear)[i] = 0;
   __syncthreads();
   unsigned int mycnt = 0;  // lane j: vertices this wave infected in view j
   const int lane = threadIdx.x & 63;
@@ -93,15 +115,22 @@ __global__ __launch_bounds__(256) void k_diff_step(int step, int64_t nv, const i
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int32_t changed = 0;
-  for (int64_t v = wave; v < nv; v += nwaves) {
-    const uint64_t cand = vm[v] & ~inf[v];  // members not yet infected
-    uint64_t newly = 0;
-    if (cand) {
-      const int64_t k0 = in_off[v], k1 = in_off[v + 1];
-      const int64_t myid = vid[v];
+  for (int64_t c = wave; c * 64 < nv; c += nwaves) {
+    const int64_t v = c * 64 + lane;
+    const bool in = v < nv;
+    const bool a = in && act_cur[v] != 0;
+    const uint64_t infl = a ? inf[v] : 0;
+    const uint64_t cand_l = a ? (vm[v] & ~infl) : 0;  // members not yet infected
+    uint64_t newly_l = 0;
+    uint64_t todo = __ballot(cand_l != 0);
+    while (todo) {
+      const int l = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const int64_t vv = c * 64 + l;
+      const uint64_t cand = __shfl(cand_l, l);
+      const int64_t k0 = in_off[vv], k1 = in_off[vv + 1];
+      const int64_t myid = vid[vv];
       bool hit = false;
-      // lane = in-edge for the loads (one dependent chain in_eid -> esrc -> front per 64
-      // in-edges), lane = view for the coins of the few edges that carry a message
       for (int64_t base = k0; base < k1; base += 64) {
         const int64_t k = base + lane;
         uint64_t f = 0;
@@ -113,25 +142,31 @@ __global__ __launch_bounds__(256) void k_diff_step(int step, int64_t nv, const i
         }
         uint64_t msg = __ballot(f != 0);
         while (msg) {
-          const int l = __builtin_ctzll(msg);
+          const int m = __builtin_ctzll(msg);
           msg &= msg - 1;
-          const uint64_t fl = __shfl(f, l);
-          const int32_t ul = __shfl(u, l);
-          if (!hit && ((fl >> lane) & 1)) hit = coin ? diff_coin(salt, vid[ul], myid, step - 1) : true;
+          const uint64_t fm = __shfl(f, m);
+          const int32_t um = __shfl(u, m);
+          if (!hit && ((fm >> lane) & 1)) hit = coin ? diff_coin(salt, vid[um], myid, step - 1) : true;
         }
         if ((__ballot(hit) & cand) == cand) break;  // every candidate view already infected
       }
-      newly = __ballot(hit) & cand;
-      if (steprow && ((newly >> lane) & 1)) steprow[v * 64 + lane] = (uint8_t)step;
-      mycnt += (unsigned int)((newly >> lane) & 1);
+      const uint64_t newly = __ballot(hit) & cand;
+      if (newly) {
+        if (lane == l) newly_l = newly;
+        if ((newly >> lane) & 1) {
+          if (steprow) steprow[vv * 64 + lane] = (uint8_t)step;
+          mycnt++;
+        }
+        for (int64_t k = out_off[vv] + lane; k < out_off[vv + 1]; k += 64) act_next[edst[k]] = 1;
+      }
     }
-    if (lane == 0) {
-      front_out[v] = newly;
-      if (newly) inf[v] |= newly;
+    if (in) {
+      front_out[v] = newly_l;
+      if (newly_l) inf[v] = infl | newly_l;
     }
-    changed |= newly != 0;
+    changed |= newly_l != 0;
   }
-  if (lane == 0 && changed) red = 1;
+  if (changed) red = 1;
   if (mycnt) atomicAdd(&acc[lane], mycnt);
   __syncthreads();
   if (threadIdx.x == 0 && red && stepflag[step] == 0) {
@@ -148,20 +183,20 @@ static unsigned dgrid(int64_t items, int per_block, unsigned cap) {
   return (unsigned)(g > cap ? cap : g);
 }
 
-void launch_diff_setup(hipStream_t s, int64_t nv, const uint64_t* vm, int64_t seed, uint64_t* inf,
-                       uint64_t* front0, uint8_t* steprow, unsigned long long* stats) {
-  k_diff_setup<<<dgrid(steprow ? nv * 8 : nv, 256, 4096), 256, 0, s>>>(nv, vm, seed, inf, front0,
-                                                                        reinterpret_cast<uint64_t*>(steprow), stats);
+void launch_diff_setup(hipStream_t s, const DevGraph& g, const uint64_t* vm, int64_t seed, uint64_t* inf,
+                       uint64_t* front0, uint8_t* act1, uint8_t* steprow, unsigned long long* stats) {
+  k_diff_setup<<<dgrid(steprow ? g.nv * 8 : g.nv, 256, 4096), 256, 0, s>>>(
+      g.nv, vm, seed, g.out_off, g.edst, inf, front0, act1, reinterpret_cast<uint64_t*>(steprow), stats);
 }
 
 void launch_diff_step(hipStream_t s, int step, const DevGraph& g, const int64_t* vid, const uint64_t* vm,
                       const uint64_t* em, uint64_t* inf, const uint64_t* front_in, uint64_t* front_out,
-                      uint8_t* steprow, const DiffSalts& salts, int coin, int32_t* stepflag,
-                      int32_t* hostflag, unsigned long long* stats) {
-  k_diff_step<<<dgrid(g.nv, 4, 4096), 256, 0, s>>>(step, g.nv, g.in_off, g.in_eid, g.esrc, vid, vm, em, inf,
-                                                    front_in, front_out, steprow, salts, coin, stepflag,
-                                                    hostflag, stats);
+                      const uint8_t* act_cur, uint8_t* act_next, uint8_t* act_clear, uint8_t* steprow,
+                      const DiffSalts& salts, int coin, int32_t* stepflag, int32_t* hostflag,
+                      unsigned long long* stats) {
+  k_diff_step<<<dgrid(g.nv, 256, 1024), 256, 0, s>>>(step, g.nv, g.in_off, g.in_eid, g.esrc, g.out_off, g.edst,
+                                                      vid, vm, em, inf, front_in, front_out, act_cur, act_next,
+                                                      act_clear, steprow, salts, coin, stepflag, hostflag, stats);
 }
-
 
 }  // namespace rgpu

@@ -122,12 +122,13 @@ struct DiffSalts {
   uint64_t s[64];
 };
 // steprow may be null (no per-vertex rows: the run does not retain); stats[view] counts infected
-void launch_diff_setup(hipStream_t s, int64_t nv, const uint64_t* vm, int64_t seed, uint64_t* inf,
-                       uint64_t* front0, uint8_t* steprow, unsigned long long* stats);
+void launch_diff_setup(hipStream_t s, const DevGraph& g, const uint64_t* vm, int64_t seed, uint64_t* inf,
+                       uint64_t* front0, uint8_t* act1, uint8_t* steprow, unsigned long long* stats);
 void launch_diff_step(hipStream_t s, int step, const DevGraph& g, const int64_t* vid, const uint64_t* vm,
                       const uint64_t* em, uint64_t* inf, const uint64_t* front_in, uint64_t* front_out,
-                      uint8_t* steprow, const DiffSalts& salts, int coin, int32_t* stepflag,
-                      int32_t* hostflag, unsigned long long* stats);
+                      const uint8_t* act_cur, uint8_t* act_next, uint8_t* act_clear, uint8_t* steprow,
+                      const DiffSalts& salts, int coin, int32_t* stepflag, int32_t* hostflag,
+                      unsigned long long* stats);
 
 // partition exchange (vertex-partitioned mode)
 constexpr int kXRecWords = 68;  // ints per boundary-row record

@@ -81,6 +81,7 @@ struct Slot {
   // BinaryDefusion (diffusion.hip): infected views, views infected last / this step, step rows
   uint64_t *dinf = nullptr, *dfront[2] = {nullptr, nullptr};
   uint8_t* dstep = nullptr;
+  uint8_t* dact[3] = {nullptr, nullptr, nullptr};  // active (message-holding) flags, rotated
   DiffSalts salts;                // coin salt per lane of the batch in flight
   unsigned long long* h_stats = nullptr;
   // state of the batch in flight
@@ -362,6 +363,7 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       s.dfront[0] = dalloc<uint64_t>(L, nv + kPad);
       s.dfront[1] = dalloc<uint64_t>(L, nv + kPad);
       s.dstep = dalloc<uint8_t>(L, rows);
+      for (int b = 0; b < 3; b++) s.dact[b] = dalloc<uint8_t>(L, (size_t)((nv + 7) / 8 + 1) * 8);
     }
     if (algo == RGPU_ALGO_PR && !s.a_pr) {
       s.pr = dalloc<double>(L, rows);
@@ -461,6 +463,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     if (rc.algo == RGPU_ALGO_DIFFUSION) {
       timed_launch(c, si, KID_DIFF, 0.0, [&] {
         launch_diff_step(s.stream, r, g, c->d_vid, s.vm, s.em, s.dinf, s.dfront[(r - 1) & 1], s.dfront[r & 1],
+                         s.dact[r % 3], s.dact[(r + 1) % 3], s.dact[(r + 2) % 3],
                          (rc.flags & RGPU_RUN_RETAIN) ? s.dstep : nullptr, s.salts, c->diff_coin, s.stepcnt,
                          c->hostflags ? s.d_hostflag : nullptr, s.stats);
       }, r, false);
@@ -600,8 +603,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   clr.n_stats = kStatWords;
   clr.flags = s.stepcnt;
   clr.n_flags = kMaxSteps;
-  if (rc.algo == RGPU_ALGO_CC) {
-    for (int b = 0; b < 3; b++) clr.act[b] = s.act[b];
+  if (rc.algo == RGPU_ALGO_CC || rc.algo == RGPU_ALGO_DIFFUSION) {
+    for (int b = 0; b < 3; b++) clr.act[b] = rc.algo == RGPU_ALGO_CC ? s.act[b] : s.dact[b];
     clr.n_act_words = (g.nv + 7) / 8 + 1;
   }
   if (s.work && c->profile)
@@ -641,8 +644,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       s.salts.s[j] = diff_salt(c->diff_coin_seed, t, w);
     }
     // Setup (superstep 0) only when defineMaxSteps > 1 (AnalysisTask.timeResponse :169)
-    launch_diff_setup(s.stream, g.nv, s.vm, rc.max_steps > 1 ? c->diff_seed_rank : -1, s.dinf, s.dfront[0],
-                      (rc.flags & RGPU_RUN_RETAIN) ? s.dstep : nullptr, s.stats);
+    launch_diff_setup(s.stream, g, s.vm, rc.max_steps > 1 ? c->diff_seed_rank : -1, s.dinf, s.dfront[0],
+                      s.dact[1], (rc.flags & RGPU_RUN_RETAIN) ? s.dstep : nullptr, s.stats);
     HIPCHK(hipGetLastError());
     s.r_launched = 0;
     if (rc.max_steps <= 1) {
@@ -754,10 +757,10 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
     c->grp_last[grp] = s.r_final;
   }
   if (rc.algo == RGPU_ALGO_DIFFUSION) {
-    // per executed superstep: vm, inf, in_off pair, front out (40 B per vertex)
-    // and per in-edge in_eid, esrc, em, the source's front word (24 B); a vertex with no
-    // candidate view skips its in-edges, so this is the full-pass (upper) figure
-    c->st.kernel_bytes[KID_DIFF] += s.r_final * (40.0 * c->g.nv + 24.0 * c->g.n_in);
+    // per executed superstep, the part every step pays: active flag read, flag
+    // clear two steps ahead, front word store (9.125 B per vertex).  Active vertices' masks and
+    // in-edges come on top and are not counted (a lower bound)
+    c->st.kernel_bytes[KID_DIFF] += s.r_final * (9.125 * c->g.nv);
     c->st.supersteps += s.r_final;
     c->grp_last[grp] = s.r_final;
   }
