@@ -1185,7 +1185,8 @@ __device__ __forceinline__ void fold_iso(unsigned int* __restrict__ iso_g, int j
 }
 
 // processBatchWindowResults summary per view (ConnectedComponents.scala:137-145) from the
-// view-major histogram hist[view][rank]; clears it for the next batch.  blockIdx.y = view,
+// view-major histogram hist[view][rank] (read only: the buffer is the batch's free label row,
+// zeroed by the memset before k_cc_hist and overwritten by the next batch).  blockIdx.y = view,
 // blockIdx.x strides over ranks; one atomic per (block, field).  stats[f*64 + view]:
 // 0 biggest 1 total 2 total>1 3 total>2 4 sum 5 sum(count>1)
 __global__ __launch_bounds__(256) void k_cc_summary(int64_t nv, int32_t* __restrict__ hist,
@@ -1200,7 +1201,6 @@ __global__ __launch_bounds__(256) void k_cc_summary(int64_t nv, int32_t* __restr
        r += (int64_t)gridDim.x * blockDim.x) {
     const int32_t c = h[r];
     if (c) {
-      h[r] = 0;
       const unsigned long long uc = (unsigned long long)c;
       big = uc > big ? uc : big;
       tot += 1;
