@@ -1096,18 +1096,19 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
 
 // ---------------------------------------------------------------- K5: CC reductions
 // label -> count histogram (ConnectedComponents.returnResults :37-42, groupBy over labels).
-// A block stages the label rows of 64 consecutive vertices in LDS (16 rows per wave), then
-// its four waves split the views (wave w takes views j = w mod 4): per view the 64 vertices
+// A block stages the label rows of 64 consecutive vertices in LDS (8 rows per wave), then
+// its eight waves split the views (wave w takes views j = w mod 8): per view the 64 vertices
 // sit on the lanes and each distinct label is added once per chunk (popcount of the lanes
 // that carry it), so the giant component costs one atomic per 64 vertices, not one per
 // vertex.  The dedup loop is serial (a ballot per distinct label), so after `rounds` labels
 // the remaining lanes (small components) issue their own atomics in one instruction.  The per-view loop is serial, latency-bound work: one chunk per block keeps ~24
-// waves per CU on it (one chunk per wave kept ~6).
+// waves per CU on it (one chunk per wave kept ~6); eight waves of 8 views each instead of four of
+// 16 halve each wave's chain (C2 serial 31.8 -> 29.0 ms).
 // Members with no kept slot in a view are isolated there: islands (count 1) that need no
 // histogram entry.  Their counts go to iso[shard][view] (64 shards: a few dozen blocks per
 // address, not thousands); the summary kernel folds them into total / sum / biggest.
 template <bool BUF>
-__global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int64_t hstride, int nviews,
+__global__ __launch_bounds__(512) void k_cc_hist(int64_t nv, int64_t hstride, int nviews,
                                                  const uint64_t* __restrict__ vm,
                                                  const uint64_t* __restrict__ vadj,
                                                  const int32_t* __restrict__ lab,
@@ -1117,15 +1118,15 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int64_t hstride, in
   __shared__ unsigned int iso[64];
   if (threadIdx.x < 64) iso[threadIdx.x] = 0;
   const int lane = lane_id(), wib = threadIdx.x >> 6;
-  const uint64_t vmask = (nviews >= 64 ? ~0ull : ((1ull << nviews) - 1)) & (0x1111111111111111ull << wib);
+  const uint64_t vmask = (nviews >= 64 ? ~0ull : ((1ull << nviews) - 1)) & (0x0101010101010101ull << wib);
   for (int64_t c = blockIdx.x; c * 64 < nv; c += gridDim.x) {
     const int64_t v0 = c * 64;
     const int nvc = (int)(nv - v0 < 64 ? nv - v0 : 64);
     {
-      int32_t r[16];  // 16 independent row loads in flight, then LDS
+      int32_t r[8];  // 8 independent row loads in flight per wave, then LDS
 #pragma unroll
-      for (int k = 0; k < 16; k++) {
-        const int i = wib * 16 + k;
+      for (int k = 0; k < 8; k++) {
+        const int i = wib * 8 + k;
         if (BUF) {
           const uint64_t mk = i < nvc ? vm[v0 + i] : 0;  // scalar: wave-uniform vertex
           r[k] = row_load(lab + (v0 + i) * 64, (mk >> lane) & 1, lane);
@@ -1134,7 +1135,7 @@ __global__ __launch_bounds__(256) void k_cc_hist(int64_t nv, int64_t hstride, in
         }
       }
 #pragma unroll
-      for (int k = 0; k < 16; k++) tile[wib * 16 + k][lane] = r[k];
+      for (int k = 0; k < 8; k++) tile[wib * 8 + k][lane] = r[k];
     }
     const uint64_t mvl = lane < nvc ? vm[v0 + lane] : 0;
     const uint64_t adl = lane < nvc ? vadj[v0 + lane] : 0;
@@ -1814,8 +1815,8 @@ void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g,
 void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso) {
   const unsigned grid = grid_for(nv, 64, 8192);
-  if (g_rowbuf) k_cc_hist<true><<<grid, 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso, g_hist_rounds);
-  else k_cc_hist<false><<<grid, 256, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso, g_hist_rounds);
+  if (g_rowbuf) k_cc_hist<true><<<grid, 512, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso, g_hist_rounds);
+  else k_cc_hist<false><<<grid, 512, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso, g_hist_rounds);
 }
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
                        unsigned long long* stats, unsigned int* iso) {
