@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RGPU_ABI_VERSION 5
+#define RGPU_ABI_VERSION 6
 
 /* error codes */
 #define RGPU_OK 0
@@ -66,7 +66,12 @@ typedef struct {
   int64_t clusters_gt2;          /* labels with count > 2 ("clustersGT2")          */
   int64_t sum_all;               /* sum of counts = |view vertices| (proportion)   */
   int64_t sum_without_islands;   /* sum of counts > 1 (proportionWithoutIslands)   */
-  int64_t supersteps;            /* supersteps executed for the batch holding it   */
+  int64_t supersteps;            /* supersteps the reference's job for this hop runs: min(maxSteps,
+                                    1 + last superstep in which a label of any of the hop's windows
+                                    changed); 0 when maxSteps <= 1 (no Setup, AnalysisTask.scala:169)
+                                    (ABI 6; before: the step count of the batch holding the view) */
+  int64_t alive_edges;           /* |E_{t,w}|: edges alive in the view's window; filled by
+                                    RGPU_RUN_PROFILE runs, else -1 (ABI 6) */
 } rgpu_cc_summary_t;
 
 typedef struct {
@@ -84,6 +89,8 @@ typedef struct {
    * and the number of updates that delta held (ABI 3) */
   double seal_ms;
   int64_t seal_incremental, seal_delta_updates;
+  /* last run, RGPU_RUN_PROFILE: sum over its views of |E_{t,w}| (else -1) (ABI 6) */
+  int64_t alive_edge_windows;
 } rgpu_stats_t;
 
 int rgpu_abi_version(void);

@@ -37,6 +37,8 @@ def lib() -> C.CDLL:
         L = C.CDLL(LIB)
         L.orc_build.restype = C.c_void_p
         L.orc_build.argtypes = [_P64, _PU8, _P64, _P64, _SZ]
+        L.orc_build_ex.restype = C.c_void_p
+        L.orc_build_ex.argtypes = [_P64, _PU8, _P64, _P64, _SZ, C.c_int]
         L.orc_free.argtypes = [C.c_void_p]
         L.orc_num_vertices.restype = _SZ
         L.orc_num_vertices.argtypes = [C.c_void_p]
@@ -64,25 +66,33 @@ def _p(a, t):
     return a.ctypes.data_as(C.POINTER(t))
 
 
-class Oracle:
-    """EntityStorage replay + reference-structured analysers on the CPU."""
+ORC_LAZY_EDGES = 1
 
-    def __init__(self, t, kind, src, dst):
+
+class Oracle:
+    """EntityStorage replay + reference-structured analysers on the CPU.
+
+    lazy=True: the replay keeps endpoint deaths in the vertices' removeLists and reads them when
+    an edge is evaluated, instead of copying them into every edge (oracle.h, ORC_LAZY_EDGES) —
+    the same answers, without the O(degree x deaths) copies that make the literal replay
+    intractable on power-law streams of 10^8 updates (configs C3/C4)."""
+
+    def __init__(self, t, kind, src, dst, lazy: bool = False):
         L = lib()
         self.t = np.ascontiguousarray(t, np.int64)
         self.kind = np.ascontiguousarray(kind, np.uint8)
         self.src = np.ascontiguousarray(src, np.int64)
         self.dst = np.ascontiguousarray(dst, np.int64)
-        self._g = L.orc_build(_p(self.t, C.c_int64), _p(self.kind, C.c_uint8), _p(self.src, C.c_int64),
-                              _p(self.dst, C.c_int64), self.t.shape[0])
+        self._g = L.orc_build_ex(_p(self.t, C.c_int64), _p(self.kind, C.c_uint8), _p(self.src, C.c_int64),
+                                 _p(self.dst, C.c_int64), self.t.shape[0], ORC_LAZY_EDGES if lazy else 0)
         if not self._g:
             raise ValueError("oracle rejected the stream (negative time or id outside [0, 2^31))")
         self.nv = L.orc_num_vertices(self._g)
         self.ne = L.orc_num_edges(self._g)
 
     @classmethod
-    def from_stream(cls, s):
-        return cls(s.t, s.kind, s.src, s.dst)
+    def from_stream(cls, s, lazy: bool = False):
+        return cls(s.t, s.kind, s.src, s.dst, lazy=lazy)
 
     def close(self):
         if self._g:

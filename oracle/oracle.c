@@ -36,10 +36,11 @@
 typedef struct {
   int64_t* k;
   uint8_t* v;
+  int64_t* s; /* lazy-edge build only: stream index of the last put per key (NULL otherwise) */
   int n, cap;
 } TMap;
 
-static int tm_put(TMap* m, int64_t k, uint8_t v) {
+static int tm_put_seq(TMap* m, int64_t k, uint8_t v, int64_t seq, int keep_seq) {
   int lo = 0, hi = m->n;
   if (m->n > 0 && m->k[m->n - 1] < k) {
     lo = hi = m->n; /* append fast path: streams are mostly time ordered */
@@ -48,21 +49,40 @@ static int tm_put(TMap* m, int64_t k, uint8_t v) {
       int mid = (lo + hi) >> 1;
       if (m->k[mid] < k) lo = mid + 1; else hi = mid;
     }
-    if (lo < m->n && m->k[lo] == k) { m->v[lo] = v; return 0; } /* last put wins */
+    if (lo < m->n && m->k[lo] == k) { /* last put wins */
+      m->v[lo] = v;
+      if (m->s) m->s[lo] = seq;
+      return 0;
+    }
   }
   if (m->n == m->cap) {
     int nc = m->cap ? m->cap * 2 : 4;
     int64_t* nk = (int64_t*)realloc(m->k, sizeof(int64_t) * nc);
+    if (!nk) return -1;
+    m->k = nk;
     uint8_t* nv = (uint8_t*)realloc(m->v, nc);
-    if (!nk || !nv) return -1;
-    m->k = nk; m->v = nv; m->cap = nc;
+    if (!nv) return -1;
+    m->v = nv;
+    if (keep_seq || m->s) {
+      int64_t* ns = (int64_t*)realloc(m->s, sizeof(int64_t) * nc);
+      if (!ns) return -1;
+      m->s = ns;
+    }
+    m->cap = nc;
   }
   memmove(m->k + lo + 1, m->k + lo, sizeof(int64_t) * (m->n - lo));
   memmove(m->v + lo + 1, m->v + lo, (size_t)(m->n - lo));
-  m->k[lo] = k; m->v[lo] = v; m->n++;
+  if (m->s) memmove(m->s + lo + 1, m->s + lo, sizeof(int64_t) * (m->n - lo));
+  m->k[lo] = k; m->v[lo] = v;
+  if (m->s) m->s[lo] = seq;
+  m->n++;
   return 0;
 }
-static void tm_free(TMap* m) { free(m->k); free(m->v); m->k = NULL; m->v = NULL; m->n = m->cap = 0; }
+static int tm_put(TMap* m, int64_t k, uint8_t v) { return tm_put_seq(m, k, v, 0, 0); }
+static void tm_free(TMap* m) {
+  free(m->k); free(m->v); free(m->s);
+  m->k = NULL; m->v = NULL; m->s = NULL; m->n = m->cap = 0;
+}
 
 /* ----------------------------------------------------------------- entities */
 typedef struct {
@@ -83,23 +103,37 @@ static int iv_push(IVec* v, int x) {
   return 0;
 }
 
-typedef struct { Entity e; int64_t src, dst; } Edge;
-typedef struct { Entity e; int64_t id; IVec out, in; } Vertex;
+/* Lazy-edge build (orc_build_ex(..., ORC_LAZY_EDGES)): an edge keeps only its OWN puts, each
+ * with the stream index of its last put; the endpoint-death puts that the literal replay copies
+ * into it (killList at creation, Edge.scala:36-44, EntityStorage.scala:262,277-278) or writes
+ * into it later (vertexRemoval's kill loops, :189-228) are read from the endpoints' removeLists
+ * when the edge is evaluated.  c = stream index of the edge's creation; si/di = endpoint
+ * vertex indices. */
+typedef struct { Entity e; int64_t src, dst; int32_t si, di; int64_t c; } Edge;
+/* dl_t/dl_s: the vertex's VertexDelete log in stream order (lazy build); dsuf[i] = min dl_t[i..] */
+typedef struct { Entity e; int64_t id; IVec out, in; int64_t *dl_t, *dl_s, *dsuf; int dn, dcap; } Vertex;
 
 /* Entity constructor (Entity.scala:18-36): previousState = {creationTime -> isInitialValue},
- * removeList = {creationTime -> false} iff !isInitialValue. */
-static void ent_init(Entity* e, int64_t t, int initial) {
+ * removeList = {creationTime -> false} iff !isInitialValue.  seq/keep: lazy-build bookkeeping. */
+static void ent_init(Entity* e, int64_t t, int initial, int64_t seq, int keep) {
   memset(e, 0, sizeof(*e));
-  tm_put(&e->hist, t, (uint8_t)(initial ? 1 : 0));
-  if (!initial) tm_put(&e->rem, t, 0);
+  tm_put_seq(&e->hist, t, (uint8_t)(initial ? 1 : 0), seq, keep);
+  if (!initial) tm_put_seq(&e->rem, t, 0, seq, keep);
   e->oldest = e->newest = t;
 }
 static void ent_check(Entity* e, int64_t t) { /* checkOldestNewest, Entity.scala:52-57 */
   if (t > e->newest) e->newest = t;
   if (e->oldest > t) e->oldest = t;
 }
-static void ent_revive(Entity* e, int64_t t) { ent_check(e, t); tm_put(&e->hist, t, 1); }       /* :41-44 */
-static void ent_kill(Entity* e, int64_t t) { ent_check(e, t); tm_put(&e->rem, t, 0); tm_put(&e->hist, t, 0); } /* :46-50 */
+static void ent_revive(Entity* e, int64_t t, int64_t seq, int keep) { /* :41-44 */
+  ent_check(e, t);
+  tm_put_seq(&e->hist, t, 1, seq, keep);
+}
+static void ent_kill(Entity* e, int64_t t, int64_t seq, int keep) { /* :46-50 */
+  ent_check(e, t);
+  tm_put_seq(&e->rem, t, 0, seq, keep);
+  tm_put_seq(&e->hist, t, 0, seq, keep);
+}
 static void edge_killlist(Entity* e, const TMap* vk) { /* Edge.killList, Edge.scala:36-44 (no checkOldestNewest) */
   for (int i = 0; i < vk->n; i++) { tm_put(&e->rem, vk->k[i], 0); tm_put(&e->hist, vk->k[i], 0); }
 }
@@ -164,6 +198,8 @@ struct orc_graph {
   Edge* es; size_t ne, cape;
   HMap vmap, emap;
   int32_t* order; /* vertex indices sorted by id (ParTrieMap iteration order is irrelevant) */
+  int lazy;       /* ORC_LAZY_EDGES: endpoint deaths read at evaluation, not copied (see Edge) */
+  int64_t seq;    /* stream index of the update being applied */
 };
 
 static uint64_t ekey(int64_t s, int64_t d) { return ((uint64_t)s << 32) | (uint64_t)d; }
@@ -177,12 +213,12 @@ static int new_vertex(orc_graph* g, int64_t t, int64_t id, int initial) {
   }
   Vertex* v = &g->vs[g->nv];
   memset(v, 0, sizeof(*v));
-  ent_init(&v->e, t, initial);
+  ent_init(&v->e, t, initial, g->seq, g->lazy);
   v->id = id;
   if (hm_put(&g->vmap, (uint64_t)id, (int32_t)g->nv) != 0) return -1;
   return (int)g->nv++;
 }
-static int new_edge(orc_graph* g, int64_t t, int64_t s, int64_t d, int initial) {
+static int new_edge(orc_graph* g, int64_t t, int64_t s, int64_t d, int initial, int si) {
   if (g->ne == g->cape) {
     size_t nc = g->cape ? g->cape * 2 : 1024;
     Edge* nes = (Edge*)realloc(g->es, sizeof(Edge) * nc);
@@ -191,8 +227,10 @@ static int new_edge(orc_graph* g, int64_t t, int64_t s, int64_t d, int initial) 
   }
   Edge* e = &g->es[g->ne];
   memset(e, 0, sizeof(*e));
-  ent_init(&e->e, t, initial);
+  ent_init(&e->e, t, initial, g->seq, g->lazy);
   e->src = s; e->dst = d;
+  e->si = e->di = si;
+  e->c = g->seq;
   if (hm_put(&g->emap, ekey(s, d), (int32_t)g->ne) != 0) return -1;
   return (int)g->ne++;
 }
@@ -200,7 +238,7 @@ static int new_edge(orc_graph* g, int64_t t, int64_t s, int64_t d, int initial) 
 /* EntityStorage.vertexAdd, :73-87 */
 static int vertex_add(orc_graph* g, int64_t t, int64_t id) {
   int32_t vi = hm_get(&g->vmap, (uint64_t)id);
-  if (vi >= 0) { ent_revive(&g->vs[vi].e, t); return vi; }
+  if (vi >= 0) { ent_revive(&g->vs[vi].e, t, g->seq, g->lazy); return vi; }
   return new_vertex(g, t, id, 1);
 }
 /* EntityStorage.getVertexOrPlaceholder, :89-97 (new vertex, then wipe()) */
@@ -214,11 +252,27 @@ static int vertex_or_placeholder(orc_graph* g, int64_t t, int64_t id) {
 /* EntityStorage.vertexRemoval, :148-232 */
 static int vertex_removal(orc_graph* g, int64_t t, int64_t id) {
   int32_t vi = hm_get(&g->vmap, (uint64_t)id);
-  if (vi >= 0) ent_kill(&g->vs[vi].e, t);
+  if (vi >= 0) ent_kill(&g->vs[vi].e, t, g->seq, g->lazy);
   else if ((vi = new_vertex(g, t, id, 0)) < 0) return -1; /* placeholder created dead, :153-156 */
   Vertex* v = &g->vs[vi];
-  for (int i = 0; i < v->in.n; i++) ent_kill(&g->es[v->in.a[i]].e, t);   /* :189-213 */
-  for (int i = 0; i < v->out.n; i++) ent_kill(&g->es[v->out.a[i]].e, t); /* :214-228 */
+  if (g->lazy) { /* the kill loops below, deferred: log the death (time, stream index) */
+    if (v->dn == v->dcap) {
+      int nc = v->dcap ? v->dcap * 2 : 4;
+      int64_t* nt = (int64_t*)realloc(v->dl_t, sizeof(int64_t) * nc);
+      if (!nt) return -1;
+      v->dl_t = nt;
+      int64_t* ns = (int64_t*)realloc(v->dl_s, sizeof(int64_t) * nc);
+      if (!ns) return -1;
+      v->dl_s = ns;
+      v->dcap = nc;
+    }
+    v->dl_t[v->dn] = t;
+    v->dl_s[v->dn] = g->seq;
+    v->dn++;
+    return 0;
+  }
+  for (int i = 0; i < v->in.n; i++) ent_kill(&g->es[v->in.a[i]].e, t, g->seq, 0);   /* :189-213 */
+  for (int i = 0; i < v->out.n; i++) ent_kill(&g->es[v->out.a[i]].e, t, g->seq, 0); /* :214-228 */
   return 0;
 }
 /* EntityStorage.edgeAdd, :237-290 (local && sameWorker order; other-worker and remote
@@ -229,19 +283,20 @@ static int edge_add(orc_graph* g, int64_t t, int64_t s, int64_t d) {
   int32_t ei = hm_get(&g->emap, ekey(s, d));
   int present = ei >= 0;
   if (!present) {
-    if ((ei = new_edge(g, t, s, d, 1)) < 0) return -1;
+    if ((ei = new_edge(g, t, s, d, 1, si)) < 0) return -1;
     if (iv_push(&g->vs[si].out, ei) != 0) return -1; /* srcVertex.addOutgoingEdge, :255 */
   }
   if (s != d) { /* :257-263 */
     int di = vertex_add(g, t, d);
     if (di < 0) return -1;
     if (!present) {
+      g->es[ei].di = di;
       if (iv_push(&g->vs[di].in, ei) != 0) return -1;
-      edge_killlist(&g->es[ei].e, &g->vs[di].e.rem);
+      if (!g->lazy) edge_killlist(&g->es[ei].e, &g->vs[di].e.rem);
     }
   }
-  if (present) ent_revive(&g->es[ei].e, t);                 /* :268-269 */
-  else edge_killlist(&g->es[ei].e, &g->vs[si].e.rem);       /* :276-278 */
+  if (present) ent_revive(&g->es[ei].e, t, g->seq, g->lazy);                /* :268-269 */
+  else if (!g->lazy) edge_killlist(&g->es[ei].e, &g->vs[si].e.rem);         /* :276-278 */
   return 0;
 }
 /* EntityStorage.edgeRemoval, :327-383 */
@@ -251,20 +306,98 @@ static int edge_removal(orc_graph* g, int64_t t, int64_t s, int64_t d) {
   int32_t ei = hm_get(&g->emap, ekey(s, d));
   int present = ei >= 0;
   if (!present) {
-    if ((ei = new_edge(g, t, s, d, 0)) < 0) return -1;      /* initialValue = false, :341 */
+    if ((ei = new_edge(g, t, s, d, 0, si)) < 0) return -1;   /* initialValue = false, :341 */
     if (iv_push(&g->vs[si].out, ei) != 0) return -1;
   }
   if (s != d) {
     int di = vertex_or_placeholder(g, t, d);
     if (di < 0) return -1;
     if (!present) {
+      g->es[ei].di = di;
       if (iv_push(&g->vs[di].in, ei) != 0) return -1;
-      edge_killlist(&g->es[ei].e, &g->vs[di].e.rem);
+      if (!g->lazy) edge_killlist(&g->es[ei].e, &g->vs[di].e.rem);
     }
   }
-  if (present) ent_kill(&g->es[ei].e, t);                   /* :365-366 */
-  else edge_killlist(&g->es[ei].e, &g->vs[si].e.rem);       /* :373-375 */
+  if (present) ent_kill(&g->es[ei].e, t, g->seq, g->lazy);                  /* :365-366 */
+  else if (!g->lazy) edge_killlist(&g->es[ei].e, &g->vs[si].e.rem);         /* :373-375 */
   return 0;
+}
+
+/* ---- lazy edges: the merged history, read on demand ----
+ * A put's effective order: own puts at 2*seq; an endpoint death logged after the edge's
+ * creation (vertexRemoval's kill loop) at 2*seq; one logged before it (copied by killList right
+ * after the creation put, Edge.scala:36-44) at 2*c+1.  At equal keys the later put wins, as in
+ * the TreeMap.  A death's key in removeList carries its LAST stream index (tm_put_seq). */
+static int64_t death_order(const Edge* e, int64_t seq) { return seq > e->c ? 2 * seq : 2 * e->c + 1; }
+
+/* largest removeList key <= t of vertex x (-1 if none), with its last stream index */
+static int64_t death_floor(const Vertex* x, int64_t t, int64_t* seq) {
+  const TMap* r = &x->e.rem;
+  int lo = 0, hi = r->n;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (r->k[mid] <= t) lo = mid + 1; else hi = mid;
+  }
+  if (lo == 0) return -1;
+  *seq = r->s[lo - 1];
+  return r->k[lo - 1];
+}
+
+/* closestTime (Entity.scala:173-183) over the merged history of a lazy edge: the own points by
+ * the reference's linear scan, the endpoints' deaths by binary search, ties by put order. */
+static void lazy_closest(const orc_graph* g, const Edge* e, int64_t time, int64_t* ct, int* val) {
+  int64_t c = -1, ord = -1;
+  int v = 0;
+  const TMap* h = &e->e.hist;
+  for (int i = 0; i < h->n; i++) {
+    int64_t k = h->k[i];
+    if (k <= time && (time - k) < (time - c)) { c = k; v = h->v[i]; ord = 2 * h->s[i]; }
+  }
+  for (int x = 0; x < 2; x++) {
+    if (x == 1 && e->di == e->si) break; /* self-loop: one endpoint */
+    int64_t sq = 0;
+    int64_t kd = death_floor(&g->vs[x ? e->di : e->si], time, &sq);
+    if (kd < 0) continue;
+    int64_t od = death_order(e, sq);
+    if (kd > c || (kd == c && od > ord)) { c = kd; v = 0; ord = od; }
+  }
+  *ct = c; *val = v;
+}
+
+/* after the replay: suffix minima of the death logs, and each lazy edge's oldestPoint, which
+ * the deferred kills would have lowered (ent_kill -> checkOldestNewest; killList does not) */
+static int lazy_finish(orc_graph* g) {
+  for (size_t i = 0; i < g->nv; i++) {
+    Vertex* x = &g->vs[i];
+    if (!x->dn) continue;
+    x->dsuf = (int64_t*)malloc(sizeof(int64_t) * x->dn);
+    if (!x->dsuf) return -1;
+    int64_t m = INT64_MAX;
+    for (int k = x->dn - 1; k >= 0; k--) { m = x->dl_t[k] < m ? x->dl_t[k] : m; x->dsuf[k] = m; }
+  }
+  for (size_t i = 0; i < g->ne; i++) {
+    Edge* e = &g->es[i];
+    for (int x = 0; x < 2; x++) {
+      if (x == 1 && e->di == e->si) break;
+      const Vertex* v = &g->vs[x ? e->di : e->si];
+      int lo = 0, hi = v->dn; /* first death logged after the creation */
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (v->dl_s[mid] <= e->c) lo = mid + 1; else hi = mid;
+      }
+      if (lo < v->dn && v->dsuf[lo] < e->e.oldest) e->e.oldest = v->dsuf[lo];
+    }
+  }
+  return 0;
+}
+
+static int edge_alive(const orc_graph* g, const Edge* e, int64_t time, int64_t window) {
+  if (!g->lazy) return ent_alive(&e->e, time, window);
+  if (time < e->e.oldest) return 0;
+  int64_t c; int v;
+  lazy_closest(g, e, time, &c, &v);
+  if (window < 0) return v;
+  return (time - c <= window) ? v : 0;
 }
 
 static const orc_graph* g_sort_ctx;
@@ -275,10 +408,17 @@ static int cmp_vid(const void* a, const void* b) {
 
 orc_graph* orc_build(const int64_t* t, const uint8_t* kind, const int64_t* src,
                      const int64_t* dst, size_t n) {
+  return orc_build_ex(t, kind, src, dst, n, 0);
+}
+
+orc_graph* orc_build_ex(const int64_t* t, const uint8_t* kind, const int64_t* src,
+                        const int64_t* dst, size_t n, int flags) {
   orc_graph* g = (orc_graph*)calloc(1, sizeof(orc_graph));
   if (!g) return NULL;
+  g->lazy = (flags & ORC_LAZY_EDGES) != 0;
   if (hm_init(&g->vmap, 1024) || hm_init(&g->emap, 1024)) { orc_free(g); return NULL; }
   for (size_t i = 0; i < n; i++) {
+    g->seq = (int64_t)i;
     /* keys >= 0, ids in [0, 2^31) (message targets are .toInt, VertexVisitor.scala:117) */
     if (t[i] < 0 || src[i] < 0 || src[i] > INT32_MAX) { orc_free(g); return NULL; }
     if ((kind[i] == ORC_EADD || kind[i] == ORC_EDEL) && (dst[i] < 0 || dst[i] > INT32_MAX)) { orc_free(g); return NULL; }
@@ -292,6 +432,7 @@ orc_graph* orc_build(const int64_t* t, const uint8_t* kind, const int64_t* src,
     }
     if (rc != 0) { orc_free(g); return NULL; }
   }
+  if (g->lazy && lazy_finish(g) != 0) { orc_free(g); return NULL; }
   g->order = (int32_t*)malloc(sizeof(int32_t) * (g->nv ? g->nv : 1));
   if (!g->order) { orc_free(g); return NULL; }
   for (size_t i = 0; i < g->nv; i++) g->order[i] = (int32_t)i;
@@ -305,6 +446,7 @@ void orc_free(orc_graph* g) {
   for (size_t i = 0; i < g->nv; i++) {
     tm_free(&g->vs[i].e.hist); tm_free(&g->vs[i].e.rem);
     free(g->vs[i].out.a); free(g->vs[i].in.a);
+    free(g->vs[i].dl_t); free(g->vs[i].dl_s); free(g->vs[i].dsuf);
   }
   for (size_t i = 0; i < g->ne; i++) { tm_free(&g->es[i].e.hist); tm_free(&g->es[i].e.rem); }
   free(g->vs); free(g->es); free(g->order);
@@ -315,28 +457,67 @@ void orc_free(orc_graph* g) {
 size_t orc_num_vertices(const orc_graph* g) { return g->nv; }
 size_t orc_num_edges(const orc_graph* g) { return g->ne; }
 
-static const Entity* find_entity(const orc_graph* g, int is_edge, int64_t s, int64_t d) {
+static const Vertex* find_vertex(const orc_graph* g, int64_t s) {
   if (s < 0 || s > INT32_MAX) return NULL;
-  if (is_edge) {
-    if (d < 0 || d > INT32_MAX) return NULL;
-    int32_t ei = hm_get(&g->emap, ekey(s, d));
-    return ei >= 0 ? &g->es[ei].e : NULL;
-  }
   int32_t vi = hm_get(&g->vmap, (uint64_t)s);
-  return vi >= 0 ? &g->vs[vi].e : NULL;
+  return vi >= 0 ? &g->vs[vi] : NULL;
+}
+static const Edge* find_edge(const orc_graph* g, int64_t s, int64_t d) {
+  if (s < 0 || s > INT32_MAX || d < 0 || d > INT32_MAX) return NULL;
+  int32_t ei = hm_get(&g->emap, ekey(s, d));
+  return ei >= 0 ? &g->es[ei] : NULL;
+}
+
+static int cmp_i64(const void* a, const void* b) {
+  int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
+  return (x > y) - (x < y);
 }
 
 long orc_history(const orc_graph* g, int is_edge, int64_t src, int64_t dst,
                  int64_t* times, uint8_t* flags, size_t cap) {
-  const Entity* e = find_entity(g, is_edge, src, dst);
-  if (!e) return -1;
+  const Entity* e;
+  if (is_edge) {
+    const Edge* x = find_edge(g, src, dst);
+    if (!x) return -1;
+    if (g->lazy) { /* merged history: every own key and endpoint death key, winner by put order */
+      size_t nk = (size_t)x->e.hist.n + (size_t)g->vs[x->si].e.rem.n +
+                  (x->di != x->si ? (size_t)g->vs[x->di].e.rem.n : 0);
+      int64_t* ks = (int64_t*)malloc(sizeof(int64_t) * (nk ? nk : 1));
+      if (!ks) return -1;
+      size_t m = 0;
+      for (int i = 0; i < x->e.hist.n; i++) ks[m++] = x->e.hist.k[i];
+      for (int i = 0; i < g->vs[x->si].e.rem.n; i++) ks[m++] = g->vs[x->si].e.rem.k[i];
+      if (x->di != x->si)
+        for (int i = 0; i < g->vs[x->di].e.rem.n; i++) ks[m++] = g->vs[x->di].e.rem.k[i];
+      qsort(ks, m, sizeof(int64_t), cmp_i64);
+      long n = 0;
+      for (size_t i = 0; i < m; i++) {
+        if (i && ks[i] == ks[i - 1]) continue;
+        int64_t c; int v;
+        lazy_closest(g, x, ks[i], &c, &v);
+        if ((size_t)n < cap) { times[n] = ks[i]; flags[n] = (uint8_t)v; }
+        n++;
+      }
+      free(ks);
+      return n;
+    }
+    e = &x->e;
+  } else {
+    const Vertex* v = find_vertex(g, src);
+    if (!v) return -1;
+    e = &v->e;
+  }
   for (int i = 0; i < e->hist.n && (size_t)i < cap; i++) { times[i] = e->hist.k[i]; flags[i] = e->hist.v[i]; }
   return e->hist.n;
 }
 
 int orc_alive(const orc_graph* g, int is_edge, int64_t src, int64_t dst, int64_t t, int64_t window) {
-  const Entity* e = find_entity(g, is_edge, src, dst);
-  return e ? ent_alive(e, t, window) : 0;
+  if (is_edge) {
+    const Edge* e = find_edge(g, src, dst);
+    return e ? edge_alive(g, e, t, window) : 0;
+  }
+  const Vertex* v = find_vertex(g, src);
+  return v ? ent_alive(&v->e, t, window) : 0;
 }
 
 /* ------------------------------------------------------------ lens helpers */
@@ -378,13 +559,13 @@ static int neighbours(const orc_graph* g, int vi, int64_t t, int64_t w, int* nb,
   int n = 0;
   for (int i = 0; i < v->out.n; i++) {
     const Edge* e = &g->es[v->out.a[i]];
-    if (!ent_alive(&e->e, t, w)) continue;
+    if (!edge_alive(g, e, t, w)) continue;
     int x = hm_get(&g->vmap, (uint64_t)e->dst);
     if (!mark[x]) { mark[x] = 1; nb[n++] = x; }
   }
   for (int i = 0; i < v->in.n; i++) {
     const Edge* e = &g->es[v->in.a[i]];
-    if (!ent_alive(&e->e, t, w)) continue;
+    if (!edge_alive(g, e, t, w)) continue;
     int x = hm_get(&g->vmap, (uint64_t)e->src);
     if (!mark[x]) { mark[x] = 1; nb[n++] = x; }
   }
@@ -518,8 +699,8 @@ done:
 static void vertex_degree(const orc_graph* g, int v, int64_t t, int64_t w, int32_t* od, int32_t* id) {
   const Vertex* x = &g->vs[v];
   int32_t o = 0, in = 0;
-  for (int i = 0; i < x->out.n; i++) o += ent_alive(&g->es[x->out.a[i]].e, t, w);
-  for (int i = 0; i < x->in.n; i++) in += ent_alive(&g->es[x->in.a[i]].e, t, w);
+  for (int i = 0; i < x->out.n; i++) o += edge_alive(g, &g->es[x->out.a[i]], t, w);
+  for (int i = 0; i < x->in.n; i++) in += edge_alive(g, &g->es[x->in.a[i]], t, w);
   *od = o; *id = in;
 }
 
@@ -558,28 +739,46 @@ int orc_pagerank(const orc_graph* g, int64_t t, const int64_t* windows, int nw, 
   double* cur = (double*)malloc(sizeof(double) * nvs);
   double* nxt = (double*)malloc(sizeof(double) * nvs);
   int32_t* od = (int32_t*)malloc(sizeof(int32_t) * nvs);
+  /* per window: alive out-edges of members whose dst is a member, as CSR (the messages
+   * messageAllOutgoingNeighbors would send and a member would read), built once per view */
+  size_t* off = (size_t*)malloc(sizeof(size_t) * (nvs + 1));
+  int* adj = NULL;
+  size_t adj_cap = 0;
   int rc = -1;
-  if (!mem || !cur || !nxt || !od) goto done;
+  if (!mem || !cur || !nxt || !od || !off) goto done;
   build_keysets(g, t, &ws, mem);
   for (int i = 0; i < ws.nwin; i++) {
     const uint8_t* m = mem + (size_t)i * nv;
-    for (size_t v = 0; v < nv; v++) {
-      cur[v] = 1.0; /* defaultPR, PageRank.scala:14 */
-      int32_t dummy;
-      vertex_degree(g, (int)v, t, ws.w[i], &od[v], &dummy);
+    size_t ne_w = 0;
+    off[0] = 0;
+    for (size_t u = 0; u < nv; u++) {
+      cur[u] = 1.0; /* defaultPR, PageRank.scala:14 */
+      od[u] = 0;
+      if (m[u]) {
+        const Vertex* x = &g->vs[u];
+        for (int k = 0; k < x->out.n; k++) {
+          const Edge* e = &g->es[x->out.a[k]];
+          if (!edge_alive(g, e, t, ws.w[i])) continue;
+          od[u]++; /* out-degree counts every alive out-edge (DegreeBasic), member dst or not */
+          int d = hm_get(&g->vmap, (uint64_t)e->dst);
+          if (!m[d]) continue;
+          if (ne_w == adj_cap) {
+            size_t nc = adj_cap ? 2 * adj_cap : 1024;
+            int* na = (int*)realloc(adj, sizeof(int) * nc);
+            if (!na) goto done;
+            adj = na; adj_cap = nc;
+          }
+          adj[ne_w++] = d;
+        }
+      }
+      off[u + 1] = ne_w;
     }
     for (int it = 0; it < iters; it++) {
       for (size_t v = 0; v < nv; v++) nxt[v] = 0.0;
       for (size_t u = 0; u < nv; u++) {
         if (!m[u]) continue;
         double c = cur[u] / (double)(od[u] > 1 ? od[u] : 1); /* max(outdeg,1), PageRank.scala:35 */
-        const Vertex* x = &g->vs[u];
-        for (int k = 0; k < x->out.n; k++) {
-          const Edge* e = &g->es[x->out.a[k]];
-          if (!ent_alive(&e->e, t, ws.w[i])) continue;
-          int d = hm_get(&g->vmap, (uint64_t)e->dst);
-          if (m[d]) nxt[d] += c;
-        }
+        for (size_t k = off[u]; k < off[u + 1]; k++) nxt[adj[k]] += c;
       }
       for (size_t v = 0; v < nv; v++) cur[v] = m[v] ? 0.15 + 0.85 * nxt[v] : 1.0; /* d = 0.85, :11 */
     }
@@ -596,7 +795,7 @@ int orc_pagerank(const orc_graph* g, int64_t t, const int64_t* windows, int nw, 
   }
   rc = 0;
 done:
-  free(mem); free(cur); free(nxt); free(od);
+  free(mem); free(cur); free(nxt); free(od); free(off); free(adj);
   return rc;
 }
 
@@ -644,7 +843,7 @@ int orc_diffusion(const orc_graph* g, int64_t t, const int64_t* windows, int nw,
     size_t qb_ = ((size_t)(((s) + 1) % 2) * nwin + ws.canon[i]) * nv;                    \
     for (int k_ = 0; k_ < x_->out.n; k_++) {                                             \
       const Edge* e_ = &g->es[x_->out.a[k_]];                                            \
-      if (!ent_alive(&e_->e, t, ws.w[i])) continue;                                      \
+      if (!edge_alive(g, e_, t, ws.w[i])) continue;                                       \
       int d_ = hm_get(&g->vmap, (uint64_t)e_->dst);                                      \
       if (!coin || dcoin(salt[i], x_->id, e_->dst, (s))) q[qb_ + d_]++;                  \
     }                                                                                    \

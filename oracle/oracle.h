@@ -32,6 +32,16 @@ typedef struct orc_graph orc_graph;
  * (EntityStorage.scala:73-453) for one Partition Manager.  Returns NULL on bad input. */
 orc_graph* orc_build(const int64_t* t, const uint8_t* kind, const int64_t* src,
                      const int64_t* dst, size_t n);
+
+/* Same replay with flags.  ORC_LAZY_EDGES: an edge stores only its own puts; the endpoint
+ * deaths that the literal replay copies into every edge (Edge.killList at creation,
+ * vertexRemoval's kill loops — O(degree x deaths) for a hub that dies often) are read from the
+ * endpoints' removeLists when the edge is evaluated, with the TreeMap's last-put-wins order
+ * kept by stream index.  Every query answers identically (tests/test_oracle_scale.py checks
+ * the two builds against each other); this one fits power-law streams of 10^8 updates. */
+#define ORC_LAZY_EDGES 1
+orc_graph* orc_build_ex(const int64_t* t, const uint8_t* kind, const int64_t* src,
+                        const int64_t* dst, size_t n, int flags);
 void orc_free(orc_graph* g);
 
 size_t orc_num_vertices(const orc_graph* g);

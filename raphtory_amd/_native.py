@@ -47,7 +47,7 @@ class NativeUnavailable(RuntimeError):
 class CCSummary(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "biggest", "total", "total_without_islands", "total_islands", "clusters_gt2",
-        "sum_all", "sum_without_islands", "supersteps")]
+        "sum_all", "sum_without_islands", "supersteps", "alive_edges")]
 
 
 class Stats(C.Structure):
@@ -58,6 +58,7 @@ class Stats(C.Structure):
         ("ms_total", C.c_double),
         ("kernel_launches", C.c_int64 * 12), ("kernel_ms", C.c_double * 12), ("kernel_bytes", C.c_double * 12),
         ("seal_ms", C.c_double), ("seal_incremental", C.c_int64), ("seal_delta_updates", C.c_int64),
+        ("alive_edge_windows", C.c_int64),
     ]
 
 
@@ -141,6 +142,9 @@ def synth() -> C.CDLL:
         s.rg_gen_gab_keyed.restype = _SZ
         s.rg_gen_gab_keyed.argtypes = [C.c_uint64, C.c_uint64, C.c_int64, _SZ, C.c_int64, C.c_int64, _P64, _PU8,
                                        _P64, _P64]
+        s.rg_gen_gab_range.restype = _SZ
+        s.rg_gen_gab_range.argtypes = [C.c_uint64, C.c_uint64, C.c_int64, _SZ, _SZ, _SZ, C.c_int, C.c_int,
+                                       C.c_int64, C.c_int64, _P64, _PU8, _P64, _P64]
         _synth = s
     return _synth
 

@@ -242,6 +242,69 @@ __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* 
   }
 }
 
+// Window bits of edge e (own history + endpoint death lists), interval or per-hop form.
+template <bool PLANAR>
+__device__ __forceinline__ void edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const HopLDS& L,
+                                          const BatchParams& bp, int64_t e, const int32_t* __restrict__ esrc,
+                                          const int32_t* __restrict__ edst, const int64_t* __restrict__ eoff,
+                                          const int64_t* __restrict__ ekey, const int64_t* __restrict__ doff,
+                                          const int64_t* __restrict__ dtime) {
+  const int K = L.K;
+  const int64_t lo = eoff[e], hi = eoff[e + 1];
+  const int32_t s = esrc[e], d = edst[e];
+  const int64_t s0 = doff[s], s1 = doff[s + 1], d0 = doff[d], d1 = doff[d + 1];
+  if (bp.sorted && bp.iv_max >= 0) {
+    const int64_t f0 = floor_idx(ekey, lo, hi, L.hop[0]);
+    const int64_t f1 = floor_idx(ekey, lo, hi, L.hop[K - 1]);
+    if (f1 - f0 <= bp.iv_max) {
+      for (int64_t i = f0 < 0 ? lo : f0; i <= f1; i++) {
+        const int64_t key = ekey[i];
+        if (!(key & 1)) continue;
+        const int64_t tf = key >> 1;
+        int b = i + 1 < hi ? hop_lb(L, ekey[i + 1] >> 1) : K;
+        // first endpoint death after tf ends the interval
+        const int64_t ps = first_after(dtime, s0, s1, tf), pd = first_after(dtime, d0, d1, tf);
+        const int64_t dn = min(ps < s1 ? dtime[ps] : INT64_MAX, pd < d1 ? dtime[pd] : INT64_MAX);
+        if (dn != INT64_MAX) b = min(b, hop_lb(L, dn));
+        interval_bits<PLANAR>(m, L, tf, hop_lb(L, tf), b);
+      }
+      return;
+    }
+  }
+  int64_t f = -1, ps = s0, pd = d0;
+  for (int k = 0; k < K; k++) {
+    const int64_t t = L.hop[k];
+    int64_t lds, ldd;  // last death time <= t of src / dst (-1: none)
+    if (bp.sorted && k > 0) {
+      f = floor_advance(ekey, f, lo, hi, t);
+      ps = death_advance(dtime, ps, s1, t);
+      pd = death_advance(dtime, pd, d1, t);
+      lds = ps > s0 ? dtime[ps - 1] : -1;
+      ldd = pd > d0 ? dtime[pd - 1] : -1;
+    } else {
+      f = floor_idx(ekey, lo, hi, t);
+      lds = s1 > s0 ? last_death(dtime, s0, s1, t) : -1;
+      ldd = d1 > d0 ? last_death(dtime, d0, d1, t) : -1;
+      if (bp.sorted) {  // k == 0: position the death cursors
+        ps = first_after(dtime, s0, s1, t);
+        pd = first_after(dtime, d0, d1, t);
+      }
+    }
+    if (f < 0) continue;
+    const int64_t key = ekey[f];
+    if (!(key & 1)) continue;
+    const int64_t ft = key >> 1;
+    // an endpoint death in (ft, t] is a later kill point (killList / vertexRemoval)
+    if (lds > ft || ldd > ft) continue;
+    const int64_t age = t - ft;
+    hop_bits<PLANAR>(m, L, age, k);
+  }
+}
+
+// The loop runs wave-uniform (lane = edge within a 64-edge group) so that profile runs can
+// count alive edges per view: the wave's 64 mask words are bit-transposed (lane j <- view j)
+// and popcounted; the block sums them in LDS, one atomicAdd per (plane, view) per block.
+__device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane);
 template <bool PLANAR>
 __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __restrict__ esrc,
                                                    const int32_t* __restrict__ edst,
@@ -249,65 +312,55 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
                                                    const int64_t* __restrict__ ekey,
                                                    const int64_t* __restrict__ doff,
                                                    const int64_t* __restrict__ dtime, BatchParams bp,
-                                                   uint64_t* __restrict__ em, int64_t estride) {
+                                                   uint64_t* __restrict__ em, int64_t estride,
+                                                   unsigned long long* __restrict__ ecnt, int64_t h0,
+                                                   int64_t own_lim) {
   __shared__ HopLDS L;
+  __shared__ unsigned int cnt_s[PLANAR ? kMaxPlanes : 1][64];
   hop_lds_init(L, bp, bp.thr_e);
-  const int K = L.K;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t lo = eoff[e], hi = eoff[e + 1];
-    const int32_t s = esrc[e], d = edst[e];
-    const int64_t s0 = doff[s], s1 = doff[s + 1], d0 = doff[d], d1 = doff[d + 1];
-    uint64_t m[PLANAR ? kMaxPlanes : 1] = {};
-    if (bp.sorted && bp.iv_max >= 0) {
-      const int64_t f0 = floor_idx(ekey, lo, hi, L.hop[0]);
-      const int64_t f1 = floor_idx(ekey, lo, hi, L.hop[K - 1]);
-      if (f1 - f0 <= bp.iv_max) {
-        for (int64_t i = f0 < 0 ? lo : f0; i <= f1; i++) {
-          const int64_t key = ekey[i];
-          if (!(key & 1)) continue;
-          const int64_t tf = key >> 1;
-          int b = i + 1 < hi ? hop_lb(L, ekey[i + 1] >> 1) : K;
-          // first endpoint death after tf ends the interval
-          const int64_t ps = first_after(dtime, s0, s1, tf), pd = first_after(dtime, d0, d1, tf);
-          const int64_t dn = min(ps < s1 ? dtime[ps] : INT64_MAX, pd < d1 ? dtime[pd] : INT64_MAX);
-          if (dn != INT64_MAX) b = min(b, hop_lb(L, dn));
-          interval_bits<PLANAR>(m, L, tf, hop_lb(L, tf), b);
-        }
-        store_bits<PLANAR>(m, bp, em, estride, e);
-        continue;
-      }
+  constexpr int NP = PLANAR ? kMaxPlanes : 1;
+  if (ecnt)
+    for (int i = threadIdx.x; i < NP * 64; i += blockDim.x) (&cnt_s[0][0])[i] = 0;
+  const int lane = lane_id();
+  uint32_t acc[NP] = {};
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); e0 < ne; e0 += stride) {
+    const int64_t e = e0 + lane;
+    uint64_t m[NP] = {};
+    if (e < ne) {
+      edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime);
+      store_bits<PLANAR>(m, bp, em, estride, e);
     }
-    int64_t f = -1, ps = s0, pd = d0;
-    for (int k = 0; k < K; k++) {
-      const int64_t t = L.hop[k];
-      int64_t lds, ldd;  // last death time <= t of src / dst (-1: none)
-      if (bp.sorted && k > 0) {
-        f = floor_advance(ekey, f, lo, hi, t);
-        ps = death_advance(dtime, ps, s1, t);
-        pd = death_advance(dtime, pd, d1, t);
-        lds = ps > s0 ? dtime[ps - 1] : -1;
-        ldd = pd > d0 ? dtime[pd - 1] : -1;
-      } else {
-        f = floor_idx(ekey, lo, hi, t);
-        lds = s1 > s0 ? last_death(dtime, s0, s1, t) : -1;
-        ldd = d1 > d0 ? last_death(dtime, d0, d1, t) : -1;
-        if (bp.sorted) {  // k == 0: position the death cursors
-          ps = first_after(dtime, s0, s1, t);
-          pd = first_after(dtime, d0, d1, t);
-        }
-      }
-      if (f < 0) continue;
-      const int64_t key = ekey[f];
-      if (!(key & 1)) continue;
-      const int64_t ft = key >> 1;
-      // an endpoint death in (ft, t] is a later kill point (killList / vertexRemoval)
-      if (lds > ft || ldd > ft) continue;
-      const int64_t age = t - ft;
-      hop_bits<PLANAR>(m, L, age, k);
+    if (ecnt) {  // an edge counts once over the partitions: where its source is owned
+      const bool mine = e < ne && esrc[e] < own_lim;
+#pragma unroll
+      for (int w = 0; w < NP; w++)
+        if (!PLANAR || w < L.W) acc[w] += __popcll(transpose64(mine ? m[w] : 0ull, lane));
     }
-    store_bits<PLANAR>(m, bp, em, estride, e);
   }
+  if (ecnt) {
+    __syncthreads();  // cnt_s cleared
+#pragma unroll
+    for (int w = 0; w < NP; w++)
+      if (acc[w]) atomicAdd(&cnt_s[w][lane], acc[w]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < NP * 64; i += blockDim.x) {  // (plane | window, bit) -> view
+      const unsigned int x = (&cnt_s[0][0])[i];
+      const int w = PLANAR ? i >> 6 : (i & 63) / L.KS, k = PLANAR ? i & 63 : (i & 63) % L.KS;
+      if (x && k < L.K && w < L.W) atomicAdd(&ecnt[(h0 + k) * L.W + w], (unsigned long long)x);
+    }
+  }
+}
+
+// Block-wide OR of the views that changed in a step (per-wave values), then one sharded
+// atomicOr (kernels.hpp, lanechg).  Call from every thread of the block; `slot` is LDS.
+__device__ __forceinline__ void publish_lanes(uint64_t lanes, unsigned long long* slot,
+                                              unsigned long long* lanechg, int step) {
+  for (int o = 32; o > 0; o >>= 1) lanes |= __shfl_xor(lanes, o);
+  if ((threadIdx.x & 63) == 0 && lanes) atomicOr(slot, (unsigned long long)lanes);
+  __syncthreads();
+  if (threadIdx.x == 0 && *slot && lanechg)
+    atomicOr(&lanechg[step * kLaneShards + (blockIdx.x & (kLaneShards - 1))], *slot);
 }
 
 // Per-step work counters, sharded 64 ways so that blocks never pile up on one address (a
@@ -362,14 +415,16 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int32_t* __restrict__ hv_seg,
                                                   const int32_t* __restrict__ segcnt,
                                                   const uint64_t* __restrict__ segor,
-                                                  int32_t* __restrict__ hbest) {
-  __shared__ unsigned long long red[3];
-  if (threadIdx.x < 3) red[threadIdx.x] = 0;
+                                                  int32_t* __restrict__ hbest,
+                                                  unsigned long long* __restrict__ lanechg) {
+  __shared__ unsigned long long red[4];
+  if (threadIdx.x < 4) red[threadIdx.x] = 0;
   __syncthreads();
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   unsigned long long members = 0, alive = 0, changed = 0;
+  uint64_t lanes = 0;  // views with a step-1 change in this wave
   for (int64_t v = wave; v < nv; v += nwaves) {
     const uint64_t mv = vm[v];
     const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
@@ -405,6 +460,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         if (ch) act2[v] = 1;
       }
       changed += ch != 0;
+      lanes |= ch;
       members += 1;
       alive += kept;
       continue;
@@ -454,6 +510,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     const uint64_t ch = __ballot(best < me);
     if (lane == 0) { cnt[v] = count; vadj[v] = any; chg1[v] = ch; }
     if (!own) continue;
+    lanes |= ch;
     if (ch) {
       changed++;
       if (lane == 0) act2[v] = 1;
@@ -474,7 +531,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     if (alive) atomicAdd(&red[1], alive);
     if (changed) atomicAdd(&red[2], changed);
   }
-  __syncthreads();
+  publish_lanes(lanes, &red[3], lanechg, 1);  // (its barrier also publishes red[0..2])
   if (threadIdx.x == 0) {
     if (red[2] && stepflag[1] == 0) {
       stepflag[1] = 1;
@@ -625,7 +682,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          const int32_t* __restrict__ lab_cur, int32_t* __restrict__ lab_next,
                                          const uint64_t* __restrict__ chg_prev,
                                          uint64_t* __restrict__ chg_next, uint8_t* __restrict__ act_next,
-                                         const TailList& tl, int lane, int32_t& changed,
+                                         const TailList& tl, int lane, int32_t& changed, uint64_t& lanes,
                                          unsigned long long& pv, unsigned long long& ps,
                                          unsigned long long& pg, const int32_t* __restrict__ hv_of = nullptr,
                                          int32_t* __restrict__ hbest = nullptr) {
@@ -720,6 +777,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
         else lab_next[v * 64 + lane] = best[i];
       }
       if (lane == 0) chg_next[v] = ch;
+      lanes |= ch;
       if (ch) {
         changed++;
         mark<TAIL>(lane == 0, (int32_t)v, act_next, tl, lane);
@@ -758,11 +816,12 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
                                                   int32_t* __restrict__ hostflag,
                                                   unsigned long long* __restrict__ work,
                                                   const int32_t* __restrict__ hv_of,
-                                                  int32_t* __restrict__ hbest) {
+                                                  int32_t* __restrict__ hbest,
+                                                  unsigned long long* __restrict__ lanechg) {
   if (stepflag[step - 1] == 0) return;
   __shared__ int32_t red;
-  __shared__ unsigned long long wred[3];
-  if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; wred[2] = 0; }
+  __shared__ unsigned long long wred[4];
+  if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; wred[2] = 0; wred[3] = 0; }
   const int64_t nwords = (nv + 7) >> 3;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -772,6 +831,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int32_t changed = 0;
+  uint64_t lanes = 0;
   unsigned long long pv = 0, ps = 0, pg = 0;
   const TailList none{nullptr, nullptr};
   for (int64_t c = wave; c * CH < nv; c += nwaves) {
@@ -786,8 +846,8 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     if (v0 + CH > nv) bits &= (1u << (nv - v0)) - 1;
     if (!bits) continue;
     cc_chunk<CH, BUF, false>(v0 + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
-                             lab_next, chg_prev, chg_next, act_next, none, lane, changed, pv, ps, pg, hv_of,
-                             hbest);
+                             lab_next, chg_prev, chg_next, act_next, none, lane, changed, lanes, pv, ps, pg,
+                             hv_of, hbest);
   }
   if (work)
     for (int o = 32; o > 0; o >>= 1) pg += __shfl_xor(pg, o);
@@ -797,7 +857,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     if (ps) atomicAdd(&wred[1], ps);
     if (pg) atomicAdd(&wred[2], pg);
   }
-  __syncthreads();
+  publish_lanes(lanes, &wred[3], lanechg, step);
   if (threadIdx.x == 0) {
     if (red && stepflag[step] == 0) {  // first writers also tell the host (mapped pinned memory)
       stepflag[step] = 1;
@@ -832,11 +892,12 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
                                                           uint8_t* act2, int32_t* __restrict__ stepflag,
                                                           int32_t* __restrict__ hostflag,
                                                           int32_t* __restrict__ info,
-                                                          unsigned long long* __restrict__ work) {
+                                                          unsigned long long* __restrict__ work,
+                                                          unsigned long long* __restrict__ lanechg) {
   __shared__ int32_t list[2][kTailListCap];
   __shared__ int nlist[2];
   __shared__ int nchanged;
-  __shared__ unsigned long long wsum[3];
+  __shared__ unsigned long long wsum[4];
   auto ACT = [&](int k) { return k == 0 ? act0 : (k == 1 ? act1 : act2); };
   const int lane = lane_id(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if (stepflag[r0 - 1] == 0) {  // the batch has halted already
@@ -873,7 +934,7 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
     if (ncur > cap) break;  // too wide for one workgroup: the full-grid kernel takes step r+1
     const int s = r + 1;
     __syncthreads();  // everyone has read nlist[p] and left the previous clear loop
-    if (threadIdx.x == 0) { nlist[p ^ 1] = 0; nchanged = 0; wsum[0] = 0; wsum[1] = 0; wsum[2] = 0; }
+    if (threadIdx.x == 0) { nlist[p ^ 1] = 0; nchanged = 0; wsum[0] = 0; wsum[1] = 0; wsum[2] = 0; wsum[3] = 0; }
     __syncthreads();
     uint8_t* a_cur = ACT(s % 3);
     uint8_t* a_next = ACT((s + 1) % 3);
@@ -883,13 +944,16 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
     uint64_t* chg_next = (s & 1) ? chg1 : chg0;
     const TailList tl{list[p ^ 1], &nlist[p ^ 1]};
     int32_t changed = 0;
+    uint64_t lanes = 0;
     unsigned long long pv = 0, ps = 0, pg = 0;
     for (int c = wid * 4; c < ncur; c += nw * 4) {
       const int k = c + (lane & 3) < ncur ? c + (lane & 3) : c;
       const uint32_t bits = ncur - c >= 4 ? 0xfu : ((1u << (ncur - c)) - 1);
       cc_chunk<4, BUF, true>((int64_t)list[p][k], bits, adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
-                             chg_prev, chg_next, a_next, tl, lane, changed, pv, ps, pg);
+                             chg_prev, chg_next, a_next, tl, lane, changed, lanes, pv, ps, pg);
     }
+    for (int o = 32; o > 0; o >>= 1) lanes |= __shfl_xor(lanes, o);
+    if (lane == 0 && lanes) atomicOr(&wsum[3], (unsigned long long)lanes);
     for (int o = 32; o > 0; o >>= 1) pg += __shfl_xor(pg, o);
     if (lane == 0) {
       if (changed) atomicAdd(&nchanged, changed);
@@ -905,6 +969,7 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
         stepflag[s] = 1;
         if (hostflag) hostflag[s] = 1;
       }
+      if (wsum[3] && lanechg) atomicOr(&lanechg[s * kLaneShards], wsum[3]);
       add_work(work, s, wsum[0], wsum[1], (unsigned long long)nch, wsum[2]);
     }
     r = s;
@@ -1736,30 +1801,32 @@ void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp,
   if (planar) k_vertex_mask<true><<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm, vstride, clr);
   else k_vertex_mask<false><<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm, vstride, clr);
 }
-void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar) {
+void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
+                      unsigned long long* ecnt, int64_t h0) {
   if (planar)
     k_edge_mask<true><<<grid_for(g.ne, 256), 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime,
-                                                           bp, em, g.ne);
+                                                           bp, em, g.ne, ecnt, h0, g.n_own);
   else
     k_edge_mask<false><<<grid_for(g.ne, 256), 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime,
-                                                            bp, em, g.ne);
+                                                            bp, em, g.ne, ecnt, h0, g.n_own);
 }
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
-                     int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb) {
+                     int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
+                     unsigned long long* lanechg) {
   const bool hv = g.n_seg > 0;
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
-                                                hb.segcnt, hb.segor, hb.best);
+                                                hb.segcnt, hb.segor, hb.best, lanechg);
 }
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
-                    unsigned long long* work, int variant, int32_t* hbest) {
+                    unsigned long long* work, int variant, unsigned long long* lanechg, int32_t* hbest) {
   const int ch = (variant & 15) == 8 ? 8 : 4;
   const bool buf = (variant & 16) != 0;
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
@@ -1771,7 +1838,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   const unsigned grid = grid_for(g.nv, 4 * ch, cap);
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
-    act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest
+    act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg
   if (ch == 8 && buf) k_cc_step2<8, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (ch == 8) k_cc_step2<8, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (buf) k_cc_step2<4, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
@@ -1804,10 +1871,10 @@ void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,
                     int32_t* lab1, uint64_t* chg0, uint64_t* chg1, uint8_t* act0, uint8_t* act1,
                     uint8_t* act2, int32_t* stepflag, int32_t* hostflag, int32_t* info,
-                    unsigned long long* work) {
+                    unsigned long long* work, unsigned long long* lanechg) {
   cap = cap < kTailListCap ? cap : kTailListCap;
 #define RGPU_TAIL_ARGS r0, rmax, cap, g.nv, g.adj_off, vm, cnt, snbr, smask, lab0, lab1, chg0, chg1, act0, act1, \
-    act2, stepflag, hostflag, info, work
+    act2, stepflag, hostflag, info, work, lanechg
   if (g_rowbuf) k_cc_tail<true><<<1, kTailThreads, 0, s>>>(RGPU_TAIL_ARGS);
   else k_cc_tail<false><<<1, kTailThreads, 0, s>>>(RGPU_TAIL_ARGS);
 #undef RGPU_TAIL_ARGS

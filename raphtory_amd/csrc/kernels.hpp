@@ -62,17 +62,28 @@ struct BatchClear {
   int64_t n_act_words = 0;  // uint64 words per act buffer
 };
 
+// Per-step OR of the views (lanes) in which some label changed: words lanechg[step*kLaneShards +
+// shard], one atomicOr per block that saw a change (sharded: thousands of blocks on one word
+// serialise at the memory side).  A view's last changing step gives the superstep count the
+// reference's job would run (AnalysisTask.endStep :208-225): min(maxSteps, last + 1).
+constexpr int kLaneShards = 8;
+constexpr int kLaneChgWords = 128 * kLaneShards;  // kMaxSteps (rgpu.cpp) x shards
+
 // K1.  planar = false: one mask word per entity, view bit w*KS + k.  planar = true (W <=
 // kMaxPlanes): one word per window w at out[w*stride + i], bit k = hop of the block.
 constexpr int kMaxPlanes = 8;
 void launch_batch_clear(hipStream_t s, const BatchClear& clr);
 void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm,
                         int64_t vstride, bool planar, const BatchClear& clr);
-void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar);
+// ecnt (profile runs, else null): alive edges per view (|E_w| of SURVEY §8(d)) added into
+// ecnt[(h0 + k) * W + w] for hop k of the block (first hop h0 of the run) and window w
+void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
+                      unsigned long long* ecnt = nullptr, int64_t h0 = 0);
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
-                     int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb);
+                     int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
+                     unsigned long long* lanechg);
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
 // (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
 // next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
@@ -94,14 +105,15 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
-                    unsigned long long* work, int variant, int32_t* hbest = nullptr);
+                    unsigned long long* work, int variant, unsigned long long* lanechg,
+                    int32_t* hbest = nullptr);
 // Many late supersteps in one single-workgroup launch while the frontier stays below `cap`
 // vertices; info[0] <- last superstep executed (host-mapped).
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,
                     int32_t* lab1, uint64_t* chg0, uint64_t* chg1, uint8_t* act0, uint8_t* act1,
                     uint8_t* act2, int32_t* stepflag, int32_t* hostflag, int32_t* info,
-                    unsigned long long* work);
+                    unsigned long long* work, unsigned long long* lanechg);
 constexpr int kIsoWords = 64 * 64;  // isolated-member counts [64 shards][64 views]
 void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso);

@@ -46,7 +46,8 @@ enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUM
                 KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_HEAVY = 8, KID_DIFF = 9, KID_N = 12 };
 
 constexpr int kMaxSteps = 128;
-constexpr int kStatWords = 7 * kViews;  // 6 per-view fields + counters row
+constexpr int kLaneOff = 7 * kViews;                     // lane-change words (kernels.hpp)
+constexpr int kStatWords = kLaneOff + kLaneChgWords;     // 6 per-view fields + counters row + lanes
 constexpr int kWorkWords = kMaxSteps * 64 * 4;
 constexpr int64_t kPad = 64;  // tail padding of per-vertex / per-slot batch arrays
 constexpr int kMaxSlots = 4;  // batches in flight (one HIP stream each; GPU_MAX_HW_QUEUES = 4)
@@ -174,6 +175,8 @@ struct rgpu_ctx {
   int algo = -1, K = 0, W = 0, G = 1, gsize = 1;
   size_t n_hops = 0;
   std::vector<rgpu_cc_summary_t> cc;
+  std::vector<int32_t> vlast;           // per view: last superstep in which one of its labels changed
+  unsigned long long* d_ecnt = nullptr; // profile runs: alive edges per view (K1 edge masks)
   std::vector<int64_t> deg;  // [view][3]
   std::vector<int64_t> dcount, dsteps;  // diffusion: infected vertices, supersteps per view
   int64_t diff_seed = 31;               // BinaryDefusion.infectedNode (BinaryDefusion.scala:10)
@@ -478,7 +481,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                      s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
                      s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
-                     c->profile ? s.work : nullptr, c->step_variant | (g_rowbuf ? 16 : 0),
+                     c->profile ? s.work : nullptr, c->step_variant | (g_rowbuf ? 16 : 0), s.stats + kLaneOff,
                      hv ? s.hv.best : nullptr);
     }, r, false);
     if (hv)
@@ -501,7 +504,8 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     timed_launch(c, si, KID_TAIL, 0.0, [&] {
       launch_cc_tail(s.stream, r0, rc.max_steps, c->tail_cap, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[0],
                      s.lab[1], s.chg[0], s.chg[1], s.act[0], s.act[1], s.act[2], s.stepcnt,
-                     c->hostflags ? s.d_hostflag : nullptr, s.d_tail, c->profile ? s.work : nullptr);
+                     c->hostflags ? s.d_hostflag : nullptr, s.d_tail, c->profile ? s.work : nullptr,
+                     s.stats + kLaneOff);
     }, r0);
     s.tail_pending = true;
   }
@@ -615,7 +619,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     s.vm = s.vm_own;
     s.em = s.em_own;
     timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv, [&] { launch_vertex_mask(s.stream, g, bp, s.vm, 0, false, clr); });
-    timed_launch(c, si, KID_MASK, be + 8.0 * g.ne, [&] { launch_edge_mask(s.stream, g, bp, s.em, false); });
+    timed_launch(c, si, KID_MASK, be + 8.0 * g.ne,
+                 [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0); });
   } else {
     MaskSet& M = c->mset[hb % kMaskSets];
     if (grp == 0) {
@@ -624,7 +629,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       const BatchClear none;
       timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv * rc.W,
                    [&] { launch_vertex_mask(s.stream, g, bp, M.vm, g.nv + kPad, true, none); });
-      timed_launch(c, si, KID_MASK, be + 8.0 * g.ne * rc.W, [&] { launch_edge_mask(s.stream, g, bp, M.em, true); });
+      timed_launch(c, si, KID_MASK, be + 8.0 * g.ne * rc.W,
+                   [&] { launch_edge_mask(s.stream, g, bp, M.em, true, c->d_ecnt, (int64_t)h0); });
       HIPCHK(hipEventRecord(M.k1, s.stream));
       M.pending = rc.G;
     } else {
@@ -667,7 +673,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     timed_launch(c, si, KID_SLOTS, b2, [&] {
       launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
-                      c->profile ? s.work : nullptr, s.hv);
+                      c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff);
     });
     if (g.n_seg > 0)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
@@ -707,6 +713,13 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
   const unsigned long long* h = s.h_stats;
   const size_t hb = (size_t)s.batch / rc.G;
   const int grp = s.batch % rc.G;
+  int32_t last[kViews] = {};  // per lane: last superstep with a label change (0: none)
+  if (rc.algo == RGPU_ALGO_CC)
+    for (int r = 1; r <= s.r_final && r < kMaxSteps; r++) {
+      unsigned long long m = 0;
+      for (int k = 0; k < kLaneShards; k++) m |= h[kLaneOff + r * kLaneShards + k];
+      for (; m; m &= m - 1) last[__builtin_ctzll(m)] = r;
+    }
   for (int k = 0; k < s.kb; k++)
     for (int wl = 0; wl < rc.gsize; wl++) {
       const int j = wl * rc.K + k;  // view bit: window-major within the batch
@@ -720,7 +733,8 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
         o.clusters_gt2 = (int64_t)h[3 * kViews + j];
         o.sum_all = (int64_t)h[4 * kViews + j];
         o.sum_without_islands = (int64_t)h[5 * kViews + j];
-        o.supersteps = s.r_final;
+        o.supersteps = s.r_final;  // per hop after the run (finish_supersteps)
+        c->vlast[view] = last[j];
       } else if (rc.algo == RGPU_ALGO_DEGREE) {
         for (int f = 0; f < 3; f++) c->deg[view * 3 + f] = (int64_t)h[f * kViews + j];
       } else if (rc.algo == RGPU_ALGO_DIFFUSION) {
@@ -974,11 +988,11 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
     timed_launch(c, 0, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.n_vkey + 8.0 * g.nv,
                  [&] { launch_vertex_mask(s.stream, g, bp, s.vm, 0, false, clr); });
     timed_launch(c, 0, KID_MASK, bytes_mask(g) - (16.0 * g.nv + 8.0) + 8.0 * c->pk.n_ekey,
-                 [&] { launch_edge_mask(s.stream, g, bp, s.em, false); });
+                 [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0); });
     if (rc.algo == RGPU_ALGO_CC) {
       timed_launch(c, 0, KID_SLOTS, g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0, [&] {
         launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
-                        s.chg[1], s.act[2], s.stepcnt, nullptr, nullptr, HeavyBuf());
+                        s.chg[1], s.act[2], s.stepcnt, nullptr, nullptr, HeavyBuf(), s.stats + kLaneOff);
       });
       s.r_final = 0;
       if (rc.max_steps > 1) {
@@ -990,7 +1004,8 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
             timed_launch(c, 0, KID_STEP, 0.0, [&] {
               launch_cc_step(s.stream, r, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                              s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
-                             s.act[(r + 2) % 3], s.stepcnt, nullptr, nullptr, c->step_variant);
+                             s.act[(r + 2) % 3], s.stepcnt, nullptr, nullptr, c->step_variant,
+                             s.stats + kLaneOff);
             }, r);
             if (cc_exchange(c, r) == 0) { s.r_final = r; break; }
           }
@@ -1041,6 +1056,34 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
     harvest(c, 0, rc);
   }
   return 0;
+}
+
+// The reference runs one job per hop for all its windows (BWindowedRangeAnalysisTask); it halts
+// at the first superstep in which no label of any window improved, or at maxSteps
+// (AnalysisTask.endStep :208-225), so every view of hop h reports min(maxSteps, 1 + the last
+// changing step over the hop's windows), or 0 when maxSteps <= 1 (no Setup, :169).  With
+// partitions the last changing step is the maximum over them.
+void finish_supersteps(rgpu_ctx* c, const RunCfg& rc) {
+  const size_t nview = rc.n_hops * rc.W;
+  if (c->partitioned && c->nparts > 1) {
+    std::vector<unsigned long long> h(nview);
+    for (size_t i = 0; i < nview; i++) h[i] = (unsigned long long)c->vlast[i];
+    unsigned long long* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(unsigned long long) * std::max<size_t>(nview, 1)));
+    Slot& s = c->slot[0];
+    HIPCHK(hipMemcpyAsync(d, h.data(), sizeof(unsigned long long) * nview, hipMemcpyHostToDevice, s.stream));
+    c->pt.xchg->allreduce_u64(d, nview, true, s.stream);
+    HIPCHK(hipMemcpyAsync(h.data(), d, sizeof(unsigned long long) * nview, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+    (void)hipFree(d);
+    for (size_t i = 0; i < nview; i++) c->vlast[i] = (int32_t)h[i];
+  }
+  for (size_t hop = 0; hop < rc.n_hops; hop++) {
+    int32_t r = 0;
+    for (int w = 0; w < rc.W; w++) r = std::max(r, c->vlast[hop * rc.W + w]);
+    const int64_t steps = rc.max_steps <= 1 ? 0 : std::min<int64_t>(rc.max_steps, (int64_t)r + 1);
+    for (int w = 0; w < rc.W; w++) c->cc[hop * rc.W + w].supersteps = steps;
+  }
 }
 
 int fail(rgpu_ctx* c, int code, const std::string& m) {
@@ -1554,6 +1597,13 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     for (int& x : c->grp_last) x = 0;
     c->n_hops = n_hops;
     c->cc.assign(algo == RGPU_ALGO_CC ? n_hops * rc.W : 0, rgpu_cc_summary_t{});
+    c->vlast.assign(algo == RGPU_ALGO_CC ? n_hops * rc.W : 0, 0);
+    c->st.alive_edge_windows = -1;
+    if (c->d_ecnt) { (void)hipFree(c->d_ecnt); c->d_ecnt = nullptr; }
+    if (flags & RGPU_RUN_PROFILE) {
+      HIPCHK(hipMalloc(&c->d_ecnt, sizeof(unsigned long long) * n_hops * rc.W));
+      HIPCHK(hipMemset(c->d_ecnt, 0, sizeof(unsigned long long) * n_hops * rc.W));
+    }
     c->deg.assign(algo == RGPU_ALGO_DEGREE ? n_hops * rc.W * 3 : 0, 0);
     c->dcount.assign(algo == RGPU_ALGO_DIFFUSION ? n_hops * rc.W : 0, 0);
     c->dsteps.assign(algo == RGPU_ALGO_DIFFUSION ? n_hops * rc.W : 0, 0);
@@ -1578,6 +1628,26 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     else run_impl(c, rc);
     for (int si = 0; si < kMaxSlots; si++)
       if (c->slot[si].stream) HIPCHK(hipStreamSynchronize(c->slot[si].stream));
+    if (algo == RGPU_ALGO_CC) finish_supersteps(c, rc);
+    if (c->d_ecnt) {  // |E_{t,w}| per view (profile runs)
+      std::vector<unsigned long long> e(n_hops * rc.W);
+      HIPCHK(hipMemcpy(e.data(), c->d_ecnt, sizeof(unsigned long long) * e.size(), hipMemcpyDeviceToHost));
+      if (c->partitioned && c->nparts > 1) {
+        HIPCHK(hipMemcpy(c->d_ecnt, e.data(), sizeof(unsigned long long) * e.size(), hipMemcpyHostToDevice));
+        c->pt.xchg->allreduce_u64(c->d_ecnt, e.size(), false, c->slot[0].stream);
+        HIPCHK(hipStreamSynchronize(c->slot[0].stream));
+        HIPCHK(hipMemcpy(e.data(), c->d_ecnt, sizeof(unsigned long long) * e.size(), hipMemcpyDeviceToHost));
+      }
+      c->st.alive_edge_windows = 0;
+      for (size_t i = 0; i < e.size(); i++) {
+        c->st.alive_edge_windows += (int64_t)e[i];
+        if (algo == RGPU_ALGO_CC) c->cc[i].alive_edges = (int64_t)e[i];
+      }
+      (void)hipFree(c->d_ecnt);
+      c->d_ecnt = nullptr;
+    } else if (algo == RGPU_ALGO_CC) {
+      for (auto& o : c->cc) o.alive_edges = -1;
+    }
     auto t1 = std::chrono::steady_clock::now();
     c->st.ms_total = std::chrono::duration<double, std::milli>(t1 - t0).count();
     c->st.launches = 0;

@@ -119,23 +119,42 @@ size_t rg_gen_gab(uint64_t seed, int64_t users, size_t inter, int64_t t0, int64_
                   int64_t* t, uint8_t* kind, int64_t* src, int64_t* dst) {
   return rg_gen_gab_keyed(seed, seed, users, inter, t0, t1, t, kind, src, dst);
 }
+size_t rg_gen_gab_range(uint64_t seed, uint64_t id_key, int64_t users, size_t inter, size_t first, size_t count,
+                        int part, int nparts, int64_t t0, int64_t t1, int64_t* t, uint8_t* kind, int64_t* src,
+                        int64_t* dst);
 size_t rg_gen_gab_keyed(uint64_t seed, uint64_t id_key, int64_t users, size_t inter, int64_t t0, int64_t t1,
                         int64_t* t, uint8_t* kind, int64_t* src, int64_t* dst) {
-  uint64_t s = seed;
+  return rg_gen_gab_range(seed, id_key, users, inter, 0, inter, 0, 1, t0, t1, t, kind, src, dst);
+}
+
+/* Utils.getPartition (Utils.scala:32-33): (|id| mod 10P) div 10 */
+static int owner_of(int64_t id, int nparts) { return (int)(((id < 0 ? -id : id) % (10 * (int64_t)nparts)) / 10); }
+
+/* Interactions [first, first + count) of the `inter`-interaction stream above (the generator
+ * draws two numbers per interaction from a counter-based splitmix64, so any range starts at
+ * state seed + 2*first*golden): a prefix is a slice of the full stream, and ranges can be drawn
+ * in chunks.  nparts > 1 keeps what partition `part` ingests (rgpu.h, partitioned mode): the
+ * VertexAdd of an owned vertex, and every EdgeAdd with an owned endpoint.  Returns the number
+ * of updates written (<= 3*count). */
+size_t rg_gen_gab_range(uint64_t seed, uint64_t id_key, int64_t users, size_t inter, size_t first, size_t count,
+                        int part, int nparts, int64_t t0, int64_t t1, int64_t* t, uint8_t* kind, int64_t* src,
+                        int64_t* dst) {
+  uint64_t s = seed + (uint64_t)(2 * first) * 0x9e3779b97f4a7c15ULL;
   PL p = pl_make(users, 2.1);
   double span_s = (double)((t1 - t0) / 1000);
   double days = span_s / 86400.0;
   const double A = 0.6, twopi = 6.283185307179586;
-  for (size_t i = 0; i < inter; i++) {
+  size_t o = 0;
+  for (size_t i = first; i < first + count && i < inter; i++) {
     double f = (double)i / (double)inter;
     double g = f + A * sin(twopi * days * f) / (twopi * days);
     int64_t ts = t0 + (int64_t)floor(g * span_s) * 1000;
     int64_t a = perm31(pl_draw(&p, &s), id_key), b = perm31(pl_draw(&p, &s), id_key);
-    size_t o = 3 * i;
-    t[o] = t[o + 1] = t[o + 2] = ts;
-    kind[o] = 0; src[o] = a; dst[o] = -1;
-    kind[o + 1] = 0; src[o + 1] = b; dst[o + 1] = -1;
-    kind[o + 2] = 2; src[o + 2] = a; dst[o + 2] = b;
+    const int oa = nparts > 1 ? owner_of(a, nparts) == part : 1;
+    const int ob = nparts > 1 ? owner_of(b, nparts) == part : 1;
+    if (oa) { t[o] = ts; kind[o] = 0; src[o] = a; dst[o] = -1; o++; }
+    if (ob) { t[o] = ts; kind[o] = 0; src[o] = b; dst[o] = -1; o++; }
+    if (oa || ob) { t[o] = ts; kind[o] = 2; src[o] = a; dst[o] = b; o++; }
   }
-  return 3 * inter;
+  return o;
 }

@@ -130,9 +130,11 @@ class TemporalGraph:
         return out
 
     def cc_summaries(self) -> np.ndarray:
-        """[n_hops, n_windows, 8] int64: the CCSummary fields of every view."""
+        """[n_hops, n_windows, 9] int64: the CCSummary fields of every view (biggest, total,
+        total_without_islands, total_islands, clusters_gt2, sum_all, sum_without_islands,
+        supersteps, alive_edges)."""
         nh, nw = len(self._hops), self.n_windows
-        out = np.zeros((nh, nw, 8), np.int64)
+        out = np.zeros((nh, nw, len(N.CCSummary._fields_)), np.int64)
         s = N.CCSummary()
         for h in range(nh):
             for w in range(nw):

@@ -74,6 +74,20 @@ def gen_gab(seed: int, users: int, interactions: int, t0: int = GAB_T0, t1: int 
     return Stream(t, k, s, d)
 
 
+def gen_gab_range(seed: int, users: int, interactions: int, first: int, count: int, part: int = 0,
+                  nparts: int = 1, t0: int = GAB_T0, t1: int = GAB_T1, id_key: int = None) -> Stream:
+    """Interactions [first, first+count) of gen_gab(seed, users, interactions): a prefix is a
+    slice of the full C4 stream, and chunks concatenate to it.  nparts > 1 keeps only what
+    partition `part` ingests (the VertexAdds of its vertices and every EdgeAdd with an endpoint
+    it owns, Utils.getPartition), so a rank holds O(stream / P) updates."""
+    count = max(0, min(count, interactions - first))
+    t, k, s, d = _alloc(3 * count)
+    n = N.synth().rg_gen_gab_range(seed, seed if id_key is None else id_key, users, interactions, first, count,
+                                   part, nparts, t0, t1, N.ptr(t, N.C.c_int64), N.ptr(k, N.C.c_uint8),
+                                   N.ptr(s, N.C.c_int64), N.ptr(d, N.C.c_int64))
+    return Stream(t[:n], k[:n], s[:n], d[:n])
+
+
 def range_hops(start: int, end: int, jump: int) -> np.ndarray:
     """Hop timestamps of a Range job: RangeAnalysisTask.restart (RangeAnalysisTask.scala:18-35)
     starts at `start`, adds `jump`, clamps to `end`, and stops once it has run `end`."""

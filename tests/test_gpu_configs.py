@@ -1,0 +1,227 @@
+"""Every BASELINE.json config at (or near) full size, HIP path against the CPU oracle.
+
+  C1  100k vertices / 1M updates, ViewLens CC at t_end            per-vertex labels, whole view
+  C2  same stream, 8,041 hourly hops x {y,m,w,d,h}                full query summaries at 64 hops
+                                                                  spread over the range + per-vertex
+                                                                  labels of those 320 views
+  C3  10M vertices / 100M power-law updates, 61 daily hops x      degree totals of every view
+      {month, week, day}, DegreeBasic + PageRank(20)              (properties) + per-vertex degrees
+                                                                  and PR (L1 <= 1e-6) at sampled hops
+  C4  the first 100M updates of the 1B GAB stream (20M users),    summaries of all 840 views
+      168 hourly hops x {y,m,w,d,h}, CC                           (properties), per-vertex labels of
+                                                                  day/hour views at sampled hops and
+                                                                  the year view at the last hop
+  C5  30M-update GAB base + one 10M-update hour tick merged       labels / PR / counts equal to a
+      into the resident graph, CC + PR(20) on the newest hour     one-shot seal of the same stream
+
+The oracle at C3/C4 size is the lazy-edge replay (oracle.h ORC_LAZY_EDGES, checked against the
+literal replay in tests/test_oracle_scale.py); it is built in a background thread while the GPU
+path ingests and seals (ctypes releases the GIL), and per-view queries run in a thread pool.
+Reference semantics: ConnectedComponents.scala:10-42,137-145; DegreeBasic.scala:16-28;
+SURVEY.md App. A.5 (PageRank spec).
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from oracle import Oracle, label_counts
+from raphtory_amd import TemporalGraph
+from raphtory_amd.analysis import cc_fields, cc_fields_from_summary
+from raphtory_amd.synth import (BATCH_WINDOWS, DAY, HOUR, MONTH, T0_README, WEEK, YEAR, gen_gab, gen_gab_range,
+                                gen_powerlaw, gen_uniform, range_hops)
+
+pytestmark = [pytest.mark.gpu, pytest.mark.fullsize]
+
+PR_L1_TOL = 1e-6  # BASELINE.json north_star: PageRank within 1e-6 L1 per view
+POOL = 8          # oracle query threads (the GPU box gives this job 16 host cores)
+
+
+def _graph(s):
+    g = TemporalGraph()
+    g.ingest_stream(s)
+    g.seal()
+    return g
+
+
+def _summary_props(summ):
+    """Invariants of processBatchWindowResults fields (ConnectedComponents.scala:137-145) on every
+    view: [hops, windows, 8] = biggest, total, >1, islands, >2, sum, sum(>1), supersteps."""
+    big, tot, nis, isl, gt2, sall, snis = (summ[..., i] for i in range(7))
+    assert np.all(tot == nis + isl) and np.all(gt2 <= nis) and np.all(big <= sall)
+    assert np.all(snis <= sall) and np.all((tot == 0) == (sall == 0))
+    assert np.all(sall - snis == isl)  # every island is one vertex
+    assert np.all((big > 0) == (sall > 0))
+    assert np.all(np.diff(sall, axis=1) <= 0)  # descending windows: nested vertex sets (shrinkWindow)
+
+
+def _check_labels(g, h, w, ids, lab, where):
+    gids, glab = g.cc_vertex_labels(h, w)
+    assert np.array_equal(gids, ids), where
+    assert np.array_equal(glab, lab), where
+
+
+# ------------------------------------------------------------------ C1
+def test_c1_view_cc_at_t_end():
+    s = gen_uniform(1, 100_000, 1_000_000)
+    t_end = int(s.t[-1])
+    with ThreadPoolExecutor(1) as ex:
+        fo = ex.submit(Oracle.from_stream, s)
+        g = _graph(s)
+        g.run("cc", [t_end], [], retain=True)  # ViewLens: no window
+        o = fo.result()
+    ((ids, lab),), steps = o.cc(t_end, [], mode=1)
+    assert len(ids) > 50_000
+    _check_labels(g, 0, 0, ids, lab, "C1")
+    exp = label_counts(lab)
+    assert g.cc_result(0, 0) == exp
+    assert cc_fields_from_summary(g.cc_summary(0, 0)) == cc_fields(exp)
+    g.close()
+
+
+# ------------------------------------------------------------------ C2
+def test_c2_range_64_spread_hops_per_vertex():
+    s = gen_uniform(1, 100_000, 1_000_000)
+    hops = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, HOUR)
+    assert len(hops) == 8041
+    pick = np.linspace(0, len(hops) - 1, 64).round().astype(int)
+    with ThreadPoolExecutor(POOL) as ex:
+        fo = ex.submit(Oracle.from_stream, s)
+        g = _graph(s)
+        g.run("cc", hops, BATCH_WINDOWS)  # the benchmark query: 630 window-major batches
+        full = g.cc_summaries()
+        _summary_props(full)
+        g.run("cc", hops[pick], BATCH_WINDOWS, retain=True)  # other batch composition, same views
+        part = g.cc_summaries()
+        o = fo.result()
+        res = list(ex.map(lambda t: o.cc(int(t), BATCH_WINDOWS, mode=1), hops[pick]))
+    for k, h in enumerate(pick):
+        assert full[h, 0, 7] == part[k, 0, 7] == res[k][1], (h, full[h, 0, 7], res[k][1])  # supersteps
+        for w in range(5):
+            ids, lab = res[k][0][w]
+            _check_labels(g, k, w, ids, lab, ("C2", int(hops[h]), w))
+            exp = cc_fields(label_counts(lab))
+            assert cc_fields_from_summary(g.cc_summary(k, w)) == exp, (h, w)
+            assert full[h, w, :7].tolist() == part[k, w, :7].tolist(), (h, w)
+    g.close()
+
+
+# ------------------------------------------------------------------ C3
+def test_c3_powerlaw_degree_and_pagerank():
+    end = T0_README + 2 * YEAR
+    s = gen_powerlaw(3, 10_000_000, 100_000_000, t0=T0_README, t1=end)
+    hops = range_hops(end - 60 * DAY, end, DAY)
+    windows = [MONTH, WEEK, DAY]
+    assert len(hops) == 61
+    with ThreadPoolExecutor(POOL) as ex:
+        fo = ex.submit(Oracle.from_stream, s, True)
+        g = _graph(s)
+        st = g.stats()
+        assert st["vertices"] > 9_000_000 and st["edges"] > 70_000_000
+        g.run("degree", hops, windows)
+        tot = np.array([[g.degree_result(h, w)[:3] for w in range(3)] for h in range(len(hops))])
+        assert np.all(np.diff(tot[..., 0], axis=1) <= 0)  # nested vertex sets
+        assert np.all(tot[..., 1] >= 0) and np.all(tot[..., 2] >= 0)
+        g.run("pagerank", hops, windows, pr_iters=20)  # the benchmark query runs clean
+        sample = [0, 30, 60]
+        g.run("degree", hops[sample], windows, retain=True)
+        gdeg = {(k, w): g.degree_vertex(k, w) for k in range(len(sample)) for w in range(3)}
+        gtot = {(k, w): g.degree_result(k, w)[:3] for k in range(len(sample)) for w in range(3)}
+        g.run("pagerank", hops[-1:], windows, pr_iters=20, retain=True)
+        gpr = [g.pr_result(0, w) for w in range(3)]
+        g.close()
+        o = fo.result()
+        # per window alone: with descending windows the running-min vertex set is the window's own
+        deg = {(k, w): ex.submit(lambda t, w: o.degree(int(t), [windows[w]])[0], hops[h], w)
+               for k, h in enumerate(sample) for w in range(3)}
+        pr = [ex.submit(lambda w: o.pagerank(int(hops[-1]), [windows[w]], iters=20)[0], w) for w in range(3)]
+        for (k, w), f in deg.items():
+            ids, od, idg = f.result()
+            gids, god, gid = gdeg[(k, w)]
+            assert np.array_equal(gids, ids) and np.array_equal(god, od) and np.array_equal(gid, idg), (k, w)
+            assert gtot[(k, w)] == (len(ids), int(od.sum()), int(idg.sum()))
+            assert tuple(tot[sample[k], w]) == gtot[(k, w)]  # the 61-hop run agrees
+        for w, f in enumerate(pr):
+            ids, p = f.result()
+            gids, gp = gpr[w]
+            assert np.array_equal(gids, ids)
+            assert np.abs(gp - p).sum() <= PR_L1_TOL, (w, np.abs(gp - p).sum())
+    o.close()
+
+
+# ------------------------------------------------------------------ C4
+def test_c4_first_100m_updates_cc():
+    users, inter = 20_000_000, 333_333_334  # the 1B-update C4 stream; its first 100M updates
+    s = gen_gab_range(4, users, inter, 0, 33_333_334)
+    assert len(s) == 100_000_002
+    end = int(s.t[-1])
+    hops = range_hops(end - 167 * HOUR, end, HOUR)
+    assert len(hops) == 168
+    pick = [0, 55, 111, 167]
+    with ThreadPoolExecutor(POOL) as ex:
+        fo = ex.submit(Oracle.from_stream, s, True)
+        g = _graph(s)
+        g.run("cc", hops, BATCH_WINDOWS)
+        full = g.cc_summaries()
+        _summary_props(full)
+        assert np.all(full[..., 5] > 0)  # the GAB stream is active every hour
+        g.run("cc", hops[pick], BATCH_WINDOWS, retain=True)
+        glab = {(k, w): g.cc_vertex_labels(k, w) for k in range(len(pick)) for w in (0, 3, 4)}
+        g.close()
+        o = fo.result()
+        short = {k: ex.submit(lambda t: o.cc(int(t), [DAY, HOUR], mode=1)[0], hops[h]) for k, h in enumerate(pick)}
+        year = ex.submit(lambda: o.cc(int(hops[-1]), [YEAR], mode=1)[0])
+        for k, f in short.items():
+            for j, w in enumerate((3, 4)):
+                ids, lab = f.result()[j]
+                gids, gl = glab[(k, w)]
+                assert np.array_equal(gids, ids) and np.array_equal(gl, lab), (pick[k], w)
+                assert cc_fields_from_summary_row(full[pick[k], w]) == cc_fields(label_counts(lab)), (pick[k], w)
+        ids, lab = year.result()[0]
+        gids, gl = glab[(len(pick) - 1, 0)]
+        assert np.array_equal(gids, ids) and np.array_equal(gl, lab)
+        assert cc_fields_from_summary_row(full[-1, 0]) == cc_fields(label_counts(lab))
+    o.close()
+
+
+def cc_fields_from_summary_row(row):
+    from raphtory_amd._native import CCSummary
+    s = CCSummary()
+    for (f, _), v in zip(CCSummary._fields_, row.tolist()):
+        setattr(s, f, v)
+    return cc_fields_from_summary(s)
+
+
+# ------------------------------------------------------------------ C5
+def test_c5_ten_million_update_tick_equals_one_shot_seal():
+    users = 20_000_000
+    base = gen_gab(4, users, 10_000_000)
+    now = int(base.t[-1])
+    tick = gen_gab(100, users, 3_333_334, t0=now + 1, t1=now + HOUR, id_key=4)
+    assert len(tick) == 10_000_002
+    now = int(tick.t[-1])
+    live = _graph(base)
+    live.ingest_stream(tick)
+    live.seal()  # merged into the resident graph (merge.hip)
+    assert live.stats()["seal_incremental"] == 1 and live.stats()["seal_delta_updates"] == len(tick)
+    one = TemporalGraph()
+    one.ingest_stream(base)
+    one.ingest_stream(tick)
+    one.seal()
+    a, b = live.stats(), one.stats()
+    for k in ("vertices", "edges", "vertex_events", "edge_events", "deaths"):
+        assert a[k] == b[k], k
+    for g in (live, one):
+        g.run("cc", [now], BATCH_WINDOWS, retain=True)
+    for w in range(5):
+        ia, la = live.cc_vertex_labels(0, w)
+        ib, lb = one.cc_vertex_labels(0, w)
+        assert np.array_equal(ia, ib) and np.array_equal(la, lb), w
+        assert live.cc_summaries()[0, w].tolist() == one.cc_summaries()[0, w].tolist()
+    for g in (live, one):
+        g.run("pagerank", [now], [HOUR], pr_iters=20, retain=True)
+    ia, pa = live.pr_result(0, 0)
+    ib, pb = one.pr_result(0, 0)
+    assert np.array_equal(ia, ib) and np.abs(pa - pb).sum() <= PR_L1_TOL
+    live.close()
+    one.close()

@@ -29,8 +29,10 @@ def check_cc(g, o, hops, windows, max_steps=100):
     g.run("cc", hops, windows, max_steps=max_steps, retain=True)
     nw = max(1, len(windows))
     for h, t in enumerate(np.asarray(hops).tolist()):
-        res, _ = o.cc(t, windows, max_steps=max_steps, mode=1)
+        res, steps = o.cc(t, windows, max_steps=max_steps, mode=1)
         for w in range(nw):
+            # the hop's job superstep count (AnalysisTask.endStep), whatever batches held its views
+            assert g.cc_summary(h, w).supersteps == steps, (t, w, g.cc_summary(h, w).supersteps, steps)
             ids, lab = res[w]
             gids, glab = g.cc_vertex_labels(h, w)
             assert np.array_equal(gids, ids), (t, w)

@@ -25,9 +25,11 @@ def _parts(s, P):
 def check_cc(lp, o, hops, windows, max_steps=100):
     lp.run("cc", hops, windows, max_steps=max_steps, retain=True)
     for h, t in enumerate(np.asarray(hops).tolist()):
-        res, _ = o.cc(t, windows, max_steps=max_steps, mode=1)
+        res, steps = o.cc(t, windows, max_steps=max_steps, mode=1)
         for w in range(max(1, len(windows))):
             ids, lab = res[w]
+            for g in lp.parts:
+                assert g.cc_summary(h, w).supersteps == steps, (t, w)
             gids, glab = lp.cc_vertex_labels(h, w)
             assert np.array_equal(gids, ids), (t, w)
             assert np.array_equal(glab, lab), (t, w)
