@@ -53,6 +53,7 @@ extern "C" {
 #define RGPU_RUN_RETAIN 1   /* keep per-vertex results of every view (for *_vertex_* queries) */
 #define RGPU_RUN_PROFILE 2  /* time every kernel launch with HIP events (rgpu_stats) */
 #define RGPU_RUN_SERIAL 4   /* one batch in flight (clean per-kernel event times) */
+#define RGPU_RUN_EDGE_COUNTS 8  /* count |E_{t,w}| per view (rgpu_cc_summary_t.alive_edges) (ABI 6) */
 
 typedef struct rgpu_ctx rgpu_ctx;
 
@@ -71,7 +72,7 @@ typedef struct {
                                     changed); 0 when maxSteps <= 1 (no Setup, AnalysisTask.scala:169)
                                     (ABI 6; before: the step count of the batch holding the view) */
   int64_t alive_edges;           /* |E_{t,w}|: edges alive in the view's window; filled by
-                                    RGPU_RUN_PROFILE runs, else -1 (ABI 6) */
+                                    RGPU_RUN_EDGE_COUNTS runs, else -1 (ABI 6) */
 } rgpu_cc_summary_t;
 
 typedef struct {
@@ -89,7 +90,7 @@ typedef struct {
    * and the number of updates that delta held (ABI 3) */
   double seal_ms;
   int64_t seal_incremental, seal_delta_updates;
-  /* last run, RGPU_RUN_PROFILE: sum over its views of |E_{t,w}| (else -1) (ABI 6) */
+  /* last run, RGPU_RUN_EDGE_COUNTS: sum over its views of |E_{t,w}| (else -1) (ABI 6) */
   int64_t alive_edge_windows;
 } rgpu_stats_t;
 

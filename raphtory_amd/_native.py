@@ -17,7 +17,7 @@ RGPU_OK = 0
 RGPU_EINVAL, RGPU_ESTATE, RGPU_EHIP, RGPU_ENOMEM, RGPU_ENOTSUP = -1, -2, -3, -4, -5
 RGPU_VADD, RGPU_VDEL, RGPU_EADD, RGPU_EDEL = 0, 1, 2, 3
 RGPU_ALGO_CC, RGPU_ALGO_DEGREE, RGPU_ALGO_PR, RGPU_ALGO_DIFFUSION = 0, 1, 2, 3
-RGPU_RUN_RETAIN, RGPU_RUN_PROFILE, RGPU_RUN_SERIAL = 1, 2, 4
+RGPU_RUN_RETAIN, RGPU_RUN_PROFILE, RGPU_RUN_SERIAL, RGPU_RUN_EDGE_COUNTS = 1, 2, 4, 8
 RGPU_XCHG_ID_BYTES, RGPU_XCHG_RCCL, RGPU_XCHG_LOOPBACK = 128, 0, 1
 ERROR_NAMES = {
     RGPU_EINVAL: "RGPU_EINVAL",

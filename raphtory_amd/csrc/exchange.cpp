@@ -35,6 +35,12 @@ class RcclExchange : public Exchange {
     std::memcpy(uid.internal, id, sizeof(uid.internal));
     ncclchk(ncclCommInitRank(&comm_, nranks, uid, rank), "ncclCommInitRank");
   }
+  RcclExchange(ncclComm_t c, int rank, int nranks) : comm_(c), r_(rank), n_(nranks) {}
+  Exchange* fork(int tag) override {
+    ncclComm_t c = nullptr;
+    ncclchk(ncclCommSplit(comm_, tag, r_, &c, nullptr), "ncclCommSplit");
+    return new RcclExchange(c, r_, n_);
+  }
   ~RcclExchange() override { (void)ncclCommDestroy(comm_); }
   int rank() const override { return r_; }
   int size() const override { return n_; }
@@ -101,9 +107,25 @@ struct LocalGroup {
 std::mutex g_reg_mu;
 std::map<uint64_t, std::weak_ptr<LocalGroup>> g_reg;
 
+std::shared_ptr<LocalGroup> local_group(uint64_t key, int nranks) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  std::shared_ptr<LocalGroup> g = g_reg[key].lock();
+  if (!g) {
+    g = std::make_shared<LocalGroup>(nranks);
+    g_reg[key] = g;
+  }
+  return g;
+}
+
 class LocalExchange : public Exchange {
  public:
-  LocalExchange(std::shared_ptr<LocalGroup> g, int rank) : g_(std::move(g)), r_(rank) {}
+  LocalExchange(std::shared_ptr<LocalGroup> g, int rank, uint64_t key) : g_(std::move(g)), r_(rank), key_(key) {}
+  Exchange* fork(int tag) override {
+    const uint64_t k = key_ * 0x9E3779B97F4A7C15ull + (uint64_t)tag + 1;  // same on every rank
+    std::shared_ptr<LocalGroup> g = local_group(k, g_->n);
+    if (g->n != g_->n) throw std::runtime_error("loopback exchange: partition counts disagree");
+    return new LocalExchange(g, r_, k);
+  }
   int rank() const override { return r_; }
   int size() const override { return g_->n; }
   void alltoall_i64(const int64_t* d_send, int64_t* d_recv, size_t n, hipStream_t s) override {
@@ -164,6 +186,7 @@ class LocalExchange : public Exchange {
  private:
   std::shared_ptr<LocalGroup> g_;
   int r_;
+  uint64_t key_;
 };
 
 }  // namespace
@@ -196,17 +219,9 @@ std::string open_exchange(const uint8_t id[kXchgIdBytes], int rank, int nranks, 
     if (std::memcmp(id, kLoopMagic, 8) == 0) {
       uint64_t key;
       std::memcpy(&key, id + 8, 8);
-      std::shared_ptr<LocalGroup> g;
-      {
-        std::lock_guard<std::mutex> lk(g_reg_mu);
-        g = g_reg[key].lock();
-        if (!g) {
-          g = std::make_shared<LocalGroup>(nranks);
-          g_reg[key] = g;
-        }
-      }
+      std::shared_ptr<LocalGroup> g = local_group(key, nranks);
       if (g->n != nranks) return "loopback exchange: partition counts disagree";
-      *out = new LocalExchange(g, rank);
+      *out = new LocalExchange(g, rank, key);
     } else {
       *out = new RcclExchange(id, rank, nranks);
     }

@@ -6,7 +6,8 @@
 // AnalysisTask.scala:208-225), and merge component sizes once per batch
 // (ncclReduceScatter of the label histogram + ncclAllReduce of the summary fields).
 //
-// Two implementations behind one interface:
+// Two implementations behind one interface (the loopback group is single-device: its
+// collectives read peers' buffers with device-local copies and kernels):
 //   RcclExchange   — RCCL communicator, one rank per GPU (the production path)
 //   LocalExchange  — partitions that live in one process (threads sharing one GPU):
 //                    the same protocol with device-to-device copies; used to test the
@@ -38,6 +39,11 @@ class Exchange {
   // d_recv[i] = sum over peers of d_send[rank*count + i]  (int32)
   virtual void reduce_scatter_i32(const int32_t* d_send, int32_t* d_recv, size_t count,
                                   hipStream_t s) = 0;
+  // A new, independent channel over the same ranks (collective: every rank calls it in the same
+  // order with the same tag).  Each batch slot of a partitioned run owns one, so that the
+  // collectives of batches in flight on different streams never share an ordering (RCCL:
+  // ncclCommSplit; loopback: a group of its own).
+  virtual Exchange* fork(int tag) = 0;
 };
 
 // id blob handed to every partition (rgpu_exchange_id / rgpu_exchange_init); returns "" or

@@ -305,7 +305,7 @@ __device__ __forceinline__ void edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1]
 // count alive edges per view: the wave's 64 mask words are bit-transposed (lane j <- view j)
 // and popcounted; the block sums them in LDS, one atomicAdd per (plane, view) per block.
 __device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane);
-template <bool PLANAR>
+template <bool PLANAR, bool COUNT>
 __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __restrict__ esrc,
                                                    const int32_t* __restrict__ edst,
                                                    const int64_t* __restrict__ eoff,
@@ -319,10 +319,10 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
   __shared__ unsigned int cnt_s[PLANAR ? kMaxPlanes : 1][64];
   hop_lds_init(L, bp, bp.thr_e);
   constexpr int NP = PLANAR ? kMaxPlanes : 1;
-  if (ecnt)
+  if (COUNT)
     for (int i = threadIdx.x; i < NP * 64; i += blockDim.x) (&cnt_s[0][0])[i] = 0;
   const int lane = lane_id();
-  uint32_t acc[NP] = {};
+  uint32_t acc[COUNT ? NP : 1] = {};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t e0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); e0 < ne; e0 += stride) {
     const int64_t e = e0 + lane;
@@ -331,14 +331,14 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
       edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime);
       store_bits<PLANAR>(m, bp, em, estride, e);
     }
-    if (ecnt) {  // an edge counts once over the partitions: where its source is owned
+    if constexpr (COUNT) {  // an edge counts once over the partitions: where its source is owned
       const bool mine = e < ne && esrc[e] < own_lim;
 #pragma unroll
       for (int w = 0; w < NP; w++)
         if (!PLANAR || w < L.W) acc[w] += __popcll(transpose64(mine ? m[w] : 0ull, lane));
     }
   }
-  if (ecnt) {
+  if constexpr (COUNT) {
     __syncthreads();  // cnt_s cleared
 #pragma unroll
     for (int w = 0; w < NP; w++)
@@ -354,13 +354,29 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
 
 // Block-wide OR of the views that changed in a step (per-wave values), then one sharded
 // atomicOr (kernels.hpp, lanechg).  Call from every thread of the block; `slot` is LDS.
+// `lanes` is wave-uniform (a ballot or an OR of ballots); callers that OR straight into the LDS
+// word pass 0.
 __device__ __forceinline__ void publish_lanes(uint64_t lanes, unsigned long long* slot,
                                               unsigned long long* lanechg, int step) {
-  for (int o = 32; o > 0; o >>= 1) lanes |= __shfl_xor(lanes, o);
   if ((threadIdx.x & 63) == 0 && lanes) atomicOr(slot, (unsigned long long)lanes);
   __syncthreads();
-  if (threadIdx.x == 0 && *slot && lanechg)
+  if (threadIdx.x == 0 && *slot && lanechg)  // result unused: the wave does not wait for it
     atomicOr(&lanechg[step * kLaneShards + (blockIdx.x & (kLaneShards - 1))], *slot);
+}
+
+// lanefold[r] = OR of the shards of step r (one wave per step), and the shards cleared for the
+// slot's next batch
+__global__ __launch_bounds__(256) void k_lane_fold(unsigned long long* __restrict__ lanechg,
+                                                   unsigned long long* __restrict__ lanefold) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+  if (r >= kLaneSteps) return;
+  unsigned long long x = lanechg[r * kLaneShards + lane];
+  if (x) lanechg[r * kLaneShards + lane] = 0;
+  for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o);
+  if (lane == 0) lanefold[r] = x;
+}
+void launch_lane_fold(hipStream_t s, unsigned long long* lanechg, unsigned long long* lanefold) {
+  k_lane_fold<<<kLaneSteps / 4, 256, 0, s>>>(lanechg, lanefold);
 }
 
 // Per-step work counters, sharded 64 ways so that blocks never pile up on one address (a
@@ -682,7 +698,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          const int32_t* __restrict__ lab_cur, int32_t* __restrict__ lab_next,
                                          const uint64_t* __restrict__ chg_prev,
                                          uint64_t* __restrict__ chg_next, uint8_t* __restrict__ act_next,
-                                         const TailList& tl, int lane, int32_t& changed, uint64_t& lanes,
+                                         const TailList& tl, int lane, int32_t& changed,
+                                         unsigned long long* __restrict__ lds_lanes,
                                          unsigned long long& pv, unsigned long long& ps,
                                          unsigned long long& pg, const int32_t* __restrict__ hv_of = nullptr,
                                          int32_t* __restrict__ hbest = nullptr) {
@@ -777,8 +794,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
         else lab_next[v * 64 + lane] = best[i];
       }
       if (lane == 0) chg_next[v] = ch;
-      lanes |= ch;
       if (ch) {
+        if (lane == 0) atomicOr(lds_lanes, (unsigned long long)ch);  // LDS: views changed this step
         changed++;
         mark<TAIL>(lane == 0, (int32_t)v, act_next, tl, lane);
         mark<TAIL>((sm[i] & ch) != 0, nb[i], act_next, tl, lane);
@@ -831,7 +848,6 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int32_t changed = 0;
-  uint64_t lanes = 0;
   unsigned long long pv = 0, ps = 0, pg = 0;
   const TailList none{nullptr, nullptr};
   for (int64_t c = wave; c * CH < nv; c += nwaves) {
@@ -846,7 +862,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     if (v0 + CH > nv) bits &= (1u << (nv - v0)) - 1;
     if (!bits) continue;
     cc_chunk<CH, BUF, false>(v0 + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
-                             lab_next, chg_prev, chg_next, act_next, none, lane, changed, lanes, pv, ps, pg,
+                             lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[3], pv, ps, pg,
                              hv_of, hbest);
   }
   if (work)
@@ -857,7 +873,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     if (ps) atomicAdd(&wred[1], ps);
     if (pg) atomicAdd(&wred[2], pg);
   }
-  publish_lanes(lanes, &wred[3], lanechg, step);
+  publish_lanes(0, &wred[3], lanechg, step);
   if (threadIdx.x == 0) {
     if (red && stepflag[step] == 0) {  // first writers also tell the host (mapped pinned memory)
       stepflag[step] = 1;
@@ -944,16 +960,13 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
     uint64_t* chg_next = (s & 1) ? chg1 : chg0;
     const TailList tl{list[p ^ 1], &nlist[p ^ 1]};
     int32_t changed = 0;
-    uint64_t lanes = 0;
     unsigned long long pv = 0, ps = 0, pg = 0;
     for (int c = wid * 4; c < ncur; c += nw * 4) {
       const int k = c + (lane & 3) < ncur ? c + (lane & 3) : c;
       const uint32_t bits = ncur - c >= 4 ? 0xfu : ((1u << (ncur - c)) - 1);
       cc_chunk<4, BUF, true>((int64_t)list[p][k], bits, adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
-                             chg_prev, chg_next, a_next, tl, lane, changed, lanes, pv, ps, pg);
+                             chg_prev, chg_next, a_next, tl, lane, changed, &wsum[3], pv, ps, pg);
     }
-    for (int o = 32; o > 0; o >>= 1) lanes |= __shfl_xor(lanes, o);
-    if (lane == 0 && lanes) atomicOr(&wsum[3], (unsigned long long)lanes);
     for (int o = 32; o > 0; o >>= 1) pg += __shfl_xor(pg, o);
     if (lane == 0) {
       if (changed) atomicAdd(&nchanged, changed);
@@ -1803,12 +1816,13 @@ void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp,
 }
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
                       unsigned long long* ecnt, int64_t h0) {
-  if (planar)
-    k_edge_mask<true><<<grid_for(g.ne, 256), 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime,
-                                                           bp, em, g.ne, ecnt, h0, g.n_own);
-  else
-    k_edge_mask<false><<<grid_for(g.ne, 256), 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime,
-                                                            bp, em, g.ne, ecnt, h0, g.n_own);
+#define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, bp, em, g.ne, ecnt, h0, g.n_own
+  const unsigned grid = grid_for(g.ne, 256);
+  if (planar && ecnt) k_edge_mask<true, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
+  else if (planar) k_edge_mask<true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
+  else if (ecnt) k_edge_mask<false, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
+  else k_edge_mask<false, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
+#undef RGPU_EM_ARGS
 }
 void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,

@@ -63,11 +63,16 @@ struct BatchClear {
 };
 
 // Per-step OR of the views (lanes) in which some label changed: words lanechg[step*kLaneShards +
-// shard], one atomicOr per block that saw a change (sharded: thousands of blocks on one word
-// serialise at the memory side).  A view's last changing step gives the superstep count the
-// reference's job would run (AnalysisTask.endStep :208-225): min(maxSteps, last + 1).
-constexpr int kLaneShards = 8;
-constexpr int kLaneChgWords = 128 * kLaneShards;  // kMaxSteps (rgpu.cpp) x shards
+// shard], one non-returning atomicOr per block that saw a change (64 shards: thousands of
+// blocks on one word serialise at the memory side; a returning or read-first form made every
+// such block wait a round trip at its end, +8 % on the C2 superstep kernel).  The summary
+// kernel folds the shards into lanefold[step] so the host copies 128 words per batch.  A view's
+// last changing step gives the superstep count the reference's job runs (AnalysisTask.endStep
+// :208-225): min(maxSteps, last + 1).
+constexpr int kLaneShards = 64;
+constexpr int kLaneSteps = 128;                          // kMaxSteps (rgpu.cpp)
+constexpr int kLaneChgWords = kLaneSteps * kLaneShards;
+void launch_lane_fold(hipStream_t s, unsigned long long* lanechg, unsigned long long* lanefold);
 
 // K1.  planar = false: one mask word per entity, view bit w*KS + k.  planar = true (W <=
 // kMaxPlanes): one word per window w at out[w*stride + i], bit k = hop of the block.

@@ -280,9 +280,11 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
   } else {
     // Partition view (the reference's PM keeps its own vertices plus SplitEdge copies,
     // EntityStorage.scala:303-305): owned vertices, ghosts = other endpoints of edges that
-    // touch an owned vertex.  Every partition is handed the whole stream, so a ghost's
-    // history (all its events) and every edge's endpoint deaths are complete here.
-    // Local rank order: owned by id, then ghosts by id; labels stay global ranks.
+    // touch an owned vertex.  The partition keeps (rgpu_ingest) every update of its own
+    // vertices, every edge update with an owned endpoint and every VertexDelete, so owned
+    // histories, kept edges' histories and every endpoint's deaths (killList) are complete;
+    // a ghost's vertex history is not (its membership comes from its owner, per hop block).
+    // Local rank order: owned by id, then ghosts by id; CC labels are vertex ids.
     const int64_t ng = (int64_t)ids.size();
     std::vector<std::atomic<uint8_t>> role(ng);  // 0 owned, 1 ghost, 2 not kept
     parallel_for((size_t)ng, nt, [&](size_t lo, size_t hi, int) {
@@ -304,7 +306,8 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
         if (role[g].load(std::memory_order_relaxed) == r) {
           g2l[g] = (int32_t)P.vid.size();
           P.vid.push_back(ids[g]);
-          P.grank.push_back((int32_t)g);
+          P.grank.push_back((int32_t)ids[g]);  // label = id (ids < 2^31): order-preserving, global
+          P.lowner.push_back((uint8_t)partition_of(ids[g], num_partitions));
           if (r == 0) P.n_own++;
         }
     P.nv = (int64_t)P.vid.size();
@@ -314,7 +317,6 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
         if (rd[i] >= 0) rd[i] = g2l[rd[i]];
       }
     });
-    P.gvid = std::move(ids);
   }
   const int64_t n_own = P.n_own;
   // an edge is kept iff both endpoints are kept and one of them is owned
@@ -326,11 +328,11 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
   // a self-loop), each segment sorted by (t, idx), equal t collapsed (last put wins)
   {
     // a record slot per (event, end): 2i = src side, 2i+1 = dst side
-    auto vkey_of = [&](size_t j) -> int64_t {
+    auto vkey_of = [&](size_t j) -> int64_t {  // owned ranks only: a ghost's history is partial here
       const size_t i = j >> 1;
       const Event& e = ev[i];
-      if (!(j & 1)) return e.kind == RGPU_EDEL || rs[i] < 0 ? -1 : rs[i];
-      return (e.kind == RGPU_EADD && rd[i] != rs[i] && rd[i] >= 0) ? rd[i] : -1;
+      if (!(j & 1)) return e.kind == RGPU_EDEL || rs[i] < 0 || rs[i] >= n_own ? -1 : rs[i];
+      return (e.kind == RGPU_EADD && rd[i] != rs[i] && rd[i] >= 0 && rd[i] < n_own) ? rd[i] : -1;
     };
     auto vmake = [&](size_t j) {
       const size_t i = j >> 1;

@@ -46,8 +46,12 @@ enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUM
                 KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_HEAVY = 8, KID_DIFF = 9, KID_N = 12 };
 
 constexpr int kMaxSteps = 128;
-constexpr int kLaneOff = 7 * kViews;                     // lane-change words (kernels.hpp)
-constexpr int kStatWords = kLaneOff + kLaneChgWords;     // 6 per-view fields + counters row + lanes
+// stats words: 6 per-view fields + counters row | folded lane words [step] | lane-change shards
+// [step][shard] (kernels.hpp).  The host copies the first kStatCopy words of a batch.
+constexpr int kFoldOff = 7 * kViews;
+constexpr int kLaneOff = kFoldOff + kLaneSteps;
+constexpr int kStatCopy = kLaneOff;
+constexpr int kStatWords = kLaneOff + kLaneChgWords;
 constexpr int kWorkWords = kMaxSteps * 64 * 4;
 constexpr int64_t kPad = 64;  // tail padding of per-vertex / per-slot batch arrays
 constexpr int kMaxSlots = 4;  // batches in flight (one HIP stream each; GPU_MAX_HW_QUEUES = 4)
@@ -328,6 +332,7 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       HIPCHK(hipHostMalloc((void**)&s.h_work, sizeof(unsigned long long) * kWorkWords));
       s.stepcnt = dalloc<int32_t>(L, kMaxSteps);
       s.stats = dalloc<unsigned long long>(L, kStatWords);
+      HIPCHK(hipMemset(s.stats, 0, sizeof(unsigned long long) * kStatWords));
     }
     if (algo == RGPU_ALGO_CC && !s.a_cc) {
       // padded so that the superstep kernel's clamped, unconditional loads stay in bounds
@@ -534,7 +539,8 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
     timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * nviews,
                  [&] { launch_cc_summary(s.stream, g, nviews, hist, s.stats, s.iso); });
   }
-  HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatWords,
+  if (rc.algo == RGPU_ALGO_CC) launch_lane_fold(s.stream, s.stats + kLaneOff, s.stats + kFoldOff);
+  HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatCopy,
                         hipMemcpyDeviceToHost, s.stream));
   if (rc.flags & RGPU_RUN_RETAIN) {
     Retained& R = c->kept[s.batch];
@@ -604,7 +610,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   std::memset(s.h_stepcnt, 0, sizeof(int32_t) * kMaxSteps);  // slot idle: no kernel writes it
   BatchClear clr;
   clr.stats = s.stats;
-  clr.n_stats = kStatWords;
+  clr.n_stats = kStatCopy;  // the lane shards are zero: cleared by the fold of the slot's previous batch
   clr.flags = s.stepcnt;
   clr.n_flags = kMaxSteps;
   if (rc.algo == RGPU_ALGO_CC || rc.algo == RGPU_ALGO_DIFFUSION) {
@@ -715,11 +721,8 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
   const int grp = s.batch % rc.G;
   int32_t last[kViews] = {};  // per lane: last superstep with a label change (0: none)
   if (rc.algo == RGPU_ALGO_CC)
-    for (int r = 1; r <= s.r_final && r < kMaxSteps; r++) {
-      unsigned long long m = 0;
-      for (int k = 0; k < kLaneShards; k++) m |= h[kLaneOff + r * kLaneShards + k];
-      for (; m; m &= m - 1) last[__builtin_ctzll(m)] = r;
-    }
+    for (int r = 1; r <= s.r_final && r < kMaxSteps; r++)
+      for (unsigned long long m = h[kFoldOff + r]; m; m &= m - 1) last[__builtin_ctzll(m)] = r;
   for (int k = 0; k < s.kb; k++)
     for (int wl = 0; wl < rc.gsize; wl++) {
       const int j = wl * rc.K + k;  // view bit: window-major within the batch
@@ -975,7 +978,7 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
     s.kb = bp.K;
     BatchClear clr;
     clr.stats = s.stats;
-    clr.n_stats = kStatWords;
+    clr.n_stats = kStatCopy;
     clr.flags = s.stepcnt;
     clr.n_flags = kMaxSteps;
     if (rc.algo == RGPU_ALGO_CC) {
@@ -1031,7 +1034,8 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
       }
     }
     // stats, retained rows (finish_batch without the single-GPU CC reductions)
-    HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatWords,
+    if (rc.algo == RGPU_ALGO_CC) launch_lane_fold(s.stream, s.stats + kLaneOff, s.stats + kFoldOff);
+    HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatCopy,
                           hipMemcpyDeviceToHost, s.stream));
     if (rc.flags & RGPU_RUN_RETAIN) {
       Retained& R = c->kept[b];
@@ -1476,7 +1480,7 @@ int rgpu_seal(rgpu_ctx* c) {
     if (c->partitioned) {
       if (c->nparts > 1) g.grank = dupload(L, P.grank);
       Part& X = c->pt;
-      X.ng = c->nparts > 1 ? (int64_t)P.gvid.size() : P.nv;
+      X.ng = P.nv;
       X.nxs = (int64_t)P.xs_v.size();
       X.nxr = (int64_t)P.xr_v.size();
       X.xs_off = P.xs_off;
@@ -1600,7 +1604,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->vlast.assign(algo == RGPU_ALGO_CC ? n_hops * rc.W : 0, 0);
     c->st.alive_edge_windows = -1;
     if (c->d_ecnt) { (void)hipFree(c->d_ecnt); c->d_ecnt = nullptr; }
-    if (flags & RGPU_RUN_PROFILE) {
+    if (flags & RGPU_RUN_EDGE_COUNTS) {
       HIPCHK(hipMalloc(&c->d_ecnt, sizeof(unsigned long long) * n_hops * rc.W));
       HIPCHK(hipMemset(c->d_ecnt, 0, sizeof(unsigned long long) * n_hops * rc.W));
     }
@@ -1629,7 +1633,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     for (int si = 0; si < kMaxSlots; si++)
       if (c->slot[si].stream) HIPCHK(hipStreamSynchronize(c->slot[si].stream));
     if (algo == RGPU_ALGO_CC) finish_supersteps(c, rc);
-    if (c->d_ecnt) {  // |E_{t,w}| per view (profile runs)
+    if (c->d_ecnt) {  // |E_{t,w}| per view (RGPU_RUN_EDGE_COUNTS)
       std::vector<unsigned long long> e(n_hops * rc.W);
       HIPCHK(hipMemcpy(e.data(), c->d_ecnt, sizeof(unsigned long long) * e.size(), hipMemcpyDeviceToHost));
       if (c->partitioned && c->nparts > 1) {
@@ -1679,7 +1683,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
 
 // id of the vertex whose global rank is l (CC labels are global ranks)
 static int64_t label_id(const rgpu_ctx* c, int32_t l) {
-  return c->nparts > 1 ? c->pk.gvid[l] : c->pk.vid[l];
+  return c->nparts > 1 ? (int64_t)l : c->pk.vid[l];  // partitioned: labels are ids
 }
 
 static int view_index(rgpu_ctx* c, size_t hop, size_t win, size_t* batch, int* lane) {

@@ -27,8 +27,8 @@ struct Packed {
   // ---- vertex partitioning (num_partitions > 1); identity when P = 1
   int part = 0, nparts = 1;
   int64_t n_own = 0;                 // ranks [0, n_own) are owned here, [n_own, nv) are ghosts
-  std::vector<int32_t> grank;        // [nv] global rank = CC label of each local rank (P > 1)
-  std::vector<int64_t> gvid;         // global vertex ids ascending (P > 1): label -> id
+  std::vector<int32_t> grank;        // [nv] CC label of each local rank = its vertex id (P > 1)
+  std::vector<uint8_t> lowner;       // [nv] owning partition of each local rank (P > 1)
   // exchange plan: per peer q, owned ranks that are ghosts on q (xs) and ghosts owned by q
   // (xr), both ascending by id, so q's xr list for this partition equals this xs list for q
   std::vector<int64_t> xs_off, xr_off;  // [P+1]
@@ -39,6 +39,18 @@ struct Packed {
 inline int partition_of(int64_t id, int nparts) {
   const int64_t a = id < 0 ? -id : id;
   return (int)((a % (10 * (int64_t)nparts)) / 10);
+}
+
+// What a partition keeps of the update stream (partitioned mode, rgpu_ingest): every update of
+// an owned vertex, every edge update with an owned endpoint (the reference routes an edge to
+// its source's PM and copies it to the destination's as a SplitEdge, EntityStorage.scala:
+// 237-314), and every VertexDelete (an endpoint death kills the edges of any partition,
+// killList / RemoteReturnDeaths, raphtoryMessages.scala:62,65).  So a rank holds O(stream/P)
+// updates whether it is handed the whole stream or only this part of it.
+inline bool partition_keeps(uint8_t kind, int64_t src, int64_t dst, int part, int nparts) {
+  if (nparts <= 1 || kind == RGPU_VDEL) return true;
+  if (partition_of(src, nparts) == part) return true;
+  return kind >= RGPU_EADD && partition_of(dst, nparts) == part;
 }
 
 struct Event {

@@ -1,0 +1,406 @@
+// xchg.hip — device side of the vertex-partitioned mode (host: rgpu.cpp).
+//
+// A partition keeps its owned vertices and ghost copies of their remote neighbours (the
+// reference's SplitEdge copies, EntityStorage.scala:303-305).  Three exchanges:
+//
+//   ghost membership   once per hop block: the owners' K1 vertex-mask words of the boundary
+//                      vertices (a ghost's own history is not on this partition).  Fixed sizes.
+//   label records      once per superstep: the ReaderWorker's VertexMessage traffic
+//                      (VertexVisitor.messageAllNeighbours, VertexVisitor.scala:112-147) as
+//                      records {entry, label, views}: one per distinct new label of a changed
+//                      boundary vertex, restricted to the views in which it has a kept
+//                      neighbour — a window-major batch (64 hops of one window) mostly changes
+//                      every lane to the same label, so a record is 16 B instead of a 256-B row.
+//   component counts   once per batch: (label, view, count) to the label's owner, which counts
+//                      at the label vertex (ConnectedComponents.returnResults :37-42 merged by
+//                      processBatchWindowResults :137).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "kernels.hpp"
+
+namespace rgpu {
+
+namespace {
+
+__device__ __forceinline__ int lane_of() { return threadIdx.x & 63; }
+__device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ int owner_of(int64_t id, int np) { return (int)(((id < 0 ? -id : id) % (10 * (int64_t)np)) / 10); }
+// record index i of a receive layout -> peer
+__device__ __forceinline__ int peer_of(const XPeers& P, int64_t i) {
+  int q = 0;
+  while (q + 1 < P.np && i >= P.pre[q + 1]) q++;
+  return q;
+}
+// rank of owned vertex `id` (ids of owned ranks ascend), or -1
+__device__ __forceinline__ int64_t owned_rank(const int64_t* __restrict__ vid, int64_t n_own, int64_t id) {
+  int64_t a = 0, b = n_own;
+  while (a < b) {
+    const int64_t m = (a + b) >> 1;
+    if (vid[m] < id) a = m + 1; else b = m;
+  }
+  return a < n_own && vid[a] == id ? a : -1;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ ghost membership
+// Send layout: peer q's words are [plane][entry] at planes * xoff[q] (receive layout mirrors it).
+__global__ __launch_bounds__(256) void k_xvm_pack(int64_t nx, const int32_t* __restrict__ xv,
+                                                  const int32_t* __restrict__ xq,
+                                                  const int64_t* __restrict__ xoff, int planes,
+                                                  const uint64_t* __restrict__ vm, int64_t vstride,
+                                                  uint64_t* __restrict__ out) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nx; e += (int64_t)gridDim.x * blockDim.x) {
+    const int q = xq[e];
+    const int64_t n = xoff[q + 1] - xoff[q], base = planes * xoff[q] + (e - xoff[q]);
+    const int32_t v = xv[e];
+    for (int p = 0; p < planes; p++) out[base + p * n] = vm[p * vstride + v];
+  }
+}
+__global__ __launch_bounds__(256) void k_xvm_unpack(int64_t nx, const int32_t* __restrict__ xv,
+                                                    const int32_t* __restrict__ xq,
+                                                    const int64_t* __restrict__ xoff, int planes,
+                                                    const uint64_t* __restrict__ in, uint64_t* __restrict__ vm,
+                                                    int64_t vstride) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nx; e += (int64_t)gridDim.x * blockDim.x) {
+    const int q = xq[e];
+    const int64_t n = xoff[q + 1] - xoff[q], base = planes * xoff[q] + (e - xoff[q]);
+    const int32_t g = xv[e];
+    for (int p = 0; p < planes; p++) vm[p * vstride + g] = in[base + p * n];
+  }
+}
+
+// ------------------------------------------------------------------ label records
+// Boundary entry e (owned vertex xv[e], peer xq[e]) is sent when the vertex was visited in the
+// step (act; null = every member, superstep 1) and changed in a view where it has a kept
+// neighbour (vadj, the OR of its kept slot masks).  Per distinct new label one record with the
+// views holding it.  A wave takes 64 entries: it counts the records per peer (lane q), reserves
+// them with one atomicAdd per (wave, peer), then writes them; scnt counts past the capacity
+// too, so the host sees an overflow and repeats the pack into a larger buffer.
+__global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const int32_t* __restrict__ xv,
+                                                   const int32_t* __restrict__ xq, const uint8_t* __restrict__ act,
+                                                   const uint64_t* __restrict__ chg_now,
+                                                   const uint64_t* __restrict__ vadj,
+                                                   const int32_t* __restrict__ lab, XRec* __restrict__ sbuf,
+                                                   unsigned long long* __restrict__ scnt) {
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t c = wave; c * 64 < nx; c += nwaves) {
+    const int64_t e = c * 64 + lane;
+    const bool ok = e < nx;
+    const int32_t v = ok ? xv[e] : 0;
+    const int q = ok ? xq[e] : 0;
+    uint64_t m = 0;
+    if (ok && (act == nullptr || act[v])) m = chg_now[v] & vadj[v];
+    const uint64_t todo = __ballot(m != 0);
+    if (!todo) continue;
+    unsigned long long cq = 0;  // lane p: records of this wave for peer p
+    for (uint64_t b = todo; b; b &= b - 1) {
+      const int L = __builtin_ctzll(b);
+      const int32_t vL = __builtin_amdgcn_readlane(v, L);
+      const int qL = __builtin_amdgcn_readlane(q, L);
+      uint64_t mm = rl64(m, L);
+      const int32_t x = lab[(int64_t)vL * 64 + lane];
+      int n = 0;
+      while (mm) {
+        const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
+        mm &= ~__ballot(((mm >> lane) & 1) && x == val);
+        n++;
+      }
+      if (lane == qL) cq += (unsigned long long)n;
+    }
+    unsigned long long off = 0;
+    if (lane < P.np && cq) off = atomicAdd(&scnt[lane], cq);
+    for (uint64_t b = todo; b; b &= b - 1) {
+      const int L = __builtin_ctzll(b);
+      const int32_t vL = __builtin_amdgcn_readlane(v, L);
+      const int qL = __builtin_amdgcn_readlane(q, L);
+      const int32_t eL = (int32_t)(c * 64 + L - P.xoff[qL]);
+      uint64_t mm = rl64(m, L);
+      const int32_t x = lab[(int64_t)vL * 64 + lane];
+      while (mm) {
+        const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
+        const uint64_t same = __ballot(((mm >> lane) & 1) && x == val);
+        const unsigned long long pos = __builtin_amdgcn_readlane((uint32_t)off, qL) |
+                                       ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(off >> 32), qL) << 32);
+        if (lane == 0 && pos < (unsigned long long)P.cap[qL]) {
+          XRec r;
+          r.e = eL;
+          r.val = val;
+          r.mask = same;
+          sbuf[P.base[qL] + pos] = r;
+        }
+        if (lane == qL) off++;
+        mm &= ~same;
+      }
+    }
+  }
+}
+
+// counts exchange words: [2q] = records for q (0 for self), [2q+1] = this partition changed a
+// label in the step (the halting vote, AnalysisTask.endStep :208-225); the counters are reset
+// for the next pack
+__global__ void k_xcounts(int np, int me, unsigned long long* __restrict__ scnt, const int32_t* __restrict__ stepflag,
+                          int64_t* __restrict__ xa) {
+  const int q = threadIdx.x;
+  if (q >= np) return;
+  xa[2 * q] = q == me ? 0 : (int64_t)scnt[q];
+  xa[2 * q + 1] = stepflag ? (stepflag[0] != 0) : 0;
+  scnt[q] = 0;
+}
+
+// ghosts whose change word a record set two supersteps ago: clear it in that parity's words
+__global__ __launch_bounds__(256) void k_xclear(XPeers P, const XRec* __restrict__ rbuf,
+                                                const int32_t* __restrict__ xrv, uint64_t* __restrict__ chg) {
+  const int64_t n = P.pre[P.np];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int q = peer_of(P, i);
+    chg[xrv[P.xoff[q] + rbuf[P.base[q] + i - P.pre[q]].e]] = 0;
+  }
+}
+
+// Records into ghost rows: the record's label in its views, and its views into the ghost's
+// change word (a ghost's records arrive together; the OR collects them).  A wave takes four
+// records, 16 lanes each covering the 64 views in 4 passes.
+__global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __restrict__ rbuf,
+                                                     const int32_t* __restrict__ xrv, int32_t* __restrict__ lab,
+                                                     uint64_t* __restrict__ chg) {
+  const int64_t n = P.pre[P.np];
+  const int lane = lane_of(), sub = lane >> 4, l16 = lane & 15;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i0 = wave * 4; i0 < n; i0 += nwaves * 4) {
+    const int64_t i = i0 + sub;
+    if (i >= n) continue;
+    const int q = peer_of(P, i);
+    const XRec r = rbuf[P.base[q] + i - P.pre[q]];
+    const int32_t g = xrv[P.xoff[q] + r.e];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int j = k * 16 + l16;
+      if ((r.mask >> j) & 1) lab[(int64_t)g * 64 + j] = r.val;
+    }
+    if (l16 == 0) atomicOr((unsigned long long*)&chg[g], (unsigned long long)r.mask);
+  }
+}
+
+// After the unpack: the first record of every ghost marks the ghost's owned neighbours that
+// share a changed view (the next frontier, as a local change would).  Heavy ghosts: k_heavy_mark.
+__global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict__ rbuf,
+                                               const int32_t* __restrict__ xrv, const uint64_t* __restrict__ chg,
+                                               const int64_t* __restrict__ adj_off, const int32_t* __restrict__ cnt,
+                                               const int32_t* __restrict__ snbr, const uint64_t* __restrict__ smask,
+                                               const int32_t* __restrict__ hv_of, uint8_t* __restrict__ act_next) {
+  const int64_t n = P.pre[P.np];
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave; i < n; i += nwaves) {
+    const int q = peer_of(P, i);
+    const int64_t k = i - P.pre[q];
+    const int32_t e = rbuf[P.base[q] + k].e;
+    if (k > 0 && rbuf[P.base[q] + k - 1].e == e) continue;  // not the ghost's first record
+    const int32_t g = xrv[P.xoff[q] + e];
+    if (hv_of && hv_of[g] >= 0) continue;
+    const uint64_t ch = chg[g];
+    const int32_t nk = cnt[g];
+    const int64_t base = adj_off[g];
+    for (int32_t c = 0; c < nk; c += 64) {
+      const int32_t j = c + lane;
+      if (j < nk && (smask[base + j] & ch)) act_next[snbr[base + j]] = 1;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ component counts
+// Label -> count of the partition's owned members (ConnectedComponents.returnResults :37-42)
+// routed to the label's owner: as k_cc_hist, a block stages 64 vertices' label rows and its
+// eight waves dedup each view's labels (after `rounds` labels, one entry per lane).  Counts of
+// labels owned here go straight into hist[view][owned rank]; the others become records
+// (label | view << 31 | count << 37) for their owner.  PASS 0 counts a block's records per
+// peer (blkcnt[q][block]); PASS 1 writes them at the scanned offsets (blkoff) and does the
+// local counting.  Members with no kept slot are islands, counted in iso as on one partition.
+template <int PASS>
+__global__ __launch_bounds__(512) void k_hist_route(XPeers P, int64_t n_own, int nviews, const int64_t* __restrict__ vid,
+                                                    const uint64_t* __restrict__ vm,
+                                                    const uint64_t* __restrict__ vadj,
+                                                    const int32_t* __restrict__ lab, int32_t* __restrict__ hist,
+                                                    unsigned int* __restrict__ iso_g, int rounds,
+                                                    int64_t* __restrict__ blkcnt, const int64_t* __restrict__ blkoff,
+                                                    unsigned long long* __restrict__ hsbuf) {
+  __shared__ int32_t tile[64][65];
+  __shared__ unsigned int iso[64];
+  __shared__ unsigned long long pc[kMaxParts];  // PASS 0: records per peer; PASS 1: running offsets
+  const int lane = lane_of(), wib = threadIdx.x >> 6;
+  if (threadIdx.x < 64) iso[threadIdx.x] = 0;
+  if (threadIdx.x < kMaxParts) pc[threadIdx.x] = 0;
+  const uint64_t vmask = (nviews >= 64 ? ~0ull : ((1ull << nviews) - 1)) & (0x0101010101010101ull << wib);
+  __syncthreads();
+  auto emit = [&](int32_t L, int j, unsigned int c, bool on) {  // per lane
+    if (!on) return;
+    const int q = owner_of(L, P.np);
+    if (q == P.me) {
+      if (PASS == 1) atomicAdd(&hist[(int64_t)j * n_own + owned_rank(vid, n_own, L)], (int32_t)c);
+      return;
+    }
+    const unsigned long long k = atomicAdd(&pc[q], 1ull);
+    if (PASS == 1)
+      hsbuf[P.base[q] + blkoff[(int64_t)q * gridDim.x + blockIdx.x] + (int64_t)k] =
+          (unsigned long long)L | ((unsigned long long)j << 31) | ((unsigned long long)c << 37);
+  };
+  for (int64_t c = blockIdx.x; c * 64 < n_own; c += gridDim.x) {
+    const int64_t v0 = c * 64;
+    const int nvc = (int)(n_own - v0 < 64 ? n_own - v0 : 64);
+    {
+      int32_t r[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = wib * 8 + k;
+        r[k] = i < nvc ? lab[(v0 + i) * 64 + lane] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) tile[wib * 8 + k][lane] = r[k];
+    }
+    const uint64_t mvl = lane < nvc ? vm[v0 + lane] : 0;
+    const uint64_t adl = lane < nvc ? vadj[v0 + lane] : 0;
+    uint64_t any = mvl;
+    for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
+    any = rl64(any, 0) & vmask;
+    __syncthreads();
+    while (any) {
+      const int j = __builtin_ctzll(any);
+      any &= any - 1;
+      const bool in_view = (mvl >> j) & 1;
+      const bool member = in_view && ((adl >> j) & 1);
+      if (PASS == 1) {
+        const uint64_t isolated = __ballot(in_view && !member);
+        if (lane == 0 && isolated) iso[j] += (unsigned)__popcll(isolated);
+      }
+      const int32_t l = tile[lane][j];
+      uint64_t todo = __ballot(member);
+      for (int it = 0; todo; it++) {
+        if (it == rounds) {
+          emit(l, j, 1u, (todo >> lane) & 1);
+          break;
+        }
+        const int leader = __builtin_ctzll(todo);
+        const int32_t L = __builtin_amdgcn_readlane(l, leader);
+        const uint64_t same = __ballot(member && l == L);
+        emit(L, j, (unsigned)__popcll(same), lane == leader);
+        todo &= ~same;
+      }
+    }
+    __syncthreads();
+  }
+  if (PASS == 0) {
+    __syncthreads();
+    if (threadIdx.x < P.np) blkcnt[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = (int64_t)pc[threadIdx.x];
+  } else {
+    __syncthreads();
+    if (threadIdx.x < 64 && iso[threadIdx.x]) atomicAdd(&iso_g[(blockIdx.x & 63) * 64 + threadIdx.x], iso[threadIdx.x]);
+  }
+}
+
+// exclusive scan of blkcnt[q][0..nb) per peer (one wave per peer) -> blkoff, and the peer's
+// total into tot[q] (the counts exchange)
+__global__ void k_blk_scan(int np, int64_t nb, const int64_t* __restrict__ blkcnt, int64_t* __restrict__ blkoff,
+                           unsigned long long* __restrict__ tot) {
+  const int q = threadIdx.x >> 6, lane = lane_of();
+  if (q >= np) return;
+  int64_t run = 0;
+  for (int64_t b0 = 0; b0 < nb; b0 += 64) {
+    const int64_t b = b0 + lane;
+    const int64_t x = b < nb ? blkcnt[q * nb + b] : 0;
+    int64_t inc = x;  // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(inc, o);
+      if (lane >= o) inc += y;
+    }
+    if (b < nb) blkoff[q * nb + b] = run + inc - x;
+    run += __shfl(inc, 63);
+  }
+  if (lane == 0) tot[q] = (unsigned long long)run;
+}
+
+// records received from the other partitions: count at the owned label vertex
+__global__ __launch_bounds__(256) void k_hist_recv(XPeers P, const unsigned long long* __restrict__ rbuf,
+                                                   const int64_t* __restrict__ vid, int64_t n_own,
+                                                   int32_t* __restrict__ hist) {
+  const int64_t n = P.pre[P.np];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int q = peer_of(P, i);
+    const unsigned long long r = rbuf[P.base[q] + i - P.pre[q]];
+    const int64_t L = (int64_t)(r & 0x7fffffffull);
+    const int j = (int)((r >> 31) & 63);
+    const int32_t c = (int32_t)(r >> 37);
+    const int64_t rk = owned_rank(vid, n_own, L);
+    if (rk >= 0) atomicAdd(&hist[(int64_t)j * n_own + rk], c);
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+static unsigned xgrid(int64_t items, int per_block, unsigned cap = 8192) {
+  int64_t g = (items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (unsigned)(g > cap ? cap : g);
+}
+void launch_xvm_pack(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff, int planes,
+                     const uint64_t* vm, int64_t vstride, uint64_t* out) {
+  if (nx > 0) k_xvm_pack<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, xq, xoff, planes, vm, vstride, out);
+}
+void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
+                       int planes, const uint64_t* in, uint64_t* vm, int64_t vstride) {
+  if (nx > 0) k_xvm_unpack<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, xq, xoff, planes, in, vm, vstride);
+}
+void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t* xv, const int32_t* xq,
+                      const uint8_t* act, const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab,
+                      XRec* sbuf, unsigned long long* scnt) {
+  if (nx > 0) k_xpack_rec<<<xgrid(nx, 4 * 64, 4096), 256, 0, s>>>(P, nx, xv, xq, act, chg_now, vadj, lab, sbuf, scnt);
+}
+void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa) {
+  k_xcounts<<<1, 64, 0, s>>>(np, me, scnt, stepflag, xa);
+}
+void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg) {
+  if (P.pre[P.np] > 0) k_xclear<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, xrv, chg);
+}
+void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
+                        uint64_t* chg) {
+  if (P.pre[P.np] > 0) k_xunpack_rec<<<xgrid(P.pre[P.np], 16), 256, 0, s>>>(P, rbuf, xrv, lab, chg);
+}
+void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
+                  const DevGraph& g, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
+                  uint8_t* act_next) {
+  if (P.pre[P.np] > 0)
+    k_xmark<<<xgrid(P.pre[P.np], 4), 256, 0, s>>>(P, rbuf, xrv, chg, g.adj_off, cnt, snbr, smask,
+                                                   g.n_seg > 0 ? g.hv_of : nullptr, act_next);
+}
+unsigned hist_route_grid(int64_t n_own) { return xgrid(n_own, 64, 8192); }
+void launch_hist_route(hipStream_t s, int pass, const XPeers& P, int64_t n_own, int nviews, const int64_t* vid,
+                       const uint64_t* vm, const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso,
+                       int64_t* blkcnt, const int64_t* blkoff, unsigned long long* hsbuf) {
+  const unsigned grid = hist_route_grid(n_own);
+  if (pass == 0)
+    k_hist_route<0><<<grid, 512, 0, s>>>(P, n_own, nviews, vid, vm, vadj, lab, hist, iso, g_hist_rounds, blkcnt,
+                                          blkoff, hsbuf);
+  else
+    k_hist_route<1><<<grid, 512, 0, s>>>(P, n_own, nviews, vid, vm, vadj, lab, hist, iso, g_hist_rounds, blkcnt,
+                                          blkoff, hsbuf);
+}
+void launch_blk_scan(hipStream_t s, int np, int64_t nb, const int64_t* blkcnt, int64_t* blkoff,
+                     unsigned long long* tot) {
+  k_blk_scan<<<1, 64 * kMaxParts, 0, s>>>(np, nb, blkcnt, blkoff, tot);
+}
+void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const int64_t* vid,
+                      int64_t n_own, int32_t* hist) {
+  if (P.pre[P.np] > 0) k_hist_recv<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, vid, n_own, hist);
+}
+
+}  // namespace rgpu

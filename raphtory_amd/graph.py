@@ -109,11 +109,12 @@ class TemporalGraph:
 
     # ------------------------------------------------------------------ run
     def run(self, algo: str, hops: Sequence[int], windows: Sequence[int] = (), max_steps: int = 100,
-            pr_iters: int = 20, retain: bool = False, profile: bool = False, serial: bool = False) -> None:
+            pr_iters: int = 20, retain: bool = False, profile: bool = False, serial: bool = False,
+            edge_counts: bool = False) -> None:
         hops = _i64(hops)
         w = _i64(list(windows))
         flags = ((N.RGPU_RUN_RETAIN if retain else 0) | (N.RGPU_RUN_PROFILE if profile else 0)
-                 | (N.RGPU_RUN_SERIAL if serial else 0))
+                 | (N.RGPU_RUN_SERIAL if serial else 0) | (N.RGPU_RUN_EDGE_COUNTS if edge_counts else 0))
         wptr = N.ptr(w, C.c_int64) if w.shape[0] else None
         self._check(self._lib.rgpu_run_view_batch(self._ctx, ALGOS[algo], N.ptr(hops, C.c_int64), hops.shape[0],
                                                   wptr, w.shape[0], max_steps, pr_iters, flags))

@@ -22,14 +22,17 @@ extern "C" void* ph_pack(const int64_t* t, const uint8_t* kind, const int64_t* s
 // partition view (num_partitions > 1): same stream, one partition's pack
 extern "C" void* ph_pack_part(const int64_t* t, const uint8_t* kind, const int64_t* src, const int64_t* dst,
                               size_t n, int part, int nparts) {
-  std::vector<Event> ev(n);
-  for (size_t i = 0; i < n; i++) ev[i] = {t[i], src[i], kind[i] >= 2 ? dst[i] : -1, kind[i]};
+  std::vector<Event> ev;  // what rgpu_ingest keeps for this partition
+  for (size_t i = 0; i < n; i++)
+    if (rgpu::partition_keeps(kind[i], src[i], kind[i] >= 2 ? dst[i] : -1, part, nparts))
+      ev.push_back({t[i], src[i], kind[i] >= 2 ? dst[i] : -1, kind[i]});
   Packed* p = new Packed();
   if (!rgpu::pack_events(ev, part, nparts, p).empty()) { delete p; return nullptr; }
   return p;
 }
-// what: 0 local vertex ids [nv], 1 global rank per local rank [nv] (P > 1), 2 send list ids of
-// peer q, 3 receive list ids of peer q, 4 edge src ids, 5 edge dst ids; returns the count
+// what: 0 local vertex ids [nv], 1 CC label per local rank [nv] (P > 1), 2 send list ids of
+// peer q, 3 receive list ids of peer q, 4 edge src ids, 5 edge dst ids, 6 owner partition per
+// local rank (P > 1); returns the count
 extern "C" int64_t ph_list(void* h, int what, int q, int64_t* out) {
   const Packed* p = (const Packed*)h;
   std::vector<int64_t> v;
@@ -39,6 +42,7 @@ extern "C" int64_t ph_list(void* h, int what, int q, int64_t* out) {
   if (what == 3) for (int64_t i = p->xr_off[q]; i < p->xr_off[q + 1]; i++) v.push_back(p->vid[p->xr_v[i]]);
   if (what == 4) for (int64_t e = 0; e < p->ne; e++) v.push_back(p->vid[p->esrc[e]]);
   if (what == 5) for (int64_t e = 0; e < p->ne; e++) v.push_back(p->vid[p->edst[e]]);
+  if (what == 6) v.assign(p->lowner.begin(), p->lowner.end());
   if (out) std::copy(v.begin(), v.end(), out);
   return (int64_t)v.size();
 }

@@ -248,3 +248,20 @@ def test_c2_full_size_properties_and_sampled_parity():
             exp = cc_fields(label_counts(res[w][1]))
             assert cc_fields_from_summary(g.cc_summary(h, w)) == exp, (h, w)
     g.close()
+
+
+def test_alive_edge_counts_vs_oracle(uniform_small):
+    """|E_{t,w}| per view (RGPU_RUN_EDGE_COUNTS, the SURVEY §8(d) byte model's edge count) equals
+    the number of edge entities the oracle finds alive (Entity.aliveAtWithWindow)."""
+    s, o, g = uniform_small
+    hops = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, 29 * DAY)
+    g.run("cc", hops, BATCH_WINDOWS, edge_counts=True)
+    summ = g.cc_summaries()
+    pairs = sorted({(int(a), int(b)) for a, b, k in zip(s.src, s.dst, s.kind) if k >= 2})
+    for h, t in enumerate(hops.tolist()):
+        for w, win in enumerate(BATCH_WINDOWS):
+            exp = sum(o.alive(True, a, b, t, win) for a, b in pairs)
+            assert summ[h, w, 8] == exp, (t, win, summ[h, w, 8], exp)
+    assert g.stats()["alive_edge_windows"] == int(summ[..., 8].sum())
+    g.run("cc", hops, BATCH_WINDOWS)
+    assert np.all(g.cc_summaries()[..., 8] == -1) and g.stats()["alive_edge_windows"] == -1

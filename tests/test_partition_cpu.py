@@ -1,9 +1,13 @@
 """Vertex-partitioned packing on the CPU: the product's host packer built
-with g++ (tests/harness.py).  Checks, per partition of P:
+with g++ (tests/harness.py), fed what rgpu_ingest keeps for the partition (partition_keeps:
+owned vertices' updates, edge updates with an owned endpoint, every VertexDelete).  Checks,
+per partition of P:
   * owned vertices are exactly Utils.getPartition(id, P) == p (Utils.scala:32-33) and ghosts
-    exactly their non-owned neighbours; edges exactly those touching an owned vertex;
-  * every owned / ghost vertex and every kept edge is alive at exactly the same (t, w) as in
-    the one-partition pack (so ghost histories and endpoint deaths are complete);
+    exactly their non-owned neighbours; edges exactly those touching an owned vertex; labels
+    are the ids and every rank knows its owner;
+  * every owned vertex and every kept edge is alive at exactly the same (t, w) as in the
+    one-partition pack (so owned histories and endpoint deaths are complete; a ghost's
+    membership comes from its owner at run time);
   * the exchange plan is symmetric: partition p's send list for q equals q's receive list
     from p, entry by entry (this is what lets boundary rows travel as (index, row) records);
   * the same plan agreement across two real processes (gloo, world size 2)."""
@@ -52,9 +56,9 @@ def test_roles_edges_and_plan(ph, P):
         own_set = set(own.tolist())
         nbrs = {b for a, b in pairs if a in own_set and a != b} | {a for a, b in pairs if b in own_set and a != b}
         assert set(ghost.tolist()) == nbrs - own_set
-        # global ranks index the global id list
-        gr = plist(ph, h, 1)
-        assert np.array_equal(all_ids[gr], vid)
+        # CC labels are the ids; owners per Utils.getPartition
+        assert np.array_equal(plist(ph, h, 1), vid)
+        assert np.array_equal(plist(ph, h, 6), get_partition(vid, P))
         kept = set(zip(plist(ph, h, 4).tolist(), plist(ph, h, 5).tolist()))
         assert kept == {(a, b) for a, b in pairs if a in own_set or b in own_set}
     assert np.array_equal(np.sort(np.concatenate(owned_union)), all_ids)
@@ -78,10 +82,11 @@ def test_partition_liveness_matches_single(ph, P):
     for p in range(P):
         hp = pack(ph, t, k, s, d, p, P)
         vid = plist(ph, hp, 0)
+        n_own = ph.ph_num(hp, 4)
         kept = list(zip(plist(ph, hp, 4).tolist(), plist(ph, hp, 5).tolist()))
         for tt in times.tolist():
             for w in (-1, 0, 40, 2000):
-                for v in vid.tolist():
+                for v in vid[:n_own].tolist():
                     bad += ph.ph_alive(hp, 0, v, -1, tt, w) != ph.ph_alive(h1, 0, v, -1, tt, w)
                 for a, b in kept[:: max(1, len(kept) // 60)]:
                     bad += ph.ph_alive(hp, 1, a, b, tt, w) != ph.ph_alive(h1, 1, a, b, tt, w)
@@ -103,7 +108,7 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     L = load_packer_harness()
-    t, k, s, d = _stream(77, 8000, 400)  # every rank is handed the whole stream
+    t, k, s, d = _stream(77, 8000, 400)  # every rank is handed the whole stream (and keeps its part)
     h = pack(L, t, k, s, d, rank, world)
     mine = {"own": plist(L, h, 0)[:L.ph_num(h, 4)].tolist(),
             "send": {p: plist(L, h, 2, p).tolist() for p in range(world)},
