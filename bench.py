@@ -1,20 +1,27 @@
 #!/usr/bin/env python3
-"""Benchmark: temporal edge-windows processed/sec for a batched-window CC Range query.
+"""Benchmark: temporal edge-windows processed/sec for a batched-window CC Range query, 1-8 GPUs.
 
-Workload (BASELINE.json configs[1], "C2"): seeded RandomSpout-shaped stream, 100k vertices,
-1M updates (30/40/10/20 % VADD/EADD/VDEL/EDEL) over one year; Range query from T0+30d to
-T0+365d hopping 1 h (8,041 hops) with batched windows {year, month, week, day, hour}, CC
-(ConnectedComponents, 100-superstep cap) on one MI355X.
+Headline workload (BASELINE.json configs[3], "C4"; the north star's 1B-event query):
+  the seeded GAB-shaped add-only stream (VADD s, VADD d, EADD s->d at one t,
+  GabUserGraphRouter.scala:31-33), 20M users, 333,333,334 interactions = 1,000,000,002 updates
+  from 2016-08-10 to 2018-05-31; Range query over the last 168 hours, hopping 1 h, batched
+  windows {year, month, week, day, hour}, ConnectedComponents (100-superstep cap).
 
   edge-windows = N_E x |windows| x |hops|   (N_E = directed edge entities)
 
 One "step" = one complete Range query (every hop x window: window filter, CSR compaction, CC
 supersteps, component-size reductions).  The packed graph is resident in HBM before timing.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): replicas —
-every rank holds the whole graph and runs its own share of a finer hop grid (rank r's hops
-are offset by r*jump/N), so per-GPU work is fixed and there is no data-path collective
-("scaling": "weak").  Timing: barrier + synchronize on both sides, max over ranks.
+N = 1: one partition (the one-GPU path).  N > 1 (python -m torch.distributed.run
+--nproc-per-node N bench.py --gpus N): vertex-partitioned, partition = rank =
+Utils.getPartition(id, N) (Utils.scala:32-33); each rank generates only the updates its
+partition keeps (O(stream/N) host memory) and the library exchanges boundary label records
+over RCCL every superstep.  The query is the same at every N ("scaling":
+"strong"); timing = barrier + synchronize on both sides, max over ranks.
+
+--config c2 is the BASELINE configs[1] query (C2, 100k vertices / 1M updates, 8,041 hourly
+hops); at N = 1 the headline line carries it as a secondary object.  c3 / c5 / diffusion are
+secondary lines.
 """
 from __future__ import annotations
 
@@ -44,8 +51,14 @@ def parse():
     p.add_argument("--profile-only", action="store_true",
                    help="only the serial HIP-event profile pass (the command rocprofv3 is run on, so "
                         "that its per-kernel averages match the roofline figures)")
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "diffusion"],
-                   help="c2 = the headline metric; diffusion = BinaryDefusion over the C2 query (secondary)")
+    p.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5", "diffusion"],
+                   help="c4 = the headline (north-star) query at every N; c2 = BASELINE configs[1]; "
+                        "diffusion = BinaryDefusion over the C2 query (secondary)")
+    p.add_argument("--no-secondary", action="store_true", help="N = 1: skip the C2 secondary object")
+    p.add_argument("--partitioned", action="store_true",
+                   help="N = 1: run the partitioned path with one partition (a one-rank RCCL channel): the "
+                        "exchange protocol's fixed costs without peers")
+    p.add_argument("--no-edge-counts", action="store_true", help="skip the SURVEY §8(d) byte-model pass")
     p.add_argument("--diff-seed", type=int, default=31,
                    help="diffusion infectedNode (BinaryDefusion.scala:10); -1 = the vertex with most EADDs as source")
     p.add_argument("--c5-users", type=int, default=20_000_000)
@@ -67,10 +80,10 @@ def dist_env():
     return rank, world, local
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (tools/gpu_profile.sh -> profiles/latest_pmc.json), or None."""
-    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
+def pmc_traffic(kernel, config="C2"):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of `config`
+    (tools/gpu_profile.sh -> profiles/latest_pmc[_c4].json), or None."""
+    path = os.path.join(ROOT, "profiles", "latest_pmc.json" if config == "C2" else f"latest_pmc_{config.lower()}.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -81,26 +94,58 @@ def pmc_traffic(kernel):
     return round(d["traffic_bytes_per_launch"]["value"]), "profiles/latest_pmc.json: " + d["traffic_bytes_per_launch"]["formula"]
 
 
-def cpu_baseline(stream, hops, windows, budget_s, n_edges):
-    """The oracle in reference structure (mode 0: lens rebuilt by linear closestTime scans every
-    superstep, adjacency re-filtered on every visit), single thread, on a bounded prefix of
-    the same hop list."""
+def cpu_info():
+    """(threads the host gives this job, nproc, CPU model): the GPU box shares its cores, and
+    says how many through OMP_NUM_THREADS (os.cpu_count() shows the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    want = int(os.environ.get("OMP_NUM_THREADS") or 0) or aff
+    model = "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "?")
+    except OSError:
+        pass
+    return max(1, min(want, aff)), os.cpu_count(), model
+
+
+def cpu_baseline(stream, hops, windows, budget_s, n_edges, what, lazy=False):
+    """The CPU oracle on the host's cores (ctypes releases the GIL: one view job per thread), over
+    hops drawn uniformly from the whole range: mode 0 = the reference's algorithmic structure
+    ("refsim": the lens rebuilt by linear closestTime scans every superstep, adjacency re-filtered
+    on every visit, queue messages; the reported value), mode 1 = the same semantics with
+    per-view caching (a fairer CPU bound, reported beside it)."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import Oracle
-    o = Oracle.from_stream(stream)
-    done, t0 = 0, time.perf_counter()
-    for t in hops.tolist():
-        o.cc(int(t), windows, max_steps=100, mode=0)
-        done += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
+    threads, nproc, model = cpu_info()
+    t0 = time.perf_counter()
+    o = Oracle.from_stream(stream, lazy=lazy)
+    build_s = time.perf_counter() - t0
+    order = np.random.default_rng(0).permutation(len(hops))  # uniform over the range
+    out = {}
+    for mode, budget in ((0, budget_s), (1, budget_s / 2)):
+        done, t0 = 0, time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            while done < len(order) and time.perf_counter() - t0 < budget:
+                batch = order[done:done + threads]
+                list(ex.map(lambda h: o.cc(int(hops[h]), windows, max_steps=100, mode=mode), batch))
+                done += len(batch)
+        dt = time.perf_counter() - t0
+        out[mode] = (n_edges * len(windows) * done / dt, done, dt)
+    o.close()
+    v0, d0, t0_ = out[0]
+    v1, d1, t1_ = out[1]
     return {
-        "value": n_edges * len(windows) * done / dt,
+        "value": v0,
         "unit": "edge-windows/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"first {done} of {len(hops)} hops x {len(windows)} windows of the same C2 query, "
-                  f"oracle refsim mode (reference algorithmic structure), {dt:.1f} s, 1 thread",
+        "nproc": nproc,
+        "cpu_model": model,
+        "sample": f"{what}: {d0} of {len(hops)} hops (uniform random over the range) x {len(windows)} windows, "
+                  f"oracle refsim mode (reference algorithmic structure), {t0_:.1f} s on {threads} threads "
+                  f"(oracle build {build_s:.1f} s, not timed); restatement, not the JVM",
+        "fast_oracle": {"value": v1, "unit": "edge-windows/s", "cores": threads,
+                        "sample": f"{d1} hops, oracle mode 1 (cached adjacency), {t1_:.1f} s"},
     }
 
 
@@ -191,68 +236,191 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def kernel_table(stats):
+    return {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                "avg_us": round(v["ms"] * 1e3 / v["launches"], 2),
+                "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
+            for k, v in stats["kernels"].items() if v["launches"]}
+
+
+def survey_bytes(summ, n_hops, windows, nv, ne, n_ev, ks, launches_step):
+    """SURVEY.md §8(d) algorithmic bytes of the query from the per-view counts the library
+    reports (|E_{t,w}| = alive_edges, R = the hop's superstep count):
+      K1  B1 = sum over hop blocks [8 N_ev + 8 (N_ent + 1) + K N_ent]
+      K2  B2 = sum over hops [N_E + sum_w (8|E_w| + 4 d |E_w| + 4 (V + 1))],  d = 2
+      K3  B3 = sum over views and executed supersteps [4 (V + 1) + 8 d |E_w| + 8 V + V / 4]
+    Superstep 1 runs inside the K2 kernel here, so the superstep kernel's share is supersteps
+    2..R."""
+    W = len(windows)
+    alive = summ[..., 8].astype(np.float64)
+    R = summ[..., 7].astype(np.float64)
+    n_ent = nv + ne
+    blocks = [min(64, n_hops - h) for h in range(0, n_hops, 64)]
+    b1 = sum(8.0 * n_ev + 8.0 * (n_ent + 1) + k * n_ent for k in blocks)
+    b2 = n_hops * ne + 16.0 * alive.sum() + n_hops * W * 4.0 * (nv + 1)
+    unit = 4.0 * (nv + 1) + 16.0 * alive + 8.0 * nv + nv / 4.0
+    b3 = float((R * unit).sum())
+    b3_step = float((np.maximum(R - 1, 0) * unit).sum())
+    t = sum(ks.get(k, {}).get("ms", 0.0) for k in ("window_mask", "cc_slots", "cc_step", "heavy", "cc_tail"))
+    t_step = ks.get("cc_step", {}).get("ms", 0.0)
+    return {"B1": b1, "B2": b2, "B3": b3, "alive_edge_windows": float(alive.sum()),
+            "supersteps_per_view_mean": float(R.mean()),
+            "K1_K2_K3_ms": t, "achieved_GBps": (b1 + b2 + b3) / max(t, 1e-9) / 1e6,
+            "cc_step": {"B3_steps_2_to_R": b3_step, "launches": launches_step,
+                        "bytes_per_launch": b3_step / max(1, launches_step),
+                        "achieved_GBps": b3_step / max(t_step, 1e-9) / 1e6}}
+
+
 def run_c4(a, rank, world, local):
-    """BASELINE configs[3] (C4): GAB-shaped add-only stream — (VADD s, VADD d, EADD s->d) triples
-    at one t (GabUserGraphRouter.scala:31-33) — 20M users, 333M interactions = 1B updates,
-    2016-08-10 -> 2018-05-31; batched windows {y,m,w,d,h}, hourly hops, the last 168 hops; CC.
-    N = 1: one graph.  N > 1: vertex-partitioned (Utils.getPartition), one partition per GPU,
-    boundary label rows exchanged over RCCL every superstep; every rank
-    generates the same seeded stream and keeps what its partition needs.  Secondary line."""
+    """The headline line: BASELINE configs[3] (C4), the 1B-update GAB-shaped stream, batched
+    windows {y,m,w,d,h} over the last 168 hourly hops, CC, on N = world GPUs (one partition per
+    GPU when N > 1)."""
     import torch
     from raphtory_amd import TemporalGraph
-    from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab, range_hops
+    from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")  # control plane; the data path is the library's RCCL
-    t0 = time.perf_counter()
-    s = gen_gab(4, a.c4_users, a.c4_interactions)
-    gen_s = time.perf_counter() - t0
-    log(f"C4 stream: {len(s)} updates generated in {gen_s:.1f} s")
     if dist is not None:
         from raphtory_amd.partitioned import open_rccl_partition
         g = open_rccl_partition(local, dist)
+    elif a.partitioned:
+        os.environ["RGPU_PARTITIONED"] = "1"
+        g = TemporalGraph(device=local)
+        g.exchange_init(TemporalGraph.exchange_id())
     else:
         g = TemporalGraph(device=local)
-    g.ingest_stream(s)
-    end = int(s.t[-1])
-    n_up = len(s)
-    del s
+    users, inter = a.c4_users, a.c4_interactions
+    t0 = time.perf_counter()
+    chunk = 20_000_000
+    n_kept = 0
+    for first in range(0, inter, chunk):  # this rank's updates only: O(stream / N) host memory
+        s = gen_gab_range(4, users, inter, first, chunk, rank, world)
+        g.ingest_stream(s)
+        n_kept += len(s)
+        del s
+    end = int(gen_gab_range(4, users, inter, inter - 1, 1).t[-1])
+    gen_s = time.perf_counter() - t0
+    log(f"rank {rank}: C4 stream generated + ingested in {gen_s:.1f} s ({n_kept} of {3 * inter} updates kept)")
     t0 = time.perf_counter()
     g.seal()
     seal_s = time.perf_counter() - t0
     st = g.stats()
-    log(f"sealed in {seal_s:.1f} s: {st['vertices']} vertices, {st['edges']} edge entities")
+
+    def total(x):
+        if dist is None:
+            return int(x)
+        t = torch.tensor([int(x)], dtype=torch.int64)
+        dist.all_reduce(t)
+        return int(t.item())
+
+    n_edges = total(st["edges_owned"])
+    n_vert = total(st["vertices"])
+    log(f"rank {rank}: sealed in {seal_s:.1f} s: {st['vertices']} owned vertices, {st['edges']} edges here; "
+        f"graph {n_vert} vertices, {n_edges} edge entities")
     hops = range_hops(end - (a.c4_hops - 1) * HOUR, end, HOUR)
     windows = BATCH_WINDOWS
-    g.run("cc", hops, windows)  # warm-up
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    if a.profile_only:
+        a.steps, a.warmup, a.no_cpu_baseline = 1, 0, True
+    for _ in range(a.warmup):
         g.run("cc", hops, windows)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    ms = (time.perf_counter() - t0) * 1e3 / a.steps
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(0 if a.profile_only else a.steps):
+        g.run("cc", hops, windows)
+    barrier()
+    elapsed = time.perf_counter() - t0
     if dist is not None:
         from raphtory_amd.replicas import max_over_ranks
-        ms = max_over_ranks(ms, dist)
-    log(f"query {ms:.1f} ms")
-    g.run("cc", hops, windows, profile=True, serial=True)
-    ks = {k: v for k, v in g.stats()["kernels"].items() if v["launches"]}
+        elapsed = max_over_ranks(elapsed, dist)
+    ms_per_step = elapsed * 1e3 / max(1, a.steps)
+    value = n_edges * len(windows) * len(hops) / (ms_per_step / 1e3)
+    if a.profile_only:
+        ms_per_step = value = None
+    log(f"rank {rank}: query {ms_per_step} ms")
     summ = g.cc_summaries()
-    out = {"config": "C4", "n_gpus": world, "updates": n_up, "vertices": st["vertices"], "edge_entities": st["edges"],
-           "vertex_events": st["vertex_events"], "edge_events": st["edge_events"], "gen_s": round(gen_s, 1),
-           "seal_s": round(seal_s, 1), "hops": len(hops), "windows": len(windows), "ms_per_query": round(ms, 2),
-           "edge_windows_per_s": st["edges"] * len(windows) * len(hops) / (ms / 1e3) if world == 1 else None,
-           "supersteps_per_batch_mean": round(g.stats()["supersteps"] / max(1, g.stats()["batches"]), 2),
-           "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3), "avg_us": round(v["ms"] * 1e3 / v["launches"], 2),
-                           "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)} for k, v in ks.items()},
-           "check": {"sum_biggest": int(summ[..., 0].sum()), "sum_total": int(summ[..., 1].sum()),
-                     "sum_members": int(summ[..., 5].sum())}}
+    roofline, ks, s8d = None, {}, None
+    if not a.no_profile_pass:
+        g.run("cc", hops, windows, profile=True, serial=True)  # collective at N > 1
+        ks = kernel_table(g.stats())
+        kraw = g.stats()["kernels"]
+        d = kraw["cc_step"]
+        gbs = d["bytes"] / (d["ms"] / 1e3) / 1e9
+        traffic, tsrc = pmc_traffic("k_cc_step2", config="C4")
+        roofline = {"bound": "hbm", "kernel": "cc_step (k_cc_step2)", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+                    "avg_launch_us": round(d["ms"] * 1e3 / d["launches"], 2),
+                    "algorithmic_bytes_per_launch": d["bytes"] / d["launches"],
+                    "bytes_model": "DESIGN.md §4 (bytes the superstep must touch per visited vertex / slot / "
+                                   "gathered label, counted by the kernel)"}
+        if not a.no_edge_counts and world == 1:
+            g.run("cc", hops, windows, edge_counts=True)
+            summ = g.cc_summaries()
+            s8d = survey_bytes(summ, len(hops), windows, st["vertices"], st["edges"],
+                               st["vertex_events"] + st["edge_events"] + st["deaths"], ks, d["launches"])
+            roofline["survey_8d"] = {"achieved": round(s8d["cc_step"]["achieved_GBps"], 1),
+                                     "frac": round(s8d["cc_step"]["achieved_GBps"] / HBM_PEAK_GBS, 4),
+                                     "bytes_per_launch": s8d["cc_step"]["bytes_per_launch"],
+                                     "note": "SURVEY §8(d) B3 over supersteps 2..R of every view (one CSR pass "
+                                             "per view per superstep) / the same launches' time"}
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from raphtory_amd.synth import gen_gab
+        sm = gen_gab(4, users // 100, inter // 100)  # the same query on the 1/100-scale stream
+        sm_end = int(sm.t[-1])
+        sm_hops = range_hops(sm_end - (a.c4_hops - 1) * HOUR, sm_end, HOUR)
+        gs = TemporalGraph(device=local)
+        gs.ingest_stream(sm)
+        gs.seal()
+        sm_edges = gs.stats()["edges"]
+        gs.close()
+        cpu = cpu_baseline(sm, sm_hops, windows, a.cpu_seconds, sm_edges,
+                           f"C4 query on the 1/100-scale GAB stream ({len(sm)} updates, {users // 100} users, "
+                           f"{sm_edges} edge entities, same span)", lazy=True)
+    secondary = None
+    if rank == 0 and world == 1 and not a.no_secondary and not a.profile_only:
+        secondary = run_c2(a, 0, 1, local, quiet=True)
     if rank == 0:
+        out = {
+            "metric": "temporal edge-windows processed/sec for batched-window CC range query",
+            "value": round(value, 1) if value is not None else None,
+            "unit": "edge-windows/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 3) if ms_per_step is not None else None,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (seeded GAB-shaped add-only stream, SURVEY.md App. B gen_gab)",
+            "config": {"workload": "C4: 1B-update GAB-shaped stream (20M users, 333,333,334 interactions), "
+                                   "168 hourly hops x 5 batched windows {y,m,w,d,h}, ConnectedComponents",
+                       "updates": 3 * inter, "vertices": n_vert, "edge_entities": n_edges, "hops": int(len(hops)),
+                       "windows": len(windows),
+                       "parallelism": ("one GPU, partitioned path (P = 1)" if a.partitioned else "one GPU")
+                                      if world == 1 else
+                                      f"vertex-partitioned x{world} (Utils.getPartition), RCCL label records",
+                       "gen_ingest_s": round(gen_s, 1), "seal_s": round(seal_s, 1),
+                       "supersteps_per_view_mean": round(float(summ[..., 7].mean()), 2),
+                       "alive_edge_windows": s8d["alive_edge_windows"] if s8d else None,
+                       "alive_edge_windows_frac": (s8d["alive_edge_windows"] / (n_edges * len(windows) * len(hops)))
+                                                  if s8d else None},
+            "roofline": roofline,
+            "survey_8d_bytes": s8d,
+            "cpu_baseline": cpu,
+            "kernels": ks,
+            "check": {"views": int(summ.shape[0] * summ.shape[1]), "sum_biggest": int(summ[..., 0].sum()),
+                      "sum_total": int(summ[..., 1].sum()), "sum_members": int(summ[..., 5].sum())},
+            "secondary": secondary,
+        }
         print(json.dumps(out), flush=True)
     g.close()
     if dist is not None:
@@ -319,31 +487,11 @@ def run_c5(a, rank, world, local):
     g.close()
 
 
-def main():
-    a = parse()
-    if a.config == "c4":
-        rank, world, local = dist_env()
-        import torch
-        torch.cuda.set_device(local)
-        return run_c4(a, rank, world, local)
-    if a.config == "c5":
-        rank, world, local = dist_env()
-        import torch
-        torch.cuda.set_device(local)
-        return run_c5(a, rank, world, local)
-    if a.config == "diffusion":
-        rank, world, local = dist_env()
-        import torch
-        torch.cuda.set_device(local)
-        return run_diffusion(a, rank, world, local)
-    if a.config == "c3":
-        rank, world, local = dist_env()
-        import torch
-        torch.cuda.set_device(local)
-        return run_c3(a, rank, world, local)
-    rank, world, local = dist_env()
+def run_c2(a, rank, world, local, quiet=False):
+    """BASELINE configs[1] (C2): the RandomSpout-shaped 1M-update stream, 8,041 hourly hops x
+    {y,m,w,d,h}, CC.  N > 1: replicas (every rank holds the 30 MB graph and runs the grid offset
+    by r*jump/N: "weak").  quiet: return the line as the headline's secondary object."""
     import torch
-    torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -372,53 +520,61 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    if a.profile_only:
-        a.steps, a.warmup, a.no_cpu_baseline = 1, 0, True
-    for _ in range(a.warmup):
+    steps, warmup = (max(a.steps, 5), max(a.warmup, 2)) if quiet else (a.steps, a.warmup)
+    profile_only = a.profile_only and not quiet
+    for _ in range(0 if profile_only else warmup):
         g.run("cc", hops, windows)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(0 if a.profile_only else a.steps):
+    for _ in range(0 if profile_only else steps):
         g.run("cc", hops, windows)
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, dist, device="cuda")
-    ms_per_step = elapsed * 1e3 / a.steps
+    ms_per_step = elapsed * 1e3 / steps
     units = n_edges * len(windows) * len(hops) * world
     value = units / (ms_per_step / 1e3)
-    if a.profile_only:  # no timed steps: report the kernel profile only
+    if profile_only:  # no timed steps: report the kernel profile only
         ms_per_step = value = None
 
     # per-kernel timing (HIP events on the library's streams) over one more pass
     roofline = None
     kstats = {}
+    s8d = None
     if not a.no_profile_pass:
         g.run("cc", hops, windows, profile=True, serial=True)
-        ks = g.stats()["kernels"]
-        kstats = {k: v for k, v in ks.items() if v["launches"]}
-        dom = max(kstats, key=lambda k: kstats[k]["ms"])
-        d = kstats[dom]
+        kstats = kernel_table(g.stats())
+        kraw = g.stats()["kernels"]
+        d = kraw["cc_step"]
         gbs = d["bytes"] / (d["ms"] / 1e3) / 1e9
-        traffic, tsrc = pmc_traffic(dom)
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+        traffic, tsrc = pmc_traffic("k_cc_step2")
+        roofline = {"bound": "hbm", "kernel": "cc_step (k_cc_step2)", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "traffic_source": tsrc,
-                    "avg_launch_us": round(d["ms"] * 1e3 / d["launches"], 2),
+                    "traffic_source": tsrc, "avg_launch_us": round(d["ms"] * 1e3 / d["launches"], 2),
                     "algorithmic_bytes_per_launch": d["bytes"] / d["launches"]}
+        if not a.no_edge_counts:
+            g.run("cc", hops, windows, edge_counts=True)
+            s8d = survey_bytes(g.cc_summaries(), len(hops), windows, st["vertices"], st["edges"],
+                               st["vertex_events"] + st["edge_events"] + st["deaths"], kstats, d["launches"])
+            roofline["survey_8d"] = {"achieved": round(s8d["cc_step"]["achieved_GBps"], 1),
+                                     "frac": round(s8d["cc_step"]["achieved_GBps"] / HBM_PEAK_GBS, 4),
+                                     "bytes_per_launch": s8d["cc_step"]["bytes_per_launch"]}
 
     summ = g.cc_summaries()
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(stream, hops, windows, a.cpu_seconds, n_edges)
+        cpu = cpu_baseline(stream, hops, windows, a.cpu_seconds, n_edges,
+                           "the same C2 stream and query")
 
+    out = None
     if rank == 0:
         out = {
             "metric": "temporal edge-windows processed/sec for batched-window CC range query",
             "value": round(value, 1) if value is not None else None,
             "unit": "edge-windows/s",
             "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
+            "steps": steps,
+            "warmup": warmup,
             "ms_per_step": round(ms_per_step, 3) if ms_per_step is not None else None,
             "higher_is_better": True,
             "scaling": "weak",
@@ -430,19 +586,32 @@ def main():
                        "edge_entities": n_edges, "hops_per_gpu": int(len(hops)), "windows": len(windows),
                        "parallelism": f"replicas x{world} (hop grid sharded, no exchange)",
                        "seal_s": round(seal_s, 3),
-                       "supersteps_per_batch_mean": round(g.stats()["supersteps"] / max(1, g.stats()["batches"]), 2),
-                       "alive_edge_windows_frac": None},
+                       "supersteps_per_view_mean": round(float(summ[..., 7].mean()), 2),
+                       "alive_edge_windows": s8d["alive_edge_windows"] if s8d else None,
+                       "alive_edge_windows_frac": (s8d["alive_edge_windows"] / (n_edges * len(windows) * len(hops)))
+                                                  if s8d else None},
             "roofline": roofline,
+            "survey_8d_bytes": s8d,
             "cpu_baseline": cpu,
-            "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
-                            "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)} for k, v in kstats.items()},
+            "kernels": kstats,
             "check": {"views": int(summ.shape[0] * summ.shape[1]),
                       "sum_biggest": int(summ[..., 0].sum()), "sum_total": int(summ[..., 1].sum())},
         }
-        print(json.dumps(out))
+        if not quiet:
+            print(json.dumps(out))
     g.close()
     if dist is not None:
         dist.destroy_process_group()
+    return out
+
+
+def main():
+    a = parse()
+    rank, world, local = dist_env()
+    import torch
+    torch.cuda.set_device(local)
+    run = {"c2": run_c2, "c3": run_c3, "c4": run_c4, "c5": run_c5, "diffusion": run_diffusion}[a.config]
+    run(a, rank, world, local)
 
 
 if __name__ == "__main__":

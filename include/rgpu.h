@@ -92,6 +92,9 @@ typedef struct {
   int64_t seal_incremental, seal_delta_updates;
   /* last run, RGPU_RUN_EDGE_COUNTS: sum over its views of |E_{t,w}| (else -1) (ABI 6) */
   int64_t alive_edge_windows;
+  /* edge entities whose source vertex this partition owns: summed over the partitions, the
+     graph's edge entities (`edges` counts every edge kept here, SplitEdge copies included) */
+  int64_t edges_owned;
 } rgpu_stats_t;
 
 int rgpu_abi_version(void);

@@ -13,7 +13,6 @@
 #include <stdexcept>
 #include <vector>
 
-#include "kernels.hpp"
 
 namespace rgpu {
 namespace {
@@ -64,9 +63,6 @@ class RcclExchange : public Exchange {
   }
   void allreduce_u64(unsigned long long* d, size_t n, bool max, hipStream_t s) override {
     ncclchk(ncclAllReduce(d, d, n, ncclUint64, max ? ncclMax : ncclSum, comm_, s), "ncclAllReduce");
-  }
-  void reduce_scatter_i32(const int32_t* d_send, int32_t* d_recv, size_t count, hipStream_t s) override {
-    ncclchk(ncclReduceScatter(d_send, d_recv, count, ncclInt32, ncclSum, comm_, s), "ncclReduceScatter");
   }
 
  private:
@@ -170,17 +166,6 @@ class LocalExchange : public Exchange {
     g_->barrier();
     hipchk(hipMemcpyAsync(d, acc.data(), n * 8, hipMemcpyHostToDevice, s), "copy");
     hipchk(hipStreamSynchronize(s), "sync");
-  }
-  void reduce_scatter_i32(const int32_t* d_send, int32_t* d_recv, size_t count, hipStream_t s) override {
-    hipchk(hipStreamSynchronize(s), "sync");
-    g_->ptr[r_] = d_send;
-    g_->barrier();
-    hipchk(hipMemcpyAsync(d_recv, d_send + r_ * count, count * 4, hipMemcpyDeviceToDevice, s), "copy");
-    for (int q = 0; q < g_->n; q++)
-      if (q != r_) launch_add_i32(s, d_recv, (const int32_t*)g_->ptr[q] + r_ * count, (int64_t)count);
-    hipchk(hipGetLastError(), "add kernel");
-    hipchk(hipStreamSynchronize(s), "sync");
-    g_->barrier();
   }
 
  private:

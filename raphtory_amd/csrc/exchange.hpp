@@ -1,10 +1,10 @@
 // exchange.hpp — the collective layer of the vertex-partitioned mode.
 //
-// One partition per GPU.  Per superstep the partitions trade changed boundary label rows
-// (ncclSend/ncclRecv, grouped), agree on halting (the counts exchange carries each
-// partition's changed-vertex count: zero everywhere = every shard voted to halt,
-// AnalysisTask.scala:208-225), and merge component sizes once per batch
-// (ncclReduceScatter of the label histogram + ncclAllReduce of the summary fields).
+// One partition per GPU.  Per superstep the partitions trade label records of their changed
+// boundary vertices (ncclSend/ncclRecv, grouped) and agree on halting (the counts exchange
+// carries each partition's vote: nobody changed = every shard voted to halt,
+// AnalysisTask.scala:208-225); once per batch they route component counts to the label owners
+// (send/recv) and merge the summary fields (ncclAllReduce).
 //
 // Two implementations behind one interface (the loopback group is single-device: its
 // collectives read peers' buffers with device-local copies and kernels):
@@ -36,9 +36,6 @@ class Exchange {
                         const size_t* recv_bytes, hipStream_t s) = 0;
   // in place over n uint64 words
   virtual void allreduce_u64(unsigned long long* d, size_t n, bool max, hipStream_t s) = 0;
-  // d_recv[i] = sum over peers of d_send[rank*count + i]  (int32)
-  virtual void reduce_scatter_i32(const int32_t* d_send, int32_t* d_recv, size_t count,
-                                  hipStream_t s) = 0;
   // A new, independent channel over the same ranks (collective: every rank calls it in the same
   // order with the same tag).  Each batch slot of a partitioned run owns one, so that the
   // collectives of batches in flight on different streams never share an ordering (RCCL:

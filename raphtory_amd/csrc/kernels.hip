@@ -450,14 +450,18 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     }
     if (hv_of && hv_of[v] >= 0) {
       // heavy vertex: its segments were compacted by k_heavy_slots, which also left the
-      // superstep-1 minima of its neighbours' ranks in hbest; neighbours of a change are
-      // marked by k_heavy_mark.  (Heavy vertices exist only with one partition.)
-      const int32_t h = hv_of[v], me = (int32_t)v;
+      // superstep-1 minima of its neighbours' labels in hbest; neighbours of a change are
+      // marked by k_heavy_mark.  A heavy ghost (partitioned mode) only needs its kept count and
+      // mask OR here: its labels come from its owner.
+      const bool own = v < n_own;
+      const int32_t h = hv_of[v], me = grank ? grank[v] : (int32_t)v;
       const int32_t x = hbest[(int64_t)h * 64 + lane];
       hbest[(int64_t)h * 64 + lane] = INT32_MAX;
-      row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
-      const int32_t best = min(me, x);
-      row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+      const int32_t best = own ? min(me, x) : me;
+      if (own) {
+        row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
+        row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+      }
       uint64_t any = 0;
       unsigned long long kept = 0;
       for (int32_t k = hv_seg[h] + lane; k < hv_seg[h + 1]; k += 64) {
@@ -475,6 +479,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         chg1[v] = ch;
         if (ch) act2[v] = 1;
       }
+      if (!own) continue;
       changed += ch != 0;
       lanes |= ch;
       members += 1;
@@ -1043,7 +1048,7 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
                                                      const uint64_t* __restrict__ em,
                                                      int32_t* __restrict__ snbr, uint64_t* __restrict__ smask,
                                                      int32_t* __restrict__ segcnt, uint64_t* __restrict__ segor,
-                                                     int32_t* __restrict__ hbest) {
+                                                     int32_t* __restrict__ hbest, const int32_t* __restrict__ grank) {
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -1081,8 +1086,9 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
       }
       count += __popcll(bal);
       any |= m;
+      const int32_t lb = (grank && m) ? grank[nb] : nb;  // setup sends the neighbour's label (id)
 #pragma unroll
-      for (int j = 0; j < 64; j++) acc[j] = ((m >> j) & 1) ? min(acc[j], nb) : acc[j];
+      for (int j = 0; j < 64; j++) acc[j] = ((m >> j) & 1) ? min(acc[j], lb) : acc[j];
     }
     for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
     if (lane == 0) { segcnt[sg] = count; segor[sg] = any; }
@@ -1105,14 +1111,14 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       const uint64_t* __restrict__ chg_prev,
                                                       const uint8_t* __restrict__ act_cur,
                                                       const int32_t* __restrict__ stepflag,
-                                                      int32_t* __restrict__ hbest) {
+                                                      int32_t* __restrict__ hbest, int64_t n_own) {
   if (stepflag[step - 1] == 0) return;
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
-    if (!act_cur[v]) continue;
+    if (v >= n_own || !act_cur[v]) continue;  // ghosts are not visited (their owner computes them)
     const int32_t n = segcnt[sg];
     if (n == 0) continue;
     const int64_t base = seg_lo[sg];
@@ -1153,14 +1159,14 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
                                                     const uint64_t* __restrict__ chg_now,
                                                     const uint8_t* __restrict__ act_cur,
                                                     uint8_t* __restrict__ act_next,
-                                                    const int32_t* __restrict__ stepflag) {
+                                                    const int32_t* __restrict__ stepflag, int64_t n_own) {
   if (stepflag[step] == 0) return;
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
-    if (act_cur && !act_cur[v]) continue;
+    if (act_cur && v < n_own && !act_cur[v]) continue;  // a ghost's word is current (set by its records)
     const uint64_t ch = chg_now[v];
     if (!ch) continue;
     const int32_t n = segcnt[sg];
@@ -1400,12 +1406,13 @@ __global__ __launch_bounds__(256) void k_heavy_degree(int64_t nseg, const int32_
                                                       const uint64_t* __restrict__ vm,
                                                       const uint64_t* __restrict__ em,
                                                       int32_t* __restrict__ outdeg, int32_t* __restrict__ indeg,
-                                                      unsigned long long* __restrict__ stats) {
+                                                      unsigned long long* __restrict__ stats, int64_t n_own) {
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
+    if (v >= n_own) continue;  // a heavy ghost: its owner counts it
     const uint64_t mv = vm[v];
     if (mv == 0) continue;
     const int64_t rel0 = seg_lo[sg] - adj_off[v], o0 = out_off[v], i0 = in_off[v];
@@ -1451,12 +1458,13 @@ __global__ __launch_bounds__(256) void k_heavy_pr(int64_t nseg, const int32_t* _
                                                   const uint64_t* __restrict__ vm,
                                                   const uint64_t* __restrict__ em,
                                                   const double* __restrict__ contrib_cur,
-                                                  double* __restrict__ hacc) {
+                                                  double* __restrict__ hacc, int64_t n_own) {
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
+    if (v >= n_own) continue;  // a heavy ghost: its owner pulls it
     const uint64_t mv = vm[v];
     if (mv == 0) continue;
     const int64_t rel0 = seg_lo[sg] - adj_off[v], i0 = in_off[v];
@@ -1626,99 +1634,7 @@ __global__ __launch_bounds__(256) void k_pr_step(int64_t nv, const int64_t* __re
   }
 }
 
-// ---------------------------------------------------------------- partition exchange
-// (host side in rgpu.cpp run_partitioned).  Send list entries are owned
-// ranks grouped by peer (xs_off); a record is 68 words: [0] entry index in the peer's list,
-// [2..3] the step's change word, [4..67] the label row.  A boundary vertex is sent when it
-// was visited in the step and changed now or in the previous step — exactly when its own
-// superstep kernel rewrote its row — so the peer's ghost rows track both label buffers.
-
-__global__ __launch_bounds__(256) void k_xpack_cc(int64_t nx, const int32_t* __restrict__ xv,
-                                                  const int32_t* __restrict__ xq,
-                                                  const int64_t* __restrict__ xoff,
-                                                  const uint8_t* __restrict__ act,
-                                                  const uint64_t* __restrict__ vm,
-                                                  const uint64_t* __restrict__ chg_now,
-                                                  const uint64_t* __restrict__ chg_prev,
-                                                  const int32_t* __restrict__ lab,
-                                                  int32_t* __restrict__ sbuf,
-                                                  int32_t* __restrict__ scnt) {
-  const int lane = lane_id();
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t c = wave; c * 64 < nx; c += nwaves) {
-    const int64_t e = c * 64 + lane;
-    const bool ok = e < nx;
-    const int32_t v = ok ? xv[e] : 0;
-    const int32_t q = ok ? xq[e] : -1;
-    bool want = ok && vm[v] != 0 && (act == nullptr || act[v] != 0);
-    const uint64_t ch = ok ? chg_now[v] : 0;
-    if (want) want = (ch | (chg_prev ? chg_prev[v] : 0ull)) != 0;
-    const uint64_t todo = __ballot(want);
-    if (!todo) continue;
-    int64_t rec = 0;
-    uint64_t rem = todo;
-    while (rem) {  // reserve record slots, one atomic per (wave, peer)
-      const int leader = __builtin_ctzll(rem);
-      const int32_t Q = __builtin_amdgcn_readlane(q, leader);
-      const uint64_t same = __ballot(want && q == Q);
-      int32_t base = 0;
-      if (lane == leader) base = atomicAdd(&scnt[Q], __popcll(same));
-      base = __builtin_amdgcn_readlane(base, leader);
-      if (want && q == Q) rec = xoff[Q] + base + __popcll(same & lanemask_lt());
-      rem &= ~same;
-    }
-    uint64_t b = todo;
-    while (b) {
-      const int L = __builtin_ctzll(b);
-      b &= b - 1;
-      const int32_t vL = __builtin_amdgcn_readlane(v, L);
-      const int32_t qL = __builtin_amdgcn_readlane(q, L);
-      const int64_t rL = (int64_t)readlane64((uint64_t)rec, L);
-      const uint64_t chL = readlane64(ch, L);
-      int32_t* r = sbuf + rL * kXRecWords;
-      r[4 + lane] = lab[(int64_t)vL * 64 + lane];
-      if (lane == 0) {
-        r[0] = (int32_t)(c * 64 + L - xoff[qL]);
-        r[1] = 0;
-        r[2] = (int32_t)(uint32_t)chL;
-        r[3] = (int32_t)(uint32_t)(chL >> 32);
-      }
-    }
-  }
-}
-
-// Records from one peer: ghost row + change word, and the ghost's owned neighbours that
-// share a view with the change join the next frontier (as a local change would do).
-__global__ __launch_bounds__(256) void k_xunpack_cc(int64_t nrec, const int32_t* __restrict__ rbuf,
-                                                    const int32_t* __restrict__ xrl,
-                                                    const int64_t* __restrict__ adj_off,
-                                                    const int32_t* __restrict__ cnt,
-                                                    const int32_t* __restrict__ snbr,
-                                                    const uint64_t* __restrict__ smask,
-                                                    int32_t* __restrict__ lab,
-                                                    uint64_t* __restrict__ chg,
-                                                    uint8_t* __restrict__ act_next) {
-  const int lane = lane_id();
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t k = wave; k < nrec; k += nwaves) {
-    const int32_t* r = rbuf + k * kXRecWords;
-    const int32_t g = xrl[r[0]];
-    const uint64_t ch = (uint64_t)(uint32_t)r[2] | ((uint64_t)(uint32_t)r[3] << 32);
-    lab[(int64_t)g * 64 + lane] = r[4 + lane];
-    if (lane == 0) chg[g] = ch;
-    if (ch) {
-      const int32_t n = cnt[g];
-      const int64_t base = adj_off[g];
-      for (int32_t c = 0; c < n; c += 64) {
-        const int32_t j = c + lane;
-        if (j < n && (smask[base + j] & ch)) act_next[snbr[base + j]] = 1;
-      }
-    }
-  }
-}
-
+// ---------------------------------------------------------------- partitioned PageRank
 // fp64 rows (PageRank contributions) of a whole list: gather into / scatter out of a
 // contiguous buffer, one wave per entry
 __global__ __launch_bounds__(256) void k_xgather_f64(int64_t n, const int32_t* __restrict__ xv,
@@ -1736,60 +1652,6 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t k = wave; k < n; k += nwaves) rows[(int64_t)xv[k] * 64 + lane] = buf[k * 64 + lane];
-}
-
-__global__ __launch_bounds__(256) void k_add_i32(int32_t* __restrict__ dst, const int32_t* __restrict__ src,
-                                                 int64_t n) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    dst[i] += src[i];
-}
-
-// Summary over this partition's slice [x0, x0+len) of the reduce-scattered view-major
-// histogram (stride ng per view): blockIdx.y = view.
-__global__ __launch_bounds__(256) void k_cc_summary_rs(const int32_t* __restrict__ chunk, int64_t x0,
-                                                       int64_t len, int64_t ng,
-                                                       unsigned long long* __restrict__ stats,
-                                                       unsigned int* __restrict__ iso) {
-  __shared__ unsigned long long red[6][4];
-  const int j = blockIdx.y;
-  if (blockIdx.x == 0) fold_iso(iso, j, stats);
-  const int64_t lo = x0 > (int64_t)j * ng ? x0 : (int64_t)j * ng;
-  const int64_t hi = (x0 + len) < (int64_t)(j + 1) * ng ? (x0 + len) : (int64_t)(j + 1) * ng;
-  unsigned long long big = 0, tot = 0, nis = 0, gt2 = 0, sum = 0, snis = 0;
-  for (int64_t r = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < hi;
-       r += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t c = chunk[r - x0];
-    if (c) {
-      const unsigned long long uc = (unsigned long long)c;
-      big = uc > big ? uc : big;
-      tot += 1;
-      nis += c > 1;
-      gt2 += c > 2;
-      sum += uc;
-      snis += c > 1 ? uc : 0;
-    }
-  }
-  unsigned long long v[6] = {big, tot, nis, gt2, sum, snis};
-#pragma unroll
-  for (int f = 0; f < 6; f++) {
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long x = __shfl_xor(v[f], o);
-      v[f] = f == 0 ? (x > v[f] ? x : v[f]) : v[f] + x;
-    }
-  }
-  const int lane = lane_id(), wib = threadIdx.x >> 6;
-  if (lane == 0)
-    for (int f = 0; f < 6; f++) red[f][wib] = v[f];
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    const int f = threadIdx.x;
-    unsigned long long a = red[f][0];
-    for (int w = 1; w < 4; w++) a = f == 0 ? (red[f][w] > a ? red[f][w] : a) : a + red[f][w];
-    if (a) {
-      if (f == 0) atomicMax(&stats[j], a);
-      else atomicAdd(&stats[f * 64 + j], a);
-    }
-  }
 }
 
 // ---------------------------------------------------------------- launchers
@@ -1864,7 +1726,7 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, co
   if (g.n_seg <= 0) return;
   k_heavy_slots<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off,
                                                             g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
-                                                            snbr, smask, hb.segcnt, hb.segor, hb.best);
+                                                            snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank);
 }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
@@ -1872,14 +1734,14 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
   if (g.n_seg <= 0) return;
   k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
-                                                             hb.best);
+                                                             hb.best, g.n_own);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
                        const HeavyBuf& hb, const uint8_t* act_cur) {
   if (g.n_seg <= 0) return;
   k_heavy_mark<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
-                                                           chg_now, act_cur, act_next, stepflag);
+                                                           chg_now, act_cur, act_next, stepflag, g.n_own);
 }
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,
@@ -1911,7 +1773,7 @@ void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const u
   if (g.n_seg > 0)
     k_heavy_degree<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_lo, g.seg_n, g.out_off,
                                                                g.in_off, g.adj_off, g.in_eid, vm, em, outdeg, indeg,
-                                                               stats);
+                                                               stats, g.nv);
 }
 void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      const int32_t* outdeg, int32_t* cnt, int32_t* snbr, uint64_t* smask,
@@ -1926,39 +1788,17 @@ void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const 
   if (g.n_seg > 0 && hacc)
     k_heavy_pr<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off,
                                                            g.in_off, g.adj_off, g.in_eid, g.esrc, vm, em, contrib_cur,
-                                                           hacc);
+                                                           hacc, g.nv);
   k_pr_step<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.in_off, vm, outdeg, cnt, snbr, smask,
                                                contrib_cur, contrib_next, pr,
                                                g.n_seg > 0 && hacc ? g.hv_of : nullptr, hacc);
 }
 
-void launch_xpack_cc(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
-                     const uint8_t* act, const uint64_t* vm, const uint64_t* chg_now,
-                     const uint64_t* chg_prev, const int32_t* lab, int32_t* sbuf, int32_t* scnt) {
-  if (nx <= 0) return;
-  k_xpack_cc<<<grid_for(nx, 4 * 64, 2048), 256, 0, s>>>(nx, xv, xq, xoff, act, vm, chg_now, chg_prev, lab,
-                                                         sbuf, scnt);
-}
-void launch_xunpack_cc(hipStream_t s, int64_t nrec, const int32_t* rbuf, const int32_t* xrl,
-                       const DevGraph& g, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
-                       int32_t* lab, uint64_t* chg, uint8_t* act_next) {
-  if (nrec <= 0) return;
-  k_xunpack_cc<<<grid_for(nrec, 4, 4096), 256, 0, s>>>(nrec, rbuf, xrl, g.adj_off, cnt, snbr, smask, lab, chg,
-                                                        act_next);
-}
 void launch_xgather_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* rows, double* buf) {
   if (n > 0) k_xgather_f64<<<grid_for(n, 4, 4096), 256, 0, s>>>(n, xv, rows, buf);
 }
 void launch_xscatter_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* buf, double* rows) {
   if (n > 0) k_xscatter_f64<<<grid_for(n, 4, 4096), 256, 0, s>>>(n, xv, buf, rows);
-}
-void launch_add_i32(hipStream_t s, int32_t* dst, const int32_t* src, int64_t n) {
-  if (n > 0) k_add_i32<<<grid_for(n, 256, 4096), 256, 0, s>>>(dst, src, n);
-}
-void launch_cc_summary_rs(hipStream_t s, int nviews, const int32_t* chunk, int64_t x0, int64_t len,
-                          int64_t ng, unsigned long long* stats, unsigned int* iso) {
-  dim3 grid(grid_for(ng, 256, 32), (unsigned)nviews);
-  k_cc_summary_rs<<<grid, 256, 0, s>>>(chunk, x0, len, ng, stats, iso);
 }
 
 }  // namespace rgpu

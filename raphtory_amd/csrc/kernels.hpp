@@ -147,19 +147,49 @@ void launch_diff_step(hipStream_t s, int step, const DevGraph& g, const int64_t*
                       const DiffSalts& salts, int coin, int32_t* stepflag, int32_t* hostflag,
                       unsigned long long* stats);
 
-// partition exchange (vertex-partitioned mode)
-constexpr int kXRecWords = 68;  // ints per boundary-row record
-void launch_xpack_cc(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
-                     const uint8_t* act, const uint64_t* vm, const uint64_t* chg_now,
-                     const uint64_t* chg_prev, const int32_t* lab, int32_t* sbuf, int32_t* scnt);
-void launch_xunpack_cc(hipStream_t s, int64_t nrec, const int32_t* rbuf, const int32_t* xrl,
-                       const DevGraph& g, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
-                       int32_t* lab, uint64_t* chg, uint8_t* act_next);
+// ---- vertex-partitioned mode (xchg.hip; host: rgpu.cpp).  Up to kMaxParts partitions.
+constexpr int kMaxParts = 8;
+// a label record: the new label `val` of boundary entry `e` (index in the sender's list for
+// the receiver) in the views `mask`
+struct XRec {
+  int32_t e;
+  int32_t val;
+  uint64_t mask;
+};
+// per-peer layout of a record buffer (by value in kernel arguments)
+struct XPeers {
+  int np = 1, me = 0;
+  int64_t base[kMaxParts] = {};     // first record of peer q's region
+  int64_t cap[kMaxParts] = {};      // records that fit in it (send side)
+  int64_t pre[kMaxParts + 1] = {};  // receive side: prefix of the records received per peer
+  int64_t xoff[kMaxParts + 1] = {}; // first entry of peer q in the send / receive list
+};
+void launch_xvm_pack(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff, int planes,
+                     const uint64_t* vm, int64_t vstride, uint64_t* out);
+void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
+                       int planes, const uint64_t* in, uint64_t* vm, int64_t vstride);
+void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t* xv, const int32_t* xq,
+                      const uint8_t* act, const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab,
+                      XRec* sbuf, unsigned long long* scnt);
+void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa);
+void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg);
+void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
+                        uint64_t* chg);
+void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
+                  const DevGraph& g, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
+                  uint8_t* act_next);
+unsigned hist_route_grid(int64_t n_own);
+void launch_hist_route(hipStream_t s, int pass, const XPeers& P, int64_t n_own, int nviews, const int64_t* vid,
+                       const uint64_t* vm, const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso,
+                       int64_t* blkcnt, const int64_t* blkoff, unsigned long long* hsbuf);
+void launch_blk_scan(hipStream_t s, int np, int64_t nb, const int64_t* blkcnt, int64_t* blkoff,
+                     unsigned long long* tot);
+void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const int64_t* vid,
+                      int64_t n_own, int32_t* hist);
+// PageRank contribution rows of a list (partitioned PageRank): gather into / scatter out of a
+// contiguous buffer
 void launch_xgather_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* rows, double* buf);
 void launch_xscatter_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* buf, double* rows);
-void launch_add_i32(hipStream_t s, int32_t* dst, const int32_t* src, int64_t n);
-void launch_cc_summary_rs(hipStream_t s, int nviews, const int32_t* chunk, int64_t x0, int64_t len,
-                          int64_t ng, unsigned long long* stats, unsigned int* iso);
 
 // incremental seal (merge.hip): a sealed base graph and a host-packed delta (rgpu_internal.hpp
 // Delta), all device pointers

@@ -505,6 +505,8 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
   P.n_vkey = (int64_t)P.vkey.size();
   P.n_ekey = (int64_t)P.ekey.size();
   P.n_in = P.in_off[P.nv];
+  P.ne_owned = 0;
+  for (int64_t e = 0; e < P.ne; e++) P.ne_owned += P.esrc[e] < n_own;
   return "";
 }
 

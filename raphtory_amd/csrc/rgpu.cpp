@@ -103,20 +103,39 @@ struct Retained {  // per batch, RGPU_RUN_RETAIN
   std::vector<uint8_t> st;    // diffusion: infection superstep per (vertex, lane), 0xFF = none
 };
 
-// device state of the vertex-partitioned mode (one partition per GPU)
+// Vertex-partitioned mode (one partition per GPU; kernels: xchg.hip).
+// Per batch slot: its own exchange channel, record buffers and counts staging.
+struct XSlot {
+  Exchange* x = nullptr;                  // this slot's channel (a fork of the ctx's)
+  XRec* sbuf = nullptr;                   // label records to send, one region per peer
+  XRec* rbuf[2] = {nullptr, nullptr};     // received, per superstep parity
+  int64_t scap[kMaxParts] = {}, rcap[kMaxParts] = {};
+  int64_t rcnt[2][kMaxParts] = {};        // records received per parity (their ghosts' change
+                                          // words are cleared two supersteps later)
+  unsigned long long* scnt = nullptr;     // [kMaxParts] records per peer of the pack in flight
+  int64_t* xab = nullptr;                 // [4P] counts words: sent (xa) | received (xb)
+  int64_t* h_xab = nullptr;               // pinned copy
+  uint64_t *vms = nullptr, *vmr = nullptr;  // ghost membership words (planes x list)
+  int vm_planes = 0;
+  int64_t* blkcnt = nullptr;              // component counts: records per (peer, block)
+  int64_t* blkoff = nullptr;
+  unsigned long long* htot = nullptr;     // [kMaxParts]
+  unsigned long long *hsbuf = nullptr, *hrbuf = nullptr;
+  int64_t hscap[kMaxParts] = {}, hrcap[kMaxParts] = {};
+  int r = 0;                              // superstep whose counts exchange is in flight
+  int64_t hrcnt[kMaxParts] = {};
+  double bytes = 0;                       // record bytes sent by this slot
+};
 struct Part {
-  Exchange* xchg = nullptr;
-  int64_t nxs = 0, nxr = 0, ng = 0, hist_total = 0;
+  Exchange* xchg = nullptr;                   // the ctx's channel (rgpu_exchange_init)
+  int64_t nxs = 0, nxr = 0;
   std::vector<int64_t> xs_off, xr_off;        // host copies of the plan offsets
-  int32_t *xs_v = nullptr, *xs_q = nullptr, *xr_v = nullptr;
-  int64_t* xs_off_d = nullptr;
-  int32_t *sbuf = nullptr, *rbuf = nullptr;   // CC boundary-row records
+  int32_t *xs_v = nullptr, *xs_q = nullptr, *xr_v = nullptr, *xr_q = nullptr;
+  int64_t *xs_off_d = nullptr, *xr_off_d = nullptr;
+  int64_t* vid_own = nullptr;                 // owned ids ascending (label owner -> owned rank)
   double *sbuf_f = nullptr, *rbuf_f = nullptr;  // PR contribution rows
-  int32_t *scnt = nullptr, *hist = nullptr, *chunk = nullptr;
-  int64_t *xa = nullptr, *xb = nullptr;       // [P][2] counts exchange (device)
-  int64_t* h_x = nullptr;                     // pinned host staging [2P]
-  int32_t* h_scnt = nullptr;                  // pinned [P + 1]
-  bool cc_ready = false, pr_ready = false;
+  bool pr_ready = false;
+  XSlot xs[4];                                // per batch slot (kMaxSlots)
   double bytes_sent = 0;
 };
 
@@ -217,17 +236,20 @@ T* dupload(std::vector<void*>& list, const std::vector<T>& h) {
 }
 
 void release_slots(rgpu_ctx* c);
+void free_part_slots(rgpu_ctx* c, bool keep_channels);
 void free_graph(rgpu_ctx* c) {
   for (void* p : c->graph_allocs) (void)hipFree(p);
   c->graph_allocs.clear();
   release_slots(c);
   c->g = DevGraph();
-  if (c->pt.h_x) (void)hipHostFree(c->pt.h_x);
-  if (c->pt.h_scnt) (void)hipHostFree(c->pt.h_scnt);
+  free_part_slots(c, true);  // the channels (communicators) outlive a re-seal
   {
     Exchange* x = c->pt.xchg;
+    XSlot xs[4];
+    for (int i = 0; i < 4; i++) xs[i].x = c->pt.xs[i].x;
     c->pt = Part();
-    c->pt.xchg = x;  // the communicator outlives a re-seal
+    c->pt.xchg = x;
+    for (int i = 0; i < 4; i++) c->pt.xs[i].x = xs[i].x;
   }
 }
 
@@ -382,29 +404,11 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       s.psmask = dalloc<uint64_t>(L, nin + nv);
     }
   }
-  if (c->partitioned) {
+  if (c->partitioned && algo == RGPU_ALGO_PR && !c->pt.pr_ready) {
     Part& X = c->pt;
-    const int P = c->nparts;
-    if (!X.h_x) {
-      HIPCHK(hipHostMalloc((void**)&X.h_x, sizeof(int64_t) * 2 * P));
-      HIPCHK(hipHostMalloc((void**)&X.h_scnt, sizeof(int32_t) * (P + 1)));
-      X.scnt = dalloc<int32_t>(LG, P);
-      X.xa = dalloc<int64_t>(LG, 2 * P);
-      X.xb = dalloc<int64_t>(LG, 2 * P);
-    }
-    if (algo == RGPU_ALGO_CC && !X.cc_ready) {
-      X.sbuf = dalloc<int32_t>(LG, (size_t)X.nxs * kXRecWords);
-      X.rbuf = dalloc<int32_t>(LG, (size_t)X.nxr * kXRecWords);
-      X.hist_total = ((int64_t)kViews * X.ng + P - 1) / P * P;
-      X.hist = dalloc<int32_t>(LG, X.hist_total);
-      X.chunk = dalloc<int32_t>(LG, X.hist_total / P);
-      X.cc_ready = true;
-    }
-    if (algo == RGPU_ALGO_PR && !X.pr_ready) {
-      X.sbuf_f = dalloc<double>(LG, (size_t)X.nxs * kViews);
-      X.rbuf_f = dalloc<double>(LG, (size_t)X.nxr * kViews);
-      X.pr_ready = true;
-    }
+    X.sbuf_f = dalloc<double>(LG, (size_t)std::max<int64_t>(X.nxs, 1) * kViews);
+    X.rbuf_f = dalloc<double>(LG, (size_t)std::max<int64_t>(X.nxr, 1) * kViews);
+    X.pr_ready = true;
   }
   for (int i = 0; i < nuse; i++) {
     Slot& s = c->slot[i];
@@ -525,20 +529,10 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
   s.phase = 1;
 }
 
-void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
+// the end of every batch: per-view stats and retained rows to the host, the mask set released
+void finish_tail(rgpu_ctx* c, int si, const RunCfg& rc) {
   Slot& s = c->slot[si];
   const DevGraph& g = c->g;
-  if (rc.algo == RGPU_ALGO_CC) {
-    const int32_t* lab = s.lab[s.r_final & 1];
-    // the other label buffer is free now: it becomes the view-major histogram (keeps the
-    // batch's working set inside the Infinity Cache with several batches in flight)
-    int32_t* hist = s.lab[(s.r_final + 1) & 1];
-    HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)g.nv * kViews, s.stream));
-    const int nviews = rc.K * rc.gsize;
-    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g.nv, g.nv, nviews, s.vm, s.vadj, lab, hist, s.iso); });
-    timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * nviews,
-                 [&] { launch_cc_summary(s.stream, g, nviews, hist, s.stats, s.iso); });
-  }
   if (rc.algo == RGPU_ALGO_CC) launch_lane_fold(s.stream, s.stats + kLaneOff, s.stats + kFoldOff);
   HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatCopy,
                         hipMemcpyDeviceToHost, s.stream));
@@ -573,6 +567,27 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
   s.evseq = ++c->evcounter;
   s.phase = 2;
 }
+
+void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
+  Slot& s = c->slot[si];
+  const DevGraph& g = c->g;
+  if (rc.algo == RGPU_ALGO_CC) {
+    const int32_t* lab = s.lab[s.r_final & 1];
+    // the other label buffer is free now: it becomes the view-major histogram (keeps the
+    // batch's working set inside the Infinity Cache with several batches in flight)
+    int32_t* hist = s.lab[(s.r_final + 1) & 1];
+    HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)g.nv * kViews, s.stream));
+    const int nviews = rc.K * rc.gsize;
+    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g.nv, g.nv, nviews, s.vm, s.vadj, lab, hist, s.iso); });
+    timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * nviews,
+                 [&] { launch_cc_summary(s.stream, g, nviews, hist, s.stats, s.iso); });
+  }
+  finish_tail(c, si, rc);
+}
+
+void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r);
+void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc);
+void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int planes);
 
 // Batch b = hop block b / G (hops [hb*K, hb*K + K)) x window group b % G.  Hop-major runs
 // (G = 1): the batch is the block, all windows in one label row, K1 per batch into the slot's
@@ -621,12 +636,17 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     HIPCHK(hipMemsetAsync(s.work, 0, sizeof(unsigned long long) * kWorkWords, s.stream));
   const double bm = bytes_mask(g);
   const double bv = 8.0 * (g.nv + 1) + 8.0 * c->pk.n_vkey, be = bm - (16.0 * g.nv + 8.0) - 8.0 * g.ne + 8.0 * c->pk.n_ekey;
+  // partitioned: K1 computes the owned vertices' masks (a ghost's history is its owner's);
+  // the ghosts' words arrive from their owners right after
+  DevGraph gk = g;
+  if (c->partitioned) gk.nv = c->pk.n_own;
   if (rc.G == 1) {
     s.vm = s.vm_own;
     s.em = s.em_own;
-    timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv, [&] { launch_vertex_mask(s.stream, g, bp, s.vm, 0, false, clr); });
+    timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv, [&] { launch_vertex_mask(s.stream, gk, bp, s.vm, 0, false, clr); });
     timed_launch(c, si, KID_MASK, be + 8.0 * g.ne,
                  [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0); });
+    if (c->partitioned) part_vm_exchange(c, si, s.vm, 0, 1);
   } else {
     MaskSet& M = c->mset[hb % kMaskSets];
     if (grp == 0) {
@@ -634,9 +654,10 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       for (int w = 0; w < rc.G; w++) HIPCHK(hipStreamWaitEvent(s.stream, M.done[w], 0));
       const BatchClear none;
       timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv * rc.W,
-                   [&] { launch_vertex_mask(s.stream, g, bp, M.vm, g.nv + kPad, true, none); });
+                   [&] { launch_vertex_mask(s.stream, gk, bp, M.vm, g.nv + kPad, true, none); });
       timed_launch(c, si, KID_MASK, be + 8.0 * g.ne * rc.W,
                    [&] { launch_edge_mask(s.stream, g, bp, M.em, true, c->d_ecnt, (int64_t)h0); });
+      if (c->partitioned) part_vm_exchange(c, si, M.vm, g.nv + kPad, rc.G);
       HIPCHK(hipEventRecord(M.k1, s.stream));
       M.pending = rc.G;
     } else {
@@ -681,11 +702,17 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                       c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff);
     });
-    if (g.n_seg > 0)
+    if (g.n_seg > 0 && !c->partitioned)  // partitioned: after the step's records are in
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[1], s.act[2], s.stepcnt, 1, s.hv, nullptr);
       });
     s.r_launched = 1;  // superstep 1 ran inside the slot kernel
+    if (c->partitioned) {
+      s.r_final = 0;
+      if (rc.max_steps <= 1) part_finish_begin(c, si, rc);
+      else part_post_step(c, si, rc, 1);
+      return;
+    }
     if (rc.max_steps <= 1) {  // AnalysisTask.timeResponse :169: no Setup when maxSteps <= 1
       s.r_final = 0;
       finish_batch(c, si, rc);
@@ -856,65 +883,371 @@ int run_impl(rgpu_ctx* c, RunCfg& rc) {
 
 
 // ------------------------------------------------------------------ vertex-partitioned runs
-// One batch at a time on slot 0, the host driving every superstep: the halting vote is
-// global (a ghost that changed on another GPU wakes local vertices), so each step ends in
-// the counts exchange.  Per superstep r (AnalysisTask.syncMessages/endStep,
-// AnalysisTask.scala:190-225, with the ReaderWorker message traffic replaced by rows):
-//   pack changed boundary rows -> all-to-all [rows for q, my changed flag] -> if anyone
-//   changed: grouped send/recv of the rows -> unpack into ghost rows + next frontier.
+// One partition per GPU; kernels in xchg.hip.  A CC batch is the one-GPU
+// batch with an exchange after every superstep r (AnalysisTask.syncMessages / endStep,
+// AnalysisTask.scala:190-225, with ReaderWorker's vertex-message traffic replaced by records):
+//   pack the records of the boundary vertices that changed -> counts all-to-all (records per
+//   peer + the partition's halting vote) -> [host] -> clear the ghost change words of step r-2
+//   -> grouped send/recv of the records -> ghost rows, ghost change words, next frontier ->
+//   superstep r+1 -> ...
+// The host reads the counts once per superstep per batch: up to three batches are in flight,
+// each on its own stream and exchange channel, and the host serves the slots in a fixed round
+// robin so that every partition issues each channel's collectives in the same order.
 DevGraph owned_view(const rgpu_ctx* c) {
   DevGraph g = c->g;
   g.nv = c->pk.n_own;  // kernels that compute per-vertex results visit owned ranks only
   return g;
 }
 
-// returns the number of partitions' vertices that changed in step r (0 = global halt)
-int64_t cc_exchange(rgpu_ctx* c, int r) {
-  Slot& s = c->slot[0];
-  Part& X = c->pt;
-  const int P = c->nparts, me = c->part;
-  HIPCHK(hipMemsetAsync(X.scnt, 0, sizeof(int32_t) * P, s.stream));
-  launch_xpack_cc(s.stream, X.nxs, X.xs_v, X.xs_q, X.xs_off_d, r == 1 ? nullptr : s.act[r % 3], s.vm,
-                  s.chg[r & 1], r == 1 ? nullptr : s.chg[(r - 1) & 1], s.lab[r & 1], X.sbuf, X.scnt);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(X.h_scnt, X.scnt, sizeof(int32_t) * P, hipMemcpyDeviceToHost, s.stream));
-  HIPCHK(hipMemcpyAsync(X.h_scnt + P, s.stepcnt + r, sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
-  HIPCHK(hipStreamSynchronize(s.stream));
-  for (int q = 0; q < P; q++) {
-    X.h_x[2 * q] = q == me ? 0 : X.h_scnt[q];
-    X.h_x[2 * q + 1] = X.h_scnt[P] != 0;
+// record buffers grow on demand (the counts are known before anything is written into them);
+// RGPU_XREC_SLACK / RGPU_XREC_INIT (records of headroom per peer / first-guess records per
+// boundary entry) exist so that tests can force the growth paths
+int g_xrec_slack = 1024, g_xrec_init = 2;
+template <class T>
+void grow_regions(T** buf, int64_t* cap, const int64_t* need, int np, hipStream_t s) {
+  bool grow = *buf == nullptr;
+  for (int q = 0; q < np; q++) grow |= need[q] > cap[q];
+  if (!grow) return;
+  HIPCHK(hipStreamSynchronize(s));
+  if (*buf) HIPCHK(hipFree(*buf));
+  *buf = nullptr;
+  int64_t tot = 0;
+  for (int q = 0; q < np; q++) {
+    cap[q] = std::max(cap[q], need[q] + need[q] / 2 + g_xrec_slack);
+    tot += cap[q];
   }
-  HIPCHK(hipMemcpyAsync(X.xa, X.h_x, sizeof(int64_t) * 2 * P, hipMemcpyHostToDevice, s.stream));
-  X.xchg->alltoall_i64(X.xa, X.xb, 2, s.stream);
-  std::vector<int64_t> sent(X.h_x, X.h_x + 2 * P);
-  HIPCHK(hipMemcpyAsync(X.h_x, X.xb, sizeof(int64_t) * 2 * P, hipMemcpyDeviceToHost, s.stream));
-  HIPCHK(hipStreamSynchronize(s.stream));
-  int64_t changed = 0;
-  for (int q = 0; q < P; q++) changed += X.h_x[2 * q + 1];
-  if (!changed) return 0;
+  HIPCHK(hipMalloc((void**)buf, sizeof(T) * (size_t)tot));
+}
+
+template <class T>
+T* alloc_regions(const int64_t* cap, int np) {
+  int64_t tot = 0;
+  for (int q = 0; q < np; q++) tot += cap[q];
+  T* p = nullptr;
+  HIPCHK(hipMalloc((void**)&p, sizeof(T) * (size_t)std::max<int64_t>(tot, 1)));
+  return p;
+}
+
+XPeers peers_layout(const rgpu_ctx* c, const int64_t* cap, const std::vector<int64_t>& xoff, const int64_t* cnt) {
+  XPeers L;
+  L.np = c->nparts;
+  L.me = c->part;
+  int64_t o = 0, p = 0;
+  for (int q = 0; q < c->nparts; q++) {
+    L.base[q] = o;
+    L.cap[q] = cap[q];
+    o += cap[q];
+    L.pre[q] = p;
+    p += cnt ? (q == c->part ? 0 : cnt[q]) : 0;
+    L.xoff[q] = xoff[q];
+  }
+  L.pre[c->nparts] = p;
+  L.xoff[c->nparts] = xoff[c->nparts];
+  return L;
+}
+
+void free_part_slots(rgpu_ctx* c, bool keep_channels) {
+  for (XSlot& xs : c->pt.xs) {
+    for (void* p : {(void*)xs.sbuf, (void*)xs.rbuf[0], (void*)xs.rbuf[1], (void*)xs.hsbuf, (void*)xs.hrbuf})
+      if (p) (void)hipFree(p);
+    if (xs.h_xab) (void)hipHostFree(xs.h_xab);
+    Exchange* x = xs.x;
+    if (!keep_channels) delete x;
+    xs = XSlot();
+    if (keep_channels) xs.x = x;
+  }
+}
+
+void ensure_part(rgpu_ctx* c, int nuse, int planes) {
+  Part& X = c->pt;
+  const int P = c->nparts;
+  auto& LG = c->graph_allocs;
+  for (int i = 0; i < nuse; i++) {
+    XSlot& xs = X.xs[i];
+    if (!xs.x) xs.x = X.xchg->fork(i + 1);  // collective: every partition forks the same slots
+    if (!xs.scnt) {
+      xs.scnt = dalloc<unsigned long long>(LG, kMaxParts);
+      HIPCHK(hipMemset(xs.scnt, 0, sizeof(unsigned long long) * kMaxParts));
+      xs.htot = dalloc<unsigned long long>(LG, kMaxParts);
+      HIPCHK(hipMemset(xs.htot, 0, sizeof(unsigned long long) * kMaxParts));
+      xs.xab = dalloc<int64_t>(LG, 4 * P);
+      HIPCHK(hipHostMalloc((void**)&xs.h_xab, sizeof(int64_t) * 4 * P));
+      const int64_t nb = hist_route_grid(c->pk.n_own);
+      xs.blkcnt = dalloc<int64_t>(LG, (size_t)kMaxParts * nb);
+      xs.blkoff = dalloc<int64_t>(LG, (size_t)kMaxParts * nb);
+    }
+    if (xs.vm_planes < planes) {
+      xs.vms = dalloc<uint64_t>(LG, (size_t)planes * std::max<int64_t>(X.nxs, 1));
+      xs.vmr = dalloc<uint64_t>(LG, (size_t)planes * std::max<int64_t>(X.nxr, 1));
+      xs.vm_planes = planes;
+    }
+    if (!xs.sbuf) {  // first guess: two records per boundary entry (both receive parities
+                     // share one layout, xs.rcap)
+      int64_t ns[kMaxParts] = {}, nr[kMaxParts] = {};
+      for (int q = 0; q < P; q++) {
+        ns[q] = g_xrec_init * (X.xs_off[q + 1] - X.xs_off[q]);
+        nr[q] = g_xrec_init * (X.xr_off[q + 1] - X.xr_off[q]);
+      }
+      grow_regions(&xs.sbuf, xs.scap, ns, P, nullptr);
+      grow_regions(&xs.rbuf[0], xs.rcap, nr, P, nullptr);
+      xs.rbuf[1] = alloc_regions<XRec>(xs.rcap, P);
+    }
+  }
+}
+
+// the boundary vertices' K1 membership words to the peers, theirs into our ghost rows
+void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int planes) {
+  Slot& s = c->slot[si];
+  Part& X = c->pt;
+  XSlot& xs = X.xs[si];
+  const int P = c->nparts, me = c->part;
+  launch_xvm_pack(s.stream, X.nxs, X.xs_v, X.xs_q, X.xs_off_d, planes, vm, vstride, xs.vms);
+  HIPCHK(hipGetLastError());
   std::vector<void*> sp(P), rp(P);
   std::vector<size_t> sb(P), rb(P);
   for (int q = 0; q < P; q++) {
-    sp[q] = X.sbuf + X.xs_off[q] * kXRecWords;
-    rp[q] = X.rbuf + X.xr_off[q] * kXRecWords;
-    sb[q] = (size_t)sent[2 * q] * kXRecWords * 4;
-    rb[q] = q == me ? 0 : (size_t)X.h_x[2 * q] * kXRecWords * 4;
-    X.bytes_sent += (double)sb[q];
+    sp[q] = xs.vms + planes * X.xs_off[q];
+    rp[q] = xs.vmr + planes * X.xr_off[q];
+    sb[q] = q == me ? 0 : sizeof(uint64_t) * planes * (size_t)(X.xs_off[q + 1] - X.xs_off[q]);
+    rb[q] = q == me ? 0 : sizeof(uint64_t) * planes * (size_t)(X.xr_off[q + 1] - X.xr_off[q]);
+    xs.bytes += (double)sb[q];
   }
-  X.xchg->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
-  for (int q = 0; q < P; q++)
-    if (q != me && rb[q])
-      launch_xunpack_cc(s.stream, X.h_x[2 * q], (const int32_t*)rp[q], X.xr_v + X.xr_off[q], c->g, s.cnt,
-                        s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[(r + 1) % 3]);
+  xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
+  launch_xvm_unpack(s.stream, X.nxr, X.xr_v, X.xr_q, X.xr_off_d, planes, xs.vmr, vm, vstride);
   HIPCHK(hipGetLastError());
-  // the vote is global: the next superstep must run even if nothing changed here
+}
+
+// after superstep r: pack its boundary records and exchange the counts; the host picks the
+// slot up in part_after_counts
+void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
+  Slot& s = c->slot[si];
+  Part& X = c->pt;
+  XSlot& xs = X.xs[si];
+  const int P = c->nparts;
+  xs.r = r;
+  s.r_launched = r;
+  if (r >= rc.max_steps) {  // the cap (AnalysisTask.endStep :214): no superstep reads step r's news
+    s.r_final = r;
+    part_finish_begin(c, si, rc);
+    return;
+  }
+  const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
+  launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
+                   s.lab[r & 1], xs.sbuf, xs.scnt);
+  launch_xcounts(s.stream, P, c->part, xs.scnt, s.stepcnt + r, xs.xab);
+  HIPCHK(hipGetLastError());
+  xs.x->alltoall_i64(xs.xab, xs.xab + 2 * P, 2, s.stream);
+  HIPCHK(hipMemcpyAsync(xs.h_xab, xs.xab, sizeof(int64_t) * 4 * P, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipEventRecord(s.ev, s.stream));
+  s.phase = 1;
+}
+
+void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
+  Slot& s = c->slot[si];
+  Part& X = c->pt;
+  XSlot& xs = X.xs[si];
+  const DevGraph& g = c->g;
+  const int P = c->nparts, me = c->part, r = xs.r;
+  const int64_t* xa = xs.h_xab;
+  const int64_t* xb = xs.h_xab + 2 * P;
+  int64_t sent[kMaxParts] = {}, recv[kMaxParts] = {};
+  bool any = false;
+  for (int q = 0; q < P; q++) {
+    sent[q] = q == me ? 0 : xa[2 * q];
+    recv[q] = q == me ? 0 : xb[2 * q];
+    any |= xb[2 * q + 1] != 0;  // the vote: some partition changed a label (self included)
+  }
+  bool over = false;
+  for (int q = 0; q < P; q++) over |= sent[q] > xs.scap[q];
+  if (over) {  // the counts were exact; the records did not all fit: pack again, larger
+    grow_regions(&xs.sbuf, xs.scap, sent, P, s.stream);
+    const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
+    launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
+                     s.lab[r & 1], xs.sbuf, xs.scnt);
+    HIPCHK(hipMemsetAsync(xs.scnt, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
+  }
+  if (!any) {  // every partition voted to halt
+    s.r_final = r;
+    part_finish_begin(c, si, rc);
+    return;
+  }
+  const int par = r & 1;
+  // ghosts whose words records of step r-2 set (their records are still in rbuf[par])
+  launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par]);
+  bool rover = false;
+  for (int q = 0; q < P; q++) rover |= recv[q] > xs.rcap[q];
+  if (rover) {  // a larger layout for both parities; the other parity's records of step r-1 are
+                // read once more (their clear, two supersteps from now), so they move over
+    int64_t old_cap[kMaxParts];
+    std::copy(xs.rcap, xs.rcap + kMaxParts, old_cap);
+    grow_regions(&xs.rbuf[par], xs.rcap, recv, P, s.stream);  // syncs: the clear above has run
+    XRec* nb = alloc_regions<XRec>(xs.rcap, P);
+    int64_t o_old = 0, o_new = 0;
+    for (int q = 0; q < P; q++) {
+      if (xs.rcnt[par ^ 1][q])
+        HIPCHK(hipMemcpyAsync(nb + o_new, xs.rbuf[par ^ 1] + o_old, sizeof(XRec) * xs.rcnt[par ^ 1][q],
+                              hipMemcpyDeviceToDevice, s.stream));
+      o_old += old_cap[q];
+      o_new += xs.rcap[q];
+    }
+    HIPCHK(hipStreamSynchronize(s.stream));
+    HIPCHK(hipFree(xs.rbuf[par ^ 1]));
+    xs.rbuf[par ^ 1] = nb;
+  }
+  {
+    const XPeers Ls = peers_layout(c, xs.scap, X.xs_off, nullptr);
+    const XPeers Lr = peers_layout(c, xs.rcap, X.xr_off, nullptr);
+    std::vector<void*> sp(P), rp(P);
+    std::vector<size_t> sb(P), rb(P);
+    for (int q = 0; q < P; q++) {
+      sp[q] = xs.sbuf + Ls.base[q];
+      rp[q] = xs.rbuf[par] + Lr.base[q];
+      sb[q] = sizeof(XRec) * (size_t)sent[q];
+      rb[q] = sizeof(XRec) * (size_t)recv[q];
+      xs.bytes += (double)sb[q];
+    }
+    xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
+  }
+  std::copy(recv, recv + kMaxParts, xs.rcnt[par]);
+  const XPeers Lin = peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]);
+  launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par]);
+  launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.cnt, s.snbr, s.smask, s.act[(r + 1) % 3]);
+  // the vote is global: superstep r+1 runs here even if nothing changed here
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(s.stepcnt + r), 1, 1, s.stream));
-  return changed;
+  const bool hv = g.n_seg > 0;
+  if (hv)  // neighbours of heavy vertices (owned ones visited in r, ghosts just received) that changed
+    timed_launch(c, si, KID_HEAVY, 0.0, [&] {
+      launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[par], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
+                        r == 1 ? nullptr : s.act[r % 3]);
+    });
+  HIPCHK(hipGetLastError());
+  // superstep r+1 over the owned vertices
+  const int n = r + 1;
+  const DevGraph go = owned_view(c);
+  if (hv)
+    timed_launch(c, si, KID_HEAVY, 0.0, [&] {
+      launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[n % 3], s.stepcnt, n, s.hv);
+    });
+  timed_launch(c, si, KID_STEP, 0.0, [&] {
+    launch_cc_step(s.stream, n, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[r & 1], s.lab[n & 1], s.chg[r & 1],
+                   s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
+                   c->profile ? s.work : nullptr, c->step_variant, s.stats + kLaneOff, hv ? s.hv.best : nullptr);
+  }, n);
+  part_post_step(c, si, rc, n);
+}
+
+// component counts: label -> count of owned members routed to the label's owner (pass 0
+// counts the records per peer, the counts travel; part_finish_end writes and sends them)
+void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc) {
+  Slot& s = c->slot[si];
+  Part& X = c->pt;
+  XSlot& xs = X.xs[si];
+  const int P = c->nparts;
+  const int nviews = rc.K * rc.gsize;
+  const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);
+  timed_launch(c, si, KID_HIST, 12.0 * c->pk.n_own, [&] {
+    launch_hist_route(s.stream, 0, L, c->pk.n_own, nviews, X.vid_own, s.vm, s.vadj, s.lab[s.r_final & 1], nullptr,
+                      s.iso, xs.blkcnt, nullptr, nullptr);
+  });
+  launch_blk_scan(s.stream, P, hist_route_grid(c->pk.n_own), xs.blkcnt, xs.blkoff, xs.htot);
+  launch_xcounts(s.stream, P, c->part, xs.htot, nullptr, xs.xab);
+  HIPCHK(hipGetLastError());
+  xs.x->alltoall_i64(xs.xab, xs.xab + 2 * P, 2, s.stream);
+  HIPCHK(hipMemcpyAsync(xs.h_xab, xs.xab, sizeof(int64_t) * 4 * P, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipEventRecord(s.ev, s.stream));
+  s.phase = 3;
+}
+
+void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
+  Slot& s = c->slot[si];
+  Part& X = c->pt;
+  XSlot& xs = X.xs[si];
+  const int P = c->nparts, me = c->part;
+  const int nviews = rc.K * rc.gsize;
+  const int64_t no = c->pk.n_own;
+  int64_t sent[kMaxParts] = {}, recv[kMaxParts] = {};
+  for (int q = 0; q < P; q++) {
+    sent[q] = q == me ? 0 : xs.h_xab[2 * q];
+    recv[q] = q == me ? 0 : xs.h_xab[2 * P + 2 * q];
+  }
+  grow_regions(&xs.hsbuf, xs.hscap, sent, P, s.stream);
+  grow_regions(&xs.hrbuf, xs.hrcap, recv, P, s.stream);
+  int32_t* hist = s.lab[(s.r_final + 1) & 1];  // the free label buffer: [view][owned rank]
+  HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)no * kViews, s.stream));
+  const XPeers Ls = peers_layout(c, xs.hscap, X.xs_off, nullptr);
+  timed_launch(c, si, KID_HIST, 12.0 * no, [&] {
+    launch_hist_route(s.stream, 1, Ls, no, nviews, X.vid_own, s.vm, s.vadj, s.lab[s.r_final & 1], hist, s.iso,
+                      xs.blkcnt, xs.blkoff, xs.hsbuf);
+  });
+  {
+    const XPeers Lr = peers_layout(c, xs.hrcap, X.xr_off, nullptr);
+    std::vector<void*> sp(P), rp(P);
+    std::vector<size_t> sb(P), rb(P);
+    for (int q = 0; q < P; q++) {
+      sp[q] = xs.hsbuf + Ls.base[q];
+      rp[q] = xs.hrbuf + Lr.base[q];
+      sb[q] = 8 * (size_t)sent[q];
+      rb[q] = 8 * (size_t)recv[q];
+      xs.bytes += (double)sb[q];
+    }
+    xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
+  }
+  launch_hist_recv(s.stream, peers_layout(c, xs.hrcap, X.xr_off, recv), xs.hrbuf, X.vid_own, no, hist);
+  const DevGraph go = owned_view(c);
+  timed_launch(c, si, KID_SUMMARY, 8.0 * no * nviews, [&] { launch_cc_summary(s.stream, go, nviews, hist, s.stats, s.iso); });
+  // processBatchWindowResults merges the shards: biggest = max, the other fields add up
+  xs.x->allreduce_u64(s.stats, kViews, true, s.stream);
+  xs.x->allreduce_u64(s.stats + kViews, 5 * kViews, false, s.stream);
+  // the batch's ghost change words back to zero (the next batch's ghosts start clean)
+  for (int par = 0; par < 2; par++) {
+    launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par]);
+    std::fill(xs.rcnt[par], xs.rcnt[par] + kMaxParts, 0);
+  }
+  HIPCHK(hipGetLastError());
+  finish_tail(c, si, rc);
+}
+
+void wait_event(hipEvent_t e) {
+  for (;;) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) HIPCHK(q);
+    __builtin_ia32_pause();
+  }
+}
+
+int run_partitioned_cc(rgpu_ctx* c, RunCfg& rc) {
+  const size_t nb = rc.nb;
+  c->st.views += (int64_t)(rc.n_hops * rc.W);
+  c->st.batches += (int64_t)nb;
+  const int nslots = run_slots(c, rc);
+  size_t next = 0;
+  for (;;) {  // fixed round robin over the slots (identical collective order on every partition)
+    bool busy = false;
+    for (int si = 0; si < nslots; si++) {
+      Slot& s = c->slot[si];
+      if (s.phase == 0) {
+        if (next < nb && can_start(c, next, rc)) {
+          start_batch(c, si, (int)next++, rc);
+          busy = true;
+        }
+        continue;
+      }
+      busy = true;
+      wait_event(s.ev);
+      if (s.phase == 1) part_after_counts(c, si, rc);
+      else if (s.phase == 3) part_finish_end(c, si, rc);
+      else harvest(c, si, rc);
+    }
+    if (!busy) break;
+  }
+  return 0;
 }
 
 void pr_exchange(rgpu_ctx* c, double* contrib) {
   Slot& s = c->slot[0];
   Part& X = c->pt;
+  Exchange* x = X.xs[0].x;
   const int P = c->nparts, me = c->part;
   launch_xgather_f64(s.stream, X.nxs, X.xs_v, contrib, X.sbuf_f);
   HIPCHK(hipGetLastError());
@@ -927,39 +1260,19 @@ void pr_exchange(rgpu_ctx* c, double* contrib) {
     rb[q] = q == me ? 0 : (size_t)(X.xr_off[q + 1] - X.xr_off[q]) * kViews * 8;
     X.bytes_sent += (double)sb[q];
   }
-  X.xchg->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
+  x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
   launch_xscatter_f64(s.stream, X.nxr, X.xr_v, X.rbuf_f, contrib);
   HIPCHK(hipGetLastError());
 }
 
-void finish_partitioned_cc(rgpu_ctx* c, const RunCfg& rc) {
-  Slot& s = c->slot[0];
-  Part& X = c->pt;
-  const int P = c->nparts, nviews = rc.K * rc.W;
-  const int32_t* lab = s.lab[s.r_final & 1];
-  // per-partition label -> count of owned members (ConnectedComponents.returnResults :37-42),
-  // summed over partitions by reduce-scatter (the cross-shard merge of
-  // processBatchWindowResults :137), each partition summarising its slice, then the summary
-  // fields all-reduced (max for biggest)
-  HIPCHK(hipMemsetAsync(X.hist, 0, sizeof(int32_t) * X.hist_total, s.stream));
-  timed_launch(c, 0, KID_HIST, 12.0 * c->pk.n_own, [&] {
-    launch_cc_hist(s.stream, c->pk.n_own, X.ng, nviews, s.vm, s.vadj, lab, X.hist, s.iso);
-  });
-  const int64_t cnt = X.hist_total / P;
-  X.xchg->reduce_scatter_i32(X.hist, X.chunk, (size_t)cnt, s.stream);
-  timed_launch(c, 0, KID_SUMMARY, 4.0 * cnt, [&] {
-    launch_cc_summary_rs(s.stream, nviews, X.chunk, cnt * c->part, cnt, X.ng, s.stats, s.iso);
-  });
-  X.xchg->allreduce_u64(s.stats, kViews, true, s.stream);
-  X.xchg->allreduce_u64(s.stats + kViews, 5 * kViews, false, s.stream);
-}
-
-int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
+// DegreeBasic / PageRank, one hop-major batch at a time on slot 0
+int run_partitioned_dp(rgpu_ctx* c, RunCfg& rc) {
   const size_t nb = rc.nb;  // hop-major (G = 1)
   c->st.views += (int64_t)(rc.n_hops * rc.W);
   c->st.batches += (int64_t)nb;
   Slot& s = c->slot[0];
   const DevGraph go = owned_view(c);
+  const DevGraph& g = c->g;
   for (size_t b = 0; b < nb; b++) {
     BatchParams bp;
     std::memset(&bp, 0, sizeof(bp));
@@ -976,86 +1289,36 @@ int run_partitioned(rgpu_ctx* c, RunCfg& rc) {
     for (int w = 0; w < rc.W; w++) { bp.thr_v[w] = rc.thr_v[w]; bp.thr_e[w] = rc.thr_e[w]; }
     s.batch = (int)b;
     s.kb = bp.K;
+    s.r_final = 0;
     BatchClear clr;
     clr.stats = s.stats;
     clr.n_stats = kStatCopy;
     clr.flags = s.stepcnt;
     clr.n_flags = kMaxSteps;
-    if (rc.algo == RGPU_ALGO_CC) {
-      for (int k = 0; k < 3; k++) clr.act[k] = s.act[k];
-      clr.n_act_words = (c->g.nv + 7) / 8 + 1;
-    }
-    const DevGraph& g = c->g;
     s.vm = s.vm_own;
     s.em = s.em_own;
-    timed_launch(c, 0, KID_MASK, 8.0 * (g.nv + 1) + 8.0 * c->pk.n_vkey + 8.0 * g.nv,
-                 [&] { launch_vertex_mask(s.stream, g, bp, s.vm, 0, false, clr); });
+    timed_launch(c, 0, KID_MASK, 8.0 * (go.nv + 1) + 8.0 * c->pk.n_vkey + 8.0 * go.nv,
+                 [&] { launch_vertex_mask(s.stream, go, bp, s.vm, 0, false, clr); });
     timed_launch(c, 0, KID_MASK, bytes_mask(g) - (16.0 * g.nv + 8.0) + 8.0 * c->pk.n_ekey,
                  [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0); });
-    if (rc.algo == RGPU_ALGO_CC) {
-      timed_launch(c, 0, KID_SLOTS, g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0, [&] {
-        launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
-                        s.chg[1], s.act[2], s.stepcnt, nullptr, nullptr, HeavyBuf(), s.stats + kLaneOff);
+    part_vm_exchange(c, 0, s.vm, 0, 1);
+    timed_launch(c, 0, KID_DEGREE, go.nv * (8.0 + 32.0 + 512.0) + (double)(g.ne + g.n_in) * 12.0, [&] {
+      launch_degree(s.stream, go, s.vm, s.em, s.outdeg, s.indeg, s.stats);
+    });
+    if (rc.algo == RGPU_ALGO_PR) {
+      timed_launch(c, 0, KID_SLOTS, go.nv * (8.0 + 24.0 + 256.0 + 1024.0) + (double)(g.n_in) * 24.0, [&] {
+        launch_pr_slots(s.stream, go, s.vm, s.em, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.pr, s.contrib[0]);
       });
-      s.r_final = 0;
-      if (rc.max_steps > 1) {
-        s.r_final = rc.max_steps;
-        if (cc_exchange(c, 1) == 0) {
-          s.r_final = 1;
-        } else {
-          for (int r = 2; r <= rc.max_steps; r++) {
-            timed_launch(c, 0, KID_STEP, 0.0, [&] {
-              launch_cc_step(s.stream, r, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
-                             s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
-                             s.act[(r + 2) % 3], s.stepcnt, nullptr, nullptr, c->step_variant,
-                             s.stats + kLaneOff);
-            }, r);
-            if (cc_exchange(c, r) == 0) { s.r_final = r; break; }
-          }
-        }
-      }
-      finish_partitioned_cc(c, rc);
-    } else {
-      timed_launch(c, 0, KID_DEGREE, go.nv * (8.0 + 32.0 + 512.0) + (double)(g.ne + g.n_in) * 12.0, [&] {
-        launch_degree(s.stream, go, s.vm, s.em, s.outdeg, s.indeg, s.stats);
-      });
-      if (rc.algo == RGPU_ALGO_PR) {
-        timed_launch(c, 0, KID_SLOTS, go.nv * (8.0 + 24.0 + 256.0 + 1024.0) + (double)(g.n_in) * 24.0, [&] {
-          launch_pr_slots(s.stream, go, s.vm, s.em, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.pr, s.contrib[0]);
+      pr_exchange(c, s.contrib[0]);
+      for (int it = 0; it < rc.pr_iters; it++) {
+        timed_launch(c, 0, KID_PR, go.nv * (8.0 + 16.0 + 4.0 + 256.0 + 1024.0) + (double)(g.n_in + go.nv) * 12.0, [&] {
+          launch_pr_step(s.stream, go, s.vm, s.em, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.contrib[it & 1],
+                         s.contrib[(it + 1) & 1], s.pr, s.hv.pacc);
         });
-        pr_exchange(c, s.contrib[0]);
-        for (int it = 0; it < rc.pr_iters; it++) {
-          timed_launch(c, 0, KID_PR, go.nv * (8.0 + 16.0 + 4.0 + 256.0 + 1024.0) + (double)(g.n_in + go.nv) * 12.0, [&] {
-            launch_pr_step(s.stream, go, s.vm, s.em, s.outdeg, s.pcnt, s.psnbr, s.psmask, s.contrib[it & 1],
-                           s.contrib[(it + 1) & 1], s.pr, nullptr);
-          });
-          if (it + 1 < rc.pr_iters) pr_exchange(c, s.contrib[(it + 1) & 1]);
-        }
+        if (it + 1 < rc.pr_iters) pr_exchange(c, s.contrib[(it + 1) & 1]);
       }
     }
-    // stats, retained rows (finish_batch without the single-GPU CC reductions)
-    if (rc.algo == RGPU_ALGO_CC) launch_lane_fold(s.stream, s.stats + kLaneOff, s.stats + kFoldOff);
-    HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatCopy,
-                          hipMemcpyDeviceToHost, s.stream));
-    if (rc.flags & RGPU_RUN_RETAIN) {
-      Retained& R = c->kept[b];
-      const size_t rows = (size_t)g.nv * kViews;
-      R.vm.resize(g.nv);
-      HIPCHK(hipMemcpyAsync(R.vm.data(), s.vm, sizeof(uint64_t) * g.nv, hipMemcpyDeviceToHost, s.stream));
-      if (rc.algo == RGPU_ALGO_CC) {
-        R.a.resize(rows);
-        HIPCHK(hipMemcpyAsync(R.a.data(), s.lab[s.r_final & 1], sizeof(int32_t) * rows,
-                              hipMemcpyDeviceToHost, s.stream));
-      } else if (rc.algo == RGPU_ALGO_DEGREE) {
-        R.a.resize(rows);
-        R.b.resize(rows);
-        HIPCHK(hipMemcpyAsync(R.a.data(), s.outdeg, sizeof(int32_t) * rows, hipMemcpyDeviceToHost, s.stream));
-        HIPCHK(hipMemcpyAsync(R.b.data(), s.indeg, sizeof(int32_t) * rows, hipMemcpyDeviceToHost, s.stream));
-      } else {
-        R.pr.resize(rows);
-        HIPCHK(hipMemcpyAsync(R.pr.data(), s.pr, sizeof(double) * rows, hipMemcpyDeviceToHost, s.stream));
-      }
-    }
+    finish_tail(c, 0, rc);
     HIPCHK(hipStreamSynchronize(s.stream));
     harvest(c, 0, rc);
   }
@@ -1138,6 +1401,8 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->tail_cap = std::max(1, env_int("RGPU_TAIL_CAP", 256));
   c->tail_maxv = std::max(0, env_int("RGPU_TAIL_MAXV", 4 << 20));
   c->delta_on = env_int("RGPU_DELTA", 1) != 0;
+  g_xrec_slack = std::max(1, env_int("RGPU_XREC_SLACK", 1024));
+  g_xrec_init = std::max(0, env_int("RGPU_XREC_INIT", 2));
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
   *out = c;
@@ -1155,8 +1420,11 @@ int rgpu_ingest(rgpu_ctx* c, const int64_t* t, const uint8_t* kind, const int64_
     for (size_t i = 0; i < n; i++) {
       if (kind[i] > RGPU_EDEL) return fail(c, RGPU_EINVAL, "unknown update kind");
       if (kind[i] >= RGPU_EADD && !dst) return fail(c, RGPU_EINVAL, "edge update without dst array");
-      c->events.push_back({t[i], src[i], kind[i] >= RGPU_EADD ? dst[i] : -1, kind[i]});
       c->newest = std::max(c->newest, t[i]);
+      const int64_t d = kind[i] >= RGPU_EADD ? dst[i] : -1;
+      // a partition keeps its own part of the stream (rgpu_internal.hpp: partition_keeps)
+      if (!partition_keeps(kind[i], src[i], d, c->part, c->nparts)) continue;
+      c->events.push_back({t[i], src[i], d, kind[i]});
     }
   } catch (const std::bad_alloc&) {
     return fail(c, RGPU_ENOMEM, "host allocation failed");
@@ -1191,7 +1459,7 @@ namespace {
 // Heavy vertices (power-law hubs): static slot lists cut into kSegSlots segments.
 void build_heavy(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L, const std::vector<int64_t>& out_off,
                  const std::vector<int64_t>& in_off) {
-  if (c->partitioned || c->heavy_t <= 0) return;
+  if (c->heavy_t <= 0) return;
   std::vector<int32_t> hv_of(g.nv, -1), hv_seg(1, 0), seg_v, seg_h, seg_n;
   std::vector<int64_t> seg_lo;
   for (int64_t v = 0; v < g.nv; v++) {
@@ -1232,6 +1500,7 @@ void finish_seal(rgpu_ctx* c) {
   Packed& P = c->pk;
   c->st.vertices = P.n_own;
   c->st.edges = P.ne;
+  c->st.edges_owned = P.ne_owned;
   c->st.vertex_events = P.n_vkey;
   c->st.edge_events = P.n_ekey;
   c->st.deaths = (int64_t)P.dtime.size();
@@ -1411,7 +1680,7 @@ void seal_delta(rgpu_ctx* c) {
       }
     }
     B.nv = B.n_own = D.nv;
-    B.ne = g.ne;
+    B.ne = B.ne_owned = g.ne;
     B.vid.swap(D.vid);
     B.doff.swap(D.doff);
     B.dtime.swap(D.dtime);
@@ -1477,10 +1746,13 @@ int rgpu_seal(rgpu_ctx* c) {
     g.in_eid = dupload(L, P.in_eid);
     g.n_own = P.n_own;
     build_heavy(c, g, L, P.out_off, P.in_off);
-    if (c->partitioned) {
-      if (c->nparts > 1) g.grank = dupload(L, P.grank);
+    if (c->partitioned) {  // CC labels are vertex ids (the label owner routes component counts)
+      if (c->nparts > kMaxParts) return fail(c, RGPU_EINVAL, "more than 8 partitions");
+      if (P.grank.empty())
+        g.grank = dupload(L, std::vector<int32_t>(P.vid.begin(), P.vid.end()));
+      else
+        g.grank = dupload(L, P.grank);
       Part& X = c->pt;
-      X.ng = P.nv;
       X.nxs = (int64_t)P.xs_v.size();
       X.nxr = (int64_t)P.xr_v.size();
       X.xs_off = P.xs_off;
@@ -1488,7 +1760,10 @@ int rgpu_seal(rgpu_ctx* c) {
       X.xs_v = dupload(L, P.xs_v);
       X.xs_q = dupload(L, P.xs_q);
       X.xr_v = dupload(L, P.xr_v);
+      X.xr_q = dupload(L, P.xr_q);
       X.xs_off_d = dupload(L, P.xs_off);
+      X.xr_off_d = dupload(L, P.xr_off);
+      X.vid_own = dupload(L, std::vector<int64_t>(P.vid.begin(), P.vid.begin() + P.n_own));
     }
     c->g = g;
     HIPCHK(hipDeviceSynchronize());
@@ -1555,7 +1830,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   // window-major batches when they pay: each window's views in their own batches (64 hops),
   // so the cheap short windows no longer ride along the long windows' supersteps (not when all
   // views fit one hop-major batch, e.g. a live query of the newest hop)
-  const bool wm = c->wmajor && !c->partitioned && rc.W >= 2 && rc.W <= kMaxPlanes &&
+  const bool wm = c->wmajor && (!c->partitioned || algo == RGPU_ALGO_CC) && rc.W >= 2 && rc.W <= kMaxPlanes &&
                   n_hops * (size_t)rc.W > (size_t)kViews;  // else one hop-major batch holds every view
   rc.G = wm ? rc.W : 1;
   rc.gsize = wm ? 1 : rc.W;
@@ -1586,6 +1861,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
       const auto ta = std::chrono::steady_clock::now();
       ensure_slots(c, algo, run_slots(c, rc));
       ensure_masks(c, rc.G, run_slots(c, rc));
+      if (c->partitioned) ensure_part(c, run_slots(c, rc), rc.G);
       if (c->hostprof) {
         HIPCHK(hipDeviceSynchronize());
         std::fprintf(stderr, "rgpu hostprof: ensure buffers %.2f ms\n",
@@ -1628,7 +1904,8 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->st.views = c->st.batches = c->st.supersteps = 0;
     auto t0 = std::chrono::steady_clock::now();
     c->pt.bytes_sent = 0;
-    if (c->partitioned) run_partitioned(c, rc);
+    if (c->partitioned && algo == RGPU_ALGO_CC) run_partitioned_cc(c, rc);
+    else if (c->partitioned) run_partitioned_dp(c, rc);
     else run_impl(c, rc);
     for (int si = 0; si < kMaxSlots; si++)
       if (c->slot[si].stream) HIPCHK(hipStreamSynchronize(c->slot[si].stream));
@@ -1683,7 +1960,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
 
 // id of the vertex whose global rank is l (CC labels are global ranks)
 static int64_t label_id(const rgpu_ctx* c, int32_t l) {
-  return c->nparts > 1 ? (int64_t)l : c->pk.vid[l];  // partitioned: labels are ids
+  return c->partitioned ? (int64_t)l : c->pk.vid[l];  // partitioned: labels are ids
 }
 
 static int view_index(rgpu_ctx* c, size_t hop, size_t win, size_t* batch, int* lane) {
@@ -1885,6 +2162,7 @@ void rgpu_close(rgpu_ctx* c) {
     for (Slot& s : c->slot)
       if (s.stream) (void)hipStreamSynchronize(s.stream);
     free_graph(c);
+    free_part_slots(c, false);
     delete c->pt.xchg;
     c->pt.xchg = nullptr;
     for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);

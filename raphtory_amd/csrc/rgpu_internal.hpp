@@ -24,6 +24,8 @@ struct Packed {
   std::vector<int32_t> in_eid;       // [in_off[nv]] edge ids of in-edges
   int64_t newest = -1;
   int64_t n_vkey = 0, n_ekey = 0, n_in = 0;  // sizes (the big arrays are dropped after upload)
+  int64_t ne_owned = 0;              // edges whose source is owned here (their sum over the
+                                     // partitions is the graph's edge entities)
   // ---- vertex partitioning (num_partitions > 1); identity when P = 1
   int part = 0, nparts = 1;
   int64_t n_own = 0;                 // ranks [0, n_own) are owned here, [n_own, nv) are ghosts

@@ -248,7 +248,10 @@ __global__ __launch_bounds__(512) void k_hist_route(XPeers P, int64_t n_own, int
     if (!on) return;
     const int q = owner_of(L, P.np);
     if (q == P.me) {
-      if (PASS == 1) atomicAdd(&hist[(int64_t)j * n_own + owned_rank(vid, n_own, L)], (int32_t)c);
+      if (PASS == 1) {
+        const int64_t rk = owned_rank(vid, n_own, L);  // always found: a label is a member's id
+        if (rk >= 0) atomicAdd(&hist[(int64_t)j * n_own + rk], (int32_t)c);
+      }
       return;
     }
     const unsigned long long k = atomicAdd(&pc[q], 1ull);

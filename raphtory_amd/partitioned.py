@@ -4,12 +4,13 @@ exchanged every superstep (RCCL), component sizes merged across partitions.
 Two ways to hold the partitions:
   * one process per GPU (torch.distributed): :func:`open_rccl_partition` gives this rank's
     TemporalGraph, joined to an RCCL communicator whose id rank 0 broadcasts;
-  * :class:`LoopbackPartitions`: all P partitions in one process (one host thread each, same
-    or different devices) over the library's loopback exchange — the same protocol, used to
-    test the partitioned path on one GPU.
+  * :class:`LoopbackPartitions`: all P partitions in one process and on ONE device (one host
+    thread each) over the library's loopback exchange — the same protocol, used to test the
+    partitioned path on one GPU (its copies and kernels read peers' buffers device-locally).
 
-Each partition must be handed the whole update stream (include/rgpu.h); runs are
-collective (every partition calls run with the same arguments).
+Each partition may be handed the whole update stream or only its part (include/rgpu.h: it
+keeps its own vertices' updates, edge updates with an owned endpoint and every VertexDelete);
+runs are collective (every partition calls run with the same arguments).
 """
 from __future__ import annotations
 
@@ -36,6 +37,9 @@ def open_rccl_partition(device: int, dist=None) -> TemporalGraph:
 class LoopbackPartitions:
     def __init__(self, nparts: int, device: int | Sequence[int] = 0):
         devs = [device] * nparts if isinstance(device, int) else list(device)
+        if len(set(devs)) != 1:
+            raise ValueError("loopback partitions share one device (use one process per GPU and RCCL "
+                             "across devices: open_rccl_partition)")
         self.parts: List[TemporalGraph] = [TemporalGraph(p, nparts, devs[p]) for p in range(nparts)]
         xid = TemporalGraph.exchange_id(loopback=True)
         for g in self.parts:

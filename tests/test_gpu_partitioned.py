@@ -15,8 +15,19 @@ pytestmark = pytest.mark.gpu
 PR_L1_TOL = 1e-6
 
 
-def _parts(s, P):
-    lp = LoopbackPartitions(P)
+def _parts(s, P, env=None):
+    import os
+    env = env or {}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        lp = LoopbackPartitions(P)  # rgpu_open reads the RGPU_* knobs
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     lp.ingest_stream(s)
     lp.seal()
     return lp
@@ -98,4 +109,67 @@ def test_partitioned_powerlaw_and_gab():
     lp = _parts(s, 3)
     end = int(s.t[-1])
     check_cc(lp, o, range_hops(end - 48 * HOUR, end, 6 * HOUR), BATCH_WINDOWS)
+    lp.close()
+
+
+@pytest.mark.parametrize("P", [5, 8])
+def test_partitioned_many_partitions_window_major(P):
+    """P up to 8 (one node's GPUs) on one GPU: window-major batches (64 hops x one window),
+    three batches in flight on their own channels; record buffers forced to start tiny so
+    that every growth path (send, receive with records still awaiting their clear, component
+    counts) runs."""
+    s = gen_uniform(13, 600, 12_000, t0=T0_README, dt=2_628_000)
+    o = Oracle.from_stream(s)
+    lp = _parts(s, P, {"RGPU_XREC_INIT": "0", "RGPU_XREC_SLACK": "1"})
+    hops = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, 2 * DAY)  # 168 hops x 5
+    check_cc(lp, o, hops, BATCH_WINDOWS)
+    lp.close()
+
+
+@pytest.mark.parametrize("heavy", ["300", "0"])
+def test_partitioned_heavy_hubs(heavy):
+    """Star hubs with thousands of leaves split into 512-slot segments on the partition that
+    owns them and as ghosts elsewhere (RGPU_HEAVY=300: every vertex above 300 static slots)."""
+    from tests.test_gpu_heavy import hubs_stream
+    s = hubs_stream()
+    o = Oracle.from_stream(s)
+    lp = _parts(s, 3, {"RGPU_HEAVY": heavy})
+    hops = range_hops(T0_README + 5 * DAY, T0_README + 70 * DAY, DAY)
+    check_cc(lp, o, hops, [MONTH, WEEK, DAY])
+    check_degree(lp, o, hops[::9], [MONTH, WEEK, DAY])
+    check_pr(lp, o, hops[::20], [MONTH, WEEK])
+    lp.close()
+
+
+def test_partitioned_filtered_ingest_equals_whole_stream():
+    """Each partition handed only its part of the stream (what rgpu_ingest keeps anyway) answers
+    exactly as when handed the whole stream."""
+    from raphtory_amd.partition import get_partition
+    s = gen_powerlaw(7, 1500, 15_000, t0=0, t1=YEAR)
+    o = Oracle.from_stream(s)
+    P = 3
+    lp = LoopbackPartitions(P)
+    for p, g in enumerate(lp.parts):
+        own_s = get_partition(s.src, P) == p
+        own_d = (s.dst >= 0) & (get_partition(np.maximum(s.dst, 0), P) == p)
+        keep = (s.kind == 1) | own_s | ((s.kind >= 2) & own_d)
+        g.ingest(s.t[keep], s.kind[keep], s.src[keep], s.dst[keep])
+    lp.seal()
+    check_cc(lp, o, range_hops(YEAR - 40 * DAY, YEAR, 8 * DAY), [MONTH, WEEK, DAY])
+    lp.close()
+
+
+def test_loopback_rejects_mixed_devices():
+    with pytest.raises(ValueError):
+        LoopbackPartitions(2, device=[0, 1])
+
+
+def test_partitioned_path_one_partition_scattered_ids():
+    """The partitioned path with P = 1 (RGPU_PARTITIONED=1, no peers): labels are vertex ids and
+    the component counts go to the label's owned rank — on power-law ids scattered over
+    [0, 2^31) (ranks differ from ids) with heavy hubs."""
+    s = gen_powerlaw(9, 3000, 40_000, t0=0, t1=YEAR)
+    o = Oracle.from_stream(s)
+    lp = _parts(s, 1, {"RGPU_PARTITIONED": "1", "RGPU_HEAVY": "200"})
+    check_cc(lp, o, range_hops(YEAR - 50 * DAY, YEAR, 5 * DAY), [MONTH, WEEK, DAY])
     lp.close()
