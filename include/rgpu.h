@@ -95,6 +95,10 @@ typedef struct {
   /* edge entities whose source vertex this partition owns: summed over the partitions, the
      graph's edge entities (`edges` counts every edge kept here, SplitEdge copies included) */
   int64_t edges_owned;
+  /* last run, partitioned mode: bytes this partition sent to its peers, in all and by kind
+     [0] ghost membership words [1] label records [2] component counts [3] PageRank rows */
+  double xchg_bytes;
+  double xchg_bytes_by[4];
 } rgpu_stats_t;
 
 int rgpu_abi_version(void);

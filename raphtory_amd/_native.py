@@ -58,7 +58,8 @@ class Stats(C.Structure):
         ("ms_total", C.c_double),
         ("kernel_launches", C.c_int64 * 12), ("kernel_ms", C.c_double * 12), ("kernel_bytes", C.c_double * 12),
         ("seal_ms", C.c_double), ("seal_incremental", C.c_int64), ("seal_delta_updates", C.c_int64),
-        ("alive_edge_windows", C.c_int64), ("edges_owned", C.c_int64),
+        ("alive_edge_windows", C.c_int64), ("edges_owned", C.c_int64), ("xchg_bytes", C.c_double),
+        ("xchg_bytes_by", C.c_double * 4),
     ]
 
 

@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -100,6 +101,32 @@ struct LocalGroup {
   }
 };
 
+// RGPU_LOOPBACK_ISOLATE=1 (measurement only, tools/part_sim.py): a partition thread holds a
+// process-wide lock from the end of one collective to the start of its next, so the partitions'
+// GPU work between collectives runs one partition at a time and per-kernel event times are
+// free of the other partitions' contention (their sum is the work P GPUs would share).
+std::mutex g_iso;
+thread_local bool t_iso_held = false;
+bool iso_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("RGPU_LOOPBACK_ISOLATE");
+    return e && *e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+void iso_enter() {  // at a collective's start, after this thread's stream has drained
+  if (t_iso_held) {
+    t_iso_held = false;
+    g_iso.unlock();
+  }
+}
+void iso_exit() {
+  if (iso_on() && !t_iso_held) {
+    g_iso.lock();
+    t_iso_held = true;
+  }
+}
+
 std::mutex g_reg_mu;
 std::map<uint64_t, std::weak_ptr<LocalGroup>> g_reg;
 
@@ -126,6 +153,7 @@ class LocalExchange : public Exchange {
   int size() const override { return g_->n; }
   void alltoall_i64(const int64_t* d_send, int64_t* d_recv, size_t n, hipStream_t s) override {
     hipchk(hipStreamSynchronize(s), "sync");
+    iso_enter();
     g_->ptr[r_] = d_send;
     g_->barrier();
     for (int q = 0; q < g_->n; q++)
@@ -133,11 +161,13 @@ class LocalExchange : public Exchange {
                             hipMemcpyDeviceToDevice, s), "copy");
     hipchk(hipStreamSynchronize(s), "sync");
     g_->barrier();
+    iso_exit();
   }
   void sendrecv(void* const* send, const size_t* send_bytes, void* const* recv,
                 const size_t* recv_bytes, hipStream_t s) override {
     const int n = g_->n;
     hipchk(hipStreamSynchronize(s), "sync");
+    iso_enter();
     g_->vptr[r_].assign(send, send + n);
     g_->vsz[r_].assign(send_bytes, send_bytes + n);
     g_->barrier();
@@ -150,12 +180,14 @@ class LocalExchange : public Exchange {
     }
     hipchk(hipStreamSynchronize(s), "sync");
     g_->barrier();
+    iso_exit();
   }
   void allreduce_u64(unsigned long long* d, size_t n, bool max, hipStream_t s) override {
     auto& mine = g_->host[r_];
     mine.resize(n);
     hipchk(hipMemcpyAsync(mine.data(), d, n * 8, hipMemcpyDeviceToHost, s), "copy");
     hipchk(hipStreamSynchronize(s), "sync");
+    iso_enter();
     g_->barrier();
     std::vector<unsigned long long> acc(g_->host[0]);
     for (int q = 1; q < g_->n; q++)
@@ -166,6 +198,7 @@ class LocalExchange : public Exchange {
     g_->barrier();
     hipchk(hipMemcpyAsync(d, acc.data(), n * 8, hipMemcpyHostToDevice, s), "copy");
     hipchk(hipStreamSynchronize(s), "sync");
+    iso_exit();
   }
 
  private:
@@ -175,6 +208,8 @@ class LocalExchange : public Exchange {
 };
 
 }  // namespace
+
+void exchange_quiesce() { iso_enter(); }
 
 std::string make_exchange_id(int kind, uint8_t out[kXchgIdBytes]) {
   std::memset(out, 0, kXchgIdBytes);

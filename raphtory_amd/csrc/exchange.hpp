@@ -46,6 +46,8 @@ class Exchange {
 // id blob handed to every partition (rgpu_exchange_id / rgpu_exchange_init); returns "" or
 // an error.  kind 0 = RCCL unique id, kind 1 = loopback group (one process).
 std::string make_exchange_id(int kind, uint8_t out[kXchgIdBytes]);
+// end of a run: a loopback partition thread gives up the measurement lock (RGPU_LOOPBACK_ISOLATE)
+void exchange_quiesce();
 std::string open_exchange(const uint8_t id[kXchgIdBytes], int rank, int nranks, int device,
                           Exchange** out);
 

@@ -1048,13 +1048,14 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
                                                      const uint64_t* __restrict__ em,
                                                      int32_t* __restrict__ snbr, uint64_t* __restrict__ smask,
                                                      int32_t* __restrict__ segcnt, uint64_t* __restrict__ segor,
-                                                     int32_t* __restrict__ hbest, const int32_t* __restrict__ grank) {
+                                                     int32_t* __restrict__ hbest, const int32_t* __restrict__ grank,
+                                                     int64_t n_own) {
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
-    const uint64_t mv = vm[v];
+    const uint64_t mv = v < n_own ? vm[v] : 0;  // a heavy ghost keeps no compacted slots
     if (mv == 0) {
       if (lane == 0) { segcnt[sg] = 0; segor[sg] = 0; }
       continue;
@@ -1159,7 +1160,16 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
                                                     const uint64_t* __restrict__ chg_now,
                                                     const uint8_t* __restrict__ act_cur,
                                                     uint8_t* __restrict__ act_next,
-                                                    const int32_t* __restrict__ stepflag, int64_t n_own) {
+                                                    const int32_t* __restrict__ stepflag, int64_t n_own,
+                                                    const int32_t* __restrict__ seg_n,
+                                                    const int64_t* __restrict__ out_off,
+                                                    const int64_t* __restrict__ in_off,
+                                                    const int64_t* __restrict__ adj_off,
+                                                    const int32_t* __restrict__ in_eid,
+                                                    const int32_t* __restrict__ esrc,
+                                                    const int32_t* __restrict__ edst,
+                                                    const uint64_t* __restrict__ vm,
+                                                    const uint64_t* __restrict__ em) {
   if (stepflag[step] == 0) return;
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -1169,6 +1179,23 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
     if (act_cur && v < n_own && !act_cur[v]) continue;  // a ghost's word is current (set by its records)
     const uint64_t ch = chg_now[v];
     if (!ch) continue;
+    if (v >= n_own) {  // heavy ghost (partitioned): its static slots of the segment, kept on the fly
+      if (!vm || !em) continue;
+      const uint64_t mv = vm[v] & ch;
+      const int64_t rel0 = seg_lo[sg] - adj_off[v], o0 = out_off[v], i0 = in_off[v];
+      const int64_t nout = out_off[v + 1] - o0;
+      const int32_t ns = seg_n[sg];
+      for (int32_t c = 0; c < ns; c += 64) {
+        if (c + lane >= ns) continue;
+        const int64_t rel = rel0 + c + lane;
+        int64_t e;
+        int32_t nb;
+        if (rel < nout) { e = o0 + rel; nb = edst[e]; }
+        else { e = in_eid[i0 + (rel - nout)]; nb = esrc[e]; }
+        if (nb != v && (em[e] & vm[nb] & mv)) act_next[nb] = 1;
+      }
+      continue;
+    }
     const int32_t n = segcnt[sg];
     const int64_t base = seg_lo[sg];
     for (int32_t c = 0; c < n; c += 64) {
@@ -1726,7 +1753,7 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, co
   if (g.n_seg <= 0) return;
   k_heavy_slots<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off,
                                                             g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
-                                                            snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank);
+                                                            snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own);
 }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
@@ -1738,10 +1765,12 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
-                       const HeavyBuf& hb, const uint8_t* act_cur) {
+                       const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm, const uint64_t* em) {
   if (g.n_seg <= 0) return;
   k_heavy_mark<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
-                                                           chg_now, act_cur, act_next, stepflag, g.n_own);
+                                                           chg_now, act_cur, act_next, stepflag, g.n_own, g.seg_n,
+                                                           g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst,
+                                                           vm, em);
 }
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,

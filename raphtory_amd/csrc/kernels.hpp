@@ -97,9 +97,12 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, co
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb);
+// vm/em (partitioned mode): heavy ghosts (ranks >= n_own) have no compacted slots; their kept
+// slots are recomputed from the static adjacency (em & vm[nb] & vm[v]) while marking
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
-                       const HeavyBuf& hb, const uint8_t* act_cur);
+                       const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm = nullptr,
+                       const uint64_t* em = nullptr);
 extern int g_sum_blocks;   // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 extern int g_hist_rounds;  // label-dedup rounds per (view, chunk) in k_cc_hist (RGPU_HIST_ROUNDS)
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
@@ -176,16 +179,21 @@ void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32
 void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
                         uint64_t* chg);
 void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
-                  const DevGraph& g, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
-                  uint8_t* act_next);
-unsigned hist_route_grid(int64_t n_own);
-void launch_hist_route(hipStream_t s, int pass, const XPeers& P, int64_t n_own, int nviews, const int64_t* vid,
+                  const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next);
+// owned id -> owned rank: ids ascend with rank; bucket b = id >> shift covers ranks
+// [boff[b], boff[b+1]) (about one id per bucket)
+struct OwnIdx {
+  const int64_t* vid = nullptr;
+  const int32_t* boff = nullptr;
+  int shift = 0;
+  int64_t n_own = 0;
+};
+// component counts routed to the label owners (one pass; remote_only: the records again, into a
+// larger buffer, without the local counts); gcnt[q] counts every record for peer q
+void launch_hist_route(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso,
-                       int64_t* blkcnt, const int64_t* blkoff, unsigned long long* hsbuf);
-void launch_blk_scan(hipStream_t s, int np, int64_t nb, const int64_t* blkcnt, int64_t* blkoff,
-                     unsigned long long* tot);
-void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const int64_t* vid,
-                      int64_t n_own, int32_t* hist);
+                       unsigned long long* gcnt, unsigned long long* hsbuf);
+void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const OwnIdx& I, int32_t* hist);
 // PageRank contribution rows of a list (partitioned PageRank): gather into / scatter out of a
 // contiguous buffer
 void launch_xgather_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* rows, double* buf);

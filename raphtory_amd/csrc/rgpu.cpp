@@ -117,14 +117,12 @@ struct XSlot {
   int64_t* h_xab = nullptr;               // pinned copy
   uint64_t *vms = nullptr, *vmr = nullptr;  // ghost membership words (planes x list)
   int vm_planes = 0;
-  int64_t* blkcnt = nullptr;              // component counts: records per (peer, block)
-  int64_t* blkoff = nullptr;
-  unsigned long long* htot = nullptr;     // [kMaxParts]
+  unsigned long long* htot = nullptr;     // [kMaxParts] component-count records per peer
   unsigned long long *hsbuf = nullptr, *hrbuf = nullptr;
   int64_t hscap[kMaxParts] = {}, hrcap[kMaxParts] = {};
   int r = 0;                              // superstep whose counts exchange is in flight
   int64_t hrcnt[kMaxParts] = {};
-  double bytes = 0;                       // record bytes sent by this slot
+  double bytes[3] = {};                   // sent by this slot: membership words, records, counts
 };
 struct Part {
   Exchange* xchg = nullptr;                   // the ctx's channel (rgpu_exchange_init)
@@ -132,7 +130,7 @@ struct Part {
   std::vector<int64_t> xs_off, xr_off;        // host copies of the plan offsets
   int32_t *xs_v = nullptr, *xs_q = nullptr, *xr_v = nullptr, *xr_q = nullptr;
   int64_t *xs_off_d = nullptr, *xr_off_d = nullptr;
-  int64_t* vid_own = nullptr;                 // owned ids ascending (label owner -> owned rank)
+  OwnIdx own;                                 // owned id -> owned rank (label owner counting)
   double *sbuf_f = nullptr, *rbuf_f = nullptr;  // PR contribution rows
   bool pr_ready = false;
   XSlot xs[4];                                // per batch slot (kMaxSlots)
@@ -697,8 +695,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     const double b2 = g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0;
     if (g.n_seg > 0)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] { launch_heavy_slots(s.stream, g, s.vm, s.em, s.snbr, s.smask, s.hv); });
-    timed_launch(c, si, KID_SLOTS, b2, [&] {
-      launch_cc_slots(s.stream, g, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
+    timed_launch(c, si, KID_SLOTS, b2, [&] {  // (partitioned: owned vertices only, gk)
+      launch_cc_slots(s.stream, gk, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                       c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff);
     });
@@ -972,9 +970,6 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
       HIPCHK(hipMemset(xs.htot, 0, sizeof(unsigned long long) * kMaxParts));
       xs.xab = dalloc<int64_t>(LG, 4 * P);
       HIPCHK(hipHostMalloc((void**)&xs.h_xab, sizeof(int64_t) * 4 * P));
-      const int64_t nb = hist_route_grid(c->pk.n_own);
-      xs.blkcnt = dalloc<int64_t>(LG, (size_t)kMaxParts * nb);
-      xs.blkoff = dalloc<int64_t>(LG, (size_t)kMaxParts * nb);
     }
     if (xs.vm_planes < planes) {
       xs.vms = dalloc<uint64_t>(LG, (size_t)planes * std::max<int64_t>(X.nxs, 1));
@@ -1010,7 +1005,7 @@ void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int pl
     rp[q] = xs.vmr + planes * X.xr_off[q];
     sb[q] = q == me ? 0 : sizeof(uint64_t) * planes * (size_t)(X.xs_off[q + 1] - X.xs_off[q]);
     rb[q] = q == me ? 0 : sizeof(uint64_t) * planes * (size_t)(X.xr_off[q + 1] - X.xr_off[q]);
-    xs.bytes += (double)sb[q];
+    xs.bytes[0] += (double)sb[q];
   }
   xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
   launch_xvm_unpack(s.stream, X.nxr, X.xr_v, X.xr_q, X.xr_off_d, planes, xs.vmr, vm, vstride);
@@ -1104,21 +1099,21 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
       rp[q] = xs.rbuf[par] + Lr.base[q];
       sb[q] = sizeof(XRec) * (size_t)sent[q];
       rb[q] = sizeof(XRec) * (size_t)recv[q];
-      xs.bytes += (double)sb[q];
+      xs.bytes[1] += (double)sb[q];
     }
     xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
   }
   std::copy(recv, recv + kMaxParts, xs.rcnt[par]);
   const XPeers Lin = peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]);
   launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par]);
-  launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.cnt, s.snbr, s.smask, s.act[(r + 1) % 3]);
+  launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3]);
   // the vote is global: superstep r+1 runs here even if nothing changed here
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(s.stepcnt + r), 1, 1, s.stream));
   const bool hv = g.n_seg > 0;
   if (hv)  // neighbours of heavy vertices (owned ones visited in r, ghosts just received) that changed
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[par], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
-                        r == 1 ? nullptr : s.act[r % 3]);
+                        r == 1 ? nullptr : s.act[r % 3], s.vm, s.em);
     });
   HIPCHK(hipGetLastError());
   // superstep r+1 over the owned vertices
@@ -1136,20 +1131,28 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   part_post_step(c, si, rc, n);
 }
 
-// component counts: label -> count of owned members routed to the label's owner (pass 0
-// counts the records per peer, the counts travel; part_finish_end writes and sends them)
+// component counts: label -> count of owned members, the labels owned elsewhere routed to their
+// owner as records (k_hist_route); their counts travel, the host picks the slot up in
+// part_finish_end
 void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc) {
   Slot& s = c->slot[si];
   Part& X = c->pt;
   XSlot& xs = X.xs[si];
   const int P = c->nparts;
   const int nviews = rc.K * rc.gsize;
+  const int64_t no = c->pk.n_own;
+  if (!xs.hsbuf) {  // first guess: one record per owned vertex and peer
+    int64_t need[kMaxParts];
+    for (int q = 0; q < P; q++) need[q] = no;
+    grow_regions(&xs.hsbuf, xs.hscap, need, P, s.stream);
+  }
+  int32_t* hist = s.lab[(s.r_final + 1) & 1];  // the free label buffer: [view][owned rank]
+  HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)no * kViews, s.stream));
   const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);
-  timed_launch(c, si, KID_HIST, 12.0 * c->pk.n_own, [&] {
-    launch_hist_route(s.stream, 0, L, c->pk.n_own, nviews, X.vid_own, s.vm, s.vadj, s.lab[s.r_final & 1], nullptr,
-                      s.iso, xs.blkcnt, nullptr, nullptr);
+  timed_launch(c, si, KID_HIST, 12.0 * no, [&] {
+    launch_hist_route(s.stream, false, L, X.own, nviews, s.vm, s.vadj, s.lab[s.r_final & 1], hist, s.iso, xs.htot,
+                      xs.hsbuf);
   });
-  launch_blk_scan(s.stream, P, hist_route_grid(c->pk.n_own), xs.blkcnt, xs.blkoff, xs.htot);
   launch_xcounts(s.stream, P, c->part, xs.htot, nullptr, xs.xab);
   HIPCHK(hipGetLastError());
   xs.x->alltoall_i64(xs.xab, xs.xab + 2 * P, 2, s.stream);
@@ -1166,20 +1169,23 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
   const int nviews = rc.K * rc.gsize;
   const int64_t no = c->pk.n_own;
   int64_t sent[kMaxParts] = {}, recv[kMaxParts] = {};
+  bool over = false;
   for (int q = 0; q < P; q++) {
     sent[q] = q == me ? 0 : xs.h_xab[2 * q];
     recv[q] = q == me ? 0 : xs.h_xab[2 * P + 2 * q];
+    over |= sent[q] > xs.hscap[q];
   }
-  grow_regions(&xs.hsbuf, xs.hscap, sent, P, s.stream);
+  int32_t* hist = s.lab[(s.r_final + 1) & 1];
+  if (over) {  // the records again into a larger buffer (the local counts are done)
+    grow_regions(&xs.hsbuf, xs.hscap, sent, P, s.stream);
+    const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);
+    launch_hist_route(s.stream, true, L, X.own, nviews, s.vm, s.vadj, s.lab[s.r_final & 1], hist, s.iso, xs.htot,
+                      xs.hsbuf);
+    HIPCHK(hipMemsetAsync(xs.htot, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
+  }
   grow_regions(&xs.hrbuf, xs.hrcap, recv, P, s.stream);
-  int32_t* hist = s.lab[(s.r_final + 1) & 1];  // the free label buffer: [view][owned rank]
-  HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)no * kViews, s.stream));
-  const XPeers Ls = peers_layout(c, xs.hscap, X.xs_off, nullptr);
-  timed_launch(c, si, KID_HIST, 12.0 * no, [&] {
-    launch_hist_route(s.stream, 1, Ls, no, nviews, X.vid_own, s.vm, s.vadj, s.lab[s.r_final & 1], hist, s.iso,
-                      xs.blkcnt, xs.blkoff, xs.hsbuf);
-  });
   {
+    const XPeers Ls = peers_layout(c, xs.hscap, X.xs_off, nullptr);
     const XPeers Lr = peers_layout(c, xs.hrcap, X.xr_off, nullptr);
     std::vector<void*> sp(P), rp(P);
     std::vector<size_t> sb(P), rb(P);
@@ -1188,11 +1194,11 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
       rp[q] = xs.hrbuf + Lr.base[q];
       sb[q] = 8 * (size_t)sent[q];
       rb[q] = 8 * (size_t)recv[q];
-      xs.bytes += (double)sb[q];
+      xs.bytes[2] += (double)sb[q];
     }
     xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
   }
-  launch_hist_recv(s.stream, peers_layout(c, xs.hrcap, X.xr_off, recv), xs.hrbuf, X.vid_own, no, hist);
+  launch_hist_recv(s.stream, peers_layout(c, xs.hrcap, X.xr_off, recv), xs.hrbuf, X.own, hist);
   const DevGraph go = owned_view(c);
   timed_launch(c, si, KID_SUMMARY, 8.0 * no * nviews, [&] { launch_cc_summary(s.stream, go, nviews, hist, s.stats, s.iso); });
   // processBatchWindowResults merges the shards: biggest = max, the other fields add up
@@ -1763,7 +1769,19 @@ int rgpu_seal(rgpu_ctx* c) {
       X.xr_q = dupload(L, P.xr_q);
       X.xs_off_d = dupload(L, P.xs_off);
       X.xr_off_d = dupload(L, P.xr_off);
-      X.vid_own = dupload(L, std::vector<int64_t>(P.vid.begin(), P.vid.begin() + P.n_own));
+      {  // owned ids ascend with rank: bucket b = id >> shift, about one id per bucket
+        int lg = 0;
+        while (((int64_t)1 << lg) < std::max<int64_t>(P.n_own, 1)) lg++;
+        const int shift = std::max(0, 31 - lg);
+        const int64_t nbk = ((int64_t)1 << 31) >> shift;
+        std::vector<int32_t> boff(nbk + 1, 0);
+        for (int64_t v = 0; v < P.n_own; v++) boff[(P.vid[v] >> shift) + 1]++;
+        for (int64_t b = 0; b < nbk; b++) boff[b + 1] += boff[b];
+        X.own.vid = dupload(L, std::vector<int64_t>(P.vid.begin(), P.vid.begin() + P.n_own));
+        X.own.boff = dupload(L, boff);
+        X.own.shift = shift;
+        X.own.n_own = P.n_own;
+      }
     }
     c->g = g;
     HIPCHK(hipDeviceSynchronize());
@@ -1904,12 +1922,19 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->st.views = c->st.batches = c->st.supersteps = 0;
     auto t0 = std::chrono::steady_clock::now();
     c->pt.bytes_sent = 0;
+    for (XSlot& xs : c->pt.xs) xs.bytes[0] = xs.bytes[1] = xs.bytes[2] = 0;
     if (c->partitioned && algo == RGPU_ALGO_CC) run_partitioned_cc(c, rc);
     else if (c->partitioned) run_partitioned_dp(c, rc);
     else run_impl(c, rc);
     for (int si = 0; si < kMaxSlots; si++)
       if (c->slot[si].stream) HIPCHK(hipStreamSynchronize(c->slot[si].stream));
     if (algo == RGPU_ALGO_CC) finish_supersteps(c, rc);
+    for (int k = 0; k < 4; k++) c->st.xchg_bytes_by[k] = 0;
+    c->st.xchg_bytes_by[3] = c->pt.bytes_sent;
+    for (const XSlot& xs : c->pt.xs)
+      for (int k = 0; k < 3; k++) c->st.xchg_bytes_by[k] += xs.bytes[k];
+    c->st.xchg_bytes = 0;
+    for (int k = 0; k < 4; k++) c->st.xchg_bytes += c->st.xchg_bytes_by[k];
     if (c->d_ecnt) {  // |E_{t,w}| per view (RGPU_RUN_EDGE_COUNTS)
       std::vector<unsigned long long> e(n_hops * rc.W);
       HIPCHK(hipMemcpy(e.data(), c->d_ecnt, sizeof(unsigned long long) * e.size(), hipMemcpyDeviceToHost));
@@ -1949,12 +1974,16 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     }
     c->steprec.clear();
   } catch (const HipFail& f) {
+    exchange_quiesce();
     return fail(c, RGPU_EHIP, f.msg);
   } catch (const std::bad_alloc&) {
+    exchange_quiesce();
     return fail(c, RGPU_ENOMEM, "host allocation failed");
   } catch (const std::exception& x) {  // exchange (RCCL / loopback) failures
+    exchange_quiesce();
     return fail(c, RGPU_EHIP, x.what());
   }
+  exchange_quiesce();
   return RGPU_OK;
 }
 

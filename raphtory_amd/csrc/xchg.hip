@@ -38,14 +38,12 @@ __device__ __forceinline__ int peer_of(const XPeers& P, int64_t i) {
   while (q + 1 < P.np && i >= P.pre[q + 1]) q++;
   return q;
 }
-// rank of owned vertex `id` (ids of owned ranks ascend), or -1
-__device__ __forceinline__ int64_t owned_rank(const int64_t* __restrict__ vid, int64_t n_own, int64_t id) {
-  int64_t a = 0, b = n_own;
-  while (a < b) {
-    const int64_t m = (a + b) >> 1;
-    if (vid[m] < id) a = m + 1; else b = m;
-  }
-  return a < n_own && vid[a] == id ? a : -1;
+// rank of owned vertex `id`, or -1 (bucket index: about one probe)
+__device__ __forceinline__ int64_t owned_rank(const OwnIdx& I, int64_t id) {
+  const int64_t b = id >> I.shift;
+  for (int64_t i = I.boff[b], e = I.boff[b + 1]; i < e; i++)
+    if (I.vid[i] == id) return i;
+  return -1;
 }
 
 }  // namespace
@@ -193,11 +191,16 @@ __global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __res
 }
 
 // After the unpack: the first record of every ghost marks the ghost's owned neighbours that
-// share a changed view (the next frontier, as a local change would).  Heavy ghosts: k_heavy_mark.
+// share a changed view (the next frontier, as a local change would).  Ghosts keep no compacted
+// slots (K2 runs over the owned vertices only): the kept views of a static slot, em[e] & vm[nb] &
+// vm[g], are recomputed here for the ghosts that changed.  Heavy ghosts: k_heavy_mark.
 __global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict__ rbuf,
                                                const int32_t* __restrict__ xrv, const uint64_t* __restrict__ chg,
-                                               const int64_t* __restrict__ adj_off, const int32_t* __restrict__ cnt,
-                                               const int32_t* __restrict__ snbr, const uint64_t* __restrict__ smask,
+                                               const int64_t* __restrict__ out_off,
+                                               const int64_t* __restrict__ in_off,
+                                               const int32_t* __restrict__ in_eid,
+                                               const int32_t* __restrict__ esrc, const int32_t* __restrict__ edst,
+                                               const uint64_t* __restrict__ vm, const uint64_t* __restrict__ em,
                                                const int32_t* __restrict__ hv_of, uint8_t* __restrict__ act_next) {
   const int64_t n = P.pre[P.np];
   const int lane = lane_of();
@@ -206,16 +209,21 @@ __global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict_
   for (int64_t i = wave; i < n; i += nwaves) {
     const int q = peer_of(P, i);
     const int64_t k = i - P.pre[q];
-    const int32_t e = rbuf[P.base[q] + k].e;
-    if (k > 0 && rbuf[P.base[q] + k - 1].e == e) continue;  // not the ghost's first record
-    const int32_t g = xrv[P.xoff[q] + e];
+    const int32_t e0 = rbuf[P.base[q] + k].e;
+    if (k > 0 && rbuf[P.base[q] + k - 1].e == e0) continue;  // not the ghost's first record
+    const int32_t g = xrv[P.xoff[q] + e0];
     if (hv_of && hv_of[g] >= 0) continue;
-    const uint64_t ch = chg[g];
-    const int32_t nk = cnt[g];
-    const int64_t base = adj_off[g];
-    for (int32_t c = 0; c < nk; c += 64) {
-      const int32_t j = c + lane;
-      if (j < nk && (smask[base + j] & ch)) act_next[snbr[base + j]] = 1;
+    const uint64_t ch = chg[g] & vm[g];
+    const int64_t o0 = out_off[g], i0 = in_off[g];
+    const int64_t nout = out_off[g + 1] - o0, ntot = nout + (in_off[g + 1] - i0);
+    for (int64_t c = 0; c < ntot; c += 64) {
+      const int64_t j = c + lane;
+      if (j >= ntot) continue;
+      int64_t e;
+      int32_t nb;
+      if (j < nout) { e = o0 + j; nb = edst[e]; }
+      else { e = in_eid[i0 + (j - nout)]; nb = esrc[e]; }
+      if (nb != g && (em[e] & vm[nb] & ch)) act_next[nb] = 1;
     }
   }
 }
@@ -225,20 +233,23 @@ __global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict_
 // routed to the label's owner: as k_cc_hist, a block stages 64 vertices' label rows and its
 // eight waves dedup each view's labels (after `rounds` labels, one entry per lane).  Counts of
 // labels owned here go straight into hist[view][owned rank]; the others become records
-// (label | view << 31 | count << 37) for their owner.  PASS 0 counts a block's records per
-// peer (blkcnt[q][block]); PASS 1 writes them at the scanned offsets (blkoff) and does the
-// local counting.  Members with no kept slot are islands, counted in iso as on one partition.
-template <int PASS>
-__global__ __launch_bounds__(512) void k_hist_route(XPeers P, int64_t n_own, int nviews, const int64_t* __restrict__ vid,
+// (label | view << 31 | count << 37), staged per peer in LDS and flushed after every chunk with
+// one atomicAdd per (block, peer).  Members with no kept slot are islands, counted in iso.
+constexpr int kStage = 256;  // staged records per peer and chunk (more: written directly)
+template <bool REMOTE_ONLY>
+__global__ __launch_bounds__(512) void k_hist_route(XPeers P, OwnIdx I, int nviews,
                                                     const uint64_t* __restrict__ vm,
                                                     const uint64_t* __restrict__ vadj,
                                                     const int32_t* __restrict__ lab, int32_t* __restrict__ hist,
                                                     unsigned int* __restrict__ iso_g, int rounds,
-                                                    int64_t* __restrict__ blkcnt, const int64_t* __restrict__ blkoff,
+                                                    unsigned long long* __restrict__ gcnt,
                                                     unsigned long long* __restrict__ hsbuf) {
   __shared__ int32_t tile[64][65];
   __shared__ unsigned int iso[64];
-  __shared__ unsigned long long pc[kMaxParts];  // PASS 0: records per peer; PASS 1: running offsets
+  __shared__ unsigned long long stage[kMaxParts][kStage];
+  __shared__ unsigned int pc[kMaxParts];
+  __shared__ unsigned long long fb[kMaxParts];
+  const int64_t n_own = I.n_own;
   const int lane = lane_of(), wib = threadIdx.x >> 6;
   if (threadIdx.x < 64) iso[threadIdx.x] = 0;
   if (threadIdx.x < kMaxParts) pc[threadIdx.x] = 0;
@@ -248,16 +259,20 @@ __global__ __launch_bounds__(512) void k_hist_route(XPeers P, int64_t n_own, int
     if (!on) return;
     const int q = owner_of(L, P.np);
     if (q == P.me) {
-      if (PASS == 1) {
-        const int64_t rk = owned_rank(vid, n_own, L);  // always found: a label is a member's id
+      if (!REMOTE_ONLY) {
+        const int64_t rk = owned_rank(I, L);  // always found: a label is a member's id
         if (rk >= 0) atomicAdd(&hist[(int64_t)j * n_own + rk], (int32_t)c);
       }
       return;
     }
-    const unsigned long long k = atomicAdd(&pc[q], 1ull);
-    if (PASS == 1)
-      hsbuf[P.base[q] + blkoff[(int64_t)q * gridDim.x + blockIdx.x] + (int64_t)k] =
-          (unsigned long long)L | ((unsigned long long)j << 31) | ((unsigned long long)c << 37);
+    const unsigned long long rec = (unsigned long long)L | ((unsigned long long)j << 31) | ((unsigned long long)c << 37);
+    const unsigned int k = atomicAdd(&pc[q], 1u);
+    if (k < kStage) {
+      stage[q][k] = rec;
+    } else {  // a chunk with more records for q than the stage holds: straight out
+      const unsigned long long pos = atomicAdd(&gcnt[q], 1ull);
+      if (pos < (unsigned long long)P.cap[q]) hsbuf[P.base[q] + (int64_t)pos] = rec;
+    }
   };
   for (int64_t c = blockIdx.x; c * 64 < n_own; c += gridDim.x) {
     const int64_t v0 = c * 64;
@@ -283,7 +298,7 @@ __global__ __launch_bounds__(512) void k_hist_route(XPeers P, int64_t n_own, int
       any &= any - 1;
       const bool in_view = (mvl >> j) & 1;
       const bool member = in_view && ((adl >> j) & 1);
-      if (PASS == 1) {
+      if (!REMOTE_ONLY) {
         const uint64_t isolated = __ballot(in_view && !member);
         if (lane == 0 && isolated) iso[j] += (unsigned)__popcll(isolated);
       }
@@ -301,41 +316,29 @@ __global__ __launch_bounds__(512) void k_hist_route(XPeers P, int64_t n_own, int
         todo &= ~same;
       }
     }
-    __syncthreads();
-  }
-  if (PASS == 0) {
-    __syncthreads();
-    if (threadIdx.x < P.np) blkcnt[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = (int64_t)pc[threadIdx.x];
-  } else {
-    __syncthreads();
-    if (threadIdx.x < 64 && iso[threadIdx.x]) atomicAdd(&iso_g[(blockIdx.x & 63) * 64 + threadIdx.x], iso[threadIdx.x]);
-  }
-}
-
-// exclusive scan of blkcnt[q][0..nb) per peer (one wave per peer) -> blkoff, and the peer's
-// total into tot[q] (the counts exchange)
-__global__ void k_blk_scan(int np, int64_t nb, const int64_t* __restrict__ blkcnt, int64_t* __restrict__ blkoff,
-                           unsigned long long* __restrict__ tot) {
-  const int q = threadIdx.x >> 6, lane = lane_of();
-  if (q >= np) return;
-  int64_t run = 0;
-  for (int64_t b0 = 0; b0 < nb; b0 += 64) {
-    const int64_t b = b0 + lane;
-    const int64_t x = b < nb ? blkcnt[q * nb + b] : 0;
-    int64_t inc = x;  // inclusive wave scan
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t y = __shfl_up(inc, o);
-      if (lane >= o) inc += y;
+    __syncthreads();  // the chunk's records are staged (and the tile is free)
+    if (threadIdx.x < P.np) {
+      const unsigned int n = pc[threadIdx.x] < kStage ? pc[threadIdx.x] : kStage;
+      fb[threadIdx.x] = n ? atomicAdd(&gcnt[threadIdx.x], (unsigned long long)n) : 0ull;
     }
-    if (b < nb) blkoff[q * nb + b] = run + inc - x;
-    run += __shfl(inc, 63);
+    __syncthreads();
+    for (int q = 0; q < P.np; q++) {
+      const unsigned int n = pc[q] < kStage ? pc[q] : kStage;
+      for (unsigned int i = threadIdx.x; i < n; i += blockDim.x) {
+        const unsigned long long pos = fb[q] + i;
+        if (pos < (unsigned long long)P.cap[q]) hsbuf[P.base[q] + (int64_t)pos] = stage[q][i];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < kMaxParts) pc[threadIdx.x] = 0;
+    __syncthreads();
   }
-  if (lane == 0) tot[q] = (unsigned long long)run;
+  if (!REMOTE_ONLY && threadIdx.x < 64 && iso[threadIdx.x])
+    atomicAdd(&iso_g[(blockIdx.x & 63) * 64 + threadIdx.x], iso[threadIdx.x]);
 }
 
 // records received from the other partitions: count at the owned label vertex
-__global__ __launch_bounds__(256) void k_hist_recv(XPeers P, const unsigned long long* __restrict__ rbuf,
-                                                   const int64_t* __restrict__ vid, int64_t n_own,
+__global__ __launch_bounds__(256) void k_hist_recv(XPeers P, const unsigned long long* __restrict__ rbuf, OwnIdx I,
                                                    int32_t* __restrict__ hist) {
   const int64_t n = P.pre[P.np];
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -344,8 +347,8 @@ __global__ __launch_bounds__(256) void k_hist_recv(XPeers P, const unsigned long
     const int64_t L = (int64_t)(r & 0x7fffffffull);
     const int j = (int)((r >> 31) & 63);
     const int32_t c = (int32_t)(r >> 37);
-    const int64_t rk = owned_rank(vid, n_own, L);
-    if (rk >= 0) atomicAdd(&hist[(int64_t)j * n_own + rk], c);
+    const int64_t rk = owned_rank(I, L);
+    if (rk >= 0) atomicAdd(&hist[(int64_t)j * I.n_own + rk], c);
   }
 }
 
@@ -379,31 +382,22 @@ void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const 
   if (P.pre[P.np] > 0) k_xunpack_rec<<<xgrid(P.pre[P.np], 16), 256, 0, s>>>(P, rbuf, xrv, lab, chg);
 }
 void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
-                  const DevGraph& g, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
-                  uint8_t* act_next) {
+                  const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next) {
   if (P.pre[P.np] > 0)
-    k_xmark<<<xgrid(P.pre[P.np], 4), 256, 0, s>>>(P, rbuf, xrv, chg, g.adj_off, cnt, snbr, smask,
-                                                   g.n_seg > 0 ? g.hv_of : nullptr, act_next);
+    k_xmark<<<xgrid(P.pre[P.np], 4), 256, 0, s>>>(P, rbuf, xrv, chg, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
+                                                   vm, em, g.n_seg > 0 ? g.hv_of : nullptr, act_next);
 }
-unsigned hist_route_grid(int64_t n_own) { return xgrid(n_own, 64, 8192); }
-void launch_hist_route(hipStream_t s, int pass, const XPeers& P, int64_t n_own, int nviews, const int64_t* vid,
+void launch_hist_route(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso,
-                       int64_t* blkcnt, const int64_t* blkoff, unsigned long long* hsbuf) {
-  const unsigned grid = hist_route_grid(n_own);
-  if (pass == 0)
-    k_hist_route<0><<<grid, 512, 0, s>>>(P, n_own, nviews, vid, vm, vadj, lab, hist, iso, g_hist_rounds, blkcnt,
-                                          blkoff, hsbuf);
+                       unsigned long long* gcnt, unsigned long long* hsbuf) {
+  const unsigned grid = xgrid(I.n_own, 64, 8192);
+  if (remote_only)
+    k_hist_route<true><<<grid, 512, 0, s>>>(P, I, nviews, vm, vadj, lab, hist, iso, g_hist_rounds, gcnt, hsbuf);
   else
-    k_hist_route<1><<<grid, 512, 0, s>>>(P, n_own, nviews, vid, vm, vadj, lab, hist, iso, g_hist_rounds, blkcnt,
-                                          blkoff, hsbuf);
+    k_hist_route<false><<<grid, 512, 0, s>>>(P, I, nviews, vm, vadj, lab, hist, iso, g_hist_rounds, gcnt, hsbuf);
 }
-void launch_blk_scan(hipStream_t s, int np, int64_t nb, const int64_t* blkcnt, int64_t* blkoff,
-                     unsigned long long* tot) {
-  k_blk_scan<<<1, 64 * kMaxParts, 0, s>>>(np, nb, blkcnt, blkoff, tot);
-}
-void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const int64_t* vid,
-                      int64_t n_own, int32_t* hist) {
-  if (P.pre[P.np] > 0) k_hist_recv<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, vid, n_own, hist);
+void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const OwnIdx& I, int32_t* hist) {
+  if (P.pre[P.np] > 0) k_hist_recv<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, I, hist);
 }
 
 }  // namespace rgpu

@@ -199,7 +199,9 @@ class TemporalGraph:
     def stats(self) -> dict:
         s = N.Stats()
         self._check(self._lib.rgpu_stats(self._ctx, C.byref(s)))
-        d = {f: getattr(s, f) for f, _ in N.Stats._fields_ if f not in ("kernel_launches", "kernel_ms", "kernel_bytes")}
+        d = {f: getattr(s, f) for f, _ in N.Stats._fields_
+             if f not in ("kernel_launches", "kernel_ms", "kernel_bytes", "xchg_bytes_by")}
+        d["xchg_bytes_by"] = {k: s.xchg_bytes_by[i] for i, k in enumerate(("membership", "records", "counts", "pagerank"))}
         d["kernels"] = {N.KERNEL_NAMES[i]: {"launches": s.kernel_launches[i], "ms": s.kernel_ms[i],
                                             "bytes": s.kernel_bytes[i]} for i in range(len(N.KERNEL_NAMES))}
         return d

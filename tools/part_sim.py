@@ -1,0 +1,74 @@
+"""One-GPU rehearsal of the vertex-partitioned C4 query: P partitions in one
+process over the loopback exchange (LoopbackPartitions), P = 1..8, on a C4-shaped prefix of the
+1B stream.  RGPU_LOOPBACK_ISOLATE=1 makes the partitions' GPU work between collectives run one
+partition at a time, so the serial profile pass's kernel times are each partition's own: their
+maximum is the compute one of P GPUs would do, their sum the partitioning's total work.  Also:
+the bytes the partitions send each other per query (by kind) and the summaries' check sums
+(identical at every P).  Prints one JSON line per P."""
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("RGPU_LOOPBACK_ISOLATE", "1")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from raphtory_amd import TemporalGraph  # noqa: E402
+from raphtory_amd.partitioned import LoopbackPartitions  # noqa: E402
+from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--users", type=int, default=20_000_000)
+    ap.add_argument("--interactions", type=int, default=33_333_334, help="prefix of the 1B stream (x3 updates)")
+    ap.add_argument("--parts", default="1,2,4,8")
+    a = ap.parse_args()
+    inter_full = 333_333_334
+    s = gen_gab_range(4, a.users, inter_full, 0, a.interactions)
+    end = int(s.t[-1])
+    hops = range_hops(end - 167 * HOUR, end, HOUR)
+    for P in [int(x) for x in a.parts.split(",")]:
+        if P == 1:
+            g = TemporalGraph()
+            g.ingest_stream(s)
+            g.seal()
+            parts = [g]
+            run = lambda **kw: g.run("cc", hops, BATCH_WINDOWS, **kw)  # noqa: E731
+        else:
+            lp = LoopbackPartitions(P)
+            lp.ingest_stream(s)
+            lp.seal()
+            parts = lp.parts
+            run = lambda **kw: lp.run("cc", hops, BATCH_WINDOWS, **kw)  # noqa: E731
+        run()
+        run(profile=True, serial=True)
+        per = []
+        ks = {}
+        for g in parts:
+            mine = 0.0
+            for k, v in g.stats()["kernels"].items():
+                if v["launches"]:
+                    ks[k] = ks.get(k, 0.0) + v["ms"]
+                    mine += v["ms"]
+            per.append(round(mine, 1))
+        by = {}
+        for g in parts:
+            for k, v in g.stats()["xchg_bytes_by"].items():
+                by[k] = by.get(k, 0.0) + v / 1e6
+        summ = parts[0].cc_summaries()
+        out = {"P": P, "kernel_ms_per_partition": per, "kernel_ms_max": max(per), "kernel_ms_total": round(sum(per), 1),
+               "kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in ks.items()},
+               "xchg_MB_per_query": {k: round(v, 1) for k, v in by.items()},
+               "vertices_here": [g.stats()["vertices"] for g in parts], "edges_here": [g.stats()["edges"] for g in parts],
+               "check": [int(summ[..., 0].sum()), int(summ[..., 1].sum()), int(summ[..., 5].sum())]}
+        print(json.dumps(out), flush=True)
+        for g in parts:
+            g.close()
+
+
+if __name__ == "__main__":
+    main()
