@@ -441,13 +441,18 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   unsigned long long members = 0, alive = 0, changed = 0;
   uint64_t lanes = 0;  // views with a step-1 change in this wave
-  for (int64_t v = wave; v < nv; v += nwaves) {
-    const uint64_t mv = vm[v];
+  // 64 vertices per wave round: the lanes read their view masks (one coalesced load), clear the
+  // non-members' count / mask words, and the wave then walks the members one by one
+  for (int64_t b0 = wave * 64; b0 < nv; b0 += nwaves * 64) {
+   const int64_t vlane = b0 + lane;
+   const uint64_t mvl = vlane < nv ? vm[vlane] : 0;
+   if (vlane < nv && mvl == 0) { cnt[vlane] = 0; vadj[vlane] = 0; }
+   uint64_t todo = __ballot(mvl != 0);
+   while (todo) {
+    const int64_t v = b0 + __builtin_ctzll(todo);
+    const uint64_t mv = readlane64(mvl, __builtin_ctzll(todo));
+    todo &= todo - 1;
     const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
-    if (mv == 0) {
-      if (lane == 0) { cnt[v] = 0; vadj[v] = 0; }
-      continue;
-    }
     if (hv_of && hv_of[v] >= 0) {
       // heavy vertex: its segments were compacted by k_heavy_slots, which also left the
       // superstep-1 minima of its neighbours' labels in hbest; neighbours of a change are
@@ -546,6 +551,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     }
     members += 1;
     alive += (unsigned long long)count;
+   }
   }
   if (lane == 0) {
     if (members) atomicAdd(&red[0], members);
@@ -855,20 +861,29 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   int32_t changed = 0;
   unsigned long long pv = 0, ps = 0, pg = 0;
   const TailList none{nullptr, nullptr};
-  for (int64_t c = wave; c * CH < nv; c += nwaves) {
-    const int64_t v0 = c * CH;
-    uint32_t bits = 0;
-    {
+  // 64 chunks per wave round: lane l reads chunk l's frontier flags (one coalesced load), and
+  // the wave then runs only the flagged chunks — a sparse frontier costs one load per 64 chunks
+  const int64_t nchunks = (nv + CH - 1) / CH;
+  for (int64_t c0 = wave * 64; c0 < nchunks; c0 += nwaves * 64) {
+    const int64_t cl = c0 + lane;
+    uint32_t fb = 0;
+    if (cl < nchunks) {
+      const int64_t v0 = cl * CH;
       const uint64_t f = CH == 8 ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
                                  : *reinterpret_cast<const uint32_t*>(act_cur + v0);
 #pragma unroll
-      for (int i = 0; i < CH; i++) bits |= ((f >> (8 * i)) & 0xffu) ? (1u << i) : 0u;
+      for (int i = 0; i < CH; i++) fb |= ((f >> (8 * i)) & 0xffu) ? (1u << i) : 0u;
+      if (v0 + CH > nv) fb &= (1u << (nv - v0)) - 1;
     }
-    if (v0 + CH > nv) bits &= (1u << (nv - v0)) - 1;
-    if (!bits) continue;
-    cc_chunk<CH, BUF, false>(v0 + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
-                             lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[3], pv, ps, pg,
-                             hv_of, hbest);
+    uint64_t todo = __ballot(fb != 0);
+    while (todo) {
+      const int L = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
+      cc_chunk<CH, BUF, false>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
+                               lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[3], pv, ps, pg,
+                               hv_of, hbest);
+    }
   }
   if (work)
     for (int o = 32; o > 0; o >>= 1) pg += __shfl_xor(pg, o);
@@ -999,37 +1014,12 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
 
 // ---------------------------------------------------------------- heavy vertices
 // A power-law hub has 1e5-1e6 slots: as one wave's serial loop it would be the whole
-// superstep.  Its static slots are cut into segments of <= kSegSlots, one wave each, and the
-// per-view minimum over a segment is formed with lane = slot: every lane loads the whole
-// label row of its neighbour (or an always-cached row of INT32_MAX when that neighbour has
-// nothing new), folds it into acc[64], and a butterfly reduce-scatter leaves the minimum of
-// view j in lane j, added to the hub's row with one coalesced atomicMin.
-
-__device__ int4 g_max_row[16] = {
-    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
-    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
-    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
-    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
-    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
-    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
-    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX},
-    {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}, {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX}};
-
-// acc[j] per lane -> returns the minimum over the wave of view `lane` (each butterfly step
-// keeps the half of the views that the lane's bit selects and takes the partner's copy).
-__device__ __forceinline__ int32_t wave_min_scatter(int32_t (&acc)[64], int lane) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const bool up = (lane & d) != 0;
-#pragma unroll
-    for (int i = 0; i < d; i++) {
-      const int32_t send = up ? acc[i] : acc[i + d];
-      const int32_t recv = __shfl_xor(send, d);
-      acc[i] = min(up ? acc[i + d] : acc[i], recv);
-    }
-  }
-  return acc[0];
-}
+// superstep.  Its static slots are cut into segments of <= kSegSlots, one wave each.  A
+// segment's wave loads 64 slots at a time (lane = slot) and then folds the kept / changed ones
+// with lane = view, as a normal vertex does (gather_min: the changed neighbours' label rows,
+// four coalesced row loads in flight); the segment's minima go to the hub's row in hbest with
+// one coalesced atomicMin.  (A lane = slot fold needs a 64-entry array per lane, which the
+// compiler demotes to scratch memory: measured 2x slower on C4.)
 
 // K2 for heavy vertices: compact each segment's kept slots (kept iff em[e] & vm[nb] & vm[v])
 // at its static position, record its count and mask OR, and fold the superstep-1 minima
@@ -1063,9 +1053,7 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
     const int64_t lo = seg_lo[sg], rel0 = lo - adj_off[v], o0 = out_off[v], i0 = in_off[v];
     const int64_t nout = out_off[v + 1] - o0;
     const int32_t ns = seg_n[sg];
-    int32_t acc[64];
-#pragma unroll
-    for (int j = 0; j < 64; j++) acc[j] = INT32_MAX;
+    int32_t best = INT32_MAX;  // lane = view
     int32_t count = 0;
     uint64_t any = 0;
     for (int32_t c = 0; c < ns; c += 64) {
@@ -1088,15 +1076,15 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
       count += __popcll(bal);
       any |= m;
       const int32_t lb = (grank && m) ? grank[nb] : nb;  // setup sends the neighbour's label (id)
-#pragma unroll
-      for (int j = 0; j < 64; j++) acc[j] = ((m >> j) & 1) ? min(acc[j], lb) : acc[j];
+      for (uint64_t b = bal; b; b &= b - 1) {  // lane = view from here: the kept slots one by one
+        const int L = __builtin_ctzll(b);
+        const int32_t q = __builtin_amdgcn_readlane(lb, L);
+        if ((readlane64(m, L) >> lane) & 1) best = min(best, q);
+      }
     }
     for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
     if (lane == 0) { segcnt[sg] = count; segor[sg] = any; }
-    if (any) {
-      const int32_t mn = wave_min_scatter(acc, lane);
-      if (mn != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], mn);
-    }
+    if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
   }
 }
 
@@ -1123,29 +1111,15 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
     const int32_t n = segcnt[sg];
     if (n == 0) continue;
     const int64_t base = seg_lo[sg];
-    int32_t acc[64];
-#pragma unroll
-    for (int j = 0; j < 64; j++) acc[j] = INT32_MAX;
-    uint64_t anyw = 0;
+    int32_t best = INT32_MAX;  // lane = view
     for (int32_t c = 0; c < n; c += 64) {
       const int32_t jj = c + lane;
       const int64_t idx = base + (jj < n ? jj : c);
       const int32_t q = snbr[idx];
       const uint64_t a = jj < n ? (smask[idx] & chg_prev[q]) : 0;
-      anyw |= a;
-      const int4* row = a ? reinterpret_cast<const int4*>(lab_cur + (int64_t)q * 64) : g_max_row;
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        const int4 x = row[k];
-        acc[4 * k + 0] = ((a >> (4 * k + 0)) & 1) ? min(acc[4 * k + 0], x.x) : acc[4 * k + 0];
-        acc[4 * k + 1] = ((a >> (4 * k + 1)) & 1) ? min(acc[4 * k + 1], x.y) : acc[4 * k + 1];
-        acc[4 * k + 2] = ((a >> (4 * k + 2)) & 1) ? min(acc[4 * k + 2], x.z) : acc[4 * k + 2];
-        acc[4 * k + 3] = ((a >> (4 * k + 3)) & 1) ? min(acc[4 * k + 3], x.w) : acc[4 * k + 3];
-      }
+      best = gather_min<false>(a, q, best, lab_cur, lane);  // lane = view: changed rows, 4 in flight
     }
-    if (__ballot(anyw != 0) == 0) continue;
-    const int32_t mn = wave_min_scatter(acc, lane);
-    if (mn != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], mn);
+    if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
   }
 }
 

@@ -183,7 +183,7 @@ struct rgpu_ctx {
   int tail_cap = 256;                   // RGPU_TAIL_CAP: widest frontier the tail kernel takes
   int64_t tail_maxv = 4 << 20;          // RGPU_TAIL_MAXV: no tail kernel above this many vertices
   std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
-  struct StepRec { int batch, step; unsigned long long pv, ps; int changed; };
+  struct StepRec { int batch, step; unsigned long long pv, ps; int changed; unsigned long long pg; };
   std::vector<StepRec> steprec;
   bool wmajor = true;                   // RGPU_WMAJOR: window-major batches when 2 <= W <= kMaxPlanes
   bool poll = true;                     // RGPU_POLL: spin on event queries instead of blocking
@@ -793,7 +793,7 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
             548.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1) + 4.0 * (double)wsum(r, 3);
       if (!c->trace_path.empty())
         for (int r = 1; r <= s.r_final; r++)
-          c->steprec.push_back({s.batch, r, wsum(r, 0), wsum(r, 1), (int)wsum(r, 2)});
+          c->steprec.push_back({s.batch, r, wsum(r, 0), wsum(r, 1), (int)wsum(r, 2), wsum(r, 3)});
     }
     c->st.supersteps += s.r_final;
     c->grp_last[grp] = s.r_final;
@@ -1960,16 +1960,16 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     for (int k = 0; k < KID_N; k++) c->st.launches += c->st.kernel_launches[k];
     FILE* tf = nullptr;
     if (!c->trace_path.empty() && (tf = std::fopen(c->trace_path.c_str(), "w")))
-      std::fprintf(tf, "kind,batch,step,kernel,ms,pv,ps,changed\n");
+      std::fprintf(tf, "kind,batch,step,kernel,ms,pv,ps,changed,pg\n");
     for (const Timed& tm : c->timed) {
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, tm.a, tm.b));
       c->st.kernel_ms[tm.kid] += ms;
-      if (tf) std::fprintf(tf, "L,%d,%d,%d,%.4f,,,\n", tm.batch, tm.step, tm.kid, ms);
+      if (tf) std::fprintf(tf, "L,%d,%d,%d,%.4f,,,,\n", tm.batch, tm.step, tm.kid, ms);
     }
     if (tf) {
       for (const auto& r : c->steprec)
-        std::fprintf(tf, "S,%d,%d,,,%llu,%llu,%d\n", r.batch, r.step, r.pv, r.ps, r.changed);
+        std::fprintf(tf, "S,%d,%d,,,%llu,%llu,%d,%llu\n", r.batch, r.step, r.pv, r.ps, r.changed, r.pg);
       std::fclose(tf);
     }
     c->steprec.clear();
