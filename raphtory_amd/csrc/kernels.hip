@@ -432,7 +432,10 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int32_t* __restrict__ segcnt,
                                                   const uint64_t* __restrict__ segor,
                                                   int32_t* __restrict__ hbest,
-                                                  unsigned long long* __restrict__ lanechg) {
+                                                  unsigned long long* __restrict__ lanechg,
+                                                  const int32_t* __restrict__ ts_e,
+                                                  const int32_t* __restrict__ ts_nb,
+                                                  const int64_t* __restrict__ ts_t, int64_t tcut) {
   __shared__ unsigned long long red[4];
   if (threadIdx.x < 4) red[threadIdx.x] = 0;
   __syncthreads();
@@ -504,13 +507,22 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     int32_t nb_keep = 0;
     for (int64_t c = 0; c < ntot; c += 64) {
       const int64_t j = c + lane;
+      if (ts_t && ts_t[base + c] < tcut) break;  // newest first: the rest are dead in every view
       uint64_t m = 0;
       int32_t nb = 0, lb = 0;
       if (j < ntot) {
         int64_t e;
-        if (j < nout) { e = o0 + j; nb = edst[e]; }
-        else { e = in_eid[i0 + (j - nout)]; nb = esrc[e]; }
-        if (nb != (int32_t)v) m = em[e] & vm[nb] & mv;
+        if (ts_e) {
+          e = ts_e[base + j];
+          nb = ts_nb[base + j];
+        } else if (j < nout) {
+          e = o0 + j;
+          nb = edst[e];
+        } else {
+          e = in_eid[i0 + (j - nout)];
+          nb = esrc[e];
+        }
+        if (nb != (int32_t)v && (!ts_t || ts_t[base + j] >= tcut)) m = em[e] & vm[nb] & mv;
         lb = grank ? grank[nb] : nb;
       }
       uint64_t bal = __ballot(m != 0);
@@ -1039,13 +1051,18 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
                                                      int32_t* __restrict__ snbr, uint64_t* __restrict__ smask,
                                                      int32_t* __restrict__ segcnt, uint64_t* __restrict__ segor,
                                                      int32_t* __restrict__ hbest, const int32_t* __restrict__ grank,
-                                                     int64_t n_own) {
+                                                     int64_t n_own, const int32_t* __restrict__ ts_e,
+                                                     const int32_t* __restrict__ ts_nb,
+                                                     const int64_t* __restrict__ ts_t, int64_t tcut) {
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
-    const uint64_t mv = v < n_own ? vm[v] : 0;  // a heavy ghost keeps no compacted slots
+    const int64_t lo0 = seg_lo[sg];
+    // a heavy ghost keeps no compacted slots; with time-ordered slots a segment whose newest
+    // edge predates the batch's cut keeps none either
+    const uint64_t mv = (v < n_own && !(ts_t && ts_t[lo0] < tcut)) ? vm[v] : 0;
     if (mv == 0) {
       if (lane == 0) { segcnt[sg] = 0; segor[sg] = 0; }
       continue;
@@ -1058,14 +1075,23 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
     uint64_t any = 0;
     for (int32_t c = 0; c < ns; c += 64) {
       const int32_t jj = c + lane;
+      if (ts_t && ts_t[lo + c] < tcut) break;
       uint64_t m = 0;
       int32_t nb = 0;
       if (jj < ns) {
         const int64_t rel = rel0 + jj;
         int64_t e;
-        if (rel < nout) { e = o0 + rel; nb = edst[e]; }
-        else { e = in_eid[i0 + (rel - nout)]; nb = esrc[e]; }
-        if (nb != v) m = em[e] & vm[nb] & mv;
+        if (ts_e) {
+          e = ts_e[lo + jj];
+          nb = ts_nb[lo + jj];
+        } else if (rel < nout) {
+          e = o0 + rel;
+          nb = edst[e];
+        } else {
+          e = in_eid[i0 + (rel - nout)];
+          nb = esrc[e];
+        }
+        if (nb != v && (!ts_t || ts_t[lo + jj] >= tcut)) m = em[e] & vm[nb] & mv;
       }
       const uint64_t bal = __ballot(m != 0);
       if (m) {
@@ -1687,7 +1713,7 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
   else k_edge_mask<false, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
 #undef RGPU_EM_ARGS
 }
-void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
@@ -1696,7 +1722,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
-                                                hb.segcnt, hb.segor, hb.best, lanechg);
+                                                hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut);
 }
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
@@ -1722,12 +1748,13 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   else k_cc_step2<4, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
 #undef RGPU_STEP_ARGS
 }
-void launch_heavy_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                         int32_t* snbr, uint64_t* smask, const HeavyBuf& hb) {
   if (g.n_seg <= 0) return;
   k_heavy_slots<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off,
                                                             g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
-                                                            snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own);
+                                                            snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own,
+                                                            g.ts_e, g.ts_nb, g.ts_t, tcut);
 }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,

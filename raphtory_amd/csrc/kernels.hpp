@@ -1,5 +1,6 @@
 // kernels.hpp — device-side graph view, batch parameters and kernel launchers.
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -41,7 +42,16 @@ struct DevGraph {
   const int32_t* seg_h = nullptr;   // [n_seg] heavy index of the segment
   const int64_t* seg_lo = nullptr;  // [n_seg] first static slot (absolute, = adj_off[v] + offset)
   const int32_t* seg_n = nullptr;   // [n_seg] static slots in the segment
+  // time-ordered static slots (tslots.hip; null: CSR order): per vertex newest last-add first
+  const int32_t* ts_e = nullptr;    // [ne + n_in] edge of the slot
+  const int32_t* ts_nb = nullptr;   // [ne + n_in] neighbour across it
+  const int64_t* ts_t = nullptr;    // [ne + n_in] the edge's last add time
 };
+// Builds ts_e / ts_nb / ts_t (device arrays of ne + n_in entries) for g; temporaries are
+// appended to `temps` (free them after the stream is synchronised).  False: not built (more
+// than 2^31 slots), the graph keeps CSR order.
+bool build_time_slots(hipStream_t s, const DevGraph& g, int32_t* ts_e, int32_t* ts_nb, int64_t* ts_t,
+                      std::vector<void*>& temps);
 constexpr int kSegSlots = 512;
 
 // Per-batch state of the heavy-vertex path (one per batch slot).
@@ -84,7 +94,8 @@ void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp,
 // ecnt[(h0 + k) * W + w] for hop k of the block (first hop h0 of the run) and window w
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
                       unsigned long long* ecnt = nullptr, int64_t h0 = 0);
-void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+// tcut: no view of the batch can keep an edge whose last add is older (time-ordered slots)
+void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
@@ -92,7 +103,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
 // (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
 // next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
-void launch_heavy_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
+void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                         int32_t* snbr, uint64_t* smask, const HeavyBuf& hb);
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,

@@ -190,6 +190,7 @@ struct rgpu_ctx {
   bool hostprof = false;                // RGPU_HOSTPROF: print host-side scheduling times
   int iv_max = 32;                      // RGPU_IVMAX: K1 interval form up to this many points (< 0 off)
   int heavy_t = 2048;                   // RGPU_HEAVY: static slots above which a vertex is split (0 off)
+  bool tslots_on = true;                // RGPU_TSLOTS: time-ordered static slots (tslots.hip)
   MaskSet mset[kMaskSets];
   int grp_last[kMaxPlanes] = {};        // supersteps of the last batch of each window group
   // last run: views (hop, win) -> batch (hop/K)*G + win/gsize, lane (win%gsize)*K + hop%K
@@ -614,6 +615,17 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     if (k > 0 && bp.hop[k] < bp.hop[k - 1]) bp.sorted = 0;
   }
   for (int w = 0; w < rc.W; w++) { bp.thr_v[w] = rc.thr_v[w]; bp.thr_e[w] = rc.thr_e[w]; }
+  // K2's cut: an edge is kept only where its floor point is an add no older than the window
+  // (age <= thr_e), so one whose last add is before min(hop) - max(window of the batch) is
+  // dead in every view of the batch
+  int64_t tcut = INT64_MIN;
+  {
+    const int w0 = rc.G == 1 ? 0 : grp * rc.gsize, w1 = rc.G == 1 ? rc.W : w0 + rc.gsize;
+    int64_t thr = 0, hmin = INT64_MAX;
+    for (int w = w0; w < w1; w++) thr = std::max(thr, rc.thr_e[w]);
+    for (int k = 0; k < bp.K; k++) hmin = std::min(hmin, bp.hop[k]);
+    if (thr < INT64_MAX / 4 && hmin > INT64_MIN / 4) tcut = hmin - thr;
+  }
   s.batch = b;
   s.kb = bp.K;
   s.r_launched = 0;
@@ -694,9 +706,9 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
     const double b2 = g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0;
     if (g.n_seg > 0)
-      timed_launch(c, si, KID_HEAVY, 0.0, [&] { launch_heavy_slots(s.stream, g, s.vm, s.em, s.snbr, s.smask, s.hv); });
+      timed_launch(c, si, KID_HEAVY, 0.0, [&] { launch_heavy_slots(s.stream, g, tcut, s.vm, s.em, s.snbr, s.smask, s.hv); });
     timed_launch(c, si, KID_SLOTS, b2, [&] {  // (partitioned: owned vertices only, gk)
-      launch_cc_slots(s.stream, gk, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
+      launch_cc_slots(s.stream, gk, tcut, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                       c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff);
     });
@@ -1404,6 +1416,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->hostprof = env_int("RGPU_HOSTPROF", 0) != 0;
   c->iv_max = env_int("RGPU_IVMAX", 32);
   c->heavy_t = env_int("RGPU_HEAVY", 2048);
+  c->tslots_on = env_int("RGPU_TSLOTS", 1) != 0;
   c->tail_cap = std::max(1, env_int("RGPU_TAIL_CAP", 256));
   c->tail_maxv = std::max(0, env_int("RGPU_TAIL_MAXV", 4 << 20));
   c->delta_on = env_int("RGPU_DELTA", 1) != 0;
@@ -1491,6 +1504,30 @@ void build_heavy(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L, const std::vec
   g.seg_h = dupload(L, seg_h);
   g.seg_lo = dupload(L, seg_lo);
   g.seg_n = dupload(L, seg_n);
+}
+
+// K2's time-ordered static slots (tslots.hip), built on the device after the adjacency
+void build_tslots(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L) {
+  const int64_t n = g.ne + g.n_in;
+  if (!c->tslots_on || n <= 0 || n > (int64_t)INT32_MAX) return;
+  int32_t* e = dalloc<int32_t>(L, n);
+  int32_t* nb = dalloc<int32_t>(L, n);
+  int64_t* t = dalloc<int64_t>(L, n);
+  std::vector<void*> T;
+  bool ok = false;
+  try {
+    ok = build_time_slots(nullptr, g, e, nb, t, T);
+    HIPCHK(hipDeviceSynchronize());
+  } catch (...) {
+    for (void* p : T) (void)hipFree(p);
+    throw;
+  }
+  for (void* p : T) (void)hipFree(p);
+  if (ok) {
+    g.ts_e = e;
+    g.ts_nb = nb;
+    g.ts_t = t;
+  }
 }
 
 const int64_t* upload_adj(std::vector<void*>& L, const std::vector<int64_t>& out_off,
@@ -1655,6 +1692,8 @@ void seal_delta(rgpu_ctx* c) {
     build_heavy(c, g, L, D.out_off, D.in_off);
     HIPCHK(hipStreamSynchronize(s));
     phase("heavy");
+    build_tslots(c, g, L);
+    phase("time-ordered slots");
     for (void* p : T) (void)hipFree(p);
     T.clear();
     (void)hipStreamDestroy(s);
@@ -1752,6 +1791,7 @@ int rgpu_seal(rgpu_ctx* c) {
     g.in_eid = dupload(L, P.in_eid);
     g.n_own = P.n_own;
     build_heavy(c, g, L, P.out_off, P.in_off);
+    build_tslots(c, g, L);
     if (c->partitioned) {  // CC labels are vertex ids (the label owner routes component counts)
       if (c->nparts > kMaxParts) return fail(c, RGPU_EINVAL, "more than 8 partitions");
       if (P.grank.empty())
