@@ -52,6 +52,35 @@ __device__ __forceinline__ void row_store(int32_t* row, int32_t x, bool on, int 
 // lanes of the 64-B lines (16 lanes each) that hold at least one view of mask m
 __device__ __forceinline__ bool line_has(uint64_t m, int lane) { return ((m >> (lane & 48)) & 0xffffull) != 0; }
 
+// Uniform label words (uw, one int32 per vertex and label buffer): when every member lane of
+// a vertex's row holds the same label x the row is kept as uw[v] = x alone (kMixed: the row in
+// the label buffer is the state).  A gather from a uniform neighbour costs its 4-B word, not
+// its 256-B row, and a uniform vertex neither reads nor writes its own row.  In a batch of
+// near-identical views (64 hourly hops of a year window) almost every row is uniform.  The
+// state of a vertex in a buffer is the pair (uw, row); every writer writes uw, and the row
+// only when mixed, so the "both buffers agree unless changed in the last two steps" rule of
+// the label rows carries over unchanged.  Rows are materialised (k_uw_rows) before anything
+// outside the superstep loop reads them.
+constexpr int32_t kMixed = -1;
+
+// fold the labels x (per lane = slot, wave-uniform loop over the lanes of `bal`) into best
+// (lane = view) on the views a of each slot
+__device__ __forceinline__ int32_t fold_uniform(uint64_t bal, uint64_t a, int32_t x, int32_t best, int lane) {
+  while (bal) {
+    const int L = __builtin_ctzll(bal);
+    bal &= bal - 1;
+    const int32_t q = __builtin_amdgcn_readlane(x, L);
+    if ((readlane64(a, L) >> lane) & 1) best = min(best, q);
+  }
+  return best;
+}
+
+// uw of a freshly computed row (lane = view, member lanes mv): x if uniform, else kMixed
+__device__ __forceinline__ int32_t row_uniform(int32_t best, uint64_t mv, int lane) {
+  const int32_t x0 = __builtin_amdgcn_readlane(best, __builtin_ctzll(mv));
+  return __ballot(((mv >> lane) & 1) && best != x0) ? kMixed : x0;
+}
+
 // floor(t) of a sorted key list (key = time*2 + alive): index of the last key <= 2t+1, or -1.
 __device__ __forceinline__ int64_t floor_idx(const int64_t* key, int64_t lo, int64_t hi, int64_t t) {
   const int64_t probe = 2 * t + 1;
@@ -435,7 +464,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   unsigned long long* __restrict__ lanechg,
                                                   const int32_t* __restrict__ ts_e,
                                                   const int32_t* __restrict__ ts_nb,
-                                                  const int64_t* __restrict__ ts_t, int64_t tcut) {
+                                                  const int64_t* __restrict__ ts_t, int64_t tcut,
+                                                  int32_t* __restrict__ uw0, int32_t* __restrict__ uw1) {
   __shared__ unsigned long long red[4];
   if (threadIdx.x < 4) red[threadIdx.x] = 0;
   __syncthreads();
@@ -467,8 +497,14 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       hbest[(int64_t)h * 64 + lane] = INT32_MAX;
       const int32_t best = own ? min(me, x) : me;
       if (own) {
-        row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
-        row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+        if (uw0) {  // label_0 = own rank on every member lane: uniform
+          const int32_t u = row_uniform(best, mv, lane);
+          if (lane == 0) { uw0[v] = me; uw1[v] = u; }
+          if (u == kMixed) row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+        } else {
+          row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
+          row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+        }
       }
       uint64_t any = 0;
       unsigned long long kept = 0;
@@ -499,7 +535,11 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     // from its owner in the step-1 exchange.
     const bool own = v < n_own;
     const int32_t me = grank ? grank[v] : (int32_t)v;
-    row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
+    if (uw0) {
+      if (lane == 0) uw0[v] = me;
+    } else {
+      row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
+    }
     const int64_t nout = o1 - o0, ntot = nout + (i1 - i0), base = o0 + i0;
     int32_t count = 0, best = me;
     uint64_t any = 0;
@@ -544,7 +584,13 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         if (((mL >> lane) & 1) && q < best) best = q;
       }
     }
-    row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+    if (uw1) {
+      const int32_t u = row_uniform(best, mv, lane);
+      if (lane == 0) uw1[v] = u;
+      if (u == kMixed) row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+    } else {
+      row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+    }
     const uint64_t ch = __ballot(best < me);
     if (lane == 0) { cnt[v] = count; vadj[v] = any; chg1[v] = ch; }
     if (!own) continue;
@@ -712,7 +758,7 @@ __device__ __forceinline__ void mark(bool want, int32_t v, uint8_t* act_next, co
 // count in vmcnt, so interleaving them with the next vertex's loads would serialise the
 // chunk.  All loads are unconditional from padded buffers (see gather_min).  A visited
 // vertex rewrites its row only if it changed now or in the previous step (the only cases
-// where the two label buffers differ).
+// where the two label buffers differ).  uw_cur / uw_next: uniform label words (null: rows only).
 template <int CH, bool BUF, bool TAIL>
 __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_t* __restrict__ adj_off,
                                          const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
@@ -725,7 +771,9 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          unsigned long long* __restrict__ lds_lanes,
                                          unsigned long long& pv, unsigned long long& ps,
                                          unsigned long long& pg, const int32_t* __restrict__ hv_of = nullptr,
-                                         int32_t* __restrict__ hbest = nullptr) {
+                                         int32_t* __restrict__ hbest = nullptr,
+                                         const int32_t* __restrict__ uw_cur = nullptr,
+                                         int32_t* __restrict__ uw_next = nullptr) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
@@ -734,12 +782,15 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     const int32_t hh_l = (okl && hv_of) ? hv_of[vl] : -1;
     const int64_t b_l = adj_off[vl];
     const uint64_t cp_l = chg_prev[vl];
+    const int32_t u_l = uw_cur ? uw_cur[vl] : kMixed;
     int64_t vv[CH];
     int32_t cur[CH];
 #pragma unroll
     for (int i = 0; i < CH; i++) {
       vv[i] = (int64_t)readlane64((uint64_t)vl, i);
-      cur[i] = row_get<BUF>(lab_cur + vv[i] * 64, (readlane64(mv_l, i) >> lane) & 1, lane);
+      const int32_t u = __builtin_amdgcn_readlane(u_l, i);
+      if (u != kMixed) cur[i] = u;  // wave-uniform: no row load
+      else cur[i] = row_get<BUF>(lab_cur + vv[i] * 64, (readlane64(mv_l, i) >> lane) & 1, lane);
     }
     // stage 2: first 64 kept slots of each vertex (clamped loads, masked by select)
     int32_t nb[CH];
@@ -754,25 +805,38 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       nb[i] = lane < n ? q : 0;
       sm[i] = lane < n ? m : 0;
     }
-    // stage 3: neighbours' change words (vertex 0's word for idle lanes, masked by sm = 0)
+    // stage 3: neighbours' change words (vertex 0's word for idle lanes, masked by sm = 0),
+    // then the uniform words of the neighbours that changed
     uint64_t act[CH];
 #pragma unroll
     for (int i = 0; i < CH; i++) {
       act[i] = sm[i] & chg_prev[nb[i]];
       pg += __popcll(act[i]);  // labels this lane's slot gathers (per lane; summed at the end)
     }
+    int32_t un[CH];
+#pragma unroll
+    for (int i = 0; i < CH; i++) un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
     // own rows are only meaningful on member lanes
 #pragma unroll
     for (int i = 0; i < CH; i++) cur[i] = ((readlane64(mv_l, i) >> lane) & 1) ? cur[i] : INT32_MAX;
-    // stage 4a: all gathers of the chunk (loads only)
+    // stage 4a: all gathers of the chunk (loads only): rows of the mixed neighbours, then the
+    // uniform ones' words
     int32_t best[CH];
+    uint64_t actr[CH];
 #pragma unroll
-    for (int i = 0; i < CH; i++) best[i] = cur[i];
+    for (int i = 0; i < CH; i++) {
+      best[i] = cur[i];
+      actr[i] = un[i] == kMixed ? act[i] : 0;
+    }
     if constexpr (CH == 4) {
-      gather_min_x4<BUF>(act, nb, best, lab_cur, lane);
+      gather_min_x4<BUF>(actr, nb, best, lab_cur, lane);
     } else {
 #pragma unroll
-      for (int i = 0; i < CH; i++) best[i] = gather_min<BUF>(act[i], nb[i], cur[i], lab_cur, lane);
+      for (int i = 0; i < CH; i++) best[i] = gather_min<BUF>(actr[i], nb[i], best[i], lab_cur, lane);
+    }
+    if (uw_cur) {
+#pragma unroll
+      for (int i = 0; i < CH; i++) best[i] = fold_uniform(__ballot(un[i] != kMixed), act[i], un[i], best[i], lane);
     }
 #pragma unroll
     for (int i = 0; i < CH; i++) {
@@ -785,7 +849,9 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
           const int32_t q = snbr[idx];
           const uint64_t a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
           pg += __popcll(a2);
-          best[i] = gather_min<BUF>(a2, q, best[i], lab_cur, lane);
+          const int32_t u2 = (uw_cur && a2) ? uw_cur[q] : kMixed;
+          best[i] = gather_min<BUF>(u2 == kMixed ? a2 : 0, q, best[i], lab_cur, lane);
+          if (uw_cur) best[i] = fold_uniform(__ballot(u2 != kMixed), a2, u2, best[i], lane);
         }
       }
     }
@@ -813,8 +879,12 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       ps += (unsigned long long)n;
       const uint64_t ch = __ballot(best[i] < cur[i]);
       if (ch || readlane64(cp_l, i)) {
-        if (BUF) row_store(lab_next + v * 64, best[i], line_has(mv, lane), lane);
-        else lab_next[v * 64 + lane] = best[i];
+        const int32_t u = uw_next ? row_uniform(best[i], mv, lane) : kMixed;
+        if (uw_next && lane == 0) uw_next[v] = u;
+        if (u == kMixed) {
+          if (BUF) row_store(lab_next + v * 64, best[i], line_has(mv, lane), lane);
+          else lab_next[v * 64 + lane] = best[i];
+        }
       }
       if (lane == 0) chg_next[v] = ch;
       if (ch) {
@@ -832,6 +902,24 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
           }
         }
       }
+    }
+  }
+}
+
+// Rows of the uniform vertices written out (lane = view, member lines only): after the last
+// superstep, for the readers outside the loop (component counts, retained labels).
+__global__ __launch_bounds__(256) void k_uw_rows(int64_t nv, const uint64_t* __restrict__ vm,
+                                                 const int32_t* __restrict__ uw, int32_t* __restrict__ lab) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t b0 = wave * 64; b0 < nv; b0 += nwaves * 64) {
+    const int64_t vl = b0 + lane;
+    const uint64_t mvl = vl < nv ? vm[vl] : 0;
+    const int32_t ul = vl < nv ? uw[vl] : kMixed;
+    for (uint64_t todo = __ballot(mvl != 0 && ul != kMixed); todo; todo &= todo - 1) {
+      const int L = __builtin_ctzll(todo);
+      row_store(lab + (b0 + L) * 64, __builtin_amdgcn_readlane(ul, L), line_has(readlane64(mvl, L), lane), lane);
     }
   }
 }
@@ -857,7 +945,8 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
                                                   unsigned long long* __restrict__ work,
                                                   const int32_t* __restrict__ hv_of,
                                                   int32_t* __restrict__ hbest,
-                                                  unsigned long long* __restrict__ lanechg) {
+                                                  unsigned long long* __restrict__ lanechg,
+                                                  const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next) {
   if (stepflag[step - 1] == 0) return;
   __shared__ int32_t red;
   __shared__ unsigned long long wred[4];
@@ -894,7 +983,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
       cc_chunk<CH, BUF, false>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
                                lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[3], pv, ps, pg,
-                               hv_of, hbest);
+                               hv_of, hbest, uw_cur, uw_next);
     }
   }
   if (work)
@@ -1126,7 +1215,8 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       const uint64_t* __restrict__ chg_prev,
                                                       const uint8_t* __restrict__ act_cur,
                                                       const int32_t* __restrict__ stepflag,
-                                                      int32_t* __restrict__ hbest, int64_t n_own) {
+                                                      int32_t* __restrict__ hbest, int64_t n_own,
+                                                      const int32_t* __restrict__ uw_cur) {
   if (stepflag[step - 1] == 0) return;
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -1143,7 +1233,10 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
       const int64_t idx = base + (jj < n ? jj : c);
       const int32_t q = snbr[idx];
       const uint64_t a = jj < n ? (smask[idx] & chg_prev[q]) : 0;
-      best = gather_min<false>(a, q, best, lab_cur, lane);  // lane = view: changed rows, 4 in flight
+      // lane = view: the changed mixed rows (4 in flight), then the uniform neighbours' words
+      const int32_t u = (uw_cur && a) ? uw_cur[q] : kMixed;
+      best = gather_min<false>(u == kMixed ? a : 0, q, best, lab_cur, lane);
+      if (uw_cur) best = fold_uniform(__ballot(u != kMixed), a, u, best, lane);
     }
     if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
   }
@@ -1341,6 +1434,170 @@ __global__ __launch_bounds__(256) void k_cc_summary(int64_t nv, int32_t* __restr
     if (a) {
       if (f == 0) atomicMax(&stats[j], a);
       else atomicAdd(&stats[f * 64 + j], a);
+    }
+  }
+}
+
+// ---- component counts from the uniform label words (one partition, kernels.hip kMixed).
+// k_cc_count: counts[label][view] (rows of 64, the root's row) += members carrying the label,
+// lane = vertex, 64 vertices per wave round.  Uniform members with the same (label, views) are
+// one row-wide atomicAdd per group; the wave keeps its most recent group in registers across
+// rounds (a giant component costs one atomic per wave, not per 64 vertices).  Mixed members
+// add their row's labels lane = view.  Every add goes through a 64-row LDS cache of count rows
+// (claimed first come, keyed by label): a giant component's root row takes one global atomic
+// per block and view instead of one per member group (month/week batches, where members'
+// view sets differ, measured 16-94 ms per batch without it on C4).  Isolated members (no kept
+// slot in the view) are islands: counted per view into iso[shard][view] as k_cc_hist does.
+// k_cc_roots: every root (a member whose label in the view is its own rank and that has a kept
+// slot there) reads its count row, folds it into the processBatchWindowResults fields per view
+// (ConnectedComponents.scala:137-145) and zeroes it again, so the count rows stay zero between
+// batches without a memset; block 0 also folds the island shards.  A batch cut off by maxSteps
+// before it converged has labels whose own label is smaller (label of a vertex within
+// maxSteps hops): scan_all then reads the count row of every non-isolated member.
+__global__ __launch_bounds__(256) void k_cc_count(int64_t nv, uint64_t vmask, const uint64_t* __restrict__ vm,
+                                                  const uint64_t* __restrict__ vadj,
+                                                  const int32_t* __restrict__ uw,
+                                                  const int32_t* __restrict__ lab,
+                                                  int32_t* __restrict__ counts, unsigned int* __restrict__ iso_g) {
+  constexpr int kRows = 64;
+  __shared__ unsigned int iso[64];
+  __shared__ int32_t ckey[kRows];
+  __shared__ unsigned int crow[kRows][64];
+  if (threadIdx.x < 64) iso[threadIdx.x] = 0;
+  if (threadIdx.x < kRows) ckey[threadIdx.x] = -1;
+  for (int i = threadIdx.x; i < kRows * 64; i += blockDim.x) (&crow[0][0])[i] = 0;
+  __syncthreads();
+  auto add = [&](int32_t x, int j, unsigned int c) {  // counts[x][j] += c
+    const int h0 = (int)(((uint32_t)x * 2654435761u) >> 26);
+    for (int p = 0; p < 4; p++) {  // four probes, then the global row
+      const int h = (h0 + p) & (kRows - 1);
+      int32_t k = ckey[h];
+      if (k == -1) {
+        k = atomicCAS(&ckey[h], -1, x);
+        if (k == -1) k = x;
+      }
+      if (k == x) {
+        atomicAdd(&crow[h][j], c);
+        return;
+      }
+    }
+    atomicAdd(&counts[(int64_t)x * 64 + j], (int32_t)c);
+  };
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned int iso_acc = 0;              // lane = view
+  int32_t sx = -1;                       // the wave's pending group: label, views, members
+  uint64_t sm = 0;
+  int32_t sc = 0;
+  for (int64_t b0 = wave * 64; b0 < nv; b0 += nwaves * 64) {
+    const int64_t v = b0 + lane;
+    const uint64_t mv = v < nv ? vm[v] & vmask : 0;
+    const uint64_t ad = v < nv ? vadj[v] : 0;
+    const int32_t x = v < nv ? uw[v] : kMixed;
+    iso_acc += (unsigned)__popcll(transpose64(mv & ~ad, lane));
+    const uint64_t m = mv & ad;
+    uint64_t todo = __ballot(m != 0 && x != kMixed);
+    while (todo) {
+      const int L = __builtin_ctzll(todo);
+      const int32_t xL = __builtin_amdgcn_readlane(x, L);
+      const uint64_t mL = readlane64(m, L);
+      const uint64_t same = __ballot(((todo >> lane) & 1) && x == xL && m == mL);
+      todo &= ~same;
+      if (xL == sx && mL == sm) {
+        sc += __popcll(same);
+      } else {
+        if (sc && ((sm >> lane) & 1)) add(sx, lane, (unsigned)sc);
+        sx = xL;
+        sm = mL;
+        sc = __popcll(same);
+      }
+    }
+    for (uint64_t mixed = __ballot(m != 0 && x == kMixed); mixed; mixed &= mixed - 1) {
+      const int L = __builtin_ctzll(mixed);
+      const uint64_t mL = readlane64(m, L);
+      if ((mL >> lane) & 1) add(lab[(b0 + L) * 64 + lane], lane, 1u);
+    }
+  }
+  if (sc && ((sm >> lane) & 1)) add(sx, lane, (unsigned)sc);
+  if (iso_acc) atomicAdd(&iso[lane], iso_acc);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kRows * 64; i += blockDim.x) {
+    const unsigned int c = (&crow[0][0])[i];
+    if (c) atomicAdd(&counts[(int64_t)ckey[i >> 6] * 64 + (i & 63)], (int32_t)c);
+  }
+  if (threadIdx.x < 64 && iso[threadIdx.x])
+    atomicAdd(&iso_g[(blockIdx.x & 63) * 64 + threadIdx.x], iso[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void k_cc_roots(int64_t nv, uint64_t vmask, const uint64_t* __restrict__ vm,
+                                                  const uint64_t* __restrict__ vadj,
+                                                  const int32_t* __restrict__ uw,
+                                                  const int32_t* __restrict__ lab, int32_t* __restrict__ counts,
+                                                  unsigned long long* __restrict__ stats,
+                                                  unsigned int* __restrict__ iso_g, int scan_all) {
+  __shared__ unsigned long long red[6][64];
+  for (int i = threadIdx.x; i < 6 * 64; i += blockDim.x) (&red[0][0])[i] = 0;
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < 64) {  // islands: count 1 each
+    const int j = threadIdx.x;
+    unsigned long long k = 0;
+    for (int sh = 0; sh < 64; sh++) {
+      const unsigned int x = iso_g[sh * 64 + j];
+      if (x) { k += x; iso_g[sh * 64 + j] = 0; }
+    }
+    if (k) {
+      atomicMax(&stats[0 * 64 + j], 1ull);
+      atomicAdd(&stats[1 * 64 + j], k);
+      atomicAdd(&stats[4 * 64 + j], k);
+    }
+  }
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned long long big = 0, tot = 0, nis = 0, gt2 = 0, sum = 0, snis = 0;  // lane = view
+  for (int64_t b0 = wave * 64; b0 < nv; b0 += nwaves * 64) {
+    const int64_t v = b0 + lane;
+    const uint64_t m = v < nv ? vm[v] & vmask & vadj[v] : 0;
+    const int32_t x = v < nv ? uw[v] : kMixed;
+    for (uint64_t cand = __ballot(m != 0 && (scan_all || x == (int32_t)v || x == kMixed)); cand; cand &= cand - 1) {
+      const int L = __builtin_ctzll(cand);
+      const int64_t r = b0 + L;
+      const uint64_t mL = readlane64(m, L);
+      const bool in = (mL >> lane) & 1;
+      const bool root = scan_all || __builtin_amdgcn_readlane(x, L) != kMixed ? in
+                                                                            : (in && lab[r * 64 + lane] == (int32_t)r);
+      const int32_t c = root ? counts[r * 64 + lane] : 0;
+      if (c) {
+        counts[r * 64 + lane] = 0;
+        const unsigned long long uc = (unsigned long long)c;
+        big = uc > big ? uc : big;
+        tot += 1;
+        nis += c > 1;
+        gt2 += c > 2;
+        sum += uc;
+        snis += c > 1 ? uc : 0;
+      }
+    }
+  }
+  if (tot) {
+    atomicMax(&red[0][lane], big);
+    atomicAdd(&red[1][lane], tot);
+    atomicAdd(&red[2][lane], nis);
+    atomicAdd(&red[3][lane], gt2);
+    atomicAdd(&red[4][lane], sum);
+    atomicAdd(&red[5][lane], snis);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int j = threadIdx.x;
+    if (red[1][j]) {
+      atomicMax(&stats[0 * 64 + j], red[0][j]);
+      atomicAdd(&stats[1 * 64 + j], red[1][j]);
+      atomicAdd(&stats[2 * 64 + j], red[2][j]);
+      atomicAdd(&stats[3 * 64 + j], red[3][j]);
+      atomicAdd(&stats[4 * 64 + j], red[4][j]);
+      atomicAdd(&stats[5 * 64 + j], red[5][j]);
     }
   }
 }
@@ -1717,19 +1974,35 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
-                     unsigned long long* lanechg) {
+                     unsigned long long* lanechg, int32_t* uw0, int32_t* uw1) {
   const bool hv = g.n_seg > 0;
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
-                                                hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut);
+                                                hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
+                                                uw0, uw1);
+}
+void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
+  k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
+}
+void launch_cc_count(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, const uint64_t* vadj,
+                     const int32_t* uw, const int32_t* lab, int32_t* counts, unsigned int* iso) {
+  const uint64_t vmask = nviews >= 64 ? ~0ull : ((1ull << nviews) - 1);
+  k_cc_count<<<grid_for(nv, 256, 4096), 256, 0, s>>>(nv, vmask, vm, vadj, uw, lab, counts, iso);
+}
+void launch_cc_roots(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, const uint64_t* vadj,
+                     const int32_t* uw, const int32_t* lab, int32_t* counts, unsigned long long* stats,
+                     unsigned int* iso, bool scan_all) {
+  const uint64_t vmask = nviews >= 64 ? ~0ull : ((1ull << nviews) - 1);
+  k_cc_roots<<<grid_for(nv, 256, 4096), 256, 0, s>>>(nv, vmask, vm, vadj, uw, lab, counts, stats, iso,
+                                                     scan_all ? 1 : 0);
 }
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
-                    unsigned long long* work, int variant, unsigned long long* lanechg, int32_t* hbest) {
+                    unsigned long long* work, int variant, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next) {
   const int ch = (variant & 15) == 8 ? 8 : 4;
   const bool buf = (variant & 16) != 0;
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
@@ -1741,7 +2014,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   const unsigned grid = grid_for(g.nv, 4 * ch, cap);
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
-    act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg
+    act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next
   if (ch == 8 && buf) k_cc_step2<8, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (ch == 8) k_cc_step2<8, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (buf) k_cc_step2<4, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
@@ -1758,11 +2031,11 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
 }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
-                         const int32_t* stepflag, int step, const HeavyBuf& hb) {
+                         const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur) {
   if (g.n_seg <= 0) return;
   k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
-                                                             hb.best, g.n_own);
+                                                             hb.best, g.n_own, uw_cur);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,

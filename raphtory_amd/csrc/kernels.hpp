@@ -99,7 +99,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
-                     unsigned long long* lanechg);
+                     unsigned long long* lanechg, int32_t* uw0 = nullptr, int32_t* uw1 = nullptr);
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
 // (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
 // next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
@@ -107,7 +107,7 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
                         int32_t* snbr, uint64_t* smask, const HeavyBuf& hb);
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
-                         const int32_t* stepflag, int step, const HeavyBuf& hb);
+                         const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr);
 // vm/em (partitioned mode): heavy ghosts (ranks >= n_own) have no compacted slots; their kept
 // slots are recomputed from the static adjacency (em & vm[nb] & vm[v]) while marking
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
@@ -119,13 +119,22 @@ extern int g_hist_rounds;  // label-dedup rounds per (view, chunk) in k_cc_hist 
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
 extern int g_rowbuf;     // label rows via buffer descriptors (RGPU_ROWBUF)
 extern int g_tail_step, g_tail_grid;  // supersteps >= tail_step use at most tail_grid blocks
+// uniform label words (kernels.hip, kMixed): rows of the uniform vertices written into lab
+void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab);
+// component counts from the uniform words (one partition): counts = zeroed [nv][64] rows, kept
+// zero by launch_cc_roots, which also folds iso and writes the summary fields into stats
+void launch_cc_count(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, const uint64_t* vadj,
+                     const int32_t* uw, const int32_t* lab, int32_t* counts, unsigned int* iso);
+void launch_cc_roots(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, const uint64_t* vadj,
+                     const int32_t* uw, const int32_t* lab, int32_t* counts, unsigned long long* stats,
+                     unsigned int* iso, bool scan_all);
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, int variant, unsigned long long* lanechg,
-                    int32_t* hbest = nullptr);
+                    int32_t* hbest = nullptr, const int32_t* uw_cur = nullptr, int32_t* uw_next = nullptr);
 // Many late supersteps in one single-workgroup launch while the frontier stays below `cap`
 // vertices; info[0] <- last superstep executed (host-mapped).
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,

@@ -66,6 +66,8 @@ struct Slot {
   int32_t *cnt = nullptr, *snbr = nullptr;
   uint64_t* smask = nullptr;
   int32_t* lab[2] = {nullptr, nullptr};
+  int32_t* uw[2] = {nullptr, nullptr};    // uniform label words of lab[0/1] (kernels.hip kMixed)
+  int32_t* counts = nullptr;              // [nv][64] component counts at the root (zero between batches)
   uint64_t* chg[2] = {nullptr, nullptr};
   int32_t *stepcnt = nullptr, *hist = nullptr;   // stepcnt[r] = 1 iff superstep r changed a label
   uint8_t* act[3] = {nullptr, nullptr, nullptr};   // CC frontier flags (byte per vertex)
@@ -180,6 +182,7 @@ struct rgpu_ctx {
   bool hostflags = true;                // superstep flags via host-mapped memory (else copies)
   int step_variant = 0;                 // RGPU_STEP_VARIANT: 0 per-vertex chain, 1 chunk-pipelined
   bool tail_on = false;                 // RGPU_TAIL: late supersteps in one-workgroup k_cc_tail launches
+  bool uw_on = true;                    // RGPU_UW: uniform label words (one partition, no tail kernel)
   int tail_cap = 256;                   // RGPU_TAIL_CAP: widest frontier the tail kernel takes
   int64_t tail_maxv = 4 << 20;          // RGPU_TAIL_MAXV: no tail kernel above this many vertices
   std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
@@ -285,6 +288,10 @@ hipEvent_t take_event(rgpu_ctx* c) {
 
 // Run `fn` (one kernel launch) on slot stream, bracketed by events in profile mode.
 // evented = false: the caller brackets a group of launches itself (see launch_chunk).
+// uniform label words (kernels.hip): one partition (ghost rows arrive as per-lane records) and
+// no tail kernel (it writes rows only)
+bool use_uw(const rgpu_ctx* c) { return c->uw_on && !c->partitioned && !c->tail_on; }
+
 template <class F>
 void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn, int step = 0, bool evented = true) {
   Slot& s = c->slot[si];
@@ -362,6 +369,12 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       s.smask = dalloc<uint64_t>(L, ne + nin + kPad);
       s.lab[0] = dalloc<int32_t>(L, rows + kPad * kViews);
       s.lab[1] = dalloc<int32_t>(L, rows + kPad * kViews);
+      s.uw[0] = dalloc<int32_t>(L, nv + kPad);
+      s.uw[1] = dalloc<int32_t>(L, nv + kPad);
+      if (use_uw(c)) {
+        s.counts = dalloc<int32_t>(L, rows + kPad * kViews);
+        HIPCHK(hipMemset(s.counts, 0, sizeof(int32_t) * (rows + kPad * kViews)));
+      }
       s.chg[0] = dalloc<uint64_t>(L, nv + kPad);
       s.chg[1] = dalloc<uint64_t>(L, nv + kPad);
       HIPCHK(hipMemset(s.chg[0], 0, sizeof(uint64_t) * (nv + kPad)));
@@ -470,6 +483,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     HIPCHK(hipEventRecord(ea, s.stream));
   }
   const bool hv = g.n_seg > 0 && rc.algo == RGPU_ALGO_CC;
+  const bool uw = use_uw(c);
   for (int r = s.r_launched + 1; r <= last; r++) {
     if (rc.algo == RGPU_ALGO_DIFFUSION) {
       timed_launch(c, si, KID_DIFF, 0.0, [&] {
@@ -483,14 +497,14 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     if (hv)  // heavy vertices: segment minima before the step, neighbour marking after it
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[(r - 1) & 1], s.chg[(r - 1) & 1], s.act[r % 3],
-                            s.stepcnt, r, s.hv);
+                            s.stepcnt, r, s.hv, uw ? s.uw[(r - 1) & 1] : nullptr);
       }, r, false);
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                      s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
                      s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                      c->profile ? s.work : nullptr, c->step_variant | (g_rowbuf ? 16 : 0), s.stats + kLaneOff,
-                     hv ? s.hv.best : nullptr);
+                     hv ? s.hv.best : nullptr, uw ? s.uw[(r - 1) & 1] : nullptr, uw ? s.uw[r & 1] : nullptr);
     }, r, false);
     if (hv)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
@@ -571,12 +585,23 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
   Slot& s = c->slot[si];
   const DevGraph& g = c->g;
   if (rc.algo == RGPU_ALGO_CC) {
-    const int32_t* lab = s.lab[s.r_final & 1];
+    int32_t* lab = s.lab[s.r_final & 1];
+    const int nviews = rc.K * rc.gsize;
+    if (use_uw(c)) {
+      const int32_t* uw = s.uw[s.r_final & 1];
+      if (rc.flags & RGPU_RUN_RETAIN) launch_uw_rows(s.stream, g.nv, s.vm, uw, lab);  // full rows to the host
+      timed_launch(c, si, KID_HIST, 28.0 * g.nv,
+                   [&] { launch_cc_count(s.stream, g.nv, nviews, s.vm, s.vadj, uw, lab, s.counts, s.iso); });
+      timed_launch(c, si, KID_SUMMARY, 20.0 * g.nv,
+                   [&] { launch_cc_roots(s.stream, g.nv, nviews, s.vm, s.vadj, uw, lab, s.counts, s.stats, s.iso,
+                                           s.r_final >= 1 && s.r_final >= rc.max_steps); });
+      finish_tail(c, si, rc);
+      return;
+    }
     // the other label buffer is free now: it becomes the view-major histogram (keeps the
     // batch's working set inside the Infinity Cache with several batches in flight)
     int32_t* hist = s.lab[(s.r_final + 1) & 1];
     HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)g.nv * kViews, s.stream));
-    const int nviews = rc.K * rc.gsize;
     timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g.nv, g.nv, nviews, s.vm, s.vadj, lab, hist, s.iso); });
     timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * nviews,
                  [&] { launch_cc_summary(s.stream, g, nviews, hist, s.stats, s.iso); });
@@ -710,7 +735,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     timed_launch(c, si, KID_SLOTS, b2, [&] {  // (partitioned: owned vertices only, gk)
       launch_cc_slots(s.stream, gk, tcut, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
-                      c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff);
+                      c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff, use_uw(c) ? s.uw[0] : nullptr,
+                      use_uw(c) ? s.uw[1] : nullptr);
     });
     if (g.n_seg > 0 && !c->partitioned)  // partitioned: after the step's records are in
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
@@ -1411,6 +1437,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   if (env_int("RGPU_TAIL_GRID", 0) > 0) g_tail_grid = env_int("RGPU_TAIL_GRID", 0);
   c->hostflags = env_int("RGPU_HOSTFLAG", 1) != 0;
   c->tail_on = env_int("RGPU_TAIL", 0) != 0;
+  c->uw_on = env_int("RGPU_UW", 1) != 0;
   c->wmajor = env_int("RGPU_WMAJOR", 1) != 0;
   c->poll = env_int("RGPU_POLL", 1) != 0;
   c->hostprof = env_int("RGPU_HOSTPROF", 0) != 0;

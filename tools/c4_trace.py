@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 from raphtory_amd import TemporalGraph  # noqa: E402
 from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops  # noqa: E402
 
-KID = {0: "window_mask", 1: "cc_slots", 2: "cc_step", 3: "cc_tail", 4: "cc_hist", 5: "cc_summary"}
+KID = {0: "window_mask", 1: "cc_slots", 2: "cc_step", 3: "cc_hist", 4: "cc_summary", 7: "cc_tail", 8: "heavy"}
 
 
 def main():
