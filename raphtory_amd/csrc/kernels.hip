@@ -413,16 +413,33 @@ void launch_lane_fold(hipStream_t s, unsigned long long* lanechg, unsigned long 
 // on one word cost more than a sparse superstep).  Layout work[(step*64 + shard)*4 + f],
 // f = visited vertices, visited slots, changed vertices, gathered labels.  Only written when
 // work != nullptr (profile / trace runs).  The halting vote is a plain flag store instead.
+// Profile-run work counters, [step][shard][kWorkFields] (rgpu.cpp turns them into bytes):
+//   supersteps: 0 visited vertices, 1 their kept slots, 2 changed vertices, 3 label lanes
+//   gathered from mixed rows, 4 slots whose neighbour's uniform word was read, 5 own-row 64-B
+//   lines read, 6 row lines written, 7 uniform words written;
+//   superstep 1 (K2): 0 members, 1 kept slots, 2 changed, 4 static slots scanned, 6, 7 as above.
+__device__ __forceinline__ void add_work(unsigned long long* work, int step, const unsigned long long (&f)[8]) {
+  if (!work) return;
+  unsigned long long* w = work + ((size_t)step * 64 + (blockIdx.x & 63)) * 8;
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if (f[i]) atomicAdd(&w[i], f[i]);
+}
 __device__ __forceinline__ void add_work(unsigned long long* work, int step, unsigned long long a,
                                          unsigned long long b, unsigned long long c,
                                          unsigned long long d = 0) {
-  if (!work) return;
-  unsigned long long* w = work + ((size_t)step * 64 + (blockIdx.x & 63)) * 4;
-  if (a) atomicAdd(&w[0], a);
-  if (b) atomicAdd(&w[1], b);
-  if (c) atomicAdd(&w[2], c);
-  if (d) atomicAdd(&w[3], d);
+  const unsigned long long f[8] = {a, b, c, d, 0, 0, 0, 0};
+  add_work(work, step, f);
 }
+// 64-B lines of a label row holding the lanes of m
+__device__ __forceinline__ unsigned row_lines(uint64_t m) {
+  return (unsigned)((m & 0xffffull) != 0) + ((m >> 16 & 0xffffull) != 0) + ((m >> 32 & 0xffffull) != 0) +
+         ((m >> 48) != 0);
+}
+// superstep work of one wave (g per lane, the rest wave-uniform)
+struct StepWork {
+  unsigned long long v = 0, s = 0, g = 0, a = 0, lr = 0, lw = 0, uw = 0;
+};
 
 // ---------------------------------------------------------------- K2: batch CSR (+ superstep 1)
 // One wave per vertex.  Static slots of rank v = its out-edges then its in-edges
@@ -472,7 +489,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  unsigned long long members = 0, alive = 0, changed = 0;
+  unsigned long long members = 0, alive = 0, changed = 0, scanned = 0, lw = 0, uwn = 0;
   uint64_t lanes = 0;  // views with a step-1 change in this wave
   // 64 vertices per wave round: the lanes read their view masks (one coalesced load), clear the
   // non-members' count / mask words, and the wave then walks the members one by one
@@ -548,6 +565,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     for (int64_t c = 0; c < ntot; c += 64) {
       const int64_t j = c + lane;
       if (ts_t && ts_t[base + c] < tcut) break;  // newest first: the rest are dead in every view
+      scanned += ntot - c < 64 ? ntot - c : 64;
       uint64_t m = 0;
       int32_t nb = 0, lb = 0;
       if (j < ntot) {
@@ -588,8 +606,11 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       const int32_t u = row_uniform(best, mv, lane);
       if (lane == 0) uw1[v] = u;
       if (u == kMixed) row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+      uwn += 2;
+      if (u == kMixed) lw += row_lines(mv);
     } else {
       row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+      lw += 2 * row_lines(mv);
     }
     const uint64_t ch = __ballot(best < me);
     if (lane == 0) { cnt[v] = count; vadj[v] = any; chg1[v] = ch; }
@@ -623,6 +644,10 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       if (hostflag) hostflag[1] = 1;
     }
     add_work(work, 1, red[0], red[1], red[2]);
+  }
+  if (work && lane == 0) {  // (uniform per wave)
+    const unsigned long long f[8] = {0, 0, 0, 0, scanned, 0, lw, uwn};
+    add_work(work, 1, f);
   }
 }
 
@@ -769,8 +794,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          uint64_t* __restrict__ chg_next, uint8_t* __restrict__ act_next,
                                          const TailList& tl, int lane, int32_t& changed,
                                          unsigned long long* __restrict__ lds_lanes,
-                                         unsigned long long& pv, unsigned long long& ps,
-                                         unsigned long long& pg, const int32_t* __restrict__ hv_of = nullptr,
+                                         StepWork& wk, const int32_t* __restrict__ hv_of = nullptr,
                                          int32_t* __restrict__ hbest = nullptr,
                                          const int32_t* __restrict__ uw_cur = nullptr,
                                          int32_t* __restrict__ uw_next = nullptr) {
@@ -789,8 +813,12 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     for (int i = 0; i < CH; i++) {
       vv[i] = (int64_t)readlane64((uint64_t)vl, i);
       const int32_t u = __builtin_amdgcn_readlane(u_l, i);
-      if (u != kMixed) cur[i] = u;  // wave-uniform: no row load
-      else cur[i] = row_get<BUF>(lab_cur + vv[i] * 64, (readlane64(mv_l, i) >> lane) & 1, lane);
+      if (u != kMixed) {
+        cur[i] = u;  // wave-uniform: no row load
+      } else {
+        cur[i] = row_get<BUF>(lab_cur + vv[i] * 64, (readlane64(mv_l, i) >> lane) & 1, lane);
+        wk.lr += row_lines(readlane64(mv_l, i));
+      }
     }
     // stage 2: first 64 kept slots of each vertex (clamped loads, masked by select)
     int32_t nb[CH];
@@ -811,11 +839,14 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
 #pragma unroll
     for (int i = 0; i < CH; i++) {
       act[i] = sm[i] & chg_prev[nb[i]];
-      pg += __popcll(act[i]);  // labels this lane's slot gathers (per lane; summed at the end)
     }
     int32_t un[CH];
 #pragma unroll
-    for (int i = 0; i < CH; i++) un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
+    for (int i = 0; i < CH; i++) {
+      un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
+      if (uw_cur) wk.a += __popcll(__ballot(act[i] != 0));
+      wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
+    }
     // own rows are only meaningful on member lanes
 #pragma unroll
     for (int i = 0; i < CH; i++) cur[i] = ((readlane64(mv_l, i) >> lane) & 1) ? cur[i] : INT32_MAX;
@@ -848,8 +879,9 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
           const int64_t idx = base + (j < n ? j : c2);
           const int32_t q = snbr[idx];
           const uint64_t a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
-          pg += __popcll(a2);
           const int32_t u2 = (uw_cur && a2) ? uw_cur[q] : kMixed;
+          if (uw_cur) wk.a += __popcll(__ballot(a2 != 0));
+          wk.g += u2 == kMixed ? __popcll(a2) : 0;
           best[i] = gather_min<BUF>(u2 == kMixed ? a2 : 0, q, best[i], lab_cur, lane);
           if (uw_cur) best[i] = fold_uniform(__ballot(u2 != kMixed), a2, u2, best[i], lane);
         }
@@ -875,15 +907,17 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       if (mv == 0) continue;
       const int64_t v = vv[i];
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
-      pv += 1;
-      ps += (unsigned long long)n;
+      wk.v += 1;
+      wk.s += (unsigned long long)n;
       const uint64_t ch = __ballot(best[i] < cur[i]);
       if (ch || readlane64(cp_l, i)) {
         const int32_t u = uw_next ? row_uniform(best[i], mv, lane) : kMixed;
         if (uw_next && lane == 0) uw_next[v] = u;
+        if (uw_next) wk.uw += 1;
         if (u == kMixed) {
           if (BUF) row_store(lab_next + v * 64, best[i], line_has(mv, lane), lane);
           else lab_next[v * 64 + lane] = best[i];
+          wk.lw += BUF ? row_lines(mv) : 4;
         }
       }
       if (lane == 0) chg_next[v] = ch;
@@ -949,8 +983,9 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
                                                   const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next) {
   if (stepflag[step - 1] == 0) return;
   __shared__ int32_t red;
-  __shared__ unsigned long long wred[4];
-  if (threadIdx.x == 0) { red = 0; wred[0] = 0; wred[1] = 0; wred[2] = 0; wred[3] = 0; }
+  __shared__ unsigned long long wred[8];  // [0..6] work fields (StepWork), [7] changed views (LDS OR)
+  if (threadIdx.x < 8) wred[threadIdx.x] = 0;
+  if (threadIdx.x == 0) red = 0;
   const int64_t nwords = (nv + 7) >> 3;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -960,7 +995,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int32_t changed = 0;
-  unsigned long long pv = 0, ps = 0, pg = 0;
+  StepWork wk;
   const TailList none{nullptr, nullptr};
   // 64 chunks per wave round: lane l reads chunk l's frontier flags (one coalesced load), and
   // the wave then runs only the flagged chunks — a sparse frontier costs one load per 64 chunks
@@ -982,25 +1017,31 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
       todo &= todo - 1;
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
       cc_chunk<CH, BUF, false>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
-                               lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[3], pv, ps, pg,
+                               lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
                                hv_of, hbest, uw_cur, uw_next);
     }
   }
   if (work)
-    for (int o = 32; o > 0; o >>= 1) pg += __shfl_xor(pg, o);
+    for (int o = 32; o > 0; o >>= 1) wk.g += __shfl_xor(wk.g, o);
   if (lane == 0) {
     if (changed) atomicAdd(&red, changed);
-    if (pv) atomicAdd(&wred[0], pv);
-    if (ps) atomicAdd(&wred[1], ps);
-    if (pg) atomicAdd(&wred[2], pg);
+    if (work) {
+      const unsigned long long f[7] = {wk.v, wk.s, 0, wk.g, wk.a, wk.lr, wk.lw};
+#pragma unroll
+      for (int i = 0; i < 7; i++)
+        if (f[i]) atomicAdd(&wred[i], f[i]);
+      if (wk.uw) atomicAdd(&wred[2], wk.uw);  // (slot 2 is free: the changed count has `red`)
+    }
   }
-  publish_lanes(0, &wred[3], lanechg, step);
+  publish_lanes(0, &wred[7], lanechg, step);
   if (threadIdx.x == 0) {
     if (red && stepflag[step] == 0) {  // first writers also tell the host (mapped pinned memory)
       stepflag[step] = 1;
       if (hostflag) hostflag[step] = 1;
     }
-    add_work(work, step, wred[0], wred[1], (unsigned long long)red, wred[2]);
+    const unsigned long long f[8] = {wred[0], wred[1], (unsigned long long)red, wred[3], wred[4], wred[5], wred[6],
+                                     wred[2]};
+    add_work(work, step, f);
   }
 }
 
@@ -1081,13 +1122,15 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
     uint64_t* chg_next = (s & 1) ? chg1 : chg0;
     const TailList tl{list[p ^ 1], &nlist[p ^ 1]};
     int32_t changed = 0;
-    unsigned long long pv = 0, ps = 0, pg = 0;
+    StepWork wk;
     for (int c = wid * 4; c < ncur; c += nw * 4) {
       const int k = c + (lane & 3) < ncur ? c + (lane & 3) : c;
       const uint32_t bits = ncur - c >= 4 ? 0xfu : ((1u << (ncur - c)) - 1);
       cc_chunk<4, BUF, true>((int64_t)list[p][k], bits, adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
-                             chg_prev, chg_next, a_next, tl, lane, changed, &wsum[3], pv, ps, pg);
+                             chg_prev, chg_next, a_next, tl, lane, changed, &wsum[3], wk);
     }
+    const unsigned long long pv = wk.v, ps = wk.s;
+    unsigned long long pg = wk.g;
     for (int o = 32; o > 0; o >>= 1) pg += __shfl_xor(pg, o);
     if (lane == 0) {
       if (changed) atomicAdd(&nchanged, changed);

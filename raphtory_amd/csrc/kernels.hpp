@@ -128,6 +128,12 @@ void launch_cc_count(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, 
 void launch_cc_roots(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, const uint64_t* vadj,
                      const int32_t* uw, const int32_t* lab, int32_t* counts, unsigned long long* stats,
                      unsigned int* iso, bool scan_all);
+// RGPU_CHECK (check.hip): structural checks, violations counted into bad[16]
+void launch_check_graph(hipStream_t s, const DevGraph& g, int64_t n_ekey, int64_t n_vkey, unsigned long long* bad);
+void launch_check_labels(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, const int32_t* lab,
+                         unsigned long long* bad);
+void launch_check_slots(hipStream_t s, int64_t nv, const int64_t* adj_off, const uint64_t* vm, const int32_t* cnt,
+                        const int32_t* snbr, const int32_t* uw0, const int32_t* uw1, unsigned long long* bad);
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,

@@ -52,7 +52,8 @@ constexpr int kFoldOff = 7 * kViews;
 constexpr int kLaneOff = kFoldOff + kLaneSteps;
 constexpr int kStatCopy = kLaneOff;
 constexpr int kStatWords = kLaneOff + kLaneChgWords;
-constexpr int kWorkWords = kMaxSteps * 64 * 4;
+constexpr int kWorkFields = 8;  // kernels.hip add_work
+constexpr int kWorkWords = kMaxSteps * 64 * kWorkFields;
 constexpr int64_t kPad = 64;  // tail padding of per-vertex / per-slot batch arrays
 constexpr int kMaxSlots = 4;  // batches in flight (one HIP stream each; GPU_MAX_HW_QUEUES = 4)
 
@@ -183,6 +184,7 @@ struct rgpu_ctx {
   int step_variant = 0;                 // RGPU_STEP_VARIANT: 0 per-vertex chain, 1 chunk-pipelined
   bool tail_on = false;                 // RGPU_TAIL: late supersteps in one-workgroup k_cc_tail launches
   bool uw_on = true;                    // RGPU_UW: uniform label words (one partition, no tail kernel)
+  bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
   int tail_cap = 256;                   // RGPU_TAIL_CAP: widest frontier the tail kernel takes
   int64_t tail_maxv = 4 << 20;          // RGPU_TAIL_MAXV: no tail kernel above this many vertices
   std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
@@ -223,11 +225,22 @@ struct rgpu_ctx {
 
 namespace {
 
+// RGPU_POISON=1 (tests): every fresh device buffer starts as 0xa5 bytes, so a read of memory
+// no kernel wrote shows up deterministically instead of depending on what the allocator reuses
+int g_poison = -1;
 template <class T>
 T* dalloc(std::vector<void*>& list, size_t n) {
   void* p = nullptr;
   HIPCHK(hipMalloc(&p, sizeof(T) * (n ? n : 1)));
   list.push_back(p);
+  if (g_poison < 0) {
+    const char* e = std::getenv("RGPU_POISON");
+    g_poison = e && std::atoi(e) != 0;
+  }
+  if (g_poison) {  // (synchronised: the batch streams are non-blocking, a null-stream memset does not order them)
+    HIPCHK(hipMemset(p, 0xa5, sizeof(T) * (n ? n : 1)));
+    HIPCHK(hipDeviceSynchronize());
+  }
   return (T*)p;
 }
 template <class T>
@@ -288,6 +301,23 @@ hipEvent_t take_event(rgpu_ctx* c) {
 
 // Run `fn` (one kernel launch) on slot stream, bracketed by events in profile mode.
 // evented = false: the caller brackets a group of launches itself (see launch_chunk).
+// RGPU_CHECK: run a check launcher on `st`, wait, and fail with the violation counts
+template <class F>
+void run_check(hipStream_t st, const char* what, F launch) {
+  unsigned long long* bad = nullptr;
+  HIPCHK(hipMalloc(&bad, 16 * sizeof(unsigned long long)));
+  unsigned long long h[16] = {};
+  HIPCHK(hipMemsetAsync(bad, 0, sizeof(h), st));
+  launch(bad);
+  HIPCHK(hipMemcpyAsync(h, bad, sizeof(h), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  (void)hipFree(bad);
+  std::string msg;
+  for (int i = 0; i < 16; i++)
+    if (h[i]) msg += " bad[" + std::to_string(i) + "]=" + std::to_string(h[i]);
+  if (!msg.empty()) throw HipFail{std::string("RGPU_CHECK ") + what + ":" + msg, RGPU_EHIP};
+}
+
 // uniform label words (kernels.hip): one partition (ghost rows arrive as per-lane records) and
 // no tail kernel (it writes rows only)
 bool use_uw(const rgpu_ctx* c) { return c->uw_on && !c->partitioned && !c->tail_on; }
@@ -587,6 +617,10 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (rc.algo == RGPU_ALGO_CC) {
     int32_t* lab = s.lab[s.r_final & 1];
     const int nviews = rc.K * rc.gsize;
+    if (c->check)
+      run_check(s.stream, "final labels", [&](unsigned long long* bad) {
+        launch_check_labels(s.stream, g.nv, s.vm, use_uw(c) ? s.uw[s.r_final & 1] : nullptr, lab, bad);
+      });
     if (use_uw(c)) {
       const int32_t* uw = s.uw[s.r_final & 1];
       if (rc.flags & RGPU_RUN_RETAIN) launch_uw_rows(s.stream, g.nv, s.vm, uw, lab);  // full rows to the host
@@ -729,7 +763,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   if (rc.algo == RGPU_ALGO_CC) {
     // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
-    const double b2 = g.nv * (8.0 + 32.0 + 512.0 + 20.0) + (double)(g.ne + g.n_in) * 24.0;
+    const double b2 = 8.0 * g.nv;  // the view-mask scan; the rest from the work counters (harvest)
     if (g.n_seg > 0)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] { launch_heavy_slots(s.stream, g, tcut, s.vm, s.em, s.snbr, s.smask, s.hv); });
     timed_launch(c, si, KID_SLOTS, b2, [&] {  // (partitioned: owned vertices only, gk)
@@ -738,6 +772,11 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
                       c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff, use_uw(c) ? s.uw[0] : nullptr,
                       use_uw(c) ? s.uw[1] : nullptr);
     });
+    if (c->check)
+      run_check(s.stream, "after K2", [&](unsigned long long* bad) {
+        launch_check_slots(s.stream, gk.nv, g.adj_off, s.vm, s.cnt, s.snbr, use_uw(c) ? s.uw[0] : nullptr,
+                           use_uw(c) ? s.uw[1] : nullptr, bad);
+      });
     if (g.n_seg > 0 && !c->partitioned)  // partitioned: after the step's records are in
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[1], s.act[2], s.stepcnt, 1, s.hv, nullptr);
@@ -809,26 +848,35 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
       }
     }
   if (rc.algo == RGPU_ALGO_CC) {
-    // superstep bytes, per executed step r >= 2: frontier bitmap read + the
-    // bitmap two steps ahead cleared (8 B per 32 vertices); per visited vertex vm, cnt,
-    // adj_off, label row in and out, change word (540 B); per slot of a visited vertex nbr,
-    // mask and the neighbour's change word (20 B).  Label gathers are not counted.
+    // algorithmic bytes from the profile run's work counters (kernels.hip
+    // add_work).  K2 (superstep 1), on top of the 8 B per vertex of the view-mask scan counted
+    // at launch: per non-member cnt + vadj cleared (12 B); per member its four offsets, cnt,
+    // vadj and change word (52 B); per static slot scanned the time-ordered slot (edge 4,
+    // neighbour 4, last-add time 8) and the two random mask words em[e], vm[nbr] (32 B; CSR
+    // order: offsets 8 instead of 16); per kept slot nbr + mask written (12 B); uniform words
+    // (4 B) and 64-B row lines written.  Supersteps r >= 2: frontier flag read + flag cleared
+    // two steps ahead (2 B per vertex; a tail-kernel step reads none); per visited vertex vm,
+    // cnt, adj_off, own change and uniform words in, change word out (40 B); per kept slot of
+    // a visited vertex nbr + mask + the neighbour's change word (20 B); per slot whose
+    // neighbour changed its uniform word (4 B); per label lane gathered from a mixed row 4 B;
+    // own row lines read and row lines written (64 B each); uniform words written (4 B).
     if (c->profile) {
       auto wsum = [&](int r, int f) {
         unsigned long long t = 0;
-        for (int k = 0; k < 64; k++) t += s.h_work[((size_t)r * 64 + k) * 4 + f];
+        for (int k = 0; k < 64; k++) t += s.h_work[((size_t)r * 64 + k) * kWorkFields + f];
         return t;
       };
-      c->st.kernel_bytes[KID_SLOTS] += 12.0 * (double)wsum(1, 1);
-      // per executed step: frontier flags read + flags two steps ahead cleared (2 B per
-      // vertex); per visited vertex vm, cnt, adj_off, own change word, label row in and out,
-      // change word out (548 B); per slot of a visited vertex nbr + mask + neighbour's change
-      // word (20 B); per gathered label (a neighbour's label in a view where it changed) 4 B.
-      // Flag stores are not counted.  (A tail-kernel step reads no bitmap: its frontier is a
-      // list in LDS.)
+      {
+        const double mem = (double)wsum(1, 0);
+        c->st.kernel_bytes[KID_SLOTS] += 12.0 * ((double)c->g.nv - mem) + 52.0 * mem +
+                                         (c->g.ts_e ? 32.0 : 24.0) * (double)wsum(1, 4) + 12.0 * (double)wsum(1, 1) +
+                                         4.0 * (double)wsum(1, 7) + 64.0 * (double)wsum(1, 6);
+      }
       for (int r = 2; r <= s.r_final; r++)
-        c->st.kernel_bytes[s.by_tail[r] ? KID_TAIL : KID_STEP] += (s.by_tail[r] ? 0.0 : 2.0 * c->g.nv) +
-            548.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1) + 4.0 * (double)wsum(r, 3);
+        c->st.kernel_bytes[s.by_tail[r] ? KID_TAIL : KID_STEP] +=
+            (s.by_tail[r] ? 0.0 : 2.0 * c->g.nv) + 40.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1) +
+            4.0 * (double)wsum(r, 4) + 4.0 * (double)wsum(r, 3) + 64.0 * (double)(wsum(r, 5) + wsum(r, 6)) +
+            4.0 * (double)wsum(r, 7);
       if (!c->trace_path.empty())
         for (int r = 1; r <= s.r_final; r++)
           c->steprec.push_back({s.batch, r, wsum(r, 0), wsum(r, 1), (int)wsum(r, 2), wsum(r, 3)});
@@ -1438,6 +1486,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->hostflags = env_int("RGPU_HOSTFLAG", 1) != 0;
   c->tail_on = env_int("RGPU_TAIL", 0) != 0;
   c->uw_on = env_int("RGPU_UW", 1) != 0;
+  c->check = env_int("RGPU_CHECK", 0) != 0;
   c->wmajor = env_int("RGPU_WMAJOR", 1) != 0;
   c->poll = env_int("RGPU_POLL", 1) != 0;
   c->hostprof = env_int("RGPU_HOSTPROF", 0) != 0;
@@ -1792,6 +1841,10 @@ int rgpu_seal(rgpu_ctx* c) {
       seal_delta(c);
       c->st.seal_incremental = 1;
       finish_seal(c);
+      if (c->check)
+        run_check(nullptr, "merged graph", [&](unsigned long long* bad) {
+          launch_check_graph(nullptr, c->g, c->pk.n_ekey, c->pk.n_vkey, bad);
+        });
       c->st.seal_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       return RGPU_OK;
     }
@@ -1852,7 +1905,12 @@ int rgpu_seal(rgpu_ctx* c) {
     }
     c->g = g;
     HIPCHK(hipDeviceSynchronize());
+    const int64_t nek = P.n_ekey, nvk = P.n_vkey;
     finish_seal(c);
+    if (c->check)
+      run_check(nullptr, "sealed graph", [&](unsigned long long* bad) {
+        launch_check_graph(nullptr, c->g, nek, nvk, bad);
+      });
   } catch (const HipFail& f) {
     return fail(c, f.code ? f.code : RGPU_EHIP, f.msg);
   } catch (const std::bad_alloc&) {
@@ -1987,6 +2045,9 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->timed.clear();
     for (int k = 0; k < KID_N; k++) { c->st.kernel_launches[k] = 0; c->st.kernel_ms[k] = 0; c->st.kernel_bytes[k] = 0; }
     c->st.views = c->st.batches = c->st.supersteps = 0;
+    // the buffers above were allocated and cleared on the null stream, which does not order
+    // the batch slots' non-blocking streams: everything lands before the first batch kernel
+    HIPCHK(hipDeviceSynchronize());
     auto t0 = std::chrono::steady_clock::now();
     c->pt.bytes_sent = 0;
     for (XSlot& xs : c->pt.xs) xs.bytes[0] = xs.bytes[1] = xs.bytes[2] = 0;
