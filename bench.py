@@ -345,12 +345,14 @@ def run_c4(a, rank, world, local):
     if a.profile_only:
         ms_per_step = value = None
     log(f"rank {rank}: query {ms_per_step} ms")
-    summ = g.cc_summaries()
+    summ = None if a.profile_only else g.cc_summaries()  # (profile-only: after the profile pass)
     roofline, ks, s8d = None, {}, None
     if not a.no_profile_pass:
         g.run("cc", hops, windows, profile=True, serial=True)  # collective at N > 1
         ks = kernel_table(g.stats())
         kraw = g.stats()["kernels"]
+        if summ is None:
+            summ = g.cc_summaries()
         d = kraw["cc_step"]
         gbs = d["bytes"] / (d["ms"] / 1e3) / 1e9
         traffic, tsrc = pmc_traffic("k_cc_step2", config="C4")

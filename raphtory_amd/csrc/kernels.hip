@@ -1305,7 +1305,10 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
                                                     const int32_t* __restrict__ esrc,
                                                     const int32_t* __restrict__ edst,
                                                     const uint64_t* __restrict__ vm,
-                                                    const uint64_t* __restrict__ em) {
+                                                    const uint64_t* __restrict__ em,
+                                                    const int32_t* __restrict__ ts_e,
+                                                    const int32_t* __restrict__ ts_nb,
+                                                    const int64_t* __restrict__ ts_t, int64_t tcut) {
   if (stepflag[step] == 0) return;
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -1318,16 +1321,26 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
     if (v >= n_own) {  // heavy ghost (partitioned): its static slots of the segment, kept on the fly
       if (!vm || !em) continue;
       const uint64_t mv = vm[v] & ch;
-      const int64_t rel0 = seg_lo[sg] - adj_off[v], o0 = out_off[v], i0 = in_off[v];
+      const int64_t lo = seg_lo[sg], rel0 = lo - adj_off[v], o0 = out_off[v], i0 = in_off[v];
       const int64_t nout = out_off[v + 1] - o0;
       const int32_t ns = seg_n[sg];
       for (int32_t c = 0; c < ns; c += 64) {
+        if (ts_t && ts_t[lo + c] < tcut) break;  // time-ordered slots: the rest predate the batch
         if (c + lane >= ns) continue;
         const int64_t rel = rel0 + c + lane;
         int64_t e;
         int32_t nb;
-        if (rel < nout) { e = o0 + rel; nb = edst[e]; }
-        else { e = in_eid[i0 + (rel - nout)]; nb = esrc[e]; }
+        if (ts_e) {
+          if (ts_t[lo + c + lane] < tcut) continue;
+          e = ts_e[lo + c + lane];
+          nb = ts_nb[lo + c + lane];
+        } else if (rel < nout) {
+          e = o0 + rel;
+          nb = edst[e];
+        } else {
+          e = in_eid[i0 + (rel - nout)];
+          nb = esrc[e];
+        }
         if (nb != v && (em[e] & vm[nb] & mv)) act_next[nb] = 1;
       }
       continue;
@@ -2082,12 +2095,13 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
-                       const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm, const uint64_t* em) {
+                       const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm, const uint64_t* em,
+                       int64_t tcut) {
   if (g.n_seg <= 0) return;
   k_heavy_mark<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
                                                            chg_now, act_cur, act_next, stepflag, g.n_own, g.seg_n,
                                                            g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst,
-                                                           vm, em);
+                                                           vm, em, g.ts_e, g.ts_nb, g.ts_t, tcut);
 }
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,

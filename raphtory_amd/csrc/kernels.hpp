@@ -113,7 +113,7 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
                        const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm = nullptr,
-                       const uint64_t* em = nullptr);
+                       const uint64_t* em = nullptr, int64_t tcut = INT64_MIN);
 extern int g_sum_blocks;   // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 extern int g_hist_rounds;  // label-dedup rounds per (view, chunk) in k_cc_hist (RGPU_HIST_ROUNDS)
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
@@ -199,11 +199,11 @@ void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32
                        int planes, const uint64_t* in, uint64_t* vm, int64_t vstride);
 void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t* xv, const int32_t* xq,
                       const uint8_t* act, const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab,
-                      XRec* sbuf, unsigned long long* scnt);
+                      const int32_t* uw, XRec* sbuf, unsigned long long* scnt);
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa);
 void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg);
 void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
-                        uint64_t* chg);
+                        uint64_t* chg, int32_t* uw = nullptr);
 void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
                   const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next);
 // owned id -> owned rank: ids ascend with rank; bucket b = id >> shift covers ranks

@@ -94,6 +94,7 @@ struct Slot {
   unsigned long long* h_stats = nullptr;
   // state of the batch in flight
   int batch = -1, phase = 0, r_launched = 0, r_final = 0, kb = 0;
+  int64_t tcut = INT64_MIN;  // the batch's window cut for time-ordered slots (start_batch)
   bool tail_pending = false;       // a k_cc_tail launch is in the last enqueued chunk
   uint8_t by_tail[kMaxSteps] = {}; // superstep r ran inside k_cc_tail (bytes accounting)
   uint64_t evseq = 0;  // order in which slot events were recorded (wait on the oldest)
@@ -318,9 +319,9 @@ void run_check(hipStream_t st, const char* what, F launch) {
   if (!msg.empty()) throw HipFail{std::string("RGPU_CHECK ") + what + ":" + msg, RGPU_EHIP};
 }
 
-// uniform label words (kernels.hip): one partition (ghost rows arrive as per-lane records) and
-// no tail kernel (it writes rows only)
-bool use_uw(const rgpu_ctx* c) { return c->uw_on && !c->partitioned && !c->tail_on; }
+// uniform label words (kernels.hip): not with the tail kernel (it writes rows only).  Partitioned:
+// ghost rows arrive as per-lane records, so the ghosts' words stay kMixed (start_batch)
+bool use_uw(const rgpu_ctx* c) { return c->uw_on && !c->tail_on; }
 
 template <class F>
 void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn, int step = 0, bool evented = true) {
@@ -401,7 +402,7 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       s.lab[1] = dalloc<int32_t>(L, rows + kPad * kViews);
       s.uw[0] = dalloc<int32_t>(L, nv + kPad);
       s.uw[1] = dalloc<int32_t>(L, nv + kPad);
-      if (use_uw(c)) {
+      if (use_uw(c) && !c->partitioned) {  // (partitioned: counts go to the label owner, xchg.hip)
         s.counts = dalloc<int32_t>(L, rows + kPad * kViews);
         HIPCHK(hipMemset(s.counts, 0, sizeof(int32_t) * (rows + kPad * kViews)));
       }
@@ -621,7 +622,7 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
       run_check(s.stream, "final labels", [&](unsigned long long* bad) {
         launch_check_labels(s.stream, g.nv, s.vm, use_uw(c) ? s.uw[s.r_final & 1] : nullptr, lab, bad);
       });
-    if (use_uw(c)) {
+    if (use_uw(c) && !c->partitioned) {
       const int32_t* uw = s.uw[s.r_final & 1];
       if (rc.flags & RGPU_RUN_RETAIN) launch_uw_rows(s.stream, g.nv, s.vm, uw, lab);  // full rows to the host
       timed_launch(c, si, KID_HIST, 28.0 * g.nv,
@@ -685,6 +686,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     for (int k = 0; k < bp.K; k++) hmin = std::min(hmin, bp.hop[k]);
     if (thr < INT64_MAX / 4 && hmin > INT64_MIN / 4) tcut = hmin - thr;
   }
+  s.tcut = tcut;
   s.batch = b;
   s.kb = bp.K;
   s.r_launched = 0;
@@ -761,6 +763,9 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     return;
   }
   if (rc.algo == RGPU_ALGO_CC) {
+    if (c->partitioned && use_uw(c) && g.nv > c->pk.n_own)  // ghosts: rows from records, words kMixed
+      for (int p = 0; p < 2; p++)
+        HIPCHK(hipMemsetAsync(s.uw[p] + c->pk.n_own, 0xff, sizeof(int32_t) * (g.nv - c->pk.n_own), s.stream));
     // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
     const double b2 = 8.0 * g.nv;  // the view-mask scan; the rest from the work counters (harvest)
@@ -1114,7 +1119,7 @@ void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
   }
   const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
   launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
-                   s.lab[r & 1], xs.sbuf, xs.scnt);
+                   s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt);
   launch_xcounts(s.stream, P, c->part, xs.scnt, s.stepcnt + r, xs.xab);
   HIPCHK(hipGetLastError());
   xs.x->alltoall_i64(xs.xab, xs.xab + 2 * P, 2, s.stream);
@@ -1144,7 +1149,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     grow_regions(&xs.sbuf, xs.scap, sent, P, s.stream);
     const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
     launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
-                     s.lab[r & 1], xs.sbuf, xs.scnt);
+                     s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt);
     HIPCHK(hipMemsetAsync(xs.scnt, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
   }
   if (!any) {  // every partition voted to halt
@@ -1191,7 +1196,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   }
   std::copy(recv, recv + kMaxParts, xs.rcnt[par]);
   const XPeers Lin = peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]);
-  launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par]);
+  launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par], use_uw(c) ? s.uw[par] : nullptr);
   launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3]);
   // the vote is global: superstep r+1 runs here even if nothing changed here
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(s.stepcnt + r), 1, 1, s.stream));
@@ -1199,7 +1204,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (hv)  // neighbours of heavy vertices (owned ones visited in r, ghosts just received) that changed
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[par], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
-                        r == 1 ? nullptr : s.act[r % 3], s.vm, s.em);
+                        r == 1 ? nullptr : s.act[r % 3], s.vm, s.em, s.tcut);
     });
   HIPCHK(hipGetLastError());
   // superstep r+1 over the owned vertices
@@ -1207,12 +1212,14 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   const DevGraph go = owned_view(c);
   if (hv)
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
-      launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[n % 3], s.stepcnt, n, s.hv);
+      launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[n % 3], s.stepcnt, n, s.hv,
+                          use_uw(c) ? s.uw[r & 1] : nullptr);
     });
   timed_launch(c, si, KID_STEP, 0.0, [&] {
     launch_cc_step(s.stream, n, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[r & 1], s.lab[n & 1], s.chg[r & 1],
                    s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
-                   c->profile ? s.work : nullptr, c->step_variant, s.stats + kLaneOff, hv ? s.hv.best : nullptr);
+                   c->profile ? s.work : nullptr, c->step_variant, s.stats + kLaneOff, hv ? s.hv.best : nullptr,
+                   use_uw(c) ? s.uw[r & 1] : nullptr, use_uw(c) ? s.uw[n & 1] : nullptr);
   }, n);
   part_post_step(c, si, rc, n);
 }
@@ -1232,6 +1239,8 @@ void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc) {
     for (int q = 0; q < P; q++) need[q] = no;
     grow_regions(&xs.hsbuf, xs.hscap, need, P, s.stream);
   }
+  if (use_uw(c))  // the owned uniform rows written out for the label owners' counts (and retained rows)
+    launch_uw_rows(s.stream, no, s.vm, s.uw[s.r_final & 1], s.lab[s.r_final & 1]);
   int32_t* hist = s.lab[(s.r_final + 1) & 1];  // the free label buffer: [view][owned rank]
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)no * kViews, s.stream));
   const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);

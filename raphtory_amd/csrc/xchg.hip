@@ -86,7 +86,8 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
                                                    const int32_t* __restrict__ xq, const uint8_t* __restrict__ act,
                                                    const uint64_t* __restrict__ chg_now,
                                                    const uint64_t* __restrict__ vadj,
-                                                   const int32_t* __restrict__ lab, XRec* __restrict__ sbuf,
+                                                   const int32_t* __restrict__ lab,
+                                                   const int32_t* __restrict__ uw, XRec* __restrict__ sbuf,
                                                    unsigned long long* __restrict__ scnt) {
   const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -106,7 +107,8 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
       const int32_t vL = __builtin_amdgcn_readlane(v, L);
       const int qL = __builtin_amdgcn_readlane(q, L);
       uint64_t mm = rl64(m, L);
-      const int32_t x = lab[(int64_t)vL * 64 + lane];
+      const int32_t uL = uw ? uw[vL] : -1;  // a uniform row is its word (kernels.hip kMixed = -1)
+      const int32_t x = uL != -1 ? uL : lab[(int64_t)vL * 64 + lane];
       int n = 0;
       while (mm) {
         const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
@@ -123,7 +125,8 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
       const int qL = __builtin_amdgcn_readlane(q, L);
       const int32_t eL = (int32_t)(c * 64 + L - P.xoff[qL]);
       uint64_t mm = rl64(m, L);
-      const int32_t x = lab[(int64_t)vL * 64 + lane];
+      const int32_t uL = uw ? uw[vL] : -1;
+      const int32_t x = uL != -1 ? uL : lab[(int64_t)vL * 64 + lane];
       while (mm) {
         const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
         const uint64_t same = __ballot(((mm >> lane) & 1) && x == val);
@@ -132,7 +135,7 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
         if (lane == 0 && pos < (unsigned long long)P.cap[qL]) {
           XRec r;
           r.e = eL;
-          r.val = val;
+          r.val = uL != -1 ? (int32_t)((uint32_t)val | 0x80000000u) : val;  // sign bit: sender uniform
           r.mask = same;
           sbuf[P.base[qL] + pos] = r;
         }
@@ -167,10 +170,13 @@ __global__ __launch_bounds__(256) void k_xclear(XPeers P, const XRec* __restrict
 
 // Records into ghost rows: the record's label in its views, and its views into the ghost's
 // change word (a ghost's records arrive together; the OR collects them).  A wave takes four
-// records, 16 lanes each covering the 64 views in 4 passes.
+// records, 16 lanes each covering the 64 views in 4 passes.  A record whose sender's row is
+// uniform (sign bit of val; it is then the ghost's only record of the step) sets the ghost's
+// uniform word instead of its row: readers only gather a ghost in the views its change word
+// holds, which are the record's.  Other records mark the ghost mixed (kernels.hip kMixed).
 __global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __restrict__ rbuf,
                                                      const int32_t* __restrict__ xrv, int32_t* __restrict__ lab,
-                                                     uint64_t* __restrict__ chg) {
+                                                     uint64_t* __restrict__ chg, int32_t* __restrict__ uw) {
   const int64_t n = P.pre[P.np];
   const int lane = lane_of(), sub = lane >> 4, l16 = lane & 15;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -181,12 +187,19 @@ __global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __res
     const int q = peer_of(P, i);
     const XRec r = rbuf[P.base[q] + i - P.pre[q]];
     const int32_t g = xrv[P.xoff[q] + r.e];
+    const bool uni = r.val < 0;
+    const int32_t val = r.val & 0x7fffffff;
+    if (!uni || !uw) {
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int j = k * 16 + l16;
-      if ((r.mask >> j) & 1) lab[(int64_t)g * 64 + j] = r.val;
+      for (int k = 0; k < 4; k++) {
+        const int j = k * 16 + l16;
+        if ((r.mask >> j) & 1) lab[(int64_t)g * 64 + j] = val;
+      }
     }
-    if (l16 == 0) atomicOr((unsigned long long*)&chg[g], (unsigned long long)r.mask);
+    if (l16 == 0) {
+      if (uw) uw[g] = uni ? val : -1;
+      atomicOr((unsigned long long*)&chg[g], (unsigned long long)r.mask);
+    }
   }
 }
 
@@ -368,8 +381,9 @@ void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32
 }
 void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t* xv, const int32_t* xq,
                       const uint8_t* act, const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab,
-                      XRec* sbuf, unsigned long long* scnt) {
-  if (nx > 0) k_xpack_rec<<<xgrid(nx, 4 * 64, 4096), 256, 0, s>>>(P, nx, xv, xq, act, chg_now, vadj, lab, sbuf, scnt);
+                      const int32_t* uw, XRec* sbuf, unsigned long long* scnt) {
+  if (nx > 0)
+    k_xpack_rec<<<xgrid(nx, 4 * 64, 4096), 256, 0, s>>>(P, nx, xv, xq, act, chg_now, vadj, lab, uw, sbuf, scnt);
 }
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa) {
   k_xcounts<<<1, 64, 0, s>>>(np, me, scnt, stepflag, xa);
@@ -378,8 +392,8 @@ void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32
   if (P.pre[P.np] > 0) k_xclear<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, xrv, chg);
 }
 void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
-                        uint64_t* chg) {
-  if (P.pre[P.np] > 0) k_xunpack_rec<<<xgrid(P.pre[P.np], 16), 256, 0, s>>>(P, rbuf, xrv, lab, chg);
+                        uint64_t* chg, int32_t* uw) {
+  if (P.pre[P.np] > 0) k_xunpack_rec<<<xgrid(P.pre[P.np], 16), 256, 0, s>>>(P, rbuf, xrv, lab, chg, uw);
 }
 void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
                   const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next) {
