@@ -437,6 +437,14 @@ __device__ __forceinline__ unsigned row_lines(uint64_t m) {
          ((m >> 48) != 0);
 }
 // superstep work of one wave (g per lane, the rest wave-uniform)
+// Items per wave round of a grid-stride loop whose lanes first load one word per item: 64
+// when the grid has at most one round of 64 per wave, else just enough to spread the items
+// over every wave.
+__device__ __forceinline__ int64_t wave_span(int64_t n, int64_t nwaves) {
+  const int64_t s = (n + nwaves - 1) / nwaves;
+  return s < 1 ? 1 : (s > 64 ? 64 : s);
+}
+
 struct StepWork {
   unsigned long long v = 0, s = 0, g = 0, a = 0, lr = 0, lw = 0, uw = 0;
 };
@@ -491,12 +499,15 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   unsigned long long members = 0, alive = 0, changed = 0, scanned = 0, lw = 0, uwn = 0;
   uint64_t lanes = 0;  // views with a step-1 change in this wave
-  // 64 vertices per wave round: the lanes read their view masks (one coalesced load), clear the
-  // non-members' count / mask words, and the wave then walks the members one by one
-  for (int64_t b0 = wave * 64; b0 < nv; b0 += nwaves * 64) {
+  // `span` (<= 64) vertices per wave round: the lanes read their view masks (one coalesced load),
+  // clear the non-members' count / mask words, and the wave then walks the members one by one.
+  // The span shrinks when the grid has more waves than 64-vertex rounds (small graphs), so every
+  // wave gets work instead of a few waves walking 64 members each.
+  const int64_t span = wave_span(nv, nwaves);
+  for (int64_t b0 = wave * span; b0 < nv; b0 += nwaves * span) {
    const int64_t vlane = b0 + lane;
-   const uint64_t mvl = vlane < nv ? vm[vlane] : 0;
-   if (vlane < nv && mvl == 0) { cnt[vlane] = 0; vadj[vlane] = 0; }
+   const uint64_t mvl = (lane < span && vlane < nv) ? vm[vlane] : 0;
+   if (lane < span && vlane < nv && mvl == 0) { cnt[vlane] = 0; vadj[vlane] = 0; }
    uint64_t todo = __ballot(mvl != 0);
    while (todo) {
     const int64_t v = b0 + __builtin_ctzll(todo);
@@ -997,13 +1008,16 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   int32_t changed = 0;
   StepWork wk;
   const TailList none{nullptr, nullptr};
-  // 64 chunks per wave round: lane l reads chunk l's frontier flags (one coalesced load), and
-  // the wave then runs only the flagged chunks — a sparse frontier costs one load per 64 chunks
+  // `span` (<= 64) chunks per wave round: lane l reads chunk l's frontier flags (one coalesced
+  // load), and the wave then runs only the flagged chunks — a sparse frontier costs one load per
+  // 64 chunks.  On a small graph the span shrinks so that the dense supersteps spread over every
+  // wave of the grid (C2: 25k chunks over 4,096 waves -> 7 per round).
   const int64_t nchunks = (nv + CH - 1) / CH;
-  for (int64_t c0 = wave * 64; c0 < nchunks; c0 += nwaves * 64) {
+  const int64_t span = wave_span(nchunks, nwaves);
+  for (int64_t c0 = wave * span; c0 < nchunks; c0 += nwaves * span) {
     const int64_t cl = c0 + lane;
     uint32_t fb = 0;
-    if (cl < nchunks) {
+    if (lane < span && cl < nchunks) {
       const int64_t v0 = cl * CH;
       const uint64_t f = CH == 8 ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
                                  : *reinterpret_cast<const uint32_t*>(act_cur + v0);

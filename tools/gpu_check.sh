@@ -18,9 +18,9 @@ step() {  # step <name> <seconds> <cmd...>
 rocminfo 2>/dev/null | grep -m1 -o 'gfx9[0-9a-z]*' > gpurun_out/arch.txt
 for s in ${STEPS:-pytest smoke bench}; do
   case $s in
-    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} ;;
+    pytest) step pytest_gpu ${PYTEST_SECS:-900} python -u -m pytest tests -m "${PYTEST_MARK:-gpu}" -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke)  step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
-    bench)  step bench 900 python bench.py ${BENCH_ARGS:-} ;;
+    bench)  step bench ${BENCH_SECS:-900} python -u bench.py ${BENCH_ARGS:-} ;;
     probe)  step probe 900 python tools/probe.py ${PROBE_CFGS:-} ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
