@@ -149,6 +149,36 @@ def cpu_baseline(stream, hops, windows, budget_s, n_edges, what, lazy=False):
     }
 
 
+def setup_latency(g, hops, windows, n=40):
+    """The per-Setup drop-in path (GpuReaderWorker): one rgpu_run_view_batch
+    per hop (1 hop x |windows|, RGPU_RUN_RETAIN) followed by rgpu_cc_result per window (the
+    label -> count map ConnectedComponents.returnResults ships, ConnectedComponents.scala:37-42),
+    over n hops drawn uniformly from the range; and the summary-only form (rgpu_cc_summary,
+    no retained rows).  Wall ms per Setup = one hop's whole batched-window job."""
+    import torch
+    pick = np.sort(np.random.default_rng(1).choice(len(hops), size=min(n, len(hops)), replace=False))
+    out = {}
+    for form in ("cc_result", "summary"):
+        ts = []
+        for h in pick:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            g.run("cc", [int(hops[h])], windows, retain=form == "cc_result")
+            if form == "cc_result":
+                for w in range(len(windows)):
+                    g.cc_result(0, w)
+            else:
+                for w in range(len(windows)):
+                    g.cc_summary(0, w)
+            ts.append((time.perf_counter() - t0) * 1e3)
+        ts = np.array(ts)
+        out[form] = {"ms_per_setup_mean": round(float(ts.mean()), 3), "ms_per_setup_median": round(float(np.median(ts)), 3),
+                     "ms_per_view_mean": round(float(ts.mean()) / len(windows), 3), "setups": int(len(ts))}
+    out["note"] = (f"{len(pick)} hops uniform over the range, one call per hop x {len(windows)} windows "
+                   "(RangeAnalysisTask restarting per hop); the batched headline answers every hop in one call")
+    return out
+
+
 def run_c3(a, rank, world, local):
     """BASELINE configs[2] (C3): power-law stream, 10M vertices / 100M updates over two years;
     Range over the last 60 days, daily hops, windows [month, week, day]; PageRank (20
@@ -563,6 +593,7 @@ def run_c2(a, rank, world, local, quiet=False):
                                      "bytes_per_launch": s8d["cc_step"]["bytes_per_launch"]}
 
     summ = g.cc_summaries()
+    drop_in = setup_latency(g, hops, windows) if rank == 0 and not profile_only else None
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(stream, hops, windows, a.cpu_seconds, n_edges,
@@ -596,6 +627,7 @@ def run_c2(a, rank, world, local, quiet=False):
             "survey_8d_bytes": s8d,
             "cpu_baseline": cpu,
             "kernels": kstats,
+            "drop_in_per_setup": drop_in,
             "check": {"views": int(summ.shape[0] * summ.shape[1]),
                       "sum_biggest": int(summ[..., 0].sum()), "sum_total": int(summ[..., 1].sum())},
         }

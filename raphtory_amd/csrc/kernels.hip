@@ -143,6 +143,9 @@ __device__ __forceinline__ void batch_clear(const BatchClear& clr) {
   for (int b = 0; b < 3; b++)
     if (clr.act[b])
       for (int64_t i = tid; i < clr.n_act_words; i += nth) reinterpret_cast<uint64_t*>(clr.act[b])[i] = 0;
+  for (int b = 0; b < 3; b++)
+    if (clr.cb[b])
+      for (int64_t i = tid; i < clr.n_cb_words; i += nth) clr.cb[b][i] = 0;
 }
 __global__ __launch_bounds__(256) void k_batch_clear(BatchClear clr) { batch_clear(clr); }
 
@@ -490,7 +493,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int32_t* __restrict__ ts_e,
                                                   const int32_t* __restrict__ ts_nb,
                                                   const int64_t* __restrict__ ts_t, int64_t tcut,
-                                                  int32_t* __restrict__ uw0, int32_t* __restrict__ uw1) {
+                                                  int32_t* __restrict__ uw0, int32_t* __restrict__ uw1,
+                                                  uint64_t* __restrict__ cb1) {
   __shared__ unsigned long long red[4];
   if (threadIdx.x < 4) red[threadIdx.x] = 0;
   __syncthreads();
@@ -550,6 +554,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         vadj[v] = any;
         chg1[v] = ch;
         if (ch) act2[v] = 1;
+        if (ch && cb1) atomicOr((unsigned long long*)&cb1[v >> 6], 1ull << (v & 63));
       }
       if (!own) continue;
       changed += ch != 0;
@@ -624,7 +629,12 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       lw += 2 * row_lines(mv);
     }
     const uint64_t ch = __ballot(best < me);
-    if (lane == 0) { cnt[v] = count; vadj[v] = any; chg1[v] = ch; }
+    if (lane == 0) {
+      cnt[v] = count;
+      vadj[v] = any;
+      chg1[v] = ch;
+      if (ch && cb1) atomicOr((unsigned long long*)&cb1[v >> 6], 1ull << (v & 63));
+    }
     if (!own) continue;
     lanes |= ch;
     if (ch) {
@@ -808,7 +818,9 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          StepWork& wk, const int32_t* __restrict__ hv_of = nullptr,
                                          int32_t* __restrict__ hbest = nullptr,
                                          const int32_t* __restrict__ uw_cur = nullptr,
-                                         int32_t* __restrict__ uw_next = nullptr) {
+                                         int32_t* __restrict__ uw_next = nullptr,
+                                         const uint64_t* __restrict__ cb_prev = nullptr,
+                                         uint64_t* __restrict__ cb_next = nullptr) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
@@ -847,16 +859,36 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     // stage 3: neighbours' change words (vertex 0's word for idle lanes, masked by sm = 0),
     // then the uniform words of the neighbours that changed
     uint64_t act[CH];
-#pragma unroll
-    for (int i = 0; i < CH; i++) {
-      act[i] = sm[i] & chg_prev[nb[i]];
-    }
     int32_t un[CH];
+    if (cb_prev) {
+      // changed-bit path: a neighbour whose bit is clear did not change in r-1 (nothing to
+      // read: one probe of an L2-resident bitmap instead of a random 8-B change word); a
+      // changed uniform neighbour's word is folded on every kept view of the slot (folding an
+      // unchanged view's label is a no-op: it is >= the label the vertex already holds, see
+      // DESIGN.md §4); only a changed mixed neighbour needs its change word and row lanes
 #pragma unroll
-    for (int i = 0; i < CH; i++) {
-      un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
-      if (uw_cur) wk.a += __popcll(__ballot(act[i] != 0));
-      wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
+      for (int i = 0; i < CH; i++) {
+        const bool hot = sm[i] != 0 && ((cb_prev[nb[i] >> 6] >> (nb[i] & 63)) & 1);
+        un[i] = hot ? uw_cur[nb[i]] : kMixed;
+        act[i] = hot ? sm[i] : 0;
+      }
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        if (un[i] == kMixed && act[i]) act[i] &= chg_prev[nb[i]];
+        wk.a += __popcll(__ballot(act[i] != 0 || un[i] != kMixed)) + 2 * __popcll(__ballot(act[i] != 0 && un[i] == kMixed));
+        wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        act[i] = sm[i] & chg_prev[nb[i]];
+      }
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
+        if (uw_cur) wk.a += __popcll(__ballot(act[i] != 0));
+        wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
+      }
     }
     // own rows are only meaningful on member lanes
 #pragma unroll
@@ -889,9 +921,19 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
           const int32_t j = c2 + lane;
           const int64_t idx = base + (j < n ? j : c2);
           const int32_t q = snbr[idx];
-          const uint64_t a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
-          const int32_t u2 = (uw_cur && a2) ? uw_cur[q] : kMixed;
-          if (uw_cur) wk.a += __popcll(__ballot(a2 != 0));
+          uint64_t a2;
+          int32_t u2;
+          if (cb_prev) {
+            const uint64_t m2 = j < n ? smask[idx] : 0;
+            const bool hot = m2 != 0 && ((cb_prev[q >> 6] >> (q & 63)) & 1);
+            u2 = hot ? uw_cur[q] : kMixed;
+            a2 = hot ? (u2 == kMixed ? m2 & chg_prev[q] : m2) : 0;
+            wk.a += __popcll(__ballot(hot)) + 2 * __popcll(__ballot(hot && u2 == kMixed));
+          } else {
+            a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
+            u2 = (uw_cur && a2) ? uw_cur[q] : kMixed;
+            if (uw_cur) wk.a += __popcll(__ballot(a2 != 0));
+          }
           wk.g += u2 == kMixed ? __popcll(a2) : 0;
           best[i] = gather_min<BUF>(u2 == kMixed ? a2 : 0, q, best[i], lab_cur, lane);
           if (uw_cur) best[i] = fold_uniform(__ballot(u2 != kMixed), a2, u2, best[i], lane);
@@ -912,6 +954,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       }
     }
     // stage 4b: publish
+    uint64_t cbits = 0;  // (lane 0) changed bits of the chunk: CH consecutive ranks, one bitmap word
 #pragma unroll
     for (int i = 0; i < CH; i++) {
       const uint64_t mv = readlane64(mv_l, i);
@@ -933,6 +976,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       }
       if (lane == 0) chg_next[v] = ch;
       if (ch) {
+        cbits |= 1ull << (v & 63);
         if (lane == 0) atomicOr(lds_lanes, (unsigned long long)ch);  // LDS: views changed this step
         changed++;
         mark<TAIL>(lane == 0, (int32_t)v, act_next, tl, lane);
@@ -948,6 +992,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
         }
       }
     }
+    if (cb_next && cbits && lane == 0) atomicOr((unsigned long long*)&cb_next[vv[0] >> 6], (unsigned long long)cbits);
   }
 }
 
@@ -991,7 +1036,9 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
                                                   const int32_t* __restrict__ hv_of,
                                                   int32_t* __restrict__ hbest,
                                                   unsigned long long* __restrict__ lanechg,
-                                                  const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next) {
+                                                  const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
+                                                  const uint64_t* __restrict__ cb_prev, uint64_t* __restrict__ cb_next,
+                                                  uint64_t* __restrict__ cb_clear, int64_t cb_words) {
   if (stepflag[step - 1] == 0) return;
   __shared__ int32_t red;
   __shared__ unsigned long long wred[8];  // [0..6] work fields (StepWork), [7] changed views (LDS OR)
@@ -1001,6 +1048,9 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
        i += (int64_t)gridDim.x * blockDim.x)
     reinterpret_cast<uint64_t*>(act_clear)[i] = 0;
+  if (cb_clear)  // changed bits: written in r, read in r+1, cleared here in r+2 (three in rotation)
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cb_words; i += (int64_t)gridDim.x * blockDim.x)
+      cb_clear[i] = 0;
   __syncthreads();
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -1032,7 +1082,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
       cc_chunk<CH, BUF, false>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
                                lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
-                               hv_of, hbest, uw_cur, uw_next);
+                               hv_of, hbest, uw_cur, uw_next, cb_prev, cb_next);
     }
   }
   if (work)
@@ -1273,7 +1323,8 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       const uint8_t* __restrict__ act_cur,
                                                       const int32_t* __restrict__ stepflag,
                                                       int32_t* __restrict__ hbest, int64_t n_own,
-                                                      const int32_t* __restrict__ uw_cur) {
+                                                      const int32_t* __restrict__ uw_cur,
+                                                      const uint64_t* __restrict__ cb_prev) {
   if (stepflag[step - 1] == 0) return;
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -1289,9 +1340,18 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
       const int32_t jj = c + lane;
       const int64_t idx = base + (jj < n ? jj : c);
       const int32_t q = snbr[idx];
-      const uint64_t a = jj < n ? (smask[idx] & chg_prev[q]) : 0;
+      uint64_t a;
+      int32_t u;
+      if (cb_prev) {  // changed-bit path (cc_chunk): uniform changed neighbours on every kept view
+        const uint64_t m = jj < n ? smask[idx] : 0;
+        const bool hot = m != 0 && ((cb_prev[q >> 6] >> (q & 63)) & 1);
+        u = hot ? uw_cur[q] : kMixed;
+        a = hot ? (u == kMixed ? m & chg_prev[q] : m) : 0;
+      } else {
+        a = jj < n ? (smask[idx] & chg_prev[q]) : 0;
+        u = (uw_cur && a) ? uw_cur[q] : kMixed;
+      }
       // lane = view: the changed mixed rows (4 in flight), then the uniform neighbours' words
-      const int32_t u = (uw_cur && a) ? uw_cur[q] : kMixed;
       best = gather_min<false>(u == kMixed ? a : 0, q, best, lab_cur, lane);
       if (uw_cur) best = fold_uniform(__ballot(u != kMixed), a, u, best, lane);
     }
@@ -2044,13 +2104,13 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
-                     unsigned long long* lanechg, int32_t* uw0, int32_t* uw1) {
+                     unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1) {
   const bool hv = g.n_seg > 0;
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
-                                                uw0, uw1);
+                                                uw0, uw1, cb1);
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
@@ -2072,7 +2132,8 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
-                    unsigned long long* work, int variant, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next) {
+                    unsigned long long* work, int variant, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next,
+                    const ChgBits& cb) {
   const int ch = (variant & 15) == 8 ? 8 : 4;
   const bool buf = (variant & 16) != 0;
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
@@ -2084,7 +2145,8 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   const unsigned grid = grid_for(g.nv, 4 * ch, cap);
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
-    act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next
+    act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
+    cb.prev, cb.next, cb.clear, cb.words
   if (ch == 8 && buf) k_cc_step2<8, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (ch == 8) k_cc_step2<8, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (buf) k_cc_step2<4, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
@@ -2101,11 +2163,12 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
 }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
-                         const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur) {
+                         const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur,
+                         const uint64_t* cb_prev) {
   if (g.n_seg <= 0) return;
   k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
-                                                             hb.best, g.n_own, uw_cur);
+                                                             hb.best, g.n_own, uw_cur, cb_prev);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,

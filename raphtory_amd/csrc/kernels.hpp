@@ -70,6 +70,8 @@ struct BatchClear {
   int64_t n_flags = 0;
   uint8_t* act[3] = {nullptr, nullptr, nullptr};
   int64_t n_act_words = 0;  // uint64 words per act buffer
+  uint64_t* cb[3] = {nullptr, nullptr, nullptr};  // changed bits (ChgBits)
+  int64_t n_cb_words = 0;
 };
 
 // Per-step OR of the views (lanes) in which some label changed: words lanechg[step*kLaneShards +
@@ -99,7 +101,8 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
-                     unsigned long long* lanechg, int32_t* uw0 = nullptr, int32_t* uw1 = nullptr);
+                     unsigned long long* lanechg, int32_t* uw0 = nullptr, int32_t* uw1 = nullptr,
+                     uint64_t* cb1 = nullptr);
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
 // (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
 // next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
@@ -107,7 +110,8 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
                         int32_t* snbr, uint64_t* smask, const HeavyBuf& hb);
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
-                         const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr);
+                         const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr,
+                         const uint64_t* cb_prev = nullptr);
 // vm/em (partitioned mode): heavy ghosts (ranks >= n_own) have no compacted slots; their kept
 // slots are recomputed from the static adjacency (em & vm[nb] & vm[v]) while marking
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
@@ -134,13 +138,24 @@ void launch_check_labels(hipStream_t s, int64_t nv, const uint64_t* vm, const in
                          unsigned long long* bad);
 void launch_check_slots(hipStream_t s, int64_t nv, const int64_t* adj_off, const uint64_t* vm, const int32_t* cnt,
                         const int32_t* snbr, const int32_t* uw0, const int32_t* uw1, unsigned long long* bad);
+// Changed bits (with uniform words only): one bit per local rank, set when the vertex's label
+// changed in a step; three bitmaps rotate (step r writes r % 3, reads (r - 1) % 3 and clears
+// (r + 1) % 3).  A superstep probes a neighbour's bit (L2-resident: 2.5 MB for 20M vertices)
+// before it touches the neighbour's words.  All null: the change words alone.
+struct ChgBits {
+  const uint64_t* prev = nullptr;
+  uint64_t* next = nullptr;
+  uint64_t* clear = nullptr;
+  int64_t words = 0;  // words cleared (every local rank, ghosts included)
+};
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, int variant, unsigned long long* lanechg,
-                    int32_t* hbest = nullptr, const int32_t* uw_cur = nullptr, int32_t* uw_next = nullptr);
+                    int32_t* hbest = nullptr, const int32_t* uw_cur = nullptr, int32_t* uw_next = nullptr,
+                    const ChgBits& cb = ChgBits());
 // Many late supersteps in one single-workgroup launch while the frontier stays below `cap`
 // vertices; info[0] <- last superstep executed (host-mapped).
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
@@ -203,7 +218,7 @@ void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t*
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa);
 void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg);
 void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
-                        uint64_t* chg, int32_t* uw = nullptr);
+                        uint64_t* chg, int32_t* uw = nullptr, uint64_t* cb = nullptr);
 void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
                   const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next);
 // owned id -> owned rank: ids ascend with rank; bucket b = id >> shift covers ranks

@@ -68,6 +68,7 @@ struct Slot {
   uint64_t* smask = nullptr;
   int32_t* lab[2] = {nullptr, nullptr};
   int32_t* uw[2] = {nullptr, nullptr};    // uniform label words of lab[0/1] (kernels.hip kMixed)
+  uint64_t* cb[3] = {nullptr, nullptr, nullptr};  // changed bits, rotated like act (kernels.hpp ChgBits)
   int32_t* counts = nullptr;              // [nv][64] component counts at the root (zero between batches)
   uint64_t* chg[2] = {nullptr, nullptr};
   int32_t *stepcnt = nullptr, *hist = nullptr;   // stepcnt[r] = 1 iff superstep r changed a label
@@ -185,6 +186,7 @@ struct rgpu_ctx {
   int step_variant = 0;                 // RGPU_STEP_VARIANT: 0 per-vertex chain, 1 chunk-pipelined
   bool tail_on = false;                 // RGPU_TAIL: late supersteps in one-workgroup k_cc_tail launches
   bool uw_on = true;                    // RGPU_UW: uniform label words (one partition, no tail kernel)
+  bool cb_on = true;                    // RGPU_CHGBITS: changed bits beside the uniform words
   bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
   int tail_cap = 256;                   // RGPU_TAIL_CAP: widest frontier the tail kernel takes
   int64_t tail_maxv = 4 << 20;          // RGPU_TAIL_MAXV: no tail kernel above this many vertices
@@ -323,6 +325,17 @@ void run_check(hipStream_t st, const char* what, F launch) {
 // ghost rows arrive as per-lane records, so the ghosts' words stay kMixed (start_batch)
 bool use_uw(const rgpu_ctx* c) { return c->uw_on && !c->tail_on; }
 
+// changed bits of superstep r (with uniform words; RGPU_CHGBITS=0 turns them off)
+ChgBits chg_bits(const rgpu_ctx* c, const Slot& s, int r) {
+  ChgBits b;
+  if (!use_uw(c) || !c->cb_on || !s.cb[0]) return b;
+  b.prev = s.cb[(r + 2) % 3];
+  b.next = s.cb[r % 3];
+  b.clear = s.cb[(r + 1) % 3];
+  b.words = (c->g.nv + 63) / 64 + 1;
+  return b;
+}
+
 template <class F>
 void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn, int step = 0, bool evented = true) {
   Slot& s = c->slot[si];
@@ -412,6 +425,7 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       HIPCHK(hipMemset(s.chg[1], 0, sizeof(uint64_t) * (nv + kPad)));
       HIPCHK(hipMemset(s.snbr, 0, sizeof(int32_t) * (ne + nin + kPad)));
       for (int b = 0; b < 3; b++) s.act[b] = dalloc<uint8_t>(L, (size_t)((nv + 7) / 8 + 1) * 8);
+      for (int b = 0; b < 3; b++) s.cb[b] = dalloc<uint64_t>(L, (size_t)((nv + 63) / 64 + 1));
       s.vadj = dalloc<uint64_t>(L, nv);
       s.work = dalloc<unsigned long long>(L, kWorkWords);
       s.iso = dalloc<unsigned int>(L, kIsoWords);  // zero between batches: the summary kernel clears it
@@ -507,13 +521,17 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
   // profile: ONE event pair around the chunk's back-to-back superstep launches (per-launch
   // pairs add ~3 us of marker latency to a ~12 us kernel; rocprofv3's per-dispatch times
   // agree with the chunk average)
+  // With heavy vertices the chunk interleaves k_heavy_gather / k_heavy_mark with the superstep
+  // kernel, so each launch gets its own pair instead (a superstep is ~1 ms there, the pair's
+  // latency noise), and the superstep kernel's average is its own, as rocprofv3 reports it.
+  const bool hv = g.n_seg > 0 && rc.algo == RGPU_ALGO_CC;
+  const bool per_launch = c->profile && hv;
   hipEvent_t ea = nullptr, eb = nullptr;
-  if (c->profile && last > s.r_launched) {
+  if (c->profile && !per_launch && last > s.r_launched) {
     ea = take_event(c);
     eb = take_event(c);
     HIPCHK(hipEventRecord(ea, s.stream));
   }
-  const bool hv = g.n_seg > 0 && rc.algo == RGPU_ALGO_CC;
   const bool uw = use_uw(c);
   for (int r = s.r_launched + 1; r <= last; r++) {
     if (rc.algo == RGPU_ALGO_DIFFUSION) {
@@ -528,20 +546,21 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     if (hv)  // heavy vertices: segment minima before the step, neighbour marking after it
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[(r - 1) & 1], s.chg[(r - 1) & 1], s.act[r % 3],
-                            s.stepcnt, r, s.hv, uw ? s.uw[(r - 1) & 1] : nullptr);
-      }, r, false);
+                            s.stepcnt, r, s.hv, uw ? s.uw[(r - 1) & 1] : nullptr, chg_bits(c, s, r).prev);
+      }, r, per_launch);
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                      s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
                      s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                      c->profile ? s.work : nullptr, c->step_variant | (g_rowbuf ? 16 : 0), s.stats + kLaneOff,
-                     hv ? s.hv.best : nullptr, uw ? s.uw[(r - 1) & 1] : nullptr, uw ? s.uw[r & 1] : nullptr);
-    }, r, false);
+                     hv ? s.hv.best : nullptr, uw ? s.uw[(r - 1) & 1] : nullptr, uw ? s.uw[r & 1] : nullptr,
+                     chg_bits(c, s, r));
+    }, r, per_launch);
     if (hv)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[r & 1], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
                           s.act[r % 3]);
-      }, r, false);
+      }, r, per_launch);
   }
   if (ea) {
     HIPCHK(hipEventRecord(eb, s.stream));
@@ -702,6 +721,11 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   if (rc.algo == RGPU_ALGO_CC || rc.algo == RGPU_ALGO_DIFFUSION) {
     for (int b = 0; b < 3; b++) clr.act[b] = rc.algo == RGPU_ALGO_CC ? s.act[b] : s.dact[b];
     clr.n_act_words = (g.nv + 7) / 8 + 1;
+    const ChgBits cb1 = rc.algo == RGPU_ALGO_CC ? chg_bits(c, s, 1) : ChgBits();
+    if (cb1.next) {
+      for (int b = 0; b < 3; b++) clr.cb[b] = s.cb[b];
+      clr.n_cb_words = cb1.words;
+    }
   }
   if (s.work && c->profile)
     HIPCHK(hipMemsetAsync(s.work, 0, sizeof(unsigned long long) * kWorkWords, s.stream));
@@ -775,7 +799,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       launch_cc_slots(s.stream, gk, tcut, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                       c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff, use_uw(c) ? s.uw[0] : nullptr,
-                      use_uw(c) ? s.uw[1] : nullptr);
+                      use_uw(c) ? s.uw[1] : nullptr, chg_bits(c, s, 1).next);
     });
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
@@ -1196,7 +1220,8 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   }
   std::copy(recv, recv + kMaxParts, xs.rcnt[par]);
   const XPeers Lin = peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]);
-  launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par], use_uw(c) ? s.uw[par] : nullptr);
+  launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par], use_uw(c) ? s.uw[par] : nullptr,
+                     chg_bits(c, s, r).next);
   launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3]);
   // the vote is global: superstep r+1 runs here even if nothing changed here
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(s.stepcnt + r), 1, 1, s.stream));
@@ -1213,13 +1238,13 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (hv)
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[n % 3], s.stepcnt, n, s.hv,
-                          use_uw(c) ? s.uw[r & 1] : nullptr);
+                          use_uw(c) ? s.uw[r & 1] : nullptr, chg_bits(c, s, n).prev);
     });
   timed_launch(c, si, KID_STEP, 0.0, [&] {
     launch_cc_step(s.stream, n, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[r & 1], s.lab[n & 1], s.chg[r & 1],
                    s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
                    c->profile ? s.work : nullptr, c->step_variant, s.stats + kLaneOff, hv ? s.hv.best : nullptr,
-                   use_uw(c) ? s.uw[r & 1] : nullptr, use_uw(c) ? s.uw[n & 1] : nullptr);
+                   use_uw(c) ? s.uw[r & 1] : nullptr, use_uw(c) ? s.uw[n & 1] : nullptr, chg_bits(c, s, n));
   }, n);
   part_post_step(c, si, rc, n);
 }
@@ -1495,6 +1520,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->hostflags = env_int("RGPU_HOSTFLAG", 1) != 0;
   c->tail_on = env_int("RGPU_TAIL", 0) != 0;
   c->uw_on = env_int("RGPU_UW", 1) != 0;
+  c->cb_on = env_int("RGPU_CHGBITS", 1) != 0;
   c->check = env_int("RGPU_CHECK", 0) != 0;
   c->wmajor = env_int("RGPU_WMAJOR", 1) != 0;
   c->poll = env_int("RGPU_POLL", 1) != 0;
@@ -2007,6 +2033,13 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   }
   rc.chunk0 = std::max(1, env_int("RGPU_CHUNK0", 12));
   rc.chunk = std::max(1, env_int("RGPU_CHUNK", 8));
+  // superstep launch knobs are re-read per run, so that one sealed graph can be A/B-timed
+  // under several settings in one process (tools/c4_ab.py); unset = the defaults
+  c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
+  c->cb_on = env_int("RGPU_CHGBITS", 1) != 0;
+  g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
+  g_tail_step = std::max(2, env_int("RGPU_TAIL_STEP", 14));
+  g_tail_grid = std::max(1, env_int("RGPU_TAIL_GRID", 1024));
   try {
     HIPCHK(hipSetDevice(c->device));
     {

@@ -176,7 +176,8 @@ __global__ __launch_bounds__(256) void k_xclear(XPeers P, const XRec* __restrict
 // holds, which are the record's.  Other records mark the ghost mixed (kernels.hip kMixed).
 __global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __restrict__ rbuf,
                                                      const int32_t* __restrict__ xrv, int32_t* __restrict__ lab,
-                                                     uint64_t* __restrict__ chg, int32_t* __restrict__ uw) {
+                                                     uint64_t* __restrict__ chg, int32_t* __restrict__ uw,
+                                                     uint64_t* __restrict__ cb) {
   const int64_t n = P.pre[P.np];
   const int lane = lane_of(), sub = lane >> 4, l16 = lane & 15;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -199,6 +200,7 @@ __global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __res
     if (l16 == 0) {
       if (uw) uw[g] = uni ? val : -1;
       atomicOr((unsigned long long*)&chg[g], (unsigned long long)r.mask);
+      if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // the ghost changed (ChgBits)
     }
   }
 }
@@ -392,8 +394,8 @@ void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32
   if (P.pre[P.np] > 0) k_xclear<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, xrv, chg);
 }
 void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
-                        uint64_t* chg, int32_t* uw) {
-  if (P.pre[P.np] > 0) k_xunpack_rec<<<xgrid(P.pre[P.np], 16), 256, 0, s>>>(P, rbuf, xrv, lab, chg, uw);
+                        uint64_t* chg, int32_t* uw, uint64_t* cb) {
+  if (P.pre[P.np] > 0) k_xunpack_rec<<<xgrid(P.pre[P.np], 16), 256, 0, s>>>(P, rbuf, xrv, lab, chg, uw, cb);
 }
 void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
                   const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next) {

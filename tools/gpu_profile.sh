@@ -10,10 +10,12 @@ O=gpurun_out/prof
 mkdir -p $O
 K=${KREGEX:-k_cc_step2}
 run() { local name=$1 secs=$2; shift 2; echo "=== $name"; timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "=== $name rc=$rc"; tail -3 "$O/$name.log"; [ $rc -eq 0 ] || exit $rc; }
-run bench 600 python bench.py ${BENCH_ARGS:-}
-grep '^{' $O/bench.log > $O/bench.json || true
-run prof_only 300 python bench.py --profile-only ${BENCH_ARGS:-}
-grep '^{' $O/prof_only.log > $O/prof_only.json || true
+if [ -z "${SKIP_BENCH:-}" ]; then
+  run bench 600 python bench.py ${BENCH_ARGS:-}
+  grep '^{' $O/bench.log > $O/bench.json || true
+  run prof_only 300 python bench.py --profile-only ${BENCH_ARGS:-}
+  grep '^{' $O/prof_only.log > $O/prof_only.json || true
+fi
 run kt 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
 run fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $O/fetch -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
 run write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O/write -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}

@@ -62,6 +62,8 @@ def main():
         summ = parts[0].cc_summaries()
         out = {"P": P, "kernel_ms_per_partition": per, "kernel_ms_max": max(per), "kernel_ms_total": round(sum(per), 1),
                "kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in ks.items()},
+               "partition0_kernels": {k: [v["launches"], round(v["ms"], 2)] for k, v in parts[0].stats()["kernels"].items()
+                                      if v["launches"]},
                "xchg_MB_per_query": {k: round(v, 1) for k, v in by.items()},
                "vertices_here": [g.stats()["vertices"] for g in parts], "edges_here": [g.stats()["edges"] for g in parts],
                "check": [int(summ[..., 0].sum()), int(summ[..., 1].sum()), int(summ[..., 5].sum())]}
