@@ -346,7 +346,8 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
                                                    const int64_t* __restrict__ dtime, BatchParams bp,
                                                    uint64_t* __restrict__ em, int64_t estride,
                                                    unsigned long long* __restrict__ ecnt, int64_t h0,
-                                                   int64_t own_lim) {
+                                                   int64_t own_lim, const uint64_t* __restrict__ vm_ends,
+                                                   int64_t vstride) {
   __shared__ HopLDS L;
   __shared__ unsigned int cnt_s[PLANAR ? kMaxPlanes : 1][64];
   hop_lds_init(L, bp, bp.thr_e);
@@ -359,15 +360,27 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
   for (int64_t e0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); e0 < ne; e0 += stride) {
     const int64_t e = e0 + lane;
     uint64_t m[NP] = {};
+    uint64_t mo[NP];  // the edge's own aliveness (the |E_w| counts)
     if (e < ne) {
       edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime);
+#pragma unroll
+      for (int w = 0; w < NP; w++) mo[w] = m[w];
+      if (vm_ends) {  // CC: both endpoints' memberships folded in (K2 then skips vm[nb])
+        const int32_t s = esrc[e], d = edst[e];
+#pragma unroll
+        for (int w = 0; w < NP; w++)
+          if (!PLANAR || w < L.W) m[w] &= vm_ends[w * vstride + s] & vm_ends[w * vstride + d];
+      }
       store_bits<PLANAR>(m, bp, em, estride, e);
+    } else {
+#pragma unroll
+      for (int w = 0; w < NP; w++) mo[w] = 0;
     }
     if constexpr (COUNT) {  // an edge counts once over the partitions: where its source is owned
       const bool mine = e < ne && esrc[e] < own_lim;
 #pragma unroll
       for (int w = 0; w < NP; w++)
-        if (!PLANAR || w < L.W) acc[w] += __popcll(transpose64(mine ? m[w] : 0ull, lane));
+        if (!PLANAR || w < L.W) acc[w] += __popcll(transpose64(mine ? mo[w] : 0ull, lane));
     }
   }
   if constexpr (COUNT) {
@@ -494,7 +507,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int32_t* __restrict__ ts_nb,
                                                   const int64_t* __restrict__ ts_t, int64_t tcut,
                                                   int32_t* __restrict__ uw0, int32_t* __restrict__ uw1,
-                                                  uint64_t* __restrict__ cb1) {
+                                                  uint64_t* __restrict__ cb1, int ends) {
   __shared__ unsigned long long red[4];
   if (threadIdx.x < 4) red[threadIdx.x] = 0;
   __syncthreads();
@@ -596,7 +609,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
           e = in_eid[i0 + (j - nout)];
           nb = esrc[e];
         }
-        if (nb != (int32_t)v && (!ts_t || ts_t[base + j] >= tcut)) m = em[e] & vm[nb] & mv;
+        if (nb != (int32_t)v && (!ts_t || ts_t[base + j] >= tcut)) m = em[e] & (ends ? mv : vm[nb]) & mv;
         lb = grank ? grank[nb] : nb;
       }
       uint64_t bal = __ballot(m != 0);
@@ -866,15 +879,19 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       // changed uniform neighbour's word is folded on every kept view of the slot (folding an
       // unchanged view's label is a no-op: it is >= the label the vertex already holds, see
       // DESIGN.md §4); only a changed mixed neighbour needs its change word and row lanes
+      // (the change word is loaded beside the uniform word, not after it: one dependent
+      // trip per hot neighbour, as without the bits)
+      uint64_t cw[CH];
 #pragma unroll
       for (int i = 0; i < CH; i++) {
         const bool hot = sm[i] != 0 && ((cb_prev[nb[i] >> 6] >> (nb[i] & 63)) & 1);
         un[i] = hot ? uw_cur[nb[i]] : kMixed;
+        cw[i] = hot ? chg_prev[nb[i]] : 0;
         act[i] = hot ? sm[i] : 0;
       }
 #pragma unroll
       for (int i = 0; i < CH; i++) {
-        if (un[i] == kMixed && act[i]) act[i] &= chg_prev[nb[i]];
+        if (un[i] == kMixed) act[i] &= cw[i];
         wk.a += __popcll(__ballot(act[i] != 0 || un[i] != kMixed)) + 2 * __popcll(__ballot(act[i] != 0 && un[i] == kMixed));
         wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
       }
@@ -915,7 +932,27 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
 #pragma unroll
     for (int i = 0; i < CH; i++) {
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
-      if (n > 64) {  // vertices with more than 64 kept slots
+      if (n > 64 && !cb_prev) {  // vertices with more than 64 kept slots: two 64-slot blocks per round,
+                                 // their slot, change-word and uniform-word loads in flight together
+        const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
+        for (int32_t c2 = 64; c2 < n; c2 += 128) {
+          const int32_t j0 = c2 + lane, j1 = c2 + 64 + lane;
+          const int64_t i0 = base + (j0 < n ? j0 : c2), i1 = base + (j1 < n ? j1 : c2);
+          const int32_t q0 = snbr[i0], q1 = snbr[i1];
+          const uint64_t m0 = smask[i0], m1 = smask[i1];
+          const uint64_t w0 = chg_prev[q0], w1 = chg_prev[q1];
+          const uint64_t a0 = j0 < n ? (m0 & w0) : 0, a1 = j1 < n ? (m1 & w1) : 0;
+          const int32_t u0 = (uw_cur && a0) ? uw_cur[q0] : kMixed, u1 = (uw_cur && a1) ? uw_cur[q1] : kMixed;
+          if (uw_cur) wk.a += __popcll(__ballot(a0 != 0)) + __popcll(__ballot(a1 != 0));
+          wk.g += (u0 == kMixed ? __popcll(a0) : 0) + (u1 == kMixed ? __popcll(a1) : 0);
+          best[i] = gather_min<BUF>(u0 == kMixed ? a0 : 0, q0, best[i], lab_cur, lane);
+          best[i] = gather_min<BUF>(u1 == kMixed ? a1 : 0, q1, best[i], lab_cur, lane);
+          if (uw_cur) {
+            best[i] = fold_uniform(__ballot(u0 != kMixed), a0, u0, best[i], lane);
+            best[i] = fold_uniform(__ballot(u1 != kMixed), a1, u1, best[i], lane);
+          }
+        }
+      } else if (n > 64) {
         const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
         for (int32_t c2 = 64; c2 < n; c2 += 64) {
           const int32_t j = c2 + lane;
@@ -927,7 +964,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
             const uint64_t m2 = j < n ? smask[idx] : 0;
             const bool hot = m2 != 0 && ((cb_prev[q >> 6] >> (q & 63)) & 1);
             u2 = hot ? uw_cur[q] : kMixed;
-            a2 = hot ? (u2 == kMixed ? m2 & chg_prev[q] : m2) : 0;
+            const uint64_t c2w = hot ? chg_prev[q] : 0;
+            a2 = hot ? (u2 == kMixed ? m2 & c2w : m2) : 0;
             wk.a += __popcll(__ballot(hot)) + 2 * __popcll(__ballot(hot && u2 == kMixed));
           } else {
             a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
@@ -1249,7 +1287,7 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
                                                      int32_t* __restrict__ hbest, const int32_t* __restrict__ grank,
                                                      int64_t n_own, const int32_t* __restrict__ ts_e,
                                                      const int32_t* __restrict__ ts_nb,
-                                                     const int64_t* __restrict__ ts_t, int64_t tcut) {
+                                                     const int64_t* __restrict__ ts_t, int64_t tcut, int ends) {
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -1287,7 +1325,7 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
           e = in_eid[i0 + (rel - nout)];
           nb = esrc[e];
         }
-        if (nb != v && (!ts_t || ts_t[lo + jj] >= tcut)) m = em[e] & vm[nb] & mv;
+        if (nb != v && (!ts_t || ts_t[lo + jj] >= tcut)) m = em[e] & (ends ? mv : vm[nb]) & mv;
       }
       const uint64_t bal = __ballot(m != 0);
       if (m) {
@@ -2091,8 +2129,9 @@ void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp,
   else k_vertex_mask<false><<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm, vstride, clr);
 }
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
-                      unsigned long long* ecnt, int64_t h0) {
-#define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, bp, em, g.ne, ecnt, h0, g.n_own
+                      unsigned long long* ecnt, int64_t h0, const uint64_t* vm_ends, int64_t vstride) {
+#define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, bp, em, g.ne, ecnt, h0, g.n_own, vm_ends, \
+    vstride
   const unsigned grid = grid_for(g.ne, 256);
   if (planar && ecnt) k_edge_mask<true, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
   else if (planar) k_edge_mask<true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
@@ -2104,13 +2143,13 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
-                     unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1) {
+                     unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends) {
   const bool hv = g.n_seg > 0;
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
-                                                uw0, uw1, cb1);
+                                                uw0, uw1, cb1, ends ? 1 : 0);
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
@@ -2146,7 +2185,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.prev, cb.next, cb.clear, cb.words
+    cb.step_reads ? cb.prev : nullptr, cb.next, cb.clear, cb.words
   if (ch == 8 && buf) k_cc_step2<8, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (ch == 8) k_cc_step2<8, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (buf) k_cc_step2<4, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
@@ -2154,12 +2193,12 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
 #undef RGPU_STEP_ARGS
 }
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
-                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb) {
+                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends) {
   if (g.n_seg <= 0) return;
   k_heavy_slots<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off,
                                                             g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
                                                             snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own,
-                                                            g.ts_e, g.ts_nb, g.ts_t, tcut);
+                                                            g.ts_e, g.ts_nb, g.ts_t, tcut, ends ? 1 : 0);
 }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,

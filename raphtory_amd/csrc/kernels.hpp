@@ -94,20 +94,23 @@ void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp,
                         int64_t vstride, bool planar, const BatchClear& clr);
 // ecnt (profile runs, else null): alive edges per view (|E_w| of SURVEY §8(d)) added into
 // ecnt[(h0 + k) * W + w] for hop k of the block (first hop h0 of the run) and window w
+// vm_ends (CC runs, one partition): the vertex masks of the same block (plane stride vstride);
+// each edge word is ANDed with both endpoints' words, so that K2 keeps a slot on em alone
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
-                      unsigned long long* ecnt = nullptr, int64_t h0 = 0);
+                      unsigned long long* ecnt = nullptr, int64_t h0 = 0, const uint64_t* vm_ends = nullptr,
+                      int64_t vstride = 0);
 // tcut: no view of the batch can keep an edge whose last add is older (time-ordered slots)
 void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
                      unsigned long long* lanechg, int32_t* uw0 = nullptr, int32_t* uw1 = nullptr,
-                     uint64_t* cb1 = nullptr);
+                     uint64_t* cb1 = nullptr, bool ends = false);
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
 // (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
 // next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
-                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb);
+                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends = false);
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr,
@@ -147,6 +150,7 @@ struct ChgBits {
   uint64_t* next = nullptr;
   uint64_t* clear = nullptr;
   int64_t words = 0;  // words cleared (every local rank, ghosts included)
+  bool step_reads = true;  // false: the superstep kernel writes / clears them but reads change words
 };
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,

@@ -186,7 +186,10 @@ struct rgpu_ctx {
   int step_variant = 0;                 // RGPU_STEP_VARIANT: 0 per-vertex chain, 1 chunk-pipelined
   bool tail_on = false;                 // RGPU_TAIL: late supersteps in one-workgroup k_cc_tail launches
   bool uw_on = true;                    // RGPU_UW: uniform label words (one partition, no tail kernel)
-  bool cb_on = true;                    // RGPU_CHGBITS: changed bits beside the uniform words
+  bool ends_on = false;                 // RGPU_EMENDS=1: K1 folds endpoint memberships into CC edge words
+                                        // (measured slower on C4: K1 55 -> 97 ms for K2 122 -> 117 ms)
+  int cb_on = 2;                        // RGPU_CHGBITS: changed bits beside the uniform words (0 off,
+                                        // 1 superstep + heavy gather read them, 2 heavy gather only)
   bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
   int tail_cap = 256;                   // RGPU_TAIL_CAP: widest frontier the tail kernel takes
   int64_t tail_maxv = 4 << 20;          // RGPU_TAIL_MAXV: no tail kernel above this many vertices
@@ -329,6 +332,12 @@ bool use_uw(const rgpu_ctx* c) { return c->uw_on && !c->tail_on; }
 ChgBits chg_bits(const rgpu_ctx* c, const Slot& s, int r) {
   ChgBits b;
   if (!use_uw(c) || !c->cb_on || !s.cb[0]) return b;
+  // RGPU_CHGBITS=2 (default): written, read by the heavy gather only, and only when there are
+  // heavy vertices.  The superstep kernel reading them measured slower on C4 (cc_step 263 ->
+  // 301 ms serial; the gather's bit probe + word loads vs one change word) and on C2; the heavy
+  // gather, which walks a hub's whole kept slot list every step, gained (119 -> 103 ms).
+  if (c->cb_on == 2 && c->g.n_seg == 0) return b;
+  b.step_reads = c->cb_on == 1;
   b.prev = s.cb[(r + 2) % 3];
   b.next = s.cb[r % 3];
   b.clear = s.cb[(r + 1) % 3];
@@ -735,12 +744,15 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   // the ghosts' words arrive from their owners right after
   DevGraph gk = g;
   if (c->partitioned) gk.nv = c->pk.n_own;
+  // CC, one partition: K1 folds both endpoints' memberships into the edge words (a ghost's
+  // membership arrives after K1 in the partitioned mode); RGPU_EMENDS=0 turns it off
+  const bool ends = rc.algo == RGPU_ALGO_CC && !c->partitioned && c->ends_on;
   if (rc.G == 1) {
     s.vm = s.vm_own;
     s.em = s.em_own;
     timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv, [&] { launch_vertex_mask(s.stream, gk, bp, s.vm, 0, false, clr); });
     timed_launch(c, si, KID_MASK, be + 8.0 * g.ne,
-                 [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0); });
+                 [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0, ends ? s.vm : nullptr, 0); });
     if (c->partitioned) part_vm_exchange(c, si, s.vm, 0, 1);
   } else {
     MaskSet& M = c->mset[hb % kMaskSets];
@@ -751,7 +763,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv * rc.W,
                    [&] { launch_vertex_mask(s.stream, gk, bp, M.vm, g.nv + kPad, true, none); });
       timed_launch(c, si, KID_MASK, be + 8.0 * g.ne * rc.W,
-                   [&] { launch_edge_mask(s.stream, g, bp, M.em, true, c->d_ecnt, (int64_t)h0); });
+                   [&] { launch_edge_mask(s.stream, g, bp, M.em, true, c->d_ecnt, (int64_t)h0, ends ? M.vm : nullptr,
+                                          g.nv + kPad); });
       if (c->partitioned) part_vm_exchange(c, si, M.vm, g.nv + kPad, rc.G);
       HIPCHK(hipEventRecord(M.k1, s.stream));
       M.pending = rc.G;
@@ -794,12 +807,13 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
     const double b2 = 8.0 * g.nv;  // the view-mask scan; the rest from the work counters (harvest)
     if (g.n_seg > 0)
-      timed_launch(c, si, KID_HEAVY, 0.0, [&] { launch_heavy_slots(s.stream, g, tcut, s.vm, s.em, s.snbr, s.smask, s.hv); });
+      timed_launch(c, si, KID_HEAVY, 0.0,
+                   [&] { launch_heavy_slots(s.stream, g, tcut, s.vm, s.em, s.snbr, s.smask, s.hv, ends); });
     timed_launch(c, si, KID_SLOTS, b2, [&] {  // (partitioned: owned vertices only, gk)
       launch_cc_slots(s.stream, gk, tcut, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                       c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff, use_uw(c) ? s.uw[0] : nullptr,
-                      use_uw(c) ? s.uw[1] : nullptr, chg_bits(c, s, 1).next);
+                      use_uw(c) ? s.uw[1] : nullptr, chg_bits(c, s, 1).next, ends);
     });
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
@@ -1520,7 +1534,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->hostflags = env_int("RGPU_HOSTFLAG", 1) != 0;
   c->tail_on = env_int("RGPU_TAIL", 0) != 0;
   c->uw_on = env_int("RGPU_UW", 1) != 0;
-  c->cb_on = env_int("RGPU_CHGBITS", 1) != 0;
+  c->cb_on = env_int("RGPU_CHGBITS", 2);
   c->check = env_int("RGPU_CHECK", 0) != 0;
   c->wmajor = env_int("RGPU_WMAJOR", 1) != 0;
   c->poll = env_int("RGPU_POLL", 1) != 0;
@@ -2036,7 +2050,8 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   // superstep launch knobs are re-read per run, so that one sealed graph can be A/B-timed
   // under several settings in one process (tools/c4_ab.py); unset = the defaults
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
-  c->cb_on = env_int("RGPU_CHGBITS", 1) != 0;
+  c->cb_on = env_int("RGPU_CHGBITS", 2);
+  c->ends_on = env_int("RGPU_EMENDS", 0) != 0;
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
   g_tail_step = std::max(2, env_int("RGPU_TAIL_STEP", 14));
   g_tail_grid = std::max(1, env_int("RGPU_TAIL_GRID", 1024));

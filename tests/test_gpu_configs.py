@@ -184,6 +184,35 @@ def test_c4_first_100m_updates_cc():
     o.close()
 
 
+def test_c4_full_1b_properties():
+    """The whole 1B-update C4 stream (the headline query): summary invariants on all 840 views,
+    and the views of three hops re-run as one hop-major batch (another batch composition, other
+    superstep interleaving, other heavy/uniform-word paths) must give the same summaries as the
+    window-major query.  The oracle cannot replay 10^9 updates inside the suite's budget; the
+    100M-update prefix above is the oracle-compared C4 case."""
+    users, inter = 20_000_000, 333_333_334
+    g = TemporalGraph()
+    for first in range(0, inter, 20_000_000):
+        s = gen_gab_range(4, users, inter, first, min(20_000_000, inter - first))
+        g.ingest_stream(s)
+        end = int(s.t[-1])
+        del s
+    g.seal()
+    st = g.stats()
+    assert st["vertices"] > 19_000_000 and st["edges"] > 280_000_000
+    hops = range_hops(end - 167 * HOUR, end, HOUR)
+    g.run("cc", hops, BATCH_WINDOWS)
+    full = g.cc_summaries()
+    _summary_props(full)
+    assert np.all(full[..., 5] > 0)
+    pick = [0, 83, 167]
+    g.run("cc", hops[pick], BATCH_WINDOWS)
+    part = g.cc_summaries()
+    for k, h in enumerate(pick):
+        assert full[h, :, :7].tolist() == part[k, :, :7].tolist(), h
+    g.close()
+
+
 def cc_fields_from_summary_row(row):
     from raphtory_amd._native import CCSummary
     s = CCSummary()

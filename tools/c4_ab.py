@@ -17,7 +17,7 @@ import torch  # noqa: E402
 from raphtory_amd import TemporalGraph  # noqa: E402
 from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops  # noqa: E402
 
-KNOBS = ("RGPU_CHGBITS", "RGPU_STEP_VARIANT", "RGPU_STEP_GRID", "RGPU_TAIL_STEP", "RGPU_TAIL_GRID", "RGPU_CHUNK0", "RGPU_CHUNK")
+KNOBS = ("RGPU_EMENDS", "RGPU_CHGBITS", "RGPU_STEP_VARIANT", "RGPU_STEP_GRID", "RGPU_TAIL_STEP", "RGPU_TAIL_GRID", "RGPU_CHUNK0", "RGPU_CHUNK")
 
 
 def main():
@@ -25,8 +25,16 @@ def main():
     ap.add_argument("--users", type=int, default=20_000_000)
     ap.add_argument("--interactions", type=int, default=333_333_334)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--heavy", default="", help="comma list of RGPU_HEAVY values: one sealed graph each")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
+    for hv in (a.heavy.split(",") if a.heavy else [None]):
+        if hv is not None:
+            os.environ["RGPU_HEAVY"] = hv
+        one_graph(a, hv)
+
+
+def one_graph(a, hv):
     t0 = time.time()
     g = TemporalGraph()
     for first in range(0, a.interactions, 20_000_000):
@@ -58,7 +66,7 @@ def main():
             ref = ref or chk
             g.run("cc", hops, BATCH_WINDOWS, profile=True, serial=True)
             ks = {k: [v["launches"], round(v["ms"], 2)] for k, v in g.stats()["kernels"].items() if v["launches"]}
-            print(json.dumps({"variant": name, "round": rnd, "ms": round(ms, 2), "same": chk == ref, "kernels": ks}),
+            print(json.dumps({"variant": name, "heavy": hv, "round": rnd, "ms": round(ms, 2), "same": chk == ref, "kernels": ks}),
                   flush=True)
     g.close()
 
