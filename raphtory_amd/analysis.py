@@ -248,6 +248,8 @@ class BinaryDefusion(Analyser):
         self.lines.append(json.dumps({"time": timestamp, "infected": end, "size": len(end)}))
 
     def processResults(self, results, timestamp, viewCompleteTime):
+        # deliberate extension: the reference's is ``???`` (:53, NotImplementedError), so a
+        # non-batched Range job of it throws there; here it prints the view line instead
         self.processViewResults(results, timestamp, viewCompleteTime)
 
     def processBatchWindowResults(self, results, timestamp, windowSet, viewCompleteTime):

@@ -146,6 +146,7 @@ __device__ __forceinline__ void batch_clear(const BatchClear& clr) {
   for (int b = 0; b < 3; b++)
     if (clr.cb[b])
       for (int64_t i = tid; i < clr.n_cb_words; i += nth) clr.cb[b][i] = 0;
+  for (int64_t i = tid; i < clr.n_ccount; i += nth) clr.ccount[i] = 0;
 }
 __global__ __launch_bounds__(256) void k_batch_clear(BatchClear clr) { batch_clear(clr); }
 
@@ -453,6 +454,17 @@ __device__ __forceinline__ unsigned row_lines(uint64_t m) {
          ((m >> 48) != 0);
 }
 // superstep work of one wave (g per lane, the rest wave-uniform)
+// DenseRule: superstep r is dense when r >= 2 and step r-1 changed at least nv / div vertices
+// (ccount[(r-1)*64 + shard]: changed vertices per step, 64 shards, summed here by each wave;
+// every block of a launch computes the same answer from counts the previous launch finished).
+// div <= 0: never.  Step 1 (K2) always writes its flags.
+__device__ __forceinline__ bool dense_rule(const int32_t* __restrict__ ccount, int r, int64_t nv, int div) {
+  if (div <= 0 || !ccount || r < 2) return false;
+  int64_t x = ccount[(r - 1) * kCountShards + (threadIdx.x & 63)];
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x * div >= nv;
+}
+
 // Items per wave round of a grid-stride loop whose lanes first load one word per item: 64
 // when the grid has at most one round of 64 per wave, else just enough to spread the items
 // over every wave.
@@ -507,7 +519,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int32_t* __restrict__ ts_nb,
                                                   const int64_t* __restrict__ ts_t, int64_t tcut,
                                                   int32_t* __restrict__ uw0, int32_t* __restrict__ uw1,
-                                                  uint64_t* __restrict__ cb1, int ends) {
+                                                  uint64_t* __restrict__ cb1, int ends,
+                                                  int32_t* __restrict__ ccount) {
   __shared__ unsigned long long red[4];
   if (threadIdx.x < 4) red[threadIdx.x] = 0;
   __syncthreads();
@@ -673,6 +686,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
   }
   publish_lanes(lanes, &red[3], lanechg, 1);  // (its barrier also publishes red[0..2])
   if (threadIdx.x == 0) {
+    if (red[2] && ccount) atomicAdd(&ccount[1 * kCountShards + (blockIdx.x & (kCountShards - 1))], (int32_t)red[2]);
     if (red[2] && stepflag[1] == 0) {
       stepflag[1] = 1;
       if (hostflag) hostflag[1] = 1;
@@ -833,7 +847,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          const int32_t* __restrict__ uw_cur = nullptr,
                                          int32_t* __restrict__ uw_next = nullptr,
                                          const uint64_t* __restrict__ cb_prev = nullptr,
-                                         uint64_t* __restrict__ cb_next = nullptr) {
+                                         uint64_t* __restrict__ cb_next = nullptr, bool skip_marks = false) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
@@ -932,27 +946,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
 #pragma unroll
     for (int i = 0; i < CH; i++) {
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
-      if (n > 64 && !cb_prev) {  // vertices with more than 64 kept slots: two 64-slot blocks per round,
-                                 // their slot, change-word and uniform-word loads in flight together
-        const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
-        for (int32_t c2 = 64; c2 < n; c2 += 128) {
-          const int32_t j0 = c2 + lane, j1 = c2 + 64 + lane;
-          const int64_t i0 = base + (j0 < n ? j0 : c2), i1 = base + (j1 < n ? j1 : c2);
-          const int32_t q0 = snbr[i0], q1 = snbr[i1];
-          const uint64_t m0 = smask[i0], m1 = smask[i1];
-          const uint64_t w0 = chg_prev[q0], w1 = chg_prev[q1];
-          const uint64_t a0 = j0 < n ? (m0 & w0) : 0, a1 = j1 < n ? (m1 & w1) : 0;
-          const int32_t u0 = (uw_cur && a0) ? uw_cur[q0] : kMixed, u1 = (uw_cur && a1) ? uw_cur[q1] : kMixed;
-          if (uw_cur) wk.a += __popcll(__ballot(a0 != 0)) + __popcll(__ballot(a1 != 0));
-          wk.g += (u0 == kMixed ? __popcll(a0) : 0) + (u1 == kMixed ? __popcll(a1) : 0);
-          best[i] = gather_min<BUF>(u0 == kMixed ? a0 : 0, q0, best[i], lab_cur, lane);
-          best[i] = gather_min<BUF>(u1 == kMixed ? a1 : 0, q1, best[i], lab_cur, lane);
-          if (uw_cur) {
-            best[i] = fold_uniform(__ballot(u0 != kMixed), a0, u0, best[i], lane);
-            best[i] = fold_uniform(__ballot(u1 != kMixed), a1, u1, best[i], lane);
-          }
-        }
-      } else if (n > 64) {
+      if (n > 64) {  // vertices with more than 64 kept slots (a two-block unrolled round measured
+                     // slower on C4: cc_step 263 -> 275 ms serial)
         const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
         for (int32_t c2 = 64; c2 < n; c2 += 64) {
           const int32_t j = c2 + lane;
@@ -1017,6 +1012,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
         cbits |= 1ull << (v & 63);
         if (lane == 0) atomicOr(lds_lanes, (unsigned long long)ch);  // LDS: views changed this step
         changed++;
+        if (skip_marks) continue;  // dense step: the next step visits every member (k_cc_step2)
         mark<TAIL>(lane == 0, (int32_t)v, act_next, tl, lane);
         mark<TAIL>((sm[i] & ch) != 0, nb[i], act_next, tl, lane);
         if (n > 64) {
@@ -1076,8 +1072,13 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
                                                   unsigned long long* __restrict__ lanechg,
                                                   const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
                                                   const uint64_t* __restrict__ cb_prev, uint64_t* __restrict__ cb_next,
-                                                  uint64_t* __restrict__ cb_clear, int64_t cb_words) {
+                                                  uint64_t* __restrict__ cb_clear, int64_t cb_words,
+                                                  int32_t* __restrict__ ccount, int dense_div) {
   if (stepflag[step - 1] == 0) return;
+  // Dense steps (DenseRule): when step r-1 changed at least nv / dense_div vertices, step r
+  // writes no next-frontier flags and step r+1 visits every member instead
+  const bool skip_marks = dense_rule(ccount, step, nv, dense_div);
+  const bool visit_all = dense_rule(ccount, step - 1, nv, dense_div);
   __shared__ int32_t red;
   __shared__ unsigned long long wred[8];  // [0..6] work fields (StepWork), [7] changed views (LDS OR)
   if (threadIdx.x < 8) wred[threadIdx.x] = 0;
@@ -1107,10 +1108,14 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
     uint32_t fb = 0;
     if (lane < span && cl < nchunks) {
       const int64_t v0 = cl * CH;
-      const uint64_t f = CH == 8 ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
-                                 : *reinterpret_cast<const uint32_t*>(act_cur + v0);
+      if (visit_all) {
+        fb = (1u << CH) - 1;
+      } else {
+        const uint64_t f = CH == 8 ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
+                                   : *reinterpret_cast<const uint32_t*>(act_cur + v0);
 #pragma unroll
-      for (int i = 0; i < CH; i++) fb |= ((f >> (8 * i)) & 0xffu) ? (1u << i) : 0u;
+        for (int i = 0; i < CH; i++) fb |= ((f >> (8 * i)) & 0xffu) ? (1u << i) : 0u;
+      }
       if (v0 + CH > nv) fb &= (1u << (nv - v0)) - 1;
     }
     uint64_t todo = __ballot(fb != 0);
@@ -1120,7 +1125,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
       cc_chunk<CH, BUF, false>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
                                lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
-                               hv_of, hbest, uw_cur, uw_next, cb_prev, cb_next);
+                               hv_of, hbest, uw_cur, uw_next, cb_prev, cb_next, skip_marks);
     }
   }
   if (work)
@@ -1137,6 +1142,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   }
   publish_lanes(0, &wred[7], lanechg, step);
   if (threadIdx.x == 0) {
+    if (red && ccount) atomicAdd(&ccount[step * kCountShards + (blockIdx.x & (kCountShards - 1))], red);
     if (red && stepflag[step] == 0) {  // first writers also tell the host (mapped pinned memory)
       stepflag[step] = 1;
       if (hostflag) hostflag[step] = 1;
@@ -1362,14 +1368,16 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       const int32_t* __restrict__ stepflag,
                                                       int32_t* __restrict__ hbest, int64_t n_own,
                                                       const int32_t* __restrict__ uw_cur,
-                                                      const uint64_t* __restrict__ cb_prev) {
+                                                      const uint64_t* __restrict__ cb_prev,
+                                                      const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all) {
   if (stepflag[step - 1] == 0) return;
+  const bool visit_all = dense_rule(ccount, step - 1, nv_all, dense_div);  // step-1 wrote no flags
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
-    if (v >= n_own || !act_cur[v]) continue;  // ghosts are not visited (their owner computes them)
+    if (v >= n_own || (!visit_all && !act_cur[v])) continue;  // ghosts are not visited (their owner computes them)
     const int32_t n = segcnt[sg];
     if (n == 0) continue;
     const int64_t base = seg_lo[sg];
@@ -1420,8 +1428,11 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
                                                     const uint64_t* __restrict__ em,
                                                     const int32_t* __restrict__ ts_e,
                                                     const int32_t* __restrict__ ts_nb,
-                                                    const int64_t* __restrict__ ts_t, int64_t tcut) {
+                                                    const int64_t* __restrict__ ts_t, int64_t tcut,
+                                                    const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all) {
   if (stepflag[step] == 0) return;
+  if (dense_rule(ccount, step, nv_all, dense_div)) return;  // dense step: the next one visits every member
+  if (dense_rule(ccount, step - 1, nv_all, dense_div)) act_cur = nullptr;  // this step visited every member
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -2143,13 +2154,14 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
-                     unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends) {
+                     unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends,
+                     int32_t* ccount) {
   const bool hv = g.n_seg > 0;
   k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
-                                                uw0, uw1, cb1, ends ? 1 : 0);
+                                                uw0, uw1, cb1, ends ? 1 : 0, ccount);
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
@@ -2172,7 +2184,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, int variant, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next,
-                    const ChgBits& cb) {
+                    const ChgBits& cb, int32_t* ccount, int dense_div) {
   const int ch = (variant & 15) == 8 ? 8 : 4;
   const bool buf = (variant & 16) != 0;
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
@@ -2185,7 +2197,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.step_reads ? cb.prev : nullptr, cb.next, cb.clear, cb.words
+    cb.step_reads ? cb.prev : nullptr, cb.next, cb.clear, cb.words, ccount, dense_div
   if (ch == 8 && buf) k_cc_step2<8, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (ch == 8) k_cc_step2<8, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (buf) k_cc_step2<4, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
@@ -2203,21 +2215,23 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur,
-                         const uint64_t* cb_prev) {
+                         const uint64_t* cb_prev, const int32_t* ccount, int dense_div) {
   if (g.n_seg <= 0) return;
   k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
-                                                             hb.best, g.n_own, uw_cur, cb_prev);
+                                                             hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
+                                                             g.n_own);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
                        const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm, const uint64_t* em,
-                       int64_t tcut) {
+                       int64_t tcut, const int32_t* ccount, int dense_div) {
   if (g.n_seg <= 0) return;
   k_heavy_mark<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
                                                            chg_now, act_cur, act_next, stepflag, g.n_own, g.seg_n,
                                                            g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst,
-                                                           vm, em, g.ts_e, g.ts_nb, g.ts_t, tcut);
+                                                           vm, em, g.ts_e, g.ts_nb, g.ts_t, tcut, ccount, dense_div,
+                                                           g.n_own);
 }
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,

@@ -72,6 +72,8 @@ struct BatchClear {
   int64_t n_act_words = 0;  // uint64 words per act buffer
   uint64_t* cb[3] = {nullptr, nullptr, nullptr};  // changed bits (ChgBits)
   int64_t n_cb_words = 0;
+  int32_t* ccount = nullptr;  // changed-vertex counts (kCountShards per step)
+  int64_t n_ccount = 0;
 };
 
 // Per-step OR of the views (lanes) in which some label changed: words lanechg[step*kLaneShards +
@@ -82,6 +84,9 @@ struct BatchClear {
 // last changing step gives the superstep count the reference's job runs (AnalysisTask.endStep
 // :208-225): min(maxSteps, last + 1).
 constexpr int kLaneShards = 64;
+// changed-vertex counts per superstep, ccount[step * kCountShards + shard] (int32, cleared per
+// batch): the dense-step rule of the superstep kernels (kernels.hip dense_rule, RGPU_DENSE)
+constexpr int kCountShards = 64;
 constexpr int kLaneSteps = 128;                          // kMaxSteps (rgpu.cpp)
 constexpr int kLaneChgWords = kLaneSteps * kLaneShards;
 void launch_lane_fold(hipStream_t s, unsigned long long* lanechg, unsigned long long* lanefold);
@@ -105,7 +110,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
                      unsigned long long* lanechg, int32_t* uw0 = nullptr, int32_t* uw1 = nullptr,
-                     uint64_t* cb1 = nullptr, bool ends = false);
+                     uint64_t* cb1 = nullptr, bool ends = false, int32_t* ccount = nullptr);
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
 // (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
 // next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
@@ -114,13 +119,14 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr,
-                         const uint64_t* cb_prev = nullptr);
+                         const uint64_t* cb_prev = nullptr, const int32_t* ccount = nullptr, int dense_div = 0);
 // vm/em (partitioned mode): heavy ghosts (ranks >= n_own) have no compacted slots; their kept
 // slots are recomputed from the static adjacency (em & vm[nb] & vm[v]) while marking
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
                        const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm = nullptr,
-                       const uint64_t* em = nullptr, int64_t tcut = INT64_MIN);
+                       const uint64_t* em = nullptr, int64_t tcut = INT64_MIN, const int32_t* ccount = nullptr,
+                       int dense_div = 0);
 extern int g_sum_blocks;   // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 extern int g_hist_rounds;  // label-dedup rounds per (view, chunk) in k_cc_hist (RGPU_HIST_ROUNDS)
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
@@ -159,7 +165,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, int variant, unsigned long long* lanechg,
                     int32_t* hbest = nullptr, const int32_t* uw_cur = nullptr, int32_t* uw_next = nullptr,
-                    const ChgBits& cb = ChgBits());
+                    const ChgBits& cb = ChgBits(), int32_t* ccount = nullptr, int dense_div = 0);
 // Many late supersteps in one single-workgroup launch while the frontier stays below `cap`
 // vertices; info[0] <- last superstep executed (host-mapped).
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
@@ -218,7 +224,8 @@ void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32
                        int planes, const uint64_t* in, uint64_t* vm, int64_t vstride);
 void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t* xv, const int32_t* xq,
                       const uint8_t* act, const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab,
-                      const int32_t* uw, XRec* sbuf, unsigned long long* scnt);
+                      const int32_t* uw, XRec* sbuf, unsigned long long* scnt, const int32_t* ccount = nullptr,
+                      int dense_div = 0, int step = 0, int64_t n_own = 0);
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa);
 void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg);
 void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,

@@ -142,11 +142,13 @@ int rgpu_rgev_decode(const uint8_t* buf, size_t bytes, int64_t* t, uint8_t* kind
     if (bytes - off < block_bytes(m)) break;
     if (checksum(p + kHeader, block_bytes(m) - kHeader) != get<uint32_t>(p + 12)) return fail("block checksum mismatch");
     const int64_t base = get<int64_t>(p + 16);
+    // untrusted: range-check the base before any addition (base + dt stays below 2^61 + 2^32)
+    if (base < 0 || base >= ((int64_t)1 << 61)) return fail("block time base out of range");
     const uint8_t* kp = p + kHeader + 4 * m;
     const uint8_t* sp = kp + pad4(m);
     const uint8_t* dp = sp + 4 * m;
     for (size_t k = 0; k < m; k++) {
-      const int64_t tt = base + get<uint32_t>(p + kHeader + 4 * k);
+      const int64_t tt = (int64_t)((uint64_t)base + get<uint32_t>(p + kHeader + 4 * k));
       const int64_t d = get<int32_t>(dp + 4 * k);
       if (const char* e = check_update(tt, kp[k], get<int32_t>(sp + 4 * k), kp[k] >= RGPU_EADD ? d : 0)) return fail(e);
       if (kp[k] < RGPU_EADD && d != -1) return fail("vertex update with a dst");

@@ -72,6 +72,7 @@ struct Slot {
   int32_t* counts = nullptr;              // [nv][64] component counts at the root (zero between batches)
   uint64_t* chg[2] = {nullptr, nullptr};
   int32_t *stepcnt = nullptr, *hist = nullptr;   // stepcnt[r] = 1 iff superstep r changed a label
+  int32_t* ccount = nullptr;                      // changed vertices per step (kernels.hpp kCountShards)
   uint8_t* act[3] = {nullptr, nullptr, nullptr};   // CC frontier flags (byte per vertex)
   uint64_t* vadj = nullptr;                         // OR of kept slot masks per vertex
   unsigned long long* work = nullptr;               // [step][64 shards][visited, slots, changed]
@@ -188,6 +189,7 @@ struct rgpu_ctx {
   bool uw_on = true;                    // RGPU_UW: uniform label words (one partition, no tail kernel)
   bool ends_on = false;                 // RGPU_EMENDS=1: K1 folds endpoint memberships into CC edge words
                                         // (measured slower on C4: K1 55 -> 97 ms for K2 122 -> 117 ms)
+  int dense = -1;                       // RGPU_DENSE: dense-step divisor (kernels.hip dense_rule; -1 by size)
   int cb_on = 2;                        // RGPU_CHGBITS: changed bits beside the uniform words (0 off,
                                         // 1 superstep + heavy gather read them, 2 heavy gather only)
   bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
@@ -328,6 +330,16 @@ void run_check(hipStream_t st, const char* what, F launch) {
 // ghost rows arrive as per-lane records, so the ghosts' words stay kMixed (start_batch)
 bool use_uw(const rgpu_ctx* c) { return c->uw_on && !c->tail_on; }
 
+// dense-step divisor (kernels.hip dense_rule; RGPU_DENSE, 0 = off).  Not with the tail kernel,
+// which builds its frontier lists from the flags.
+// Default 4 on graphs of more than 2M vertices (C4: 529 -> 507 ms, `heavy` 103 -> 89 ms; 16:
+// 536 ms); off below (C2: 127.5 -> 132.3 ms with it: a small graph's flags are cached anyway).
+int dense_div(const rgpu_ctx* c) {
+  if (c->tail_on) return 0;
+  if (c->dense >= 0) return c->dense;
+  return c->g.nv > ((int64_t)1 << 21) ? 4 : 0;
+}
+
 // changed bits of superstep r (with uniform words; RGPU_CHGBITS=0 turns them off)
 ChgBits chg_bits(const rgpu_ctx* c, const Slot& s, int r) {
   ChgBits b;
@@ -412,6 +424,7 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       HIPCHK(hipHostMalloc((void**)&s.h_stats, sizeof(unsigned long long) * kStatWords));
       HIPCHK(hipHostMalloc((void**)&s.h_work, sizeof(unsigned long long) * kWorkWords));
       s.stepcnt = dalloc<int32_t>(L, kMaxSteps);
+      s.ccount = dalloc<int32_t>(L, (size_t)kMaxSteps * kCountShards);
       s.stats = dalloc<unsigned long long>(L, kStatWords);
       HIPCHK(hipMemset(s.stats, 0, sizeof(unsigned long long) * kStatWords));
     }
@@ -555,7 +568,8 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     if (hv)  // heavy vertices: segment minima before the step, neighbour marking after it
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[(r - 1) & 1], s.chg[(r - 1) & 1], s.act[r % 3],
-                            s.stepcnt, r, s.hv, uw ? s.uw[(r - 1) & 1] : nullptr, chg_bits(c, s, r).prev);
+                            s.stepcnt, r, s.hv, uw ? s.uw[(r - 1) & 1] : nullptr, chg_bits(c, s, r).prev, s.ccount,
+                            dense_div(c));
       }, r, per_launch);
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
@@ -563,12 +577,12 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
                      s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                      c->profile ? s.work : nullptr, c->step_variant | (g_rowbuf ? 16 : 0), s.stats + kLaneOff,
                      hv ? s.hv.best : nullptr, uw ? s.uw[(r - 1) & 1] : nullptr, uw ? s.uw[r & 1] : nullptr,
-                     chg_bits(c, s, r));
+                     chg_bits(c, s, r), s.ccount, dense_div(c));
     }, r, per_launch);
     if (hv)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[r & 1], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
-                          s.act[r % 3]);
+                          s.act[r % 3], nullptr, nullptr, INT64_MIN, s.ccount, dense_div(c));
       }, r, per_launch);
   }
   if (ea) {
@@ -730,6 +744,10 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   if (rc.algo == RGPU_ALGO_CC || rc.algo == RGPU_ALGO_DIFFUSION) {
     for (int b = 0; b < 3; b++) clr.act[b] = rc.algo == RGPU_ALGO_CC ? s.act[b] : s.dact[b];
     clr.n_act_words = (g.nv + 7) / 8 + 1;
+    if (rc.algo == RGPU_ALGO_CC) {
+      clr.ccount = s.ccount;
+      clr.n_ccount = (int64_t)kMaxSteps * kCountShards;
+    }
     const ChgBits cb1 = rc.algo == RGPU_ALGO_CC ? chg_bits(c, s, 1) : ChgBits();
     if (cb1.next) {
       for (int b = 0; b < 3; b++) clr.cb[b] = s.cb[b];
@@ -813,7 +831,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       launch_cc_slots(s.stream, gk, tcut, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                       c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff, use_uw(c) ? s.uw[0] : nullptr,
-                      use_uw(c) ? s.uw[1] : nullptr, chg_bits(c, s, 1).next, ends);
+                      use_uw(c) ? s.uw[1] : nullptr, chg_bits(c, s, 1).next, ends, s.ccount);
     });
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
@@ -1157,7 +1175,8 @@ void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
   }
   const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
   launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
-                   s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt);
+                   s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
+                   c->pk.n_own);
   launch_xcounts(s.stream, P, c->part, xs.scnt, s.stepcnt + r, xs.xab);
   HIPCHK(hipGetLastError());
   xs.x->alltoall_i64(xs.xab, xs.xab + 2 * P, 2, s.stream);
@@ -1187,7 +1206,8 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     grow_regions(&xs.sbuf, xs.scap, sent, P, s.stream);
     const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
     launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
-                     s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt);
+                     s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
+                   c->pk.n_own);
     HIPCHK(hipMemsetAsync(xs.scnt, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
   }
   if (!any) {  // every partition voted to halt
@@ -1243,7 +1263,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (hv)  // neighbours of heavy vertices (owned ones visited in r, ghosts just received) that changed
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[par], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
-                        r == 1 ? nullptr : s.act[r % 3], s.vm, s.em, s.tcut);
+                        r == 1 ? nullptr : s.act[r % 3], s.vm, s.em, s.tcut, s.ccount, dense_div(c));
     });
   HIPCHK(hipGetLastError());
   // superstep r+1 over the owned vertices
@@ -1252,13 +1272,14 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (hv)
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[n % 3], s.stepcnt, n, s.hv,
-                          use_uw(c) ? s.uw[r & 1] : nullptr, chg_bits(c, s, n).prev);
+                          use_uw(c) ? s.uw[r & 1] : nullptr, chg_bits(c, s, n).prev, s.ccount, dense_div(c));
     });
   timed_launch(c, si, KID_STEP, 0.0, [&] {
     launch_cc_step(s.stream, n, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[r & 1], s.lab[n & 1], s.chg[r & 1],
                    s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
                    c->profile ? s.work : nullptr, c->step_variant, s.stats + kLaneOff, hv ? s.hv.best : nullptr,
-                   use_uw(c) ? s.uw[r & 1] : nullptr, use_uw(c) ? s.uw[n & 1] : nullptr, chg_bits(c, s, n));
+                   use_uw(c) ? s.uw[r & 1] : nullptr, use_uw(c) ? s.uw[n & 1] : nullptr, chg_bits(c, s, n), s.ccount,
+                   dense_div(c));
   }, n);
   part_post_step(c, si, rc, n);
 }
@@ -2051,6 +2072,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   // under several settings in one process (tools/c4_ab.py); unset = the defaults
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   c->cb_on = env_int("RGPU_CHGBITS", 2);
+  c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   c->ends_on = env_int("RGPU_EMENDS", 0) != 0;
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
   g_tail_step = std::max(2, env_int("RGPU_TAIL_STEP", 14));

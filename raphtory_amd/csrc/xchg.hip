@@ -46,6 +46,15 @@ __device__ __forceinline__ int64_t owned_rank(const OwnIdx& I, int64_t id) {
   return -1;
 }
 
+// kernels.hip dense_rule(ccount, r - 1): superstep r ran with every member visited (its flags
+// were not written by a dense step r - 1)
+__device__ __forceinline__ bool dense_after(const int32_t* __restrict__ ccount, int r, int64_t nv, int div) {
+  if (div <= 0 || !ccount || r < 3) return false;
+  int64_t x = ccount[(r - 2) * kCountShards + (threadIdx.x & 63)];
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x * div >= nv;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ ghost membership
@@ -88,8 +97,11 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
                                                    const uint64_t* __restrict__ vadj,
                                                    const int32_t* __restrict__ lab,
                                                    const int32_t* __restrict__ uw, XRec* __restrict__ sbuf,
-                                                   unsigned long long* __restrict__ scnt) {
+                                                   unsigned long long* __restrict__ scnt,
+                                                   const int32_t* __restrict__ ccount, int dense_div, int step,
+                                                   int64_t n_own) {
   const int lane = lane_of();
+  if (dense_after(ccount, step, n_own, dense_div)) act = nullptr;  // the step visited every member
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t c = wave; c * 64 < nx; c += nwaves) {
@@ -383,9 +395,11 @@ void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32
 }
 void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t* xv, const int32_t* xq,
                       const uint8_t* act, const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab,
-                      const int32_t* uw, XRec* sbuf, unsigned long long* scnt) {
+                      const int32_t* uw, XRec* sbuf, unsigned long long* scnt, const int32_t* ccount, int dense_div,
+                      int step, int64_t n_own) {
   if (nx > 0)
-    k_xpack_rec<<<xgrid(nx, 4 * 64, 4096), 256, 0, s>>>(P, nx, xv, xq, act, chg_now, vadj, lab, uw, sbuf, scnt);
+    k_xpack_rec<<<xgrid(nx, 4 * 64, 4096), 256, 0, s>>>(P, nx, xv, xq, act, chg_now, vadj, lab, uw, sbuf, scnt,
+                                                         ccount, dense_div, step, n_own);
 }
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa) {
   k_xcounts<<<1, 64, 0, s>>>(np, me, scnt, stepflag, xa);
