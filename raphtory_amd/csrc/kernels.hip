@@ -15,6 +15,8 @@
 //   k_pr_slots/k_pr_step  PageRank spec
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <climits>
 #include <cstdint>
 
@@ -476,6 +478,14 @@ __device__ __forceinline__ int64_t wave_span(int64_t n, int64_t nwaves) {
 struct StepWork {
   unsigned long long v = 0, s = 0, g = 0, a = 0, lr = 0, lw = 0, uw = 0;
 };
+// The work counters of a launch without a work buffer: every update compiles away (the counters
+// otherwise hold 14 VGPRs through the superstep kernel)
+struct NoCount {
+  __device__ NoCount& operator+=(unsigned long long) { return *this; }
+};
+struct NoWork {
+  NoCount v, s, g, a, lr, lw, uw;
+};
 
 // ---------------------------------------------------------------- K2: batch CSR (+ superstep 1)
 // One wave per vertex.  Static slots of rank v = its out-edges then its in-edges
@@ -832,7 +842,7 @@ __device__ __forceinline__ void mark(bool want, int32_t v, uint8_t* act_next, co
 // chunk.  All loads are unconditional from padded buffers (see gather_min).  A visited
 // vertex rewrites its row only if it changed now or in the previous step (the only cases
 // where the two label buffers differ).  uw_cur / uw_next: uniform label words (null: rows only).
-template <int CH, bool BUF, bool TAIL>
+template <int CH, bool BUF, bool TAIL, class WK>
 __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_t* __restrict__ adj_off,
                                          const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
                                          const int32_t* __restrict__ snbr,
@@ -842,11 +852,10 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          uint64_t* __restrict__ chg_next, uint8_t* __restrict__ act_next,
                                          const TailList& tl, int lane, int32_t& changed,
                                          unsigned long long* __restrict__ lds_lanes,
-                                         StepWork& wk, const int32_t* __restrict__ hv_of = nullptr,
+                                         WK& wk, const int32_t* __restrict__ hv_of = nullptr,
                                          int32_t* __restrict__ hbest = nullptr,
                                          const int32_t* __restrict__ uw_cur = nullptr,
                                          int32_t* __restrict__ uw_next = nullptr,
-                                         const uint64_t* __restrict__ cb_prev = nullptr,
                                          uint64_t* __restrict__ cb_next = nullptr, bool skip_marks = false) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
@@ -887,39 +896,15 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     // then the uniform words of the neighbours that changed
     uint64_t act[CH];
     int32_t un[CH];
-    if (cb_prev) {
-      // changed-bit path: a neighbour whose bit is clear did not change in r-1 (nothing to
-      // read: one probe of an L2-resident bitmap instead of a random 8-B change word); a
-      // changed uniform neighbour's word is folded on every kept view of the slot (folding an
-      // unchanged view's label is a no-op: it is >= the label the vertex already holds, see
-      // DESIGN.md §4); only a changed mixed neighbour needs its change word and row lanes
-      // (the change word is loaded beside the uniform word, not after it: one dependent
-      // trip per hot neighbour, as without the bits)
-      uint64_t cw[CH];
 #pragma unroll
-      for (int i = 0; i < CH; i++) {
-        const bool hot = sm[i] != 0 && ((cb_prev[nb[i] >> 6] >> (nb[i] & 63)) & 1);
-        un[i] = hot ? uw_cur[nb[i]] : kMixed;
-        cw[i] = hot ? chg_prev[nb[i]] : 0;
-        act[i] = hot ? sm[i] : 0;
-      }
+    for (int i = 0; i < CH; i++) {
+      act[i] = sm[i] & chg_prev[nb[i]];
+    }
 #pragma unroll
-      for (int i = 0; i < CH; i++) {
-        if (un[i] == kMixed) act[i] &= cw[i];
-        wk.a += __popcll(__ballot(act[i] != 0 || un[i] != kMixed)) + 2 * __popcll(__ballot(act[i] != 0 && un[i] == kMixed));
-        wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < CH; i++) {
-        act[i] = sm[i] & chg_prev[nb[i]];
-      }
-#pragma unroll
-      for (int i = 0; i < CH; i++) {
-        un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
-        if (uw_cur) wk.a += __popcll(__ballot(act[i] != 0));
-        wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
-      }
+    for (int i = 0; i < CH; i++) {
+      un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
+      if (uw_cur) wk.a += __popcll(__ballot(act[i] != 0));
+      wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
     }
     // own rows are only meaningful on member lanes
 #pragma unroll
@@ -953,20 +938,9 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
           const int32_t j = c2 + lane;
           const int64_t idx = base + (j < n ? j : c2);
           const int32_t q = snbr[idx];
-          uint64_t a2;
-          int32_t u2;
-          if (cb_prev) {
-            const uint64_t m2 = j < n ? smask[idx] : 0;
-            const bool hot = m2 != 0 && ((cb_prev[q >> 6] >> (q & 63)) & 1);
-            u2 = hot ? uw_cur[q] : kMixed;
-            const uint64_t c2w = hot ? chg_prev[q] : 0;
-            a2 = hot ? (u2 == kMixed ? m2 & c2w : m2) : 0;
-            wk.a += __popcll(__ballot(hot)) + 2 * __popcll(__ballot(hot && u2 == kMixed));
-          } else {
-            a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
-            u2 = (uw_cur && a2) ? uw_cur[q] : kMixed;
-            if (uw_cur) wk.a += __popcll(__ballot(a2 != 0));
-          }
+          const uint64_t a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
+          const int32_t u2 = (uw_cur && a2) ? uw_cur[q] : kMixed;
+          if (uw_cur) wk.a += __popcll(__ballot(a2 != 0));
           wk.g += u2 == kMixed ? __popcll(a2) : 0;
           best[i] = gather_min<BUF>(u2 == kMixed ? a2 : 0, q, best[i], lab_cur, lane);
           if (uw_cur) best[i] = fold_uniform(__ballot(u2 != kMixed), a2, u2, best[i], lane);
@@ -1051,8 +1025,9 @@ __global__ __launch_bounds__(256) void k_uw_rows(int64_t nv, const uint64_t* __r
 // Superstep kernel (full grid).  Step r visits the vertices flagged in act_cur (bytes, plain
 // idempotent stores by step r-1), CH consecutive ranks per wave-chunk, and clears act_clear
 // (read two steps ago, written next step).
-template <int CH, bool BUF>
-__global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const int64_t* __restrict__ adj_off,
+// MINW > 1: amdgpu_waves_per_eu(MINW) (a VGPR cap; RGPU_STEP_VARIANT | 64 selects 6 waves/SIMD)
+template <int CH, bool BUF, int MINW, bool PROF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void k_cc_step2(int step, int64_t nv, const int64_t* __restrict__ adj_off,
                                                   const uint64_t* __restrict__ vm,
                                                   const int32_t* __restrict__ cnt,
                                                   const int32_t* __restrict__ snbr,
@@ -1071,7 +1046,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
                                                   int32_t* __restrict__ hbest,
                                                   unsigned long long* __restrict__ lanechg,
                                                   const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
-                                                  const uint64_t* __restrict__ cb_prev, uint64_t* __restrict__ cb_next,
+                                                  uint64_t* __restrict__ cb_next,
                                                   uint64_t* __restrict__ cb_clear, int64_t cb_words,
                                                   int32_t* __restrict__ ccount, int dense_div) {
   if (stepflag[step - 1] == 0) return;
@@ -1095,7 +1070,7 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int32_t changed = 0;
-  StepWork wk;
+  std::conditional_t<PROF, StepWork, NoWork> wk;
   const TailList none{nullptr, nullptr};
   // `span` (<= 64) chunks per wave round: lane l reads chunk l's frontier flags (one coalesced
   // load), and the wave then runs only the flagged chunks — a sparse frontier costs one load per
@@ -1125,14 +1100,14 @@ __global__ __launch_bounds__(256) void k_cc_step2(int step, int64_t nv, const in
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
       cc_chunk<CH, BUF, false>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
                                lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
-                               hv_of, hbest, uw_cur, uw_next, cb_prev, cb_next, skip_marks);
+                               hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks);
     }
   }
-  if (work)
+  if constexpr (PROF)
     for (int o = 32; o > 0; o >>= 1) wk.g += __shfl_xor(wk.g, o);
   if (lane == 0) {
     if (changed) atomicAdd(&red, changed);
-    if (work) {
+    if constexpr (PROF) {
       const unsigned long long f[7] = {wk.v, wk.s, 0, wk.g, wk.a, wk.lr, wk.lw};
 #pragma unroll
       for (int i = 0; i < 7; i++)
@@ -1388,7 +1363,7 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
       const int32_t q = snbr[idx];
       uint64_t a;
       int32_t u;
-      if (cb_prev) {  // changed-bit path (cc_chunk): uniform changed neighbours on every kept view
+      if (cb_prev) {  // changed bits: uniform changed neighbours on every kept view (exact)
         const uint64_t m = jj < n ? smask[idx] : 0;
         const bool hot = m != 0 && ((cb_prev[q >> 6] >> (q & 63)) & 1);
         u = hot ? uw_cur[q] : kMixed;
@@ -2185,7 +2160,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, int variant, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next,
                     const ChgBits& cb, int32_t* ccount, int dense_div) {
-  const int ch = (variant & 15) == 8 ? 8 : 4;
+  const int ch = (variant & 15) == 8 ? 8 : 4;  // (variant & 96: VGPR caps, see k_cc_step2)
   const bool buf = (variant & 16) != 0;
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
   // A small graph's dense supersteps are latency-bound and share the GPU with the other batch
@@ -2197,11 +2172,15 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.step_reads ? cb.prev : nullptr, cb.next, cb.clear, cb.words, ccount, dense_div
-  if (ch == 8 && buf) k_cc_step2<8, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else if (ch == 8) k_cc_step2<8, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else if (buf) k_cc_step2<4, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else k_cc_step2<4, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+    cb.next, cb.clear, cb.words, ccount, dense_div
+  // work != null (profile runs): the counting instantiation; the timed runs use the lean one
+  if (ch == 8 && buf) k_cc_step2<8, true, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else if (ch == 8) k_cc_step2<8, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else if (buf) k_cc_step2<4, true, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else if ((variant & 64) && work) k_cc_step2<4, false, 6, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else if (variant & 64) k_cc_step2<4, false, 6, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else if (work) k_cc_step2<4, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else k_cc_step2<4, false, 1, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
 #undef RGPU_STEP_ARGS
 }
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,

@@ -147,16 +147,15 @@ void launch_check_labels(hipStream_t s, int64_t nv, const uint64_t* vm, const in
                          unsigned long long* bad);
 void launch_check_slots(hipStream_t s, int64_t nv, const int64_t* adj_off, const uint64_t* vm, const int32_t* cnt,
                         const int32_t* snbr, const int32_t* uw0, const int32_t* uw1, unsigned long long* bad);
-// Changed bits (with uniform words only): one bit per local rank, set when the vertex's label
-// changed in a step; three bitmaps rotate (step r writes r % 3, reads (r - 1) % 3 and clears
-// (r + 1) % 3).  A superstep probes a neighbour's bit (L2-resident: 2.5 MB for 20M vertices)
-// before it touches the neighbour's words.  All null: the change words alone.
+// Changed bits (with uniform words and heavy vertices): one bit per local rank, set when the
+// vertex's label changed in a step; three bitmaps rotate (step r writes r % 3, the hub gather of
+// step r+1 reads it, step r+2 clears it).  The hub gather probes a neighbour's bit (L2-resident:
+// 2.5 MB for 20M vertices) before it touches the neighbour's words.  All null: off.
 struct ChgBits {
   const uint64_t* prev = nullptr;
   uint64_t* next = nullptr;
   uint64_t* clear = nullptr;
   int64_t words = 0;  // words cleared (every local rank, ghosts included)
-  bool step_reads = true;  // false: the superstep kernel writes / clears them but reads change words
 };
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,

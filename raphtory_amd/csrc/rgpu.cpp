@@ -190,8 +190,7 @@ struct rgpu_ctx {
   bool ends_on = false;                 // RGPU_EMENDS=1: K1 folds endpoint memberships into CC edge words
                                         // (measured slower on C4: K1 55 -> 97 ms for K2 122 -> 117 ms)
   int dense = -1;                       // RGPU_DENSE: dense-step divisor (kernels.hip dense_rule; -1 by size)
-  int cb_on = 2;                        // RGPU_CHGBITS: changed bits beside the uniform words (0 off,
-                                        // 1 superstep + heavy gather read them, 2 heavy gather only)
+  int cb_on = 1;                        // RGPU_CHGBITS=0: no changed bits (kernels.hpp ChgBits)
   bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
   int tail_cap = 256;                   // RGPU_TAIL_CAP: widest frontier the tail kernel takes
   int64_t tail_maxv = 4 << 20;          // RGPU_TAIL_MAXV: no tail kernel above this many vertices
@@ -344,12 +343,11 @@ int dense_div(const rgpu_ctx* c) {
 ChgBits chg_bits(const rgpu_ctx* c, const Slot& s, int r) {
   ChgBits b;
   if (!use_uw(c) || !c->cb_on || !s.cb[0]) return b;
-  // RGPU_CHGBITS=2 (default): written, read by the heavy gather only, and only when there are
+  // Written by the superstep kernels, read by the heavy gather only, and only when there are
   // heavy vertices.  The superstep kernel reading them measured slower on C4 (cc_step 263 ->
-  // 301 ms serial; the gather's bit probe + word loads vs one change word) and on C2; the heavy
+  // 301 ms serial; the bit probe then the words vs one change word) and on C2; the heavy
   // gather, which walks a hub's whole kept slot list every step, gained (119 -> 103 ms).
-  if (c->cb_on == 2 && c->g.n_seg == 0) return b;
-  b.step_reads = c->cb_on == 1;
+  if (c->g.n_seg == 0) return b;
   b.prev = s.cb[(r + 2) % 3];
   b.next = s.cb[r % 3];
   b.clear = s.cb[(r + 1) % 3];
@@ -1555,7 +1553,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->hostflags = env_int("RGPU_HOSTFLAG", 1) != 0;
   c->tail_on = env_int("RGPU_TAIL", 0) != 0;
   c->uw_on = env_int("RGPU_UW", 1) != 0;
-  c->cb_on = env_int("RGPU_CHGBITS", 2);
+  c->cb_on = env_int("RGPU_CHGBITS", 1);
   c->check = env_int("RGPU_CHECK", 0) != 0;
   c->wmajor = env_int("RGPU_WMAJOR", 1) != 0;
   c->poll = env_int("RGPU_POLL", 1) != 0;
@@ -2071,7 +2069,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   // superstep launch knobs are re-read per run, so that one sealed graph can be A/B-timed
   // under several settings in one process (tools/c4_ab.py); unset = the defaults
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
-  c->cb_on = env_int("RGPU_CHGBITS", 2);
+  c->cb_on = env_int("RGPU_CHGBITS", 1);
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   c->ends_on = env_int("RGPU_EMENDS", 0) != 0;
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));

@@ -5,7 +5,7 @@ timeout -k 10 300 python -u -m pytest tests -m "gpu and not fullsize" -x -q -p n
 tail -2 gpurun_out/pytest_fast.log
 RGPU_DENSE=1000 timeout -k 10 300 python -u -m pytest tests -m "gpu and not fullsize" -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/pytest_dense.log 2>&1 || { tail -30 gpurun_out/pytest_dense.log; exit 1; }
 tail -2 gpurun_out/pytest_dense.log
-timeout -k 10 700 python -u tools/c4_ab.py ${AB_ARGS:---heavy 2048,512 base: d4:RGPU_DENSE=4 d16:RGPU_DENSE=16} > gpurun_out/c4_ab.log 2>&1 || exit $?
-for v in ${C2_ENV:-RGPU_DENSE=0 RGPU_DENSE=4}; do
+timeout -k 10 700 python -u tools/c4_ab.py ${AB_ARGS:-base: w6:RGPU_STEP_VARIANT=68} > gpurun_out/c4_ab.log 2>&1 || exit $?
+for v in ${C2_ENV:-RGPU_STEP_VARIANT=4 RGPU_STEP_VARIANT=68}; do
   env $v timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline --no-edge-counts --steps 5 --warmup 2 > gpurun_out/c2_$v.log 2>&1 || exit $?
 done
