@@ -283,11 +283,14 @@ __device__ __forceinline__ void edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1]
                                           const BatchParams& bp, int64_t e, const int32_t* __restrict__ esrc,
                                           const int32_t* __restrict__ edst, const int64_t* __restrict__ eoff,
                                           const int64_t* __restrict__ ekey, const int64_t* __restrict__ doff,
-                                          const int64_t* __restrict__ dtime) {
+                                          const int64_t* __restrict__ dtime, const uint64_t* __restrict__ dbits) {
   const int K = L.K;
   const int64_t lo = eoff[e], hi = eoff[e + 1];
   const int32_t s = esrc[e], d = edst[e];
-  const int64_t s0 = doff[s], s1 = doff[s + 1], d0 = doff[d], d1 = doff[d + 1];
+  // endpoints without deaths (an L2-resident bit each) skip their death-list offsets: an empty
+  // list [0, 0) reads as "no death" everywhere below
+  const bool ds = !dbits || ((dbits[s >> 6] >> (s & 63)) & 1), dd = !dbits || ((dbits[d >> 6] >> (d & 63)) & 1);
+  const int64_t s0 = ds ? doff[s] : 0, s1 = ds ? doff[s + 1] : 0, d0 = dd ? doff[d] : 0, d1 = dd ? doff[d + 1] : 0;
   if (bp.sorted && bp.iv_max >= 0) {
     const int64_t f0 = floor_idx(ekey, lo, hi, L.hop[0]);
     const int64_t f1 = floor_idx(ekey, lo, hi, L.hop[K - 1]);
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
                                                    uint64_t* __restrict__ em, int64_t estride,
                                                    unsigned long long* __restrict__ ecnt, int64_t h0,
                                                    int64_t own_lim, const uint64_t* __restrict__ vm_ends,
-                                                   int64_t vstride) {
+                                                   int64_t vstride, const uint64_t* __restrict__ dbits) {
   __shared__ HopLDS L;
   __shared__ unsigned int cnt_s[PLANAR ? kMaxPlanes : 1][64];
   hop_lds_init(L, bp, bp.thr_e);
@@ -365,7 +368,7 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
     uint64_t m[NP] = {};
     uint64_t mo[NP];  // the edge's own aliveness (the |E_w| counts)
     if (e < ne) {
-      edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime);
+      edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime, dbits);
 #pragma unroll
       for (int w = 0; w < NP; w++) mo[w] = m[w];
       if (vm_ends) {  // CC: both endpoints' memberships folded in (K2 then skips vm[nb])
@@ -2117,7 +2120,7 @@ void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp,
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
                       unsigned long long* ecnt, int64_t h0, const uint64_t* vm_ends, int64_t vstride) {
 #define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, bp, em, g.ne, ecnt, h0, g.n_own, vm_ends, \
-    vstride
+    vstride, g.dbits
   const unsigned grid = grid_for(g.ne, 256);
   if (planar && ecnt) k_edge_mask<true, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
   else if (planar) k_edge_mask<true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);

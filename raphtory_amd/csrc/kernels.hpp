@@ -26,6 +26,7 @@ struct DevGraph {
   int64_t nv = 0, ne = 0, n_in = 0;
   const int64_t *voff = nullptr, *vkey = nullptr;    // vertex histories
   const int64_t *doff = nullptr, *dtime = nullptr;   // vertex death lists
+  const uint64_t* dbits = nullptr;                   // bit v: vertex v has a death (null: read doff)
   const int32_t *esrc = nullptr, *edst = nullptr;    // edges sorted by (src, dst)
   const int64_t *eoff = nullptr, *ekey = nullptr;    // edge own histories
   const int64_t *out_off = nullptr, *in_off = nullptr;

@@ -1683,6 +1683,16 @@ const int64_t* upload_adj(std::vector<void*>& L, const std::vector<int64_t>& out
   return dupload(L, adj);
 }
 
+// one bit per vertex: it has a death (K1 skips the death-list offsets of an edge whose
+// endpoints have none; DevGraph.dbits)
+const uint64_t* upload_death_bits(std::vector<void*>& L, const std::vector<int64_t>& doff) {
+  const int64_t nv = doff.empty() ? 0 : (int64_t)doff.size() - 1;
+  std::vector<uint64_t> bits((size_t)(nv + 63) / 64 + 1, 0);
+  for (int64_t v = 0; v < nv; v++)
+    if (doff[v + 1] > doff[v]) bits[v >> 6] |= 1ull << (v & 63);
+  return dupload(L, bits);
+}
+
 void finish_seal(rgpu_ctx* c) {
   Packed& P = c->pk;
   c->st.vertices = P.n_own;
@@ -1831,6 +1841,7 @@ void seal_delta(rgpu_ctx* c) {
     g.adj_off = upload_adj(L, D.out_off, D.in_off);
     g.doff = dupload(L, D.doff);
     g.dtime = dupload(L, D.dtime);
+    g.dbits = upload_death_bits(L, D.doff);
     HIPCHK(hipStreamSynchronize(s));
     phase("adjacency");
     build_heavy(c, g, L, D.out_off, D.in_off);
@@ -1929,6 +1940,7 @@ int rgpu_seal(rgpu_ctx* c) {
     g.vkey = dupload(L, P.vkey);
     g.doff = dupload(L, P.doff);
     g.dtime = dupload(L, P.dtime);
+    g.dbits = upload_death_bits(L, P.doff);
     g.esrc = dupload(L, P.esrc);
     g.edst = dupload(L, P.edst);
     g.eoff = dupload(L, P.eoff);
