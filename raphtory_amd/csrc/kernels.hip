@@ -505,6 +505,7 @@ struct NoWork {
 // bitmap and stepcnt[1]; vadj[v] = OR of v's kept slot masks (v isolated in view j iff bit j
 // is clear).
 
+template <bool PROF>  // PROF = false: the work counters compile away (launch_cc_slots: work == null)
 __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int64_t* __restrict__ out_off,
                                                   const int64_t* __restrict__ in_off,
@@ -540,7 +541,9 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  unsigned long long members = 0, alive = 0, changed = 0, scanned = 0, lw = 0, uwn = 0;
+  using Ctr = std::conditional_t<PROF, unsigned long long, NoCount>;
+  Ctr members{}, alive{}, scanned{}, lw{}, uwn{};
+  unsigned long long changed = 0;
   uint64_t lanes = 0;  // views with a step-1 change in this wave
   // `span` (<= 64) vertices per wave round: the lanes read their view masks (one coalesced load),
   // clear the non-members' count / mask words, and the wave then walks the members one by one.
@@ -693,8 +696,10 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
    }
   }
   if (lane == 0) {
-    if (members) atomicAdd(&red[0], members);
-    if (alive) atomicAdd(&red[1], alive);
+    if constexpr (PROF) {
+      if (members) atomicAdd(&red[0], members);
+      if (alive) atomicAdd(&red[1], alive);
+    }
     if (changed) atomicAdd(&red[2], changed);
   }
   publish_lanes(lanes, &red[3], lanechg, 1);  // (its barrier also publishes red[0..2])
@@ -706,9 +711,11 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     }
     add_work(work, 1, red[0], red[1], red[2]);
   }
-  if (work && lane == 0) {  // (uniform per wave)
-    const unsigned long long f[8] = {0, 0, 0, 0, scanned, 0, lw, uwn};
-    add_work(work, 1, f);
+  if constexpr (PROF) {
+    if (work && lane == 0) {  // (uniform per wave)
+      const unsigned long long f[8] = {0, 0, 0, 0, scanned, 0, lw, uwn};
+      add_work(work, 1, f);
+    }
   }
 }
 
@@ -2135,7 +2142,8 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends,
                      int32_t* ccount) {
   const bool hv = g.n_seg > 0;
-  k_cc_slots<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
+  auto* kern = work ? k_cc_slots<true> : k_cc_slots<false>;
+  kern<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
