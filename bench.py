@@ -91,7 +91,8 @@ def pmc_traffic(kernel, config="C2"):
         return None, None
     if kernel not in d.get("FETCH_SIZE", {}).get("kernel", ""):
         return None, None
-    return round(d["traffic_bytes_per_launch"]["value"]), "profiles/latest_pmc.json: " + d["traffic_bytes_per_launch"]["formula"]
+    return (round(d["traffic_bytes_per_launch"]["value"]),
+            os.path.relpath(path, ROOT) + ": " + d["traffic_bytes_per_launch"]["formula"])
 
 
 def cpu_info():
@@ -267,10 +268,29 @@ def log(msg):
 
 
 def kernel_table(stats):
+    """Per kernel group: launches, serial ms, and GB/s of the DESIGN.md §4 byte model (None where
+    the group has no byte model: the hub kernels)."""
     return {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
                 "avg_us": round(v["ms"] * 1e3 / v["launches"], 2),
-                "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
+                "GBps": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1) if v["bytes"] > 0 else None}
             for k, v in stats["kernels"].items() if v["launches"]}
+
+
+def profile_passes(g, hops, windows):
+    """Two serial profiled passes of the same query: a counting pass (the kernels' work counters ->
+    DESIGN.md §4 bytes per kernel) and a lean pass (RGPU_PROF_LEAN=1: the same launches on the
+    instantiations the timed runs use, under HIP events -> ms).  Returns {kernel: {launches, ms,
+    bytes}} with bytes from the first and launches / ms from the second."""
+    g.run("cc", hops, windows, profile=True, serial=True)
+    counted = g.stats()["kernels"]
+    os.environ["RGPU_PROF_LEAN"] = "1"
+    try:
+        g.run("cc", hops, windows, profile=True, serial=True)
+    finally:
+        os.environ.pop("RGPU_PROF_LEAN", None)
+    lean = g.stats()["kernels"]
+    return {k: {"launches": v["launches"], "ms": v["ms"], "bytes": counted.get(k, {}).get("bytes", 0.0),
+                "ms_counting_pass": counted.get(k, {}).get("ms", 0.0)} for k, v in lean.items()}
 
 
 def survey_bytes(summ, n_hops, windows, nv, ne, n_ev, ks, launches_step):
@@ -378,9 +398,8 @@ def run_c4(a, rank, world, local):
     summ = None if a.profile_only else g.cc_summaries()  # (profile-only: after the profile pass)
     roofline, ks, s8d = None, {}, None
     if not a.no_profile_pass:
-        g.run("cc", hops, windows, profile=True, serial=True)  # collective at N > 1
-        ks = kernel_table(g.stats())
-        kraw = g.stats()["kernels"]
+        kraw = profile_passes(g, hops, windows)  # collective at N > 1
+        ks = kernel_table({"kernels": kraw})
         if summ is None:
             summ = g.cc_summaries()
         d = kraw["cc_step"]
@@ -390,8 +409,10 @@ def run_c4(a, rank, world, local):
                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
                     "avg_launch_us": round(d["ms"] * 1e3 / d["launches"], 2),
                     "algorithmic_bytes_per_launch": d["bytes"] / d["launches"],
+                    "avg_launch_us_counting_pass": round(d["ms_counting_pass"] * 1e3 / d["launches"], 2),
                     "bytes_model": "DESIGN.md §4 (bytes the superstep must touch per visited vertex / slot / "
-                                   "gathered label, counted by the kernel)"}
+                                   "gathered label, counted by the kernel in a counting pass); time = the same "
+                                   "launches of the lean instantiation the timed query runs (RGPU_PROF_LEAN)"}
         if not a.no_edge_counts and world == 1:
             g.run("cc", hops, windows, edge_counts=True)
             summ = g.cc_summaries()
@@ -574,9 +595,8 @@ def run_c2(a, rank, world, local, quiet=False):
     kstats = {}
     s8d = None
     if not a.no_profile_pass:
-        g.run("cc", hops, windows, profile=True, serial=True)
-        kstats = kernel_table(g.stats())
-        kraw = g.stats()["kernels"]
+        kraw = profile_passes(g, hops, windows)
+        kstats = kernel_table({"kernels": kraw})
         d = kraw["cc_step"]
         gbs = d["bytes"] / (d["ms"] / 1e3) / 1e9
         traffic, tsrc = pmc_traffic("k_cc_step2")

@@ -1373,9 +1373,11 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
       const int32_t q = snbr[idx];
       uint64_t a;
       int32_t u;
-      if (cb_prev) {  // changed bits: uniform changed neighbours on every kept view (exact)
-        const uint64_t m = jj < n ? smask[idx] : 0;
-        const bool hot = m != 0 && ((cb_prev[q >> 6] >> (q & 63)) & 1);
+      if (cb_prev) {  // changed bits: uniform changed neighbours on every kept view (exact);
+                      // the slot's mask word is read only for a changed neighbour (the walk streams
+                      // the hub's slot list: 4 B instead of 12 B per unchanged neighbour)
+        const bool hot = jj < n && ((cb_prev[q >> 6] >> (q & 63)) & 1);
+        const uint64_t m = hot ? smask[idx] : 0;
         u = hot ? uw_cur[q] : kMixed;
         a = hot ? (u == kMixed ? m & chg_prev[q] : m) : 0;
       } else {

@@ -189,6 +189,7 @@ struct rgpu_ctx {
   bool uw_on = true;                    // RGPU_UW: uniform label words (one partition, no tail kernel)
   bool ends_on = false;                 // RGPU_EMENDS=1: K1 folds endpoint memberships into CC edge words
                                         // (measured slower on C4: K1 55 -> 97 ms for K2 122 -> 117 ms)
+  bool prof_lean = false;               // RGPU_PROF_LEAN (work_buf)
   int dense = -1;                       // RGPU_DENSE: dense-step divisor (kernels.hip dense_rule; -1 by size)
   int cb_on = 1;                        // RGPU_CHGBITS=0: no changed bits (kernels.hpp ChgBits)
   bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
@@ -328,6 +329,13 @@ void run_check(hipStream_t st, const char* what, F launch) {
 // uniform label words (kernels.hip): not with the tail kernel (it writes rows only).  Partitioned:
 // ghost rows arrive as per-lane records, so the ghosts' words stay kMixed (start_batch)
 bool use_uw(const rgpu_ctx* c) { return c->uw_on && !c->tail_on; }
+
+// The work-counter buffer of a profile run.  RGPU_PROF_LEAN=1: none, so the superstep and K2
+// kernels run their lean instantiations (the ones timed runs use) under the profile events; a
+// counting pass and a lean pass of the same query give bytes and times of the same launches.
+unsigned long long* work_buf(const rgpu_ctx* c, const Slot& s) {
+  return c->profile && !c->prof_lean ? s.work : nullptr;
+}
 
 // dense-step divisor (kernels.hip dense_rule; RGPU_DENSE, 0 = off).  Not with the tail kernel,
 // which builds its frontier lists from the flags.
@@ -573,7 +581,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                      s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
                      s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
-                     c->profile ? s.work : nullptr, c->step_variant | (g_rowbuf ? 16 : 0), s.stats + kLaneOff,
+                     work_buf(c, s), c->step_variant | (g_rowbuf ? 16 : 0), s.stats + kLaneOff,
                      hv ? s.hv.best : nullptr, uw ? s.uw[(r - 1) & 1] : nullptr, uw ? s.uw[r & 1] : nullptr,
                      chg_bits(c, s, r), s.ccount, dense_div(c));
     }, r, per_launch);
@@ -828,7 +836,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     timed_launch(c, si, KID_SLOTS, b2, [&] {  // (partitioned: owned vertices only, gk)
       launch_cc_slots(s.stream, gk, tcut, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
-                      c->profile ? s.work : nullptr, s.hv, s.stats + kLaneOff, use_uw(c) ? s.uw[0] : nullptr,
+                      work_buf(c, s), s.hv, s.stats + kLaneOff, use_uw(c) ? s.uw[0] : nullptr,
                       use_uw(c) ? s.uw[1] : nullptr, chg_bits(c, s, 1).next, ends, s.ccount);
     });
     if (c->check)
@@ -1275,7 +1283,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   timed_launch(c, si, KID_STEP, 0.0, [&] {
     launch_cc_step(s.stream, n, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[r & 1], s.lab[n & 1], s.chg[r & 1],
                    s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
-                   c->profile ? s.work : nullptr, c->step_variant, s.stats + kLaneOff, hv ? s.hv.best : nullptr,
+                   work_buf(c, s), c->step_variant, s.stats + kLaneOff, hv ? s.hv.best : nullptr,
                    use_uw(c) ? s.uw[r & 1] : nullptr, use_uw(c) ? s.uw[n & 1] : nullptr, chg_bits(c, s, n), s.ccount,
                    dense_div(c));
   }, n);
@@ -2082,6 +2090,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   // under several settings in one process (tools/c4_ab.py); unset = the defaults
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   c->cb_on = env_int("RGPU_CHGBITS", 1);
+  c->prof_lean = env_int("RGPU_PROF_LEAN", 0) != 0;
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   c->ends_on = env_int("RGPU_EMENDS", 0) != 0;
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
