@@ -463,7 +463,9 @@ __device__ __forceinline__ unsigned row_lines(uint64_t m) {
 // (ccount[(r-1)*64 + shard]: changed vertices per step, 64 shards, summed here by each wave;
 // every block of a launch computes the same answer from counts the previous launch finished).
 // div <= 0: never.  Step 1 (K2) always writes its flags.
+constexpr int kUwFirst = 1 << 20;  // dense_div flag: visit-all steps read uniform words first
 __device__ __forceinline__ bool dense_rule(const int32_t* __restrict__ ccount, int r, int64_t nv, int div) {
+  div &= kUwFirst - 1;
   if (div <= 0 || !ccount || r < 2) return false;
   int64_t x = ccount[(r - 1) * kCountShards + (threadIdx.x & 63)];
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
@@ -866,7 +868,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          int32_t* __restrict__ hbest = nullptr,
                                          const int32_t* __restrict__ uw_cur = nullptr,
                                          int32_t* __restrict__ uw_next = nullptr,
-                                         uint64_t* __restrict__ cb_next = nullptr, bool skip_marks = false) {
+                                         uint64_t* __restrict__ cb_next = nullptr, bool skip_marks = false,
+                                         bool uw_first = false) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
@@ -906,15 +909,30 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     // then the uniform words of the neighbours that changed
     uint64_t act[CH];
     int32_t un[CH];
+    if (uw_first) {
+      // a step that visits every member (dense predecessor): most neighbours changed, so read
+      // the neighbour's uniform word first and fold it on every kept view of the slot (exact:
+      // an unchanged view's label cannot lower ours); only a mixed neighbour
+      // needs its change word and row lanes — one dependent trip less per uniform neighbour
 #pragma unroll
-    for (int i = 0; i < CH; i++) {
-      act[i] = sm[i] & chg_prev[nb[i]];
-    }
+      for (int i = 0; i < CH; i++) un[i] = sm[i] ? uw_cur[nb[i]] : kMixed;
 #pragma unroll
-    for (int i = 0; i < CH; i++) {
-      un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
-      if (uw_cur) wk.a += __popcll(__ballot(act[i] != 0));
-      wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
+      for (int i = 0; i < CH; i++) {
+        act[i] = un[i] != kMixed ? sm[i] : (sm[i] ? sm[i] & chg_prev[nb[i]] : 0);
+        wk.a += __popcll(__ballot(sm[i] != 0)) + 2 * __popcll(__ballot(sm[i] != 0 && un[i] == kMixed));
+        wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        act[i] = sm[i] & chg_prev[nb[i]];
+      }
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
+        if (uw_cur) wk.a += __popcll(__ballot(act[i] != 0));
+        wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
+      }
     }
     // own rows are only meaningful on member lanes
 #pragma unroll
@@ -1110,7 +1128,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
       cc_chunk<CH, BUF, false>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
                                lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
-                               hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks);
+                               hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks,
+                               visit_all && uw_cur && (dense_div & kUwFirst));
     }
   }
   if constexpr (PROF)
