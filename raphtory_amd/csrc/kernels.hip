@@ -507,7 +507,9 @@ struct NoWork {
 // bitmap and stepcnt[1]; vadj[v] = OR of v's kept slot masks (v isolated in view j iff bit j
 // is clear).
 
-template <bool PROF>  // PROF = false: the work counters compile away (launch_cc_slots: work == null)
+// PROF = false: the work counters compile away (launch_cc_slots: work == null).  G: members whose
+// first slot chunk is loaded together (RGPU_SLOTS_GROUP)
+template <bool PROF, int G>
 __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int64_t* __restrict__ out_off,
                                                   const int64_t* __restrict__ in_off,
@@ -557,10 +559,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
    const uint64_t mvl = (lane < span && vlane < nv) ? vm[vlane] : 0;
    if (lane < span && vlane < nv && mvl == 0) { cnt[vlane] = 0; vadj[vlane] = 0; }
    uint64_t todo = __ballot(mvl != 0);
-   while (todo) {
-    const int64_t v = b0 + __builtin_ctzll(todo);
-    const uint64_t mv = readlane64(mvl, __builtin_ctzll(todo));
-    todo &= todo - 1;
+   // one member: have0 = its first 64 slots were loaded by the group prefetch below (m0 / nb0)
+   auto one = [&](const int64_t v, const uint64_t mv, const bool have0, const uint64_t m0, const int32_t nb0) {
     const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
     if (hv_of && hv_of[v] >= 0) {
       // heavy vertex: its segments were compacted by k_heavy_slots, which also left the
@@ -600,12 +600,12 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         if (ch) act2[v] = 1;
         if (ch && cb1) atomicOr((unsigned long long*)&cb1[v >> 6], 1ull << (v & 63));
       }
-      if (!own) continue;
+      if (!own) return;
       changed += ch != 0;
       lanes |= ch;
       members += 1;
       alive += kept;
-      continue;
+      return;
     }
     // label = global rank (== local rank with one partition).  A ghost (v >= n_own) only
     // gets its slots (to its owned neighbours) and label_0 rows here: its label_1 row comes
@@ -624,11 +624,14 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     int32_t nb_keep = 0;
     for (int64_t c = 0; c < ntot; c += 64) {
       const int64_t j = c + lane;
-      if (ts_t && ts_t[base + c] < tcut) break;  // newest first: the rest are dead in every view
+      const bool pre = c == 0 && have0;
+      if (!pre && ts_t && ts_t[base + c] < tcut) break;  // newest first: the rest are dead in every view
       scanned += ntot - c < 64 ? ntot - c : 64;
-      uint64_t m = 0;
-      int32_t nb = 0, lb = 0;
-      if (j < ntot) {
+      uint64_t m = pre ? m0 : 0;
+      int32_t nb = pre ? nb0 : 0, lb = 0;
+      if (pre) {
+        lb = grank ? grank[nb] : nb;
+      } else if (j < ntot) {
         int64_t e;
         if (ts_e) {
           e = ts_e[base + j];
@@ -679,7 +682,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       chg1[v] = ch;
       if (ch && cb1) atomicOr((unsigned long long*)&cb1[v >> 6], 1ull << (v & 63));
     }
-    if (!own) continue;
+    if (!own) return;
     lanes |= ch;
     if (ch) {
       changed++;
@@ -695,6 +698,54 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     }
     members += 1;
     alive += (unsigned long long)count;
+   };
+   while (todo) {
+    // G members at a time: with time-ordered slots, the first 64 slots of each (edge, neighbour,
+    // last add, then em[e] / vm[nb]) are loaded for all of them before any is processed
+    int64_t gv[G];
+    uint64_t gm[G];
+#pragma unroll
+    for (int k = 0; k < G; k++) {
+      gv[k] = -1;
+      gm[k] = 0;
+      if (todo) {
+        const int L = __builtin_ctzll(todo);
+        gv[k] = b0 + L;
+        gm[k] = readlane64(mvl, L);
+        todo &= todo - 1;
+      }
+    }
+    bool ok[G], live[G];  // live: this lane holds one of the member's first slots, kept by time
+    int32_t pe[G], pnb[G];
+    uint64_t pm[G];
+#pragma unroll
+    for (int k = 0; k < G; k++) {
+      ok[k] = false;
+      live[k] = false;
+      pe[k] = 0;
+      pnb[k] = 0;
+      pm[k] = 0;
+      const int64_t v = gv[k];
+      if (G > 1 && v >= 0 && ts_e && !(hv_of && hv_of[v] >= 0)) {
+        const int64_t base = out_off[v] + in_off[v];
+        const int64_t ntot = out_off[v + 1] + in_off[v + 1] - base;
+        if (ntot > 0 && ts_t[base] >= tcut) {
+          ok[k] = true;
+          if (lane < ntot) {
+            pe[k] = ts_e[base + lane];
+            pnb[k] = ts_nb[base + lane];
+            live[k] = ts_t[base + lane] >= tcut;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < G; k++)
+      if (live[k] && pnb[k] != (int32_t)gv[k])
+        pm[k] = em[pe[k]] & (ends ? gm[k] : vm[pnb[k]]) & gm[k];
+#pragma unroll
+    for (int k = 0; k < G; k++)
+      if (gv[k] >= 0) one(gv[k], gm[k], ok[k], pm[k], pnb[k]);
    }
   }
   if (lane == 0) {
@@ -2125,6 +2176,7 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
+int g_slots_group = 1;  // K2 members per prefetch group (RGPU_SLOTS_GROUP)
 int g_rowbuf = 0;
 int g_sum_blocks = 32;  // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 int g_hist_rounds = 4;  // (C2: 64 rounds 145 ms, 4 rounds 138 ms; 1 round 147 ms)
@@ -2163,7 +2215,9 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends,
                      int32_t* ccount) {
   const bool hv = g.n_seg > 0;
-  auto* kern = work ? k_cc_slots<true> : k_cc_slots<false>;
+  auto* kern = work ? k_cc_slots<true, 1>
+                    : g_slots_group >= 4 ? k_cc_slots<false, 4>
+                    : g_slots_group == 2 ? k_cc_slots<false, 2> : k_cc_slots<false, 1>;
   kern<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
