@@ -463,9 +463,7 @@ __device__ __forceinline__ unsigned row_lines(uint64_t m) {
 // (ccount[(r-1)*64 + shard]: changed vertices per step, 64 shards, summed here by each wave;
 // every block of a launch computes the same answer from counts the previous launch finished).
 // div <= 0: never.  Step 1 (K2) always writes its flags.
-constexpr int kUwFirst = 1 << 20;  // dense_div flag: visit-all steps read uniform words first
 __device__ __forceinline__ bool dense_rule(const int32_t* __restrict__ ccount, int r, int64_t nv, int div) {
-  div &= kUwFirst - 1;
   if (div <= 0 || !ccount || r < 2) return false;
   int64_t x = ccount[(r - 1) * kCountShards + (threadIdx.x & 63)];
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
@@ -507,9 +505,7 @@ struct NoWork {
 // bitmap and stepcnt[1]; vadj[v] = OR of v's kept slot masks (v isolated in view j iff bit j
 // is clear).
 
-// PROF = false: the work counters compile away (launch_cc_slots: work == null).  G: members whose
-// first slot chunk is loaded together (RGPU_SLOTS_GROUP)
-template <bool PROF, int G>
+template <bool PROF>  // PROF = false: the work counters compile away (launch_cc_slots: work == null)
 __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int64_t* __restrict__ out_off,
                                                   const int64_t* __restrict__ in_off,
@@ -559,8 +555,10 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
    const uint64_t mvl = (lane < span && vlane < nv) ? vm[vlane] : 0;
    if (lane < span && vlane < nv && mvl == 0) { cnt[vlane] = 0; vadj[vlane] = 0; }
    uint64_t todo = __ballot(mvl != 0);
-   // one member: have0 = its first 64 slots were loaded by the group prefetch below (m0 / nb0)
-   auto one = [&](const int64_t v, const uint64_t mv, const bool have0, const uint64_t m0, const int32_t nb0) {
+   while (todo) {
+    const int64_t v = b0 + __builtin_ctzll(todo);
+    const uint64_t mv = readlane64(mvl, __builtin_ctzll(todo));
+    todo &= todo - 1;
     const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
     if (hv_of && hv_of[v] >= 0) {
       // heavy vertex: its segments were compacted by k_heavy_slots, which also left the
@@ -600,12 +598,12 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         if (ch) act2[v] = 1;
         if (ch && cb1) atomicOr((unsigned long long*)&cb1[v >> 6], 1ull << (v & 63));
       }
-      if (!own) return;
+      if (!own) continue;
       changed += ch != 0;
       lanes |= ch;
       members += 1;
       alive += kept;
-      return;
+      continue;
     }
     // label = global rank (== local rank with one partition).  A ghost (v >= n_own) only
     // gets its slots (to its owned neighbours) and label_0 rows here: its label_1 row comes
@@ -624,14 +622,11 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     int32_t nb_keep = 0;
     for (int64_t c = 0; c < ntot; c += 64) {
       const int64_t j = c + lane;
-      const bool pre = c == 0 && have0;
-      if (!pre && ts_t && ts_t[base + c] < tcut) break;  // newest first: the rest are dead in every view
+      if (ts_t && ts_t[base + c] < tcut) break;  // newest first: the rest are dead in every view
       scanned += ntot - c < 64 ? ntot - c : 64;
-      uint64_t m = pre ? m0 : 0;
-      int32_t nb = pre ? nb0 : 0, lb = 0;
-      if (pre) {
-        lb = grank ? grank[nb] : nb;
-      } else if (j < ntot) {
+      uint64_t m = 0;
+      int32_t nb = 0, lb = 0;
+      if (j < ntot) {
         int64_t e;
         if (ts_e) {
           e = ts_e[base + j];
@@ -682,7 +677,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       chg1[v] = ch;
       if (ch && cb1) atomicOr((unsigned long long*)&cb1[v >> 6], 1ull << (v & 63));
     }
-    if (!own) return;
+    if (!own) continue;
     lanes |= ch;
     if (ch) {
       changed++;
@@ -698,54 +693,6 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     }
     members += 1;
     alive += (unsigned long long)count;
-   };
-   while (todo) {
-    // G members at a time: with time-ordered slots, the first 64 slots of each (edge, neighbour,
-    // last add, then em[e] / vm[nb]) are loaded for all of them before any is processed
-    int64_t gv[G];
-    uint64_t gm[G];
-#pragma unroll
-    for (int k = 0; k < G; k++) {
-      gv[k] = -1;
-      gm[k] = 0;
-      if (todo) {
-        const int L = __builtin_ctzll(todo);
-        gv[k] = b0 + L;
-        gm[k] = readlane64(mvl, L);
-        todo &= todo - 1;
-      }
-    }
-    bool ok[G], live[G];  // live: this lane holds one of the member's first slots, kept by time
-    int32_t pe[G], pnb[G];
-    uint64_t pm[G];
-#pragma unroll
-    for (int k = 0; k < G; k++) {
-      ok[k] = false;
-      live[k] = false;
-      pe[k] = 0;
-      pnb[k] = 0;
-      pm[k] = 0;
-      const int64_t v = gv[k];
-      if (G > 1 && v >= 0 && ts_e && !(hv_of && hv_of[v] >= 0)) {
-        const int64_t base = out_off[v] + in_off[v];
-        const int64_t ntot = out_off[v + 1] + in_off[v + 1] - base;
-        if (ntot > 0 && ts_t[base] >= tcut) {
-          ok[k] = true;
-          if (lane < ntot) {
-            pe[k] = ts_e[base + lane];
-            pnb[k] = ts_nb[base + lane];
-            live[k] = ts_t[base + lane] >= tcut;
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < G; k++)
-      if (live[k] && pnb[k] != (int32_t)gv[k])
-        pm[k] = em[pe[k]] & (ends ? gm[k] : vm[pnb[k]]) & gm[k];
-#pragma unroll
-    for (int k = 0; k < G; k++)
-      if (gv[k] >= 0) one(gv[k], gm[k], ok[k], pm[k], pnb[k]);
    }
   }
   if (lane == 0) {
@@ -919,8 +866,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          int32_t* __restrict__ hbest = nullptr,
                                          const int32_t* __restrict__ uw_cur = nullptr,
                                          int32_t* __restrict__ uw_next = nullptr,
-                                         uint64_t* __restrict__ cb_next = nullptr, bool skip_marks = false,
-                                         bool uw_first = false) {
+                                         uint64_t* __restrict__ cb_next = nullptr, bool skip_marks = false) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
@@ -960,30 +906,15 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     // then the uniform words of the neighbours that changed
     uint64_t act[CH];
     int32_t un[CH];
-    if (uw_first) {
-      // a step that visits every member (dense predecessor): most neighbours changed, so read
-      // the neighbour's uniform word first and fold it on every kept view of the slot (exact:
-      // an unchanged view's label cannot lower ours); only a mixed neighbour
-      // needs its change word and row lanes — one dependent trip less per uniform neighbour
 #pragma unroll
-      for (int i = 0; i < CH; i++) un[i] = sm[i] ? uw_cur[nb[i]] : kMixed;
+    for (int i = 0; i < CH; i++) {
+      act[i] = sm[i] & chg_prev[nb[i]];
+    }
 #pragma unroll
-      for (int i = 0; i < CH; i++) {
-        act[i] = un[i] != kMixed ? sm[i] : (sm[i] ? sm[i] & chg_prev[nb[i]] : 0);
-        wk.a += __popcll(__ballot(sm[i] != 0)) + 2 * __popcll(__ballot(sm[i] != 0 && un[i] == kMixed));
-        wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < CH; i++) {
-        act[i] = sm[i] & chg_prev[nb[i]];
-      }
-#pragma unroll
-      for (int i = 0; i < CH; i++) {
-        un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
-        if (uw_cur) wk.a += __popcll(__ballot(act[i] != 0));
-        wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
-      }
+    for (int i = 0; i < CH; i++) {
+      un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
+      if (uw_cur) wk.a += __popcll(__ballot(act[i] != 0));
+      wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
     }
     // own rows are only meaningful on member lanes
 #pragma unroll
@@ -1179,8 +1110,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
       cc_chunk<CH, BUF, false>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
                                lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
-                               hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks,
-                               visit_all && uw_cur && (dense_div & kUwFirst));
+                               hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks);
     }
   }
   if constexpr (PROF)
@@ -2176,7 +2106,6 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
-int g_slots_group = 1;  // K2 members per prefetch group (RGPU_SLOTS_GROUP)
 int g_rowbuf = 0;
 int g_sum_blocks = 32;  // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 int g_hist_rounds = 4;  // (C2: 64 rounds 145 ms, 4 rounds 138 ms; 1 round 147 ms)
@@ -2215,9 +2144,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends,
                      int32_t* ccount) {
   const bool hv = g.n_seg > 0;
-  auto* kern = work ? k_cc_slots<true, 1>
-                    : g_slots_group >= 4 ? k_cc_slots<false, 4>
-                    : g_slots_group == 2 ? k_cc_slots<false, 2> : k_cc_slots<false, 1>;
+  auto* kern = work ? k_cc_slots<true> : k_cc_slots<false>;
   kern<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,

@@ -190,7 +190,6 @@ struct rgpu_ctx {
   bool ends_on = false;                 // RGPU_EMENDS=1: K1 folds endpoint memberships into CC edge words
                                         // (measured slower on C4: K1 55 -> 97 ms for K2 122 -> 117 ms)
   bool prof_lean = false;               // RGPU_PROF_LEAN (work_buf)
-  bool uw_first = false;                // RGPU_UWFIRST: visit-all steps read uniform words first
   int dense = -1;                       // RGPU_DENSE: dense-step divisor (kernels.hip dense_rule; -1 by size)
   int cb_on = 1;                        // RGPU_CHGBITS=0: no changed bits (kernels.hpp ChgBits)
   bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
@@ -344,8 +343,8 @@ unsigned long long* work_buf(const rgpu_ctx* c, const Slot& s) {
 // 536 ms); off below (C2: 127.5 -> 132.3 ms with it: a small graph's flags are cached anyway).
 int dense_div(const rgpu_ctx* c) {
   if (c->tail_on) return 0;
-  const int d = c->dense >= 0 ? c->dense : (c->g.nv > ((int64_t)1 << 21) ? 4 : 0);
-  return d > 0 && c->uw_first ? d | (1 << 20) : d;  // kernels.hip kUwFirst
+  if (c->dense >= 0) return c->dense;
+  return c->g.nv > ((int64_t)1 << 21) ? 4 : 0;
 }
 
 // changed bits of superstep r (with uniform words; RGPU_CHGBITS=0 turns them off)
@@ -2092,11 +2091,9 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   c->cb_on = env_int("RGPU_CHGBITS", 1);
   c->prof_lean = env_int("RGPU_PROF_LEAN", 0) != 0;
-  c->uw_first = env_int("RGPU_UWFIRST", 0) != 0;
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   c->ends_on = env_int("RGPU_EMENDS", 0) != 0;
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
-  g_slots_group = std::max(1, env_int("RGPU_SLOTS_GROUP", 1));
   g_tail_step = std::max(2, env_int("RGPU_TAIL_STEP", 14));
   g_tail_grid = std::max(1, env_int("RGPU_TAIL_GRID", 1024));
   try {

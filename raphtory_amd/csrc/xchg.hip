@@ -49,7 +49,6 @@ __device__ __forceinline__ int64_t owned_rank(const OwnIdx& I, int64_t id) {
 // kernels.hip dense_rule(ccount, r - 1): superstep r ran with every member visited (its flags
 // were not written by a dense step r - 1)
 __device__ __forceinline__ bool dense_after(const int32_t* __restrict__ ccount, int r, int64_t nv, int div) {
-  div &= (1 << 20) - 1;  // (kernels.hip kUwFirst flag)
   if (div <= 0 || !ccount || r < 3) return false;
   int64_t x = ccount[(r - 2) * kCountShards + (threadIdx.x & 63)];
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
