@@ -58,11 +58,12 @@ __global__ __launch_bounds__(256) void k_diff_setup(int64_t nv, const uint64_t* 
     const uint64_t m = v == seed ? vm[v] : 0;
     inf[v] = m;
     front0[v] = m;
-    if (m) {
+    if (m)
       for (uint64_t b = m; b; b &= b - 1) atomicAdd(&stats[__builtin_ctzll(b)], 1ull);  // infected counts
-      for (int64_t k = out_off[v]; k < out_off[v + 1]; k++) act1[edst[k]] = 1;
-    }
   }
+  // the seed's out-neighbours, spread over the whole grid (a hub seed has millions)
+  if (seed >= 0 && vm[seed])
+    for (int64_t k = out_off[seed] + i0; k < out_off[seed + 1]; k += stride) act1[edst[k]] = 1;
   if (!steprow) return;  // rows only when the run retains per-vertex results
   for (int64_t i = i0; i < nv * 8; i += stride) {
     uint64_t w = ~0ull;
