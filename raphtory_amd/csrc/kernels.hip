@@ -470,20 +470,6 @@ __device__ __forceinline__ bool dense_rule(const int32_t* __restrict__ ccount, i
   return x * div >= nv;
 }
 
-// Streamed loads / stores (NT): data touched once per launch (a visited vertex's slot list, K2's
-// time-ordered slots and its compacted output) marked non-temporal, so it does not evict the
-// randomly re-read neighbour words (change / uniform words, masks) from L2 and the Infinity Cache
-template <bool NT, class T>
-__device__ __forceinline__ T ld_s(const T* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-template <bool NT, class T>
-__device__ __forceinline__ void st_s(T* p, T x) {
-  if constexpr (NT) __builtin_nontemporal_store(x, p);
-  else *p = x;
-}
-
 // Items per wave round of a grid-stride loop whose lanes first load one word per item: 64
 // when the grid has at most one round of 64 per wave, else just enough to spread the items
 // over every wave.
@@ -519,7 +505,7 @@ struct NoWork {
 // bitmap and stepcnt[1]; vadj[v] = OR of v's kept slot masks (v isolated in view j iff bit j
 // is clear).
 
-template <bool PROF, bool NT>  // PROF = false: the work counters compile away (launch_cc_slots: work == null)
+template <bool PROF>  // PROF = false: the work counters compile away (launch_cc_slots: work == null)
 __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int64_t* __restrict__ out_off,
                                                   const int64_t* __restrict__ in_off,
@@ -643,8 +629,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       if (j < ntot) {
         int64_t e;
         if (ts_e) {
-          e = ld_s<NT>(&ts_e[base + j]);
-          nb = ld_s<NT>(&ts_nb[base + j]);
+          e = ts_e[base + j];
+          nb = ts_nb[base + j];
         } else if (j < nout) {
           e = o0 + j;
           nb = edst[e];
@@ -652,14 +638,14 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
           e = in_eid[i0 + (j - nout)];
           nb = esrc[e];
         }
-        if (nb != (int32_t)v && (!ts_t || ld_s<NT>(&ts_t[base + j]) >= tcut)) m = em[e] & (ends ? mv : vm[nb]) & mv;
+        if (nb != (int32_t)v && (!ts_t || ts_t[base + j] >= tcut)) m = em[e] & (ends ? mv : vm[nb]) & mv;
         lb = grank ? grank[nb] : nb;
       }
       uint64_t bal = __ballot(m != 0);
       if (m) {
         const int64_t pos = base + count + __popcll(bal & lanemask_lt());
-        st_s<NT>(&snbr[pos], nb);
-        st_s<NT>(&smask[pos], m);
+        snbr[pos] = nb;
+        smask[pos] = m;
       }
       count += __popcll(bal);
       m_keep = m;
@@ -866,7 +852,7 @@ __device__ __forceinline__ void mark(bool want, int32_t v, uint8_t* act_next, co
 // chunk.  All loads are unconditional from padded buffers (see gather_min).  A visited
 // vertex rewrites its row only if it changed now or in the previous step (the only cases
 // where the two label buffers differ).  uw_cur / uw_next: uniform label words (null: rows only).
-template <int CH, bool BUF, bool TAIL, class WK, bool NT = false>
+template <int CH, bool BUF, bool TAIL, class WK>
 __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_t* __restrict__ adj_off,
                                          const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
                                          const int32_t* __restrict__ snbr,
@@ -911,8 +897,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       const int32_t n = __builtin_amdgcn_readlane(n_l, i);
       const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
       const int64_t idx = base + (lane < n ? lane : 0);
-      const int32_t q = ld_s<NT>(&snbr[idx]);
-      const uint64_t m = ld_s<NT>(&smask[idx]);
+      const int32_t q = snbr[idx];
+      const uint64_t m = smask[idx];
       nb[i] = lane < n ? q : 0;
       sm[i] = lane < n ? m : 0;
     }
@@ -961,8 +947,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
         for (int32_t c2 = 64; c2 < n; c2 += 64) {
           const int32_t j = c2 + lane;
           const int64_t idx = base + (j < n ? j : c2);
-          const int32_t q = ld_s<NT>(&snbr[idx]);
-          const uint64_t a2 = j < n ? (ld_s<NT>(&smask[idx]) & chg_prev[q]) : 0;
+          const int32_t q = snbr[idx];
+          const uint64_t a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
           const int32_t u2 = (uw_cur && a2) ? uw_cur[q] : kMixed;
           if (uw_cur) wk.a += __popcll(__ballot(a2 != 0));
           wk.g += u2 == kMixed ? __popcll(a2) : 0;
@@ -1050,7 +1036,7 @@ __global__ __launch_bounds__(256) void k_uw_rows(int64_t nv, const uint64_t* __r
 // idempotent stores by step r-1), CH consecutive ranks per wave-chunk, and clears act_clear
 // (read two steps ago, written next step).
 // MINW > 1: amdgpu_waves_per_eu(MINW) (a VGPR cap; RGPU_STEP_VARIANT | 64 selects 6 waves/SIMD)
-template <int CH, bool BUF, int MINW, bool PROF, bool NT = false>
+template <int CH, bool BUF, int MINW, bool PROF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void k_cc_step2(int step, int64_t nv, const int64_t* __restrict__ adj_off,
                                                   const uint64_t* __restrict__ vm,
                                                   const int32_t* __restrict__ cnt,
@@ -1122,7 +1108,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
       const int L = __builtin_ctzll(todo);
       todo &= todo - 1;
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
-      cc_chunk<CH, BUF, false, decltype(wk), NT>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
+      cc_chunk<CH, BUF, false>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
                                lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
                                hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks);
     }
@@ -2120,7 +2106,6 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
-int g_nt = 0;         // streamed slot loads / stores non-temporal (RGPU_NT; ld_s / st_s)
 int g_rowbuf = 0;
 int g_sum_blocks = 32;  // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 int g_hist_rounds = 4;  // (C2: 64 rounds 145 ms, 4 rounds 138 ms; 1 round 147 ms)
@@ -2159,7 +2144,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends,
                      int32_t* ccount) {
   const bool hv = g.n_seg > 0;
-  auto* kern = work ? k_cc_slots<true, false> : g_nt ? k_cc_slots<false, true> : k_cc_slots<false, false>;
+  auto* kern = work ? k_cc_slots<true> : k_cc_slots<false>;
   kern<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
@@ -2208,7 +2193,6 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   else if ((variant & 64) && work) k_cc_step2<4, false, 6, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (variant & 64) k_cc_step2<4, false, 6, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else if (work) k_cc_step2<4, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else if (g_nt) k_cc_step2<4, false, 1, false, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else k_cc_step2<4, false, 1, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
 #undef RGPU_STEP_ARGS
 }

@@ -130,7 +130,6 @@ void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, co
                        int dense_div = 0);
 extern int g_sum_blocks;   // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 extern int g_hist_rounds;  // label-dedup rounds per (view, chunk) in k_cc_hist (RGPU_HIST_ROUNDS)
-extern int g_nt;  // K2 / superstep slot streams non-temporal (RGPU_NT)
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
 extern int g_rowbuf;     // label rows via buffer descriptors (RGPU_ROWBUF)
 extern int g_tail_step, g_tail_grid;  // supersteps >= tail_step use at most tail_grid blocks

@@ -2094,7 +2094,6 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   c->ends_on = env_int("RGPU_EMENDS", 0) != 0;
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
-  g_nt = env_int("RGPU_NT", 0) != 0 ? 1 : 0;
   g_tail_step = std::max(2, env_int("RGPU_TAIL_STEP", 14));
   g_tail_grid = std::max(1, env_int("RGPU_TAIL_GRID", 1024));
   try {
