@@ -190,6 +190,7 @@ struct rgpu_ctx {
   bool ends_on = false;                 // RGPU_EMENDS=1: K1 folds endpoint memberships into CC edge words
                                         // (measured slower on C4: K1 55 -> 97 ms for K2 122 -> 117 ms)
   bool prof_lean = false;               // RGPU_PROF_LEAN (work_buf)
+  int inject_fail = 0;                  // RGPU_INJECT_FAIL=n (tests): the n-th batch start of a run throws
   int dense = -1;                       // RGPU_DENSE: dense-step divisor (kernels.hip dense_rule; -1 by size)
   int cb_on = 1;                        // RGPU_CHGBITS=0: no changed bits (kernels.hpp ChgBits)
   bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
@@ -708,6 +709,8 @@ bool can_start(const rgpu_ctx* c, size_t b, const RunCfg& rc) {
 void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   Slot& s = c->slot[si];
   const DevGraph& g = c->g;
+  if (c->inject_fail > 0 && --c->inject_fail == 0)  // fault injection (tests): after earlier batches ran
+    throw HipFail{"RGPU_INJECT_FAIL: injected failure at batch " + std::to_string(b)};
   const size_t hb = (size_t)b / rc.G;
   const int grp = b % rc.G;
   BatchParams bp;
@@ -1520,6 +1523,38 @@ void finish_supersteps(rgpu_ctx* c, const RunCfg& rc) {
   }
 }
 
+// After a failed run (a HIP / RCCL / exchange error or a failed allocation mid-run): the slots may
+// hold a batch in any phase, and the per-batch state that only a batch's last kernels bring back
+// to zero (count rows, island shards, lane-change shards, hub minima, record counts) may be
+// dirty.  Drain the streams and drop every slot and exchange-slot buffer, so that the next run
+// allocates them fresh and clean; the run's results are invalid.
+void drop_alloc(std::vector<void*>& L, void* p) {
+  if (!p) return;
+  auto it = std::find(L.begin(), L.end(), p);
+  if (it == L.end()) return;
+  (void)hipFree(p);
+  L.erase(it);
+}
+void reset_after_failure(rgpu_ctx* c) {
+  for (Slot& s : c->slot)
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+  (void)hipDeviceSynchronize();
+  (void)hipGetLastError();
+  auto& LG = c->graph_allocs;
+  for (Slot& s : c->slot)
+    for (void* p : {(void*)s.hv.segcnt, (void*)s.hv.segor, (void*)s.hv.best, (void*)s.hv.pacc}) drop_alloc(LG, p);
+  for (XSlot& xs : c->pt.xs)
+    for (void* p : {(void*)xs.scnt, (void*)xs.htot, (void*)xs.xab, (void*)xs.vms, (void*)xs.vmr}) drop_alloc(LG, p);
+  release_slots(c);
+  free_part_slots(c, true);
+  c->algo = -1;
+  c->cc.clear();
+  c->vlast.clear();
+  c->kept.clear();
+  c->retained = false;
+  if (c->d_ecnt) { (void)hipFree(c->d_ecnt); c->d_ecnt = nullptr; }
+}
+
 int fail(rgpu_ctx* c, int code, const std::string& m) {
   if (c) c->err = m;
   return code;
@@ -2091,6 +2126,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   c->cb_on = env_int("RGPU_CHGBITS", 1);
   c->prof_lean = env_int("RGPU_PROF_LEAN", 0) != 0;
+  c->inject_fail = env_int("RGPU_INJECT_FAIL", 0);
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   c->ends_on = env_int("RGPU_EMENDS", 0) != 0;
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
@@ -2201,12 +2237,15 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->steprec.clear();
   } catch (const HipFail& f) {
     exchange_quiesce();
+    reset_after_failure(c);
     return fail(c, RGPU_EHIP, f.msg);
   } catch (const std::bad_alloc&) {
     exchange_quiesce();
+    reset_after_failure(c);
     return fail(c, RGPU_ENOMEM, "host allocation failed");
   } catch (const std::exception& x) {  // exchange (RCCL / loopback) failures
     exchange_quiesce();
+    reset_after_failure(c);
     return fail(c, RGPU_EHIP, x.what());
   }
   exchange_quiesce();

@@ -17,22 +17,26 @@ def pytest_runtest_logstart(nodeid, location):
     _current["test"], _current["t0"] = nodeid, time.time()
 
 
-def _heartbeat(config, period=45.0):
-    """A line on the terminal every `period` s while a test runs: the full-size config tests run
-    for minutes between two pytest outputs, and the GPU box takes a silent command for hung."""
+def _heartbeat(period=45.0):
+    """A line on stderr every `period` s while a test runs: the full-size config tests run for
+    minutes between two pytest outputs, and the GPU box takes a silent command for hung.  The
+    thread writes to a duplicate of fd 2 taken before any capture starts, so it never touches
+    pytest's (single-threaded) capture manager."""
     import threading
     import time
+
+    try:
+        fd = os.dup(2)
+    except OSError:
+        return
 
     def beat():
         while True:
             time.sleep(period)
-            tr = config.pluginmanager.get_plugin("terminalreporter")  # registered after this hook
-            capman = config.pluginmanager.get_plugin("capturemanager")
-            if _current["test"] and tr is not None and capman is not None:
+            if _current["test"]:
                 try:
-                    with capman.global_and_fixture_disabled():  # past the test's output capture
-                        tr.write_line(f"[heartbeat] {_current['test']} running {time.time() - _current['t0']:.0f} s")
-                except Exception:  # noqa: BLE001 - a heartbeat must never fail a test
+                    os.write(fd, f"[heartbeat] {_current['test']} running {time.time() - _current['t0']:.0f} s\n".encode())
+                except OSError:  # a heartbeat must never fail a test
                     pass
 
     threading.Thread(target=beat, daemon=True).start()
@@ -42,7 +46,7 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
     config.addinivalue_line("markers", "fullsize: a BASELINE config at full size (minutes; deselect with "
                                        "-m 'gpu and not fullsize' for quick iterations)")
-    _heartbeat(config, float(os.environ.get("RGPU_HEARTBEAT_S", "45")))
+    _heartbeat(float(os.environ.get("RGPU_HEARTBEAT_S", "45")))
 
 
 def _ensure_built():

@@ -12,20 +12,17 @@ from raphtory_amd.synth import YEAR, gen_gab, gen_powerlaw, gen_uniform
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "raphtory_amd", "csrc")
-OUT = os.path.join(ROOT, "tests", "_build")
 FLAGS = {"asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"],
          "tsan": ["-fsanitize=thread"]}
 
 
-def _build(kind):
-    os.makedirs(OUT, exist_ok=True)
-    exe = os.path.join(OUT, f"packer_{kind}")
+def _build(kind, out):
+    """Built fresh from the current sources into the test's temp dir on every run (never a cached
+    binary whose sources or sanitizer runtime may differ)."""
+    exe = os.path.join(str(out), f"packer_{kind}")
     srcs = [os.path.join(ROOT, "tests", "packer_sanitize.cpp"), os.path.join(CSRC, "packer.cpp")]
-    if not os.path.exists(exe) or any(os.path.getmtime(s) > os.path.getmtime(exe)
-                                      for s in srcs + [os.path.join(CSRC, "rgpu_internal.hpp")]):
-        subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-pthread", *FLAGS[kind], "-I", CSRC, "-o", exe + ".tmp", *srcs],
-                       check=True)
-        os.replace(exe + ".tmp", exe)
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-pthread", *FLAGS[kind], "-I", CSRC, "-o", exe, *srcs],
+                   check=True)
     return exe
 
 
@@ -49,7 +46,7 @@ def _streams():
 
 @pytest.mark.parametrize("kind", ["asan", "tsan"])
 def test_packer_under_sanitizer(kind, tmp_path):
-    exe = _build(kind)
+    exe = _build(kind, tmp_path)
     env = dict(os.environ, RGPU_THREADS="8", ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", TSAN_OPTIONS="halt_on_error=1")
     for name, t, k, s, d in _streams():
