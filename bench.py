@@ -70,6 +70,8 @@ def parse():
     p.add_argument("--c4-users", type=int, default=20_000_000)
     p.add_argument("--c4-interactions", type=int, default=333_333_334, help="x3 updates (1B at the default)")
     p.add_argument("--c4-hops", type=int, default=168)
+    p.add_argument("--vertex-order", default="locality", choices=["locality", "id"],
+                   help="local vertex order of the sealed graph (rgpu_set_vertex_order; A/B runs)")
     return p.parse_args()
 
 
@@ -341,6 +343,8 @@ def run_c4(a, rank, world, local):
         g.exchange_init(TemporalGraph.exchange_id())
     else:
         g = TemporalGraph(device=local)
+    if a.vertex_order != "locality":
+        g.set_vertex_order(a.vertex_order)
     users, inter = a.c4_users, a.c4_interactions
     t0 = time.perf_counter()
     chunk = 20_000_000
@@ -493,7 +497,7 @@ def run_c5(a, rank, world, local):
     from raphtory_amd import TemporalGraph
     from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab
     s = gen_gab(4, a.c5_users, a.c5_base)
-    g = TemporalGraph(device=local)
+    g = TemporalGraph(device=local, vertex_order="id")  # live: later seals merge incrementally
     g.ingest_stream(s)
     t0 = time.perf_counter()
     g.seal()

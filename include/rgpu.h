@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RGPU_ABI_VERSION 6
+#define RGPU_ABI_VERSION 7
 
 /* error codes */
 #define RGPU_OK 0
@@ -140,9 +140,20 @@ int rgpu_ingest_rgev(rgpu_ctx* ctx, const uint8_t* buf, size_t bytes, size_t* co
 /* Sort + merge + pack the ingested stream into SoA histories and copy them to HBM.
  * Live ingest (IngestionWorker.scala:31-256 keeps appending while LiveAnalysisTask.scala:13-107
  * re-runs): after the first seal, rgpu_ingest + rgpu_seal again merges only the new updates
- * into the HBM-resident graph (merge.hip; one partition, RGPU_DELTA=0 forces a full re-pack).
+ * into the HBM-resident graph (merge.hip; one partition in RGPU_ORDER_ID order, RGPU_DELTA=0
+ * forces a full re-pack).
  * The new updates count as later in stream order than every sealed one. */
 int rgpu_seal(rgpu_ctx* ctx);
+
+/* Local vertex order of the next full seal (ABI 7).  Results and labels do not depend on it.
+ *   RGPU_ORDER_LOCALITY (default): vertices ranked by activity, hubs clustered in cache-line
+ *     groups spread over the rank range: the superstep gathers hit L2 more often.
+ *     A later rgpu_seal on such a context re-packs the whole stream.
+ *   RGPU_ORDER_ID: ids ascending.  Needed by live ingest: a later rgpu_seal then merges only the
+ *     new updates into the resident graph (IngestionWorker / LiveAnalysisTask contexts). */
+#define RGPU_ORDER_LOCALITY 0
+#define RGPU_ORDER_ID 1
+int rgpu_set_vertex_order(rgpu_ctx* ctx, int order);
 
 /* Newest ingested time: the watermark ReaderWorker.processTimeCheckRequest compares
  * against (ReaderWorker.scala:259-274). */

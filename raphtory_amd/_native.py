@@ -19,6 +19,7 @@ RGPU_VADD, RGPU_VDEL, RGPU_EADD, RGPU_EDEL = 0, 1, 2, 3
 RGPU_ALGO_CC, RGPU_ALGO_DEGREE, RGPU_ALGO_PR, RGPU_ALGO_DIFFUSION = 0, 1, 2, 3
 RGPU_RUN_RETAIN, RGPU_RUN_PROFILE, RGPU_RUN_SERIAL, RGPU_RUN_EDGE_COUNTS = 1, 2, 4, 8
 RGPU_XCHG_ID_BYTES, RGPU_XCHG_RCCL, RGPU_XCHG_LOOPBACK = 128, 0, 1
+RGPU_ORDER_LOCALITY, RGPU_ORDER_ID = 0, 1
 ERROR_NAMES = {
     RGPU_EINVAL: "RGPU_EINVAL",
     RGPU_ESTATE: "RGPU_ESTATE",
@@ -36,7 +37,7 @@ EXPORTS = [
     "rgpu_cc_vertex_labels", "rgpu_degree_result", "rgpu_degree_vertex", "rgpu_pr_result",
     "rgpu_stats", "rgpu_last_error", "rgpu_close",
     "rgpu_rgev_encode", "rgpu_rgev_decode", "rgpu_rgev_last_error", "rgpu_ingest_rgev",
-    "rgpu_set_diffusion", "rgpu_diffusion_result", "rgpu_diffusion_vertex",
+    "rgpu_set_diffusion", "rgpu_diffusion_result", "rgpu_diffusion_vertex", "rgpu_set_vertex_order",
 ]
 
 
@@ -76,6 +77,7 @@ _SIGS = {
     "rgpu_ingest": (C.c_int, [_CTX, _P64, _PU8, _P64, _P64, _SZ]),
     "rgpu_seal": (C.c_int, [_CTX]),
     "rgpu_newest_time": (C.c_int, [_CTX, _P64]),
+    "rgpu_set_vertex_order": (C.c_int, [_CTX, C.c_int]),
     "rgpu_exchange_id": (C.c_int, [C.c_int, C.c_char_p]),
     "rgpu_exchange_init": (C.c_int, [_CTX, C.c_char_p]),
     "rgpu_run_view_batch": (C.c_int, [_CTX, C.c_int, _P64, _SZ, _P64, _SZ, C.c_int, C.c_int, C.c_int]),
@@ -118,7 +120,9 @@ def rgpu() -> C.CDLL:
         except OSError as e:  # pragma: no cover - depends on the box
             raise NativeUnavailable(f"cannot load {path}: {e}") from e
         for name, (res, args) in _SIGS.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:  # an older library (same-box A/B runs): the entry point stays unbound
+                continue
             fn.restype = res
             fn.argtypes = args
         _lib = lib

@@ -194,6 +194,43 @@ class DegreeBasic(Analyser):
             self.processWindowResults(window, timestamp, windowSet[i], viewCompleteTime)
 
 
+class DegreeRanking(Analyser):
+    """S/core/analysis/Algorithms/DegreeRanking.scala:8-124.  Per shard (totalV, totalOut, totalIn,
+    top 20 by in-degree); the lines merge the shards' top lists and keep the best 20 by in-degree
+    ("bestusers").  The top list is computed on the GPU for every view (k_deg_top_merge); ties go
+    by ascending id (the reference's order under ties is ParTrieMap's, unordered)."""
+    algo = "degree"
+
+    def defineMaxSteps(self) -> int:  # :30
+        return 1
+
+    def returnResults(self, graph, hop, win):  # :14-26
+        return graph.degree_result(hop, win)
+
+    @staticmethod
+    def _body(results) -> str:
+        tv = sum(r[0] for r in results)
+        te = sum(r[2] for r in results)
+        deg = (te / tv) if tv else float("nan")  # Int.toDouble / Int.toDouble: 0.0/0.0 = NaN
+        top = sorted((u for r in results for u in r[3]), key=lambda u: (-u[2], u[0]))[:20]  # sortBy(_._3) desc
+        best = "[" + ",".join(f'{{"id":{i},"indegree":{d_in},"outdegree":{d_out}}}' for i, d_out, d_in in top) + "]"
+        return f'"vertices":{tv},"edges":{te},"degree":{java_float_str(deg, double=True)},"bestusers":{best}'
+
+    def processResults(self, results, timestamp, viewCompleteTime):  # :32-55
+        self.lines.append(f'{{"time":{timestamp},{self._body(results)},"viewTime":{viewCompleteTime},"concatTime":0}},')
+
+    def processViewResults(self, results, timestamp, viewCompleteTime):  # :57-80
+        self.processResults(results, timestamp, viewCompleteTime)
+
+    def processWindowResults(self, results, timestamp, windowSize, viewCompleteTime):  # :82-111
+        self.lines.append(f'{{"time":{timestamp},"windowsize":{windowSize},{self._body(results)},'
+                          f'"viewTime":{viewCompleteTime},"concatTime":0}},')
+
+    def processBatchWindowResults(self, results, timestamp, windowSet, viewCompleteTime):  # :113-123
+        for i, window in enumerate(results):
+            self.processWindowResults(window, timestamp, windowSet[i], viewCompleteTime)
+
+
 class PageRank(Analyser):
     """PageRank as specified in SURVEY.md App. A.5 (constants of
     examples/random/depricated/PageRank.scala:11-45; 20 iterations per BASELINE config C3)."""
@@ -374,3 +411,95 @@ class BWindowedRangeAnalysisTask(RangeAnalysisTask):
 
     def windowSet(self):  # noqa: N802
         return self.windows
+
+
+# ---------------------------------------------------------------- live tasks
+class LiveAnalysisTask(AnalysisTask):
+    """S/core/analysis/Tasks/LiveTasks/LiveAnalysisTask.scala:13-107.  One ``tick()`` is one job of
+    the repeating live task: its time check (TimeCheck to every partition, ReaderWorker.
+    processTimeCheckRequest :259-274: ok iff timestamp <= the partition's newest time) and, when
+    every partition is ok, the view at ``timestamp()`` — ``liveTime`` = the minimum newest time
+    over the partitions (setLiveTime :20-27).  The first job runs at that minimum; then
+    (``restart`` :33-48, ``restartTime`` :29-31):
+      * event time: the next timestamp is liveTime + repeatTime, where liveTime is the minimum
+        taken at the previous successful check — the job waits until every partition has
+        ingested that far;
+      * processing time: after repeatTime ms the job runs at the then-current minimum.
+    A failed check returns None (the reference re-checks after 1 s, :96-100).  The job runs an
+    un-windowed view and prints processResults lines (AnalysisTask.processResults :82)."""
+
+    def __init__(self, graphs, analyser, repeat_time: int, event_time: bool, **kw):
+        super().__init__(graphs, analyser, **kw)
+        self.repeat_time = int(repeat_time)
+        self.event_time = bool(event_time)
+        self.current_timestamp = 1  # :15
+        self.live_time = 0
+        self.first_time = True
+        self._pending = False       # a restart happened: the next tick checks the new timestamp
+
+    def timestamp(self) -> int:
+        return self.current_timestamp
+
+    def hops(self):
+        return np.asarray([self.current_timestamp], np.int64)
+
+    def _set_live_time(self, newest: List[int]) -> None:  # :20-27
+        self.live_time = min(newest)
+        if not self.event_time or self.first_time:
+            self.first_time = False
+            self.current_timestamp = self.live_time
+
+    def restart(self) -> None:  # :33-48
+        if self.repeat_time > 0:
+            self.current_timestamp = (self.live_time + self.repeat_time) if self.event_time else self.live_time
+            self._pending = True
+
+    def tick(self) -> Optional[List[str]]:
+        """One live job: None if some partition has not ingested timestamp() yet, else the lines
+        the job printed (then the task restarts for the next job, if repeatTime > 0)."""
+        if not self.first_time and not self._pending:
+            return []  # repeatTime <= 0: the task ran once and stopped
+        newest = [g.newest_time() for g in self.graphs]
+        if any(self.current_timestamp > n for n in newest):  # TimeResponse(ok = false)
+            return None
+        self._set_live_time(newest)
+        self._pending = False
+        a = self.analyser
+        n0 = len(a.lines)
+        ts = self.current_timestamp
+        max_steps = a.defineMaxSteps()
+        t0 = time.perf_counter()
+        for g in self.graphs:
+            if hasattr(a, "prepare"):
+                a.prepare(g)
+            g.run(a.algo, [ts], [], max_steps=max_steps if a.algo in ("cc", "diffusion") else 100,
+                  pr_iters=max_steps if a.algo == "pagerank" else 0, retain=self.retain)
+        vt = int(round((time.perf_counter() - t0) * 1e3))
+        a.processResults([a.returnResults(g, 0, 0) for g in self.graphs], ts, vt)
+        self.restart()
+        return a.lines[n0:]
+
+    def run(self) -> List[str]:
+        out = self.tick()
+        if out is None:
+            raise TimeNotIngested(f"{self.current_timestamp} is yet to be ingested")
+        return out
+
+
+class WindowedLiveAnalysisTask(LiveAnalysisTask):
+    """LiveTasks/WindowedLiveAnalysisTask.scala:7-10: takes a window but never overrides
+    windowSize(), so the job runs un-windowed (reproduced)."""
+
+    def __init__(self, graphs, analyser, repeat_time, event_time, window: int, **kw):
+        super().__init__(graphs, analyser, repeat_time, event_time, **kw)
+        self.window = window  # unused, as in the reference
+
+
+class BWindowedLiveAnalysisTask(LiveAnalysisTask):
+    """LiveTasks/BWindowedLiveAnalysisTask.scala:9-26: takes a window set but never overrides
+    windowSet(); its result() inversion is never called (processResults reads the raw results,
+    AnalysisTask.scala:82), so the job is the un-windowed one."""
+
+    def __init__(self, graphs, analyser, repeat_time, event_time, windows: Sequence[int], **kw):
+        super().__init__(graphs, analyser, repeat_time, event_time, **kw)
+        self.windows = list(windows)  # unused, as in the reference

@@ -50,7 +50,8 @@ __global__ __launch_bounds__(256) void k_check_graph(DevGraph g, int64_t n_ekey,
 __global__ __launch_bounds__(256) void k_check_slots(int64_t nv, const int64_t* __restrict__ adj_off,
                                                      const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
                                                      const int32_t* __restrict__ snbr, const int32_t* __restrict__ uw0,
-                                                     const int32_t* __restrict__ uw1, unsigned long long* bad) {
+                                                     const int32_t* __restrict__ uw1, const int32_t* __restrict__ grank,
+                                                     unsigned long long* bad) {
   const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t nth = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = tid; v < nv; v += nth) {
@@ -66,29 +67,31 @@ __global__ __launch_bounds__(256) void k_check_slots(int64_t nv, const int64_t* 
       if (q < 0 || q >= nv) bump(bad, 11);
     }
     if (uw0) {
-      if (uw0[v] != (int32_t)v) bump(bad, 13);
-      if (uw1[v] != -1 && (uw1[v] < 0 || uw1[v] >= nv)) bump(bad, 12);
+      const int32_t me = grank ? grank[v] : (int32_t)v;
+      if (uw0[v] != (me == INT32_MAX ? -1 : me)) bump(bad, 13);
+      const int32_t u1 = uw_label(uw1[v]);
+      if (u1 != -1 && (u1 < 0 || (!grank && u1 >= nv))) bump(bad, 12);
     }
   }
 }
 
 __global__ __launch_bounds__(256) void k_check_labels(int64_t nv, const uint64_t* __restrict__ vm,
                                                       const int32_t* __restrict__ uw, const int32_t* __restrict__ lab,
-                                                      unsigned long long* bad) {
+                                                      const int32_t* __restrict__ grank, unsigned long long* bad) {
   const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t nth = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = tid; v < nv; v += nth) {
     const uint64_t m = vm[v];
     if (!m) continue;
-    const int32_t x = uw ? uw[v] : -1;
+    const int32_t x = uw ? uw_label(uw[v]) : -1;
     if (x != -1) {
-      if (x < 0 || x >= nv) bump(bad, 14);
+      if (x < 0 || (!grank && x >= nv)) bump(bad, 14);
       continue;
     }
     for (int j = 0; j < 64; j++)
       if ((m >> j) & 1) {
         const int32_t l = lab[v * 64 + j];
-        if (l < 0 || l >= nv) bump(bad, 15);
+        if (l < 0 || (!grank && l >= nv)) bump(bad, 15);
       }
   }
 }
@@ -96,15 +99,16 @@ __global__ __launch_bounds__(256) void k_check_labels(int64_t nv, const uint64_t
 }  // namespace
 
 void launch_check_labels(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, const int32_t* lab,
-                         unsigned long long* bad) {
-  k_check_labels<<<1024, 256, 0, s>>>(nv, vm, uw, lab, bad);
+                         unsigned long long* bad, const int32_t* grank) {
+  k_check_labels<<<1024, 256, 0, s>>>(nv, vm, uw, lab, grank, bad);
 }
 void launch_check_graph(hipStream_t s, const DevGraph& g, int64_t n_ekey, int64_t n_vkey, unsigned long long* bad) {
   k_check_graph<<<1024, 256, 0, s>>>(g, n_ekey, n_vkey, bad);
 }
 void launch_check_slots(hipStream_t s, int64_t nv, const int64_t* adj_off, const uint64_t* vm, const int32_t* cnt,
-                        const int32_t* snbr, const int32_t* uw0, const int32_t* uw1, unsigned long long* bad) {
-  k_check_slots<<<1024, 256, 0, s>>>(nv, adj_off, vm, cnt, snbr, uw0, uw1, bad);
+                        const int32_t* snbr, const int32_t* uw0, const int32_t* uw1, unsigned long long* bad,
+                        const int32_t* grank) {
+  k_check_slots<<<1024, 256, 0, s>>>(nv, adj_off, vm, cnt, snbr, uw0, uw1, grank, bad);
 }
 
 }  // namespace rgpu

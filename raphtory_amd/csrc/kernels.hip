@@ -63,7 +63,13 @@ __device__ __forceinline__ bool line_has(uint64_t m, int lane) { return ((m >> (
 // only when mixed, so the "both buffers agree unless changed in the last two steps" rule of
 // the label rows carries over unchanged.  Rows are materialised (k_uw_rows) before anything
 // outside the superstep loop reads them.
-constexpr int32_t kMixed = -1;
+// kMixed, kChgFlag, uw_label, uw_word: kernels.hpp.  A uniform word also carries bit 31
+// (kChgFlag) when the vertex's label changed in the step that wrote it, so a neighbour reads one
+// random 4-B word per slot (label and "changed" together) instead of its 8-B change word and then
+// the word.  Only mixed neighbours (kMixed) need their change word and row.  A flag left over from
+// an older step (a vertex not visited since) only makes a reader fold an unchanged label, which
+// changes nothing: L_r(v) = min over the ball of radius r, and the neighbour's current label was
+// already folded into v's when the neighbour last changed.
 
 // fold the labels x (per lane = slot, wave-uniform loop over the lanes of `bal`) into best
 // (lane = view) on the views a of each slot
@@ -77,10 +83,11 @@ __device__ __forceinline__ int32_t fold_uniform(uint64_t bal, uint64_t a, int32_
   return best;
 }
 
-// uw of a freshly computed row (lane = view, member lanes mv): x if uniform, else kMixed
+// uw of a freshly computed row (lane = view, member lanes mv): x if uniform, else kMixed.  The
+// label INT32_MAX is kept as a row (its flagged form would read as kMixed).
 __device__ __forceinline__ int32_t row_uniform(int32_t best, uint64_t mv, int lane) {
   const int32_t x0 = __builtin_amdgcn_readlane(best, __builtin_ctzll(mv));
-  return __ballot(((mv >> lane) & 1) && best != x0) ? kMixed : x0;
+  return (x0 == INT32_MAX || __ballot(((mv >> lane) & 1) && best != x0)) ? kMixed : x0;
 }
 
 // floor(t) of a sorted key list (key = time*2 + alive): index of the last key <= 2t+1, or -1.
@@ -437,7 +444,7 @@ void launch_lane_fold(hipStream_t s, unsigned long long* lanechg, unsigned long 
 // work != nullptr (profile / trace runs).  The halting vote is a plain flag store instead.
 // Profile-run work counters, [step][shard][kWorkFields] (rgpu.cpp turns them into bytes):
 //   supersteps: 0 visited vertices, 1 their kept slots, 2 changed vertices, 3 label lanes
-//   gathered from mixed rows, 4 slots whose neighbour's uniform word was read, 5 own-row 64-B
+//   gathered from mixed rows, 4 slots whose (mixed) neighbour's change word was read, 5 own-row 64-B
 //   lines read, 6 row lines written, 7 uniform words written;
 //   superstep 1 (K2): 0 members, 1 kept slots, 2 changed, 4 static slots scanned, 6, 7 as above.
 __device__ __forceinline__ void add_work(unsigned long long* work, int step, const unsigned long long (&f)[8]) {
@@ -545,18 +552,18 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
   Ctr members{}, alive{}, scanned{}, lw{}, uwn{};
   unsigned long long changed = 0;
   uint64_t lanes = 0;  // views with a step-1 change in this wave
-  // `span` (<= 64) vertices per wave round: the lanes read their view masks (one coalesced load),
-  // clear the non-members' count / mask words, and the wave then walks the members one by one.
-  // The span shrinks when the grid has more waves than 64-vertex rounds (small graphs), so every
-  // wave gets work instead of a few waves walking 64 members each.
-  const int64_t span = wave_span(nv, nwaves);
-  for (int64_t b0 = wave * span; b0 < nv; b0 += nwaves * span) {
-   const int64_t vlane = b0 + lane;
-   const uint64_t mvl = (lane < span && vlane < nv) ? vm[vlane] : 0;
-   if (lane < span && vlane < nv && mvl == 0) { cnt[vlane] = 0; vadj[vlane] = 0; }
+  // Vertices are dealt to the waves cyclically (rank v goes to wave v mod nwaves): in the locality
+  // order (packer.cpp locality_order) ranks are sorted by activity, so consecutive ranks have
+  // similar slot counts, and a contiguous run per wave would hand one wave all the busiest
+  // vertices.  Per round the lanes read 64 vertices' view masks, clear the non-members' count /
+  // mask words, and the wave then walks the members one by one.
+  for (int64_t k0 = 0; wave + k0 * nwaves < nv; k0 += 64) {
+   const int64_t vlane = wave + (k0 + lane) * nwaves;
+   const uint64_t mvl = vlane < nv ? vm[vlane] : 0;
+   if (vlane < nv && mvl == 0) { cnt[vlane] = 0; vadj[vlane] = 0; }
    uint64_t todo = __ballot(mvl != 0);
    while (todo) {
-    const int64_t v = b0 + __builtin_ctzll(todo);
+    const int64_t v = wave + (k0 + __builtin_ctzll(todo)) * nwaves;
     const uint64_t mv = readlane64(mvl, __builtin_ctzll(todo));
     todo &= todo - 1;
     const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
@@ -573,7 +580,9 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       if (own) {
         if (uw0) {  // label_0 = own rank on every member lane: uniform
           const int32_t u = row_uniform(best, mv, lane);
-          if (lane == 0) { uw0[v] = me; uw1[v] = u; }
+          const bool ch1 = __ballot(best < me) != 0;  // (a ballot of the whole wave, outside lane 0's branch)
+          if (lane == 0) { uw0[v] = me == INT32_MAX ? kMixed : me; uw1[v] = uw_word(u, ch1); }
+          if (me == INT32_MAX) row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
           if (u == kMixed) row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
         } else {
           row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
@@ -611,7 +620,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     const bool own = v < n_own;
     const int32_t me = grank ? grank[v] : (int32_t)v;
     if (uw0) {
-      if (lane == 0) uw0[v] = me;
+      if (lane == 0) uw0[v] = me == INT32_MAX ? kMixed : me;
+      if (me == INT32_MAX) row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
     } else {
       row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
     }
@@ -662,7 +672,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     }
     if (uw1) {
       const int32_t u = row_uniform(best, mv, lane);
-      if (lane == 0) uw1[v] = u;
+      const bool ch1 = __ballot(best < me) != 0;  // (a ballot of the whole wave, outside lane 0's branch)
+      if (lane == 0) uw1[v] = uw_word(u, ch1);
       if (u == kMixed) row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
       uwn += 2;
       if (u == kMixed) lw += row_lines(mv);
@@ -876,6 +887,10 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     const int64_t b_l = adj_off[vl];
     const uint64_t cp_l = chg_prev[vl];
     const int32_t u_l = uw_cur ? uw_cur[vl] : kMixed;
+    // the vertex's word in the buffer this step writes: a flag left there by a change two steps
+    // ago is cleared below when the vertex does not rewrite the word (else every reader of the
+    // next step would fold this vertex again)
+    const int32_t un_l = uw_next ? uw_next[vl] : kMixed;
     int64_t vv[CH];
     int32_t cur[CH];
 #pragma unroll
@@ -883,7 +898,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       vv[i] = (int64_t)readlane64((uint64_t)vl, i);
       const int32_t u = __builtin_amdgcn_readlane(u_l, i);
       if (u != kMixed) {
-        cur[i] = u;  // wave-uniform: no row load
+        cur[i] = u & 0x7fffffff;  // wave-uniform: no row load
       } else {
         cur[i] = row_get<BUF>(lab_cur + vv[i] * 64, (readlane64(mv_l, i) >> lane) & 1, lane);
         wk.lr += row_lines(readlane64(mv_l, i));
@@ -902,20 +917,43 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       nb[i] = lane < n ? q : 0;
       sm[i] = lane < n ? m : 0;
     }
-    // stage 3: neighbours' change words (vertex 0's word for idle lanes, masked by sm = 0),
-    // then the uniform words of the neighbours that changed
+    // stage 3: with uniform words, every slot's neighbour word (label + changed flag: one random
+    // 4-B load; vertex 0's word for idle lanes, masked by sm = 0), then the change words of the
+    // mixed neighbours only (a wave-uniform branch: most chunks have none).  A uniform neighbour
+    // that changed is folded on every kept view of the slot (exact: kernels.hpp uw_word).
+    // Without uniform words: every neighbour's change word.
     uint64_t act[CH];
     int32_t un[CH];
+    if (uw_cur) {
+      int32_t w[CH];
 #pragma unroll
-    for (int i = 0; i < CH; i++) {
-      act[i] = sm[i] & chg_prev[nb[i]];
+      for (int i = 0; i < CH; i++) w[i] = uw_cur[nb[i]];
+      uint64_t mixed = 0;
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        act[i] = (w[i] != kMixed && w[i] < 0) ? sm[i] : 0;
+        un[i] = w[i] == kMixed ? kMixed : (w[i] & 0x7fffffff);
+        mixed |= __ballot(w[i] == kMixed && sm[i] != 0);
+      }
+      if (mixed) {
+        uint64_t cw[CH];
+#pragma unroll
+        for (int i = 0; i < CH; i++) cw[i] = chg_prev[(w[i] == kMixed && sm[i] != 0) ? nb[i] : 0];
+#pragma unroll
+        for (int i = 0; i < CH; i++) {
+          if (w[i] == kMixed) act[i] = sm[i] & cw[i];
+          wk.a += __popcll(__ballot(w[i] == kMixed && sm[i] != 0));  // change words read
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        act[i] = sm[i] & chg_prev[nb[i]];
+        un[i] = kMixed;
+      }
     }
 #pragma unroll
-    for (int i = 0; i < CH; i++) {
-      un[i] = (uw_cur && act[i]) ? uw_cur[nb[i]] : kMixed;
-      if (uw_cur) wk.a += __popcll(__ballot(act[i] != 0));
-      wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
-    }
+    for (int i = 0; i < CH; i++) wk.g += un[i] == kMixed ? __popcll(act[i]) : 0;  // lanes gathered from rows (per lane)
     // own rows are only meaningful on member lanes
 #pragma unroll
     for (int i = 0; i < CH; i++) cur[i] = ((readlane64(mv_l, i) >> lane) & 1) ? cur[i] : INT32_MAX;
@@ -936,7 +974,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     }
     if (uw_cur) {
 #pragma unroll
-      for (int i = 0; i < CH; i++) best[i] = fold_uniform(__ballot(un[i] != kMixed), act[i], un[i], best[i], lane);
+      for (int i = 0; i < CH; i++)
+        best[i] = fold_uniform(__ballot(un[i] != kMixed && act[i] != 0), act[i], un[i], best[i], lane);
     }
 #pragma unroll
     for (int i = 0; i < CH; i++) {
@@ -948,12 +987,25 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
           const int32_t j = c2 + lane;
           const int64_t idx = base + (j < n ? j : c2);
           const int32_t q = snbr[idx];
-          const uint64_t a2 = j < n ? (smask[idx] & chg_prev[q]) : 0;
-          const int32_t u2 = (uw_cur && a2) ? uw_cur[q] : kMixed;
-          if (uw_cur) wk.a += __popcll(__ballot(a2 != 0));
+          const uint64_t m2 = j < n ? smask[idx] : 0;
+          uint64_t a2;
+          int32_t u2 = kMixed;
+          if (uw_cur) {  // as stage 3
+            const int32_t w2 = uw_cur[q];
+            a2 = (w2 != kMixed && w2 < 0) ? m2 : 0;
+            u2 = w2 == kMixed ? kMixed : (w2 & 0x7fffffff);
+            const bool mx = w2 == kMixed && m2 != 0;
+            if (__ballot(mx)) {
+              const uint64_t c2 = chg_prev[mx ? q : 0];
+              if (mx) a2 = m2 & c2;
+              wk.a += __popcll(__ballot(mx));
+            }
+          } else {
+            a2 = m2 & chg_prev[q];
+          }
           wk.g += u2 == kMixed ? __popcll(a2) : 0;
           best[i] = gather_min<BUF>(u2 == kMixed ? a2 : 0, q, best[i], lab_cur, lane);
-          if (uw_cur) best[i] = fold_uniform(__ballot(u2 != kMixed), a2, u2, best[i], lane);
+          if (uw_cur) best[i] = fold_uniform(__ballot(u2 != kMixed && a2 != 0), a2, u2, best[i], lane);
         }
       }
     }
@@ -983,13 +1035,16 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       const uint64_t ch = __ballot(best[i] < cur[i]);
       if (ch || readlane64(cp_l, i)) {
         const int32_t u = uw_next ? row_uniform(best[i], mv, lane) : kMixed;
-        if (uw_next && lane == 0) uw_next[v] = u;
+        if (uw_next && lane == 0) uw_next[v] = uw_word(u, ch != 0);
         if (uw_next) wk.uw += 1;
         if (u == kMixed) {
           if (BUF) row_store(lab_next + v * 64, best[i], line_has(mv, lane), lane);
           else lab_next[v * 64 + lane] = best[i];
           wk.lw += BUF ? row_lines(mv) : 4;
         }
+      } else if (uw_next) {
+        const int32_t un = __builtin_amdgcn_readlane(un_l, i);
+        if (un != kMixed && un < 0 && lane == 0) uw_next[v] = un & 0x7fffffff;  // stale flag
       }
       if (lane == 0) chg_next[v] = ch;
       if (ch) {
@@ -1027,7 +1082,8 @@ __global__ __launch_bounds__(256) void k_uw_rows(int64_t nv, const uint64_t* __r
     const int32_t ul = vl < nv ? uw[vl] : kMixed;
     for (uint64_t todo = __ballot(mvl != 0 && ul != kMixed); todo; todo &= todo - 1) {
       const int L = __builtin_ctzll(todo);
-      row_store(lab + (b0 + L) * 64, __builtin_amdgcn_readlane(ul, L), line_has(readlane64(mvl, L), lane), lane);
+      row_store(lab + (b0 + L) * 64, __builtin_amdgcn_readlane(ul, L) & 0x7fffffff, line_has(readlane64(mvl, L), lane),
+                lane);
     }
   }
 }
@@ -1082,16 +1138,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
   int32_t changed = 0;
   std::conditional_t<PROF, StepWork, NoWork> wk;
   const TailList none{nullptr, nullptr};
-  // `span` (<= 64) chunks per wave round: lane l reads chunk l's frontier flags (one coalesced
-  // load), and the wave then runs only the flagged chunks — a sparse frontier costs one load per
-  // 64 chunks.  On a small graph the span shrinks so that the dense supersteps spread over every
-  // wave of the grid (C2: 25k chunks over 4,096 waves -> 7 per round).
+  // Chunks are dealt to the waves cyclically (chunk c goes to wave c mod nwaves, as K2 deals
+  // vertices): per round lane l reads its chunk's frontier flags, and the wave then runs only the
+  // flagged chunks — a sparse frontier costs one load per 64 chunks.  Every wave of the grid gets
+  // work on a small graph too, and the busy chunks of the locality order (runs of hubs) spread
+  // over the waves instead of queueing behind one.
   const int64_t nchunks = (nv + CH - 1) / CH;
-  const int64_t span = wave_span(nchunks, nwaves);
-  for (int64_t c0 = wave * span; c0 < nchunks; c0 += nwaves * span) {
-    const int64_t cl = c0 + lane;
+  for (int64_t k0 = 0; wave + k0 * nwaves < nchunks; k0 += 64) {
+    const int64_t cl = wave + (k0 + lane) * nwaves;
     uint32_t fb = 0;
-    if (lane < span && cl < nchunks) {
+    if (cl < nchunks) {
       const int64_t v0 = cl * CH;
       if (visit_all) {
         fb = (1u << CH) - 1;
@@ -1108,7 +1164,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
       const int L = __builtin_ctzll(todo);
       todo &= todo - 1;
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
-      cc_chunk<CH, BUF, false>((c0 + L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
+      cc_chunk<CH, BUF, false>((wave + (k0 + L) * nwaves) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
                                lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
                                hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks);
     }
@@ -1285,9 +1341,10 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
     const int64_t lo0 = seg_lo[sg];
-    // a heavy ghost keeps no compacted slots; with time-ordered slots a segment whose newest
-    // edge predates the batch's cut keeps none either
-    const uint64_t mv = (v < n_own && !(ts_t && ts_t[lo0] < tcut)) ? vm[v] : 0;
+    // a heavy ghost (partitioned) is compacted too: k_heavy_mark walks its kept slots when its
+    // owner's records say it changed.  With time-ordered slots a segment whose newest edge
+    // predates the batch's cut keeps none.
+    const uint64_t mv = !(ts_t && ts_t[lo0] < tcut) ? vm[v] : 0;
     if (mv == 0) {
       if (lane == 0) { segcnt[sg] = 0; segor[sg] = 0; }
       continue;
@@ -1335,7 +1392,8 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
     }
     for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
     if (lane == 0) { segcnt[sg] = count; segor[sg] = any; }
-    if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
+    if (best != INT32_MAX && v < n_own) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);  // (a ghost's
+                                                                                             // labels are its owner's)
   }
 }
 
@@ -1378,11 +1436,11 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                       // the hub's slot list: 4 B instead of 12 B per unchanged neighbour)
         const bool hot = jj < n && ((cb_prev[q >> 6] >> (q & 63)) & 1);
         const uint64_t m = hot ? smask[idx] : 0;
-        u = hot ? uw_cur[q] : kMixed;
+        u = hot ? uw_label(uw_cur[q]) : kMixed;
         a = hot ? (u == kMixed ? m & chg_prev[q] : m) : 0;
       } else {
         a = jj < n ? (smask[idx] & chg_prev[q]) : 0;
-        u = (uw_cur && a) ? uw_cur[q] : kMixed;
+        u = (uw_cur && a) ? uw_label(uw_cur[q]) : kMixed;
       }
       // lane = view: the changed mixed rows (4 in flight), then the uniform neighbours' words
       best = gather_min<false>(u == kMixed ? a : 0, q, best, lab_cur, lane);
@@ -1428,33 +1486,6 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
     if (act_cur && v < n_own && !act_cur[v]) continue;  // a ghost's word is current (set by its records)
     const uint64_t ch = chg_now[v];
     if (!ch) continue;
-    if (v >= n_own) {  // heavy ghost (partitioned): its static slots of the segment, kept on the fly
-      if (!vm || !em) continue;
-      const uint64_t mv = vm[v] & ch;
-      const int64_t lo = seg_lo[sg], rel0 = lo - adj_off[v], o0 = out_off[v], i0 = in_off[v];
-      const int64_t nout = out_off[v + 1] - o0;
-      const int32_t ns = seg_n[sg];
-      for (int32_t c = 0; c < ns; c += 64) {
-        if (ts_t && ts_t[lo + c] < tcut) break;  // time-ordered slots: the rest predate the batch
-        if (c + lane >= ns) continue;
-        const int64_t rel = rel0 + c + lane;
-        int64_t e;
-        int32_t nb;
-        if (ts_e) {
-          if (ts_t[lo + c + lane] < tcut) continue;
-          e = ts_e[lo + c + lane];
-          nb = ts_nb[lo + c + lane];
-        } else if (rel < nout) {
-          e = o0 + rel;
-          nb = edst[e];
-        } else {
-          e = in_eid[i0 + (rel - nout)];
-          nb = esrc[e];
-        }
-        if (nb != v && (em[e] & vm[nb] & mv)) act_next[nb] = 1;
-      }
-      continue;
-    }
     const int32_t n = segcnt[sg];
     const int64_t base = seg_lo[sg];
     for (int32_t c = 0; c < n; c += 64) {
@@ -1660,7 +1691,7 @@ __global__ __launch_bounds__(256) void k_cc_count(int64_t nv, uint64_t vmask, co
     const int64_t v = b0 + lane;
     const uint64_t mv = v < nv ? vm[v] & vmask : 0;
     const uint64_t ad = v < nv ? vadj[v] : 0;
-    const int32_t x = v < nv ? uw[v] : kMixed;
+    const int32_t x = v < nv ? uw_label(uw[v]) : kMixed;
     iso_acc += (unsigned)__popcll(transpose64(mv & ~ad, lane));
     const uint64_t m = mv & ad;
     uint64_t todo = __ballot(m != 0 && x != kMixed);
@@ -1701,7 +1732,8 @@ __global__ __launch_bounds__(256) void k_cc_roots(int64_t nv, uint64_t vmask, co
                                                   const int32_t* __restrict__ uw,
                                                   const int32_t* __restrict__ lab, int32_t* __restrict__ counts,
                                                   unsigned long long* __restrict__ stats,
-                                                  unsigned int* __restrict__ iso_g, int scan_all) {
+                                                  unsigned int* __restrict__ iso_g, int scan_all,
+                                                  const int32_t* __restrict__ grank, int rows_by_rank) {
   __shared__ unsigned long long red[6][64];
   for (int i = threadIdx.x; i < 6 * 64; i += blockDim.x) (&red[0][0])[i] = 0;
   __syncthreads();
@@ -1725,14 +1757,16 @@ __global__ __launch_bounds__(256) void k_cc_roots(int64_t nv, uint64_t vmask, co
   for (int64_t b0 = wave * 64; b0 < nv; b0 += nwaves * 64) {
     const int64_t v = b0 + lane;
     const uint64_t m = v < nv ? vm[v] & vmask & vadj[v] : 0;
-    const int32_t x = v < nv ? uw[v] : kMixed;
-    for (uint64_t cand = __ballot(m != 0 && (scan_all || x == (int32_t)v || x == kMixed)); cand; cand &= cand - 1) {
+    const int32_t x = (v < nv && uw) ? uw_label(uw[v]) : kMixed;
+    const int32_t me = v < nv ? (grank ? grank[v] : (int32_t)v) : -2;  // the vertex's own label
+    for (uint64_t cand = __ballot(m != 0 && (scan_all || x == me || x == kMixed)); cand; cand &= cand - 1) {
       const int L = __builtin_ctzll(cand);
-      const int64_t r = b0 + L;
+      const int32_t meL = __builtin_amdgcn_readlane(me, L);
+      const int64_t r = rows_by_rank ? b0 + L : (int64_t)meL;  // its count row
       const uint64_t mL = readlane64(m, L);
       const bool in = (mL >> lane) & 1;
       const bool root = scan_all || __builtin_amdgcn_readlane(x, L) != kMixed ? in
-                                                                            : (in && lab[r * 64 + lane] == (int32_t)r);
+                                                                            : (in && lab[(b0 + L) * 64 + lane] == meL);
       const int32_t c = root ? counts[r * 64 + lane] : 0;
       if (c) {
         counts[r * 64 + lane] = 0;
@@ -1792,6 +1826,29 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane) {
   return x;
 }
 
+// DegreeRanking / DegreeBasic top-20 (DegreeRanking.scala:14-26, DegreeBasic.scala:16-28): per view
+// the 20 members with the largest in-degree, ties by ascending id (the reference's ParTrieMap order
+// is unordered).  A candidate is key = in-degree << 32 | ~label (labels are order-preserving with
+// ids), so a larger key wins; 0 = none.  TOP: k_degree keeps every lane's (view's) best 20 in
+// registers over the vertices its wave scans and writes them out ([wave][view][kTop], sorted);
+// k_deg_top_merge (one block per view) merges the waves' lists and the heavy vertices (their
+// in-degrees are completed by k_heavy_degree after k_degree).
+template <int N>
+__device__ __forceinline__ void top_insert(uint64_t (&tk)[N], int32_t (&tp)[N], uint64_t x, int32_t xp) {
+  if (x <= tk[N - 1]) return;
+#pragma unroll
+  for (int i = 0; i < N; i++)
+    if (x > tk[i]) {
+      const uint64_t a = tk[i];
+      const int32_t b = tp[i];
+      tk[i] = x;
+      tp[i] = xp;
+      x = a;
+      xp = b;
+    }
+}
+
+template <bool TOP>
 __global__ __launch_bounds__(256) void k_degree(int64_t nv, const int64_t* __restrict__ out_off,
                                                 const int64_t* __restrict__ in_off,
                                                 const int32_t* __restrict__ in_eid,
@@ -1800,7 +1857,13 @@ __global__ __launch_bounds__(256) void k_degree(int64_t nv, const int64_t* __res
                                                 int32_t* __restrict__ outdeg,
                                                 int32_t* __restrict__ indeg,
                                                 unsigned long long* __restrict__ stats,
-                                                const int32_t* __restrict__ hv_of) {
+                                                const int32_t* __restrict__ hv_of,
+                                                const int32_t* __restrict__ grank,
+                                                uint64_t* __restrict__ cand_key, int32_t* __restrict__ cand_pos) {
+  uint64_t tk[TOP ? kTop : 1];
+  int32_t tp[TOP ? kTop : 1];
+#pragma unroll
+  for (int i = 0; i < (TOP ? kTop : 1); i++) { tk[i] = 0; tp[i] = -1; }
   __shared__ unsigned long long red[3][64];
   for (int i = threadIdx.x; i < 3 * 64; i += blockDim.x) (&red[0][0])[i] = 0;
   __syncthreads();
@@ -1831,9 +1894,22 @@ __global__ __launch_bounds__(256) void k_degree(int64_t nv, const int64_t* __res
       tv += in_view;
       to += od;
       ti += id;
+      if constexpr (TOP) {
+        if (in_view && !(hv_of && hv_of[v] >= 0)) {  // (heavy vertices: k_deg_top_merge)
+          const uint32_t lb = grank ? (uint32_t)grank[v] : (uint32_t)v;
+          top_insert(tk, tp, ((uint64_t)(uint32_t)id << 32) | (uint32_t)~lb, (int32_t)v);
+        }
+      }
     }
     outdeg[v * 64 + lane] = od;
     indeg[v * 64 + lane] = id;
+  }
+  if constexpr (TOP) {
+#pragma unroll
+    for (int i = 0; i < kTop; i++) {
+      cand_key[(wave * 64 + lane) * kTop + i] = tk[i];
+      cand_pos[(wave * 64 + lane) * kTop + i] = tp[i];
+    }
   }
   atomicAdd(&red[0][lane], tv);
   atomicAdd(&red[1][lane], to);
@@ -1889,6 +1965,73 @@ __global__ __launch_bounds__(256) void k_heavy_degree(int64_t nseg, const int32_
       atomicAdd(&indeg[(int64_t)v * 64 + lane], ci);
       atomicAdd(&stats[2 * 64 + lane], (unsigned long long)ci);
     }
+  }
+}
+
+// One block per view: the waves' candidate lists and the heavy vertices -> the view's top 20
+// (key, local rank, out-degree); keys of 0 pad a short list.
+__global__ __launch_bounds__(256) void k_deg_top_merge(int64_t ncand_waves, const uint64_t* __restrict__ cand_key,
+                                                       const int32_t* __restrict__ cand_pos, int64_t n_heavy,
+                                                       const int32_t* __restrict__ hv_seg,
+                                                       const int32_t* __restrict__ seg_v, int64_t n_own,
+                                                       const uint64_t* __restrict__ vm,
+                                                       const int32_t* __restrict__ indeg,
+                                                       const int32_t* __restrict__ outdeg,
+                                                       const int32_t* __restrict__ grank,
+                                                       unsigned long long* __restrict__ top_key,
+                                                       int32_t* __restrict__ top_pos, int32_t* __restrict__ top_out) {
+  const int j = blockIdx.x;
+  uint64_t tk[kTop];
+  int32_t tp[kTop];
+#pragma unroll
+  for (int i = 0; i < kTop; i++) { tk[i] = 0; tp[i] = -1; }
+  for (int64_t w = threadIdx.x; w < ncand_waves; w += blockDim.x) {
+    const int64_t b = (w * 64 + j) * kTop;
+    for (int i = 0; i < kTop; i++) {
+      const uint64_t x = cand_key[b + i];
+      if (x <= tk[kTop - 1]) break;  // each list is sorted, descending
+      top_insert(tk, tp, x, cand_pos[b + i]);
+    }
+  }
+  for (int64_t h = threadIdx.x; h < n_heavy; h += blockDim.x) {
+    const int32_t v = seg_v[hv_seg[h]];
+    if (v >= n_own || !((vm[v] >> j) & 1)) continue;  // (a heavy ghost is its owner's)
+    const uint32_t lb = grank ? (uint32_t)grank[v] : (uint32_t)v;
+    top_insert(tk, tp, ((uint64_t)(uint32_t)indeg[(int64_t)v * 64 + j] << 32) | (uint32_t)~lb, v);
+  }
+  // 20 rounds of a block-wide maximum over the threads' heads (keys are distinct)
+  __shared__ unsigned long long wbest[4];
+  __shared__ unsigned long long best;
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  for (int r = 0; r < kTop; r++) {
+    unsigned long long x = tk[0];
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long y = shfl_xor64(x, o);
+      x = y > x ? y : x;
+    }
+    if (lane == 0) wbest[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long m = wbest[0];
+      for (int k = 1; k < (int)(blockDim.x >> 6); k++) m = wbest[k] > m ? wbest[k] : m;
+      best = m;
+    }
+    __syncthreads();
+    const unsigned long long m = best;
+    if (m != 0 && tk[0] == m) {  // the winner pops its head
+      top_key[j * kTop + r] = m;
+      top_pos[j * kTop + r] = tp[0];
+      top_out[j * kTop + r] = outdeg[(int64_t)tp[0] * 64 + j];
+#pragma unroll
+      for (int i = 0; i < kTop - 1; i++) { tk[i] = tk[i + 1]; tp[i] = tp[i + 1]; }
+      tk[kTop - 1] = 0;
+      tp[kTop - 1] = -1;
+    } else if (m == 0 && threadIdx.x == 0) {
+      top_key[j * kTop + r] = 0;
+      top_pos[j * kTop + r] = -1;
+      top_out[j * kTop + r] = 0;
+    }
+    __syncthreads();
   }
 }
 
@@ -2161,10 +2304,10 @@ void launch_cc_count(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, 
 }
 void launch_cc_roots(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, const uint64_t* vadj,
                      const int32_t* uw, const int32_t* lab, int32_t* counts, unsigned long long* stats,
-                     unsigned int* iso, bool scan_all) {
+                     unsigned int* iso, bool scan_all, const int32_t* grank, bool rows_by_rank) {
   const uint64_t vmask = nviews >= 64 ? ~0ull : ((1ull << nviews) - 1);
   k_cc_roots<<<grid_for(nv, 256, 4096), 256, 0, s>>>(nv, vmask, vm, vadj, uw, lab, counts, stats, iso,
-                                                     scan_all ? 1 : 0);
+                                                     scan_all ? 1 : 0, grank, rows_by_rank ? 1 : 0);
 }
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
@@ -2248,14 +2391,25 @@ void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hi
   dim3 grid(grid_for(g.nv, 256, (unsigned)g_sum_blocks), (unsigned)nviews);
   k_cc_summary<<<grid, 256, 0, s>>>(g.nv, hist, stats, iso);
 }
+int64_t deg_top_waves(int64_t nv) { return (int64_t)grid_for(nv, 4, 2048) * 4; }
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
-                   int32_t* outdeg, int32_t* indeg, unsigned long long* stats) {
-  k_degree<<<grid_for(g.nv, 4, 2048), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, vm, em,
-                                                     outdeg, indeg, stats, g.n_seg > 0 ? g.hv_of : nullptr);
+                   int32_t* outdeg, int32_t* indeg, unsigned long long* stats, const DegTop* top) {
+  const unsigned grid = grid_for(g.nv, 4, 2048);
+  const int32_t* hv = g.n_seg > 0 ? g.hv_of : nullptr;
+  if (top)
+    k_degree<true><<<grid, 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, vm, em, outdeg, indeg, stats, hv,
+                                        g.grank, top->cand_key, top->cand_pos);
+  else
+    k_degree<false><<<grid, 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, vm, em, outdeg, indeg, stats, hv,
+                                         nullptr, nullptr, nullptr);
   if (g.n_seg > 0)
     k_heavy_degree<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_lo, g.seg_n, g.out_off,
                                                                g.in_off, g.adj_off, g.in_eid, vm, em, outdeg, indeg,
                                                                stats, g.nv);
+  if (top)
+    k_deg_top_merge<<<kViews, 256, 0, s>>>((int64_t)grid * 4, top->cand_key, top->cand_pos, g.n_seg > 0 ? g.n_heavy : 0,
+                                           g.hv_seg, g.seg_v, g.nv, vm, indeg, outdeg, g.grank, top->key, top->pos,
+                                           top->out);
 }
 void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      const int32_t* outdeg, int32_t* cnt, int32_t* snbr, uint64_t* smask,

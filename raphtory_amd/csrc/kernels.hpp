@@ -3,11 +3,23 @@
 #include <vector>
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdint>
 
 namespace rgpu {
 
 constexpr int kViews = 64;  // views per batch = wavefront width (lane j <-> view j)
+
+// Uniform label words (kernels.hip): uw[v] = the label every member lane of v holds, or kMixed
+// when they differ (the row is then the state).  Bit 31 (kChgFlag) of a uniform word is set when
+// the label changed in the superstep that wrote the word; a uniform label is never INT32_MAX, so
+// a flagged word never reads as kMixed.
+constexpr int32_t kMixed = -1;
+constexpr int32_t kChgFlag = INT32_MIN;
+__host__ __device__ inline int32_t uw_label(int32_t w) { return w == kMixed ? kMixed : (w & 0x7fffffff); }
+__host__ __device__ inline int32_t uw_word(int32_t u, bool changed) {
+  return (u != kMixed && changed) ? (int32_t)((uint32_t)u | 0x80000000u) : u;
+}
 
 // One batch of views: hops[K] x windows[W], view bit j = w*KS + k (window-major, KS = hop
 // stride of the run, K <= KS hops in this batch, KS*W <= 64).  Window-major order keeps the
@@ -139,15 +151,18 @@ void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t
 // zero by launch_cc_roots, which also folds iso and writes the summary fields into stats
 void launch_cc_count(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, const uint64_t* vadj,
                      const int32_t* uw, const int32_t* lab, int32_t* counts, unsigned int* iso);
+// grank: the label of each rank (null: the rank itself); counts rows are indexed by label, or
+// (rows_by_rank, partitioned: labels are ids) by the rank
 void launch_cc_roots(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, const uint64_t* vadj,
                      const int32_t* uw, const int32_t* lab, int32_t* counts, unsigned long long* stats,
-                     unsigned int* iso, bool scan_all);
+                     unsigned int* iso, bool scan_all, const int32_t* grank = nullptr, bool rows_by_rank = false);
 // RGPU_CHECK (check.hip): structural checks, violations counted into bad[16]
 void launch_check_graph(hipStream_t s, const DevGraph& g, int64_t n_ekey, int64_t n_vkey, unsigned long long* bad);
 void launch_check_labels(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, const int32_t* lab,
-                         unsigned long long* bad);
+                         unsigned long long* bad, const int32_t* grank = nullptr);
 void launch_check_slots(hipStream_t s, int64_t nv, const int64_t* adj_off, const uint64_t* vm, const int32_t* cnt,
-                        const int32_t* snbr, const int32_t* uw0, const int32_t* uw1, unsigned long long* bad);
+                        const int32_t* snbr, const int32_t* uw0, const int32_t* uw1, unsigned long long* bad,
+                        const int32_t* grank = nullptr);
 // Changed bits (with uniform words and heavy vertices): one bit per local rank, set when the
 // vertex's label changed in a step; three bitmaps rotate (step r writes r % 3, the hub gather of
 // step r+1 reads it, step r+2 clears it).  The hub gather probes a neighbour's bit (L2-resident:
@@ -178,8 +193,19 @@ void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, cons
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso);
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
                        unsigned long long* stats, unsigned int* iso);
+// DegreeRanking top-20 per view (kernels.hip k_deg_top_merge): key = in-degree << 32 | ~label
+constexpr int kTop = 20;
+struct DegTop {
+  uint64_t* cand_key = nullptr;   // [deg_top_waves(nv)][64][kTop] per-wave candidates
+  int32_t* cand_pos = nullptr;
+  unsigned long long* key = nullptr;  // [64][kTop] result (0: none)
+  int32_t* pos = nullptr;             // its local rank
+  int32_t* out = nullptr;             // its out-degree
+};
+int64_t deg_top_waves(int64_t nv);
+// top: also the top-20 by in-degree of every view (null: totals and rows only)
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
-                   int32_t* outdeg, int32_t* indeg, unsigned long long* stats);
+                   int32_t* outdeg, int32_t* indeg, unsigned long long* stats, const DegTop* top = nullptr);
 void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                      const int32_t* outdeg, int32_t* cnt, int32_t* snbr, uint64_t* smask,
                      double* pr, double* contrib);
@@ -235,17 +261,20 @@ void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_
 // owned id -> owned rank: ids ascend with rank; bucket b = id >> shift covers ranks
 // [boff[b], boff[b+1]) (about one id per bucket)
 struct OwnIdx {
-  const int64_t* vid = nullptr;
+  const int64_t* vid = nullptr;   // owned ids ascending
   const int32_t* boff = nullptr;
+  const int32_t* pos = nullptr;   // local rank of the k-th owned id (null: k itself)
   int shift = 0;
   int64_t n_own = 0;
 };
-// component counts routed to the label owners (one pass; remote_only: the records again, into a
-// larger buffer, without the local counts); gcnt[q] counts every record for peer q
-void launch_hist_route(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
-                       const uint64_t* vm, const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso,
-                       unsigned long long* gcnt, unsigned long long* hsbuf);
-void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const OwnIdx& I, int32_t* hist);
+// component counts of the owned members (xchg.hip k_part_count): owned labels counted at their
+// count rows (counts[local rank][view]), the others routed to the label owners (remote_only: the
+// records again, into a larger buffer, without the local counts); gcnt[q] counts every record for
+// peer q.  uw may be null (rows only).
+void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
+                       const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,
+                       unsigned int* iso, unsigned long long* gcnt, unsigned long long* hsbuf);
+void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const OwnIdx& I, int32_t* counts);
 // PageRank contribution rows of a list (partitioned PageRank): gather into / scatter out of a
 // contiguous buffer
 void launch_xgather_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* rows, double* buf);

@@ -238,8 +238,28 @@ inline int bits_for(uint64_t maxv) {
 
 }  // namespace
 
+// Locality order.  The superstep and K2 gather one random word per slot from the
+// neighbour (uniform / change word, view mask); on a power-law graph most slots point at a few
+// hubs.  Ranking vertices by activity (updates naming them, a proxy for degree), most active
+// first, packs the hubs' words into few cache lines, so the hot set stays L2-resident.  The
+// superstep kernel and K2 deal chunks / vertices to the waves cyclically, so the busy low ranks
+// spread over every wave (kernels.hip).
+std::vector<int32_t> locality_order(const std::vector<int32_t>& act, int nt) {
+  const int64_t n = (int64_t)act.size();
+  std::vector<uint64_t> key(n);
+  parallel_for((size_t)n, nt, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; i++) key[i] = ((uint64_t)(uint32_t)(INT32_MAX - act[i]) << 32) | (uint64_t)i;
+  });
+  parallel_sort(key, nt, std::less<uint64_t>());  // activity descending, index ascending
+  std::vector<int32_t> ord(n);
+  parallel_for((size_t)n, nt, [&](size_t lo, size_t hi, int) {
+    for (size_t i = lo; i < hi; i++) ord[i] = (int32_t)(key[i] & 0xffffffffu);
+  });
+  return ord;
+}
+
 std::string pack_events(const std::vector<Event>& ev, int partition, int num_partitions,
-                        Packed* out) {
+                        Packed* out, bool locality) {
   if (num_partitions < 1 || partition < 0 || partition >= num_partitions) return "bad partition";
   const int nt = num_threads();
   const size_t n = ev.size();
@@ -274,9 +294,49 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
         rd[i] = (int32_t)(std::lower_bound(ids.begin(), ids.end(), ev[i].dst) - ids.begin());
     }
   });
-  if (num_partitions == 1) {
+  // activity of every id (updates naming it): the locality order's ranking
+  std::vector<int32_t> act;
+  if (locality) {
+    std::vector<std::atomic<int32_t>> a(ids.size());
+    parallel_for(ids.size(), nt, [&](size_t lo, size_t hi, int) {
+      for (size_t g = lo; g < hi; g++) a[g].store(0, std::memory_order_relaxed);
+    });
+    parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
+      for (size_t i = lo; i < hi; i++) {
+        a[rs[i]].fetch_add(1, std::memory_order_relaxed);
+        if (rd[i] >= 0 && rd[i] != rs[i]) a[rd[i]].fetch_add(1, std::memory_order_relaxed);
+      }
+    });
+    act.resize(ids.size());
+    for (size_t g = 0; g < ids.size(); g++) act[g] = a[g].load(std::memory_order_relaxed);
+  }
+  P.relabeled = locality;
+  if (num_partitions == 1 && !locality) {
     P.nv = P.n_own = (int64_t)ids.size();
     P.vid = std::move(ids);
+  } else if (num_partitions == 1) {
+    // labels stay id ranks (order-preserving); local rank = position in the locality order
+    const int64_t nv = (int64_t)ids.size();
+    const std::vector<int32_t> ord = locality_order(act, nt);
+    std::vector<int32_t> pos(nv);
+    P.nv = P.n_own = nv;
+    P.vid.resize(nv);
+    P.grank.resize(nv);
+    parallel_for((size_t)nv, nt, [&](size_t lo, size_t hi, int) {
+      for (size_t k = lo; k < hi; k++) {
+        pos[ord[k]] = (int32_t)k;
+        P.vid[k] = ids[ord[k]];
+        P.grank[k] = ord[k];
+      }
+    });
+    P.by_id = pos;
+    P.lid = std::move(ids);
+    parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
+      for (size_t i = lo; i < hi; i++) {
+        rs[i] = pos[rs[i]];
+        if (rd[i] >= 0) rd[i] = pos[rd[i]];
+      }
+    });
   } else {
     // Partition view (the reference's PM keeps its own vertices plus SplitEdge copies,
     // EntityStorage.scala:303-305): owned vertices, ghosts = other endpoints of edges that
@@ -301,15 +361,30 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
       }
     });
     std::vector<int32_t> g2l(ng, -1);
-    for (int r = 0; r < 2; r++)
+    for (int r = 0; r < 2; r++) {
+      std::vector<int32_t> gs;  // global ranks of this role, ids ascending
       for (int64_t g = 0; g < ng; g++)
-        if (role[g].load(std::memory_order_relaxed) == r) {
-          g2l[g] = (int32_t)P.vid.size();
-          P.vid.push_back(ids[g]);
-          P.grank.push_back((int32_t)ids[g]);  // label = id (ids < 2^31): order-preserving, global
-          P.lowner.push_back((uint8_t)partition_of(ids[g], num_partitions));
-          if (r == 0) P.n_own++;
+        if (role[g].load(std::memory_order_relaxed) == r) gs.push_back((int32_t)g);
+      if (locality) {  // owned and ghost ranks each in their own locality order
+        std::vector<int32_t> a(gs.size());
+        for (size_t k = 0; k < gs.size(); k++) a[k] = act[gs[k]];
+        const std::vector<int32_t> ord = locality_order(a, nt);
+        std::vector<int32_t> o2(gs.size());
+        for (size_t k = 0; k < gs.size(); k++) o2[k] = gs[ord[k]];
+        if (r == 0) {  // owned local ranks in id order
+          P.by_id.resize(gs.size());
+          for (size_t k = 0; k < gs.size(); k++) P.by_id[ord[k]] = (int32_t)(P.vid.size() + k);
         }
+        gs.swap(o2);
+      }
+      for (int32_t g : gs) {
+        g2l[g] = (int32_t)P.vid.size();
+        P.vid.push_back(ids[g]);
+        P.grank.push_back((int32_t)ids[g]);  // label = id (ids < 2^31): order-preserving, global
+        P.lowner.push_back((uint8_t)partition_of(ids[g], num_partitions));
+        if (r == 0) P.n_own++;
+      }
+    }
     P.nv = (int64_t)P.vid.size();
     parallel_for(n, nt, [&](size_t lo, size_t hi, int) {
       for (size_t i = lo; i < hi; i++) {
@@ -491,8 +566,8 @@ std::string pack_events(const std::vector<Event>& ev, int partition, int num_par
   P.xs_off.assign(np + 1, 0);
   P.xr_off.assign(np + 1, 0);
   for (int q = 0; q < np; q++) {
-    for (auto* L : {&S[q], &R[q]}) {
-      std::sort(L->begin(), L->end());
+    for (auto* L : {&S[q], &R[q]}) {  // by id (local ranks need not follow ids)
+      std::sort(L->begin(), L->end(), [&](int32_t x, int32_t y) { return P.vid[x] < P.vid[y]; });
       L->erase(std::unique(L->begin(), L->end()), L->end());
     }
     P.xs_v.insert(P.xs_v.end(), S[q].begin(), S[q].end());

@@ -79,6 +79,8 @@ struct Slot {
   unsigned long long* h_work = nullptr;
   unsigned long long* stats = nullptr;
   int32_t *outdeg = nullptr, *indeg = nullptr;
+  DegTop top;                     // DegreeRanking top-20 per view (degree runs)
+  unsigned long long* h_top = nullptr;  // pinned copy: [64][kTop] keys | [64][kTop] ranks, out-degrees (int32)
   double *pr = nullptr, *contrib[2] = {nullptr, nullptr};
   int32_t *pcnt = nullptr, *psnbr = nullptr;
   uint64_t* psmask = nullptr;
@@ -174,6 +176,7 @@ struct rgpu_ctx {
   bool sealed = false;
   size_t n_sealed = 0;                  // events[0, n_sealed) are in the resident graph
   bool delta_on = true;                 // RGPU_DELTA: merge later updates into it (else re-pack)
+  int vertex_order = RGPU_ORDER_LOCALITY;  // rgpu_set_vertex_order: local rank order of a full seal
   Packed pk;
   DevGraph g;
   std::vector<void*> graph_allocs;
@@ -214,6 +217,8 @@ struct rgpu_ctx {
   std::vector<int32_t> vlast;           // per view: last superstep in which one of its labels changed
   unsigned long long* d_ecnt = nullptr; // profile runs: alive edges per view (K1 edge masks)
   std::vector<int64_t> deg;  // [view][3]
+  struct TopEnt { int64_t id; int32_t out, in; };
+  std::vector<TopEnt> degtop;  // [view][kTop] (id -1: none)
   std::vector<int64_t> dcount, dsteps;  // diffusion: infected vertices, supersteps per view
   int64_t diff_seed = 31;               // BinaryDefusion.infectedNode (BinaryDefusion.scala:10)
   uint64_t diff_coin_seed = 0;
@@ -287,6 +292,7 @@ void release_slots(rgpu_ctx* c) {
     if (s.h_tail) (void)hipHostFree(s.h_tail);
     if (s.h_stats) (void)hipHostFree(s.h_stats);
     if (s.h_work) (void)hipHostFree(s.h_work);
+    if (s.h_top) (void)hipHostFree(s.h_top);
     if (s.ev) (void)hipEventDestroy(s.ev);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot();
@@ -444,7 +450,7 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       s.lab[1] = dalloc<int32_t>(L, rows + kPad * kViews);
       s.uw[0] = dalloc<int32_t>(L, nv + kPad);
       s.uw[1] = dalloc<int32_t>(L, nv + kPad);
-      if (use_uw(c) && !c->partitioned) {  // (partitioned: counts go to the label owner, xchg.hip)
+      if (use_uw(c) || c->partitioned) {  // component counts at the root's row (zero between batches)
         s.counts = dalloc<int32_t>(L, rows + kPad * kViews);
         HIPCHK(hipMemset(s.counts, 0, sizeof(int32_t) * (rows + kPad * kViews)));
       }
@@ -469,6 +475,15 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
     if ((algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) && !s.a_deg) {
       s.outdeg = dalloc<int32_t>(L, rows);
       s.indeg = dalloc<int32_t>(L, rows);
+    }
+    if (algo == RGPU_ALGO_DEGREE && !s.top.key) {
+      const size_t nc = (size_t)deg_top_waves(nv) * kViews * kTop;
+      s.top.cand_key = dalloc<uint64_t>(L, nc);
+      s.top.cand_pos = dalloc<int32_t>(L, nc);
+      s.top.key = dalloc<unsigned long long>(L, kViews * kTop);
+      s.top.pos = dalloc<int32_t>(L, kViews * kTop);
+      s.top.out = dalloc<int32_t>(L, kViews * kTop);
+      HIPCHK(hipHostMalloc((void**)&s.h_top, sizeof(unsigned long long) * kViews * kTop * 2));
     }
     if (algo == RGPU_ALGO_PR && !s.h_pr && c->g.n_seg > 0) {
       s.hv.pacc = dalloc<double>(LG, (size_t)c->g.n_heavy * kViews);  // zero between uses
@@ -629,6 +644,14 @@ void finish_tail(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (rc.algo == RGPU_ALGO_CC) launch_lane_fold(s.stream, s.stats + kLaneOff, s.stats + kFoldOff);
   HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatCopy,
                         hipMemcpyDeviceToHost, s.stream));
+  if (rc.algo == RGPU_ALGO_DEGREE) {  // the top-20 lists
+    HIPCHK(hipMemcpyAsync(s.h_top, s.top.key, sizeof(unsigned long long) * kViews * kTop, hipMemcpyDeviceToHost,
+                          s.stream));
+    int32_t* hp = reinterpret_cast<int32_t*>(s.h_top + kViews * kTop);
+    HIPCHK(hipMemcpyAsync(hp, s.top.pos, sizeof(int32_t) * kViews * kTop, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipMemcpyAsync(hp + kViews * kTop, s.top.out, sizeof(int32_t) * kViews * kTop, hipMemcpyDeviceToHost,
+                          s.stream));
+  }
   if (rc.flags & RGPU_RUN_RETAIN) {
     Retained& R = c->kept[s.batch];
     const size_t rows = (size_t)g.nv * kViews;
@@ -669,7 +692,8 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
     const int nviews = rc.K * rc.gsize;
     if (c->check)
       run_check(s.stream, "final labels", [&](unsigned long long* bad) {
-        launch_check_labels(s.stream, g.nv, s.vm, use_uw(c) ? s.uw[s.r_final & 1] : nullptr, lab, bad);
+        launch_check_labels(s.stream, c->partitioned ? c->pk.n_own : g.nv, s.vm, use_uw(c) ? s.uw[s.r_final & 1] : nullptr,
+                            lab, bad, g.grank);
       });
     if (use_uw(c) && !c->partitioned) {
       const int32_t* uw = s.uw[s.r_final & 1];
@@ -678,7 +702,7 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
                    [&] { launch_cc_count(s.stream, g.nv, nviews, s.vm, s.vadj, uw, lab, s.counts, s.iso); });
       timed_launch(c, si, KID_SUMMARY, 20.0 * g.nv,
                    [&] { launch_cc_roots(s.stream, g.nv, nviews, s.vm, s.vadj, uw, lab, s.counts, s.stats, s.iso,
-                                           s.r_final >= 1 && s.r_final >= rc.max_steps); });
+                                           s.r_final >= 1 && s.r_final >= rc.max_steps, g.grank); });
       finish_tail(c, si, rc);
       return;
     }
@@ -845,7 +869,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
         launch_check_slots(s.stream, gk.nv, g.adj_off, s.vm, s.cnt, s.snbr, use_uw(c) ? s.uw[0] : nullptr,
-                           use_uw(c) ? s.uw[1] : nullptr, bad);
+                           use_uw(c) ? s.uw[1] : nullptr, bad, g.grank);
       });
     if (g.n_seg > 0 && !c->partitioned)  // partitioned: after the step's records are in
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
@@ -868,7 +892,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     }
   } else {
     timed_launch(c, si, KID_DEGREE, g.nv * (8.0 + 32.0 + 512.0) + (double)(g.ne + g.n_in) * 12.0, [&] {
-      launch_degree(s.stream, g, s.vm, s.em, s.outdeg, s.indeg, s.stats);
+      launch_degree(s.stream, g, s.vm, s.em, s.outdeg, s.indeg, s.stats,
+                    rc.algo == RGPU_ALGO_DEGREE ? &s.top : nullptr);
     });
     if (rc.algo == RGPU_ALGO_PR) {
       timed_launch(c, si, KID_SLOTS, g.nv * (8.0 + 24.0 + 256.0 + 1024.0) + (double)(g.n_in) * 24.0, [&] {
@@ -885,6 +910,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     finish_batch(c, si, rc);
   }
 }
+
+int64_t label_id(const rgpu_ctx* c, int32_t l);
 
 void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
   Slot& s = c->slot[si];
@@ -912,6 +939,15 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
         c->vlast[view] = last[j];
       } else if (rc.algo == RGPU_ALGO_DEGREE) {
         for (int f = 0; f < 3; f++) c->deg[view * 3 + f] = (int64_t)h[f * kViews + j];
+        const int32_t* hp = reinterpret_cast<const int32_t*>(s.h_top + kViews * kTop);
+        for (int i = 0; i < kTop; i++) {
+          const unsigned long long key = s.h_top[j * kTop + i];
+          rgpu_ctx::TopEnt& e = c->degtop[view * kTop + i];
+          if (key == 0) { e = {-1, 0, 0}; continue; }
+          e.id = label_id(c, (int32_t)~(uint32_t)(key & 0xffffffffull));
+          e.in = (int32_t)(key >> 32);
+          e.out = hp[kViews * kTop + j * kTop + i];
+        }
       } else if (rc.algo == RGPU_ALGO_DIFFUSION) {
         c->dcount[view] = (int64_t)h[j];
         c->dsteps[view] = s.r_final;
@@ -927,9 +963,10 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
     // (4 B) and 64-B row lines written.  Supersteps r >= 2: frontier flag read + flag cleared
     // two steps ahead (2 B per vertex; a tail-kernel step reads none); per visited vertex vm,
     // cnt, adj_off, own change and uniform words in, change word out (40 B); per kept slot of
-    // a visited vertex nbr + mask + the neighbour's change word (20 B); per slot whose
-    // neighbour changed its uniform word (4 B); per label lane gathered from a mixed row 4 B;
-    // own row lines read and row lines written (64 B each); uniform words written (4 B).
+    // a visited vertex nbr + mask (12 B) and the neighbour's uniform word (4 B; without uniform
+    // words its change word, 8 B); per slot of a mixed neighbour its change word (8 B); per
+    // label lane gathered from a mixed row 4 B; own row lines read and row lines written (64 B
+    // each); uniform words written (4 B).
     if (c->profile) {
       auto wsum = [&](int r, int f) {
         unsigned long long t = 0;
@@ -942,10 +979,11 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
                                          (c->g.ts_e ? 32.0 : 24.0) * (double)wsum(1, 4) + 12.0 * (double)wsum(1, 1) +
                                          4.0 * (double)wsum(1, 7) + 64.0 * (double)wsum(1, 6);
       }
+      const double per_slot = use_uw(c) ? 16.0 : 20.0;
       for (int r = 2; r <= s.r_final; r++)
         c->st.kernel_bytes[s.by_tail[r] ? KID_TAIL : KID_STEP] +=
-            (s.by_tail[r] ? 0.0 : 2.0 * c->g.nv) + 40.0 * (double)wsum(r, 0) + 20.0 * (double)wsum(r, 1) +
-            4.0 * (double)wsum(r, 4) + 4.0 * (double)wsum(r, 3) + 64.0 * (double)(wsum(r, 5) + wsum(r, 6)) +
+            (s.by_tail[r] ? 0.0 : 2.0 * c->g.nv) + 40.0 * (double)wsum(r, 0) + per_slot * (double)wsum(r, 1) +
+            8.0 * (double)wsum(r, 4) + 4.0 * (double)wsum(r, 3) + 64.0 * (double)(wsum(r, 5) + wsum(r, 6)) +
             4.0 * (double)wsum(r, 7);
       if (!c->trace_path.empty())
         for (int r = 1; r <= s.r_final; r++)
@@ -1293,9 +1331,9 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   part_post_step(c, si, rc, n);
 }
 
-// component counts: label -> count of owned members, the labels owned elsewhere routed to their
-// owner as records (k_hist_route); their counts travel, the host picks the slot up in
-// part_finish_end
+// component counts: label -> count of owned members at the label's count row when the label is
+// owned here, the others routed to their owner as records (k_part_count); their counts travel,
+// the host picks the slot up in part_finish_end
 void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc) {
   Slot& s = c->slot[si];
   Part& X = c->pt;
@@ -1303,19 +1341,18 @@ void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc) {
   const int P = c->nparts;
   const int nviews = rc.K * rc.gsize;
   const int64_t no = c->pk.n_own;
-  if (!xs.hsbuf) {  // first guess: one record per owned vertex and peer
+  if (!xs.hsbuf) {  // first guess: 1/16 record per owned vertex and peer (the LDS cache folds most)
     int64_t need[kMaxParts];
-    for (int q = 0; q < P; q++) need[q] = no;
+    for (int q = 0; q < P; q++) need[q] = no / 16;
     grow_regions(&xs.hsbuf, xs.hscap, need, P, s.stream);
   }
-  if (use_uw(c))  // the owned uniform rows written out for the label owners' counts (and retained rows)
-    launch_uw_rows(s.stream, no, s.vm, s.uw[s.r_final & 1], s.lab[s.r_final & 1]);
-  int32_t* hist = s.lab[(s.r_final + 1) & 1];  // the free label buffer: [view][owned rank]
-  HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)no * kViews, s.stream));
+  const int32_t* uw = use_uw(c) ? s.uw[s.r_final & 1] : nullptr;
+  if (uw && (rc.flags & RGPU_RUN_RETAIN))  // full rows of the owned vertices for the host
+    launch_uw_rows(s.stream, no, s.vm, uw, s.lab[s.r_final & 1]);
   const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);
-  timed_launch(c, si, KID_HIST, 12.0 * no, [&] {
-    launch_hist_route(s.stream, false, L, X.own, nviews, s.vm, s.vadj, s.lab[s.r_final & 1], hist, s.iso, xs.htot,
-                      xs.hsbuf);
+  timed_launch(c, si, KID_HIST, 28.0 * no, [&] {
+    launch_part_count(s.stream, false, L, X.own, nviews, s.vm, s.vadj, uw, s.lab[s.r_final & 1], s.counts, s.iso,
+                      xs.htot, xs.hsbuf);
   });
   launch_xcounts(s.stream, P, c->part, xs.htot, nullptr, xs.xab);
   HIPCHK(hipGetLastError());
@@ -1339,12 +1376,20 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
     recv[q] = q == me ? 0 : xs.h_xab[2 * P + 2 * q];
     over |= sent[q] > xs.hscap[q];
   }
-  int32_t* hist = s.lab[(s.r_final + 1) & 1];
-  if (over) {  // the records again into a larger buffer (the local counts are done)
+  const int32_t* uw = use_uw(c) ? s.uw[s.r_final & 1] : nullptr;
+  if (over) {  // the records again into a larger buffer (the local counts are done); the LDS cache
+               // may fold them differently, but the sums per (label, view) are the same
+    HIPCHK(hipMemsetAsync(xs.htot, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
     grow_regions(&xs.hsbuf, xs.hscap, sent, P, s.stream);
     const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);
-    launch_hist_route(s.stream, true, L, X.own, nviews, s.vm, s.vadj, s.lab[s.r_final & 1], hist, s.iso, xs.htot,
-                      xs.hsbuf);
+    launch_part_count(s.stream, true, L, X.own, nviews, s.vm, s.vadj, uw, s.lab[s.r_final & 1], s.counts, s.iso,
+                      xs.htot, xs.hsbuf);
+    HIPCHK(hipMemcpyAsync(xs.h_xab, xs.htot, sizeof(int64_t) * P, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+    for (int q = 0; q < P; q++)
+      if (q != me && xs.h_xab[q] != sent[q])
+        throw HipFail{"component-count records: second pass sent " + std::to_string(xs.h_xab[q]) + " to peer " +
+                      std::to_string(q) + ", the counts exchange announced " + std::to_string(sent[q])};
     HIPCHK(hipMemsetAsync(xs.htot, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
   }
   grow_regions(&xs.hrbuf, xs.hrcap, recv, P, s.stream);
@@ -1362,9 +1407,12 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
     }
     xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
   }
-  launch_hist_recv(s.stream, peers_layout(c, xs.hrcap, X.xr_off, recv), xs.hrbuf, X.own, hist);
-  const DevGraph go = owned_view(c);
-  timed_launch(c, si, KID_SUMMARY, 8.0 * no * nviews, [&] { launch_cc_summary(s.stream, go, nviews, hist, s.stats, s.iso); });
+  launch_hist_recv(s.stream, peers_layout(c, xs.hrcap, X.xr_off, recv), xs.hrbuf, X.own, s.counts);
+  // roots: every owned member whose label is its own id reads (and zeroes) its count row
+  timed_launch(c, si, KID_SUMMARY, 20.0 * no, [&] {
+    launch_cc_roots(s.stream, no, nviews, s.vm, s.vadj, uw, s.lab[s.r_final & 1], s.counts, s.stats, s.iso,
+                    s.r_final >= 1 && s.r_final >= rc.max_steps, c->g.grank, true);
+  });
   // processBatchWindowResults merges the shards: biggest = max, the other fields add up
   xs.x->allreduce_u64(s.stats, kViews, true, s.stream);
   xs.x->allreduce_u64(s.stats + kViews, 5 * kViews, false, s.stream);
@@ -1473,7 +1521,7 @@ int run_partitioned_dp(rgpu_ctx* c, RunCfg& rc) {
                  [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0); });
     part_vm_exchange(c, 0, s.vm, 0, 1);
     timed_launch(c, 0, KID_DEGREE, go.nv * (8.0 + 32.0 + 512.0) + (double)(g.ne + g.n_in) * 12.0, [&] {
-      launch_degree(s.stream, go, s.vm, s.em, s.outdeg, s.indeg, s.stats);
+      launch_degree(s.stream, go, s.vm, s.em, s.outdeg, s.indeg, s.stats, rc.algo == RGPU_ALGO_DEGREE ? &s.top : nullptr);
     });
     if (rc.algo == RGPU_ALGO_PR) {
       timed_launch(c, 0, KID_SLOTS, go.nv * (8.0 + 24.0 + 256.0 + 1024.0) + (double)(g.n_in) * 24.0, [&] {
@@ -1522,6 +1570,15 @@ void finish_supersteps(rgpu_ctx* c, const RunCfg& rc) {
     for (int w = 0; w < rc.W; w++) c->cc[hop * rc.W + w].supersteps = steps;
   }
 }
+
+// id of the vertex whose label is l: partitioned, labels are ids; else id ranks
+int64_t label_id(const rgpu_ctx* c, int32_t l) {
+  if (c->partitioned) return (int64_t)l;
+  return c->pk.lid.empty() ? c->pk.vid[l] : c->pk.lid[l];
+}
+
+// the k-th owned vertex in ascending id order (result lists are ascending by id)
+int64_t own_at(const rgpu_ctx* c, int64_t k) { return c->pk.by_id.empty() ? k : (int64_t)c->pk.by_id[k]; }
 
 // After a failed run (a HIP / RCCL / exchange error or a failed allocation mid-run): the slots may
 // hold a batch in any phase, and the per-batch state that only a batch's last kernels bring back
@@ -1958,7 +2015,8 @@ int rgpu_seal(rgpu_ctx* c) {
     c->sealed = false;
     c->st.seal_incremental = 0;
     c->st.seal_delta_updates = 0;
-    if (c->delta_on && !c->partitioned && c->n_sealed > 0 && c->g.nv > 0) {
+    // (a locality-ordered base has no monotone rank maps to merge into: it is re-packed)
+    if (c->delta_on && !c->partitioned && c->n_sealed > 0 && c->g.nv > 0 && !c->pk.relabeled) {
       // live ingest: merge the delta into the resident graph
       seal_delta(c);
       c->st.seal_incremental = 1;
@@ -1970,7 +2028,7 @@ int rgpu_seal(rgpu_ctx* c) {
       c->st.seal_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       return RGPU_OK;
     }
-    std::string e = pack_events(c->events, c->part, c->nparts, &c->pk);
+    std::string e = pack_events(c->events, c->part, c->nparts, &c->pk, c->vertex_order == RGPU_ORDER_LOCALITY);
     if (!e.empty()) return fail(c, RGPU_EINVAL, e);
     free_graph(c);
     const Packed& P = c->pk;
@@ -1995,12 +2053,11 @@ int rgpu_seal(rgpu_ctx* c) {
     g.n_own = P.n_own;
     build_heavy(c, g, L, P.out_off, P.in_off);
     build_tslots(c, g, L);
+    if (!c->partitioned && !P.grank.empty()) g.grank = dupload(L, P.grank);  // locality order: labels are id ranks
     if (c->partitioned) {  // CC labels are vertex ids (the label owner routes component counts)
       if (c->nparts > kMaxParts) return fail(c, RGPU_EINVAL, "more than 8 partitions");
-      if (P.grank.empty())
-        g.grank = dupload(L, std::vector<int32_t>(P.vid.begin(), P.vid.end()));
-      else
-        g.grank = dupload(L, P.grank);
+      // (also with P = 1, where a relabeled pack's grank holds id ranks)
+      g.grank = dupload(L, std::vector<int32_t>(P.vid.begin(), P.vid.end()));
       Part& X = c->pt;
       X.nxs = (int64_t)P.xs_v.size();
       X.nxr = (int64_t)P.xr_v.size();
@@ -2012,15 +2069,19 @@ int rgpu_seal(rgpu_ctx* c) {
       X.xr_q = dupload(L, P.xr_q);
       X.xs_off_d = dupload(L, P.xs_off);
       X.xr_off_d = dupload(L, P.xr_off);
-      {  // owned ids ascend with rank: bucket b = id >> shift, about one id per bucket
+      {  // owned ids ascending (index = the count-table row of the label): bucket b = id >> shift,
+         // about one id per bucket
+        std::vector<int64_t> ids((size_t)P.n_own);
+        for (int64_t k = 0; k < P.n_own; k++) ids[k] = P.vid[P.by_id.empty() ? k : P.by_id[k]];
         int lg = 0;
         while (((int64_t)1 << lg) < std::max<int64_t>(P.n_own, 1)) lg++;
         const int shift = std::max(0, 31 - lg);
         const int64_t nbk = ((int64_t)1 << 31) >> shift;
         std::vector<int32_t> boff(nbk + 1, 0);
-        for (int64_t v = 0; v < P.n_own; v++) boff[(P.vid[v] >> shift) + 1]++;
+        for (int64_t k = 0; k < P.n_own; k++) boff[(ids[k] >> shift) + 1]++;
         for (int64_t b = 0; b < nbk; b++) boff[b + 1] += boff[b];
-        X.own.vid = dupload(L, std::vector<int64_t>(P.vid.begin(), P.vid.begin() + P.n_own));
+        X.own.vid = dupload(L, ids);
+        X.own.pos = P.by_id.empty() ? nullptr : dupload(L, P.by_id);
         X.own.boff = dupload(L, boff);
         X.own.shift = shift;
         X.own.n_own = P.n_own;
@@ -2040,6 +2101,14 @@ int rgpu_seal(rgpu_ctx* c) {
     return fail(c, RGPU_ENOMEM, "host allocation failed");
   }
   c->st.seal_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return RGPU_OK;
+}
+
+int rgpu_set_vertex_order(rgpu_ctx* c, int order) {
+  if (!c) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (order != RGPU_ORDER_LOCALITY && order != RGPU_ORDER_ID) return fail(c, RGPU_EINVAL, "unknown vertex order");
+  c->vertex_order = order;
   return RGPU_OK;
 }
 
@@ -2162,13 +2231,18 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
       HIPCHK(hipMemset(c->d_ecnt, 0, sizeof(unsigned long long) * n_hops * rc.W));
     }
     c->deg.assign(algo == RGPU_ALGO_DEGREE ? n_hops * rc.W * 3 : 0, 0);
+    c->degtop.assign(algo == RGPU_ALGO_DEGREE ? n_hops * rc.W * kTop : 0, rgpu_ctx::TopEnt{-1, 0, 0});
     c->dcount.assign(algo == RGPU_ALGO_DIFFUSION ? n_hops * rc.W : 0, 0);
     c->dsteps.assign(algo == RGPU_ALGO_DIFFUSION ? n_hops * rc.W : 0, 0);
     if (algo == RGPU_ALGO_DIFFUSION) {
-      // ids ascend with rank: the seed's rank by binary search (-1: not in the graph)
+      // the seed's rank by binary search over the ids in ascending order (-1: not in the graph)
       const auto& vid = c->pk.vid;
-      auto it = std::lower_bound(vid.begin(), vid.begin() + c->g.nv, c->diff_seed);
-      c->diff_seed_rank = (it != vid.begin() + c->g.nv && *it == c->diff_seed) ? (int64_t)(it - vid.begin()) : -1;
+      int64_t a = 0, b = c->pk.n_own;
+      while (a < b) {
+        const int64_t m = (a + b) / 2;
+        if (vid[own_at(c, m)] < c->diff_seed) a = m + 1; else b = m;
+      }
+      c->diff_seed_rank = (a < c->pk.n_own && vid[own_at(c, a)] == c->diff_seed) ? own_at(c, a) : -1;
       if (c->g.nv) HIPCHK(hipMemcpy(c->d_vid, vid.data(), sizeof(int64_t) * c->g.nv, hipMemcpyHostToDevice));
     }
     c->kept.clear();
@@ -2252,10 +2326,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   return RGPU_OK;
 }
 
-// id of the vertex whose global rank is l (CC labels are global ranks)
-static int64_t label_id(const rgpu_ctx* c, int32_t l) {
-  return c->partitioned ? (int64_t)l : c->pk.vid[l];  // partitioned: labels are ids
-}
+
 
 static int view_index(rgpu_ctx* c, size_t hop, size_t win, size_t* batch, int* lane) {
   if (hop >= c->n_hops || win >= (size_t)c->W) return fail(c, RGPU_EINVAL, "view index out of range");
@@ -2285,7 +2356,8 @@ int rgpu_cc_vertex_labels(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
   size_t k = 0;
-  for (int64_t v = 0; v < c->pk.n_own; v++) {
+  for (int64_t k_ = 0; k_ < c->pk.n_own; k_++) {
+    const int64_t v = own_at(c, k_);
     if (!((R.vm[v] >> j) & 1)) continue;
     if (k < cap) {
       ids[k] = c->pk.vid[v];
@@ -2307,7 +2379,7 @@ int rgpu_cc_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* labels, int32_t
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
   std::vector<int32_t> lab;
-  for (int64_t v = 0; v < c->pk.n_own; v++)
+  for (int64_t v = 0; v < c->pk.n_own; v++)  // (any order: sorted below)
     if ((R.vm[v] >> j) & 1) lab.push_back(R.a[(size_t)v * kViews + j]);
   std::sort(lab.begin(), lab.end());
   size_t k = 0;
@@ -2332,7 +2404,8 @@ int rgpu_degree_vertex(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int32_
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
   size_t k = 0;
-  for (int64_t v = 0; v < c->pk.n_own; v++) {
+  for (int64_t k_ = 0; k_ < c->pk.n_own; k_++) {
+    const int64_t v = own_at(c, k_);
     if (!((R.vm[v] >> j) & 1)) continue;
     if (k < cap) {
       ids[k] = c->pk.vid[v];
@@ -2354,25 +2427,12 @@ int rgpu_degree_result(rgpu_ctx* c, size_t hop, size_t win, int64_t tot[3], int6
   int j;
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   for (int f = 0; f < 3; f++) tot[f] = c->deg[(hop * c->W + win) * 3 + f];
-  if (top_id && top_out && top_in) {
-    for (int i = 0; i < 20; i++) { top_id[i] = -1; top_out[i] = 0; top_in[i] = 0; }
-    if (c->retained) {
-      const Retained& R = c->kept[b];
-      std::vector<int64_t> vs;
-      for (int64_t v = 0; v < c->pk.n_own; v++)
-        if ((R.vm[v] >> j) & 1) vs.push_back(v);
-      // DegreeBasic sorts by in-degree descending (:26); ParTrieMap tie order is not
-      // deterministic, ties here go by ascending id
-      auto key = [&](int64_t v) { return R.b[(size_t)v * kViews + j]; };
-      size_t m = std::min<size_t>(20, vs.size());
-      std::partial_sort(vs.begin(), vs.begin() + m, vs.end(), [&](int64_t x, int64_t y) {
-        return key(x) != key(y) ? key(x) > key(y) : x < y;
-      });
-      for (size_t i = 0; i < m; i++) {
-        top_id[i] = c->pk.vid[vs[i]];
-        top_out[i] = R.a[(size_t)vs[i] * kViews + j];
-        top_in[i] = R.b[(size_t)vs[i] * kViews + j];
-      }
+  if (top_id && top_out && top_in) {  // the device top-20 (k_deg_top_merge), ties by ascending id
+    for (int i = 0; i < kTop; i++) {
+      const rgpu_ctx::TopEnt& e = c->degtop[(hop * c->W + win) * kTop + i];
+      top_id[i] = e.id;
+      top_out[i] = e.id < 0 ? 0 : e.out;
+      top_in[i] = e.id < 0 ? 0 : e.in;
     }
   }
   return RGPU_OK;
@@ -2388,7 +2448,8 @@ int rgpu_pr_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, double* pr
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
   size_t k = 0;
-  for (int64_t v = 0; v < c->pk.n_own; v++) {
+  for (int64_t k_ = 0; k_ < c->pk.n_own; k_++) {
+    const int64_t v = own_at(c, k_);
     if (!((R.vm[v] >> j) & 1)) continue;
     if (k < cap) { ids[k] = c->pk.vid[v]; pr[k] = R.pr[(size_t)v * kViews + j]; }
     k++;
@@ -2429,7 +2490,8 @@ int rgpu_diffusion_vertex(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
   size_t k = 0;
-  for (int64_t v = 0; v < c->pk.n_own; v++) {
+  for (int64_t k_ = 0; k_ < c->pk.n_own; k_++) {
+    const int64_t v = own_at(c, k_);
     const uint8_t r = R.st[(size_t)v * kViews + j];
     if (r == 0xFF) continue;  // returnResults keeps infected vertices only (:43-49)
     if (k < cap) { ids[k] = c->pk.vid[v]; steps[k] = r; }

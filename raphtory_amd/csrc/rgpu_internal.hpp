@@ -29,7 +29,13 @@ struct Packed {
   // ---- vertex partitioning (num_partitions > 1); identity when P = 1
   int part = 0, nparts = 1;
   int64_t n_own = 0;                 // ranks [0, n_own) are owned here, [n_own, nv) are ghosts
-  std::vector<int32_t> grank;        // [nv] CC label of each local rank = its vertex id (P > 1)
+  // ---- local rank order (pack_events `locality`): ranks are ids ascending, or (relabeled) a
+  // locality order: vertices by activity, most active first
+  bool relabeled = false;
+  std::vector<int64_t> lid;          // P = 1 relabeled: id of label l (labels are id ranks)
+  std::vector<int32_t> by_id;        // relabeled: owned local ranks in ascending id order
+  std::vector<int32_t> grank;        // [nv] CC label of each local rank: its vertex id (P > 1) or
+                                     // its id rank (P = 1 relabeled); empty: the rank itself
   std::vector<uint8_t> lowner;       // [nv] owning partition of each local rank (P > 1)
   // exchange plan: per peer q, owned ranks that are ghosts on q (xs) and ghosts owned by q
   // (xr), both ascending by id, so q's xr list for this partition equals this xs list for q
@@ -62,8 +68,11 @@ struct Event {
 };
 
 // Host packer (packer.cpp).  Returns empty string or an error message.
+// locality = true: local ranks in locality order (Packed.relabeled); false: ids ascending
 std::string pack_events(const std::vector<Event>& ev, int partition, int num_partitions,
-                        Packed* out);
+                        Packed* out, bool locality = false);
+// locality order of n vertices from their activity: position -> index in [0, n)
+std::vector<int32_t> locality_order(const std::vector<int32_t>& act, int nt);
 
 // Incremental seal (live ingest), host half.  Updates ev[first, n)
 // arrive after a sealed one-partition base; every one of them comes later in stream order

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
       const int32_t vL = __builtin_amdgcn_readlane(v, L);
       const int qL = __builtin_amdgcn_readlane(q, L);
       uint64_t mm = rl64(m, L);
-      const int32_t uL = uw ? uw[vL] : -1;  // a uniform row is its word (kernels.hip kMixed = -1)
+      const int32_t uL = uw ? uw_label(uw[vL]) : -1;  // a uniform row is its word (kernels.hip kMixed = -1)
       const int32_t x = uL != -1 ? uL : lab[(int64_t)vL * 64 + lane];
       int n = 0;
       while (mm) {
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
       const int qL = __builtin_amdgcn_readlane(q, L);
       const int32_t eL = (int32_t)(c * 64 + L - P.xoff[qL]);
       uint64_t mm = rl64(m, L);
-      const int32_t uL = uw ? uw[vL] : -1;
+      const int32_t uL = uw ? uw_label(uw[vL]) : -1;
       const int32_t x = uL != -1 ? uL : lab[(int64_t)vL * 64 + lane];
       while (mm) {
         const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __res
       }
     }
     if (l16 == 0) {
-      if (uw) uw[g] = uni ? val : -1;
+      if (uw) uw[g] = uni ? uw_word(val, true) : -1;  // the ghost changed in this step (kChgFlag)
       atomicOr((unsigned long long*)&chg[g], (unsigned long long)r.mask);
       if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // the ghost changed (ChgBits)
     }
@@ -257,125 +257,156 @@ __global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict_
 
 // ------------------------------------------------------------------ component counts
 // Label -> count of the partition's owned members (ConnectedComponents.returnResults :37-42)
-// routed to the label's owner: as k_cc_hist, a block stages 64 vertices' label rows and its
-// eight waves dedup each view's labels (after `rounds` labels, one entry per lane).  Counts of
-// labels owned here go straight into hist[view][owned rank]; the others become records
-// (label | view << 31 | count << 37), staged per peer in LDS and flushed after every chunk with
-// one atomicAdd per (block, peer).  Members with no kept slot are islands, counted in iso.
-constexpr int kStage = 256;  // staged records per peer and chunk (more: written directly)
+// Component counts, partitioned (ConnectedComponents.returnResults :37-42 merged by
+// processBatchWindowResults :137): as kernels.hip k_cc_count, from the owned members' uniform
+// words (a group of uniform members with the same (label, views) is one row-wide add) or rows
+// (mixed members, lane = view), through a 64-row LDS cache keyed by label.  A label owned here is
+// counted at its count row (the label vertex's local rank, through OwnIdx); any other label
+// becomes records (label | view << 31 | count << 37) for its owner — the cache turns the giant
+// component of a block into one record per view.  Records are reserved per (wave | block, peer)
+// with one atomicAdd; gcnt[q] counts every record for peer q (past the capacity too, so the host
+// sees an overflow and runs the REMOTE_ONLY pass again into a larger buffer).  Members with no
+// kept slot in a view are islands (iso[shard][view]).
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int d) {
+  const uint32_t lo = __shfl_xor((uint32_t)x, d), hi = __shfl_xor((uint32_t)(x >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane) {  // (kernels.hip)
+  const uint64_t M[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                         0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const int d = 32 >> k;
+    const uint64_t y = shfl_xor64(x, d);
+    x = (lane & d) ? ((x & ~M[k]) | ((y & ~M[k]) >> d)) : ((x & M[k]) | ((y & M[k]) << d));
+  }
+  return x;
+}
+// count row (local rank) of owned label x
+__device__ __forceinline__ int64_t label_row(const OwnIdx& I, int32_t x) {
+  const int64_t k = owned_rank(I, x);
+  return k < 0 ? -1 : (I.pos ? (int64_t)I.pos[k] : k);
+}
+__device__ __forceinline__ unsigned long long count_rec(int32_t x, int j, unsigned c) {
+  return (unsigned long long)(uint32_t)x | ((unsigned long long)j << 31) | ((unsigned long long)c << 37);
+}
+// wave-wide: the lanes with `on` send (x, j, c) (remote labels) or add it (owned labels)
 template <bool REMOTE_ONLY>
-__global__ __launch_bounds__(512) void k_hist_route(XPeers P, OwnIdx I, int nviews,
-                                                    const uint64_t* __restrict__ vm,
-                                                    const uint64_t* __restrict__ vadj,
-                                                    const int32_t* __restrict__ lab, int32_t* __restrict__ hist,
-                                                    unsigned int* __restrict__ iso_g, int rounds,
+__device__ __forceinline__ void count_direct(bool on, int32_t x, int j, unsigned c, const XPeers& P, const OwnIdx& I,
+                                             int32_t* __restrict__ counts, unsigned long long* __restrict__ gcnt,
+                                             unsigned long long* __restrict__ hsbuf, int lane) {
+  const int q = on ? owner_of(x, P.np) : -1;
+  if (!REMOTE_ONLY && q == P.me) {
+    const int64_t r = label_row(I, x);  // always found: a label is a member's id
+    if (r >= 0) atomicAdd(&counts[r * 64 + j], (int32_t)c);
+  }
+  for (uint64_t todo = __ballot(q >= 0 && q != P.me); todo;) {
+    const int qL = __builtin_amdgcn_readlane(q, __builtin_ctzll(todo));
+    const uint64_t mine = __ballot(q == qL);
+    todo &= ~mine;
+    unsigned long long base = 0;
+    if (lane == __builtin_ctzll(mine)) base = atomicAdd(&gcnt[qL], (unsigned long long)__popcll(mine));
+    base = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(base >> 32), __builtin_ctzll(mine)) << 32) |
+           __builtin_amdgcn_readlane((uint32_t)base, __builtin_ctzll(mine));
+    if (q == qL) {
+      const unsigned long long pos = base + __popcll(mine & (lane ? (~0ull >> (64 - lane)) : 0ull));
+      if (pos < (unsigned long long)P.cap[qL]) hsbuf[P.base[qL] + (int64_t)pos] = count_rec(x, j, c);
+    }
+  }
+}
+template <bool REMOTE_ONLY>
+__global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t vmask, const uint64_t* __restrict__ vm,
+                                                    const uint64_t* __restrict__ vadj, const int32_t* __restrict__ uw,
+                                                    const int32_t* __restrict__ lab, int32_t* __restrict__ counts,
+                                                    unsigned int* __restrict__ iso_g,
                                                     unsigned long long* __restrict__ gcnt,
                                                     unsigned long long* __restrict__ hsbuf) {
-  __shared__ int32_t tile[64][65];
+  // The cache is private to a wave (16 rows each): a wave's operations run in a fixed order, so
+  // the records it emits are the same on every run — the REMOTE_ONLY pass after a send-buffer
+  // overflow must emit exactly the records the counts exchange announced.
+  constexpr int kRows = 16;
   __shared__ unsigned int iso[64];
-  __shared__ unsigned long long stage[kMaxParts][kStage];
-  __shared__ unsigned int pc[kMaxParts];
-  __shared__ unsigned long long fb[kMaxParts];
-  const int64_t n_own = I.n_own;
+  __shared__ int32_t ckey_s[4][kRows];
+  __shared__ unsigned int crow_s[4][kRows][64];
   const int lane = lane_of(), wib = threadIdx.x >> 6;
+  int32_t* ckey = ckey_s[wib];
+  unsigned int (*crow)[64] = crow_s[wib];
   if (threadIdx.x < 64) iso[threadIdx.x] = 0;
-  if (threadIdx.x < kMaxParts) pc[threadIdx.x] = 0;
-  const uint64_t vmask = (nviews >= 64 ? ~0ull : ((1ull << nviews) - 1)) & (0x0101010101010101ull << wib);
+  if (lane < kRows) ckey[lane] = -1;
+  for (int h = 0; h < kRows; h++) crow[h][lane] = 0;
   __syncthreads();
-  auto emit = [&](int32_t L, int j, unsigned int c, bool on) {  // per lane
-    if (!on) return;
-    const int q = owner_of(L, P.np);
-    if (q == P.me) {
-      if (!REMOTE_ONLY) {
-        const int64_t rk = owned_rank(I, L);  // always found: a label is a member's id
-        if (rk >= 0) atomicAdd(&hist[(int64_t)j * n_own + rk], (int32_t)c);
+  auto cached = [&](int32_t x, int j, unsigned c) -> bool {  // per lane
+    const int h0 = (int)(((uint32_t)x * 2654435761u) >> 28);
+    for (int p = 0; p < 4; p++) {
+      const int h = (h0 + p) & (kRows - 1);
+      int32_t k = ckey[h];
+      if (k == -1) {
+        k = atomicCAS(&ckey[h], -1, x);
+        if (k == -1) k = x;
       }
-      return;
+      if (k == x) {
+        atomicAdd(&crow[h][j], c);
+        return true;
+      }
     }
-    const unsigned long long rec = (unsigned long long)L | ((unsigned long long)j << 31) | ((unsigned long long)c << 37);
-    const unsigned int k = atomicAdd(&pc[q], 1u);
-    if (k < kStage) {
-      stage[q][k] = rec;
-    } else {  // a chunk with more records for q than the stage holds: straight out
-      const unsigned long long pos = atomicAdd(&gcnt[q], 1ull);
-      if (pos < (unsigned long long)P.cap[q]) hsbuf[P.base[q] + (int64_t)pos] = rec;
-    }
+    return false;
   };
-  for (int64_t c = blockIdx.x; c * 64 < n_own; c += gridDim.x) {
-    const int64_t v0 = c * 64;
-    const int nvc = (int)(n_own - v0 < 64 ? n_own - v0 : 64);
-    {
-      int32_t r[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int i = wib * 8 + k;
-        r[k] = i < nvc ? lab[(v0 + i) * 64 + lane] : 0;
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) tile[wib * 8 + k][lane] = r[k];
+  const int64_t n_own = I.n_own;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned int iso_acc = 0;  // lane = view
+  for (int64_t b0 = wave * 64; b0 < n_own; b0 += nwaves * 64) {
+    const int64_t v = b0 + lane;
+    const uint64_t mv = v < n_own ? vm[v] & vmask : 0;
+    const uint64_t ad = v < n_own ? vadj[v] : 0;
+    const int32_t x = (v < n_own && uw) ? uw_label(uw[v]) : kMixed;
+    if (!REMOTE_ONLY) iso_acc += (unsigned)__popcll(transpose64(mv & ~ad, lane));
+    const uint64_t m = mv & ad;
+    uint64_t todo = __ballot(m != 0 && x != kMixed);
+    while (todo) {  // uniform members, grouped by (label, views): lane = view
+      const int L = __builtin_ctzll(todo);
+      const int32_t xL = __builtin_amdgcn_readlane(x, L);
+      const uint64_t mL = rl64(m, L);
+      const uint64_t same = __ballot(((todo >> lane) & 1) && x == xL && m == mL);
+      todo &= ~same;
+      const bool on = (mL >> lane) & 1;
+      const unsigned c = (unsigned)__popcll(same);
+      const bool hit = on && cached(xL, lane, c);
+      count_direct<REMOTE_ONLY>(on && !hit, xL, lane, c, P, I, counts, gcnt, hsbuf, lane);
     }
-    const uint64_t mvl = lane < nvc ? vm[v0 + lane] : 0;
-    const uint64_t adl = lane < nvc ? vadj[v0 + lane] : 0;
-    uint64_t any = mvl;
-    for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
-    any = rl64(any, 0) & vmask;
-    __syncthreads();
-    while (any) {
-      const int j = __builtin_ctzll(any);
-      any &= any - 1;
-      const bool in_view = (mvl >> j) & 1;
-      const bool member = in_view && ((adl >> j) & 1);
-      if (!REMOTE_ONLY) {
-        const uint64_t isolated = __ballot(in_view && !member);
-        if (lane == 0 && isolated) iso[j] += (unsigned)__popcll(isolated);
-      }
-      const int32_t l = tile[lane][j];
-      uint64_t todo = __ballot(member);
-      for (int it = 0; todo; it++) {
-        if (it == rounds) {
-          emit(l, j, 1u, (todo >> lane) & 1);
-          break;
-        }
-        const int leader = __builtin_ctzll(todo);
-        const int32_t L = __builtin_amdgcn_readlane(l, leader);
-        const uint64_t same = __ballot(member && l == L);
-        emit(L, j, (unsigned)__popcll(same), lane == leader);
-        todo &= ~same;
-      }
+    for (uint64_t mixed = __ballot(m != 0 && x == kMixed); mixed; mixed &= mixed - 1) {  // rows
+      const int L = __builtin_ctzll(mixed);
+      const uint64_t mL = rl64(m, L);
+      const bool on = (mL >> lane) & 1;
+      const int32_t l = on ? lab[(b0 + L) * 64 + lane] : 0;
+      const bool hit = on && cached(l, lane, 1u);
+      count_direct<REMOTE_ONLY>(on && !hit, l, lane, 1u, P, I, counts, gcnt, hsbuf, lane);
     }
-    __syncthreads();  // the chunk's records are staged (and the tile is free)
-    if (threadIdx.x < P.np) {
-      const unsigned int n = pc[threadIdx.x] < kStage ? pc[threadIdx.x] : kStage;
-      fb[threadIdx.x] = n ? atomicAdd(&gcnt[threadIdx.x], (unsigned long long)n) : 0ull;
-    }
-    __syncthreads();
-    for (int q = 0; q < P.np; q++) {
-      const unsigned int n = pc[q] < kStage ? pc[q] : kStage;
-      for (unsigned int i = threadIdx.x; i < n; i += blockDim.x) {
-        const unsigned long long pos = fb[q] + i;
-        if (pos < (unsigned long long)P.cap[q]) hsbuf[P.base[q] + (int64_t)pos] = stage[q][i];
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x < kMaxParts) pc[threadIdx.x] = 0;
-    __syncthreads();
   }
+  for (int h = 0; h < kRows; h++) {  // the wave's cache: owned labels at their rows, the rest as records
+    const int32_t k = ckey[h];
+    if (k == -1) continue;
+    const unsigned int c = crow[h][lane];
+    count_direct<REMOTE_ONLY>(c != 0, k, lane, c, P, I, counts, gcnt, hsbuf, lane);
+  }
+  if (!REMOTE_ONLY && iso_acc) atomicAdd(&iso[lane], iso_acc);
+  __syncthreads();
   if (!REMOTE_ONLY && threadIdx.x < 64 && iso[threadIdx.x])
     atomicAdd(&iso_g[(blockIdx.x & 63) * 64 + threadIdx.x], iso[threadIdx.x]);
 }
 
-// records received from the other partitions: count at the owned label vertex
+// records received from the other partitions: count at the owned label vertex's row
 __global__ __launch_bounds__(256) void k_hist_recv(XPeers P, const unsigned long long* __restrict__ rbuf, OwnIdx I,
-                                                   int32_t* __restrict__ hist) {
+                                                   int32_t* __restrict__ counts) {
   const int64_t n = P.pre[P.np];
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int q = peer_of(P, i);
     const unsigned long long r = rbuf[P.base[q] + i - P.pre[q]];
-    const int64_t L = (int64_t)(r & 0x7fffffffull);
+    const int32_t L = (int32_t)(r & 0x7fffffffull);
     const int j = (int)((r >> 31) & 63);
     const int32_t c = (int32_t)(r >> 37);
-    const int64_t rk = owned_rank(I, L);
-    if (rk >= 0) atomicAdd(&hist[(int64_t)j * I.n_own + rk], c);
+    const int64_t row = label_row(I, L);
+    if (row >= 0) atomicAdd(&counts[row * 64 + j], c);
   }
 }
 
@@ -417,17 +448,18 @@ void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_
     k_xmark<<<xgrid(P.pre[P.np], 4), 256, 0, s>>>(P, rbuf, xrv, chg, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
                                                    vm, em, g.n_seg > 0 ? g.hv_of : nullptr, act_next);
 }
-void launch_hist_route(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
-                       const uint64_t* vm, const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso,
-                       unsigned long long* gcnt, unsigned long long* hsbuf) {
-  const unsigned grid = xgrid(I.n_own, 64, 8192);
+void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
+                       const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,
+                       unsigned int* iso, unsigned long long* gcnt, unsigned long long* hsbuf) {
+  const uint64_t vmask = nviews >= 64 ? ~0ull : ((1ull << nviews) - 1);
+  const unsigned grid = xgrid(I.n_own, 256, 2048);
   if (remote_only)
-    k_hist_route<true><<<grid, 512, 0, s>>>(P, I, nviews, vm, vadj, lab, hist, iso, g_hist_rounds, gcnt, hsbuf);
+    k_part_count<true><<<grid, 256, 0, s>>>(P, I, vmask, vm, vadj, uw, lab, counts, iso, gcnt, hsbuf);
   else
-    k_hist_route<false><<<grid, 512, 0, s>>>(P, I, nviews, vm, vadj, lab, hist, iso, g_hist_rounds, gcnt, hsbuf);
+    k_part_count<false><<<grid, 256, 0, s>>>(P, I, vmask, vm, vadj, uw, lab, counts, iso, gcnt, hsbuf);
 }
-void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const OwnIdx& I, int32_t* hist) {
-  if (P.pre[P.np] > 0) k_hist_recv<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, I, hist);
+void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const OwnIdx& I, int32_t* counts) {
+  if (P.pre[P.np] > 0) k_hist_recv<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, I, counts);
 }
 
 }  // namespace rgpu

@@ -28,7 +28,9 @@ def _i64(a) -> np.ndarray:
 
 
 class TemporalGraph:
-    def __init__(self, partition: int = 0, num_partitions: int = 1, device: int = 0):
+    def __init__(self, partition: int = 0, num_partitions: int = 1, device: int = 0, vertex_order: str = "locality"):
+        """vertex_order: "locality" (default: hubs clustered for cache reuse) or "id" (ids ascending;
+        live ingest needs it, so that later seals merge incrementally) — rgpu_set_vertex_order."""
         self._lib = N.rgpu()
         ctx = C.c_void_p()
         rc = self._lib.rgpu_open(partition, num_partitions, device, C.byref(ctx))
@@ -36,6 +38,8 @@ class TemporalGraph:
             raise RGPUError(rc, f"rgpu_open(partition={partition}, num_partitions={num_partitions}, "
                                 f"device={device}) failed")
         self._ctx = ctx
+        if vertex_order != "locality":  # (the library's default)
+            self.set_vertex_order(vertex_order)
         self._hops: Optional[np.ndarray] = None
         self._windows: List[int] = []
 
@@ -60,6 +64,10 @@ class TemporalGraph:
             self.close()
         except Exception:
             pass
+
+    def set_vertex_order(self, order: str) -> None:
+        code = {"locality": N.RGPU_ORDER_LOCALITY, "id": N.RGPU_ORDER_ID}[order]
+        self._check(self._lib.rgpu_set_vertex_order(self._ctx, code))
 
     # ------------------------------------------------------------------ ingest
     def ingest(self, t, kind, src, dst) -> None:

@@ -32,6 +32,7 @@ def load_packer_harness():
     L.ph_num.argtypes = [C.c_void_p, C.c_int]
     L.ph_list.restype = C.c_int64
     L.ph_list.argtypes = [C.c_void_p, C.c_int, C.c_int, P64]
+    L.ph_set_locality.argtypes = [C.c_int]
     L.ph_delta_check.restype = C.c_int
     L.ph_delta_check.argtypes = [P64, PU8, P64, P64, C.c_size_t, C.c_size_t]
     return L

@@ -11,12 +11,16 @@
 using rgpu::Event;
 using rgpu::Packed;
 
+// local vertex order of the next packs (pack_events `locality`: 1 = RGPU_ORDER_LOCALITY)
+static bool g_locality = false;
+extern "C" void ph_set_locality(int on) { g_locality = on != 0; }
+
 extern "C" void* ph_pack(const int64_t* t, const uint8_t* kind, const int64_t* src, const int64_t* dst,
                          size_t n) {
   std::vector<Event> ev(n);
   for (size_t i = 0; i < n; i++) ev[i] = {t[i], src[i], kind[i] >= 2 ? dst[i] : -1, kind[i]};
   Packed* p = new Packed();
-  if (!rgpu::pack_events(ev, 0, 1, p).empty()) { delete p; return nullptr; }
+  if (!rgpu::pack_events(ev, 0, 1, p, g_locality).empty()) { delete p; return nullptr; }
   return p;
 }
 // partition view (num_partitions > 1): same stream, one partition's pack
@@ -27,7 +31,7 @@ extern "C" void* ph_pack_part(const int64_t* t, const uint8_t* kind, const int64
     if (rgpu::partition_keeps(kind[i], src[i], kind[i] >= 2 ? dst[i] : -1, part, nparts))
       ev.push_back({t[i], src[i], kind[i] >= 2 ? dst[i] : -1, kind[i]});
   Packed* p = new Packed();
-  if (!rgpu::pack_events(ev, part, nparts, p).empty()) { delete p; return nullptr; }
+  if (!rgpu::pack_events(ev, part, nparts, p, g_locality).empty()) { delete p; return nullptr; }
   return p;
 }
 // what: 0 local vertex ids [nv], 1 CC label per local rank [nv] (P > 1), 2 send list ids of
@@ -43,6 +47,42 @@ extern "C" int64_t ph_list(void* h, int what, int q, int64_t* out) {
   if (what == 4) for (int64_t e = 0; e < p->ne; e++) v.push_back(p->vid[p->esrc[e]]);
   if (what == 5) for (int64_t e = 0; e < p->ne; e++) v.push_back(p->vid[p->edst[e]]);
   if (what == 6) v.assign(p->lowner.begin(), p->lowner.end());
+  if (what == 7)  // owned ids in the order of by_id (ascending ids when it is right)
+    for (int64_t k = 0; k < p->n_own; k++) v.push_back(p->vid[p->by_id.empty() ? k : p->by_id[k]]);
+  if (what == 8)  // the id of every local rank's label (P = 1 relabeled: lid[grank]; P > 1: grank)
+    for (int64_t r = 0; r < p->nv; r++)
+      v.push_back(p->grank.empty() ? p->vid[r] : p->nparts > 1 ? p->grank[r] : p->lid[p->grank[r]]);
+  if (what == 9)  // per edge: its history keys, with the edge's (src id, dst id) first
+    for (int64_t e = 0; e < p->ne; e++) {
+      v.push_back(p->vid[p->esrc[e]]);
+      v.push_back(p->vid[p->edst[e]]);
+      v.push_back(p->eoff[e + 1] - p->eoff[e]);
+      for (int64_t k = p->eoff[e]; k < p->eoff[e + 1]; k++) v.push_back(p->ekey[k]);
+    }
+  if (what == 10)  // per local rank: id, vertex history size + keys, death count + times
+    for (int64_t r = 0; r < p->nv; r++) {
+      v.push_back(p->vid[r]);
+      v.push_back(p->voff[r + 1] - p->voff[r]);
+      for (int64_t k = p->voff[r]; k < p->voff[r + 1]; k++) v.push_back(p->vkey[k]);
+      v.push_back(p->doff[r + 1] - p->doff[r]);
+      for (int64_t k = p->doff[r]; k < p->doff[r + 1]; k++) v.push_back(p->dtime[k]);
+    }
+  if (what == 11) {  // structural checks of any order: 0 = fine, else the first failed check
+    int bad = 0;
+    for (int64_t e = 0; e + 1 < p->ne && !bad; e++)
+      if (p->esrc[e] > p->esrc[e + 1] || (p->esrc[e] == p->esrc[e + 1] && p->edst[e] >= p->edst[e + 1])) bad = 1;
+    for (int64_t v2 = 0; v2 < p->nv && !bad; v2++)
+      for (int64_t k = p->in_off[v2]; k < p->in_off[v2 + 1]; k++) {
+        const int32_t e = p->in_eid[k];
+        if (p->edst[e] != v2 || (k > p->in_off[v2] && p->esrc[p->in_eid[k - 1]] >= p->esrc[e])) bad = 2;
+      }
+    for (int64_t k = 0; k + 1 < (int64_t)p->by_id.size() && !bad; k++)
+      if (p->vid[p->by_id[k]] >= p->vid[p->by_id[k + 1]]) bad = 3;
+    if (p->relabeled && p->nparts == 1 && !bad)
+      for (int64_t r = 0; r < p->nv; r++)
+        if (p->lid[p->grank[r]] != p->vid[r] || p->by_id[p->grank[r]] != r) { bad = 4; break; }
+    v.push_back(bad);
+  }
   if (out) std::copy(v.begin(), v.end(), out);
   return (int64_t)v.size();
 }
@@ -66,6 +106,11 @@ static int64_t last_death(const Packed* p, int32_t r, int64_t t) {
 extern "C" int ph_alive(void* h, int is_edge, int64_t src, int64_t dst, int64_t t, int64_t window) {
   const Packed* p = (const Packed*)h;
   auto rank = [&](int64_t id) -> int64_t {  // local order is (owned, ghost) by id: search both runs
+    if (p->relabeled) {  // locality order: a scan (test sizes)
+      for (int64_t r = 0; r < p->nv; r++)
+        if (p->vid[r] == id) return r;
+      return -1;
+    }
     for (auto [lo, hi] : {std::pair<int64_t, int64_t>{0, p->n_own}, {p->n_own, p->nv}}) {
       auto it = std::lower_bound(p->vid.begin() + lo, p->vid.begin() + hi, id);
       if (it != p->vid.begin() + hi && *it == id) return it - p->vid.begin();

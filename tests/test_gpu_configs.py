@@ -7,10 +7,14 @@
   C3  10M vertices / 100M power-law updates, 61 daily hops x      degree totals of every view
       {month, week, day}, DegreeBasic + PageRank(20)              (properties) + per-vertex degrees
                                                                   and PR (L1 <= 1e-6) at sampled hops
-  C4  the first 100M updates of the 1B GAB stream (20M users),    summaries of all 840 views
-      168 hourly hops x {y,m,w,d,h}, CC                           (properties), per-vertex labels of
-                                                                  day/hour views at sampled hops and
-                                                                  the year view at the last hop
+  C4  prefixes of the 1B GAB stream (20M users; 100M and 300M    summaries of all 840 views
+      updates), 168 hourly hops x {y,m,w,d,h}, CC                 (properties); at 8 / 4 hops spread
+                                                                  over the 168, every window: summary,
+                                                                  supersteps and a checksum of every
+                                                                  member's label vs the oracle's
+                                                                  committed goldens
+      the whole 1B stream                                         summary invariants + another batch
+                                                                  composition of three hops
   C5  30M-update GAB base + one 10M-update hour tick merged       labels / PR / counts equal to a
       into the resident graph, CC + PR(20) on the newest hour     one-shot seal of the same stream
 
@@ -20,6 +24,8 @@ path ingests and seals (ctypes releases the GIL), and per-view queries run in a 
 Reference semantics: ConnectedComponents.scala:10-42,137-145; DegreeBasic.scala:16-28;
 SURVEY.md App. A.5 (PageRank spec).
 """
+import json
+import os
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -30,6 +36,7 @@ from raphtory_amd import TemporalGraph
 from raphtory_amd.analysis import cc_fields, cc_fields_from_summary
 from raphtory_amd.synth import (BATCH_WINDOWS, DAY, HOUR, MONTH, T0_README, WEEK, YEAR, gen_gab, gen_gab_range,
                                 gen_powerlaw, gen_uniform, range_hops)
+from tests.goldens import label_checksum
 
 pytestmark = [pytest.mark.gpu, pytest.mark.fullsize]
 
@@ -37,8 +44,8 @@ PR_L1_TOL = 1e-6  # BASELINE.json north_star: PageRank within 1e-6 L1 per view
 POOL = 8          # oracle query threads (the GPU box gives this job 16 host cores)
 
 
-def _graph(s):
-    g = TemporalGraph()
+def _graph(s, order="locality"):
+    g = TemporalGraph(vertex_order=order)
     g.ingest_stream(s)
     g.seal()
     return g
@@ -127,61 +134,74 @@ def test_c3_powerlaw_degree_and_pagerank():
         g.run("degree", hops[sample], windows, retain=True)
         gdeg = {(k, w): g.degree_vertex(k, w) for k in range(len(sample)) for w in range(3)}
         gtot = {(k, w): g.degree_result(k, w)[:3] for k in range(len(sample)) for w in range(3)}
-        g.run("pagerank", hops[-1:], windows, pr_iters=20, retain=True)
-        gpr = [g.pr_result(0, w) for w in range(3)]
+        gtop = {(k, w): g.degree_result(k, w)[3] for k in range(len(sample)) for w in range(3)}
+        g.run("pagerank", hops[sample], windows, pr_iters=20, retain=True)
+        gpr = {(k, w): g.pr_result(k, w) for k in range(len(sample)) for w in range(3)}
         g.close()
         o = fo.result()
         # per window alone: with descending windows the running-min vertex set is the window's own
         deg = {(k, w): ex.submit(lambda t, w: o.degree(int(t), [windows[w]])[0], hops[h], w)
                for k, h in enumerate(sample) for w in range(3)}
-        pr = [ex.submit(lambda w: o.pagerank(int(hops[-1]), [windows[w]], iters=20)[0], w) for w in range(3)]
+        pr = {(k, w): ex.submit(lambda t, w: o.pagerank(int(t), [windows[w]], iters=20)[0], hops[h], w)
+              for k, h in enumerate(sample) for w in range(3)}
         for (k, w), f in deg.items():
             ids, od, idg = f.result()
             gids, god, gid = gdeg[(k, w)]
             assert np.array_equal(gids, ids) and np.array_equal(god, od) and np.array_equal(gid, idg), (k, w)
             assert gtot[(k, w)] == (len(ids), int(od.sum()), int(idg.sum()))
             assert tuple(tot[sample[k], w]) == gtot[(k, w)]  # the 61-hop run agrees
-        for w, f in enumerate(pr):
+            top = np.lexsort((ids, -idg.astype(np.int64)))[:20]  # DegreeRanking: in-degree desc, ties by id
+            assert gtop[(k, w)] == [(int(ids[i]), int(od[i]), int(idg[i])) for i in top], (k, w)
+        for (k, w), f in pr.items():  # PageRank at three hops, every window
             ids, p = f.result()
-            gids, gp = gpr[w]
+            gids, gp = gpr[(k, w)]
             assert np.array_equal(gids, ids)
-            assert np.abs(gp - p).sum() <= PR_L1_TOL, (w, np.abs(gp - p).sum())
+            assert np.abs(gp - p).sum() <= PR_L1_TOL, (k, w, np.abs(gp - p).sum())
     o.close()
 
 
 # ------------------------------------------------------------------ C4
-def test_c4_first_100m_updates_cc():
-    users, inter = 20_000_000, 333_333_334  # the 1B-update C4 stream; its first 100M updates
-    s = gen_gab_range(4, users, inter, 0, 33_333_334)
-    assert len(s) == 100_000_002
-    end = int(s.t[-1])
+_GOLD_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c4_prefix_goldens.json")
+_GOLD = json.load(open(_GOLD_PATH))["prefixes"] if os.path.exists(_GOLD_PATH) else {}
+
+
+@pytest.mark.parametrize("inter", sorted(_GOLD, key=int))
+def test_c4_prefix_vs_oracle_goldens(inter):
+    """C4 on prefixes of the 1B stream against the oracle's results committed by
+    tools/make_c4_goldens.py: the whole 168-hop x 5-window query, and at every sampled hop (spread
+    over the 168) every window (year, month, week, day, hour): summary fields, the hop's superstep
+    count, member count and the checksum of every member's (id, label)."""
+    P = _GOLD[inter]
+    n = int(inter)
+    g = TemporalGraph()
+    for first in range(0, n, 20_000_000):
+        s = gen_gab_range(4, 20_000_000, 333_333_334, first, min(20_000_000, n - first))
+        g.ingest_stream(s)
+        end = int(s.t[-1])
+        del s
+    g.seal()
+    assert g.stats()["vertices"] == P["vertices"]
     hops = range_hops(end - 167 * HOUR, end, HOUR)
-    assert len(hops) == 168
-    pick = [0, 55, 111, 167]
-    with ThreadPoolExecutor(POOL) as ex:
-        fo = ex.submit(Oracle.from_stream, s, True)
-        g = _graph(s)
-        g.run("cc", hops, BATCH_WINDOWS)
-        full = g.cc_summaries()
-        _summary_props(full)
-        assert np.all(full[..., 5] > 0)  # the GAB stream is active every hour
-        g.run("cc", hops[pick], BATCH_WINDOWS, retain=True)
-        glab = {(k, w): g.cc_vertex_labels(k, w) for k in range(len(pick)) for w in (0, 3, 4)}
-        g.close()
-        o = fo.result()
-        short = {k: ex.submit(lambda t: o.cc(int(t), [DAY, HOUR], mode=1)[0], hops[h]) for k, h in enumerate(pick)}
-        year = ex.submit(lambda: o.cc(int(hops[-1]), [YEAR], mode=1)[0])
-        for k, f in short.items():
-            for j, w in enumerate((3, 4)):
-                ids, lab = f.result()[j]
-                gids, gl = glab[(k, w)]
-                assert np.array_equal(gids, ids) and np.array_equal(gl, lab), (pick[k], w)
-                assert cc_fields_from_summary_row(full[pick[k], w]) == cc_fields(label_counts(lab)), (pick[k], w)
-        ids, lab = year.result()[0]
-        gids, gl = glab[(len(pick) - 1, 0)]
-        assert np.array_equal(gids, ids) and np.array_equal(gl, lab)
-        assert cc_fields_from_summary_row(full[-1, 0]) == cc_fields(label_counts(lab))
-    o.close()
+    assert len(hops) == P["n_hops"] and int(hops[0]) == P["hop0"]
+    g.run("cc", hops, BATCH_WINDOWS)
+    full = g.cc_summaries()
+    _summary_props(full)
+    pick = sorted(int(h) for h in P["hops"])
+    g.run("cc", hops[pick], BATCH_WINDOWS, retain=True)
+    for k, h in enumerate(pick):
+        rec = P["hops"][str(h)]
+        assert int(hops[h]) == rec["t"]
+        assert full[h, 0, 7] == rec["supersteps"], (h, full[h, 0, 7], rec["supersteps"])
+        for w in range(5):
+            exp = rec["windows"][w]
+            got = dict(zip(("biggest", "total", "total_without_islands", "total_islands", "clusters_gt2", "sum_all",
+                            "sum_without_islands"), full[h, w, :7].tolist()))
+            for f in ("biggest", "total", "total_without_islands", "clusters_gt2", "sum_all", "sum_without_islands"):
+                assert got[f] == exp[f], (h, w, f, got[f], exp[f])
+            ids, lab = g.cc_vertex_labels(k, w)
+            assert len(ids) == exp["members"], (h, w)
+            assert label_checksum(ids, lab) == exp["label_checksum"], (h, w)
+    g.close()
 
 
 def test_c4_full_1b_properties():
@@ -229,7 +249,7 @@ def test_c5_ten_million_update_tick_equals_one_shot_seal():
     tick = gen_gab(100, users, 3_333_334, t0=now + 1, t1=now + HOUR, id_key=4)
     assert len(tick) == 10_000_002
     now = int(tick.t[-1])
-    live = _graph(base)
+    live = _graph(base, "id")
     live.ingest_stream(tick)
     live.seal()  # merged into the resident graph (merge.hip)
     assert live.stats()["seal_incremental"] == 1 and live.stats()["seal_delta_updates"] == len(tick)

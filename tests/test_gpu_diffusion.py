@@ -125,7 +125,7 @@ def test_diffusion_after_live_delta_seals():
     # array must follow the merged graph (rgpu_seal's delta path)
     s = gen_uniform(5, 1500, 30000, dt=31_536 * 33)
     n = len(s.t)
-    g = TemporalGraph()
+    g = TemporalGraph(vertex_order="id")
     cuts = [0, n // 3, 2 * n // 3, n]
     for a, b in zip(cuts[:-1], cuts[1:]):
         g.ingest(s.t[a:b], s.kind[a:b], s.src[a:b], s.dst[a:b])

@@ -36,7 +36,7 @@ def _cut(arrs, lo, hi):
 
 def _live(arrs, cuts, check):
     """Ingest arrs in the chunks given by `cuts`, sealing after each; check(g, prefix) each time."""
-    g = TemporalGraph()
+    g = TemporalGraph(vertex_order="id")  # later seals merge into it (rgpu_set_vertex_order)
     bounds = [0] + list(cuts) + [len(arrs[0])]
     for k in range(len(bounds) - 1):
         g.ingest(*_cut(arrs, bounds[k], bounds[k + 1]))
@@ -159,7 +159,7 @@ def test_live_powerlaw_heavy_vertices_and_gab():
 
 
 def test_live_seal_errors_and_noop():
-    g = TemporalGraph()
+    g = TemporalGraph(vertex_order="id")
     g.ingest([1, 2], [2, 2], [1, 2], [2, 3])
     g.seal()
     g.seal()  # nothing new: no-op

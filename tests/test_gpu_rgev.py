@@ -44,7 +44,7 @@ def test_rgev_ingest_matches_oracle_and_array_ingest():
 def test_rgev_live_seals_and_bad_bytes():
     s = gen_uniform(22, 400, 9_000, t0=T0_README, dt=3_500_000)
     hops = range_hops(T0_README + 30 * DAY, T0_README + 360 * DAY, 30 * DAY)
-    with TemporalGraph() as g:
+    with TemporalGraph(vertex_order="id") as g:
         cut = 5_000
         _feed(g, rgev.encode(s.t[:cut], s.kind[:cut], s.src[:cut], s.dst[:cut]), 4096)
         g.seal()

@@ -85,3 +85,58 @@ def test_live_delta_host_half_matches_one_shot_pack(ph, seed, tie, shuffle, thre
     rc = ph.ph_delta_check(t.ctypes.data_as(P64), k.ctypes.data_as(PU8), s.ctypes.data_as(P64),
                            d.ctypes.data_as(P64), len(t), int(len(t) * frac))
     assert rc == 0, f"check {rc} failed"
+
+
+def _records(ph, h, what):
+    """plist records (kind 9 edges / 10 vertices) -> {first id(s): the rest}"""
+    from harness import plist
+    x = plist(ph, h, what).tolist()
+    out, i = {}, 0
+    while i < len(x):
+        if what == 9:
+            key, n = (x[i], x[i + 1]), x[i + 2]
+            out[key] = tuple(x[i + 3:i + 3 + n])
+            i += 3 + n
+        else:
+            vid, n = x[i], x[i + 1]
+            hist = tuple(x[i + 2:i + 2 + n])
+            m = x[i + 2 + n]
+            out[vid] = (hist, tuple(x[i + 3 + n:i + 3 + n + m]))
+            i += 3 + n + m
+    return out
+
+
+@pytest.mark.parametrize("seed,tie,shuffle,threads,nv", [(21, 1, False, "1", 40), (22, 3, True, "8", 40),
+                                                         (23, 2, False, "8", 3000)])
+def test_locality_order_is_the_same_graph(ph, seed, tie, shuffle, threads, nv, monkeypatch):
+    """RGPU_ORDER_LOCALITY (packer.cpp locality_order) only renumbers the local ranks: per id the
+    same vertex history and death list, per (src id, dst id) the same edge history (ties
+    resolved the same way), labels still the id ranks, by_id ascending, CSR and in-edge order
+    intact; and the liveness decisions equal the oracle's."""
+    from harness import plist
+    monkeypatch.setenv("RGPU_THREADS", threads)
+    t, k, s, d = _stream(seed, 20_000, nv, tie, shuffle)
+    ph.ph_set_locality(0)
+    h0 = _pack(ph, t, k, s, d)
+    ph.ph_set_locality(1)
+    try:
+        h1 = _pack(ph, t, k, s, d)
+    finally:
+        ph.ph_set_locality(0)
+    assert plist(ph, h1, 11).tolist() == [0]
+    assert _records(ph, h0, 9) == _records(ph, h1, 9)
+    assert _records(ph, h0, 10) == _records(ph, h1, 10)
+    ids1 = plist(ph, h1, 7)
+    assert np.array_equal(ids1, plist(ph, h0, 0))          # by_id lists the ids ascending
+    assert np.array_equal(plist(ph, h1, 8), plist(ph, h1, 0))  # every rank's label is its own id
+    if nv >= 3000:  # the ranks really moved: most active first within a group
+        assert not np.array_equal(plist(ph, h1, 0), plist(ph, h0, 0))
+    o = Oracle(t, k, s, d)
+    bad = 0
+    for tt in np.unique(t)[:: max(1, len(np.unique(t)) // 25)].tolist():
+        for w in (-1, 30, 5000):
+            for v in range(0, nv, max(1, nv // 40)):
+                bad += ph.ph_alive(h1, 0, v, -1, tt, w) != o.alive(False, v, -1, tt, w)
+    assert bad == 0
+    ph.ph_free(h0)
+    ph.ph_free(h1)

@@ -137,3 +137,38 @@ def test_partition_plan_world2_gloo():
         p.join(60)
         assert p.exitcode == 0
     assert ok and cover and nsend > 0
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_locality_order_partitions(ph, P):
+    """Partitioned packs in RGPU_ORDER_LOCALITY: owned and ghost ranks each reordered, yet the same
+    owned / ghost id sets, labels = ids, the same kept edges, and exchange lists that still pair
+    up by id between every two partitions (entry i of p's list for q is entry i of q's list)."""
+    t, k, s, d = _stream(40 + P, 6000, 300)
+    ph.ph_set_locality(1)
+    try:
+        hl = [pack(ph, t, k, s, d, p, P) for p in range(P)]
+    finally:
+        ph.ph_set_locality(0)
+    hi = [pack(ph, t, k, s, d, p, P) for p in range(P)]
+    for p in range(P):
+        a, b = hl[p], hi[p]
+        assert plist(ph, a, 11).tolist() == [0]
+        na = ph.ph_num(a, 4)
+        assert na == ph.ph_num(b, 4)
+        va, vb = plist(ph, a, 0), plist(ph, b, 0)
+        assert sorted(va[:na].tolist()) == vb[:na].tolist() and sorted(va[na:].tolist()) == vb[na:].tolist()
+        assert np.array_equal(plist(ph, a, 7), vb[:na])
+        assert np.array_equal(plist(ph, a, 1), va)  # labels are ids
+        ka = sorted(zip(plist(ph, a, 4).tolist(), plist(ph, a, 5).tolist()))
+        kb = sorted(zip(plist(ph, b, 4).tolist(), plist(ph, b, 5).tolist()))
+        assert ka == kb
+        for q in range(P):
+            assert np.array_equal(plist(ph, a, 2, q), plist(ph, b, 2, q))
+            assert np.array_equal(plist(ph, a, 3, q), plist(ph, b, 3, q))
+    for p in range(P):
+        for q in range(P):
+            if q != p:
+                assert np.array_equal(plist(ph, hl[p], 2, q), plist(ph, hl[q], 3, p))
+    for h in hl + hi:
+        ph.ph_free(h)

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 B=raphtory_amd/_build/librgpu.so
 cp "$B" gpurun_out/librgpu_new.so
-for i in 1 2; do
+for i in $(seq 1 ${ROUNDS:-2}); do
   for v in new ${AB_TAG:-r1}; do
     if [ "$v" = new ]; then cp gpurun_out/librgpu_new.so "$B"; else cp "abtest/librgpu_$v.so" "$B"; fi
     timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile-pass ${BENCH_ARGS:-} \

@@ -60,11 +60,22 @@ def main():
             for k, v in g.stats()["xchg_bytes_by"].items():
                 by[k] = by.get(k, 0.0) + v / 1e6
         summ = parts[0].cc_summaries()
+        # modelled exchange time per partition: the bytes it sends, spread over its P-1 xGMI links
+        # (point-to-point, ~153 GB/s each per the MI355X platform figures in the task brief) — a
+        # bandwidth term only; the number of exchange rounds (one per superstep per batch, plus one
+        # membership and one counts round per batch) is reported beside it
+        link = 153e9
+        xms = [(g.stats()["xchg_bytes"] / max(1, P - 1)) / link * 1e3 if P > 1 else 0.0 for g in parts]
+        tot = [round(k + x, 1) for k, x in zip(per, xms)]
+        rounds = parts[0].stats()["supersteps"] + 2 * parts[0].stats()["batches"]
         out = {"P": P, "kernel_ms_per_partition": per, "kernel_ms_max": max(per), "kernel_ms_total": round(sum(per), 1),
                "kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in ks.items()},
                "partition0_kernels": {k: [v["launches"], round(v["ms"], 2)] for k, v in parts[0].stats()["kernels"].items()
                                       if v["launches"]},
                "xchg_MB_per_query": {k: round(v, 1) for k, v in by.items()},
+               "xchg_model_ms_per_partition": [round(x, 2) for x in xms], "xchg_link_GBps": link / 1e9,
+               "xchg_rounds_per_partition": rounds,
+               "kernel_plus_xchg_ms_max": max(tot),
                "vertices_here": [g.stats()["vertices"] for g in parts], "edges_here": [g.stats()["edges"] for g in parts],
                "check": [int(summ[..., 0].sum()), int(summ[..., 1].sum()), int(summ[..., 5].sum())]}
         print(json.dumps(out), flush=True)
