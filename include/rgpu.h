@@ -48,6 +48,7 @@ extern "C" {
 #define RGPU_ALGO_DEGREE 1 /* S/core/analysis/Algorithms/DegreeBasic.scala (and DegreeRanking) */
 #define RGPU_ALGO_PR 2     /* PageRank per SURVEY.md App. A.5 (reference PageRank.scala is broken) */
 #define RGPU_ALGO_DIFFUSION 3 /* S/core/analysis/Algorithms/BinaryDefusion.scala (ABI 5) */
+#define RGPU_ALGO_VP 4     /* a generic vertex program, rgpu_set_vertex_program (ABI 7) */
 
 /* rgpu_run_view_batch flags */
 #define RGPU_RUN_RETAIN 1   /* keep per-vertex results of every view (for *_vertex_* queries) */
@@ -82,7 +83,7 @@ typedef struct {
   double ms_total;               /* wall ms inside the last rgpu_run_view_batch */
   /* per-kernel event timing (RGPU_RUN_PROFILE): 0=window_mask 1=slots 2=cc_step 3=cc_hist
    * 4=cc_summary 5=pr_step 6=degree 7=cc_tail (late supersteps, one workgroup)
-   * 8=heavy (hub segment kernels) 9=diffusion step 10-11 reserved */
+   * 8=heavy (hub segment kernels) 9=diffusion step 10=vertex-program step 11 reserved */
   int64_t kernel_launches[12];
   double kernel_ms[12];
   double kernel_bytes[12];       /* algorithmic bytes summed over launches */
@@ -235,6 +236,40 @@ int rgpu_diffusion_result(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* infect
  * the view, ascending id.  Needs RGPU_RUN_RETAIN. */
 int rgpu_diffusion_vertex(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, int32_t* steps,
                           size_t cap, size_t* n);
+
+/* Generic VertexVisitor messaging (ABI 7; VertexVisitor.scala:81-166): a
+ * user Analyser whose analyse() folds its message queue with min or max runs on the GPU as a
+ * vertex program, with the reference's BSP structure (AnalysisTask / ReaderWorker):
+ *   setup (superstep 0, only when maxSteps > 1): every view member sets its state
+ *     (getOrSetCompValue) to its own id (RGPU_VP_INIT_ID) or init_value (seed_value at the vertex
+ *     seed_id; RGPU_VP_INIT_VALUE); the senders — every member, or only the seed — message their
+ *     neighbours in `direction` (messageAllOutgoingNeighbors / messageAllIngoingNeighbors /
+ *     messageAllNeighbours, over edges alive in the view) the value state + step_add (saturating);
+ *   superstep r >= 1: a member holding messages folds them and its state with `reduce`; if that
+ *     changes its state it keeps it and messages again, else it votes to halt;
+ *   the job halts at the first superstep in which no state changed in any window of the hop, or
+ *     at maxSteps.
+ * CC = {ALL, MIN, INIT_ID, SEND_ALL, step_add 0}; hop distance from a seed over out-edges = {OUT,
+ * MIN, INIT_VALUE init_value INT64_MAX seed_value 0, SEND_SEED, step_add 1}.  One partition;
+ * max_steps <= 127.  Oracle: oracle.h orc_vertex_program. */
+#define RGPU_VP_OUT 0
+#define RGPU_VP_IN 1
+#define RGPU_VP_ALL 2
+#define RGPU_VP_MIN 0
+#define RGPU_VP_MAX 1
+#define RGPU_VP_INIT_ID 0
+#define RGPU_VP_INIT_VALUE 1
+#define RGPU_VP_SEND_ALL 0
+#define RGPU_VP_SEND_SEED 1
+typedef struct {
+  int32_t direction, reduce, init, senders;
+  int64_t init_value, seed_id, seed_value, step_add;
+} rgpu_vertex_program_t;
+int rgpu_set_vertex_program(rgpu_ctx* ctx, const rgpu_vertex_program_t* program);
+/* every member's final state of view (hop, win), ascending id (needs RGPU_RUN_RETAIN) */
+int rgpu_vp_result(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, int64_t* values, size_t cap, size_t* n);
+/* supersteps the reference's job for that hop runs (as rgpu_cc_summary_t.supersteps) */
+int rgpu_vp_supersteps(rgpu_ctx* ctx, size_t hop, int64_t* supersteps);
 
 int rgpu_stats(rgpu_ctx* ctx, rgpu_stats_t* out);
 const char* rgpu_last_error(rgpu_ctx* ctx);

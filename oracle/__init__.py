@@ -55,6 +55,10 @@ def lib() -> C.CDLL:
         L.orc_degree.argtypes = [C.c_void_p, C.c_int64, _P64, C.c_int, _P64, _P32, _P32, _SZ, C.POINTER(_SZ)]
         L.orc_pagerank.restype = C.c_int
         L.orc_pagerank.argtypes = [C.c_void_p, C.c_int64, _P64, C.c_int, C.c_int, _P64, _PD, _SZ, C.POINTER(_SZ)]
+        L.orc_vertex_program.restype = C.c_int
+        L.orc_vertex_program.argtypes = [C.c_void_p, C.c_int64, _P64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_int64, _P64, _P64, _SZ,
+                                         C.POINTER(_SZ), C.POINTER(C.c_int)]
         L.orc_diffusion.restype = C.c_int
         L.orc_diffusion.argtypes = [C.c_void_p, C.c_int64, _P64, C.c_int, C.c_int, C.c_int64, C.c_uint64,
                                     C.c_int, _P64, _P32, _SZ, C.POINTER(_SZ), C.POINTER(C.c_int)]
@@ -161,6 +165,28 @@ class Oracle:
         if rc != 0:
             raise RuntimeError("orc_pagerank failed")
         return [(ids[i * cap:i * cap + n[i]].copy(), pr[i * cap:i * cap + n[i]].copy()) for i in range(nw)]
+
+    VP_DIRS = {"out": 0, "in": 1, "all": 2}
+    VP_REDUCE = {"min": 0, "max": 1}
+
+    def vertex_program(self, t: int, windows: Sequence[int] = (), max_steps: int = 100, direction: str = "all",
+                       reduce: str = "min", init: str = "id", senders: str = "all", init_value: int = 0,
+                       seed_id: int = -1, seed_value: int = 0, step_add: int = 0):
+        """generic VertexVisitor messaging (oracle.h orc_vertex_program) -> ([(ids, states)] per
+        window, supersteps)"""
+        w, nw = self._win(windows)
+        cap = max(1, self.nv)
+        ids = np.empty(nw * cap, np.int64)
+        vals = np.empty(nw * cap, np.int64)
+        n = (C.c_size_t * nw)()
+        steps = C.c_int()
+        rc = lib().orc_vertex_program(self._g, t, _p(w, C.c_int64) if len(w) else None, len(w), max_steps,
+                                      self.VP_DIRS[direction], self.VP_REDUCE[reduce], 0 if init == "id" else 1,
+                                      0 if senders == "all" else 1, init_value, seed_id, seed_value, step_add,
+                                      _p(ids, C.c_int64), _p(vals, C.c_int64), cap, n, C.byref(steps))
+        if rc != 0:
+            raise RuntimeError("orc_vertex_program failed")
+        return [(ids[i * cap:i * cap + n[i]].copy(), vals[i * cap:i * cap + n[i]].copy()) for i in range(nw)], steps.value
 
     def diffusion(self, t: int, windows: Sequence[int] = (), max_steps: int = 100, seed_id: int = 31,
                   coin_seed: int = 0, coin: bool = True):

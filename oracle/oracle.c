@@ -898,3 +898,122 @@ done:
   free(mem); free(inf); free(q); free(list);
   return rc;
 }
+
+/* ------------------------------------------------------- vertex program */
+static int64_t vp_add(int64_t a, int64_t b) { /* saturating a + b */
+  if (b > 0 && a > INT64_MAX - b) return INT64_MAX;
+  if (b < 0 && a < INT64_MIN - b) return INT64_MIN;
+  return a + b;
+}
+/* keys(outgoingProcessing) (dir 0), keys(incomingProcessing) (1) or their union (2) after
+ * viewAtWithWindow (Vertex.scala:70-74); a self-loop is an outgoing key only
+ * (EntityStorage.scala:257) */
+static int vp_neighbours(const orc_graph* g, int vi, int64_t t, int64_t w, int dir, int* nb, uint8_t* mark) {
+  const Vertex* v = &g->vs[vi];
+  int n = 0;
+  if (dir != 1)
+    for (int i = 0; i < v->out.n; i++) {
+      const Edge* e = &g->es[v->out.a[i]];
+      if (!edge_alive(g, e, t, w)) continue;
+      int x = hm_get(&g->vmap, (uint64_t)e->dst);
+      if (!mark[x]) { mark[x] = 1; nb[n++] = x; }
+    }
+  if (dir != 0)
+    for (int i = 0; i < v->in.n; i++) {
+      const Edge* e = &g->es[v->in.a[i]];
+      if (!edge_alive(g, e, t, w)) continue;
+      int x = hm_get(&g->vmap, (uint64_t)e->src);
+      if (!mark[x]) { mark[x] = 1; nb[n++] = x; }
+    }
+  for (int i = 0; i < n; i++) mark[nb[i]] = 0;
+  return n;
+}
+
+int orc_vertex_program(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int max_steps,
+                       int dir, int reduce, int init, int senders, int64_t init_value, int64_t seed_id,
+                       int64_t seed_value, int64_t step_add, int64_t* ids, int64_t* values, size_t cap,
+                       size_t* n_out, int* steps) {
+  WinSet ws;
+  if (winset_init(&ws, windows, nw) != 0 || dir < 0 || dir > 2 || reduce < 0 || reduce > 1) return -1;
+  size_t nv = g->nv, nvs = nv ? nv : 1;
+  int nwin = ws.nwin;
+  uint8_t* mem = (uint8_t*)calloc((size_t)nwin * nvs, 1);
+  uint8_t* sset = (uint8_t*)calloc((size_t)nwin * nvs, 1);       /* computationValues contains */
+  int64_t* st = (int64_t*)malloc(sizeof(int64_t) * nwin * nvs);
+  int64_t* qv = (int64_t*)malloc(sizeof(int64_t) * 2 * nwin * nvs); /* queue fold, even/odd parity */
+  uint32_t* qc = (uint32_t*)calloc((size_t)2 * nwin * nvs, sizeof(uint32_t));
+  int* nb = (int*)malloc(sizeof(int) * nvs);
+  int* list = (int*)malloc(sizeof(int) * nvs);
+  uint8_t* mark = (uint8_t*)calloc(nvs, 1);
+  int rc = -1;
+  int32_t sv = (seed_id >= 0 && seed_id < ((int64_t)1 << 31)) ? hm_get(&g->vmap, (uint64_t)seed_id) : -1;
+  if (!mem || !sset || !st || !qv || !qc || !nb || !list || !mark) goto done;
+  *steps = 0;
+  build_keysets(g, t, &ws, mem);
+#define VSEND(i, s, val, v)                                                        \
+  do {                                                                             \
+    int nn_ = vp_neighbours(g, (v), t, ws.w[i], dir, nb, mark);                    \
+    size_t qb_ = ((size_t)(((s) + 1) % 2) * nwin + ws.canon[i]) * nv;              \
+    for (int q_ = 0; q_ < nn_; q_++) {                                             \
+      size_t x_ = qb_ + nb[q_];                                                    \
+      if (qc[x_] == 0 || (reduce == 0 ? (val) < qv[x_] : (val) > qv[x_])) qv[x_] = (val); \
+      qc[x_]++;                                                                    \
+    }                                                                              \
+  } while (0)
+  if (max_steps > 1) { /* AnalysisTask.timeResponse :169 */
+    for (int i = 0; i < nwin; i++) {
+      int c = ws.canon[i];
+      for (size_t v = 0; v < nv; v++) {
+        if (!mem[(size_t)i * nv + v]) continue;
+        size_t li = (size_t)c * nv + v;
+        if (!sset[li]) { /* getOrSetCompValue */
+          sset[li] = 1;
+          st[li] = init == 0 ? g->vs[v].id : ((int32_t)v == sv ? seed_value : init_value);
+        }
+        if (senders == 0 || (int32_t)v == sv) VSEND(i, 0, vp_add(st[li], step_add), (int)v);
+      }
+    }
+    for (int s = 1;; s++) {
+      long totalKeys = 0, votes = 0;
+      for (int i = 0; i < nwin; i++) {
+        int c = ws.canon[i];
+        size_t qb = ((size_t)(s % 2) * nwin + c) * nv;
+        int nl = 0;
+        for (size_t v = 0; v < nv; v++) /* getVerticesWithMessages, WindowLens.scala:149-158 */
+          if (mem[(size_t)i * nv + v] && qc[qb + v] > 0) list[nl++] = (int)v;
+        totalKeys += nl;
+        for (int a = 0; a < nl; a++) {
+          int v = list[a];
+          int64_t m = qv[qb + v];
+          qc[qb + v] = 0; /* clearQueue */
+          size_t li = (size_t)c * nv + v;
+          int64_t cur = st[li];
+          int64_t nx = reduce == 0 ? (m < cur ? m : cur) : (m > cur ? m : cur);
+          if (nx != cur) { st[li] = nx; VSEND(i, s, vp_add(nx, step_add), v); }
+          else votes++;
+        }
+      }
+      *steps = s;
+      if (s == max_steps || totalKeys == votes) break;
+    }
+  }
+#undef VSEND
+  for (int i = 0; i < nwin; i++) {
+    int c = ws.canon[i];
+    size_t k = 0;
+    for (size_t r = 0; r < nv; r++) {
+      int v = g->order[r];
+      if (!mem[(size_t)i * nv + v]) continue;
+      if (k >= cap) goto done;
+      size_t li = (size_t)c * nv + v;
+      ids[(size_t)i * cap + k] = g->vs[v].id;
+      values[(size_t)i * cap + k] = sset[li] ? st[li] : (init == 0 ? g->vs[v].id : ((int32_t)v == sv ? seed_value : init_value));
+      k++;
+    }
+    n_out[i] = k;
+  }
+  rc = 0;
+done:
+  free(mem); free(sset); free(st); free(qv); free(qc); free(nb); free(list); free(mark);
+  return rc;
+}

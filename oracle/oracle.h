@@ -77,6 +77,20 @@ int orc_degree(const orc_graph* g, int64_t t, const int64_t* windows, int nw,
 int orc_diffusion(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int max_steps,
                   int64_t seed_id, uint64_t coin_seed, int coin, int64_t* ids, int32_t* step_out,
                   size_t cap, size_t* n_out, int* steps);
+/* Generic vertex program (VertexVisitor messaging, VertexVisitor.scala:81-166) through the
+ * reference's BSP structure (as orc_cc): Setup (superstep 0, only when maxSteps > 1) sets every
+ * member's state to init (getOrSetCompValue) and the senders (every member, or only the seed)
+ * message their neighbours in direction dir (0 = messageAllOutgoingNeighbors, 1 =
+ * messageAllIngoingNeighbors, 2 = messageAllNeighbours) the value state + step_add (saturating);
+ * superstep s: a member holding messages folds them with reduce (0 = min, 1 = max); if the fold
+ * of its state and that changes the state it keeps it and messages again, else it votes to halt;
+ * halt when every message holder voted, or at s == maxSteps.  init: 0 = own id, 1 = init_value
+ * (seed_value at the seed).  senders: 0 = all members, 1 = the seed.  Per window: every member's
+ * state (ascending id). */
+int orc_vertex_program(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int max_steps,
+                       int dir, int reduce, int init, int senders, int64_t init_value, int64_t seed_id,
+                       int64_t seed_value, int64_t step_add, int64_t* ids, int64_t* values, size_t cap,
+                       size_t* n_out, int* steps);
 int orc_pagerank(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int iters,
                  int64_t* ids, double* pr, size_t cap, size_t* n_out);
 

@@ -16,7 +16,7 @@ BUILD_DIR = os.path.join(_HERE, "_build")
 RGPU_OK = 0
 RGPU_EINVAL, RGPU_ESTATE, RGPU_EHIP, RGPU_ENOMEM, RGPU_ENOTSUP = -1, -2, -3, -4, -5
 RGPU_VADD, RGPU_VDEL, RGPU_EADD, RGPU_EDEL = 0, 1, 2, 3
-RGPU_ALGO_CC, RGPU_ALGO_DEGREE, RGPU_ALGO_PR, RGPU_ALGO_DIFFUSION = 0, 1, 2, 3
+RGPU_ALGO_CC, RGPU_ALGO_DEGREE, RGPU_ALGO_PR, RGPU_ALGO_DIFFUSION, RGPU_ALGO_VP = 0, 1, 2, 3, 4
 RGPU_RUN_RETAIN, RGPU_RUN_PROFILE, RGPU_RUN_SERIAL, RGPU_RUN_EDGE_COUNTS = 1, 2, 4, 8
 RGPU_XCHG_ID_BYTES, RGPU_XCHG_RCCL, RGPU_XCHG_LOOPBACK = 128, 0, 1
 RGPU_ORDER_LOCALITY, RGPU_ORDER_ID = 0, 1
@@ -28,7 +28,7 @@ ERROR_NAMES = {
     RGPU_ENOTSUP: "RGPU_ENOTSUP",
 }
 KERNEL_NAMES = ["window_mask", "cc_slots", "cc_step", "cc_hist", "cc_summary", "pr_step", "degree", "cc_tail",
-                "heavy", "diffusion", "-", "-"]
+                "heavy", "diffusion", "vp_step", "-"]
 
 # exported symbols of librgpu.so, exactly the declarations of include/rgpu.h
 EXPORTS = [
@@ -38,6 +38,7 @@ EXPORTS = [
     "rgpu_stats", "rgpu_last_error", "rgpu_close",
     "rgpu_rgev_encode", "rgpu_rgev_decode", "rgpu_rgev_last_error", "rgpu_ingest_rgev",
     "rgpu_set_diffusion", "rgpu_diffusion_result", "rgpu_diffusion_vertex", "rgpu_set_vertex_order",
+    "rgpu_set_vertex_program", "rgpu_vp_result", "rgpu_vp_supersteps",
 ]
 
 
@@ -49,6 +50,11 @@ class CCSummary(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "biggest", "total", "total_without_islands", "total_islands", "clusters_gt2",
         "sum_all", "sum_without_islands", "supersteps", "alive_edges")]
+
+
+class VertexProgram(C.Structure):
+    _fields_ = [("direction", C.c_int32), ("reduce", C.c_int32), ("init", C.c_int32), ("senders", C.c_int32),
+                ("init_value", C.c_int64), ("seed_id", C.c_int64), ("seed_value", C.c_int64), ("step_add", C.c_int64)]
 
 
 class Stats(C.Structure):
@@ -88,6 +94,9 @@ _SIGS = {
     "rgpu_degree_vertex": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P32, _P32, _SZ, C.POINTER(_SZ)]),
     "rgpu_pr_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _PD, _SZ, C.POINTER(_SZ)]),
     "rgpu_set_diffusion": (C.c_int, [_CTX, C.c_int64, C.c_uint64, C.c_int]),
+    "rgpu_set_vertex_program": (C.c_int, [_CTX, C.POINTER(VertexProgram)]),
+    "rgpu_vp_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P64, _SZ, C.POINTER(_SZ)]),
+    "rgpu_vp_supersteps": (C.c_int, [_CTX, _SZ, _P64]),
     "rgpu_diffusion_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P64]),
     "rgpu_diffusion_vertex": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P32, _SZ, C.POINTER(_SZ)]),
     "rgpu_stats": (C.c_int, [_CTX, C.POINTER(Stats)]),

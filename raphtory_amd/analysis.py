@@ -295,6 +295,69 @@ class BinaryDefusion(Analyser):
             self.lines.append(json.dumps({"time": timestamp, "windowsize": w, "infected": end, "size": len(end)}))
 
 
+class VertexProgram(Analyser):
+    """A user Analyser written against the VertexVisitor messaging surface (VertexVisitor.scala:
+    81-166) whose analyse() folds its message queue with min or max — run on the GPU as a vertex
+    program (include/rgpu.h rgpu_set_vertex_program, raphtory_amd/csrc/vp.hip):
+
+        setup():   setCompValue(key, init); if sender: messageAll<direction>(state + step_add)
+        analyse(): m = fold(messageQueue); if fold(state, m) != state: setCompValue(key, that);
+                   messageAll<direction>(that + step_add) else voteToHalt()
+
+    ``returnResults`` gives {id: state} for the view's members; the lines list the members whose
+    state differs from ``init_value`` (or every member for init="id")."""
+    algo = "vp"
+
+    def __init__(self, args: Sequence[str] = (), direction: str = "all", reduce: str = "min", init: str = "id",
+                 senders: str = "all", init_value: int = 0, seed_id: int = -1, seed_value: int = 0,
+                 step_add: int = 0, max_steps: int = 100):
+        super().__init__(args)
+        self.program = dict(direction=direction, reduce=reduce, init=init, senders=senders, init_value=init_value,
+                            seed_id=seed_id, seed_value=seed_value, step_add=step_add)
+        self.max_steps = max_steps
+
+    def defineMaxSteps(self) -> int:  # noqa: N802
+        return self.max_steps
+
+    def prepare(self, graph) -> None:
+        graph.set_vertex_program(**self.program)
+
+    def returnResults(self, graph, hop, win):  # noqa: N802
+        ids, vals = graph.vp_result(hop, win)
+        return dict(zip(ids.tolist(), vals.tolist()))
+
+    def _line(self, results, timestamp, window=None) -> str:
+        merged: Dict[int, int] = {}
+        for part in results:
+            merged.update(part)
+        keep = merged if self.program["init"] == "id" else \
+            {k: v for k, v in merged.items() if v != self.program["init_value"]}
+        d = {"time": timestamp}
+        if window is not None:
+            d["windowsize"] = window
+        d.update({"vertices": len(merged), "reached": len(keep), "states": sorted(keep.items())})
+        return json.dumps(d)
+
+    def processResults(self, results, timestamp, viewCompleteTime):  # noqa: N802
+        self.lines.append(self._line(results, timestamp))
+
+    def processWindowResults(self, results, timestamp, windowSize, viewCompleteTime):  # noqa: N802
+        self.lines.append(self._line(results, timestamp, windowSize))
+
+    def processBatchWindowResults(self, results, timestamp, windowSet, viewCompleteTime):  # noqa: N802
+        for i, window in enumerate(results):
+            self.lines.append(self._line(window, timestamp, windowSet[i]))
+
+
+class HopDistance(VertexProgram):
+    """Out-edge hop distance from a seed vertex (a taint / reachability analyser, as the
+    reference's example BinaryDefusion spreads from infectedNode, without its coin)."""
+
+    def __init__(self, args: Sequence[str] = (), seed_id: int = 31, direction: str = "out", max_steps: int = 100):
+        super().__init__(args, direction=direction, reduce="min", init="value", senders="seed",
+                         init_value=2**63 - 1, seed_id=seed_id, seed_value=0, step_add=1, max_steps=max_steps)
+
+
 # ---------------------------------------------------------------- tasks
 class TimeNotIngested(RuntimeError):
     """TimeCheck failed (ReaderWorker.processTimeCheckRequest :259-274); the reference retries in 10 s."""
@@ -340,7 +403,7 @@ class AnalysisTask:
         for g in self.graphs:
             if hasattr(a, "prepare"):
                 a.prepare(g)
-            g.run(a.algo, hops, windows, max_steps=max_steps if a.algo in ("cc", "diffusion") else 100,
+            g.run(a.algo, hops, windows, max_steps=max_steps if a.algo in ("cc", "diffusion", "vp") else 100,
                   pr_iters=max_steps if a.algo == "pagerank" else 0, retain=self.retain)
         self.view_ms = (time.perf_counter() - t0) * 1e3 / max(1, len(hops))
         vt = int(round(self.view_ms))
@@ -472,7 +535,7 @@ class LiveAnalysisTask(AnalysisTask):
         for g in self.graphs:
             if hasattr(a, "prepare"):
                 a.prepare(g)
-            g.run(a.algo, [ts], [], max_steps=max_steps if a.algo in ("cc", "diffusion") else 100,
+            g.run(a.algo, [ts], [], max_steps=max_steps if a.algo in ("cc", "diffusion", "vp") else 100,
                   pr_iters=max_steps if a.algo == "pagerank" else 0, retain=self.retain)
         vt = int(round((time.perf_counter() - t0) * 1e3))
         a.processResults([a.returnResults(g, 0, 0) for g in self.graphs], ts, vt)

@@ -186,17 +186,34 @@ struct HopLDS {
   int64_t hop[kViews];
   int64_t thr[kViews];
   int K, W, KS;
+  int64_t jump;  // > 0: hop[k] = hop[0] + k * jump (a Range job's hops; hop_lb is arithmetic)
+  double inv;    // 1 / jump
 };
 __device__ __forceinline__ void hop_lds_init(HopLDS& L, const BatchParams& bp, const int64_t* thr) {
   if (threadIdx.x < kViews) {
     L.hop[threadIdx.x] = bp.hop[threadIdx.x];
     L.thr[threadIdx.x] = thr[threadIdx.x];
   }
-  if (threadIdx.x == 0) { L.K = bp.K; L.W = bp.W; L.KS = bp.KS; }
+  if (threadIdx.x == 0) {
+    L.K = bp.K; L.W = bp.W; L.KS = bp.KS;
+    L.jump = bp.jump;
+    L.inv = bp.jump > 0 ? 1.0 / (double)bp.jump : 0.0;
+  }
   __syncthreads();
 }
-// first hop index with hop >= x (K if none)
+// first hop index with hop >= x (K if none).  Evenly spaced hops (every Range job's hops but a
+// clamped last one): ceil((x - hop0) / jump) from a double product, corrected by one integer
+// compare each way (exact: |x - hop0| < 2^53) — no dependent LDS probes.
 __device__ __forceinline__ int hop_lb(const HopLDS& L, int64_t x) {
+  if (L.jump > 0) {
+    const int64_t d = x - L.hop[0];
+    if (d <= 0) return 0;
+    if (x > L.hop[L.K - 1]) return L.K;
+    int64_t k = (int64_t)((double)d * L.inv);
+    if (k * L.jump < d) k++;
+    if (k > 0 && (k - 1) * L.jump >= d) k--;
+    return (int)k;
+  }
   int a = 0, b = L.K;
   while (a < b) {
     const int m = (a + b) >> 1;
@@ -1091,7 +1108,7 @@ __global__ __launch_bounds__(256) void k_uw_rows(int64_t nv, const uint64_t* __r
 // Superstep kernel (full grid).  Step r visits the vertices flagged in act_cur (bytes, plain
 // idempotent stores by step r-1), CH consecutive ranks per wave-chunk, and clears act_clear
 // (read two steps ago, written next step).
-// MINW > 1: amdgpu_waves_per_eu(MINW) (a VGPR cap; RGPU_STEP_VARIANT | 64 selects 6 waves/SIMD)
+// MINW > 1: amdgpu_waves_per_eu(MINW) (a VGPR cap; a 6-wave cap measured slower)
 template <int CH, bool BUF, int MINW, bool PROF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void k_cc_step2(int step, int64_t nv, const int64_t* __restrict__ adj_off,
                                                   const uint64_t* __restrict__ vm,
@@ -2249,7 +2266,6 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
-int g_rowbuf = 0;
 int g_sum_blocks = 32;  // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 int g_hist_rounds = 4;  // (C2: 64 rounds 145 ms, 4 rounds 138 ms; 1 round 147 ms)
 int g_tail_step = 14;
@@ -2316,26 +2332,20 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, int variant, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next,
                     const ChgBits& cb, int32_t* ccount, int dense_div) {
-  const int ch = (variant & 15) == 8 ? 8 : 4;  // (variant & 96: VGPR caps, see k_cc_step2)
-  const bool buf = (variant & 16) != 0;
+  (void)variant;  // (8-vertex chunks, buffer-descriptor rows and a VGPR-capped build measured slower: removed)
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
   // A small graph's dense supersteps are latency-bound and share the GPU with the other batch
   // slots too: a 1,024-block cap measured 4 % faster on C2 (100k vertices) and 2 % slower on a
   // 4.7M-vertex C4-shaped graph, hence the size rule (RGPU_STEP_GRID overrides it).
   const unsigned full = g_step_grid > 0 ? (unsigned)g_step_grid : (g.nv <= ((int64_t)1 << 21) ? 1024u : 4096u);
   const unsigned cap = step >= g_tail_step ? (full < (unsigned)g_tail_grid ? full : (unsigned)g_tail_grid) : full;
-  const unsigned grid = grid_for(g.nv, 4 * ch, cap);
+  const unsigned grid = grid_for(g.nv, 16, cap);
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
     cb.next, cb.clear, cb.words, ccount, dense_div
   // work != null (profile runs): the counting instantiation; the timed runs use the lean one
-  if (ch == 8 && buf) k_cc_step2<8, true, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else if (ch == 8) k_cc_step2<8, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else if (buf) k_cc_step2<4, true, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else if ((variant & 64) && work) k_cc_step2<4, false, 6, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else if (variant & 64) k_cc_step2<4, false, 6, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else if (work) k_cc_step2<4, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  if (work) k_cc_step2<4, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else k_cc_step2<4, false, 1, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
 #undef RGPU_STEP_ARGS
 }
@@ -2376,15 +2386,13 @@ void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g,
   cap = cap < kTailListCap ? cap : kTailListCap;
 #define RGPU_TAIL_ARGS r0, rmax, cap, g.nv, g.adj_off, vm, cnt, snbr, smask, lab0, lab1, chg0, chg1, act0, act1, \
     act2, stepflag, hostflag, info, work, lanechg
-  if (g_rowbuf) k_cc_tail<true><<<1, kTailThreads, 0, s>>>(RGPU_TAIL_ARGS);
-  else k_cc_tail<false><<<1, kTailThreads, 0, s>>>(RGPU_TAIL_ARGS);
+  k_cc_tail<false><<<1, kTailThreads, 0, s>>>(RGPU_TAIL_ARGS);
 #undef RGPU_TAIL_ARGS
 }
 void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, const uint64_t* vm,
                     const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso) {
   const unsigned grid = grid_for(nv, 64, 8192);
-  if (g_rowbuf) k_cc_hist<true><<<grid, 512, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso, g_hist_rounds);
-  else k_cc_hist<false><<<grid, 512, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso, g_hist_rounds);
+  k_cc_hist<false><<<grid, 512, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso, g_hist_rounds);
 }
 void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
                        unsigned long long* stats, unsigned int* iso) {

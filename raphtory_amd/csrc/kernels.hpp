@@ -31,6 +31,7 @@ struct BatchParams {
   int64_t hop[kViews];    // view timestamps (RangeAnalysisTask hop times)
   int64_t thr_v[kViews];  // vertex-set window of window index w: min(w_0..w_w)  (shrinkWindow)
   int64_t thr_e[kViews];  // edge window of window index w: w_w (viewAtWithWindow(t, setWindow))
+  int64_t jump;           // > 0: hop[k] = hop[0] + k * jump for every k < K (K1's arithmetic hop search)
 };
 
 // Sealed partition resident in HBM.
@@ -143,7 +144,6 @@ void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, co
 extern int g_sum_blocks;   // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 extern int g_hist_rounds;  // label-dedup rounds per (view, chunk) in k_cc_hist (RGPU_HIST_ROUNDS)
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
-extern int g_rowbuf;     // label rows via buffer descriptors (RGPU_ROWBUF)
 extern int g_tail_step, g_tail_grid;  // supersteps >= tail_step use at most tail_grid blocks
 // uniform label words (kernels.hip, kMixed): rows of the uniform vertices written into lab
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab);
@@ -213,6 +213,21 @@ void launch_pr_slots(hipStream_t s, const DevGraph& g, const uint64_t* vm, const
 void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,
                     const int32_t* outdeg, const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const double* contrib_cur, double* contrib_next, double* pr, double* hacc);
+
+// Generic vertex programs (vp.hip; include/rgpu.h rgpu_vertex_program_t): direction 0 out / 1 in /
+// 2 all, reduce 0 min / 1 max, init 0 own id / 1 init_value (seed_value at the seed), senders 0 all
+// members / 1 the seed; seed_rank = the seed's local rank (-1: none)
+struct VpParams {
+  int32_t dir = 2, reduce = 0, init = 0, senders = 0;
+  int64_t init_value = 0, seed_rank = -1, seed_value = 0, step_add = 0;
+};
+void launch_vp_setup(hipStream_t s, const DevGraph& g, const VpParams& p, const int64_t* vid, const uint64_t* vm,
+                     const uint64_t* em, int32_t* cnt, int32_t* snbr, uint64_t* smask, int64_t* st0, uint64_t* chg0);
+void launch_vp_go(hipStream_t s, int32_t* stepflag);
+void launch_vp_step(hipStream_t s, int step, const DevGraph& g, const VpParams& p, const uint64_t* vm,
+                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, const int64_t* st_cur,
+                    int64_t* st_next, const uint64_t* chg_prev, uint64_t* chg_next, int32_t* stepflag,
+                    int32_t* hostflag, unsigned long long* lanechg);
 
 // BinaryDefusion (diffusion.hip): per-lane coin salts of a batch (view j -> (hop, window))
 struct DiffSalts {

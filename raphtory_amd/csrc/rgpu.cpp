@@ -43,7 +43,7 @@ struct HipFail {
   } while (0)
 
 enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUMMARY = 4,
-                KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_HEAVY = 8, KID_DIFF = 9, KID_N = 12 };
+                KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_HEAVY = 8, KID_DIFF = 9, KID_VP = 10, KID_N = 12 };
 
 constexpr int kMaxSteps = 128;
 // stats words: 6 per-view fields + counters row | folded lane words [step] | lane-change shards
@@ -59,7 +59,8 @@ constexpr int kMaxSlots = 4;  // batches in flight (one HIP stream each; GPU_MAX
 
 struct Slot {
   // buffers allocated for this slot (slots are allocated lazily: a run uses min(slots, batches))
-  bool a_cc = false, a_deg = false, a_pr = false, h_cc = false, h_pr = false, a_diff = false;
+  bool a_cc = false, a_deg = false, a_pr = false, h_cc = false, h_pr = false, a_diff = false, a_vp = false;
+  int64_t* vst[2] = {nullptr, nullptr};  // vertex program state rows [nv][64] (int64), Jacobi
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   uint64_t *vm = nullptr, *em = nullptr;          // masks of the batch in flight
@@ -106,6 +107,7 @@ struct Slot {
 
 struct Retained {  // per batch, RGPU_RUN_RETAIN
   std::vector<uint64_t> vm;
+  std::vector<int64_t> v64;   // vertex program: states
   std::vector<int32_t> a, b;  // CC: labels | degree: out, in
   std::vector<double> pr;
   std::vector<uint8_t> st;    // diffusion: infection superstep per (vertex, lane), 0xFF = none
@@ -187,11 +189,8 @@ struct rgpu_ctx {
   Slot slot[kMaxSlots];
   int nslots = 2;
   bool hostflags = true;                // superstep flags via host-mapped memory (else copies)
-  int step_variant = 0;                 // RGPU_STEP_VARIANT: 0 per-vertex chain, 1 chunk-pipelined
   bool tail_on = false;                 // RGPU_TAIL: late supersteps in one-workgroup k_cc_tail launches
   bool uw_on = true;                    // RGPU_UW: uniform label words (one partition, no tail kernel)
-  bool ends_on = false;                 // RGPU_EMENDS=1: K1 folds endpoint memberships into CC edge words
-                                        // (measured slower on C4: K1 55 -> 97 ms for K2 122 -> 117 ms)
   bool prof_lean = false;               // RGPU_PROF_LEAN (work_buf)
   int inject_fail = 0;                  // RGPU_INJECT_FAIL=n (tests): the n-th batch start of a run throws
   int dense = -1;                       // RGPU_DENSE: dense-step divisor (kernels.hip dense_rule; -1 by size)
@@ -220,6 +219,10 @@ struct rgpu_ctx {
   struct TopEnt { int64_t id; int32_t out, in; };
   std::vector<TopEnt> degtop;  // [view][kTop] (id -1: none)
   std::vector<int64_t> dcount, dsteps;  // diffusion: infected vertices, supersteps per view
+  VpParams vp;                          // rgpu_set_vertex_program
+  int64_t vp_seed_id = -1;
+  bool vp_set = false;
+  std::vector<int64_t> vpsteps;         // vertex program: supersteps per hop (as CC)
   int64_t diff_seed = 31;               // BinaryDefusion.infectedNode (BinaryDefusion.scala:10)
   uint64_t diff_coin_seed = 0;
   int diff_coin = 1;
@@ -489,6 +492,15 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       s.hv.pacc = dalloc<double>(LG, (size_t)c->g.n_heavy * kViews);  // zero between uses
       HIPCHK(hipMemset(s.hv.pacc, 0, sizeof(double) * (size_t)c->g.n_heavy * kViews));
     }
+    if (algo == RGPU_ALGO_VP && !s.a_vp) {
+      if (!s.cnt) s.cnt = dalloc<int32_t>(L, nv + kPad);
+      if (!s.snbr) s.snbr = dalloc<int32_t>(L, ne + nin + kPad);
+      if (!s.smask) s.smask = dalloc<uint64_t>(L, ne + nin + kPad);
+      for (int b = 0; b < 2; b++) {
+        if (!s.chg[b]) s.chg[b] = dalloc<uint64_t>(L, nv + kPad);
+        s.vst[b] = dalloc<int64_t>(L, rows);
+      }
+    }
     if (algo == RGPU_ALGO_DIFFUSION && !s.a_diff) {
       s.dinf = dalloc<uint64_t>(L, nv + kPad);
       s.dfront[0] = dalloc<uint64_t>(L, nv + kPad);
@@ -518,8 +530,9 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
     if (algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_PR) s.a_deg = true;
     if (algo == RGPU_ALGO_PR) s.a_pr = true;
     if (algo == RGPU_ALGO_DIFFUSION) s.a_diff = true;
+    if (algo == RGPU_ALGO_VP) s.a_vp = true;
   }
-  if (algo == RGPU_ALGO_DIFFUSION && !c->d_vid) c->d_vid = dalloc<int64_t>(L, nv);
+  if ((algo == RGPU_ALGO_DIFFUSION || algo == RGPU_ALGO_VP) && !c->d_vid) c->d_vid = dalloc<int64_t>(L, nv);
 }
 
 struct RunCfg {
@@ -578,6 +591,14 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
   }
   const bool uw = use_uw(c);
   for (int r = s.r_launched + 1; r <= last; r++) {
+    if (rc.algo == RGPU_ALGO_VP) {
+      timed_launch(c, si, KID_VP, 0.0, [&] {
+        launch_vp_step(s.stream, r, g, c->vp, s.vm, s.cnt, s.snbr, s.smask, s.vst[(r - 1) & 1], s.vst[r & 1],
+                       s.chg[(r - 1) & 1], s.chg[r & 1], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
+                       s.stats + kLaneOff);
+      }, r, false);
+      continue;
+    }
     if (rc.algo == RGPU_ALGO_DIFFUSION) {
       timed_launch(c, si, KID_DIFF, 0.0, [&] {
         launch_diff_step(s.stream, r, g, c->d_vid, s.vm, s.em, s.dinf, s.dfront[(r - 1) & 1], s.dfront[r & 1],
@@ -597,7 +618,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                      s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
                      s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
-                     work_buf(c, s), c->step_variant | (g_rowbuf ? 16 : 0), s.stats + kLaneOff,
+                     work_buf(c, s), 0, s.stats + kLaneOff,
                      hv ? s.hv.best : nullptr, uw ? s.uw[(r - 1) & 1] : nullptr, uw ? s.uw[r & 1] : nullptr,
                      chg_bits(c, s, r), s.ccount, dense_div(c));
     }, r, per_launch);
@@ -609,7 +630,8 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
   }
   if (ea) {
     HIPCHK(hipEventRecord(eb, s.stream));
-    c->timed.push_back({rc.algo == RGPU_ALGO_DIFFUSION ? KID_DIFF : KID_STEP, si, s.batch, s.r_launched + 1, ea, eb, 0.0});
+    c->timed.push_back({rc.algo == RGPU_ALGO_DIFFUSION ? KID_DIFF : rc.algo == RGPU_ALGO_VP ? KID_VP : KID_STEP, si,
+                        s.batch, s.r_launched + 1, ea, eb, 0.0});
   }
   s.r_launched = last;
   if (rc.algo == RGPU_ALGO_CC && c->tail_on && g.n_seg == 0 && g.nv <= c->tail_maxv &&
@@ -641,7 +663,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
 void finish_tail(rgpu_ctx* c, int si, const RunCfg& rc) {
   Slot& s = c->slot[si];
   const DevGraph& g = c->g;
-  if (rc.algo == RGPU_ALGO_CC) launch_lane_fold(s.stream, s.stats + kLaneOff, s.stats + kFoldOff);
+  if (rc.algo == RGPU_ALGO_CC || rc.algo == RGPU_ALGO_VP) launch_lane_fold(s.stream, s.stats + kLaneOff, s.stats + kFoldOff);
   HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatCopy,
                         hipMemcpyDeviceToHost, s.stream));
   if (rc.algo == RGPU_ALGO_DEGREE) {  // the top-20 lists
@@ -661,6 +683,10 @@ void finish_tail(rgpu_ctx* c, int si, const RunCfg& rc) {
       R.a.resize(rows);
       HIPCHK(hipMemcpyAsync(R.a.data(), s.lab[s.r_final & 1], sizeof(int32_t) * rows,
                             hipMemcpyDeviceToHost, s.stream));
+    } else if (rc.algo == RGPU_ALGO_VP) {
+      R.v64.resize(rows);
+      HIPCHK(hipMemcpyAsync(R.v64.data(), s.vst[s.r_final & 1], sizeof(int64_t) * rows, hipMemcpyDeviceToHost,
+                            s.stream));
     } else if (rc.algo == RGPU_ALGO_DIFFUSION) {
       R.st.resize(rows);
       HIPCHK(hipMemcpyAsync(R.st.data(), s.dstep, rows, hipMemcpyDeviceToHost, s.stream));
@@ -730,6 +756,17 @@ bool can_start(const rgpu_ctx* c, size_t b, const RunCfg& rc) {
   return c->mset[(b / rc.G) % kMaskSets].pending == 0;  // set still read by an older block
 }
 
+// the hops' common step when a block's hops are evenly spaced (K1 then finds hop indices
+// arithmetically), else 0
+int64_t even_jump(const BatchParams& bp) {
+  if (bp.K < 2 || !bp.sorted) return 0;
+  const int64_t j = bp.hop[1] - bp.hop[0];
+  if (j <= 0 || j > ((int64_t)1 << 40)) return 0;
+  for (int k = 2; k < bp.K; k++)
+    if (bp.hop[k] - bp.hop[k - 1] != j) return 0;
+  return j;
+}
+
 void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   Slot& s = c->slot[si];
   const DevGraph& g = c->g;
@@ -749,6 +786,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     bp.hop[k] = rc.hops[h0 + k];
     if (k > 0 && bp.hop[k] < bp.hop[k - 1]) bp.sorted = 0;
   }
+  bp.jump = even_jump(bp);
   for (int w = 0; w < rc.W; w++) { bp.thr_v[w] = rc.thr_v[w]; bp.thr_e[w] = rc.thr_e[w]; }
   // K2's cut: an edge is kept only where its floor point is an add no older than the window
   // (age <= thr_e), so one whose last add is before min(hop) - max(window of the batch) is
@@ -795,9 +833,9 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   // the ghosts' words arrive from their owners right after
   DevGraph gk = g;
   if (c->partitioned) gk.nv = c->pk.n_own;
-  // CC, one partition: K1 folds both endpoints' memberships into the edge words (a ghost's
-  // membership arrives after K1 in the partitioned mode); RGPU_EMENDS=0 turns it off
-  const bool ends = rc.algo == RGPU_ALGO_CC && !c->partitioned && c->ends_on;
+  // (K1 folding both endpoints' memberships into the CC edge words measured slower on C4: K1 55 ->
+  // 97 ms for K2 122 -> 117 ms; the kernels keep the path, off)
+  const bool ends = false;
   if (rc.G == 1) {
     s.vm = s.vm_own;
     s.em = s.em_own;
@@ -826,6 +864,20 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     s.em = M.em + (size_t)grp * g.ne;
     launch_batch_clear(s.stream, clr);
     HIPCHK(hipGetLastError());
+  }
+  if (rc.algo == RGPU_ALGO_VP) {  // setup (superstep 0), only when maxSteps > 1 (AnalysisTask.timeResponse :169)
+    launch_vp_setup(s.stream, g, c->vp, c->d_vid, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vst[0], s.chg[0]);
+    HIPCHK(hipGetLastError());
+    s.r_launched = 0;
+    if (rc.max_steps <= 1) {
+      s.r_final = 0;
+      finish_batch(c, si, rc);
+    } else {
+      launch_vp_go(s.stream, s.stepcnt);
+      const int last = c->grp_last[grp];
+      launch_chunk(c, si, rc, last > 0 ? std::max(2, std::min(rc.chunk0, last + 1)) : rc.chunk0);
+    }
+    return;
   }
   if (rc.algo == RGPU_ALGO_DIFFUSION) {
     // coin salts: lane j = wl*K + k is hop h0 + k, window grp*gsize + wl (include/rgpu.h)
@@ -919,7 +971,7 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
   const size_t hb = (size_t)s.batch / rc.G;
   const int grp = s.batch % rc.G;
   int32_t last[kViews] = {};  // per lane: last superstep with a label change (0: none)
-  if (rc.algo == RGPU_ALGO_CC)
+  if (rc.algo == RGPU_ALGO_CC || rc.algo == RGPU_ALGO_VP)
     for (int r = 1; r <= s.r_final && r < kMaxSteps; r++)
       for (unsigned long long m = h[kFoldOff + r]; m; m &= m - 1) last[__builtin_ctzll(m)] = r;
   for (int k = 0; k < s.kb; k++)
@@ -951,6 +1003,8 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
       } else if (rc.algo == RGPU_ALGO_DIFFUSION) {
         c->dcount[view] = (int64_t)h[j];
         c->dsteps[view] = s.r_final;
+      } else if (rc.algo == RGPU_ALGO_VP) {
+        c->vlast[view] = last[j];
       }
     }
   if (rc.algo == RGPU_ALGO_CC) {
@@ -989,6 +1043,10 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
         for (int r = 1; r <= s.r_final; r++)
           c->steprec.push_back({s.batch, r, wsum(r, 0), wsum(r, 1), (int)wsum(r, 2), wsum(r, 3)});
     }
+    c->st.supersteps += s.r_final;
+    c->grp_last[grp] = s.r_final;
+  }
+  if (rc.algo == RGPU_ALGO_VP) {
     c->st.supersteps += s.r_final;
     c->grp_last[grp] = s.r_final;
   }
@@ -1324,7 +1382,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   timed_launch(c, si, KID_STEP, 0.0, [&] {
     launch_cc_step(s.stream, n, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[r & 1], s.lab[n & 1], s.chg[r & 1],
                    s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
-                   work_buf(c, s), c->step_variant, s.stats + kLaneOff, hv ? s.hv.best : nullptr,
+                   work_buf(c, s), 0, s.stats + kLaneOff, hv ? s.hv.best : nullptr,
                    use_uw(c) ? s.uw[r & 1] : nullptr, use_uw(c) ? s.uw[n & 1] : nullptr, chg_bits(c, s, n), s.ccount,
                    dense_div(c));
   }, n);
@@ -1504,6 +1562,7 @@ int run_partitioned_dp(rgpu_ctx* c, RunCfg& rc) {
       bp.hop[k] = rc.hops[h0 + k];
       if (k > 0 && bp.hop[k] < bp.hop[k - 1]) bp.sorted = 0;
     }
+    bp.jump = even_jump(bp);
     for (int w = 0; w < rc.W; w++) { bp.thr_v[w] = rc.thr_v[w]; bp.thr_e[w] = rc.thr_e[w]; }
     s.batch = (int)b;
     s.kb = bp.K;
@@ -1643,11 +1702,9 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->device = device;
   c->partitioned = num_partitions > 1 || env_int("RGPU_PARTITIONED", 0) != 0;
   c->nslots = std::max(1, std::min(kMaxSlots, env_int("RGPU_SLOTS", 3)));
-  c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   if (env_int("RGPU_STEP_GRID", 0) > 0) g_step_grid = env_int("RGPU_STEP_GRID", 0);
   if (env_int("RGPU_HIST_ROUNDS", 0) > 0) g_hist_rounds = env_int("RGPU_HIST_ROUNDS", 0);
   if (env_int("RGPU_SUMMARY_BLOCKS", 0) > 0) g_sum_blocks = env_int("RGPU_SUMMARY_BLOCKS", 0);
-  g_rowbuf = env_int("RGPU_ROWBUF", 0);
   if (env_int("RGPU_TAIL_STEP", 0) > 0) g_tail_step = env_int("RGPU_TAIL_STEP", 0);
   if (env_int("RGPU_TAIL_GRID", 0) > 0) g_tail_grid = env_int("RGPU_TAIL_GRID", 0);
   c->hostflags = env_int("RGPU_HOSTFLAG", 1) != 0;
@@ -2144,13 +2201,14 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   if (!c->sealed) return fail(c, RGPU_ESTATE, "rgpu_run_view_batch before rgpu_seal");
   if (c->partitioned && !c->pt.xchg)
     return fail(c, RGPU_ESTATE, "partitioned context: call rgpu_exchange_init before running");
-  if (algo < RGPU_ALGO_CC || algo > RGPU_ALGO_DIFFUSION) return fail(c, RGPU_EINVAL, "unknown algo");
-  if (algo == RGPU_ALGO_DIFFUSION && c->partitioned)
-    return fail(c, RGPU_EINVAL, "diffusion runs need one partition");
+  if (algo < RGPU_ALGO_CC || algo > RGPU_ALGO_VP) return fail(c, RGPU_EINVAL, "unknown algo");
+  if ((algo == RGPU_ALGO_DIFFUSION || algo == RGPU_ALGO_VP) && c->partitioned)
+    return fail(c, RGPU_EINVAL, "diffusion and vertex-program runs need one partition");
+  if (algo == RGPU_ALGO_VP && !c->vp_set) return fail(c, RGPU_ESTATE, "rgpu_set_vertex_program before a vertex-program run");
   if (!hops || n_hops == 0) return fail(c, RGPU_EINVAL, "no hops");
   if (n_w > (size_t)kViews) return fail(c, RGPU_EINVAL, "more than 64 windows in one batch");
   if (n_w && !windows) return fail(c, RGPU_EINVAL, "null window array");
-  if ((algo == RGPU_ALGO_CC || algo == RGPU_ALGO_DIFFUSION) && max_steps > kMaxSteps - 1)
+  if ((algo == RGPU_ALGO_CC || algo == RGPU_ALGO_DIFFUSION || algo == RGPU_ALGO_VP) && max_steps > kMaxSteps - 1)
     return fail(c, RGPU_EINVAL, "max_steps above 127");
   if (algo == RGPU_ALGO_PR && (pr_iters < 0 || pr_iters > 100000))
     return fail(c, RGPU_EINVAL, "bad pr_iters");
@@ -2192,12 +2250,10 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   rc.chunk = std::max(1, env_int("RGPU_CHUNK", 8));
   // superstep launch knobs are re-read per run, so that one sealed graph can be A/B-timed
   // under several settings in one process (tools/c4_ab.py); unset = the defaults
-  c->step_variant = env_int("RGPU_STEP_VARIANT", 4);
   c->cb_on = env_int("RGPU_CHGBITS", 1);
   c->prof_lean = env_int("RGPU_PROF_LEAN", 0) != 0;
   c->inject_fail = env_int("RGPU_INJECT_FAIL", 0);
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
-  c->ends_on = env_int("RGPU_EMENDS", 0) != 0;
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
   g_tail_step = std::max(2, env_int("RGPU_TAIL_STEP", 14));
   g_tail_grid = std::max(1, env_int("RGPU_TAIL_GRID", 1024));
@@ -2223,7 +2279,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     for (int& x : c->grp_last) x = 0;
     c->n_hops = n_hops;
     c->cc.assign(algo == RGPU_ALGO_CC ? n_hops * rc.W : 0, rgpu_cc_summary_t{});
-    c->vlast.assign(algo == RGPU_ALGO_CC ? n_hops * rc.W : 0, 0);
+    c->vlast.assign((algo == RGPU_ALGO_CC || algo == RGPU_ALGO_VP) ? n_hops * rc.W : 0, 0);
     c->st.alive_edge_windows = -1;
     if (c->d_ecnt) { (void)hipFree(c->d_ecnt); c->d_ecnt = nullptr; }
     if (flags & RGPU_RUN_EDGE_COUNTS) {
@@ -2234,15 +2290,17 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->degtop.assign(algo == RGPU_ALGO_DEGREE ? n_hops * rc.W * kTop : 0, rgpu_ctx::TopEnt{-1, 0, 0});
     c->dcount.assign(algo == RGPU_ALGO_DIFFUSION ? n_hops * rc.W : 0, 0);
     c->dsteps.assign(algo == RGPU_ALGO_DIFFUSION ? n_hops * rc.W : 0, 0);
-    if (algo == RGPU_ALGO_DIFFUSION) {
+    if (algo == RGPU_ALGO_DIFFUSION || algo == RGPU_ALGO_VP) {
       // the seed's rank by binary search over the ids in ascending order (-1: not in the graph)
       const auto& vid = c->pk.vid;
+      const int64_t seed = algo == RGPU_ALGO_VP ? c->vp_seed_id : c->diff_seed;
       int64_t a = 0, b = c->pk.n_own;
       while (a < b) {
         const int64_t m = (a + b) / 2;
-        if (vid[own_at(c, m)] < c->diff_seed) a = m + 1; else b = m;
+        if (vid[own_at(c, m)] < seed) a = m + 1; else b = m;
       }
-      c->diff_seed_rank = (a < c->pk.n_own && vid[own_at(c, a)] == c->diff_seed) ? own_at(c, a) : -1;
+      const int64_t rk = (a < c->pk.n_own && vid[own_at(c, a)] == seed) ? own_at(c, a) : -1;
+      if (algo == RGPU_ALGO_VP) c->vp.seed_rank = rk; else c->diff_seed_rank = rk;
       if (c->g.nv) HIPCHK(hipMemcpy(c->d_vid, vid.data(), sizeof(int64_t) * c->g.nv, hipMemcpyHostToDevice));
     }
     c->kept.clear();
@@ -2265,6 +2323,14 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     for (int si = 0; si < kMaxSlots; si++)
       if (c->slot[si].stream) HIPCHK(hipStreamSynchronize(c->slot[si].stream));
     if (algo == RGPU_ALGO_CC) finish_supersteps(c, rc);
+    if (algo == RGPU_ALGO_VP) {  // per hop, as CC's: min(maxSteps, 1 + the last changing step of its windows)
+      c->vpsteps.assign(n_hops, 0);
+      for (size_t hop = 0; hop < n_hops; hop++) {
+        int32_t r = 0;
+        for (int w = 0; w < rc.W; w++) r = std::max(r, c->vlast[hop * rc.W + w]);
+        c->vpsteps[hop] = max_steps <= 1 ? 0 : std::min<int64_t>(max_steps, (int64_t)r + 1);
+      }
+    }
     for (int k = 0; k < 4; k++) c->st.xchg_bytes_by[k] = 0;
     c->st.xchg_bytes_by[3] = c->pt.bytes_sent;
     for (const XSlot& xs : c->pt.xs)
@@ -2498,6 +2564,53 @@ int rgpu_diffusion_vertex(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int
     k++;
   }
   *n = k;
+  return RGPU_OK;
+}
+
+int rgpu_set_vertex_program(rgpu_ctx* c, const rgpu_vertex_program_t* p) {
+  if (!c || !p) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (p->direction < RGPU_VP_OUT || p->direction > RGPU_VP_ALL || p->reduce < RGPU_VP_MIN || p->reduce > RGPU_VP_MAX ||
+      p->init < RGPU_VP_INIT_ID || p->init > RGPU_VP_INIT_VALUE || p->senders < RGPU_VP_SEND_ALL ||
+      p->senders > RGPU_VP_SEND_SEED)
+    return fail(c, RGPU_EINVAL, "bad vertex program");
+  c->vp.dir = p->direction;
+  c->vp.reduce = p->reduce;
+  c->vp.init = p->init;
+  c->vp.senders = p->senders;
+  c->vp.init_value = p->init_value;
+  c->vp.seed_value = p->seed_value;
+  c->vp.step_add = p->step_add;
+  c->vp_seed_id = p->seed_id;
+  c->vp_set = true;
+  return RGPU_OK;
+}
+
+int rgpu_vp_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int64_t* values, size_t cap, size_t* n) {
+  if (!c || !n) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_VP || !c->retained) return fail(c, RGPU_ESTATE, "needs a vertex-program run with RGPU_RUN_RETAIN");
+  size_t b;
+  int j;
+  if (int e = view_index(c, hop, win, &b, &j)) return e;
+  const Retained& R = c->kept[b];
+  size_t k = 0;
+  for (int64_t k_ = 0; k_ < c->pk.n_own; k_++) {
+    const int64_t v = own_at(c, k_);
+    if (!((R.vm[v] >> j) & 1)) continue;
+    if (k < cap) { ids[k] = c->pk.vid[v]; values[k] = R.v64[(size_t)v * kViews + j]; }
+    k++;
+  }
+  *n = k;
+  return RGPU_OK;
+}
+
+int rgpu_vp_supersteps(rgpu_ctx* c, size_t hop, int64_t* supersteps) {
+  if (!c || !supersteps) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_VP) return fail(c, RGPU_ESTATE, "last run was not a vertex program");
+  if (hop >= c->vpsteps.size()) return fail(c, RGPU_EINVAL, "hop index out of range");
+  *supersteps = c->vpsteps[hop];
   return RGPU_OK;
 }
 

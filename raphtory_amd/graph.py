@@ -20,7 +20,9 @@ class RGPUError(RuntimeError):
 
 
 ALGOS = {"cc": N.RGPU_ALGO_CC, "degree": N.RGPU_ALGO_DEGREE, "pagerank": N.RGPU_ALGO_PR,
-         "diffusion": N.RGPU_ALGO_DIFFUSION}
+         "diffusion": N.RGPU_ALGO_DIFFUSION, "vp": N.RGPU_ALGO_VP}
+VP_DIRS = {"out": 0, "in": 1, "all": 2}
+VP_REDUCE = {"min": 0, "max": 1}
 
 
 def _i64(a) -> np.ndarray:
@@ -203,6 +205,23 @@ class TemporalGraph:
         ids, steps = self._sized(self._lib.rgpu_diffusion_vertex, hop, win,
                                  lambda n: ([(np.empty(n, np.int64), C.c_int64), (np.empty(n, np.int32), C.c_int32)], 2))
         return ids, steps
+
+    def set_vertex_program(self, direction: str = "all", reduce: str = "min", init: str = "id", senders: str = "all",
+                           init_value: int = 0, seed_id: int = -1, seed_value: int = 0, step_add: int = 0) -> None:
+        """A generic vertex program for later run("vp", ...) calls (rgpu_set_vertex_program)."""
+        p = N.VertexProgram(VP_DIRS[direction], VP_REDUCE[reduce], 0 if init == "id" else 1,
+                            0 if senders == "all" else 1, init_value, seed_id, seed_value, step_add)
+        self._check(self._lib.rgpu_set_vertex_program(self._ctx, C.byref(p)))
+
+    def vp_result(self, hop: int, win: int) -> Tuple[np.ndarray, np.ndarray]:
+        """(ids, final states) of the view's members, ascending id (needs retain)"""
+        return self._sized(self._lib.rgpu_vp_result, hop, win,
+                           lambda n: ([(np.empty(n, np.int64), C.c_int64), (np.empty(n, np.int64), C.c_int64)], 2))
+
+    def vp_supersteps(self, hop: int) -> int:
+        out = C.c_int64()
+        self._check(self._lib.rgpu_vp_supersteps(self._ctx, hop, C.byref(out)))
+        return out.value
 
     def stats(self) -> dict:
         s = N.Stats()

@@ -6,5 +6,5 @@ cd "$(dirname "$0")/.."
 tag=$1; shift
 d=raphtory_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -shared \
-  -o "abtest/librgpu_$tag.so" $d/kernels.hip $d/xchg.hip $d/tslots.hip $d/check.hip $d/merge.hip $d/diffusion.hip $d/rgpu.cpp $d/packer.cpp \
+  -o "abtest/librgpu_$tag.so" $d/kernels.hip $d/xchg.hip $d/tslots.hip $d/check.hip $d/merge.hip $d/diffusion.hip $d/vp.hip $d/rgpu.cpp $d/packer.cpp \
   $d/exchange.cpp $d/rgev.cpp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

@@ -1,5 +1,5 @@
 """Same-process A/B of superstep launch knobs on one sealed C4 graph (the knobs rgpu re-reads
-per run: RGPU_STEP_VARIANT, RGPU_STEP_GRID, RGPU_TAIL_STEP, RGPU_TAIL_GRID, RGPU_CHUNK0,
+per run: RGPU_STEP_GRID, RGPU_TAIL_STEP, RGPU_TAIL_GRID, RGPU_CHUNK0,
 RGPU_CHUNK).  Variants are "name:K=V,K=V" (empty = defaults); each is timed twice, interleaved,
 with a serial profile pass for its per-kernel times; the summaries must agree across variants.
 One JSON line per variant and round."""
@@ -17,7 +17,7 @@ import torch  # noqa: E402
 from raphtory_amd import TemporalGraph  # noqa: E402
 from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops  # noqa: E402
 
-KNOBS = ("RGPU_DENSE", "RGPU_EMENDS", "RGPU_CHGBITS", "RGPU_STEP_VARIANT", "RGPU_STEP_GRID", "RGPU_TAIL_STEP", "RGPU_TAIL_GRID", "RGPU_CHUNK0", "RGPU_CHUNK")
+KNOBS = ("RGPU_DENSE", "RGPU_CHGBITS", "RGPU_STEP_GRID", "RGPU_TAIL_STEP", "RGPU_TAIL_GRID", "RGPU_CHUNK0", "RGPU_CHUNK")
 
 
 def main():
