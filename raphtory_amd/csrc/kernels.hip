@@ -1323,6 +1323,14 @@ __global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int 
 }
 
 // ---------------------------------------------------------------- heavy vertices
+// Profile runs: the hub kernels' work, for their byte model (rgpu.cpp harvest), in the work
+// buffer's step-0 row (supersteps start at 1): [shard][f], f = 0 segments visited by the gather,
+// 1 slots it streamed, 2 hot slots (changed neighbour), 3 hot slots of mixed neighbours, 4 label
+// lanes gathered from rows, 5 slots walked by the mark, 6 static slots scanned by K2's segment
+// pass, 7 slots it kept.  One atomic per wave and field.
+__device__ __forceinline__ void heavy_work(unsigned long long* work, int f, unsigned long long x) {
+  if (work && x && (threadIdx.x & 63) == 0) atomicAdd(&work[(blockIdx.x & 63) * 8 + f], x);
+}
 // A power-law hub has 1e5-1e6 slots: as one wave's serial loop it would be the whole
 // superstep.  Its static slots are cut into segments of <= kSegSlots, one wave each.  A
 // segment's wave loads 64 slots at a time (lane = slot) and then folds the kept / changed ones
@@ -1351,10 +1359,12 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
                                                      int32_t* __restrict__ hbest, const int32_t* __restrict__ grank,
                                                      int64_t n_own, const int32_t* __restrict__ ts_e,
                                                      const int32_t* __restrict__ ts_nb,
-                                                     const int64_t* __restrict__ ts_t, int64_t tcut, int ends) {
+                                                     const int64_t* __restrict__ ts_t, int64_t tcut, int ends,
+                                                     unsigned long long* __restrict__ work) {
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned long long w_scan = 0, w_kept = 0;
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
     const int64_t lo0 = seg_lo[sg];
@@ -1375,6 +1385,7 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
     for (int32_t c = 0; c < ns; c += 64) {
       const int32_t jj = c + lane;
       if (ts_t && ts_t[lo + c] < tcut) break;
+      w_scan += ns - c < 64 ? ns - c : 64;
       uint64_t m = 0;
       int32_t nb = 0;
       if (jj < ns) {
@@ -1409,9 +1420,12 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
     }
     for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
     if (lane == 0) { segcnt[sg] = count; segor[sg] = any; }
+    w_kept += (unsigned long long)count;
     if (best != INT32_MAX && v < n_own) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);  // (a ghost's
                                                                                              // labels are its owner's)
   }
+  heavy_work(work, 6, w_scan);
+  heavy_work(work, 7, w_kept);
 }
 
 // Superstep r, before the full-grid kernel: minimum over each segment of a flagged heavy
@@ -1429,17 +1443,20 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       int32_t* __restrict__ hbest, int64_t n_own,
                                                       const int32_t* __restrict__ uw_cur,
                                                       const uint64_t* __restrict__ cb_prev,
-                                                      const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all) {
+                                                      const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
+                                                      unsigned long long* __restrict__ work) {
   if (stepflag[step - 1] == 0) return;
   const bool visit_all = dense_rule(ccount, step - 1, nv_all, dense_div);  // step-1 wrote no flags
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned long long w_seg = 0, w_slots = 0, w_hot = 0, w_mixed = 0, w_lanes = 0;
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
     if (v >= n_own || (!visit_all && !act_cur[v])) continue;  // ghosts are not visited (their owner computes them)
     const int32_t n = segcnt[sg];
     if (n == 0) continue;
+    if (work) { w_seg++; w_slots += (unsigned long long)n; }
     const int64_t base = seg_lo[sg];
     int32_t best = INT32_MAX;  // lane = view
     for (int32_t c = 0; c < n; c += 64) {
@@ -1460,11 +1477,23 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
         u = (uw_cur && a) ? uw_label(uw_cur[q]) : kMixed;
       }
       // lane = view: the changed mixed rows (4 in flight), then the uniform neighbours' words
+      if (work) {
+        w_hot += __popcll(__ballot(a != 0));
+        w_mixed += __popcll(__ballot(a != 0 && u == kMixed));
+        unsigned long long g = u == kMixed ? (unsigned long long)__popcll(a) : 0ull;
+        for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o);
+        w_lanes += g;
+      }
       best = gather_min<false>(u == kMixed ? a : 0, q, best, lab_cur, lane);
       if (uw_cur) best = fold_uniform(__ballot(u != kMixed), a, u, best, lane);
     }
     if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
   }
+  heavy_work(work, 0, w_seg);
+  heavy_work(work, 1, w_slots);
+  heavy_work(work, 2, w_hot);
+  heavy_work(work, 3, w_mixed);
+  heavy_work(work, 4, w_lanes);
 }
 
 // Superstep r, after the full-grid kernel: the neighbours of every heavy vertex that changed
@@ -1491,13 +1520,15 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
                                                     const int32_t* __restrict__ ts_e,
                                                     const int32_t* __restrict__ ts_nb,
                                                     const int64_t* __restrict__ ts_t, int64_t tcut,
-                                                    const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all) {
+                                                    const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
+                                                    unsigned long long* __restrict__ work) {
   if (stepflag[step] == 0) return;
   if (dense_rule(ccount, step, nv_all, dense_div)) return;  // dense step: the next one visits every member
   if (dense_rule(ccount, step - 1, nv_all, dense_div)) act_cur = nullptr;  // this step visited every member
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  unsigned long long w_walk = 0;
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
     if (act_cur && v < n_own && !act_cur[v]) continue;  // a ghost's word is current (set by its records)
@@ -1505,11 +1536,13 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
     if (!ch) continue;
     const int32_t n = segcnt[sg];
     const int64_t base = seg_lo[sg];
+    w_walk += (unsigned long long)n;
     for (int32_t c = 0; c < n; c += 64) {
       const int32_t jj = c + lane;
       if (jj < n && (smask[base + jj] & ch)) act_next[snbr[base + jj]] = 1;
     }
   }
+  heavy_work(work, 5, w_walk);
 }
 
 // ---------------------------------------------------------------- K5: CC reductions
@@ -2350,33 +2383,33 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
 #undef RGPU_STEP_ARGS
 }
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
-                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends) {
+                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends, unsigned long long* work) {
   if (g.n_seg <= 0) return;
   k_heavy_slots<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off,
                                                             g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
                                                             snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own,
-                                                            g.ts_e, g.ts_nb, g.ts_t, tcut, ends ? 1 : 0);
+                                                            g.ts_e, g.ts_nb, g.ts_t, tcut, ends ? 1 : 0, work);
 }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur,
-                         const uint64_t* cb_prev, const int32_t* ccount, int dense_div) {
+                         const uint64_t* cb_prev, const int32_t* ccount, int dense_div, unsigned long long* work) {
   if (g.n_seg <= 0) return;
   k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
                                                              hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
-                                                             g.n_own);
+                                                             g.n_own, work);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
                        const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm, const uint64_t* em,
-                       int64_t tcut, const int32_t* ccount, int dense_div) {
+                       int64_t tcut, const int32_t* ccount, int dense_div, unsigned long long* work) {
   if (g.n_seg <= 0) return;
   k_heavy_mark<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
                                                            chg_now, act_cur, act_next, stepflag, g.n_own, g.seg_n,
                                                            g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst,
                                                            vm, em, g.ts_e, g.ts_nb, g.ts_t, tcut, ccount, dense_div,
-                                                           g.n_own);
+                                                           g.n_own, work);
 }
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,

@@ -1,5 +1,6 @@
 // kernels.hpp — device-side graph view, batch parameters and kernel launchers.
 #pragma once
+#include <string>
 #include <vector>
 #include <hip/hip_runtime.h>
 
@@ -128,19 +129,22 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
 // (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
 // next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
+// work (profile runs, else null): the hub kernels' work counters (kernels.hip heavy_work)
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
-                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends = false);
+                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends = false,
+                        unsigned long long* work = nullptr);
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr,
-                         const uint64_t* cb_prev = nullptr, const int32_t* ccount = nullptr, int dense_div = 0);
+                         const uint64_t* cb_prev = nullptr, const int32_t* ccount = nullptr, int dense_div = 0,
+                         unsigned long long* work = nullptr);
 // vm/em (partitioned mode): heavy ghosts (ranks >= n_own) have no compacted slots; their kept
 // slots are recomputed from the static adjacency (em & vm[nb] & vm[v]) while marking
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
                        const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm = nullptr,
                        const uint64_t* em = nullptr, int64_t tcut = INT64_MIN, const int32_t* ccount = nullptr,
-                       int dense_div = 0);
+                       int dense_div = 0, unsigned long long* work = nullptr);
 extern int g_sum_blocks;   // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 extern int g_hist_rounds;  // label-dedup rounds per (view, chunk) in k_cc_hist (RGPU_HIST_ROUNDS)
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
@@ -329,5 +333,42 @@ void launch_edge_hist(hipStream_t s, bool write, const MergeIn& m, int64_t ne2, 
 void launch_vertex_hist(hipStream_t s, bool write, const MergeIn& m, int64_t* cnt_off, int64_t* vkey2);
 void launch_merge_in(hipStream_t s, const MergeIn& m, const int32_t* eo2n, const int32_t* npos,
                      const int64_t* in_off2, int32_t* in_eid2);
+
+// ---- live-ingest delta packer on the device (gdelta.hip; the host half packer.cpp pack_delta /
+// finish_delta builds the same arrays, rgpu_internal.hpp Delta)
+struct DevEvent {  // = rgpu::Event (rgpu_internal.hpp): the host's update records, uploaded as they are
+  int64_t t, src, dst;
+  uint8_t kind, pad[7];
+};
+struct DeltaDev {
+  int64_t nd = 0, nv_old = 0, nv2 = 0;
+  int64_t* vid2 = nullptr;                       // merged ids ascending (graph list)
+  int32_t *old2new = nullptr, *new2old = nullptr;
+  int64_t ndv = 0, ndvk = 0;                     // delta vertex points per rank, collapsed
+  int32_t* dv_rank = nullptr;
+  int64_t *dv_off = nullptr, *dv_key = nullptr;
+  int64_t ndd = 0;                               // delta deaths per rank (times, last delta index)
+  int32_t* dd_rank = nullptr;
+  int64_t *dd_off = nullptr, *dd_t = nullptr, *dd_last = nullptr;
+  int64_t nde = 0;                               // delta edges (distinct (s, d)), their base edge
+  int32_t *de_s = nullptr, *de_d = nullptr, *de_base = nullptr;
+  int64_t *de_koff = nullptr, *de_key = nullptr; // collapsed, tie-resolved own points
+  int64_t n_new = 0, nni = 0;                    // new edges (s << 32 | d), their in-edge records
+  int64_t* nn_key = nullptr;
+  int32_t* nn_didx = nullptr;
+  int64_t* ni_key = nullptr;
+  int32_t* ni_idx = nullptr;
+  int64_t *out_off = nullptr, *in_off = nullptr, *adj_off = nullptr;  // merged (graph list)
+  int64_t *doff = nullptr, *dtime = nullptr;
+  uint64_t* dbits = nullptr;
+  int64_t n_in = 0, ndt = 0;
+  std::vector<int32_t> heavy;                    // ranks with more than heavy_t static slots
+  std::vector<int64_t> heavy_a0, heavy_deg;      // their first static slot and slot count
+};
+// ev[0, n): the updates since the last seal; vid0: the base ids (device).  Device arrays go to
+// T (temporaries) or L (the merged graph).  Returns "" or the first invalid update's message.
+std::string gpu_pack_delta(hipStream_t s, const DevEvent* ev, int64_t n, const DevGraph& g0, const int64_t* vid0,
+                           int64_t heavy_t, DeltaDev* out, std::vector<void*>& T, std::vector<void*>& L);
+void launch_scatter_i32(hipStream_t s, int64_t n, const int32_t* idx, const int32_t* val, int32_t* out);
 
 }  // namespace rgpu

@@ -178,6 +178,10 @@ struct rgpu_ctx {
   bool sealed = false;
   size_t n_sealed = 0;                  // events[0, n_sealed) are in the resident graph
   bool delta_on = true;                 // RGPU_DELTA: merge later updates into it (else re-pack)
+  bool delta_host = false;              // RGPU_DELTA=2: the host delta packer (A/B; default the device one)
+  int64_t* g_vid = nullptr;             // device delta packer: the resident graph's ids (graph list)
+  bool vid_stale = false;               // pk.vid lags g_vid (downloaded when results name ids)
+  int64_t n_dtime = -1;                 // device delta packer: death times (pk.dtime is not kept)
   int vertex_order = RGPU_ORDER_LOCALITY;  // rgpu_set_vertex_order: local rank order of a full seal
   Packed pk;
   DevGraph g;
@@ -272,6 +276,7 @@ void free_part_slots(rgpu_ctx* c, bool keep_channels);
 void free_graph(rgpu_ctx* c) {
   for (void* p : c->graph_allocs) (void)hipFree(p);
   c->graph_allocs.clear();
+  c->g_vid = nullptr;
   release_slots(c);
   c->g = DevGraph();
   free_part_slots(c, true);  // the channels (communicators) outlive a re-seal
@@ -612,7 +617,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[(r - 1) & 1], s.chg[(r - 1) & 1], s.act[r % 3],
                             s.stepcnt, r, s.hv, uw ? s.uw[(r - 1) & 1] : nullptr, chg_bits(c, s, r).prev, s.ccount,
-                            dense_div(c));
+                            dense_div(c), work_buf(c, s));
       }, r, per_launch);
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
@@ -625,7 +630,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     if (hv)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[r & 1], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
-                          s.act[r % 3], nullptr, nullptr, INT64_MIN, s.ccount, dense_div(c));
+                          s.act[r % 3], nullptr, nullptr, INT64_MIN, s.ccount, dense_div(c), work_buf(c, s));
       }, r, per_launch);
   }
   if (ea) {
@@ -911,7 +916,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     const double b2 = 8.0 * g.nv;  // the view-mask scan; the rest from the work counters (harvest)
     if (g.n_seg > 0)
       timed_launch(c, si, KID_HEAVY, 0.0,
-                   [&] { launch_heavy_slots(s.stream, g, tcut, s.vm, s.em, s.snbr, s.smask, s.hv, ends); });
+                   [&] { launch_heavy_slots(s.stream, g, tcut, s.vm, s.em, s.snbr, s.smask, s.hv, ends, work_buf(c, s)); });
     timed_launch(c, si, KID_SLOTS, b2, [&] {  // (partitioned: owned vertices only, gk)
       launch_cc_slots(s.stream, gk, tcut, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
@@ -925,7 +930,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       });
     if (g.n_seg > 0 && !c->partitioned)  // partitioned: after the step's records are in
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
-        launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[1], s.act[2], s.stepcnt, 1, s.hv, nullptr);
+        launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[1], s.act[2], s.stepcnt, 1, s.hv, nullptr, nullptr,
+                          nullptr, INT64_MIN, nullptr, 0, work_buf(c, s));
       });
     s.r_launched = 1;  // superstep 1 ran inside the slot kernel
     if (c->partitioned) {
@@ -1033,6 +1039,14 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
                                          (c->g.ts_e ? 32.0 : 24.0) * (double)wsum(1, 4) + 12.0 * (double)wsum(1, 1) +
                                          4.0 * (double)wsum(1, 7) + 64.0 * (double)wsum(1, 6);
       }
+      // hub kernels (kernels.hip heavy_work, the step-0 row): per segment the gather visits, its
+      // metadata and the hub's minima row (32 + 256 B); per slot it streams the neighbour (4 B) and
+      // its changed bit (1/8 B, L2); per hot slot mask + uniform word (12 B), a mixed one's change
+      // word (8 B) and its gathered lanes (4 B each); per slot the mark walks nbr + mask (12 B);
+      // per static slot K2's segment pass scans (as K2: 32 B) and per kept slot it writes (12 B)
+      c->st.kernel_bytes[KID_HEAVY] += 288.0 * wsum(0, 0) + 4.125 * wsum(0, 1) + 12.0 * wsum(0, 2) +
+                                       8.0 * wsum(0, 3) + 4.0 * wsum(0, 4) + 12.0 * wsum(0, 5) +
+                                       32.0 * wsum(0, 6) + 12.0 * wsum(0, 7);
       const double per_slot = use_uw(c) ? 16.0 : 20.0;
       for (int r = 2; r <= s.r_final; r++)
         c->st.kernel_bytes[s.by_tail[r] ? KID_TAIL : KID_STEP] +=
@@ -1630,6 +1644,24 @@ void finish_supersteps(rgpu_ctx* c, const RunCfg& rc) {
   }
 }
 
+int fail(rgpu_ctx* c, int code, const std::string& m);
+// After device-packed merges the ids live in HBM (g_vid); the host copy follows when a result
+// names vertices.  Returns an RGPU_* code.
+int sync_vid(rgpu_ctx* c) {
+  if (!c->vid_stale) return RGPU_OK;
+  try {
+    c->pk.vid.resize((size_t)c->g.nv);
+    if (c->g.nv)
+      HIPCHK(hipMemcpy(c->pk.vid.data(), c->g_vid, sizeof(int64_t) * c->g.nv, hipMemcpyDeviceToHost));
+  } catch (const HipFail& f) {
+    return fail(c, RGPU_EHIP, f.msg);
+  } catch (const std::bad_alloc&) {
+    return fail(c, RGPU_ENOMEM, "host allocation failed");
+  }
+  c->vid_stale = false;
+  return RGPU_OK;
+}
+
 // id of the vertex whose label is l: partitioned, labels are ids; else id ranks
 int64_t label_id(const rgpu_ctx* c, int32_t l) {
   if (c->partitioned) return (int64_t)l;
@@ -1721,6 +1753,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->tail_cap = std::max(1, env_int("RGPU_TAIL_CAP", 256));
   c->tail_maxv = std::max(0, env_int("RGPU_TAIL_MAXV", 4 << 20));
   c->delta_on = env_int("RGPU_DELTA", 1) != 0;
+  c->delta_host = env_int("RGPU_DELTA", 1) == 2;
   g_xrec_slack = std::max(1, env_int("RGPU_XREC_SLACK", 1024));
   g_xrec_init = std::max(0, env_int("RGPU_XREC_INIT", 2));
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
@@ -1777,17 +1810,17 @@ int rgpu_ingest_rgev(rgpu_ctx* c, const uint8_t* buf, size_t bytes, size_t* cons
 namespace {
 
 // Heavy vertices (power-law hubs): static slot lists cut into kSegSlots segments.
-void build_heavy(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L, const std::vector<int64_t>& out_off,
-                 const std::vector<int64_t>& in_off) {
-  if (c->heavy_t <= 0) return;
-  std::vector<int32_t> hv_of(g.nv, -1), hv_seg(1, 0), seg_v, seg_h, seg_n;
+// hv: the heavy ranks ascending, a0 / deg: their first static slot and slot count
+void build_heavy_list(DevGraph& g, std::vector<void*>& L, const std::vector<int32_t>& hv,
+                      const std::vector<int64_t>& a0s, const std::vector<int64_t>& degs) {
+  if (hv.empty()) return;
+  std::vector<int32_t> hv_seg(1, 0), seg_v, seg_h, seg_n, hidx(hv.size());
   std::vector<int64_t> seg_lo;
-  for (int64_t v = 0; v < g.nv; v++) {
-    const int64_t deg = (out_off[v + 1] - out_off[v]) + (in_off[v + 1] - in_off[v]);
-    if (deg <= c->heavy_t) continue;
+  for (size_t k = 0; k < hv.size(); k++) {
+    const int32_t v = hv[k];
+    const int64_t deg = degs[k], a0 = a0s[k];
     const int32_t h = (int32_t)(hv_seg.size() - 1);
-    hv_of[v] = h;
-    const int64_t a0 = out_off[v] + in_off[v];
+    hidx[k] = h;
     for (int64_t o = 0; o < deg; o += kSegSlots) {
       seg_v.push_back((int32_t)v);
       seg_h.push_back(h);
@@ -1796,15 +1829,43 @@ void build_heavy(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L, const std::vec
     }
     hv_seg.push_back((int32_t)seg_v.size());
   }
-  if (seg_v.empty()) return;
   g.n_heavy = (int64_t)hv_seg.size() - 1;
   g.n_seg = (int64_t)seg_v.size();
-  g.hv_of = dupload(L, hv_of);
+  {  // hv_of: -1 but at the heavy ranks (a scatter on the device: no O(V) host array)
+    int32_t* hv_of = dalloc<int32_t>(L, g.nv);
+    std::vector<void*> T;
+    try {
+      HIPCHK(hipMemsetAsync(hv_of, 0xff, sizeof(int32_t) * g.nv, nullptr));
+      const int32_t* d_hv = dupload(T, hv);
+      const int32_t* d_h = dupload(T, hidx);
+      launch_scatter_i32(nullptr, (int64_t)hv.size(), d_hv, d_h, hv_of);
+      HIPCHK(hipStreamSynchronize(nullptr));
+    } catch (...) {
+      for (void* p : T) (void)hipFree(p);
+      throw;
+    }
+    for (void* p : T) (void)hipFree(p);
+    g.hv_of = hv_of;
+  }
   g.hv_seg = dupload(L, hv_seg);
   g.seg_v = dupload(L, seg_v);
   g.seg_h = dupload(L, seg_h);
   g.seg_lo = dupload(L, seg_lo);
   g.seg_n = dupload(L, seg_n);
+}
+void build_heavy(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L, const std::vector<int64_t>& out_off,
+                 const std::vector<int64_t>& in_off) {
+  if (c->heavy_t <= 0) return;
+  std::vector<int32_t> hv;
+  std::vector<int64_t> a0, deg;
+  for (int64_t v = 0; v < g.nv; v++) {
+    const int64_t d = (out_off[v + 1] - out_off[v]) + (in_off[v + 1] - in_off[v]);
+    if (d <= c->heavy_t) continue;
+    hv.push_back((int32_t)v);
+    a0.push_back(out_off[v] + in_off[v]);
+    deg.push_back(d);
+  }
+  build_heavy_list(g, L, hv, a0, deg);
 }
 
 // K2's time-ordered static slots (tslots.hip), built on the device after the adjacency
@@ -1857,7 +1918,7 @@ void finish_seal(rgpu_ctx* c) {
   c->st.edges_owned = P.ne_owned;
   c->st.vertex_events = P.n_vkey;
   c->st.edge_events = P.n_ekey;
-  c->st.deaths = (int64_t)P.dtime.size();
+  c->st.deaths = c->n_dtime >= 0 ? c->n_dtime : (int64_t)P.dtime.size();
   c->n_sealed = c->events.size();
   c->sealed = true;
   if (!c->partitioned) {  // the big arrays live in HBM only (the delta merge keeps them there)
@@ -1867,10 +1928,12 @@ void finish_seal(rgpu_ctx* c) {
 }
 
 // Incremental seal: merge the updates ingested since the last seal into the resident graph
-// (merge.hip).  Host: delta-sized sorts + O(V) offsets; device: every big array.
+// (merge.hip).  The delta arrays come from the device packer (gdelta.hip: the tick's updates
+// are uploaded once and never come back) or, RGPU_DELTA=2, from the host packer (packer.cpp
+// pack_delta / finish_delta: delta-sized sorts + O(V) offsets on the host).
 void seal_delta(rgpu_ctx* c) {
   Packed& B = c->pk;
-  Delta D;
+  const bool dev = !c->delta_host;
   auto tp = std::chrono::steady_clock::now();
   auto phase = [&](const char* what) {  // RGPU_HOSTPROF: host-side phase times
     if (!c->hostprof) return;
@@ -1879,31 +1942,18 @@ void seal_delta(rgpu_ctx* c) {
                  std::chrono::duration<double, std::milli>(now - tp).count());
     tp = now;
   };
-  std::string e = pack_delta(c->events, c->n_sealed, B, &D);
-  phase("pack");
-  if (!e.empty()) throw HipFail{e, RGPU_EINVAL};
+  static_assert(sizeof(Event) == sizeof(DevEvent) && offsetof(Event, kind) == offsetof(DevEvent, kind),
+                "the device packer reads the host's update records as they are");
+  Delta D;      // host packer
+  DeltaDev DD;  // device packer
   std::vector<void*> T;  // temporaries
   std::vector<void*> L;  // the merged graph
   hipStream_t s = nullptr;
   try {
     HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     const DevGraph& g0 = c->g;
-    const int64_t nde = (int64_t)D.de_s.size();
-    std::vector<int32_t> base_eid(nde, -1);
-    if (nde) {
-      int32_t* qs = dupload(T, D.de_qs);
-      int32_t* qd = dupload(T, D.de_qd);
-      int32_t* res = dalloc<int32_t>(T, nde);
-      launch_edge_find(s, nde, qs, qd, g0.out_off, g0.edst, res);
-      HIPCHK(hipMemcpyAsync(base_eid.data(), res, sizeof(int32_t) * nde, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-    }
-    phase("lookup");
-    finish_delta(B, base_eid, &D);
-    phase("finish");
     MergeIn m;
     m.nv_old = g0.nv;
-    m.nv2 = D.nv;
     m.ne_old = g0.ne;
     m.nin_old = g0.n_in;
     m.esrc = g0.esrc;
@@ -1914,37 +1964,98 @@ void seal_delta(rgpu_ctx* c) {
     m.voff = g0.voff;
     m.vkey = g0.vkey;
     m.in_off = g0.in_off;
-    m.old2new = dupload(T, D.old2new);
-    m.new2old = dupload(T, D.new2old);
-    m.n_new = (int64_t)D.nn_key.size();
-    m.nde = nde;
-    m.nn_key = dupload(T, D.nn_key);
-    m.nn_didx = dupload(T, D.nn_didx);
-    m.de_base = dupload(T, D.de_base);
-    m.dkoff = dupload(T, D.de_koff);
-    m.dkey = dupload(T, D.de_key);
-    m.ndd = (int64_t)D.dd_rank.size();
-    m.dd_rank = dupload(T, D.dd_rank);
-    m.dd_off = dupload(T, D.dd_off);
-    m.dd_t = dupload(T, D.dd_t);
-    m.ndv = (int64_t)D.dv_rank.size();
-    m.dv_rank = dupload(T, D.dv_rank);
-    m.dv_off = dupload(T, D.dv_off);
-    m.dv_key = dupload(T, D.dv_key);
     m.nvk_old = B.n_vkey;
-    m.ndvk = (int64_t)D.dv_key.size();
+    int64_t nv2 = 0, n_in2 = 0;
+    if (dev) {
+      if (!c->g_vid) {  // the first merge into a full seal: its ids, once
+        c->g_vid = dalloc<int64_t>(c->graph_allocs, g0.nv);
+        HIPCHK(hipMemcpyAsync(c->g_vid, B.vid.data(), sizeof(int64_t) * g0.nv, hipMemcpyHostToDevice, s));
+      }
+      const int64_t n = (int64_t)(c->events.size() - c->n_sealed);
+      DevEvent* ev = dalloc<DevEvent>(T, n);
+      HIPCHK(hipMemcpyAsync(ev, c->events.data() + c->n_sealed, sizeof(Event) * n, hipMemcpyHostToDevice, s));
+      phase("upload");
+      std::string e;
+      try {
+        e = gpu_pack_delta(s, ev, n, g0, c->g_vid, c->heavy_t, &DD, T, L);
+      } catch (const std::runtime_error& x) {
+        throw HipFail{x.what()};
+      }
+      if (!e.empty()) throw HipFail{e, RGPU_EINVAL};
+      phase("pack");
+      nv2 = DD.nv2;
+      n_in2 = DD.n_in;
+      m.old2new = DD.old2new;
+      m.new2old = DD.new2old;
+      m.n_new = DD.n_new;
+      m.nde = DD.nde;
+      m.nn_key = DD.nn_key;
+      m.nn_didx = DD.nn_didx;
+      m.de_base = DD.de_base;
+      m.dkoff = DD.de_koff;
+      m.dkey = DD.de_key;
+      m.ndd = DD.ndd;
+      m.dd_rank = DD.dd_rank;
+      m.dd_off = DD.dd_off;
+      m.dd_t = DD.dd_t;
+      m.ndv = DD.ndv;
+      m.dv_rank = DD.dv_rank;
+      m.dv_off = DD.dv_off;
+      m.dv_key = DD.dv_key;
+      m.ndvk = DD.ndvk;
+      m.nni = DD.nni;
+      m.ni_key = DD.ni_key;
+      m.ni_idx = DD.ni_idx;
+    } else {
+      std::string e = pack_delta(c->events, c->n_sealed, B, &D);
+      phase("pack");
+      if (!e.empty()) throw HipFail{e, RGPU_EINVAL};
+      const int64_t nde = (int64_t)D.de_s.size();
+      std::vector<int32_t> base_eid(nde, -1);
+      if (nde) {
+        int32_t* qs = dupload(T, D.de_qs);
+        int32_t* qd = dupload(T, D.de_qd);
+        int32_t* res = dalloc<int32_t>(T, nde);
+        launch_edge_find(s, nde, qs, qd, g0.out_off, g0.edst, res);
+        HIPCHK(hipMemcpyAsync(base_eid.data(), res, sizeof(int32_t) * nde, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+      }
+      phase("lookup");
+      finish_delta(B, base_eid, &D);
+      phase("finish");
+      nv2 = D.nv;
+      n_in2 = D.in_off[D.nv];
+      m.old2new = dupload(T, D.old2new);
+      m.new2old = dupload(T, D.new2old);
+      m.n_new = (int64_t)D.nn_key.size();
+      m.nde = nde;
+      m.nn_key = dupload(T, D.nn_key);
+      m.nn_didx = dupload(T, D.nn_didx);
+      m.de_base = dupload(T, D.de_base);
+      m.dkoff = dupload(T, D.de_koff);
+      m.dkey = dupload(T, D.de_key);
+      m.ndd = (int64_t)D.dd_rank.size();
+      m.dd_rank = dupload(T, D.dd_rank);
+      m.dd_off = dupload(T, D.dd_off);
+      m.dd_t = dupload(T, D.dd_t);
+      m.ndv = (int64_t)D.dv_rank.size();
+      m.dv_rank = dupload(T, D.dv_rank);
+      m.dv_off = dupload(T, D.dv_off);
+      m.dv_key = dupload(T, D.dv_key);
+      m.ndvk = (int64_t)D.dv_key.size();
+      m.nni = (int64_t)D.ni_key.size();
+      m.ni_key = dupload(T, D.ni_key);
+      m.ni_idx = dupload(T, D.ni_idx);
+    }
+    m.nv2 = nv2;
     m.coll = dalloc<int64_t>(T, m.ndvk + 1);
     m.coll_tmp = dalloc<int64_t>(T, scan_tmp_words(std::max<int64_t>(m.ndvk, 1)));
-    m.nni = (int64_t)D.ni_key.size();
-    m.ni_key = dupload(T, D.ni_key);
-    m.ni_idx = dupload(T, D.ni_idx);
-
     HIPCHK(hipStreamSynchronize(s));
     phase("upload");
     DevGraph g;
-    g.nv = g.n_own = D.nv;
+    g.nv = g.n_own = nv2;
     g.ne = g0.ne + m.n_new;
-    g.n_in = D.in_off[D.nv];
+    g.n_in = n_in2;
     int32_t* esrc2 = dalloc<int32_t>(L, g.ne);
     int32_t* edst2 = dalloc<int32_t>(L, g.ne);
     int32_t* eo2n = dalloc<int32_t>(T, g0.ne);
@@ -1981,8 +2092,8 @@ void seal_delta(rgpu_ctx* c) {
     launch_vertex_hist(s, true, m, voff2, vkey2);
     HIPCHK(hipStreamSynchronize(s));
     phase("hist kernels");
-    // adjacency offsets (host-merged), in-edges
-    int64_t* in_off2 = dupload(L, D.in_off);
+    // adjacency offsets, in-edges
+    const int64_t* in_off2 = dev ? DD.in_off : dupload(L, D.in_off);
     int32_t* in_eid2 = dalloc<int32_t>(L, g.n_in);
     launch_merge_in(s, m, eo2n, npos, in_off2, in_eid2);
     HIPCHK(hipGetLastError());
@@ -1994,14 +2105,26 @@ void seal_delta(rgpu_ctx* c) {
     g.vkey = vkey2;
     g.in_off = in_off2;
     g.in_eid = in_eid2;
-    g.out_off = dupload(L, D.out_off);
-    g.adj_off = upload_adj(L, D.out_off, D.in_off);
-    g.doff = dupload(L, D.doff);
-    g.dtime = dupload(L, D.dtime);
-    g.dbits = upload_death_bits(L, D.doff);
+    if (dev) {
+      g.out_off = DD.out_off;
+      g.adj_off = DD.adj_off;
+      g.doff = DD.doff;
+      g.dtime = DD.dtime;
+      g.dbits = DD.dbits;
+    } else {
+      g.out_off = dupload(L, D.out_off);
+      g.adj_off = upload_adj(L, D.out_off, D.in_off);
+      g.doff = dupload(L, D.doff);
+      g.dtime = dupload(L, D.dtime);
+      g.dbits = upload_death_bits(L, D.doff);
+    }
     HIPCHK(hipStreamSynchronize(s));
     phase("adjacency");
-    build_heavy(c, g, L, D.out_off, D.in_off);
+    if (dev) {
+      if (c->heavy_t > 0) build_heavy_list(g, L, DD.heavy, DD.heavy_a0, DD.heavy_deg);
+    } else {
+      build_heavy(c, g, L, D.out_off, D.in_off);
+    }
     HIPCHK(hipStreamSynchronize(s));
     phase("heavy");
     build_tslots(c, g, L);
@@ -2017,6 +2140,7 @@ void seal_delta(rgpu_ctx* c) {
     c->graph_allocs.swap(L);
     L.clear();
     c->g = g;
+    c->g_vid = dev ? DD.vid2 : nullptr;
     for (Slot& sl : c->slot) {
       sl.hv = HeavyBuf();
       sl.h_cc = sl.h_pr = false;
@@ -2036,20 +2160,28 @@ void seal_delta(rgpu_ctx* c) {
         }
       }
     }
-    B.nv = B.n_own = D.nv;
+    B.nv = B.n_own = nv2;
     B.ne = B.ne_owned = g.ne;
-    B.vid.swap(D.vid);
-    B.doff.swap(D.doff);
-    B.dtime.swap(D.dtime);
-    B.out_off.swap(D.out_off);
-    B.in_off.swap(D.in_off);
+    if (dev) {  // the host keeps no offsets; its ids follow on demand (host_vid)
+      c->vid_stale = true;
+      c->n_dtime = DD.ndt;
+      for (auto* v : {&B.doff, &B.dtime, &B.out_off, &B.in_off}) std::vector<int64_t>().swap(*v);
+    } else {
+      B.vid.swap(D.vid);
+      B.doff.swap(D.doff);
+      B.dtime.swap(D.dtime);
+      B.out_off.swap(D.out_off);
+      B.in_off.swap(D.in_off);
+      c->n_dtime = -1;
+    }
     B.n_vkey = nvk;
     B.n_ekey = nek;
     B.n_in = g.n_in;
     B.newest = c->newest;
-    c->st.seal_delta_updates = D.nd;
+    c->st.seal_delta_updates = dev ? DD.nd : D.nd;
     phase("swap");
   } catch (...) {
+    if (s) (void)hipStreamSynchronize(s);
     for (void* p : T) (void)hipFree(p);
     for (void* p : L) (void)hipFree(p);
     if (s) (void)hipStreamDestroy(s);
@@ -2088,6 +2220,8 @@ int rgpu_seal(rgpu_ctx* c) {
     std::string e = pack_events(c->events, c->part, c->nparts, &c->pk, c->vertex_order == RGPU_ORDER_LOCALITY);
     if (!e.empty()) return fail(c, RGPU_EINVAL, e);
     free_graph(c);
+    c->vid_stale = false;
+    c->n_dtime = -1;
     const Packed& P = c->pk;
     auto& L = c->graph_allocs;
     DevGraph g;
@@ -2286,6 +2420,8 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
       HIPCHK(hipMalloc(&c->d_ecnt, sizeof(unsigned long long) * n_hops * rc.W));
       HIPCHK(hipMemset(c->d_ecnt, 0, sizeof(unsigned long long) * n_hops * rc.W));
     }
+    if (algo == RGPU_ALGO_DEGREE || algo == RGPU_ALGO_DIFFUSION || algo == RGPU_ALGO_VP)
+      if (int e = sync_vid(c)) return e;  // (seed ranks and top lists name ids)
     c->deg.assign(algo == RGPU_ALGO_DEGREE ? n_hops * rc.W * 3 : 0, 0);
     c->degtop.assign(algo == RGPU_ALGO_DEGREE ? n_hops * rc.W * kTop : 0, rgpu_ctx::TopEnt{-1, 0, 0});
     c->dcount.assign(algo == RGPU_ALGO_DIFFUSION ? n_hops * rc.W : 0, 0);
@@ -2421,6 +2557,7 @@ int rgpu_cc_vertex_labels(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int
   int j;
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
+  if (int e = sync_vid(c)) return e;
   size_t k = 0;
   for (int64_t k_ = 0; k_ < c->pk.n_own; k_++) {
     const int64_t v = own_at(c, k_);
@@ -2444,6 +2581,7 @@ int rgpu_cc_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* labels, int32_t
   int j;
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
+  if (int e = sync_vid(c)) return e;
   std::vector<int32_t> lab;
   for (int64_t v = 0; v < c->pk.n_own; v++)  // (any order: sorted below)
     if ((R.vm[v] >> j) & 1) lab.push_back(R.a[(size_t)v * kViews + j]);
@@ -2469,6 +2607,7 @@ int rgpu_degree_vertex(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int32_
   int j;
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
+  if (int e = sync_vid(c)) return e;
   size_t k = 0;
   for (int64_t k_ = 0; k_ < c->pk.n_own; k_++) {
     const int64_t v = own_at(c, k_);
@@ -2513,6 +2652,7 @@ int rgpu_pr_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, double* pr
   int j;
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
+  if (int e = sync_vid(c)) return e;
   size_t k = 0;
   for (int64_t k_ = 0; k_ < c->pk.n_own; k_++) {
     const int64_t v = own_at(c, k_);
@@ -2555,6 +2695,7 @@ int rgpu_diffusion_vertex(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int
   int j;
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
+  if (int e = sync_vid(c)) return e;
   size_t k = 0;
   for (int64_t k_ = 0; k_ < c->pk.n_own; k_++) {
     const int64_t v = own_at(c, k_);
@@ -2594,6 +2735,7 @@ int rgpu_vp_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int64_t* v
   int j;
   if (int e = view_index(c, hop, win, &b, &j)) return e;
   const Retained& R = c->kept[b];
+  if (int e = sync_vid(c)) return e;
   size_t k = 0;
   for (int64_t k_ = 0; k_ < c->pk.n_own; k_++) {
     const int64_t v = own_at(c, k_);

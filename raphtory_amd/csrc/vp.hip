@@ -1,0 +1,212 @@
+// vp.hip — generic vertex programs on the GPU (rgpu_set_vertex_program, include/rgpu.h; SURVEY.md
+// §8(f) row 4): the VertexVisitor messaging surface (messageAllOutgoingNeighbors /
+// messageAllIngoingNeighbors / messageAllNeighbours, getOrSetCompValue / setCompValue,
+// voteToHalt; VertexVisitor.scala:81-166) for an Analyser whose analyse() folds its message queue
+// with min or max.  Semantics: oracle.h orc_vertex_program.  Lane = view, as in CC: one pass over
+// the batch's pull slots serves its 64 views.
+//
+//   k_vp_slots  per member, the neighbours whose messages it receives — the senders that name it
+//               in the program's direction — kept iff em[e] & vm[sender] & vm[v], compacted at the
+//               vertex's static slot offset (out + in edges; every direction fits)
+//   k_vp_init   setup (superstep 0): the members' state rows (int64) and the senders' change words
+//   k_vp_step   superstep r: per member, the fold (min / max) of sender state + step_add over the
+//               kept slots whose sender changed in r-1 (those sent it a message); a member whose
+//               state the fold changes keeps it and sends next step, the others vote to halt
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "kernels.hpp"
+
+namespace rgpu {
+
+namespace {
+
+__device__ __forceinline__ int lane_of() { return threadIdx.x & 63; }
+__device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+__device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {
+  if (b > 0 && a > INT64_MAX - b) return INT64_MAX;
+  if (b < 0 && a < INT64_MIN - b) return INT64_MIN;
+  return a + b;
+}
+
+// pull slots of v: for direction OUT the in-edges' sources and a self-loop; IN: the out-edges'
+// targets but v itself (a self-loop never enters incomingEdges, EntityStorage.scala:257); ALL: both
+__global__ __launch_bounds__(256) void k_vp_slots(int64_t nv, int dir, const int64_t* __restrict__ out_off,
+                                                  const int64_t* __restrict__ in_off,
+                                                  const int64_t* __restrict__ adj_off,
+                                                  const int32_t* __restrict__ in_eid,
+                                                  const int32_t* __restrict__ esrc,
+                                                  const int32_t* __restrict__ edst,
+                                                  const uint64_t* __restrict__ vm, const uint64_t* __restrict__ em,
+                                                  int32_t* __restrict__ cnt, int32_t* __restrict__ snbr,
+                                                  uint64_t* __restrict__ smask) {
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    const uint64_t mv = vm[v];
+    if (mv == 0) {
+      if (lane == 0) cnt[v] = 0;
+      continue;
+    }
+    const int64_t o0 = out_off[v], nout = out_off[v + 1] - o0, i0 = in_off[v], nin = in_off[v + 1] - i0;
+    const int64_t base = adj_off[v];
+    int32_t count = 0;
+    for (int part = 0; part < 2; part++) {  // 0: in-edges (senders of OUT / ALL), 1: out-edges
+      if (part == 0 && dir == 1) continue;
+      if (part == 1 && dir == 0) {
+        // OUT: only a self-loop of the out-edges sends to v (out-edges are sorted by target)
+        int64_t a = o0, b = o0 + nout;
+        while (a < b) {
+          const int64_t m = (a + b) >> 1;
+          if (edst[m] < (int32_t)v) a = m + 1; else b = m;
+        }
+        if (lane == 0 && a < o0 + nout && edst[a] == (int32_t)v) {
+          const uint64_t m = em[a] & mv;
+          if (m) {
+            snbr[base + count] = (int32_t)v;
+            smask[base + count] = m;
+          }
+          count += m != 0;
+        }
+        count = __builtin_amdgcn_readlane(count, 0);
+        continue;
+      }
+      const int64_t n = part == 0 ? nin : nout;
+      for (int64_t c = 0; c < n; c += 64) {
+        const int64_t j = c + lane;
+        uint64_t m = 0;
+        int32_t nb = 0;
+        if (j < n) {
+          const int32_t e = part == 0 ? in_eid[i0 + j] : (int32_t)(o0 + j);
+          nb = part == 0 ? esrc[e] : edst[e];
+          if (!(part == 1 && dir == 1 && nb == (int32_t)v)) m = em[e] & vm[nb] & mv;
+        }
+        const uint64_t bal = __ballot(m != 0);
+        if (m) {
+          const int64_t pos = base + count + __popcll(bal & lanes_below(lane));
+          snbr[pos] = nb;
+          smask[pos] = m;
+        }
+        count += __popcll(bal);
+      }
+    }
+    if (lane == 0) cnt[v] = count;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_vp_init(int64_t nv, VpParams p, const int32_t* __restrict__ grank,
+                                                 const int64_t* __restrict__ vid, const uint64_t* __restrict__ vm,
+                                                 int64_t* __restrict__ st, uint64_t* __restrict__ chg) {
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    const uint64_t mv = vm[v];
+    const int64_t x = p.init == 0 ? vid[v] : (v == p.seed_rank ? p.seed_value : p.init_value);
+    st[v * 64 + lane] = x;
+    if (lane == 0) chg[v] = (p.senders == 0 || v == p.seed_rank) ? mv : 0ull;  // the setup's senders
+  }
+}
+// superstep 1 always runs after a setup (its halting vote counts the message holders)
+__global__ void k_vp_go(int32_t* __restrict__ stepflag) { stepflag[0] = 1; }
+
+template <int RED>
+__global__ __launch_bounds__(256) void k_vp_step(int step, int64_t nv, int64_t step_add, const int64_t* __restrict__ adj_off,
+                                                 const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
+                                                 const int32_t* __restrict__ snbr, const uint64_t* __restrict__ smask,
+                                                 const int64_t* __restrict__ st_cur, int64_t* __restrict__ st_next,
+                                                 const uint64_t* __restrict__ chg_prev, uint64_t* __restrict__ chg_next,
+                                                 int32_t* __restrict__ stepflag, int32_t* __restrict__ hostflag,
+                                                 unsigned long long* __restrict__ lanechg) {
+  if (stepflag[step - 1] == 0) return;  // the job halted (AnalysisTask.endStep)
+  __shared__ unsigned long long lanes_s;
+  if (threadIdx.x == 0) lanes_s = 0;
+  __syncthreads();
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t ident = RED == 0 ? INT64_MAX : INT64_MIN;
+  uint64_t lanes = 0;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    const uint64_t mv = vm[v];
+    if (mv == 0) continue;
+    const int32_t n = cnt[v];
+    const int64_t base = adj_off[v];
+    const int64_t cur = st_cur[v * 64 + lane];
+    int64_t m = ident;
+    bool got = false;  // lane = view: a message arrived (moreMessages)
+    for (int32_t c = 0; c < n; c += 64) {
+      const int32_t j = c + lane;
+      int32_t nb = 0;
+      uint64_t a = 0;
+      if (j < n) {
+        nb = snbr[base + j];
+        a = smask[base + j] & chg_prev[nb];
+      }
+      for (uint64_t bal = __ballot(a != 0); bal; bal &= bal - 1) {
+        const int L = __builtin_ctzll(bal);
+        const int32_t q = __builtin_amdgcn_readlane(nb, L);
+        if ((rl64(a, L) >> lane) & 1) {
+          const int64_t x = sat_add(st_cur[(int64_t)q * 64 + lane], step_add);
+          m = RED == 0 ? (x < m ? x : m) : (x > m ? x : m);
+          got = true;
+        }
+      }
+    }
+    const bool member = (mv >> lane) & 1;
+    const int64_t nx = (member && got) ? (RED == 0 ? (m < cur ? m : cur) : (m > cur ? m : cur)) : cur;
+    const uint64_t ch = __ballot(member && nx != cur);
+    st_next[v * 64 + lane] = nx;
+    if (lane == 0) chg_next[v] = ch;
+    lanes |= ch;
+  }
+  if (lane == 0 && lanes) atomicOr(&lanes_s, (unsigned long long)lanes);
+  __syncthreads();
+  if (threadIdx.x == 0 && lanes_s) {
+    atomicOr(&lanechg[step * kLaneShards + (blockIdx.x & (kLaneShards - 1))], lanes_s);
+    if (stepflag[step] == 0) {
+      stepflag[step] = 1;
+      if (hostflag) hostflag[step] = 1;
+    }
+  }
+}
+
+unsigned vgrid(int64_t items, int per_block, unsigned cap) {
+  int64_t g = (items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (unsigned)(g > cap ? cap : g);
+}
+
+}  // namespace
+
+void launch_vp_setup(hipStream_t s, const DevGraph& g, const VpParams& p, const int64_t* vid, const uint64_t* vm,
+                     const uint64_t* em, int32_t* cnt, int32_t* snbr, uint64_t* smask, int64_t* st0, uint64_t* chg0) {
+  const unsigned grid = vgrid(g.nv, 4, 8192);
+  k_vp_slots<<<grid, 256, 0, s>>>(g.nv, p.dir, g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em, cnt,
+                                  snbr, smask);
+  k_vp_init<<<grid, 256, 0, s>>>(g.nv, p, g.grank, vid, vm, st0, chg0);
+}
+void launch_vp_go(hipStream_t s, int32_t* stepflag) { k_vp_go<<<1, 1, 0, s>>>(stepflag); }
+
+void launch_vp_step(hipStream_t s, int step, const DevGraph& g, const VpParams& p, const uint64_t* vm,
+                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, const int64_t* st_cur,
+                    int64_t* st_next, const uint64_t* chg_prev, uint64_t* chg_next, int32_t* stepflag,
+                    int32_t* hostflag, unsigned long long* lanechg) {
+  const unsigned grid = vgrid(g.nv, 4, 8192);
+  if (p.reduce == 0)
+    k_vp_step<0><<<grid, 256, 0, s>>>(step, g.nv, p.step_add, g.adj_off, vm, cnt, snbr, smask, st_cur, st_next,
+                                      chg_prev, chg_next, stepflag, hostflag, lanechg);
+  else
+    k_vp_step<1><<<grid, 256, 0, s>>>(step, g.nv, p.step_add, g.adj_off, vm, cnt, snbr, smask, st_cur, st_next,
+                                      chg_prev, chg_next, stepflag, hostflag, lanechg);
+}
+
+}  // namespace rgpu

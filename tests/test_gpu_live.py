@@ -168,3 +168,71 @@ def test_live_seal_errors_and_noop():
     with pytest.raises(RGPUError):
         g.seal()
     g.close()
+
+
+def _packer_graph(monkeypatch, mode):
+    monkeypatch.setenv("RGPU_DELTA", mode)  # read when the context is created
+    g = TemporalGraph(vertex_order="id")
+    monkeypatch.delenv("RGPU_DELTA")
+    return g
+
+
+@pytest.mark.parametrize("stream", ["ties", "shuffled", "deaths_powerlaw"])
+def test_live_device_packer_equals_host_packer(stream, monkeypatch):
+    """The device delta packer (gdelta.hip, the default) and the host one (packer.cpp pack_delta /
+    finish_delta, RGPU_DELTA=2) merge the same ticks into the same graph: stats, and every CC
+    label and degree of a spread of views after each seal (both also match the oracle above)."""
+    if stream == "ties":
+        arrs = list(_growing_tie_stream(11, 12_000, nv_max=600))
+        cuts = [3001, 3002, 7777, 9000]
+        wins = [5000, 1000, 200]
+    elif stream == "shuffled":  # out of order: the device packer's time sort
+        s = gen_uniform(5, 300, 9000, t0=0, dt=1000)
+        p = np.random.default_rng(5).permutation(len(s))
+        arrs = [s.t[p], s.kind[p], s.src[p], s.dst[p]]
+        cuts = [3000, 6000, 8000]
+        wins = [2_000_000, 300_000]
+    else:
+        s = gen_powerlaw(9, 3000, 30_000, t0=0, t1=YEAR)
+        arrs = [s.t, s.kind, s.src, s.dst]
+        cuts = [10_000, 10_001, 22_000]
+        wins = [MONTH, WEEK]
+    end = int(np.max(arrs[0]))
+    hops = np.linspace(end // 3, end, 6).astype(np.int64)
+    gd, gh = _packer_graph(monkeypatch, "1"), _packer_graph(monkeypatch, "2")
+    bounds = [0] + cuts + [len(arrs[0])]
+    for k in range(len(bounds) - 1):
+        for g in (gd, gh):
+            g.ingest(*_cut(arrs, bounds[k], bounds[k + 1]))
+            g.seal()
+        a, b = gd.stats(), gh.stats()
+        for key in ("vertices", "edges", "vertex_events", "edge_events", "deaths", "seal_incremental"):
+            assert a[key] == b[key], (k, key, a[key], b[key])
+        for g in (gd, gh):
+            g.run("cc", hops, wins, retain=True)
+        for h in range(len(hops)):
+            for w in range(len(wins)):
+                x, y = gd.cc_vertex_labels(h, w), gh.cc_vertex_labels(h, w)
+                assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]), (k, h, w)
+        for g in (gd, gh):
+            g.run("degree", hops[::2], wins, retain=True)
+        for h in range(len(hops[::2])):
+            for w in range(len(wins)):
+                x, y = gd.degree_vertex(h, w), gh.degree_vertex(h, w)
+                assert all(np.array_equal(u, v) for u, v in zip(x, y)), (k, h, w)
+    gd.close()
+    gh.close()
+
+
+def test_live_device_packer_invalid_update_messages(monkeypatch):
+    """the device packer reports the first invalid update of the tick as the host one does,
+    and the resident graph stays as it was"""
+    for mode in ("1", "2"):
+        g = _packer_graph(monkeypatch, mode)
+        g.ingest([1, 2], [2, 2], [1, 2], [2, 3])
+        g.seal()
+        g.ingest([3, -4, 5], [2, 2, 2], [1, 1, 1], [2, 2, 1 << 40])  # a bad time first, then a bad id
+        with pytest.raises(RGPUError, match="time out of range"):
+            g.seal()
+        assert g.stats()["vertices"] == 3
+        g.close()
