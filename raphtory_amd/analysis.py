@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import json
 import math
+import threading
 import time
 from typing import Dict, List, Optional, Sequence
 
@@ -400,11 +401,7 @@ class AnalysisTask:
         a = self.analyser
         max_steps = a.defineMaxSteps()
         t0 = time.perf_counter()
-        for g in self.graphs:
-            if hasattr(a, "prepare"):
-                a.prepare(g)
-            g.run(a.algo, hops, windows, max_steps=max_steps if a.algo in ("cc", "diffusion", "vp") else 100,
-                  pr_iters=max_steps if a.algo == "pagerank" else 0, retain=self.retain)
+        _run_all(self.graphs, a, hops, windows, max_steps, self.retain)
         self.view_ms = (time.perf_counter() - t0) * 1e3 / max(1, len(hops))
         vt = int(round(self.view_ms))
         for h, t in enumerate(hops.tolist()):
@@ -476,6 +473,34 @@ class BWindowedRangeAnalysisTask(RangeAnalysisTask):
         return self.windows
 
 
+def _run_all(graphs, a, hops, windows, max_steps, retain) -> None:
+    """One job on every partition.  Runs are collective in partitioned mode (the partitions
+    exchange per superstep), so with several partitions in this process each runs on its own
+    thread, as the reference's Readers run concurrently."""
+    def one(g):
+        if hasattr(a, "prepare"):
+            a.prepare(g)
+        g.run(a.algo, hops, windows, max_steps=max_steps if a.algo in ("cc", "diffusion", "vp") else 100,
+              pr_iters=max_steps if a.algo == "pagerank" else 0, retain=retain)
+    if len(graphs) == 1:
+        one(graphs[0])
+        return
+    errs = []
+
+    def body(g):
+        try:
+            one(g)
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            errs.append(e)
+    th = [threading.Thread(target=body, args=(g,)) for g in graphs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
 # ---------------------------------------------------------------- live tasks
 class LiveAnalysisTask(AnalysisTask):
     """S/core/analysis/Tasks/LiveTasks/LiveAnalysisTask.scala:13-107.  One ``tick()`` is one job of
@@ -498,6 +523,7 @@ class LiveAnalysisTask(AnalysisTask):
         self.current_timestamp = 1  # :15
         self.live_time = 0
         self.first_time = True
+        self.last_job_time = None   # the timestamp of the last job that ran
         self._pending = False       # a restart happened: the next tick checks the new timestamp
 
     def timestamp(self) -> int:
@@ -532,11 +558,8 @@ class LiveAnalysisTask(AnalysisTask):
         ts = self.current_timestamp
         max_steps = a.defineMaxSteps()
         t0 = time.perf_counter()
-        for g in self.graphs:
-            if hasattr(a, "prepare"):
-                a.prepare(g)
-            g.run(a.algo, [ts], [], max_steps=max_steps if a.algo in ("cc", "diffusion", "vp") else 100,
-                  pr_iters=max_steps if a.algo == "pagerank" else 0, retain=self.retain)
+        _run_all(self.graphs, a, [ts], [], max_steps, self.retain)
+        self.last_job_time = ts
         vt = int(round((time.perf_counter() - t0) * 1e3))
         a.processResults([a.returnResults(g, 0, 0) for g in self.graphs], ts, vt)
         self.restart()

@@ -172,12 +172,47 @@ __global__ __launch_bounds__(kB) void k_ids(int64_t m, const uint32_t* __restric
                                             const int32_t* __restrict__ pos, int64_t* __restrict__ ids) {
   GLOOP(p, m) if (head[p]) ids[pos[p]] = key[p];
 }
-__global__ __launch_bounds__(kB) void k_isnew(int64_t nid, const int64_t* __restrict__ ids, const int64_t* __restrict__ vid0,
-                                              int64_t nv_old, uint8_t* __restrict__ isnew) {
-  GLOOP(k, nid) {
-    const int64_t j = lower(vid0, nv_old, ids[k]);
-    isnew[k] = !(j < nv_old && vid0[j] == ids[k]);
+// ---- partition roles (partitioned mode: pack_events' owned / ghost / not kept).  Owner of an id:
+// Utils.getPartition (rgpu_internal.hpp partition_of); nparts = 0: one partition, all owned.
+// Rank order = ascending key, key = id for owned vertices and kGhost | id for ghosts (owned by
+// id, then ghosts by id), so both rank maps stay monotone and the position formulas hold.
+constexpr int64_t kGhost = (int64_t)1 << 31;
+__device__ __forceinline__ bool owned_id(int64_t id, int part, int nparts) {
+  return nparts <= 0 || (int)((id % (10 * (int64_t)nparts)) / 10) == part;
+}
+// a non-owned endpoint of an edge update whose other endpoint is owned is kept as a ghost
+__global__ __launch_bounds__(kB) void k_ghost_need(int64_t m, const uint32_t* __restrict__ key,
+                                                   const uint32_t* __restrict__ val, const int32_t* __restrict__ head,
+                                                   const int32_t* __restrict__ pos, const DevEvent* __restrict__ ev,
+                                                   int part, int nparts, uint8_t* __restrict__ need) {
+  GLOOP(p, m) {
+    if (key[p] == kNoId) continue;
+    const uint32_t slot = val[p];
+    const DevEvent e = ev[slot >> 1];
+    if (e.kind < RGPU_EADD || e.src == e.dst) continue;
+    const int64_t me = (slot & 1) ? e.dst : e.src, other = (slot & 1) ? e.src : e.dst;
+    if (!owned_id(me, part, nparts) && owned_id(other, part, nparts)) need[pos[p] + head[p] - 1] = 1;
   }
+}
+// per distinct delta id: its rank-order key (-1: not kept here) and whether it is new
+__global__ __launch_bounds__(kB) void k_roles(int64_t nid, const int64_t* __restrict__ ids,
+                                              const int64_t* __restrict__ vid0, int64_t nv_old, int part, int nparts,
+                                              const uint8_t* __restrict__ need, int64_t* __restrict__ keyk,
+                                              uint8_t* __restrict__ isnew) {
+  GLOOP(k, nid) {
+    const int64_t id = ids[k];
+    const bool own = owned_id(id, part, nparts);
+    const int64_t key = own ? id : (kGhost | id);
+    const int64_t j = lower(vid0, nv_old, key);
+    const bool inbase = j < nv_old && vid0[j] == key;
+    const bool keep = own || inbase || (need && need[k]);
+    keyk[k] = keep ? key : -1;
+    isnew[k] = keep && !inbase;
+  }
+}
+__global__ __launch_bounds__(kB) void k_count_below(int64_t n, const int64_t* __restrict__ a, int64_t x,
+                                                    int64_t* __restrict__ out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out = lower(a, n, x);
 }
 __global__ __launch_bounds__(kB) void k_place_old(int64_t nv_old, const int64_t* __restrict__ vid0,
                                                   const int64_t* __restrict__ nid, int64_t nnew, int64_t* __restrict__ vid2,
@@ -200,9 +235,9 @@ __global__ __launch_bounds__(kB) void k_place_new(int64_t nnew, const int64_t* _
 }
 // every sorted slot p: its update's endpoint rank (the id's merged rank, a search in vid2 once
 // per distinct id through the run head)
-__global__ __launch_bounds__(kB) void k_idrank(int64_t nid, const int64_t* __restrict__ ids, const int64_t* __restrict__ vid2,
+__global__ __launch_bounds__(kB) void k_idrank(int64_t nid, const int64_t* __restrict__ keyk, const int64_t* __restrict__ vid2,
                                                int64_t nv2, int32_t* __restrict__ idrank) {
-  GLOOP(k, nid) idrank[k] = (int32_t)lower(vid2, nv2, ids[k]);
+  GLOOP(k, nid) idrank[k] = keyk[k] >= 0 ? (int32_t)lower(vid2, nv2, keyk[k]) : -1;
 }
 __global__ __launch_bounds__(kB) void k_ranks(int64_t m, const uint32_t* __restrict__ key, const uint32_t* __restrict__ val,
                                               const int32_t* __restrict__ head, const int32_t* __restrict__ pos,
@@ -228,15 +263,17 @@ __device__ __forceinline__ int64_t ord_at(const uint32_t* __restrict__ ord, int6
 
 // ---- vertex points: record 2q = the update's source (not for EdgeDelete), 2q+1 = its
 // destination (EdgeAdd, not a self-loop); value = 2i + endpoint
+// (owned ranks only: a ghost's history lives on its owner)
 __global__ __launch_bounds__(kB) void k_vrec(int64_t n, const DevEvent* __restrict__ ev, const uint32_t* __restrict__ ord,
-                                             const int32_t* __restrict__ rs, const int32_t* __restrict__ rd, uint32_t sent,
-                                             uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
+                                             const int32_t* __restrict__ rs, const int32_t* __restrict__ rd, int64_t n_own,
+                                             uint32_t sent, uint32_t* __restrict__ key, uint32_t* __restrict__ val) {
   GLOOP(q, n) {
     const int64_t i = ord_at(ord, q);
     const uint8_t kd = ev[i].kind;
-    key[2 * q] = kd != RGPU_EDEL ? (uint32_t)rs[i] : sent;
+    const int32_t a = rs[i], b = rd[i];
+    key[2 * q] = (kd != RGPU_EDEL && a >= 0 && a < n_own) ? (uint32_t)a : sent;
     val[2 * q] = (uint32_t)(2 * i);
-    key[2 * q + 1] = (kd == RGPU_EADD && rd[i] != rs[i]) ? (uint32_t)rd[i] : sent;
+    key[2 * q + 1] = (kd == RGPU_EADD && b != a && b >= 0 && b < n_own) ? (uint32_t)b : sent;
     val[2 * q + 1] = (uint32_t)(2 * i + 1);
   }
 }
@@ -276,44 +313,100 @@ __global__ __launch_bounds__(kB) void k_vfill(int64_t m, const uint32_t* __restr
   if (blockIdx.x == 0 && threadIdx.x == 0) dv_off[spos[m]] = kpos[m];
 }
 
-// ---- deaths: record q = the update's source if it is a VertexDelete; value = i
-__global__ __launch_bounds__(kB) void k_drec(int64_t n, const DevEvent* __restrict__ ev, const uint32_t* __restrict__ ord,
-                                             const int32_t* __restrict__ rs, uint32_t sent, uint32_t* __restrict__ key,
-                                             uint32_t* __restrict__ val) {
-  GLOOP(q, n) {
-    const int64_t i = ord_at(ord, q);
-    key[q] = ev[i].kind == RGPU_VDEL ? (uint32_t)rs[i] : sent;
-    val[q] = (uint32_t)i;
+// ---- deaths: the tick's VertexDeletes in (time, index) order, after the orphans (deaths of ids
+// that were not kept here when they arrived: partitioned mode keeps every VertexDelete, and an id
+// that later turns ghost needs its earlier deaths, which count as base deaths: last index 0)
+__global__ __launch_bounds__(kB) void k_del_flags(int64_t n, const DevEvent* __restrict__ ev,
+                                                  const uint32_t* __restrict__ ord, int32_t* __restrict__ f) {
+  GLOOP(q, n + 1) f[q] = q < n && ev[ord_at(ord, q)].kind == RGPU_VDEL;
+}
+__global__ __launch_bounds__(kB) void k_del_list(int64_t n, const uint32_t* __restrict__ ord, const int32_t* __restrict__ f,
+                                                 const int64_t* __restrict__ pos, uint32_t* __restrict__ delq) {
+  GLOOP(q, n) if (f[q]) delq[pos[q]] = (uint32_t)ord_at(ord, q);
+}
+__global__ __launch_bounds__(kB) void k_orph_rec(int64_t no, const int64_t* __restrict__ oid, const int64_t* __restrict__ ot,
+                                                 const int64_t* __restrict__ vid2, int64_t nv2, uint32_t sent,
+                                                 uint64_t* __restrict__ rt, uint32_t* __restrict__ rrank,
+                                                 int64_t* __restrict__ rlast, int64_t* __restrict__ rid,
+                                                 uint32_t* __restrict__ perm) {
+  GLOOP(k, no) {
+    const int64_t key = kGhost | oid[k];  // (an owned id is always kept: orphans are never owned)
+    const int64_t j = lower(vid2, nv2, key);
+    rrank[k] = j < nv2 && vid2[j] == key ? (uint32_t)j : sent;
+    rt[k] = (uint64_t)ot[k];
+    rlast[k] = 0;
+    rid[k] = oid[k];
+    perm[k] = (uint32_t)k;
   }
 }
-__global__ __launch_bounds__(kB) void k_dfill(int64_t m, const uint32_t* __restrict__ key, const uint32_t* __restrict__ val,
-                                              const DevEvent* __restrict__ ev, const int32_t* __restrict__ kept,
-                                              const int32_t* __restrict__ start, const int64_t* __restrict__ kpos,
-                                              const int64_t* __restrict__ spos, int32_t* __restrict__ dd_rank,
-                                              int64_t* __restrict__ dd_off, int64_t* __restrict__ dd_t,
-                                              int64_t* __restrict__ dd_last) {
-  GLOOP(p, m) {
+__global__ __launch_bounds__(kB) void k_del_rec(int64_t nd, int64_t no, const uint32_t* __restrict__ delq,
+                                                const DevEvent* __restrict__ ev, const int32_t* __restrict__ rs, uint32_t sent,
+                                                uint64_t* __restrict__ rt, uint32_t* __restrict__ rrank,
+                                                int64_t* __restrict__ rlast, int64_t* __restrict__ rid,
+                                                uint32_t* __restrict__ perm) {
+  GLOOP(j, nd) {
+    const uint32_t i = delq[j];
+    rrank[no + j] = rs[i] >= 0 ? (uint32_t)rs[i] : sent;
+    rt[no + j] = (uint64_t)ev[i].t;
+    rlast[no + j] = (int64_t)i + 1;
+    rid[no + j] = ev[i].src;
+    perm[no + j] = (uint32_t)(no + j);
+  }
+}
+__global__ __launch_bounds__(kB) void k_gather_u32(int64_t n, const uint32_t* __restrict__ perm,
+                                                   const uint32_t* __restrict__ a, uint32_t* __restrict__ out) {
+  GLOOP(k, n) out[k] = a[perm[k]];
+}
+// records sorted by (rank, time, last): kept = last of its (rank, time) run; start = first of its rank
+__global__ __launch_bounds__(kB) void k_drun_flags(int64_t R, const uint32_t* __restrict__ rk, const uint32_t* __restrict__ perm,
+                                                   const uint64_t* __restrict__ rt, uint32_t sent,
+                                                   int32_t* __restrict__ kept, int32_t* __restrict__ start) {
+  GLOOP(p, R + 1) {
+    int32_t k = 0, st = 0;
+    if (p < R && rk[p] != sent) {
+      st = p == 0 || rk[p - 1] != rk[p];
+      k = !(p + 1 < R && rk[p + 1] == rk[p] && rt[perm[p + 1]] == rt[perm[p]]);
+    }
+    kept[p] = k;
+    start[p] = st;
+  }
+}
+__global__ __launch_bounds__(kB) void k_dfill(int64_t R, const uint32_t* __restrict__ rk, const uint32_t* __restrict__ perm,
+                                              const uint64_t* __restrict__ rt, const int64_t* __restrict__ rlast,
+                                              const int32_t* __restrict__ kept, const int32_t* __restrict__ start,
+                                              const int64_t* __restrict__ kpos, const int64_t* __restrict__ spos,
+                                              int32_t* __restrict__ dd_rank, int64_t* __restrict__ dd_off,
+                                              int64_t* __restrict__ dd_t, int64_t* __restrict__ dd_last) {
+  GLOOP(p, R) {
     if (start[p]) {
-      dd_rank[spos[p]] = (int32_t)key[p];
+      dd_rank[spos[p]] = (int32_t)rk[p];
       dd_off[spos[p]] = kpos[p];
     }
     if (kept[p]) {
-      dd_t[kpos[p]] = ev[val[p]].t;
-      dd_last[kpos[p]] = (int64_t)val[p] + 1;
+      dd_t[kpos[p]] = (int64_t)rt[perm[p]];
+      dd_last[kpos[p]] = rlast[perm[p]];
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) dd_off[spos[m]] = kpos[m];
+  if (blockIdx.x == 0 && threadIdx.x == 0) dd_off[spos[R]] = kpos[R];
 }
 
 // ---- edge points: key = src * nv2 + dst for edge updates (sentinel nv2^2); value = i
+// (kept iff both endpoints are kept and one is owned; cnt = the kept records)
 __global__ __launch_bounds__(kB) void k_erec(int64_t n, const DevEvent* __restrict__ ev, const uint32_t* __restrict__ ord,
                                              const int32_t* __restrict__ rs, const int32_t* __restrict__ rd, uint64_t nv2,
-                                             uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+                                             int64_t n_own, uint64_t* __restrict__ key, uint32_t* __restrict__ val,
+                                             unsigned long long* __restrict__ cnt) {
+  unsigned long long c = 0;
   GLOOP(q, n) {
     const int64_t i = ord_at(ord, q);
-    key[q] = ev[i].kind >= RGPU_EADD ? (uint64_t)rs[i] * nv2 + (uint64_t)rd[i] : nv2 * nv2;
+    const int32_t a = rs[i], b = rd[i];
+    const bool kept = ev[i].kind >= RGPU_EADD && a >= 0 && b >= 0 && (a < n_own || b < n_own);
+    key[q] = kept ? (uint64_t)a * nv2 + (uint64_t)b : nv2 * nv2;
     val[q] = (uint32_t)i;
+    c += kept;
   }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
 }
 __global__ __launch_bounds__(kB) void k_egroups(int64_t m, const uint64_t* __restrict__ key, int32_t* __restrict__ start) {
   GLOOP(p, m + 1) start[p] = p < m && (p == 0 || key[p] != key[p - 1]);
@@ -519,6 +612,52 @@ __global__ __launch_bounds__(kB) void k_scatter_i32(int64_t n, const int32_t* __
   GLOOP(k, n) out[idx[k]] = val[k];
 }
 
+// ---- partition metadata of a merged partitioned graph (what pack_events + rgpu_seal build on
+// the host for a full seal): labels = ids, the exchange plan, the owned-id index
+__global__ __launch_bounds__(kB) void k_grank(int64_t nv, const int64_t* __restrict__ keys, int32_t* __restrict__ grank) {
+  GLOOP(v, nv) grank[v] = (int32_t)(keys[v] & (kGhost - 1));
+}
+// an edge between owned v and ghost g (owner q): v goes on the send list to q, g on the receive
+// list from q (ranks ascend with ids within a role, so (q, rank) order is pack_events' (q, id))
+__global__ __launch_bounds__(kB) void k_cut_pairs(int64_t ne, const int32_t* __restrict__ esrc,
+                                                  const int32_t* __restrict__ edst, const int64_t* __restrict__ keys,
+                                                  int64_t n_own, int nparts, uint64_t* __restrict__ sk,
+                                                  uint64_t* __restrict__ rk) {
+  const uint64_t sent = (uint64_t)nparts << 32;
+  GLOOP(e, ne) {
+    const int32_t a = esrc[e], b = edst[e];
+    if ((a < n_own) == (b < n_own)) {
+      sk[e] = rk[e] = sent;
+      continue;
+    }
+    const int32_t own = a < n_own ? a : b, gh = a < n_own ? b : a;
+    const int64_t id = keys[gh] & (kGhost - 1);
+    const uint64_t q = (uint64_t)((id % (10 * (int64_t)nparts)) / 10);
+    sk[e] = (q << 32) | (uint32_t)own;
+    rk[e] = (q << 32) | (uint32_t)gh;
+  }
+}
+__global__ __launch_bounds__(kB) void k_uniq_flags(int64_t n, const uint64_t* __restrict__ k, uint64_t sent,
+                                                   int32_t* __restrict__ f) {
+  GLOOP(p, n + 1) f[p] = p < n && k[p] != sent && (p == 0 || k[p] != k[p - 1]);
+}
+__global__ __launch_bounds__(kB) void k_uniq_fill(int64_t n, const uint64_t* __restrict__ k, const int32_t* __restrict__ f,
+                                                  const int32_t* __restrict__ pos, int32_t* __restrict__ v,
+                                                  int32_t* __restrict__ q) {
+  GLOOP(p, n) if (f[p]) {
+    v[pos[p]] = (int32_t)(k[p] & 0xffffffffu);
+    q[pos[p]] = (int32_t)(k[p] >> 32);
+  }
+}
+__global__ __launch_bounds__(kB) void k_q_offsets(int64_t n, const int32_t* __restrict__ q, int nparts,
+                                                  int64_t* __restrict__ off) {
+  GLOOP(p, nparts + 1) off[p] = lower(q, n, (int32_t)p);
+}
+__global__ __launch_bounds__(kB) void k_bucket_counts(int64_t n, const int64_t* __restrict__ ids, int shift,
+                                                      int32_t* __restrict__ cnt) {
+  GLOOP(k, n) atomicAdd(&cnt[ids[k] >> shift], 1);
+}
+
 }  // namespace
 
 void launch_scatter_i32(hipStream_t s, int64_t n, const int32_t* idx, const int32_t* val, int32_t* out) {
@@ -526,7 +665,8 @@ void launch_scatter_i32(hipStream_t s, int64_t n, const int32_t* idx, const int3
 }
 
 std::string gpu_pack_delta(hipStream_t s, const DevEvent* ev, int64_t n, const DevGraph& g0, const int64_t* vid0,
-                           int64_t heavy_t, DeltaDev* out, std::vector<void*>& T, std::vector<void*>& L) {
+                           const DeltaPart& P, int64_t heavy_t, DeltaDev* out, std::vector<void*>& T,
+                           std::vector<void*>& L) {
   Mem M{T, L};
   DeltaDev& D = *out;
   D = DeltaDev();
@@ -564,17 +704,40 @@ std::string gpu_pack_delta(hipStream_t s, const DevEvent* ev, int64_t n, const D
   const int64_t nid = fetch(s, hpos + m);
   int64_t* ids = M.alloc<int64_t>(nid);
   k_ids<<<gridn(m), kB, 0, s>>>(m, k1, head, hpos, ids);
+  // roles and rank-order keys; the new keys ascending
+  uint8_t* need = nullptr;
+  if (P.nparts > 0) {
+    need = M.alloc<uint8_t>(nid);
+    GCHK(hipMemsetAsync(need, 0, nid, s));
+    k_ghost_need<<<gridn(m), kB, 0, s>>>(m, k1, v1, head, hpos, ev, P.part, P.nparts, need);
+  }
+  int64_t* keyk = M.alloc<int64_t>(nid);
   uint8_t* isnew = M.alloc<uint8_t>(nid);
-  k_isnew<<<gridn(nid), kB, 0, s>>>(nid, ids, vid0, nv_old, isnew);
+  k_roles<<<gridn(nid), kB, 0, s>>>(nid, ids, vid0, nv_old, P.part, P.nparts, need, keyk, isnew);
   int64_t* nidv = M.alloc<int64_t>(nid);
   int* nsel = M.alloc<int>(1);
   {
     size_t b = 0;
-    GCHK(hipcub::DeviceSelect::Flagged(nullptr, b, ids, isnew, nidv, nsel, (int)nid, s));
+    GCHK(hipcub::DeviceSelect::Flagged(nullptr, b, keyk, isnew, nidv, nsel, (int)nid, s));
     void* t = M.temp(b);
-    GCHK(hipcub::DeviceSelect::Flagged(t, b, ids, isnew, nidv, nsel, (int)nid, s));
+    GCHK(hipcub::DeviceSelect::Flagged(t, b, keyk, isnew, nidv, nsel, (int)nid, s));
   }
   const int64_t nnew = fetch(s, nsel);
+  if (P.nparts > 0 && nnew > 1) {  // owned keys, then ghost keys: ascending again
+    uint64_t* sorted = (uint64_t*)M.alloc<int64_t>(nnew);
+    size_t b = 0;
+    GCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, b, (const uint64_t*)nidv, sorted, (int)nnew, 0, 32, s));
+    void* t = M.temp(b);
+    GCHK(hipcub::DeviceRadixSort::SortKeys(t, b, (const uint64_t*)nidv, sorted, (int)nnew, 0, 32, s));
+    nidv = (int64_t*)sorted;
+  }
+  int64_t n_own2 = nv_old + nnew;
+  if (P.nparts > 0) {
+    int64_t* below = M.alloc<int64_t>(1);
+    k_count_below<<<1, 64, 0, s>>>(nnew, nidv, kGhost, below);
+    n_own2 = P.n_own_old + fetch(s, below);
+  }
+  D.n_own2 = n_own2;
   const int64_t nv2 = nv_old + nnew;
   if (nv2 > (int64_t)INT32_MAX - 1) return "more than 2^31 - 1 vertices";
   D.nv2 = nv2;
@@ -584,7 +747,7 @@ std::string gpu_pack_delta(hipStream_t s, const DevEvent* ev, int64_t n, const D
   if (nv_old) k_place_old<<<gridn(nv_old), kB, 0, s>>>(nv_old, vid0, nidv, nnew, D.vid2, D.old2new, D.new2old);
   if (nnew) k_place_new<<<gridn(nnew), kB, 0, s>>>(nnew, nidv, vid0, nv_old, D.vid2, D.new2old);
   int32_t* idrank = M.alloc<int32_t>(nid);
-  k_idrank<<<gridn(nid), kB, 0, s>>>(nid, ids, D.vid2, nv2, idrank);
+  k_idrank<<<gridn(nid), kB, 0, s>>>(nid, keyk, D.vid2, nv2, idrank);
   int32_t* rs = M.alloc<int32_t>(n);
   int32_t* rd = M.alloc<int32_t>(n);
   GCHK(hipMemsetAsync(rd, 0xff, sizeof(int32_t) * n, s));
@@ -606,7 +769,7 @@ std::string gpu_pack_delta(hipStream_t s, const DevEvent* ev, int64_t n, const D
   int64_t* kpos = M.alloc<int64_t>(m + 1);
   int64_t* spos = M.alloc<int64_t>(m + 1);
   // ---- vertex points
-  k_vrec<<<gridn(n), kB, 0, s>>>(n, ev, ord, rs, rd, vsent, k0, v0);
+  k_vrec<<<gridn(n), kB, 0, s>>>(n, ev, ord, rs, rd, n_own2, vsent, k0, v0);
   sort_pairs(M, s, k0, k1, v0, v1, m, vbits);
   k_run_flags<<<gridn(m + 1), kB, 0, s>>>(m, k1, v1, 1, vsent, ev, kept, start);
   excl_sum(M, s, kept, kpos, m + 1);
@@ -623,23 +786,64 @@ std::string gpu_pack_delta(hipStream_t s, const DevEvent* ev, int64_t n, const D
   D.dv_off = M.alloc<int64_t>(D.ndv + 1);
   D.dv_key = M.alloc<int64_t>(D.ndvk);
   k_vfill<<<gridn(m), kB, 0, s>>>(m, k1, v1, ev, kept, start, kpos, spos, D.dv_rank, D.dv_off, D.dv_key);
-  // ---- deaths (VertexDelete is rare: skipped when the tick has none)
-  if (n_vdel) {
-    k_drec<<<gridn(n), kB, 0, s>>>(n, ev, ord, rs, vsent, k0, v0);
-    sort_pairs(M, s, k0, k1, v0, v1, n, vbits);
-    k_run_flags<<<gridn(n + 1), kB, 0, s>>>(n, k1, v1, 0, vsent, ev, kept, start);
-    excl_sum(M, s, kept, kpos, n + 1);
-    excl_sum(M, s, start, spos, n + 1);
+  // ---- deaths (VertexDelete is rare: compacted first; skipped when there are none)
+  if (n_vdel || P.n_orph) {
+    int64_t* dpos = kpos;  // (reused)
+    uint32_t* delq = k0;
+    if (n_vdel) {
+      k_del_flags<<<gridn(n + 1), kB, 0, s>>>(n, ev, ord, kept);
+      excl_sum(M, s, kept, dpos, n + 1);
+      k_del_list<<<gridn(n), kB, 0, s>>>(n, ord, kept, dpos, delq);
+    }
+    const int64_t no = P.n_orph, R = no + n_vdel;
+    uint64_t* rt = M.alloc<uint64_t>(R);
+    uint64_t* rt1 = M.alloc<uint64_t>(R);
+    uint32_t* rrank = M.alloc<uint32_t>(R);
+    uint32_t* rk1 = M.alloc<uint32_t>(R);
+    uint32_t* rk2 = M.alloc<uint32_t>(R);
+    int64_t* rlast = M.alloc<int64_t>(R);
+    int64_t* rid = M.alloc<int64_t>(R);
+    uint32_t* perm0 = M.alloc<uint32_t>(R);
+    uint32_t* perm1 = M.alloc<uint32_t>(R);
+    uint32_t* perm2 = M.alloc<uint32_t>(R);
+    if (no) k_orph_rec<<<gridn(no), kB, 0, s>>>(no, P.orph_id, P.orph_t, D.vid2, nv2, vsent, rt, rrank, rlast, rid, perm0);
+    if (n_vdel) k_del_rec<<<gridn(n_vdel), kB, 0, s>>>(n_vdel, no, delq, ev, rs, vsent, rt, rrank, rlast, rid, perm0);
+    // (time, record order), then rank: both stable
+    sort_pairs(M, s, rt, rt1, perm0, perm1, R, 61);
+    k_gather_u32<<<gridn(R), kB, 0, s>>>(R, perm1, rrank, rk1);
+    sort_pairs(M, s, rk1, rk2, perm1, perm2, R, bits_for((uint64_t)nv2));
+    int32_t* dk = M.alloc<int32_t>(R + 1);
+    int32_t* dst = M.alloc<int32_t>(R + 1);
+    int64_t* dkp = M.alloc<int64_t>(R + 1);
+    int64_t* dsp = M.alloc<int64_t>(R + 1);
+    k_drun_flags<<<gridn(R + 1), kB, 0, s>>>(R, rk2, perm2, rt, vsent, dk, dst);
+    excl_sum(M, s, dk, dkp, R + 1);
+    excl_sum(M, s, dst, dsp, R + 1);
     int64_t t2[2];
-    GCHK(hipMemcpyAsync(&t2[0], kpos + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    GCHK(hipMemcpyAsync(&t2[1], spos + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    GCHK(hipMemcpyAsync(&t2[0], dkp + R, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    GCHK(hipMemcpyAsync(&t2[1], dsp + R, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    // deaths of ids still not kept here: the orphans of the next seal (host list)
+    std::vector<uint32_t> hr(R);
+    std::vector<int64_t> hid(R), ht(R);
+    if (P.nparts > 0) {
+      GCHK(hipMemcpyAsync(hr.data(), rrank, sizeof(uint32_t) * R, hipMemcpyDeviceToHost, s));
+      GCHK(hipMemcpyAsync(hid.data(), rid, sizeof(int64_t) * R, hipMemcpyDeviceToHost, s));
+      GCHK(hipMemcpyAsync(ht.data(), rt, sizeof(int64_t) * R, hipMemcpyDeviceToHost, s));
+    }
     GCHK(hipStreamSynchronize(s));
+    if (P.nparts > 0)
+      for (int64_t k = 0; k < R; k++)
+        if (hr[k] == vsent) {
+          D.orph_id.push_back(hid[k]);
+          D.orph_t.push_back(ht[k]);
+        }
     D.ndd = t2[1];
     D.dd_rank = M.alloc<int32_t>(D.ndd);
     D.dd_off = M.alloc<int64_t>(D.ndd + 1);
     D.dd_t = M.alloc<int64_t>(t2[0]);
     D.dd_last = M.alloc<int64_t>(t2[0]);
-    k_dfill<<<gridn(n), kB, 0, s>>>(n, k1, v1, ev, kept, start, kpos, spos, D.dd_rank, D.dd_off, D.dd_t, D.dd_last);
+    k_dfill<<<gridn(R), kB, 0, s>>>(R, rk2, perm2, rt, rlast, dk, dst, dkp, dsp, D.dd_rank, D.dd_off, D.dd_t,
+                                    D.dd_last);
   }
   // ---- edge points grouped by (src, dst)
   if (n_eupd) {
@@ -647,9 +851,11 @@ std::string gpu_pack_delta(hipStream_t s, const DevEvent* ev, int64_t n, const D
     uint64_t* ek1 = M.alloc<uint64_t>(n);
     uint32_t* pval = M.alloc<uint32_t>(n);
     const uint64_t nvu = (uint64_t)nv2;
-    k_erec<<<gridn(n), kB, 0, s>>>(n, ev, ord, rs, rd, nvu, ek0, v0);
+    unsigned long long* ecnt = (unsigned long long*)M.alloc<int64_t>(1);
+    GCHK(hipMemsetAsync(ecnt, 0, sizeof(unsigned long long), s));
+    k_erec<<<gridn(n), kB, 0, s>>>(n, ev, ord, rs, rd, nvu, n_own2, ek0, v0, ecnt);
     sort_pairs(M, s, ek0, ek1, v0, pval, n, bits_for(nvu * nvu));
-    const int64_t nr = n_eupd;  // the valid records come first
+    const int64_t nr = (int64_t)fetch(s, ecnt);  // the kept records come first
     int32_t* gpos = hpos;       // (reused: m + 1 >= nr + 1)
     k_egroups<<<gridn(nr + 1), kB, 0, s>>>(nr, ek1, start);
     excl_sum(M, s, start, gpos, nr + 1);
@@ -747,6 +953,67 @@ std::string gpu_pack_delta(hipStream_t s, const DevEvent* ev, int64_t n, const D
       GCHK(hipStreamSynchronize(s));
     }
   }
+  GCHK(hipGetLastError());
+  GCHK(hipStreamSynchronize(s));
+  return "";
+}
+
+namespace {
+// (q, rank) pairs -> distinct, ascending; per-q offsets (device and host)
+void plan_list(Mem& M, hipStream_t s, uint64_t* k0, uint64_t* k1, int64_t ne, int nparts, int32_t** v, int32_t** q,
+               int64_t** off_d, std::vector<int64_t>& off, int64_t* n_out) {
+  const uint64_t sent = (uint64_t)nparts << 32;
+  if (ne > 0) {
+    size_t b = 0;
+    const int eb = 32 + bits_for((uint64_t)nparts);
+    GCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, b, k0, k1, (int)ne, 0, eb, s));
+    void* t = M.temp(b);
+    GCHK(hipcub::DeviceRadixSort::SortKeys(t, b, k0, k1, (int)ne, 0, eb, s));
+  }
+  int32_t* f = M.alloc<int32_t>(ne + 1);
+  int32_t* pos = M.alloc<int32_t>(ne + 1);
+  k_uniq_flags<<<gridn(ne + 1), kB, 0, s>>>(ne, k1, sent, f);
+  excl_sum(M, s, f, pos, ne + 1);
+  const int64_t n = fetch(s, pos + ne);
+  *v = M.alloc<int32_t>(n, true);
+  *q = M.alloc<int32_t>(n, true);
+  if (ne) k_uniq_fill<<<gridn(ne), kB, 0, s>>>(ne, k1, f, pos, *v, *q);
+  *off_d = M.alloc<int64_t>(nparts + 1, true);
+  k_q_offsets<<<1, kB, 0, s>>>(n, *q, nparts, *off_d);
+  off.resize(nparts + 1);
+  GCHK(hipMemcpyAsync(off.data(), *off_d, sizeof(int64_t) * (nparts + 1), hipMemcpyDeviceToHost, s));
+  GCHK(hipStreamSynchronize(s));
+  *n_out = n;
+}
+}  // namespace
+
+std::string gpu_part_meta(hipStream_t s, const int64_t* keys, int64_t nv, int64_t n_own, const int32_t* esrc,
+                          const int32_t* edst, int64_t ne, int nparts, PartMeta* out, std::vector<void*>& T,
+                          std::vector<void*>& L) {
+  Mem M{T, L};
+  PartMeta& X = *out;
+  X = PartMeta();
+  X.grank = M.alloc<int32_t>(nv, true);
+  if (nv) k_grank<<<gridn(nv), kB, 0, s>>>(nv, keys, X.grank);
+  uint64_t* sk = M.alloc<uint64_t>(ne);
+  uint64_t* rk = M.alloc<uint64_t>(ne);
+  uint64_t* k1 = M.alloc<uint64_t>(ne);
+  if (ne) k_cut_pairs<<<gridn(ne), kB, 0, s>>>(ne, esrc, edst, keys, n_own, nparts, sk, rk);
+  plan_list(M, s, sk, k1, ne, nparts, &X.xs_v, &X.xs_q, &X.xs_off_d, X.xs_off, &X.nxs);
+  plan_list(M, s, rk, k1, ne, nparts, &X.xr_v, &X.xr_q, &X.xr_off_d, X.xr_off, &X.nxr);
+  // owned ids ascending (the owned keys are the ids), bucketed by id >> shift (about one id per
+  // bucket; rgpu_seal's full-seal index)
+  X.own_vid = M.alloc<int64_t>(n_own, true);
+  if (n_own) GCHK(hipMemcpyAsync(X.own_vid, keys, sizeof(int64_t) * n_own, hipMemcpyDeviceToDevice, s));
+  int lg = 0;
+  while (((int64_t)1 << lg) < std::max<int64_t>(n_own, 1)) lg++;
+  X.shift = std::max(0, 31 - lg);
+  const int64_t nbk = ((int64_t)1 << 31) >> X.shift;
+  int32_t* cnt = M.alloc<int32_t>(nbk + 1);
+  GCHK(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (nbk + 1), s));
+  if (n_own) k_bucket_counts<<<gridn(n_own), kB, 0, s>>>(n_own, X.own_vid, X.shift, cnt);
+  X.own_boff = M.alloc<int32_t>(nbk + 1, true);
+  excl_sum(M, s, cnt, X.own_boff, nbk + 1);
   GCHK(hipGetLastError());
   GCHK(hipStreamSynchronize(s));
   return "";

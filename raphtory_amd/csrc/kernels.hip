@@ -494,12 +494,22 @@ __device__ __forceinline__ bool dense_rule(const int32_t* __restrict__ ccount, i
   return x * div >= nv;
 }
 
-// Items per wave round of a grid-stride loop whose lanes first load one word per item: 64
-// when the grid has at most one round of 64 per wave, else just enough to spread the items
-// over every wave.
-__device__ __forceinline__ int64_t wave_span(int64_t n, int64_t nwaves) {
+
+// Group-cyclic dealing of n items over the waves of a grid-stride loop: items go in groups of G
+// consecutive ones (G a power of two, gmax at most, about n / nwaves when that is smaller), group
+// g to wave g mod nwaves; in round r lane l takes item l mod G of the wave's group r * 64/G + l / G.
+// G consecutive items keep the lanes' first loads in whole cache lines (G = 16 view masks or 32
+// chunk flag words = one 128-B line), and dealing the groups cyclically spreads a run of busy items
+// (the locality order puts the hubs first) over many waves.  Small graphs get small groups, so
+// that every wave has work.
+__device__ __forceinline__ int deal_group(int64_t n, int64_t nwaves, int gmax) {
   const int64_t s = (n + nwaves - 1) / nwaves;
-  return s < 1 ? 1 : (s > 64 ? 64 : s);
+  int G = 1;
+  while (G < s && G < gmax) G <<= 1;
+  return G;
+}
+__device__ __forceinline__ int64_t dealt_item(int64_t wave, int64_t nwaves, int64_t r, int G, int l) {
+  return (wave + (r * (64 / G) + l / G) * nwaves) * G + (l & (G - 1));
 }
 
 struct StepWork {
@@ -569,18 +579,18 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
   Ctr members{}, alive{}, scanned{}, lw{}, uwn{};
   unsigned long long changed = 0;
   uint64_t lanes = 0;  // views with a step-1 change in this wave
-  // Vertices are dealt to the waves cyclically (rank v goes to wave v mod nwaves): in the locality
-  // order (packer.cpp locality_order) ranks are sorted by activity, so consecutive ranks have
-  // similar slot counts, and a contiguous run per wave would hand one wave all the busiest
-  // vertices.  Per round the lanes read 64 vertices' view masks, clear the non-members' count /
-  // mask words, and the wave then walks the members one by one.
-  for (int64_t k0 = 0; wave + k0 * nwaves < nv; k0 += 64) {
-   const int64_t vlane = wave + (k0 + lane) * nwaves;
+  // Vertices are dealt in groups of up to 16 (deal_group): in the locality order (packer.cpp
+  // locality_order) ranks are sorted by activity, so a contiguous run of 64 per wave would hand one
+  // wave the 64 busiest vertices.  Per round the lanes read 64 vertices' view masks, clear the
+  // non-members' count / mask words, and the wave then walks the members one by one.
+  const int G = deal_group(nv, nwaves, 16);
+  for (int64_t r = 0; (wave + r * (64 / G) * nwaves) * G < nv; r++) {
+   const int64_t vlane = dealt_item(wave, nwaves, r, G, lane);
    const uint64_t mvl = vlane < nv ? vm[vlane] : 0;
    if (vlane < nv && mvl == 0) { cnt[vlane] = 0; vadj[vlane] = 0; }
    uint64_t todo = __ballot(mvl != 0);
    while (todo) {
-    const int64_t v = wave + (k0 + __builtin_ctzll(todo)) * nwaves;
+    const int64_t v = dealt_item(wave, nwaves, r, G, __builtin_ctzll(todo));
     const uint64_t mv = readlane64(mvl, __builtin_ctzll(todo));
     todo &= todo - 1;
     const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
@@ -1155,14 +1165,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
   int32_t changed = 0;
   std::conditional_t<PROF, StepWork, NoWork> wk;
   const TailList none{nullptr, nullptr};
-  // Chunks are dealt to the waves cyclically (chunk c goes to wave c mod nwaves, as K2 deals
-  // vertices): per round lane l reads its chunk's frontier flags, and the wave then runs only the
-  // flagged chunks — a sparse frontier costs one load per 64 chunks.  Every wave of the grid gets
-  // work on a small graph too, and the busy chunks of the locality order (runs of hubs) spread
-  // over the waves instead of queueing behind one.
+  // Chunks are dealt in groups of up to 32 (deal_group, as K2 deals vertices): per round lane l
+  // reads its chunk's frontier flags (whole lines), and the wave then runs only the flagged
+  // chunks — a sparse frontier costs one load per 64 chunks.  Every wave of the grid gets work on
+  // a small graph too, and the busy chunks of the locality order (runs of hubs) spread over the
+  // waves instead of queueing behind one.
   const int64_t nchunks = (nv + CH - 1) / CH;
-  for (int64_t k0 = 0; wave + k0 * nwaves < nchunks; k0 += 64) {
-    const int64_t cl = wave + (k0 + lane) * nwaves;
+  const int G = deal_group(nchunks, nwaves, 32);
+  for (int64_t r = 0; (wave + r * (64 / G) * nwaves) * G < nchunks; r++) {
+    const int64_t cl = dealt_item(wave, nwaves, r, G, lane);
     uint32_t fb = 0;
     if (cl < nchunks) {
       const int64_t v0 = cl * CH;
@@ -1181,7 +1192,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
       const int L = __builtin_ctzll(todo);
       todo &= todo - 1;
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
-      cc_chunk<CH, BUF, false>((wave + (k0 + L) * nwaves) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
+      cc_chunk<CH, BUF, false>(dealt_item(wave, nwaves, r, G, L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
                                lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
                                hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks);
     }

@@ -364,11 +364,36 @@ struct DeltaDev {
   int64_t n_in = 0, ndt = 0;
   std::vector<int32_t> heavy;                    // ranks with more than heavy_t static slots
   std::vector<int64_t> heavy_a0, heavy_deg;      // their first static slot and slot count
+  int64_t n_own2 = 0;                            // owned ranks [0, n_own2) of the merged graph
+  std::vector<int64_t> orph_id, orph_t;          // deaths of ids not kept here (partitioned mode)
+};
+// Partitioned mode (nparts 0: one partition).  Ids are the graph's rank-order keys: the id for
+// an owned vertex, 2^31 | id for a ghost.  Orphans: deaths of ids not kept here (device arrays).
+struct DeltaPart {
+  int part = 0, nparts = 0;
+  int64_t n_own_old = 0;
+  const int64_t *orph_id = nullptr, *orph_t = nullptr;
+  int64_t n_orph = 0;
 };
 // ev[0, n): the updates since the last seal; vid0: the base ids (device).  Device arrays go to
 // T (temporaries) or L (the merged graph).  Returns "" or the first invalid update's message.
 std::string gpu_pack_delta(hipStream_t s, const DevEvent* ev, int64_t n, const DevGraph& g0, const int64_t* vid0,
-                           int64_t heavy_t, DeltaDev* out, std::vector<void*>& T, std::vector<void*>& L);
+                           const DeltaPart& P, int64_t heavy_t, DeltaDev* out, std::vector<void*>& T,
+                           std::vector<void*>& L);
 void launch_scatter_i32(hipStream_t s, int64_t n, const int32_t* idx, const int32_t* val, int32_t* out);
+// Partition metadata of a merged partitioned graph (keys: its rank-order keys, DeltaPart)
+struct PartMeta {
+  int32_t* grank = nullptr;                     // [nv] CC label = vertex id
+  int32_t *xs_v = nullptr, *xs_q = nullptr, *xr_v = nullptr, *xr_q = nullptr;  // exchange plan
+  int64_t *xs_off_d = nullptr, *xr_off_d = nullptr;
+  std::vector<int64_t> xs_off, xr_off;
+  int64_t nxs = 0, nxr = 0;
+  int64_t* own_vid = nullptr;                   // owned ids ascending
+  int32_t* own_boff = nullptr;                  // their buckets (id >> shift)
+  int shift = 0;
+};
+std::string gpu_part_meta(hipStream_t s, const int64_t* keys, int64_t nv, int64_t n_own, const int32_t* esrc,
+                          const int32_t* edst, int64_t ne, int nparts, PartMeta* out, std::vector<void*>& T,
+                          std::vector<void*>& L);
 
 }  // namespace rgpu

@@ -182,6 +182,7 @@ struct rgpu_ctx {
   int64_t* g_vid = nullptr;             // device delta packer: the resident graph's ids (graph list)
   bool vid_stale = false;               // pk.vid lags g_vid (downloaded when results name ids)
   int64_t n_dtime = -1;                 // device delta packer: death times (pk.dtime is not kept)
+  std::vector<int64_t> orph_id, orph_t; // partitioned: deaths of ids not kept here (DeltaPart)
   int vertex_order = RGPU_ORDER_LOCALITY;  // rgpu_set_vertex_order: local rank order of a full seal
   Packed pk;
   DevGraph g;
@@ -1653,6 +1654,8 @@ int sync_vid(rgpu_ctx* c) {
     c->pk.vid.resize((size_t)c->g.nv);
     if (c->g.nv)
       HIPCHK(hipMemcpy(c->pk.vid.data(), c->g_vid, sizeof(int64_t) * c->g.nv, hipMemcpyDeviceToHost));
+    if (c->partitioned)  // (rank-order keys: 2^31 | id for a ghost)
+      for (int64_t v = c->pk.n_own; v < c->g.nv; v++) c->pk.vid[v] &= ((int64_t)1 << 31) - 1;
   } catch (const HipFail& f) {
     return fail(c, RGPU_EHIP, f.msg);
   } catch (const std::bad_alloc&) {
@@ -1967,17 +1970,31 @@ void seal_delta(rgpu_ctx* c) {
     m.nvk_old = B.n_vkey;
     int64_t nv2 = 0, n_in2 = 0;
     if (dev) {
-      if (!c->g_vid) {  // the first merge into a full seal: its ids, once
+      if (!c->g_vid) {  // the first merge into a full seal: its rank-order keys, once (DeltaPart)
+        std::vector<int64_t> keys(B.vid);
+        if (c->partitioned)
+          for (int64_t v = B.n_own; v < B.nv; v++) keys[v] |= (int64_t)1 << 31;
         c->g_vid = dalloc<int64_t>(c->graph_allocs, g0.nv);
-        HIPCHK(hipMemcpyAsync(c->g_vid, B.vid.data(), sizeof(int64_t) * g0.nv, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpy(c->g_vid, keys.data(), sizeof(int64_t) * g0.nv, hipMemcpyHostToDevice));
       }
       const int64_t n = (int64_t)(c->events.size() - c->n_sealed);
       DevEvent* ev = dalloc<DevEvent>(T, n);
       HIPCHK(hipMemcpyAsync(ev, c->events.data() + c->n_sealed, sizeof(Event) * n, hipMemcpyHostToDevice, s));
       phase("upload");
+      DeltaPart dp;
+      if (c->partitioned) {
+        dp.part = c->part;
+        dp.nparts = c->nparts;
+        dp.n_own_old = B.n_own;
+        dp.n_orph = (int64_t)c->orph_id.size();
+        if (dp.n_orph) {
+          dp.orph_id = dupload(T, c->orph_id);
+          dp.orph_t = dupload(T, c->orph_t);
+        }
+      }
       std::string e;
       try {
-        e = gpu_pack_delta(s, ev, n, g0, c->g_vid, c->heavy_t, &DD, T, L);
+        e = gpu_pack_delta(s, ev, n, g0, c->g_vid, dp, c->heavy_t, &DD, T, L);
       } catch (const std::runtime_error& x) {
         throw HipFail{x.what()};
       }
@@ -2053,7 +2070,8 @@ void seal_delta(rgpu_ctx* c) {
     HIPCHK(hipStreamSynchronize(s));
     phase("upload");
     DevGraph g;
-    g.nv = g.n_own = nv2;
+    g.nv = nv2;
+    g.n_own = dev ? DD.n_own2 : nv2;
     g.ne = g0.ne + m.n_new;
     g.n_in = n_in2;
     int32_t* esrc2 = dalloc<int32_t>(L, g.ne);
@@ -2129,6 +2147,18 @@ void seal_delta(rgpu_ctx* c) {
     phase("heavy");
     build_tslots(c, g, L);
     phase("time-ordered slots");
+    PartMeta PM;
+    int64_t ne_owned = g.ne;
+    if (c->partitioned) {  // labels = ids, the exchange plan and the owned-id index of the merged graph
+      try {
+        (void)gpu_part_meta(s, DD.vid2, nv2, g.n_own, esrc2, edst2, g.ne, c->nparts, &PM, T, L);
+      } catch (const std::runtime_error& x) {
+        throw HipFail{x.what()};
+      }
+      g.grank = PM.grank;
+      HIPCHK(hipMemcpy(&ne_owned, DD.out_off + g.n_own, sizeof(int64_t), hipMemcpyDeviceToHost));  // (owned first)
+      phase("partition plan");
+    }
     for (void* p : T) (void)hipFree(p);
     T.clear();
     (void)hipStreamDestroy(s);
@@ -2141,6 +2171,33 @@ void seal_delta(rgpu_ctx* c) {
     L.clear();
     c->g = g;
     c->g_vid = dev ? DD.vid2 : nullptr;
+    if (c->partitioned) {  // the old plan's buffers went with the old graph; channels stay
+      free_part_slots(c, true);
+      Exchange* x = c->pt.xchg;
+      XSlot xs[4];
+      for (int i = 0; i < 4; i++) xs[i].x = c->pt.xs[i].x;
+      c->pt = Part();
+      c->pt.xchg = x;
+      for (int i = 0; i < 4; i++) c->pt.xs[i].x = xs[i].x;
+      Part& X = c->pt;
+      X.nxs = PM.nxs;
+      X.nxr = PM.nxr;
+      X.xs_off = PM.xs_off;
+      X.xr_off = PM.xr_off;
+      X.xs_v = PM.xs_v;
+      X.xs_q = PM.xs_q;
+      X.xr_v = PM.xr_v;
+      X.xr_q = PM.xr_q;
+      X.xs_off_d = PM.xs_off_d;
+      X.xr_off_d = PM.xr_off_d;
+      X.own.vid = PM.own_vid;
+      X.own.pos = nullptr;
+      X.own.boff = PM.own_boff;
+      X.own.shift = PM.shift;
+      X.own.n_own = g.n_own;
+      c->orph_id.swap(DD.orph_id);
+      c->orph_t.swap(DD.orph_t);
+    }
     for (Slot& sl : c->slot) {
       sl.hv = HeavyBuf();
       sl.h_cc = sl.h_pr = false;
@@ -2160,8 +2217,10 @@ void seal_delta(rgpu_ctx* c) {
         }
       }
     }
-    B.nv = B.n_own = nv2;
-    B.ne = B.ne_owned = g.ne;
+    B.nv = nv2;
+    B.n_own = g.n_own;
+    B.ne = g.ne;
+    B.ne_owned = ne_owned;
     if (dev) {  // the host keeps no offsets; its ids follow on demand (host_vid)
       c->vid_stale = true;
       c->n_dtime = DD.ndt;
@@ -2205,7 +2264,8 @@ int rgpu_seal(rgpu_ctx* c) {
     c->st.seal_incremental = 0;
     c->st.seal_delta_updates = 0;
     // (a locality-ordered base has no monotone rank maps to merge into: it is re-packed)
-    if (c->delta_on && !c->partitioned && c->n_sealed > 0 && c->g.nv > 0 && !c->pk.relabeled) {
+    // (a locality-ordered base is re-packed; the partitioned merge needs the device packer)
+    if (c->delta_on && c->n_sealed > 0 && c->g.nv > 0 && !c->pk.relabeled && !(c->partitioned && c->delta_host)) {
       // live ingest: merge the delta into the resident graph
       seal_delta(c);
       c->st.seal_incremental = 1;
@@ -2222,6 +2282,18 @@ int rgpu_seal(rgpu_ctx* c) {
     free_graph(c);
     c->vid_stale = false;
     c->n_dtime = -1;
+    c->orph_id.clear();
+    c->orph_t.clear();
+    if (c->partitioned && !c->pk.relabeled) {  // deaths of ids not kept here (a later merge may ghost them)
+      const Packed& Q = c->pk;
+      for (const Event& ev : c->events) {
+        if (ev.kind != RGPU_VDEL || partition_of(ev.src, c->nparts) == c->part) continue;
+        if (!std::binary_search(Q.vid.begin() + Q.n_own, Q.vid.end(), ev.src)) {
+          c->orph_id.push_back(ev.src);
+          c->orph_t.push_back(ev.t);
+        }
+      }
+    }
     const Packed& P = c->pk;
     auto& L = c->graph_allocs;
     DevGraph g;

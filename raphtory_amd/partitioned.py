@@ -22,12 +22,13 @@ import numpy as np
 from .graph import TemporalGraph
 
 
-def open_rccl_partition(device: int, dist=None) -> TemporalGraph:
-    """This rank's partition (partition = rank, P = world size), joined to the RCCL group."""
+def open_rccl_partition(device: int, dist=None, vertex_order: str = "locality") -> TemporalGraph:
+    """This rank's partition (partition = rank, P = world size), joined to the RCCL group.
+    vertex_order "id": later seals merge into the resident partition (live ingest)."""
     if dist is None:
         import torch.distributed as dist
     rank, world = dist.get_rank(), dist.get_world_size()
-    g = TemporalGraph(rank, world, device)
+    g = TemporalGraph(rank, world, device, vertex_order=vertex_order)
     box = [TemporalGraph.exchange_id() if rank == 0 else None]
     dist.broadcast_object_list(box, src=0)
     g.exchange_init(box[0])  # collective: every rank joins the communicator here
@@ -35,12 +36,13 @@ def open_rccl_partition(device: int, dist=None) -> TemporalGraph:
 
 
 class LoopbackPartitions:
-    def __init__(self, nparts: int, device: int | Sequence[int] = 0):
+    def __init__(self, nparts: int, device: int | Sequence[int] = 0, vertex_order: str = "locality"):
         devs = [device] * nparts if isinstance(device, int) else list(device)
         if len(set(devs)) != 1:
             raise ValueError("loopback partitions share one device (use one process per GPU and RCCL "
                              "across devices: open_rccl_partition)")
-        self.parts: List[TemporalGraph] = [TemporalGraph(p, nparts, devs[p]) for p in range(nparts)]
+        self.parts: List[TemporalGraph] = [TemporalGraph(p, nparts, devs[p], vertex_order=vertex_order)
+                                           for p in range(nparts)]
         xid = TemporalGraph.exchange_id(loopback=True)
         for g in self.parts:
             g.exchange_init(xid)
@@ -66,6 +68,13 @@ class LoopbackPartitions:
     def ingest_stream(self, s) -> None:
         for g in self.parts:
             g.ingest_stream(s)
+
+    def ingest(self, t, kind, src, dst) -> None:
+        for g in self.parts:
+            g.ingest(t, kind, src, dst)
+
+    def stats(self) -> list:
+        return [g.stats() for g in self.parts]
 
     def seal(self) -> None:
         self._all(lambda g: g.seal())

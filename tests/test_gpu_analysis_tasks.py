@@ -52,7 +52,8 @@ def test_degree_ranking_top20_without_retain(heavy, monkeypatch):
                 assert top == exp[w], (t, w)
         # the result lines of a batched-window range job
         a = DegreeRanking()
-        task = BWindowedRangeAnalysisTask([g], a, int(hops[0]), int(hops[-1]), 20 * DAY, wins, retain_results=False)
+        # (the range ends at the newest ingested time: a later end waits for ingestion)
+        task = BWindowedRangeAnalysisTask([g], a, int(hops[0]), int(s.t.max()), 20 * DAY, wins, retain_results=False)
         lines = task.run()
         want = []
         for t in task.hops().tolist():
@@ -119,6 +120,7 @@ def test_live_tasks_event_time(cls):
                 if out is None:  # not ingested yet: the job waits
                     assert ts > newest
                     break
+                ts = task.last_job_time
                 if live_time is None:
                     assert ts == newest  # the first job: the minimum newest time
                 else:
@@ -145,6 +147,6 @@ def test_live_task_processing_time_and_partitions():
         lo = hi
         ts_exp = min(p.newest_time() for p in lp.parts)
         out = task.tick()
-        assert out is not None and task.timestamp() == ts_exp
+        assert out is not None and task.last_job_time == ts_exp
         assert _strip(out) == _strip([_cc_line(Oracle(*[x[:hi] for x in arrs]), ts_exp)])
     lp.close()

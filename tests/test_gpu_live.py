@@ -236,3 +236,35 @@ def test_live_device_packer_invalid_update_messages(monkeypatch):
             g.seal()
         assert g.stats()["vertices"] == 3
         g.close()
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_live_partitioned_loopback_ticks(P):
+    """Live ticks into vertex partitions (the C5 shape at P ranks, here as loopback partitions on one
+    GPU): every seal after the first merges on the device (ghosts appear as edges reach them, a
+    ghost's earlier deaths follow it in).  After each tick the partitioned CC equals the oracle over
+    the whole prefix, and every partition's graph equals a one-shot seal of the same prefix."""
+    from raphtory_amd.partitioned import LoopbackPartitions
+    from tests.test_gpu_parity import check_cc
+    arrs = list(_growing_tie_stream(13, 9000, nv_max=400))
+    cuts = [2001, 2002, 5003, 7000]
+    wins = [5000, 1000, 200]
+    lp = LoopbackPartitions(P, vertex_order="id")
+    bounds = [0] + cuts + [len(arrs[0])]
+    for k in range(len(bounds) - 1):
+        lp.ingest(*_cut(arrs, bounds[k], bounds[k + 1]))
+        lp.seal()
+        for st in lp.stats():
+            assert st["seal_incremental"] == (1 if k else 0)
+        pre = _cut(arrs, 0, bounds[k + 1])
+        end = int(pre[0][-1])
+        hops = np.arange(0, end + 20, max(41, end // 10), dtype=np.int64)
+        check_cc(lp, Oracle(*pre), hops, wins)
+        one = LoopbackPartitions(P, vertex_order="id")
+        one.ingest(*pre)
+        one.seal()
+        for a, b in zip(lp.stats(), one.stats()):
+            for key in ("vertices", "edges", "edges_owned", "vertex_events", "edge_events", "deaths"):
+                assert a[key] == b[key], (k, key, a[key], b[key])
+        one.close()
+    lp.close()
