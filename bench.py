@@ -488,63 +488,106 @@ def run_c4(a, rank, world, local):
 
 
 def run_c5(a, rank, world, local):
-    """BASELINE configs[4] (C5), one GPU: live analysis under ingest.  A GAB-shaped base
-    (default 100M updates, 20M users) is sealed once; then every hour tick the Router's next
-    10M updates (one hour of stream time past the newest point) are ingested and merged into
-    the HBM-resident graph by the incremental seal (merge.hip), and CC (batched windows
-    {y,m,w,d,h}) and PageRank (20 iterations, hour window) are re-run on the newest hour, as
-    LiveAnalysisTask does (LiveAnalysisTask.scala:13-107).  Reported: sustained updates/s over
-    the whole loop (ingest + merge + both analyses), the merge alone, and per-tick latencies.
-    Generating the updates (the Router's side) is outside the timed region.  Secondary line."""
+    """BASELINE configs[4] (C5): live analysis under ingest.  A GAB-shaped base (default 100M
+    updates, 20M users) is sealed once; then every hour tick the Router's next 10M updates (one
+    hour of stream time past the newest point) are ingested and merged into the HBM-resident
+    graph by the incremental seal (gdelta.hip + merge.hip), and CC (batched windows {y,m,w,d,h})
+    and PageRank (20 iterations, hour window) are re-run on the newest hour at the live time
+    (the minimum newest time over the partitions), as LiveAnalysisTask does
+    (LiveAnalysisTask.scala:13-107).  N > 1: one vertex partition per GPU (RCCL), each rank
+    ingesting and merging its own part of every tick (the partitioned device merge).  Reported:
+    sustained updates/s of the stream over the whole loop (ingest + merge + both analyses, max
+    over ranks per tick), the merge alone, and per-tick latencies.  Generating the updates (the
+    Router's side) is outside the timed region.  Secondary line."""
     import torch
     from raphtory_amd import TemporalGraph
-    from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab
-    s = gen_gab(4, a.c5_users, a.c5_base)
-    g = TemporalGraph(device=local, vertex_order="id")  # live: later seals merge incrementally
+    from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")  # control plane; the data path is the library's RCCL
+        from raphtory_amd.partitioned import open_rccl_partition
+        g = open_rccl_partition(local, dist, vertex_order="id")  # live: later seals merge
+    elif a.partitioned:
+        os.environ["RGPU_PARTITIONED"] = "1"
+        g = TemporalGraph(device=local, vertex_order="id")
+        g.exchange_init(TemporalGraph.exchange_id())
+    else:
+        g = TemporalGraph(device=local, vertex_order="id")
+
+    def reduce(x, op):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=op)
+        return t.item()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    MIN, MAX = (dist.ReduceOp.MIN, dist.ReduceOp.MAX) if dist is not None else (None, None)
+    s = gen_gab_range(4, a.c5_users, a.c5_base, 0, a.c5_base, rank, world)
+    n_base = 3 * a.c5_base
     g.ingest_stream(s)
+    del s
+    barrier()
     t0 = time.perf_counter()
     g.seal()
-    base_seal_s = time.perf_counter() - t0
-    now = int(s.t[-1])
-    n_base = len(s)
-    del s
-    log(f"C5 base: {n_base} updates sealed in {base_seal_s:.1f} s")
+    base_seal_s = reduce(time.perf_counter() - t0, MAX)
+    now = int(reduce(g.newest_time(), MAX))
+    log(f"rank {rank}: C5 base: {n_base} updates ({g.stats()['vertices']} owned vertices here) sealed in "
+        f"{base_seal_s:.1f} s")
     ticks = []
     for i in range(a.c5_ticks + 1):  # tick 0 is warm-up
-        d = gen_gab(100 + i, a.c5_users, a.c5_tick, t0=now + 1, t1=now + HOUR, id_key=4)
-        now = int(d.t[-1])
-        torch.cuda.synchronize()
+        d = gen_gab_range(100 + i, a.c5_users, a.c5_tick, 0, a.c5_tick, rank, world, t0=now + 1,
+                          t1=now + HOUR, id_key=4)
+        now += HOUR
+        barrier()
         t0 = time.perf_counter()
         g.ingest_stream(d)
         t1 = time.perf_counter()
         g.seal()
         t2 = time.perf_counter()
-        g.run("cc", [now], BATCH_WINDOWS)
+        live = int(reduce(g.newest_time(), MIN))  # LiveAnalysisTask.setLiveTime
+        g.run("cc", [live], BATCH_WINDOWS)
         t3 = time.perf_counter()
-        g.run("pagerank", [now], [HOUR], pr_iters=20)
+        g.run("pagerank", [live], [HOUR], pr_iters=20)
         torch.cuda.synchronize()
         t4 = time.perf_counter()
         st = g.stats()
         assert st["seal_incremental"] == 1
-        ticks.append({"updates": len(d), "ingest_ms": (t1 - t0) * 1e3, "merge_ms": (t2 - t1) * 1e3,
-                      "cc_ms": (t3 - t2) * 1e3, "pr_ms": (t4 - t3) * 1e3, "total_ms": (t4 - t0) * 1e3,
-                      "vertices": st["vertices"], "edges": st["edges"]})
-        log(f"tick {i}: " + " ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}"
-                                     for k, v in ticks[-1].items()))
+        rec = {"updates": 3 * a.c5_tick, "ingest_ms": (t1 - t0) * 1e3, "merge_ms": (t2 - t1) * 1e3,
+               "cc_ms": (t3 - t2) * 1e3, "pr_ms": (t4 - t3) * 1e3, "total_ms": (t4 - t0) * 1e3}
+        for k in ("ingest_ms", "merge_ms", "cc_ms", "pr_ms", "total_ms"):
+            rec[k] = reduce(rec[k], MAX)
+        rec["vertices"] = int(reduce(st["vertices"], dist.ReduceOp.SUM) if dist is not None else st["vertices"])
+        rec["edges"] = int(reduce(st["edges_owned"], dist.ReduceOp.SUM) if dist is not None else st["edges"])
+        ticks.append(rec)
+        if rank == 0:
+            log(f"tick {i}: " + " ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}"
+                                         for k, v in rec.items()))
     tt = ticks[1:]
     up = sum(t["updates"] for t in tt)
     wall = sum(t["total_ms"] for t in tt) / 1e3
     merge = sum(t["ingest_ms"] + t["merge_ms"] for t in tt) / 1e3
-    out = {"config": "C5", "n_gpus": 1, "base_updates": n_base, "base_seal_s": round(base_seal_s, 1),
+    out = {"config": "C5", "n_gpus": world, "base_updates": n_base, "base_seal_s": round(base_seal_s, 1),
            "ticks": len(tt), "updates_per_tick": tt[0]["updates"] if tt else 0,
            "live_updates_per_s": up / wall if wall else None,
            "ingest_merge_updates_per_s": up / merge if merge else None,
            "mean_ms": {k: round(sum(t[k] for t in tt) / len(tt), 1)
                        for k in ("ingest_ms", "merge_ms", "cc_ms", "pr_ms", "total_ms")},
            "final_vertices": tt[-1]["vertices"] if tt else None, "final_edges": tt[-1]["edges"] if tt else None,
-           "analysis": "CC over {y,m,w,d,h} + PageRank(20, hour) on the newest hour, every tick"}
-    print(json.dumps(out), flush=True)
+           "parallelism": (f"vertex-partitioned x{world}, RCCL" if world > 1 else
+                           "one GPU, partitioned path (P = 1)" if a.partitioned else "one GPU"),
+           "delta_packer": "host (RGPU_DELTA=2)" if os.environ.get("RGPU_DELTA") == "2" else "device (gdelta.hip)",
+           "analysis": "CC over {y,m,w,d,h} + PageRank(20, hour) at the live time, every tick"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     g.close()
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def run_c2(a, rank, world, local, quiet=False):

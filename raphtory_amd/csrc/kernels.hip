@@ -568,7 +568,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int64_t* __restrict__ ts_t, int64_t tcut,
                                                   int32_t* __restrict__ uw0, int32_t* __restrict__ uw1,
                                                   uint64_t* __restrict__ cb1, int ends,
-                                                  int32_t* __restrict__ ccount) {
+                                                  int32_t* __restrict__ ccount, int gmax) {
   __shared__ unsigned long long red[4];
   if (threadIdx.x < 4) red[threadIdx.x] = 0;
   __syncthreads();
@@ -579,11 +579,10 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
   Ctr members{}, alive{}, scanned{}, lw{}, uwn{};
   unsigned long long changed = 0;
   uint64_t lanes = 0;  // views with a step-1 change in this wave
-  // Vertices are dealt in groups of up to 16 (deal_group): in the locality order (packer.cpp
-  // locality_order) ranks are sorted by activity, so a contiguous run of 64 per wave would hand one
-  // wave the 64 busiest vertices.  Per round the lanes read 64 vertices' view masks, clear the
-  // non-members' count / mask words, and the wave then walks the members one by one.
-  const int G = deal_group(nv, nwaves, 16);
+  // Vertices are dealt in groups of up to gmax (deal_group; RGPU_DEAL_SLOTS): per round the lanes
+  // read 64 vertices' view masks, clear the non-members' count / mask words, and the wave then
+  // walks the members one by one.
+  const int G = deal_group(nv, nwaves, gmax);
   for (int64_t r = 0; (wave + r * (64 / G) * nwaves) * G < nv; r++) {
    const int64_t vlane = dealt_item(wave, nwaves, r, G, lane);
    const uint64_t mvl = vlane < nv ? vm[vlane] : 0;
@@ -1141,7 +1140,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
                                                   const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
                                                   uint64_t* __restrict__ cb_next,
                                                   uint64_t* __restrict__ cb_clear, int64_t cb_words,
-                                                  int32_t* __restrict__ ccount, int dense_div) {
+                                                  int32_t* __restrict__ ccount, int dense_div, int gmax) {
   if (stepflag[step - 1] == 0) return;
   // Dense steps (DenseRule): when step r-1 changed at least nv / dense_div vertices, step r
   // writes no next-frontier flags and step r+1 visits every member instead
@@ -1165,13 +1164,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
   int32_t changed = 0;
   std::conditional_t<PROF, StepWork, NoWork> wk;
   const TailList none{nullptr, nullptr};
-  // Chunks are dealt in groups of up to 32 (deal_group, as K2 deals vertices): per round lane l
-  // reads its chunk's frontier flags (whole lines), and the wave then runs only the flagged
+  // Chunks are dealt in groups of up to gmax (deal_group, as K2 deals vertices; RGPU_DEAL_STEP):
+  // per round lane l reads its chunk's frontier flags, and the wave then runs only the flagged
   // chunks — a sparse frontier costs one load per 64 chunks.  Every wave of the grid gets work on
-  // a small graph too, and the busy chunks of the locality order (runs of hubs) spread over the
-  // waves instead of queueing behind one.
+  // a small graph too.  Small groups spread a run of busy chunks over many waves (a frontier is
+  // clustered in rank order, the more so in the locality order); whole-line flag loads favour
+  // large ones.
   const int64_t nchunks = (nv + CH - 1) / CH;
-  const int G = deal_group(nchunks, nwaves, 32);
+  const int G = deal_group(nchunks, nwaves, gmax);
   for (int64_t r = 0; (wave + r * (64 / G) * nwaves) * G < nchunks; r++) {
     const int64_t cl = dealt_item(wave, nwaves, r, G, lane);
     uint32_t fb = 0;
@@ -2310,6 +2310,9 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
+int g_deal_slots = 16;  // deal_group maxima of K2 / the superstep kernel (RGPU_DEAL_SLOTS / _STEP;
+                        // C4 A/B, profiles/r03/c4_ab_deal.log: K2 16 ≈ 64 < 1, step 1 ≈ 4 << 64)
+int g_deal_step = 4;
 int g_sum_blocks = 32;  // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 int g_hist_rounds = 4;  // (C2: 64 rounds 145 ms, 4 rounds 138 ms; 1 round 147 ms)
 int g_tail_step = 14;
@@ -2352,7 +2355,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
-                                                uw0, uw1, cb1, ends ? 1 : 0, ccount);
+                                                uw0, uw1, cb1, ends ? 1 : 0, ccount, g_deal_slots);
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
@@ -2387,7 +2390,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.next, cb.clear, cb.words, ccount, dense_div
+    cb.next, cb.clear, cb.words, ccount, dense_div, g_deal_step
   // work != null (profile runs): the counting instantiation; the timed runs use the lean one
   if (work) k_cc_step2<4, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else k_cc_step2<4, false, 1, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);

@@ -147,6 +147,7 @@ void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, co
                        int dense_div = 0, unsigned long long* work = nullptr);
 extern int g_sum_blocks;   // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
 extern int g_hist_rounds;  // label-dedup rounds per (view, chunk) in k_cc_hist (RGPU_HIST_ROUNDS)
+extern int g_deal_slots, g_deal_step;  // deal_group maxima (kernels.hip; RGPU_DEAL_SLOTS / RGPU_DEAL_STEP)
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
 extern int g_tail_step, g_tail_grid;  // supersteps >= tail_step use at most tail_grid blocks
 // uniform label words (kernels.hip, kMixed): rows of the uniform vertices written into lab

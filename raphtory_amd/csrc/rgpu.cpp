@@ -2461,6 +2461,11 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   c->inject_fail = env_int("RGPU_INJECT_FAIL", 0);
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
+  {  // powers of two up to 64
+    auto pow2 = [](int x) { int g = 1; while (g < x && g < 64) g <<= 1; return g; };
+    g_deal_slots = pow2(env_int("RGPU_DEAL_SLOTS", 16));
+    g_deal_step = pow2(env_int("RGPU_DEAL_STEP", 4));
+  }
   g_tail_step = std::max(2, env_int("RGPU_TAIL_STEP", 14));
   g_tail_grid = std::max(1, env_int("RGPU_TAIL_GRID", 1024));
   try {

@@ -32,6 +32,8 @@ def main():
     end = int(s.t[-1])
     hops = range_hops(end - 167 * HOUR, end, HOUR)
     for P in [int(x) for x in a.parts.split(",")]:
+        t0 = time.time()
+        print(f"P={P}: packing", file=sys.stderr, flush=True)
         if P == 1:
             g = TemporalGraph()
             g.ingest_stream(s)
@@ -44,7 +46,9 @@ def main():
             lp.seal()
             parts = lp.parts
             run = lambda **kw: lp.run("cc", hops, BATCH_WINDOWS, **kw)  # noqa: E731
+        print(f"P={P}: sealed in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
         run()
+        print(f"P={P}: warm run done", file=sys.stderr, flush=True)
         run(profile=True, serial=True)
         per = []
         ks = {}
