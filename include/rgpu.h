@@ -83,7 +83,8 @@ typedef struct {
   double ms_total;               /* wall ms inside the last rgpu_run_view_batch */
   /* per-kernel event timing (RGPU_RUN_PROFILE): 0=window_mask 1=slots 2=cc_step 3=cc_hist
    * 4=cc_summary 5=pr_step 6=degree 7=cc_tail (late supersteps, one workgroup)
-   * 8=heavy (hub segment kernels) 9=diffusion step 10=vertex-program step 11 reserved */
+   * 8=heavy (hub segment kernels) 9=diffusion step 10=vertex-program step
+   * 11=edge_mask (K1's edge masks; 0 = its vertex masks) */
   int64_t kernel_launches[12];
   double kernel_ms[12];
   double kernel_bytes[12];       /* algorithmic bytes summed over launches */

@@ -19,6 +19,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <cstring>
 
 #include "kernels.hpp"
 
@@ -363,11 +364,39 @@ __device__ __forceinline__ void edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1]
   }
 }
 
+// Inline edge bits (K2 of a CC batch): the window bits of a simple static slot (tslots.hip: the
+// edge's history is one add point at tf and neither endpoint ever died) for the batch's own views,
+// computed where K2 streams the slot's time word instead of loaded from K1's em[e], a random 8-B
+// load per static slot and the bulk of K2's traffic.  Such an edge is alive in view (t, w) iff
+// tf <= t <= tf + w.  Any other slot reads em[e], which K1 then writes for the other edges only
+// (k_edge_mask SKIP).  (Running K1's whole edge_bits inline for them instead took K2 from 77 to 123
+// VGPRs.)
+__device__ __forceinline__ uint64_t simple_bits(const HopLDS& L, int sorted, int64_t tf) {
+  uint64_t m[1] = {0};
+  if (sorted) {
+    interval_bits<false>(m, L, tf, hop_lb(L, tf), L.K);
+  } else {
+    for (int k = 0; k < L.K; k++)
+      if (L.hop[k] >= tf) hop_bits<false>(m, L, L.hop[k] - tf, k);
+  }
+  return m[0];
+}
+// an edge whose bits K2 computes itself (the same test as tslots.hip k_slot_keys)
+__device__ __forceinline__ bool edge_simple(int64_t lo, int64_t hi, const int64_t* __restrict__ ekey, int32_t s,
+                                            int32_t d, const int64_t* __restrict__ doff,
+                                            const uint64_t* __restrict__ dbits) {
+  if (hi - lo != 1 || !(ekey[lo] & 1)) return false;
+  const bool ds = dbits ? ((dbits[s >> 6] >> (s & 63)) & 1) : doff[s + 1] > doff[s];
+  const bool dd = dbits ? ((dbits[d >> 6] >> (d & 63)) & 1) : doff[d + 1] > doff[d];
+  return !ds && !dd;
+}
+
 // The loop runs wave-uniform (lane = edge within a 64-edge group) so that profile runs can
 // count alive edges per view: the wave's 64 mask words are bit-transposed (lane j <- view j)
 // and popcounted; the block sums them in LDS, one atomicAdd per (plane, view) per block.
 __device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane);
-template <bool PLANAR, bool COUNT>
+// SKIP: simple edges (edge_simple) are left unwritten: every reader computes their bits itself
+template <bool PLANAR, bool COUNT, bool SKIP>
 __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __restrict__ esrc,
                                                    const int32_t* __restrict__ edst,
                                                    const int64_t* __restrict__ eoff,
@@ -391,6 +420,7 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
     const int64_t e = e0 + lane;
     uint64_t m[NP] = {};
     uint64_t mo[NP];  // the edge's own aliveness (the |E_w| counts)
+    if (SKIP && e < ne && edge_simple(eoff[e], eoff[e + 1], ekey, esrc[e], edst[e], doff, dbits)) continue;
     if (e < ne) {
       edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime, dbits);
 #pragma unroll
@@ -486,9 +516,14 @@ __device__ __forceinline__ unsigned row_lines(uint64_t m) {
 // DenseRule: superstep r is dense when r >= 2 and step r-1 changed at least nv / div vertices
 // (ccount[(r-1)*64 + shard]: changed vertices per step, 64 shards, summed here by each wave;
 // every block of a launch computes the same answer from counts the previous launch finished).
-// div <= 0: never.  Step 1 (K2) always writes its flags.
+// div <= 0: never.  Step 1 (K2) is always dense when the rule is on: with every member sending
+// its own id, every member with a kept slot to a smaller label changes and every member next to a
+// change is flagged, so step 2 visits the members anyway (C4 trace: step 2 visited as many vertices
+// as step 1 in all 15 batches), and K2's random 1-B flag stores per kept slot buy nothing.
 __device__ __forceinline__ bool dense_rule(const int32_t* __restrict__ ccount, int r, int64_t nv, int div) {
-  if (div <= 0 || !ccount || r < 2) return false;
+  if (div <= 0 || !ccount || r < 1) return false;
+  if (r == 1) return (div & kDense1) != 0;
+  div &= kDense1 - 1;
   int64_t x = ccount[(r - 1) * kCountShards + (threadIdx.x & 63)];
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
   return x * div >= nv;
@@ -539,7 +574,9 @@ struct NoWork {
 // bitmap and stepcnt[1]; vadj[v] = OR of v's kept slot masks (v isolated in view j iff bit j
 // is clear).
 
-template <bool PROF>  // PROF = false: the work counters compile away (launch_cc_slots: work == null)
+// PROF = false: the work counters compile away (launch_cc_slots: work == null).  IEM: inline edge
+// bits (slot_bits; time-ordered slots required), em unused
+template <bool PROF, bool IEM>
 __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int64_t* __restrict__ out_off,
                                                   const int64_t* __restrict__ in_off,
@@ -568,9 +605,12 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int64_t* __restrict__ ts_t, int64_t tcut,
                                                   int32_t* __restrict__ uw0, int32_t* __restrict__ uw1,
                                                   uint64_t* __restrict__ cb1, int ends,
-                                                  int32_t* __restrict__ ccount, int gmax) {
+                                                  int32_t* __restrict__ ccount, int gmax, BatchParams ebp,
+                                                  int dense1) {
   __shared__ unsigned long long red[4];
+  __shared__ HopLDS L;
   if (threadIdx.x < 4) red[threadIdx.x] = 0;
+  if constexpr (IEM) hop_lds_init(L, ebp, ebp.thr_e);  // (its barrier also publishes red)
   __syncthreads();
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -630,7 +670,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         cnt[v] = 0;
         vadj[v] = any;
         chg1[v] = ch;
-        if (ch) act2[v] = 1;
+        if (ch && !dense1) act2[v] = 1;
         if (ch && cb1) atomicOr((unsigned long long*)&cb1[v >> 6], 1ull << (v & 63));
       }
       if (!own) continue;
@@ -658,7 +698,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     int32_t nb_keep = 0;
     for (int64_t c = 0; c < ntot; c += 64) {
       const int64_t j = c + lane;
-      if (ts_t && ts_t[base + c] < tcut) break;  // newest first: the rest are dead in every view
+      if (ts_t && ts_time(ts_t[base + c]) < tcut) break;  // newest first: the rest are dead in every view
       scanned += ntot - c < 64 ? ntot - c : 64;
       uint64_t m = 0;
       int32_t nb = 0, lb = 0;
@@ -674,7 +714,14 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
           e = in_eid[i0 + (j - nout)];
           nb = esrc[e];
         }
-        if (nb != (int32_t)v && (!ts_t || ts_t[base + j] >= tcut)) m = em[e] & (ends ? mv : vm[nb]) & mv;
+        const int64_t tsw = ts_t ? ts_t[base + j] : 0;
+        if (nb != (int32_t)v && (!ts_t || ts_time(tsw) >= tcut)) {
+          if constexpr (IEM) {
+            m = (ts_simple(tsw) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[e]) & vm[nb] & mv;
+          } else {
+            m = em[e] & (ends ? mv : vm[nb]) & mv;
+          }
+        }
         lb = grank ? grank[nb] : nb;
       }
       uint64_t bal = __ballot(m != 0);
@@ -718,6 +765,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     lanes |= ch;
     if (ch) {
       changed++;
+    }
+    if (ch && !dense1) {  // (a dense step 1: step 2 visits every member, dense_rule)
       if (lane == 0) act2[v] = 1;
       if (ntot <= 64) {  // one slot chunk: mark from registers, no re-read of the stored slots
         if (m_keep & ch) act2[nb_keep] = 1;
@@ -1177,8 +1226,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
     uint32_t fb = 0;
     if (cl < nchunks) {
       const int64_t v0 = cl * CH;
-      if (visit_all) {
-        fb = (1u << CH) - 1;
+      if (visit_all) {  // every member: the chunk's view masks (32 B per lane, one line per 2 lanes)
+#pragma unroll
+        for (int i = 0; i < CH; i++) fb |= (v0 + i < nv && vm[v0 + i] != 0) ? (1u << i) : 0u;
       } else {
         const uint64_t f = CH == 8 ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
                                    : *reinterpret_cast<const uint32_t*>(act_cur + v0);
@@ -1353,6 +1403,7 @@ __device__ __forceinline__ void heavy_work(unsigned long long* work, int f, unsi
 // K2 for heavy vertices: compact each segment's kept slots (kept iff em[e] & vm[nb] & vm[v])
 // at its static position, record its count and mask OR, and fold the superstep-1 minima
 // (neighbours' ranks, ConnectedComponents.setup sends own ids) into hbest.
+template <bool IEM>
 __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t* __restrict__ seg_v,
                                                      const int32_t* __restrict__ seg_h,
                                                      const int64_t* __restrict__ seg_lo,
@@ -1371,7 +1422,9 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
                                                      int64_t n_own, const int32_t* __restrict__ ts_e,
                                                      const int32_t* __restrict__ ts_nb,
                                                      const int64_t* __restrict__ ts_t, int64_t tcut, int ends,
-                                                     unsigned long long* __restrict__ work) {
+                                                     unsigned long long* __restrict__ work, BatchParams ebp) {
+  __shared__ HopLDS L;
+  if constexpr (IEM) hop_lds_init(L, ebp, ebp.thr_e);
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -1382,7 +1435,7 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
     // a heavy ghost (partitioned) is compacted too: k_heavy_mark walks its kept slots when its
     // owner's records say it changed.  With time-ordered slots a segment whose newest edge
     // predates the batch's cut keeps none.
-    const uint64_t mv = !(ts_t && ts_t[lo0] < tcut) ? vm[v] : 0;
+    const uint64_t mv = !(ts_t && ts_time(ts_t[lo0]) < tcut) ? vm[v] : 0;
     if (mv == 0) {
       if (lane == 0) { segcnt[sg] = 0; segor[sg] = 0; }
       continue;
@@ -1395,7 +1448,7 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
     uint64_t any = 0;
     for (int32_t c = 0; c < ns; c += 64) {
       const int32_t jj = c + lane;
-      if (ts_t && ts_t[lo + c] < tcut) break;
+      if (ts_t && ts_time(ts_t[lo + c]) < tcut) break;
       w_scan += ns - c < 64 ? ns - c : 64;
       uint64_t m = 0;
       int32_t nb = 0;
@@ -1412,7 +1465,14 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
           e = in_eid[i0 + (rel - nout)];
           nb = esrc[e];
         }
-        if (nb != v && (!ts_t || ts_t[lo + jj] >= tcut)) m = em[e] & (ends ? mv : vm[nb]) & mv;
+        const int64_t tsw = ts_t ? ts_t[lo + jj] : 0;
+        if (nb != v && (!ts_t || ts_time(tsw) >= tcut)) {
+          if constexpr (IEM) {
+            m = (ts_simple(tsw) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[e]) & vm[nb] & mv;
+          } else {
+            m = em[e] & (ends ? mv : vm[nb]) & mv;
+          }
+        }
       }
       const uint64_t bal = __ballot(m != 0);
       if (m) {
@@ -2333,14 +2393,17 @@ void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp,
   else k_vertex_mask<false><<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm, vstride, clr);
 }
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
-                      unsigned long long* ecnt, int64_t h0, const uint64_t* vm_ends, int64_t vstride) {
+                      unsigned long long* ecnt, int64_t h0, const uint64_t* vm_ends, int64_t vstride,
+                      bool skip_simple) {
 #define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, bp, em, g.ne, ecnt, h0, g.n_own, vm_ends, \
     vstride, g.dbits
   const unsigned grid = grid_for(g.ne, 256);
-  if (planar && ecnt) k_edge_mask<true, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
-  else if (planar) k_edge_mask<true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
-  else if (ecnt) k_edge_mask<false, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
-  else k_edge_mask<false, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
+  if (planar && ecnt) k_edge_mask<true, true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
+  else if (planar && skip_simple) k_edge_mask<true, false, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
+  else if (planar) k_edge_mask<true, false, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
+  else if (ecnt) k_edge_mask<false, true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
+  else if (skip_simple) k_edge_mask<false, false, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
+  else k_edge_mask<false, false, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
 #undef RGPU_EM_ARGS
 }
 void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
@@ -2348,14 +2411,19 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
                      unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends,
-                     int32_t* ccount) {
+                     int32_t* ccount, const BatchParams* ebp, int dense_div) {
   const bool hv = g.n_seg > 0;
-  auto* kern = work ? k_cc_slots<true> : k_cc_slots<false>;
+  const bool iem = ebp != nullptr && g.ts_t != nullptr;
+  auto* kern = work ? (iem ? k_cc_slots<true, true> : k_cc_slots<true, false>)
+                    : (iem ? k_cc_slots<false, true> : k_cc_slots<false, false>);
+  BatchParams bp0;
+  if (!iem) std::memset(&bp0, 0, sizeof(bp0));
   kern<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
-                                                uw0, uw1, cb1, ends ? 1 : 0, ccount, g_deal_slots);
+                                                uw0, uw1, cb1, ends ? 1 : 0, ccount, g_deal_slots, iem ? *ebp : bp0,
+                                                dense_div > 0 && (dense_div & kDense1) && ccount ? 1 : 0);
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
@@ -2397,12 +2465,16 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
 #undef RGPU_STEP_ARGS
 }
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
-                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends, unsigned long long* work) {
+                        int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends, unsigned long long* work,
+                        const BatchParams* ebp) {
   if (g.n_seg <= 0) return;
-  k_heavy_slots<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off,
-                                                            g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
-                                                            snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own,
-                                                            g.ts_e, g.ts_nb, g.ts_t, tcut, ends ? 1 : 0, work);
+  const bool iem = ebp != nullptr && g.ts_t != nullptr;
+  BatchParams bp0;
+  if (!iem) std::memset(&bp0, 0, sizeof(bp0));
+  (iem ? k_heavy_slots<true> : k_heavy_slots<false>)<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(
+      g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
+      snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own, g.ts_e, g.ts_nb, g.ts_t, tcut, ends ? 1 : 0, work,
+      iem ? *ebp : bp0);
 }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,

@@ -60,8 +60,12 @@ struct DevGraph {
   // time-ordered static slots (tslots.hip; null: CSR order): per vertex newest last-add first
   const int32_t* ts_e = nullptr;    // [ne + n_in] edge of the slot
   const int32_t* ts_nb = nullptr;   // [ne + n_in] neighbour across it
-  const int64_t* ts_t = nullptr;    // [ne + n_in] the edge's last add time
+  const int64_t* ts_t = nullptr;    // [ne + n_in] 2 * the edge's last add time + simple (tslots.hip)
 };
+// a ts_t word: the edge's last add time, and whether the slot is simple (one add point, no
+// endpoint deaths: K2 derives its window bits from the time alone)
+__host__ __device__ inline int64_t ts_time(int64_t x) { return x >> 1; }
+__host__ __device__ inline bool ts_simple(int64_t x) { return x & 1; }
 // Builds ts_e / ts_nb / ts_t (device arrays of ne + n_in entries) for g; temporaries are
 // appended to `temps` (free them after the stream is synchronised).  False: not built (more
 // than 2^31 slots), the graph keeps CSR order.
@@ -102,6 +106,9 @@ constexpr int kLaneShards = 64;
 // changed-vertex counts per superstep, ccount[step * kCountShards + shard] (int32, cleared per
 // batch): the dense-step rule of the superstep kernels (kernels.hip dense_rule, RGPU_DENSE)
 constexpr int kCountShards = 64;
+// dense_div | kDense1: superstep 1 (K2) is dense too (it writes no frontier flags, step 2 visits
+// every member; kernels.hip dense_rule).  RGPU_DENSE1 (default on).
+constexpr int kDense1 = 1 << 30;
 constexpr int kLaneSteps = 128;                          // kMaxSteps (rgpu.cpp)
 constexpr int kLaneChgWords = kLaneSteps * kLaneShards;
 void launch_lane_fold(hipStream_t s, unsigned long long* lanechg, unsigned long long* lanefold);
@@ -118,21 +125,25 @@ void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp,
 // each edge word is ANDed with both endpoints' words, so that K2 keeps a slot on em alone
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
                       unsigned long long* ecnt = nullptr, int64_t h0 = 0, const uint64_t* vm_ends = nullptr,
-                      int64_t vstride = 0);
+                      int64_t vstride = 0, bool skip_simple = false);
 // tcut: no view of the batch can keep an edge whose last add is older (time-ordered slots)
+// ebp (time-ordered slots only; else null): the batch's hops and edge windows, non-planar bit layout
+// (view bit w*KS + k): K2 computes the window bits of simple slots inline (kernels.hip simple_bits)
+// and reads em only for the others (K1 then runs with skip_simple)
 void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
                      unsigned long long* lanechg, int32_t* uw0 = nullptr, int32_t* uw1 = nullptr,
-                     uint64_t* cb1 = nullptr, bool ends = false, int32_t* ccount = nullptr);
+                     uint64_t* cb1 = nullptr, bool ends = false, int32_t* ccount = nullptr,
+                     const BatchParams* ebp = nullptr, int dense_div = 0);
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
 // (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
 // next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
 // work (profile runs, else null): the hub kernels' work counters (kernels.hip heavy_work)
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                         int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends = false,
-                        unsigned long long* work = nullptr);
+                        unsigned long long* work = nullptr, const BatchParams* ebp = nullptr);
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr,

@@ -43,7 +43,8 @@ struct HipFail {
   } while (0)
 
 enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUMMARY = 4,
-                KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_HEAVY = 8, KID_DIFF = 9, KID_VP = 10, KID_N = 12 };
+                KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_HEAVY = 8, KID_DIFF = 9, KID_VP = 10, KID_EMASK = 11,
+                KID_N = 12 };
 
 constexpr int kMaxSteps = 128;
 // stats words: 6 per-view fields + counters row | folded lane words [step] | lane-change shards
@@ -64,6 +65,7 @@ struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   uint64_t *vm = nullptr, *em = nullptr;          // masks of the batch in flight
+  bool iem = false;                               // the batch's K2 computes edge bits inline (em unused)
   uint64_t *vm_own = nullptr, *em_own = nullptr;  // this slot's own (hop-major batches)
   int32_t *cnt = nullptr, *snbr = nullptr;
   uint64_t* smask = nullptr;
@@ -212,6 +214,8 @@ struct rgpu_ctx {
   int iv_max = 32;                      // RGPU_IVMAX: K1 interval form up to this many points (< 0 off)
   int heavy_t = 2048;                   // RGPU_HEAVY: static slots above which a vertex is split (0 off)
   bool tslots_on = true;                // RGPU_TSLOTS: time-ordered static slots (tslots.hip)
+  bool iem_on = true;                   // RGPU_IEM: CC's K2 computes edge bits inline (no K1 edge masks)
+  bool dense1 = true;                   // RGPU_DENSE1: K2 is a dense step (kernels.hpp kDense1)
   MaskSet mset[kMaskSets];
   int grp_last[kMaxPlanes] = {};        // supersteps of the last batch of each window group
   // last run: views (hop, win) -> batch (hop/K)*G + win/gsize, lane (win%gsize)*K + hop%K
@@ -359,8 +363,8 @@ unsigned long long* work_buf(const rgpu_ctx* c, const Slot& s) {
 // 536 ms); off below (C2: 127.5 -> 132.3 ms with it: a small graph's flags are cached anyway).
 int dense_div(const rgpu_ctx* c) {
   if (c->tail_on) return 0;
-  if (c->dense >= 0) return c->dense;
-  return c->g.nv > ((int64_t)1 << 21) ? 4 : 0;
+  const int d = c->dense >= 0 ? c->dense : (c->g.nv > ((int64_t)1 << 21) ? 4 : 0);
+  return d > 0 && c->dense1 ? (d | kDense1) : d;
 }
 
 // changed bits of superstep r (with uniform words; RGPU_CHGBITS=0 turns them off)
@@ -842,12 +846,26 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   // (K1 folding both endpoints' memberships into the CC edge words measured slower on C4: K1 55 ->
   // 97 ms for K2 122 -> 117 ms; the kernels keep the path, off)
   const bool ends = false;
+  // Inline edge bits (kernels.hip simple_bits): CC's K2 computes the window bits of the simple
+  // slots (one add point, no endpoint deaths) for the batch's own windows from the time-ordered
+  // slot words, so K1 writes edge masks only for the other edges (all of them for the |E_w|
+  // counts of an RGPU_RUN_EDGE_COUNTS run).  The partitioned mode keeps K1's full edge masks:
+  // its ghost marking (k_xmark) walks them.
+  const bool iem = c->iem_on && rc.algo == RGPU_ALGO_CC && g.ts_t && !c->partitioned;
+  BatchParams ebp = bp;  // the batch's edge windows, view bit w*KS + k
+  if (rc.G > 1) {
+    ebp.W = 1;
+    ebp.thr_e[0] = rc.thr_e[grp];
+  }
+  const bool skip_simple = iem && !c->d_ecnt;
+  s.iem = iem;
   if (rc.G == 1) {
     s.vm = s.vm_own;
     s.em = s.em_own;
     timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv, [&] { launch_vertex_mask(s.stream, gk, bp, s.vm, 0, false, clr); });
-    timed_launch(c, si, KID_MASK, be + 8.0 * g.ne,
-                 [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0, ends ? s.vm : nullptr, 0); });
+    timed_launch(c, si, KID_EMASK, be + 8.0 * g.ne, [&] {
+      launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0, ends ? s.vm : nullptr, 0, skip_simple);
+    });
     if (c->partitioned) part_vm_exchange(c, si, s.vm, 0, 1);
   } else {
     MaskSet& M = c->mset[hb % kMaskSets];
@@ -857,9 +875,10 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       const BatchClear none;
       timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv * rc.W,
                    [&] { launch_vertex_mask(s.stream, gk, bp, M.vm, g.nv + kPad, true, none); });
-      timed_launch(c, si, KID_MASK, be + 8.0 * g.ne * rc.W,
-                   [&] { launch_edge_mask(s.stream, g, bp, M.em, true, c->d_ecnt, (int64_t)h0, ends ? M.vm : nullptr,
-                                          g.nv + kPad); });
+      timed_launch(c, si, KID_EMASK, be + 8.0 * g.ne * rc.W, [&] {
+        launch_edge_mask(s.stream, g, bp, M.em, true, c->d_ecnt, (int64_t)h0, ends ? M.vm : nullptr, g.nv + kPad,
+                         skip_simple);
+      });
       if (c->partitioned) part_vm_exchange(c, si, M.vm, g.nv + kPad, rc.G);
       HIPCHK(hipEventRecord(M.k1, s.stream));
       M.pending = rc.G;
@@ -917,12 +936,16 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     const double b2 = 8.0 * g.nv;  // the view-mask scan; the rest from the work counters (harvest)
     if (g.n_seg > 0)
       timed_launch(c, si, KID_HEAVY, 0.0,
-                   [&] { launch_heavy_slots(s.stream, g, tcut, s.vm, s.em, s.snbr, s.smask, s.hv, ends, work_buf(c, s)); });
+                   [&] {
+                     launch_heavy_slots(s.stream, g, tcut, s.vm, s.em, s.snbr, s.smask, s.hv, ends, work_buf(c, s),
+                                        iem ? &ebp : nullptr);
+                   });
     timed_launch(c, si, KID_SLOTS, b2, [&] {  // (partitioned: owned vertices only, gk)
       launch_cc_slots(s.stream, gk, tcut, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                       work_buf(c, s), s.hv, s.stats + kLaneOff, use_uw(c) ? s.uw[0] : nullptr,
-                      use_uw(c) ? s.uw[1] : nullptr, chg_bits(c, s, 1).next, ends, s.ccount);
+                      use_uw(c) ? s.uw[1] : nullptr, chg_bits(c, s, 1).next, ends, s.ccount, iem ? &ebp : nullptr,
+                      dense_div(c));
     });
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
@@ -932,7 +955,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     if (g.n_seg > 0 && !c->partitioned)  // partitioned: after the step's records are in
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[1], s.act[2], s.stepcnt, 1, s.hv, nullptr, nullptr,
-                          nullptr, INT64_MIN, nullptr, 0, work_buf(c, s));
+                          nullptr, INT64_MIN, s.ccount, dense_div(c), work_buf(c, s));
       });
     s.r_launched = 1;  // superstep 1 ran inside the slot kernel
     if (c->partitioned) {
@@ -1037,7 +1060,10 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
       {
         const double mem = (double)wsum(1, 0);
         c->st.kernel_bytes[KID_SLOTS] += 12.0 * ((double)c->g.nv - mem) + 52.0 * mem +
-                                         (c->g.ts_e ? 32.0 : 24.0) * (double)wsum(1, 4) + 12.0 * (double)wsum(1, 1) +
+                                         // per static slot: slot words (ts_e 4 + ts_nb 4 + ts_t 8, or the
+                                         // CSR's 8), em[e] 8 unless inline (slot_bits), vm[nb] 8
+                                         ((c->g.ts_e ? 32.0 : 24.0) - (s.iem ? 8.0 : 0.0)) * (double)wsum(1, 4) +
+                                         12.0 * (double)wsum(1, 1) +
                                          4.0 * (double)wsum(1, 7) + 64.0 * (double)wsum(1, 6);
       }
       // hub kernels (kernels.hip heavy_work, the step-0 row): per segment the gather visits, its
@@ -1591,7 +1617,7 @@ int run_partitioned_dp(rgpu_ctx* c, RunCfg& rc) {
     s.em = s.em_own;
     timed_launch(c, 0, KID_MASK, 8.0 * (go.nv + 1) + 8.0 * c->pk.n_vkey + 8.0 * go.nv,
                  [&] { launch_vertex_mask(s.stream, go, bp, s.vm, 0, false, clr); });
-    timed_launch(c, 0, KID_MASK, bytes_mask(g) - (16.0 * g.nv + 8.0) + 8.0 * c->pk.n_ekey,
+    timed_launch(c, 0, KID_EMASK, bytes_mask(g) - (16.0 * g.nv + 8.0) + 8.0 * c->pk.n_ekey,
                  [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0); });
     part_vm_exchange(c, 0, s.vm, 0, 1);
     timed_launch(c, 0, KID_DEGREE, go.nv * (8.0 + 32.0 + 512.0) + (double)(g.ne + g.n_in) * 12.0, [&] {
@@ -2460,6 +2486,8 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   c->prof_lean = env_int("RGPU_PROF_LEAN", 0) != 0;
   c->inject_fail = env_int("RGPU_INJECT_FAIL", 0);
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
+  c->iem_on = env_int("RGPU_IEM", 1) != 0;
+  c->dense1 = env_int("RGPU_DENSE1", 1) != 0;
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
   {  // powers of two up to 64
     auto pow2 = [](int x) { int g = 1; while (g < x && g < 64) g <<= 1; return g; };

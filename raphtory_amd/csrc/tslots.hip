@@ -10,7 +10,12 @@
 //
 //   ts_e[p]  edge of static slot p       (p in [adj_off[v], adj_off[v+1]), newest first)
 //   ts_nb[p] the neighbour across it
-//   ts_t[p]  the edge's last add time    (INT64_MIN: never added)
+//   ts_t[p]  2 * (the edge's last add time) + simple   (INT64_MIN: never added; ts_time / ts_simple
+//            in kernels.hpp)
+//
+// simple = the edge's history is one add point and neither endpoint ever died: its aliveness in
+// any view (t, w) is then tf <= t <= tf + w with tf = ts_time, so K2 computes the slot's window
+// bits from the word it already streams (kernels.hip slot_bits) instead of reading em[e].
 //
 // The order only changes which kept slot lands where inside the vertex's kept range: CC is a
 // minimum over the kept slots, so results are unchanged.
@@ -26,7 +31,9 @@ __global__ __launch_bounds__(256) void k_slot_keys(int64_t nv, const int64_t* __
                                                    const int64_t* __restrict__ in_off,
                                                    const int32_t* __restrict__ in_eid,
                                                    const int64_t* __restrict__ eoff,
-                                                   const int64_t* __restrict__ ekey, int64_t* __restrict__ key,
+                                                   const int64_t* __restrict__ ekey, const int32_t* __restrict__ esrc,
+                                                   const int32_t* __restrict__ edst, const int64_t* __restrict__ doff,
+                                                   const uint64_t* __restrict__ dbits, int64_t* __restrict__ key,
                                                    int32_t* __restrict__ val) {
   // one wave per vertex, lanes over its slots (out-edges then in-edges, CSR order)
   const int lane = threadIdx.x & 63;
@@ -38,9 +45,17 @@ __global__ __launch_bounds__(256) void k_slot_keys(int64_t nv, const int64_t* __
     for (int64_t j = lane; j < ntot; j += 64) {
       const int32_t e = j < nout ? (int32_t)(o0 + j) : in_eid[i0 + (j - nout)];
       int64_t t = INT64_MIN;  // last add point: histories are sorted, key = 2 * time + alive
-      for (int64_t i = eoff[e + 1] - 1; i >= eoff[e]; i--)
+      const int64_t h0 = eoff[e], h1 = eoff[e + 1];
+      for (int64_t i = h1 - 1; i >= h0; i--)
         if (ekey[i] & 1) { t = ekey[i] >> 1; break; }
-      key[base + j] = t;
+      bool simple = h1 - h0 == 1 && t != INT64_MIN;
+      if (simple) {
+        const int32_t a = esrc[e], b = edst[e];
+        const bool da = dbits ? ((dbits[a >> 6] >> (a & 63)) & 1) : doff[a + 1] > doff[a];
+        const bool db = dbits ? ((dbits[b >> 6] >> (b & 63)) & 1) : doff[b + 1] > doff[b];
+        simple = !da && !db;
+      }
+      key[base + j] = t == INT64_MIN ? INT64_MIN : 2 * t + (simple ? 1 : 0);
       val[base + j] = e;
     }
   }
@@ -80,7 +95,8 @@ bool build_time_slots(hipStream_t s, const DevGraph& g, int32_t* ts_e, int32_t* 
   };
   int64_t* key = static_cast<int64_t*>(tmp(sizeof(int64_t) * n));
   int32_t* val = static_cast<int32_t*>(tmp(sizeof(int32_t) * n));
-  k_slot_keys<<<grid_waves(g.nv), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, g.eoff, g.ekey, key, val);
+  k_slot_keys<<<grid_waves(g.nv), 256, 0, s>>>(g.nv, g.out_off, g.in_off, g.in_eid, g.eoff, g.ekey, g.esrc, g.edst,
+                                               g.doff, g.dbits, key, val);
   size_t bytes = 0;
   if (hipcub::DeviceSegmentedSort::SortPairsDescending(nullptr, bytes, key, ts_t, val, ts_e, (int)n, (int)g.nv,
                                                        g.adj_off, g.adj_off + 1, s) != hipSuccess)

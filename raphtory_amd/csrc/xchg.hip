@@ -49,7 +49,9 @@ __device__ __forceinline__ int64_t owned_rank(const OwnIdx& I, int64_t id) {
 // kernels.hip dense_rule(ccount, r - 1): superstep r ran with every member visited (its flags
 // were not written by a dense step r - 1)
 __device__ __forceinline__ bool dense_after(const int32_t* __restrict__ ccount, int r, int64_t nv, int div) {
-  if (div <= 0 || !ccount || r < 3) return false;
+  if (div <= 0 || !ccount || r < 2) return false;
+  if (r == 2) return (div & kDense1) != 0;  // step 1 (K2) dense (kernels.hpp kDense1)
+  div &= kDense1 - 1;
   int64_t x = ccount[(r - 2) * kCountShards + (threadIdx.x & 63)];
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
   return x * div >= nv;
@@ -290,11 +292,33 @@ __device__ __forceinline__ int64_t label_row(const OwnIdx& I, int32_t x) {
 __device__ __forceinline__ unsigned long long count_rec(int32_t x, int j, unsigned c) {
   return (unsigned long long)(uint32_t)x | ((unsigned long long)j << 31) | ((unsigned long long)c << 37);
 }
-// wave-wide: the lanes with `on` send (x, j, c) (remote labels) or add it (owned labels)
+// A wave's outgoing count records are staged in LDS, kStage per peer, and reserved in the send
+// buffer with one atomicAdd per flush: one global atomic per (group of records, peer) serialised
+// on the 8 gcnt words (~10 ns each at the memory side, DESIGN.md §4 lesson 1) and made the
+// partitioned count pass ~20x the one-partition one.  The flush order is fixed per wave, so a
+// REMOTE_ONLY re-run emits the same records per peer (in another order at most).
+constexpr int kStage = 64;
+struct CountStage {
+  unsigned long long (*rec)[kStage];  // [peer][kStage], wave-private LDS
+  int* n;                             // [peer] staged records
+};
+__device__ __forceinline__ void stage_flush(const CountStage& st, int q, const XPeers& P,
+                                            unsigned long long* __restrict__ gcnt,
+                                            unsigned long long* __restrict__ hsbuf, int lane) {
+  const int n = st.n[q];
+  if (n == 0) return;
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(&gcnt[q], (unsigned long long)n);
+  base = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(base >> 32), 0) << 32) |
+         __builtin_amdgcn_readlane((uint32_t)base, 0);
+  if (lane < n && base + lane < (unsigned long long)P.cap[q]) hsbuf[P.base[q] + (int64_t)(base + lane)] = st.rec[q][lane];
+  if (lane == 0) st.n[q] = 0;
+}
+// wave-wide: the lanes with `on` send (x, j, c) (remote labels, staged) or add it (owned labels)
 template <bool REMOTE_ONLY>
 __device__ __forceinline__ void count_direct(bool on, int32_t x, int j, unsigned c, const XPeers& P, const OwnIdx& I,
                                              int32_t* __restrict__ counts, unsigned long long* __restrict__ gcnt,
-                                             unsigned long long* __restrict__ hsbuf, int lane) {
+                                             unsigned long long* __restrict__ hsbuf, int lane, const CountStage& st) {
   const int q = on ? owner_of(x, P.np) : -1;
   if (!REMOTE_ONLY && q == P.me) {
     const int64_t r = label_row(I, x);  // always found: a label is a member's id
@@ -304,14 +328,11 @@ __device__ __forceinline__ void count_direct(bool on, int32_t x, int j, unsigned
     const int qL = __builtin_amdgcn_readlane(q, __builtin_ctzll(todo));
     const uint64_t mine = __ballot(q == qL);
     todo &= ~mine;
-    unsigned long long base = 0;
-    if (lane == __builtin_ctzll(mine)) base = atomicAdd(&gcnt[qL], (unsigned long long)__popcll(mine));
-    base = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(base >> 32), __builtin_ctzll(mine)) << 32) |
-           __builtin_amdgcn_readlane((uint32_t)base, __builtin_ctzll(mine));
-    if (q == qL) {
-      const unsigned long long pos = base + __popcll(mine & (lane ? (~0ull >> (64 - lane)) : 0ull));
-      if (pos < (unsigned long long)P.cap[qL]) hsbuf[P.base[qL] + (int64_t)pos] = count_rec(x, j, c);
-    }
+    const int n = __popcll(mine);
+    if (st.n[qL] + n > kStage) stage_flush(st, qL, P, gcnt, hsbuf, lane);
+    const int c0 = st.n[qL];
+    if (q == qL) st.rec[qL][c0 + __popcll(mine & (lane ? (~0ull >> (64 - lane)) : 0ull))] = count_rec(x, j, c);
+    if (lane == 0) st.n[qL] = c0 + n;
   }
 }
 template <bool REMOTE_ONLY>
@@ -328,11 +349,15 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
   __shared__ unsigned int iso[64];
   __shared__ int32_t ckey_s[4][kRows];
   __shared__ unsigned int crow_s[4][kRows][64];
+  __shared__ unsigned long long srec_s[4][kMaxParts][kStage];
+  __shared__ int sn_s[4][kMaxParts];
   const int lane = lane_of(), wib = threadIdx.x >> 6;
   int32_t* ckey = ckey_s[wib];
   unsigned int (*crow)[64] = crow_s[wib];
+  const CountStage st{srec_s[wib], sn_s[wib]};
   if (threadIdx.x < 64) iso[threadIdx.x] = 0;
   if (lane < kRows) ckey[lane] = -1;
+  if (lane < kMaxParts) st.n[lane] = 0;
   for (int h = 0; h < kRows; h++) crow[h][lane] = 0;
   __syncthreads();
   auto cached = [&](int32_t x, int j, unsigned c) -> bool {  // per lane
@@ -372,7 +397,7 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
       const bool on = (mL >> lane) & 1;
       const unsigned c = (unsigned)__popcll(same);
       const bool hit = on && cached(xL, lane, c);
-      count_direct<REMOTE_ONLY>(on && !hit, xL, lane, c, P, I, counts, gcnt, hsbuf, lane);
+      count_direct<REMOTE_ONLY>(on && !hit, xL, lane, c, P, I, counts, gcnt, hsbuf, lane, st);
     }
     for (uint64_t mixed = __ballot(m != 0 && x == kMixed); mixed; mixed &= mixed - 1) {  // rows
       const int L = __builtin_ctzll(mixed);
@@ -380,15 +405,16 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
       const bool on = (mL >> lane) & 1;
       const int32_t l = on ? lab[(b0 + L) * 64 + lane] : 0;
       const bool hit = on && cached(l, lane, 1u);
-      count_direct<REMOTE_ONLY>(on && !hit, l, lane, 1u, P, I, counts, gcnt, hsbuf, lane);
+      count_direct<REMOTE_ONLY>(on && !hit, l, lane, 1u, P, I, counts, gcnt, hsbuf, lane, st);
     }
   }
   for (int h = 0; h < kRows; h++) {  // the wave's cache: owned labels at their rows, the rest as records
     const int32_t k = ckey[h];
     if (k == -1) continue;
     const unsigned int c = crow[h][lane];
-    count_direct<REMOTE_ONLY>(c != 0, k, lane, c, P, I, counts, gcnt, hsbuf, lane);
+    count_direct<REMOTE_ONLY>(c != 0, k, lane, c, P, I, counts, gcnt, hsbuf, lane, st);
   }
+  for (int q = 0; q < P.np; q++) stage_flush(st, q, P, gcnt, hsbuf, lane);
   if (!REMOTE_ONLY && iso_acc) atomicAdd(&iso[lane], iso_acc);
   __syncthreads();
   if (!REMOTE_ONLY && threadIdx.x < 64 && iso[threadIdx.x])
