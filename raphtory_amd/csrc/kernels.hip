@@ -606,7 +606,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   int32_t* __restrict__ uw0, int32_t* __restrict__ uw1,
                                                   uint64_t* __restrict__ cb1, int ends,
                                                   int32_t* __restrict__ ccount, int gmax, BatchParams ebp,
-                                                  int dense1) {
+                                                  int dense1, const int32_t* __restrict__ ts_g) {
   __shared__ unsigned long long red[4];
   __shared__ HopLDS L;
   if (threadIdx.x < 4) red[threadIdx.x] = 0;
@@ -722,7 +722,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
             m = em[e] & (ends ? mv : vm[nb]) & mv;
           }
         }
-        lb = grank ? grank[nb] : nb;
+        lb = ts_g ? ts_g[base + j] : (grank ? grank[nb] : nb);
       }
       uint64_t bal = __ballot(m != 0);
       if (m) {
@@ -1422,7 +1422,8 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
                                                      int64_t n_own, const int32_t* __restrict__ ts_e,
                                                      const int32_t* __restrict__ ts_nb,
                                                      const int64_t* __restrict__ ts_t, int64_t tcut, int ends,
-                                                     unsigned long long* __restrict__ work, BatchParams ebp) {
+                                                     unsigned long long* __restrict__ work, BatchParams ebp,
+                                                     const int32_t* __restrict__ ts_g) {
   __shared__ HopLDS L;
   if constexpr (IEM) hop_lds_init(L, ebp, ebp.thr_e);
   const int lane = lane_id();
@@ -1482,7 +1483,7 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
       }
       count += __popcll(bal);
       any |= m;
-      const int32_t lb = (grank && m) ? grank[nb] : nb;  // setup sends the neighbour's label (id)
+      const int32_t lb = (grank && m) ? (ts_g ? ts_g[lo + jj] : grank[nb]) : nb;  // setup sends the neighbour's label (id)
       for (uint64_t b = bal; b; b &= b - 1) {  // lane = view from here: the kept slots one by one
         const int L = __builtin_ctzll(b);
         const int32_t q = __builtin_amdgcn_readlane(lb, L);
@@ -2370,6 +2371,7 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
+int g_slot_labels = 1;  // K2 streams the neighbours' labels (DevGraph.ts_g; RGPU_TSG)
 int g_deal_slots = 16;  // deal_group maxima of K2 / the superstep kernel (RGPU_DEAL_SLOTS / _STEP;
                         // C4 A/B, profiles/r03/c4_ab_deal.log: K2 16 ≈ 64 < 1, step 1 ≈ 4 << 64)
 int g_deal_step = 4;
@@ -2423,7 +2425,8 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
                                                 uw0, uw1, cb1, ends ? 1 : 0, ccount, g_deal_slots, iem ? *ebp : bp0,
-                                                dense_div > 0 && (dense_div & kDense1) && ccount ? 1 : 0);
+                                                dense_div > 0 && (dense_div & kDense1) && ccount ? 1 : 0,
+                                                g_slot_labels ? g.ts_g : nullptr);
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
@@ -2474,7 +2477,7 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
   (iem ? k_heavy_slots<true> : k_heavy_slots<false>)<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(
       g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
       snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own, g.ts_e, g.ts_nb, g.ts_t, tcut, ends ? 1 : 0, work,
-      iem ? *ebp : bp0);
+      iem ? *ebp : bp0, g_slot_labels ? g.ts_g : nullptr);
 }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,

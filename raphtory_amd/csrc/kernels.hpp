@@ -61,6 +61,8 @@ struct DevGraph {
   const int32_t* ts_e = nullptr;    // [ne + n_in] edge of the slot
   const int32_t* ts_nb = nullptr;   // [ne + n_in] neighbour across it
   const int64_t* ts_t = nullptr;    // [ne + n_in] 2 * the edge's last add time + simple (tslots.hip)
+  const int32_t* ts_g = nullptr;    // [ne + n_in] grank[ts_nb] (with grank): K2 streams the neighbour's
+                                    // label instead of a random grank read per slot
 };
 // a ts_t word: the edge's last add time, and whether the slot is simple (one add point, no
 // endpoint deaths: K2 derives its window bits from the time alone)
@@ -71,6 +73,7 @@ __host__ __device__ inline bool ts_simple(int64_t x) { return x & 1; }
 // than 2^31 slots), the graph keeps CSR order.
 bool build_time_slots(hipStream_t s, const DevGraph& g, int32_t* ts_e, int32_t* ts_nb, int64_t* ts_t,
                       std::vector<void*>& temps);
+void build_slot_labels(hipStream_t s, int64_t n, const int32_t* ts_nb, const int32_t* grank, int32_t* ts_g);
 constexpr int kSegSlots = 512;
 
 // Per-batch state of the heavy-vertex path (one per batch slot).
@@ -160,6 +163,7 @@ extern int g_sum_blocks;   // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOC
 extern int g_hist_rounds;  // label-dedup rounds per (view, chunk) in k_cc_hist (RGPU_HIST_ROUNDS)
 extern int g_deal_slots, g_deal_step;  // deal_group maxima (kernels.hip; RGPU_DEAL_SLOTS / RGPU_DEAL_STEP)
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
+extern int g_slot_labels;  // K2 reads DevGraph.ts_g (RGPU_TSG)
 extern int g_tail_step, g_tail_grid;  // supersteps >= tail_step use at most tail_grid blocks
 // uniform label words (kernels.hip, kMixed): rows of the uniform vertices written into lab
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab);

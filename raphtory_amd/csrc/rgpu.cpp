@@ -1921,6 +1921,17 @@ void build_tslots(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L) {
   }
 }
 
+// the neighbours' labels (grank) in time-ordered slot order, once grank is known
+void build_tslot_labels(DevGraph& g, std::vector<void*>& L) {
+  if (!g.ts_nb || !g.grank) return;
+  const int64_t n = g.ne + g.n_in;
+  int32_t* tg = dalloc<int32_t>(L, n);
+  build_slot_labels(nullptr, n, g.ts_nb, g.grank, tg);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  g.ts_g = tg;
+}
+
 const int64_t* upload_adj(std::vector<void*>& L, const std::vector<int64_t>& out_off,
                           const std::vector<int64_t>& in_off) {
   const int64_t nv = (int64_t)out_off.size() - 1;
@@ -2182,6 +2193,7 @@ void seal_delta(rgpu_ctx* c) {
         throw HipFail{x.what()};
       }
       g.grank = PM.grank;
+      build_tslot_labels(g, L);
       HIPCHK(hipMemcpy(&ne_owned, DD.out_off + g.n_own, sizeof(int64_t), hipMemcpyDeviceToHost));  // (owned first)
       phase("partition plan");
     }
@@ -2342,11 +2354,15 @@ int rgpu_seal(rgpu_ctx* c) {
     g.n_own = P.n_own;
     build_heavy(c, g, L, P.out_off, P.in_off);
     build_tslots(c, g, L);
-    if (!c->partitioned && !P.grank.empty()) g.grank = dupload(L, P.grank);  // locality order: labels are id ranks
+    if (!c->partitioned && !P.grank.empty()) {  // locality order: labels are id ranks
+      g.grank = dupload(L, P.grank);
+      build_tslot_labels(g, L);
+    }
     if (c->partitioned) {  // CC labels are vertex ids (the label owner routes component counts)
       if (c->nparts > kMaxParts) return fail(c, RGPU_EINVAL, "more than 8 partitions");
       // (also with P = 1, where a relabeled pack's grank holds id ranks)
       g.grank = dupload(L, std::vector<int32_t>(P.vid.begin(), P.vid.end()));
+      build_tslot_labels(g, L);
       Part& X = c->pt;
       X.nxs = (int64_t)P.xs_v.size();
       X.nxr = (int64_t)P.xr_v.size();
@@ -2489,6 +2505,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   c->iem_on = env_int("RGPU_IEM", 1) != 0;
   c->dense1 = env_int("RGPU_DENSE1", 1) != 0;
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
+  g_slot_labels = env_int("RGPU_TSG", 1);
   {  // powers of two up to 64
     auto pow2 = [](int x) { int g = 1; while (g < x && g < 64) g <<= 1; return g; };
     g_deal_slots = pow2(env_int("RGPU_DEAL_SLOTS", 16));

@@ -76,6 +76,12 @@ __global__ __launch_bounds__(256) void k_slot_nbrs(int64_t nv, const int64_t* __
   }
 }
 
+__global__ __launch_bounds__(256) void k_slot_labels(int64_t n, const int32_t* __restrict__ ts_nb,
+                                                     const int32_t* __restrict__ grank, int32_t* __restrict__ ts_g) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x)
+    ts_g[p] = grank[ts_nb[p]];
+}
+
 unsigned grid_waves(int64_t n) {
   const int64_t g = (n + 3) / 4;
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 16384));
@@ -107,6 +113,10 @@ bool build_time_slots(hipStream_t s, const DevGraph& g, int32_t* ts_e, int32_t* 
     return false;
   k_slot_nbrs<<<grid_waves(g.nv), 256, 0, s>>>(g.nv, g.adj_off, g.esrc, g.edst, ts_e, ts_nb);
   return hipGetLastError() == hipSuccess;
+}
+
+void build_slot_labels(hipStream_t s, int64_t n, const int32_t* ts_nb, const int32_t* grank, int32_t* ts_g) {
+  k_slot_labels<<<(unsigned)std::min<int64_t>((n + 255) / 256, 65536), 256, 0, s>>>(n, ts_nb, grank, ts_g);
 }
 
 }  // namespace rgpu

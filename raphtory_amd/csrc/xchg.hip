@@ -300,25 +300,29 @@ __device__ __forceinline__ unsigned long long count_rec(int32_t x, int j, unsign
 constexpr int kStage = 64;
 struct CountStage {
   unsigned long long (*rec)[kStage];  // [peer][kStage], wave-private LDS
-  int* n;                             // [peer] staged records
+  int n;                              // lane q: records staged for peer q (a register, not LDS: the
+                                      // lanes read it right after another lane's update)
 };
-__device__ __forceinline__ void stage_flush(const CountStage& st, int q, const XPeers& P,
+// wave-uniform: reserve peer q's staged records in the send buffer and write them out
+__device__ __forceinline__ void stage_flush(CountStage& st, int q, const XPeers& P,
                                             unsigned long long* __restrict__ gcnt,
                                             unsigned long long* __restrict__ hsbuf, int lane) {
-  const int n = st.n[q];
+  const int n = __builtin_amdgcn_readlane(st.n, q);
   if (n == 0) return;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the other lanes' LDS record stores
   unsigned long long base = 0;
   if (lane == 0) base = atomicAdd(&gcnt[q], (unsigned long long)n);
   base = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(base >> 32), 0) << 32) |
          __builtin_amdgcn_readlane((uint32_t)base, 0);
   if (lane < n && base + lane < (unsigned long long)P.cap[q]) hsbuf[P.base[q] + (int64_t)(base + lane)] = st.rec[q][lane];
-  if (lane == 0) st.n[q] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // read before the slots are reused
+  if (lane == q) st.n = 0;
 }
 // wave-wide: the lanes with `on` send (x, j, c) (remote labels, staged) or add it (owned labels)
 template <bool REMOTE_ONLY>
 __device__ __forceinline__ void count_direct(bool on, int32_t x, int j, unsigned c, const XPeers& P, const OwnIdx& I,
                                              int32_t* __restrict__ counts, unsigned long long* __restrict__ gcnt,
-                                             unsigned long long* __restrict__ hsbuf, int lane, const CountStage& st) {
+                                             unsigned long long* __restrict__ hsbuf, int lane, CountStage& st) {
   const int q = on ? owner_of(x, P.np) : -1;
   if (!REMOTE_ONLY && q == P.me) {
     const int64_t r = label_row(I, x);  // always found: a label is a member's id
@@ -329,10 +333,10 @@ __device__ __forceinline__ void count_direct(bool on, int32_t x, int j, unsigned
     const uint64_t mine = __ballot(q == qL);
     todo &= ~mine;
     const int n = __popcll(mine);
-    if (st.n[qL] + n > kStage) stage_flush(st, qL, P, gcnt, hsbuf, lane);
-    const int c0 = st.n[qL];
+    if (__builtin_amdgcn_readlane(st.n, qL) + n > kStage) stage_flush(st, qL, P, gcnt, hsbuf, lane);
+    const int c0 = __builtin_amdgcn_readlane(st.n, qL);
     if (q == qL) st.rec[qL][c0 + __popcll(mine & (lane ? (~0ull >> (64 - lane)) : 0ull))] = count_rec(x, j, c);
-    if (lane == 0) st.n[qL] = c0 + n;
+    if (lane == qL) st.n = c0 + n;
   }
 }
 template <bool REMOTE_ONLY>
@@ -350,14 +354,12 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
   __shared__ int32_t ckey_s[4][kRows];
   __shared__ unsigned int crow_s[4][kRows][64];
   __shared__ unsigned long long srec_s[4][kMaxParts][kStage];
-  __shared__ int sn_s[4][kMaxParts];
   const int lane = lane_of(), wib = threadIdx.x >> 6;
   int32_t* ckey = ckey_s[wib];
   unsigned int (*crow)[64] = crow_s[wib];
-  const CountStage st{srec_s[wib], sn_s[wib]};
+  CountStage st{srec_s[wib], 0};
   if (threadIdx.x < 64) iso[threadIdx.x] = 0;
   if (lane < kRows) ckey[lane] = -1;
-  if (lane < kMaxParts) st.n[lane] = 0;
   for (int h = 0; h < kRows; h++) crow[h][lane] = 0;
   __syncthreads();
   auto cached = [&](int32_t x, int j, unsigned c) -> bool {  // per lane
