@@ -17,6 +17,11 @@ constexpr int kViews = 64;  // views per batch = wavefront width (lane j <-> vie
 // a flagged word never reads as kMixed.
 constexpr int32_t kMixed = -1;
 constexpr int32_t kChgFlag = INT32_MIN;
+// Partitioned mode: the word of a ghost that received no record in the last two steps of the
+// buffer's parity — uniform and unchanged (its label is never read: readers fold a neighbour's word
+// only when flagged).  Without it such a ghost read as kMixed, and every slot to it cost a second
+// dependent load (its change word) in the superstep kernel.
+constexpr int32_t kGhostQuiet = 0x7f7f7f7f;
 __host__ __device__ inline int32_t uw_label(int32_t w) { return w == kMixed ? kMixed : (w & 0x7fffffff); }
 __host__ __device__ inline int32_t uw_word(int32_t u, bool changed) {
   return (u != kMixed && changed) ? (int32_t)((uint32_t)u | 0x80000000u) : u;
@@ -288,11 +293,15 @@ void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t*
                       const int32_t* uw, XRec* sbuf, unsigned long long* scnt, const int32_t* ccount = nullptr,
                       int dense_div = 0, int step = 0, int64_t n_own = 0);
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa);
-void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg);
+void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg,
+                   int32_t* uw = nullptr);
 void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
                         uint64_t* chg, int32_t* uw = nullptr, uint64_t* cb = nullptr);
+// tcut / ebp: the batch's slot cut and (inline edge bits; null: em for every slot) its edge windows;
+// ccount / dense_div / step: nothing is marked when superstep `step` is dense
 void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
-                  const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next);
+                  const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next, int64_t tcut,
+                  const BatchParams* ebp, const int32_t* ccount, int dense_div, int step);
 // owned id -> owned rank: ids ascend with rank; bucket b = id >> shift covers ranks
 // [boff[b], boff[b+1]) (about one id per bucket)
 struct OwnIdx {

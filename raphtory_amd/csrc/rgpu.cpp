@@ -65,7 +65,8 @@ struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   uint64_t *vm = nullptr, *em = nullptr;          // masks of the batch in flight
-  bool iem = false;                               // the batch's K2 computes edge bits inline (em unused)
+  bool iem = false;                               // the batch computes simple slots' edge bits inline
+  BatchParams ebp{};                              // its hops and edge windows (view bit w*KS + k)
   uint64_t *vm_own = nullptr, *em_own = nullptr;  // this slot's own (hop-major batches)
   int32_t *cnt = nullptr, *snbr = nullptr;
   uint64_t* smask = nullptr;
@@ -347,7 +348,7 @@ void run_check(hipStream_t st, const char* what, F launch) {
 }
 
 // uniform label words (kernels.hip): not with the tail kernel (it writes rows only).  Partitioned:
-// ghost rows arrive as per-lane records, so the ghosts' words stay kMixed (start_batch)
+// ghosts: words from uniform records, kMixed for mixed ones, kGhostQuiet otherwise (start_batch, k_xclear)
 bool use_uw(const rgpu_ctx* c) { return c->uw_on && !c->tail_on; }
 
 // The work-counter buffer of a profile run.  RGPU_PROF_LEAN=1: none, so the superstep and K2
@@ -849,9 +850,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   // Inline edge bits (kernels.hip simple_bits): CC's K2 computes the window bits of the simple
   // slots (one add point, no endpoint deaths) for the batch's own windows from the time-ordered
   // slot words, so K1 writes edge masks only for the other edges (all of them for the |E_w|
-  // counts of an RGPU_RUN_EDGE_COUNTS run).  The partitioned mode keeps K1's full edge masks:
-  // its ghost marking (k_xmark) walks them.
-  const bool iem = c->iem_on && rc.algo == RGPU_ALGO_CC && g.ts_t && !c->partitioned;
+  // counts of an RGPU_RUN_EDGE_COUNTS run).  The partitioned ghost marking (k_xmark) does the same.
+  const bool iem = c->iem_on && rc.algo == RGPU_ALGO_CC && g.ts_t;
   BatchParams ebp = bp;  // the batch's edge windows, view bit w*KS + k
   if (rc.G > 1) {
     ebp.W = 1;
@@ -859,6 +859,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   }
   const bool skip_simple = iem && !c->d_ecnt;
   s.iem = iem;
+  s.ebp = ebp;
   if (rc.G == 1) {
     s.vm = s.vm_own;
     s.em = s.em_own;
@@ -928,9 +929,9 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     return;
   }
   if (rc.algo == RGPU_ALGO_CC) {
-    if (c->partitioned && use_uw(c) && g.nv > c->pk.n_own)  // ghosts: rows from records, words kMixed
+    if (c->partitioned && use_uw(c) && g.nv > c->pk.n_own)  // ghosts: quiet until a record arrives (kGhostQuiet)
       for (int p = 0; p < 2; p++)
-        HIPCHK(hipMemsetAsync(s.uw[p] + c->pk.n_own, 0xff, sizeof(int32_t) * (g.nv - c->pk.n_own), s.stream));
+        HIPCHK(hipMemsetAsync(s.uw[p] + c->pk.n_own, 0x7f, sizeof(int32_t) * (g.nv - c->pk.n_own), s.stream));
     // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
     const double b2 = 8.0 * g.nv;  // the view-mask scan; the rest from the work counters (harvest)
@@ -1363,7 +1364,8 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   }
   const int par = r & 1;
   // ghosts whose words records of step r-2 set (their records are still in rbuf[par])
-  launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par]);
+  launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par],
+                use_uw(c) ? s.uw[par] : nullptr);
   bool rover = false;
   for (int q = 0; q < P; q++) rover |= recv[q] > xs.rcap[q];
   if (rover) {  // a larger layout for both parities; the other parity's records of step r-1 are
@@ -1402,7 +1404,8 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   const XPeers Lin = peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]);
   launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par], use_uw(c) ? s.uw[par] : nullptr,
                      chg_bits(c, s, r).next);
-  launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3]);
+  launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3], s.tcut,
+               s.iem ? &s.ebp : nullptr, s.ccount, dense_div(c), r);
   // the vote is global: superstep r+1 runs here even if nothing changed here
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(s.stepcnt + r), 1, 1, s.stream));
   const bool hv = g.n_seg > 0;
@@ -1517,7 +1520,8 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
   xs.x->allreduce_u64(s.stats + kViews, 5 * kViews, false, s.stream);
   // the batch's ghost change words back to zero (the next batch's ghosts start clean)
   for (int par = 0; par < 2; par++) {
-    launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par]);
+    launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par],
+                use_uw(c) ? s.uw[par] : nullptr);
     std::fill(xs.rcnt[par], xs.rcnt[par] + kMaxParts, 0);
   }
   HIPCHK(hipGetLastError());

@@ -18,8 +18,10 @@
 
 #include <climits>
 #include <cstdint>
+#include <cstring>
 
 #include "kernels.hpp"
+#include "window_bits.hpp"
 
 namespace rgpu {
 
@@ -172,13 +174,17 @@ __global__ void k_xcounts(int np, int me, unsigned long long* __restrict__ scnt,
   scnt[q] = 0;
 }
 
-// ghosts whose change word a record set two supersteps ago: clear it in that parity's words
+// ghosts whose change word a record set two supersteps ago: clear it in that parity's words, and
+// set their uniform word back to kGhostQuiet (uw non-null)
 __global__ __launch_bounds__(256) void k_xclear(XPeers P, const XRec* __restrict__ rbuf,
-                                                const int32_t* __restrict__ xrv, uint64_t* __restrict__ chg) {
+                                                const int32_t* __restrict__ xrv, uint64_t* __restrict__ chg,
+                                                int32_t* __restrict__ uw) {
   const int64_t n = P.pre[P.np];
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int q = peer_of(P, i);
-    chg[xrv[P.xoff[q] + rbuf[P.base[q] + i - P.pre[q]].e]] = 0;
+    const int32_t g = xrv[P.xoff[q] + rbuf[P.base[q] + i - P.pre[q]].e];
+    chg[g] = 0;
+    if (uw) uw[g] = kGhostQuiet;
   }
 }
 
@@ -221,8 +227,12 @@ __global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __res
 
 // After the unpack: the first record of every ghost marks the ghost's owned neighbours that
 // share a changed view (the next frontier, as a local change would).  Ghosts keep no compacted
-// slots (K2 runs over the owned vertices only): the kept views of a static slot, em[e] & vm[nb] &
-// vm[g], are recomputed here for the ghosts that changed.  Heavy ghosts: k_heavy_mark.
+// slots (K2 runs over the owned vertices only): the kept views of a static slot, bits & vm[nb] &
+// vm[g], are recomputed here for the ghosts that changed, over the time-ordered slots up to the
+// batch's cut (bits: K2's inline edge bits for a simple slot, else em[e]; without time-ordered
+// slots the CSR order and em).  Nothing to mark when superstep r is dense (the next one visits
+// every member).  Heavy ghosts: k_heavy_mark.
+template <bool TS>
 __global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict__ rbuf,
                                                const int32_t* __restrict__ xrv, const uint64_t* __restrict__ chg,
                                                const int64_t* __restrict__ out_off,
@@ -230,7 +240,15 @@ __global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict_
                                                const int32_t* __restrict__ in_eid,
                                                const int32_t* __restrict__ esrc, const int32_t* __restrict__ edst,
                                                const uint64_t* __restrict__ vm, const uint64_t* __restrict__ em,
-                                               const int32_t* __restrict__ hv_of, uint8_t* __restrict__ act_next) {
+                                               const int32_t* __restrict__ hv_of, uint8_t* __restrict__ act_next,
+                                               const int64_t* __restrict__ adj_off, const int32_t* __restrict__ ts_e,
+                                               const int32_t* __restrict__ ts_nb, const int64_t* __restrict__ ts_t,
+                                               int64_t tcut, BatchParams ebp, int iem,
+                                               const int32_t* __restrict__ ccount, int dense_div, int step,
+                                               int64_t n_own) {
+  if (dense_after(ccount, step + 1, n_own, dense_div)) return;  // step r dense: r+1 visits every member
+  __shared__ HopLDS L;
+  if (TS && iem) hop_lds_init(L, ebp, ebp.thr_e);
   const int64_t n = P.pre[P.np];
   const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -243,6 +261,21 @@ __global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict_
     const int32_t g = xrv[P.xoff[q] + e0];
     if (hv_of && hv_of[g] >= 0) continue;
     const uint64_t ch = chg[g] & vm[g];
+    if (TS) {
+      const int64_t a = adj_off[g], ntot = adj_off[g + 1] - a;
+      for (int64_t c = 0; c < ntot; c += 64) {
+        if (ts_time(ts_t[a + c]) < tcut) break;  // newest first: the rest are dead in every view
+        const int64_t j = c + lane;
+        if (j >= ntot) continue;
+        const int64_t tsw = ts_t[a + j];
+        if (ts_time(tsw) < tcut) continue;
+        const int32_t nb = ts_nb[a + j];
+        if (nb == g) continue;
+        const uint64_t bits = (iem && ts_simple(tsw)) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[ts_e[a + j]];
+        if (bits & vm[nb] & ch) act_next[nb] = 1;
+      }
+      continue;
+    }
     const int64_t o0 = out_off[g], i0 = in_off[g];
     const int64_t nout = out_off[g + 1] - o0, ntot = nout + (in_off[g + 1] - i0);
     for (int64_t c = 0; c < ntot; c += 64) {
@@ -463,18 +496,24 @@ void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t*
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa) {
   k_xcounts<<<1, 64, 0, s>>>(np, me, scnt, stepflag, xa);
 }
-void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg) {
-  if (P.pre[P.np] > 0) k_xclear<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, xrv, chg);
+void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg, int32_t* uw) {
+  if (P.pre[P.np] > 0) k_xclear<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, xrv, chg, uw);
 }
 void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
                         uint64_t* chg, int32_t* uw, uint64_t* cb) {
   if (P.pre[P.np] > 0) k_xunpack_rec<<<xgrid(P.pre[P.np], 16), 256, 0, s>>>(P, rbuf, xrv, lab, chg, uw, cb);
 }
 void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
-                  const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next) {
-  if (P.pre[P.np] > 0)
-    k_xmark<<<xgrid(P.pre[P.np], 4), 256, 0, s>>>(P, rbuf, xrv, chg, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst,
-                                                   vm, em, g.n_seg > 0 ? g.hv_of : nullptr, act_next);
+                  const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next, int64_t tcut,
+                  const BatchParams* ebp, const int32_t* ccount, int dense_div, int step) {
+  if (P.pre[P.np] <= 0) return;
+  BatchParams bp0;
+  if (!ebp) std::memset(&bp0, 0, sizeof(bp0));
+  auto* kern = g.ts_t ? k_xmark<true> : k_xmark<false>;
+  kern<<<xgrid(P.pre[P.np], 4), 256, 0, s>>>(P, rbuf, xrv, chg, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
+                                             g.n_seg > 0 ? g.hv_of : nullptr, act_next, g.adj_off, g.ts_e, g.ts_nb,
+                                             g.ts_t, tcut, ebp ? *ebp : bp0, ebp ? 1 : 0, ccount, dense_div, step,
+                                             g.n_own);
 }
 void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,

@@ -76,6 +76,10 @@ def main():
                "kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in ks.items()},
                "partition0_kernels": {k: [v["launches"], round(v["ms"], 2)] for k, v in parts[0].stats()["kernels"].items()
                                       if v["launches"]},
+               # algorithmic bytes (the counting pass's work counters) summed over the
+               # partitions: more bytes than at P = 1 = more work, not slower work
+               "kernel_GB_sum_by_kernel": {k: round(sum(g.stats()["kernels"][k].get("bytes", 0.0) for g in parts) / 1e9, 2)
+                                           for k in ks},
                "xchg_MB_per_query": {k: round(v, 1) for k, v in by.items()},
                "xchg_model_ms_per_partition": [round(x, 2) for x in xms], "xchg_link_GBps": link / 1e9,
                "xchg_rounds_per_partition": rounds,
