@@ -528,13 +528,30 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
    const int64_t vlane = dealt_item(wave, nwaves, r, G, lane);
    const uint64_t mvl = vlane < nv ? vm[vlane] : 0;
    if (vlane < nv && mvl == 0) { cnt[vlane] = 0; vadj[vlane] = 0; }
+   // The round's members' offsets, hub flags and (time-ordered) newest slot times, loaded by
+   // their lanes at once: the member walk below starts each vertex at its slot loads instead of
+   // two dependent trips (offsets, then the cut check) per member.
+   int64_t o0l = 0, i0l = 0, tfl = INT64_MAX;
+   int32_t noutl = 0, ntotl = 0;
+   bool hvl = false;
+   if (mvl) {
+     o0l = out_off[vlane];
+     i0l = in_off[vlane];
+     noutl = (int32_t)(out_off[vlane + 1] - o0l);
+     ntotl = noutl + (int32_t)(in_off[vlane + 1] - i0l);
+     hvl = hv_of && hv_of[vlane] >= 0;
+     if (ts_t && ntotl > 0) tfl = ts_time(ts_t[o0l + i0l]);
+   }
+   const uint64_t heavyl = __ballot(hvl);
    uint64_t todo = __ballot(mvl != 0);
    while (todo) {
-    const int64_t v = dealt_item(wave, nwaves, r, G, __builtin_ctzll(todo));
-    const uint64_t mv = readlane64(mvl, __builtin_ctzll(todo));
+    const int Lm = __builtin_ctzll(todo);
+    const int64_t v = dealt_item(wave, nwaves, r, G, Lm);
+    const uint64_t mv = readlane64(mvl, Lm);
     todo &= todo - 1;
-    const int64_t o0 = out_off[v], o1 = out_off[v + 1], i0 = in_off[v], i1 = in_off[v + 1];
-    if (hv_of && hv_of[v] >= 0) {
+    const int64_t o0 = (int64_t)readlane64((uint64_t)o0l, Lm), i0 = (int64_t)readlane64((uint64_t)i0l, Lm);
+    const int64_t tfirst = (int64_t)readlane64((uint64_t)tfl, Lm);
+    if ((heavyl >> Lm) & 1) {
       // heavy vertex: its segments were compacted by k_heavy_slots, which also left the
       // superstep-1 minima of its neighbours' labels in hbest; neighbours of a change are
       // marked by k_heavy_mark.  A heavy ghost (partitioned mode) only needs its kept count and
@@ -592,14 +609,16 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     } else {
       row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
     }
-    const int64_t nout = o1 - o0, ntot = nout + (i1 - i0), base = o0 + i0;
+    const int64_t nout = __builtin_amdgcn_readlane(noutl, Lm), ntot = __builtin_amdgcn_readlane(ntotl, Lm),
+                  base = o0 + i0;
     int32_t count = 0, best = me;
     uint64_t any = 0;
     uint64_t m_keep = 0;  // ntot <= 64: this lane's slot stays in registers for the marking below
     int32_t nb_keep = 0;
     for (int64_t c = 0; c < ntot; c += 64) {
       const int64_t j = c + lane;
-      if (ts_t && ts_time(ts_t[base + c]) < tcut) break;  // newest first: the rest are dead in every view
+      // newest first: the rest are dead in every view (chunk 0: the hoisted time)
+      if (ts_t && (c == 0 ? tfirst : ts_time(ts_t[base + c])) < tcut) break;
       scanned += ntot - c < 64 ? ntot - c : 64;
       uint64_t m = 0;
       int32_t nb = 0, lb = 0;

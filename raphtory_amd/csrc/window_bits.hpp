@@ -103,10 +103,30 @@ __device__ __forceinline__ void hop_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1],
 // tf <= t <= tf + w.  Any other slot reads em[e], which K1 then writes for the other edges only
 // (k_edge_mask SKIP).  (Running K1's whole edge_bits inline for them instead took K2 from 77 to 123
 // VGPRs.)
+// first hop index with hop >= x, by a binary search of the LDS table (few registers: K2 runs this
+// per static slot, and the arithmetic form of hop_lb cost it a wave of occupancy)
+__device__ __forceinline__ int hop_lb_search(const HopLDS& L, int64_t x) {
+  int lo = 0, n = L.K;
+  while (n > 0) {
+    const int h = n >> 1;
+    if (L.hop[lo + h] < x) {
+      lo += h + 1;
+      n -= h + 1;
+    } else {
+      n = h;
+    }
+  }
+  return lo;
+}
 __device__ __forceinline__ uint64_t simple_bits(const HopLDS& L, int sorted, int64_t tf) {
   uint64_t m[1] = {0};
-  if (sorted) {
-    interval_bits<false>(m, L, tf, hop_lb(L, tf), L.K);
+  if (sorted) {  // hops [first >= tf, first > tf + w) of each window
+    const int a = hop_lb_search(L, tf);
+    const int64_t tlast = L.hop[L.K - 1];
+    for (int w = 0; w < L.W; w++) {  // (a window reaching past the last hop: no search, no overflow)
+      const int u = L.thr[w] >= tlast - tf ? L.K : hop_lb_search(L, tf + L.thr[w] + 1);
+      m[0] |= range_bits(a, u) << (w * L.KS);
+    }
   } else {
     for (int k = 0; k < L.K; k++)
       if (L.hop[k] >= tf) hop_bits<false>(m, L, L.hop[k] - tf, k);

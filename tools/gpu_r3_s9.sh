@@ -2,8 +2,8 @@
 mkdir -p gpurun_out
 timeout -k 10 480 python -u -m pytest tests -m "gpu and not fullsize" -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/pytest_fast.log 2>&1 || { tail -40 gpurun_out/pytest_fast.log; exit 1; }
 tail -2 gpurun_out/pytest_fast.log
-AB='base: nod1:RGPU_DENSE1=0 k1em:RGPU_IEM=0' 
-timeout -k 10 700 python -u tools/c4_ab.py --steps 2 base: notsg:RGPU_TSG=0 nod1:RGPU_DENSE1=0 k1em:RGPU_IEM=0 > gpurun_out/c4_ab.log 2>&1 || { tail -20 gpurun_out/c4_ab.log; exit 1; }
+
+timeout -k 10 700 python -u tools/c4_ab.py --steps 2 ${AB:-base: notsg:RGPU_TSG=0} > gpurun_out/c4_ab.log 2>&1 || { tail -20 gpurun_out/c4_ab.log; exit 1; }
 python - <<'PY'
 import json
 for l in open("gpurun_out/c4_ab.log"):
@@ -13,4 +13,4 @@ for l in open("gpurun_out/c4_ab.log"):
     d = json.loads(l); k = d["kernels"]
     print(d["variant"], d["round"], d["ms"], d["same"], {n: k[n] for n in k})
 PY
-PARTS=1,8 bash tools/gpu_r3_part.sh
+[ -n "${NOPART:-}" ] || PARTS=1,8 bash tools/gpu_r3_part.sh

@@ -49,7 +49,9 @@ def main():
         print(f"P={P}: sealed in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
         run()
         print(f"P={P}: warm run done", file=sys.stderr, flush=True)
+        t_prof = time.time()
         run(profile=True, serial=True)
+        t_prof = time.time() - t_prof
         per = []
         ks = {}
         for g in parts:
@@ -84,6 +86,9 @@ def main():
                "xchg_model_ms_per_partition": [round(x, 2) for x in xms], "xchg_link_GBps": link / 1e9,
                "xchg_rounds_per_partition": rounds,
                "kernel_plus_xchg_ms_max": max(tot),
+               # the serial profiled run's wall time over P: one partition's share of everything the
+               # timers above leave out too (exchange pack / unpack / mark kernels, host turns)
+               "serial_wall_ms_per_partition": round(t_prof * 1e3 / P, 1),
                "vertices_here": [g.stats()["vertices"] for g in parts], "edges_here": [g.stats()["edges"] for g in parts],
                "check": [int(summ[..., 0].sum()), int(summ[..., 1].sum()), int(summ[..., 5].sum())]}
         print(json.dumps(out), flush=True)
