@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RGPU_ABI_VERSION 7
+#define RGPU_ABI_VERSION 8
 
 /* error codes */
 #define RGPU_OK 0
@@ -84,10 +84,11 @@ typedef struct {
   /* per-kernel event timing (RGPU_RUN_PROFILE): 0=window_mask 1=slots 2=cc_step 3=cc_hist
    * 4=cc_summary 5=pr_step 6=degree 7=cc_tail (late supersteps, one workgroup)
    * 8=heavy (hub segment kernels) 9=diffusion step 10=vertex-program step
-   * 11=edge_mask (K1's edge masks; 0 = its vertex masks) */
-  int64_t kernel_launches[12];
-  double kernel_ms[12];
-  double kernel_bytes[12];       /* algorithmic bytes summed over launches */
+   * 11=edge_mask (K1's edge masks; 0 = its vertex masks) 12=xchg (partitioned mode: the exchange's
+   * pack / unpack / mark / clear / membership kernels, ABI 8) 13-15 reserved */
+  int64_t kernel_launches[16];  /* (12 before ABI 8) */
+  double kernel_ms[16];
+  double kernel_bytes[16];       /* algorithmic bytes summed over launches */
   /* last rgpu_seal: wall ms, 1 if it merged a delta into the resident graph (live ingest),
    * and the number of updates that delta held (ABI 3) */
   double seal_ms;

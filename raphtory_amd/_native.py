@@ -28,7 +28,7 @@ ERROR_NAMES = {
     RGPU_ENOTSUP: "RGPU_ENOTSUP",
 }
 KERNEL_NAMES = ["window_mask", "cc_slots", "cc_step", "cc_hist", "cc_summary", "pr_step", "degree", "cc_tail",
-                "heavy", "diffusion", "vp_step", "edge_mask"]
+                "heavy", "diffusion", "vp_step", "edge_mask", "xchg", "-13", "-14", "-15"]
 
 # exported symbols of librgpu.so, exactly the declarations of include/rgpu.h
 EXPORTS = [
@@ -63,7 +63,7 @@ class Stats(C.Structure):
         ("vertex_events", C.c_int64), ("edge_events", C.c_int64), ("deaths", C.c_int64),
         ("views", C.c_int64), ("batches", C.c_int64), ("supersteps", C.c_int64), ("launches", C.c_int64),
         ("ms_total", C.c_double),
-        ("kernel_launches", C.c_int64 * 12), ("kernel_ms", C.c_double * 12), ("kernel_bytes", C.c_double * 12),
+        ("kernel_launches", C.c_int64 * 16), ("kernel_ms", C.c_double * 16), ("kernel_bytes", C.c_double * 16),
         ("seal_ms", C.c_double), ("seal_incremental", C.c_int64), ("seal_delta_updates", C.c_int64),
         ("alive_edge_windows", C.c_int64), ("edges_owned", C.c_int64), ("xchg_bytes", C.c_double),
         ("xchg_bytes_by", C.c_double * 4),
