@@ -544,6 +544,116 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
    }
    const uint64_t heavyl = __ballot(hvl);
    uint64_t todo = __ballot(mvl != 0);
+   if (ts_e && ts_t) {
+     // Light members (at most 64 static slots, not hubs) are packed into 64-lane passes: lane =
+     // slot over the concatenated slot lists of consecutive members, so one round of loads serves
+     // every member of the pack instead of one dependent trip per member.  A member whose newest
+     // slot predates the cut takes no lanes.
+     const int32_t neff = (tfl < tcut) ? 0 : ntotl;
+     const int32_t mel = mvl ? (grank ? grank[vlane] : (int32_t)vlane) : 0;
+     uint64_t light = todo & ~heavyl & __ballot(ntotl <= 64);
+     todo &= ~light;
+     while (light) {
+      uint64_t pack = 0;
+      int sum = 0, myL = 0, myj = 0;
+      while (light) {
+        const int Lp = __builtin_ctzll(light);
+        const int n = __builtin_amdgcn_readlane(neff, Lp);
+        if (pack && sum + n > 64) break;
+        if (lane >= sum && lane < sum + n) { myL = Lp; myj = lane - sum; }
+        pack |= 1ull << Lp;
+        sum += n;
+        light &= light - 1;
+      }
+      // every lane of the pack: its member, slot and kept views
+      const bool on = lane < sum;
+      const int64_t vmy = dealt_item(wave, nwaves, r, G, myL);
+      const int64_t bmy = (int64_t)__shfl(o0l + i0l, myL);
+      const uint64_t mvmy = ((uint64_t)(uint32_t)__shfl((int)(mvl >> 32), myL) << 32) | (uint32_t)__shfl((int)mvl, myL);
+      uint64_t m = 0;
+      int32_t nb = 0, lb = 0;
+      if (on) {
+        const int64_t p = bmy + myj;
+        const int64_t tsw = ts_t[p];
+        nb = ts_nb[p];
+        const int32_t e = ts_e[p];
+        if (nb != (int32_t)vmy && ts_time(tsw) >= tcut) {
+          if constexpr (IEM) {
+            m = (ts_simple(tsw) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[e]) & vm[nb] & mvmy;
+          } else {
+            m = em[e] & (ends ? mvmy : vm[nb]) & mvmy;
+          }
+        }
+        lb = ts_g ? ts_g[p] : (grank ? grank[nb] : nb);
+      }
+      const uint64_t bal = __ballot(m != 0);
+      if (m) {  // compacted at the member's static offset, in lane order within the member
+        const uint64_t below = lanemask_lt() & ~((1ull << (lane - myj)) - 1);
+        const int64_t pos = bmy + __popcll(bal & below);
+        snbr[pos] = nb;
+        smask[pos] = m;
+      }
+      // per member of the pack: superstep 1 (lane = view) and its words
+      int pre = 0;
+      for (uint64_t pk = pack; pk; pk &= pk - 1) {
+        const int Lp = __builtin_ctzll(pk);
+        const int n = __builtin_amdgcn_readlane(neff, Lp);
+        const uint64_t span = n == 0 ? 0ull : ((n >= 64 ? ~0ull : ((1ull << n) - 1)) << pre);
+        pre += n;
+        const int64_t v = dealt_item(wave, nwaves, r, G, Lp);
+        const uint64_t mv = readlane64(mvl, Lp);
+        const bool own = v < n_own;
+        const int32_t me = __builtin_amdgcn_readlane(mel, Lp);
+        if (uw0) {
+          if (lane == 0) uw0[v] = me == INT32_MAX ? kMixed : me;
+          if (me == INT32_MAX) row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
+        } else {
+          row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
+        }
+        const uint64_t kept = bal & span;
+        const int32_t count = __popcll(kept);
+        scanned += (unsigned long long)n;
+        int32_t best = me;
+        uint64_t any = 0;
+        if (own) {
+          for (uint64_t b = kept; b; b &= b - 1) {
+            const int K = __builtin_ctzll(b);
+            const int32_t q = __builtin_amdgcn_readlane(lb, K);
+            const uint64_t mK = readlane64(m, K);
+            any |= mK;
+            if (((mK >> lane) & 1) && q < best) best = q;
+          }
+        }
+        if (uw1) {
+          const int32_t u = row_uniform(best, mv, lane);
+          const bool ch1 = __ballot(best < me) != 0;
+          if (lane == 0) uw1[v] = uw_word(u, ch1);
+          if (u == kMixed) row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+          uwn += 2;
+          if (u == kMixed) lw += row_lines(mv);
+        } else {
+          row_store(lab1 + v * 64, best, line_has(mv, lane), lane);
+          lw += 2 * row_lines(mv);
+        }
+        const uint64_t ch = __ballot(best < me);
+        if (lane == 0) {
+          cnt[v] = count;
+          vadj[v] = any;
+          chg1[v] = ch;
+          if (ch && cb1) atomicOr((unsigned long long*)&cb1[v >> 6], 1ull << (v & 63));
+        }
+        if (!own) continue;
+        lanes |= ch;
+        if (ch) changed++;
+        if (ch && !dense1) {  // (a dense step 1: step 2 visits every member, dense_rule)
+          if (lane == 0) act2[v] = 1;
+          if (((span >> lane) & 1) && (m & ch)) act2[nb] = 1;
+        }
+        members += 1;
+        alive += (unsigned long long)count;
+      }
+     }
+   }
    while (todo) {
     const int Lm = __builtin_ctzll(todo);
     const int64_t v = dealt_item(wave, nwaves, r, G, Lm);
