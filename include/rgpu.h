@@ -84,8 +84,9 @@ typedef struct {
   /* per-kernel event timing (RGPU_RUN_PROFILE): 0=window_mask 1=slots 2=cc_step 3=cc_hist
    * 4=cc_summary 5=pr_step 6=degree 7=cc_tail (late supersteps, one workgroup)
    * 8=heavy (hub segment kernels) 9=diffusion step 10=vertex-program step
-   * 11=edge_mask (K1's edge masks; 0 = its vertex masks) 12=xchg (partitioned mode: the exchange's
-   * pack / unpack / mark / clear / membership kernels, ABI 8) 13-15 reserved */
+   * 11=edge_mask (K1's edge masks; 0 = its vertex masks) 12=xchg (partitioned mode: ghost membership
+   * words and received counts) 13=xchg_pack (label records) 14=xchg_unpack (records into ghost words /
+   * rows, the clear two steps later) 15=xchg_mark (owned neighbours of changed ghosts) (ABI 8) */
   int64_t kernel_launches[16];  /* (12 before ABI 8) */
   double kernel_ms[16];
   double kernel_bytes[16];       /* algorithmic bytes summed over launches */

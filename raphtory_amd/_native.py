@@ -28,7 +28,7 @@ ERROR_NAMES = {
     RGPU_ENOTSUP: "RGPU_ENOTSUP",
 }
 KERNEL_NAMES = ["window_mask", "cc_slots", "cc_step", "cc_hist", "cc_summary", "pr_step", "degree", "cc_tail",
-                "heavy", "diffusion", "vp_step", "edge_mask", "xchg", "-13", "-14", "-15"]
+                "heavy", "diffusion", "vp_step", "edge_mask", "xchg", "xchg_pack", "xchg_unpack", "xchg_mark"]
 
 # exported symbols of librgpu.so, exactly the declarations of include/rgpu.h
 EXPORTS = [

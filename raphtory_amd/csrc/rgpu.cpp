@@ -44,7 +44,7 @@ struct HipFail {
 
 enum KernelId { KID_MASK = 0, KID_SLOTS = 1, KID_STEP = 2, KID_HIST = 3, KID_SUMMARY = 4,
                 KID_PR = 5, KID_DEGREE = 6, KID_TAIL = 7, KID_HEAVY = 8, KID_DIFF = 9, KID_VP = 10, KID_EMASK = 11,
-                KID_XCHG = 12, KID_N = 16 };
+                KID_XCHG = 12, KID_XPACK = 13, KID_XUNPACK = 14, KID_XMARK = 15, KID_N = 16 };
 
 constexpr int kMaxSteps = 128;
 // stats words: 6 per-view fields + counters row | folded lane words [step] | lane-change shards
@@ -1321,7 +1321,7 @@ void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
     return;
   }
   const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
-  timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
+  timed_launch(c, si, KID_XPACK, 0.0, [&] { launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
                    s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
                    c->pk.n_own); });
   launch_xcounts(s.stream, P, c->part, xs.scnt, s.stepcnt + r, xs.xab);
@@ -1352,7 +1352,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (over) {  // the counts were exact; the records did not all fit: pack again, larger
     grow_regions(&xs.sbuf, xs.scap, sent, P, s.stream);
     const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
-    timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
+    timed_launch(c, si, KID_XPACK, 0.0, [&] { launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
                      s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
                    c->pk.n_own); });
     HIPCHK(hipMemsetAsync(xs.scnt, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
@@ -1364,7 +1364,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   }
   const int par = r & 1;
   // ghosts whose words records of step r-2 set (their records are still in rbuf[par])
-  timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par],
+  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par],
                 use_uw(c) ? s.uw[par] : nullptr); });
   bool rover = false;
   for (int q = 0; q < P; q++) rover |= recv[q] > xs.rcap[q];
@@ -1402,9 +1402,9 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   }
   std::copy(recv, recv + kMaxParts, xs.rcnt[par]);
   const XPeers Lin = peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]);
-  timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par], use_uw(c) ? s.uw[par] : nullptr,
+  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par], use_uw(c) ? s.uw[par] : nullptr,
                      chg_bits(c, s, r).next); });
-  timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3], s.tcut,
+  timed_launch(c, si, KID_XMARK, 0.0, [&] { launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3], s.tcut,
                s.iem ? &s.ebp : nullptr, s.ccount, dense_div(c), r); });
   // the vote is global: superstep r+1 runs here even if nothing changed here
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(s.stepcnt + r), 1, 1, s.stream));
@@ -1520,7 +1520,7 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
   xs.x->allreduce_u64(s.stats + kViews, 5 * kViews, false, s.stream);
   // the batch's ghost change words back to zero (the next batch's ghosts start clean)
   for (int par = 0; par < 2; par++) {
-    timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par],
+    timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par],
                 use_uw(c) ? s.uw[par] : nullptr); });
     std::fill(xs.rcnt[par], xs.rcnt[par] + kMaxParts, 0);
   }

@@ -33,6 +33,7 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
   const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), l);
   return ((uint64_t)hi << 32) | lo;
 }
+__device__ __forceinline__ uint64_t lanemask_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 __device__ __forceinline__ int owner_of(int64_t id, int np) { return (int)(((id < 0 ? -id : id) % (10 * (int64_t)np)) / 10); }
 // record index i of a receive layout -> peer
 __device__ __forceinline__ int peer_of(const XPeers& P, int64_t i) {
@@ -115,16 +116,25 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
     const int q = ok ? xq[e] : 0;
     uint64_t m = 0;
     if (ok && (act == nullptr || act[v])) m = chg_now[v] & vadj[v];
-    const uint64_t todo = __ballot(m != 0);
-    if (!todo) continue;
+    if (!__ballot(m != 0)) continue;
+    // A uniform sender (its word is its row) has one label: one record, written by its own lane.
+    // Only mixed senders walk their distinct labels one by one (lane = view).
+    const int32_t u = (m != 0 && uw) ? uw_label(uw[v]) : kMixed;
+    const bool uni = m != 0 && u != kMixed;
+    const uint64_t mixed = __ballot(m != 0 && !uni);
     unsigned long long cq = 0;  // lane p: records of this wave for peer p
-    for (uint64_t b = todo; b; b &= b - 1) {
+    uint64_t mypeer = 0;        // the uniform lanes sending to this lane's peer
+    for (int p = 0; p < P.np; p++) {
+      const uint64_t b = __ballot(uni && q == p);
+      if (lane == p) cq = (unsigned long long)__popcll(b);
+      if (q == p) mypeer = b;
+    }
+    for (uint64_t b = mixed; b; b &= b - 1) {
       const int L = __builtin_ctzll(b);
       const int32_t vL = __builtin_amdgcn_readlane(v, L);
       const int qL = __builtin_amdgcn_readlane(q, L);
       uint64_t mm = rl64(m, L);
-      const int32_t uL = uw ? uw_label(uw[vL]) : -1;  // a uniform row is its word (kernels.hip kMixed = -1)
-      const int32_t x = uL != -1 ? uL : lab[(int64_t)vL * 64 + lane];
+      const int32_t x = lab[(int64_t)vL * 64 + lane];
       int n = 0;
       while (mm) {
         const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
@@ -135,14 +145,27 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
     }
     unsigned long long off = 0;
     if (lane < P.np && cq) off = atomicAdd(&scnt[lane], cq);
-    for (uint64_t b = todo; b; b &= b - 1) {
+    if (uni) {  // uniform records first, in lane order per peer
+      const unsigned long long pos = (unsigned long long)__shfl((long long)off, q) + __popcll(mypeer & lanemask_below(lane));
+      if (pos < (unsigned long long)P.cap[q]) {
+        XRec r;
+        r.e = (int32_t)(e - P.xoff[q]);
+        r.val = (int32_t)((uint32_t)u | 0x80000000u);  // sign bit: sender uniform
+        r.mask = m;
+        sbuf[P.base[q] + pos] = r;
+      }
+    }
+    for (int p = 0; p < P.np; p++) {
+      const uint64_t b = __ballot(uni && q == p);
+      if (lane == p) off += (unsigned long long)__popcll(b);
+    }
+    for (uint64_t b = mixed; b; b &= b - 1) {
       const int L = __builtin_ctzll(b);
       const int32_t vL = __builtin_amdgcn_readlane(v, L);
       const int qL = __builtin_amdgcn_readlane(q, L);
       const int32_t eL = (int32_t)(c * 64 + L - P.xoff[qL]);
       uint64_t mm = rl64(m, L);
-      const int32_t uL = uw ? uw_label(uw[vL]) : -1;
-      const int32_t x = uL != -1 ? uL : lab[(int64_t)vL * 64 + lane];
+      const int32_t x = lab[(int64_t)vL * 64 + lane];
       while (mm) {
         const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
         const uint64_t same = __ballot(((mm >> lane) & 1) && x == val);
@@ -151,7 +174,7 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
         if (lane == 0 && pos < (unsigned long long)P.cap[qL]) {
           XRec r;
           r.e = eL;
-          r.val = uL != -1 ? (int32_t)((uint32_t)val | 0x80000000u) : val;  // sign bit: sender uniform
+          r.val = val;
           r.mask = same;
           sbuf[P.base[qL] + pos] = r;
         }
@@ -189,38 +212,49 @@ __global__ __launch_bounds__(256) void k_xclear(XPeers P, const XRec* __restrict
 }
 
 // Records into ghost rows: the record's label in its views, and its views into the ghost's
-// change word (a ghost's records arrive together; the OR collects them).  A wave takes four
-// records, 16 lanes each covering the 64 views in 4 passes.  A record whose sender's row is
-// uniform (sign bit of val; it is then the ghost's only record of the step) sets the ghost's
-// uniform word instead of its row: readers only gather a ghost in the views its change word
-// holds, which are the record's.  Other records mark the ghost mixed (kernels.hip kMixed).
+// change word (a ghost's records arrive together; the OR collects them).  A record whose sender's
+// row is uniform (sign bit of val; it is then the ghost's only record of the step) sets the
+// ghost's uniform word instead of its row, lane = record: readers only gather a ghost in the views
+// its change word holds, which are the record's.  Other records mark the ghost mixed (kernels.hip
+// kMixed), one per wave iteration with lane = view.  (Four records per wave, 16 lanes each, with
+// two atomics per record, made the unpack the largest partitioned kernel.)
 __global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __restrict__ rbuf,
                                                      const int32_t* __restrict__ xrv, int32_t* __restrict__ lab,
                                                      uint64_t* __restrict__ chg, int32_t* __restrict__ uw,
                                                      uint64_t* __restrict__ cb) {
   const int64_t n = P.pre[P.np];
-  const int lane = lane_of(), sub = lane >> 4, l16 = lane & 15;
+  const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t i0 = wave * 4; i0 < n; i0 += nwaves * 4) {
-    const int64_t i = i0 + sub;
-    if (i >= n) continue;
-    const int q = peer_of(P, i);
-    const XRec r = rbuf[P.base[q] + i - P.pre[q]];
-    const int32_t g = xrv[P.xoff[q] + r.e];
-    const bool uni = r.val < 0;
-    const int32_t val = r.val & 0x7fffffff;
-    if (!uni || !uw) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int j = k * 16 + l16;
-        if ((r.mask >> j) & 1) lab[(int64_t)g * 64 + j] = val;
-      }
+  for (int64_t i0 = wave * 64; i0 < n; i0 += nwaves * 64) {
+    // lane = record: a uniform record is its ghost's only record of the step, so its word and
+    // change word are plain stores; mixed records (rows, OR-ed change words) one by one below
+    const int64_t i = i0 + lane;
+    const bool ok = i < n;
+    XRec r{0, 0, 0};
+    int32_t g = 0;
+    if (ok) {
+      const int q = peer_of(P, i);
+      r = rbuf[P.base[q] + i - P.pre[q]];
+      g = xrv[P.xoff[q] + r.e];
     }
-    if (l16 == 0) {
-      if (uw) uw[g] = uni ? uw_word(val, true) : -1;  // the ghost changed in this step (kChgFlag)
-      atomicOr((unsigned long long*)&chg[g], (unsigned long long)r.mask);
-      if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // the ghost changed (ChgBits)
+    const bool uni = ok && uw && r.val < 0;
+    if (uni) {
+      uw[g] = uw_word(r.val & 0x7fffffff, true);  // the ghost changed in this step (kChgFlag)
+      chg[g] = r.mask;
+      if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // (ChgBits)
+    }
+    for (uint64_t b = __ballot(ok && !uni); b; b &= b - 1) {
+      const int L = __builtin_ctzll(b);
+      const int32_t gL = __builtin_amdgcn_readlane(g, L);
+      const int32_t val = __builtin_amdgcn_readlane(r.val, L) & 0x7fffffff;
+      const uint64_t mL = rl64(r.mask, L);
+      if ((mL >> lane) & 1) lab[(int64_t)gL * 64 + lane] = val;
+      if (lane == 0) {
+        if (uw) uw[gL] = kMixed;
+        atomicOr((unsigned long long*)&chg[gL], (unsigned long long)mL);
+        if (cb) atomicOr((unsigned long long*)&cb[gL >> 6], 1ull << (gL & 63));
+      }
     }
   }
 }
@@ -501,7 +535,7 @@ void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32
 }
 void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
                         uint64_t* chg, int32_t* uw, uint64_t* cb) {
-  if (P.pre[P.np] > 0) k_xunpack_rec<<<xgrid(P.pre[P.np], 16), 256, 0, s>>>(P, rbuf, xrv, lab, chg, uw, cb);
+  if (P.pre[P.np] > 0) k_xunpack_rec<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, xrv, lab, chg, uw, cb);
 }
 void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
                   const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next, int64_t tcut,
