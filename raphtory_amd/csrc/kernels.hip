@@ -1260,8 +1260,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
 #pragma unroll
         for (int i = 0; i < CH; i++) fb |= (v0 + i < nv && vm[v0 + i] != 0) ? (1u << i) : 0u;
       } else {
-        const uint64_t f = CH == 8 ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
-                                   : *reinterpret_cast<const uint32_t*>(act_cur + v0);
+        const uint64_t f = CH == 8   ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
+                           : CH == 4 ? *reinterpret_cast<const uint32_t*>(act_cur + v0)
+                                     : *reinterpret_cast<const uint16_t*>(act_cur + v0);
 #pragma unroll
         for (int i = 0; i < CH; i++) fb |= ((f >> (8 * i)) & 0xffu) ? (1u << i) : 0u;
       }
@@ -2402,6 +2403,7 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
 int g_slot_labels = 1;  // K2 streams the neighbours' labels (DevGraph.ts_g; RGPU_TSG)
+int g_step_ch = 4;      // vertices per superstep chunk (RGPU_STEP_CH: 2 or 4; A/B)
 int g_deal_slots = 16;  // deal_group maxima of K2 / the superstep kernel (RGPU_DEAL_SLOTS / _STEP;
                         // C4 A/B, profiles/r03/c4_ab_deal.log: K2 16 ≈ 64 < 1, step 1 ≈ 4 << 64)
 int g_deal_step = 4;
@@ -2494,6 +2496,8 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
     cb.next, cb.clear, cb.words, ccount, dense_div, g_deal_step
   // work != null (profile runs): the counting instantiation; the timed runs use the lean one
   if (work) k_cc_step2<4, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else if (g_step_ch == 2) k_cc_step2<2, false, 1, false><<<grid_for(g.nv, 8, cap), 256, 0, s>>>(RGPU_STEP_ARGS);
+  else if (g_step_ch == 5) k_cc_step2<4, false, 5, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
   else k_cc_step2<4, false, 1, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
 #undef RGPU_STEP_ARGS
 }

@@ -145,8 +145,10 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
     }
     unsigned long long off = 0;
     if (lane < P.np && cq) off = atomicAdd(&scnt[lane], cq);
+    // (the shuffle runs with every lane active: a lane reading an inactive lane's register gets 0)
+    const unsigned long long qoff = (unsigned long long)__shfl((long long)off, q);
     if (uni) {  // uniform records first, in lane order per peer
-      const unsigned long long pos = (unsigned long long)__shfl((long long)off, q) + __popcll(mypeer & lanemask_below(lane));
+      const unsigned long long pos = qoff + __popcll(mypeer & lanemask_below(lane));
       if (pos < (unsigned long long)P.cap[q]) {
         XRec r;
         r.e = (int32_t)(e - P.xoff[q]);
@@ -279,7 +281,7 @@ __global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict_
                                                const int32_t* __restrict__ ts_nb, const int64_t* __restrict__ ts_t,
                                                int64_t tcut, BatchParams ebp, int iem,
                                                const int32_t* __restrict__ ccount, int dense_div, int step,
-                                               int64_t n_own) {
+                                               int64_t n_own, int64_t nv_all) {
   if (dense_after(ccount, step + 1, n_own, dense_div)) return;  // step r dense: r+1 visits every member
   __shared__ HopLDS L;
   if (TS && iem) hop_lds_init(L, ebp, ebp.thr_e);
@@ -292,7 +294,11 @@ __global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict_
     const int64_t k = i - P.pre[q];
     const int32_t e0 = rbuf[P.base[q] + k].e;
     if (k > 0 && rbuf[P.base[q] + k - 1].e == e0) continue;  // not the ghost's first record
+    // (bounds guards: a record outside the plan is a bug upstream — the parity tests see its
+    // missing marks — and must not become a fault that takes the device down)
+    if (e0 < 0 || e0 >= P.xoff[q + 1] - P.xoff[q]) continue;
     const int32_t g = xrv[P.xoff[q] + e0];
+    if (g < 0 || g >= nv_all) continue;
     if (hv_of && hv_of[g] >= 0) continue;
     const uint64_t ch = chg[g] & vm[g];
     if (TS) {
@@ -547,7 +553,7 @@ void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_
   kern<<<xgrid(P.pre[P.np], 4), 256, 0, s>>>(P, rbuf, xrv, chg, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
                                              g.n_seg > 0 ? g.hv_of : nullptr, act_next, g.adj_off, g.ts_e, g.ts_nb,
                                              g.ts_t, tcut, ebp ? *ebp : bp0, ebp ? 1 : 0, ccount, dense_div, step,
-                                             g.n_own);
+                                             g.n_own, g.nv);
 }
 void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,
