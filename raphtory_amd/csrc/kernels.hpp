@@ -289,10 +289,20 @@ void launch_xvm_pack(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t
                      const uint64_t* vm, int64_t vstride, uint64_t* out);
 void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
                        int planes, const uint64_t* in, uint64_t* vm, int64_t vstride);
-void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t* xv, const int32_t* xq,
-                      const uint8_t* act, const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab,
-                      const int32_t* uw, XRec* sbuf, unsigned long long* scnt, const int32_t* ccount = nullptr,
-                      int dense_div = 0, int step = 0, int64_t n_own = 0);
+// The send plan by boundary vertex (built from the (peer, vertex) lists, build_xsend): the owned
+// boundary vertices ascending, the peers holding each as a ghost (bit mask), and its entry index in
+// each of those peers' lists.  The record pack reads a vertex's words once for all its peers.
+struct XSend {
+  int64_t nb = 0;
+  const int32_t* v = nullptr;    // [nb] owned rank
+  const int32_t* e = nullptr;    // [nb][kMaxParts] entry index in the list for peer q
+  const uint32_t* pm = nullptr;  // [nb] peers
+};
+XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
+                  std::vector<void*>& T, std::vector<void*>& L);
+void launch_xpack_rec(hipStream_t s, const XPeers& P, const XSend& X, const uint8_t* act, const uint64_t* chg_now,
+                      const uint64_t* vadj, const int32_t* lab, const int32_t* uw, XRec* sbuf, unsigned long long* scnt,
+                      const int32_t* ccount = nullptr, int dense_div = 0, int step = 0, int64_t n_own = 0);
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa);
 void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg,
                    int32_t* uw = nullptr);

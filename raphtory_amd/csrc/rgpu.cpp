@@ -144,6 +144,7 @@ struct Part {
   int32_t *xs_v = nullptr, *xs_q = nullptr, *xr_v = nullptr, *xr_q = nullptr;
   int64_t *xs_off_d = nullptr, *xr_off_d = nullptr;
   OwnIdx own;                                 // owned id -> owned rank (label owner counting)
+  XSend xsend;                                // the send plan by boundary vertex (record pack)
   double *sbuf_f = nullptr, *rbuf_f = nullptr;  // PR contribution rows
   bool pr_ready = false;
   XSlot xs[4];                                // per batch slot (kMaxSlots)
@@ -1321,7 +1322,7 @@ void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
     return;
   }
   const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
-  timed_launch(c, si, KID_XPACK, 0.0, [&] { launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
+  timed_launch(c, si, KID_XPACK, 0.0, [&] { launch_xpack_rec(s.stream, L, X.xsend, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
                    s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
                    c->pk.n_own); });
   launch_xcounts(s.stream, P, c->part, xs.scnt, s.stepcnt + r, xs.xab);
@@ -1352,7 +1353,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (over) {  // the counts were exact; the records did not all fit: pack again, larger
     grow_regions(&xs.sbuf, xs.scap, sent, P, s.stream);
     const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
-    timed_launch(c, si, KID_XPACK, 0.0, [&] { launch_xpack_rec(s.stream, L, X.nxs, X.xs_v, X.xs_q, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
+    timed_launch(c, si, KID_XPACK, 0.0, [&] { launch_xpack_rec(s.stream, L, X.xsend, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
                      s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
                    c->pk.n_own); });
     HIPCHK(hipMemsetAsync(xs.scnt, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
@@ -1925,6 +1926,20 @@ void build_tslots(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L) {
   }
 }
 
+// the send plan by boundary vertex (xchg.hip build_xsend), from the (peer, vertex) lists
+XSend build_send_plan(int64_t n_own, const Part& X, std::vector<void*>& L) {
+  std::vector<void*> T;
+  XSend xs;
+  try {
+    xs = build_xsend(nullptr, n_own, X.nxs, X.xs_v, X.xs_q, X.xs_off_d, T, L);
+  } catch (const std::runtime_error& e) {
+    for (void* p : T) (void)hipFree(p);
+    throw HipFail{e.what()};
+  }
+  for (void* p : T) (void)hipFree(p);
+  return xs;
+}
+
 // the neighbours' labels (grank) in time-ordered slot order, once grank is known
 void build_tslot_labels(DevGraph& g, std::vector<void*>& L) {
   if (!g.ts_nb || !g.grank) return;
@@ -2232,6 +2247,7 @@ void seal_delta(rgpu_ctx* c) {
       X.xr_q = PM.xr_q;
       X.xs_off_d = PM.xs_off_d;
       X.xr_off_d = PM.xr_off_d;
+      X.xsend = build_send_plan(g.n_own, X, L);
       X.own.vid = PM.own_vid;
       X.own.pos = nullptr;
       X.own.boff = PM.own_boff;
@@ -2378,6 +2394,7 @@ int rgpu_seal(rgpu_ctx* c) {
       X.xr_q = dupload(L, P.xr_q);
       X.xs_off_d = dupload(L, P.xs_off);
       X.xr_off_d = dupload(L, P.xr_off);
+      X.xsend = build_send_plan(P.n_own, X, L);
       {  // owned ids ascending (index = the count-table row of the label): bucket b = id >> shift,
          // about one id per bucket
         std::vector<int64_t> ids((size_t)P.n_own);

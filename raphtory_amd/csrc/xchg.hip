@@ -20,6 +20,11 @@
 #include <cstdint>
 #include <cstring>
 
+#include <hipcub/device/device_scan.hpp>
+
+#include <stdexcept>
+#include <vector>
+
 #include "kernels.hpp"
 #include "window_bits.hpp"
 
@@ -96,8 +101,82 @@ __global__ __launch_bounds__(256) void k_xvm_unpack(int64_t nx, const int32_t* _
 // views holding it.  A wave takes 64 entries: it counts the records per peer (lane q), reserves
 // them with one atomicAdd per (wave, peer), then writes them; scnt counts past the capacity
 // too, so the host sees an overflow and repeats the pack into a larger buffer.
-__global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const int32_t* __restrict__ xv,
-                                                   const int32_t* __restrict__ xq, const uint8_t* __restrict__ act,
+// A wave takes a run of kPackRun chunks of 64 boundary vertices: it counts its records per peer over
+// the whole run, reserves them with one atomicAdd per peer, then writes them.  (Runs of 16 chunks,
+// to cut the reservations on the 8 counters, measured 4.7x slower at P = 8: the pack is bound by
+// each chunk's chain of dependent loads, and fewer, longer waves hide less of it.)
+constexpr int kPackRun = 1;
+__device__ __forceinline__ void pack_chunk(bool write, const XPeers& P, const XSend& X, int64_t c,
+                                           const uint8_t* __restrict__ act, const uint64_t* __restrict__ chg_now,
+                                           const uint64_t* __restrict__ vadj, const int32_t* __restrict__ lab,
+                                           const int32_t* __restrict__ uw, XRec* __restrict__ sbuf,
+                                           unsigned long long& cq, unsigned long long& off, int lane) {
+  // lane = boundary vertex (ascending owned rank): its words are read once for all its peers
+  const int64_t b = c * 64 + lane;
+  const bool ok = b < X.nb;
+  const int32_t v = ok ? X.v[b] : 0;
+  const uint32_t pm = ok ? X.pm[b] : 0u;
+  uint64_t m = 0;
+  if (ok && (act == nullptr || act[v])) m = chg_now[v] & vadj[v];
+  if (!__ballot(m != 0)) return;
+  // A uniform sender (its word is its row) has one label: one record per peer, written by its own
+  // lane.  Only mixed senders walk their distinct labels one by one (lane = view).
+  const int32_t u = (m != 0 && uw) ? uw_label(uw[v]) : kMixed;
+  const bool uni = m != 0 && u != kMixed;
+  const uint64_t mixed = __ballot(m != 0 && !uni);
+  for (int p = 0; p < P.np; p++) {  // uniform records, in lane order per peer
+    const uint64_t bp = __ballot(uni && ((pm >> p) & 1));
+    if (!bp) continue;
+    if (write) {
+      const unsigned long long base = __builtin_amdgcn_readlane((uint32_t)off, p) |
+                                      ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(off >> 32), p) << 32);
+      if ((bp >> lane) & 1) {
+        const unsigned long long pos = base + __popcll(bp & lanemask_below(lane));
+        if (pos < (unsigned long long)P.cap[p]) {
+          XRec r;
+          r.e = X.e[b * kMaxParts + p];
+          r.val = (int32_t)((uint32_t)u | 0x80000000u);  // sign bit: sender uniform
+          r.mask = m;
+          sbuf[P.base[p] + pos] = r;
+        }
+      }
+      if (lane == p) off += (unsigned long long)__popcll(bp);
+    } else if (lane == p) {
+      cq += (unsigned long long)__popcll(bp);
+    }
+  }
+  for (uint64_t bb = mixed; bb; bb &= bb - 1) {  // mixed senders: per distinct label, per peer
+    const int L = __builtin_ctzll(bb);
+    const int32_t vL = __builtin_amdgcn_readlane(v, L);
+    const uint32_t pmL = __builtin_amdgcn_readlane(pm, L);
+    const int64_t bL = c * 64 + L;
+    uint64_t mm = rl64(m, L);
+    const int32_t x = lab[(int64_t)vL * 64 + lane];
+    while (mm) {
+      const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
+      const uint64_t same = __ballot(((mm >> lane) & 1) && x == val);
+      if (write) {
+        for (uint32_t pp = pmL; pp; pp &= pp - 1) {
+          const int p = __builtin_ctz(pp);
+          const unsigned long long pos = __builtin_amdgcn_readlane((uint32_t)off, p) |
+                                         ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(off >> 32), p) << 32);
+          if (lane == 0 && pos < (unsigned long long)P.cap[p]) {
+            XRec r;
+            r.e = X.e[bL * kMaxParts + p];
+            r.val = val;
+            r.mask = same;
+            sbuf[P.base[p] + pos] = r;
+          }
+          if (lane == p) off++;
+        }
+      } else if (lane < 32 && ((pmL >> lane) & 1)) {
+        cq++;
+      }
+      mm &= ~same;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, XSend X, const uint8_t* __restrict__ act,
                                                    const uint64_t* __restrict__ chg_now,
                                                    const uint64_t* __restrict__ vadj,
                                                    const int32_t* __restrict__ lab,
@@ -109,81 +188,37 @@ __global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, int64_t nx, const i
   if (dense_after(ccount, step, n_own, dense_div)) act = nullptr;  // the step visited every member
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t c = wave; c * 64 < nx; c += nwaves) {
-    const int64_t e = c * 64 + lane;
-    const bool ok = e < nx;
-    const int32_t v = ok ? xv[e] : 0;
-    const int q = ok ? xq[e] : 0;
-    uint64_t m = 0;
-    if (ok && (act == nullptr || act[v])) m = chg_now[v] & vadj[v];
-    if (!__ballot(m != 0)) continue;
-    // A uniform sender (its word is its row) has one label: one record, written by its own lane.
-    // Only mixed senders walk their distinct labels one by one (lane = view).
-    const int32_t u = (m != 0 && uw) ? uw_label(uw[v]) : kMixed;
-    const bool uni = m != 0 && u != kMixed;
-    const uint64_t mixed = __ballot(m != 0 && !uni);
-    unsigned long long cq = 0;  // lane p: records of this wave for peer p
-    uint64_t mypeer = 0;        // the uniform lanes sending to this lane's peer
-    for (int p = 0; p < P.np; p++) {
-      const uint64_t b = __ballot(uni && q == p);
-      if (lane == p) cq = (unsigned long long)__popcll(b);
-      if (q == p) mypeer = b;
-    }
-    for (uint64_t b = mixed; b; b &= b - 1) {
-      const int L = __builtin_ctzll(b);
-      const int32_t vL = __builtin_amdgcn_readlane(v, L);
-      const int qL = __builtin_amdgcn_readlane(q, L);
-      uint64_t mm = rl64(m, L);
-      const int32_t x = lab[(int64_t)vL * 64 + lane];
-      int n = 0;
-      while (mm) {
-        const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
-        mm &= ~__ballot(((mm >> lane) & 1) && x == val);
-        n++;
-      }
-      if (lane == qL) cq += (unsigned long long)n;
-    }
-    unsigned long long off = 0;
+  const int64_t nchunks = (X.nb + 63) / 64;
+  for (int64_t c0 = wave * kPackRun; c0 < nchunks; c0 += nwaves * kPackRun) {
+    const int64_t c1 = c0 + kPackRun < nchunks ? c0 + kPackRun : nchunks;
+    unsigned long long cq = 0, off = 0;  // lane p: this run's records for peer p, then its next position
+    for (int64_t c = c0; c < c1; c++) pack_chunk(false, P, X, c, act, chg_now, vadj, lab, uw, sbuf, cq, off, lane);
+    if (!__ballot(cq != 0)) continue;
     if (lane < P.np && cq) off = atomicAdd(&scnt[lane], cq);
-    // (the shuffle runs with every lane active: a lane reading an inactive lane's register gets 0)
-    const unsigned long long qoff = (unsigned long long)__shfl((long long)off, q);
-    if (uni) {  // uniform records first, in lane order per peer
-      const unsigned long long pos = qoff + __popcll(mypeer & lanemask_below(lane));
-      if (pos < (unsigned long long)P.cap[q]) {
-        XRec r;
-        r.e = (int32_t)(e - P.xoff[q]);
-        r.val = (int32_t)((uint32_t)u | 0x80000000u);  // sign bit: sender uniform
-        r.mask = m;
-        sbuf[P.base[q] + pos] = r;
-      }
-    }
-    for (int p = 0; p < P.np; p++) {
-      const uint64_t b = __ballot(uni && q == p);
-      if (lane == p) off += (unsigned long long)__popcll(b);
-    }
-    for (uint64_t b = mixed; b; b &= b - 1) {
-      const int L = __builtin_ctzll(b);
-      const int32_t vL = __builtin_amdgcn_readlane(v, L);
-      const int qL = __builtin_amdgcn_readlane(q, L);
-      const int32_t eL = (int32_t)(c * 64 + L - P.xoff[qL]);
-      uint64_t mm = rl64(m, L);
-      const int32_t x = lab[(int64_t)vL * 64 + lane];
-      while (mm) {
-        const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
-        const uint64_t same = __ballot(((mm >> lane) & 1) && x == val);
-        const unsigned long long pos = __builtin_amdgcn_readlane((uint32_t)off, qL) |
-                                       ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(off >> 32), qL) << 32);
-        if (lane == 0 && pos < (unsigned long long)P.cap[qL]) {
-          XRec r;
-          r.e = eL;
-          r.val = val;
-          r.mask = same;
-          sbuf[P.base[qL] + pos] = r;
-        }
-        if (lane == qL) off++;
-        mm &= ~same;
-      }
-    }
+    for (int64_t c = c0; c < c1; c++) pack_chunk(true, P, X, c, act, chg_now, vadj, lab, uw, sbuf, cq, off, lane);
+  }
+}
+
+// ------------------------------------------------------------------ send index (per boundary vertex)
+__global__ __launch_bounds__(256) void k_xsend_flag(int64_t nx, const int32_t* __restrict__ xv,
+                                                    int32_t* __restrict__ flag) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nx; e += (int64_t)gridDim.x * blockDim.x)
+    flag[xv[e]] = 1;  // (idempotent plain stores)
+}
+__global__ __launch_bounds__(256) void k_xsend_list(int64_t n_own, const int32_t* __restrict__ flag,
+                                                    const int32_t* __restrict__ pos, int32_t* __restrict__ xb) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n_own; v += (int64_t)gridDim.x * blockDim.x)
+    if (flag[v]) xb[pos[v]] = (int32_t)v;
+}
+__global__ __launch_bounds__(256) void k_xsend_entries(int64_t nx, const int32_t* __restrict__ xv,
+                                                       const int32_t* __restrict__ xq, const int64_t* __restrict__ xoff,
+                                                       const int32_t* __restrict__ pos, int32_t* __restrict__ xe,
+                                                       uint32_t* __restrict__ pm) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nx; e += (int64_t)gridDim.x * blockDim.x) {
+    const int q = xq[e];
+    const int64_t b = pos[xv[e]];
+    xe[b * kMaxParts + q] = (int32_t)(e - xoff[q]);
+    atomicOr(&pm[b], 1u << q);
   }
 }
 
@@ -525,13 +560,49 @@ void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32
                        int planes, const uint64_t* in, uint64_t* vm, int64_t vstride) {
   if (nx > 0) k_xvm_unpack<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, xq, xoff, planes, in, vm, vstride);
 }
-void launch_xpack_rec(hipStream_t s, const XPeers& P, int64_t nx, const int32_t* xv, const int32_t* xq,
-                      const uint8_t* act, const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab,
-                      const int32_t* uw, XRec* sbuf, unsigned long long* scnt, const int32_t* ccount, int dense_div,
-                      int step, int64_t n_own) {
-  if (nx > 0)
-    k_xpack_rec<<<xgrid(nx, 4 * 64, 4096), 256, 0, s>>>(P, nx, xv, xq, act, chg_now, vadj, lab, uw, sbuf, scnt,
-                                                         ccount, dense_div, step, n_own);
+void launch_xpack_rec(hipStream_t s, const XPeers& P, const XSend& X, const uint8_t* act, const uint64_t* chg_now,
+                      const uint64_t* vadj, const int32_t* lab, const int32_t* uw, XRec* sbuf, unsigned long long* scnt,
+                      const int32_t* ccount, int dense_div, int step, int64_t n_own) {
+  if (X.nb > 0)
+    k_xpack_rec<<<xgrid(X.nb, 4 * 64 * kPackRun, 4096), 256, 0, s>>>(P, X, act, chg_now, vadj, lab, uw, sbuf, scnt, ccount,
+                                                           dense_div, step, n_own);
+}
+XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
+                  std::vector<void*>& T, std::vector<void*>& L) {
+  auto alloc = [&](std::vector<void*>& list, size_t bytes) {
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) throw std::runtime_error("build_xsend: hipMalloc");
+    list.push_back(p);
+    return p;
+  };
+  XSend X;
+  if (nx <= 0 || n_own <= 0) return X;
+  int32_t* flag = (int32_t*)alloc(T, sizeof(int32_t) * (n_own + 1));
+  int32_t* pos = (int32_t*)alloc(T, sizeof(int32_t) * (n_own + 1));
+  if (hipMemsetAsync(flag, 0, sizeof(int32_t) * (n_own + 1), s) != hipSuccess) throw std::runtime_error("build_xsend");
+  k_xsend_flag<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, flag);
+  size_t tb = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, pos, (int)(n_own + 1), s);
+  void* tmp = alloc(T, tb);
+  if (hipcub::DeviceScan::ExclusiveSum(tmp, tb, flag, pos, (int)(n_own + 1), s) != hipSuccess)
+    throw std::runtime_error("build_xsend: scan");
+  int32_t nb = 0;
+  if (hipMemcpyAsync(&nb, pos + n_own, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    throw std::runtime_error("build_xsend: count");
+  X.nb = nb;
+  int32_t* xb = (int32_t*)alloc(L, sizeof(int32_t) * nb);
+  int32_t* xe = (int32_t*)alloc(L, sizeof(int32_t) * nb * kMaxParts);
+  uint32_t* pm = (uint32_t*)alloc(L, sizeof(uint32_t) * nb);
+  if (hipMemsetAsync(pm, 0, sizeof(uint32_t) * nb, s) != hipSuccess) throw std::runtime_error("build_xsend");
+  k_xsend_list<<<xgrid(n_own, 256), 256, 0, s>>>(n_own, flag, pos, xb);
+  k_xsend_entries<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, xq, xoff, pos, xe, pm);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    throw std::runtime_error("build_xsend: kernels");
+  X.v = xb;
+  X.e = xe;
+  X.pm = pm;
+  return X;
 }
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa) {
   k_xcounts<<<1, 64, 0, s>>>(np, me, scnt, stepflag, xa);
