@@ -2403,7 +2403,7 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 // ---------------------------------------------------------------- launchers
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
 int g_slot_labels = 1;  // K2 streams the neighbours' labels (DevGraph.ts_g; RGPU_TSG)
-int g_step_ch = 4;      // vertices per superstep chunk (RGPU_STEP_CH: 2 or 4; A/B)
+int g_step_ch = 2;      // vertices per superstep chunk (RGPU_STEP_CH: 2 or 4)
 int g_deal_slots = 16;  // deal_group maxima of K2 / the superstep kernel (RGPU_DEAL_SLOTS / _STEP;
                         // C4 A/B, profiles/r03/c4_ab_deal.log: K2 16 ≈ 64 < 1, step 1 ≈ 4 << 64)
 int g_deal_step = 4;
@@ -2495,10 +2495,17 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
     cb.next, cb.clear, cb.words, ccount, dense_div, g_deal_step
   // work != null (profile runs): the counting instantiation; the timed runs use the lean one
-  if (work) k_cc_step2<4, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else if (g_step_ch == 2) k_cc_step2<2, false, 1, false><<<grid_for(g.nv, 8, cap), 256, 0, s>>>(RGPU_STEP_ARGS);
-  else if (g_step_ch == 5) k_cc_step2<4, false, 5, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else k_cc_step2<4, false, 1, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  // 2-vertex chunks (default): 73 VGPRs, 6 waves/SIMD against 97 and 4 for 4-vertex chunks; same-box
+  // A/B (tools/c4_ab.py, profiles/r03/c4_ab_step_ch.log): C4 369 -> 345 ms, C2 135 -> 120 ms.
+  // RGPU_STEP_CH=4 keeps the 4-vertex chunks.
+  const unsigned grid2 = grid_for(g.nv, 8, cap);
+  if (g_step_ch == 4) {
+    if (work) k_cc_step2<4, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+    else k_cc_step2<4, false, 1, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
+  } else {
+    if (work) k_cc_step2<2, false, 1, true><<<grid2, 256, 0, s>>>(RGPU_STEP_ARGS);
+    else k_cc_step2<2, false, 1, false><<<grid2, 256, 0, s>>>(RGPU_STEP_ARGS);
+  }
 #undef RGPU_STEP_ARGS
 }
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,

@@ -85,6 +85,27 @@ def test_tail_chains_vs_oracle(mode):
     g.close()
 
 
+@pytest.mark.parametrize("ch", ["2", "4"])
+def test_superstep_chunk_sizes_vs_oracle(ch, monkeypatch):
+    """The superstep kernel with 2-vertex (default) and 4-vertex chunks (RGPU_STEP_CH, read per
+    run) against the oracle: chains up to past the cap, and a hub-free uniform stream."""
+    monkeypatch.setenv("RGPU_STEP_CH", ch)
+    st = chains_stream([1, 4, 31, 64, 98, 99, 100, 101, 140], seed=11)
+    o = Oracle.from_stream(st)
+    g = graph_env(st, {})
+    hops = range_hops(T0_README + 10 * DAY, T0_README + 40 * DAY, 3 * DAY)
+    for cap in (100, 37):
+        g.run("cc", hops, [YEAR, MONTH, WEEK], max_steps=cap, retain=True)
+        for h, t in enumerate(hops.tolist()):
+            res, steps = o.cc(t, [YEAR, MONTH, WEEK], max_steps=cap, mode=1)
+            for w in range(3):
+                assert g.cc_summary(h, w).supersteps == steps, (ch, cap, t, w)
+                ids, lab = res[w]
+                gids, glab = g.cc_vertex_labels(h, w)
+                assert np.array_equal(gids, ids) and np.array_equal(glab, lab), (ch, cap, t, w)
+    g.close()
+
+
 def test_tail_modes_agree_on_c2_slice():
     """C2 stream, 1,200 hourly hops: every mode gives identical summaries for all 6,000 views
     (superstep counts included: they are per hop, whatever batches held the views), and identical
