@@ -1547,7 +1547,7 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       const int32_t* __restrict__ uw_cur,
                                                       const uint64_t* __restrict__ cb_prev,
                                                       const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
-                                                      unsigned long long* __restrict__ work) {
+                                                      unsigned long long* __restrict__ work, int pipe) {
   if (stepflag[step - 1] == 0) return;
   const bool visit_all = dense_rule(ccount, step - 1, nv_all, dense_div);  // step-1 wrote no flags
   const int lane = lane_id();
@@ -1562,6 +1562,41 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
     if (work) { w_seg++; w_slots += (unsigned long long)n; }
     const int64_t base = seg_lo[sg];
     int32_t best = INT32_MAX;  // lane = view
+    if (pipe && cb_prev && uw_cur && n <= kSegSlots) {
+      // Loads first over the segment's (at most 8) chunks: neighbours, their changed-bit words,
+      // then the hot slots' masks and words, then the folds — three dependent trips per segment
+      // instead of three per chunk.
+      constexpr int NC = kSegSlots / 64;
+      int32_t q[NC];
+      uint64_t cbw[NC], m[NC];
+      int32_t u[NC];
+#pragma unroll
+      for (int k = 0; k < NC; k++) q[k] = k * 64 < n ? snbr[base + (k * 64 + lane < n ? k * 64 + lane : k * 64)] : 0;
+#pragma unroll
+      for (int k = 0; k < NC; k++) cbw[k] = k * 64 < n ? cb_prev[q[k] >> 6] : 0;
+#pragma unroll
+      for (int k = 0; k < NC; k++) {
+        const bool hot = k * 64 + lane < n && ((cbw[k] >> (q[k] & 63)) & 1);
+        m[k] = hot ? smask[base + k * 64 + lane] : 0;
+        u[k] = hot ? uw_label(uw_cur[q[k]]) : kMixed;
+      }
+#pragma unroll
+      for (int k = 0; k < NC; k++) {
+        if (k * 64 >= n) break;
+        const uint64_t a = (m[k] && u[k] == kMixed) ? (m[k] & chg_prev[q[k]]) : m[k];
+        if (work) {
+          w_hot += __popcll(__ballot(a != 0));
+          w_mixed += __popcll(__ballot(a != 0 && u[k] == kMixed));
+          unsigned long long g = u[k] == kMixed ? (unsigned long long)__popcll(a) : 0ull;
+          for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o);
+          w_lanes += g;
+        }
+        best = gather_min<false>(u[k] == kMixed ? a : 0, q[k], best, lab_cur, lane);
+        best = fold_uniform(__ballot(u[k] != kMixed), a, u[k], best, lane);
+      }
+      if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
+      continue;
+    }
     for (int32_t c = 0; c < n; c += 64) {
       const int32_t jj = c + lane;
       const int64_t idx = base + (jj < n ? jj : c);
@@ -2404,6 +2439,7 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
 int g_slot_labels = 1;  // K2 streams the neighbours' labels (DevGraph.ts_g; RGPU_TSG)
 int g_step_ch = 2;      // vertices per superstep chunk (RGPU_STEP_CH: 2 or 4)
+int g_hub_pipe = 1;     // hub gather loads a segment's chunks first (RGPU_HUB_PIPE)
 int g_deal_slots = 16;  // deal_group maxima of K2 / the superstep kernel (RGPU_DEAL_SLOTS / _STEP;
                         // C4 A/B, profiles/r03/c4_ab_deal.log: K2 16 ≈ 64 < 1, step 1 ≈ 4 << 64)
 int g_deal_step = 4;
@@ -2528,7 +2564,7 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
   k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
                                                              hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
-                                                             g.n_own, work);
+                                                             g.n_own, work, g_hub_pipe);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,

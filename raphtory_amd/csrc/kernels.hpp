@@ -170,6 +170,7 @@ extern int g_deal_slots, g_deal_step;  // deal_group maxima (kernels.hip; RGPU_D
 extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
 extern int g_slot_labels;  // K2 reads DevGraph.ts_g (RGPU_TSG)
 extern int g_step_ch;      // superstep chunk size (RGPU_STEP_CH)
+extern int g_hub_pipe;     // loads-first hub gather (RGPU_HUB_PIPE)
 extern int g_tail_step, g_tail_grid;  // supersteps >= tail_step use at most tail_grid blocks
 // uniform label words (kernels.hip, kMixed): rows of the uniform vertices written into lab
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab);

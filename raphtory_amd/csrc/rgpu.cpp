@@ -2528,6 +2528,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
   g_slot_labels = env_int("RGPU_TSG", 1);
   g_step_ch = env_int("RGPU_STEP_CH", 2) == 4 ? 4 : 2;  // superstep chunk: 2 (default) or 4 vertices
+  g_hub_pipe = env_int("RGPU_HUB_PIPE", 1);
   {  // powers of two up to 64
     auto pow2 = [](int x) { int g = 1; while (g < x && g < 64) g <<= 1; return g; };
     g_deal_slots = pow2(env_int("RGPU_DEAL_SLOTS", 16));
