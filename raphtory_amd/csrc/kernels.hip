@@ -507,8 +507,10 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   int32_t* __restrict__ uw0, int32_t* __restrict__ uw1,
                                                   uint64_t* __restrict__ cb1, int ends,
                                                   int32_t* __restrict__ ccount, int gmax, BatchParams ebp,
-                                                  int dense1, const int32_t* __restrict__ ts_g) {
+                                                  int dense1, const int32_t* __restrict__ ts_g,
+                                                  int32_t* __restrict__ mneg) {
   __shared__ unsigned long long red[4];
+  int32_t wmin = INT32_MAX;  // lane = view: the minimum label of this wave's owned members
   __shared__ HopLDS L;
   if (threadIdx.x < 4) red[threadIdx.x] = 0;
   if constexpr (IEM) hop_lds_init(L, ebp, ebp.thr_e);  // (its barrier also publishes red)
@@ -610,6 +612,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         } else {
           row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
         }
+        if (own && ((mv >> lane) & 1)) wmin = min(wmin, me);
         const uint64_t kept = bal & span;
         const int32_t count = __popcll(kept);
         scanned += (unsigned long long)n;
@@ -668,6 +671,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       // mask OR here: its labels come from its owner.
       const bool own = v < n_own;
       const int32_t h = hv_of[v], me = grank ? grank[v] : (int32_t)v;
+      if (own && ((mv >> lane) & 1)) wmin = min(wmin, me);
       const int32_t x = hbest[(int64_t)h * 64 + lane];
       hbest[(int64_t)h * 64 + lane] = INT32_MAX;
       const int32_t best = own ? min(me, x) : me;
@@ -713,6 +717,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     // from its owner in the step-1 exchange.
     const bool own = v < n_own;
     const int32_t me = grank ? grank[v] : (int32_t)v;
+    if (own && ((mv >> lane) & 1)) wmin = min(wmin, me);
     if (uw0) {
       if (lane == 0) uw0[v] = me == INT32_MAX ? kMixed : me;
       if (me == INT32_MAX) row_store(lab0 + v * 64, me, line_has(mv, lane), lane);
@@ -818,6 +823,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
     }
     if (changed) atomicAdd(&red[2], changed);
   }
+  if (mneg && wmin != INT32_MAX) atomicMax(&mneg[(blockIdx.x & (kMinShards - 1)) * 64 + lane], INT32_MAX - wmin);
   publish_lanes(lanes, &red[3], lanechg, 1);  // (its barrier also publishes red[0..2])
   if (threadIdx.x == 0) {
     if (red[2] && ccount) atomicAdd(&ccount[1 * kCountShards + (blockIdx.x & (kCountShards - 1))], (int32_t)red[2]);
@@ -924,6 +930,19 @@ __device__ __forceinline__ void gather_min_x4(const uint64_t (&act)[4], const in
   }
 }
 
+// lane j: the batch's minimum member label in view j (mneg, kernels.hpp), or INT32_MIN when unknown
+__device__ __forceinline__ int32_t final_label(const int32_t* __restrict__ mneg, int lane) {
+  if (!mneg) return INT32_MIN;
+  int32_t x = 0;
+#pragma unroll
+  for (int sh = 0; sh < kMinShards; sh++) x = max(x, mneg[sh * 64 + lane]);
+  return x ? INT32_MAX - x : INT32_MIN;
+}
+// wave-uniform: a uniform word u holds the final label on every member lane of mv
+__device__ __forceinline__ bool holds_final(int32_t u, uint64_t mv, int32_t mfin, int lane) {
+  return u != kMixed && __ballot(((mv >> lane) & 1) && (u & 0x7fffffff) != mfin) == 0;
+}
+
 // Frontier list of the single-workgroup tail kernel (k_cc_tail), in LDS.
 constexpr int kTailListCap = 2048;
 struct TailList {
@@ -982,12 +1001,13 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          int32_t* __restrict__ hbest = nullptr,
                                          const int32_t* __restrict__ uw_cur = nullptr,
                                          int32_t* __restrict__ uw_next = nullptr,
-                                         uint64_t* __restrict__ cb_next = nullptr, bool skip_marks = false) {
+                                         uint64_t* __restrict__ cb_next = nullptr, bool skip_marks = false,
+                                         int32_t mfin = INT32_MIN) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
     const uint64_t mv_l = okl ? vm[vl] : 0;
-    const int32_t n_l = okl ? cnt[vl] : 0;  // 0 for a heavy vertex (its slots are in segments)
+    int32_t n_l = okl ? cnt[vl] : 0;  // 0 for a heavy vertex (its slots are in segments)
     const int32_t hh_l = (okl && hv_of) ? hv_of[vl] : -1;
     const int64_t b_l = adj_off[vl];
     const uint64_t cp_l = chg_prev[vl];
@@ -998,6 +1018,11 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     const int32_t un_l = uw_next ? uw_next[vl] : kMixed;
     int64_t vv[CH];
     int32_t cur[CH];
+    if (mfin != INT32_MIN) {  // (wave-uniform) a vertex that holds the final label gathers nothing
+#pragma unroll
+      for (int i = 0; i < CH; i++)
+        if (holds_final(__builtin_amdgcn_readlane(u_l, i), readlane64(mv_l, i), mfin, lane) && lane == i) n_l = 0;
+    }
 #pragma unroll
     for (int i = 0; i < CH; i++) {
       vv[i] = (int64_t)readlane64((uint64_t)vl, i);
@@ -1219,8 +1244,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
                                                   const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
                                                   uint64_t* __restrict__ cb_next,
                                                   uint64_t* __restrict__ cb_clear, int64_t cb_words,
-                                                  int32_t* __restrict__ ccount, int dense_div, int gmax) {
+                                                  int32_t* __restrict__ ccount, int dense_div, int gmax,
+                                                  const int32_t* __restrict__ mneg) {
   if (stepflag[step - 1] == 0) return;
+  const int32_t mfin = final_label(mneg, threadIdx.x & 63);
   // Dense steps (DenseRule): when step r-1 changed at least nv / dense_div vertices, step r
   // writes no next-frontier flags and step r+1 visits every member instead
   const bool skip_marks = dense_rule(ccount, step, nv, dense_div);
@@ -1275,7 +1302,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
       cc_chunk<CH, BUF, false>(dealt_item(wave, nwaves, r, G, L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
                                lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
-                               hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks);
+                               hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks, mfin);
     }
   }
   if constexpr (PROF)
@@ -1547,8 +1574,11 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       const int32_t* __restrict__ uw_cur,
                                                       const uint64_t* __restrict__ cb_prev,
                                                       const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
-                                                      unsigned long long* __restrict__ work, int pipe) {
+                                                      unsigned long long* __restrict__ work, int pipe,
+                                                      const uint64_t* __restrict__ vm,
+                                                      const int32_t* __restrict__ mneg) {
   if (stepflag[step - 1] == 0) return;
+  const int32_t mfin = (vm && uw_cur) ? final_label(mneg, threadIdx.x & 63) : INT32_MIN;
   const bool visit_all = dense_rule(ccount, step - 1, nv_all, dense_div);  // step-1 wrote no flags
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -1559,6 +1589,7 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
     if (v >= n_own || (!visit_all && !act_cur[v])) continue;  // ghosts are not visited (their owner computes them)
     const int32_t n = segcnt[sg];
     if (n == 0) continue;
+    if (mfin != INT32_MIN && holds_final(uw_cur[v], vm[v], mfin, lane)) continue;  // its label is final
     if (work) { w_seg++; w_slots += (unsigned long long)n; }
     const int64_t base = seg_lo[sg];
     int32_t best = INT32_MAX;  // lane = view
@@ -2440,6 +2471,7 @@ int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
 int g_slot_labels = 1;  // K2 streams the neighbours' labels (DevGraph.ts_g; RGPU_TSG)
 int g_step_ch = 2;      // vertices per superstep chunk (RGPU_STEP_CH: 2 or 4)
 int g_hub_pipe = 1;     // hub gather loads a segment's chunks first (RGPU_HUB_PIPE)
+int g_final_skip = 1;   // vertices holding their view's minimum member label skip gathers (RGPU_FINAL)
 int g_deal_slots = 16;  // deal_group maxima of K2 / the superstep kernel (RGPU_DEAL_SLOTS / _STEP;
                         // C4 A/B, profiles/r03/c4_ab_deal.log: K2 16 ≈ 64 < 1, step 1 ≈ 4 << 64)
 int g_deal_step = 4;
@@ -2481,7 +2513,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
                      unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends,
-                     int32_t* ccount, const BatchParams* ebp, int dense_div) {
+                     int32_t* ccount, const BatchParams* ebp, int dense_div, int32_t* mneg) {
   const bool hv = g.n_seg > 0;
   const bool iem = ebp != nullptr && g.ts_t != nullptr;
   auto* kern = work ? (iem ? k_cc_slots<true, true> : k_cc_slots<true, false>)
@@ -2494,7 +2526,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
                                                 uw0, uw1, cb1, ends ? 1 : 0, ccount, g_deal_slots, iem ? *ebp : bp0,
                                                 dense_div > 0 && (dense_div & kDense1) && ccount ? 1 : 0,
-                                                g_slot_labels ? g.ts_g : nullptr);
+                                                g_slot_labels ? g.ts_g : nullptr, mneg);
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
@@ -2517,7 +2549,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, int variant, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next,
-                    const ChgBits& cb, int32_t* ccount, int dense_div) {
+                    const ChgBits& cb, int32_t* ccount, int dense_div, const int32_t* mneg) {
   (void)variant;  // (8-vertex chunks, buffer-descriptor rows and a VGPR-capped build measured slower: removed)
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
   // A small graph's dense supersteps are latency-bound and share the GPU with the other batch
@@ -2529,7 +2561,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.next, cb.clear, cb.words, ccount, dense_div, g_deal_step
+    cb.next, cb.clear, cb.words, ccount, dense_div, g_deal_step, (uw_cur && g_final_skip) ? mneg : nullptr
   // work != null (profile runs): the counting instantiation; the timed runs use the lean one
   // 2-vertex chunks (default): 73 VGPRs, 6 waves/SIMD against 97 and 4 for 4-vertex chunks; same-box
   // A/B (tools/c4_ab.py, profiles/r03/c4_ab_step_ch.log): C4 369 -> 345 ms, C2 135 -> 120 ms.
@@ -2559,12 +2591,14 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur,
-                         const uint64_t* cb_prev, const int32_t* ccount, int dense_div, unsigned long long* work) {
+                         const uint64_t* cb_prev, const int32_t* ccount, int dense_div, unsigned long long* work,
+                         const uint64_t* vm, const int32_t* mneg) {
   if (g.n_seg <= 0) return;
   k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
                                                              hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
-                                                             g.n_own, work, g_hub_pipe);
+                                                             g.n_own, work, g_hub_pipe, vm,
+                                                             g_final_skip ? mneg : nullptr);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,

@@ -114,6 +114,12 @@ constexpr int kLaneShards = 64;
 // changed-vertex counts per superstep, ccount[step * kCountShards + shard] (int32, cleared per
 // batch): the dense-step rule of the superstep kernels (kernels.hip dense_rule, RGPU_DENSE)
 constexpr int kCountShards = 64;
+// Per-view minimum member label of a batch, sharded: mneg[shard][view] = INT32_MAX - min label of the
+// shard's members (0: none), atomicMax-ed by K2 and cleared with the batch's counts.  A uniform vertex
+// whose label equals that minimum on every member lane holds its final label: no neighbour's label
+// is smaller in any of its views, so the superstep kernel and the hub gather skip its gathers.
+constexpr int kMinShards = 16;
+constexpr int kMinWords = kMinShards * 64;
 // dense_div | kDense1: superstep 1 (K2) is dense too (it writes no frontier flags, step 2 visits
 // every member; kernels.hip dense_rule).  RGPU_DENSE1 (default on).
 constexpr int kDense1 = 1 << 30;
@@ -144,7 +150,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
                      unsigned long long* lanechg, int32_t* uw0 = nullptr, int32_t* uw1 = nullptr,
                      uint64_t* cb1 = nullptr, bool ends = false, int32_t* ccount = nullptr,
-                     const BatchParams* ebp = nullptr, int dense_div = 0);
+                     const BatchParams* ebp = nullptr, int dense_div = 0, int32_t* mneg = nullptr);
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
 // (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
 // next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
@@ -156,7 +162,8 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr,
                          const uint64_t* cb_prev = nullptr, const int32_t* ccount = nullptr, int dense_div = 0,
-                         unsigned long long* work = nullptr);
+                         unsigned long long* work = nullptr, const uint64_t* vm = nullptr,
+                         const int32_t* mneg = nullptr);
 // vm/em (partitioned mode): heavy ghosts (ranks >= n_own) have no compacted slots; their kept
 // slots are recomputed from the static adjacency (em & vm[nb] & vm[v]) while marking
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
@@ -171,6 +178,7 @@ extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 
 extern int g_slot_labels;  // K2 reads DevGraph.ts_g (RGPU_TSG)
 extern int g_step_ch;      // superstep chunk size (RGPU_STEP_CH)
 extern int g_hub_pipe;     // loads-first hub gather (RGPU_HUB_PIPE)
+extern int g_final_skip;   // final-label skip in the superstep kernel and the hub gather (RGPU_FINAL)
 extern int g_tail_step, g_tail_grid;  // supersteps >= tail_step use at most tail_grid blocks
 // uniform label words (kernels.hip, kMixed): rows of the uniform vertices written into lab
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab);
@@ -207,7 +215,8 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, int variant, unsigned long long* lanechg,
                     int32_t* hbest = nullptr, const int32_t* uw_cur = nullptr, int32_t* uw_next = nullptr,
-                    const ChgBits& cb = ChgBits(), int32_t* ccount = nullptr, int dense_div = 0);
+                    const ChgBits& cb = ChgBits(), int32_t* ccount = nullptr, int dense_div = 0,
+                    const int32_t* mneg = nullptr);
 // Many late supersteps in one single-workgroup launch while the frontier stays below `cap`
 // vertices; info[0] <- last superstep executed (host-mapped).
 void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,

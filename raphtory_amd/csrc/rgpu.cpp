@@ -369,6 +369,12 @@ int dense_div(const rgpu_ctx* c) {
   return d > 0 && c->dense1 ? (d | kDense1) : d;
 }
 
+// the batch's per-view minimum member labels (kernels.hpp kMinShards), behind the changed-vertex
+// counts; one partition only (a partition's minimum is not the graph's)
+int32_t* min_labels(const rgpu_ctx* c, const Slot& s) {
+  return (c->partitioned || !s.ccount) ? nullptr : s.ccount + (size_t)kMaxSteps * kCountShards;
+}
+
 // changed bits of superstep r (with uniform words; RGPU_CHGBITS=0 turns them off)
 ChgBits chg_bits(const rgpu_ctx* c, const Slot& s, int r) {
   ChgBits b;
@@ -452,7 +458,7 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       HIPCHK(hipHostMalloc((void**)&s.h_stats, sizeof(unsigned long long) * kStatWords));
       HIPCHK(hipHostMalloc((void**)&s.h_work, sizeof(unsigned long long) * kWorkWords));
       s.stepcnt = dalloc<int32_t>(L, kMaxSteps);
-      s.ccount = dalloc<int32_t>(L, (size_t)kMaxSteps * kCountShards);
+      s.ccount = dalloc<int32_t>(L, (size_t)kMaxSteps * kCountShards + kMinWords);  // + the minimum labels (mneg)
       s.stats = dalloc<unsigned long long>(L, kStatWords);
       HIPCHK(hipMemset(s.stats, 0, sizeof(unsigned long long) * kStatWords));
     }
@@ -624,7 +630,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[(r - 1) & 1], s.chg[(r - 1) & 1], s.act[r % 3],
                             s.stepcnt, r, s.hv, uw ? s.uw[(r - 1) & 1] : nullptr, chg_bits(c, s, r).prev, s.ccount,
-                            dense_div(c), work_buf(c, s));
+                            dense_div(c), work_buf(c, s), s.vm, min_labels(c, s));
       }, r, per_launch);
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
@@ -632,7 +638,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
                      s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                      work_buf(c, s), 0, s.stats + kLaneOff,
                      hv ? s.hv.best : nullptr, uw ? s.uw[(r - 1) & 1] : nullptr, uw ? s.uw[r & 1] : nullptr,
-                     chg_bits(c, s, r), s.ccount, dense_div(c));
+                     chg_bits(c, s, r), s.ccount, dense_div(c), min_labels(c, s));
     }, r, per_launch);
     if (hv)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
@@ -829,7 +835,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     clr.n_act_words = (g.nv + 7) / 8 + 1;
     if (rc.algo == RGPU_ALGO_CC) {
       clr.ccount = s.ccount;
-      clr.n_ccount = (int64_t)kMaxSteps * kCountShards;
+      clr.n_ccount = (int64_t)kMaxSteps * kCountShards + kMinWords;
     }
     const ChgBits cb1 = rc.algo == RGPU_ALGO_CC ? chg_bits(c, s, 1) : ChgBits();
     if (cb1.next) {
@@ -947,7 +953,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
                       s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
                       work_buf(c, s), s.hv, s.stats + kLaneOff, use_uw(c) ? s.uw[0] : nullptr,
                       use_uw(c) ? s.uw[1] : nullptr, chg_bits(c, s, 1).next, ends, s.ccount, iem ? &ebp : nullptr,
-                      dense_div(c));
+                      dense_div(c), min_labels(c, s));
     });
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
@@ -2529,6 +2535,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   g_slot_labels = env_int("RGPU_TSG", 1);
   g_step_ch = env_int("RGPU_STEP_CH", 2) == 4 ? 4 : 2;  // superstep chunk: 2 (default) or 4 vertices
   g_hub_pipe = env_int("RGPU_HUB_PIPE", 1);
+  g_final_skip = env_int("RGPU_FINAL", 1);
   {  // powers of two up to 64
     auto pow2 = [](int x) { int g = 1; while (g < x && g < 64) g <<= 1; return g; };
     g_deal_slots = pow2(env_int("RGPU_DEAL_SLOTS", 16));

@@ -17,7 +17,7 @@ import torch  # noqa: E402
 from raphtory_amd import TemporalGraph  # noqa: E402
 from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops  # noqa: E402
 
-KNOBS = ("RGPU_HUB_PIPE", "RGPU_STEP_CH", "RGPU_TSG", "RGPU_IEM", "RGPU_DENSE1", "RGPU_DEAL_SLOTS", "RGPU_DEAL_STEP", "RGPU_DENSE", "RGPU_CHGBITS", "RGPU_STEP_GRID", "RGPU_TAIL_STEP", "RGPU_TAIL_GRID", "RGPU_CHUNK0", "RGPU_CHUNK")
+KNOBS = ("RGPU_FINAL", "RGPU_HUB_PIPE", "RGPU_STEP_CH", "RGPU_TSG", "RGPU_IEM", "RGPU_DENSE1", "RGPU_DEAL_SLOTS", "RGPU_DEAL_STEP", "RGPU_DENSE", "RGPU_CHGBITS", "RGPU_STEP_GRID", "RGPU_TAIL_STEP", "RGPU_TAIL_GRID", "RGPU_CHUNK0", "RGPU_CHUNK")
 
 
 def main():
