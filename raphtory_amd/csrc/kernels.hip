@@ -1057,7 +1057,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     if (uw_cur) {
       int32_t w[CH];
 #pragma unroll
-      for (int i = 0; i < CH; i++) w[i] = uw_cur[nb[i]];
+      for (int i = 0; i < CH; i++) w[i] = uw_cur[nb[i]];  // (unconditional: skipping the loads of slotless
+                                                         // vertices with a branch measured 367 vs 347 ms on C4)
       uint64_t mixed = 0;
 #pragma unroll
       for (int i = 0; i < CH; i++) {
