@@ -94,7 +94,8 @@ def pmc_traffic(kernel, config="C2"):
     if kernel not in d.get("FETCH_SIZE", {}).get("kernel", ""):
         return None, None
     return (round(d["traffic_bytes_per_launch"]["value"]),
-            os.path.relpath(path, ROOT) + ": " + d["traffic_bytes_per_launch"]["formula"])
+            os.path.relpath(path, ROOT) + " [" + d["FETCH_SIZE"]["kernel"] + "]: "
+            + d["traffic_bytes_per_launch"]["formula"])
 
 
 def cpu_info():

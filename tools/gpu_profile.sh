@@ -24,18 +24,25 @@ import csv, glob, json, sys
 k = sys.argv[1]
 out = {}
 for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-    vals, durs = [], []
+    by = {}  # per template instantiation: the lean and the profiling superstep differ
     for f in glob.glob(f"gpurun_out/prof/{ctr.split('_')[0].lower()}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") == ctr and k in r.get("Kernel_Name", ""):
+                name = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+                vals, durs = by.setdefault(name, ([], []))
                 vals.append(float(r["Counter_Value"]))
                 try:
                     durs.append((float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) / 1e3)
                 except (KeyError, ValueError):
                     pass
-    if vals:
-        out[ctr] = {"kernel": k, "dispatches": len(vals), "mean_kb_per_dispatch": sum(vals) / len(vals),
-                    "total_kb": sum(vals), "mean_dispatch_us_under_pmc": sum(durs) / len(durs) if durs else None}
+    if by:
+        # the lean instantiation (last template flag false: no work counters) the timed run launches
+        lean = [n for n in by if n.endswith("false>")] or list(by)
+        name = max(lean, key=lambda n: len(by[n][0]))
+        vals, durs = by[name]
+        out[ctr] = {"kernel": name, "dispatches": len(vals), "mean_kb_per_dispatch": sum(vals) / len(vals),
+                    "total_kb": sum(vals), "mean_dispatch_us_under_pmc": sum(durs) / len(durs) if durs else None,
+                    "other_instantiations": {n: len(v[0]) for n, v in by.items() if n != name}}
 if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
     out["traffic_bytes_per_launch"] = {
         "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM section: gfx950 FETCH_SIZE counts "
