@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD_DIR = os.path.join(_HERE, "_build")
 
 # error codes / constants mirrored from include/rgpu.h
+ABI_VERSION = 8
 RGPU_OK = 0
 RGPU_EINVAL, RGPU_ESTATE, RGPU_EHIP, RGPU_ENOMEM, RGPU_ENOTSUP = -1, -2, -3, -4, -5
 RGPU_VADD, RGPU_VDEL, RGPU_EADD, RGPU_EDEL = 0, 1, 2, 3
@@ -128,12 +129,17 @@ def rgpu() -> C.CDLL:
             lib = C.CDLL(path)
         except OSError as e:  # pragma: no cover - depends on the box
             raise NativeUnavailable(f"cannot load {path}: {e}") from e
+        missing = [name for name in _SIGS if getattr(lib, name, None) is None]
+        if missing:
+            raise NativeUnavailable(f"{path} lacks entry points {missing}: rebuild it")
         for name, (res, args) in _SIGS.items():
-            fn = getattr(lib, name, None)
-            if fn is None:  # an older library (same-box A/B runs): the entry point stays unbound
-                continue
+            fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        # the Stats / CCSummary layouts above are those of this ABI version (rgpu.h RGPU_ABI_VERSION)
+        abi = lib.rgpu_abi_version()
+        if abi != ABI_VERSION:
+            raise NativeUnavailable(f"{path} speaks ABI {abi}, these bindings ABI {ABI_VERSION}: rebuild it")
         _lib = lib
     return _lib
 

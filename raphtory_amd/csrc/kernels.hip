@@ -10,7 +10,7 @@
 //   k_cc_slots     K2  per-view adjacency filter (Vertex.viewAtWithWindow, Vertex.scala:70-74)
 //                      compacted into a batch CSR with a 64-bit view mask per slot
 //   k_cc_step      K3  one CC superstep for all views (ConnectedComponents.analyse :19-35)
-//   k_cc_hist/summary K5 label->count histogram + processBatchWindowResults summary (:137-145)
+//   k_cc_count/roots K5 label->count at the root's row + processBatchWindowResults summary (:137-145)
 //   k_degree       DegreeBasic.returnResults (DegreeBasic.scala:16-28)
 //   k_pr_slots/k_pr_step  PageRank spec
 #include <hip/hip_runtime.h>
@@ -895,41 +895,6 @@ __device__ __forceinline__ int32_t gather_min(uint64_t act, int32_t nb, int32_t 
   return best;
 }
 
-// Gathers of a whole 4-vertex chunk, interleaved: each round takes up to two changed
-// neighbours of every vertex (8 row loads in flight), then folds them.  Vertex positions
-// are static (unrolled), so no register is dynamically indexed.
-template <bool BUF>
-__device__ __forceinline__ void gather_min_x4(const uint64_t (&act)[4], const int32_t (&nb)[4],
-                                              int32_t (&best)[4], const int32_t* __restrict__ lab_cur,
-                                              int lane) {
-  uint64_t bal[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) bal[i] = __ballot(act[i] != 0);
-  while (bal[0] | bal[1] | bal[2] | bal[3]) {
-    int32_t x[4][2];
-    bool on[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        on[i][h] = false;
-        x[i][h] = INT32_MAX;
-        if (bal[i]) {  // wave-uniform
-          const int L = __builtin_ctzll(bal[i]);
-          bal[i] &= bal[i] - 1;
-          const int32_t q = __builtin_amdgcn_readlane(nb[i], L);
-          on[i][h] = (readlane64(act[i], L) >> lane) & 1;
-          x[i][h] = row_get<BUF>(lab_cur + (int64_t)q * 64, on[i][h], lane);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int h = 0; h < 2; h++) best[i] = min(best[i], on[i][h] ? x[i][h] : INT32_MAX);
-  }
-}
-
 // lane j: the batch's minimum member label in view j (mneg, kernels.hpp), or INT32_MIN when unknown
 __device__ __forceinline__ int32_t final_label(const int32_t* __restrict__ mneg, int lane) {
   if (!mneg) return INT32_MIN;
@@ -938,44 +903,16 @@ __device__ __forceinline__ int32_t final_label(const int32_t* __restrict__ mneg,
   for (int sh = 0; sh < kMinShards; sh++) x = max(x, mneg[sh * 64 + lane]);
   return x ? INT32_MAX - x : INT32_MIN;
 }
-// wave-uniform: a uniform word u holds the final label on every member lane of mv
+// wave-uniform call with every lane active (lane j holds view j's mfin): a uniform word u holds the
+// final label on every member lane of mv.  A lane whose view has no member in the batch (mfin
+// INT32_MIN) is not a member lane of any vertex, so it never votes against.
 __device__ __forceinline__ bool holds_final(int32_t u, uint64_t mv, int32_t mfin, int lane) {
   return u != kMixed && __ballot(((mv >> lane) & 1) && (u & 0x7fffffff) != mfin) == 0;
 }
 
-// Frontier list of the single-workgroup tail kernel (k_cc_tail), in LDS.
-constexpr int kTailListCap = 2048;
-struct TailList {
-  int32_t* list;  // next frontier
-  int* n;         // its length; may run past kTailListCap (the entries past it are dropped)
-};
-
-// Set the frontier flag of v (byte per vertex) and report whether it was clear before.
-__device__ __forceinline__ bool flag_fresh(uint8_t* act, int64_t v) {
-  uint32_t* w = reinterpret_cast<uint32_t*>(act + (v & ~(int64_t)3));
-  const int sh = 8 * (int)(v & 3);
-  return (atomicOr(w, 1u << sh) & (0xffu << sh)) == 0;
-}
-// Wave-uniform call: append the lanes with `fresh` to the list.
-__device__ __forceinline__ void list_append(bool fresh, int32_t v, const TailList& tl, int lane) {
-  const uint64_t b = __ballot(fresh);
-  if (!b) return;
-  int base = 0;
-  if (lane == 0) base = atomicAdd(tl.n, __popcll(b));
-  base = __builtin_amdgcn_readlane(base, 0);
-  const int idx = base + __popcll(b & lanemask_lt());
-  if (fresh && idx < kTailListCap) tl.list[idx] = v;
-}
-// Next-frontier flag of v on the lanes with `want`: a plain byte store (full-grid kernel:
-// idempotent, no RMW) or flag + list append (tail kernel).  Wave-uniform call.
-template <bool TAIL>
-__device__ __forceinline__ void mark(bool want, int32_t v, uint8_t* act_next, const TailList& tl, int lane) {
-  if (!TAIL) {
-    if (want) act_next[v] = 1;
-  } else {
-    const bool fresh = want && flag_fresh(act_next, v);
-    list_append(fresh, v, tl, lane);
-  }
+// Next-frontier flag of v on the lanes with `want`: a plain byte store (idempotent, no RMW).
+__device__ __forceinline__ void mark(bool want, int32_t v, uint8_t* act_next) {
+  if (want) act_next[v] = 1;
 }
 
 // One CH-vertex chunk of a superstep.  Vertex i (< CH) of the chunk is readlane(vl, i) and
@@ -987,7 +924,7 @@ __device__ __forceinline__ void mark(bool want, int32_t v, uint8_t* act_next, co
 // chunk.  All loads are unconditional from padded buffers (see gather_min).  A visited
 // vertex rewrites its row only if it changed now or in the previous step (the only cases
 // where the two label buffers differ).  uw_cur / uw_next: uniform label words (null: rows only).
-template <int CH, bool BUF, bool TAIL, class WK>
+template <int CH, bool BUF, class WK>
 __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_t* __restrict__ adj_off,
                                          const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
                                          const int32_t* __restrict__ snbr,
@@ -995,14 +932,14 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          const int32_t* __restrict__ lab_cur, int32_t* __restrict__ lab_next,
                                          const uint64_t* __restrict__ chg_prev,
                                          uint64_t* __restrict__ chg_next, uint8_t* __restrict__ act_next,
-                                         const TailList& tl, int lane, int32_t& changed,
+                                         int lane, int32_t& changed,
                                          unsigned long long* __restrict__ lds_lanes,
                                          WK& wk, const int32_t* __restrict__ hv_of = nullptr,
                                          int32_t* __restrict__ hbest = nullptr,
                                          const int32_t* __restrict__ uw_cur = nullptr,
                                          int32_t* __restrict__ uw_next = nullptr,
                                          uint64_t* __restrict__ cb_next = nullptr, bool skip_marks = false,
-                                         int32_t mfin = INT32_MIN) {
+                                         int32_t mfin = INT32_MIN, bool use_fin = false) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
@@ -1018,10 +955,12 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     const int32_t un_l = uw_next ? uw_next[vl] : kMixed;
     int64_t vv[CH];
     int32_t cur[CH];
-    if (mfin != INT32_MIN) {  // (wave-uniform) a vertex that holds the final label gathers nothing
+    if (use_fin) {  // (wave-uniform) a vertex that holds the final label gathers nothing
 #pragma unroll
-      for (int i = 0; i < CH; i++)
-        if (holds_final(__builtin_amdgcn_readlane(u_l, i), readlane64(mv_l, i), mfin, lane) && lane == i) n_l = 0;
+      for (int i = 0; i < CH; i++) {
+        const bool fin = holds_final(__builtin_amdgcn_readlane(u_l, i), readlane64(mv_l, i), mfin, lane);
+        if (fin && lane == i) n_l = 0;
+      }
     }
 #pragma unroll
     for (int i = 0; i < CH; i++) {
@@ -1097,12 +1036,8 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
       best[i] = cur[i];
       actr[i] = un[i] == kMixed ? act[i] : 0;
     }
-    if constexpr (CH == 4) {
-      gather_min_x4<BUF>(actr, nb, best, lab_cur, lane);
-    } else {
 #pragma unroll
-      for (int i = 0; i < CH; i++) best[i] = gather_min<BUF>(actr[i], nb[i], best[i], lab_cur, lane);
-    }
+    for (int i = 0; i < CH; i++) best[i] = gather_min<BUF>(actr[i], nb[i], best[i], lab_cur, lane);
     if (uw_cur) {
 #pragma unroll
       for (int i = 0; i < CH; i++)
@@ -1183,15 +1118,15 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
         if (lane == 0) atomicOr(lds_lanes, (unsigned long long)ch);  // LDS: views changed this step
         changed++;
         if (skip_marks) continue;  // dense step: the next step visits every member (k_cc_step2)
-        mark<TAIL>(lane == 0, (int32_t)v, act_next, tl, lane);
-        mark<TAIL>((sm[i] & ch) != 0, nb[i], act_next, tl, lane);
+        mark(lane == 0, (int32_t)v, act_next);
+        mark((sm[i] & ch) != 0, nb[i], act_next);
         if (n > 64) {
           const int64_t base = (int64_t)readlane64((uint64_t)b_l, i);
           for (int32_t c2 = 64; c2 < n; c2 += 64) {
             const int32_t j = c2 + lane;
             const int64_t idx = base + (j < n ? j : c2);
             const int32_t q = snbr[idx];
-            mark<TAIL>(j < n && (smask[idx] & ch) != 0, q, act_next, tl, lane);
+            mark(j < n && (smask[idx] & ch) != 0, q, act_next);
           }
         }
       }
@@ -1270,7 +1205,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   int32_t changed = 0;
   std::conditional_t<PROF, StepWork, NoWork> wk;
-  const TailList none{nullptr, nullptr};
   // Chunks are dealt in groups of up to gmax (deal_group, as K2 deals vertices; RGPU_DEAL_STEP):
   // per round lane l reads its chunk's frontier flags, and the wave then runs only the flagged
   // chunks — a sparse frontier costs one load per 64 chunks.  Every wave of the grid gets work on
@@ -1301,9 +1235,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
       const int L = __builtin_ctzll(todo);
       todo &= todo - 1;
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
-      cc_chunk<CH, BUF, false>(dealt_item(wave, nwaves, r, G, L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
-                               lab_next, chg_prev, chg_next, act_next, none, lane, changed, &wred[7], wk,
-                               hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks, mfin);
+      cc_chunk<CH, BUF>(dealt_item(wave, nwaves, r, G, L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
+                        lab_next, chg_prev, chg_next, act_next, lane, changed, &wred[7], wk,
+                               hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks, mfin, mneg != nullptr && uw_cur);
     }
   }
   if constexpr (PROF)
@@ -1329,117 +1263,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
                                      wred[2]};
     add_work(work, step, f);
   }
-}
-
-// Late supersteps touch tens to hundreds of vertices (long chains converging), yet as
-// separate full-grid launches each pays ~8-10 us of launch + dependent-load latency.
-// k_cc_tail runs them back to back inside ONE workgroup (16 waves on one CU) with a barrier
-// between supersteps: one workgroup's global stores are visible to its own waves after
-// __syncthreads (same CU, same L1), so no grid-wide synchronisation is needed.  The frontier
-// is a list in LDS, deduplicated through the same byte flags (atomicOr) the full-grid kernel
-// uses, and the superstep body is cc_chunk itself, on the same label / change-word / flag
-// buffers with the same rotation — so the two kernels hand over at any superstep: when the
-// next frontier holds more than `cap` vertices the tail stops, its flags complete in
-// act[(r+1)%3], and the full-grid kernel takes superstep r+1.  info[0] = the last superstep
-// executed (r0-1 if none).
-constexpr int kTailThreads = 1024;
-
-template <bool BUF>
-__global__ __launch_bounds__(kTailThreads) void k_cc_tail(int r0, int rmax, int cap, int64_t nv,
-                                                          const int64_t* __restrict__ adj_off,
-                                                          const uint64_t* __restrict__ vm,
-                                                          const int32_t* __restrict__ cnt,
-                                                          const int32_t* __restrict__ snbr,
-                                                          const uint64_t* __restrict__ smask,
-                                                          int32_t* lab0, int32_t* lab1, uint64_t* chg0,
-                                                          uint64_t* chg1, uint8_t* act0, uint8_t* act1,
-                                                          uint8_t* act2, int32_t* __restrict__ stepflag,
-                                                          int32_t* __restrict__ hostflag,
-                                                          int32_t* __restrict__ info,
-                                                          unsigned long long* __restrict__ work,
-                                                          unsigned long long* __restrict__ lanechg) {
-  __shared__ int32_t list[2][kTailListCap];
-  __shared__ int nlist[2];
-  __shared__ int nchanged;
-  __shared__ unsigned long long wsum[4];
-  auto ACT = [&](int k) { return k == 0 ? act0 : (k == 1 ? act1 : act2); };
-  const int lane = lane_id(), wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if (stepflag[r0 - 1] == 0) {  // the batch has halted already
-    if (threadIdx.x == 0) info[0] = r0 - 1;
-    return;
-  }
-  if (threadIdx.x == 0) { nlist[0] = 0; nlist[1] = 0; }
-  __syncthreads();
-  {  // frontier of step r0 (flags act[r0%3]) -> list 0; clear act[(r0+2)%3] (frontier of r0-1)
-    const uint64_t* a = reinterpret_cast<const uint64_t*>(ACT(r0 % 3));
-    uint64_t* z = reinterpret_cast<uint64_t*>(ACT((r0 + 2) % 3));
-    const int64_t nwords = (nv + 7) >> 3;
-    for (int64_t i = threadIdx.x; i < nwords; i += blockDim.x) {
-      const uint64_t f = a[i];
-      z[i] = 0;
-      if (f) {
-        uint32_t bits = 0;
-#pragma unroll
-        for (int k = 0; k < 8; k++) bits |= ((f >> (8 * k)) & 0xffu) ? (1u << k) : 0u;
-        int idx = atomicAdd(&nlist[0], __popc(bits));
-        while (bits) {
-          const int k = __builtin_ctz(bits);
-          bits &= bits - 1;
-          if (idx < kTailListCap) list[0][idx] = (int32_t)(i * 8 + k);
-          idx++;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  int p = 0, r = r0 - 1;  // r: last superstep executed
-  for (;;) {
-    const int ncur = nlist[p];
-    if (ncur > cap) break;  // too wide for one workgroup: the full-grid kernel takes step r+1
-    const int s = r + 1;
-    __syncthreads();  // everyone has read nlist[p] and left the previous clear loop
-    if (threadIdx.x == 0) { nlist[p ^ 1] = 0; nchanged = 0; wsum[0] = 0; wsum[1] = 0; wsum[2] = 0; wsum[3] = 0; }
-    __syncthreads();
-    uint8_t* a_cur = ACT(s % 3);
-    uint8_t* a_next = ACT((s + 1) % 3);
-    const int32_t* lab_cur = ((s - 1) & 1) ? lab1 : lab0;
-    int32_t* lab_next = (s & 1) ? lab1 : lab0;
-    const uint64_t* chg_prev = ((s - 1) & 1) ? chg1 : chg0;
-    uint64_t* chg_next = (s & 1) ? chg1 : chg0;
-    const TailList tl{list[p ^ 1], &nlist[p ^ 1]};
-    int32_t changed = 0;
-    StepWork wk;
-    for (int c = wid * 4; c < ncur; c += nw * 4) {
-      const int k = c + (lane & 3) < ncur ? c + (lane & 3) : c;
-      const uint32_t bits = ncur - c >= 4 ? 0xfu : ((1u << (ncur - c)) - 1);
-      cc_chunk<4, BUF, true>((int64_t)list[p][k], bits, adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
-                             chg_prev, chg_next, a_next, tl, lane, changed, &wsum[3], wk);
-    }
-    const unsigned long long pv = wk.v, ps = wk.s;
-    unsigned long long pg = wk.g;
-    for (int o = 32; o > 0; o >>= 1) pg += __shfl_xor(pg, o);
-    if (lane == 0) {
-      if (changed) atomicAdd(&nchanged, changed);
-      if (pv) atomicAdd(&wsum[0], pv);
-      if (ps) atomicAdd(&wsum[1], ps);
-      if (pg) atomicAdd(&wsum[2], pg);
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < ncur; k += blockDim.x) a_cur[list[p][k]] = 0;  // step s consumed them
-    const int nch = nchanged;
-    if (threadIdx.x == 0) {
-      if (nch) {
-        stepflag[s] = 1;
-        if (hostflag) hostflag[s] = 1;
-      }
-      if (wsum[3] && lanechg) atomicOr(&lanechg[s * kLaneShards], wsum[3]);
-      add_work(work, s, wsum[0], wsum[1], (unsigned long long)nch, wsum[2]);
-    }
-    r = s;
-    p ^= 1;
-    if (nch == 0 || s >= rmax) break;
-  }
-  if (threadIdx.x == 0) info[0] = r;
 }
 
 // ---------------------------------------------------------------- heavy vertices
@@ -1575,11 +1398,12 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       const int32_t* __restrict__ uw_cur,
                                                       const uint64_t* __restrict__ cb_prev,
                                                       const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
-                                                      unsigned long long* __restrict__ work, int pipe,
+                                                      unsigned long long* __restrict__ work,
                                                       const uint64_t* __restrict__ vm,
                                                       const int32_t* __restrict__ mneg) {
   if (stepflag[step - 1] == 0) return;
-  const int32_t mfin = (vm && uw_cur) ? final_label(mneg, threadIdx.x & 63) : INT32_MIN;
+  const bool use_fin = vm && uw_cur && mneg;
+  const int32_t mfin = use_fin ? final_label(mneg, threadIdx.x & 63) : INT32_MIN;
   const bool visit_all = dense_rule(ccount, step - 1, nv_all, dense_div);  // step-1 wrote no flags
   const int lane = lane_id();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
@@ -1590,11 +1414,11 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
     if (v >= n_own || (!visit_all && !act_cur[v])) continue;  // ghosts are not visited (their owner computes them)
     const int32_t n = segcnt[sg];
     if (n == 0) continue;
-    if (mfin != INT32_MIN && holds_final(uw_cur[v], vm[v], mfin, lane)) continue;  // its label is final
+    if (use_fin && holds_final(uw_cur[v], vm[v], mfin, lane)) continue;  // its label is final (wave-uniform)
     if (work) { w_seg++; w_slots += (unsigned long long)n; }
     const int64_t base = seg_lo[sg];
     int32_t best = INT32_MAX;  // lane = view
-    if (pipe && cb_prev && uw_cur && n <= kSegSlots) {
+    if (cb_prev && uw_cur && n <= kSegSlots) {
       // Loads first over the segment's (at most 8) chunks: neighbours, their changed-bit words,
       // then the hot slots' masks and words, then the folds — three dependent trips per segment
       // instead of three per chunk.
@@ -1716,81 +1540,6 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
 }
 
 // ---------------------------------------------------------------- K5: CC reductions
-// label -> count histogram (ConnectedComponents.returnResults :37-42, groupBy over labels).
-// A block stages the label rows of 64 consecutive vertices in LDS (8 rows per wave), then
-// its eight waves split the views (wave w takes views j = w mod 8): per view the 64 vertices
-// sit on the lanes and each distinct label is added once per chunk (popcount of the lanes
-// that carry it), so the giant component costs one atomic per 64 vertices, not one per
-// vertex.  The dedup loop is serial (a ballot per distinct label), so after `rounds` labels
-// the remaining lanes (small components) issue their own atomics in one instruction.  The per-view loop is serial, latency-bound work: one chunk per block keeps ~24
-// waves per CU on it (one chunk per wave kept ~6); eight waves of 8 views each instead of four of
-// 16 halve each wave's chain (C2 serial 31.8 -> 29.0 ms).
-// Members with no kept slot in a view are isolated there: islands (count 1) that need no
-// histogram entry.  Their counts go to iso[shard][view] (64 shards: a few dozen blocks per
-// address, not thousands); the summary kernel folds them into total / sum / biggest.
-template <bool BUF>
-__global__ __launch_bounds__(512) void k_cc_hist(int64_t nv, int64_t hstride, int nviews,
-                                                 const uint64_t* __restrict__ vm,
-                                                 const uint64_t* __restrict__ vadj,
-                                                 const int32_t* __restrict__ lab,
-                                                 int32_t* __restrict__ hist,
-                                                 unsigned int* __restrict__ iso_g, int rounds) {
-  __shared__ int32_t tile[64][65];
-  __shared__ unsigned int iso[64];
-  if (threadIdx.x < 64) iso[threadIdx.x] = 0;
-  const int lane = lane_id(), wib = threadIdx.x >> 6;
-  const uint64_t vmask = (nviews >= 64 ? ~0ull : ((1ull << nviews) - 1)) & (0x0101010101010101ull << wib);
-  for (int64_t c = blockIdx.x; c * 64 < nv; c += gridDim.x) {
-    const int64_t v0 = c * 64;
-    const int nvc = (int)(nv - v0 < 64 ? nv - v0 : 64);
-    {
-      int32_t r[8];  // 8 independent row loads in flight per wave, then LDS
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int i = wib * 8 + k;
-        if (BUF) {
-          const uint64_t mk = i < nvc ? vm[v0 + i] : 0;  // scalar: wave-uniform vertex
-          r[k] = row_load(lab + (v0 + i) * 64, (mk >> lane) & 1, lane);
-        } else {
-          r[k] = i < nvc ? lab[(v0 + i) * 64 + lane] : 0;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) tile[wib * 8 + k][lane] = r[k];
-    }
-    const uint64_t mvl = lane < nvc ? vm[v0 + lane] : 0;
-    const uint64_t adl = lane < nvc ? vadj[v0 + lane] : 0;
-    uint64_t any = mvl;  // views with at least one member in this chunk (OR over lanes)
-    for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
-    any = readlane64(any, 0) & vmask;
-    __syncthreads();
-    while (any) {
-      const int j = __builtin_ctzll(any);
-      any &= any - 1;
-      const bool in_view = (mvl >> j) & 1;
-      const bool member = in_view && ((adl >> j) & 1);
-      const uint64_t isolated = __ballot(in_view && !member);
-      if (lane == 0 && isolated) iso[j] += (unsigned)__popcll(isolated);  // view j: this wave only
-      const int32_t l = tile[lane][j];
-      uint64_t todo = __ballot(member);
-      for (int it = 0; todo; it++) {
-        if (it == rounds) {  // the rest: one atomic per lane, all issued at once
-          if ((todo >> lane) & 1) atomicAdd(&hist[(int64_t)j * hstride + l], 1);
-          break;
-        }
-        const int leader = __builtin_ctzll(todo);
-        const int32_t L = __builtin_amdgcn_readlane(l, leader);
-        const uint64_t same = __ballot(member && l == L);
-        if (lane == leader) atomicAdd(&hist[(int64_t)j * hstride + L], __popcll(same));
-        todo &= ~same;
-      }
-    }
-    __syncthreads();  // the tile is rewritten by the next chunk
-  }
-  if (threadIdx.x < 64 && iso[threadIdx.x])
-    atomicAdd(&iso_g[(blockIdx.x & 63) * 64 + threadIdx.x], iso[threadIdx.x]);
-}
-
 // Fold the isolated-member shards of view j into the summary (islands: count 1 each) and
 // clear them for the next batch.  Called by block (0, j) of a summary kernel.
 __device__ __forceinline__ void fold_iso(unsigned int* __restrict__ iso_g, int j,
@@ -1806,55 +1555,6 @@ __device__ __forceinline__ void fold_iso(unsigned int* __restrict__ iso_g, int j
   }
 }
 
-// processBatchWindowResults summary per view (ConnectedComponents.scala:137-145) from the
-// view-major histogram hist[view][rank] (read only: the buffer is the batch's free label row,
-// zeroed by the memset before k_cc_hist and overwritten by the next batch).  blockIdx.y = view,
-// blockIdx.x strides over ranks; one atomic per (block, field).  stats[f*64 + view]:
-// 0 biggest 1 total 2 total>1 3 total>2 4 sum 5 sum(count>1)
-__global__ __launch_bounds__(256) void k_cc_summary(int64_t nv, int32_t* __restrict__ hist,
-                                                    unsigned long long* __restrict__ stats,
-                                                    unsigned int* __restrict__ iso) {
-  __shared__ unsigned long long red[6][4];
-  const int j = blockIdx.y;
-  if (blockIdx.x == 0) fold_iso(iso, j, stats);
-  int32_t* h = hist + (int64_t)j * nv;
-  unsigned long long big = 0, tot = 0, nis = 0, gt2 = 0, sum = 0, snis = 0;
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nv;
-       r += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t c = h[r];
-    if (c) {
-      const unsigned long long uc = (unsigned long long)c;
-      big = uc > big ? uc : big;
-      tot += 1;
-      nis += c > 1;
-      gt2 += c > 2;
-      sum += uc;
-      snis += c > 1 ? uc : 0;
-    }
-  }
-  unsigned long long v[6] = {big, tot, nis, gt2, sum, snis};
-#pragma unroll
-  for (int f = 0; f < 6; f++) {
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long x = __shfl_xor(v[f], o);
-      v[f] = f == 0 ? (x > v[f] ? x : v[f]) : v[f] + x;
-    }
-  }
-  const int lane = lane_id(), wib = threadIdx.x >> 6;
-  if (lane == 0)
-    for (int f = 0; f < 6; f++) red[f][wib] = v[f];
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    const int f = threadIdx.x;
-    unsigned long long a = red[f][0];
-    for (int w = 1; w < 4; w++) a = f == 0 ? (red[f][w] > a ? red[f][w] : a) : a + red[f][w];
-    if (a) {
-      if (f == 0) atomicMax(&stats[j], a);
-      else atomicAdd(&stats[f * 64 + j], a);
-    }
-  }
-}
-
 // ---- component counts from the uniform label words (one partition, kernels.hip kMixed).
 // k_cc_count: counts[label][view] (rows of 64, the root's row) += members carrying the label,
 // lane = vertex, 64 vertices per wave round.  Uniform members with the same (label, views) are
@@ -1864,7 +1564,7 @@ __global__ __launch_bounds__(256) void k_cc_summary(int64_t nv, int32_t* __restr
 // (claimed first come, keyed by label): a giant component's root row takes one global atomic
 // per block and view instead of one per member group (month/week batches, where members'
 // view sets differ, measured 16-94 ms per batch without it on C4).  Isolated members (no kept
-// slot in the view) are islands: counted per view into iso[shard][view] as k_cc_hist does.
+// slot in the view) are islands: counted per view into iso[shard][view] (64 shards).
 // k_cc_roots: every root (a member whose label in the view is its own rank and that has a kept
 // slot there) reads its count row, folds it into the processBatchWindowResults fields per view
 // (ConnectedComponents.scala:137-145) and zeroes it again, so the count rows stay zero between
@@ -2468,18 +2168,12 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 }
 
 // ---------------------------------------------------------------- launchers
-int g_step_grid = 0;  // 0: by graph size (see launch_cc_step)
-int g_slot_labels = 1;  // K2 streams the neighbours' labels (DevGraph.ts_g; RGPU_TSG)
-int g_step_ch = 2;      // vertices per superstep chunk (RGPU_STEP_CH: 2 or 4)
-int g_hub_pipe = 1;     // hub gather loads a segment's chunks first (RGPU_HUB_PIPE)
-int g_final_skip = 1;   // vertices holding their view's minimum member label skip gathers (RGPU_FINAL)
-int g_deal_slots = 16;  // deal_group maxima of K2 / the superstep kernel (RGPU_DEAL_SLOTS / _STEP;
-                        // C4 A/B, profiles/r03/c4_ab_deal.log: K2 16 ≈ 64 < 1, step 1 ≈ 4 << 64)
-int g_deal_step = 4;
-int g_sum_blocks = 32;  // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
-int g_hist_rounds = 4;  // (C2: 64 rounds 145 ms, 4 rounds 138 ms; 1 round 147 ms)
-int g_tail_step = 14;
-int g_tail_grid = 1024;
+// Launch constants (measured on MI355X).
+// deal_group maxima of K2 / the superstep kernel (C4 A/B, profiles/r03/c4_ab_deal.log: K2 16 ~ 64 < 1,
+// superstep 4 << 64)
+constexpr int kDealSlots = 16, kDealStep = 4;
+// supersteps >= kLateStep have small frontiers: at most kLateGrid blocks, the GPU left to the other batches
+constexpr int kLateStep = 14, kLateGrid = 1024;
 
 static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
   int64_t g = (items + per_block - 1) / per_block;
@@ -2525,9 +2219,9 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                                                 g.edst, g.grank, vm, em, cnt, snbr, smask, vadj, lab0, lab1, chg1, act2,
                                                 stepflag, hostflag, work, hv ? g.hv_of : nullptr, g.hv_seg,
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
-                                                uw0, uw1, cb1, ends ? 1 : 0, ccount, g_deal_slots, iem ? *ebp : bp0,
+                                                uw0, uw1, cb1, ends ? 1 : 0, ccount, kDealSlots, iem ? *ebp : bp0,
                                                 dense_div > 0 && (dense_div & kDense1) && ccount ? 1 : 0,
-                                                g_slot_labels ? g.ts_g : nullptr, mneg);
+                                                g.ts_g, mneg);
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
@@ -2549,32 +2243,24 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
-                    unsigned long long* work, int variant, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next,
+                    unsigned long long* work, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next,
                     const ChgBits& cb, int32_t* ccount, int dense_div, const int32_t* mneg) {
-  (void)variant;  // (8-vertex chunks, buffer-descriptor rows and a VGPR-capped build measured slower: removed)
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
   // A small graph's dense supersteps are latency-bound and share the GPU with the other batch
   // slots too: a 1,024-block cap measured 4 % faster on C2 (100k vertices) and 2 % slower on a
   // 4.7M-vertex C4-shaped graph, hence the size rule (RGPU_STEP_GRID overrides it).
-  const unsigned full = g_step_grid > 0 ? (unsigned)g_step_grid : (g.nv <= ((int64_t)1 << 21) ? 1024u : 4096u);
-  const unsigned cap = step >= g_tail_step ? (full < (unsigned)g_tail_grid ? full : (unsigned)g_tail_grid) : full;
-  const unsigned grid = grid_for(g.nv, 16, cap);
+  const unsigned full = g.nv <= ((int64_t)1 << 21) ? 1024u : 4096u;
+  const unsigned cap = step >= kLateStep ? (full < (unsigned)kLateGrid ? full : (unsigned)kLateGrid) : full;
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
 #define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.next, cb.clear, cb.words, ccount, dense_div, g_deal_step, (uw_cur && g_final_skip) ? mneg : nullptr
-  // work != null (profile runs): the counting instantiation; the timed runs use the lean one
-  // 2-vertex chunks (default): 73 VGPRs, 6 waves/SIMD against 97 and 4 for 4-vertex chunks; same-box
-  // A/B (tools/c4_ab.py, profiles/r03/c4_ab_step_ch.log): C4 369 -> 345 ms, C2 135 -> 120 ms.
-  // RGPU_STEP_CH=4 keeps the 4-vertex chunks.
+    cb.next, cb.clear, cb.words, ccount, dense_div, kDealStep, uw_cur ? mneg : nullptr
+  // work != null (profile runs): the counting instantiation; the timed runs use the lean one.
+  // 2-vertex chunks: 73 VGPRs, 6 waves/SIMD against 97 and 4 for 4-vertex chunks; same-box A/B
+  // (profiles/r03/c4_ab_step_ch.log): C4 369 -> 345 ms, C2 135 -> 120 ms.
   const unsigned grid2 = grid_for(g.nv, 8, cap);
-  if (g_step_ch == 4) {
-    if (work) k_cc_step2<4, false, 1, true><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-    else k_cc_step2<4, false, 1, false><<<grid, 256, 0, s>>>(RGPU_STEP_ARGS);
-  } else {
-    if (work) k_cc_step2<2, false, 1, true><<<grid2, 256, 0, s>>>(RGPU_STEP_ARGS);
-    else k_cc_step2<2, false, 1, false><<<grid2, 256, 0, s>>>(RGPU_STEP_ARGS);
-  }
+  if (work) k_cc_step2<2, false, 1, true><<<grid2, 256, 0, s>>>(RGPU_STEP_ARGS);
+  else k_cc_step2<2, false, 1, false><<<grid2, 256, 0, s>>>(RGPU_STEP_ARGS);
 #undef RGPU_STEP_ARGS
 }
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
@@ -2587,7 +2273,7 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
   (iem ? k_heavy_slots<true> : k_heavy_slots<false>)<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(
       g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
       snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own, g.ts_e, g.ts_nb, g.ts_t, tcut, ends ? 1 : 0, work,
-      iem ? *ebp : bp0, g_slot_labels ? g.ts_g : nullptr);
+      iem ? *ebp : bp0, g.ts_g);
 }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
@@ -2598,8 +2284,7 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
   k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
                                                              hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
-                                                             g.n_own, work, g_hub_pipe, vm,
-                                                             g_final_skip ? mneg : nullptr);
+                                                             g.n_own, work, vm, mneg);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
@@ -2611,27 +2296,6 @@ void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, co
                                                            g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst,
                                                            vm, em, g.ts_e, g.ts_nb, g.ts_t, tcut, ccount, dense_div,
                                                            g.n_own, work);
-}
-void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
-                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,
-                    int32_t* lab1, uint64_t* chg0, uint64_t* chg1, uint8_t* act0, uint8_t* act1,
-                    uint8_t* act2, int32_t* stepflag, int32_t* hostflag, int32_t* info,
-                    unsigned long long* work, unsigned long long* lanechg) {
-  cap = cap < kTailListCap ? cap : kTailListCap;
-#define RGPU_TAIL_ARGS r0, rmax, cap, g.nv, g.adj_off, vm, cnt, snbr, smask, lab0, lab1, chg0, chg1, act0, act1, \
-    act2, stepflag, hostflag, info, work, lanechg
-  k_cc_tail<false><<<1, kTailThreads, 0, s>>>(RGPU_TAIL_ARGS);
-#undef RGPU_TAIL_ARGS
-}
-void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, const uint64_t* vm,
-                    const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso) {
-  const unsigned grid = grid_for(nv, 64, 8192);
-  k_cc_hist<false><<<grid, 512, 0, s>>>(nv, hstride, nviews, vm, vadj, lab, hist, iso, g_hist_rounds);
-}
-void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
-                       unsigned long long* stats, unsigned int* iso) {
-  dim3 grid(grid_for(g.nv, 256, (unsigned)g_sum_blocks), (unsigned)nviews);
-  k_cc_summary<<<grid, 256, 0, s>>>(g.nv, hist, stats, iso);
 }
 int64_t deg_top_waves(int64_t nv) { return (int64_t)grid_for(nv, 4, 2048) * 4; }
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,

@@ -171,15 +171,6 @@ void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, co
                        const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm = nullptr,
                        const uint64_t* em = nullptr, int64_t tcut = INT64_MIN, const int32_t* ccount = nullptr,
                        int dense_div = 0, unsigned long long* work = nullptr);
-extern int g_sum_blocks;   // blocks per view of k_cc_summary (RGPU_SUMMARY_BLOCKS)
-extern int g_hist_rounds;  // label-dedup rounds per (view, chunk) in k_cc_hist (RGPU_HIST_ROUNDS)
-extern int g_deal_slots, g_deal_step;  // deal_group maxima (kernels.hip; RGPU_DEAL_SLOTS / RGPU_DEAL_STEP)
-extern int g_step_grid;  // max blocks of the superstep kernel (RGPU_STEP_GRID; 0 = by graph size)
-extern int g_slot_labels;  // K2 reads DevGraph.ts_g (RGPU_TSG)
-extern int g_step_ch;      // superstep chunk size (RGPU_STEP_CH)
-extern int g_hub_pipe;     // loads-first hub gather (RGPU_HUB_PIPE)
-extern int g_final_skip;   // final-label skip in the superstep kernel and the hub gather (RGPU_FINAL)
-extern int g_tail_step, g_tail_grid;  // supersteps >= tail_step use at most tail_grid blocks
 // uniform label words (kernels.hip, kMixed): rows of the uniform vertices written into lab
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab);
 // component counts from the uniform words (one partition): counts = zeroed [nv][64] rows, kept
@@ -213,22 +204,11 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
-                    unsigned long long* work, int variant, unsigned long long* lanechg,
+                    unsigned long long* work, unsigned long long* lanechg,
                     int32_t* hbest = nullptr, const int32_t* uw_cur = nullptr, int32_t* uw_next = nullptr,
                     const ChgBits& cb = ChgBits(), int32_t* ccount = nullptr, int dense_div = 0,
                     const int32_t* mneg = nullptr);
-// Many late supersteps in one single-workgroup launch while the frontier stays below `cap`
-// vertices; info[0] <- last superstep executed (host-mapped).
-void launch_cc_tail(hipStream_t s, int r0, int rmax, int cap, const DevGraph& g, const uint64_t* vm,
-                    const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, int32_t* lab0,
-                    int32_t* lab1, uint64_t* chg0, uint64_t* chg1, uint8_t* act0, uint8_t* act1,
-                    uint8_t* act2, int32_t* stepflag, int32_t* hostflag, int32_t* info,
-                    unsigned long long* work, unsigned long long* lanechg);
 constexpr int kIsoWords = 64 * 64;  // isolated-member counts [64 shards][64 views]
-void launch_cc_hist(hipStream_t s, int64_t nv, int64_t hstride, int nviews, const uint64_t* vm,
-                    const uint64_t* vadj, const int32_t* lab, int32_t* hist, unsigned int* iso);
-void launch_cc_summary(hipStream_t s, const DevGraph& g, int nviews, int32_t* hist,
-                       unsigned long long* stats, unsigned int* iso);
 // DegreeRanking top-20 per view (kernels.hip k_deg_top_merge): key = in-degree << 32 | ~label
 constexpr int kTop = 20;
 struct DegTop {

@@ -57,6 +57,9 @@ constexpr int kWorkFields = 8;  // kernels.hip add_work
 constexpr int kWorkWords = kMaxSteps * 64 * kWorkFields;
 constexpr int64_t kPad = 64;  // tail padding of per-vertex / per-slot batch arrays
 constexpr int kMaxSlots = 4;  // batches in flight (one HIP stream each; GPU_MAX_HW_QUEUES = 4)
+// supersteps per host enqueue: the first chunk of a batch (capped by the step count its window's
+// previous batch halted at), then the rest
+constexpr int kChunk0 = 12, kChunk = 8;
 
 struct Slot {
   // buffers allocated for this slot (slots are allocated lazily: a run uses min(slots, batches))
@@ -90,9 +93,7 @@ struct Slot {
   uint64_t* psmask = nullptr;
   int32_t* h_stepcnt = nullptr;   // host-mapped superstep flags, written by the kernels
   int32_t* d_hostflag = nullptr;  // device address of h_stepcnt
-  int32_t* h_tail = nullptr;      // host-mapped: [0] last superstep a k_cc_tail launch executed
-  int32_t* d_tail = nullptr;
-  unsigned int* iso = nullptr;    // isolated-member counts [64 shards][64 views] (k_cc_hist)
+  unsigned int* iso = nullptr;    // isolated-member counts [64 shards][64 views] (k_cc_count)
   HeavyBuf hv;                    // heavy-vertex segment state (graphs with hubs)
   // BinaryDefusion (diffusion.hip): infected views, views infected last / this step, step rows
   uint64_t *dinf = nullptr, *dfront[2] = {nullptr, nullptr};
@@ -103,8 +104,6 @@ struct Slot {
   // state of the batch in flight
   int batch = -1, phase = 0, r_launched = 0, r_final = 0, kb = 0;
   int64_t tcut = INT64_MIN;  // the batch's window cut for time-ordered slots (start_batch)
-  bool tail_pending = false;       // a k_cc_tail launch is in the last enqueued chunk
-  uint8_t by_tail[kMaxSteps] = {}; // superstep r ran inside k_cc_tail (bytes accounting)
   uint64_t evseq = 0;  // order in which slot events were recorded (wait on the oldest)
 };
 
@@ -196,28 +195,18 @@ struct rgpu_ctx {
   std::vector<void*> slot_allocs;
   int64_t cap_nv = 0, cap_ne = 0, cap_nin = 0;
   Slot slot[kMaxSlots];
-  int nslots = 2;
-  bool hostflags = true;                // superstep flags via host-mapped memory (else copies)
-  bool tail_on = false;                 // RGPU_TAIL: late supersteps in one-workgroup k_cc_tail launches
-  bool uw_on = true;                    // RGPU_UW: uniform label words (one partition, no tail kernel)
+  int nslots = 3;                       // batches in flight (2 / 4 measured slower on C4)
   bool prof_lean = false;               // RGPU_PROF_LEAN (work_buf)
   int inject_fail = 0;                  // RGPU_INJECT_FAIL=n (tests): the n-th batch start of a run throws
   int dense = -1;                       // RGPU_DENSE: dense-step divisor (kernels.hip dense_rule; -1 by size)
-  int cb_on = 1;                        // RGPU_CHGBITS=0: no changed bits (kernels.hpp ChgBits)
   bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
-  int tail_cap = 256;                   // RGPU_TAIL_CAP: widest frontier the tail kernel takes
-  int64_t tail_maxv = 4 << 20;          // RGPU_TAIL_MAXV: no tail kernel above this many vertices
   std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
   struct StepRec { int batch, step; unsigned long long pv, ps; int changed; unsigned long long pg; };
   std::vector<StepRec> steprec;
   bool wmajor = true;                   // RGPU_WMAJOR: window-major batches when 2 <= W <= kMaxPlanes
-  bool poll = true;                     // RGPU_POLL: spin on event queries instead of blocking
   bool hostprof = false;                // RGPU_HOSTPROF: print host-side scheduling times
   int iv_max = 32;                      // RGPU_IVMAX: K1 interval form up to this many points (< 0 off)
   int heavy_t = 2048;                   // RGPU_HEAVY: static slots above which a vertex is split (0 off)
-  bool tslots_on = true;                // RGPU_TSLOTS: time-ordered static slots (tslots.hip)
-  bool iem_on = true;                   // RGPU_IEM: CC's K2 computes edge bits inline (no K1 edge masks)
-  bool dense1 = true;                   // RGPU_DENSE1: K2 is a dense step (kernels.hpp kDense1)
   MaskSet mset[kMaskSets];
   int grp_last[kMaxPlanes] = {};        // supersteps of the last batch of each window group
   // last run: views (hop, win) -> batch (hop/K)*G + win/gsize, lane (win%gsize)*K + hop%K
@@ -304,7 +293,6 @@ void release_slots(rgpu_ctx* c) {
   c->d_vid = nullptr;
   for (Slot& s : c->slot) {
     if (s.h_stepcnt) (void)hipHostFree(s.h_stepcnt);
-    if (s.h_tail) (void)hipHostFree(s.h_tail);
     if (s.h_stats) (void)hipHostFree(s.h_stats);
     if (s.h_work) (void)hipHostFree(s.h_work);
     if (s.h_top) (void)hipHostFree(s.h_top);
@@ -348,9 +336,6 @@ void run_check(hipStream_t st, const char* what, F launch) {
   if (!msg.empty()) throw HipFail{std::string("RGPU_CHECK ") + what + ":" + msg, RGPU_EHIP};
 }
 
-// uniform label words (kernels.hip): not with the tail kernel (it writes rows only).  Partitioned:
-// ghosts: words from uniform records, kMixed for mixed ones, kGhostQuiet otherwise (start_batch, k_xclear)
-bool use_uw(const rgpu_ctx* c) { return c->uw_on && !c->tail_on; }
 
 // The work-counter buffer of a profile run.  RGPU_PROF_LEAN=1: none, so the superstep and K2
 // kernels run their lean instantiations (the ones timed runs use) under the profile events; a
@@ -359,14 +344,13 @@ unsigned long long* work_buf(const rgpu_ctx* c, const Slot& s) {
   return c->profile && !c->prof_lean ? s.work : nullptr;
 }
 
-// dense-step divisor (kernels.hip dense_rule; RGPU_DENSE, 0 = off).  Not with the tail kernel,
-// which builds its frontier lists from the flags.
+// dense-step divisor (kernels.hip dense_rule; RGPU_DENSE, 0 = off); K2 is then dense too (kDense1:
+// step 2 visited exactly as many vertices as step 1 in all 15 C4 batches).
 // Default 4 on graphs of more than 2M vertices (C4: 529 -> 507 ms, `heavy` 103 -> 89 ms; 16:
 // 536 ms); off below (C2: 127.5 -> 132.3 ms with it: a small graph's flags are cached anyway).
 int dense_div(const rgpu_ctx* c) {
-  if (c->tail_on) return 0;
   const int d = c->dense >= 0 ? c->dense : (c->g.nv > ((int64_t)1 << 21) ? 4 : 0);
-  return d > 0 && c->dense1 ? (d | kDense1) : d;
+  return d > 0 ? (d | kDense1) : d;
 }
 
 // the batch's per-view minimum member labels (kernels.hpp kMinShards), behind the changed-vertex
@@ -378,7 +362,7 @@ int32_t* min_labels(const rgpu_ctx* c, const Slot& s) {
 // changed bits of superstep r (with uniform words; RGPU_CHGBITS=0 turns them off)
 ChgBits chg_bits(const rgpu_ctx* c, const Slot& s, int r) {
   ChgBits b;
-  if (!use_uw(c) || !c->cb_on || !s.cb[0]) return b;
+  if (!s.cb[0]) return b;
   // Written by the superstep kernels, read by the heavy gather only, and only when there are
   // heavy vertices.  The superstep kernel reading them measured slower on C4 (cc_step 263 ->
   // 301 ms serial; the bit probe then the words vs one change word) and on C2; the heavy
@@ -453,8 +437,6 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       HIPCHK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
       HIPCHK(hipHostMalloc((void**)&s.h_stepcnt, sizeof(int32_t) * kMaxSteps, hipHostMallocMapped));
       HIPCHK(hipHostGetDevicePointer((void**)&s.d_hostflag, s.h_stepcnt, 0));
-      HIPCHK(hipHostMalloc((void**)&s.h_tail, sizeof(int32_t) * 4, hipHostMallocMapped));
-      HIPCHK(hipHostGetDevicePointer((void**)&s.d_tail, s.h_tail, 0));
       HIPCHK(hipHostMalloc((void**)&s.h_stats, sizeof(unsigned long long) * kStatWords));
       HIPCHK(hipHostMalloc((void**)&s.h_work, sizeof(unsigned long long) * kWorkWords));
       s.stepcnt = dalloc<int32_t>(L, kMaxSteps);
@@ -471,10 +453,9 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       s.lab[1] = dalloc<int32_t>(L, rows + kPad * kViews);
       s.uw[0] = dalloc<int32_t>(L, nv + kPad);
       s.uw[1] = dalloc<int32_t>(L, nv + kPad);
-      if (use_uw(c) || c->partitioned) {  // component counts at the root's row (zero between batches)
-        s.counts = dalloc<int32_t>(L, rows + kPad * kViews);
-        HIPCHK(hipMemset(s.counts, 0, sizeof(int32_t) * (rows + kPad * kViews)));
-      }
+      // component counts at the root's row (zero between batches)
+      s.counts = dalloc<int32_t>(L, rows + kPad * kViews);
+      HIPCHK(hipMemset(s.counts, 0, sizeof(int32_t) * (rows + kPad * kViews)));
       s.chg[0] = dalloc<uint64_t>(L, nv + kPad);
       s.chg[1] = dalloc<uint64_t>(L, nv + kPad);
       HIPCHK(hipMemset(s.chg[0], 0, sizeof(uint64_t) * (nv + kPad)));
@@ -607,12 +588,11 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
     eb = take_event(c);
     HIPCHK(hipEventRecord(ea, s.stream));
   }
-  const bool uw = use_uw(c);
   for (int r = s.r_launched + 1; r <= last; r++) {
     if (rc.algo == RGPU_ALGO_VP) {
       timed_launch(c, si, KID_VP, 0.0, [&] {
         launch_vp_step(s.stream, r, g, c->vp, s.vm, s.cnt, s.snbr, s.smask, s.vst[(r - 1) & 1], s.vst[r & 1],
-                       s.chg[(r - 1) & 1], s.chg[r & 1], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
+                       s.chg[(r - 1) & 1], s.chg[r & 1], s.stepcnt, s.d_hostflag,
                        s.stats + kLaneOff);
       }, r, false);
       continue;
@@ -622,22 +602,22 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
         launch_diff_step(s.stream, r, g, c->d_vid, s.vm, s.em, s.dinf, s.dfront[(r - 1) & 1], s.dfront[r & 1],
                          s.dact[r % 3], s.dact[(r + 1) % 3], s.dact[(r + 2) % 3],
                          (rc.flags & RGPU_RUN_RETAIN) ? s.dstep : nullptr, s.salts, c->diff_coin, s.stepcnt,
-                         c->hostflags ? s.d_hostflag : nullptr, s.stats);
+                         s.d_hostflag, s.stats);
       }, r, false);
       continue;
     }
     if (hv)  // heavy vertices: segment minima before the step, neighbour marking after it
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[(r - 1) & 1], s.chg[(r - 1) & 1], s.act[r % 3],
-                            s.stepcnt, r, s.hv, uw ? s.uw[(r - 1) & 1] : nullptr, chg_bits(c, s, r).prev, s.ccount,
+                            s.stepcnt, r, s.hv, s.uw[(r - 1) & 1], chg_bits(c, s, r).prev, s.ccount,
                             dense_div(c), work_buf(c, s), s.vm, min_labels(c, s));
       }, r, per_launch);
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
                      s.chg[(r - 1) & 1], s.chg[r & 1], s.act[r % 3], s.act[(r + 1) % 3],
-                     s.act[(r + 2) % 3], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
-                     work_buf(c, s), 0, s.stats + kLaneOff,
-                     hv ? s.hv.best : nullptr, uw ? s.uw[(r - 1) & 1] : nullptr, uw ? s.uw[r & 1] : nullptr,
+                     s.act[(r + 2) % 3], s.stepcnt, s.d_hostflag,
+                     work_buf(c, s), s.stats + kLaneOff,
+                     hv ? s.hv.best : nullptr, s.uw[(r - 1) & 1], s.uw[r & 1],
                      chg_bits(c, s, r), s.ccount, dense_div(c), min_labels(c, s));
     }, r, per_launch);
     if (hv)
@@ -652,23 +632,6 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
                         s.batch, s.r_launched + 1, ea, eb, 0.0});
   }
   s.r_launched = last;
-  if (rc.algo == RGPU_ALGO_CC && c->tail_on && g.n_seg == 0 && g.nv <= c->tail_maxv &&
-      s.r_launched < rc.max_steps) {
-    // the rest of the supersteps in one workgroup while the frontier stays narrow; it stops
-    // (and the host continues with full-grid launches) at the first wide frontier
-    const int r0 = s.r_launched + 1;
-    s.h_tail[0] = -1;
-    timed_launch(c, si, KID_TAIL, 0.0, [&] {
-      launch_cc_tail(s.stream, r0, rc.max_steps, c->tail_cap, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[0],
-                     s.lab[1], s.chg[0], s.chg[1], s.act[0], s.act[1], s.act[2], s.stepcnt,
-                     c->hostflags ? s.d_hostflag : nullptr, s.d_tail, c->profile ? s.work : nullptr,
-                     s.stats + kLaneOff);
-    }, r0);
-    s.tail_pending = true;
-  }
-  if (!c->hostflags)
-    HIPCHK(hipMemcpyAsync(s.h_stepcnt, s.stepcnt, sizeof(int32_t) * kMaxSteps, hipMemcpyDeviceToHost,
-                          s.stream));
   if (c->profile && rc.algo == RGPU_ALGO_CC)
     HIPCHK(hipMemcpyAsync(s.h_work, s.work, sizeof(unsigned long long) * kWorkWords,
                           hipMemcpyDeviceToHost, s.stream));
@@ -736,27 +699,16 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
     const int nviews = rc.K * rc.gsize;
     if (c->check)
       run_check(s.stream, "final labels", [&](unsigned long long* bad) {
-        launch_check_labels(s.stream, c->partitioned ? c->pk.n_own : g.nv, s.vm, use_uw(c) ? s.uw[s.r_final & 1] : nullptr,
+        launch_check_labels(s.stream, c->partitioned ? c->pk.n_own : g.nv, s.vm, s.uw[s.r_final & 1],
                             lab, bad, g.grank);
       });
-    if (use_uw(c) && !c->partitioned) {
-      const int32_t* uw = s.uw[s.r_final & 1];
-      if (rc.flags & RGPU_RUN_RETAIN) launch_uw_rows(s.stream, g.nv, s.vm, uw, lab);  // full rows to the host
-      timed_launch(c, si, KID_HIST, 28.0 * g.nv,
-                   [&] { launch_cc_count(s.stream, g.nv, nviews, s.vm, s.vadj, uw, lab, s.counts, s.iso); });
-      timed_launch(c, si, KID_SUMMARY, 20.0 * g.nv,
-                   [&] { launch_cc_roots(s.stream, g.nv, nviews, s.vm, s.vadj, uw, lab, s.counts, s.stats, s.iso,
-                                           s.r_final >= 1 && s.r_final >= rc.max_steps, g.grank); });
-      finish_tail(c, si, rc);
-      return;
-    }
-    // the other label buffer is free now: it becomes the view-major histogram (keeps the
-    // batch's working set inside the Infinity Cache with several batches in flight)
-    int32_t* hist = s.lab[(s.r_final + 1) & 1];
-    HIPCHK(hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)g.nv * kViews, s.stream));
-    timed_launch(c, si, KID_HIST, 12.0 * g.nv, [&] { launch_cc_hist(s.stream, g.nv, g.nv, nviews, s.vm, s.vadj, lab, hist, s.iso); });
-    timed_launch(c, si, KID_SUMMARY, 8.0 * g.nv * nviews,
-                 [&] { launch_cc_summary(s.stream, g, nviews, hist, s.stats, s.iso); });
+    const int32_t* uw = s.uw[s.r_final & 1];
+    if (rc.flags & RGPU_RUN_RETAIN) launch_uw_rows(s.stream, g.nv, s.vm, uw, lab);  // full rows to the host
+    timed_launch(c, si, KID_HIST, 28.0 * g.nv,
+                 [&] { launch_cc_count(s.stream, g.nv, nviews, s.vm, s.vadj, uw, lab, s.counts, s.iso); });
+    timed_launch(c, si, KID_SUMMARY, 20.0 * g.nv,
+                 [&] { launch_cc_roots(s.stream, g.nv, nviews, s.vm, s.vadj, uw, lab, s.counts, s.stats, s.iso,
+                                         s.r_final >= 1 && s.r_final >= rc.max_steps, g.grank); });
   }
   finish_tail(c, si, rc);
 }
@@ -822,8 +774,6 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   s.kb = bp.K;
   s.r_launched = 0;
   s.r_final = 0;
-  s.tail_pending = false;
-  std::memset(s.by_tail, 0, sizeof(s.by_tail));
   std::memset(s.h_stepcnt, 0, sizeof(int32_t) * kMaxSteps);  // slot idle: no kernel writes it
   BatchClear clr;
   clr.stats = s.stats;
@@ -858,7 +808,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   // slots (one add point, no endpoint deaths) for the batch's own windows from the time-ordered
   // slot words, so K1 writes edge masks only for the other edges (all of them for the |E_w|
   // counts of an RGPU_RUN_EDGE_COUNTS run).  The partitioned ghost marking (k_xmark) does the same.
-  const bool iem = c->iem_on && rc.algo == RGPU_ALGO_CC && g.ts_t;
+  const bool iem = rc.algo == RGPU_ALGO_CC && g.ts_t;
   BatchParams ebp = bp;  // the batch's edge windows, view bit w*KS + k
   if (rc.G > 1) {
     ebp.W = 1;
@@ -936,7 +886,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     return;
   }
   if (rc.algo == RGPU_ALGO_CC) {
-    if (c->partitioned && use_uw(c) && g.nv > c->pk.n_own)  // ghosts: quiet until a record arrives (kGhostQuiet)
+    if (c->partitioned && g.nv > c->pk.n_own)  // ghosts: quiet until a record arrives (kGhostQuiet)
       for (int p = 0; p < 2; p++)
         HIPCHK(hipMemsetAsync(s.uw[p] + c->pk.n_own, 0x7f, sizeof(int32_t) * (g.nv - c->pk.n_own), s.stream));
     // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
@@ -950,15 +900,15 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
                    });
     timed_launch(c, si, KID_SLOTS, b2, [&] {  // (partitioned: owned vertices only, gk)
       launch_cc_slots(s.stream, gk, tcut, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
-                      s.chg[1], s.act[2], s.stepcnt, c->hostflags ? s.d_hostflag : nullptr,
-                      work_buf(c, s), s.hv, s.stats + kLaneOff, use_uw(c) ? s.uw[0] : nullptr,
-                      use_uw(c) ? s.uw[1] : nullptr, chg_bits(c, s, 1).next, ends, s.ccount, iem ? &ebp : nullptr,
+                      s.chg[1], s.act[2], s.stepcnt, s.d_hostflag,
+                      work_buf(c, s), s.hv, s.stats + kLaneOff, s.uw[0],
+                      s.uw[1], chg_bits(c, s, 1).next, ends, s.ccount, iem ? &ebp : nullptr,
                       dense_div(c), min_labels(c, s));
     });
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
-        launch_check_slots(s.stream, gk.nv, g.adj_off, s.vm, s.cnt, s.snbr, use_uw(c) ? s.uw[0] : nullptr,
-                           use_uw(c) ? s.uw[1] : nullptr, bad, g.grank);
+        launch_check_slots(s.stream, gk.nv, g.adj_off, s.vm, s.cnt, s.snbr, s.uw[0],
+                           s.uw[1], bad, g.grank);
       });
     if (g.n_seg > 0 && !c->partitioned)  // partitioned: after the step's records are in
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
@@ -976,7 +926,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       s.r_final = 0;
       finish_batch(c, si, rc);
     } else {
-      // first chunk: up to the step the group's previous batch halted at (then the tail kernel)
+      // first chunk: up to the step the group's previous batch halted at
       const int last = c->grp_last[grp];
       launch_chunk(c, si, rc, last > 0 ? std::max(1, std::min(rc.chunk0, last)) : rc.chunk0);
     }
@@ -1053,7 +1003,7 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
     // neighbour 4, last-add time 8) and the two random mask words em[e], vm[nbr] (32 B; CSR
     // order: offsets 8 instead of 16); per kept slot nbr + mask written (12 B); uniform words
     // (4 B) and 64-B row lines written.  Supersteps r >= 2: frontier flag read + flag cleared
-    // two steps ahead (2 B per vertex; a tail-kernel step reads none); per visited vertex vm,
+    // two steps ahead (2 B per vertex); per visited vertex vm,
     // cnt, adj_off, own change and uniform words in, change word out (40 B); per kept slot of
     // a visited vertex nbr + mask (12 B) and the neighbour's uniform word (4 B; without uniform
     // words its change word, 8 B); per slot of a mixed neighbour its change word (8 B); per
@@ -1082,10 +1032,10 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
       c->st.kernel_bytes[KID_HEAVY] += 288.0 * wsum(0, 0) + 4.125 * wsum(0, 1) + 12.0 * wsum(0, 2) +
                                        8.0 * wsum(0, 3) + 4.0 * wsum(0, 4) + 12.0 * wsum(0, 5) +
                                        32.0 * wsum(0, 6) + 12.0 * wsum(0, 7);
-      const double per_slot = use_uw(c) ? 16.0 : 20.0;
+      const double per_slot = 16.0;
       for (int r = 2; r <= s.r_final; r++)
-        c->st.kernel_bytes[s.by_tail[r] ? KID_TAIL : KID_STEP] +=
-            (s.by_tail[r] ? 0.0 : 2.0 * c->g.nv) + 40.0 * (double)wsum(r, 0) + per_slot * (double)wsum(r, 1) +
+        c->st.kernel_bytes[KID_STEP] +=
+            2.0 * c->g.nv + 40.0 * (double)wsum(r, 0) + per_slot * (double)wsum(r, 1) +
             8.0 * (double)wsum(r, 4) + 4.0 * (double)wsum(r, 3) + 64.0 * (double)(wsum(r, 5) + wsum(r, 6)) +
             4.0 * (double)wsum(r, 7);
       if (!c->trace_path.empty())
@@ -1138,14 +1088,6 @@ int run_impl(rgpu_ctx* c, RunCfg& rc) {
       HIPCHK(q);
       progressed = true;
       if (s.phase == 1) {
-        if (s.tail_pending) {
-          const int rd = s.h_tail[0];
-          if (rd < s.r_launched || rd > rc.max_steps)
-            throw HipFail{"k_cc_tail reported superstep " + std::to_string(rd)};
-          for (int r = s.r_launched + 1; r <= rd; r++) s.by_tail[r] = 1;
-          s.r_launched = rd;
-          s.tail_pending = false;
-        }
         int r0 = 0;
         for (int r = 1; r <= s.r_launched; r++)
           if (s.h_stepcnt[r] == 0) { r0 = r; break; }
@@ -1164,13 +1106,7 @@ int run_impl(rgpu_ctx* c, RunCfg& rc) {
         if (c->slot[si].phase != 0 && (oldest < 0 || c->slot[si].evseq < c->slot[oldest].evseq)) oldest = si;
       // nothing ready.  Polling (default) reacts to whichever slot finishes first; blocking on
       // the oldest event left the other slots idle behind it (-8 % on the C2 query)
-      if (oldest >= 0 && !c->poll) {
-        const auto t0 = clk::now();
-        HIPCHK(hipEventSynchronize(c->slot[oldest].ev));
-        t_block += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-      } else {
-        __builtin_ia32_pause();
-      }
+      if (oldest >= 0) __builtin_ia32_pause();
     }
   }
   if (c->hostprof)
@@ -1198,9 +1134,8 @@ DevGraph owned_view(const rgpu_ctx* c) {
   return g;
 }
 
-// record buffers grow on demand (the counts are known before anything is written into them);
-// RGPU_XREC_SLACK / RGPU_XREC_INIT (records of headroom per peer / first-guess records per
-// boundary entry) exist so that tests can force the growth paths
+// record buffers grow on demand (the counts are known before anything is written into them):
+// records of headroom per peer / first-guess records per boundary entry (RGPU_XREC_TINY)
 int g_xrec_slack = 1024, g_xrec_init = 2;
 template <class T>
 void grow_regions(T** buf, int64_t* cap, const int64_t* need, int np, hipStream_t s) {
@@ -1329,7 +1264,7 @@ void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
   }
   const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
   timed_launch(c, si, KID_XPACK, 0.0, [&] { launch_xpack_rec(s.stream, L, X.xsend, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
-                   s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
+                   s.lab[r & 1], s.uw[r & 1], xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
                    c->pk.n_own); });
   launch_xcounts(s.stream, P, c->part, xs.scnt, s.stepcnt + r, xs.xab);
   HIPCHK(hipGetLastError());
@@ -1360,7 +1295,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     grow_regions(&xs.sbuf, xs.scap, sent, P, s.stream);
     const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
     timed_launch(c, si, KID_XPACK, 0.0, [&] { launch_xpack_rec(s.stream, L, X.xsend, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
-                     s.lab[r & 1], use_uw(c) ? s.uw[r & 1] : nullptr, xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
+                     s.lab[r & 1], s.uw[r & 1], xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
                    c->pk.n_own); });
     HIPCHK(hipMemsetAsync(xs.scnt, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
   }
@@ -1372,7 +1307,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   const int par = r & 1;
   // ghosts whose words records of step r-2 set (their records are still in rbuf[par])
   timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par],
-                use_uw(c) ? s.uw[par] : nullptr); });
+                s.uw[par]); });
   bool rover = false;
   for (int q = 0; q < P; q++) rover |= recv[q] > xs.rcap[q];
   if (rover) {  // a larger layout for both parities; the other parity's records of step r-1 are
@@ -1409,7 +1344,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   }
   std::copy(recv, recv + kMaxParts, xs.rcnt[par]);
   const XPeers Lin = peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]);
-  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par], use_uw(c) ? s.uw[par] : nullptr,
+  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par], s.uw[par],
                      chg_bits(c, s, r).next); });
   timed_launch(c, si, KID_XMARK, 0.0, [&] { launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3], s.tcut,
                s.iem ? &s.ebp : nullptr, s.ccount, dense_div(c), r); });
@@ -1428,13 +1363,13 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (hv)
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[n % 3], s.stepcnt, n, s.hv,
-                          use_uw(c) ? s.uw[r & 1] : nullptr, chg_bits(c, s, n).prev, s.ccount, dense_div(c));
+                          s.uw[r & 1], chg_bits(c, s, n).prev, s.ccount, dense_div(c));
     });
   timed_launch(c, si, KID_STEP, 0.0, [&] {
     launch_cc_step(s.stream, n, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[r & 1], s.lab[n & 1], s.chg[r & 1],
                    s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
-                   work_buf(c, s), 0, s.stats + kLaneOff, hv ? s.hv.best : nullptr,
-                   use_uw(c) ? s.uw[r & 1] : nullptr, use_uw(c) ? s.uw[n & 1] : nullptr, chg_bits(c, s, n), s.ccount,
+                   work_buf(c, s), s.stats + kLaneOff, hv ? s.hv.best : nullptr,
+                   s.uw[r & 1], s.uw[n & 1], chg_bits(c, s, n), s.ccount,
                    dense_div(c));
   }, n);
   part_post_step(c, si, rc, n);
@@ -1455,7 +1390,7 @@ void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc) {
     for (int q = 0; q < P; q++) need[q] = no / 16;
     grow_regions(&xs.hsbuf, xs.hscap, need, P, s.stream);
   }
-  const int32_t* uw = use_uw(c) ? s.uw[s.r_final & 1] : nullptr;
+  const int32_t* uw = s.uw[s.r_final & 1];
   if (uw && (rc.flags & RGPU_RUN_RETAIN))  // full rows of the owned vertices for the host
     launch_uw_rows(s.stream, no, s.vm, uw, s.lab[s.r_final & 1]);
   const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);
@@ -1485,7 +1420,7 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
     recv[q] = q == me ? 0 : xs.h_xab[2 * P + 2 * q];
     over |= sent[q] > xs.hscap[q];
   }
-  const int32_t* uw = use_uw(c) ? s.uw[s.r_final & 1] : nullptr;
+  const int32_t* uw = s.uw[s.r_final & 1];
   if (over) {  // the records again into a larger buffer (the local counts are done); the LDS cache
                // may fold them differently, but the sums per (label, view) are the same
     HIPCHK(hipMemsetAsync(xs.htot, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
@@ -1528,7 +1463,7 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
   // the batch's ghost change words back to zero (the next batch's ghosts start clean)
   for (int par = 0; par < 2; par++) {
     timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par],
-                use_uw(c) ? s.uw[par] : nullptr); });
+                s.uw[par]); });
     std::fill(xs.rcnt[par], xs.rcnt[par] + kMaxParts, 0);
   }
   HIPCHK(hipGetLastError());
@@ -1773,29 +1708,18 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->nparts = num_partitions;
   c->device = device;
   c->partitioned = num_partitions > 1 || env_int("RGPU_PARTITIONED", 0) != 0;
-  c->nslots = std::max(1, std::min(kMaxSlots, env_int("RGPU_SLOTS", 3)));
-  if (env_int("RGPU_STEP_GRID", 0) > 0) g_step_grid = env_int("RGPU_STEP_GRID", 0);
-  if (env_int("RGPU_HIST_ROUNDS", 0) > 0) g_hist_rounds = env_int("RGPU_HIST_ROUNDS", 0);
-  if (env_int("RGPU_SUMMARY_BLOCKS", 0) > 0) g_sum_blocks = env_int("RGPU_SUMMARY_BLOCKS", 0);
-  if (env_int("RGPU_TAIL_STEP", 0) > 0) g_tail_step = env_int("RGPU_TAIL_STEP", 0);
-  if (env_int("RGPU_TAIL_GRID", 0) > 0) g_tail_grid = env_int("RGPU_TAIL_GRID", 0);
-  c->hostflags = env_int("RGPU_HOSTFLAG", 1) != 0;
-  c->tail_on = env_int("RGPU_TAIL", 0) != 0;
-  c->uw_on = env_int("RGPU_UW", 1) != 0;
-  c->cb_on = env_int("RGPU_CHGBITS", 1);
   c->check = env_int("RGPU_CHECK", 0) != 0;
   c->wmajor = env_int("RGPU_WMAJOR", 1) != 0;
-  c->poll = env_int("RGPU_POLL", 1) != 0;
   c->hostprof = env_int("RGPU_HOSTPROF", 0) != 0;
   c->iv_max = env_int("RGPU_IVMAX", 32);
   c->heavy_t = env_int("RGPU_HEAVY", 2048);
-  c->tslots_on = env_int("RGPU_TSLOTS", 1) != 0;
-  c->tail_cap = std::max(1, env_int("RGPU_TAIL_CAP", 256));
-  c->tail_maxv = std::max(0, env_int("RGPU_TAIL_MAXV", 4 << 20));
   c->delta_on = env_int("RGPU_DELTA", 1) != 0;
   c->delta_host = env_int("RGPU_DELTA", 1) == 2;
-  g_xrec_slack = std::max(1, env_int("RGPU_XREC_SLACK", 1024));
-  g_xrec_init = std::max(0, env_int("RGPU_XREC_INIT", 2));
+  {  // RGPU_XREC_TINY (tests): record buffers start tiny, so that every growth path runs
+    const bool tiny = env_int("RGPU_XREC_TINY", 0) != 0;
+    g_xrec_slack = tiny ? 1 : 1024;
+    g_xrec_init = tiny ? 0 : 2;
+  }
   if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
   *out = c;
@@ -1911,7 +1835,7 @@ void build_heavy(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L, const std::vec
 // K2's time-ordered static slots (tslots.hip), built on the device after the adjacency
 void build_tslots(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L) {
   const int64_t n = g.ne + g.n_in;
-  if (!c->tslots_on || n <= 0 || n > (int64_t)INT32_MAX) return;
+  if (n <= 0 || n > (int64_t)INT32_MAX) return;  // (int32 slot words)
   int32_t* e = dalloc<int32_t>(L, n);
   int32_t* nb = dalloc<int32_t>(L, n);
   int64_t* t = dalloc<int64_t>(L, n);
@@ -2521,28 +2445,12 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     rc.wval[w] = n_w ? windows[w] : -1;
     rc.thr_v[w] = run_min;  // WindowLens.shrinkWindow keeps the running intersection
   }
-  rc.chunk0 = std::max(1, env_int("RGPU_CHUNK0", 12));
-  rc.chunk = std::max(1, env_int("RGPU_CHUNK", 8));
-  // superstep launch knobs are re-read per run, so that one sealed graph can be A/B-timed
-  // under several settings in one process (tools/c4_ab.py); unset = the defaults
-  c->cb_on = env_int("RGPU_CHGBITS", 1);
+  rc.chunk0 = kChunk0;
+  rc.chunk = kChunk;
+  // knobs re-read per run (profile passes and tests on one sealed graph)
   c->prof_lean = env_int("RGPU_PROF_LEAN", 0) != 0;
   c->inject_fail = env_int("RGPU_INJECT_FAIL", 0);
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
-  c->iem_on = env_int("RGPU_IEM", 1) != 0;
-  c->dense1 = env_int("RGPU_DENSE1", 1) != 0;
-  g_step_grid = std::max(0, env_int("RGPU_STEP_GRID", 0));
-  g_slot_labels = env_int("RGPU_TSG", 1);
-  g_step_ch = env_int("RGPU_STEP_CH", 2) == 4 ? 4 : 2;  // superstep chunk: 2 (default) or 4 vertices
-  g_hub_pipe = env_int("RGPU_HUB_PIPE", 1);
-  g_final_skip = env_int("RGPU_FINAL", 1);
-  {  // powers of two up to 64
-    auto pow2 = [](int x) { int g = 1; while (g < x && g < 64) g <<= 1; return g; };
-    g_deal_slots = pow2(env_int("RGPU_DEAL_SLOTS", 16));
-    g_deal_step = pow2(env_int("RGPU_DEAL_STEP", 4));
-  }
-  g_tail_step = std::max(2, env_int("RGPU_TAIL_STEP", 14));
-  g_tail_grid = std::max(1, env_int("RGPU_TAIL_GRID", 1024));
   try {
     HIPCHK(hipSetDevice(c->device));
     {

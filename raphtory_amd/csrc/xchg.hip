@@ -582,7 +582,7 @@ XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, c
   if (hipMemsetAsync(flag, 0, sizeof(int32_t) * (n_own + 1), s) != hipSuccess) throw std::runtime_error("build_xsend");
   k_xsend_flag<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, flag);
   size_t tb = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, pos, (int)(n_own + 1), s);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, pos, (int)(n_own + 1), s);
   void* tmp = alloc(T, tb);
   if (hipcub::DeviceScan::ExclusiveSum(tmp, tb, flag, pos, (int)(n_own + 1), s) != hipSuccess)
     throw std::runtime_error("build_xsend: scan");

@@ -1,8 +1,11 @@
-"""Late supersteps in the one-workgroup tail kernel (k_cc_tail) against the full-grid superstep
-kernel and the CPU oracle.  The two kernels share buffers and hand over at any superstep, so
-every combination of where the tail starts (RGPU_CHUNK0) and how narrow a frontier it takes
-(RGPU_TAIL_CAP: small caps force hand-backs to the full-grid kernel mid-batch) must give the
-same bit-exact CC labels / component maps / summaries (ConnectedComponents.scala:10-42,137-145)."""
+"""Batch compositions and superstep paths of the CC query against the CPU oracle: window-major
+batches (64 hops of one window, the default), hop-major batches (all windows of a hop in one
+row, RGPU_WMAJOR=0), one batch in flight (RGPU_RUN_SERIAL), dense supersteps forced on almost
+every step (RGPU_DENSE), and the final-label skip (a vertex holding its view's minimum member
+label gathers nothing) on hub graphs and partial batches.  Every mode must give the same
+bit-exact CC labels / component maps / summaries and per-hop superstep counts
+(ConnectedComponents.scala:10-42,137-145; AnalysisTask.scala:208-225)."""
+import contextlib
 import os
 
 import numpy as np
@@ -15,15 +18,29 @@ from raphtory_amd.synth import BATCH_WINDOWS, DAY, HOUR, MONTH, T0_README, WEEK,
 
 pytestmark = pytest.mark.gpu
 
+# (rgpu_open env, run kwargs)
 MODES = [
-    {},                                                    # defaults (window-major, full-grid steps)
-    {"RGPU_TAIL": "1"},                                    # tail kernel after the first chunk
-    {"RGPU_TAIL": "1", "RGPU_CHUNK0": "1", "RGPU_TAIL_CAP": "3"},  # tail from step 3, hands back often
-    {"RGPU_TAIL": "1", "RGPU_CHUNK0": "2", "RGPU_CHUNK": "1", "RGPU_TAIL_CAP": "40", "RGPU_POLL": "0"},
-    {"RGPU_WMAJOR": "0", "RGPU_TAIL": "1"},                # hop-major batches (all windows per row)
-    {"RGPU_WMAJOR": "0", "RGPU_SLOTS": "1"},
+    ({}, {}),                                   # defaults (window-major, three batches in flight)
+    ({"RGPU_WMAJOR": "0"}, {}),                  # hop-major batches (all windows per row)
+    ({"RGPU_WMAJOR": "0"}, {"serial": True}),    # hop-major, one batch in flight
+    ({"RGPU_DENSE": "1000"}, {}),                # dense supersteps nearly everywhere
 ]
-MODE_IDS = ["default", "tail", "tail-cap3", "tail-cap40-blocking", "hopmajor-tail", "hopmajor-serial"]
+MODE_IDS = ["default", "hopmajor", "hopmajor-serial", "dense"]
+
+
+@contextlib.contextmanager
+def envset(env):
+    """the RGPU_* knobs of a mode, for rgpu_open and for every run inside (RGPU_DENSE is read per run)"""
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def graph_env(stream, env):
@@ -65,13 +82,16 @@ def chains_stream(lengths, seed=7, noise=3000, nverts=4000):
 
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
-def test_tail_chains_vs_oracle(mode):
+def test_chains_vs_oracle(mode, monkeypatch):
+    env, kw = mode
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     st = chains_stream([1, 4, 31, 64, 98, 99, 100, 101, 140])
     o = Oracle.from_stream(st)
-    g = graph_env(st, mode)
+    g = graph_env(st, env)
     hops = range_hops(T0_README + 10 * DAY, T0_README + 40 * DAY, 2 * DAY)
     for cap in (100, 37):
-        g.run("cc", hops, [YEAR, MONTH, WEEK], max_steps=cap, retain=True)
+        g.run("cc", hops, [YEAR, MONTH, WEEK], max_steps=cap, retain=True, **kw)
         for h, t in enumerate(hops.tolist()):
             res, steps = o.cc(t, [YEAR, MONTH, WEEK], max_steps=cap, mode=1)
             for w in range(3):
@@ -85,45 +105,49 @@ def test_tail_chains_vs_oracle(mode):
     g.close()
 
 
-@pytest.mark.parametrize("ch", ["2", "4"])
-def test_superstep_chunk_sizes_vs_oracle(ch, monkeypatch):
-    """The superstep kernel with 2-vertex (default) and 4-vertex chunks (RGPU_STEP_CH, read per
-    run) against the oracle: chains up to past the cap, and a hub-free uniform stream."""
-    monkeypatch.setenv("RGPU_STEP_CH", ch)
-    st = chains_stream([1, 4, 31, 64, 98, 99, 100, 101, 140], seed=11)
+@pytest.mark.parametrize("heavy", ["300", "2048"])
+@pytest.mark.parametrize("n_hops", [1, 5, 40])
+def test_final_label_skip_hubs_partial_batches(heavy, n_hops):
+    """The final-label skip (kernels.hip holds_final: a uniform vertex whose word equals its views'
+    minimum member label on every member lane gathers nothing, in the superstep kernel and the
+    hub gather) on star hubs cut into segments (RGPU_HEAVY=300) or kept whole, with batches of
+    fewer than 64 views (1 and 5 hops x 3 windows: lanes without members) and full ones."""
+    from tests.test_gpu_heavy import hubs_stream
+    st = hubs_stream(seed=5)
     o = Oracle.from_stream(st)
-    g = graph_env(st, {})
-    hops = range_hops(T0_README + 10 * DAY, T0_README + 40 * DAY, 3 * DAY)
-    for cap in (100, 37):
-        g.run("cc", hops, [YEAR, MONTH, WEEK], max_steps=cap, retain=True)
-        for h, t in enumerate(hops.tolist()):
-            res, steps = o.cc(t, [YEAR, MONTH, WEEK], max_steps=cap, mode=1)
-            for w in range(3):
-                assert g.cc_summary(h, w).supersteps == steps, (ch, cap, t, w)
-                ids, lab = res[w]
-                gids, glab = g.cc_vertex_labels(h, w)
-                assert np.array_equal(gids, ids) and np.array_equal(glab, lab), (ch, cap, t, w)
+    g = graph_env(st, {"RGPU_HEAVY": heavy})
+    hops = range_hops(T0_README + 5 * DAY, T0_README + 70 * DAY, DAY)[:n_hops]
+    wins = [MONTH, WEEK, DAY]
+    g.run("cc", hops, wins, retain=True)
+    for h, t in enumerate(hops.tolist()):
+        res, steps = o.cc(t, wins, mode=1)
+        for w in range(3):
+            assert g.cc_summary(h, w).supersteps == steps, (heavy, t, w)
+            ids, lab = res[w]
+            gids, glab = g.cc_vertex_labels(h, w)
+            assert np.array_equal(gids, ids) and np.array_equal(glab, lab), (heavy, t, w)
     g.close()
 
 
-def test_tail_modes_agree_on_c2_slice():
+def test_modes_agree_on_c2_slice():
     """C2 stream, 1,200 hourly hops: every mode gives identical summaries for all 6,000 views
     (superstep counts included: they are per hop, whatever batches held the views), and identical
     per-vertex labels on sampled hops."""
     s = gen_uniform(1, 100_000, 1_000_000)
     hops = range_hops(T0_README + 200 * DAY, T0_README + 250 * DAY, HOUR)[:1200]
     ref_summ, ref_lab = None, None
-    for mode in MODES:
-        g = graph_env(s, mode)
-        g.run("cc", hops, BATCH_WINDOWS, retain=True)
+    for env, kw in MODES:
+        with envset(env):
+            g = graph_env(s, env)
+            g.run("cc", hops, BATCH_WINDOWS, retain=True, **kw)
         summ = g.cc_summaries()
         labs = [g.cc_vertex_labels(h, w)[1] for h in (0, 599, 1199) for w in range(5)]
         g.close()
         if ref_summ is None:
             ref_summ, ref_lab = summ[..., :8], labs
             continue
-        assert np.array_equal(summ[..., :8], ref_summ), mode
-        assert all(np.array_equal(a, b) for a, b in zip(labs, ref_lab)), mode
+        assert np.array_equal(summ[..., :8], ref_summ), env
+        assert all(np.array_equal(a, b) for a, b in zip(labs, ref_lab)), env
 
 
 @pytest.mark.parametrize("ivmax", ["-1", "0", "3", "96"])

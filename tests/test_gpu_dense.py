@@ -14,7 +14,7 @@ from oracle import Oracle
 from raphtory_amd.synth import BATCH_WINDOWS, DAY, HOUR, MONTH, T0_README, WEEK, gen_gab, range_hops
 from tests.test_gpu_heavy import check_vs_oracle, hubs_stream
 from tests.test_gpu_partitioned import _parts, check_cc
-from tests.test_gpu_tail import graph_env
+from tests.test_gpu_batch_modes import graph_env
 
 pytestmark = pytest.mark.gpu
 

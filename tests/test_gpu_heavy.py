@@ -8,7 +8,7 @@ import pytest
 from oracle import Oracle, label_counts
 from raphtory_amd.analysis import cc_fields, cc_fields_from_summary
 from raphtory_amd.synth import BATCH_WINDOWS, DAY, HOUR, MONTH, T0_README, WEEK, YEAR, Stream, gen_gab, gen_powerlaw, range_hops
-from tests.test_gpu_tail import graph_env
+from tests.test_gpu_batch_modes import graph_env
 
 pytestmark = pytest.mark.gpu
 

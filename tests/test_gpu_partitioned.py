@@ -120,7 +120,7 @@ def test_partitioned_many_partitions_window_major(P):
     counts) runs."""
     s = gen_uniform(13, 600, 12_000, t0=T0_README, dt=2_628_000)
     o = Oracle.from_stream(s)
-    lp = _parts(s, P, {"RGPU_XREC_INIT": "0", "RGPU_XREC_SLACK": "1"})
+    lp = _parts(s, P, {"RGPU_XREC_TINY": "1"})
     hops = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, 2 * DAY)  # 168 hops x 5
     check_cc(lp, o, hops, BATCH_WINDOWS)
     lp.close()

@@ -21,7 +21,6 @@ for s in ${STEPS:-pytest smoke bench}; do
     pytest) step pytest_gpu ${PYTEST_SECS:-900} python -u -m pytest tests -m "${PYTEST_MARK:-gpu}" -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke)  step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
     bench)  step bench ${BENCH_SECS:-900} python -u bench.py ${BENCH_ARGS:-} ;;
-    probe)  step probe 900 python tools/probe.py ${PROBE_CFGS:-} ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

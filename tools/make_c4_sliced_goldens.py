@@ -1,0 +1,163 @@
+"""TEST INFRASTRUCTURE: oracle goldens for the views of the REAL 1B-update C4 headline query
+(BASELINE configs[3]: 168 hourly hops x {year, month, week, day, hour}), computed from a time
+slice of the stream, committed as tests/golden/c4_sliced_goldens.json.
+
+Why a slice is exact (Entity.scala:173-201):
+  * C4 is add-only (GabUserGraphRouter.scala:31-33: VertexAdd src, VertexAdd dst, EdgeAdd at one
+    t), so every history point is an add and no vertex ever dies (no killList entries).
+  * aliveAtWithWindow(t, w) = floor(t) is an add and t - floor(t).time <= w.  For an add-only
+    history that holds iff the entity has a point in [t - w, t], and then floor(t) is the newest
+    such point — which the slice holds as well.  Points older than t - w decide nothing.
+  * The batched vertex set of window i uses min(w_0..w_i) (shrinkWindow); for the descending
+    {y, m, w, d, h} that is w_i itself, so dropping the year window changes no other window's
+    vertex set, and each window's edges use w_i alone (WindowLens.scala:54-65).
+  * CC labels after R rounds are min{id(u): dist_w(u, v) <= R} with R = min(100, the hop's
+    superstep count).  A hop whose month/week/day/hour views converge before the year view only
+    runs empty rounds for them, and a capped hop caps every window at 100 either way: the
+    per-window labels do not depend on whether the year view rides along.  (The hop's
+    superstep count does — it is not recorded here.)
+So the views (t, w) for t in [hop0, hop167], w <= month, depend only on the interactions with
+time >= hop0 - month: ~37 days, ~56M of the 1B updates, which the oracle replays in ~8 GB.
+The year window (a year of the stream) stays out: ~550M updates do not fit the oracle here.
+
+tests/test_c4_slice.py checks the argument on the 100M-update prefix, whose views the oracle
+replayed in full (tests/golden/c4_prefix_goldens.json): the sliced replay must give the same
+summary, member count and label checksum in every window it covers.
+
+The slice's first interaction is found by bisection on the generator itself (gen_gab_range
+draws any interaction range; times are monotone in the index, synth.c rg_gen_gab_range).
+
+usage: python tools/make_c4_sliced_goldens.py [--hops 8] [--threads 8]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle import Oracle  # noqa: E402
+from raphtory_amd.synth import BATCH_WINDOWS, HOUR, MONTH, gen_gab_range, range_hops  # noqa: E402
+from tools.make_c4_goldens import picks, view_record  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden", "c4_sliced_goldens.json")
+SEED, USERS, INTER = 4, 20_000_000, 333_333_334
+
+
+def t_of(i: int, inter: int = INTER) -> int:
+    """time of interaction i of the `inter`-interaction C4 stream"""
+    return int(gen_gab_range(SEED, USERS, inter, i, 1).t[0])
+
+
+def first_at(t_from: int, n: int, inter: int = INTER) -> int:
+    """first interaction index in [0, n) with time >= t_from (n if none)"""
+    lo, hi = 0, n
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if t_of(mid, inter) >= t_from:
+            hi = mid
+        else:
+            lo = mid + 1
+    return lo
+
+
+def headline_hops(n: int, inter: int = INTER) -> np.ndarray:
+    """the C4 query's 168 hourly hops ending at the newest update of the first n interactions"""
+    end = t_of(n - 1, inter)
+    return range_hops(end - 167 * HOUR, end, HOUR)
+
+
+def sliced_stream(n: int, t_from: int, inter: int = INTER, chunk: int = 20_000_000):
+    """interactions [first_at(t_from), n) as one stream, and that first index"""
+    first = first_at(t_from, n, inter)
+    parts = [gen_gab_range(SEED, USERS, inter, a, min(chunk, n - a)) for a in range(first, n, chunk)]
+    from raphtory_amd.synth import Stream
+    cat = Stream(*(np.concatenate([getattr(p, f) for p in parts]) for f in ("t", "kind", "src", "dst")))
+    return cat, first
+
+
+def sliced_views(n: int, windows, sel, threads: int, inter: int = INTER, log=print):
+    """oracle per-window records at the sampled hop indices `sel` of the query over the first n
+    interactions, replaying only the interactions that can be alive in the widest window given"""
+    t0 = time.time()
+    hops = headline_hops(n, inter)
+    s, first = sliced_stream(n, int(hops[0]) - max(windows), inter)
+    o = Oracle.from_stream(s, True)
+    meta = {"first_interaction": int(first), "slice_updates": int(len(s)), "slice_t0": int(s.t[0]),
+            "vertices": int(o.nv), "edges": int(o.ne), "hop0": int(hops[0]), "n_hops": int(len(hops))}
+    del s
+    log(f"slice of {n} interactions from {first}: {meta['slice_updates']} updates, oracle built in "
+        f"{time.time() - t0:.0f} s ({o.nv} vertices, {o.ne} edges)")
+
+    def one(h):
+        res, _ = o.cc(int(hops[h]), windows, mode=1)
+        return h, [view_record(ids, lab) for ids, lab in res]
+
+    views = {}
+    with ThreadPoolExecutor(threads) as ex:
+        for h, recs in ex.map(one, sel):
+            views[str(h)] = {"t": int(hops[h]), "windows": recs}
+            log(f"  hop {h}: {time.time() - t0:.0f} s")
+    o.close()
+    return meta, views
+
+
+def verify_prefix(threads: int, out_path: str) -> bool:
+    """the slice argument on the 100M-update prefix, month window included: the sliced replay
+    against the full-prefix replay committed in tests/golden/c4_prefix_goldens.json"""
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "c4_prefix_goldens.json")))["prefixes"]
+    lines = []
+
+    def log(m):
+        print(m, flush=True)
+        lines.append(m)
+
+    ok = True
+    for key in sorted(gold, key=int):
+        P = gold[key]
+        n = int(key)
+        sel = sorted(int(h) for h in P["hops"])
+        meta, views = sliced_views(n, BATCH_WINDOWS[1:], sel, threads, log=log)
+        for h in sel:
+            for k, rec in enumerate(views[str(h)]["windows"]):
+                same = rec == P["hops"][str(h)]["windows"][1 + k]
+                ok &= same
+                log(f"prefix {n} interactions, hop {h}, window {BATCH_WINDOWS[1 + k]}: "
+                    f"members {rec['members']}, checksum {rec['label_checksum']} "
+                    f"{'== full replay' if same else '!= FULL REPLAY'}")
+    log("slice equivalence: " + ("all views equal" if ok else "MISMATCH"))
+    os.makedirs(os.path.dirname(out_path), exist_ok=True)
+    with open(out_path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return ok
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--hops", type=int, default=8, help="hops sampled over the 168")
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--verify-prefix", action="store_true",
+                    help="check the slice argument against the full-prefix goldens (month..hour)")
+    a = ap.parse_args()
+    if a.verify_prefix:
+        sys.exit(0 if verify_prefix(a.threads, os.path.join(ROOT, "profiles", "r04", "c4_slice_equivalence.txt"))
+                 else 1)
+    windows = BATCH_WINDOWS[1:]  # month, week, day, hour
+    assert windows[0] == MONTH
+    t0 = time.time()
+    sel = picks(168, a.hops)
+    meta, views = sliced_views(INTER, windows, sel, a.threads, log=lambda m: print(m, flush=True))
+    data = {"note": __doc__.split("\n\n")[0], "interactions": INTER, "updates": 3 * INTER,
+            "windows": list(windows), "window_index_in_query": [1, 2, 3, 4], **meta, "hops": views}
+    with open(OUT, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
+    print(f"done in {time.time() - t0:.0f} s -> {OUT}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
