@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RGPU_ABI_VERSION 8
+#define RGPU_ABI_VERSION 9
 
 /* error codes */
 #define RGPU_OK 0
@@ -171,7 +171,9 @@ int rgpu_newest_time(rgpu_ctx* ctx, int64_t* out);
  *
  * rgpu_exchange_id: make the id blob (RGPU_XCHG_ID_BYTES) once, on one rank, and hand it to
  *   every partition (RGPU_XCHG_RCCL: an ncclUniqueId — one process per GPU;
- *   RGPU_XCHG_LOOPBACK: partitions living in one process, e.g. to test on one GPU).
+ *   RGPU_XCHG_LOOPBACK: partitions living in one process, e.g. to test on one GPU;
+ *   RGPU_XCHG_SHM (ABI 9): one process per partition on one host, collectives staged through
+ *   POSIX shared memory — processes sharing a GPU, or a host without an RCCL transport).
  * rgpu_exchange_init: join the group (collective over the P partitions; before the first
  *   run).  A no-op when num_partitions == 1.
  * A partitioned run is collective too: every partition calls rgpu_run_view_batch with the
@@ -181,6 +183,7 @@ int rgpu_newest_time(rgpu_ctx* ctx, int64_t* out);
 #define RGPU_XCHG_ID_BYTES 128
 #define RGPU_XCHG_RCCL 0
 #define RGPU_XCHG_LOOPBACK 1
+#define RGPU_XCHG_SHM 2
 int rgpu_exchange_id(int kind, uint8_t* out /* RGPU_XCHG_ID_BYTES */);
 int rgpu_exchange_init(rgpu_ctx* ctx, const void* id /* RGPU_XCHG_ID_BYTES */);
 

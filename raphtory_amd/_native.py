@@ -13,13 +13,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD_DIR = os.path.join(_HERE, "_build")
 
 # error codes / constants mirrored from include/rgpu.h
-ABI_VERSION = 8
+ABI_VERSION = 9
 RGPU_OK = 0
 RGPU_EINVAL, RGPU_ESTATE, RGPU_EHIP, RGPU_ENOMEM, RGPU_ENOTSUP = -1, -2, -3, -4, -5
 RGPU_VADD, RGPU_VDEL, RGPU_EADD, RGPU_EDEL = 0, 1, 2, 3
 RGPU_ALGO_CC, RGPU_ALGO_DEGREE, RGPU_ALGO_PR, RGPU_ALGO_DIFFUSION, RGPU_ALGO_VP = 0, 1, 2, 3, 4
 RGPU_RUN_RETAIN, RGPU_RUN_PROFILE, RGPU_RUN_SERIAL, RGPU_RUN_EDGE_COUNTS = 1, 2, 4, 8
-RGPU_XCHG_ID_BYTES, RGPU_XCHG_RCCL, RGPU_XCHG_LOOPBACK = 128, 0, 1
+RGPU_XCHG_ID_BYTES, RGPU_XCHG_RCCL, RGPU_XCHG_LOOPBACK, RGPU_XCHG_SHM = 128, 0, 1, 2
 RGPU_ORDER_LOCALITY, RGPU_ORDER_ID = 0, 1
 ERROR_NAMES = {
     RGPU_EINVAL: "RGPU_EINVAL",

@@ -47,7 +47,9 @@ __global__ __launch_bounds__(256) void k_check_graph(DevGraph g, int64_t n_ekey,
     }
 }
 
-__global__ __launch_bounds__(256) void k_check_slots(int64_t nv, const int64_t* __restrict__ adj_off,
+// nv: the vertices whose slots are checked (partitioned: the owned ones); nv_all: every local rank (a
+// kept slot of an owned vertex may name a ghost)
+__global__ __launch_bounds__(256) void k_check_slots(int64_t nv, int64_t nv_all, const int64_t* __restrict__ adj_off,
                                                      const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
                                                      const int32_t* __restrict__ snbr, const int32_t* __restrict__ uw0,
                                                      const int32_t* __restrict__ uw1, const int32_t* __restrict__ grank,
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(256) void k_check_slots(int64_t nv, const int64_t* 
     }
     for (int64_t k = 0; k < n; k++) {
       const int32_t q = snbr[adj_off[v] + k];
-      if (q < 0 || q >= nv) bump(bad, 11);
+      if (q < 0 || q >= nv_all) bump(bad, 11);
     }
     if (uw0) {
       const int32_t me = grank ? grank[v] : (int32_t)v;
@@ -105,10 +107,10 @@ void launch_check_labels(hipStream_t s, int64_t nv, const uint64_t* vm, const in
 void launch_check_graph(hipStream_t s, const DevGraph& g, int64_t n_ekey, int64_t n_vkey, unsigned long long* bad) {
   k_check_graph<<<1024, 256, 0, s>>>(g, n_ekey, n_vkey, bad);
 }
-void launch_check_slots(hipStream_t s, int64_t nv, const int64_t* adj_off, const uint64_t* vm, const int32_t* cnt,
-                        const int32_t* snbr, const int32_t* uw0, const int32_t* uw1, unsigned long long* bad,
-                        const int32_t* grank) {
-  k_check_slots<<<1024, 256, 0, s>>>(nv, adj_off, vm, cnt, snbr, uw0, uw1, grank, bad);
+void launch_check_slots(hipStream_t s, int64_t nv, int64_t nv_all, const int64_t* adj_off, const uint64_t* vm,
+                        const int32_t* cnt, const int32_t* snbr, const int32_t* uw0, const int32_t* uw1,
+                        unsigned long long* bad, const int32_t* grank) {
+  k_check_slots<<<1024, 256, 0, s>>>(nv, nv_all, adj_off, vm, cnt, snbr, uw0, uw1, grank, bad);
 }
 
 }  // namespace rgpu

@@ -12,6 +12,8 @@
 //   LocalExchange  — partitions that live in one process (threads sharing one GPU):
 //                    the same protocol with device-to-device copies; used to test the
 //                    partitioned path on a single GPU.
+//   ShmExchange    — one process per partition on one host, staged through POSIX shared
+//                    memory (processes sharing a GPU; the multi-process protocol without RCCL).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -44,7 +46,8 @@ class Exchange {
 };
 
 // id blob handed to every partition (rgpu_exchange_id / rgpu_exchange_init); returns "" or
-// an error.  kind 0 = RCCL unique id, kind 1 = loopback group (one process).
+// an error.  kind 0 = RCCL unique id, kind 1 = loopback group (one process), kind 2 = shared-memory
+// group (processes on one host).
 std::string make_exchange_id(int kind, uint8_t out[kXchgIdBytes]);
 // end of a run: a loopback partition thread gives up the measurement lock (RGPU_LOOPBACK_ISOLATE)
 void exchange_quiesce();

@@ -20,6 +20,7 @@
 #include <climits>
 #include <cstdint>
 #include <cstring>
+#include <cstdlib>
 
 #include "kernels.hpp"
 #include "window_bits.hpp"
@@ -1265,6 +1266,237 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) 
   }
 }
 
+// Packed superstep (default).  A wave takes 64 vertices per round (lane = vertex, dealt in
+// groups of consecutive ranks): their frontier flags and then the flagged members' metadata (view
+// mask, kept-slot count and offset, change word, uniform words, hub index) in one coalesced load
+// each.  The kept slots of the members with at most 64 of them are packed into 64-lane passes
+// (lane = slot over the concatenated slot lists, as K2 packs its light members): one round of slot
+// loads and one of neighbour words per pass serves every member in it, instead of one dependent
+// chain per 2-vertex chunk.  The fold then runs per member (lane = view) from registers: uniform
+// neighbours' words, and the label rows of mixed neighbours (gather_min).  Every member's new
+// uniform word, change word and own frontier flag are stored lane-parallel at the end of the round.
+// Members with more than 64 kept slots take the chunk path (cc_chunk) one at a time, before the
+// packs (so its registers do not add to the round's).
+template <bool BUF, bool PROF>
+__global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const int64_t* __restrict__ adj_off,
+                                                    const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
+                                                    const int32_t* __restrict__ snbr, const uint64_t* __restrict__ smask,
+                                                    const int32_t* __restrict__ lab_cur, int32_t* __restrict__ lab_next,
+                                                    const uint64_t* __restrict__ chg_prev, uint64_t* __restrict__ chg_next,
+                                                    const uint8_t* __restrict__ act_cur, uint8_t* __restrict__ act_next,
+                                                    uint8_t* __restrict__ act_clear, int32_t* __restrict__ stepflag,
+                                                    int32_t* __restrict__ hostflag, unsigned long long* __restrict__ work,
+                                                    const int32_t* __restrict__ hv_of, int32_t* __restrict__ hbest,
+                                                    unsigned long long* __restrict__ lanechg,
+                                                    const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
+                                                    uint64_t* __restrict__ cb_next, uint64_t* __restrict__ cb_clear,
+                                                    int64_t cb_words, int32_t* __restrict__ ccount, int dense_div, int gmax,
+                                                    const int32_t* __restrict__ mneg) {
+  if (stepflag[step - 1] == 0) return;
+  const int lane = lane_id();
+  const bool use_fin = mneg != nullptr && uw_cur != nullptr;
+  const int32_t mfin = final_label(mneg, lane);
+  const bool skip_marks = dense_rule(ccount, step, nv, dense_div);
+  const bool visit_all = dense_rule(ccount, step - 1, nv, dense_div);
+  __shared__ int32_t red;
+  __shared__ unsigned long long wred[8];  // [0..6] work fields (StepWork), [7] changed views (LDS OR)
+  if (threadIdx.x < 8) wred[threadIdx.x] = 0;
+  if (threadIdx.x == 0) red = 0;
+  const int64_t nwords = (nv + 7) >> 3;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords; i += (int64_t)gridDim.x * blockDim.x)
+    reinterpret_cast<uint64_t*>(act_clear)[i] = 0;
+  if (cb_clear)
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cb_words; i += (int64_t)gridDim.x * blockDim.x)
+      cb_clear[i] = 0;
+  __syncthreads();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  int32_t changed = 0;
+  uint64_t lanes_or = 0;
+  std::conditional_t<PROF, StepWork, NoWork> wk;
+  const int G = deal_group(nv, nwaves, gmax);
+  for (int64_t r = 0; (wave + r * (64 / G) * nwaves) * G < nv; r++) {
+    const int64_t vl = dealt_item(wave, nwaves, r, G, lane);
+    const bool inb = vl < nv;
+    uint64_t mv = 0;
+    bool flag = false;
+    if (inb) {
+      if (visit_all) {
+        mv = vm[vl];
+        flag = mv != 0;
+      } else {
+        flag = act_cur[vl] != 0;
+      }
+    }
+    uint64_t todo = __ballot(flag);
+    if (!todo) continue;
+    int32_t n = flag ? cnt[vl] : 0;  // 0 for a heavy vertex (its slots are in segments)
+    // members with more than 64 kept slots: the chunk path, one vertex at a time
+    for (uint64_t big = __ballot(flag && n > 64); big; big &= big - 1) {
+      const int L = __builtin_ctzll(big);
+      cc_chunk<2, BUF>((int64_t)readlane64((uint64_t)vl, L), 1u, adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
+                       chg_prev, chg_next, act_next, lane, changed, &wred[7], wk, hv_of, hbest, uw_cur, uw_next, cb_next,
+                       skip_marks, mfin, use_fin);
+    }
+    bool mine = flag && n <= 64;  // this lane's member is handled below
+    if (!__ballot(mine)) continue;
+    int64_t base = 0;
+    uint64_t cp = 0;
+    int32_t u = kMixed, un = kMixed, hh = -1;
+    if (mine) {
+      if (!visit_all) mv = vm[vl];
+      base = adj_off[vl];
+      cp = chg_prev[vl];
+      if (uw_cur) u = uw_cur[vl];
+      if (uw_next) un = uw_next[vl];
+      if (hv_of) hh = hv_of[vl];
+    }
+    mine = mine && mv != 0;  // (a flagged non-member has nothing to do)
+    todo = __ballot(mine);
+    if (!todo) continue;
+    if (use_fin) {  // a member that holds its views' final label gathers nothing
+      for (uint64_t t = todo; t; t &= t - 1) {
+        const int L = __builtin_ctzll(t);
+        const bool fin = holds_final(__builtin_amdgcn_readlane(u, L), readlane64(mv, L), mfin, lane);
+        if (fin && lane == L) n = 0;
+      }
+    }
+    // results of the round, lane = member
+    uint64_t my_ch = 0;
+    int32_t my_w = 0;
+    bool has_w = false;
+    uint64_t pend = todo;
+    while (pend) {
+      // the next pack: members in lane order while their slots fit 64 lanes
+      uint64_t pack = 0;
+      int sum = 0, myL = 0, myj = 0;
+      while (pend) {
+        const int Lp = __builtin_ctzll(pend);
+        const int k = __builtin_amdgcn_readlane(n, Lp);
+        if (pack && sum + k > 64) break;
+        if (lane >= sum && lane < sum + k) { myL = Lp; myj = lane - sum; }
+        pack |= 1ull << Lp;
+        sum += k;
+        pend &= pend - 1;
+      }
+      const bool on = lane < sum;
+      // lane = slot: the slot, then the neighbour's word (vertex 0's for idle lanes: masked by sm = 0)
+      const int64_t bmy = (int64_t)(((uint64_t)(uint32_t)__shfl((int)((uint64_t)base >> 32), myL) << 32) |
+                                    (uint32_t)__shfl((int)base, myL));
+      const int64_t idx = on ? bmy + myj : 0;
+      const int32_t q = snbr[idx];
+      const uint64_t m = smask[idx];
+      const int32_t nbp = on ? q : 0;
+      const uint64_t smp = on ? m : 0;
+      uint64_t act = 0;
+      int32_t unp = kMixed;
+      if (uw_cur) {
+        const int32_t w = uw_cur[nbp];
+        act = (w != kMixed && w < 0) ? smp : 0;
+        unp = w == kMixed ? kMixed : (w & 0x7fffffff);
+        const bool mx = w == kMixed && smp != 0;
+        const uint64_t mixed = __ballot(mx);
+        if (mixed) {
+          const uint64_t cw = chg_prev[mx ? nbp : 0];
+          if (mx) act = smp & cw;
+          wk.a += __popcll(mixed);
+        }
+      } else {
+        act = smp & chg_prev[nbp];
+      }
+      wk.g += unp == kMixed ? __popcll(act) : 0;
+      uint64_t markp = 0;  // lane = slot: its neighbour joins the next frontier
+      int pre = 0;
+      for (uint64_t pk = pack; pk; pk &= pk - 1) {
+        const int L = __builtin_ctzll(pk);
+        const int k = __builtin_amdgcn_readlane(n, L);
+        const uint64_t span = k == 0 ? 0ull : ((k >= 64 ? ~0ull : ((1ull << k) - 1)) << pre);
+        pre += k;
+        const uint64_t mvL = readlane64(mv, L);
+        const int64_t v = (int64_t)readlane64((uint64_t)vl, L);
+        const int32_t uL = __builtin_amdgcn_readlane(u, L);
+        const bool mem = (mvL >> lane) & 1;
+        int32_t cur;
+        if (uL != kMixed) {
+          cur = uL & 0x7fffffff;
+        } else {
+          cur = row_get<BUF>(lab_cur + v * 64, mem, lane);
+          wk.lr += row_lines(mvL);
+        }
+        cur = mem ? cur : INT32_MAX;
+        const bool inspan = (span >> lane) & 1;
+        int32_t best = gather_min<BUF>(inspan && unp == kMixed ? act : 0, nbp, cur, lab_cur, lane);
+        if (uw_cur) best = fold_uniform(__ballot(inspan && unp != kMixed && act != 0), act, unp, best, lane);
+        const int32_t hL = __builtin_amdgcn_readlane(hh, L);
+        if (hL >= 0) {  // a hub: the step's minima over its segments (k_heavy_gather), reset for the next step
+          const int32_t x = hbest[(int64_t)hL * 64 + lane];
+          hbest[(int64_t)hL * 64 + lane] = INT32_MAX;
+          best = min(best, mem ? x : INT32_MAX);
+        }
+        wk.v += 1;
+        wk.s += (unsigned long long)k;
+        const uint64_t ch = __ballot(best < cur);
+        if (ch || readlane64(cp, L)) {  // both label buffers differ: rewrite the word (and row)
+          const int32_t uu = uw_next ? row_uniform(best, mvL, lane) : kMixed;
+          if (lane == L) { my_w = uw_word(uu, ch != 0); has_w = uw_next != nullptr; }
+          if (uw_next) wk.uw += 1;
+          if (uu == kMixed) {
+            if (BUF) row_store(lab_next + v * 64, best, line_has(mvL, lane), lane);
+            else lab_next[v * 64 + lane] = best;
+            wk.lw += BUF ? row_lines(mvL) : 4;
+          }
+        } else if (uw_next) {
+          const int32_t unL = __builtin_amdgcn_readlane(un, L);
+          if (unL != kMixed && unL < 0 && lane == L) { my_w = unL & 0x7fffffff; has_w = true; }  // stale flag
+        }
+        if (lane == L) my_ch = ch;
+        if (ch) {
+          lanes_or |= ch;
+          changed++;
+          if (inspan && (smp & ch)) markp = 1;
+        }
+      }
+      if (!skip_marks && markp) act_next[nbp] = 1;
+    }
+    // the round's members, lane-parallel: words, change words, own frontier flags, changed bits
+    if (mine) {
+      if (has_w) uw_next[vl] = my_w;
+      chg_next[vl] = my_ch;
+      if (my_ch && !skip_marks) act_next[vl] = 1;
+    }
+    if (cb_next) {  // a dealt group is G consecutive, G-aligned ranks: one bitmap word, one atomic per group
+      const uint64_t cbm = __ballot(mine && my_ch != 0);
+      const int gl = lane & ~(G - 1);
+      const uint64_t sub = (cbm >> gl) & (G >= 64 ? ~0ull : ((1ull << G) - 1));
+      if (lane == gl && sub) atomicOr((unsigned long long*)&cb_next[vl >> 6], (unsigned long long)(sub << (vl & 63)));
+    }
+  }
+  if (lanes_or && lane == 0) atomicOr(&wred[7], (unsigned long long)lanes_or);
+  if constexpr (PROF)
+    for (int o = 32; o > 0; o >>= 1) wk.g += __shfl_xor(wk.g, o);
+  if (lane == 0) {
+    if (changed) atomicAdd(&red, changed);
+    if constexpr (PROF) {
+      const unsigned long long f[7] = {wk.v, wk.s, 0, wk.g, wk.a, wk.lr, wk.lw};
+#pragma unroll
+      for (int i = 0; i < 7; i++)
+        if (f[i]) atomicAdd(&wred[i], f[i]);
+      if (wk.uw) atomicAdd(&wred[2], wk.uw);
+    }
+  }
+  publish_lanes(0, &wred[7], lanechg, step);
+  if (threadIdx.x == 0) {
+    if (red && ccount) atomicAdd(&ccount[step * kCountShards + (blockIdx.x & (kCountShards - 1))], red);
+    if (red && stepflag[step] == 0) {
+      stepflag[step] = 1;
+      if (hostflag) hostflag[step] = 1;
+    }
+    const unsigned long long f[8] = {wred[0], wred[1], (unsigned long long)red, wred[3], wred[4], wred[5], wred[6],
+                                     wred[2]};
+    add_work(work, step, f);
+  }
+}
+
 // ---------------------------------------------------------------- heavy vertices
 // Profile runs: the hub kernels' work, for their byte model (rgpu.cpp harvest), in the work
 // buffer's step-0 row (supersteps start at 1): [shard][f], f = 0 segments visited by the gather,
@@ -2258,6 +2490,17 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   // work != null (profile runs): the counting instantiation; the timed runs use the lean one.
   // 2-vertex chunks: 73 VGPRs, 6 waves/SIMD against 97 and 4 for 4-vertex chunks; same-box A/B
   // (profiles/r03/c4_ab_step_ch.log): C4 369 -> 345 ms, C2 135 -> 120 ms.
+  const int ab = [] { const char* e = std::getenv("RGPU_AB"); return e ? std::atoi(e) : 1; }();  // (A/B, temporary)
+  if (ab) {
+#define RGPU_PK_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
+    act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
+    cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr
+    const unsigned gridp = grid_for(g.nv, 256, cap);
+    if (work) k_cc_step_pk<false, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
+    else k_cc_step_pk<false, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
+#undef RGPU_PK_ARGS
+    return;
+  }
   const unsigned grid2 = grid_for(g.nv, 8, cap);
   if (work) k_cc_step2<2, false, 1, true><<<grid2, 256, 0, s>>>(RGPU_STEP_ARGS);
   else k_cc_step2<2, false, 1, false><<<grid2, 256, 0, s>>>(RGPU_STEP_ARGS);

@@ -186,7 +186,7 @@ void launch_cc_roots(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, 
 void launch_check_graph(hipStream_t s, const DevGraph& g, int64_t n_ekey, int64_t n_vkey, unsigned long long* bad);
 void launch_check_labels(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, const int32_t* lab,
                          unsigned long long* bad, const int32_t* grank = nullptr);
-void launch_check_slots(hipStream_t s, int64_t nv, const int64_t* adj_off, const uint64_t* vm, const int32_t* cnt,
+void launch_check_slots(hipStream_t s, int64_t nv, int64_t nv_all, const int64_t* adj_off, const uint64_t* vm, const int32_t* cnt,
                         const int32_t* snbr, const int32_t* uw0, const int32_t* uw1, unsigned long long* bad,
                         const int32_t* grank = nullptr);
 // Changed bits (with uniform words and heavy vertices): one bit per local rank, set when the
@@ -279,30 +279,53 @@ void launch_xvm_pack(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t
                      const uint64_t* vm, int64_t vstride, uint64_t* out);
 void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
                        int planes, const uint64_t* in, uint64_t* vm, int64_t vstride);
-// The send plan by boundary vertex (built from the (peer, vertex) lists, build_xsend): the owned
-// boundary vertices ascending, the peers holding each as a ghost (bit mask), and its entry index in
-// each of those peers' lists.  The record pack reads a vertex's words once for all its peers.
+// The send plan by boundary vertex (build_xsend, from the (peer, vertex) send lists): the owned
+// boundary vertices ascending (boundary index b), each owned rank's b (-1: not a boundary vertex),
+// and each send entry's b.  Label records name a vertex by b (one broadcast list for every peer).
 struct XSend {
   int64_t nb = 0;
-  const int32_t* v = nullptr;    // [nb] owned rank
-  const int32_t* e = nullptr;    // [nb][kMaxParts] entry index in the list for peer q
-  const uint32_t* pm = nullptr;  // [nb] peers
+  const int32_t* v = nullptr;     // [nb] owned rank of boundary vertex b
+  const int32_t* bidx = nullptr;  // [n_own] b of owned rank v, or -1
+  const int32_t* eb = nullptr;    // [nx] b of send entry e
 };
-XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
-                  std::vector<void*>& T, std::vector<void*>& L);
-void launch_xpack_rec(hipStream_t s, const XPeers& P, const XSend& X, const uint8_t* act, const uint64_t* chg_now,
-                      const uint64_t* vadj, const int32_t* lab, const int32_t* uw, XRec* sbuf, unsigned long long* scnt,
-                      const int32_t* ccount = nullptr, int dense_div = 0, int step = 0, int64_t n_own = 0);
-void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa);
-void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg,
-                   int32_t* uw = nullptr);
-void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
-                        uint64_t* chg, int32_t* uw = nullptr, uint64_t* cb = nullptr);
+XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, std::vector<void*>& T,
+                  std::vector<void*>& L);
+// receive tables: ghost rank of (peer q, q's boundary index b) = tab[toff[q] + b], -1 if q's vertex b
+// has no ghost here
+struct XTab {
+  int32_t* tab = nullptr;
+  int64_t toff[kMaxParts + 1] = {};
+};
+// tmp[i]: the sender's boundary index of receive entry i (xr_v[i], from peer xr_q[i])
+void launch_xtab_fill(hipStream_t s, int64_t n, const int32_t* xr_v, const int32_t* xr_q, const int32_t* tmp,
+                      const XTab& T, unsigned long long* err);
+// After superstep `step`: this partition's broadcast label records (xchg.hip: U records into su, at
+// most nb; M records into sm, cnt[1] counts past mcap so the host can grow and pack again)
+void launch_xbc_pack(hipStream_t s, int64_t n_own, const XSend& X, const uint8_t* act, const uint64_t* chg_now,
+                     const uint64_t* vadj, const uint64_t* vm, const int32_t* lab, const int32_t* uw,
+                     unsigned long long* su, XRec* sm, int64_t mcap, unsigned long long* cnt, const int32_t* ccount,
+                     int dense_div, int step);
+// counts words (4 per peer): U records, M records, the halting vote; cnt reset
+void launch_xbc_counts(hipStream_t s, int np, int me, unsigned long long* cnt, const int32_t* stepflag, int64_t* xa);
+// component-count records (2 words per peer); scnt reset
+void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, int64_t* xa);
+// a received broadcast: U and M receive regions per peer, with the records received (pre), the
+// tables, the ghost range and the out-of-plan record counter
+struct XBcIn {
+  XPeers U, M;
+  const unsigned long long* ru = nullptr;
+  const XRec* rm = nullptr;
+  XTab T;
+  int64_t n_own = 0, nv = 0;
+  unsigned long long* err = nullptr;
+};
+void launch_xbc_clear(hipStream_t s, const XBcIn& I, uint64_t* chg, int32_t* uw);
+void launch_xbc_unpack(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg, int32_t* uw, uint64_t* cb = nullptr);
 // tcut / ebp: the batch's slot cut and (inline edge bits; null: em for every slot) its edge windows;
 // ccount / dense_div / step: nothing is marked when superstep `step` is dense
-void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
-                  const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next, int64_t tcut,
-                  const BatchParams* ebp, const int32_t* ccount, int dense_div, int step);
+void launch_xbc_mark(hipStream_t s, const XBcIn& I, const uint64_t* chg, const DevGraph& g, const uint64_t* vm,
+                     const uint64_t* em, uint8_t* act_next, int64_t tcut, const BatchParams* ebp, const int32_t* ccount,
+                     int dense_div, int step);
 // owned id -> owned rank: ids ascend with rank; bucket b = id >> shift covers ranks
 // [boff[b], boff[b+1]) (about one id per bucket)
 struct OwnIdx {

@@ -119,13 +119,21 @@ struct Retained {  // per batch, RGPU_RUN_RETAIN
 // Per batch slot: its own exchange channel, record buffers and counts staging.
 struct XSlot {
   Exchange* x = nullptr;                  // this slot's channel (a fork of the ctx's)
-  XRec* sbuf = nullptr;                   // label records to send, one region per peer
-  XRec* rbuf[2] = {nullptr, nullptr};     // received, per superstep parity
-  int64_t scap[kMaxParts] = {}, rcap[kMaxParts] = {};
-  int64_t rcnt[2][kMaxParts] = {};        // records received per parity (their ghosts' change
-                                          // words are cleared two supersteps later)
-  unsigned long long* scnt = nullptr;     // [kMaxParts] records per peer of the pack in flight
-  int64_t* xab = nullptr;                 // [4P] counts words: sent (xa) | received (xb)
+  // broadcast label records (xchg.hip k_xbc_pack): one list for every peer
+  unsigned long long* su = nullptr;       // U records to send: at most one per boundary vertex (sized by
+                                          // the plan: grows only when a live merge grows the plan)
+  int64_t su_cap = 0, ru_cap = 0;
+  XRec* sm = nullptr;                     // M records to send
+  int64_t smcap = 0;
+  unsigned long long* ru[2] = {nullptr, nullptr};  // received U records per superstep parity, region q
+                                                   // = peer q's boundary count (never grows)
+  XRec* rm[2] = {nullptr, nullptr};       // received M records per parity
+  int64_t rmcap[kMaxParts] = {};
+  int64_t rucnt[2][kMaxParts] = {}, rmcnt[2][kMaxParts] = {};  // records received per parity (their
+                                          // ghosts' words are cleared two supersteps later)
+  unsigned long long* cnt = nullptr;      // [2] U / M records of the pack in flight
+  unsigned long long* err = nullptr;      // received records outside the plan (xchg.hip bc_rec)
+  int64_t* xab = nullptr;                 // [8P] counts words: sent (xa) | received (xb)
   int64_t* h_xab = nullptr;               // pinned copy
   uint64_t *vms = nullptr, *vmr = nullptr;  // ghost membership words (planes x list)
   int vm_planes = 0;
@@ -144,6 +152,9 @@ struct Part {
   int64_t *xs_off_d = nullptr, *xr_off_d = nullptr;
   OwnIdx own;                                 // owned id -> owned rank (label owner counting)
   XSend xsend;                                // the send plan by boundary vertex (record pack)
+  XTab tab;                                   // receive tables of the broadcast records
+  int64_t nbq[kMaxParts] = {};                // boundary vertices of every partition
+  bool tab_ready = false;
   double *sbuf_f = nullptr, *rbuf_f = nullptr;  // PR contribution rows
   bool pr_ready = false;
   XSlot xs[4];                                // per batch slot (kMaxSlots)
@@ -198,6 +209,7 @@ struct rgpu_ctx {
   int nslots = 3;                       // batches in flight (2 / 4 measured slower on C4)
   bool prof_lean = false;               // RGPU_PROF_LEAN (work_buf)
   int inject_fail = 0;                  // RGPU_INJECT_FAIL=n (tests): the n-th batch start of a run throws
+  bool inject_rec = false;              // RGPU_INJECT_FAIL=rec (tests): corrupt one received label record
   int dense = -1;                       // RGPU_DENSE: dense-step divisor (kernels.hip dense_rule; -1 by size)
   bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
   std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
@@ -907,7 +919,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     });
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
-        launch_check_slots(s.stream, gk.nv, g.adj_off, s.vm, s.cnt, s.snbr, s.uw[0],
+        launch_check_slots(s.stream, gk.nv, g.nv, g.adj_off, s.vm, s.cnt, s.snbr, s.uw[0],
                            s.uw[1], bad, g.grank);
       });
     if (g.n_seg > 0 && !c->partitioned)  // partitioned: after the step's records are in
@@ -1182,7 +1194,8 @@ XPeers peers_layout(const rgpu_ctx* c, const int64_t* cap, const std::vector<int
 
 void free_part_slots(rgpu_ctx* c, bool keep_channels) {
   for (XSlot& xs : c->pt.xs) {
-    for (void* p : {(void*)xs.sbuf, (void*)xs.rbuf[0], (void*)xs.rbuf[1], (void*)xs.hsbuf, (void*)xs.hrbuf})
+    for (void* p : {(void*)xs.su, (void*)xs.sm, (void*)xs.ru[0], (void*)xs.ru[1], (void*)xs.rm[0], (void*)xs.rm[1],
+                    (void*)xs.hsbuf, (void*)xs.hrbuf})
       if (p) (void)hipFree(p);
     if (xs.h_xab) (void)hipHostFree(xs.h_xab);
     Exchange* x = xs.x;
@@ -1192,36 +1205,101 @@ void free_part_slots(rgpu_ctx* c, bool keep_channels) {
   }
 }
 
+void drop_alloc(std::vector<void*>& L, void* p);
+// The broadcast records' receive tables (once per sealed graph; collective): every partition's
+// boundary count, and for every receive entry the sender's boundary index of its vertex (the
+// send plans are aligned: entry e of q's list for us is our receive entry xr_off[q] + e).
+void ensure_tab(rgpu_ctx* c) {
+  Part& X = c->pt;
+  if (X.tab_ready) return;
+  const int P = c->nparts, me = c->part;
+  hipStream_t st = c->slot[0].stream;
+  auto& LG = c->graph_allocs;
+  std::vector<void*> T;
+  try {
+    int64_t* d = dalloc<int64_t>(T, 2 * P);
+    std::vector<int64_t> h(2 * P, X.xsend.nb);
+    HIPCHK(hipMemcpy(d, h.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice));
+    X.xchg->alltoall_i64(d, d + P, 1, st);
+    HIPCHK(hipMemcpyAsync(h.data(), d, sizeof(int64_t) * 2 * P, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    int64_t o = 0;
+    for (int q = 0; q < P; q++) {
+      X.nbq[q] = q == me ? 0 : h[P + q];
+      X.tab.toff[q] = o;
+      o += X.nbq[q];
+    }
+    X.tab.toff[P] = o;
+    drop_alloc(LG, X.tab.tab);  // (a rebuild after a seal that kept the graph)
+    X.tab.tab = dalloc<int32_t>(LG, std::max<int64_t>(o, 1));
+    HIPCHK(hipMemsetAsync(X.tab.tab, 0xff, sizeof(int32_t) * std::max<int64_t>(o, 1), st));
+    int32_t* tmp = dalloc<int32_t>(T, std::max<int64_t>(X.nxr, 1));
+    std::vector<void*> sp(P), rp(P);
+    std::vector<size_t> sb(P), rb(P);
+    for (int q = 0; q < P; q++) {
+      sp[q] = (void*)(X.xsend.eb ? X.xsend.eb + X.xs_off[q] : nullptr);
+      rp[q] = tmp + X.xr_off[q];
+      sb[q] = q == me ? 0 : sizeof(int32_t) * (size_t)(X.xs_off[q + 1] - X.xs_off[q]);
+      rb[q] = q == me ? 0 : sizeof(int32_t) * (size_t)(X.xr_off[q + 1] - X.xr_off[q]);
+    }
+    X.xchg->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), st);
+    unsigned long long* err = dalloc<unsigned long long>(T, 1);
+    HIPCHK(hipMemsetAsync(err, 0, sizeof(unsigned long long), st));
+    launch_xtab_fill(st, X.nxr, X.xr_v, X.xr_q, tmp, X.tab, err);
+    HIPCHK(hipGetLastError());
+    unsigned long long herr = 0;
+    HIPCHK(hipMemcpyAsync(&herr, err, sizeof(herr), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (herr) throw HipFail{"exchange plan: " + std::to_string(herr) + " receive entries name no boundary vertex of their sender"};
+  } catch (...) {
+    for (void* p : T) (void)hipFree(p);
+    throw;
+  }
+  for (void* p : T) (void)hipFree(p);
+  X.tab_ready = true;
+}
+
 void ensure_part(rgpu_ctx* c, int nuse, int planes) {
   Part& X = c->pt;
   const int P = c->nparts;
   auto& LG = c->graph_allocs;
+  ensure_tab(c);
   for (int i = 0; i < nuse; i++) {
     XSlot& xs = X.xs[i];
     if (!xs.x) xs.x = X.xchg->fork(i + 1);  // collective: every partition forks the same slots
-    if (!xs.scnt) {
-      xs.scnt = dalloc<unsigned long long>(LG, kMaxParts);
-      HIPCHK(hipMemset(xs.scnt, 0, sizeof(unsigned long long) * kMaxParts));
+    if (!xs.cnt) {
+      xs.cnt = dalloc<unsigned long long>(LG, 2);
+      HIPCHK(hipMemset(xs.cnt, 0, sizeof(unsigned long long) * 2));
+      xs.err = dalloc<unsigned long long>(LG, 1);
       xs.htot = dalloc<unsigned long long>(LG, kMaxParts);
       HIPCHK(hipMemset(xs.htot, 0, sizeof(unsigned long long) * kMaxParts));
-      xs.xab = dalloc<int64_t>(LG, 4 * P);
-      HIPCHK(hipHostMalloc((void**)&xs.h_xab, sizeof(int64_t) * 4 * P));
+      xs.xab = dalloc<int64_t>(LG, 8 * P);
+      HIPCHK(hipHostMalloc((void**)&xs.h_xab, sizeof(int64_t) * 8 * P));
     }
+    HIPCHK(hipMemset(xs.err, 0, sizeof(unsigned long long)));
     if (xs.vm_planes < planes) {
       xs.vms = dalloc<uint64_t>(LG, (size_t)planes * std::max<int64_t>(X.nxs, 1));
       xs.vmr = dalloc<uint64_t>(LG, (size_t)planes * std::max<int64_t>(X.nxr, 1));
       xs.vm_planes = planes;
     }
-    if (!xs.sbuf) {  // first guess: two records per boundary entry (both receive parities
-                     // share one layout, xs.rcap)
+    if (xs.su_cap < X.xsend.nb || xs.ru_cap < X.tab.toff[P] || !xs.su) {
+      // U records: worst case one per boundary vertex, sent and received (sized by the plan: no
+      // growth during a run, no host sizing)
+      for (void* p : {(void*)xs.su, (void*)xs.ru[0], (void*)xs.ru[1]})
+        if (p) HIPCHK(hipFree(p));
+      xs.su_cap = std::max<int64_t>(X.xsend.nb, 1);
+      xs.ru_cap = std::max<int64_t>(X.tab.toff[P], 1);
+      HIPCHK(hipMalloc((void**)&xs.su, sizeof(unsigned long long) * (size_t)xs.su_cap));
+      for (int p = 0; p < 2; p++) HIPCHK(hipMalloc((void**)&xs.ru[p], sizeof(unsigned long long) * (size_t)xs.ru_cap));
+    }
+    if (!xs.sm) {
+      // M records: a first guess, grown on demand (both receive parities share one layout, xs.rmcap)
       int64_t ns[kMaxParts] = {}, nr[kMaxParts] = {};
-      for (int q = 0; q < P; q++) {
-        ns[q] = g_xrec_init * (X.xs_off[q + 1] - X.xs_off[q]);
-        nr[q] = g_xrec_init * (X.xr_off[q + 1] - X.xr_off[q]);
-      }
-      grow_regions(&xs.sbuf, xs.scap, ns, P, nullptr);
-      grow_regions(&xs.rbuf[0], xs.rcap, nr, P, nullptr);
-      xs.rbuf[1] = alloc_regions<XRec>(xs.rcap, P);
+      ns[0] = g_xrec_init * X.xsend.nb / 16;
+      for (int q = 0; q < P; q++) nr[q] = g_xrec_init * X.nbq[q] / 16;
+      grow_regions(&xs.sm, &xs.smcap, ns, 1, nullptr);
+      grow_regions(&xs.rm[0], xs.rmcap, nr, P, nullptr);
+      xs.rm[1] = alloc_regions<XRec>(xs.rmcap, P);
     }
   }
 }
@@ -1248,6 +1326,47 @@ void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int pl
   HIPCHK(hipGetLastError());
 }
 
+// the broadcast label records of superstep r (U into xs.su, M into xs.sm)
+void part_pack(rgpu_ctx* c, int si, int r) {
+  Slot& s = c->slot[si];
+  Part& X = c->pt;
+  XSlot& xs = X.xs[si];
+  timed_launch(c, si, KID_XPACK, 0.0, [&] {
+    launch_xbc_pack(s.stream, c->pk.n_own, X.xsend, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj, s.vm,
+                    s.lab[r & 1], s.uw[r & 1], xs.su, xs.sm, xs.smcap, xs.cnt, s.ccount, dense_div(c), r);
+  });
+}
+
+// a received broadcast of parity par: regions and record counts (xchg.hip XBcIn)
+XBcIn bc_in(const rgpu_ctx* c, const XSlot& xs, int par) {
+  XBcIn I;
+  const int P = c->nparts;
+  I.U.np = I.M.np = P;
+  I.U.me = I.M.me = c->part;
+  int64_t bu = 0, bm = 0, pu = 0, pm = 0;
+  for (int q = 0; q < P; q++) {
+    I.U.base[q] = bu;
+    I.U.cap[q] = c->pt.nbq[q];
+    bu += c->pt.nbq[q];
+    I.U.pre[q] = pu;
+    pu += xs.rucnt[par][q];
+    I.M.base[q] = bm;
+    I.M.cap[q] = xs.rmcap[q];
+    bm += xs.rmcap[q];
+    I.M.pre[q] = pm;
+    pm += xs.rmcnt[par][q];
+  }
+  I.U.pre[P] = pu;
+  I.M.pre[P] = pm;
+  I.ru = xs.ru[par];
+  I.rm = xs.rm[par];
+  I.T = c->pt.tab;
+  I.n_own = c->pk.n_own;
+  I.nv = c->g.nv;
+  I.err = xs.err;
+  return I;
+}
+
 // after superstep r: pack its boundary records and exchange the counts; the host picks the
 // slot up in part_after_counts
 void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
@@ -1262,14 +1381,11 @@ void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
     part_finish_begin(c, si, rc);
     return;
   }
-  const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
-  timed_launch(c, si, KID_XPACK, 0.0, [&] { launch_xpack_rec(s.stream, L, X.xsend, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
-                   s.lab[r & 1], s.uw[r & 1], xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
-                   c->pk.n_own); });
-  launch_xcounts(s.stream, P, c->part, xs.scnt, s.stepcnt + r, xs.xab);
+  part_pack(c, si, r);
+  launch_xbc_counts(s.stream, P, c->part, xs.cnt, s.stepcnt + r, xs.xab);
   HIPCHK(hipGetLastError());
-  xs.x->alltoall_i64(xs.xab, xs.xab + 2 * P, 2, s.stream);
-  HIPCHK(hipMemcpyAsync(xs.h_xab, xs.xab, sizeof(int64_t) * 4 * P, hipMemcpyDeviceToHost, s.stream));
+  xs.x->alltoall_i64(xs.xab, xs.xab + 4 * P, 4, s.stream);
+  HIPCHK(hipMemcpyAsync(xs.h_xab, xs.xab, sizeof(int64_t) * 8 * P, hipMemcpyDeviceToHost, s.stream));
   HIPCHK(hipEventRecord(s.ev, s.stream));
   s.phase = 1;
 }
@@ -1281,23 +1397,25 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   const DevGraph& g = c->g;
   const int P = c->nparts, me = c->part, r = xs.r;
   const int64_t* xa = xs.h_xab;
-  const int64_t* xb = xs.h_xab + 2 * P;
-  int64_t sent[kMaxParts] = {}, recv[kMaxParts] = {};
+  const int64_t* xb = xs.h_xab + 4 * P;
+  int64_t sent_u = 0, sent_m = 0, recv_u[kMaxParts] = {}, recv_m[kMaxParts] = {};
   bool any = false;
   for (int q = 0; q < P; q++) {
-    sent[q] = q == me ? 0 : xa[2 * q];
-    recv[q] = q == me ? 0 : xb[2 * q];
-    any |= xb[2 * q + 1] != 0;  // the vote: some partition changed a label (self included)
+    if (q != me) {
+      sent_u = std::max(sent_u, xa[4 * q]);  // (the same broadcast for every peer)
+      sent_m = std::max(sent_m, xa[4 * q + 1]);
+      recv_u[q] = xb[4 * q];
+      recv_m[q] = xb[4 * q + 1];
+      if (recv_u[q] > X.nbq[q])
+        throw HipFail{"exchange: peer " + std::to_string(q) + " announced " + std::to_string(recv_u[q]) +
+                      " U records for " + std::to_string(X.nbq[q]) + " boundary vertices"};
+    }
+    any |= xb[4 * q + 2] != 0;  // the vote: some partition changed a label (self included)
   }
-  bool over = false;
-  for (int q = 0; q < P; q++) over |= sent[q] > xs.scap[q];
-  if (over) {  // the counts were exact; the records did not all fit: pack again, larger
-    grow_regions(&xs.sbuf, xs.scap, sent, P, s.stream);
-    const XPeers L = peers_layout(c, xs.scap, X.xs_off, nullptr);
-    timed_launch(c, si, KID_XPACK, 0.0, [&] { launch_xpack_rec(s.stream, L, X.xsend, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
-                     s.lab[r & 1], s.uw[r & 1], xs.sbuf, xs.scnt, s.ccount, dense_div(c), r,
-                   c->pk.n_own); });
-    HIPCHK(hipMemsetAsync(xs.scnt, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
+  if (sent_m > xs.smcap) {  // the counts were exact; the M records did not all fit: pack again, larger
+    grow_regions(&xs.sm, &xs.smcap, &sent_m, 1, s.stream);
+    part_pack(c, si, r);
+    HIPCHK(hipMemsetAsync(xs.cnt, 0, sizeof(unsigned long long) * 2, s.stream));
   }
   if (!any) {  // every partition voted to halt
     s.r_final = r;
@@ -1305,49 +1423,63 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     return;
   }
   const int par = r & 1;
-  // ghosts whose words records of step r-2 set (their records are still in rbuf[par])
-  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par],
-                s.uw[par]); });
+  // ghosts whose words records of step r-2 set (their records are still in ru / rm [par])
+  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xbc_clear(s.stream, bc_in(c, xs, par), s.chg[par], s.uw[par]); });
   bool rover = false;
-  for (int q = 0; q < P; q++) rover |= recv[q] > xs.rcap[q];
-  if (rover) {  // a larger layout for both parities; the other parity's records of step r-1 are
+  for (int q = 0; q < P; q++) rover |= recv_m[q] > xs.rmcap[q];
+  if (rover) {  // a larger M layout for both parities; the other parity's records of step r-1 are
                 // read once more (their clear, two supersteps from now), so they move over
     int64_t old_cap[kMaxParts];
-    std::copy(xs.rcap, xs.rcap + kMaxParts, old_cap);
-    grow_regions(&xs.rbuf[par], xs.rcap, recv, P, s.stream);  // syncs: the clear above has run
-    XRec* nb = alloc_regions<XRec>(xs.rcap, P);
+    std::copy(xs.rmcap, xs.rmcap + kMaxParts, old_cap);
+    grow_regions(&xs.rm[par], xs.rmcap, recv_m, P, s.stream);  // syncs: the clear above has run
+    XRec* nb = alloc_regions<XRec>(xs.rmcap, P);
     int64_t o_old = 0, o_new = 0;
     for (int q = 0; q < P; q++) {
-      if (xs.rcnt[par ^ 1][q])
-        HIPCHK(hipMemcpyAsync(nb + o_new, xs.rbuf[par ^ 1] + o_old, sizeof(XRec) * xs.rcnt[par ^ 1][q],
+      if (xs.rmcnt[par ^ 1][q])
+        HIPCHK(hipMemcpyAsync(nb + o_new, xs.rm[par ^ 1] + o_old, sizeof(XRec) * xs.rmcnt[par ^ 1][q],
                               hipMemcpyDeviceToDevice, s.stream));
       o_old += old_cap[q];
-      o_new += xs.rcap[q];
+      o_new += xs.rmcap[q];
     }
     HIPCHK(hipStreamSynchronize(s.stream));
-    HIPCHK(hipFree(xs.rbuf[par ^ 1]));
-    xs.rbuf[par ^ 1] = nb;
+    HIPCHK(hipFree(xs.rm[par ^ 1]));
+    xs.rm[par ^ 1] = nb;
   }
-  {
-    const XPeers Ls = peers_layout(c, xs.scap, X.xs_off, nullptr);
-    const XPeers Lr = peers_layout(c, xs.rcap, X.xr_off, nullptr);
+  std::copy(recv_u, recv_u + kMaxParts, xs.rucnt[par]);
+  std::copy(recv_m, recv_m + kMaxParts, xs.rmcnt[par]);
+  const XBcIn in = bc_in(c, xs, par);
+  {  // the broadcast: our U list and M list to every peer, theirs into their regions
     std::vector<void*> sp(P), rp(P);
     std::vector<size_t> sb(P), rb(P);
     for (int q = 0; q < P; q++) {
-      sp[q] = xs.sbuf + Ls.base[q];
-      rp[q] = xs.rbuf[par] + Lr.base[q];
-      sb[q] = sizeof(XRec) * (size_t)sent[q];
-      rb[q] = sizeof(XRec) * (size_t)recv[q];
+      sp[q] = xs.su;
+      rp[q] = xs.ru[par] + in.U.base[q];
+      sb[q] = q == me ? 0 : sizeof(unsigned long long) * (size_t)sent_u;
+      rb[q] = q == me ? 0 : sizeof(unsigned long long) * (size_t)recv_u[q];
+      xs.bytes[1] += (double)sb[q];
+    }
+    xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
+    for (int q = 0; q < P; q++) {
+      sp[q] = xs.sm;
+      rp[q] = xs.rm[par] + in.M.base[q];
+      sb[q] = q == me ? 0 : sizeof(XRec) * (size_t)sent_m;
+      rb[q] = q == me ? 0 : sizeof(XRec) * (size_t)recv_m[q];
       xs.bytes[1] += (double)sb[q];
     }
     xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
   }
-  std::copy(recv, recv + kMaxParts, xs.rcnt[par]);
-  const XPeers Lin = peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]);
-  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xunpack_rec(s.stream, Lin, xs.rbuf[par], X.xr_v, s.lab[par], s.chg[par], s.uw[par],
-                     chg_bits(c, s, r).next); });
-  timed_launch(c, si, KID_XMARK, 0.0, [&] { launch_xmark(s.stream, Lin, xs.rbuf[par], X.xr_v, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3], s.tcut,
-               s.iem ? &s.ebp : nullptr, s.ccount, dense_div(c), r); });
+  if (c->inject_rec)  // fault injection (tests): one received U record names no boundary vertex
+    for (int q = 0; q < P; q++)
+      if (recv_u[q]) {
+        HIPCHK(hipMemsetAsync((char*)(xs.ru[par] + in.U.base[q]) + 4, 0xff, 4, s.stream));
+        c->inject_rec = false;
+        break;
+      }
+  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xbc_unpack(s.stream, in, s.lab[par], s.chg[par], s.uw[par], chg_bits(c, s, r).next); });
+  timed_launch(c, si, KID_XMARK, 0.0, [&] {
+    launch_xbc_mark(s.stream, in, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3], s.tcut, s.iem ? &s.ebp : nullptr,
+                    s.ccount, dense_div(c), r);
+  });
   // the vote is global: superstep r+1 runs here even if nothing changed here
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(s.stepcnt + r), 1, 1, s.stream));
   const bool hv = g.n_seg > 0;
@@ -1398,7 +1530,7 @@ void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc) {
     launch_part_count(s.stream, false, L, X.own, nviews, s.vm, s.vadj, uw, s.lab[s.r_final & 1], s.counts, s.iso,
                       xs.htot, xs.hsbuf);
   });
-  launch_xcounts(s.stream, P, c->part, xs.htot, nullptr, xs.xab);
+  launch_xcounts(s.stream, P, c->part, xs.htot, xs.xab);
   HIPCHK(hipGetLastError());
   xs.x->alltoall_i64(xs.xab, xs.xab + 2 * P, 2, s.stream);
   HIPCHK(hipMemcpyAsync(xs.h_xab, xs.xab, sizeof(int64_t) * 4 * P, hipMemcpyDeviceToHost, s.stream));
@@ -1462,9 +1594,9 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
   xs.x->allreduce_u64(s.stats + kViews, 5 * kViews, false, s.stream);
   // the batch's ghost change words back to zero (the next batch's ghosts start clean)
   for (int par = 0; par < 2; par++) {
-    timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xclear(s.stream, peers_layout(c, xs.rcap, X.xr_off, xs.rcnt[par]), xs.rbuf[par], X.xr_v, s.chg[par],
-                s.uw[par]); });
-    std::fill(xs.rcnt[par], xs.rcnt[par] + kMaxParts, 0);
+    timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xbc_clear(s.stream, bc_in(c, xs, par), s.chg[par], s.uw[par]); });
+    std::fill(xs.rucnt[par], xs.rucnt[par] + kMaxParts, 0);
+    std::fill(xs.rmcnt[par], xs.rmcnt[par] + kMaxParts, 0);
   }
   HIPCHK(hipGetLastError());
   finish_tail(c, si, rc);
@@ -1667,7 +1799,8 @@ void reset_after_failure(rgpu_ctx* c) {
   for (Slot& s : c->slot)
     for (void* p : {(void*)s.hv.segcnt, (void*)s.hv.segor, (void*)s.hv.best, (void*)s.hv.pacc}) drop_alloc(LG, p);
   for (XSlot& xs : c->pt.xs)
-    for (void* p : {(void*)xs.scnt, (void*)xs.htot, (void*)xs.xab, (void*)xs.vms, (void*)xs.vmr}) drop_alloc(LG, p);
+    for (void* p : {(void*)xs.cnt, (void*)xs.err, (void*)xs.htot, (void*)xs.xab, (void*)xs.vms, (void*)xs.vmr})
+      drop_alloc(LG, p);
   release_slots(c);
   free_part_slots(c, true);
   c->algo = -1;
@@ -1861,7 +1994,7 @@ XSend build_send_plan(int64_t n_own, const Part& X, std::vector<void*>& L) {
   std::vector<void*> T;
   XSend xs;
   try {
-    xs = build_xsend(nullptr, n_own, X.nxs, X.xs_v, X.xs_q, X.xs_off_d, T, L);
+    xs = build_xsend(nullptr, n_own, X.nxs, X.xs_v, T, L);
   } catch (const std::runtime_error& e) {
     for (void* p : T) (void)hipFree(p);
     throw HipFail{e.what()};
@@ -2244,6 +2377,9 @@ int rgpu_seal(rgpu_ctx* c) {
   const auto t0 = std::chrono::steady_clock::now();
   try {
     HIPCHK(hipSetDevice(c->device));
+    // partitioned: the broadcast records' receive tables name the peers' boundary lists, which any
+    // partition's seal may change — every partition rebuilds them (collectively) at its next run
+    c->pt.tab_ready = false;
     if (c->n_sealed > 0 && c->n_sealed == c->events.size()) {  // nothing new since the last seal
       c->sealed = true;
       return RGPU_OK;
@@ -2376,7 +2512,7 @@ int rgpu_newest_time(rgpu_ctx* c, int64_t* out) {
 }
 
 int rgpu_exchange_id(int kind, uint8_t* out) {
-  if (!out || (kind != RGPU_XCHG_RCCL && kind != RGPU_XCHG_LOOPBACK)) return RGPU_EINVAL;
+  if (!out || (kind != RGPU_XCHG_RCCL && kind != RGPU_XCHG_LOOPBACK && kind != RGPU_XCHG_SHM)) return RGPU_EINVAL;
   return make_exchange_id(kind, out).empty() ? RGPU_OK : RGPU_EHIP;
 }
 
@@ -2450,6 +2586,10 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   // knobs re-read per run (profile passes and tests on one sealed graph)
   c->prof_lean = env_int("RGPU_PROF_LEAN", 0) != 0;
   c->inject_fail = env_int("RGPU_INJECT_FAIL", 0);
+  {
+    const char* e = std::getenv("RGPU_INJECT_FAIL");
+    c->inject_rec = e && std::strcmp(e, "rec") == 0;
+  }
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   try {
     HIPCHK(hipSetDevice(c->device));
@@ -2571,6 +2711,18 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
       std::fclose(tf);
     }
     c->steprec.clear();
+    // (after the run's last collective, so that every partition has left the exchange)
+    if (c->partitioned) {  // received label records outside the exchange plan (xchg.hip bc_rec): a bug upstream
+      unsigned long long bad = 0;
+      for (const XSlot& xs : c->pt.xs)
+        if (xs.err) {
+          unsigned long long e = 0;
+          HIPCHK(hipMemcpy(&e, xs.err, sizeof(e), hipMemcpyDeviceToHost));
+          bad += e;
+        }
+      if (bad)
+        throw HipFail{"exchange: " + std::to_string(bad) + " received label records outside the receive plan"};
+    }
   } catch (const HipFail& f) {
     exchange_quiesce();
     reset_after_failure(c);

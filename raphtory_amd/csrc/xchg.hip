@@ -94,108 +94,81 @@ __global__ __launch_bounds__(256) void k_xvm_unpack(int64_t nx, const int32_t* _
   }
 }
 
-// ------------------------------------------------------------------ label records
-// Boundary entry e (owned vertex xv[e], peer xq[e]) is sent when the vertex was visited in the
-// step (act; null = every member, superstep 1) and changed in a view where it has a kept
-// neighbour (vadj, the OR of its kept slot masks).  Per distinct new label one record with the
-// views holding it.  A wave takes 64 entries: it counts the records per peer (lane q), reserves
-// them with one atomicAdd per (wave, peer), then writes them; scnt counts past the capacity
-// too, so the host sees an overflow and repeats the pack into a larger buffer.
-// A wave takes a run of kPackRun chunks of 64 boundary vertices: it counts its records per peer over
-// the whole run, reserves them with one atomicAdd per peer, then writes them.  (Runs of 16 chunks,
-// to cut the reservations on the 8 counters, measured 4.7x slower at P = 8: the pack is bound by
-// each chunk's chain of dependent loads, and fewer, longer waves hide less of it.)
-constexpr int kPackRun = 1;
-__device__ __forceinline__ void pack_chunk(bool write, const XPeers& P, const XSend& X, int64_t c,
-                                           const uint8_t* __restrict__ act, const uint64_t* __restrict__ chg_now,
-                                           const uint64_t* __restrict__ vadj, const int32_t* __restrict__ lab,
-                                           const int32_t* __restrict__ uw, XRec* __restrict__ sbuf,
-                                           unsigned long long& cq, unsigned long long& off, int lane) {
-  // lane = boundary vertex (ascending owned rank): its words are read once for all its peers
-  const int64_t b = c * 64 + lane;
-  const bool ok = b < X.nb;
-  const int32_t v = ok ? X.v[b] : 0;
-  const uint32_t pm = ok ? X.pm[b] : 0u;
-  uint64_t m = 0;
-  if (ok && (act == nullptr || act[v])) m = chg_now[v] & vadj[v];
-  if (!__ballot(m != 0)) return;
-  // A uniform sender (its word is its row) has one label: one record per peer, written by its own
-  // lane.  Only mixed senders walk their distinct labels one by one (lane = view).
-  const int32_t u = (m != 0 && uw) ? uw_label(uw[v]) : kMixed;
-  const bool uni = m != 0 && u != kMixed;
-  const uint64_t mixed = __ballot(m != 0 && !uni);
-  for (int p = 0; p < P.np; p++) {  // uniform records, in lane order per peer
-    const uint64_t bp = __ballot(uni && ((pm >> p) & 1));
-    if (!bp) continue;
-    if (write) {
-      const unsigned long long base = __builtin_amdgcn_readlane((uint32_t)off, p) |
-                                      ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(off >> 32), p) << 32);
-      if ((bp >> lane) & 1) {
-        const unsigned long long pos = base + __popcll(bp & lanemask_below(lane));
-        if (pos < (unsigned long long)P.cap[p]) {
-          XRec r;
-          r.e = X.e[b * kMaxParts + p];
-          r.val = (int32_t)((uint32_t)u | 0x80000000u);  // sign bit: sender uniform
-          r.mask = m;
-          sbuf[P.base[p] + pos] = r;
-        }
-      }
-      if (lane == p) off += (unsigned long long)__popcll(bp);
-    } else if (lane == p) {
-      cq += (unsigned long long)__popcll(bp);
-    }
-  }
-  for (uint64_t bb = mixed; bb; bb &= bb - 1) {  // mixed senders: per distinct label, per peer
-    const int L = __builtin_ctzll(bb);
-    const int32_t vL = __builtin_amdgcn_readlane(v, L);
-    const uint32_t pmL = __builtin_amdgcn_readlane(pm, L);
-    const int64_t bL = c * 64 + L;
-    uint64_t mm = rl64(m, L);
-    const int32_t x = lab[(int64_t)vL * 64 + lane];
-    while (mm) {
-      const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
-      const uint64_t same = __ballot(((mm >> lane) & 1) && x == val);
-      if (write) {
-        for (uint32_t pp = pmL; pp; pp &= pp - 1) {
-          const int p = __builtin_ctz(pp);
-          const unsigned long long pos = __builtin_amdgcn_readlane((uint32_t)off, p) |
-                                         ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(off >> 32), p) << 32);
-          if (lane == 0 && pos < (unsigned long long)P.cap[p]) {
-            XRec r;
-            r.e = X.e[bL * kMaxParts + p];
-            r.val = val;
-            r.mask = same;
-            sbuf[P.base[p] + pos] = r;
-          }
-          if (lane == p) off++;
-        }
-      } else if (lane < 32 && ((pmL >> lane) & 1)) {
-        cq++;
-      }
-      mm &= ~same;
-    }
-  }
-}
-__global__ __launch_bounds__(256) void k_xpack_rec(XPeers P, XSend X, const uint8_t* __restrict__ act,
-                                                   const uint64_t* __restrict__ chg_now,
-                                                   const uint64_t* __restrict__ vadj,
-                                                   const int32_t* __restrict__ lab,
-                                                   const int32_t* __restrict__ uw, XRec* __restrict__ sbuf,
-                                                   unsigned long long* __restrict__ scnt,
-                                                   const int32_t* __restrict__ ccount, int dense_div, int step,
-                                                   int64_t n_own) {
+// ------------------------------------------------------------------ label records (broadcast)
+// After superstep r every partition broadcasts ONE list of records for its changed boundary
+// vertices to all peers (the ReaderWorker's VertexMessage traffic, VertexVisitor.messageAllNeighbours
+// :112-120, sent once per vertex instead of once per (vertex, peer)).  A boundary vertex is named by
+// its index b in the sender's boundary list (ascending owned rank); a receiver maps (peer q, b) to
+// its ghost rank through tab[toff[q] + b] (-1: q's vertex is no ghost here, the record is skipped).
+//   U record (8 B): b << 32 | label — a uniform sender (kernels.hpp kMixed) that changed in every
+//                   member view where it has a kept neighbour: the ghost takes the label as its
+//                   uniform word and changed in all views (its readers fold a changed uniform
+//                   neighbour on every kept view of the slot; kept masks lie inside the sender's
+//                   kept-neighbour views, so "all" marks exactly the same neighbours).
+//   M record (16 B, XRec): {b, label, views} per distinct new label of a mixed sender, or the one
+//                   label of a uniform sender that changed in only part of its views.
+// A sender's U records need at most nb slots (one per boundary vertex): U buffers are sized for the
+// worst case at plan time and never grow; M records (mixed senders: rare) grow on demand.
+__global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, const int32_t* __restrict__ bidx,
+                                                  const uint8_t* __restrict__ act, const uint64_t* __restrict__ chg_now,
+                                                  const uint64_t* __restrict__ vadj, const uint64_t* __restrict__ vm,
+                                                  const int32_t* __restrict__ lab, const int32_t* __restrict__ uw,
+                                                  unsigned long long* __restrict__ su, XRec* __restrict__ sm, int64_t mcap,
+                                                  unsigned long long* __restrict__ cnt, const int32_t* __restrict__ ccount,
+                                                  int dense_div, int step) {
   const int lane = lane_of();
   if (dense_after(ccount, step, n_own, dense_div)) act = nullptr;  // the step visited every member
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t nchunks = (X.nb + 63) / 64;
-  for (int64_t c0 = wave * kPackRun; c0 < nchunks; c0 += nwaves * kPackRun) {
-    const int64_t c1 = c0 + kPackRun < nchunks ? c0 + kPackRun : nchunks;
-    unsigned long long cq = 0, off = 0;  // lane p: this run's records for peer p, then its next position
-    for (int64_t c = c0; c < c1; c++) pack_chunk(false, P, X, c, act, chg_now, vadj, lab, uw, sbuf, cq, off, lane);
-    if (!__ballot(cq != 0)) continue;
-    if (lane < P.np && cq) off = atomicAdd(&scnt[lane], cq);
-    for (int64_t c = c0; c < c1; c++) pack_chunk(true, P, X, c, act, chg_now, vadj, lab, uw, sbuf, cq, off, lane);
+  for (int64_t v0 = wave * 64; v0 < n_own; v0 += nwaves * 64) {
+    // lane = owned vertex: every load coalesced
+    const int64_t v = v0 + lane;
+    const bool ok = v < n_own;
+    const int32_t b = ok ? bidx[v] : -1;
+    const bool vis = b >= 0 && (act == nullptr || act[v]);
+    const uint64_t m = vis ? chg_now[v] & vadj[v] : 0;
+    if (!__ballot(m != 0)) continue;
+    const int32_t u = m ? uw_label(uw[v]) : kMixed;
+    const bool full = m != 0 && u != kMixed && m == (vm[v] & vadj[v]);
+    const uint64_t bu = __ballot(full);
+    if (bu) {
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(&cnt[0], (unsigned long long)__popcll(bu));
+      base = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(base >> 32), 0) << 32) |
+             __builtin_amdgcn_readlane((uint32_t)base, 0);
+      if (full) su[base + __popcll(bu & lanemask_below(lane))] = ((unsigned long long)(uint32_t)b << 32) | (uint32_t)u;
+    }
+    for (uint64_t mb = __ballot(m != 0 && !full); mb; mb &= mb - 1) {  // M senders, one at a time
+      const int L = __builtin_ctzll(mb);
+      const int32_t bL = __builtin_amdgcn_readlane(b, L);
+      const int32_t uL = __builtin_amdgcn_readlane(u, L);
+      const uint64_t mL = rl64(m, L);
+      if (uL != kMixed) {  // uniform, partly changed: its one label in the changed views
+        unsigned long long pos = 0;
+        if (lane == 0) {
+          pos = atomicAdd(&cnt[1], 1ull);
+          if (pos < (unsigned long long)mcap) sm[pos] = XRec{bL, uL, mL};
+        }
+        continue;
+      }
+      const int64_t vL = v0 + L;
+      const int32_t x = lab[vL * 64 + lane];
+      int k = 0;  // distinct labels over the changed views: count, reserve, write
+      for (uint64_t mm = mL; mm; k++) {
+        const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
+        mm &= ~__ballot(((mm >> lane) & 1) && x == val);
+      }
+      unsigned long long pos = 0;
+      if (lane == 0) pos = atomicAdd(&cnt[1], (unsigned long long)k);
+      pos = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(pos >> 32), 0) << 32) |
+            __builtin_amdgcn_readlane((uint32_t)pos, 0);
+      for (uint64_t mm = mL; mm; pos++) {
+        const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
+        const uint64_t same = __ballot(((mm >> lane) & 1) && x == val);
+        if (lane == 0 && pos < (unsigned long long)mcap) sm[pos] = XRec{bL, val, same};
+        mm &= ~same;
+      }
+    }
   }
 }
 
@@ -206,89 +179,142 @@ __global__ __launch_bounds__(256) void k_xsend_flag(int64_t nx, const int32_t* _
     flag[xv[e]] = 1;  // (idempotent plain stores)
 }
 __global__ __launch_bounds__(256) void k_xsend_list(int64_t n_own, const int32_t* __restrict__ flag,
-                                                    const int32_t* __restrict__ pos, int32_t* __restrict__ xb) {
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n_own; v += (int64_t)gridDim.x * blockDim.x)
-    if (flag[v]) xb[pos[v]] = (int32_t)v;
+                                                    const int32_t* __restrict__ pos, int32_t* __restrict__ xb,
+                                                    int32_t* __restrict__ bidx) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n_own; v += (int64_t)gridDim.x * blockDim.x) {
+    const bool f = flag[v] != 0;
+    if (f) xb[pos[v]] = (int32_t)v;
+    bidx[v] = f ? pos[v] : -1;
+  }
 }
 __global__ __launch_bounds__(256) void k_xsend_entries(int64_t nx, const int32_t* __restrict__ xv,
-                                                       const int32_t* __restrict__ xq, const int64_t* __restrict__ xoff,
-                                                       const int32_t* __restrict__ pos, int32_t* __restrict__ xe,
-                                                       uint32_t* __restrict__ pm) {
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nx; e += (int64_t)gridDim.x * blockDim.x) {
-    const int q = xq[e];
-    const int64_t b = pos[xv[e]];
-    xe[b * kMaxParts + q] = (int32_t)(e - xoff[q]);
-    atomicOr(&pm[b], 1u << q);
+                                                       const int32_t* __restrict__ pos, int32_t* __restrict__ eb) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nx; e += (int64_t)gridDim.x * blockDim.x)
+    eb[e] = pos[xv[e]];
+}
+// receive tables: peer q's boundary index of receive entry i (tmp) -> the ghost rank it names
+__global__ __launch_bounds__(256) void k_xtab_fill(int64_t n, const int32_t* __restrict__ xr_v,
+                                                   const int32_t* __restrict__ xr_q, const int32_t* __restrict__ tmp,
+                                                   XTab T, unsigned long long* __restrict__ err) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int q = xr_q[i];
+    const int32_t b = tmp[i];
+    if (b < 0 || (int64_t)b >= T.toff[q + 1] - T.toff[q]) {
+      atomicAdd(err, 1ull);
+      continue;
+    }
+    T.tab[T.toff[q] + b] = xr_v[i];
   }
 }
 
-// counts exchange words: [2q] = records for q (0 for self), [2q+1] = this partition changed a
-// label in the step (the halting vote, AnalysisTask.endStep :208-225); the counters are reset
-// for the next pack
-__global__ void k_xcounts(int np, int me, unsigned long long* __restrict__ scnt, const int32_t* __restrict__ stepflag,
-                          int64_t* __restrict__ xa) {
+// counts exchange words, 4 per peer: [4q] U records, [4q+1] M records (the same broadcast list
+// for every peer; 0 for self), [4q+2] this partition changed a label in the step (the halting vote,
+// AnalysisTask.endStep :208-225), [4q+3] 0.  The counters are reset for the next pack.
+__global__ void k_xbc_counts(int np, int me, unsigned long long* __restrict__ cnt, const int32_t* __restrict__ stepflag,
+                             int64_t* __restrict__ xa) {
+  const int q = threadIdx.x;  // one wave: every lane reads the counters before lane 0 resets them
+  const unsigned long long nu = cnt[0], nm = cnt[1];
+  if (q < np) {
+    xa[4 * q] = q == me ? 0 : (int64_t)nu;
+    xa[4 * q + 1] = q == me ? 0 : (int64_t)nm;
+    xa[4 * q + 2] = stepflag ? (stepflag[0] != 0) : 0;
+    xa[4 * q + 3] = 0;
+  }
+  if (q == 0) cnt[0] = cnt[1] = 0;
+}
+// component-count records (one region per peer): [2q] = records for q, [2q+1] = 0
+__global__ void k_xcounts(int np, int me, unsigned long long* __restrict__ scnt, int64_t* __restrict__ xa) {
   const int q = threadIdx.x;
   if (q >= np) return;
   xa[2 * q] = q == me ? 0 : (int64_t)scnt[q];
-  xa[2 * q + 1] = stepflag ? (stepflag[0] != 0) : 0;
+  xa[2 * q + 1] = 0;
   scnt[q] = 0;
 }
 
-// ghosts whose change word a record set two supersteps ago: clear it in that parity's words, and
-// set their uniform word back to kGhostQuiet (uw non-null)
-__global__ __launch_bounds__(256) void k_xclear(XPeers P, const XRec* __restrict__ rbuf,
-                                                const int32_t* __restrict__ xrv, uint64_t* __restrict__ chg,
-                                                int32_t* __restrict__ uw) {
-  const int64_t n = P.pre[P.np];
+// record i of a received broadcast (U records of every peer, then M records of every peer, XBcIn)
+// -> the ghost it names (-1: none here; out-of-plan records are counted into err and skipped — a
+// bug upstream, reported by the run instead of faulting the device)
+__device__ __forceinline__ int64_t bc_total(const XBcIn& I) { return I.U.pre[I.U.np] + I.M.pre[I.M.np]; }
+// (b, label, views, is_u) of record i and the ghost it names
+__device__ __forceinline__ int32_t bc_rec(const XBcIn& I, int64_t i, int32_t& b, int32_t& val, uint64_t& mask, bool& isu,
+                                          bool& first) {
+  const int64_t nu = I.U.pre[I.U.np];
+  int q;
+  first = true;
+  if (i < nu) {
+    q = peer_of(I.U, i);
+    const unsigned long long r = I.ru[I.U.base[q] + i - I.U.pre[q]];
+    b = (int32_t)(r >> 32);
+    val = (int32_t)(uint32_t)r;
+    mask = ~0ull;
+    isu = true;
+  } else {
+    const int64_t k = i - nu;
+    q = peer_of(I.M, k);
+    const int64_t j = I.M.base[q] + k - I.M.pre[q];
+    const XRec r = I.rm[j];
+    b = r.e;
+    val = r.val;
+    mask = r.mask;
+    isu = false;
+    first = k == I.M.pre[q] || I.rm[j - 1].e != b;  // a mixed sender's records are consecutive
+  }
+  if (b < 0 || (int64_t)b >= I.T.toff[q + 1] - I.T.toff[q]) {
+    atomicAdd(I.err, 1ull);
+    return -1;
+  }
+  const int32_t g = I.T.tab[I.T.toff[q] + b];
+  if (g >= 0 && (g < I.n_own || g >= I.nv)) {
+    atomicAdd(I.err, 1ull);
+    return -1;
+  }
+  return g;
+}
+
+// ghosts whose words records of two supersteps ago set: clear their change words in that parity and
+// set their uniform word back to kGhostQuiet
+__global__ __launch_bounds__(256) void k_xbc_clear(XBcIn I, uint64_t* __restrict__ chg, int32_t* __restrict__ uw) {
+  const int64_t n = bc_total(I);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int q = peer_of(P, i);
-    const int32_t g = xrv[P.xoff[q] + rbuf[P.base[q] + i - P.pre[q]].e];
+    int32_t b, val;
+    uint64_t mask;
+    bool isu, first;
+    const int32_t g = bc_rec(I, i, b, val, mask, isu, first);
+    if (g < 0) continue;
     chg[g] = 0;
-    if (uw) uw[g] = kGhostQuiet;
+    uw[g] = kGhostQuiet;
   }
 }
 
-// Records into ghost rows: the record's label in its views, and its views into the ghost's
-// change word (a ghost's records arrive together; the OR collects them).  A record whose sender's
-// row is uniform (sign bit of val; it is then the ghost's only record of the step) sets the
-// ghost's uniform word instead of its row, lane = record: readers only gather a ghost in the views
-// its change word holds, which are the record's.  Other records mark the ghost mixed (kernels.hip
-// kMixed), one per wave iteration with lane = view.  (Four records per wave, 16 lanes each, with
-// two atomics per record, made the unpack the largest partitioned kernel.)
-__global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __restrict__ rbuf,
-                                                     const int32_t* __restrict__ xrv, int32_t* __restrict__ lab,
-                                                     uint64_t* __restrict__ chg, int32_t* __restrict__ uw,
-                                                     uint64_t* __restrict__ cb) {
-  const int64_t n = P.pre[P.np];
+// Records into ghost words / rows, lane = record: a U record's ghost takes the label as its uniform
+// word (changed flag set) and changed in every view (plain stores: a ghost has one sender and a U
+// sender sends one record).  M records mark the ghost mixed (kMixed) and write the label into the
+// row lanes of their views, the views OR-ed into the change word (one per wave iteration, lane = view).
+__global__ __launch_bounds__(256) void k_xbc_unpack(XBcIn I, int32_t* __restrict__ lab, uint64_t* __restrict__ chg,
+                                                    int32_t* __restrict__ uw, uint64_t* __restrict__ cb) {
+  const int64_t n = bc_total(I);
   const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t i0 = wave * 64; i0 < n; i0 += nwaves * 64) {
-    // lane = record: a uniform record is its ghost's only record of the step, so its word and
-    // change word are plain stores; mixed records (rows, OR-ed change words) one by one below
     const int64_t i = i0 + lane;
-    const bool ok = i < n;
-    XRec r{0, 0, 0};
-    int32_t g = 0;
-    if (ok) {
-      const int q = peer_of(P, i);
-      r = rbuf[P.base[q] + i - P.pre[q]];
-      g = xrv[P.xoff[q] + r.e];
-    }
-    const bool uni = ok && uw && r.val < 0;
-    if (uni) {
-      uw[g] = uw_word(r.val & 0x7fffffff, true);  // the ghost changed in this step (kChgFlag)
-      chg[g] = r.mask;
+    int32_t b = 0, val = 0, g = -1;
+    uint64_t mask = 0;
+    bool isu = false, first = false;
+    if (i < n) g = bc_rec(I, i, b, val, mask, isu, first);
+    if (g >= 0 && isu) {
+      uw[g] = uw_word(val, true);
+      chg[g] = ~0ull;
       if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // (ChgBits)
     }
-    for (uint64_t b = __ballot(ok && !uni); b; b &= b - 1) {
-      const int L = __builtin_ctzll(b);
+    for (uint64_t bb = __ballot(g >= 0 && !isu); bb; bb &= bb - 1) {
+      const int L = __builtin_ctzll(bb);
       const int32_t gL = __builtin_amdgcn_readlane(g, L);
-      const int32_t val = __builtin_amdgcn_readlane(r.val, L) & 0x7fffffff;
-      const uint64_t mL = rl64(r.mask, L);
-      if ((mL >> lane) & 1) lab[(int64_t)gL * 64 + lane] = val;
+      const int32_t vL = __builtin_amdgcn_readlane(val, L);
+      const uint64_t mL = rl64(mask, L);
+      if ((mL >> lane) & 1) lab[(int64_t)gL * 64 + lane] = vL;
       if (lane == 0) {
-        if (uw) uw[gL] = kMixed;
+        uw[gL] = kMixed;
         atomicOr((unsigned long long*)&chg[gL], (unsigned long long)mL);
         if (cb) atomicOr((unsigned long long*)&cb[gL >> 6], 1ull << (gL & 63));
       }
@@ -296,71 +322,117 @@ __global__ __launch_bounds__(256) void k_xunpack_rec(XPeers P, const XRec* __res
   }
 }
 
-// After the unpack: the first record of every ghost marks the ghost's owned neighbours that
-// share a changed view (the next frontier, as a local change would).  Ghosts keep no compacted
-// slots (K2 runs over the owned vertices only): the kept views of a static slot, bits & vm[nb] &
-// vm[g], are recomputed here for the ghosts that changed, over the time-ordered slots up to the
-// batch's cut (bits: K2's inline edge bits for a simple slot, else em[e]; without time-ordered
-// slots the CSR order and em).  Nothing to mark when superstep r is dense (the next one visits
-// every member).  Heavy ghosts: k_heavy_mark.
+// After the unpack: every changed ghost (a U record, or the first M record of its sender) marks its
+// owned neighbours that share a changed view (the next frontier, as a local change would).  Ghosts
+// keep no compacted slots (K2 runs over the owned vertices only): the kept views of a static slot,
+// bits & vm[nb] & vm[g], are recomputed here over the time-ordered slots up to the batch's cut (bits:
+// K2's inline edge bits for a simple slot, else em[e]; without time-ordered slots the CSR order and
+// em).  A ghost holds only its edges to this partition's vertices (a few slots), so a wave takes 64
+// records (lane = record) and packs their ghosts' slot lists into 64-lane passes (lane = slot), as K2
+// packs its light members; ghosts with more than 64 static slots walk theirs one at a time.  Nothing
+// to mark when superstep r is dense (the next one visits every member).  Heavy ghosts: k_heavy_mark.
 template <bool TS>
-__global__ __launch_bounds__(256) void k_xmark(XPeers P, const XRec* __restrict__ rbuf,
-                                               const int32_t* __restrict__ xrv, const uint64_t* __restrict__ chg,
-                                               const int64_t* __restrict__ out_off,
-                                               const int64_t* __restrict__ in_off,
-                                               const int32_t* __restrict__ in_eid,
-                                               const int32_t* __restrict__ esrc, const int32_t* __restrict__ edst,
-                                               const uint64_t* __restrict__ vm, const uint64_t* __restrict__ em,
-                                               const int32_t* __restrict__ hv_of, uint8_t* __restrict__ act_next,
-                                               const int64_t* __restrict__ adj_off, const int32_t* __restrict__ ts_e,
-                                               const int32_t* __restrict__ ts_nb, const int64_t* __restrict__ ts_t,
-                                               int64_t tcut, BatchParams ebp, int iem,
-                                               const int32_t* __restrict__ ccount, int dense_div, int step,
-                                               int64_t n_own, int64_t nv_all) {
-  if (dense_after(ccount, step + 1, n_own, dense_div)) return;  // step r dense: r+1 visits every member
+__device__ __forceinline__ void mark_slot(int64_t p, int32_t g, uint64_t ch, const int64_t* __restrict__ ts_t,
+                                          const int32_t* __restrict__ ts_nb, const int32_t* __restrict__ ts_e,
+                                          int64_t tcut, const HopLDS& L, const BatchParams& ebp, int iem,
+                                          const uint64_t* __restrict__ vm, const uint64_t* __restrict__ em,
+                                          uint8_t* __restrict__ act_next) {
+  const int64_t tsw = ts_t[p];
+  if (ts_time(tsw) < tcut) return;
+  const int32_t nb = ts_nb[p];
+  if (nb == g) return;
+  const uint64_t bits = (iem && ts_simple(tsw)) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[ts_e[p]];
+  if (bits & vm[nb] & ch) act_next[nb] = 1;
+}
+template <bool TS>
+__global__ __launch_bounds__(256) void k_xbc_mark(XBcIn I, const uint64_t* __restrict__ chg,
+                                                  const int64_t* __restrict__ out_off,
+                                                  const int64_t* __restrict__ in_off,
+                                                  const int32_t* __restrict__ in_eid,
+                                                  const int32_t* __restrict__ esrc, const int32_t* __restrict__ edst,
+                                                  const uint64_t* __restrict__ vm, const uint64_t* __restrict__ em,
+                                                  const int32_t* __restrict__ hv_of, uint8_t* __restrict__ act_next,
+                                                  const int64_t* __restrict__ adj_off, const int32_t* __restrict__ ts_e,
+                                                  const int32_t* __restrict__ ts_nb, const int64_t* __restrict__ ts_t,
+                                                  int64_t tcut, BatchParams ebp, int iem,
+                                                  const int32_t* __restrict__ ccount, int dense_div, int step) {
+  if (dense_after(ccount, step + 1, I.n_own, dense_div)) return;  // step r dense: r+1 visits every member
   __shared__ HopLDS L;
   if (TS && iem) hop_lds_init(L, ebp, ebp.thr_e);
-  const int64_t n = P.pre[P.np];
+  const int64_t n = bc_total(I);
   const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t i = wave; i < n; i += nwaves) {
-    const int q = peer_of(P, i);
-    const int64_t k = i - P.pre[q];
-    const int32_t e0 = rbuf[P.base[q] + k].e;
-    if (k > 0 && rbuf[P.base[q] + k - 1].e == e0) continue;  // not the ghost's first record
-    // (bounds guards: a record outside the plan is a bug upstream — the parity tests see its
-    // missing marks — and must not become a fault that takes the device down)
-    if (e0 < 0 || e0 >= P.xoff[q + 1] - P.xoff[q]) continue;
-    const int32_t g = xrv[P.xoff[q] + e0];
-    if (g < 0 || g >= nv_all) continue;
-    if (hv_of && hv_of[g] >= 0) continue;
-    const uint64_t ch = chg[g] & vm[g];
-    if (TS) {
-      const int64_t a = adj_off[g], ntot = adj_off[g + 1] - a;
-      for (int64_t c = 0; c < ntot; c += 64) {
-        if (ts_time(ts_t[a + c]) < tcut) break;  // newest first: the rest are dead in every view
-        const int64_t j = c + lane;
-        if (j >= ntot) continue;
-        const int64_t tsw = ts_t[a + j];
-        if (ts_time(tsw) < tcut) continue;
-        const int32_t nb = ts_nb[a + j];
-        if (nb == g) continue;
-        const uint64_t bits = (iem && ts_simple(tsw)) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[ts_e[a + j]];
-        if (bits & vm[nb] & ch) act_next[nb] = 1;
+  for (int64_t i0 = wave * 64; i0 < n; i0 += nwaves * 64) {
+    // lane = record: its ghost, when it is the ghost's first record and the ghost is no hub
+    const int64_t i = i0 + lane;
+    int32_t b, val, g = -1;
+    uint64_t mask;
+    bool isu = false, first = false;
+    if (i < n) g = bc_rec(I, i, b, val, mask, isu, first);
+    const bool go = g >= 0 && first && !(hv_of && hv_of[g] >= 0);
+    uint64_t ch = 0;
+    int64_t a = 0;
+    int32_t k = 0;
+    if (go) {
+      ch = chg[g] & vm[g];
+      if (TS) {
+        a = adj_off[g];
+        k = (int32_t)(adj_off[g + 1] - a);
+      } else {
+        a = out_off[g];
+        k = (int32_t)((out_off[g + 1] - a) + (in_off[g + 1] - in_off[g]));
+      }
+      if (ch == 0) k = 0;
+    }
+    if (!TS) {  // CSR order (no time-ordered slots): one ghost at a time, lane = slot
+      for (uint64_t t = __ballot(k > 0); t; t &= t - 1) {
+        const int Lg = __builtin_ctzll(t);
+        const int32_t gL = __builtin_amdgcn_readlane(g, Lg);
+        const uint64_t chL = rl64(ch, Lg);
+        const int64_t o0 = out_off[gL], i0e = in_off[gL];
+        const int64_t nout = out_off[gL + 1] - o0, ntot = nout + (in_off[gL + 1] - i0e);
+        for (int64_t c = 0; c < ntot; c += 64) {
+          const int64_t j = c + lane;
+          if (j >= ntot) continue;
+          int64_t e;
+          int32_t nb;
+          if (j < nout) { e = o0 + j; nb = edst[e]; }
+          else { e = in_eid[i0e + (j - nout)]; nb = esrc[e]; }
+          if (nb != gL && (em[e] & vm[nb] & chL)) act_next[nb] = 1;
+        }
       }
       continue;
     }
-    const int64_t o0 = out_off[g], i0 = in_off[g];
-    const int64_t nout = out_off[g + 1] - o0, ntot = nout + (in_off[g + 1] - i0);
-    for (int64_t c = 0; c < ntot; c += 64) {
-      const int64_t j = c + lane;
-      if (j >= ntot) continue;
-      int64_t e;
-      int32_t nb;
-      if (j < nout) { e = o0 + j; nb = edst[e]; }
-      else { e = in_eid[i0 + (j - nout)]; nb = esrc[e]; }
-      if (nb != g && (em[e] & vm[nb] & ch)) act_next[nb] = 1;
+    // ghosts with more than 64 static slots: one at a time (newest first: stop at the cut)
+    for (uint64_t t = __ballot(k > 64); t; t &= t - 1) {
+      const int Lg = __builtin_ctzll(t);
+      const int32_t gL = __builtin_amdgcn_readlane(g, Lg);
+      const uint64_t chL = rl64(ch, Lg);
+      const int64_t aL = (int64_t)rl64((uint64_t)a, Lg);
+      const int32_t kL = __builtin_amdgcn_readlane(k, Lg);
+      for (int32_t c = 0; c < kL; c += 64) {
+        if (ts_time(ts_t[aL + c]) < tcut) break;
+        if (c + lane < kL) mark_slot<TS>(aL + c + lane, gL, chL, ts_t, ts_nb, ts_e, tcut, L, ebp, iem, vm, em, act_next);
+      }
+    }
+    // the others packed, lane = slot
+    uint64_t pend = __ballot(k > 0 && k <= 64);
+    while (pend) {
+      int sum = 0, myL = 0, myj = 0;
+      while (pend) {
+        const int Lp = __builtin_ctzll(pend);
+        const int kk = __builtin_amdgcn_readlane(k, Lp);
+        if (sum && sum + kk > 64) break;
+        if (lane >= sum && lane < sum + kk) { myL = Lp; myj = lane - sum; }
+        sum += kk;
+        pend &= pend - 1;
+      }
+      const int64_t aL = (int64_t)(((uint64_t)(uint32_t)__shfl((int)((uint64_t)a >> 32), myL) << 32) |
+                                   (uint32_t)__shfl((int)a, myL));
+      const uint64_t chL = ((uint64_t)(uint32_t)__shfl((int)(ch >> 32), myL) << 32) | (uint32_t)__shfl((int)ch, myL);
+      const int32_t gL = __shfl(g, myL);
+      if (lane < sum) mark_slot<TS>(aL + myj, gL, chL, ts_t, ts_nb, ts_e, tcut, L, ebp, iem, vm, em, act_next);
     }
   }
 }
@@ -560,15 +632,16 @@ void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32
                        int planes, const uint64_t* in, uint64_t* vm, int64_t vstride) {
   if (nx > 0) k_xvm_unpack<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, xq, xoff, planes, in, vm, vstride);
 }
-void launch_xpack_rec(hipStream_t s, const XPeers& P, const XSend& X, const uint8_t* act, const uint64_t* chg_now,
-                      const uint64_t* vadj, const int32_t* lab, const int32_t* uw, XRec* sbuf, unsigned long long* scnt,
-                      const int32_t* ccount, int dense_div, int step, int64_t n_own) {
-  if (X.nb > 0)
-    k_xpack_rec<<<xgrid(X.nb, 4 * 64 * kPackRun, 4096), 256, 0, s>>>(P, X, act, chg_now, vadj, lab, uw, sbuf, scnt, ccount,
-                                                           dense_div, step, n_own);
+void launch_xbc_pack(hipStream_t s, int64_t n_own, const XSend& X, const uint8_t* act, const uint64_t* chg_now,
+                     const uint64_t* vadj, const uint64_t* vm, const int32_t* lab, const int32_t* uw,
+                     unsigned long long* su, XRec* sm, int64_t mcap, unsigned long long* cnt, const int32_t* ccount,
+                     int dense_div, int step) {
+  if (X.nb > 0 && n_own > 0)
+    k_xbc_pack<<<xgrid(n_own, 256, 4096), 256, 0, s>>>(n_own, X.bidx, act, chg_now, vadj, vm, lab, uw, su, sm, mcap,
+                                                       cnt, ccount, dense_div, step);
 }
-XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, const int32_t* xq, const int64_t* xoff,
-                  std::vector<void*>& T, std::vector<void*>& L) {
+XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, std::vector<void*>& T,
+                  std::vector<void*>& L) {
   auto alloc = [&](std::vector<void*>& list, size_t bytes) {
     void* p = nullptr;
     if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) throw std::runtime_error("build_xsend: hipMalloc");
@@ -592,39 +665,46 @@ XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, c
     throw std::runtime_error("build_xsend: count");
   X.nb = nb;
   int32_t* xb = (int32_t*)alloc(L, sizeof(int32_t) * nb);
-  int32_t* xe = (int32_t*)alloc(L, sizeof(int32_t) * nb * kMaxParts);
-  uint32_t* pm = (uint32_t*)alloc(L, sizeof(uint32_t) * nb);
-  if (hipMemsetAsync(pm, 0, sizeof(uint32_t) * nb, s) != hipSuccess) throw std::runtime_error("build_xsend");
-  k_xsend_list<<<xgrid(n_own, 256), 256, 0, s>>>(n_own, flag, pos, xb);
-  k_xsend_entries<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, xq, xoff, pos, xe, pm);
+  int32_t* bidx = (int32_t*)alloc(L, sizeof(int32_t) * n_own);
+  int32_t* eb = (int32_t*)alloc(L, sizeof(int32_t) * nx);
+  k_xsend_list<<<xgrid(n_own, 256), 256, 0, s>>>(n_own, flag, pos, xb, bidx);
+  k_xsend_entries<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, pos, eb);
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
     throw std::runtime_error("build_xsend: kernels");
   X.v = xb;
-  X.e = xe;
-  X.pm = pm;
+  X.bidx = bidx;
+  X.eb = eb;
   return X;
 }
-void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, const int32_t* stepflag, int64_t* xa) {
-  k_xcounts<<<1, 64, 0, s>>>(np, me, scnt, stepflag, xa);
+void launch_xtab_fill(hipStream_t s, int64_t n, const int32_t* xr_v, const int32_t* xr_q, const int32_t* tmp,
+                      const XTab& T, unsigned long long* err) {
+  if (n > 0) k_xtab_fill<<<xgrid(n, 256), 256, 0, s>>>(n, xr_v, xr_q, tmp, T, err);
 }
-void launch_xclear(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, uint64_t* chg, int32_t* uw) {
-  if (P.pre[P.np] > 0) k_xclear<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, xrv, chg, uw);
+void launch_xbc_counts(hipStream_t s, int np, int me, unsigned long long* cnt, const int32_t* stepflag, int64_t* xa) {
+  k_xbc_counts<<<1, 64, 0, s>>>(np, me, cnt, stepflag, xa);
 }
-void launch_xunpack_rec(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, int32_t* lab,
-                        uint64_t* chg, int32_t* uw, uint64_t* cb) {
-  if (P.pre[P.np] > 0) k_xunpack_rec<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, xrv, lab, chg, uw, cb);
+void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, int64_t* xa) {
+  k_xcounts<<<1, 64, 0, s>>>(np, me, scnt, xa);
 }
-void launch_xmark(hipStream_t s, const XPeers& P, const XRec* rbuf, const int32_t* xrv, const uint64_t* chg,
-                  const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next, int64_t tcut,
-                  const BatchParams* ebp, const int32_t* ccount, int dense_div, int step) {
-  if (P.pre[P.np] <= 0) return;
+void launch_xbc_clear(hipStream_t s, const XBcIn& I, uint64_t* chg, int32_t* uw) {
+  const int64_t n = I.U.pre[I.U.np] + I.M.pre[I.M.np];
+  if (n > 0) k_xbc_clear<<<xgrid(n, 256), 256, 0, s>>>(I, chg, uw);
+}
+void launch_xbc_unpack(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg, int32_t* uw, uint64_t* cb) {
+  const int64_t n = I.U.pre[I.U.np] + I.M.pre[I.M.np];
+  if (n > 0) k_xbc_unpack<<<xgrid(n, 256), 256, 0, s>>>(I, lab, chg, uw, cb);
+}
+void launch_xbc_mark(hipStream_t s, const XBcIn& I, const uint64_t* chg, const DevGraph& g, const uint64_t* vm,
+                     const uint64_t* em, uint8_t* act_next, int64_t tcut, const BatchParams* ebp, const int32_t* ccount,
+                     int dense_div, int step) {
+  const int64_t n = I.U.pre[I.U.np] + I.M.pre[I.M.np];
+  if (n <= 0) return;
   BatchParams bp0;
   if (!ebp) std::memset(&bp0, 0, sizeof(bp0));
-  auto* kern = g.ts_t ? k_xmark<true> : k_xmark<false>;
-  kern<<<xgrid(P.pre[P.np], 4), 256, 0, s>>>(P, rbuf, xrv, chg, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
-                                             g.n_seg > 0 ? g.hv_of : nullptr, act_next, g.adj_off, g.ts_e, g.ts_nb,
-                                             g.ts_t, tcut, ebp ? *ebp : bp0, ebp ? 1 : 0, ccount, dense_div, step,
-                                             g.n_own, g.nv);
+  auto* kern = g.ts_t ? k_xbc_mark<true> : k_xbc_mark<false>;
+  kern<<<xgrid(n, 256), 256, 0, s>>>(I, chg, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
+                                   g.n_seg > 0 ? g.hv_of : nullptr, act_next, g.adj_off, g.ts_e, g.ts_nb, g.ts_t, tcut,
+                                   ebp ? *ebp : bp0, ebp ? 1 : 0, ccount, dense_div, step);
 }
 void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,

@@ -98,11 +98,14 @@ class TemporalGraph:
 
     # ------------------------------------------------------------------ partitions
     @staticmethod
-    def exchange_id(loopback: bool = False) -> bytes:
-        """Id blob for rgpu_exchange_init: an RCCL unique id (one process per GPU; make it on
-        one rank and broadcast it) or a loopback group key (partitions in one process)."""
+    def exchange_id(loopback: bool = False, kind: str = None) -> bytes:
+        """Id blob for rgpu_exchange_init (make it on one rank and broadcast it): kind "rccl" (an
+        RCCL unique id: one process per GPU), "loopback" (partitions in one process) or "shm"
+        (one process per partition on one host, staged through shared memory)."""
+        kind = kind or ("loopback" if loopback else "rccl")
+        code = {"rccl": N.RGPU_XCHG_RCCL, "loopback": N.RGPU_XCHG_LOOPBACK, "shm": N.RGPU_XCHG_SHM}[kind]
         buf = C.create_string_buffer(N.RGPU_XCHG_ID_BYTES)
-        rc = N.rgpu().rgpu_exchange_id(N.RGPU_XCHG_LOOPBACK if loopback else N.RGPU_XCHG_RCCL, buf)
+        rc = N.rgpu().rgpu_exchange_id(code, buf)
         if rc != 0:
             raise RGPUError(rc, "rgpu_exchange_id failed")
         return buf.raw

@@ -22,14 +22,15 @@ import numpy as np
 from .graph import TemporalGraph
 
 
-def open_rccl_partition(device: int, dist=None, vertex_order: str = "locality") -> TemporalGraph:
-    """This rank's partition (partition = rank, P = world size), joined to the RCCL group.
+def open_rccl_partition(device: int, dist=None, vertex_order: str = "locality", kind: str = "rccl") -> TemporalGraph:
+    """This rank's partition (partition = rank, P = world size), joined to the RCCL group
+    (kind "shm": the shared-memory group of processes on one host instead).
     vertex_order "id": later seals merge into the resident partition (live ingest)."""
     if dist is None:
         import torch.distributed as dist
     rank, world = dist.get_rank(), dist.get_world_size()
     g = TemporalGraph(rank, world, device, vertex_order=vertex_order)
-    box = [TemporalGraph.exchange_id() if rank == 0 else None]
+    box = [TemporalGraph.exchange_id(kind=kind) if rank == 0 else None]
     dist.broadcast_object_list(box, src=0)
     g.exchange_init(box[0])  # collective: every rank joins the communicator here
     return g

@@ -58,3 +58,24 @@ def test_run_after_injected_failure(which, monkeypatch):
             res, _ = o.cc(t, BATCH_WINDOWS, mode=1)
             for w in range(len(BATCH_WINDOWS)):
                 assert cc_fields_from_summary(g.cc_summary(h * 5, w)) == cc_fields(label_counts(res[w][1]))
+
+
+def test_corrupt_label_record_is_reported(monkeypatch):
+    """Partitioned mode: a received label record that names no boundary vertex of its sender (a
+    bug upstream, injected with RGPU_INJECT_FAIL=rec) is counted on the device, skipped instead of
+    becoming an out-of-bounds store, and the run fails with RGPU_EHIP naming the count; the next
+    run on the same partitions gives the oracle's results (include/rgpu.h error contract)."""
+    from raphtory_amd.partitioned import LoopbackPartitions
+    from tests.test_gpu_partitioned import check_cc
+    s = gen_uniform(7, 800, 20_000, t0=T0_README, dt=1_576_800)
+    hops = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, 6 * DAY)
+    o = Oracle.from_stream(s)
+    lp = LoopbackPartitions(3)
+    lp.ingest_stream(s)
+    lp.seal()
+    monkeypatch.setenv("RGPU_INJECT_FAIL", "rec")
+    with pytest.raises(RGPUError, match="outside the receive plan"):
+        lp.run("cc", hops, BATCH_WINDOWS)
+    monkeypatch.delenv("RGPU_INJECT_FAIL")
+    check_cc(lp, o, hops, BATCH_WINDOWS)
+    lp.close()

@@ -1,0 +1,63 @@
+"""Same-process A/B timing on one sealed graph (measurement tool, not part of the product): the
+C4 stream (or a prefix) is generated and sealed once, then the CC query runs under each setting
+of one environment variable that the library reads per launch, in interleaved rounds.  Prints
+one JSON line per (round, setting): wall ms of the query and, with --profile, the serial
+per-kernel ms of a lean profile pass (RGPU_PROF_LEAN).
+
+usage: python tools/ab.py --var RGPU_AB --values 0,1 [--interactions N] [--rounds 2] [--profile]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from raphtory_amd import TemporalGraph  # noqa: E402
+from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--var", required=True)
+    ap.add_argument("--values", required=True)
+    ap.add_argument("--interactions", type=int, default=333_333_334)
+    ap.add_argument("--users", type=int, default=20_000_000)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--profile", action="store_true")
+    a = ap.parse_args()
+    g = TemporalGraph()
+    t0 = time.time()
+    for first in range(0, a.interactions, 20_000_000):
+        s = gen_gab_range(4, a.users, 333_333_334, first, min(20_000_000, a.interactions - first))
+        g.ingest_stream(s)
+        end = int(s.t[-1])
+        del s
+    g.seal()
+    print(f"sealed in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    hops = range_hops(end - 167 * HOUR, end, HOUR)
+    ref = None
+    for rnd in range(a.rounds):
+        for val in a.values.split(","):
+            os.environ[a.var] = val
+            g.run("cc", hops, BATCH_WINDOWS)  # warm
+            t = time.perf_counter()
+            g.run("cc", hops, BATCH_WINDOWS)
+            ms = (time.perf_counter() - t) * 1e3
+            summ = g.cc_summaries()[..., :8]
+            same = ref is None or bool((summ == ref).all())
+            ref = summ if ref is None else ref
+            out = {"round": rnd, a.var: val, "query_ms": round(ms, 2), "summaries_equal": same}
+            if a.profile:
+                os.environ["RGPU_PROF_LEAN"] = "1"
+                g.run("cc", hops, BATCH_WINDOWS, profile=True, serial=True)
+                os.environ.pop("RGPU_PROF_LEAN")
+                out["serial_ms"] = {k: round(v["ms"], 1) for k, v in g.stats()["kernels"].items() if v["launches"]}
+            print(json.dumps(out), flush=True)
+    g.close()
+
+
+if __name__ == "__main__":
+    main()
