@@ -49,8 +49,11 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-profile-pass", action="store_true")
     p.add_argument("--profile-only", action="store_true",
-                   help="only the serial HIP-event profile pass (the command rocprofv3 is run on, so "
+                   help="only the serial HIP-event profile passes (the command rocprofv3 is run on, so "
                         "that its per-kernel averages match the roofline figures)")
+    p.add_argument("--lean-pass-only", action="store_true",
+                   help="with --profile-only: the lean profile pass alone (no counting pass), so that a "
+                        "rocprofv3 kernel trace holds exactly the launches bench.py times")
     p.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5", "diffusion"],
                    help="c4 = the headline (north-star) query at every N; c2 = BASELINE configs[1]; "
                         "diffusion = BinaryDefusion over the C2 query (secondary)")
@@ -279,13 +282,16 @@ def kernel_table(stats):
             for k, v in stats["kernels"].items() if v["launches"]}
 
 
-def profile_passes(g, hops, windows):
+def profile_passes(g, hops, windows, lean_only=False):
     """Two serial profiled passes of the same query: a counting pass (the kernels' work counters ->
     DESIGN.md §4 bytes per kernel) and a lean pass (RGPU_PROF_LEAN=1: the same launches on the
     instantiations the timed runs use, under HIP events -> ms).  Returns {kernel: {launches, ms,
-    bytes}} with bytes from the first and launches / ms from the second."""
-    g.run("cc", hops, windows, profile=True, serial=True)
-    counted = g.stats()["kernels"]
+    bytes}} with bytes from the first and launches / ms from the second.  lean_only: the lean pass
+    alone (the command a rocprofv3 kernel trace runs, so that its per-kernel sums are this pass's)."""
+    counted = {}
+    if not lean_only:
+        g.run("cc", hops, windows, profile=True, serial=True)
+        counted = g.stats()["kernels"]
     os.environ["RGPU_PROF_LEAN"] = "1"
     try:
         g.run("cc", hops, windows, profile=True, serial=True)
@@ -403,7 +409,7 @@ def run_c4(a, rank, world, local):
     summ = None if a.profile_only else g.cc_summaries()  # (profile-only: after the profile pass)
     roofline, ks, s8d = None, {}, None
     if not a.no_profile_pass:
-        kraw = profile_passes(g, hops, windows)  # collective at N > 1
+        kraw = profile_passes(g, hops, windows, lean_only=a.lean_pass_only)  # collective at N > 1
         ks = kernel_table({"kernels": kraw})
         if summ is None:
             summ = g.cc_summaries()

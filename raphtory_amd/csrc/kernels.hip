@@ -293,6 +293,25 @@ __device__ __forceinline__ bool edge_simple(int64_t lo, int64_t hi, const int64_
   return !ds && !dd;
 }
 
+// simple edges (edge_simple) of a graph: the edge-mask kernel's SKIP byte model (rgpu.cpp bytes_emask)
+__global__ __launch_bounds__(256) void k_count_simple(int64_t ne, const int32_t* __restrict__ esrc,
+                                                      const int32_t* __restrict__ edst,
+                                                      const int64_t* __restrict__ eoff,
+                                                      const int64_t* __restrict__ ekey,
+                                                      const int64_t* __restrict__ doff,
+                                                      const uint64_t* __restrict__ dbits,
+                                                      unsigned long long* __restrict__ out) {
+  unsigned long long k = 0;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x)
+    k += edge_simple(eoff[e], eoff[e + 1], ekey, esrc[e], edst[e], doff, dbits);
+  for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o);
+  if ((threadIdx.x & 63) == 0 && k) atomicAdd(out, k);
+}
+void launch_count_simple(hipStream_t s, const DevGraph& g, unsigned long long* out) {
+  if (g.ne > 0)
+    k_count_simple<<<1024, 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dbits, out);
+}
+
 // The loop runs wave-uniform (lane = edge within a 64-edge group) so that profile runs can
 // count alive edges per view: the wave's 64 mask words are bit-transposed (lane j <- view j)
 // and popcounted; the block sums them in LDS, one atomicAdd per (plane, view) per block.

@@ -144,6 +144,8 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
 // ebp (time-ordered slots only; else null): the batch's hops and edge windows, non-planar bit layout
 // (view bit w*KS + k): K2 computes the window bits of simple slots inline (kernels.hip simple_bits)
 // and reads em only for the others (K1 then runs with skip_simple)
+// edges whose bits K2 computes itself (kernels.hip edge_simple), added into *out
+void launch_count_simple(hipStream_t s, const DevGraph& g, unsigned long long* out);
 void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,

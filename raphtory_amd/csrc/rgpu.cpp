@@ -225,6 +225,7 @@ struct rgpu_ctx {
   int algo = -1, K = 0, W = 0, G = 1, gsize = 1;
   size_t n_hops = 0;
   std::vector<rgpu_cc_summary_t> cc;
+  int64_t n_simple = -1;                // simple edges (kernels.hip edge_simple; the K1 edge byte model)
   std::vector<int32_t> vlast;           // per view: last superstep in which one of its labels changed
   unsigned long long* d_ecnt = nullptr; // profile runs: alive edges per view (K1 edge masks)
   std::vector<int64_t> deg;  // [view][3]
@@ -577,9 +578,17 @@ uint64_t diff_salt(uint64_t coin_seed, int64_t t, int64_t w) {
   return hmix64(coin_seed ^ hmix64((uint64_t)t ^ hmix64((uint64_t)w)));
 }
 
-// algorithmic bytes: see rgpu_stats_t.kernel_bytes
-double bytes_mask(const DevGraph& g) {
-  return 8.0 * (g.nv + 1) + 8.0 * g.nv + 8.0 * (g.ne + 1) + 16.0 * g.ne + 8.0 * g.ne;
+
+// K1 edge masks: per edge its offsets (8), its endpoints (8) and their death bits; an edge the
+// SKIP instantiation leaves to K2 (simple: one add point, no endpoint deaths) costs its one
+// history point (8) more and nothing else; every other edge its history points, two death-list
+// offsets per endpoint (16) and one mask word per plane.
+double bytes_emask(const rgpu_ctx* c, int planes, bool skip_simple) {
+  const DevGraph& g = c->g;
+  const double ne = (double)g.ne, simple = skip_simple ? (double)std::max<int64_t>(c->n_simple, 0) : 0.0;
+  const double keys = (double)c->pk.n_ekey;
+  return 8.0 * (ne + 1) + 8.0 * ne + (skip_simple ? 8.0 * simple : 0.0) + 8.0 * (keys - simple) +
+         (16.0 + 8.0 * planes) * (ne - simple);
 }
 
 void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
@@ -807,8 +816,10 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   }
   if (s.work && c->profile)
     HIPCHK(hipMemsetAsync(s.work, 0, sizeof(unsigned long long) * kWorkWords, s.stream));
-  const double bm = bytes_mask(g);
-  const double bv = 8.0 * (g.nv + 1) + 8.0 * c->pk.n_vkey, be = bm - (16.0 * g.nv + 8.0) - 8.0 * g.ne + 8.0 * c->pk.n_ekey;
+  // K1 byte models.  Vertex masks: offsets, two floor probes per vertex (the
+  // interval form's binary searches; the points between them are not counted: a lower bound) and
+  // the plane stores.  Edge masks: see bytes_emask.
+  const double bv = 8.0 * (g.nv + 1) + 16.0 * g.nv;
   // partitioned: K1 computes the owned vertices' masks (a ghost's history is its owner's);
   // the ghosts' words arrive from their owners right after
   DevGraph gk = g;
@@ -833,7 +844,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     s.vm = s.vm_own;
     s.em = s.em_own;
     timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv, [&] { launch_vertex_mask(s.stream, gk, bp, s.vm, 0, false, clr); });
-    timed_launch(c, si, KID_EMASK, be + 8.0 * g.ne, [&] {
+    timed_launch(c, si, KID_EMASK, bytes_emask(c, 1, skip_simple), [&] {
       launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0, ends ? s.vm : nullptr, 0, skip_simple);
     });
     if (c->partitioned) part_vm_exchange(c, si, s.vm, 0, 1);
@@ -845,7 +856,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       const BatchClear none;
       timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv * rc.W,
                    [&] { launch_vertex_mask(s.stream, gk, bp, M.vm, g.nv + kPad, true, none); });
-      timed_launch(c, si, KID_EMASK, be + 8.0 * g.ne * rc.W, [&] {
+      timed_launch(c, si, KID_EMASK, bytes_emask(c, rc.W, skip_simple), [&] {
         launch_edge_mask(s.stream, g, bp, M.em, true, c->d_ecnt, (int64_t)h0, ends ? M.vm : nullptr, g.nv + kPad,
                          skip_simple);
       });
@@ -1693,9 +1704,9 @@ int run_partitioned_dp(rgpu_ctx* c, RunCfg& rc) {
     clr.n_flags = kMaxSteps;
     s.vm = s.vm_own;
     s.em = s.em_own;
-    timed_launch(c, 0, KID_MASK, 8.0 * (go.nv + 1) + 8.0 * c->pk.n_vkey + 8.0 * go.nv,
+    timed_launch(c, 0, KID_MASK, 8.0 * (go.nv + 1) + 16.0 * go.nv + 8.0 * go.nv,
                  [&] { launch_vertex_mask(s.stream, go, bp, s.vm, 0, false, clr); });
-    timed_launch(c, 0, KID_EMASK, bytes_mask(g) - (16.0 * g.nv + 8.0) + 8.0 * c->pk.n_ekey,
+    timed_launch(c, 0, KID_EMASK, bytes_emask(c, 1, false),
                  [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0); });
     part_vm_exchange(c, 0, s.vm, 0, 1);
     timed_launch(c, 0, KID_DEGREE, go.nv * (8.0 + 32.0 + 512.0) + (double)(g.ne + g.n_in) * 12.0, [&] {
@@ -2035,6 +2046,19 @@ const uint64_t* upload_death_bits(std::vector<void*>& L, const std::vector<int64
 
 void finish_seal(rgpu_ctx* c) {
   Packed& P = c->pk;
+  {  // simple edges (the K1 edge byte model)
+    unsigned long long* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(unsigned long long)));
+    HIPCHK(hipMemset(d, 0, sizeof(unsigned long long)));
+    unsigned long long h = 0;
+    launch_count_simple(nullptr, c->g, d);
+    const hipError_t e1 = hipGetLastError();
+    const hipError_t e2 = hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    HIPCHK(e1);
+    HIPCHK(e2);
+    c->n_simple = (int64_t)h;
+  }
   c->st.vertices = P.n_own;
   c->st.edges = P.ne;
   c->st.edges_owned = P.ne_owned;
