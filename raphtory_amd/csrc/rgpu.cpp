@@ -183,14 +183,20 @@ struct Timed {
 }  // namespace
 
 struct rgpu_ctx {
-  std::mutex mu;
+  // Locks.  mu: the resident graph and every run / result call (10 ReaderWorkers share a ctx).
+  // ingest_mu: the update log (rgpu_ingest, the watermark), so that ingestion goes on while a run
+  // holds mu (IngestionWorker keeps applying updates while LiveAnalysisTask runs,
+  // IngestionWorker.scala:31-61).  seal_mu: one seal at a time; a live merge builds the merged
+  // graph holding only seal_mu (runs on the resident graph go on) and takes mu to swap it in.
+  std::mutex mu, ingest_mu, seal_mu;
   int part = 0, nparts = 1, device = 0;
   bool partitioned = false;  // nparts > 1, or RGPU_PARTITIONED=1 (the partitioned path with P = 1)
   std::string err;
-  std::vector<Event> events;
+  std::vector<Event> events;            // the update log from absolute index ev_base on
+  size_t ev_base = 0;                   // updates dropped from the front of the log (sealed, live contexts)
   int64_t newest = -1;
-  bool sealed = false;
-  size_t n_sealed = 0;                  // events[0, n_sealed) are in the resident graph
+  bool sealed = false;                  // a graph is resident (a seal has succeeded)
+  size_t n_sealed = 0;                  // updates [0, n_sealed) (absolute) are in the resident graph
   bool delta_on = true;                 // RGPU_DELTA: merge later updates into it (else re-pack)
   bool delta_host = false;              // RGPU_DELTA=2: the host delta packer (A/B; default the device one)
   int64_t* g_vid = nullptr;             // device delta packer: the resident graph's ids (graph list)
@@ -1873,7 +1879,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
 int rgpu_ingest(rgpu_ctx* c, const int64_t* t, const uint8_t* kind, const int64_t* src,
                 const int64_t* dst, size_t n) {
   if (!c) return RGPU_EINVAL;
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::lock_guard<std::mutex> lk(c->ingest_mu);  // (not mu: ingestion goes on during runs and merges)
   if (n && (!t || !kind || !src)) return fail(c, RGPU_EINVAL, "null input array");
   try {
     const size_t need = c->events.size() + n;  // geometric growth: live ingest appends often
@@ -1890,7 +1896,6 @@ int rgpu_ingest(rgpu_ctx* c, const int64_t* t, const uint8_t* kind, const int64_
   } catch (const std::bad_alloc&) {
     return fail(c, RGPU_ENOMEM, "host allocation failed");
   }
-  c->sealed = false;
   return RGPU_OK;
 }
 
@@ -2044,7 +2049,7 @@ const uint64_t* upload_death_bits(std::vector<void*>& L, const std::vector<int64
   return dupload(L, bits);
 }
 
-void finish_seal(rgpu_ctx* c) {
+void finish_seal(rgpu_ctx* c, size_t n_end) {
   Packed& P = c->pk;
   {  // simple edges (the K1 edge byte model)
     unsigned long long* d = nullptr;
@@ -2065,7 +2070,7 @@ void finish_seal(rgpu_ctx* c) {
   c->st.vertex_events = P.n_vkey;
   c->st.edge_events = P.n_ekey;
   c->st.deaths = c->n_dtime >= 0 ? c->n_dtime : (int64_t)P.dtime.size();
-  c->n_sealed = c->events.size();
+  c->n_sealed = n_end;
   c->sealed = true;
   if (!c->partitioned) {  // the big arrays live in HBM only (the delta merge keeps them there)
     for (auto* v : {&P.voff, &P.vkey, &P.eoff, &P.ekey}) std::vector<int64_t>().swap(*v);
@@ -2073,11 +2078,28 @@ void finish_seal(rgpu_ctx* c) {
   }
 }
 
+// A live context (device merges, id order) never re-packs the whole log: once sealed, its updates
+// are dropped from the host log (a C4-size base would otherwise keep 32 GB of records and copy them
+// whenever the log grows).  Others keep the log for their re-packs.  holding: ingest_mu is held.
+void drop_sealed_log(rgpu_ctx* c, bool holding) {
+  if (!c->delta_on || c->delta_host || c->pk.relabeled || c->g.nv == 0) return;
+  std::unique_lock<std::mutex> il(c->ingest_mu, std::defer_lock);
+  if (!holding) il.lock();
+  const size_t k = c->n_sealed - c->ev_base;
+  if (k == 0) return;
+  c->events.erase(c->events.begin(), c->events.begin() + k);
+  if (c->events.capacity() > 4 * std::max<size_t>(c->events.size(), 1 << 20)) c->events.shrink_to_fit();
+  c->ev_base = c->n_sealed;
+}
+
 // Incremental seal: merge the updates ingested since the last seal into the resident graph
 // (merge.hip).  The delta arrays come from the device packer (gdelta.hip: the tick's updates
 // are uploaded once and never come back) or, RGPU_DELTA=2, from the host packer (packer.cpp
 // pack_delta / finish_delta: delta-sized sorts + O(V) offsets on the host).
-void seal_delta(rgpu_ctx* c) {
+// n_end: the updates [n_sealed, n_end) (absolute) are merged.  swap: locked (c->mu) right before the
+// merged graph replaces the resident one — everything before it runs while runs on the resident
+// graph go on (live ingest); the caller keeps it locked for finish_seal.
+void seal_delta(rgpu_ctx* c, size_t n_end, std::unique_lock<std::mutex>& swap) {
   Packed& B = c->pk;
   const bool dev = !c->delta_host;
   auto tp = std::chrono::steady_clock::now();
@@ -2113,16 +2135,20 @@ void seal_delta(rgpu_ctx* c) {
     m.nvk_old = B.n_vkey;
     int64_t nv2 = 0, n_in2 = 0;
     if (dev) {
-      if (!c->g_vid) {  // the first merge into a full seal: its rank-order keys, once (DeltaPart)
+      int64_t* gvid = c->g_vid;
+      if (!gvid) {  // the first merge into a full seal: its rank-order keys (DeltaPart)
         std::vector<int64_t> keys(B.vid);
         if (c->partitioned)
           for (int64_t v = B.n_own; v < B.nv; v++) keys[v] |= (int64_t)1 << 31;
-        c->g_vid = dalloc<int64_t>(c->graph_allocs, g0.nv);
-        HIPCHK(hipMemcpy(c->g_vid, keys.data(), sizeof(int64_t) * g0.nv, hipMemcpyHostToDevice));
+        gvid = dalloc<int64_t>(T, g0.nv);
+        HIPCHK(hipMemcpy(gvid, keys.data(), sizeof(int64_t) * g0.nv, hipMemcpyHostToDevice));
       }
-      const int64_t n = (int64_t)(c->events.size() - c->n_sealed);
+      const int64_t n = (int64_t)(n_end - c->n_sealed);
       DevEvent* ev = dalloc<DevEvent>(T, n);
-      HIPCHK(hipMemcpyAsync(ev, c->events.data() + c->n_sealed, sizeof(Event) * n, hipMemcpyHostToDevice, s));
+      {  // (the log may grow meanwhile: ingestion waits only for this copy)
+        std::lock_guard<std::mutex> il(c->ingest_mu);
+        HIPCHK(hipMemcpy(ev, c->events.data() + (c->n_sealed - c->ev_base), sizeof(Event) * n, hipMemcpyHostToDevice));
+      }
       phase("upload");
       DeltaPart dp;
       if (c->partitioned) {
@@ -2137,7 +2163,7 @@ void seal_delta(rgpu_ctx* c) {
       }
       std::string e;
       try {
-        e = gpu_pack_delta(s, ev, n, g0, c->g_vid, dp, c->heavy_t, &DD, T, L);
+        e = gpu_pack_delta(s, ev, n, g0, gvid, dp, c->heavy_t, &DD, T, L);
       } catch (const std::runtime_error& x) {
         throw HipFail{x.what()};
       }
@@ -2167,7 +2193,7 @@ void seal_delta(rgpu_ctx* c) {
       m.ni_key = DD.ni_key;
       m.ni_idx = DD.ni_idx;
     } else {
-      std::string e = pack_delta(c->events, c->n_sealed, B, &D);
+      std::string e = pack_delta(c->events, c->n_sealed, B, &D);  // (host packer: ev_base = 0, ingest_mu held)
       phase("pack");
       if (!e.empty()) throw HipFail{e, RGPU_EINVAL};
       const int64_t nde = (int64_t)D.de_s.size();
@@ -2307,9 +2333,10 @@ void seal_delta(rgpu_ctx* c) {
     T.clear();
     (void)hipStreamDestroy(s);
     s = nullptr;
-    // swap in the merged graph; batch slots and mask sets stay if they fit (else they are
-    // reallocated on the next run with 2x headroom for the ticks to come)
+    // swap in the merged graph (runs stop here); batch slots and mask sets stay if they fit (else
+    // they are reallocated on the next run with 2x headroom for the ticks to come)
     phase("free temps");
+    swap.lock();
     for (void* p : c->graph_allocs) (void)hipFree(p);
     c->graph_allocs.swap(L);
     L.clear();
@@ -2397,34 +2424,54 @@ void seal_delta(rgpu_ctx* c) {
 
 int rgpu_seal(rgpu_ctx* c) {
   if (!c) return RGPU_EINVAL;
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::lock_guard<std::mutex> sl(c->seal_mu);
   const auto t0 = std::chrono::steady_clock::now();
+  size_t n_end;
+  {
+    std::lock_guard<std::mutex> il(c->ingest_mu);
+    n_end = c->ev_base + c->events.size();
+  }
+  std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+  std::unique_lock<std::mutex> il(c->ingest_mu, std::defer_lock);
   try {
     HIPCHK(hipSetDevice(c->device));
-    // partitioned: the broadcast records' receive tables name the peers' boundary lists, which any
-    // partition's seal may change — every partition rebuilds them (collectively) at its next run
-    c->pt.tab_ready = false;
-    if (c->n_sealed > 0 && c->n_sealed == c->events.size()) {  // nothing new since the last seal
+    if (c->n_sealed > 0 && c->n_sealed == n_end) {  // nothing new since the last seal
+      lk.lock();
+      // partitioned: the broadcast records' receive tables name the peers' boundary lists, which any
+      // partition's seal may change — every partition rebuilds them (collectively) at its next run
+      c->pt.tab_ready = false;
       c->sealed = true;
       return RGPU_OK;
     }
-    c->sealed = false;
-    c->st.seal_incremental = 0;
-    c->st.seal_delta_updates = 0;
-    // (a locality-ordered base has no monotone rank maps to merge into: it is re-packed)
-    // (a locality-ordered base is re-packed; the partitioned merge needs the device packer)
+    // (a locality-ordered base has no monotone rank maps to merge into: it is re-packed; the
+    // partitioned merge needs the device packer)
     if (c->delta_on && c->n_sealed > 0 && c->g.nv > 0 && !c->pk.relabeled && !(c->partitioned && c->delta_host)) {
-      // live ingest: merge the delta into the resident graph
-      seal_delta(c);
+      // live ingest: merge the delta into the resident graph.  The device packer builds it while runs
+      // and ingestion go on; the host packer (RGPU_DELTA=2) reads the log, so ingestion waits.
+      if (c->delta_host) {
+        il.lock();
+        n_end = c->ev_base + c->events.size();  // (what the host packer will read)
+      }
+      seal_delta(c, n_end, lk);  // returns with mu locked
+      c->pt.tab_ready = false;
       c->st.seal_incremental = 1;
-      finish_seal(c);
+      finish_seal(c, n_end);
       if (c->check)
         run_check(nullptr, "merged graph", [&](unsigned long long* bad) {
           launch_check_graph(nullptr, c->g, c->pk.n_ekey, c->pk.n_vkey, bad);
         });
+      drop_sealed_log(c, il.owns_lock());
       c->st.seal_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       return RGPU_OK;
     }
+    lk.lock();
+    il.lock();
+    n_end = c->ev_base + c->events.size();  // (the whole log is packed)
+    c->pt.tab_ready = false;
+    c->sealed = false;
+    c->st.seal_incremental = 0;
+    c->st.seal_delta_updates = 0;
+    if (c->ev_base) return fail(c, RGPU_ESTATE, "the update log before the resident graph was dropped: cannot re-pack");
     std::string e = pack_events(c->events, c->part, c->nparts, &c->pk, c->vertex_order == RGPU_ORDER_LOCALITY);
     if (!e.empty()) return fail(c, RGPU_EINVAL, e);
     free_graph(c);
@@ -2506,11 +2553,12 @@ int rgpu_seal(rgpu_ctx* c) {
     c->g = g;
     HIPCHK(hipDeviceSynchronize());
     const int64_t nek = P.n_ekey, nvk = P.n_vkey;
-    finish_seal(c);
+    finish_seal(c, n_end);
     if (c->check)
       run_check(nullptr, "sealed graph", [&](unsigned long long* bad) {
         launch_check_graph(nullptr, c->g, nek, nvk, bad);
       });
+    drop_sealed_log(c, true);
   } catch (const HipFail& f) {
     return fail(c, f.code ? f.code : RGPU_EHIP, f.msg);
   } catch (const std::bad_alloc&) {
@@ -2530,7 +2578,7 @@ int rgpu_set_vertex_order(rgpu_ctx* c, int order) {
 
 int rgpu_newest_time(rgpu_ctx* c, int64_t* out) {
   if (!c || !out) return RGPU_EINVAL;
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::lock_guard<std::mutex> lk(c->ingest_mu);
   *out = c->newest;
   return RGPU_OK;
 }

@@ -273,3 +273,69 @@ def test_live_partitioned_loopback_ticks(P):
                 assert a[key] == b[key], (k, key, a[key], b[key])
         one.close()
     lp.close()
+
+
+def test_live_ingest_and_merge_concurrent_with_runs():
+    """Live analysis under concurrent ingest (IngestionWorker keeps applying updates while
+    LiveAnalysisTask runs, IngestionWorker.scala:31-61, LiveAnalysisTask.scala:55-105): while the
+    main thread runs CC on the resident graph at tick i's live time, a second thread ingests tick
+    i+1 and seals it (the merged graph is built beside the resident one and swapped in between
+    runs).  Every run equals the oracle over the stream through tick i at that time (later points
+    are invisible to a view at the live time), and after the last tick the merged graph equals a
+    one-shot seal.  The sealed prefix of the log is dropped on the host as the ticks go (the
+    whole-stream check below re-ingests from the arrays)."""
+    import threading
+    users = 4000
+    base = gen_gab(4, users, 20_000)
+    now = int(base.t[-1])
+    ticks = []
+    for i in range(5):
+        ticks.append(gen_gab(100 + i, users, 4000, t0=now + 1, t1=now + HOUR, id_key=4))
+        now = int(ticks[-1].t[-1])
+    g = TemporalGraph(vertex_order="id")
+    g.ingest_stream(base)
+    g.seal()
+    err = []
+
+    def ingest_merge(s):
+        try:
+            g.ingest_stream(s)
+            g.seal()
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+
+    prefix = [base]
+    ingest_merge(ticks[0])
+    prefix.append(ticks[0])
+    wins = [MONTH, DAY, HOUR]
+    for i in range(len(ticks)):
+        assert not err, err
+        live = int(prefix[-1].t[-1])
+        th = threading.Thread(target=ingest_merge, args=(ticks[i + 1],)) if i + 1 < len(ticks) else None
+        if th:
+            th.start()
+        g.run("cc", [live, live - HOUR // 2], wins, retain=True)
+        if th:
+            th.join()
+        cat = [np.concatenate([getattr(s, f) for s in prefix]) for f in ("t", "kind", "src", "dst")]
+        o = Oracle(*cat)
+        for h, t in enumerate([live, live - HOUR // 2]):
+            res, steps = o.cc(t, wins, mode=1)
+            for w in range(len(wins)):
+                ids, lab = res[w]
+                gids, glab = g.cc_vertex_labels(h, w)
+                assert np.array_equal(gids, ids) and np.array_equal(glab, lab), (i, t, w)
+                assert g.cc_summary(h, w).supersteps == steps
+        o.close()
+        if i + 1 < len(ticks):
+            prefix.append(ticks[i + 1])
+    assert not err, err
+    one = TemporalGraph()
+    for s in prefix:
+        one.ingest_stream(s)
+    one.seal()
+    a, b = g.stats(), one.stats()
+    for k in ("vertices", "edges", "vertex_events", "edge_events"):
+        assert a[k] == b[k], k
+    g.close()
+    one.close()
