@@ -180,6 +180,18 @@ struct Timed {
   double bytes;
 };
 
+// A merged graph built beside the resident one (seal_delta), waiting to replace it (apply_merged).
+struct Merged {
+  bool valid = false, dev = true;
+  DevGraph g;
+  std::vector<void*> L;                   // its device allocations
+  int64_t* vid2 = nullptr;                // device packer: its ids
+  int64_t ndt = -1, nd = 0, ne_owned = 0, nvk = 0, nek = 0, nv2 = 0;
+  PartMeta PM;
+  std::vector<int64_t> orph_id, orph_t;   // partitioned: deaths of ids not kept
+  std::vector<int64_t> hvid, hdoff, hdtime, hout_off, hin_off;  // host packer: host arrays
+};
+
 }  // namespace
 
 struct rgpu_ctx {
@@ -206,6 +218,7 @@ struct rgpu_ctx {
   int vertex_order = RGPU_ORDER_LOCALITY;  // rgpu_set_vertex_order: local rank order of a full seal
   Packed pk;
   DevGraph g;
+  Merged pending;                       // a merged graph that replaces g before the next run / seal
   std::vector<void*> graph_allocs;
   // batch-slot and mask-set buffers, sized for cap_* >= the graph (a live-ingest merge that
   // still fits keeps them: reallocating tens of GB per merge would dominate the tick)
@@ -289,6 +302,8 @@ T* dupload(std::vector<void*>& list, const std::vector<T>& h) {
 void release_slots(rgpu_ctx* c);
 void free_part_slots(rgpu_ctx* c, bool keep_channels);
 void free_graph(rgpu_ctx* c) {
+  for (void* p : c->pending.L) (void)hipFree(p);  // (a parked merged graph)
+  c->pending = Merged();
   for (void* p : c->graph_allocs) (void)hipFree(p);
   c->graph_allocs.clear();
   c->g_vid = nullptr;
@@ -2078,6 +2093,106 @@ void finish_seal(rgpu_ctx* c, size_t n_end) {
   }
 }
 
+// Replace the resident graph by a merged one (under mu, between runs).  The last run's results
+// named the old graph's ranks: they go.  Batch slots and mask sets stay if they fit (else they are
+// reallocated on the next run with 2x headroom for the ticks to come).
+void apply_merged(rgpu_ctx* c, Merged& M) {
+  Packed& B = c->pk;
+  const DevGraph g = M.g;
+  const bool dev = M.dev;
+  const int64_t nv2 = M.nv2, ne_owned = M.ne_owned, nvk = M.nvk, nek = M.nek;
+  PartMeta& PM = M.PM;
+  for (void* p : c->graph_allocs) (void)hipFree(p);
+  c->graph_allocs.swap(M.L);
+  c->g = g;
+  c->g_vid = M.vid2;
+  if (c->partitioned) {  // the old plan's buffers went with the old graph; channels stay
+    free_part_slots(c, true);
+    Exchange* x = c->pt.xchg;
+    XSlot xs[4];
+    for (int i = 0; i < 4; i++) xs[i].x = c->pt.xs[i].x;
+    c->pt = Part();
+    c->pt.xchg = x;
+    for (int i = 0; i < 4; i++) c->pt.xs[i].x = xs[i].x;
+    Part& X = c->pt;
+    X.nxs = PM.nxs;
+    X.nxr = PM.nxr;
+    X.xs_off = PM.xs_off;
+    X.xr_off = PM.xr_off;
+    X.xs_v = PM.xs_v;
+    X.xs_q = PM.xs_q;
+    X.xr_v = PM.xr_v;
+    X.xr_q = PM.xr_q;
+    X.xs_off_d = PM.xs_off_d;
+    X.xr_off_d = PM.xr_off_d;
+    X.xsend = build_send_plan(g.n_own, X, c->graph_allocs);
+    X.own.vid = PM.own_vid;
+    X.own.pos = nullptr;
+    X.own.boff = PM.own_boff;
+    X.own.shift = PM.shift;
+    X.own.n_own = g.n_own;
+    c->orph_id.swap(M.orph_id);
+    c->orph_t.swap(M.orph_t);
+  }
+  for (Slot& sl : c->slot) {
+    sl.hv = HeavyBuf();
+    sl.h_cc = sl.h_pr = false;
+  }
+  if (g.nv > c->cap_nv || g.ne > c->cap_ne || g.n_in > c->cap_nin) {
+    release_slots(c);
+    c->cap_nv = 2 * g.nv;  // doubling: a growing live graph re-allocates O(log) times
+    c->cap_ne = 2 * g.ne;
+    c->cap_nin = 2 * g.n_in;
+  } else {
+    for (int i = 0; i < c->nslots; i++) {  // per-rank state that K2 does not rewrite
+      Slot& sl = c->slot[i];
+      if (sl.chg[0]) {
+        HIPCHK(hipMemset(sl.chg[0], 0, sizeof(uint64_t) * (c->cap_nv + kPad)));
+        HIPCHK(hipMemset(sl.chg[1], 0, sizeof(uint64_t) * (c->cap_nv + kPad)));
+        HIPCHK(hipMemset(sl.snbr, 0, sizeof(int32_t) * (c->cap_ne + c->cap_nin + kPad)));
+      }
+    }
+  }
+  B.nv = nv2;
+  B.n_own = g.n_own;
+  B.ne = g.ne;
+  B.ne_owned = ne_owned;
+  if (dev) {  // the host keeps no offsets; its ids follow on demand (host_vid)
+    c->vid_stale = true;
+    c->n_dtime = M.ndt;
+    for (auto* v : {&B.doff, &B.dtime, &B.out_off, &B.in_off}) std::vector<int64_t>().swap(*v);
+  } else {
+    B.vid.swap(M.hvid);
+    B.doff.swap(M.hdoff);
+    B.dtime.swap(M.hdtime);
+    B.out_off.swap(M.hout_off);
+    B.in_off.swap(M.hin_off);
+    c->n_dtime = -1;
+  }
+  B.n_vkey = nvk;
+  B.n_ekey = nek;
+  B.n_in = g.n_in;
+  {
+    std::lock_guard<std::mutex> il(c->ingest_mu);
+    B.newest = c->newest;
+  }
+  c->st.seal_delta_updates = M.nd;
+  c->algo = -1;  // (results of the last run named the old graph)
+  c->cc.clear();
+  c->vlast.clear();
+  c->kept.clear();
+  c->retained = false;
+  c->pt.tab_ready = false;
+  M = Merged();
+}
+
+// the parked merged graph (if any) replaces the resident one (under mu)
+void apply_pending(rgpu_ctx* c) {
+  if (!c->pending.valid) return;
+  apply_merged(c, c->pending);
+  finish_seal(c, c->n_sealed);
+}
+
 // A live context (device merges, id order) never re-packs the whole log: once sealed, its updates
 // are dropped from the host log (a C4-size base would otherwise keep 32 GB of records and copy them
 // whenever the log grows).  Others keep the log for their re-packs.  holding: ingest_mu is held.
@@ -2096,10 +2211,10 @@ void drop_sealed_log(rgpu_ctx* c, bool holding) {
 // (merge.hip).  The delta arrays come from the device packer (gdelta.hip: the tick's updates
 // are uploaded once and never come back) or, RGPU_DELTA=2, from the host packer (packer.cpp
 // pack_delta / finish_delta: delta-sized sorts + O(V) offsets on the host).
-// n_end: the updates [n_sealed, n_end) (absolute) are merged.  swap: locked (c->mu) right before the
-// merged graph replaces the resident one — everything before it runs while runs on the resident
-// graph go on (live ingest); the caller keeps it locked for finish_seal.
-void seal_delta(rgpu_ctx* c, size_t n_end, std::unique_lock<std::mutex>& swap) {
+
+// Builds the merged graph of the resident one and the updates [n_sealed, n_end) (absolute) into M,
+// beside the resident graph: runs on it go on meanwhile (live ingest).  apply_merged swaps it in.
+void seal_delta(rgpu_ctx* c, size_t n_end, Merged& M) {
   Packed& B = c->pk;
   const bool dev = !c->delta_host;
   auto tp = std::chrono::steady_clock::now();
@@ -2333,84 +2448,30 @@ void seal_delta(rgpu_ctx* c, size_t n_end, std::unique_lock<std::mutex>& swap) {
     T.clear();
     (void)hipStreamDestroy(s);
     s = nullptr;
-    // swap in the merged graph (runs stop here); batch slots and mask sets stay if they fit (else
-    // they are reallocated on the next run with 2x headroom for the ticks to come)
-    phase("free temps");
-    swap.lock();
-    for (void* p : c->graph_allocs) (void)hipFree(p);
-    c->graph_allocs.swap(L);
-    L.clear();
-    c->g = g;
-    c->g_vid = dev ? DD.vid2 : nullptr;
-    if (c->partitioned) {  // the old plan's buffers went with the old graph; channels stay
-      free_part_slots(c, true);
-      Exchange* x = c->pt.xchg;
-      XSlot xs[4];
-      for (int i = 0; i < 4; i++) xs[i].x = c->pt.xs[i].x;
-      c->pt = Part();
-      c->pt.xchg = x;
-      for (int i = 0; i < 4; i++) c->pt.xs[i].x = xs[i].x;
-      Part& X = c->pt;
-      X.nxs = PM.nxs;
-      X.nxr = PM.nxr;
-      X.xs_off = PM.xs_off;
-      X.xr_off = PM.xr_off;
-      X.xs_v = PM.xs_v;
-      X.xs_q = PM.xs_q;
-      X.xr_v = PM.xr_v;
-      X.xr_q = PM.xr_q;
-      X.xs_off_d = PM.xs_off_d;
-      X.xr_off_d = PM.xr_off_d;
-      X.xsend = build_send_plan(g.n_own, X, L);
-      X.own.vid = PM.own_vid;
-      X.own.pos = nullptr;
-      X.own.boff = PM.own_boff;
-      X.own.shift = PM.shift;
-      X.own.n_own = g.n_own;
-      c->orph_id.swap(DD.orph_id);
-      c->orph_t.swap(DD.orph_t);
-    }
-    for (Slot& sl : c->slot) {
-      sl.hv = HeavyBuf();
-      sl.h_cc = sl.h_pr = false;
-    }
-    if (g.nv > c->cap_nv || g.ne > c->cap_ne || g.n_in > c->cap_nin) {
-      release_slots(c);
-      c->cap_nv = 2 * g.nv;  // doubling: a growing live graph re-allocates O(log) times
-      c->cap_ne = 2 * g.ne;
-      c->cap_nin = 2 * g.n_in;
+    // the merged graph, ready to replace the resident one (apply_merged)
+    M.g = g;
+    M.L.swap(L);
+    M.dev = dev;
+    M.vid2 = dev ? DD.vid2 : nullptr;
+    M.ndt = dev ? DD.ndt : -1;
+    M.nd = dev ? DD.nd : D.nd;
+    M.PM = std::move(PM);
+    M.ne_owned = ne_owned;
+    M.nvk = nvk;
+    M.nek = nek;
+    M.nv2 = nv2;
+    if (dev) {
+      M.orph_id.swap(DD.orph_id);
+      M.orph_t.swap(DD.orph_t);
     } else {
-      for (int i = 0; i < c->nslots; i++) {  // per-rank state that K2 does not rewrite
-        Slot& sl = c->slot[i];
-        if (sl.chg[0]) {
-          HIPCHK(hipMemset(sl.chg[0], 0, sizeof(uint64_t) * (c->cap_nv + kPad)));
-          HIPCHK(hipMemset(sl.chg[1], 0, sizeof(uint64_t) * (c->cap_nv + kPad)));
-          HIPCHK(hipMemset(sl.snbr, 0, sizeof(int32_t) * (c->cap_ne + c->cap_nin + kPad)));
-        }
-      }
+      M.hvid.swap(D.vid);
+      M.hdoff.swap(D.doff);
+      M.hdtime.swap(D.dtime);
+      M.hout_off.swap(D.out_off);
+      M.hin_off.swap(D.in_off);
     }
-    B.nv = nv2;
-    B.n_own = g.n_own;
-    B.ne = g.ne;
-    B.ne_owned = ne_owned;
-    if (dev) {  // the host keeps no offsets; its ids follow on demand (host_vid)
-      c->vid_stale = true;
-      c->n_dtime = DD.ndt;
-      for (auto* v : {&B.doff, &B.dtime, &B.out_off, &B.in_off}) std::vector<int64_t>().swap(*v);
-    } else {
-      B.vid.swap(D.vid);
-      B.doff.swap(D.doff);
-      B.dtime.swap(D.dtime);
-      B.out_off.swap(D.out_off);
-      B.in_off.swap(D.in_off);
-      c->n_dtime = -1;
-    }
-    B.n_vkey = nvk;
-    B.n_ekey = nek;
-    B.n_in = g.n_in;
-    B.newest = c->newest;
-    c->st.seal_delta_updates = dev ? DD.nd : D.nd;
-    phase("swap");
+    M.valid = true;
+    phase("built");
   } catch (...) {
     if (s) (void)hipStreamSynchronize(s);
     for (void* p : T) (void)hipFree(p);
@@ -2448,18 +2509,39 @@ int rgpu_seal(rgpu_ctx* c) {
     if (c->delta_on && c->n_sealed > 0 && c->g.nv > 0 && !c->pk.relabeled && !(c->partitioned && c->delta_host)) {
       // live ingest: merge the delta into the resident graph.  The device packer builds it while runs
       // and ingestion go on; the host packer (RGPU_DELTA=2) reads the log, so ingestion waits.
+      if (c->pending.valid) {  // a graph parked by the previous seal goes in first: this one builds on it
+        lk.lock();
+        apply_pending(c);
+        lk.unlock();
+      }
       if (c->delta_host) {
         il.lock();
         n_end = c->ev_base + c->events.size();  // (what the host packer will read)
       }
-      seal_delta(c, n_end, lk);  // returns with mu locked
-      c->pt.tab_ready = false;
-      c->st.seal_incremental = 1;
-      finish_seal(c, n_end);
+      Merged M;
+      seal_delta(c, n_end, M);
       if (c->check)
         run_check(nullptr, "merged graph", [&](unsigned long long* bad) {
-          launch_check_graph(nullptr, c->g, c->pk.n_ekey, c->pk.n_vkey, bad);
+          launch_check_graph(nullptr, M.g, M.nek, M.nvk, bad);
         });
+      lk.lock();
+      c->st.seal_incremental = 1;
+      if (c->algo < 0) {  // no results to keep: swap it in now
+        apply_merged(c, M);
+        finish_seal(c, n_end);
+      } else {  // the last run's results stay readable: the next run (or seal) swaps it in
+        c->pending = std::move(M);
+        const Merged& P = c->pending;
+        c->st.vertices = P.g.n_own;
+        c->st.edges = P.g.ne;
+        c->st.edges_owned = P.ne_owned;
+        c->st.vertex_events = P.nvk;
+        c->st.edge_events = P.nek;
+        c->st.deaths = P.dev ? P.ndt : (int64_t)P.hdtime.size();
+        c->st.seal_delta_updates = P.nd;
+        c->n_sealed = n_end;
+        c->sealed = true;
+      }
       drop_sealed_log(c, il.owns_lock());
       c->st.seal_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       return RGPU_OK;
@@ -2665,6 +2747,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   try {
     HIPCHK(hipSetDevice(c->device));
+    apply_pending(c);  // a run sees every seal that finished before it started
     {
       const auto ta = std::chrono::steady_clock::now();
       ensure_slots(c, algo, run_slots(c, rc));
@@ -3052,6 +3135,7 @@ const char* rgpu_last_error(rgpu_ctx* c) { return c ? c->err.c_str() : "null con
 void rgpu_close(rgpu_ctx* c) {
   if (!c) return;
   {
+    std::lock_guard<std::mutex> sl(c->seal_mu);
     std::lock_guard<std::mutex> lk(c->mu);
     (void)hipSetDevice(c->device);
     for (Slot& s : c->slot)
