@@ -210,7 +210,9 @@ int rgpu_cc_vertex_labels(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, i
                           size_t cap, size_t* n);
 
 /* DegreeBasic.returnResults (DegreeBasic.scala:16-28): tot = {totalV, totalOut, totalIn};
- * top-20 by in-degree (ties by ascending id) when RGPU_RUN_RETAIN was set, else zeros. */
+ * top-20 by in-degree (ties by ascending id), computed on the device in every degree run
+ * (no RGPU_RUN_RETAIN needed); slots past the view's vertex count hold id -1 and zero degrees.
+ * top_id/top_out/top_in may all be NULL to skip the list. */
 int rgpu_degree_result(rgpu_ctx* ctx, size_t hop, size_t win, int64_t tot[3], int64_t* top_id,
                        int32_t* top_out, int32_t* top_in);
 

@@ -88,6 +88,31 @@ __device__ __forceinline__ int32_t fold_uniform(uint64_t bal, uint64_t a, int32_
 
 // uw of a freshly computed row (lane = view, member lanes mv): x if uniform, else kMixed.  The
 // label INT32_MAX is kept as a row (its flagged form would read as kMixed).
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int d) {
+  const uint32_t lo = __shfl_xor((uint32_t)x, d), hi = __shfl_xor((uint32_t)(x >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+// fold_uniform by distinct label, smallest first: the smallest label among the remaining lanes is
+// final on every view its lanes cover (no remaining lane can lower those views), and lanes whose
+// views are all covered drop out.  A hub's changed neighbours in a converging view carry few
+// distinct labels, so this is a few rounds (two wave reductions each) instead of one round per
+// lane; the last few lanes go lane by lane (folding a larger label into a covered view is a no-op).
+__device__ __forceinline__ int32_t fold_uniform_by_label(uint64_t bal, uint64_t a, int32_t x, int32_t best, int lane) {
+  bal &= __ballot(a != 0);
+  uint64_t done = 0;
+  while (__popcll(bal) > 8) {
+    int32_t y = ((bal >> lane) & 1) ? x : INT32_MAX;
+    for (int o = 32; o > 0; o >>= 1) y = min(y, __shfl_xor(y, o));
+    const uint64_t sel = __ballot(((bal >> lane) & 1) && x == y);
+    uint64_t cov = ((sel >> lane) & 1) ? a : 0ull;
+    for (int o = 32; o > 0; o >>= 1) cov |= shfl_xor64(cov, o);
+    cov &= ~done;
+    if ((cov >> lane) & 1) best = min(best, y);
+    done |= cov;
+    bal &= ~sel & __ballot((a & ~done) != 0);
+  }
+  return fold_uniform(bal, a, x, best, lane);
+}
 __device__ __forceinline__ int32_t row_uniform(int32_t best, uint64_t mv, int lane) {
   const int32_t x0 = __builtin_amdgcn_readlane(best, __builtin_ctzll(mv));
   return (x0 == INT32_MAX || __ballot(((mv >> lane) & 1) && best != x0)) ? kMixed : x0;
@@ -1651,7 +1676,7 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
                                                       unsigned long long* __restrict__ work,
                                                       const uint64_t* __restrict__ vm,
-                                                      const int32_t* __restrict__ mneg) {
+                                                      const int32_t* __restrict__ mneg, int by_label) {
   if (stepflag[step - 1] == 0) return;
   const bool use_fin = vm && uw_cur && mneg;
   const int32_t mfin = use_fin ? final_label(mneg, threadIdx.x & 63) : INT32_MIN;
@@ -1699,7 +1724,8 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
           w_lanes += g;
         }
         best = gather_min<false>(u[k] == kMixed ? a : 0, q[k], best, lab_cur, lane);
-        best = fold_uniform(__ballot(u[k] != kMixed), a, u[k], best, lane);
+        best = by_label ? fold_uniform_by_label(__ballot(u[k] != kMixed), a, u[k], best, lane)
+                        : fold_uniform(__ballot(u[k] != kMixed), a, u[k], best, lane);
       }
       if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
       continue;
@@ -1730,7 +1756,9 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
         w_lanes += g;
       }
       best = gather_min<false>(u == kMixed ? a : 0, q, best, lab_cur, lane);
-      if (uw_cur) best = fold_uniform(__ballot(u != kMixed), a, u, best, lane);
+      if (uw_cur)
+        best = by_label ? fold_uniform_by_label(__ballot(u != kMixed), a, u, best, lane)
+                        : fold_uniform(__ballot(u != kMixed), a, u, best, lane);
     }
     if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
   }
@@ -1981,10 +2009,6 @@ __global__ __launch_bounds__(256) void k_cc_roots(int64_t nv, uint64_t vmask, co
 // totals (V, sum out, sum in) into stats[f*64 + view].
 // 64x64 bit-matrix transpose across the wave: lane r holds row r (bit c = column c) and gets
 // column r back (bit s = row s).  Six butterfly levels of 64-bit shuffles.
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t x, int d) {
-  const uint32_t lo = __shfl_xor((uint32_t)x, d), hi = __shfl_xor((uint32_t)(x >> 32), d);
-  return ((uint64_t)hi << 32) | lo;
-}
 __device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane) {
   const uint64_t M[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
                          0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
@@ -2426,6 +2450,12 @@ constexpr int kDealSlots = 16, kDealStep = 4;
 // supersteps >= kLateStep have small frontiers: at most kLateGrid blocks, the GPU left to the other batches
 constexpr int kLateStep = 14, kLateGrid = 1024;
 
+// (A/B, temporary) RGPU_AB bits: 1 packed superstep, 2 hub fold by label
+static int ab_flags() {
+  const char* e = std::getenv("RGPU_AB");
+  return e ? std::atoi(e) : 3;
+}
+
 static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
   int64_t g = (items + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -2509,8 +2539,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   // work != null (profile runs): the counting instantiation; the timed runs use the lean one.
   // 2-vertex chunks: 73 VGPRs, 6 waves/SIMD against 97 and 4 for 4-vertex chunks; same-box A/B
   // (profiles/r03/c4_ab_step_ch.log): C4 369 -> 345 ms, C2 135 -> 120 ms.
-  const int ab = [] { const char* e = std::getenv("RGPU_AB"); return e ? std::atoi(e) : 1; }();  // (A/B, temporary)
-  if (ab) {
+  if (ab_flags() & 1) {
 #define RGPU_PK_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
     cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr
@@ -2546,7 +2575,7 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
   k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
                                                              hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
-                                                             g.n_own, work, vm, mneg);
+                                                             g.n_own, work, vm, mneg, (ab_flags() & 2) != 0);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
