@@ -520,6 +520,19 @@ struct NoWork {
 // bitmap and stepcnt[1]; vadj[v] = OR of v's kept slot masks (v isolated in view j iff bit j
 // is clear).
 
+// A kept slot's view bits before the own mask: the edge's window bits (inline for simple slots)
+// and the neighbour's membership.  With ebp.simple_ends the simple slots skip the neighbour's mask:
+// their bits already imply it (BatchParams::simple_ends).
+__device__ __forceinline__ uint64_t slot_bits(const HopLDS& L, const BatchParams& ebp, int64_t tsw,
+                                              const uint64_t* __restrict__ em, int64_t e,
+                                              const uint64_t* __restrict__ vm, int32_t nb) {
+  if (ts_simple(tsw)) {
+    const uint64_t b = simple_bits(L, ebp.sorted, ts_time(tsw));
+    return ebp.simple_ends ? b : b & vm[nb];
+  }
+  return em[e] & vm[nb];
+}
+
 // PROF = false: the work counters compile away (launch_cc_slots: work == null).  IEM: inline edge
 // bits (slot_bits; time-ordered slots required), em unused
 template <bool PROF, bool IEM>
@@ -626,7 +639,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         const int32_t e = ts_e[p];
         if (nb != (int32_t)vmy && ts_time(tsw) >= tcut) {
           if constexpr (IEM) {
-            m = (ts_simple(tsw) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[e]) & vm[nb] & mvmy;
+            m = slot_bits(L, ebp, tsw, em, e, vm, nb) & mvmy;
           } else {
             m = em[e] & (ends ? mvmy : vm[nb]) & mvmy;
           }
@@ -797,7 +810,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         const int64_t tsw = ts_t ? ts_t[base + j] : 0;
         if (nb != (int32_t)v && (!ts_t || ts_time(tsw) >= tcut)) {
           if constexpr (IEM) {
-            m = (ts_simple(tsw) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[e]) & vm[nb] & mv;
+            m = slot_bits(L, ebp, tsw, em, e, vm, nb) & mv;
           } else {
             m = em[e] & (ends ? mv : vm[nb]) & mv;
           }
@@ -1162,7 +1175,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
         cbits |= 1ull << (v & 63);
         if (lane == 0) atomicOr(lds_lanes, (unsigned long long)ch);  // LDS: views changed this step
         changed++;
-        if (skip_marks) continue;  // dense step: the next step visits every member (k_cc_step2)
+        if (skip_marks) continue;  // dense step: the next step visits every member
         mark(lane == 0, (int32_t)v, act_next);
         mark((sm[i] & ch) != 0, nb[i], act_next);
         if (n > 64) {
@@ -1199,118 +1212,9 @@ __global__ __launch_bounds__(256) void k_uw_rows(int64_t nv, const uint64_t* __r
   }
 }
 
-// Superstep kernel (full grid).  Step r visits the vertices flagged in act_cur (bytes, plain
-// idempotent stores by step r-1), CH consecutive ranks per wave-chunk, and clears act_clear
-// (read two steps ago, written next step).
-// MINW > 1: amdgpu_waves_per_eu(MINW) (a VGPR cap; a 6-wave cap measured slower)
-template <int CH, bool BUF, int MINW, bool PROF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void k_cc_step2(int step, int64_t nv, const int64_t* __restrict__ adj_off,
-                                                  const uint64_t* __restrict__ vm,
-                                                  const int32_t* __restrict__ cnt,
-                                                  const int32_t* __restrict__ snbr,
-                                                  const uint64_t* __restrict__ smask,
-                                                  const int32_t* __restrict__ lab_cur,
-                                                  int32_t* __restrict__ lab_next,
-                                                  const uint64_t* __restrict__ chg_prev,
-                                                  uint64_t* __restrict__ chg_next,
-                                                  const uint8_t* __restrict__ act_cur,
-                                                  uint8_t* __restrict__ act_next,
-                                                  uint8_t* __restrict__ act_clear,
-                                                  int32_t* __restrict__ stepflag,
-                                                  int32_t* __restrict__ hostflag,
-                                                  unsigned long long* __restrict__ work,
-                                                  const int32_t* __restrict__ hv_of,
-                                                  int32_t* __restrict__ hbest,
-                                                  unsigned long long* __restrict__ lanechg,
-                                                  const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
-                                                  uint64_t* __restrict__ cb_next,
-                                                  uint64_t* __restrict__ cb_clear, int64_t cb_words,
-                                                  int32_t* __restrict__ ccount, int dense_div, int gmax,
-                                                  const int32_t* __restrict__ mneg) {
-  if (stepflag[step - 1] == 0) return;
-  const int32_t mfin = final_label(mneg, threadIdx.x & 63);
-  // Dense steps (DenseRule): when step r-1 changed at least nv / dense_div vertices, step r
-  // writes no next-frontier flags and step r+1 visits every member instead
-  const bool skip_marks = dense_rule(ccount, step, nv, dense_div);
-  const bool visit_all = dense_rule(ccount, step - 1, nv, dense_div);
-  __shared__ int32_t red;
-  __shared__ unsigned long long wred[8];  // [0..6] work fields (StepWork), [7] changed views (LDS OR)
-  if (threadIdx.x < 8) wred[threadIdx.x] = 0;
-  if (threadIdx.x == 0) red = 0;
-  const int64_t nwords = (nv + 7) >> 3;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords;
-       i += (int64_t)gridDim.x * blockDim.x)
-    reinterpret_cast<uint64_t*>(act_clear)[i] = 0;
-  if (cb_clear)  // changed bits: written in r, read in r+1, cleared here in r+2 (three in rotation)
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cb_words; i += (int64_t)gridDim.x * blockDim.x)
-      cb_clear[i] = 0;
-  __syncthreads();
-  const int lane = lane_id();
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  int32_t changed = 0;
-  std::conditional_t<PROF, StepWork, NoWork> wk;
-  // Chunks are dealt in groups of up to gmax (deal_group, as K2 deals vertices; RGPU_DEAL_STEP):
-  // per round lane l reads its chunk's frontier flags, and the wave then runs only the flagged
-  // chunks — a sparse frontier costs one load per 64 chunks.  Every wave of the grid gets work on
-  // a small graph too.  Small groups spread a run of busy chunks over many waves (a frontier is
-  // clustered in rank order, the more so in the locality order); whole-line flag loads favour
-  // large ones.
-  const int64_t nchunks = (nv + CH - 1) / CH;
-  const int G = deal_group(nchunks, nwaves, gmax);
-  for (int64_t r = 0; (wave + r * (64 / G) * nwaves) * G < nchunks; r++) {
-    const int64_t cl = dealt_item(wave, nwaves, r, G, lane);
-    uint32_t fb = 0;
-    if (cl < nchunks) {
-      const int64_t v0 = cl * CH;
-      if (visit_all) {  // every member: the chunk's view masks (32 B per lane, one line per 2 lanes)
-#pragma unroll
-        for (int i = 0; i < CH; i++) fb |= (v0 + i < nv && vm[v0 + i] != 0) ? (1u << i) : 0u;
-      } else {
-        const uint64_t f = CH == 8   ? *reinterpret_cast<const uint64_t*>(act_cur + v0)
-                           : CH == 4 ? *reinterpret_cast<const uint32_t*>(act_cur + v0)
-                                     : *reinterpret_cast<const uint16_t*>(act_cur + v0);
-#pragma unroll
-        for (int i = 0; i < CH; i++) fb |= ((f >> (8 * i)) & 0xffu) ? (1u << i) : 0u;
-      }
-      if (v0 + CH > nv) fb &= (1u << (nv - v0)) - 1;
-    }
-    uint64_t todo = __ballot(fb != 0);
-    while (todo) {
-      const int L = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)fb, L);
-      cc_chunk<CH, BUF>(dealt_item(wave, nwaves, r, G, L) * CH + (lane & (CH - 1)), bits, adj_off, vm, cnt, snbr, smask, lab_cur,
-                        lab_next, chg_prev, chg_next, act_next, lane, changed, &wred[7], wk,
-                               hv_of, hbest, uw_cur, uw_next, cb_next, skip_marks, mfin, mneg != nullptr && uw_cur);
-    }
-  }
-  if constexpr (PROF)
-    for (int o = 32; o > 0; o >>= 1) wk.g += __shfl_xor(wk.g, o);
-  if (lane == 0) {
-    if (changed) atomicAdd(&red, changed);
-    if constexpr (PROF) {
-      const unsigned long long f[7] = {wk.v, wk.s, 0, wk.g, wk.a, wk.lr, wk.lw};
-#pragma unroll
-      for (int i = 0; i < 7; i++)
-        if (f[i]) atomicAdd(&wred[i], f[i]);
-      if (wk.uw) atomicAdd(&wred[2], wk.uw);  // (slot 2 is free: the changed count has `red`)
-    }
-  }
-  publish_lanes(0, &wred[7], lanechg, step);
-  if (threadIdx.x == 0) {
-    if (red && ccount) atomicAdd(&ccount[step * kCountShards + (blockIdx.x & (kCountShards - 1))], red);
-    if (red && stepflag[step] == 0) {  // first writers also tell the host (mapped pinned memory)
-      stepflag[step] = 1;
-      if (hostflag) hostflag[step] = 1;
-    }
-    const unsigned long long f[8] = {wred[0], wred[1], (unsigned long long)red, wred[3], wred[4], wred[5], wred[6],
-                                     wred[2]};
-    add_work(work, step, f);
-  }
-}
-
-// Packed superstep (default).  A wave takes 64 vertices per round (lane = vertex, dealt in
+// Superstep kernel (full grid; the packed form).  Step r visits the vertices flagged in act_cur
+// (bytes, plain idempotent stores by step r-1) and clears act_clear (read two steps ago, written
+// next step).  A wave takes 64 vertices per round (lane = vertex, dealt in
 // groups of consecutive ranks): their frontier flags and then the flagged members' metadata (view
 // mask, kept-slot count and offset, change word, uniform words, hub index) in one coalesced load
 // each.  The kept slots of the members with at most 64 of them are packed into 64-lane passes
@@ -1627,7 +1531,7 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
         const int64_t tsw = ts_t ? ts_t[lo + jj] : 0;
         if (nb != v && (!ts_t || ts_time(tsw) >= tcut)) {
           if constexpr (IEM) {
-            m = (ts_simple(tsw) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[e]) & vm[nb] & mv;
+            m = slot_bits(L, ebp, tsw, em, e, vm, nb) & mv;
           } else {
             m = em[e] & (ends ? mv : vm[nb]) & mv;
           }
@@ -1676,7 +1580,7 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
                                                       unsigned long long* __restrict__ work,
                                                       const uint64_t* __restrict__ vm,
-                                                      const int32_t* __restrict__ mneg, int by_label) {
+                                                      const int32_t* __restrict__ mneg) {
   if (stepflag[step - 1] == 0) return;
   const bool use_fin = vm && uw_cur && mneg;
   const int32_t mfin = use_fin ? final_label(mneg, threadIdx.x & 63) : INT32_MIN;
@@ -1724,8 +1628,7 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
           w_lanes += g;
         }
         best = gather_min<false>(u[k] == kMixed ? a : 0, q[k], best, lab_cur, lane);
-        best = by_label ? fold_uniform_by_label(__ballot(u[k] != kMixed), a, u[k], best, lane)
-                        : fold_uniform(__ballot(u[k] != kMixed), a, u[k], best, lane);
+        best = fold_uniform_by_label(__ballot(u[k] != kMixed), a, u[k], best, lane);
       }
       if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
       continue;
@@ -1756,9 +1659,7 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
         w_lanes += g;
       }
       best = gather_min<false>(u == kMixed ? a : 0, q, best, lab_cur, lane);
-      if (uw_cur)
-        best = by_label ? fold_uniform_by_label(__ballot(u != kMixed), a, u, best, lane)
-                        : fold_uniform(__ballot(u != kMixed), a, u, best, lane);
+      if (uw_cur) best = fold_uniform_by_label(__ballot(u != kMixed), a, u, best, lane);
     }
     if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
   }
@@ -2446,15 +2347,9 @@ __global__ __launch_bounds__(256) void k_xscatter_f64(int64_t n, const int32_t* 
 // Launch constants (measured on MI355X).
 // deal_group maxima of K2 / the superstep kernel (C4 A/B, profiles/r03/c4_ab_deal.log: K2 16 ~ 64 < 1,
 // superstep 4 << 64)
-constexpr int kDealSlots = 16, kDealStep = 4;
+constexpr int kDealSlots = 16;
 // supersteps >= kLateStep have small frontiers: at most kLateGrid blocks, the GPU left to the other batches
 constexpr int kLateStep = 14, kLateGrid = 1024;
-
-// (A/B, temporary) RGPU_AB bits: 1 packed superstep, 2 hub fold by label
-static int ab_flags() {
-  const char* e = std::getenv("RGPU_AB");
-  return e ? std::atoi(e) : 3;
-}
 
 static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
   int64_t g = (items + per_block - 1) / per_block;
@@ -2529,30 +2424,20 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
   // A small graph's dense supersteps are latency-bound and share the GPU with the other batch
   // slots too: a 1,024-block cap measured 4 % faster on C2 (100k vertices) and 2 % slower on a
-  // 4.7M-vertex C4-shaped graph, hence the size rule (RGPU_STEP_GRID overrides it).
+  // 4.7M-vertex C4-shaped graph, hence the size rule.
   const unsigned full = g.nv <= ((int64_t)1 << 21) ? 1024u : 4096u;
   const unsigned cap = step >= kLateStep ? (full < (unsigned)kLateGrid ? full : (unsigned)kLateGrid) : full;
   const int32_t* hv_of = hbest ? g.hv_of : nullptr;
-#define RGPU_STEP_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
-    act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.next, cb.clear, cb.words, ccount, dense_div, kDealStep, uw_cur ? mneg : nullptr
   // work != null (profile runs): the counting instantiation; the timed runs use the lean one.
-  // 2-vertex chunks: 73 VGPRs, 6 waves/SIMD against 97 and 4 for 4-vertex chunks; same-box A/B
-  // (profiles/r03/c4_ab_step_ch.log): C4 369 -> 345 ms, C2 135 -> 120 ms.
-  if (ab_flags() & 1) {
+  // Same-box A/B against the 2-vertex-chunk kernel it replaced (profiles/r04/ab_packed_step.jsonl):
+  // C4 serial cc_step 207.6 -> 155.1 ms, query 343 -> 286 ms.
 #define RGPU_PK_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
     cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr
-    const unsigned gridp = grid_for(g.nv, 256, cap);
-    if (work) k_cc_step_pk<false, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
-    else k_cc_step_pk<false, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
+  const unsigned gridp = grid_for(g.nv, 256, cap);
+  if (work) k_cc_step_pk<false, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
+  else k_cc_step_pk<false, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
 #undef RGPU_PK_ARGS
-    return;
-  }
-  const unsigned grid2 = grid_for(g.nv, 8, cap);
-  if (work) k_cc_step2<2, false, 1, true><<<grid2, 256, 0, s>>>(RGPU_STEP_ARGS);
-  else k_cc_step2<2, false, 1, false><<<grid2, 256, 0, s>>>(RGPU_STEP_ARGS);
-#undef RGPU_STEP_ARGS
 }
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                         int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends, unsigned long long* work,
@@ -2575,7 +2460,7 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
   k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
                                                              hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
-                                                             g.n_own, work, vm, mneg, (ab_flags() & 2) != 0);
+                                                             g.n_own, work, vm, mneg);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,

@@ -38,6 +38,10 @@ struct BatchParams {
   int64_t thr_v[kViews];  // vertex-set window of window index w: min(w_0..w_w)  (shrinkWindow)
   int64_t thr_e[kViews];  // edge window of window index w: w_w (viewAtWithWindow(t, setWindow))
   int64_t jump;           // > 0: hop[k] = hop[0] + k * jump for every k < K (K1's arithmetic hop search)
+  // every view's vertex window equals its edge window (descending window lists): then a simple
+  // slot's window bits imply both endpoints' membership (an EADD is a `+` point of both endpoints,
+  // neither of which ever dies), so K2 / the ghost marking skip the neighbour's mask read for it
+  int simple_ends;
 };
 
 // Sealed partition resident in HBM.

@@ -859,6 +859,11 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     ebp.thr_e[0] = rc.thr_e[grp];
   }
   const bool skip_simple = iem && !c->d_ecnt;
+  {
+    const int w0 = rc.G == 1 ? 0 : grp * rc.gsize, w1 = rc.G == 1 ? rc.W : w0 + rc.gsize;
+    ebp.simple_ends = 1;
+    for (int w = w0; w < w1; w++) ebp.simple_ends &= rc.thr_v[w] == rc.thr_e[w];
+  }
   s.iem = iem;
   s.ebp = ebp;
   if (rc.G == 1) {
@@ -2020,8 +2025,10 @@ void build_tslots(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L) {
   }
 }
 
+}  // extern "C" (a C++ helper: it returns a struct)
+
 // the send plan by boundary vertex (xchg.hip build_xsend), from the (peer, vertex) lists
-XSend build_send_plan(int64_t n_own, const Part& X, std::vector<void*>& L) {
+static XSend build_send_plan(int64_t n_own, const Part& X, std::vector<void*>& L) {
   std::vector<void*> T;
   XSend xs;
   try {
@@ -2033,6 +2040,8 @@ XSend build_send_plan(int64_t n_own, const Part& X, std::vector<void*>& L) {
   for (void* p : T) (void)hipFree(p);
   return xs;
 }
+
+extern "C" {
 
 // the neighbours' labels (grank) in time-ordered slot order, once grank is known
 void build_tslot_labels(DevGraph& g, std::vector<void*>& L) {

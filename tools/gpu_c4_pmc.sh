@@ -8,7 +8,7 @@ O=gpurun_out/c4pmc; mkdir -p $O
 A="--config c4 --c4-interactions ${C4I:-33333334} --c4-users ${C4U:-5000000}"
 timeout -k 10 300 python3 bench.py $A > $O/bench.log 2>&1 || exit $?
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 400 rocprofv3 --pmc $c --kernel-include-regex k_cc_step2 -d $O/$c -o run --output-format csv -- python3 bench.py $A > $O/$c.log 2>&1 || exit $?
+  timeout -k 10 400 rocprofv3 --pmc $c --kernel-include-regex k_cc_step_pk -d $O/$c -o run --output-format csv -- python3 bench.py $A > $O/$c.log 2>&1 || exit $?
 done
 python3 - <<'PY'
 import csv, glob, json

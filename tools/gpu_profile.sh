@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/prof
 mkdir -p $O
-K=${KREGEX:-k_cc_step2}
+K=${KREGEX:-k_cc_step_pk}
 run() { local name=$1 secs=$2; shift 2; echo "=== $name"; timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "=== $name rc=$rc"; tail -3 "$O/$name.log"; [ $rc -eq 0 ] || exit $rc; }
 if [ -z "${SKIP_BENCH:-}" ]; then
   run bench 600 python bench.py ${BENCH_ARGS:-}
