@@ -392,6 +392,8 @@ def run_c4(a, rank, world, local):
 
     if a.profile_only:
         a.steps, a.warmup, a.no_cpu_baseline = 1, 0, True
+    if a.lean_pass_only:  # a rocprofv3 trace of this command holds the serial lean pass alone
+        a.no_edge_counts = True
     for _ in range(a.warmup):
         g.run("cc", hops, windows)
     barrier()

@@ -16,9 +16,9 @@ if [ -z "${SKIP_BENCH:-}" ]; then
   run prof_only 300 python bench.py --profile-only ${BENCH_ARGS:-}
   grep '^{' $O/prof_only.log > $O/prof_only.json || true
 fi
-run kt 600 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
-run fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $O/fetch -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
-run write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O/write -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
+run kt ${STEP_SECS:-600} rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
+run fetch ${STEP_SECS:-600} rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $O/fetch -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
+run write ${STEP_SECS:-600} rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O/write -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
 python3 - "$K" <<'PY'
 import csv, glob, json, sys
 k = sys.argv[1]
