@@ -100,13 +100,13 @@ __global__ __launch_bounds__(256) void k_xvm_unpack(int64_t nx, const int32_t* _
 // :112-120, sent once per vertex instead of once per (vertex, peer)).  A boundary vertex is named by
 // its index b in the sender's boundary list (ascending owned rank); a receiver maps (peer q, b) to
 // its ghost rank through tab[toff[q] + b] (-1: q's vertex is no ghost here, the record is skipped).
-//   U record (8 B): b << 32 | label — a uniform sender (kernels.hpp kMixed) that changed in every
-//                   member view where it has a kept neighbour: the ghost takes the label as its
-//                   uniform word and changed in all views (its readers fold a changed uniform
-//                   neighbour on every kept view of the slot; kept masks lie inside the sender's
-//                   kept-neighbour views, so "all" marks exactly the same neighbours).
-//   M record (16 B, XRec): {b, label, views} per distinct new label of a mixed sender, or the one
-//                   label of a uniform sender that changed in only part of its views.
+//   U record (8 B): b << 32 | label — a uniform sender (kernels.hpp kMixed) that changed in any
+//                   view where it has a kept neighbour: the ghost takes the label as its uniform
+//                   word with the changed flag, exactly as a local uniform vertex's word reads
+//                   (readers fold a changed uniform neighbour on every kept view of the slot; in
+//                   the views where it did not change the label is its current one, so the fold
+//                   changes nothing there).
+//   M record (16 B, XRec): {b, label, views} per distinct new label of a mixed sender.
 // A sender's U records need at most nb slots (one per boundary vertex): U buffers are sized for the
 // worst case at plan time and never grow; M records (mixed senders: rare) grow on demand.
 __global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, const int32_t* __restrict__ bidx,
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, const int32_t* 
     const uint64_t m = vis ? chg_now[v] & vadj[v] : 0;
     if (!__ballot(m != 0)) continue;
     const int32_t u = m ? uw_label(uw[v]) : kMixed;
-    const bool full = m != 0 && u != kMixed && m == (vm[v] & vadj[v]);
+    const bool full = m != 0 && u != kMixed;
     const uint64_t bu = __ballot(full);
     if (bu) {
       unsigned long long base = 0;
@@ -138,19 +138,10 @@ __global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, const int32_t* 
              __builtin_amdgcn_readlane((uint32_t)base, 0);
       if (full) su[base + __popcll(bu & lanemask_below(lane))] = ((unsigned long long)(uint32_t)b << 32) | (uint32_t)u;
     }
-    for (uint64_t mb = __ballot(m != 0 && !full); mb; mb &= mb - 1) {  // M senders, one at a time
+    for (uint64_t mb = __ballot(m != 0 && !full); mb; mb &= mb - 1) {  // mixed senders, one at a time
       const int L = __builtin_ctzll(mb);
       const int32_t bL = __builtin_amdgcn_readlane(b, L);
-      const int32_t uL = __builtin_amdgcn_readlane(u, L);
       const uint64_t mL = rl64(m, L);
-      if (uL != kMixed) {  // uniform, partly changed: its one label in the changed views
-        unsigned long long pos = 0;
-        if (lane == 0) {
-          pos = atomicAdd(&cnt[1], 1ull);
-          if (pos < (unsigned long long)mcap) sm[pos] = XRec{bL, uL, mL};
-        }
-        continue;
-      }
       const int64_t vL = v0 + L;
       const int32_t x = lab[vL * 64 + lane];
       int k = 0;  // distinct labels over the changed views: count, reserve, write
