@@ -614,7 +614,9 @@ def run_c5(a, rank, world, local):
     up = upd_ticks * len(ticks)
     n_v = int(reduce(st["vertices"], dist.ReduceOp.SUM) if dist is not None else st["vertices"])
     n_e = int(reduce(st["edges_owned"], dist.ReduceOp.SUM) if dist is not None else st["edges"])
-    out = {"config": "C5", "n_gpus": world, "base_updates": n_base, "base_seal_s": round(base_seal_s, 1),
+    out = {"metric": "live updates/s sustained (ingest + merge + CC {y,m,w,d,h} + PageRank per tick)",
+           "value": up / wall if wall else None, "unit": "updates/s", "higher_is_better": True,
+           "config": "C5", "n_gpus": world, "base_updates": n_base, "base_seal_s": round(base_seal_s, 1),
            "ticks": len(ticks), "updates_per_tick": upd_ticks,
            "live_updates_per_s": up / wall if wall else None, "wall_s": round(wall, 3),
            "sustained_note": "every tick included (tick 0's ingest + merge too), first ingest to last analysis",

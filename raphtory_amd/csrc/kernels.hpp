@@ -307,12 +307,18 @@ void launch_xtab_fill(hipStream_t s, int64_t n, const int32_t* xr_v, const int32
                       const XTab& T, unsigned long long* err);
 // After superstep `step`: this partition's broadcast label records (xchg.hip: U records into su, at
 // most nb; M records into sm, cnt[1] counts past mcap so the host can grow and pack again)
+// The pack of superstep `step`'s broadcast records (xchg.hip k_xbc_pack): per 64-boundary-vertex
+// chunk a count pass (ccnt[c] = U << 32 | M records), a device scan into coff (coff[nchunks] = the
+// totals; ccnt[nchunks] must be 0), then the write pass.  write_only: coff is current (a repack
+// into a larger M buffer).  ccnt / coff hold (nb + 63) / 64 + 1 words, scan_tmp xbc_scan_bytes(nb).
+size_t xbc_scan_bytes(int64_t nb);
 void launch_xbc_pack(hipStream_t s, int64_t n_own, const XSend& X, const uint8_t* act, const uint64_t* chg_now,
-                     const uint64_t* vadj, const uint64_t* vm, const int32_t* lab, const int32_t* uw,
-                     unsigned long long* su, XRec* sm, int64_t mcap, unsigned long long* cnt, const int32_t* ccount,
-                     int dense_div, int step);
-// counts words (4 per peer): U records, M records, the halting vote; cnt reset
-void launch_xbc_counts(hipStream_t s, int np, int me, unsigned long long* cnt, const int32_t* stepflag, int64_t* xa);
+                     const uint64_t* vadj, const int32_t* lab, const int32_t* uw, unsigned long long* su, XRec* sm,
+                     int64_t mcap, unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp,
+                     size_t scan_bytes, const int32_t* ccount, int dense_div, int step, bool write_only);
+// counts words (4 per peer): U records, M records (tot = the pack's scanned totals), the halting vote
+void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* tot, const int32_t* stepflag,
+                       int64_t* xa);
 // component-count records (2 words per peer); scnt reset
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, int64_t* xa);
 // a received broadcast: U and M receive regions per peer, with the records received (pre), the

@@ -131,7 +131,9 @@ struct XSlot {
   int64_t rmcap[kMaxParts] = {};
   int64_t rucnt[2][kMaxParts] = {}, rmcnt[2][kMaxParts] = {};  // records received per parity (their
                                           // ghosts' words are cleared two supersteps later)
-  unsigned long long* cnt = nullptr;      // [2] U / M records of the pack in flight
+  unsigned long long *ccnt = nullptr, *coff = nullptr;  // the pack's per-chunk counts and their scan
+  void* scan_tmp = nullptr;               // (xchg.hip launch_xbc_pack; sized with su)
+  size_t scan_bytes = 0;
   unsigned long long* err = nullptr;      // received records outside the plan (xchg.hip bc_rec)
   int64_t* xab = nullptr;                 // [8P] counts words: sent (xa) | received (xb)
   int64_t* h_xab = nullptr;               // pinned copy
@@ -1232,7 +1234,7 @@ XPeers peers_layout(const rgpu_ctx* c, const int64_t* cap, const std::vector<int
 void free_part_slots(rgpu_ctx* c, bool keep_channels) {
   for (XSlot& xs : c->pt.xs) {
     for (void* p : {(void*)xs.su, (void*)xs.sm, (void*)xs.ru[0], (void*)xs.ru[1], (void*)xs.rm[0], (void*)xs.rm[1],
-                    (void*)xs.hsbuf, (void*)xs.hrbuf})
+                    (void*)xs.hsbuf, (void*)xs.hrbuf, (void*)xs.ccnt, (void*)xs.coff, xs.scan_tmp})
       if (p) (void)hipFree(p);
     if (xs.h_xab) (void)hipHostFree(xs.h_xab);
     Exchange* x = xs.x;
@@ -1304,9 +1306,7 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
   for (int i = 0; i < nuse; i++) {
     XSlot& xs = X.xs[i];
     if (!xs.x) xs.x = X.xchg->fork(i + 1);  // collective: every partition forks the same slots
-    if (!xs.cnt) {
-      xs.cnt = dalloc<unsigned long long>(LG, 2);
-      HIPCHK(hipMemset(xs.cnt, 0, sizeof(unsigned long long) * 2));
+    if (!xs.err) {
       xs.err = dalloc<unsigned long long>(LG, 1);
       xs.htot = dalloc<unsigned long long>(LG, kMaxParts);
       HIPCHK(hipMemset(xs.htot, 0, sizeof(unsigned long long) * kMaxParts));
@@ -1322,12 +1322,20 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
     if (xs.su_cap < X.xsend.nb || xs.ru_cap < X.tab.toff[P] || !xs.su) {
       // U records: worst case one per boundary vertex, sent and received (sized by the plan: no
       // growth during a run, no host sizing)
-      for (void* p : {(void*)xs.su, (void*)xs.ru[0], (void*)xs.ru[1]})
+      for (void* p : {(void*)xs.su, (void*)xs.ru[0], (void*)xs.ru[1], (void*)xs.ccnt, (void*)xs.coff, xs.scan_tmp})
         if (p) HIPCHK(hipFree(p));
       xs.su_cap = std::max<int64_t>(X.xsend.nb, 1);
       xs.ru_cap = std::max<int64_t>(X.tab.toff[P], 1);
       HIPCHK(hipMalloc((void**)&xs.su, sizeof(unsigned long long) * (size_t)xs.su_cap));
       for (int p = 0; p < 2; p++) HIPCHK(hipMalloc((void**)&xs.ru[p], sizeof(unsigned long long) * (size_t)xs.ru_cap));
+      // the pack's chunk counts and offsets (ccnt[nchunks] stays 0: coff[nchunks] = the totals)
+      const size_t nck = (size_t)((xs.su_cap + 63) / 64 + 1);
+      HIPCHK(hipMalloc((void**)&xs.ccnt, sizeof(unsigned long long) * nck));
+      HIPCHK(hipMalloc((void**)&xs.coff, sizeof(unsigned long long) * nck));
+      HIPCHK(hipMemset(xs.ccnt, 0, sizeof(unsigned long long) * nck));
+      HIPCHK(hipMemset(xs.coff, 0, sizeof(unsigned long long) * nck));
+      xs.scan_bytes = std::max<size_t>(xbc_scan_bytes(xs.su_cap), 16);
+      HIPCHK(hipMalloc(&xs.scan_tmp, xs.scan_bytes));
     }
     if (!xs.sm) {
       // M records: a first guess, grown on demand (both receive parities share one layout, xs.rmcap)
@@ -1363,15 +1371,22 @@ void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int pl
   HIPCHK(hipGetLastError());
 }
 
-// the broadcast label records of superstep r (U into xs.su, M into xs.sm)
-void part_pack(rgpu_ctx* c, int si, int r) {
+// the broadcast label records of superstep r (U into xs.su, M into xs.sm).  write_only: the
+// offsets of the last pack are current (a repack into a larger M buffer)
+void part_pack(rgpu_ctx* c, int si, int r, bool write_only = false) {
   Slot& s = c->slot[si];
   Part& X = c->pt;
   XSlot& xs = X.xs[si];
   timed_launch(c, si, KID_XPACK, 0.0, [&] {
-    launch_xbc_pack(s.stream, c->pk.n_own, X.xsend, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj, s.vm,
-                    s.lab[r & 1], s.uw[r & 1], xs.su, xs.sm, xs.smcap, xs.cnt, s.ccount, dense_div(c), r);
+    launch_xbc_pack(s.stream, c->pk.n_own, X.xsend, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
+                    s.lab[r & 1], s.uw[r & 1], xs.su, xs.sm, xs.smcap, xs.ccnt, xs.coff, xs.scan_tmp, xs.scan_bytes,
+                    s.ccount, dense_div(c), r, write_only);
   });
+}
+// the pack's totals word (U << 32 | M), or null without boundary vertices
+const unsigned long long* pack_totals(const rgpu_ctx* c, const XSlot& xs) {
+  const int64_t nb = c->pt.xsend.nb;
+  return nb > 0 ? xs.coff + (nb + 63) / 64 : nullptr;
 }
 
 // a received broadcast of parity par: regions and record counts (xchg.hip XBcIn)
@@ -1419,7 +1434,7 @@ void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
     return;
   }
   part_pack(c, si, r);
-  launch_xbc_counts(s.stream, P, c->part, xs.cnt, s.stepcnt + r, xs.xab);
+  launch_xbc_counts(s.stream, P, c->part, pack_totals(c, xs), s.stepcnt + r, xs.xab);
   HIPCHK(hipGetLastError());
   xs.x->alltoall_i64(xs.xab, xs.xab + 4 * P, 4, s.stream);
   HIPCHK(hipMemcpyAsync(xs.h_xab, xs.xab, sizeof(int64_t) * 8 * P, hipMemcpyDeviceToHost, s.stream));
@@ -1451,8 +1466,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   }
   if (sent_m > xs.smcap) {  // the counts were exact; the M records did not all fit: pack again, larger
     grow_regions(&xs.sm, &xs.smcap, &sent_m, 1, s.stream);
-    part_pack(c, si, r);
-    HIPCHK(hipMemsetAsync(xs.cnt, 0, sizeof(unsigned long long) * 2, s.stream));
+    part_pack(c, si, r, true);
   }
   if (!any) {  // every partition voted to halt
     s.r_final = r;
@@ -1836,7 +1850,7 @@ void reset_after_failure(rgpu_ctx* c) {
   for (Slot& s : c->slot)
     for (void* p : {(void*)s.hv.segcnt, (void*)s.hv.segor, (void*)s.hv.best, (void*)s.hv.pacc}) drop_alloc(LG, p);
   for (XSlot& xs : c->pt.xs)
-    for (void* p : {(void*)xs.cnt, (void*)xs.err, (void*)xs.htot, (void*)xs.xab, (void*)xs.vms, (void*)xs.vmr})
+    for (void* p : {(void*)xs.err, (void*)xs.htot, (void*)xs.xab, (void*)xs.vms, (void*)xs.vmr})
       drop_alloc(LG, p);
   release_slots(c);
   free_part_slots(c, true);

@@ -109,57 +109,76 @@ __global__ __launch_bounds__(256) void k_xvm_unpack(int64_t nx, const int32_t* _
 //   M record (16 B, XRec): {b, label, views} per distinct new label of a mixed sender.
 // A sender's U records need at most nb slots (one per boundary vertex): U buffers are sized for the
 // worst case at plan time and never grow; M records (mixed senders: rare) grow on demand.
-__global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, const int32_t* __restrict__ bidx,
+// The pack runs in two passes over chunks of 64 consecutive boundary vertices (lane = b, the owned
+// rank X.v[b]): the count pass writes each chunk's U and M record counts (ccnt[c] = U << 32 | M),
+// a device scan turns them into offsets, and the write pass puts the records there.  No shared
+// counter: one atomic per wave on a single address serialised at the memory side (DESIGN.md §4
+// lesson 1) and was most of the one-pass pack's time.  A mixed sender's distinct labels are found
+// on its row (lane = view); rows of up to kRowsInFlight senders are loaded before any is folded.
+constexpr int kRowsInFlight = 4;
+__device__ __forceinline__ int distinct_labels(int32_t x, uint64_t mm, int lane) {
+  int k = 0;
+  while (mm) {
+    const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
+    mm &= ~__ballot(((mm >> lane) & 1) && x == val);
+    k++;
+  }
+  return k;
+}
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, int64_t nb, const int32_t* __restrict__ xb,
                                                   const uint8_t* __restrict__ act, const uint64_t* __restrict__ chg_now,
-                                                  const uint64_t* __restrict__ vadj, const uint64_t* __restrict__ vm,
-                                                  const int32_t* __restrict__ lab, const int32_t* __restrict__ uw,
-                                                  unsigned long long* __restrict__ su, XRec* __restrict__ sm, int64_t mcap,
-                                                  unsigned long long* __restrict__ cnt, const int32_t* __restrict__ ccount,
-                                                  int dense_div, int step) {
+                                                  const uint64_t* __restrict__ vadj, const int32_t* __restrict__ lab,
+                                                  const int32_t* __restrict__ uw, unsigned long long* __restrict__ su,
+                                                  XRec* __restrict__ sm, int64_t mcap,
+                                                  unsigned long long* __restrict__ ccnt,
+                                                  const unsigned long long* __restrict__ coff,
+                                                  const int32_t* __restrict__ ccount, int dense_div, int step) {
   const int lane = lane_of();
   if (dense_after(ccount, step, n_own, dense_div)) act = nullptr;  // the step visited every member
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t v0 = wave * 64; v0 < n_own; v0 += nwaves * 64) {
-    // lane = owned vertex: every load coalesced
-    const int64_t v = v0 + lane;
-    const bool ok = v < n_own;
-    const int32_t b = ok ? bidx[v] : -1;
-    const bool vis = b >= 0 && (act == nullptr || act[v]);
+  const int64_t nchunks = (nb + 63) >> 6;
+  for (int64_t c = wave; c < nchunks; c += nwaves) {
+    const int64_t b = c * 64 + lane;
+    const int32_t v = b < nb ? xb[b] : -1;
+    const bool vis = v >= 0 && (act == nullptr || act[v]);
     const uint64_t m = vis ? chg_now[v] & vadj[v] : 0;
-    if (!__ballot(m != 0)) continue;
     const int32_t u = m ? uw_label(uw[v]) : kMixed;
-    const bool full = m != 0 && u != kMixed;
+    const bool full = m != 0 && u != kMixed;  // a uniform sender: one U record
     const uint64_t bu = __ballot(full);
-    if (bu) {
-      unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(&cnt[0], (unsigned long long)__popcll(bu));
-      base = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(base >> 32), 0) << 32) |
-             __builtin_amdgcn_readlane((uint32_t)base, 0);
-      if (full) su[base + __popcll(bu & lanemask_below(lane))] = ((unsigned long long)(uint32_t)b << 32) | (uint32_t)u;
+    unsigned long long uo = 0, mo = 0;
+    if constexpr (WRITE) {
+      const unsigned long long o = coff[c];
+      uo = o >> 32;
+      mo = o & 0xffffffffull;
+      if (full) su[uo + __popcll(bu & lanemask_below(lane))] = ((unsigned long long)(uint32_t)b << 32) | (uint32_t)u;
     }
-    for (uint64_t mb = __ballot(m != 0 && !full); mb; mb &= mb - 1) {  // mixed senders, one at a time
-      const int L = __builtin_ctzll(mb);
-      const int32_t bL = __builtin_amdgcn_readlane(b, L);
-      const uint64_t mL = rl64(m, L);
-      const int64_t vL = v0 + L;
-      const int32_t x = lab[vL * 64 + lane];
-      int k = 0;  // distinct labels over the changed views: count, reserve, write
-      for (uint64_t mm = mL; mm; k++) {
-        const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
-        mm &= ~__ballot(((mm >> lane) & 1) && x == val);
-      }
-      unsigned long long pos = 0;
-      if (lane == 0) pos = atomicAdd(&cnt[1], (unsigned long long)k);
-      pos = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(pos >> 32), 0) << 32) |
-            __builtin_amdgcn_readlane((uint32_t)pos, 0);
-      for (uint64_t mm = mL; mm; pos++) {
-        const int32_t val = __builtin_amdgcn_readlane(x, __builtin_ctzll(mm));
-        const uint64_t same = __ballot(((mm >> lane) & 1) && x == val);
-        if (lane == 0 && pos < (unsigned long long)mcap) sm[pos] = XRec{bL, val, same};
-        mm &= ~same;
+    unsigned long long nm = 0;
+    uint64_t mixed = __ballot(m != 0 && !full);
+    while (mixed) {  // mixed senders, kRowsInFlight rows at a time
+      int Ls[kRowsInFlight];
+      int32_t x[kRowsInFlight];
+      int k = 0;
+      for (; k < kRowsInFlight && mixed; k++, mixed &= mixed - 1) Ls[k] = __builtin_ctzll(mixed);
+      for (int i = 0; i < k; i++) x[i] = lab[(int64_t)__builtin_amdgcn_readlane(v, Ls[i]) * 64 + lane];
+      for (int i = 0; i < k; i++) {
+        const uint64_t mL = rl64(m, Ls[i]);
+        if constexpr (!WRITE) {
+          nm += (unsigned long long)distinct_labels(x[i], mL, lane);
+        } else {
+          const int32_t bL = (int32_t)(c * 64 + Ls[i]);
+          for (uint64_t mm = mL; mm; mo++) {
+            const int32_t val = __builtin_amdgcn_readlane(x[i], __builtin_ctzll(mm));
+            const uint64_t same = __ballot(((mm >> lane) & 1) && x[i] == val);
+            if (lane == 0 && mo < (unsigned long long)mcap) sm[mo] = XRec{bL, val, same};
+            mm &= ~same;
+          }
+        }
       }
     }
+    if constexpr (!WRITE)
+      if (lane == 0) ccnt[c] = ((unsigned long long)__popcll(bu) << 32) | nm;
   }
 }
 
@@ -200,18 +219,17 @@ __global__ __launch_bounds__(256) void k_xtab_fill(int64_t n, const int32_t* __r
 
 // counts exchange words, 4 per peer: [4q] U records, [4q+1] M records (the same broadcast list
 // for every peer; 0 for self), [4q+2] this partition changed a label in the step (the halting vote,
-// AnalysisTask.endStep :208-225), [4q+3] 0.  The counters are reset for the next pack.
-__global__ void k_xbc_counts(int np, int me, unsigned long long* __restrict__ cnt, const int32_t* __restrict__ stepflag,
-                             int64_t* __restrict__ xa) {
-  const int q = threadIdx.x;  // one wave: every lane reads the counters before lane 0 resets them
-  const unsigned long long nu = cnt[0], nm = cnt[1];
+// AnalysisTask.endStep :208-225), [4q+3] 0.  tot = the pack's scanned totals (U << 32 | M).
+__global__ void k_xbc_counts(int np, int me, const unsigned long long* __restrict__ tot,
+                             const int32_t* __restrict__ stepflag, int64_t* __restrict__ xa) {
+  const int q = threadIdx.x;
+  const unsigned long long t = tot ? *tot : 0ull;
   if (q < np) {
-    xa[4 * q] = q == me ? 0 : (int64_t)nu;
-    xa[4 * q + 1] = q == me ? 0 : (int64_t)nm;
+    xa[4 * q] = q == me ? 0 : (int64_t)(t >> 32);
+    xa[4 * q + 1] = q == me ? 0 : (int64_t)(t & 0xffffffffull);
     xa[4 * q + 2] = stepflag ? (stepflag[0] != 0) : 0;
     xa[4 * q + 3] = 0;
   }
-  if (q == 0) cnt[0] = cnt[1] = 0;
 }
 // component-count records (one region per peer): [2q] = records for q, [2q+1] = 0
 __global__ void k_xcounts(int np, int me, unsigned long long* __restrict__ scnt, int64_t* __restrict__ xa) {
@@ -625,13 +643,28 @@ void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32
                        int planes, const uint64_t* in, uint64_t* vm, int64_t vstride) {
   if (nx > 0) k_xvm_unpack<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, xq, xoff, planes, in, vm, vstride);
 }
+size_t xbc_scan_bytes(int64_t nb) {
+  const int n = (int)(((nb + 63) >> 6) + 1);
+  size_t tb = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr, n);
+  return tb;
+}
 void launch_xbc_pack(hipStream_t s, int64_t n_own, const XSend& X, const uint8_t* act, const uint64_t* chg_now,
-                     const uint64_t* vadj, const uint64_t* vm, const int32_t* lab, const int32_t* uw,
-                     unsigned long long* su, XRec* sm, int64_t mcap, unsigned long long* cnt, const int32_t* ccount,
-                     int dense_div, int step) {
-  if (X.nb > 0 && n_own > 0)
-    k_xbc_pack<<<xgrid(n_own, 256, 4096), 256, 0, s>>>(n_own, X.bidx, act, chg_now, vadj, vm, lab, uw, su, sm, mcap,
-                                                       cnt, ccount, dense_div, step);
+                     const uint64_t* vadj, const int32_t* lab, const int32_t* uw, unsigned long long* su, XRec* sm,
+                     int64_t mcap, unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp,
+                     size_t scan_bytes, const int32_t* ccount, int dense_div, int step, bool write_only) {
+  if (X.nb <= 0) return;
+  const int64_t nchunks = (X.nb + 63) >> 6;
+  const unsigned grid = xgrid(nchunks, 4, 4096);
+  if (!write_only) {
+    k_xbc_pack<false><<<grid, 256, 0, s>>>(n_own, X.nb, X.v, act, chg_now, vadj, lab, uw, su, sm, mcap, ccnt, coff,
+                                           ccount, dense_div, step);
+    // ccnt[nchunks] stays 0: coff[nchunks] = the totals
+    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ccnt, coff, (int)(nchunks + 1), s) != hipSuccess)
+      throw std::runtime_error("xbc pack: scan");
+  }
+  k_xbc_pack<true><<<grid, 256, 0, s>>>(n_own, X.nb, X.v, act, chg_now, vadj, lab, uw, su, sm, mcap, ccnt, coff, ccount,
+                                        dense_div, step);
 }
 XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, std::vector<void*>& T,
                   std::vector<void*>& L) {
@@ -673,8 +706,9 @@ void launch_xtab_fill(hipStream_t s, int64_t n, const int32_t* xr_v, const int32
                       const XTab& T, unsigned long long* err) {
   if (n > 0) k_xtab_fill<<<xgrid(n, 256), 256, 0, s>>>(n, xr_v, xr_q, tmp, T, err);
 }
-void launch_xbc_counts(hipStream_t s, int np, int me, unsigned long long* cnt, const int32_t* stepflag, int64_t* xa) {
-  k_xbc_counts<<<1, 64, 0, s>>>(np, me, cnt, stepflag, xa);
+void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* tot, const int32_t* stepflag,
+                       int64_t* xa) {
+  k_xbc_counts<<<1, 64, 0, s>>>(np, me, tot, stepflag, xa);
 }
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, int64_t* xa) {
   k_xcounts<<<1, 64, 0, s>>>(np, me, scnt, xa);
