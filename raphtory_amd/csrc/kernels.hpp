@@ -319,6 +319,10 @@ void launch_xbc_pack(hipStream_t s, int64_t n_own, const XSend& X, const uint8_t
 // counts words (4 per peer): U records, M records (tot = the pack's scanned totals), the halting vote
 void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* tot, const int32_t* stepflag,
                        int64_t* xa);
+// the per-view minimum member labels (mneg) folded into 64 words w / w stored back into shard 0
+// (partitioned final labels: the host all-reduces w with max in between)
+void launch_min_fold(hipStream_t s, const int32_t* mneg, unsigned long long* w);
+void launch_min_store(hipStream_t s, const unsigned long long* w, int32_t* mneg);
 // component-count records (2 words per peer); scnt reset
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, int64_t* xa);
 // a received broadcast: U and M receive regions per peer, with the records received (pre), the

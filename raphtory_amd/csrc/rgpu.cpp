@@ -135,6 +135,7 @@ struct XSlot {
   void* scan_tmp = nullptr;               // (xchg.hip launch_xbc_pack; sized with su)
   size_t scan_bytes = 0;
   unsigned long long* err = nullptr;      // received records outside the plan (xchg.hip bc_rec)
+  unsigned long long* mfin = nullptr;     // [64] the batch's minimum member labels, all-reduced
   int64_t* xab = nullptr;                 // [8P] counts words: sent (xa) | received (xb)
   int64_t* h_xab = nullptr;               // pinned copy
   uint64_t *vms = nullptr, *vmr = nullptr;  // ghost membership words (planes x list)
@@ -391,8 +392,11 @@ int dense_div(const rgpu_ctx* c) {
 
 // the batch's per-view minimum member labels (kernels.hpp kMinShards), behind the changed-vertex
 // counts; one partition only (a partition's minimum is not the graph's)
+// the batch's per-view minimum member labels (kernels.hip final_label), written by K2; partitioned,
+// part_min_labels makes them global before superstep 2
 int32_t* min_labels(const rgpu_ctx* c, const Slot& s) {
-  return (c->partitioned || !s.ccount) ? nullptr : s.ccount + (size_t)kMaxSteps * kCountShards;
+  (void)c;
+  return s.ccount ? s.ccount + (size_t)kMaxSteps * kCountShards : nullptr;
 }
 
 // changed bits of superstep r (with uniform words; RGPU_CHGBITS=0 turns them off)
@@ -759,6 +763,7 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
 
 void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r);
 void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc);
+void part_min_labels(rgpu_ctx* c, int si);
 void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int planes);
 
 // Batch b = hop block b / G (hops [hb*K, hb*K + K)) x window group b % G.  Hop-major runs
@@ -969,6 +974,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     s.r_launched = 1;  // superstep 1 ran inside the slot kernel
     if (c->partitioned) {
       s.r_final = 0;
+      if (rc.max_steps > 1) part_min_labels(c, si);
       if (rc.max_steps <= 1) part_finish_begin(c, si, rc);
       else part_post_step(c, si, rc, 1);
       return;
@@ -1308,6 +1314,7 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
     if (!xs.x) xs.x = X.xchg->fork(i + 1);  // collective: every partition forks the same slots
     if (!xs.err) {
       xs.err = dalloc<unsigned long long>(LG, 1);
+      xs.mfin = dalloc<unsigned long long>(LG, 64);
       xs.htot = dalloc<unsigned long long>(LG, kMaxParts);
       HIPCHK(hipMemset(xs.htot, 0, sizeof(unsigned long long) * kMaxParts));
       xs.xab = dalloc<int64_t>(LG, 8 * P);
@@ -1368,6 +1375,20 @@ void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int pl
   }
   xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
   timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_xvm_unpack(s.stream, X.nxr, X.xr_v, X.xr_q, X.xr_off_d, planes, xs.vmr, vm, vstride); });
+  HIPCHK(hipGetLastError());
+}
+
+// The final-label skip across partitions: K2 left this partition's per-view minimum member labels
+// in mneg; the minimum over every partition is the view's (a member holding it in all its views is
+// final everywhere).  Collective on the slot's channel, at the same point on every partition.
+void part_min_labels(rgpu_ctx* c, int si) {
+  Slot& s = c->slot[si];
+  XSlot& xs = c->pt.xs[si];
+  int32_t* mn = min_labels(c, s);
+  if (!mn) return;
+  launch_min_fold(s.stream, mn, xs.mfin);
+  xs.x->allreduce_u64(xs.mfin, 64, true, s.stream);
+  launch_min_store(s.stream, xs.mfin, mn);
   HIPCHK(hipGetLastError());
 }
 
@@ -1546,14 +1567,15 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (hv)
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[n % 3], s.stepcnt, n, s.hv,
-                          s.uw[r & 1], chg_bits(c, s, n).prev, s.ccount, dense_div(c));
+                          s.uw[r & 1], chg_bits(c, s, n).prev, s.ccount, dense_div(c), work_buf(c, s), s.vm,
+                          min_labels(c, s));
     });
   timed_launch(c, si, KID_STEP, 0.0, [&] {
     launch_cc_step(s.stream, n, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[r & 1], s.lab[n & 1], s.chg[r & 1],
                    s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
                    work_buf(c, s), s.stats + kLaneOff, hv ? s.hv.best : nullptr,
                    s.uw[r & 1], s.uw[n & 1], chg_bits(c, s, n), s.ccount,
-                   dense_div(c));
+                   dense_div(c), min_labels(c, s));
   }, n);
   part_post_step(c, si, rc, n);
 }
@@ -1850,7 +1872,7 @@ void reset_after_failure(rgpu_ctx* c) {
   for (Slot& s : c->slot)
     for (void* p : {(void*)s.hv.segcnt, (void*)s.hv.segor, (void*)s.hv.best, (void*)s.hv.pacc}) drop_alloc(LG, p);
   for (XSlot& xs : c->pt.xs)
-    for (void* p : {(void*)xs.err, (void*)xs.htot, (void*)xs.xab, (void*)xs.vms, (void*)xs.vmr})
+    for (void* p : {(void*)xs.err, (void*)xs.mfin, (void*)xs.htot, (void*)xs.xab, (void*)xs.vms, (void*)xs.vmr})
       drop_alloc(LG, p);
   release_slots(c);
   free_part_slots(c, true);

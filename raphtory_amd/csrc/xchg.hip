@@ -629,6 +629,22 @@ __global__ __launch_bounds__(256) void k_hist_recv(XPeers P, const unsigned long
   }
 }
 
+// ------------------------------------------------------------------ final labels across partitions
+// The batch's per-view minimum member label (kernels.hip final_label: INT32_MAX - label in kMinShards
+// shards, 0 = no member) over every partition: the shards folded into 64 words here, all-reduced
+// (max) by the host, stored back into shard 0 (the others hold local values, never larger).
+__global__ void k_min_fold(const int32_t* __restrict__ mneg, unsigned long long* __restrict__ w) {
+  const int j = threadIdx.x;
+  if (j >= 64) return;
+  int32_t x = 0;
+  for (int sh = 0; sh < kMinShards; sh++) x = max(x, mneg[sh * 64 + j]);
+  w[j] = (unsigned long long)(uint32_t)x;
+}
+__global__ void k_min_store(const unsigned long long* __restrict__ w, int32_t* __restrict__ mneg) {
+  const int j = threadIdx.x;
+  if (j < 64) mneg[j] = (int32_t)w[j];
+}
+
 // ------------------------------------------------------------------ launchers
 static unsigned xgrid(int64_t items, int per_block, unsigned cap = 8192) {
   int64_t g = (items + per_block - 1) / per_block;
@@ -710,6 +726,8 @@ void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* 
                        int64_t* xa) {
   k_xbc_counts<<<1, 64, 0, s>>>(np, me, tot, stepflag, xa);
 }
+void launch_min_fold(hipStream_t s, const int32_t* mneg, unsigned long long* w) { k_min_fold<<<1, 64, 0, s>>>(mneg, w); }
+void launch_min_store(hipStream_t s, const unsigned long long* w, int32_t* mneg) { k_min_store<<<1, 64, 0, s>>>(w, mneg); }
 void launch_xcounts(hipStream_t s, int np, int me, unsigned long long* scnt, int64_t* xa) {
   k_xcounts<<<1, 64, 0, s>>>(np, me, scnt, xa);
 }
