@@ -521,16 +521,13 @@ struct NoWork {
 // is clear).
 
 // A kept slot's view bits before the own mask: the edge's window bits (inline for simple slots)
-// and the neighbour's membership.  With ebp.simple_ends the simple slots skip the neighbour's mask:
-// their bits already imply it (BatchParams::simple_ends).
+// and the neighbour's membership.  With ebp.simple_ends the nodeath slots skip the neighbour's
+// mask: their bits already imply it (BatchParams::simple_ends).
 __device__ __forceinline__ uint64_t slot_bits(const HopLDS& L, const BatchParams& ebp, int64_t tsw,
                                               const uint64_t* __restrict__ em, int64_t e,
                                               const uint64_t* __restrict__ vm, int32_t nb) {
-  if (ts_simple(tsw)) {
-    const uint64_t b = simple_bits(L, ebp.sorted, ts_time(tsw));
-    return ebp.simple_ends ? b : b & vm[nb];
-  }
-  return em[e] & vm[nb];
+  const uint64_t b = ts_simple(tsw) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[e];
+  return (ebp.simple_ends && ts_nodeath(tsw)) ? b : b & vm[nb];
 }
 
 // PROF = false: the work counters compile away (launch_cc_slots: work == null).  IEM: inline edge

@@ -38,7 +38,7 @@ struct BatchParams {
   int64_t thr_v[kViews];  // vertex-set window of window index w: min(w_0..w_w)  (shrinkWindow)
   int64_t thr_e[kViews];  // edge window of window index w: w_w (viewAtWithWindow(t, setWindow))
   int64_t jump;           // > 0: hop[k] = hop[0] + k * jump for every k < K (K1's arithmetic hop search)
-  // every view's vertex window equals its edge window (descending window lists): then a simple
+  // every view's vertex window equals its edge window (descending window lists): then a nodeath
   // slot's window bits imply both endpoints' membership (an EADD is a `+` point of both endpoints,
   // neither of which ever dies), so K2 / the ghost marking skip the neighbour's mask read for it
   int simple_ends;
@@ -69,14 +69,17 @@ struct DevGraph {
   // time-ordered static slots (tslots.hip; null: CSR order): per vertex newest last-add first
   const int32_t* ts_e = nullptr;    // [ne + n_in] edge of the slot
   const int32_t* ts_nb = nullptr;   // [ne + n_in] neighbour across it
-  const int64_t* ts_t = nullptr;    // [ne + n_in] 2 * the edge's last add time + simple (tslots.hip)
+  const int64_t* ts_t = nullptr;    // [ne + n_in] 4 * the edge's last add time + 2 nodeath + simple (tslots.hip)
   const int32_t* ts_g = nullptr;    // [ne + n_in] grank[ts_nb] (with grank): K2 streams the neighbour's
                                     // label instead of a random grank read per slot
 };
-// a ts_t word: the edge's last add time, and whether the slot is simple (one add point, no
-// endpoint deaths: K2 derives its window bits from the time alone)
-__host__ __device__ inline int64_t ts_time(int64_t x) { return x >> 1; }
+// a ts_t word: the edge's last add time; whether neither endpoint ever died (nodeath: the edge's
+// window bits then imply both endpoints' membership when the vertex and edge windows agree,
+// BatchParams::simple_ends); whether the slot is simple (one add point and nodeath: K2 derives its
+// window bits from the time alone)
+__host__ __device__ inline int64_t ts_time(int64_t x) { return x >> 2; }
 __host__ __device__ inline bool ts_simple(int64_t x) { return x & 1; }
+__host__ __device__ inline bool ts_nodeath(int64_t x) { return x & 2; }
 // Builds ts_e / ts_nb / ts_t (device arrays of ne + n_in entries) for g; temporaries are
 // appended to `temps` (free them after the stream is synchronised).  False: not built (more
 // than 2^31 slots), the graph keeps CSR order.

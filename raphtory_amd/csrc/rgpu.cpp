@@ -158,6 +158,7 @@ struct Part {
   XTab tab;                                   // receive tables of the broadcast records
   int64_t nbq[kMaxParts] = {};                // boundary vertices of every partition
   bool tab_ready = false;
+  bool no_deaths = false;                     // no partition's graph holds a vertex death (ensure_tab)
   double *sbuf_f = nullptr, *rbuf_f = nullptr;  // PR contribution rows
   bool pr_ready = false;
   XSlot xs[4];                                // per batch slot (kMaxSlots)
@@ -764,7 +765,8 @@ void finish_batch(rgpu_ctx* c, int si, const RunCfg& rc) {
 void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r);
 void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc);
 void part_min_labels(rgpu_ctx* c, int si);
-void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int planes);
+void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int planes, bool free);
+bool ghost_vm_free(const rgpu_ctx* c, const RunCfg& rc);
 
 // Batch b = hop block b / G (hops [hb*K, hb*K + K)) x window group b % G.  Hop-major runs
 // (G = 1): the batch is the block, all windows in one label row, K1 per batch into the slot's
@@ -880,7 +882,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     timed_launch(c, si, KID_EMASK, bytes_emask(c, 1, skip_simple), [&] {
       launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0, ends ? s.vm : nullptr, 0, skip_simple);
     });
-    if (c->partitioned) part_vm_exchange(c, si, s.vm, 0, 1);
+    if (c->partitioned) part_vm_exchange(c, si, s.vm, 0, 1, ghost_vm_free(c, rc));
   } else {
     MaskSet& M = c->mset[hb % kMaskSets];
     if (grp == 0) {
@@ -893,7 +895,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
         launch_edge_mask(s.stream, g, bp, M.em, true, c->d_ecnt, (int64_t)h0, ends ? M.vm : nullptr, g.nv + kPad,
                          skip_simple);
       });
-      if (c->partitioned) part_vm_exchange(c, si, M.vm, g.nv + kPad, rc.G);
+      if (c->partitioned) part_vm_exchange(c, si, M.vm, g.nv + kPad, rc.G, ghost_vm_free(c, rc));
       HIPCHK(hipEventRecord(M.k1, s.stream));
       M.pending = rc.G;
     } else {
@@ -1262,15 +1264,18 @@ void ensure_tab(rgpu_ctx* c) {
   auto& LG = c->graph_allocs;
   std::vector<void*> T;
   try {
+    // every partition's boundary count, and whether its graph holds a vertex death (2 nb + deaths)
     int64_t* d = dalloc<int64_t>(T, 2 * P);
-    std::vector<int64_t> h(2 * P, X.xsend.nb);
+    std::vector<int64_t> h(2 * P, 2 * X.xsend.nb + (c->st.deaths > 0 ? 1 : 0));
     HIPCHK(hipMemcpy(d, h.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice));
     X.xchg->alltoall_i64(d, d + P, 1, st);
     HIPCHK(hipMemcpyAsync(h.data(), d, sizeof(int64_t) * 2 * P, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     int64_t o = 0;
+    X.no_deaths = c->st.deaths == 0;
     for (int q = 0; q < P; q++) {
-      X.nbq[q] = q == me ? 0 : h[P + q];
+      if (q != me && (h[P + q] & 1)) X.no_deaths = false;
+      X.nbq[q] = q == me ? 0 : h[P + q] >> 1;
       X.tab.toff[q] = o;
       o += X.nbq[q];
     }
@@ -1356,12 +1361,30 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
   }
 }
 
+// CC runs whose views all have equal vertex and edge windows, on graphs where no partition holds a
+// vertex death, read no ghost membership: every slot is nodeath, and its window bits imply both
+// endpoints' membership (BatchParams::simple_ends).  The ghost rows are then set to every view
+// (readers AND them with bits that imply them) and the exchange is skipped.  The same decision on
+// every partition: the windows are the query's, no_deaths is agreed in ensure_tab.
+bool ghost_vm_free(const rgpu_ctx* c, const RunCfg& rc) {
+  if (!c->partitioned || rc.algo != RGPU_ALGO_CC || !c->pt.no_deaths || !c->g.ts_t) return false;
+  for (int w = 0; w < rc.W; w++)
+    if (rc.thr_v[w] != rc.thr_e[w]) return false;
+  return true;
+}
+
 // the boundary vertices' K1 membership words to the peers, theirs into our ghost rows
-void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int planes) {
+void part_vm_exchange(rgpu_ctx* c, int si, uint64_t* vm, int64_t vstride, int planes, bool free) {
   Slot& s = c->slot[si];
   Part& X = c->pt;
   XSlot& xs = X.xs[si];
   const int P = c->nparts, me = c->part;
+  if (free) {
+    const int64_t no = c->pk.n_own, ng = c->g.nv - no;
+    for (int p = 0; p < planes && ng > 0; p++)
+      HIPCHK(hipMemsetAsync(vm + (size_t)p * vstride + no, 0xff, sizeof(uint64_t) * (size_t)ng, s.stream));
+    return;
+  }
   timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_xvm_pack(s.stream, X.nxs, X.xs_v, X.xs_q, X.xs_off_d, planes, vm, vstride, xs.vms); });
   HIPCHK(hipGetLastError());
   std::vector<void*> sp(P), rp(P);
@@ -1770,7 +1793,7 @@ int run_partitioned_dp(rgpu_ctx* c, RunCfg& rc) {
                  [&] { launch_vertex_mask(s.stream, go, bp, s.vm, 0, false, clr); });
     timed_launch(c, 0, KID_EMASK, bytes_emask(c, 1, false),
                  [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0); });
-    part_vm_exchange(c, 0, s.vm, 0, 1);
+    part_vm_exchange(c, 0, s.vm, 0, 1, false);
     timed_launch(c, 0, KID_DEGREE, go.nv * (8.0 + 32.0 + 512.0) + (double)(g.ne + g.n_in) * 12.0, [&] {
       launch_degree(s.stream, go, s.vm, s.em, s.outdeg, s.indeg, s.stats, rc.algo == RGPU_ALGO_DEGREE ? &s.top : nullptr);
     });

@@ -10,12 +10,13 @@
 //
 //   ts_e[p]  edge of static slot p       (p in [adj_off[v], adj_off[v+1]), newest first)
 //   ts_nb[p] the neighbour across it
-//   ts_t[p]  2 * (the edge's last add time) + simple   (INT64_MIN: never added; ts_time / ts_simple
-//            in kernels.hpp)
+//   ts_t[p]  4 * (the edge's last add time) + 2 nodeath + simple   (INT64_MIN: never added;
+//            ts_time / ts_nodeath / ts_simple in kernels.hpp)
 //
-// simple = the edge's history is one add point and neither endpoint ever died: its aliveness in
-// any view (t, w) is then tf <= t <= tf + w with tf = ts_time, so K2 computes the slot's window
-// bits from the word it already streams (kernels.hip slot_bits) instead of reading em[e].
+// nodeath = neither endpoint ever died; simple = nodeath and the edge's history is one add point:
+// its aliveness in any view (t, w) is then tf <= t <= tf + w with tf = ts_time, so K2 computes the
+// slot's window bits from the word it already streams (kernels.hip slot_bits) instead of reading
+// em[e].  A nodeath slot's bits imply both endpoints' membership (BatchParams::simple_ends).
 //
 // The order only changes which kept slot lands where inside the vertex's kept range: CC is a
 // minimum over the kept slots, so results are unchanged.
@@ -48,14 +49,12 @@ __global__ __launch_bounds__(256) void k_slot_keys(int64_t nv, const int64_t* __
       const int64_t h0 = eoff[e], h1 = eoff[e + 1];
       for (int64_t i = h1 - 1; i >= h0; i--)
         if (ekey[i] & 1) { t = ekey[i] >> 1; break; }
-      bool simple = h1 - h0 == 1 && t != INT64_MIN;
-      if (simple) {
-        const int32_t a = esrc[e], b = edst[e];
-        const bool da = dbits ? ((dbits[a >> 6] >> (a & 63)) & 1) : doff[a + 1] > doff[a];
-        const bool db = dbits ? ((dbits[b >> 6] >> (b & 63)) & 1) : doff[b + 1] > doff[b];
-        simple = !da && !db;
-      }
-      key[base + j] = t == INT64_MIN ? INT64_MIN : 2 * t + (simple ? 1 : 0);
+      const int32_t a = esrc[e], b = edst[e];
+      const bool da = dbits ? ((dbits[a >> 6] >> (a & 63)) & 1) : doff[a + 1] > doff[a];
+      const bool db = dbits ? ((dbits[b >> 6] >> (b & 63)) & 1) : doff[b + 1] > doff[b];
+      const bool nodeath = !da && !db && t != INT64_MIN;
+      const bool simple = nodeath && h1 - h0 == 1;
+      key[base + j] = t == INT64_MIN ? INT64_MIN : 4 * t + (nodeath ? 2 : 0) + (simple ? 1 : 0);
       val[base + j] = e;
     }
   }

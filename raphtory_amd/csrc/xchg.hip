@@ -350,10 +350,9 @@ __device__ __forceinline__ void mark_slot(int64_t p, int32_t g, uint64_t ch, con
   if (ts_time(tsw) < tcut) return;
   const int32_t nb = ts_nb[p];
   if (nb == g) return;
-  // (a simple slot with ebp.simple_ends: its bits imply nb's membership, BatchParams::simple_ends)
-  const bool simple = iem && ts_simple(tsw);
-  const uint64_t bits = simple ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[ts_e[p]];
-  if (bits & ch & ((simple && ebp.simple_ends) ? ~0ull : vm[nb])) act_next[nb] = 1;
+  // (a nodeath slot with ebp.simple_ends: its bits imply nb's membership, BatchParams::simple_ends)
+  const uint64_t bits = (iem && ts_simple(tsw)) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[ts_e[p]];
+  if (bits & ch & ((iem && ebp.simple_ends && ts_nodeath(tsw)) ? ~0ull : vm[nb])) act_next[nb] = 1;
 }
 template <bool TS>
 __global__ __launch_bounds__(256) void k_xbc_mark(XBcIn I, const uint64_t* __restrict__ chg,
