@@ -360,8 +360,9 @@ struct OwnIdx {
 // peer q.  uw may be null (rows only).
 void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,
-                       unsigned int* iso, unsigned long long* gcnt, unsigned long long* hsbuf);
-void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const OwnIdx& I, int32_t* counts);
+                       unsigned int* iso, unsigned long long* gcnt, XRec* hsbuf);
+// records {label, count, views} received: counted at the owned label's rows
+void launch_hist_recv(hipStream_t s, const XPeers& P, const XRec* rbuf, const OwnIdx& I, int32_t* counts);
 // PageRank contribution rows of a list (partitioned PageRank): gather into / scatter out of a
 // contiguous buffer
 void launch_xgather_f64(hipStream_t s, int64_t n, const int32_t* xv, const double* rows, double* buf);

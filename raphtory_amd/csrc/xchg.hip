@@ -479,24 +479,24 @@ __device__ __forceinline__ int64_t label_row(const OwnIdx& I, int32_t x) {
   const int64_t k = owned_rank(I, x);
   return k < 0 ? -1 : (I.pos ? (int64_t)I.pos[k] : k);
 }
-__device__ __forceinline__ unsigned long long count_rec(int32_t x, int j, unsigned c) {
-  return (unsigned long long)(uint32_t)x | ((unsigned long long)j << 31) | ((unsigned long long)c << 37);
-}
-// A wave's outgoing count records are staged in LDS, kStage per peer, and reserved in the send
-// buffer with one atomicAdd per flush: one global atomic per (group of records, peer) serialised
-// on the 8 gcnt words (~10 ns each at the memory side, DESIGN.md §4 lesson 1) and made the
-// partitioned count pass ~20x the one-partition one.  The flush order is fixed per wave, so a
-// REMOTE_ONLY re-run emits the same records per peer (in another order at most).
-constexpr int kStage = 64;
+// Count records are XRec {label, count, views}: `count` members carry `label` in every view of
+// `views`.  A uniform member group (the same label over the same views, kernels.hip k_cc_count)
+// whose label is remote is ONE record for all its views instead of one 8-B record per view, so a
+// small component that lives through many hops of a long window costs one record per group.
+// A wave's outgoing records are staged in LDS, kStage per peer, and reserved in the send buffer
+// with one atomicAdd per flush: one global atomic per (group of records, peer) serialised on the
+// gcnt words (~10 ns each at the memory side, DESIGN.md §4 lesson 1).  The flush order is fixed per
+// wave, so a REMOTE_ONLY re-run emits the same records per peer (in another order at most).
+constexpr int kStage = 32;
 struct CountStage {
-  unsigned long long (*rec)[kStage];  // [peer][kStage], wave-private LDS
-  int n;                              // lane q: records staged for peer q (a register, not LDS: the
-                                      // lanes read it right after another lane's update)
+  XRec (*rec)[kStage];  // [peer][kStage], wave-private LDS
+  int n;                // lane q: records staged for peer q (a register, not LDS: the lanes read it
+                        // right after another lane's update)
 };
 // wave-uniform: reserve peer q's staged records in the send buffer and write them out
 __device__ __forceinline__ void stage_flush(CountStage& st, int q, const XPeers& P,
-                                            unsigned long long* __restrict__ gcnt,
-                                            unsigned long long* __restrict__ hsbuf, int lane) {
+                                            unsigned long long* __restrict__ gcnt, XRec* __restrict__ hsbuf,
+                                            int lane) {
   const int n = __builtin_amdgcn_readlane(st.n, q);
   if (n == 0) return;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the other lanes' LDS record stores
@@ -508,25 +508,37 @@ __device__ __forceinline__ void stage_flush(CountStage& st, int q, const XPeers&
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // read before the slots are reused
   if (lane == q) st.n = 0;
 }
-// wave-wide: the lanes with `on` send (x, j, c) (remote labels, staged) or add it (owned labels)
+// wave-uniform (x, views, c): added at the count row when x is owned here, else one staged record
 template <bool REMOTE_ONLY>
-__device__ __forceinline__ void count_direct(bool on, int32_t x, int j, unsigned c, const XPeers& P, const OwnIdx& I,
-                                             int32_t* __restrict__ counts, unsigned long long* __restrict__ gcnt,
-                                             unsigned long long* __restrict__ hsbuf, int lane, CountStage& st) {
-  const int q = on ? owner_of(x, P.np) : -1;
-  if (!REMOTE_ONLY && q == P.me) {
-    const int64_t r = label_row(I, x);  // always found: a label is a member's id
-    if (r >= 0) atomicAdd(&counts[r * 64 + j], (int32_t)c);
+__device__ __forceinline__ void emit_count(int32_t x, uint64_t views, unsigned c, const XPeers& P, const OwnIdx& I,
+                                           int32_t* __restrict__ counts, unsigned long long* __restrict__ gcnt,
+                                           XRec* __restrict__ hsbuf, int lane, CountStage& st) {
+  if (views == 0 || c == 0) return;
+  const int q = owner_of(x, P.np);
+  if (q == P.me) {
+    if (!REMOTE_ONLY) {
+      const int64_t r = label_row(I, x);  // always found: a label is a member's id
+      if (r >= 0 && ((views >> lane) & 1)) atomicAdd(&counts[r * 64 + lane], (int32_t)c);
+    }
+    return;
   }
-  for (uint64_t todo = __ballot(q >= 0 && q != P.me); todo;) {
-    const int qL = __builtin_amdgcn_readlane(q, __builtin_ctzll(todo));
-    const uint64_t mine = __ballot(q == qL);
-    todo &= ~mine;
-    const int n = __popcll(mine);
-    if (__builtin_amdgcn_readlane(st.n, qL) + n > kStage) stage_flush(st, qL, P, gcnt, hsbuf, lane);
-    const int c0 = __builtin_amdgcn_readlane(st.n, qL);
-    if (q == qL) st.rec[qL][c0 + __popcll(mine & (lane ? (~0ull >> (64 - lane)) : 0ull))] = count_rec(x, j, c);
-    if (lane == qL) st.n = c0 + n;
+  if (__builtin_amdgcn_readlane(st.n, q) + 1 > kStage) stage_flush(st, q, P, gcnt, hsbuf, lane);
+  const int c0 = __builtin_amdgcn_readlane(st.n, q);
+  if (lane == 0) st.rec[q][c0] = XRec{x, (int32_t)c, views};
+  if (lane == q) st.n = c0 + 1;
+}
+// per lane (lane = view) label l with count c on the lanes of `on`: grouped by (label, count)
+template <bool REMOTE_ONLY>
+__device__ __forceinline__ void emit_lanes(bool on, int32_t l, unsigned c, const XPeers& P, const OwnIdx& I,
+                                           int32_t* __restrict__ counts, unsigned long long* __restrict__ gcnt,
+                                           XRec* __restrict__ hsbuf, int lane, CountStage& st) {
+  for (uint64_t rest = __ballot(on); rest;) {
+    const int L = __builtin_ctzll(rest);
+    const int32_t xL = __builtin_amdgcn_readlane(l, L);
+    const unsigned cL = (unsigned)__builtin_amdgcn_readlane((int)c, L);
+    const uint64_t same = __ballot(((rest >> lane) & 1) && l == xL && c == cL);
+    rest &= ~same;
+    emit_count<REMOTE_ONLY>(xL, same, cL, P, I, counts, gcnt, hsbuf, lane, st);
   }
 }
 template <bool REMOTE_ONLY>
@@ -534,8 +546,7 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
                                                     const uint64_t* __restrict__ vadj, const int32_t* __restrict__ uw,
                                                     const int32_t* __restrict__ lab, int32_t* __restrict__ counts,
                                                     unsigned int* __restrict__ iso_g,
-                                                    unsigned long long* __restrict__ gcnt,
-                                                    unsigned long long* __restrict__ hsbuf) {
+                                                    unsigned long long* __restrict__ gcnt, XRec* __restrict__ hsbuf) {
   // The cache is private to a wave (16 rows each): a wave's operations run in a fixed order, so
   // the records it emits are the same on every run — the REMOTE_ONLY pass after a send-buffer
   // overflow must emit exactly the records the counts exchange announced.
@@ -543,7 +554,7 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
   __shared__ unsigned int iso[64];
   __shared__ int32_t ckey_s[4][kRows];
   __shared__ unsigned int crow_s[4][kRows][64];
-  __shared__ unsigned long long srec_s[4][kMaxParts][kStage];
+  __shared__ XRec srec_s[4][kMaxParts][kStage];
   const int lane = lane_of(), wib = threadIdx.x >> 6;
   int32_t* ckey = ckey_s[wib];
   unsigned int (*crow)[64] = crow_s[wib];
@@ -589,7 +600,7 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
       const bool on = (mL >> lane) & 1;
       const unsigned c = (unsigned)__popcll(same);
       const bool hit = on && cached(xL, lane, c);
-      count_direct<REMOTE_ONLY>(on && !hit, xL, lane, c, P, I, counts, gcnt, hsbuf, lane, st);
+      emit_count<REMOTE_ONLY>(xL, __ballot(on && !hit), c, P, I, counts, gcnt, hsbuf, lane, st);
     }
     for (uint64_t mixed = __ballot(m != 0 && x == kMixed); mixed; mixed &= mixed - 1) {  // rows
       const int L = __builtin_ctzll(mixed);
@@ -597,14 +608,21 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
       const bool on = (mL >> lane) & 1;
       const int32_t l = on ? lab[(b0 + L) * 64 + lane] : 0;
       const bool hit = on && cached(l, lane, 1u);
-      count_direct<REMOTE_ONLY>(on && !hit, l, lane, 1u, P, I, counts, gcnt, hsbuf, lane, st);
+      emit_lanes<REMOTE_ONLY>(on && !hit, l, 1u, P, I, counts, gcnt, hsbuf, lane, st);
     }
   }
   for (int h = 0; h < kRows; h++) {  // the wave's cache: owned labels at their rows, the rest as records
     const int32_t k = ckey[h];
     if (k == -1) continue;
     const unsigned int c = crow[h][lane];
-    count_direct<REMOTE_ONLY>(c != 0, k, lane, c, P, I, counts, gcnt, hsbuf, lane, st);
+    if (owner_of(k, P.np) == P.me) {
+      if (!REMOTE_ONLY) {
+        const int64_t r = label_row(I, k);
+        if (r >= 0 && c) atomicAdd(&counts[r * 64 + lane], (int32_t)c);
+      }
+      continue;
+    }
+    emit_lanes<REMOTE_ONLY>(c != 0, k, c, P, I, counts, gcnt, hsbuf, lane, st);
   }
   for (int q = 0; q < P.np; q++) stage_flush(st, q, P, gcnt, hsbuf, lane);
   if (!REMOTE_ONLY && iso_acc) atomicAdd(&iso[lane], iso_acc);
@@ -613,18 +631,30 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
     atomicAdd(&iso_g[(blockIdx.x & 63) * 64 + threadIdx.x], iso[threadIdx.x]);
 }
 
-// records received from the other partitions: count at the owned label vertex's row
-__global__ __launch_bounds__(256) void k_hist_recv(XPeers P, const unsigned long long* __restrict__ rbuf, OwnIdx I,
+// records received from the other partitions: counted at the owned label vertex's row (lane =
+// record for the lookups, then lane = view per record)
+__global__ __launch_bounds__(256) void k_hist_recv(XPeers P, const XRec* __restrict__ rbuf, OwnIdx I,
                                                    int32_t* __restrict__ counts) {
   const int64_t n = P.pre[P.np];
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int q = peer_of(P, i);
-    const unsigned long long r = rbuf[P.base[q] + i - P.pre[q]];
-    const int32_t L = (int32_t)(r & 0x7fffffffull);
-    const int j = (int)((r >> 31) & 63);
-    const int32_t c = (int32_t)(r >> 37);
-    const int64_t row = label_row(I, L);
-    if (row >= 0) atomicAdd(&counts[row * 64 + j], c);
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i0 = wave * 64; i0 < n; i0 += nwaves * 64) {
+    const int64_t i = i0 + lane;
+    int64_t row = -1;
+    XRec r{0, 0, 0};
+    if (i < n) {
+      const int q = peer_of(P, i);
+      r = rbuf[P.base[q] + i - P.pre[q]];
+      row = label_row(I, r.e);
+    }
+    for (uint64_t t = __ballot(row >= 0); t; t &= t - 1) {
+      const int L = __builtin_ctzll(t);
+      const int64_t rowL = (int64_t)rl64((uint64_t)row, L);
+      const uint64_t mL = rl64(r.mask, L);
+      const int32_t cL = __builtin_amdgcn_readlane(r.val, L);
+      if ((mL >> lane) & 1) atomicAdd(&counts[rowL * 64 + lane], cL);
+    }
   }
 }
 
@@ -752,7 +782,7 @@ void launch_xbc_mark(hipStream_t s, const XBcIn& I, const uint64_t* chg, const D
 }
 void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,
-                       unsigned int* iso, unsigned long long* gcnt, unsigned long long* hsbuf) {
+                       unsigned int* iso, unsigned long long* gcnt, XRec* hsbuf) {
   const uint64_t vmask = nviews >= 64 ? ~0ull : ((1ull << nviews) - 1);
   const unsigned grid = xgrid(I.n_own, 256, 2048);
   if (remote_only)
@@ -760,7 +790,7 @@ void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const O
   else
     k_part_count<false><<<grid, 256, 0, s>>>(P, I, vmask, vm, vadj, uw, lab, counts, iso, gcnt, hsbuf);
 }
-void launch_hist_recv(hipStream_t s, const XPeers& P, const unsigned long long* rbuf, const OwnIdx& I, int32_t* counts) {
+void launch_hist_recv(hipStream_t s, const XPeers& P, const XRec* rbuf, const OwnIdx& I, int32_t* counts) {
   if (P.pre[P.np] > 0) k_hist_recv<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, I, counts);
 }
 
