@@ -945,10 +945,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   }
   if (rc.algo == RGPU_ALGO_CC) {
     if (c->partitioned && g.nv > c->pk.n_own)  // ghosts: quiet until a record arrives (kGhostQuiet)
-      for (int p = 0; p < 2; p++) {
+      for (int p = 0; p < 2; p++)
         HIPCHK(hipMemsetAsync(s.uw[p] + c->pk.n_own, 0x7f, sizeof(int32_t) * (g.nv - c->pk.n_own), s.stream));
-        HIPCHK(hipMemsetAsync(s.chg[p] + c->pk.n_own, 0, sizeof(uint64_t) * (g.nv - c->pk.n_own), s.stream));
-      }
     // bytes: per vertex vm + 4 offsets + label rows 0/1 + cnt/vadj/chg; per static slot index,
     // em, vm[nb]; kept slots written (12 B each, counted in harvest)
     const double b2 = 8.0 * g.nv;  // the view-mask scan; the rest from the work counters (harvest)
@@ -1520,17 +1518,18 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     return;
   }
   const int par = r & 1;
-  // (No per-step clear of the ghosts that records of step r-2 set: a ghost word or row lane left
-  // from an earlier superstep of the batch carries a label its vertex has since lowered or kept,
-  // and labels only fall, so folding it changes nothing — at most one extra fold.  The batch
-  // starts with every ghost word quiet and every ghost change word clear.)
+  // ghosts whose words records of step r-2 set (their records are still in ru / rm [par]).  The
+  // clear is needed: a U record sets the ghost's change word to every view, and a later M record
+  // ORs into it, so without the clear its readers would gather row lanes no record of this batch
+  // wrote; hub marking reads a ghost hub's change word as this step's news too.
+  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xbc_clear(s.stream, bc_in(c, xs, par), s.chg[par], s.uw[par]); });
   bool rover = false;
   for (int q = 0; q < P; q++) rover |= recv_m[q] > xs.rmcap[q];
   if (rover) {  // a larger M layout for both parities; the other parity's records of step r-1 are
-                // read once more (the batch-end clear, part_finish_end), so they move over
+                // read once more (their clear, two supersteps from now), so they move over
     int64_t old_cap[kMaxParts];
     std::copy(xs.rmcap, xs.rmcap + kMaxParts, old_cap);
-    grow_regions(&xs.rm[par], xs.rmcap, recv_m, P, s.stream);  // (syncs the stream)
+    grow_regions(&xs.rm[par], xs.rmcap, recv_m, P, s.stream);  // syncs: the clear above has run
     XRec* nb = alloc_regions<XRec>(xs.rmcap, P);
     int64_t o_old = 0, o_new = 0;
     for (int q = 0; q < P; q++) {

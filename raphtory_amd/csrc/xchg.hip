@@ -48,6 +48,7 @@ __device__ __forceinline__ int peer_of(const XPeers& P, int64_t i) {
 }
 // rank of owned vertex `id`, or -1 (bucket index: about one probe)
 __device__ __forceinline__ int64_t owned_rank(const OwnIdx& I, int64_t id) {
+  if (id < 0 || id >= ((int64_t)1 << 31)) return -1;  // (the buckets cover the id range [0, 2^31))
   const int64_t b = id >> I.shift;
   for (int64_t i = I.boff[b], e = I.boff[b + 1]; i < e; i++)
     if (I.vid[i] == id) return i;
