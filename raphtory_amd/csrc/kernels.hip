@@ -1692,7 +1692,8 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
                                                     const int32_t* __restrict__ ts_nb,
                                                     const int64_t* __restrict__ ts_t, int64_t tcut,
                                                     const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
-                                                    unsigned long long* __restrict__ work) {
+                                                    unsigned long long* __restrict__ work,
+                                                    const int32_t* __restrict__ uw_ghost) {
   if (stepflag[step] == 0) return;
   if (dense_rule(ccount, step, nv_all, dense_div)) return;  // dense step: the next one visits every member
   if (dense_rule(ccount, step - 1, nv_all, dense_div)) act_cur = nullptr;  // this step visited every member
@@ -1703,7 +1704,9 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
   for (int64_t sg = wave; sg < nseg; sg += nwaves) {
     const int32_t v = seg_v[sg];
     if (act_cur && v < n_own && !act_cur[v]) continue;  // a ghost's word is current (set by its records)
-    const uint64_t ch = chg_now[v];
+    // a ghost hub's U record sets its uniform word (changed: every view) and no change word
+    const int32_t wg = (uw_ghost && v >= n_own) ? uw_ghost[v] : kMixed;
+    const uint64_t ch = (wg != kMixed && wg < 0) ? ~0ull : chg_now[v];
     if (!ch) continue;
     const int32_t n = segcnt[sg];
     const int64_t base = seg_lo[sg];
@@ -2462,13 +2465,14 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
                        const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm, const uint64_t* em,
-                       int64_t tcut, const int32_t* ccount, int dense_div, unsigned long long* work) {
+                       int64_t tcut, const int32_t* ccount, int dense_div, unsigned long long* work,
+                       const int32_t* uw_ghost) {
   if (g.n_seg <= 0) return;
   k_heavy_mark<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
                                                            chg_now, act_cur, act_next, stepflag, g.n_own, g.seg_n,
                                                            g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst,
                                                            vm, em, g.ts_e, g.ts_nb, g.ts_t, tcut, ccount, dense_div,
-                                                           g.n_own, work);
+                                                           g.n_own, work, uw_ghost);
 }
 int64_t deg_top_waves(int64_t nv) { return (int64_t)grid_for(nv, 4, 2048) * 4; }
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,

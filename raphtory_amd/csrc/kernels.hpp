@@ -179,7 +179,7 @@ void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, co
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
                        const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm = nullptr,
                        const uint64_t* em = nullptr, int64_t tcut = INT64_MIN, const int32_t* ccount = nullptr,
-                       int dense_div = 0, unsigned long long* work = nullptr);
+                       int dense_div = 0, unsigned long long* work = nullptr, const int32_t* uw_ghost = nullptr);
 // uniform label words (kernels.hip, kMixed): rows of the uniform vertices written into lab
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab);
 // component counts from the uniform words (one partition): counts = zeroed [nv][64] rows, kept
@@ -339,12 +339,13 @@ struct XBcIn {
   unsigned long long* err = nullptr;
 };
 void launch_xbc_clear(hipStream_t s, const XBcIn& I, uint64_t* chg, int32_t* uw);
-void launch_xbc_unpack(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg, int32_t* uw, uint64_t* cb = nullptr);
-// tcut / ebp: the batch's slot cut and (inline edge bits; null: em for every slot) its edge windows;
-// ccount / dense_div / step: nothing is marked when superstep `step` is dense
-void launch_xbc_mark(hipStream_t s, const XBcIn& I, const uint64_t* chg, const DevGraph& g, const uint64_t* vm,
-                     const uint64_t* em, uint8_t* act_next, int64_t tcut, const BatchParams* ebp, const int32_t* ccount,
-                     int dense_div, int step);
+// a superstep's received records applied to the ghost words / rows / change words (cb: changed
+// bits) and the ghosts' owned neighbours marked in act_next.  tcut / ebp: the batch's slot cut and
+// (inline edge bits; null: em for every slot) its edge windows; ccount / dense_div / step: nothing
+// is marked when superstep `step` is dense
+void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg, int32_t* uw, uint64_t* cb,
+                      const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next, int64_t tcut,
+                      const BatchParams* ebp, const int32_t* ccount, int dense_div, int step);
 // owned id -> owned rank: ids ascend with rank; bucket b = id >> shift covers ranks
 // [boff[b], boff[b+1]) (about one id per bucket)
 struct OwnIdx {

@@ -1518,10 +1518,10 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     return;
   }
   const int par = r & 1;
-  // ghosts whose words records of step r-2 set (their records are still in ru / rm [par]).  The
-  // clear is needed: a U record sets the ghost's change word to every view, and a later M record
-  // ORs into it, so without the clear its readers would gather row lanes no record of this batch
-  // wrote; hub marking reads a ghost hub's change word as this step's news too.
+  // ghosts whose words records of step r-2 set (their records are still in ru / rm [par]): their
+  // words go quiet and the M records' change words are cleared, so that this parity holds only
+  // step r's news (an M record ORs its views into the change word; hub marking reads a ghost hub's
+  // word and change word as this step's).
   timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xbc_clear(s.stream, bc_in(c, xs, par), s.chg[par], s.uw[par]); });
   bool rover = false;
   for (int q = 0; q < P; q++) rover |= recv_m[q] > xs.rmcap[q];
@@ -1573,10 +1573,9 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
         c->inject_rec = false;
         break;
       }
-  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xbc_unpack(s.stream, in, s.lab[par], s.chg[par], s.uw[par], chg_bits(c, s, r).next); });
   timed_launch(c, si, KID_XMARK, 0.0, [&] {
-    launch_xbc_mark(s.stream, in, s.chg[par], g, s.vm, s.em, s.act[(r + 1) % 3], s.tcut, s.iem ? &s.ebp : nullptr,
-                    s.ccount, dense_div(c), r);
+    launch_xbc_apply(s.stream, in, s.lab[par], s.chg[par], s.uw[par], chg_bits(c, s, r).next, g, s.vm, s.em,
+                     s.act[(r + 1) % 3], s.tcut, s.iem ? &s.ebp : nullptr, s.ccount, dense_div(c), r);
   });
   // the vote is global: superstep r+1 runs here even if nothing changed here
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(s.stepcnt + r), 1, 1, s.stream));
@@ -1584,7 +1583,8 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (hv)  // neighbours of heavy vertices (owned ones visited in r, ghosts just received) that changed
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[par], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
-                        r == 1 ? nullptr : s.act[r % 3], s.vm, s.em, s.tcut, s.ccount, dense_div(c));
+                        r == 1 ? nullptr : s.act[r % 3], s.vm, s.em, s.tcut, s.ccount, dense_div(c), work_buf(c, s),
+                        s.uw[par]);
     });
   HIPCHK(hipGetLastError());
   // superstep r+1 over the owned vertices

@@ -245,9 +245,10 @@ __global__ void k_xcounts(int np, int me, unsigned long long* __restrict__ scnt,
 // -> the ghost it names (-1: none here; out-of-plan records are counted into err and skipped — a
 // bug upstream, reported by the run instead of faulting the device)
 __device__ __forceinline__ int64_t bc_total(const XBcIn& I) { return I.U.pre[I.U.np] + I.M.pre[I.M.np]; }
-// (b, label, views, is_u) of record i and the ghost it names
+// (b, label, views, is_u) of record i and the ghost it names; for an M record also its index in rm
+// and the end of its sender's region (mj, mend; -1 for a U record)
 __device__ __forceinline__ int32_t bc_rec(const XBcIn& I, int64_t i, int32_t& b, int32_t& val, uint64_t& mask, bool& isu,
-                                          bool& first) {
+                                          bool& first, int64_t* mj = nullptr, int64_t* mend = nullptr) {
   const int64_t nu = I.U.pre[I.U.np];
   int q;
   first = true;
@@ -258,6 +259,7 @@ __device__ __forceinline__ int32_t bc_rec(const XBcIn& I, int64_t i, int32_t& b,
     val = (int32_t)(uint32_t)r;
     mask = ~0ull;
     isu = true;
+    if (mj) *mj = *mend = -1;
   } else {
     const int64_t k = i - nu;
     q = peer_of(I.M, k);
@@ -268,6 +270,10 @@ __device__ __forceinline__ int32_t bc_rec(const XBcIn& I, int64_t i, int32_t& b,
     mask = r.mask;
     isu = false;
     first = k == I.M.pre[q] || I.rm[j - 1].e != b;  // a mixed sender's records are consecutive
+    if (mj) {
+      *mj = j;
+      *mend = I.M.base[q] + (I.M.pre[q + 1] - I.M.pre[q]);
+    }
   }
   if (b < 0 || (int64_t)b >= I.T.toff[q + 1] - I.T.toff[q]) {
     atomicAdd(I.err, 1ull);
@@ -281,8 +287,8 @@ __device__ __forceinline__ int32_t bc_rec(const XBcIn& I, int64_t i, int32_t& b,
   return g;
 }
 
-// ghosts whose words records of two supersteps ago set: clear their change words in that parity and
-// set their uniform word back to kGhostQuiet
+// ghosts whose words records of two supersteps ago set: uniform word back to kGhostQuiet, and for
+// an M record the change word cleared in that parity (a U record writes no change word)
 __global__ __launch_bounds__(256) void k_xbc_clear(XBcIn I, uint64_t* __restrict__ chg, int32_t* __restrict__ uw) {
   const int64_t n = bc_total(I);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -291,56 +297,26 @@ __global__ __launch_bounds__(256) void k_xbc_clear(XBcIn I, uint64_t* __restrict
     bool isu, first;
     const int32_t g = bc_rec(I, i, b, val, mask, isu, first);
     if (g < 0) continue;
-    chg[g] = 0;
+    if (!isu) chg[g] = 0;
     uw[g] = kGhostQuiet;
   }
 }
 
-// Records into ghost words / rows, lane = record: a U record's ghost takes the label as its uniform
-// word (changed flag set) and changed in every view (plain stores: a ghost has one sender and a U
-// sender sends one record).  M records mark the ghost mixed (kMixed) and write the label into the
-// row lanes of their views, the views OR-ed into the change word (one per wave iteration, lane = view).
-__global__ __launch_bounds__(256) void k_xbc_unpack(XBcIn I, int32_t* __restrict__ lab, uint64_t* __restrict__ chg,
-                                                    int32_t* __restrict__ uw, uint64_t* __restrict__ cb) {
-  const int64_t n = bc_total(I);
-  const int lane = lane_of();
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t i0 = wave * 64; i0 < n; i0 += nwaves * 64) {
-    const int64_t i = i0 + lane;
-    int32_t b = 0, val = 0, g = -1;
-    uint64_t mask = 0;
-    bool isu = false, first = false;
-    if (i < n) g = bc_rec(I, i, b, val, mask, isu, first);
-    if (g >= 0 && isu) {
-      uw[g] = uw_word(val, true);
-      chg[g] = ~0ull;
-      if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // (ChgBits)
-    }
-    for (uint64_t bb = __ballot(g >= 0 && !isu); bb; bb &= bb - 1) {
-      const int L = __builtin_ctzll(bb);
-      const int32_t gL = __builtin_amdgcn_readlane(g, L);
-      const int32_t vL = __builtin_amdgcn_readlane(val, L);
-      const uint64_t mL = rl64(mask, L);
-      if ((mL >> lane) & 1) lab[(int64_t)gL * 64 + lane] = vL;
-      if (lane == 0) {
-        uw[gL] = kMixed;
-        atomicOr((unsigned long long*)&chg[gL], (unsigned long long)mL);
-        if (cb) atomicOr((unsigned long long*)&cb[gL >> 6], 1ull << (gL & 63));
-      }
-    }
-  }
-}
-
-// After the unpack: every changed ghost (a U record, or the first M record of its sender) marks its
+// A superstep's received records applied and their ghosts' neighbours marked, in one pass (lane =
+// record).  Apply: a U record's ghost takes the label as its uniform word with the changed flag (a
+// plain store: a ghost has one sender and a U sender sends one record; no change word — readers of
+// a changed uniform word fold it on every kept view of the slot, and hub marking reads the word);
+// M records mark the ghost mixed (kMixed), write the label into the row lanes of their views and OR
+// the views into its change word (one per wave iteration, lane = view).  Mark: every changed ghost
+// (a U record, or the first M record of its sender with the union of the sender's masks) flags its
 // owned neighbours that share a changed view (the next frontier, as a local change would).  Ghosts
 // keep no compacted slots (K2 runs over the owned vertices only): the kept views of a static slot,
-// bits & vm[nb] & vm[g], are recomputed here over the time-ordered slots up to the batch's cut (bits:
+// bits & vm[nb] & vm[g], are recomputed over the time-ordered slots up to the batch's cut (bits:
 // K2's inline edge bits for a simple slot, else em[e]; without time-ordered slots the CSR order and
-// em).  A ghost holds only its edges to this partition's vertices (a few slots), so a wave takes 64
-// records (lane = record) and packs their ghosts' slot lists into 64-lane passes (lane = slot), as K2
-// packs its light members; ghosts with more than 64 static slots walk theirs one at a time.  Nothing
-// to mark when superstep r is dense (the next one visits every member).  Heavy ghosts: k_heavy_mark.
+// em).  A ghost holds only its edges to this partition's vertices (a few slots), so the wave packs
+// its records' ghosts' slot lists into 64-lane passes (lane = slot), as K2 packs its light members;
+// ghosts with more than 64 static slots walk theirs one at a time.  Nothing to mark when superstep
+// r is dense (the next one visits every member).  Heavy ghosts: k_heavy_mark.
 template <bool TS>
 __device__ __forceinline__ void mark_slot(int64_t p, int32_t g, uint64_t ch, const int64_t* __restrict__ ts_t,
                                           const int32_t* __restrict__ ts_nb, const int32_t* __restrict__ ts_e,
@@ -356,18 +332,19 @@ __device__ __forceinline__ void mark_slot(int64_t p, int32_t g, uint64_t ch, con
   if (bits & ch & ((iem && ebp.simple_ends && ts_nodeath(tsw)) ? ~0ull : vm[nb])) act_next[nb] = 1;
 }
 template <bool TS>
-__global__ __launch_bounds__(256) void k_xbc_mark(XBcIn I, const uint64_t* __restrict__ chg,
-                                                  const int64_t* __restrict__ out_off,
-                                                  const int64_t* __restrict__ in_off,
-                                                  const int32_t* __restrict__ in_eid,
-                                                  const int32_t* __restrict__ esrc, const int32_t* __restrict__ edst,
-                                                  const uint64_t* __restrict__ vm, const uint64_t* __restrict__ em,
-                                                  const int32_t* __restrict__ hv_of, uint8_t* __restrict__ act_next,
-                                                  const int64_t* __restrict__ adj_off, const int32_t* __restrict__ ts_e,
-                                                  const int32_t* __restrict__ ts_nb, const int64_t* __restrict__ ts_t,
-                                                  int64_t tcut, BatchParams ebp, int iem,
-                                                  const int32_t* __restrict__ ccount, int dense_div, int step) {
-  if (dense_after(ccount, step + 1, I.n_own, dense_div)) return;  // step r dense: r+1 visits every member
+__global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict__ lab, uint64_t* __restrict__ chg,
+                                                   int32_t* __restrict__ uw, uint64_t* __restrict__ cb,
+                                                   const int64_t* __restrict__ out_off,
+                                                   const int64_t* __restrict__ in_off,
+                                                   const int32_t* __restrict__ in_eid,
+                                                   const int32_t* __restrict__ esrc, const int32_t* __restrict__ edst,
+                                                   const uint64_t* __restrict__ vm, const uint64_t* __restrict__ em,
+                                                   const int32_t* __restrict__ hv_of, uint8_t* __restrict__ act_next,
+                                                   const int64_t* __restrict__ adj_off, const int32_t* __restrict__ ts_e,
+                                                   const int32_t* __restrict__ ts_nb, const int64_t* __restrict__ ts_t,
+                                                   int64_t tcut, BatchParams ebp, int iem,
+                                                   const int32_t* __restrict__ ccount, int dense_div, int step) {
+  const bool do_mark = !dense_after(ccount, step + 1, I.n_own, dense_div);  // step r dense: r+1 visits every member
   __shared__ HopLDS L;
   if (TS && iem) hop_lds_init(L, ebp, ebp.thr_e);
   const int64_t n = bc_total(I);
@@ -375,18 +352,40 @@ __global__ __launch_bounds__(256) void k_xbc_mark(XBcIn I, const uint64_t* __res
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t i0 = wave * 64; i0 < n; i0 += nwaves * 64) {
-    // lane = record: its ghost, when it is the ghost's first record and the ghost is no hub
     const int64_t i = i0 + lane;
-    int32_t b, val, g = -1;
-    uint64_t mask;
+    int32_t b = 0, val = 0, g = -1;
+    uint64_t mask = 0;
     bool isu = false, first = false;
-    if (i < n) g = bc_rec(I, i, b, val, mask, isu, first);
+    int64_t mj = -1, mend = -1;
+    if (i < n) g = bc_rec(I, i, b, val, mask, isu, first, &mj, &mend);
+    // apply
+    if (g >= 0 && isu) {
+      uw[g] = uw_word(val, true);
+      if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // (ChgBits)
+    }
+    for (uint64_t bb = __ballot(g >= 0 && !isu); bb; bb &= bb - 1) {
+      const int L = __builtin_ctzll(bb);
+      const int32_t gL = __builtin_amdgcn_readlane(g, L);
+      const int32_t vL = __builtin_amdgcn_readlane(val, L);
+      const uint64_t mL = rl64(mask, L);
+      if ((mL >> lane) & 1) lab[(int64_t)gL * 64 + lane] = vL;
+      if (lane == 0) {
+        uw[gL] = kMixed;
+        atomicOr((unsigned long long*)&chg[gL], (unsigned long long)mL);
+        if (cb) atomicOr((unsigned long long*)&cb[gL >> 6], 1ull << (gL & 63));
+      }
+    }
+    if (!do_mark) continue;
+    // mark: lane = record, its ghost when it is the ghost's first record and the ghost is no hub
     const bool go = g >= 0 && first && !(hv_of && hv_of[g] >= 0);
     uint64_t ch = 0;
     int64_t a = 0;
     int32_t k = 0;
     if (go) {
-      ch = chg[g] & vm[g];
+      uint64_t views = mask;  // U: every view; M: the union of the sender's records of this step
+      if (!isu)
+        for (int64_t j = mj + 1; j < mend && I.rm[j].e == b; j++) views |= I.rm[j].mask;
+      ch = views & vm[g];
       if (TS) {
         a = adj_off[g];
         k = (int32_t)(adj_off[g + 1] - a);
@@ -649,13 +648,18 @@ __global__ __launch_bounds__(256) void k_hist_recv(XPeers P, const XRec* __restr
       r = rbuf[P.base[q] + i - P.pre[q]];
       row = label_row(I, r.e);
     }
-    for (uint64_t t = __ballot(row >= 0); t; t &= t - 1) {
+    // a record with few views: its lane adds them; many views: the wave adds its row (lane = view)
+    const bool wide = row >= 0 && __popcll(r.mask) > 8;
+    for (uint64_t m = (row >= 0 && !wide) ? r.mask : 0ull; m; m &= m - 1)
+      atomicAdd(&counts[row * 64 + __builtin_ctzll(m)], r.val);
+    for (uint64_t t = __ballot(wide); t; t &= t - 1) {
       const int L = __builtin_ctzll(t);
       const int64_t rowL = (int64_t)rl64((uint64_t)row, L);
       const uint64_t mL = rl64(r.mask, L);
       const int32_t cL = __builtin_amdgcn_readlane(r.val, L);
       if ((mL >> lane) & 1) atomicAdd(&counts[rowL * 64 + lane], cL);
     }
+
   }
 }
 
@@ -765,19 +769,15 @@ void launch_xbc_clear(hipStream_t s, const XBcIn& I, uint64_t* chg, int32_t* uw)
   const int64_t n = I.U.pre[I.U.np] + I.M.pre[I.M.np];
   if (n > 0) k_xbc_clear<<<xgrid(n, 256), 256, 0, s>>>(I, chg, uw);
 }
-void launch_xbc_unpack(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg, int32_t* uw, uint64_t* cb) {
-  const int64_t n = I.U.pre[I.U.np] + I.M.pre[I.M.np];
-  if (n > 0) k_xbc_unpack<<<xgrid(n, 256), 256, 0, s>>>(I, lab, chg, uw, cb);
-}
-void launch_xbc_mark(hipStream_t s, const XBcIn& I, const uint64_t* chg, const DevGraph& g, const uint64_t* vm,
-                     const uint64_t* em, uint8_t* act_next, int64_t tcut, const BatchParams* ebp, const int32_t* ccount,
-                     int dense_div, int step) {
+void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg, int32_t* uw, uint64_t* cb,
+                      const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next, int64_t tcut,
+                      const BatchParams* ebp, const int32_t* ccount, int dense_div, int step) {
   const int64_t n = I.U.pre[I.U.np] + I.M.pre[I.M.np];
   if (n <= 0) return;
   BatchParams bp0;
   if (!ebp) std::memset(&bp0, 0, sizeof(bp0));
-  auto* kern = g.ts_t ? k_xbc_mark<true> : k_xbc_mark<false>;
-  kern<<<xgrid(n, 256), 256, 0, s>>>(I, chg, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
+  auto* kern = g.ts_t ? k_xbc_apply<true> : k_xbc_apply<false>;
+  kern<<<xgrid(n, 256), 256, 0, s>>>(I, lab, chg, uw, cb, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
                                    g.n_seg > 0 ? g.hv_of : nullptr, act_next, g.adj_off, g.ts_e, g.ts_nb, g.ts_t, tcut,
                                    ebp ? *ebp : bp0, ebp ? 1 : 0, ccount, dense_div, step);
 }
