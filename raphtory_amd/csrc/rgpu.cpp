@@ -696,6 +696,9 @@ void finish_tail(rgpu_ctx* c, int si, const RunCfg& rc) {
   if (rc.algo == RGPU_ALGO_CC || rc.algo == RGPU_ALGO_VP) launch_lane_fold(s.stream, s.stats + kLaneOff, s.stats + kFoldOff);
   HIPCHK(hipMemcpyAsync(s.h_stats, s.stats, sizeof(unsigned long long) * kStatCopy,
                         hipMemcpyDeviceToHost, s.stream));
+  if (c->profile && rc.algo == RGPU_ALGO_CC && s.work)  // the batch's work counters (the partitioned
+    HIPCHK(hipMemcpyAsync(s.h_work, s.work, sizeof(unsigned long long) * kWorkWords,  // path copies them here only)
+                          hipMemcpyDeviceToHost, s.stream));
   if (rc.algo == RGPU_ALGO_DEGREE) {  // the top-20 lists
     HIPCHK(hipMemcpyAsync(s.h_top, s.top.key, sizeof(unsigned long long) * kViews * kTop, hipMemcpyDeviceToHost,
                           s.stream));
@@ -1952,7 +1955,8 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
     g_xrec_slack = tiny ? 1 : 1024;
     g_xrec_init = tiny ? 0 : 2;
   }
-  if (const char* tp = std::getenv("RGPU_TRACE")) c->trace_path = tp;
+  if (const char* tp = std::getenv("RGPU_TRACE"))  // (a partition's trace: path + ".p<partition>")
+    c->trace_path = num_partitions > 1 ? std::string(tp) + ".p" + std::to_string(partition) : std::string(tp);
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
   *out = c;
   return RGPU_OK;

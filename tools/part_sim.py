@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--users", type=int, default=20_000_000)
     ap.add_argument("--interactions", type=int, default=33_333_334, help="prefix of the 1B stream (x3 updates)")
     ap.add_argument("--parts", default="1,2,4,8")
+    ap.add_argument("--trace", default="", help="directory: per-superstep trace CSVs (RGPU_TRACE) of the profile pass")
     a = ap.parse_args()
     inter_full = 333_333_334
     s = gen_gab_range(4, a.users, inter_full, 0, a.interactions)
@@ -33,6 +34,9 @@ def main():
     hops = range_hops(end - 167 * HOUR, end, HOUR)
     for P in [int(x) for x in a.parts.split(",")]:
         t0 = time.time()
+        if a.trace:  # read when a context opens; a partition's file gets ".p<partition>"
+            os.makedirs(a.trace, exist_ok=True)
+            os.environ["RGPU_TRACE"] = os.path.join(a.trace, f"trace_P{P}.csv")
         print(f"P={P}: packing", file=sys.stderr, flush=True)
         if P == 1:
             g = TemporalGraph()
