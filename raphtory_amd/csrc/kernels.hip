@@ -563,7 +563,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   uint64_t* __restrict__ cb1, int ends,
                                                   int32_t* __restrict__ ccount, int gmax, BatchParams ebp,
                                                   int dense1, const int32_t* __restrict__ ts_g,
-                                                  int32_t* __restrict__ mneg) {
+                                                  int32_t* __restrict__ mneg, const uint8_t* __restrict__ gpeer,
+                                                  uint8_t* __restrict__ pmask) {
   __shared__ unsigned long long red[4];
   int32_t wmin = INT32_MAX;  // lane = view: the minimum label of this wave's owned members
   __shared__ HopLDS L;
@@ -643,6 +644,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         }
         lb = ts_g ? ts_g[p] : (grank ? grank[nb] : nb);
       }
+      // partitioned: the peer owning a ghost neighbour across a kept slot (pmask, k_xbc_pack)
+      const uint32_t pbit = (m && gpeer && nb >= (int32_t)n_own) ? (1u << gpeer[nb - n_own]) : 0u;
       const uint64_t bal = __ballot(m != 0);
       if (m) {  // compacted at the member's static offset, in lane order within the member
         const uint64_t below = lanemask_lt() & ~((1ull << (lane - myj)) - 1);
@@ -673,15 +676,18 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         scanned += (unsigned long long)n;
         int32_t best = me;
         uint64_t any = 0;
+        uint32_t pm = 0;
         if (own) {
           for (uint64_t b = kept; b; b &= b - 1) {
             const int K = __builtin_ctzll(b);
             const int32_t q = __builtin_amdgcn_readlane(lb, K);
             const uint64_t mK = readlane64(m, K);
+            pm |= (uint32_t)__builtin_amdgcn_readlane((int)pbit, K);
             any |= mK;
             if (((mK >> lane) & 1) && q < best) best = q;
           }
         }
+        if (pmask && lane == 0) pmask[v] = (uint8_t)pm;
         if (uw1) {
           const int32_t u = row_uniform(best, mv, lane);
           const bool ch1 = __ballot(best < me) != 0;
@@ -754,6 +760,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       }
       const uint64_t ch = __ballot(best < me);
       if (lane == 0) {
+        if (pmask) pmask[v] = 0xff;  // (a hub: every peer)
         cnt[v] = 0;
         vadj[v] = any;
         chg1[v] = ch;
@@ -783,6 +790,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                   base = o0 + i0;
     int32_t count = 0, best = me;
     uint64_t any = 0;
+    uint32_t pm = 0;      // partitioned: peers owning a ghost neighbour across a kept slot
     uint64_t m_keep = 0;  // ntot <= 64: this lane's slot stays in registers for the marking below
     int32_t nb_keep = 0;
     for (int64_t c = 0; c < ntot; c += 64) {
@@ -814,6 +822,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         }
         lb = ts_g ? ts_g[base + j] : (grank ? grank[nb] : nb);
       }
+      const uint32_t pbit = (m && gpeer && nb >= (int32_t)n_own) ? (1u << gpeer[nb - n_own]) : 0u;
       uint64_t bal = __ballot(m != 0);
       if (m) {
         const int64_t pos = base + count + __popcll(bal & lanemask_lt());
@@ -829,6 +838,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         bal &= bal - 1;
         const int32_t q = __builtin_amdgcn_readlane(lb, L);
         const uint64_t mL = readlane64(m, L);
+        pm |= (uint32_t)__builtin_amdgcn_readlane((int)pbit, L);
         any |= mL;
         if (((mL >> lane) & 1) && q < best) best = q;
       }
@@ -849,6 +859,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       cnt[v] = count;
       vadj[v] = any;
       chg1[v] = ch;
+      if (pmask) pmask[v] = (uint8_t)pm;
       if (ch && cb1) atomicOr((unsigned long long*)&cb1[v >> 6], 1ull << (v & 63));
     }
     if (!own) continue;
@@ -2384,7 +2395,8 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
                      unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends,
-                     int32_t* ccount, const BatchParams* ebp, int dense_div, int32_t* mneg) {
+                     int32_t* ccount, const BatchParams* ebp, int dense_div, int32_t* mneg,
+                     const uint8_t* gpeer, uint8_t* pmask) {
   const bool hv = g.n_seg > 0;
   const bool iem = ebp != nullptr && g.ts_t != nullptr;
   auto* kern = work ? (iem ? k_cc_slots<true, true> : k_cc_slots<true, false>)
@@ -2397,7 +2409,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
                                                 uw0, uw1, cb1, ends ? 1 : 0, ccount, kDealSlots, iem ? *ebp : bp0,
                                                 dense_div > 0 && (dense_div & kDense1) && ccount ? 1 : 0,
-                                                g.ts_g, mneg);
+                                                g.ts_g, mneg, gpeer, pmask);
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);

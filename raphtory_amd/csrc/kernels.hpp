@@ -159,7 +159,10 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
                      unsigned long long* lanechg, int32_t* uw0 = nullptr, int32_t* uw1 = nullptr,
                      uint64_t* cb1 = nullptr, bool ends = false, int32_t* ccount = nullptr,
-                     const BatchParams* ebp = nullptr, int dense_div = 0, int32_t* mneg = nullptr);
+                     const BatchParams* ebp = nullptr, int dense_div = 0, int32_t* mneg = nullptr,
+                     const uint8_t* gpeer = nullptr, uint8_t* pmask = nullptr);
+// (partitioned: gpeer[g - n_own] = the partition owning ghost g; pmask[v] = the peers owning a ghost
+// neighbour of owned v across a kept slot of the batch, every peer for a hub)
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
 // (before launch_cc_slots); per superstep, segment gathers (before launch_cc_step) and
 // next-frontier marking of the heavy vertices' neighbours (after it; step 1: after slots)
@@ -269,6 +272,7 @@ void launch_diff_step(hipStream_t s, int step, const DevGraph& g, const int64_t*
 
 // ---- vertex-partitioned mode (xchg.hip; host: rgpu.cpp).  Up to kMaxParts partitions.
 constexpr int kMaxParts = 8;
+static_assert(kMaxParts <= 8, "a peer mask (K2 pmask, one byte per vertex) holds one bit per partition");
 // a label record: the new label `val` of boundary entry `e` (index in the sender's list for
 // the receiver) in the views `mask`
 struct XRec {
@@ -310,18 +314,20 @@ void launch_xtab_fill(hipStream_t s, int64_t n, const int32_t* xr_v, const int32
                       const XTab& T, unsigned long long* err);
 // After superstep `step`: this partition's broadcast label records (xchg.hip: U records into su, at
 // most nb; M records into sm, cnt[1] counts past mcap so the host can grow and pack again)
-// The pack of superstep `step`'s broadcast records (xchg.hip k_xbc_pack): per 64-boundary-vertex
-// chunk a count pass (ccnt[c] = U << 32 | M records), a device scan into coff (coff[nchunks] = the
-// totals; ccnt[nchunks] must be 0), then the write pass.  write_only: coff is current (a repack
-// into a larger M buffer).  ccnt / coff hold (nb + 63) / 64 + 1 words, scan_tmp xbc_scan_bytes(nb).
-size_t xbc_scan_bytes(int64_t nb);
-void launch_xbc_pack(hipStream_t s, int64_t n_own, const XSend& X, const uint8_t* act, const uint64_t* chg_now,
-                     const uint64_t* vadj, const int32_t* lab, const int32_t* uw, unsigned long long* su, XRec* sm,
-                     int64_t mcap, unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp,
-                     size_t scan_bytes, const int32_t* ccount, int dense_div, int step, bool write_only);
-// counts words (4 per peer): U records, M records (tot = the pack's scanned totals), the halting vote
-void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* tot, const int32_t* stepflag,
-                       int64_t* xa);
+// The pack of a superstep's label records (xchg.hip k_xbc_pack): per 64-owned-rank chunk (one word
+// of cb_now, the step's changed bits) a count pass (ccnt[q * nch + c] = U << 32 | M records for
+// peer q), a device scan into coff (ccnt[np * nch] must be 0), then the write pass into peer q's
+// regions su + q * ucap, sm + q * mcap.  write_only: coff is current (a repack into larger M
+// regions).  ccnt / coff hold nch * np + 1 words, scan_tmp xbc_scan_bytes(n_own, np).
+size_t xbc_scan_bytes(int64_t n_own, int np);
+void launch_xbc_pack(hipStream_t s, int64_t n_own, int np, const XSend& X, const uint64_t* cb_now,
+                     const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab, const int32_t* uw,
+                     const uint8_t* pmask, unsigned long long* su, int64_t ucap, XRec* sm, int64_t mcap,
+                     unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp, size_t scan_bytes,
+                     bool write_only);
+// counts words (4 per peer): U records, M records (coff / nch: the pack's scan), the halting vote
+void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* coff, int64_t nch,
+                       const int32_t* stepflag, int64_t* xa);
 // the per-view minimum member labels (mneg) folded into 64 words w / w stored back into shard 0
 // (partitioned final labels: the host all-reduces w with max in between)
 void launch_min_fold(hipStream_t s, const int32_t* mneg, unsigned long long* w);

@@ -120,11 +120,13 @@ struct Retained {  // per batch, RGPU_RUN_RETAIN
 struct XSlot {
   Exchange* x = nullptr;                  // this slot's channel (a fork of the ctx's)
   // broadcast label records (xchg.hip k_xbc_pack): one list for every peer
-  unsigned long long* su = nullptr;       // U records to send: at most one per boundary vertex (sized by
-                                          // the plan: grows only when a live merge grows the plan)
+  unsigned long long* su = nullptr;       // U records to send, peer q's at q * su_cap: at most one per
+                                          // boundary vertex (sized by the plan: grows only when a live
+                                          // merge grows the plan)
   int64_t su_cap = 0, ru_cap = 0;
-  XRec* sm = nullptr;                     // M records to send
+  XRec* sm = nullptr;                     // M records to send, peer q's at q * smcap (grown on demand)
   int64_t smcap = 0;
+  uint8_t* pmask = nullptr;               // [nv] peers that read an owned vertex in the batch (K2)
   unsigned long long* ru[2] = {nullptr, nullptr};  // received U records per superstep parity, region q
                                                    // = peer q's boundary count (never grows)
   XRec* rm[2] = {nullptr, nullptr};       // received M records per parity
@@ -159,6 +161,7 @@ struct Part {
   int64_t nbq[kMaxParts] = {};                // boundary vertices of every partition
   bool tab_ready = false;
   bool no_deaths = false;                     // no partition's graph holds a vertex death (ensure_tab)
+  uint8_t* gpeer = nullptr;                   // [nv - n_own] the partition owning ghost g (getPartition)
   double *sbuf_f = nullptr, *rbuf_f = nullptr;  // PR contribution rows
   bool pr_ready = false;
   XSlot xs[4];                                // per batch slot (kMaxSlots)
@@ -408,7 +411,8 @@ ChgBits chg_bits(const rgpu_ctx* c, const Slot& s, int r) {
   // heavy vertices.  The superstep kernel reading them measured slower on C4 (cc_step 263 ->
   // 301 ms serial; the bit probe then the words vs one change word) and on C2; the heavy
   // gather, which walks a hub's whole kept slot list every step, gained (119 -> 103 ms).
-  if (c->g.n_seg == 0) return b;
+  // (partitioned: the record pack reads them too)
+  if (c->g.n_seg == 0 && !c->partitioned) return b;
   b.prev = s.cb[(r + 2) % 3];
   b.next = s.cb[r % 3];
   b.clear = s.cb[(r + 1) % 3];
@@ -964,7 +968,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
                       s.chg[1], s.act[2], s.stepcnt, s.d_hostflag,
                       work_buf(c, s), s.hv, s.stats + kLaneOff, s.uw[0],
                       s.uw[1], chg_bits(c, s, 1).next, ends, s.ccount, iem ? &ebp : nullptr,
-                      dense_div(c), min_labels(c, s));
+                      dense_div(c), min_labels(c, s), c->partitioned ? c->pt.gpeer : nullptr,
+                      c->partitioned ? c->pt.xs[si].pmask : nullptr);
     });
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
@@ -1245,7 +1250,7 @@ XPeers peers_layout(const rgpu_ctx* c, const int64_t* cap, const std::vector<int
 void free_part_slots(rgpu_ctx* c, bool keep_channels) {
   for (XSlot& xs : c->pt.xs) {
     for (void* p : {(void*)xs.su, (void*)xs.sm, (void*)xs.ru[0], (void*)xs.ru[1], (void*)xs.rm[0], (void*)xs.rm[1],
-                    (void*)xs.hsbuf, (void*)xs.hrbuf, (void*)xs.ccnt, (void*)xs.coff, xs.scan_tmp})
+                    (void*)xs.hsbuf, (void*)xs.hrbuf, (void*)xs.ccnt, (void*)xs.coff, xs.scan_tmp, (void*)xs.pmask})
       if (p) (void)hipFree(p);
     if (xs.h_xab) (void)hipHostFree(xs.h_xab);
     Exchange* x = xs.x;
@@ -1256,6 +1261,7 @@ void free_part_slots(rgpu_ctx* c, bool keep_channels) {
 }
 
 void drop_alloc(std::vector<void*>& L, void* p);
+int sync_vid(rgpu_ctx* c);
 // The broadcast records' receive tables (once per sealed graph; collective): every partition's
 // boundary count, and for every receive entry the sender's boundary index of its vertex (the
 // send plans are aligned: entry e of q's list for us is our receive entry xr_off[q] + e).
@@ -1304,12 +1310,33 @@ void ensure_tab(rgpu_ctx* c) {
     HIPCHK(hipMemcpyAsync(&herr, err, sizeof(herr), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (herr) throw HipFail{"exchange plan: " + std::to_string(herr) + " receive entries name no boundary vertex of their sender"};
+    // ghost -> owning partition, Utils.getPartition (K2's peer masks: whom an owned vertex's records go to)
+    if (sync_vid(c) != RGPU_OK) throw HipFail{"exchange plan: vertex ids"};
+    const int64_t ng = c->g.nv - c->pk.n_own;
+    std::vector<uint8_t> gp((size_t)std::max<int64_t>(ng, 1), 0);
+    for (int64_t k = 0; k < ng; k++) {
+      const int64_t id = c->pk.vid[(size_t)(c->pk.n_own + k)];
+      gp[(size_t)k] = (uint8_t)(((id < 0 ? -id : id) % (10 * (int64_t)P)) / 10);
+    }
+    drop_alloc(LG, X.gpeer);
+    X.gpeer = dalloc<uint8_t>(LG, gp.size());
+    HIPCHK(hipMemcpy(X.gpeer, gp.data(), gp.size(), hipMemcpyHostToDevice));
   } catch (...) {
     for (void* p : T) (void)hipFree(p);
     throw;
   }
   for (void* p : T) (void)hipFree(p);
   X.tab_ready = true;
+}
+
+// the M send regions: P of xs.smcap records each (peer q's at q * smcap), at least `need` each
+void grow_sm(XSlot& xs, int P, int64_t need, hipStream_t s) {
+  if (xs.sm && need <= xs.smcap) return;
+  HIPCHK(hipStreamSynchronize(s));
+  if (xs.sm) HIPCHK(hipFree(xs.sm));
+  xs.sm = nullptr;
+  xs.smcap = std::max(xs.smcap, need + need / 2 + g_xrec_slack);
+  HIPCHK(hipMalloc((void**)&xs.sm, sizeof(XRec) * (size_t)xs.smcap * P));
 }
 
 void ensure_part(rgpu_ctx* c, int nuse, int planes) {
@@ -1335,29 +1362,31 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
       xs.vm_planes = planes;
     }
     if (xs.su_cap < X.xsend.nb || xs.ru_cap < X.tab.toff[P] || !xs.su) {
-      // U records: worst case one per boundary vertex, sent and received (sized by the plan: no
-      // growth during a run, no host sizing)
-      for (void* p : {(void*)xs.su, (void*)xs.ru[0], (void*)xs.ru[1], (void*)xs.ccnt, (void*)xs.coff, xs.scan_tmp})
+      // U records: worst case one per boundary vertex and peer, sent and received (sized by the
+      // plan: no growth during a run, no host sizing)
+      for (void* p : {(void*)xs.su, (void*)xs.ru[0], (void*)xs.ru[1], (void*)xs.ccnt, (void*)xs.coff, xs.scan_tmp,
+                      (void*)xs.pmask})
         if (p) HIPCHK(hipFree(p));
       xs.su_cap = std::max<int64_t>(X.xsend.nb, 1);
       xs.ru_cap = std::max<int64_t>(X.tab.toff[P], 1);
-      HIPCHK(hipMalloc((void**)&xs.su, sizeof(unsigned long long) * (size_t)xs.su_cap));
+      HIPCHK(hipMalloc((void**)&xs.su, sizeof(unsigned long long) * (size_t)xs.su_cap * P));
       for (int p = 0; p < 2; p++) HIPCHK(hipMalloc((void**)&xs.ru[p], sizeof(unsigned long long) * (size_t)xs.ru_cap));
-      // the pack's chunk counts and offsets (ccnt[nchunks] stays 0: coff[nchunks] = the totals)
-      const size_t nck = (size_t)((xs.su_cap + 63) / 64 + 1);
+      // the pack's per-(peer, chunk) counts and offsets (ccnt[P * nch] stays 0)
+      const int64_t no = c->pk.n_own, nch = (no + 63) / 64;
+      const size_t nck = (size_t)(nch * P + 1);
       HIPCHK(hipMalloc((void**)&xs.ccnt, sizeof(unsigned long long) * nck));
       HIPCHK(hipMalloc((void**)&xs.coff, sizeof(unsigned long long) * nck));
       HIPCHK(hipMemset(xs.ccnt, 0, sizeof(unsigned long long) * nck));
       HIPCHK(hipMemset(xs.coff, 0, sizeof(unsigned long long) * nck));
-      xs.scan_bytes = std::max<size_t>(xbc_scan_bytes(xs.su_cap), 16);
+      xs.scan_bytes = std::max<size_t>(xbc_scan_bytes(no, P), 16);
       HIPCHK(hipMalloc(&xs.scan_tmp, xs.scan_bytes));
+      HIPCHK(hipMalloc((void**)&xs.pmask, (size_t)std::max<int64_t>(c->g.nv, 1)));
     }
     if (!xs.sm) {
       // M records: a first guess, grown on demand (both receive parities share one layout, xs.rmcap)
-      int64_t ns[kMaxParts] = {}, nr[kMaxParts] = {};
-      ns[0] = g_xrec_init * X.xsend.nb / 16;
+      int64_t nr[kMaxParts] = {};
+      grow_sm(xs, P, g_xrec_init * X.xsend.nb / 16, nullptr);
       for (int q = 0; q < P; q++) nr[q] = g_xrec_init * X.nbq[q] / 16;
-      grow_regions(&xs.sm, &xs.smcap, ns, 1, nullptr);
       grow_regions(&xs.rm[0], xs.rmcap, nr, P, nullptr);
       xs.rm[1] = alloc_regions<XRec>(xs.rmcap, P);
     }
@@ -1418,22 +1447,18 @@ void part_min_labels(rgpu_ctx* c, int si) {
   HIPCHK(hipGetLastError());
 }
 
-// the broadcast label records of superstep r (U into xs.su, M into xs.sm).  write_only: the
-// offsets of the last pack are current (a repack into a larger M buffer)
+// the label records of superstep r for every peer (U into xs.su, M into xs.sm, peer q's regions),
+// from the step's changed bits and K2's peer masks.  write_only: the offsets of the last pack are
+// current (a repack into larger M regions)
 void part_pack(rgpu_ctx* c, int si, int r, bool write_only = false) {
   Slot& s = c->slot[si];
   Part& X = c->pt;
   XSlot& xs = X.xs[si];
   timed_launch(c, si, KID_XPACK, 0.0, [&] {
-    launch_xbc_pack(s.stream, c->pk.n_own, X.xsend, r == 1 ? nullptr : s.act[r % 3], s.chg[r & 1], s.vadj,
-                    s.lab[r & 1], s.uw[r & 1], xs.su, xs.sm, xs.smcap, xs.ccnt, xs.coff, xs.scan_tmp, xs.scan_bytes,
-                    s.ccount, dense_div(c), r, write_only);
+    launch_xbc_pack(s.stream, c->pk.n_own, c->nparts, X.xsend, chg_bits(c, s, r).next, s.chg[r & 1], s.vadj,
+                    s.lab[r & 1], s.uw[r & 1], xs.pmask, xs.su, xs.su_cap, xs.sm, xs.smcap, xs.ccnt, xs.coff,
+                    xs.scan_tmp, xs.scan_bytes, write_only);
   });
-}
-// the pack's totals word (U << 32 | M), or null without boundary vertices
-const unsigned long long* pack_totals(const rgpu_ctx* c, const XSlot& xs) {
-  const int64_t nb = c->pt.xsend.nb;
-  return nb > 0 ? xs.coff + (nb + 63) / 64 : nullptr;
 }
 
 // a received broadcast of parity par: regions and record counts (xchg.hip XBcIn)
@@ -1481,7 +1506,8 @@ void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
     return;
   }
   part_pack(c, si, r);
-  launch_xbc_counts(s.stream, P, c->part, pack_totals(c, xs), s.stepcnt + r, xs.xab);
+  launch_xbc_counts(s.stream, P, c->part, X.xsend.nb > 0 ? xs.coff : nullptr, (c->pk.n_own + 63) / 64, s.stepcnt + r,
+                    xs.xab);
   HIPCHK(hipGetLastError());
   xs.x->alltoall_i64(xs.xab, xs.xab + 4 * P, 4, s.stream);
   HIPCHK(hipMemcpyAsync(xs.h_xab, xs.xab, sizeof(int64_t) * 8 * P, hipMemcpyDeviceToHost, s.stream));
@@ -1497,12 +1523,13 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   const int P = c->nparts, me = c->part, r = xs.r;
   const int64_t* xa = xs.h_xab;
   const int64_t* xb = xs.h_xab + 4 * P;
-  int64_t sent_u = 0, sent_m = 0, recv_u[kMaxParts] = {}, recv_m[kMaxParts] = {};
+  int64_t sent_u[kMaxParts] = {}, sent_m[kMaxParts] = {}, max_m = 0, recv_u[kMaxParts] = {}, recv_m[kMaxParts] = {};
   bool any = false;
   for (int q = 0; q < P; q++) {
     if (q != me) {
-      sent_u = std::max(sent_u, xa[4 * q]);  // (the same broadcast for every peer)
-      sent_m = std::max(sent_m, xa[4 * q + 1]);
+      sent_u[q] = xa[4 * q];
+      sent_m[q] = xa[4 * q + 1];
+      max_m = std::max(max_m, sent_m[q]);
       recv_u[q] = xb[4 * q];
       recv_m[q] = xb[4 * q + 1];
       if (recv_u[q] > X.nbq[q])
@@ -1511,8 +1538,8 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     }
     any |= xb[4 * q + 2] != 0;  // the vote: some partition changed a label (self included)
   }
-  if (sent_m > xs.smcap) {  // the counts were exact; the M records did not all fit: pack again, larger
-    grow_regions(&xs.sm, &xs.smcap, &sent_m, 1, s.stream);
+  if (max_m > xs.smcap) {  // the counts were exact; the M records did not all fit: pack again, larger
+    grow_sm(xs, P, max_m, s.stream);
     part_pack(c, si, r, true);
   }
   if (!any) {  // every partition voted to halt
@@ -1553,17 +1580,17 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     std::vector<void*> sp(P), rp(P);
     std::vector<size_t> sb(P), rb(P);
     for (int q = 0; q < P; q++) {
-      sp[q] = xs.su;
+      sp[q] = xs.su + (size_t)q * xs.su_cap;
       rp[q] = xs.ru[par] + in.U.base[q];
-      sb[q] = q == me ? 0 : sizeof(unsigned long long) * (size_t)sent_u;
+      sb[q] = q == me ? 0 : sizeof(unsigned long long) * (size_t)sent_u[q];
       rb[q] = q == me ? 0 : sizeof(unsigned long long) * (size_t)recv_u[q];
       xs.bytes[1] += (double)sb[q];
     }
     xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
     for (int q = 0; q < P; q++) {
-      sp[q] = xs.sm;
+      sp[q] = xs.sm + (size_t)q * xs.smcap;
       rp[q] = xs.rm[par] + in.M.base[q];
-      sb[q] = q == me ? 0 : sizeof(XRec) * (size_t)sent_m;
+      sb[q] = q == me ? 0 : sizeof(XRec) * (size_t)sent_m[q];
       rb[q] = q == me ? 0 : sizeof(XRec) * (size_t)recv_m[q];
       xs.bytes[1] += (double)sb[q];
     }
@@ -1956,7 +1983,7 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
     g_xrec_init = tiny ? 0 : 2;
   }
   if (const char* tp = std::getenv("RGPU_TRACE"))  // (a partition's trace: path + ".p<partition>")
-    c->trace_path = num_partitions > 1 ? std::string(tp) + ".p" + std::to_string(partition) : std::string(tp);
+    c->trace_path = num_partitions > 1 ? std::string(tp) + ".p" + std::to_string(partition_id) : std::string(tp);
   if (hipSetDevice(device) != hipSuccess) { delete c; return RGPU_EHIP; }
   *out = c;
   return RGPU_OK;

@@ -110,12 +110,16 @@ __global__ __launch_bounds__(256) void k_xvm_unpack(int64_t nx, const int32_t* _
 //   M record (16 B, XRec): {b, label, views} per distinct new label of a mixed sender.
 // A sender's U records need at most nb slots (one per boundary vertex): U buffers are sized for the
 // worst case at plan time and never grow; M records (mixed senders: rare) grow on demand.
-// The pack runs in two passes over chunks of 64 consecutive boundary vertices (lane = b, the owned
-// rank X.v[b]): the count pass writes each chunk's U and M record counts (ccnt[c] = U << 32 | M),
-// a device scan turns them into offsets, and the write pass puts the records there.  No shared
-// counter: one atomic per wave on a single address serialised at the memory side (DESIGN.md §4
-// lesson 1) and was most of the one-pass pack's time.  A mixed sender's distinct labels are found
-// on its row (lane = view); rows of up to kRowsInFlight senders are loaded before any is folded.
+// The pack runs in two passes over chunks of 64 consecutive owned ranks (lane = vertex; one word
+// of the step's changed bits per chunk, so an unchanged chunk costs one scalar load): the count
+// pass writes each (peer, chunk)'s U and M record counts (ccnt[q * nch + c] = U << 32 | M), a device
+// scan turns them into offsets, and the write pass puts the records in peer q's region (U at
+// q * ucap, M at q * mcap).  A changed boundary vertex is sent only to the peers in pmask: those
+// owning a ghost neighbour across one of its kept slots in the batch (K2) — no other partition's
+// vertex reads it in this batch (kept slots are symmetric: both sides compute em & vm & vm).  No
+// shared counter: one atomic per wave on a single address serialised at the memory side
+// (DESIGN.md §4 lesson 1).  A mixed sender's distinct labels are found on its row (lane = view);
+// rows of up to kRowsInFlight senders are loaded before any is folded.
 constexpr int kRowsInFlight = 4;
 __device__ __forceinline__ int distinct_labels(int32_t x, uint64_t mm, int lane) {
   int k = 0;
@@ -127,59 +131,92 @@ __device__ __forceinline__ int distinct_labels(int32_t x, uint64_t mm, int lane)
   return k;
 }
 template <bool WRITE>
-__global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, int64_t nb, const int32_t* __restrict__ xb,
-                                                  const uint8_t* __restrict__ act, const uint64_t* __restrict__ chg_now,
+__global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, int np, const int32_t* __restrict__ bidx,
+                                                  const uint64_t* __restrict__ cb_now,
+                                                  const uint64_t* __restrict__ chg_now,
                                                   const uint64_t* __restrict__ vadj, const int32_t* __restrict__ lab,
-                                                  const int32_t* __restrict__ uw, unsigned long long* __restrict__ su,
+                                                  const int32_t* __restrict__ uw, const uint8_t* __restrict__ pmask,
+                                                  unsigned long long* __restrict__ su, int64_t ucap,
                                                   XRec* __restrict__ sm, int64_t mcap,
                                                   unsigned long long* __restrict__ ccnt,
-                                                  const unsigned long long* __restrict__ coff,
-                                                  const int32_t* __restrict__ ccount, int dense_div, int step) {
+                                                  const unsigned long long* __restrict__ coff) {
   const int lane = lane_of();
-  if (dense_after(ccount, step, n_own, dense_div)) act = nullptr;  // the step visited every member
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t nchunks = (nb + 63) >> 6;
-  for (int64_t c = wave; c < nchunks; c += nwaves) {
-    const int64_t b = c * 64 + lane;
-    const int32_t v = b < nb ? xb[b] : -1;
-    const bool vis = v >= 0 && (act == nullptr || act[v]);
-    const uint64_t m = vis ? chg_now[v] & vadj[v] : 0;
-    const int32_t u = m ? uw_label(uw[v]) : kMixed;
-    const bool full = m != 0 && u != kMixed;  // a uniform sender: one U record
-    const uint64_t bu = __ballot(full);
-    unsigned long long uo = 0, mo = 0;
-    if constexpr (WRITE) {
-      const unsigned long long o = coff[c];
-      uo = o >> 32;
-      mo = o & 0xffffffffull;
-      if (full) su[uo + __popcll(bu & lanemask_below(lane))] = ((unsigned long long)(uint32_t)b << 32) | (uint32_t)u;
+  const int64_t nch = (n_own + 63) >> 6;
+  for (int64_t c = wave; c < nch; c += nwaves) {
+    const uint64_t w = cb_now[c];  // (wave-uniform: a scalar load)
+    if (w == 0) {
+      if (!WRITE && lane < np) ccnt[(int64_t)lane * nch + c] = 0;
+      continue;
     }
-    unsigned long long nm = 0;
-    uint64_t mixed = __ballot(m != 0 && !full);
-    while (mixed) {  // mixed senders, kRowsInFlight rows at a time
-      int Ls[kRowsInFlight];
-      int32_t x[kRowsInFlight];
-      int k = 0;
-      for (; k < kRowsInFlight && mixed; k++, mixed &= mixed - 1) Ls[k] = __builtin_ctzll(mixed);
-      for (int i = 0; i < k; i++) x[i] = lab[(int64_t)__builtin_amdgcn_readlane(v, Ls[i]) * 64 + lane];
-      for (int i = 0; i < k; i++) {
-        const uint64_t mL = rl64(m, Ls[i]);
-        if constexpr (!WRITE) {
-          nm += (unsigned long long)distinct_labels(x[i], mL, lane);
-        } else {
-          const int32_t bL = (int32_t)(c * 64 + Ls[i]);
-          for (uint64_t mm = mL; mm; mo++) {
+    const int64_t v = c * 64 + lane;
+    const bool ch = ((w >> lane) & 1) && v < n_own;
+    const int32_t b = ch ? bidx[v] : -1;
+    const uint64_t m = b >= 0 ? chg_now[v] & vadj[v] : 0;
+    const uint32_t pm = m ? pmask[v] : 0u;
+    const int32_t u = pm ? uw_label(uw[v]) : kMixed;
+    const bool full = pm != 0 && u != kMixed;  // a uniform sender: one U record per peer in pm
+    const uint64_t mixed0 = __ballot(pm != 0 && u == kMixed);
+    if constexpr (!WRITE) {
+      unsigned long long nm = 0;  // lane q: M records for peer q
+      for (uint64_t mixed = mixed0; mixed;) {
+        int Ls[kRowsInFlight];
+        int32_t x[kRowsInFlight];
+        int k = 0;
+        for (; k < kRowsInFlight && mixed; k++, mixed &= mixed - 1) Ls[k] = __builtin_ctzll(mixed);
+        for (int i = 0; i < k; i++) x[i] = lab[(c * 64 + Ls[i]) * 64 + lane];
+        for (int i = 0; i < k; i++) {
+          const int d = distinct_labels(x[i], rl64(m, Ls[i]), lane);
+          const uint32_t pL = (uint32_t)__builtin_amdgcn_readlane((int)pm, Ls[i]);
+          if (lane < np && ((pL >> lane) & 1)) nm += (unsigned long long)d;
+        }
+      }
+      unsigned long long nu = 0;
+      for (int q = 0; q < np; q++) {
+        const unsigned long long cq = (unsigned long long)__popcll(__ballot(full && ((pm >> q) & 1)));
+        if (lane == q) nu = cq;
+      }
+      if (lane < np) ccnt[(int64_t)lane * nch + c] = (nu << 32) | nm;
+    } else {
+      unsigned long long uo = 0, mo = 0;  // lane q: peer q's offsets in its regions
+      if (lane < np) {
+        const unsigned long long o = coff[(int64_t)lane * nch + c], o0 = coff[(int64_t)lane * nch];
+        uo = (o >> 32) - (o0 >> 32);
+        mo = (o & 0xffffffffull) - (o0 & 0xffffffffull);
+      }
+      for (int q = 0; q < np; q++) {
+        const bool mine = full && ((pm >> q) & 1);
+        const uint64_t bu = __ballot(mine);
+        if (!bu) continue;
+        const unsigned long long base = (unsigned long long)__builtin_amdgcn_readlane((int)(uint32_t)uo, q);
+        if (mine)
+          su[(int64_t)q * ucap + (int64_t)(base + __popcll(bu & lanemask_below(lane)))] =
+              ((unsigned long long)(uint32_t)b << 32) | (uint32_t)u;
+      }
+      for (uint64_t mixed = mixed0; mixed;) {
+        int Ls[kRowsInFlight];
+        int32_t x[kRowsInFlight];
+        int k = 0;
+        for (; k < kRowsInFlight && mixed; k++, mixed &= mixed - 1) Ls[k] = __builtin_ctzll(mixed);
+        for (int i = 0; i < k; i++) x[i] = lab[(c * 64 + Ls[i]) * 64 + lane];
+        for (int i = 0; i < k; i++) {
+          const uint64_t mL = rl64(m, Ls[i]);
+          const int32_t bL = __builtin_amdgcn_readlane(b, Ls[i]);
+          const uint32_t pL = (uint32_t)__builtin_amdgcn_readlane((int)pm, Ls[i]);
+          for (uint64_t mm = mL; mm;) {
             const int32_t val = __builtin_amdgcn_readlane(x[i], __builtin_ctzll(mm));
             const uint64_t same = __ballot(((mm >> lane) & 1) && x[i] == val);
-            if (lane == 0 && mo < (unsigned long long)mcap) sm[mo] = XRec{bL, val, same};
             mm &= ~same;
+            // lane q < np writes peer q's copy
+            if (lane < np && ((pL >> lane) & 1)) {
+              if (mo < (unsigned long long)mcap) sm[(int64_t)lane * mcap + (int64_t)mo] = XRec{bL, val, same};
+              mo++;
+            }
           }
         }
       }
     }
-    if constexpr (!WRITE)
-      if (lane == 0) ccnt[c] = ((unsigned long long)__popcll(bu) << 32) | nm;
   }
 }
 
@@ -218,16 +255,17 @@ __global__ __launch_bounds__(256) void k_xtab_fill(int64_t n, const int32_t* __r
   }
 }
 
-// counts exchange words, 4 per peer: [4q] U records, [4q+1] M records (the same broadcast list
-// for every peer; 0 for self), [4q+2] this partition changed a label in the step (the halting vote,
-// AnalysisTask.endStep :208-225), [4q+3] 0.  tot = the pack's scanned totals (U << 32 | M).
-__global__ void k_xbc_counts(int np, int me, const unsigned long long* __restrict__ tot,
+// counts exchange words, 4 per peer: [4q] U records for q, [4q+1] M records for q (0 for self),
+// [4q+2] this partition changed a label in the step (the halting vote, AnalysisTask.endStep
+// :208-225), [4q+3] 0.  coff = the pack's scanned per-(peer, chunk) offsets (null: no records).
+__global__ void k_xbc_counts(int np, int me, const unsigned long long* __restrict__ coff, int64_t nch,
                              const int32_t* __restrict__ stepflag, int64_t* __restrict__ xa) {
   const int q = threadIdx.x;
-  const unsigned long long t = tot ? *tot : 0ull;
   if (q < np) {
-    xa[4 * q] = q == me ? 0 : (int64_t)(t >> 32);
-    xa[4 * q + 1] = q == me ? 0 : (int64_t)(t & 0xffffffffull);
+    unsigned long long t = 0;
+    if (coff && q != me) t = coff[(int64_t)(q + 1) * nch] - coff[(int64_t)q * nch];
+    xa[4 * q] = (int64_t)(t >> 32);
+    xa[4 * q + 1] = (int64_t)(t & 0xffffffffull);
     xa[4 * q + 2] = stepflag ? (stepflag[0] != 0) : 0;
     xa[4 * q + 3] = 0;
   }
@@ -693,28 +731,29 @@ void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32
                        int planes, const uint64_t* in, uint64_t* vm, int64_t vstride) {
   if (nx > 0) k_xvm_unpack<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, xq, xoff, planes, in, vm, vstride);
 }
-size_t xbc_scan_bytes(int64_t nb) {
-  const int n = (int)(((nb + 63) >> 6) + 1);
+size_t xbc_scan_bytes(int64_t n_own, int np) {
+  const int n = (int)(((n_own + 63) >> 6) * np + 1);
   size_t tb = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr, n);
   return tb;
 }
-void launch_xbc_pack(hipStream_t s, int64_t n_own, const XSend& X, const uint8_t* act, const uint64_t* chg_now,
-                     const uint64_t* vadj, const int32_t* lab, const int32_t* uw, unsigned long long* su, XRec* sm,
-                     int64_t mcap, unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp,
-                     size_t scan_bytes, const int32_t* ccount, int dense_div, int step, bool write_only) {
-  if (X.nb <= 0) return;
-  const int64_t nchunks = (X.nb + 63) >> 6;
-  const unsigned grid = xgrid(nchunks, 4, 4096);
+void launch_xbc_pack(hipStream_t s, int64_t n_own, int np, const XSend& X, const uint64_t* cb_now,
+                     const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab, const int32_t* uw,
+                     const uint8_t* pmask, unsigned long long* su, int64_t ucap, XRec* sm, int64_t mcap,
+                     unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp, size_t scan_bytes,
+                     bool write_only) {
+  if (X.nb <= 0 || n_own <= 0) return;
+  const int64_t nch = (n_own + 63) >> 6;
+  const unsigned grid = xgrid(nch, 4, 4096);
   if (!write_only) {
-    k_xbc_pack<false><<<grid, 256, 0, s>>>(n_own, X.nb, X.v, act, chg_now, vadj, lab, uw, su, sm, mcap, ccnt, coff,
-                                           ccount, dense_div, step);
-    // ccnt[nchunks] stays 0: coff[nchunks] = the totals
-    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ccnt, coff, (int)(nchunks + 1), s) != hipSuccess)
+    k_xbc_pack<false><<<grid, 256, 0, s>>>(n_own, np, X.bidx, cb_now, chg_now, vadj, lab, uw, pmask, su, ucap, sm, mcap,
+                                           ccnt, coff);
+    // ccnt[np * nch] stays 0: coff[q * nch] .. coff[(q + 1) * nch] = peer q's records
+    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ccnt, coff, (int)(nch * np + 1), s) != hipSuccess)
       throw std::runtime_error("xbc pack: scan");
   }
-  k_xbc_pack<true><<<grid, 256, 0, s>>>(n_own, X.nb, X.v, act, chg_now, vadj, lab, uw, su, sm, mcap, ccnt, coff, ccount,
-                                        dense_div, step);
+  k_xbc_pack<true><<<grid, 256, 0, s>>>(n_own, np, X.bidx, cb_now, chg_now, vadj, lab, uw, pmask, su, ucap, sm, mcap,
+                                        ccnt, coff);
 }
 XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, std::vector<void*>& T,
                   std::vector<void*>& L) {
@@ -756,9 +795,9 @@ void launch_xtab_fill(hipStream_t s, int64_t n, const int32_t* xr_v, const int32
                       const XTab& T, unsigned long long* err) {
   if (n > 0) k_xtab_fill<<<xgrid(n, 256), 256, 0, s>>>(n, xr_v, xr_q, tmp, T, err);
 }
-void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* tot, const int32_t* stepflag,
-                       int64_t* xa) {
-  k_xbc_counts<<<1, 64, 0, s>>>(np, me, tot, stepflag, xa);
+void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* coff, int64_t nch,
+                       const int32_t* stepflag, int64_t* xa) {
+  k_xbc_counts<<<1, 64, 0, s>>>(np, me, coff, nch, stepflag, xa);
 }
 void launch_min_fold(hipStream_t s, const int32_t* mneg, unsigned long long* w) { k_min_fold<<<1, 64, 0, s>>>(mneg, w); }
 void launch_min_store(hipStream_t s, const unsigned long long* w, int32_t* mneg) { k_min_store<<<1, 64, 0, s>>>(w, mneg); }
