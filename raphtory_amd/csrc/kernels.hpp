@@ -367,7 +367,14 @@ struct OwnIdx {
 // peer q.  uw may be null (rows only).
 void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,
-                       unsigned int* iso, unsigned long long* gcnt, XRec* hsbuf);
+                       unsigned int* iso, unsigned long long* gcnt, XRec* hsbuf, const int32_t* mneg = nullptr,
+                       unsigned int* fin_g = nullptr);
+// members carrying the view's global minimum label (mneg) are counted into fin_g (64 shards x 64
+// views) instead of records; fold them into w (zeroing the shards), all-reduce w, and the label's
+// owner adds w at the label's count row
+void launch_min_count_fold(hipStream_t s, unsigned int* fin_g, unsigned long long* w);
+void launch_min_count_add(hipStream_t s, const unsigned long long* w, const int32_t* mneg, const OwnIdx& I, int np,
+                          int me, int32_t* counts);
 // records {label, count, views} received: counted at the owned label's rows
 void launch_hist_recv(hipStream_t s, const XPeers& P, const XRec* rbuf, const OwnIdx& I, int32_t* counts);
 // PageRank contribution rows of a list (partitioned PageRank): gather into / scatter out of a

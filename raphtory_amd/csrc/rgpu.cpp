@@ -138,6 +138,7 @@ struct XSlot {
   size_t scan_bytes = 0;
   unsigned long long* err = nullptr;      // received records outside the plan (xchg.hip bc_rec)
   unsigned long long* mfin = nullptr;     // [64] the batch's minimum member labels, all-reduced
+  unsigned int* fin_g = nullptr;          // [64 x 64] members carrying them, per shard and view
   int64_t* xab = nullptr;                 // [8P] counts words: sent (xa) | received (xb)
   int64_t* h_xab = nullptr;               // pinned copy
   uint64_t *vms = nullptr, *vmr = nullptr;  // ghost membership words (planes x list)
@@ -984,7 +985,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     s.r_launched = 1;  // superstep 1 ran inside the slot kernel
     if (c->partitioned) {
       s.r_final = 0;
-      if (rc.max_steps > 1) part_min_labels(c, si);
+      part_min_labels(c, si);  // (also the count pass's minimum-label counts, part_finish_begin)
       if (rc.max_steps <= 1) part_finish_begin(c, si, rc);
       else part_post_step(c, si, rc, 1);
       return;
@@ -1350,6 +1351,8 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
     if (!xs.err) {
       xs.err = dalloc<unsigned long long>(LG, 1);
       xs.mfin = dalloc<unsigned long long>(LG, 64);
+      xs.fin_g = dalloc<unsigned int>(LG, 64 * 64);
+      HIPCHK(hipMemset(xs.fin_g, 0, sizeof(unsigned int) * 64 * 64));
       xs.htot = dalloc<unsigned long long>(LG, kMaxParts);
       HIPCHK(hipMemset(xs.htot, 0, sizeof(unsigned long long) * kMaxParts));
       xs.xab = dalloc<int64_t>(LG, 8 * P);
@@ -1657,7 +1660,7 @@ void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc) {
   const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);
   timed_launch(c, si, KID_HIST, 28.0 * no, [&] {
     launch_part_count(s.stream, false, L, X.own, nviews, s.vm, s.vadj, uw, s.lab[s.r_final & 1], s.counts, s.iso,
-                      xs.htot, xs.hsbuf);
+                      xs.htot, xs.hsbuf, min_labels(c, s), xs.fin_g);
   });
   launch_xcounts(s.stream, P, c->part, xs.htot, xs.xab);
   HIPCHK(hipGetLastError());
@@ -1688,7 +1691,7 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
     grow_regions(&xs.hsbuf, xs.hscap, sent, P, s.stream);
     const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);
     launch_part_count(s.stream, true, L, X.own, nviews, s.vm, s.vadj, uw, s.lab[s.r_final & 1], s.counts, s.iso,
-                      xs.htot, xs.hsbuf);
+                      xs.htot, xs.hsbuf, min_labels(c, s), xs.fin_g);
     HIPCHK(hipMemcpyAsync(xs.h_xab, xs.htot, sizeof(int64_t) * P, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipStreamSynchronize(s.stream));
     for (int q = 0; q < P; q++)
@@ -1713,6 +1716,11 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
     xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
   }
   timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_hist_recv(s.stream, peers_layout(c, xs.hrcap, X.xr_off, recv), xs.hrbuf, X.own, s.counts); });
+  // the minimum label's members, counted on every partition (k_part_count): summed, added by its owner
+  launch_min_count_fold(s.stream, xs.fin_g, xs.mfin);
+  xs.x->allreduce_u64(xs.mfin, 64, false, s.stream);
+  launch_min_count_add(s.stream, xs.mfin, min_labels(c, s), X.own, P, me, s.counts);
+  HIPCHK(hipGetLastError());
   // roots: every owned member whose label is its own id reads (and zeroes) its count row
   timed_launch(c, si, KID_SUMMARY, 20.0 * no, [&] {
     launch_cc_roots(s.stream, no, nviews, s.vm, s.vadj, uw, s.lab[s.r_final & 1], s.counts, s.stats, s.iso,
@@ -1928,7 +1936,7 @@ void reset_after_failure(rgpu_ctx* c) {
   for (Slot& s : c->slot)
     for (void* p : {(void*)s.hv.segcnt, (void*)s.hv.segor, (void*)s.hv.best, (void*)s.hv.pacc}) drop_alloc(LG, p);
   for (XSlot& xs : c->pt.xs)
-    for (void* p : {(void*)xs.err, (void*)xs.mfin, (void*)xs.htot, (void*)xs.xab, (void*)xs.vms, (void*)xs.vmr})
+    for (void* p : {(void*)xs.err, (void*)xs.mfin, (void*)xs.fin_g, (void*)xs.htot, (void*)xs.xab, (void*)xs.vms, (void*)xs.vmr})
       drop_alloc(LG, p);
   release_slots(c);
   free_part_slots(c, true);

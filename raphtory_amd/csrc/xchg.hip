@@ -584,12 +584,14 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
                                                     const uint64_t* __restrict__ vadj, const int32_t* __restrict__ uw,
                                                     const int32_t* __restrict__ lab, int32_t* __restrict__ counts,
                                                     unsigned int* __restrict__ iso_g,
-                                                    unsigned long long* __restrict__ gcnt, XRec* __restrict__ hsbuf) {
+                                                    unsigned long long* __restrict__ gcnt, XRec* __restrict__ hsbuf,
+                                                    const int32_t* __restrict__ mneg, unsigned int* __restrict__ fin_g) {
   // The cache is private to a wave (16 rows each): a wave's operations run in a fixed order, so
   // the records it emits are the same on every run — the REMOTE_ONLY pass after a send-buffer
   // overflow must emit exactly the records the counts exchange announced.
   constexpr int kRows = 16;
   __shared__ unsigned int iso[64];
+  __shared__ unsigned int fin[64];
   __shared__ int32_t ckey_s[4][kRows];
   __shared__ unsigned int crow_s[4][kRows][64];
   __shared__ XRec srec_s[4][kMaxParts][kStage];
@@ -597,7 +599,7 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
   int32_t* ckey = ckey_s[wib];
   unsigned int (*crow)[64] = crow_s[wib];
   CountStage st{srec_s[wib], 0};
-  if (threadIdx.x < 64) iso[threadIdx.x] = 0;
+  if (threadIdx.x < 64) iso[threadIdx.x] = 0, fin[threadIdx.x] = 0;
   if (lane < kRows) ckey[lane] = -1;
   for (int h = 0; h < kRows; h++) crow[h][lane] = 0;
   __syncthreads();
@@ -621,6 +623,17 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   unsigned int iso_acc = 0;  // lane = view
+  // The view's global minimum member label (part_min_labels) is very likely its giant component,
+  // whose members sit on every partition: they are counted here per view (fin_acc) and summed over
+  // the partitions by an all-reduce (launch_min_count) instead of records that all converge on one
+  // count row of one partition.
+  int32_t mfin = INT32_MIN;
+  if (mneg) {
+    int32_t x = 0;
+    for (int sh = 0; sh < kMinShards; sh++) x = max(x, mneg[sh * 64 + lane]);
+    mfin = x ? INT32_MAX - x : INT32_MIN;
+  }
+  unsigned int fin_acc = 0;
   for (int64_t b0 = wave * 64; b0 < n_own; b0 += nwaves * 64) {
     const int64_t v = b0 + lane;
     const uint64_t mv = v < n_own ? vm[v] & vmask : 0;
@@ -635,16 +648,21 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
       const uint64_t mL = rl64(m, L);
       const uint64_t same = __ballot(((todo >> lane) & 1) && x == xL && m == mL);
       todo &= ~same;
-      const bool on = (mL >> lane) & 1;
+      const bool fl = ((mL >> lane) & 1) && xL == mfin;
+      const bool on = ((mL >> lane) & 1) && !fl;
       const unsigned c = (unsigned)__popcll(same);
+      if (fl) fin_acc += c;
       const bool hit = on && cached(xL, lane, c);
       emit_count<REMOTE_ONLY>(xL, __ballot(on && !hit), c, P, I, counts, gcnt, hsbuf, lane, st);
     }
     for (uint64_t mixed = __ballot(m != 0 && x == kMixed); mixed; mixed &= mixed - 1) {  // rows
       const int L = __builtin_ctzll(mixed);
       const uint64_t mL = rl64(m, L);
-      const bool on = (mL >> lane) & 1;
-      const int32_t l = on ? lab[(b0 + L) * 64 + lane] : 0;
+      const bool mem = (mL >> lane) & 1;
+      const int32_t l = mem ? lab[(b0 + L) * 64 + lane] : 0;
+      const bool fl = mem && l == mfin;
+      const bool on = mem && !fl;
+      if (fl) fin_acc += 1u;
       const bool hit = on && cached(l, lane, 1u);
       emit_lanes<REMOTE_ONLY>(on && !hit, l, 1u, P, I, counts, gcnt, hsbuf, lane, st);
     }
@@ -664,9 +682,12 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
   }
   for (int q = 0; q < P.np; q++) stage_flush(st, q, P, gcnt, hsbuf, lane);
   if (!REMOTE_ONLY && iso_acc) atomicAdd(&iso[lane], iso_acc);
+  if (!REMOTE_ONLY && fin_acc) atomicAdd(&fin[lane], fin_acc);
   __syncthreads();
   if (!REMOTE_ONLY && threadIdx.x < 64 && iso[threadIdx.x])
     atomicAdd(&iso_g[(blockIdx.x & 63) * 64 + threadIdx.x], iso[threadIdx.x]);
+  if (!REMOTE_ONLY && fin_g && threadIdx.x < 64 && fin[threadIdx.x])
+    atomicAdd(&fin_g[(blockIdx.x & 63) * 64 + threadIdx.x], fin[threadIdx.x]);
 }
 
 // records received from the other partitions: counted at the owned label vertex's row (lane =
@@ -715,6 +736,32 @@ __global__ void k_min_fold(const int32_t* __restrict__ mneg, unsigned long long*
 __global__ void k_min_store(const unsigned long long* __restrict__ w, int32_t* __restrict__ mneg) {
   const int j = threadIdx.x;
   if (j < 64) mneg[j] = (int32_t)w[j];
+}
+
+// The minimum-label counts (k_part_count fin_g, 64 shards x 64 views): folded into w (and the
+// shards zeroed for the next batch); after the all-reduce (sum) over the partitions the label's
+// owner adds them at the label's count row
+__global__ void k_min_count_fold(unsigned int* __restrict__ fin_g, unsigned long long* __restrict__ w) {
+  const int j = threadIdx.x;
+  if (j >= 64) return;
+  unsigned long long t = 0;
+  for (int sh = 0; sh < 64; sh++) {
+    t += fin_g[sh * 64 + j];
+    fin_g[sh * 64 + j] = 0;
+  }
+  w[j] = t;
+}
+__global__ void k_min_count_add(const unsigned long long* __restrict__ w, const int32_t* __restrict__ mneg, OwnIdx I,
+                                int np, int me, int32_t* __restrict__ counts) {
+  const int j = threadIdx.x;
+  if (j >= 64 || w[j] == 0) return;
+  int32_t x = 0;
+  for (int sh = 0; sh < kMinShards; sh++) x = max(x, mneg[sh * 64 + j]);
+  if (!x) return;
+  const int32_t l = INT32_MAX - x;
+  if (owner_of(l, np) != me) return;
+  const int64_t r = label_row(I, l);
+  if (r >= 0) counts[r * 64 + j] += (int32_t)w[j];  // (one thread per view: no race)
 }
 
 // ------------------------------------------------------------------ launchers
@@ -822,13 +869,21 @@ void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg
 }
 void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,
-                       unsigned int* iso, unsigned long long* gcnt, XRec* hsbuf) {
+                       unsigned int* iso, unsigned long long* gcnt, XRec* hsbuf, const int32_t* mneg,
+                       unsigned int* fin_g) {
   const uint64_t vmask = nviews >= 64 ? ~0ull : ((1ull << nviews) - 1);
   const unsigned grid = xgrid(I.n_own, 256, 2048);
   if (remote_only)
-    k_part_count<true><<<grid, 256, 0, s>>>(P, I, vmask, vm, vadj, uw, lab, counts, iso, gcnt, hsbuf);
+    k_part_count<true><<<grid, 256, 0, s>>>(P, I, vmask, vm, vadj, uw, lab, counts, iso, gcnt, hsbuf, mneg, fin_g);
   else
-    k_part_count<false><<<grid, 256, 0, s>>>(P, I, vmask, vm, vadj, uw, lab, counts, iso, gcnt, hsbuf);
+    k_part_count<false><<<grid, 256, 0, s>>>(P, I, vmask, vm, vadj, uw, lab, counts, iso, gcnt, hsbuf, mneg, fin_g);
+}
+void launch_min_count_fold(hipStream_t s, unsigned int* fin_g, unsigned long long* w) {
+  k_min_count_fold<<<1, 64, 0, s>>>(fin_g, w);
+}
+void launch_min_count_add(hipStream_t s, const unsigned long long* w, const int32_t* mneg, const OwnIdx& I, int np,
+                          int me, int32_t* counts) {
+  k_min_count_add<<<1, 64, 0, s>>>(w, mneg, I, np, me, counts);
 }
 void launch_hist_recv(hipStream_t s, const XPeers& P, const XRec* rbuf, const OwnIdx& I, int32_t* counts) {
   if (P.pre[P.np] > 0) k_hist_recv<<<xgrid(P.pre[P.np], 256), 256, 0, s>>>(P, rbuf, I, counts);
