@@ -546,16 +546,18 @@ __device__ __forceinline__ void stage_flush(CountStage& st, int q, const XPeers&
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // read before the slots are reused
   if (lane == q) st.n = 0;
 }
-// wave-uniform (x, views, c): added at the count row when x is owned here, else one staged record
+// wave-uniform (x, views, c): added at the count row when x is owned here, else one staged record.
+// row: x's count row when the caller looked it up already (the lanes' lookups run in parallel
+// before the serial group loops: a lookup is two dependent global loads), else -2
 template <bool REMOTE_ONLY>
 __device__ __forceinline__ void emit_count(int32_t x, uint64_t views, unsigned c, const XPeers& P, const OwnIdx& I,
                                            int32_t* __restrict__ counts, unsigned long long* __restrict__ gcnt,
-                                           XRec* __restrict__ hsbuf, int lane, CountStage& st) {
+                                           XRec* __restrict__ hsbuf, int lane, CountStage& st, int64_t row = -2) {
   if (views == 0 || c == 0) return;
   const int q = owner_of(x, P.np);
   if (q == P.me) {
     if (!REMOTE_ONLY) {
-      const int64_t r = label_row(I, x);  // always found: a label is a member's id
+      const int64_t r = row != -2 ? row : label_row(I, x);  // always found: a label is a member's id
       if (r >= 0 && ((views >> lane) & 1)) atomicAdd(&counts[r * 64 + lane], (int32_t)c);
     }
     return;
@@ -565,18 +567,20 @@ __device__ __forceinline__ void emit_count(int32_t x, uint64_t views, unsigned c
   if (lane == 0) st.rec[q][c0] = XRec{x, (int32_t)c, views};
   if (lane == q) st.n = c0 + 1;
 }
-// per lane (lane = view) label l with count c on the lanes of `on`: grouped by (label, count)
+// per lane (lane = view) label l with count c on the lanes of `on`: grouped by (label, count); the
+// lanes look their owned labels' rows up first, in parallel
 template <bool REMOTE_ONLY>
 __device__ __forceinline__ void emit_lanes(bool on, int32_t l, unsigned c, const XPeers& P, const OwnIdx& I,
                                            int32_t* __restrict__ counts, unsigned long long* __restrict__ gcnt,
                                            XRec* __restrict__ hsbuf, int lane, CountStage& st) {
+  const int64_t rl = (!REMOTE_ONLY && on && owner_of(l, P.np) == P.me) ? label_row(I, l) : -1;
   for (uint64_t rest = __ballot(on); rest;) {
     const int L = __builtin_ctzll(rest);
     const int32_t xL = __builtin_amdgcn_readlane(l, L);
     const unsigned cL = (unsigned)__builtin_amdgcn_readlane((int)c, L);
     const uint64_t same = __ballot(((rest >> lane) & 1) && l == xL && c == cL);
     rest &= ~same;
-    emit_count<REMOTE_ONLY>(xL, same, cL, P, I, counts, gcnt, hsbuf, lane, st);
+    emit_count<REMOTE_ONLY>(xL, same, cL, P, I, counts, gcnt, hsbuf, lane, st, (int64_t)rl64((uint64_t)rl, L));
   }
 }
 template <bool REMOTE_ONLY>
@@ -642,6 +646,8 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
     if (!REMOTE_ONLY) iso_acc += (unsigned)__popcll(transpose64(mv & ~ad, lane));
     const uint64_t m = mv & ad;
     uint64_t todo = __ballot(m != 0 && x != kMixed);
+    // the lanes' owned labels' count rows, looked up in parallel before the group loop
+    const int64_t rx = (!REMOTE_ONLY && m != 0 && x != kMixed && owner_of(x, P.np) == P.me) ? label_row(I, x) : -1;
     while (todo) {  // uniform members, grouped by (label, views): lane = view
       const int L = __builtin_ctzll(todo);
       const int32_t xL = __builtin_amdgcn_readlane(x, L);
@@ -653,7 +659,8 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
       const unsigned c = (unsigned)__popcll(same);
       if (fl) fin_acc += c;
       const bool hit = on && cached(xL, lane, c);
-      emit_count<REMOTE_ONLY>(xL, __ballot(on && !hit), c, P, I, counts, gcnt, hsbuf, lane, st);
+      emit_count<REMOTE_ONLY>(xL, __ballot(on && !hit), c, P, I, counts, gcnt, hsbuf, lane, st,
+                              (int64_t)rl64((uint64_t)rx, L));
     }
     for (uint64_t mixed = __ballot(m != 0 && x == kMixed); mixed; mixed &= mixed - 1) {  // rows
       const int L = __builtin_ctzll(mixed);
@@ -667,15 +674,16 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
       emit_lanes<REMOTE_ONLY>(on && !hit, l, 1u, P, I, counts, gcnt, hsbuf, lane, st);
     }
   }
-  for (int h = 0; h < kRows; h++) {  // the wave's cache: owned labels at their rows, the rest as records
+  // the wave's cache: owned labels at their rows (looked up in parallel, lane h), the rest as records
+  const int32_t kl = lane < kRows ? ckey[lane] : -1;
+  const int64_t rk = (!REMOTE_ONLY && kl != -1 && owner_of(kl, P.np) == P.me) ? label_row(I, kl) : -1;
+  for (int h = 0; h < kRows; h++) {
     const int32_t k = ckey[h];
     if (k == -1) continue;
     const unsigned int c = crow[h][lane];
     if (owner_of(k, P.np) == P.me) {
-      if (!REMOTE_ONLY) {
-        const int64_t r = label_row(I, k);
-        if (r >= 0 && c) atomicAdd(&counts[r * 64 + lane], (int32_t)c);
-      }
+      const int64_t r = (int64_t)rl64((uint64_t)rk, h);
+      if (!REMOTE_ONLY && r >= 0 && c) atomicAdd(&counts[r * 64 + lane], (int32_t)c);
       continue;
     }
     emit_lanes<REMOTE_ONLY>(c != 0, k, c, P, I, counts, gcnt, hsbuf, lane, st);
