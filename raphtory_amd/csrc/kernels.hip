@@ -532,7 +532,7 @@ __device__ __forceinline__ uint64_t slot_bits(const HopLDS& L, const BatchParams
 
 // PROF = false: the work counters compile away (launch_cc_slots: work == null).  IEM: inline edge
 // bits (slot_bits; time-ordered slots required), em unused
-template <bool PROF, bool IEM>
+template <bool PROF, bool IEM, bool PART>
 __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int64_t* __restrict__ out_off,
                                                   const int64_t* __restrict__ in_off,
@@ -645,7 +645,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         lb = ts_g ? ts_g[p] : (grank ? grank[nb] : nb);
       }
       // partitioned: the peer owning a ghost neighbour across a kept slot (pmask, k_xbc_pack)
-      const uint32_t pbit = (m && gpeer && nb >= (int32_t)n_own) ? (1u << gpeer[nb - n_own]) : 0u;
+      uint32_t pbit = 0u;
+      if constexpr (PART) pbit = (m && nb >= (int32_t)n_own) ? (1u << gpeer[nb - n_own]) : 0u;
       const uint64_t bal = __ballot(m != 0);
       if (m) {  // compacted at the member's static offset, in lane order within the member
         const uint64_t below = lanemask_lt() & ~((1ull << (lane - myj)) - 1);
@@ -682,12 +683,13 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
             const int K = __builtin_ctzll(b);
             const int32_t q = __builtin_amdgcn_readlane(lb, K);
             const uint64_t mK = readlane64(m, K);
-            pm |= (uint32_t)__builtin_amdgcn_readlane((int)pbit, K);
+            if constexpr (PART) pm |= (uint32_t)__builtin_amdgcn_readlane((int)pbit, K);
             any |= mK;
             if (((mK >> lane) & 1) && q < best) best = q;
           }
         }
-        if (pmask && lane == 0) pmask[v] = (uint8_t)pm;
+        if constexpr (PART)
+          if (lane == 0) pmask[v] = (uint8_t)pm;
         if (uw1) {
           const int32_t u = row_uniform(best, mv, lane);
           const bool ch1 = __ballot(best < me) != 0;
@@ -760,7 +762,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       }
       const uint64_t ch = __ballot(best < me);
       if (lane == 0) {
-        if (pmask) pmask[v] = 0xff;  // (a hub: every peer)
+        if constexpr (PART) pmask[v] = 0xff;  // (a hub: every peer)
         cnt[v] = 0;
         vadj[v] = any;
         chg1[v] = ch;
@@ -822,7 +824,8 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         }
         lb = ts_g ? ts_g[base + j] : (grank ? grank[nb] : nb);
       }
-      const uint32_t pbit = (m && gpeer && nb >= (int32_t)n_own) ? (1u << gpeer[nb - n_own]) : 0u;
+      uint32_t pbit = 0u;
+      if constexpr (PART) pbit = (m && nb >= (int32_t)n_own) ? (1u << gpeer[nb - n_own]) : 0u;
       uint64_t bal = __ballot(m != 0);
       if (m) {
         const int64_t pos = base + count + __popcll(bal & lanemask_lt());
@@ -838,7 +841,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
         bal &= bal - 1;
         const int32_t q = __builtin_amdgcn_readlane(lb, L);
         const uint64_t mL = readlane64(m, L);
-        pm |= (uint32_t)__builtin_amdgcn_readlane((int)pbit, L);
+        if constexpr (PART) pm |= (uint32_t)__builtin_amdgcn_readlane((int)pbit, L);
         any |= mL;
         if (((mL >> lane) & 1) && q < best) best = q;
       }
@@ -859,7 +862,7 @@ __global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
       cnt[v] = count;
       vadj[v] = any;
       chg1[v] = ch;
-      if (pmask) pmask[v] = (uint8_t)pm;
+      if constexpr (PART) pmask[v] = (uint8_t)pm;
       if (ch && cb1) atomicOr((unsigned long long*)&cb1[v >> 6], 1ull << (v & 63));
     }
     if (!own) continue;
@@ -2399,8 +2402,12 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      const uint8_t* gpeer, uint8_t* pmask) {
   const bool hv = g.n_seg > 0;
   const bool iem = ebp != nullptr && g.ts_t != nullptr;
-  auto* kern = work ? (iem ? k_cc_slots<true, true> : k_cc_slots<true, false>)
-                    : (iem ? k_cc_slots<false, true> : k_cc_slots<false, false>);
+  // (partitioned: the peer masks; gpeer and pmask both set)
+  auto* kern = (gpeer && pmask)
+                   ? (work ? (iem ? k_cc_slots<true, true, true> : k_cc_slots<true, false, true>)
+                           : (iem ? k_cc_slots<false, true, true> : k_cc_slots<false, false, true>))
+                   : (work ? (iem ? k_cc_slots<true, true, false> : k_cc_slots<true, false, false>)
+                           : (iem ? k_cc_slots<false, true, false> : k_cc_slots<false, false, false>));
   BatchParams bp0;
   if (!iem) std::memset(&bp0, 0, sizeof(bp0));
   kern<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
