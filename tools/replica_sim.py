@@ -1,7 +1,7 @@
 """One-GPU rehearsal of the C4 query on R full graph replicas (SURVEY.md §8(e) "Graph replicas ...
 with hop batches split across GPUs need zero exchange. Report both"): the 1B stream (or a prefix)
 is sealed once, and every replica's share of the 168 hops x 5 windows runs alone on the GPU, timed
-with a device synchronisation around it; the slowest replica is what R GPUs would take (no
+with the library's synchronous run call around it; the slowest replica is what R GPUs would take (no
 exchange: a replica's results are final for its views, and the summaries are concatenated).
 
 Two splits of the query's views:
@@ -35,15 +35,13 @@ WEIGHT = {0: 11.0, 1: 5.0, 2: 2.5, 3: 1.5, 4: 1.0}
 
 def timed(g, calls):
     """Run the calls [(hops, windows)] back to back; (ms of the runs, [summaries per call]).
-    A run returns with its results on the host; the summaries are read outside the timing."""
-    import torch
+    A run returns when its results are on the host (rgpu_run_view_batch is synchronous); the
+    summaries are read outside the timing."""
     ms = 0.0
     out = []
     for hops, wins in calls:
-        torch.cuda.synchronize()
         t = time.perf_counter()
         g.run("cc", hops, wins)
-        torch.cuda.synchronize()
         ms += (time.perf_counter() - t) * 1e3
         out.append(g.cc_summaries()[..., :7].copy())
     return ms, out
