@@ -245,7 +245,8 @@ struct rgpu_ctx {
   bool wmajor = true;                   // RGPU_WMAJOR: window-major batches when 2 <= W <= kMaxPlanes
   bool hostprof = false;                // RGPU_HOSTPROF: print host-side scheduling times
   int iv_max = 32;                      // RGPU_IVMAX: K1 interval form up to this many points (< 0 off)
-  int heavy_t = 2048;                   // RGPU_HEAVY: static slots above which a vertex is split (0 off)
+  int heavy_t = 2048;                   // static slots above which a vertex is split (hub_threshold)
+  int heavy_env = -1;                   // RGPU_HEAVY (0: off), or -1: hub_threshold's rule
   MaskSet mset[kMaskSets];
   int grp_last[kMaxPlanes] = {};        // supersteps of the last batch of each window group
   // last run: views (hop, win) -> batch (hop/K)*G + win/gsize, lane (win%gsize)*K + hop%K
@@ -1982,7 +1983,8 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->wmajor = env_int("RGPU_WMAJOR", 1) != 0;
   c->hostprof = env_int("RGPU_HOSTPROF", 0) != 0;
   c->iv_max = env_int("RGPU_IVMAX", 32);
-  c->heavy_t = env_int("RGPU_HEAVY", 2048);
+  c->heavy_env = env_int("RGPU_HEAVY", -1);
+  c->heavy_t = c->heavy_env >= 0 ? c->heavy_env : 2048;
   c->delta_on = env_int("RGPU_DELTA", 1) != 0;
   c->delta_host = env_int("RGPU_DELTA", 1) == 2;
   {  // RGPU_XREC_TINY (tests): record buffers start tiny, so that every growth path runs
@@ -2087,6 +2089,20 @@ void build_heavy_list(DevGraph& g, std::vector<void*>& L, const std::vector<int3
   g.seg_lo = dupload(L, seg_lo);
   g.seg_n = dupload(L, seg_n);
 }
+// The hub threshold (static slots): RGPU_HEAVY when set; else 2048 for one partition and, for a
+// partition of a vertex-partitioned graph, scaled with its owned vertices (2048 at 16M, at least
+// 256).  A superstep or K2 launch lasts as long as its slowest wave, and a wave walks a non-hub
+// member's slots one chunk after another: with a few owned vertices per wave (8 partitions) that
+// tail is the launch.  Measured on the 300M-update prefix at P = 8, slowest partition: 2048 ->
+// 118 ms, 512 -> 102, 256 -> 98, 128 -> 99, 64 -> 107 (profiles/r04/part_sim_heavy*.jsonl); the
+// 1B graph in one partition: 2048 273 ms, 512 286, 256 296 (hub passes grow).
+int hub_threshold(const rgpu_ctx* c, int64_t n_own) {
+  if (c->heavy_env >= 0) return c->heavy_env;
+  if (!c->partitioned) return 2048;
+  const int64_t t = (int64_t)2048 * n_own / ((int64_t)1 << 24);
+  return (int)std::max<int64_t>(256, std::min<int64_t>(2048, t));
+}
+
 void build_heavy(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L, const std::vector<int64_t>& out_off,
                  const std::vector<int64_t>& in_off) {
   if (c->heavy_t <= 0) return;
@@ -2387,6 +2403,7 @@ void seal_delta(rgpu_ctx* c, size_t n_end, Merged& M) {
         }
       }
       std::string e;
+      c->heavy_t = hub_threshold(c, B.n_own);  // (the partition's owned count before the merge)
       try {
         e = gpu_pack_delta(s, ev, n, g0, gvid, dp, c->heavy_t, &DD, T, L);
       } catch (const std::runtime_error& x) {
@@ -2701,6 +2718,7 @@ int rgpu_seal(rgpu_ctx* c) {
     g.adj_off = upload_adj(L, P.out_off, P.in_off);
     g.in_eid = dupload(L, P.in_eid);
     g.n_own = P.n_own;
+    c->heavy_t = hub_threshold(c, P.n_own);
     build_heavy(c, g, L, P.out_off, P.in_off);
     build_tslots(c, g, L);
     if (!c->partitioned && !P.grank.empty()) {  // locality order: labels are id ranks
