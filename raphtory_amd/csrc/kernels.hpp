@@ -314,20 +314,19 @@ void launch_xtab_fill(hipStream_t s, int64_t n, const int32_t* xr_v, const int32
                       const XTab& T, unsigned long long* err);
 // After superstep `step`: this partition's broadcast label records (xchg.hip: U records into su, at
 // most nb; M records into sm, cnt[1] counts past mcap so the host can grow and pack again)
-// The pack of a superstep's label records (xchg.hip k_xbc_pack): per unit of 512 owned ranks (eight
-// words of cb_now, the step's changed bits) a count pass (ccnt[q * nun + u] = U << 32 | M records
-// for peer q), a device scan into coff (ccnt[np * nun] must be 0), then the write pass into peer
-// q's regions su + q * ucap, sm + q * mcap.  write_only: coff is current (a repack into larger M
-// regions).  ccnt / coff hold xbc_units(n_own) * np + 1 words, scan_tmp xbc_scan_bytes(n_own, np).
+// The pack of a superstep's label records (xchg.hip k_xbc_pack): per 64-owned-rank chunk (one word
+// of cb_now, the step's changed bits) a count pass (ccnt[q * nch + c] = U << 32 | M records for
+// peer q), a device scan into coff (ccnt[np * nch] must be 0), then the write pass into peer q's
+// regions su + q * ucap, sm + q * mcap.  write_only: coff is current (a repack into larger M
+// regions).  ccnt / coff hold nch * np + 1 words, scan_tmp xbc_scan_bytes(n_own, np).
 size_t xbc_scan_bytes(int64_t n_own, int np);
-int64_t xbc_units(int64_t n_own);  // the pack's units (ccnt / coff hold units * np + 1 words)
 void launch_xbc_pack(hipStream_t s, int64_t n_own, int np, const XSend& X, const uint64_t* cb_now,
                      const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab, const int32_t* uw,
                      const uint8_t* pmask, unsigned long long* su, int64_t ucap, XRec* sm, int64_t mcap,
                      unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp, size_t scan_bytes,
                      bool write_only);
-// counts words (4 per peer): U records, M records (coff / nun: the pack's scan), the halting vote
-void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* coff, int64_t nun,
+// counts words (4 per peer): U records, M records (coff / nch: the pack's scan), the halting vote
+void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* coff, int64_t nch,
                        const int32_t* stepflag, int64_t* xa);
 // the per-view minimum member labels (mneg) folded into 64 words w / w stored back into shard 0
 // (partitioned final labels: the host all-reduces w with max in between)

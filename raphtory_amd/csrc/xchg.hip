@@ -110,19 +110,17 @@ __global__ __launch_bounds__(256) void k_xvm_unpack(int64_t nx, const int32_t* _
 //   M record (16 B, XRec): {b, label, views} per distinct new label of a mixed sender.
 // A sender's U records need at most nb slots (one per boundary vertex): U buffers are sized for the
 // worst case at plan time and never grow; M records (mixed senders: rare) grow on demand.
-// The pack runs in two passes over units of kPackWords x 64 consecutive owned ranks (a wave per
-// unit, lane = vertex of one 64-rank chunk at a time; one word of the step's changed bits per
-// chunk, so an unchanged chunk costs one scalar load): the count pass writes each (peer, unit)'s
-// U and M record counts (ccnt[q * nun + u] = U << 32 | M), a device scan turns them into offsets,
-// and the write pass puts the records in peer q's region (U at q * ucap, M at q * mcap).  (Units
-// of 512 ranks keep the scan short: it runs every superstep, mostly over nearly empty units.)  A changed boundary vertex is sent only to the peers in pmask: those
+// The pack runs in two passes over chunks of 64 consecutive owned ranks (lane = vertex; one word
+// of the step's changed bits per chunk, so an unchanged chunk costs one scalar load): the count
+// pass writes each (peer, chunk)'s U and M record counts (ccnt[q * nch + c] = U << 32 | M), a device
+// scan turns them into offsets, and the write pass puts the records in peer q's region (U at
+// q * ucap, M at q * mcap).  A changed boundary vertex is sent only to the peers in pmask: those
 // owning a ghost neighbour across one of its kept slots in the batch (K2) — no other partition's
 // vertex reads it in this batch (kept slots are symmetric: both sides compute em & vm & vm).  No
 // shared counter: one atomic per wave on a single address serialised at the memory side
 // (DESIGN.md §4 lesson 1).  A mixed sender's distinct labels are found on its row (lane = view);
 // rows of up to kRowsInFlight senders are loaded before any is folded.
 constexpr int kRowsInFlight = 4;
-constexpr int kPackWords = 8;
 __device__ __forceinline__ int distinct_labels(int32_t x, uint64_t mm, int lane) {
   int k = 0;
   while (mm) {
@@ -145,41 +143,58 @@ __global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, int np, const i
   const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t nch = (n_own + 63) >> 6, nun = (nch + kPackWords - 1) / kPackWords;
-  for (int64_t u0 = wave; u0 < nun; u0 += nwaves) {
-    // lane q: peer q's running counts (count pass) or offsets in its regions (write pass)
-    unsigned long long nu = 0, nm = 0;
-    if constexpr (WRITE) {
-      if (lane < np) {
-        const unsigned long long o = coff[(int64_t)lane * nun + u0], o0 = coff[(int64_t)lane * nun];
-        nu = (o >> 32) - (o0 >> 32);
-        nm = (o & 0xffffffffull) - (o0 & 0xffffffffull);
-      }
+  const int64_t nch = (n_own + 63) >> 6;
+  for (int64_t c = wave; c < nch; c += nwaves) {
+    const uint64_t w = cb_now[c];  // (wave-uniform: a scalar load)
+    if (w == 0) {
+      if (!WRITE && lane < np) ccnt[(int64_t)lane * nch + c] = 0;
+      continue;
     }
-    const int64_t c1 = (u0 + 1) * kPackWords < nch ? (u0 + 1) * kPackWords : nch;
-    for (int64_t c = u0 * kPackWords; c < c1; c++) {
-      const uint64_t w = cb_now[c];  // (wave-uniform: a scalar load)
-      if (w == 0) continue;
-      const int64_t v = c * 64 + lane;
-      const bool chd = ((w >> lane) & 1) && v < n_own;
-      const int32_t b = chd ? bidx[v] : -1;
-      const uint64_t m = b >= 0 ? chg_now[v] & vadj[v] : 0;
-      const uint32_t pm = m ? pmask[v] : 0u;
-      const int32_t u = pm ? uw_label(uw[v]) : kMixed;
-      const bool full = pm != 0 && u != kMixed;  // a uniform sender: one U record per peer in pm
+    const int64_t v = c * 64 + lane;
+    const bool ch = ((w >> lane) & 1) && v < n_own;
+    const int32_t b = ch ? bidx[v] : -1;
+    const uint64_t m = b >= 0 ? chg_now[v] & vadj[v] : 0;
+    const uint32_t pm = m ? pmask[v] : 0u;
+    const int32_t u = pm ? uw_label(uw[v]) : kMixed;
+    const bool full = pm != 0 && u != kMixed;  // a uniform sender: one U record per peer in pm
+    const uint64_t mixed0 = __ballot(pm != 0 && u == kMixed);
+    if constexpr (!WRITE) {
+      unsigned long long nm = 0;  // lane q: M records for peer q
+      for (uint64_t mixed = mixed0; mixed;) {
+        int Ls[kRowsInFlight];
+        int32_t x[kRowsInFlight];
+        int k = 0;
+        for (; k < kRowsInFlight && mixed; k++, mixed &= mixed - 1) Ls[k] = __builtin_ctzll(mixed);
+        for (int i = 0; i < k; i++) x[i] = lab[(c * 64 + Ls[i]) * 64 + lane];
+        for (int i = 0; i < k; i++) {
+          const int d = distinct_labels(x[i], rl64(m, Ls[i]), lane);
+          const uint32_t pL = (uint32_t)__builtin_amdgcn_readlane((int)pm, Ls[i]);
+          if (lane < np && ((pL >> lane) & 1)) nm += (unsigned long long)d;
+        }
+      }
+      unsigned long long nu = 0;
+      for (int q = 0; q < np; q++) {
+        const unsigned long long cq = (unsigned long long)__popcll(__ballot(full && ((pm >> q) & 1)));
+        if (lane == q) nu = cq;
+      }
+      if (lane < np) ccnt[(int64_t)lane * nch + c] = (nu << 32) | nm;
+    } else {
+      unsigned long long uo = 0, mo = 0;  // lane q: peer q's offsets in its regions
+      if (lane < np) {
+        const unsigned long long o = coff[(int64_t)lane * nch + c], o0 = coff[(int64_t)lane * nch];
+        uo = (o >> 32) - (o0 >> 32);
+        mo = (o & 0xffffffffull) - (o0 & 0xffffffffull);
+      }
       for (int q = 0; q < np; q++) {
         const bool mine = full && ((pm >> q) & 1);
         const uint64_t bu = __ballot(mine);
         if (!bu) continue;
-        if constexpr (WRITE) {
-          const unsigned long long base = (unsigned long long)__builtin_amdgcn_readlane((int)(uint32_t)nu, q);
-          if (mine)
-            su[(int64_t)q * ucap + (int64_t)(base + __popcll(bu & lanemask_below(lane)))] =
-                ((unsigned long long)(uint32_t)b << 32) | (uint32_t)u;
-        }
-        if (lane == q) nu += (unsigned long long)__popcll(bu);
+        const unsigned long long base = (unsigned long long)__builtin_amdgcn_readlane((int)(uint32_t)uo, q);
+        if (mine)
+          su[(int64_t)q * ucap + (int64_t)(base + __popcll(bu & lanemask_below(lane)))] =
+              ((unsigned long long)(uint32_t)b << 32) | (uint32_t)u;
       }
-      for (uint64_t mixed = __ballot(pm != 0 && u == kMixed); mixed;) {  // rows, kRowsInFlight at a time
+      for (uint64_t mixed = mixed0; mixed;) {
         int Ls[kRowsInFlight];
         int32_t x[kRowsInFlight];
         int k = 0;
@@ -187,27 +202,21 @@ __global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, int np, const i
         for (int i = 0; i < k; i++) x[i] = lab[(c * 64 + Ls[i]) * 64 + lane];
         for (int i = 0; i < k; i++) {
           const uint64_t mL = rl64(m, Ls[i]);
+          const int32_t bL = __builtin_amdgcn_readlane(b, Ls[i]);
           const uint32_t pL = (uint32_t)__builtin_amdgcn_readlane((int)pm, Ls[i]);
-          if constexpr (!WRITE) {
-            const int d = distinct_labels(x[i], mL, lane);
-            if (lane < np && ((pL >> lane) & 1)) nm += (unsigned long long)d;
-          } else {
-            const int32_t bL = __builtin_amdgcn_readlane(b, Ls[i]);
-            for (uint64_t mm = mL; mm;) {
-              const int32_t val = __builtin_amdgcn_readlane(x[i], __builtin_ctzll(mm));
-              const uint64_t same = __ballot(((mm >> lane) & 1) && x[i] == val);
-              mm &= ~same;
-              if (lane < np && ((pL >> lane) & 1)) {  // lane q writes peer q's copy
-                if (nm < (unsigned long long)mcap) sm[(int64_t)lane * mcap + (int64_t)nm] = XRec{bL, val, same};
-                nm++;
-              }
+          for (uint64_t mm = mL; mm;) {
+            const int32_t val = __builtin_amdgcn_readlane(x[i], __builtin_ctzll(mm));
+            const uint64_t same = __ballot(((mm >> lane) & 1) && x[i] == val);
+            mm &= ~same;
+            // lane q < np writes peer q's copy
+            if (lane < np && ((pL >> lane) & 1)) {
+              if (mo < (unsigned long long)mcap) sm[(int64_t)lane * mcap + (int64_t)mo] = XRec{bL, val, same};
+              mo++;
             }
           }
         }
       }
     }
-    if constexpr (!WRITE)
-      if (lane < np) ccnt[(int64_t)lane * nun + u0] = (nu << 32) | nm;
   }
 }
 
@@ -777,9 +786,8 @@ void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32
                        int planes, const uint64_t* in, uint64_t* vm, int64_t vstride) {
   if (nx > 0) k_xvm_unpack<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, xq, xoff, planes, in, vm, vstride);
 }
-int64_t xbc_units(int64_t n_own) { return (((n_own + 63) >> 6) + kPackWords - 1) / kPackWords; }
 size_t xbc_scan_bytes(int64_t n_own, int np) {
-  const int n = (int)(xbc_units(n_own) * np + 1);
+  const int n = (int)(((n_own + 63) >> 6) * np + 1);
   size_t tb = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr, n);
   return tb;
@@ -790,13 +798,13 @@ void launch_xbc_pack(hipStream_t s, int64_t n_own, int np, const XSend& X, const
                      unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp, size_t scan_bytes,
                      bool write_only) {
   if (X.nb <= 0 || n_own <= 0) return;
-  const int64_t nun = xbc_units(n_own);
-  const unsigned grid = xgrid(nun, 4, 4096);
+  const int64_t nch = (n_own + 63) >> 6;
+  const unsigned grid = xgrid(nch, 4, 4096);
   if (!write_only) {
     k_xbc_pack<false><<<grid, 256, 0, s>>>(n_own, np, X.bidx, cb_now, chg_now, vadj, lab, uw, pmask, su, ucap, sm, mcap,
                                            ccnt, coff);
-    // ccnt[np * nun] stays 0: coff[q * nun] .. coff[(q + 1) * nun] = peer q's records
-    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ccnt, coff, (int)(nun * np + 1), s) != hipSuccess)
+    // ccnt[np * nch] stays 0: coff[q * nch] .. coff[(q + 1) * nch] = peer q's records
+    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ccnt, coff, (int)(nch * np + 1), s) != hipSuccess)
       throw std::runtime_error("xbc pack: scan");
   }
   k_xbc_pack<true><<<grid, 256, 0, s>>>(n_own, np, X.bidx, cb_now, chg_now, vadj, lab, uw, pmask, su, ucap, sm, mcap,
