@@ -1250,7 +1250,7 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
                                                     const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
                                                     uint64_t* __restrict__ cb_next, uint64_t* __restrict__ cb_clear,
                                                     int64_t cb_words, int32_t* __restrict__ ccount, int dense_div, int gmax,
-                                                    const int32_t* __restrict__ mneg, int ab) {
+                                                    const int32_t* __restrict__ mneg) {
   if (stepflag[step - 1] == 0) return;
   const int lane = lane_id();
   const bool use_fin = mneg != nullptr && uw_cur != nullptr;
@@ -1325,59 +1325,48 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
     int32_t my_w = 0;
     bool has_w = false;
     uint64_t pend = todo;
-    // A pack (members in lane order while their slots fit 64 lanes): built, its loads issued (slot,
-    // neighbour word, mixed neighbours' change words), then folded per member.  With ab & 2 two packs
-    // are in flight: the second pack's loads are issued before the first is folded.
-    struct Pack {
+    while (pend) {
+      // the next pack: members in lane order while their slots fit 64 lanes
       uint64_t pack = 0;
-      int32_t nbp = 0, unp = kMixed;
-      uint64_t smp = 0, act = 0;
-    };
-    auto build = [&](Pack& P) {
       int sum = 0, myL = 0, myj = 0;
-      P.pack = 0;
       while (pend) {
         const int Lp = __builtin_ctzll(pend);
         const int k = __builtin_amdgcn_readlane(n, Lp);
-        if (P.pack && sum + k > 64) break;
+        if (pack && sum + k > 64) break;
         if (lane >= sum && lane < sum + k) { myL = Lp; myj = lane - sum; }
-        P.pack |= 1ull << Lp;
+        pack |= 1ull << Lp;
         sum += k;
         pend &= pend - 1;
       }
       const bool on = lane < sum;
-      // lane = slot: the slot (vertex 0's for idle lanes: masked by sm = 0)
+      // lane = slot: the slot, then the neighbour's word (vertex 0's for idle lanes: masked by sm = 0)
       const int64_t bmy = (int64_t)(((uint64_t)(uint32_t)__shfl((int)((uint64_t)base >> 32), myL) << 32) |
                                     (uint32_t)__shfl((int)base, myL));
       const int64_t idx = on ? bmy + myj : 0;
       const int32_t q = snbr[idx];
       const uint64_t m = smask[idx];
-      P.nbp = on ? q : 0;
-      P.smp = on ? m : 0;
-    };
-    auto words = [&](Pack& P) {  // the neighbour's word, and a mixed neighbour's change word
-      P.act = 0;
-      P.unp = kMixed;
+      const int32_t nbp = on ? q : 0;
+      const uint64_t smp = on ? m : 0;
+      uint64_t act = 0;
+      int32_t unp = kMixed;
       if (uw_cur) {
-        const int32_t w = uw_cur[P.nbp];
-        P.act = (w != kMixed && w < 0) ? P.smp : 0;
-        P.unp = w == kMixed ? kMixed : (w & 0x7fffffff);
-        const bool mx = w == kMixed && P.smp != 0;
+        const int32_t w = uw_cur[nbp];
+        act = (w != kMixed && w < 0) ? smp : 0;
+        unp = w == kMixed ? kMixed : (w & 0x7fffffff);
+        const bool mx = w == kMixed && smp != 0;
         const uint64_t mixed = __ballot(mx);
         if (mixed) {
-          const uint64_t cw = chg_prev[mx ? P.nbp : 0];
-          if (mx) P.act = P.smp & cw;
+          const uint64_t cw = chg_prev[mx ? nbp : 0];
+          if (mx) act = smp & cw;
           wk.a += __popcll(mixed);
         }
       } else {
-        P.act = P.smp & chg_prev[P.nbp];
+        act = smp & chg_prev[nbp];
       }
-      wk.g += P.unp == kMixed ? __popcll(P.act) : 0;
-    };
-    auto fold = [&](const Pack& P) {
+      wk.g += unp == kMixed ? __popcll(act) : 0;
       uint64_t markp = 0;  // lane = slot: its neighbour joins the next frontier
       int pre = 0;
-      for (uint64_t pk = P.pack; pk; pk &= pk - 1) {
+      for (uint64_t pk = pack; pk; pk &= pk - 1) {
         const int L = __builtin_ctzll(pk);
         const int k = __builtin_amdgcn_readlane(n, L);
         const uint64_t span = k == 0 ? 0ull : ((k >= 64 ? ~0ull : ((1ull << k) - 1)) << pre);
@@ -1395,12 +1384,8 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
         }
         cur = mem ? cur : INT32_MAX;
         const bool inspan = (span >> lane) & 1;
-        int32_t best = gather_min<BUF>(inspan && P.unp == kMixed ? P.act : 0, P.nbp, cur, lab_cur, lane);
-        if (uw_cur) {
-          const uint64_t ub = __ballot(inspan && P.unp != kMixed && P.act != 0);
-          best = (ab & 1) ? fold_uniform_by_label(ub, P.act, P.unp, best, lane)
-                          : fold_uniform(ub, P.act, P.unp, best, lane);
-        }
+        int32_t best = gather_min<BUF>(inspan && unp == kMixed ? act : 0, nbp, cur, lab_cur, lane);
+        if (uw_cur) best = fold_uniform(__ballot(inspan && unp != kMixed && act != 0), act, unp, best, lane);
         const int32_t hL = __builtin_amdgcn_readlane(hh, L);
         if (hL >= 0) {  // a hub: the step's minima over its segments (k_heavy_gather), reset for the next step
           const int32_t x = hbest[(int64_t)hL * 64 + lane];
@@ -1427,28 +1412,10 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
         if (ch) {
           lanes_or |= ch;
           changed++;
-          if (inspan && (P.smp & ch)) markp = 1;
+          if (inspan && (smp & ch)) markp = 1;
         }
       }
-      if (!skip_marks && markp) act_next[P.nbp] = 1;
-    };
-    if (ab & 2) {
-      while (pend) {
-        Pack A, B;
-        build(A);
-        if (pend) build(B);
-        words(A);
-        if (B.pack) words(B);
-        fold(A);
-        if (B.pack) fold(B);
-      }
-    } else {
-      while (pend) {
-        Pack A;
-        build(A);
-        words(A);
-        fold(A);
-      }
+      if (!skip_marks && markp) act_next[nbp] = 1;
     }
     // the round's members, lane-parallel: words, change words, own frontier flags, changed bits
     if (mine) {
@@ -2398,12 +2365,6 @@ constexpr int kDealSlots = 16;
 // supersteps >= kLateStep have small frontiers: at most kLateGrid blocks, the GPU left to the other batches
 constexpr int kLateStep = 14, kLateGrid = 1024;
 
-// (A/B, temporary) RGPU_AB bits: 1 superstep folds uniform neighbours by label, 2 two packs in flight
-static int ab_flags() {
-  const char* e = std::getenv("RGPU_AB");
-  return e ? std::atoi(e) : 0;
-}
-
 static unsigned grid_for(int64_t items, int per_block, unsigned cap = 8192) {
   int64_t g = (items + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -2491,7 +2452,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   // C4 serial cc_step 207.6 -> 155.1 ms, query 343 -> 286 ms.
 #define RGPU_PK_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr, ab_flags()
+    cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr
   const unsigned gridp = grid_for(g.nv, 256, cap);
   if (work) k_cc_step_pk<false, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
   else k_cc_step_pk<false, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
