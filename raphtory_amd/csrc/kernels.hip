@@ -1385,7 +1385,7 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
         cur = mem ? cur : INT32_MAX;
         const bool inspan = (span >> lane) & 1;
         int32_t best = gather_min<BUF>(inspan && unp == kMixed ? act : 0, nbp, cur, lab_cur, lane);
-        if (uw_cur) best = fold_uniform(__ballot(inspan && unp != kMixed && act != 0), act, unp, best, lane);
+        if (uw_cur) best = fold_uniform_by_label(__ballot(inspan && unp != kMixed && act != 0), act, unp, best, lane);
         const int32_t hL = __builtin_amdgcn_readlane(hh, L);
         if (hL >= 0) {  // a hub: the step's minima over its segments (k_heavy_gather), reset for the next step
           const int32_t x = hbest[(int64_t)hL * 64 + lane];
