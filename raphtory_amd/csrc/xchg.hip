@@ -401,17 +401,23 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
       uw[g] = uw_word(val, true);
       if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // (ChgBits)
     }
-    for (uint64_t bb = __ballot(g >= 0 && !isu); bb; bb &= bb - 1) {
+    // M records: a record with few views writes its row lanes itself; one with many, the wave
+    // (lane = view), one record at a time
+    const bool mrec = g >= 0 && !isu;
+    const bool wide = mrec && __popcll(mask) > 8;
+    if (mrec) {
+      uw[g] = kMixed;
+      atomicOr((unsigned long long*)&chg[g], (unsigned long long)mask);
+      if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));
+      if (!wide)
+        for (uint64_t mm = mask; mm; mm &= mm - 1) lab[(int64_t)g * 64 + __builtin_ctzll(mm)] = val;
+    }
+    for (uint64_t bb = __ballot(wide); bb; bb &= bb - 1) {
       const int L = __builtin_ctzll(bb);
       const int32_t gL = __builtin_amdgcn_readlane(g, L);
       const int32_t vL = __builtin_amdgcn_readlane(val, L);
       const uint64_t mL = rl64(mask, L);
       if ((mL >> lane) & 1) lab[(int64_t)gL * 64 + lane] = vL;
-      if (lane == 0) {
-        uw[gL] = kMixed;
-        atomicOr((unsigned long long*)&chg[gL], (unsigned long long)mL);
-        if (cb) atomicOr((unsigned long long*)&cb[gL >> 6], 1ull << (gL & 63));
-      }
     }
     if (!do_mark) continue;
     // mark: lane = record, its ghost when it is the ghost's first record and the ghost is no hub
