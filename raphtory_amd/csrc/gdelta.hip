@@ -1005,10 +1005,13 @@ std::string gpu_part_meta(hipStream_t s, const int64_t* keys, int64_t nv, int64_
   // bucket; rgpu_seal's full-seal index)
   X.own_vid = M.alloc<int64_t>(n_own, true);
   if (n_own) GCHK(hipMemcpyAsync(X.own_vid, keys, sizeof(int64_t) * n_own, hipMemcpyDeviceToDevice, s));
-  int lg = 0;
-  while (((int64_t)1 << lg) < std::max<int64_t>(n_own, 1)) lg++;
-  X.shift = std::max(0, 31 - lg);
-  const int64_t nbk = ((int64_t)1 << 31) >> X.shift;
+  X.id_max = -1;
+  if (n_own) {
+    GCHK(hipMemcpyAsync(&X.id_max, keys + n_own - 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    GCHK(hipStreamSynchronize(s));
+  }
+  X.shift = own_bucket_shift(n_own, X.id_max);
+  const int64_t nbk = (std::max<int64_t>(X.id_max, 0) >> X.shift) + 1;
   int32_t* cnt = M.alloc<int32_t>(nbk + 1);
   GCHK(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (nbk + 1), s));
   if (n_own) k_bucket_counts<<<gridn(n_own), kB, 0, s>>>(n_own, X.own_vid, X.shift, cnt);

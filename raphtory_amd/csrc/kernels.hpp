@@ -356,11 +356,21 @@ void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg
 // [boff[b], boff[b+1]) (about one id per bucket)
 struct OwnIdx {
   const int64_t* vid = nullptr;   // owned ids ascending
-  const int32_t* boff = nullptr;
+  const int32_t* boff = nullptr;  // bucket b = id >> shift: vid[boff[b] .. boff[b + 1])
   const int32_t* pos = nullptr;   // local rank of the k-th owned id (null: k itself)
   int shift = 0;
   int64_t n_own = 0;
+  int64_t id_max = -1;            // the largest owned id (the buckets cover [0, id_max])
 };
+// bucket shift of an OwnIdx: about one owned id per bucket over the ids' range [0, id_max] (not
+// [0, 2^31): ids packed densely below 2^31 would otherwise put dozens of owned ids in a bucket, a
+// serial walk of dependent loads per lookup)
+inline int own_bucket_shift(int64_t n_own, int64_t id_max) {
+  int lg = 0, bits = 0;
+  while (((int64_t)1 << lg) < (n_own > 1 ? n_own : 1)) lg++;
+  while (bits < 62 && (id_max >> bits) > 0) bits++;
+  return bits > lg ? bits - lg : 0;
+}
 // component counts of the owned members (xchg.hip k_part_count): owned labels counted at their
 // count rows (counts[local rank][view]), the others routed to the label owners (remote_only: the
 // records again, into a larger buffer, without the local counts); gcnt[q] counts every record for
@@ -472,8 +482,9 @@ struct PartMeta {
   std::vector<int64_t> xs_off, xr_off;
   int64_t nxs = 0, nxr = 0;
   int64_t* own_vid = nullptr;                   // owned ids ascending
-  int32_t* own_boff = nullptr;                  // their buckets (id >> shift)
+  int32_t* own_boff = nullptr;                  // their buckets (id >> shift, own_bucket_shift)
   int shift = 0;
+  int64_t id_max = -1;
 };
 std::string gpu_part_meta(hipStream_t s, const int64_t* keys, int64_t nv, int64_t n_own, const int32_t* esrc,
                           const int32_t* edst, int64_t ne, int nparts, PartMeta* out, std::vector<void*>& T,

@@ -1702,6 +1702,11 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
     HIPCHK(hipMemsetAsync(xs.htot, 0, sizeof(unsigned long long) * kMaxParts, s.stream));
   }
   grow_regions(&xs.hrbuf, xs.hrcap, recv, P, s.stream);
+  if (!c->trace_path.empty()) {  // trace: step -1 = the batch's count records (pv sent, ps received)
+    unsigned long long ts = 0, tr = 0;
+    for (int q = 0; q < P; q++) ts += sent[q], tr += recv[q];
+    c->steprec.push_back({s.batch, -1, ts, tr, 0, 0});
+  }
   {
     const XPeers Ls = peers_layout(c, xs.hscap, X.xs_off, nullptr);
     const XPeers Lr = peers_layout(c, xs.hrcap, X.xr_off, nullptr);
@@ -2257,6 +2262,7 @@ void apply_merged(rgpu_ctx* c, Merged& M) {
     X.own.boff = PM.own_boff;
     X.own.shift = PM.shift;
     X.own.n_own = g.n_own;
+    X.own.id_max = PM.id_max;
     c->orph_id.swap(M.orph_id);
     c->orph_t.swap(M.orph_t);
   }
@@ -2746,10 +2752,9 @@ int rgpu_seal(rgpu_ctx* c) {
          // about one id per bucket
         std::vector<int64_t> ids((size_t)P.n_own);
         for (int64_t k = 0; k < P.n_own; k++) ids[k] = P.vid[P.by_id.empty() ? k : P.by_id[k]];
-        int lg = 0;
-        while (((int64_t)1 << lg) < std::max<int64_t>(P.n_own, 1)) lg++;
-        const int shift = std::max(0, 31 - lg);
-        const int64_t nbk = ((int64_t)1 << 31) >> shift;
+        const int64_t id_max = ids.empty() ? -1 : *std::max_element(ids.begin(), ids.end());
+        const int shift = own_bucket_shift(P.n_own, id_max);
+        const int64_t nbk = (std::max<int64_t>(id_max, 0) >> shift) + 1;
         std::vector<int32_t> boff(nbk + 1, 0);
         for (int64_t k = 0; k < P.n_own; k++) boff[(ids[k] >> shift) + 1]++;
         for (int64_t b = 0; b < nbk; b++) boff[b + 1] += boff[b];
@@ -2758,6 +2763,7 @@ int rgpu_seal(rgpu_ctx* c) {
         X.own.boff = dupload(L, boff);
         X.own.shift = shift;
         X.own.n_own = P.n_own;
+        X.own.id_max = id_max;
       }
     }
     c->g = g;

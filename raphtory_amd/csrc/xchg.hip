@@ -48,7 +48,7 @@ __device__ __forceinline__ int peer_of(const XPeers& P, int64_t i) {
 }
 // rank of owned vertex `id`, or -1 (bucket index: about one probe)
 __device__ __forceinline__ int64_t owned_rank(const OwnIdx& I, int64_t id) {
-  if (id < 0 || id >= ((int64_t)1 << 31)) return -1;  // (the buckets cover the id range [0, 2^31))
+  if (id < 0 || id > I.id_max) return -1;  // (the buckets cover [0, id_max])
   const int64_t b = id >> I.shift;
   for (int64_t i = I.boff[b], e = I.boff[b + 1]; i < e; i++)
     if (I.vid[i] == id) return i;
@@ -705,34 +705,71 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
 }
 
 // records received from the other partitions: counted at the owned label vertex's row (lane =
-// record for the lookups, then lane = view per record)
+// record for the lookups, then lane = view per record).  A label whose members sit on every
+// partition (a big component that is not its views' minimum label, k_part_count fin_acc) arrives
+// as records from every wave of every sender, all for one count row: a wave folds its records'
+// counts in a private LDS cache keyed by row first (16 rows), so a hot row costs one global atomic
+// per (wave, view) instead of one per record and view (the per-address atomics serialise at the
+// memory side: 2-5 ms per batch on the owner before, profiles/r04/part_sim_p8_hist_trace.txt).
+// One chunk of 64 records per wave: the lookups are dependent loads, and chunks walked in turn by
+// one wave serialise them.
 __global__ __launch_bounds__(256) void k_hist_recv(XPeers P, const XRec* __restrict__ rbuf, OwnIdx I,
                                                    int32_t* __restrict__ counts) {
+  constexpr int kRows = 16;
+  __shared__ int32_t ckey_s[4][kRows];
+  __shared__ int32_t crow_s[4][kRows][64];
+  const int lane = lane_of(), wib = threadIdx.x >> 6;
+  int32_t* ckey = ckey_s[wib];
+  if (lane < kRows) ckey[lane] = -1;
+  for (int h = 0; h < kRows; h++) crow_s[wib][h][lane] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // per lane: view j of count row `row` takes c (cached when the row has or gets a cache row; the
+  // rows are indexed through the __shared__ array itself, so that the add stays an LDS atomic — a
+  // flat one waits for the wave's outstanding global atomics)
+  auto add = [&](int32_t row, int j, int32_t c) {
+    const int h0 = (int)(((uint32_t)row * 2654435761u) >> 28);
+    for (int p = 0; p < 4; p++) {
+      const int h = (h0 + p) & (kRows - 1);
+      int32_t k = ckey[h];
+      if (k == -1) {
+        k = atomicCAS(&ckey[h], -1, row);
+        if (k == -1) k = row;
+      }
+      if (k == row) {
+        atomicAdd(&crow_s[wib][h][j], c);
+        return;
+      }
+    }
+    atomicAdd(&counts[(int64_t)row * 64 + j], c);
+  };
   const int64_t n = P.pre[P.np];
-  const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t i0 = wave * 64; i0 < n; i0 += nwaves * 64) {
     const int64_t i = i0 + lane;
-    int64_t row = -1;
+    int32_t row = -1;
     XRec r{0, 0, 0};
     if (i < n) {
       const int q = peer_of(P, i);
       r = rbuf[P.base[q] + i - P.pre[q]];
-      row = label_row(I, r.e);
+      row = (int32_t)label_row(I, r.e);  // (< n_own < 2^31)
     }
     // a record with few views: its lane adds them; many views: the wave adds its row (lane = view)
     const bool wide = row >= 0 && __popcll(r.mask) > 8;
-    for (uint64_t m = (row >= 0 && !wide) ? r.mask : 0ull; m; m &= m - 1)
-      atomicAdd(&counts[row * 64 + __builtin_ctzll(m)], r.val);
+    for (uint64_t m = (row >= 0 && !wide) ? r.mask : 0ull; m; m &= m - 1) add(row, __builtin_ctzll(m), r.val);
     for (uint64_t t = __ballot(wide); t; t &= t - 1) {
       const int L = __builtin_ctzll(t);
-      const int64_t rowL = (int64_t)rl64((uint64_t)row, L);
+      const int32_t rowL = __builtin_amdgcn_readlane(row, L);
       const uint64_t mL = rl64(r.mask, L);
       const int32_t cL = __builtin_amdgcn_readlane(r.val, L);
-      if ((mL >> lane) & 1) atomicAdd(&counts[rowL * 64 + lane], cL);
+      if ((mL >> lane) & 1) add(rowL, lane, cL);
     }
-
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  for (int h = 0; h < kRows; h++) {
+    const int32_t k = ckey[h];
+    const int32_t c = crow_s[wib][h][lane];
+    if (k != -1 && c) atomicAdd(&counts[(int64_t)k * 64 + lane], c);
   }
 }
 
@@ -886,7 +923,10 @@ void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const O
                        unsigned int* iso, unsigned long long* gcnt, XRec* hsbuf, const int32_t* mneg,
                        unsigned int* fin_g) {
   const uint64_t vmask = nviews >= 64 ? ~0ull : ((1ull << nviews) - 1);
-  const unsigned grid = xgrid(I.n_own, 256, 2048);
+  // 16 chunks of 64 members per wave: a wave flushes its label cache once, as records, so fewer
+  // waves emit fewer records (one per cached label and count group) and flush less (grid 2048 ->
+  // 512 at 2.2M members: 7.3 -> 5.0 ms per partition and query, profiles/r04/ab_part_count_grid.jsonl)
+  const unsigned grid = xgrid(I.n_own, 256 * 16, 2048);
   if (remote_only)
     k_part_count<true><<<grid, 256, 0, s>>>(P, I, vmask, vm, vadj, uw, lab, counts, iso, gcnt, hsbuf, mneg, fin_g);
   else
