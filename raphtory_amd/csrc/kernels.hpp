@@ -354,6 +354,19 @@ void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg
                       const BatchParams* ebp, const int32_t* ccount, int dense_div, int step);
 // owned id -> owned rank: ids ascend with rank; bucket b = id >> shift covers ranks
 // [boff[b], boff[b+1]) (about one id per bucket)
+// Work units of the record pack and the partitioned counts (xchg.hip): chunks of 64 consecutive owned
+// ranks, except the first kSplitChunks chunks, each split kSplitWays ways by mixed member.  Owned
+// ranks are in activity order (packer.cpp locality_order), so those chunks hold the partition's
+// hubs, which are mostly mixed: one wave walking 64 hub rows in turn was the whole launch (0.8 ms
+// of a year batch's count kernel, 0.3-0.4 ms of a record pack pass, profiles/r04).  Unit u < hs *
+// kSplitWays: chunk u / kSplitWays, the mixed members whose index among the chunk's mixed members
+// is u % kSplitWays (mod kSplitWays), and the uniform ones with sub-unit 0; after that one unit per
+// chunk.
+constexpr int kSplitChunks = 128, kSplitWays = 16;
+__host__ __device__ inline int64_t xbc_units(int64_t n_own) {
+  const int64_t nch = (n_own + 63) >> 6, hs = nch < kSplitChunks ? nch : kSplitChunks;
+  return nch + hs * (kSplitWays - 1);
+}
 struct OwnIdx {
   const int64_t* vid = nullptr;   // owned ids ascending
   const int32_t* boff = nullptr;  // bucket b = id >> shift: vid[boff[b] .. boff[b + 1])

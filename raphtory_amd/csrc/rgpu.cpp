@@ -1375,9 +1375,9 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
       xs.ru_cap = std::max<int64_t>(X.tab.toff[P], 1);
       HIPCHK(hipMalloc((void**)&xs.su, sizeof(unsigned long long) * (size_t)xs.su_cap * P));
       for (int p = 0; p < 2; p++) HIPCHK(hipMalloc((void**)&xs.ru[p], sizeof(unsigned long long) * (size_t)xs.ru_cap));
-      // the pack's per-(peer, chunk) counts and offsets (ccnt[P * nch] stays 0)
-      const int64_t no = c->pk.n_own, nch = (no + 63) / 64;
-      const size_t nck = (size_t)(nch * P + 1);
+      // the pack's per-(peer, unit) counts and offsets (ccnt[P * units] stays 0)
+      const int64_t no = c->pk.n_own;
+      const size_t nck = (size_t)(xbc_units(no) * P + 1);
       HIPCHK(hipMalloc((void**)&xs.ccnt, sizeof(unsigned long long) * nck));
       HIPCHK(hipMalloc((void**)&xs.coff, sizeof(unsigned long long) * nck));
       HIPCHK(hipMemset(xs.ccnt, 0, sizeof(unsigned long long) * nck));
@@ -1510,7 +1510,7 @@ void part_post_step(rgpu_ctx* c, int si, const RunCfg& rc, int r) {
     return;
   }
   part_pack(c, si, r);
-  launch_xbc_counts(s.stream, P, c->part, X.xsend.nb > 0 ? xs.coff : nullptr, (c->pk.n_own + 63) / 64, s.stepcnt + r,
+  launch_xbc_counts(s.stream, P, c->part, X.xsend.nb > 0 ? xs.coff : nullptr, xbc_units(c->pk.n_own), s.stepcnt + r,
                     xs.xab);
   HIPCHK(hipGetLastError());
   xs.x->alltoall_i64(xs.xab, xs.xab + 4 * P, 4, s.stream);

@@ -110,9 +110,10 @@ __global__ __launch_bounds__(256) void k_xvm_unpack(int64_t nx, const int32_t* _
 //   M record (16 B, XRec): {b, label, views} per distinct new label of a mixed sender.
 // A sender's U records need at most nb slots (one per boundary vertex): U buffers are sized for the
 // worst case at plan time and never grow; M records (mixed senders: rare) grow on demand.
-// The pack runs in two passes over chunks of 64 consecutive owned ranks (lane = vertex; one word
-// of the step's changed bits per chunk, so an unchanged chunk costs one scalar load): the count
-// pass writes each (peer, chunk)'s U and M record counts (ccnt[q * nch + c] = U << 32 | M), a device
+// The pack runs in two passes over units (kernels.hpp xbc_units: chunks of 64 consecutive owned
+// ranks, the hub chunks split by mixed member; lane = vertex; one word of the step's changed bits
+// per chunk, so an unchanged chunk costs one scalar load): the count pass writes each (peer,
+// unit)'s U and M record counts (ccnt[q * units + u] = U << 32 | M), a device
 // scan turns them into offsets, and the write pass puts the records in peer q's region (U at
 // q * ucap, M at q * mcap).  A changed boundary vertex is sent only to the peers in pmask: those
 // owning a ghost neighbour across one of its kept slots in the batch (K2) — no other partition's
@@ -121,6 +122,24 @@ __global__ __launch_bounds__(256) void k_xvm_unpack(int64_t nx, const int32_t* _
 // (DESIGN.md §4 lesson 1).  A mixed sender's distinct labels are found on its row (lane = view);
 // rows of up to kRowsInFlight senders are loaded before any is folded.
 constexpr int kRowsInFlight = 4;
+// unit -> (chunk, sub-unit; -1: the whole chunk) (kernels.hpp xbc_units)
+__device__ __forceinline__ int64_t unit_chunk(int64_t un, int64_t nch, int& sub) {
+  const int64_t hs = nch < kSplitChunks ? nch : kSplitChunks;
+  if (un < hs * kSplitWays) {
+    sub = (int)(un % kSplitWays);
+    return un / kSplitWays;
+  }
+  sub = -1;
+  return hs + (un - hs * kSplitWays);
+}
+// the mixed members (lane mask) a sub-unit takes: every kSplitWays-th, from the sub-th (wave-uniform)
+__device__ __forceinline__ uint64_t split_rows(uint64_t m, int sub) {
+  if (sub < 0) return m;
+  uint64_t r = 0;
+  for (int k = 0; m; m &= m - 1, k++)
+    if (k % kSplitWays == sub) r |= m & (~m + 1);
+  return r;
+}
 __device__ __forceinline__ int distinct_labels(int32_t x, uint64_t mm, int lane) {
   int k = 0;
   while (mm) {
@@ -143,11 +162,13 @@ __global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, int np, const i
   const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t nch = (n_own + 63) >> 6;
-  for (int64_t c = wave; c < nch; c += nwaves) {
+  const int64_t nch = (n_own + 63) >> 6, nun = xbc_units(n_own);
+  for (int64_t un = wave; un < nun; un += nwaves) {
+    int sub;
+    const int64_t c = unit_chunk(un, nch, sub);
     const uint64_t w = cb_now[c];  // (wave-uniform: a scalar load)
     if (w == 0) {
-      if (!WRITE && lane < np) ccnt[(int64_t)lane * nch + c] = 0;
+      if (!WRITE && lane < np) ccnt[(int64_t)lane * nun + un] = 0;
       continue;
     }
     const int64_t v = c * 64 + lane;
@@ -156,8 +177,8 @@ __global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, int np, const i
     const uint64_t m = b >= 0 ? chg_now[v] & vadj[v] : 0;
     const uint32_t pm = m ? pmask[v] : 0u;
     const int32_t u = pm ? uw_label(uw[v]) : kMixed;
-    const bool full = pm != 0 && u != kMixed;  // a uniform sender: one U record per peer in pm
-    const uint64_t mixed0 = __ballot(pm != 0 && u == kMixed);
+    const bool full = pm != 0 && u != kMixed && sub <= 0;  // a uniform sender: one U record per peer in pm
+    const uint64_t mixed0 = split_rows(__ballot(pm != 0 && u == kMixed), sub);
     if constexpr (!WRITE) {
       unsigned long long nm = 0;  // lane q: M records for peer q
       for (uint64_t mixed = mixed0; mixed;) {
@@ -177,11 +198,11 @@ __global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, int np, const i
         const unsigned long long cq = (unsigned long long)__popcll(__ballot(full && ((pm >> q) & 1)));
         if (lane == q) nu = cq;
       }
-      if (lane < np) ccnt[(int64_t)lane * nch + c] = (nu << 32) | nm;
+      if (lane < np) ccnt[(int64_t)lane * nun + un] = (nu << 32) | nm;
     } else {
       unsigned long long uo = 0, mo = 0;  // lane q: peer q's offsets in its regions
       if (lane < np) {
-        const unsigned long long o = coff[(int64_t)lane * nch + c], o0 = coff[(int64_t)lane * nch];
+        const unsigned long long o = coff[(int64_t)lane * nun + un], o0 = coff[(int64_t)lane * nun];
         uo = (o >> 32) - (o0 >> 32);
         mo = (o & 0xffffffffull) - (o0 & 0xffffffffull);
       }
@@ -258,12 +279,12 @@ __global__ __launch_bounds__(256) void k_xtab_fill(int64_t n, const int32_t* __r
 // counts exchange words, 4 per peer: [4q] U records for q, [4q+1] M records for q (0 for self),
 // [4q+2] this partition changed a label in the step (the halting vote, AnalysisTask.endStep
 // :208-225), [4q+3] 0.  coff = the pack's scanned per-(peer, chunk) offsets (null: no records).
-__global__ void k_xbc_counts(int np, int me, const unsigned long long* __restrict__ coff, int64_t nch,
+__global__ void k_xbc_counts(int np, int me, const unsigned long long* __restrict__ coff, int64_t nun,
                              const int32_t* __restrict__ stepflag, int64_t* __restrict__ xa) {
   const int q = threadIdx.x;
   if (q < np) {
     unsigned long long t = 0;
-    if (coff && q != me) t = coff[(int64_t)(q + 1) * nch] - coff[(int64_t)q * nch];
+    if (coff && q != me) t = coff[(int64_t)(q + 1) * nun] - coff[(int64_t)q * nun];
     xa[4 * q] = (int64_t)(t >> 32);
     xa[4 * q + 1] = (int64_t)(t & 0xffffffffull);
     xa[4 * q + 2] = stepflag ? (stepflag[0] != 0) : 0;
@@ -644,16 +665,22 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
     mfin = x ? INT32_MAX - x : INT32_MIN;
   }
   unsigned int fin_acc = 0;
-  for (int64_t b0 = wave * 64; b0 < n_own; b0 += nwaves * 64) {
+  // units (kernels.hpp xbc_units): a hub chunk's mixed members are split over kSplitWays waves
+  const int64_t nch = (n_own + 63) >> 6, nun = xbc_units(n_own);
+  for (int64_t un = wave; un < nun; un += nwaves) {
+    int sub;
+    const int64_t b0 = unit_chunk(un, nch, sub) * 64;
     const int64_t v = b0 + lane;
     const uint64_t mv = v < n_own ? vm[v] & vmask : 0;
     const uint64_t ad = v < n_own ? vadj[v] : 0;
     const int32_t x = (v < n_own && uw) ? uw_label(uw[v]) : kMixed;
-    if (!REMOTE_ONLY) iso_acc += (unsigned)__popcll(transpose64(mv & ~ad, lane));
+    if (!REMOTE_ONLY && sub <= 0) iso_acc += (unsigned)__popcll(transpose64(mv & ~ad, lane));
     const uint64_t m = mv & ad;
-    uint64_t todo = __ballot(m != 0 && x != kMixed);
+    uint64_t todo = __ballot(m != 0 && x != kMixed && sub <= 0);
     // the lanes' owned labels' count rows, looked up in parallel before the group loop
-    const int64_t rx = (!REMOTE_ONLY && m != 0 && x != kMixed && owner_of(x, P.np) == P.me) ? label_row(I, x) : -1;
+    const int64_t rx = (!REMOTE_ONLY && sub <= 0 && m != 0 && x != kMixed && owner_of(x, P.np) == P.me)
+                           ? label_row(I, x)
+                           : -1;
     while (todo) {  // uniform members, grouped by (label, views): lane = view
       const int L = __builtin_ctzll(todo);
       const int32_t xL = __builtin_amdgcn_readlane(x, L);
@@ -668,7 +695,7 @@ __global__ __launch_bounds__(256) void k_part_count(XPeers P, OwnIdx I, uint64_t
       emit_count<REMOTE_ONLY>(xL, __ballot(on && !hit), c, P, I, counts, gcnt, hsbuf, lane, st,
                               (int64_t)rl64((uint64_t)rx, L));
     }
-    for (uint64_t mixed = __ballot(m != 0 && x == kMixed); mixed; mixed &= mixed - 1) {  // rows
+    for (uint64_t mixed = split_rows(__ballot(m != 0 && x == kMixed), sub); mixed; mixed &= mixed - 1) {  // rows
       const int L = __builtin_ctzll(mixed);
       const uint64_t mL = rl64(m, L);
       const bool mem = (mL >> lane) & 1;
@@ -830,7 +857,7 @@ void launch_xvm_unpack(hipStream_t s, int64_t nx, const int32_t* xv, const int32
   if (nx > 0) k_xvm_unpack<<<xgrid(nx, 256), 256, 0, s>>>(nx, xv, xq, xoff, planes, in, vm, vstride);
 }
 size_t xbc_scan_bytes(int64_t n_own, int np) {
-  const int n = (int)(((n_own + 63) >> 6) * np + 1);
+  const int n = (int)(xbc_units(n_own) * np + 1);
   size_t tb = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr, n);
   return tb;
@@ -841,13 +868,13 @@ void launch_xbc_pack(hipStream_t s, int64_t n_own, int np, const XSend& X, const
                      unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp, size_t scan_bytes,
                      bool write_only) {
   if (X.nb <= 0 || n_own <= 0) return;
-  const int64_t nch = (n_own + 63) >> 6;
-  const unsigned grid = xgrid(nch, 4, 4096);
+  const int64_t nun = xbc_units(n_own);
+  const unsigned grid = xgrid(nun, 4, 4096);
   if (!write_only) {
     k_xbc_pack<false><<<grid, 256, 0, s>>>(n_own, np, X.bidx, cb_now, chg_now, vadj, lab, uw, pmask, su, ucap, sm, mcap,
                                            ccnt, coff);
-    // ccnt[np * nch] stays 0: coff[q * nch] .. coff[(q + 1) * nch] = peer q's records
-    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ccnt, coff, (int)(nch * np + 1), s) != hipSuccess)
+    // ccnt[np * nun] stays 0: coff[q * nun] .. coff[(q + 1) * nun] = peer q's records
+    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ccnt, coff, (int)(nun * np + 1), s) != hipSuccess)
       throw std::runtime_error("xbc pack: scan");
   }
   k_xbc_pack<true><<<grid, 256, 0, s>>>(n_own, np, X.bidx, cb_now, chg_now, vadj, lab, uw, pmask, su, ucap, sm, mcap,
@@ -926,7 +953,7 @@ void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const O
   // 16 chunks of 64 members per wave: a wave flushes its label cache once, as records, so fewer
   // waves emit fewer records (one per cached label and count group) and flush less (grid 2048 ->
   // 512 at 2.2M members: 7.3 -> 5.0 ms per partition and query, profiles/r04/ab_part_count_grid.jsonl)
-  const unsigned grid = xgrid(I.n_own, 256 * 16, 2048);
+  const unsigned grid = xgrid(xbc_units(I.n_own), 4 * 16, 2048);
   if (remote_only)
     k_part_count<true><<<grid, 256, 0, s>>>(P, I, vmask, vm, vadj, uw, lab, counts, iso, gcnt, hsbuf, mneg, fin_g);
   else
