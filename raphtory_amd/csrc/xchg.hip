@@ -410,8 +410,14 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
   const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t i0 = wave * 64; i0 < n; i0 += nwaves * 64) {
-    const int64_t i = i0 + lane;
+  // records -> lanes: groups of 8 consecutive records (one 64-B line of U records), a wave's 8
+  // groups 1/8 of the records apart.  A sender's records are in its rank order, so its hubs come
+  // first, and their ghosts here are the ones with the most slots to walk: consecutive records in a
+  // wave put up to 64 of those walks on one wave (one at a time, ~4 us each: the launch), spread
+  // records put a few on each.
+  const int64_t ncw = (n + 63) >> 6;  // chunk-waves
+  for (int64_t cw = wave; cw < ncw; cw += nwaves) {
+    const int64_t i = (((int64_t)(lane >> 3) * ncw + cw) << 3) + (lane & 7);
     int32_t b = 0, val = 0, g = -1;
     uint64_t mask = 0;
     bool isu = false, first = false;

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--interactions", type=int, default=33_333_334, help="prefix of the 1B stream (x3 updates)")
     ap.add_argument("--parts", default="1,2,4,8")
     ap.add_argument("--trace", default="", help="directory: per-superstep trace CSVs (RGPU_TRACE) of the profile pass")
+    ap.add_argument("--profile-rounds", type=int, default=2,
+                    help="profile passes; the one with the smallest slowest-partition time is reported")
     a = ap.parse_args()
     inter_full = 333_333_334
     s = gen_gab_range(4, a.users, inter_full, 0, a.interactions)
@@ -53,18 +55,24 @@ def main():
         print(f"P={P}: sealed in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
         run()
         print(f"P={P}: warm run done", file=sys.stderr, flush=True)
-        t_prof = time.time()
-        run(profile=True, serial=True)
-        t_prof = time.time() - t_prof
-        per = []
-        ks = {}
-        for g in parts:
-            mine = 0.0
-            for k, v in g.stats()["kernels"].items():
-                if v["launches"]:
-                    ks[k] = ks.get(k, 0.0) + v["ms"]
-                    mine += v["ms"]
-            per.append(round(mine, 1))
+        best = None
+        for _ in range(max(1, a.profile_rounds)):
+            t_prof = time.time()
+            run(profile=True, serial=True)
+            t_prof = time.time() - t_prof
+            per = []
+            ks = {}
+            for g in parts:
+                mine = 0.0
+                for k, v in g.stats()["kernels"].items():
+                    if v["launches"]:
+                        ks[k] = ks.get(k, 0.0) + v["ms"]
+                        mine += v["ms"]
+                per.append(round(mine, 1))
+            p0 = {k: [v["launches"], round(v["ms"], 2)] for k, v in parts[0].stats()["kernels"].items() if v["launches"]}
+            if best is None or max(per) < max(best[0]):
+                best = (per, ks, p0, t_prof)
+        per, ks, p0, t_prof = best
         by = {}
         for g in parts:
             for k, v in g.stats()["xchg_bytes_by"].items():
@@ -80,8 +88,7 @@ def main():
         rounds = parts[0].stats()["supersteps"] + 2 * parts[0].stats()["batches"]
         out = {"P": P, "kernel_ms_per_partition": per, "kernel_ms_max": max(per), "kernel_ms_total": round(sum(per), 1),
                "kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in ks.items()},
-               "partition0_kernels": {k: [v["launches"], round(v["ms"], 2)] for k, v in parts[0].stats()["kernels"].items()
-                                      if v["launches"]},
+               "partition0_kernels": p0, "profile_rounds": a.profile_rounds,
                # algorithmic bytes (the counting pass's work counters) summed over the
                # partitions: more bytes than at P = 1 = more work, not slower work
                "kernel_GB_sum_by_kernel": {k: round(sum(g.stats()["kernels"][k].get("bytes", 0.0) for g in parts) / 1e9, 2)
