@@ -430,7 +430,8 @@ def run_c4(a, rank, world, local):
                                    "launches of the lean instantiation the timed query runs (RGPU_PROF_LEAN)"}
         if traffic:  # the memory system's real rate and its waste (the progress signal beside frac)
             roofline["traffic_rate_GBps"] = round(traffic / (d["ms"] / d["launches"] / 1e3) / 1e9, 1)
-            roofline["traffic_over_algorithmic"] = round(traffic / (d["bytes"] / d["launches"]), 2)
+            if d["bytes"] > 0:  # (--lean-pass-only runs no counting pass: no algorithmic bytes)
+                roofline["traffic_over_algorithmic"] = round(traffic / (d["bytes"] / d["launches"]), 2)
         if not a.no_edge_counts and world == 1:
             g.run("cc", hops, windows, edge_counts=True)
             summ = g.cc_summaries()
