@@ -355,7 +355,8 @@ void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg
 // owned id -> owned rank: ids ascend with rank; bucket b = id >> shift covers ranks
 // [boff[b], boff[b+1]) (about one id per bucket)
 // Work units of the record pack and the partitioned counts (xchg.hip): chunks of 64 consecutive owned
-// ranks, except the first kSplitChunks chunks, each split kSplitWays ways by mixed member.  Owned
+// ranks, except the first kSplitChunks chunks, each split kSplitWays ways by mixed member.  (Tried on
+// N = 1's k_cc_count / k_cc_roots too: no change there, 6.3 / 4.1 vs 6.7 / 4.2 ms per query.)  Owned
 // ranks are in activity order (packer.cpp locality_order), so those chunks hold the partition's
 // hubs, which are mostly mixed: one wave walking 64 hub rows in turn was the whole launch (0.8 ms
 // of a year batch's count kernel, 0.3-0.4 ms of a record pack pass, profiles/r04).  Unit u < hs *
@@ -366,6 +367,24 @@ constexpr int kSplitChunks = 128, kSplitWays = 16;
 __host__ __device__ inline int64_t xbc_units(int64_t n_own) {
   const int64_t nch = (n_own + 63) >> 6, hs = nch < kSplitChunks ? nch : kSplitChunks;
   return nch + hs * (kSplitWays - 1);
+}
+// unit -> (chunk, sub-unit; -1: the whole chunk)
+__device__ __forceinline__ int64_t unit_chunk(int64_t un, int64_t nch, int& sub) {
+  const int64_t hs = nch < kSplitChunks ? nch : kSplitChunks;
+  if (un < hs * kSplitWays) {
+    sub = (int)(un % kSplitWays);
+    return un / kSplitWays;
+  }
+  sub = -1;
+  return hs + (un - hs * kSplitWays);
+}
+// the members (lane mask) a sub-unit takes: every kSplitWays-th, from the sub-th (wave-uniform)
+__device__ __forceinline__ uint64_t split_rows(uint64_t m, int sub) {
+  if (sub < 0) return m;
+  uint64_t r = 0;
+  for (int k = 0; m; m &= m - 1, k++)
+    if (k % kSplitWays == sub) r |= m & (~m + 1);
+  return r;
 }
 struct OwnIdx {
   const int64_t* vid = nullptr;   // owned ids ascending

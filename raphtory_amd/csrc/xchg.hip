@@ -122,24 +122,6 @@ __global__ __launch_bounds__(256) void k_xvm_unpack(int64_t nx, const int32_t* _
 // (DESIGN.md §4 lesson 1).  A mixed sender's distinct labels are found on its row (lane = view);
 // rows of up to kRowsInFlight senders are loaded before any is folded.
 constexpr int kRowsInFlight = 4;
-// unit -> (chunk, sub-unit; -1: the whole chunk) (kernels.hpp xbc_units)
-__device__ __forceinline__ int64_t unit_chunk(int64_t un, int64_t nch, int& sub) {
-  const int64_t hs = nch < kSplitChunks ? nch : kSplitChunks;
-  if (un < hs * kSplitWays) {
-    sub = (int)(un % kSplitWays);
-    return un / kSplitWays;
-  }
-  sub = -1;
-  return hs + (un - hs * kSplitWays);
-}
-// the mixed members (lane mask) a sub-unit takes: every kSplitWays-th, from the sub-th (wave-uniform)
-__device__ __forceinline__ uint64_t split_rows(uint64_t m, int sub) {
-  if (sub < 0) return m;
-  uint64_t r = 0;
-  for (int k = 0; m; m &= m - 1, k++)
-    if (k % kSplitWays == sub) r |= m & (~m + 1);
-  return r;
-}
 __device__ __forceinline__ int distinct_labels(int32_t x, uint64_t mm, int lane) {
   int k = 0;
   while (mm) {
