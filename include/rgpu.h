@@ -14,7 +14,10 @@
  *   - device memory (and, later, communicators) are owned by the rgpu_ctx.
  *   - result buffers are caller-allocated with (cap, *n); if *n > cap, call again.
  *   - calls on one ctx are serialised by an internal mutex (10 ReaderWorker actors run
- *     concurrently on reader-dispatcher, application.conf:246-264).
+ *     concurrently on reader-dispatcher, application.conf:246-264), with two exceptions for live
+ *     ingest (ABI 9): rgpu_ingest takes only the update log's lock, so it never waits for a run;
+ *     rgpu_seal takes a seal lock (one seal at a time) and holds the run mutex only briefly, so a
+ *     seal may run concurrently with rgpu_run_view_batch and the result calls (see rgpu_seal).
  *   - times are int64 milliseconds >= 0; vertex ids are int64 in [0, 2^31)
  *     (message targets are truncated with .toInt, VertexVisitor.scala:117-122).
  */
@@ -146,7 +149,20 @@ int rgpu_ingest_rgev(rgpu_ctx* ctx, const uint8_t* buf, size_t bytes, size_t* co
  * re-runs): after the first seal, rgpu_ingest + rgpu_seal again merges only the new updates
  * into the HBM-resident graph (merge.hip; one partition in RGPU_ORDER_ID order, RGPU_DELTA=0
  * forces a full re-pack).
- * The new updates count as later in stream order than every sealed one. */
+ * The new updates count as later in stream order than every sealed one.
+ * Concurrency (ABI 9, IngestionWorker keeps applying updates while LiveAnalysisTask runs):
+ *   - rgpu_ingest may be called while a run or a seal is in progress; a seal packs the updates
+ *     ingested before it started.  An ingest does not unseal the context: a run after an ingest
+ *     without a seal analyses the resident graph (the updates since the last seal wait for the
+ *     next one).
+ *   - a delta seal builds the merged graph beside the resident one while runs go on.  If the last
+ *     run's results are still readable (a run has happened on the resident graph), the merged graph
+ *     is PARKED: rgpu_cc_*, rgpu_degree_*, rgpu_pr_* keep answering for the run they came from, and
+ *     the next rgpu_run_view_batch (or rgpu_seal) swaps the parked graph in first.  rgpu_stats'
+ *     entity counts (vertices, edges, *_events, deaths, seal_*) describe the newest sealed graph,
+ *     i.e. the parked one while one is parked.
+ *   - a full re-pack (first seal, RGPU_DELTA=0, a locality-ordered base) holds the run mutex
+ *     throughout. */
 int rgpu_seal(rgpu_ctx* ctx);
 
 /* Local vertex order of the next full seal (ABI 7).  Results and labels do not depend on it.

@@ -30,6 +30,26 @@ void ncclchk(ncclResult_t e, const char* what) {
   if (e != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(e));
 }
 
+// The HIP runtime stages a copy through the CPU when a pointer it is handed lies in no live device
+// allocation (a freed buffer, or a range running past an allocation's end), and a bad one then
+// faults inside the runtime's host memcpy: a SIGSEGV with no word about which buffer (the round-4
+// P = 8 rehearsal crash in LocalExchange::sendrecv).  The loopback and shared-memory
+// collectives check every device range they copy from or into first, and throw naming it.
+void check_dev_range(const void* p, size_t bytes, const char* what, int rank, int peer) {
+  if (!bytes) return;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  const hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p);
+  const uintptr_t a = (uintptr_t)p, b = (uintptr_t)base;
+  if (e != hipSuccess || a < b || a - b + bytes > size)
+    throw std::runtime_error(std::string("exchange: rank ") + std::to_string(rank) + " " + what + " (peer " +
+                             std::to_string(peer) + "): " + std::to_string(bytes) + " bytes at " +
+                             std::to_string(a) + " are not inside one live device allocation" +
+                             (e == hipSuccess ? " (allocation of " + std::to_string(size) + " bytes at offset " +
+                                                    std::to_string((long long)(a - b)) + ")"
+                                              : std::string(" (no allocation)")));
+}
+
 const char kLoopMagic[8] = {'R', 'G', 'P', 'U', 'L', 'O', 'O', 'P'};
 const char kShmMagic[8] = {'R', 'G', 'P', 'U', 'S', 'H', 'M', '1'};
 
@@ -112,6 +132,20 @@ class RcclExchange : public Exchange {
 // Partitions of one process rendezvous here.  Every collective is: drain own stream,
 // publish pointers, barrier, pull from the peers' buffers, drain, barrier (so no peer
 // reuses a buffer that is still being read).
+// A partition that does not arrive within the barrier timeout (RGPU_XCHG_TIMEOUT seconds; default
+// 120 for loopback partitions, which are threads of one process that start their runs together,
+// and 600 for processes over shared memory, whose first collective can wait for a peer's seal of
+// minutes) breaks the group: the waiting partitions throw, and every later collective on the group
+// throws too (an arrival counted before the timeout would otherwise release a later barrier early
+// and pair collectives that do not belong together).
+int barrier_timeout_s(int dflt) {
+  static const int t = [] {
+    const char* e = std::getenv("RGPU_XCHG_TIMEOUT");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  return t > 0 ? t : dflt;
+}
+
 struct LocalGroup {
   explicit LocalGroup(int n) : n(n), ptr(n), vptr(n), vsz(n), host(n) {}
   int n;
@@ -119,12 +153,14 @@ struct LocalGroup {
   std::condition_variable cv;
   int arrived = 0;
   uint64_t gen = 0;
+  bool broken = false;
   std::vector<const void*> ptr;
   std::vector<std::vector<void*>> vptr;
   std::vector<std::vector<size_t>> vsz;
   std::vector<std::vector<unsigned long long>> host;
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
+    if (broken) throw std::runtime_error("loopback exchange: channel broken by an earlier barrier timeout");
     const uint64_t g = gen;
     if (++arrived == n) {
       arrived = 0;
@@ -132,8 +168,12 @@ struct LocalGroup {
       cv.notify_all();
     } else {
       // a partition that never arrives (its thread failed) must not hang the others forever
-      if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g; }))
+      if (!cv.wait_for(lk, std::chrono::seconds(barrier_timeout_s(120)), [&] { return gen != g || broken; }) ||
+          broken) {
+        broken = true;
+        cv.notify_all();
         throw std::runtime_error("loopback exchange: a partition did not reach the barrier");
+      }
     }
   }
 };
@@ -204,6 +244,11 @@ class LocalExchange : public Exchange {
                 const size_t* recv_bytes, hipStream_t s) override {
     const int n = g_->n;
     hipchk(hipStreamSynchronize(s), "sync");
+    for (int q = 0; q < n; q++)
+      if (q != r_) {
+        check_dev_range(send[q], send_bytes[q], "send region", r_, q);
+        check_dev_range(recv[q], recv_bytes[q], "receive region", r_, q);
+      }
     iso_enter();
     g_->vptr[r_].assign(send, send + n);
     g_->vsz[r_].assign(send_bytes, send_bytes + n);
@@ -258,6 +303,7 @@ constexpr int kShmMaxRanks = 64;
 struct ShmCtl {
   std::atomic<uint64_t> arrived;
   std::atomic<uint64_t> gen;
+  std::atomic<uint64_t> broken;              // a barrier timed out: the channel is unusable (barrier())
   std::atomic<uint64_t> size[kShmMaxRanks];  // bytes of each rank's data segment
 };
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "process-shared atomics");
@@ -319,6 +365,11 @@ class ShmExchange : public Exchange {
     uint8_t* mine = own(tot);
     uint64_t* tab = (uint64_t*)mine;
     size_t off = sizeof(uint64_t) * 2 * n_;
+    for (int q = 0; q < n_; q++)
+      if (q != r_) {
+        check_dev_range(send[q], send_bytes[q], "send region", r_, q);
+        check_dev_range(recv[q], recv_bytes[q], "receive region", r_, q);
+      }
     for (int q = 0; q < n_; q++) {
       const size_t b = q == r_ ? 0 : send_bytes[q];
       tab[2 * q] = off;
@@ -360,7 +411,11 @@ class ShmExchange : public Exchange {
     std::snprintf(b, sizeof(b), "/rgpu_%016llx_%s%d", (unsigned long long)key_, r < 0 ? "ctl" : "r", r < 0 ? 0 : r);
     return b;
   }
+  // Timeout: RGPU_XCHG_TIMEOUT, default 600 s (barrier_timeout_s).  A timed-out barrier marks the channel broken
+  // in the shared control segment, so every rank's later collective on it throws instead of being
+  // released early by the arrival counted before the timeout.
   void barrier() {
+    if (ctl_->broken.load()) throw std::runtime_error("shm exchange: channel broken by an earlier barrier timeout");
     const uint64_t g = ctl_->gen.load();
     if (ctl_->arrived.fetch_add(1) + 1 == (uint64_t)n_) {
       ctl_->arrived.store(0);
@@ -370,8 +425,11 @@ class ShmExchange : public Exchange {
     const auto t0 = std::chrono::steady_clock::now();
     while (ctl_->gen.load() == g) {
       std::this_thread::yield();
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+      if (ctl_->broken.load()) throw std::runtime_error("shm exchange: channel broken by a peer's barrier timeout");
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(barrier_timeout_s(600))) {
+        ctl_->broken.store(1);
         throw std::runtime_error("shm exchange: a partition did not reach the barrier");
+      }
     }
   }
   uint8_t* own(size_t bytes) {  // our data segment, at least `bytes` long
@@ -379,7 +437,12 @@ class ShmExchange : public Exchange {
       const size_t want = std::max(bytes, mapped_[r_] * 2);
       if (map_[r_]) munmap(map_[r_], mapped_[r_]);
       map_[r_] = nullptr;
+      // posix_fallocate reserves the tmpfs pages now: on a small /dev/shm an ftruncate alone would
+      // succeed and the first store past the free space would raise SIGBUS instead of an error
       if (ftruncate(fd_[r_], (off_t)want) != 0) throw std::runtime_error("shm exchange: ftruncate");
+      if (const int e = posix_fallocate(fd_[r_], 0, (off_t)want))
+        throw std::runtime_error(std::string("shm exchange: no room for a ") + std::to_string(want) +
+                                 "-byte segment in /dev/shm: " + std::strerror(e));
       void* p = mmap(nullptr, want, PROT_READ | PROT_WRITE, MAP_SHARED, fd_[r_], 0);
       if (p == MAP_FAILED) throw std::runtime_error("shm exchange: mmap");
       map_[r_] = p;

@@ -393,6 +393,8 @@ struct OwnIdx {
   int shift = 0;
   int64_t n_own = 0;
   int64_t id_max = -1;            // the largest owned id (the buckets cover [0, id_max])
+  unsigned long long* err = nullptr;  // lookups of a label owned here that found no owned vertex:
+                                      // a bug upstream, counted and reported by the run (RGPU_EHIP)
 };
 // bucket shift of an OwnIdx: about one owned id per bucket over the ids' range [0, id_max] (not
 // [0, 2^31): ids packed densely below 2^31 would otherwise put dozens of owned ids in a bucket, a

@@ -27,6 +27,7 @@
 #include "exchange.hpp"
 #include "kernels.hpp"
 #include "rgpu_internal.hpp"
+#include "xregions.hpp"
 
 using namespace rgpu;
 
@@ -162,6 +163,7 @@ struct Part {
   int64_t nbq[kMaxParts] = {};                // boundary vertices of every partition
   bool tab_ready = false;
   bool no_deaths = false;                     // no partition's graph holds a vertex death (ensure_tab)
+  bool all_tslots = false;                    // every partition has time-ordered slots (ensure_tab)
   uint8_t* gpeer = nullptr;                   // [nv - n_own] the partition owning ghost g (getPartition)
   double *sbuf_f = nullptr, *rbuf_f = nullptr;  // PR contribution rows
   bool pr_ready = false;
@@ -237,6 +239,8 @@ struct rgpu_ctx {
   bool prof_lean = false;               // RGPU_PROF_LEAN (work_buf)
   int inject_fail = 0;                  // RGPU_INJECT_FAIL=n (tests): the n-th batch start of a run throws
   bool inject_rec = false;              // RGPU_INJECT_FAIL=rec (tests): corrupt one received label record
+  bool inject_cnt = false;              // RGPU_INJECT_FAIL=cnt (tests): one received count record names a
+                                        // label routed here that no owned vertex holds
   int dense = -1;                       // RGPU_DENSE: dense-step divisor (kernels.hip dense_rule; -1 by size)
   bool check = false;                   // RGPU_CHECK: structural checks after seal and K2 (check.hip)
   std::string trace_path;               // RGPU_TRACE: per-launch / per-step CSV (profile runs)
@@ -1275,18 +1279,23 @@ void ensure_tab(rgpu_ctx* c) {
   auto& LG = c->graph_allocs;
   std::vector<void*> T;
   try {
-    // every partition's boundary count, and whether its graph holds a vertex death (2 nb + deaths)
+    // every partition's boundary count, whether its graph holds a vertex death, and whether it
+    // lacks time-ordered slots (4 nb + 2 no-tslots + deaths): ghost_vm_free must decide the same on
+    // every partition, and build_tslots leaves ts_t null on a partition without edges (or past
+    // int32 slot words)
     int64_t* d = dalloc<int64_t>(T, 2 * P);
-    std::vector<int64_t> h(2 * P, 2 * X.xsend.nb + (c->st.deaths > 0 ? 1 : 0));
+    std::vector<int64_t> h(2 * P, 4 * X.xsend.nb + (c->g.ts_t ? 0 : 2) + (c->st.deaths > 0 ? 1 : 0));
     HIPCHK(hipMemcpy(d, h.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice));
     X.xchg->alltoall_i64(d, d + P, 1, st);
     HIPCHK(hipMemcpyAsync(h.data(), d, sizeof(int64_t) * 2 * P, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     int64_t o = 0;
     X.no_deaths = c->st.deaths == 0;
+    X.all_tslots = c->g.ts_t != nullptr;
     for (int q = 0; q < P; q++) {
       if (q != me && (h[P + q] & 1)) X.no_deaths = false;
-      X.nbq[q] = q == me ? 0 : h[P + q] >> 1;
+      if (q != me && (h[P + q] & 2)) X.all_tslots = false;
+      X.nbq[q] = q == me ? 0 : h[P + q] >> 2;
       X.tab.toff[q] = o;
       o += X.nbq[q];
     }
@@ -1346,6 +1355,8 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
   const int P = c->nparts;
   auto& LG = c->graph_allocs;
   ensure_tab(c);
+  if (!X.own.err) X.own.err = dalloc<unsigned long long>(LG, 1);  // (goes with the graph: apply_merged / free_graph)
+  HIPCHK(hipMemset(X.own.err, 0, sizeof(unsigned long long)));
   for (int i = 0; i < nuse; i++) {
     XSlot& xs = X.xs[i];
     if (!xs.x) xs.x = X.xchg->fork(i + 1);  // collective: every partition forks the same slots
@@ -1401,9 +1412,11 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
 // vertex death, read no ghost membership: every slot is nodeath, and its window bits imply both
 // endpoints' membership (BatchParams::simple_ends).  The ghost rows are then set to every view
 // (readers AND them with bits that imply them) and the exchange is skipped.  The same decision on
-// every partition: the windows are the query's, no_deaths is agreed in ensure_tab.
+// every partition: the windows are the query's, no_deaths and all_tslots are agreed in ensure_tab
+// (a partition's own ts_t is not: one without edges has none, and deciding on it alone would send
+// that partition into a membership exchange its peers skip).
 bool ghost_vm_free(const rgpu_ctx* c, const RunCfg& rc) {
-  if (!c->partitioned || rc.algo != RGPU_ALGO_CC || !c->pt.no_deaths || !c->g.ts_t) return false;
+  if (!c->partitioned || rc.algo != RGPU_ALGO_CC || !c->pt.no_deaths || !c->pt.all_tslots) return false;
   for (int w = 0; w < rc.W; w++)
     if (rc.thr_v[w] != rc.thr_e[w]) return false;
   return true;
@@ -1525,28 +1538,19 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   XSlot& xs = X.xs[si];
   const DevGraph& g = c->g;
   const int P = c->nparts, me = c->part, r = xs.r;
-  const int64_t* xa = xs.h_xab;
-  const int64_t* xb = xs.h_xab + 4 * P;
-  int64_t sent_u[kMaxParts] = {}, sent_m[kMaxParts] = {}, max_m = 0, recv_u[kMaxParts] = {}, recv_m[kMaxParts] = {};
-  bool any = false;
-  for (int q = 0; q < P; q++) {
-    if (q != me) {
-      sent_u[q] = xa[4 * q];
-      sent_m[q] = xa[4 * q + 1];
-      max_m = std::max(max_m, sent_m[q]);
-      recv_u[q] = xb[4 * q];
-      recv_m[q] = xb[4 * q + 1];
-      if (recv_u[q] > X.nbq[q])
-        throw HipFail{"exchange: peer " + std::to_string(q) + " announced " + std::to_string(recv_u[q]) +
-                      " U records for " + std::to_string(X.nbq[q]) + " boundary vertices"};
-    }
-    any |= xb[4 * q + 2] != 0;  // the vote: some partition changed a label (self included)
+  // record counts per peer and the vote (xregions.hpp; the region arithmetic is CPU-tested)
+  XferPlan xp;
+  {
+    const std::string e = xfer_counts(P, me, xs.h_xab, xs.h_xab + 4 * P, X.nbq, &xp);
+    if (!e.empty()) throw HipFail{e};
   }
-  if (max_m > xs.smcap) {  // the counts were exact; the M records did not all fit: pack again, larger
-    grow_sm(xs, P, max_m, s.stream);
+  const int64_t* recv_u = xp.recv_u;
+  const int64_t* recv_m = xp.recv_m;
+  if (xp.max_m > xs.smcap) {  // the counts were exact; the M records did not all fit: pack again, larger
+    grow_sm(xs, P, xp.max_m, s.stream);
     part_pack(c, si, r, true);
   }
-  if (!any) {  // every partition voted to halt
+  if (!xp.any) {  // every partition voted to halt
     s.r_final = r;
     part_finish_begin(c, si, rc);
     return;
@@ -1580,21 +1584,28 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   std::copy(recv_u, recv_u + kMaxParts, xs.rucnt[par]);
   std::copy(recv_m, recv_m + kMaxParts, xs.rmcnt[par]);
   const XBcIn in = bc_in(c, xs, par);
+  {
+    int64_t rm_alloc = 0;
+    for (int q = 0; q < P; q++) rm_alloc += xs.rmcap[q];  // (grow_regions / alloc_regions: sum of the caps)
+    const std::string e = xfer_layout(&xp, X.nbq, xs.su_cap, xs.smcap, xs.rmcap, xs.su_cap * P, xs.smcap * P,
+                                      xs.ru_cap, rm_alloc);
+    if (!e.empty()) throw HipFail{e};
+  }
   {  // the broadcast: our U list and M list to every peer, theirs into their regions
     std::vector<void*> sp(P), rp(P);
     std::vector<size_t> sb(P), rb(P);
     for (int q = 0; q < P; q++) {
-      sp[q] = xs.su + (size_t)q * xs.su_cap;
-      rp[q] = xs.ru[par] + in.U.base[q];
-      sb[q] = q == me ? 0 : sizeof(unsigned long long) * (size_t)sent_u[q];
+      sp[q] = xs.su + xp.su_off[q];
+      rp[q] = xs.ru[par] + xp.ru_off[q];
+      sb[q] = q == me ? 0 : sizeof(unsigned long long) * (size_t)xp.sent_u[q];
       rb[q] = q == me ? 0 : sizeof(unsigned long long) * (size_t)recv_u[q];
       xs.bytes[1] += (double)sb[q];
     }
     xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
     for (int q = 0; q < P; q++) {
-      sp[q] = xs.sm + (size_t)q * xs.smcap;
-      rp[q] = xs.rm[par] + in.M.base[q];
-      sb[q] = q == me ? 0 : sizeof(XRec) * (size_t)sent_m[q];
+      sp[q] = xs.sm + xp.sm_off[q];
+      rp[q] = xs.rm[par] + xp.rm_off[q];
+      sb[q] = q == me ? 0 : sizeof(XRec) * (size_t)xp.sent_m[q];
       rb[q] = q == me ? 0 : sizeof(XRec) * (size_t)recv_m[q];
       xs.bytes[1] += (double)sb[q];
     }
@@ -1721,6 +1732,18 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
     }
     xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
   }
+  if (c->inject_cnt)  // fault injection (tests): one received count record names a label that getPartition
+                      // routes here but no owned vertex holds (above every owned id)
+    for (int q = 0; q < P; q++)
+      if (recv[q]) {
+        const int64_t m = 10 * (int64_t)P;
+        const int32_t bad = (int32_t)(((int64_t)INT32_MAX - m) / m * m + 10 * me);
+        HIPCHK(hipMemcpyAsync(xs.hrbuf + peers_layout(c, xs.hrcap, X.xr_off, recv).base[q], &bad, sizeof(bad),
+                              hipMemcpyHostToDevice, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));  // (&bad is a stack word)
+        c->inject_cnt = false;
+        break;
+      }
   timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_hist_recv(s.stream, peers_layout(c, xs.hrcap, X.xr_off, recv), xs.hrbuf, X.own, s.counts); });
   // the minimum label's members, counted on every partition (k_part_count): summed, added by its owner
   launch_min_count_fold(s.stream, xs.fin_g, xs.mfin);
@@ -2227,16 +2250,31 @@ void finish_seal(rgpu_ctx* c, size_t n_end) {
 // Replace the resident graph by a merged one (under mu, between runs).  The last run's results
 // named the old graph's ranks: they go.  Batch slots and mask sets stay if they fit (else they are
 // reallocated on the next run with 2x headroom for the ticks to come).
+// Exception safety: every step that can throw before the commit point (the send plan, which
+// allocates) builds into the merged graph's own allocations, so a throw there leaves both the
+// resident graph and M intact.  At the commit point M is emptied (a throw after it cannot make a
+// later apply_pending re-install freed pointers), and the steps after it only clear slot state:
+// if one throws, the slots are released and reallocated by the next run.
 void apply_merged(rgpu_ctx* c, Merged& M) {
+  XSend xsend;
+  if (c->partitioned) {  // (allocates: before the commit point, into M.L)
+    Part tmp;
+    tmp.nxs = M.PM.nxs;
+    tmp.xs_v = M.PM.xs_v;
+    xsend = build_send_plan(M.g.n_own, tmp, M.L);
+  }
+  // ---- commit point: nothing below throws until the slot clears
+  Merged T = std::move(M);
+  M = Merged();
   Packed& B = c->pk;
-  const DevGraph g = M.g;
-  const bool dev = M.dev;
-  const int64_t nv2 = M.nv2, ne_owned = M.ne_owned, nvk = M.nvk, nek = M.nek;
-  PartMeta& PM = M.PM;
-  for (void* p : c->graph_allocs) (void)hipFree(p);
-  c->graph_allocs.swap(M.L);
+  const DevGraph g = T.g;
+  const bool dev = T.dev;
+  PartMeta& PM = T.PM;
+  std::vector<void*> old;
+  old.swap(c->graph_allocs);
+  c->graph_allocs.swap(T.L);
   c->g = g;
-  c->g_vid = M.vid2;
+  c->g_vid = T.vid2;
   if (c->partitioned) {  // the old plan's buffers went with the old graph; channels stay
     free_part_slots(c, true);
     Exchange* x = c->pt.xchg;
@@ -2256,66 +2294,72 @@ void apply_merged(rgpu_ctx* c, Merged& M) {
     X.xr_q = PM.xr_q;
     X.xs_off_d = PM.xs_off_d;
     X.xr_off_d = PM.xr_off_d;
-    X.xsend = build_send_plan(g.n_own, X, c->graph_allocs);
+    X.xsend = xsend;
     X.own.vid = PM.own_vid;
     X.own.pos = nullptr;
     X.own.boff = PM.own_boff;
     X.own.shift = PM.shift;
     X.own.n_own = g.n_own;
     X.own.id_max = PM.id_max;
-    c->orph_id.swap(M.orph_id);
-    c->orph_t.swap(M.orph_t);
+    c->orph_id.swap(T.orph_id);
+    c->orph_t.swap(T.orph_t);
   }
   for (Slot& sl : c->slot) {
     sl.hv = HeavyBuf();
     sl.h_cc = sl.h_pr = false;
   }
-  if (g.nv > c->cap_nv || g.ne > c->cap_ne || g.n_in > c->cap_nin) {
-    release_slots(c);
-    c->cap_nv = 2 * g.nv;  // doubling: a growing live graph re-allocates O(log) times
-    c->cap_ne = 2 * g.ne;
-    c->cap_nin = 2 * g.n_in;
-  } else {
-    for (int i = 0; i < c->nslots; i++) {  // per-rank state that K2 does not rewrite
-      Slot& sl = c->slot[i];
-      if (sl.chg[0]) {
-        HIPCHK(hipMemset(sl.chg[0], 0, sizeof(uint64_t) * (c->cap_nv + kPad)));
-        HIPCHK(hipMemset(sl.chg[1], 0, sizeof(uint64_t) * (c->cap_nv + kPad)));
-        HIPCHK(hipMemset(sl.snbr, 0, sizeof(int32_t) * (c->cap_ne + c->cap_nin + kPad)));
-      }
-    }
-  }
-  B.nv = nv2;
+  B.nv = T.nv2;
   B.n_own = g.n_own;
   B.ne = g.ne;
-  B.ne_owned = ne_owned;
+  B.ne_owned = T.ne_owned;
   if (dev) {  // the host keeps no offsets; its ids follow on demand (host_vid)
     c->vid_stale = true;
-    c->n_dtime = M.ndt;
+    c->n_dtime = T.ndt;
     for (auto* v : {&B.doff, &B.dtime, &B.out_off, &B.in_off}) std::vector<int64_t>().swap(*v);
   } else {
-    B.vid.swap(M.hvid);
-    B.doff.swap(M.hdoff);
-    B.dtime.swap(M.hdtime);
-    B.out_off.swap(M.hout_off);
-    B.in_off.swap(M.hin_off);
+    B.vid.swap(T.hvid);
+    B.doff.swap(T.hdoff);
+    B.dtime.swap(T.hdtime);
+    B.out_off.swap(T.hout_off);
+    B.in_off.swap(T.hin_off);
     c->n_dtime = -1;
   }
-  B.n_vkey = nvk;
-  B.n_ekey = nek;
+  B.n_vkey = T.nvk;
+  B.n_ekey = T.nek;
   B.n_in = g.n_in;
   {
     std::lock_guard<std::mutex> il(c->ingest_mu);
     B.newest = c->newest;
   }
-  c->st.seal_delta_updates = M.nd;
+  c->st.seal_delta_updates = T.nd;
   c->algo = -1;  // (results of the last run named the old graph)
   c->cc.clear();
   c->vlast.clear();
   c->kept.clear();
   c->retained = false;
   c->pt.tab_ready = false;
-  M = Merged();
+  for (void* p : old) (void)hipFree(p);  // (the slots' kernels have finished: runs hold mu)
+  // slot state that K2 does not rewrite, for the new graph
+  if (g.nv > c->cap_nv || g.ne > c->cap_ne || g.n_in > c->cap_nin) {
+    release_slots(c);
+    c->cap_nv = 2 * g.nv;  // doubling: a growing live graph re-allocates O(log) times
+    c->cap_ne = 2 * g.ne;
+    c->cap_nin = 2 * g.n_in;
+  } else {
+    try {
+      for (int i = 0; i < c->nslots; i++) {
+        Slot& sl = c->slot[i];
+        if (sl.chg[0]) {
+          HIPCHK(hipMemset(sl.chg[0], 0, sizeof(uint64_t) * (c->cap_nv + kPad)));
+          HIPCHK(hipMemset(sl.chg[1], 0, sizeof(uint64_t) * (c->cap_nv + kPad)));
+          HIPCHK(hipMemset(sl.snbr, 0, sizeof(int32_t) * (c->cap_ne + c->cap_nin + kPad)));
+        }
+      }
+    } catch (...) {
+      release_slots(c);  // the next run allocates fresh, cleared slots
+      throw;
+    }
+  }
 }
 
 // the parked merged graph (if any) replaces the resident one (under mu)
@@ -2637,16 +2681,21 @@ int rgpu_seal(rgpu_ctx* c) {
       c->sealed = true;
       return RGPU_OK;
     }
-    // (a locality-ordered base has no monotone rank maps to merge into: it is re-packed; the
-    // partitioned merge needs the device packer)
-    if (c->delta_on && c->n_sealed > 0 && c->g.nv > 0 && !c->pk.relabeled && !(c->partitioned && c->delta_host)) {
+    // A graph parked by the previous seal goes in first (this one builds on it), and the decision
+    // reads the resident graph: both under mu, since a run may be swapping the parked graph in at
+    // this moment (apply_pending).  After this point the resident graph (c->g, c->pk's metadata,
+    // c->g_vid, the orphan lists) stays as it is until this seal swaps its result in: only a seal
+    // parks a graph or re-packs, and seal_mu is held, so seal_delta reads it without mu while runs
+    // read it too.  (A locality-ordered base has no monotone rank maps to merge into: it is
+    // re-packed; the partitioned merge needs the device packer.)
+    bool incremental;
+    lk.lock();
+    apply_pending(c);
+    incremental = c->delta_on && c->n_sealed > 0 && c->g.nv > 0 && !c->pk.relabeled && !(c->partitioned && c->delta_host);
+    lk.unlock();
+    if (incremental) {
       // live ingest: merge the delta into the resident graph.  The device packer builds it while runs
       // and ingestion go on; the host packer (RGPU_DELTA=2) reads the log, so ingestion waits.
-      if (c->pending.valid) {  // a graph parked by the previous seal goes in first: this one builds on it
-        lk.lock();
-        apply_pending(c);
-        lk.unlock();
-      }
       if (c->delta_host) {
         il.lock();
         n_end = c->ev_base + c->events.size();  // (what the host packer will read)
@@ -2877,6 +2926,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   {
     const char* e = std::getenv("RGPU_INJECT_FAIL");
     c->inject_rec = e && std::strcmp(e, "rec") == 0;
+    c->inject_cnt = e && std::strcmp(e, "cnt") == 0;
   }
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   try {
@@ -3011,6 +3061,12 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
         }
       if (bad)
         throw HipFail{"exchange: " + std::to_string(bad) + " received label records outside the receive plan"};
+      if (c->pt.own.err) {  // component counts of labels routed here that no owned vertex holds (xchg.hip label_row)
+        unsigned long long e = 0;
+        HIPCHK(hipMemcpy(&e, c->pt.own.err, sizeof(e), hipMemcpyDeviceToHost));
+        if (e)
+          throw HipFail{"component counts: " + std::to_string(e) + " lookups of a label routed here found no owned vertex"};
+      }
     }
   } catch (const HipFail& f) {
     exchange_quiesce();

@@ -527,10 +527,16 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane) {  // (ker
   }
   return x;
 }
-// count row (local rank) of owned label x
+// count row (local rank) of label x, which getPartition places here.  A label is a member's id, so
+// the lookup always finds it; a miss (id out of the buckets' range, or absent) is counted into
+// I.err, and the run fails after its last collective instead of dropping the count.
 __device__ __forceinline__ int64_t label_row(const OwnIdx& I, int32_t x) {
   const int64_t k = owned_rank(I, x);
-  return k < 0 ? -1 : (I.pos ? (int64_t)I.pos[k] : k);
+  if (k < 0) {
+    if (I.err) atomicAdd(I.err, 1ull);
+    return -1;
+  }
+  return I.pos ? (int64_t)I.pos[k] : k;
 }
 // Count records are XRec {label, count, views}: `count` members carry `label` in every view of
 // `views`.  A uniform member group (the same label over the same views, kernels.hip k_cc_count)
@@ -572,7 +578,7 @@ __device__ __forceinline__ void emit_count(int32_t x, uint64_t views, unsigned c
   const int q = owner_of(x, P.np);
   if (q == P.me) {
     if (!REMOTE_ONLY) {
-      const int64_t r = row != -2 ? row : label_row(I, x);  // always found: a label is a member's id
+      const int64_t r = row != -2 ? row : label_row(I, x);  // (a miss is counted into I.err)
       if (r >= 0 && ((views >> lane) & 1)) atomicAdd(&counts[r * 64 + lane], (int32_t)c);
     }
     return;

@@ -173,3 +173,22 @@ def test_partitioned_path_one_partition_scattered_ids():
     lp = _parts(s, 1, {"RGPU_PARTITIONED": "1", "RGPU_HEAVY": "200"})
     check_cc(lp, o, range_hops(YEAR - 50 * DAY, YEAR, 5 * DAY), [MONTH, WEEK, DAY])
     lp.close()
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_partitioned_partition_without_edges(P):
+    """A partition that owns only vertex adds (no edge has an endpoint it owns) has no time-ordered
+    slots; the ghost-membership decision (ghost_vm_free) must still be the same on every partition
+    (ensure_tab agrees on it), or that partition enters an exchange its peers skip."""
+    from raphtory_amd.partition import get_partition
+    from raphtory_amd.synth import Stream
+    s = gen_gab(21, 2000, 6000)
+    e = s.kind == 2
+    keep = ~e | ((get_partition(s.src, P) == 0) & (get_partition(np.maximum(s.dst, 0), P) == 0))
+    s = Stream(s.t[keep], s.kind[keep], s.src[keep], s.dst[keep])
+    assert np.any(get_partition(s.src[s.kind == 0], P) == P - 1)  # the edgeless partition owns vertices
+    o = Oracle.from_stream(s)
+    lp = _parts(s, P)
+    end = int(s.t[-1])
+    check_cc(lp, o, range_hops(end - 30 * DAY, end, 2 * DAY), BATCH_WINDOWS)
+    lp.close()

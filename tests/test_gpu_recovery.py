@@ -79,3 +79,24 @@ def test_corrupt_label_record_is_reported(monkeypatch):
     monkeypatch.delenv("RGPU_INJECT_FAIL")
     check_cc(lp, o, hops, BATCH_WINDOWS)
     lp.close()
+
+
+def test_corrupt_count_record_is_reported(monkeypatch):
+    """Partitioned mode: a received component-count record whose label getPartition routes here but
+    no owned vertex holds (injected with RGPU_INJECT_FAIL=cnt) is counted on the device
+    (xchg.hip label_row) instead of being dropped, and the run fails with RGPU_EHIP naming the
+    count; the next run on the same partitions gives the oracle's results."""
+    from raphtory_amd.partitioned import LoopbackPartitions
+    from tests.test_gpu_partitioned import check_cc
+    s = gen_uniform(7, 800, 20_000, t0=T0_README, dt=1_576_800)
+    hops = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, 6 * DAY)
+    o = Oracle.from_stream(s)
+    lp = LoopbackPartitions(3)
+    lp.ingest_stream(s)
+    lp.seal()
+    monkeypatch.setenv("RGPU_INJECT_FAIL", "cnt")
+    with pytest.raises(RGPUError, match="found no owned vertex"):
+        lp.run("cc", hops, BATCH_WINDOWS)
+    monkeypatch.delenv("RGPU_INJECT_FAIL")
+    check_cc(lp, o, hops, BATCH_WINDOWS)
+    lp.close()
