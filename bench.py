@@ -158,6 +158,52 @@ def cpu_baseline(stream, hops, windows, budget_s, n_edges, what, lazy=False):
     }
 
 
+def cpu_same_config(inter, users, hops, budget_s, n_edges):
+    """The CPU oracle on the headline's own stream and views: the day and hour views of
+    the real 1B-update query, at hops drawn uniformly from its 168, replayed from the time slice
+    [hop0 - day, hop167] of the stream (exact: on an add-only stream a view (t, w) depends only on
+    the updates in [t - w, t], tools/make_c4_sliced_goldens.py, tests/test_c4_slice.py).  Windows
+    [day, hour] keep their vertex sets (the running minimum of [y,m,w,d,h] at those positions is the
+    window itself).  The slice holds only the entities active in the last 8 days, where the
+    reference's lens scans every vertex of its shard each superstep (ReaderWorker.scala:171,202), so
+    this CPU time is a lower bound on the reference structure's.  Value = edge entities of the whole
+    graph x 2 windows x hops done / time, the metric's own definition."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import Oracle
+    from raphtory_amd.synth import DAY, HOUR, Stream, gen_gab_range
+    from tools.make_c4_sliced_goldens import first_at
+    threads, _, _ = cpu_info()
+    t0 = time.perf_counter()
+    first = first_at(int(hops[0]) - DAY, inter, inter)
+    parts = [gen_gab_range(4, users, inter, f, min(10_000_000, inter - f)) for f in range(first, inter, 10_000_000)]
+    sl = Stream(*(np.concatenate([getattr(p, k) for p in parts]) for k in ("t", "kind", "src", "dst")))
+    del parts
+    o = Oracle.from_stream(sl, lazy=True)
+    n_slice = len(sl)
+    del sl
+    build_s = time.perf_counter() - t0
+    order = np.random.default_rng(0).permutation(len(hops))
+    out = {}
+    for mode, budget in ((0, budget_s), (1, budget_s / 2)):
+        done, t1 = 0, time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            while done < len(order) and time.perf_counter() - t1 < budget:
+                batch = order[done:done + threads]
+                list(ex.map(lambda h: o.cc(int(hops[h]), [DAY, HOUR], max_steps=100, mode=mode), batch))
+                done += len(batch)
+        dt = time.perf_counter() - t1
+        out[mode] = (n_edges * 2 * done / dt, done, dt)
+    o.close()
+    return {"value": out[0][0], "unit": "edge-windows/s", "cores": threads, "kind": "port",
+            "windows": "day, hour (2 of the query's 5)",
+            "sample": f"the 1B headline's own day and hour views: {out[0][1]} of {len(hops)} hops (uniform random), "
+                      f"oracle refsim mode, {out[0][2]:.1f} s on {threads} threads, replayed from the time slice "
+                      f"[hop0 - day, hop167] ({n_slice} updates; slice + oracle build {build_s:.1f} s, not timed); "
+                      "a lower bound on the reference structure's time (its lens scans every shard vertex)",
+            "fast_oracle": {"value": out[1][0], "unit": "edge-windows/s",
+                            "sample": f"{out[1][1]} hops, oracle mode 1 (cached adjacency), {out[1][2]:.1f} s"}}
+
+
 def setup_latency(g, hops, windows, n=40):
     """The per-Setup drop-in path (GpuReaderWorker): one rgpu_run_view_batch
     per hop (1 hop x |windows|, RGPU_RUN_RETAIN) followed by rgpu_cc_result per window (the
@@ -456,6 +502,8 @@ def run_c4(a, rank, world, local):
         cpu = cpu_baseline(sm, sm_hops, windows, a.cpu_seconds, sm_edges,
                            f"C4 query on the 1/100-scale GAB stream ({len(sm)} updates, {users // 100} users, "
                            f"{sm_edges} edge entities, same span)", lazy=True)
+        if inter == 333_333_334 and len(hops) == 168:  # the headline query itself
+            cpu["same_config"] = cpu_same_config(inter, users, hops, a.cpu_seconds, n_edges)
     secondary = None
     if rank == 0 and world == 1 and not a.no_secondary and not a.profile_only:
         secondary = run_c2(a, 0, 1, local, quiet=True)

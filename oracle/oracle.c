@@ -1017,3 +1017,202 @@ done:
   free(mem); free(sset); free(st); free(qv); free(qc); free(nb); free(list); free(mark);
   return rc;
 }
+
+/* ============================================================ add-only streams (C4 / GAB)
+ * A memory-compact restatement for streams of VertexAdds and EdgeAdds only, in time order
+ * (GabUserGraphRouter.scala:31-33 emits nothing else).  Every history point is then an add, and
+ * Entity.aliveAtWithWindow (Entity.scala:193-201) — floor(t) is an add and t - floor(t) <= w —
+ * holds iff the entity has a point in [t - w, t] (the floor is the newest point <= t).  A vertex
+ * has a point at its VertexAdds and at every EdgeAdd touching it (EntityStorage.scala:240,259);
+ * an edge (s,d) at its EdgeAdds.  So the view (t, w) is read off the time-sorted stream itself:
+ * its members are the endpoints of the updates with time in [t - w_v, t] (w_v = min(w_0..w_i),
+ * WindowLens.shrinkWindow), its edges the EdgeAdds in [t - w_i, t] (WindowLens.scala:54-65) — no
+ * per-entity TreeMap, so a year of the 1B-update C4 stream fits in memory.
+ * ConnectedComponents (ConnectedComponents.scala:10-35) runs as the Jacobi form of its BSP:
+ * label_r(v) = min(label_{r-1}(v), label_{r-1}(u) for u in N(v)) over members and edges with both
+ * ends members (a message to a non-member is never processed, WindowLens.scala:41-50).  A vertex
+ * whose neighbour did not change in r-1 already received that label, so this is the message form
+ * of orc_cc exactly.  The hop's supersteps: a window's labels change in steps 1..D_w exactly (the
+ * vertex at distance k from its component minimum changes at step k), so the BSP, which halts
+ * when no window improved (AnalysisTask.scala:208-225), runs min(maxSteps, 1 + max_w D_w) steps.
+ * Checked against orc_cc on random add-only streams and the C4 prefix goldens
+ * (tests/test_oracle_addonly.py). */
+struct orc_addonly {
+  const int64_t* t;      /* the caller's time column (kept alive by the caller) */
+  size_t n;
+  int32_t *s, *d;        /* dense ranks of src / dst (d = -1 for a VertexAdd) */
+  int64_t* ids;          /* rank -> id, ascending */
+  size_t nv;
+};
+
+
+orc_addonly* orc_addonly_build(const int64_t* t, const uint8_t* kind, const int64_t* src, const int64_t* dst,
+                               size_t n) {
+  orc_addonly* a = (orc_addonly*)calloc(1, sizeof(orc_addonly));
+  if (!a) return NULL;
+  a->t = t;
+  a->n = n;
+  a->s = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
+  a->d = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
+  HMap m;
+  memset(&m, 0, sizeof(m));
+  int64_t* tmp = NULL;
+  size_t k = 0;
+  if (!a->s || !a->d || hm_init(&m, 1 << 20) != 0) goto fail;
+  for (size_t i = 0; i < n; i++) { /* validation, then the distinct ids in first-seen order */
+    if ((kind[i] != ORC_VADD && kind[i] != ORC_EADD) || t[i] < 0 || (i && t[i] < t[i - 1])) goto fail;
+    for (int e = 0; e < (kind[i] == ORC_EADD ? 2 : 1); e++) {
+      const int64_t id = e ? dst[i] : src[i];
+      if (id < 0 || id >= ((int64_t)1 << 31)) goto fail;
+      if (hm_get(&m, (uint64_t)id) < 0) {
+        if (hm_put(&m, (uint64_t)id, (int32_t)k) != 0) goto fail;
+        k++;
+      }
+    }
+  }
+  a->nv = k;
+  a->ids = (int64_t*)malloc(sizeof(int64_t) * (k ? k : 1));
+  tmp = (int64_t*)malloc(sizeof(int64_t) * (k ? k : 1));
+  if (!a->ids || !tmp) goto fail;
+  for (size_t i = 0; i < m.cap; i++)
+    if (m.vals[i] >= 0) a->ids[m.vals[i]] = (int64_t)m.keys[i];
+  memcpy(tmp, a->ids, sizeof(int64_t) * k);
+  qsort(tmp, k, sizeof(int64_t), cmp_i64);  /* ranks in id order: min label = min rank */
+  for (size_t r = 0; r < k; r++) hm_put(&m, (uint64_t)tmp[r], (int32_t)r);
+  memcpy(a->ids, tmp, sizeof(int64_t) * k);
+  for (size_t i = 0; i < n; i++) {
+    a->s[i] = hm_get(&m, (uint64_t)src[i]);
+    a->d[i] = kind[i] == ORC_EADD ? hm_get(&m, (uint64_t)dst[i]) : -1;
+  }
+  free(tmp);
+  free(m.keys);
+  free(m.vals);
+  return a;
+fail:
+  free(tmp);
+  free(m.keys);
+  free(m.vals);
+  orc_addonly_free(a);
+  return NULL;
+}
+
+void orc_addonly_free(orc_addonly* a) {
+  if (!a) return;
+  free(a->s);
+  free(a->d);
+  free(a->ids);
+  free(a);
+}
+
+size_t orc_addonly_num_vertices(const orc_addonly* a) { return a->nv; }
+
+static size_t first_ge(const int64_t* t, size_t n, int64_t x) { /* first index with t >= x */
+  size_t lo = 0, hi = n;
+  while (lo < hi) {
+    size_t mid = (lo + hi) / 2;
+    if (t[mid] >= x) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+/* one window: members (mem), labels after min(max_steps, D + 1) Jacobi steps; returns D, the
+ * last step in which a label changed (capped runs: max_steps), or -1 on allocation failure */
+static int addonly_window(const orc_addonly* a, int64_t tq, int64_t wv, int64_t we, int max_steps, uint8_t* mem,
+                          int32_t* lab) {
+  const size_t nv = a->nv, hi = first_ge(a->t, a->n, tq == INT64_MAX ? tq : tq + 1);
+  const size_t lv = wv < 0 ? 0 : first_ge(a->t, hi, tq - wv < 0 ? 0 : tq - wv);
+  const size_t le = we < 0 ? 0 : first_ge(a->t, hi, tq - we < 0 ? 0 : tq - we);
+  memset(mem, 0, nv);
+  for (size_t i = lv; i < hi; i++) {
+    mem[a->s[i]] = 1;
+    if (a->d[i] >= 0) mem[a->d[i]] = 1;
+  }
+  for (size_t v = 0; v < nv; v++) lab[v] = (int32_t)v;
+  if (max_steps <= 1) return 0;
+  size_t* off = (size_t*)calloc(nv + 1, sizeof(size_t));
+  int32_t* nxt = (int32_t*)malloc(sizeof(int32_t) * (nv ? nv : 1));
+  uint8_t* chg = (uint8_t*)malloc(nv ? nv : 1);
+  uint8_t* chn = (uint8_t*)malloc(nv ? nv : 1);
+  int32_t* adj = NULL;
+  int D = -1;
+  if (!off || !nxt || !chg || !chn) goto out;
+  for (size_t i = le; i < hi; i++) {
+    const int32_t s = a->s[i], d = a->d[i];
+    if (d < 0 || !mem[s] || !mem[d]) continue;
+    off[s + 1]++;
+    off[d + 1]++;
+  }
+  for (size_t v = 0; v < nv; v++) off[v + 1] += off[v];
+  adj = (int32_t*)malloc(sizeof(int32_t) * (off[nv] ? off[nv] : 1));
+  if (!adj) goto out;
+  {
+    size_t* fill = (size_t*)malloc(sizeof(size_t) * (nv ? nv : 1));
+    if (!fill) goto out;
+    memcpy(fill, off, sizeof(size_t) * nv);
+    for (size_t i = le; i < hi; i++) {
+      const int32_t s = a->s[i], d = a->d[i];
+      if (d < 0 || !mem[s] || !mem[d]) continue;
+      adj[fill[s]++] = d;
+      adj[fill[d]++] = s;
+    }
+    free(fill);
+  }
+  /* Setup (superstep 0): every member sends its own id; supersteps 1..: the changed ones send */
+  for (size_t v = 0; v < nv; v++) chg[v] = mem[v];
+  D = 0;
+  for (int r = 1;; r++) {
+    memcpy(nxt, lab, sizeof(int32_t) * nv);
+    for (size_t u = 0; u < nv; u++) {
+      if (!chg[u]) continue;
+      const int32_t x = lab[u];
+      for (size_t k = off[u]; k < off[u + 1]; k++)
+        if (x < nxt[adj[k]]) nxt[adj[k]] = x;
+    }
+    int any = 0;
+    for (size_t v = 0; v < nv; v++) {
+      chn[v] = nxt[v] < lab[v];
+      any |= chn[v];
+    }
+    memcpy(lab, nxt, sizeof(int32_t) * nv);
+    { uint8_t* x = chg; chg = chn; chn = x; }
+    if (any) D = r;
+    if (!any || r == max_steps) break;
+  }
+out:
+  free(off); free(nxt); free(chg); free(chn); free(adj);
+  return D;
+}
+
+int orc_addonly_cc(const orc_addonly* a, int64_t t, const int64_t* windows, int nw, int max_steps, int64_t* ids,
+                   int64_t* labels, size_t cap, size_t* n_out, int* steps) {
+  if (nw < 0 || nw > 64) return -1;
+  const size_t nv = a->nv, nvs = nv ? nv : 1;
+  uint8_t* mem = (uint8_t*)malloc(nvs);
+  int32_t* lab = (int32_t*)malloc(sizeof(int32_t) * nvs);
+  int rc = -1, dmax = 0;
+  if (!mem || !lab) goto done;
+  int64_t run_min = INT64_MAX;
+  for (int i = 0; i < (nw ? nw : 1); i++) {
+    const int64_t we = nw ? windows[i] : -1;
+    if (nw && we < 0) goto done;
+    if (nw && we < run_min) run_min = we;
+    const int D = addonly_window(a, t, nw ? run_min : -1, we, max_steps, mem, lab);
+    if (D < 0) goto done;
+    if (D > dmax) dmax = D;
+    size_t k = 0;
+    for (size_t v = 0; v < nv; v++) {
+      if (!mem[v]) continue;
+      if (k >= cap) goto done;
+      ids[(size_t)i * cap + k] = a->ids[v];
+      labels[(size_t)i * cap + k] = a->ids[lab[v]];
+      k++;
+    }
+    n_out[i] = k;
+  }
+  *steps = max_steps <= 1 ? 0 : (dmax + 1 < max_steps ? dmax + 1 : max_steps);
+  rc = 0;
+done:
+  free(mem);
+  free(lab);
+  return rc;
+}

@@ -94,6 +94,20 @@ int orc_vertex_program(const orc_graph* g, int64_t t, const int64_t* windows, in
 int orc_pagerank(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int iters,
                  int64_t* ids, double* pr, size_t cap, size_t* n_out);
 
+/* Add-only streams (VertexAdds and EdgeAdds in time order — the GAB / C4 shape): a
+ * memory-compact restatement that reads each view off the time-sorted stream (oracle.c, "add-only
+ * streams", for why that is exact) instead of replaying it into per-entity TreeMaps.  The caller
+ * keeps t alive while the object lives.  NULL on another kind, a time out of order, or a bad id.
+ * orc_addonly_cc: orc_cc's output contract (per window the members in ascending id and their
+ * labels; the hop's superstep count). */
+typedef struct orc_addonly orc_addonly;
+orc_addonly* orc_addonly_build(const int64_t* t, const uint8_t* kind, const int64_t* src, const int64_t* dst,
+                               size_t n);
+void orc_addonly_free(orc_addonly* a);
+size_t orc_addonly_num_vertices(const orc_addonly* a);
+int orc_addonly_cc(const orc_addonly* a, int64_t t, const int64_t* windows, int nw, int max_steps, int64_t* ids,
+                   int64_t* labels, size_t cap, size_t* n_out, int* steps);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,7 +16,6 @@ S/ = mainproject/cluster/src/main/scala/com/raphtory/ in the reference.
 from __future__ import annotations
 
 import json
-import math
 import threading
 import time
 from typing import Dict, List, Optional, Sequence
@@ -24,32 +23,15 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from .graph import TemporalGraph
+from .jfloat import double_to_string, float_to_string
 from .synth import range_hops
 
 
 # ---------------------------------------------------------------- JVM number printing
 def java_float_str(x, double: bool = False) -> str:
-    """Float.toString / Double.toString shape (plain decimal in [1e-3, 1e7), else
-    d.dddE±n; shortest round-trip digits).  JDK-12 digit strings are parity-unpinned."""
-    v = float(np.float64(x) if double else np.float32(x))
-    if math.isnan(v):
-        return "NaN"
-    if math.isinf(v):
-        return "Infinity" if v > 0 else "-Infinity"
-    r = repr(v) if double else np.format_float_positional(np.float32(x), unique=True, trim="-")
-    if v != 0 and not (1e-3 <= abs(v) < 1e7):
-        s = np.format_float_scientific(np.float64(v) if double else np.float32(v), unique=True, trim="-")
-        mant, exp = s.split("e")
-        if "." not in mant:
-            mant += ".0"
-        return f"{mant}E{int(exp)}"
-    if "e" in r or "E" in r:
-        r = np.format_float_positional(np.float64(v), unique=True, trim="-")
-    if "." not in r:
-        r += ".0"
-    if r.endswith("."):
-        r += "0"
-    return r
+    """Float.toString / Double.toString as the reference's JDK 12 prints them: the FloatingDecimal
+    digit generation restated in jfloat.py (not always the shortest round-trip string)."""
+    return double_to_string(float(x)) if double else float_to_string(float(np.float32(x)))
 
 
 # ---------------------------------------------------------------- analysers

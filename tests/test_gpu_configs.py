@@ -13,10 +13,16 @@
                                                                   supersteps and a checksum of every
                                                                   member's label vs the oracle's
                                                                   committed goldens
-      the whole 1B stream                                         summary invariants + another batch
-                                                                  composition of three hops
+      the whole 1B stream                                         summary invariants on all 840 views;
+                                                                  at 8 hops every window (year too)
+                                                                  and the hop's supersteps vs the
+                                                                  sliced oracle's goldens; another
+                                                                  batch composition of those hops
   C5  30M-update GAB base + one 10M-update hour tick merged       labels / PR / counts equal to a
       into the resident graph, CC + PR(20) on the newest hour     one-shot seal of the same stream
+      the bench's C5: 100M-update base + 6 ticks of 10M updates,  every window after ticks 0 and 5 vs
+      each merged live, CC {y,m,w,d,h} at the live time           the add-only oracle's goldens; PR(20,
+                                                                  hour) at tick 5 vs the oracle (L1)
 
 The oracle at C3/C4 size is the lazy-edge replay (oracle.h ORC_LAZY_EDGES, checked against the
 literal replay in tests/test_oracle_scale.py); it is built in a background thread while the GPU
@@ -225,10 +231,11 @@ def test_c4_full_1b_vs_sliced_oracle_goldens():
     fields, member count and the checksum of every member's (id, label).  The oracle replays the
     stream's last 37 days, which is exact for these windows on an add-only stream
     (tools/make_c4_sliced_goldens.py; tests/test_c4_slice.py checks it on the 100M prefix).
-    The year views (a year of the stream does not fit the oracle here) are checked by the
-    invariants and by another batch composition: the sampled hops re-run as one hop-major batch
-    (other superstep interleaving, other heavy / uniform-word paths) give the window-major
-    query's summaries."""
+    The year views (round 5): the add-only restatement of the oracle over the year slice
+    (tools/make_c4_sliced_goldens.py --year; it reproduces the literal replay's month..hour records
+    at every sampled hop) gives their records and the hops' superstep counts too.  The sampled hops
+    re-run as one hop-major batch (other superstep interleaving, other heavy / uniform-word paths)
+    must also give the window-major query's summaries."""
     users, inter = 20_000_000, 333_333_334
     g = TemporalGraph()
     for first in range(0, inter, 20_000_000):
@@ -254,6 +261,8 @@ def test_c4_full_1b_vs_sliced_oracle_goldens():
         for k, h in enumerate(pick):
             rec = _SLICED["hops"][str(h)]
             assert int(hops[h]) == rec["t"]
+            if "supersteps" in rec:  # (the year views are in: the hop's count is the oracle's)
+                assert full[h, 0, 7] == rec["supersteps"], (h, full[h, 0, 7], rec["supersteps"])
             for j, w in enumerate(_SLICED["window_index_in_query"]):
                 ids, lab = g.cc_vertex_labels(k, w)
                 _check_view(full[h, w], ids, lab, rec["windows"][j], ("1B", h, w))
@@ -338,3 +347,50 @@ def test_c5_ten_million_update_tick_equals_one_shot_seal():
     assert np.array_equal(ia, ib) and np.abs(pa - pb).sum() <= PR_L1_TOL
     live.close()
     one.close()
+
+
+_C5_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5_goldens.json")
+
+
+@pytest.mark.skipif(not os.path.exists(_C5_PATH), reason="no C5 goldens")
+def test_c5_live_at_size_vs_oracle():
+    """BASELINE configs[4] as bench.py --config c5 runs it at N = 1: the 100M-update base sealed, then
+    6 hour ticks of 10M updates each ingested and merged into the resident graph (the live path:
+    device delta packer + merge; after the first run every merged graph is parked and swapped in by
+    the next run).  After ticks 0 and 5, CC over {y,m,w,d,h} at the live time (the newest update,
+    LiveAnalysisTask.setLiveTime) against the oracle's goldens (tools/make_c5_goldens.py: the
+    add-only restatement over the whole C5 stream): every window's summary fields, member count and
+    (id, label) checksum, and the hop's superstep count.  After tick 5, PageRank(20, hour) against
+    the literal oracle replaying the updates of the last hour (an add-only view depends on nothing
+    older), L1 <= 1e-6."""
+    from tools.make_c5_goldens import c5_stream
+    G = json.load(open(_C5_PATH))
+    base, ticks = c5_stream()
+    g = _graph(base, "id")
+    del base
+    for i, tick in enumerate(ticks):
+        g.ingest_stream(tick)
+        g.seal()
+        assert g.stats()["seal_incremental"] == 1
+        live = g.newest_time()
+        rec = G["at"].get(str(i))
+        g.run("cc", [live], BATCH_WINDOWS, retain=rec is not None)
+        if rec is None:
+            continue
+        assert live == rec["live"]
+        full = g.cc_summaries()
+        assert full[0, 0, 7] == rec["supersteps"], (i, full[0, 0, 7], rec["supersteps"])
+        for w in range(5):
+            ids, lab = g.cc_vertex_labels(0, w)
+            _check_view(full[0, w], ids, lab, rec["windows"][w], ("C5 tick", i, w))
+    # PageRank(20) over the newest hour, against the literal replay of the updates of the last hour
+    # (from every tick: ticks overlap in time; the base ends hours before)
+    g.run("pagerank", [live], [HOUR], pr_iters=20, retain=True)
+    keep = [x.t >= live - HOUR for x in ticks]
+    o = Oracle(*(np.concatenate([getattr(x, f)[k] for x, k in zip(ticks, keep)]) for f in ("t", "kind", "src", "dst")))
+    (ids, pr), = o.pagerank(live, [HOUR], iters=20)
+    gids, gpr = g.pr_result(0, 0)
+    assert np.array_equal(gids, ids)
+    assert np.abs(gpr - pr).sum() <= PR_L1_TOL
+    o.close()
+    g.close()

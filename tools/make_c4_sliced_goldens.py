@@ -27,7 +27,15 @@ summary, member count and label checksum in every window it covers.
 The slice's first interaction is found by bisection on the generator itself (gen_gab_range
 draws any interaction range; times are monotone in the index, synth.c rg_gen_gab_range).
 
-usage: python tools/make_c4_sliced_goldens.py [--hops 8] [--threads 8]
+Round 5, --year: the year views too.  A year of the stream (~550M updates) does not fit the
+literal replay here (~200 B per update), so the add-only restatement (oracle.h orc_addonly_*, the
+view read off the time-sorted stream; checked against the literal replay in
+tests/test_oracle_addonly.py and on the 100M / 300M prefix goldens) replays the year slice and
+gives all five windows and the hop's superstep count.  Its month / week / day / hour records must
+equal the literal-replay records already in the file (the run stops otherwise); the year records
+and the superstep counts are added.
+
+usage: python tools/make_c4_sliced_goldens.py [--hops 8] [--threads 8] [--year]
 """
 import argparse
 import json
@@ -137,13 +145,89 @@ def verify_prefix(threads: int, out_path: str) -> bool:
     return ok
 
 
+def sliced_arrays(n: int, t_from: int, inter: int = INTER, chunk: int = 20_000_000):
+    """interactions [first_at(t_from), n) generated straight into preallocated columns (no
+    concatenated copy: a year slice is ~550M updates), and that first index"""
+    first = first_at(t_from, n, inter)
+    m = 3 * (n - first)
+    t, k, s, d = (np.empty(m, np.int64), np.empty(m, np.uint8), np.empty(m, np.int64), np.empty(m, np.int64))
+    o = 0
+    for a in range(first, n, chunk):
+        p = gen_gab_range(SEED, USERS, inter, a, min(chunk, n - a))
+        q = len(p)
+        t[o:o + q], k[o:o + q], s[o:o + q], d[o:o + q] = p.t, p.kind, p.src, p.dst
+        o += q
+        del p
+    assert o == m
+    return (t, k, s, d), first
+
+
+def year_views(n: int, sel, threads: int, inter: int = INTER, log=print):
+    """all five windows and the hop's superstep count at the sampled hops, by the add-only
+    restatement over the year slice"""
+    from oracle import AddOnlyOracle
+    from raphtory_amd.synth import YEAR
+    t0 = time.time()
+    hops = headline_hops(n, inter)
+    (t, k, s, d), first = sliced_arrays(n, int(hops[0]) - YEAR, inter)
+    log(f"year slice from interaction {first}: {len(t)} updates generated in {time.time() - t0:.0f} s")
+    o = AddOnlyOracle(t, k, s, d)
+    meta = {"year_first_interaction": int(first), "year_slice_updates": int(len(t)), "year_slice_t0": int(t[0]),
+            "year_slice_vertices": int(o.nv)}
+    del k, s, d
+    log(f"add-only oracle built in {time.time() - t0:.0f} s ({o.nv} vertices)")
+
+    def one(h):
+        res, steps = o.cc(int(hops[h]), BATCH_WINDOWS)
+        return h, steps, [view_record(ids, lab) for ids, lab in res]
+
+    views = {}
+    with ThreadPoolExecutor(threads) as ex:
+        for h, steps, recs in ex.map(one, sel):
+            views[str(h)] = {"t": int(hops[h]), "supersteps": int(steps), "windows": recs}
+            log(f"  hop {h}: {steps} supersteps, {time.time() - t0:.0f} s")
+    o.close()
+    return meta, views
+
+
+def add_year(threads: int):
+    data = json.load(open(OUT))
+    assert data["windows"] == BATCH_WINDOWS[1:] and data["window_index_in_query"] == [1, 2, 3, 4]
+    sel = sorted(int(h) for h in data["hops"])
+    meta, views = year_views(INTER, sel, threads, log=lambda m: print(m, flush=True))
+    for h in sel:
+        old = data["hops"][str(h)]
+        new = views[str(h)]
+        assert new["t"] == old["t"], h
+        # the literal replay's month..hour records (already committed) must be reproduced exactly
+        for j in range(4):
+            if new["windows"][1 + j] != old["windows"][j]:
+                raise SystemExit(f"hop {h} window {BATCH_WINDOWS[1 + j]}: add-only {new['windows'][1 + j]} != "
+                                 f"literal {old['windows'][j]}")
+        print(f"hop {h}: month..hour == literal replay; year members {new['windows'][0]['members']}, "
+              f"{new['supersteps']} supersteps", flush=True)
+        data["hops"][str(h)] = {"t": new["t"], "supersteps": new["supersteps"], "windows": new["windows"]}
+    data["windows"] = list(BATCH_WINDOWS)
+    data["window_index_in_query"] = [0, 1, 2, 3, 4]
+    data["year_oracle"] = ("add-only restatement (oracle.h orc_addonly_cc) over the year slice; month..hour "
+                           "equal to the literal replay over the 37-day slice")
+    data.update(meta)
+    with open(OUT, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
+    print(f"-> {OUT}", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--hops", type=int, default=8, help="hops sampled over the 168")
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--verify-prefix", action="store_true",
                     help="check the slice argument against the full-prefix goldens (month..hour)")
+    ap.add_argument("--year", action="store_true",
+                    help="add the year views and superstep counts (add-only oracle over the year slice)")
     a = ap.parse_args()
+    if a.year:
+        return add_year(a.threads)
     if a.verify_prefix:
         sys.exit(0 if verify_prefix(a.threads, os.path.join(ROOT, "profiles", "r04", "c4_slice_equivalence.txt"))
                  else 1)
