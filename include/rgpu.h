@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define RGPU_ABI_VERSION 9
+#define RGPU_ABI_VERSION 10
 
 /* error codes */
 #define RGPU_OK 0
@@ -202,6 +202,13 @@ int rgpu_newest_time(rgpu_ctx* ctx, int64_t* out);
 #define RGPU_XCHG_SHM 2
 int rgpu_exchange_id(int kind, uint8_t* out /* RGPU_XCHG_ID_BYTES */);
 int rgpu_exchange_init(rgpu_ctx* ctx, const void* id /* RGPU_XCHG_ID_BYTES */);
+/* rgpu_exchange_probe (ABI 10): the partitioned superstep's fixed cost on this context's channel,
+ * measured — `rounds` repetitions of a round's collectives and host round trip besides its kernels
+ * (the counts all-to-all, the counts' copy to the host and the host's wait, the two grouped
+ * send/recv of the label records; AnalysisTask's per-superstep barrier, AnalysisTask.scala:208-225)
+ * and of a 64-word all-reduce.  us[4] = round mean, round median, all-reduce mean, all-reduce median,
+ * in microseconds.  Collective: every partition calls it with the same rounds. */
+int rgpu_exchange_probe(rgpu_ctx* ctx, int rounds, double* us /* [4] */);
 
 /* Run one analyser over every (hop, window) view: hops[n_hops] are the Range hop
  * timestamps (RangeAnalysisTask.restart, RangeAnalysisTask.scala:18-35), windows[n_w]

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD_DIR = os.path.join(_HERE, "_build")
 
 # error codes / constants mirrored from include/rgpu.h
-ABI_VERSION = 9
+ABI_VERSION = 10
 RGPU_OK = 0
 RGPU_EINVAL, RGPU_ESTATE, RGPU_EHIP, RGPU_ENOMEM, RGPU_ENOTSUP = -1, -2, -3, -4, -5
 RGPU_VADD, RGPU_VDEL, RGPU_EADD, RGPU_EDEL = 0, 1, 2, 3
@@ -39,7 +39,7 @@ EXPORTS = [
     "rgpu_stats", "rgpu_last_error", "rgpu_close",
     "rgpu_rgev_encode", "rgpu_rgev_decode", "rgpu_rgev_last_error", "rgpu_ingest_rgev",
     "rgpu_set_diffusion", "rgpu_diffusion_result", "rgpu_diffusion_vertex", "rgpu_set_vertex_order",
-    "rgpu_set_vertex_program", "rgpu_vp_result", "rgpu_vp_supersteps",
+    "rgpu_set_vertex_program", "rgpu_vp_result", "rgpu_vp_supersteps", "rgpu_exchange_probe",
 ]
 
 
@@ -87,6 +87,7 @@ _SIGS = {
     "rgpu_set_vertex_order": (C.c_int, [_CTX, C.c_int]),
     "rgpu_exchange_id": (C.c_int, [C.c_int, C.c_char_p]),
     "rgpu_exchange_init": (C.c_int, [_CTX, C.c_char_p]),
+    "rgpu_exchange_probe": (C.c_int, [_CTX, C.c_int, _PD]),
     "rgpu_run_view_batch": (C.c_int, [_CTX, C.c_int, _P64, _SZ, _P64, _SZ, C.c_int, C.c_int, C.c_int]),
     "rgpu_cc_summary": (C.c_int, [_CTX, _SZ, _SZ, C.POINTER(CCSummary)]),
     "rgpu_cc_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P32, _SZ, C.POINTER(_SZ)]),

@@ -204,11 +204,32 @@ __device__ __forceinline__ void store_bits(const uint64_t (&m)[PLANAR ? kMaxPlan
 
 // (the hop table and the interval / per-hop window bits: window_bits.hpp)
 
+// The floors at a sorted block's first and last hop.  carry == 2: the entity's floor at the run's
+// previous block's last hop (fc[i], relative to lo; that hop <= hop[0]) is advanced instead of
+// searched — a history rarely has a point between two adjacent blocks, so this is one compare in
+// place of a binary search (§8(f) row 2, RangeAnalysisTask.restart's hop after hop).  The floor
+// at the last hop is advanced from the first's either way (few points fall inside a block).
+__device__ __forceinline__ void block_floors(const int64_t* __restrict__ key, int64_t lo, int64_t hi,
+                                             const BatchParams& bp, const HopLDS& L, const int32_t* __restrict__ fc,
+                                             int64_t i, int64_t& f0, int64_t& f1) {
+  if (bp.carry == 2) {
+    const int32_t c = fc[i];
+    f0 = floor_advance(key, c < 0 ? -1 : lo + c, lo, hi, L.hop[0]);
+  } else {
+    f0 = floor_idx(key, lo, hi, L.hop[0]);
+  }
+  f1 = bp.carry ? floor_advance(key, f0, lo, hi, L.hop[L.K - 1]) : floor_idx(key, lo, hi, L.hop[L.K - 1]);
+}
+__device__ __forceinline__ void store_carry(int32_t* __restrict__ fc, const BatchParams& bp, int64_t i, int64_t f1,
+                                            int64_t lo) {
+  if (bp.carry) fc[i] = f1 < 0 ? -1 : (int32_t)(f1 - lo);
+}
+
 template <bool PLANAR>
 __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* __restrict__ voff,
                                                      const int64_t* __restrict__ vkey, BatchParams bp,
                                                      uint64_t* __restrict__ vm, int64_t vstride,
-                                                     BatchClear clr) {
+                                                     BatchClear clr, int32_t* __restrict__ fc) {
   __shared__ HopLDS L;
   hop_lds_init(L, bp, bp.thr_v);
   batch_clear(clr);
@@ -217,10 +238,12 @@ __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* 
        v += (int64_t)gridDim.x * blockDim.x) {
     const int64_t lo = voff[v], hi = voff[v + 1];
     uint64_t m[PLANAR ? kMaxPlanes : 1] = {};
-    if (bp.sorted && bp.iv_max >= 0) {
-      const int64_t f0 = floor_idx(vkey, lo, hi, L.hop[0]);
-      const int64_t f1 = floor_idx(vkey, lo, hi, L.hop[K - 1]);
-      if (f1 - f0 <= bp.iv_max) {  // f1 < 0: dead at every hop
+    int64_t f = -1;
+    if (bp.sorted) {
+      int64_t f0, f1;
+      block_floors(vkey, lo, hi, bp, L, fc, v, f0, f1);
+      store_carry(fc, bp, v, f1, lo);
+      if (bp.iv_max >= 0 && f1 - f0 <= bp.iv_max) {  // f1 < 0: dead at every hop
         for (int64_t i = f0 < 0 ? lo : f0; i <= f1; i++) {
           const int64_t key = vkey[i];
           if (!(key & 1)) continue;  // a deletion: dead over its interval
@@ -231,11 +254,11 @@ __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* 
         store_bits<PLANAR>(m, bp, vm, vstride, v);
         continue;
       }
+      f = f0;
     }
-    int64_t f = -1;
     for (int k = 0; k < K; k++) {
       const int64_t t = L.hop[k];
-      f = (bp.sorted && k > 0) ? floor_advance(vkey, f, lo, hi, t) : floor_idx(vkey, lo, hi, t);
+      if (k > 0 || !bp.sorted) f = bp.sorted ? floor_advance(vkey, f, lo, hi, t) : floor_idx(vkey, lo, hi, t);
       if (f < 0) continue;
       const int64_t key = vkey[f];
       if (!(key & 1)) continue;  // floor is a deletion
@@ -252,7 +275,8 @@ __device__ __forceinline__ void edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1]
                                           const BatchParams& bp, int64_t e, const int32_t* __restrict__ esrc,
                                           const int32_t* __restrict__ edst, const int64_t* __restrict__ eoff,
                                           const int64_t* __restrict__ ekey, const int64_t* __restrict__ doff,
-                                          const int64_t* __restrict__ dtime, const uint64_t* __restrict__ dbits) {
+                                          const int64_t* __restrict__ dtime, const uint64_t* __restrict__ dbits,
+                                          int32_t* __restrict__ fc) {
   const int K = L.K;
   const int64_t lo = eoff[e], hi = eoff[e + 1];
   const int32_t s = esrc[e], d = edst[e];
@@ -260,10 +284,13 @@ __device__ __forceinline__ void edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1]
   // list [0, 0) reads as "no death" everywhere below
   const bool ds = !dbits || ((dbits[s >> 6] >> (s & 63)) & 1), dd = !dbits || ((dbits[d >> 6] >> (d & 63)) & 1);
   const int64_t s0 = ds ? doff[s] : 0, s1 = ds ? doff[s + 1] : 0, d0 = dd ? doff[d] : 0, d1 = dd ? doff[d + 1] : 0;
-  if (bp.sorted && bp.iv_max >= 0) {
-    const int64_t f0 = floor_idx(ekey, lo, hi, L.hop[0]);
-    const int64_t f1 = floor_idx(ekey, lo, hi, L.hop[K - 1]);
-    if (f1 - f0 <= bp.iv_max) {
+  int64_t fb0 = -1;
+  if (bp.sorted) {
+    int64_t f0, f1;
+    block_floors(ekey, lo, hi, bp, L, fc, e, f0, f1);
+    store_carry(fc, bp, e, f1, lo);
+    fb0 = f0;
+    if (bp.iv_max >= 0 && f1 - f0 <= bp.iv_max) {
       for (int64_t i = f0 < 0 ? lo : f0; i <= f1; i++) {
         const int64_t key = ekey[i];
         if (!(key & 1)) continue;
@@ -289,7 +316,7 @@ __device__ __forceinline__ void edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1]
       lds = ps > s0 ? dtime[ps - 1] : -1;
       ldd = pd > d0 ? dtime[pd - 1] : -1;
     } else {
-      f = floor_idx(ekey, lo, hi, t);
+      f = bp.sorted ? fb0 : floor_idx(ekey, lo, hi, t);  // (k == 0 of a sorted block: block_floors)
       lds = s1 > s0 ? last_death(dtime, s0, s1, t) : -1;
       ldd = d1 > d0 ? last_death(dtime, d0, d1, t) : -1;
       if (bp.sorted) {  // k == 0: position the death cursors
@@ -352,7 +379,8 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
                                                    uint64_t* __restrict__ em, int64_t estride,
                                                    unsigned long long* __restrict__ ecnt, int64_t h0,
                                                    int64_t own_lim, const uint64_t* __restrict__ vm_ends,
-                                                   int64_t vstride, const uint64_t* __restrict__ dbits) {
+                                                   int64_t vstride, const uint64_t* __restrict__ dbits,
+                                                   int32_t* __restrict__ fc) {
   __shared__ HopLDS L;
   __shared__ unsigned int cnt_s[PLANAR ? kMaxPlanes : 1][64];
   hop_lds_init(L, bp, bp.thr_e);
@@ -368,7 +396,7 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
     uint64_t mo[NP];  // the edge's own aliveness (the |E_w| counts)
     if (SKIP && e < ne && edge_simple(eoff[e], eoff[e + 1], ekey, esrc[e], edst[e], doff, dbits)) continue;
     if (e < ne) {
-      edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime, dbits);
+      edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime, dbits, fc);
 #pragma unroll
       for (int w = 0; w < NP; w++) mo[w] = m[w];
       if (vm_ends) {  // CC: both endpoints' memberships folded in (K2 then skips vm[nb])
@@ -2375,15 +2403,19 @@ void launch_batch_clear(hipStream_t s, const BatchClear& clr) {
   k_batch_clear<<<16, 256, 0, s>>>(clr);
 }
 void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm,
-                        int64_t vstride, bool planar, const BatchClear& clr) {
-  if (planar) k_vertex_mask<true><<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm, vstride, clr);
-  else k_vertex_mask<false><<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, bp, vm, vstride, clr);
+                        int64_t vstride, bool planar, const BatchClear& clr, int32_t* fc) {
+  BatchParams b = bp;
+  if (!fc || !bp.sorted) b.carry = 0;
+  if (planar) k_vertex_mask<true><<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, b, vm, vstride, clr, fc);
+  else k_vertex_mask<false><<<grid_for(g.nv, 256), 256, 0, s>>>(g.nv, g.voff, g.vkey, b, vm, vstride, clr, fc);
 }
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
                       unsigned long long* ecnt, int64_t h0, const uint64_t* vm_ends, int64_t vstride,
-                      bool skip_simple) {
-#define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, bp, em, g.ne, ecnt, h0, g.n_own, vm_ends, \
-    vstride, g.dbits
+                      bool skip_simple, int32_t* fc) {
+  BatchParams b = bp;
+  if (!fc || !bp.sorted) b.carry = 0;
+#define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, b, em, g.ne, ecnt, h0, g.n_own, vm_ends, \
+    vstride, g.dbits, fc
   const unsigned grid = grid_for(g.ne, 256);
   if (planar && ecnt) k_edge_mask<true, true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
   else if (planar && skip_simple) k_edge_mask<true, false, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);

@@ -42,6 +42,10 @@ struct BatchParams {
   // slot's window bits imply both endpoints' membership (an EADD is a `+` point of both endpoints,
   // neither of which ever dies), so K2 / the ghost marking skip the neighbour's mask read for it
   int simple_ends;
+  // K1 floor carry across a run's hop blocks (§8(f) row 2): 0 off; 1 write each
+  // entity's floor index at hop[K-1] into the carry array; 2 also read the previous block's (its
+  // last hop <= this block's hop[0]) and advance it instead of searching the history from scratch
+  int carry;
 };
 
 // Sealed partition resident in HBM.
@@ -138,15 +142,16 @@ void launch_lane_fold(hipStream_t s, unsigned long long* lanechg, unsigned long 
 // kMaxPlanes): one word per window w at out[w*stride + i], bit k = hop of the block.
 constexpr int kMaxPlanes = 8;
 void launch_batch_clear(hipStream_t s, const BatchClear& clr);
+// fc (bp.carry != 0): per-entity floor carry, int32 index relative to the entity's first point (-1 none)
 void launch_vertex_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* vm,
-                        int64_t vstride, bool planar, const BatchClear& clr);
+                        int64_t vstride, bool planar, const BatchClear& clr, int32_t* fc = nullptr);
 // ecnt (profile runs, else null): alive edges per view (|E_w| of SURVEY §8(d)) added into
 // ecnt[(h0 + k) * W + w] for hop k of the block (first hop h0 of the run) and window w
 // vm_ends (CC runs, one partition): the vertex masks of the same block (plane stride vstride);
 // each edge word is ANDed with both endpoints' words, so that K2 keeps a slot on em alone
 void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, uint64_t* em, bool planar,
                       unsigned long long* ecnt = nullptr, int64_t h0 = 0, const uint64_t* vm_ends = nullptr,
-                      int64_t vstride = 0, bool skip_simple = false);
+                      int64_t vstride = 0, bool skip_simple = false, int32_t* fc = nullptr);
 // tcut: no view of the batch can keep an edge whose last add is older (time-ordered slots)
 // ebp (time-ordered slots only; else null): the batch's hops and edge windows, non-planar bit layout
 // (view bit w*KS + k): K2 computes the window bits of simple slots inline (kernels.hip simple_bits)

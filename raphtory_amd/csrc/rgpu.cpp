@@ -252,6 +252,13 @@ struct rgpu_ctx {
   int heavy_t = 2048;                   // static slots above which a vertex is split (hub_threshold)
   int heavy_env = -1;                   // RGPU_HEAVY (0: off), or -1: hub_threshold's rule
   MaskSet mset[kMaskSets];
+  // K1 floor carry across a run's hop blocks (BatchParams::carry; RGPU_K1_CARRY=0 turns it off):
+  // per-entity floor index at the last K1'd block's last hop, that hop, and an event after that
+  // K1 (the next block's K1, on another slot's stream, waits for it)
+  int32_t *k1c_v = nullptr, *k1c_e = nullptr;
+  hipEvent_t k1_ev = nullptr;
+  int64_t k1_last = INT64_MIN;          // INT64_MIN: no carry to read
+  bool k1_carry = true;
   int grp_last[kMaxPlanes] = {};        // supersteps of the last batch of each window group
   // last run: views (hop, win) -> batch (hop/K)*G + win/gsize, lane (win%gsize)*K + hop%K
   int algo = -1, K = 0, W = 0, G = 1, gsize = 1;
@@ -353,6 +360,10 @@ void release_slots(rgpu_ctx* c) {
       if (e) (void)hipEventDestroy(e);
     m = MaskSet();
   }
+  c->k1c_v = c->k1c_e = nullptr;  // (in slot_allocs)
+  if (c->k1_ev) (void)hipEventDestroy(c->k1_ev);
+  c->k1_ev = nullptr;
+  c->k1_last = INT64_MIN;
 }
 
 hipEvent_t take_event(rgpu_ctx* c) {
@@ -446,6 +457,12 @@ void timed_launch(rgpu_ctx* c, int si, int kid, double bytes, F fn, int step = 0
 void ensure_masks(rgpu_ctx* c, int G, int nuse) {
   auto& L = c->slot_allocs;
   const int64_t nv = c->cap_nv, ne = c->cap_ne;
+  if (c->k1_carry && !c->k1c_v) {
+    c->k1c_v = dalloc<int32_t>(L, nv);
+    c->k1c_e = dalloc<int32_t>(L, ne);
+    HIPCHK(hipEventCreateWithFlags(&c->k1_ev, hipEventDisableTiming));
+  }
+  c->k1_last = INT64_MIN;  // (called once per run, before its first block)
   if (G == 1) {
     for (int i = 0; i < nuse; i++) {
       Slot& s = c->slot[i];
@@ -888,13 +905,27 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   }
   s.iem = iem;
   s.ebp = ebp;
+  // K1 floor carry (BatchParams::carry): read the previous block's floors when its last hop is
+  // not after this block's first; write this block's for the next
+  const bool k1_runs = rc.G == 1 || grp == 0;
+  if (k1_runs && c->k1_carry && c->k1c_v && bp.sorted) {
+    bp.carry = c->k1_last != INT64_MIN && c->k1_last <= bp.hop[0] ? 2 : 1;
+    if (bp.carry == 2) HIPCHK(hipStreamWaitEvent(s.stream, c->k1_ev, 0));
+    c->k1_last = bp.hop[bp.K - 1];
+  } else if (k1_runs) {
+    c->k1_last = INT64_MIN;
+  }
+  int32_t* fcv = bp.carry ? c->k1c_v : nullptr;
+  int32_t* fce = bp.carry ? c->k1c_e : nullptr;
   if (rc.G == 1) {
     s.vm = s.vm_own;
     s.em = s.em_own;
-    timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv, [&] { launch_vertex_mask(s.stream, gk, bp, s.vm, 0, false, clr); });
+    timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv, [&] { launch_vertex_mask(s.stream, gk, bp, s.vm, 0, false, clr, fcv); });
     timed_launch(c, si, KID_EMASK, bytes_emask(c, 1, skip_simple), [&] {
-      launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0, ends ? s.vm : nullptr, 0, skip_simple);
+      launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0, ends ? s.vm : nullptr, 0, skip_simple,
+                       fce);
     });
+    if (bp.carry) HIPCHK(hipEventRecord(c->k1_ev, s.stream));
     if (c->partitioned) part_vm_exchange(c, si, s.vm, 0, 1, ghost_vm_free(c, rc));
   } else {
     MaskSet& M = c->mset[hb % kMaskSets];
@@ -903,11 +934,12 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       for (int w = 0; w < rc.G; w++) HIPCHK(hipStreamWaitEvent(s.stream, M.done[w], 0));
       const BatchClear none;
       timed_launch(c, si, KID_MASK, bv + 8.0 * g.nv * rc.W,
-                   [&] { launch_vertex_mask(s.stream, gk, bp, M.vm, g.nv + kPad, true, none); });
+                   [&] { launch_vertex_mask(s.stream, gk, bp, M.vm, g.nv + kPad, true, none, fcv); });
       timed_launch(c, si, KID_EMASK, bytes_emask(c, rc.W, skip_simple), [&] {
         launch_edge_mask(s.stream, g, bp, M.em, true, c->d_ecnt, (int64_t)h0, ends ? M.vm : nullptr, g.nv + kPad,
-                         skip_simple);
+                         skip_simple, fce);
       });
+      if (bp.carry) HIPCHK(hipEventRecord(c->k1_ev, s.stream));
       if (c->partitioned) part_vm_exchange(c, si, M.vm, g.nv + kPad, rc.G, ghost_vm_free(c, rc));
       HIPCHK(hipEventRecord(M.k1, s.stream));
       M.pending = rc.G;
@@ -2865,6 +2897,96 @@ int rgpu_exchange_init(rgpu_ctx* c, const void* id) {
   return RGPU_OK;
 }
 
+// The partitioned superstep's fixed cost on this context's channel:
+// `rounds` repetitions of what a superstep round costs besides its kernels' work, on slot 0's
+// channel and a stream of its own — the counts all-to-all (4 words per peer) behind a one-node
+// stand-in for the counts kernel, the counts' copy to the host and the host's wait for it (the
+// host sizes the record transfers from them), and the two grouped send/recv of the label records
+// (8 bytes per peer) — then `rounds` all-reduces of 64 words (the per-batch minimum labels and
+// counts).  us[0..3]: round mean / median, all-reduce mean / median, microseconds (3 warm-up
+// repetitions each, not counted).  Collective: every partition calls it.
+int rgpu_exchange_probe(rgpu_ctx* c, int rounds, double* us) {
+  if (!c || !us || rounds <= 0) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->partitioned || !c->pt.xchg)
+    return fail(c, RGPU_ESTATE, "exchange probe: a partitioned context after rgpu_exchange_init");
+  const int P = c->nparts, me = c->part;
+  hipStream_t st = nullptr;
+  hipEvent_t ev = nullptr;
+  int64_t* hx = nullptr;
+  std::vector<void*> T;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    XSlot& xs = c->pt.xs[0];
+    if (!xs.x) xs.x = c->pt.xchg->fork(1);  // (the channel slot 0's runs use: collective, as in ensure_part)
+    int64_t* xab = dalloc<int64_t>(T, 8 * P);
+    unsigned long long* rec = dalloc<unsigned long long>(T, 4 * P);
+    unsigned long long* red = dalloc<unsigned long long>(T, 64);
+    HIPCHK(hipMemset(rec, 0, sizeof(unsigned long long) * 4 * P));
+    HIPCHK(hipMemset(red, 0, sizeof(unsigned long long) * 64));
+    HIPCHK(hipHostMalloc((void**)&hx, sizeof(int64_t) * 8 * P));
+    std::vector<void*> sp(P), rp(P);
+    std::vector<size_t> sb(P), rb(P);
+    for (int q = 0; q < P; q++) {
+      sp[q] = rec + q;
+      rp[q] = rec + 2 * P + q;
+      sb[q] = rb[q] = q == me ? 0 : sizeof(unsigned long long);
+    }
+    using clk = std::chrono::steady_clock;
+    std::vector<double> tr, ta;
+    auto t_last = clk::now();
+    for (int i = 0; i < rounds + 3; i++) {
+      HIPCHK(hipMemsetAsync(xab, 0, sizeof(int64_t) * 4 * P, st));  // (stands in for the counts kernel)
+      xs.x->alltoall_i64(xab, xab + 4 * P, 4, st);
+      HIPCHK(hipMemcpyAsync(hx, xab, sizeof(int64_t) * 8 * P, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipEventRecord(ev, st));
+      HIPCHK(hipEventSynchronize(ev));  // the host reads the counts
+      const auto t = clk::now();
+      if (i >= 3) tr.push_back(std::chrono::duration<double, std::micro>(t - t_last).count());
+      t_last = t;
+      xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), st);  // U records
+      xs.x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), st);  // M records
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    for (int i = 0; i < rounds + 3; i++) {
+      const auto t0 = clk::now();
+      xs.x->allreduce_u64(red, 64, true, st);
+      HIPCHK(hipStreamSynchronize(st));
+      if (i >= 3) ta.push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+    }
+    auto stat = [](std::vector<double> v, double* o) {
+      double sum = 0;
+      for (double x : v) sum += x;
+      std::sort(v.begin(), v.end());
+      o[0] = sum / (double)v.size();
+      o[1] = v[v.size() / 2];
+    };
+    stat(tr, us);
+    stat(ta, us + 2);
+  } catch (const HipFail& f) {
+    exchange_quiesce();
+    for (void* p : T) (void)hipFree(p);
+    if (hx) (void)hipHostFree(hx);
+    if (ev) (void)hipEventDestroy(ev);
+    if (st) (void)hipStreamDestroy(st);
+    return fail(c, RGPU_EHIP, f.msg);
+  } catch (const std::exception& x) {
+    exchange_quiesce();
+    for (void* p : T) (void)hipFree(p);
+    if (hx) (void)hipHostFree(hx);
+    if (ev) (void)hipEventDestroy(ev);
+    if (st) (void)hipStreamDestroy(st);
+    return fail(c, RGPU_EHIP, std::string("exchange probe: ") + x.what());
+  }
+  for (void* p : T) (void)hipFree(p);
+  (void)hipHostFree(hx);
+  (void)hipEventDestroy(ev);
+  (void)hipStreamDestroy(st);
+  return RGPU_OK;
+}
+
 int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hops,
                         const int64_t* windows, size_t n_w, int max_steps, int pr_iters,
                         int flags) {
@@ -2929,6 +3051,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->inject_cnt = e && std::strcmp(e, "cnt") == 0;
   }
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
+  c->k1_carry = env_int("RGPU_K1_CARRY", 1) != 0;
   try {
     HIPCHK(hipSetDevice(c->device));
     apply_pending(c);  // a run sees every seal that finished before it started

@@ -115,6 +115,14 @@ class TemporalGraph:
             raise ValueError("exchange id must be RGPU_XCHG_ID_BYTES long")
         self._check(self._lib.rgpu_exchange_init(self._ctx, xid))
 
+    def exchange_probe(self, rounds: int = 200) -> dict:
+        """rgpu_exchange_probe: the partitioned superstep's fixed cost on this context's channel
+        (collective: every partition calls it) -> microseconds per round / per 64-word all-reduce"""
+        us = (C.c_double * 4)()
+        self._check(self._lib.rgpu_exchange_probe(self._ctx, int(rounds), us))
+        return {"round_us_mean": us[0], "round_us_median": us[1], "allreduce_us_mean": us[2],
+                "allreduce_us_median": us[3], "rounds": int(rounds)}
+
     def newest_time(self) -> int:
         out = C.c_int64()
         self._check(self._lib.rgpu_newest_time(self._ctx, C.byref(out)))

@@ -177,3 +177,48 @@ def test_window_mask_forms_vs_oracle(ivmax):
         for w in range(3):
             assert np.array_equal(g.cc_vertex_labels(h, w)[1], res[w][1]), (ivmax, t, w)
     g.close()
+
+
+@pytest.mark.parametrize("wmajor", ["1", "0"])
+def test_k1_floor_carry_equals_from_scratch(wmajor):
+    """§8(f) row 2, K1 part (BatchParams::carry): each hop block's window masks start from the floor
+    indices the previous block left at its last hop instead of searching every history afresh.
+    Against the from-scratch path (RGPU_K1_CARRY=0) and the oracle: a uniform stream with vertex
+    and edge deletions (interval form and endpoint death lists), power-law hubs whose histories take
+    the per-hop form, many blocks of hourly hops, hops that go backwards between blocks (the carry
+    must not be read there), and degree / PageRank runs (their K1 carries too)."""
+    from raphtory_amd.synth import gen_powerlaw
+    uni = gen_uniform(17, 700, 40_000, t0=T0_README, dt=788_400)
+    pl = gen_powerlaw(4, 1500, 30_000, t0=0, t1=YEAR)
+    cases = [(uni, range_hops(T0_README + 20 * DAY, T0_README + 300 * DAY, 14 * HOUR)),
+             (pl, range_hops(YEAR - 120 * DAY, YEAR, 9 * HOUR))]
+    for s, hops in cases:
+        back = np.concatenate([hops[200:264], hops[:64], hops[64:140]])  # block 2 starts before block 1 ends
+        o = Oracle.from_stream(s)
+        for hs in (hops, back):
+            res = {}
+            for carry in ("1", "0"):
+                with envset({"RGPU_K1_CARRY": carry, "RGPU_WMAJOR": wmajor}):
+                    g = graph_env(s, {"RGPU_WMAJOR": wmajor})
+                    g.run("cc", hs, BATCH_WINDOWS, retain=True)
+                    summ = g.cc_summaries().copy()
+                    labs = [g.cc_vertex_labels(h, w) for h in range(0, len(hs), 23) for w in range(5)]
+                    g.run("degree", hs[::11], [MONTH, DAY], retain=True)
+                    deg = [g.degree_vertex(h, w) for h in range(len(hs[::11])) for w in range(2)]
+                    g.run("pagerank", hs[::40], [WEEK], retain=True, pr_iters=10)
+                    pr = [g.pr_result(h, 0) for h in range(len(hs[::40]))]
+                    g.close()
+                res[carry] = (summ, labs, deg, pr)
+            a, b = res["1"], res["0"]
+            assert np.array_equal(a[0], b[0])
+            for (i1, l1), (i2, l2) in zip(a[1], b[1]):
+                assert np.array_equal(i1, i2) and np.array_equal(l1, l2)
+            for x, y in zip(a[2], b[2]):
+                assert all(np.array_equal(p, q) for p, q in zip(x, y))
+            for (i1, p1), (i2, p2) in zip(a[3], b[3]):
+                assert np.array_equal(i1, i2) and np.array_equal(p1, p2)
+            for k, h in enumerate(range(0, len(hs), 23)):
+                r, _ = o.cc(int(hs[h]), BATCH_WINDOWS, mode=1)
+                for w in range(5):
+                    gi, gl = a[1][k * 5 + w]
+                    assert np.array_equal(gi, r[w][0]) and np.array_equal(gl, r[w][1]), (h, w)

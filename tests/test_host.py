@@ -27,7 +27,7 @@ def test_abi_library_exports_every_declared_symbol():
     for name in decl:
         assert hasattr(lib, name), name
     lib.rgpu_abi_version.restype = ctypes.c_int
-    assert lib.rgpu_abi_version() == 9
+    assert lib.rgpu_abi_version() == 10
     # error path needs no device: null context
     lib.rgpu_last_error.restype = ctypes.c_char_p
     lib.rgpu_last_error.argtypes = [ctypes.c_void_p]

@@ -27,17 +27,23 @@ def main():
     ap.add_argument("--users", type=int, default=20_000_000)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--config", default="c4", choices=["c4", "c2"], help="c2: the 8,041-hop C2 query instead")
     a = ap.parse_args()
     g = TemporalGraph()
     t0 = time.time()
-    for first in range(0, a.interactions, 20_000_000):
-        s = gen_gab_range(4, a.users, 333_333_334, first, min(20_000_000, a.interactions - first))
-        g.ingest_stream(s)
-        end = int(s.t[-1])
-        del s
+    if a.config == "c2":  # bench.py run_c2's stream and hops
+        from raphtory_amd.synth import DAY, T0_README, gen_uniform
+        g.ingest_stream(gen_uniform(1, 100_000, 1_000_000))
+        hops = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, HOUR)
+    else:
+        for first in range(0, a.interactions, 20_000_000):
+            s = gen_gab_range(4, a.users, 333_333_334, first, min(20_000_000, a.interactions - first))
+            g.ingest_stream(s)
+            end = int(s.t[-1])
+            del s
+        hops = range_hops(end - 167 * HOUR, end, HOUR)
     g.seal()
     print(f"sealed in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
-    hops = range_hops(end - 167 * HOUR, end, HOUR)
     ref = None
     for rnd in range(a.rounds):
         for val in a.values.split(","):

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--users", type=int, default=20_000_000)
     ap.add_argument("--interactions", type=int, default=333_333_334)
     ap.add_argument("--out", default="gpurun_out/c4_trace.csv")
+    ap.add_argument("--lean", action="store_true", help="time the lean kernels (RGPU_PROF_LEAN): launch times only")
     a = ap.parse_args()
     inter_full = 333_333_334
     t0 = time.time()
@@ -37,10 +38,13 @@ def main():
           flush=True)
     hops = range_hops(end - 167 * HOUR, end, HOUR)
     g.run("cc", hops, BATCH_WINDOWS)
+    if a.lean:
+        os.environ["RGPU_PROF_LEAN"] = "1"
     g.run("cc", hops, BATCH_WINDOWS, profile=True, serial=True)
     st = g.stats()
     print({k: round(v["ms"], 2) for k, v in st["kernels"].items()}, flush=True)
     g.close()
+    digest(a.out)
 
 
 def digest(path):
@@ -52,6 +56,14 @@ def digest(path):
             steps[b].append((int(r["step"]), int(r["pv"]), int(r["ps"]), int(r["changed"]), int(r["pg"] or 0)))
         else:
             ms[(b, KID.get(int(r["kernel"]), r["kernel"]))] += float(r["ms"])
+    # cc_step ms by (window group, superstep) over the batches (window-major: batch % 5 = window)
+    by = collections.defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        if r["kind"] != "S" and KID.get(int(r["kernel"])) == "cc_step":
+            by[(int(r["batch"]) % 5, int(r["step"]))] += float(r["ms"])
+    for w in range(5):
+        row = [(k[1], round(v, 1)) for k, v in sorted(by.items()) if k[0] == w]
+        print(f"window {w}: cc_step {sum(v for _, v in row):7.1f} ms; by step {row}")
     for b in sorted(steps):
         st = steps[b]
         pv = sum(x[1] for x in st)

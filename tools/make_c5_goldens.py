@@ -7,7 +7,8 @@ runs ~1.6 h past now: the generator's diurnal shape), but an add-only history is
 add times whatever the arrival order (every put is an add; equal times collapse to an add), so the
 stream sorted by time has the same views, and the add-only restatement of the oracle (oracle.h
 orc_addonly_*, checked against the literal replay in tests/test_oracle_addonly.py) replays all
-160M updates and gives ConnectedComponents over
+stream as ingested up to a tick (base + ticks 0..i; 160M updates at the last) and gives
+ConnectedComponents over
 {year, month, week, day, hour} at the live time after a tick: per window the summary fields
 (ConnectedComponents.scala:137-145), member count and (id, label) checksum, and the hop's superstep
 count.  The live time after tick i is the newest update time so far (LiveAnalysisTask.setLiveTime,
@@ -50,26 +51,23 @@ def c5_stream():
 def main():
     t0 = time.time()
     base, ticks = c5_stream()
-    cols = [np.concatenate([getattr(base, f)] + [getattr(x, f) for x in ticks]) for f in ("t", "kind", "src", "dst")]
     lives = np.maximum.accumulate([int(x.t.max()) for x in ticks]).tolist()  # newest time after tick i
     n_base = len(base)
-    del base, ticks
-    order = np.argsort(cols[0], kind="stable")
-    cols = [c[order] for c in cols]
-    del order
-    o = AddOnlyOracle(*cols)
-    print(f"C5 stream {len(cols[0])} updates, add-only oracle built in {time.time() - t0:.0f} s ({o.nv} vertices)",
-          flush=True)
-    del cols
     out = {"note": __doc__.split("\n\n")[0], "users": USERS, "base_interactions": BASE, "base_updates": n_base,
            "tick_interactions": TICK, "ticks": TICKS, "windows": list(BATCH_WINDOWS), "at": {}}
     for i in CHECK_TICKS:
+        # the stream as ingested up to tick i (the next ticks overlap tick i's times: they are not in yet)
+        cols = [np.concatenate([getattr(base, f)] + [getattr(x, f) for x in ticks[:i + 1]])
+                for f in ("t", "kind", "src", "dst")]
+        order = np.argsort(cols[0], kind="stable")
+        o = AddOnlyOracle(*(c[order] for c in cols))
+        del cols, order
         res, steps = o.cc(lives[i], BATCH_WINDOWS)
         out["at"][str(i)] = {"live": lives[i], "supersteps": int(steps),
                              "windows": [view_record(ids, lab) for ids, lab in res]}
         print(f"tick {i}: live {lives[i]}, {steps} supersteps, members "
               f"{[r['members'] for r in out['at'][str(i)]['windows']]} ({time.time() - t0:.0f} s)", flush=True)
-    o.close()
+        o.close()
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     print(f"-> {OUT}", flush=True)

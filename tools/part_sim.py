@@ -4,7 +4,16 @@ process over the loopback exchange (LoopbackPartitions), P = 1..8, on a C4-shape
 partition at a time, so the serial profile pass's kernel times are each partition's own: their
 maximum is the compute one of P GPUs would do, their sum the partitioning's total work.  Also:
 the bytes the partitions send each other per query (by kind) and the summaries' check sums
-(identical at every P).  Prints one JSON line per P."""
+(identical at every P).  Prints one JSON line per P.
+
+Round 5 (the model must carry the exchange's fixed per-superstep costs): before the
+partitions, a P = 1 partitioned context on a real RCCL channel measures one superstep round's
+fixed cost (rgpu_exchange_probe: counts all-to-all, the counts' copy to the host and the host's
+wait, two grouped send/recv) and a 64-word all-reduce.  Each partition's model then adds, beside
+its kernel ms and the xGMI bandwidth term, rounds x that round cost + batches x 2 all-reduces,
+serialised (no overlap with the other batch slots: an upper bound on what they cost; the kernel
+ms alone is the lower bound).  RCCL at P = 8 adds peer latency that one rank does not have; the
+line reports the ratio at the measured cost and with an extra 25 / 50 us per round."""
 import argparse
 import json
 import os
@@ -29,7 +38,17 @@ def main():
     ap.add_argument("--trace", default="", help="directory: per-superstep trace CSVs (RGPU_TRACE) of the profile pass")
     ap.add_argument("--profile-rounds", type=int, default=2,
                     help="profile passes; the one with the smallest slowest-partition time is reported")
+    ap.add_argument("--probe-rounds", type=int, default=500, help="rgpu_exchange_probe rounds (0: skip)")
     a = ap.parse_args()
+    probe = None
+    if a.probe_rounds > 0:  # one RCCL rank: the fixed cost of a round without peer latency
+        os.environ["RGPU_PARTITIONED"] = "1"
+        gp = TemporalGraph()
+        del os.environ["RGPU_PARTITIONED"]
+        gp.exchange_init(TemporalGraph.exchange_id(kind="rccl"))
+        probe = gp.exchange_probe(a.probe_rounds)
+        gp.close()
+        print(json.dumps({"exchange_probe_rccl_p1": probe}), flush=True)
     inter_full = 333_333_334
     s = gen_gab_range(4, a.users, inter_full, 0, a.interactions)
     end = int(s.t[-1])
@@ -85,7 +104,13 @@ def main():
         link = 153e9
         xms = [(g.stats()["xchg_bytes"] / max(1, P - 1)) / link * 1e3 if P > 1 else 0.0 for g in parts]
         tot = [round(k + x, 1) for k, x in zip(per, xms)]
-        rounds = parts[0].stats()["supersteps"] + 2 * parts[0].stats()["batches"]
+        st0 = parts[0].stats()
+        rounds = st0["supersteps"] + 2 * st0["batches"]
+        fixed = {}
+        if probe is not None and P > 1:
+            for extra in (0, 25, 50):
+                f_ms = (rounds * (probe["round_us_median"] + extra) + 2 * st0["batches"] * probe["allreduce_us_median"]) / 1e3
+                fixed[f"+{extra}us_per_round"] = round(f_ms, 1)
         out = {"P": P, "kernel_ms_per_partition": per, "kernel_ms_max": max(per), "kernel_ms_total": round(sum(per), 1),
                "kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in ks.items()},
                "partition0_kernels": p0, "profile_rounds": a.profile_rounds,
@@ -97,6 +122,10 @@ def main():
                "xchg_model_ms_per_partition": [round(x, 2) for x in xms], "xchg_link_GBps": link / 1e9,
                "xchg_rounds_per_partition": rounds,
                "kernel_plus_xchg_ms_max": max(tot),
+               # the fixed per-round cost serialised on top (rgpu_exchange_probe, RCCL, one rank), per
+               # partition; the model = kernel ms + bandwidth term + this
+               "fixed_round_ms": fixed,
+               "model_ms_max_with_fixed": {k: round(max(tot) + v, 1) for k, v in fixed.items()},
                # the serial profiled run's wall time over P: one partition's share of everything the
                # timers above leave out too (exchange pack / unpack / mark kernels, host turns)
                "serial_wall_ms_per_partition": round(t_prof * 1e3 / P, 1),
