@@ -1278,7 +1278,7 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
                                                     const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
                                                     uint64_t* __restrict__ cb_next, uint64_t* __restrict__ cb_clear,
                                                     int64_t cb_words, int32_t* __restrict__ ccount, int dense_div, int gmax,
-                                                    const int32_t* __restrict__ mneg) {
+                                                    const int32_t* __restrict__ mneg, const uint64_t* __restrict__ cb_prev) {
   if (stepflag[step - 1] == 0) return;
   const int lane = lane_id();
   const bool use_fin = mneg != nullptr && uw_cur != nullptr;
@@ -1375,21 +1375,26 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
       const uint64_t m = smask[idx];
       const int32_t nbp = on ? q : 0;
       const uint64_t smp = on ? m : 0;
+      // cb_prev (RGPU_CBF): the neighbour's changed bit (one bit per vertex: an L2-resident
+      // bitmap) first; a neighbour that did not change in step r-1 contributes nothing to the
+      // fold (it still joins the next frontier below, through smp), so its word / change word (a
+      // random line each, most of them Infinity-Cache reads) is not loaded
+      const uint64_t sma = (cb_prev && smp && !((cb_prev[nbp >> 6] >> (nbp & 63)) & 1)) ? 0 : smp;
       uint64_t act = 0;
       int32_t unp = kMixed;
       if (uw_cur) {
-        const int32_t w = uw_cur[nbp];
-        act = (w != kMixed && w < 0) ? smp : 0;
+        const int32_t w = (cb_prev && !sma) ? 0 : uw_cur[nbp];
+        act = (w != kMixed && w < 0) ? sma : 0;
         unp = w == kMixed ? kMixed : (w & 0x7fffffff);
-        const bool mx = w == kMixed && smp != 0;
+        const bool mx = w == kMixed && sma != 0;
         const uint64_t mixed = __ballot(mx);
         if (mixed) {
           const uint64_t cw = chg_prev[mx ? nbp : 0];
-          if (mx) act = smp & cw;
+          if (mx) act = sma & cw;
           wk.a += __popcll(mixed);
         }
       } else {
-        act = smp & chg_prev[nbp];
+        act = sma & chg_prev[nbp];
       }
       wk.g += unp == kMixed ? __popcll(act) : 0;
       uint64_t markp = 0;  // lane = slot: its neighbour joins the next frontier
@@ -2471,7 +2476,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next,
-                    const ChgBits& cb, int32_t* ccount, int dense_div, const int32_t* mneg) {
+                    const ChgBits& cb, int32_t* ccount, int dense_div, const int32_t* mneg, bool cbf) {
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
   // A small graph's dense supersteps are latency-bound and share the GPU with the other batch
   // slots too: a 1,024-block cap measured 4 % faster on C2 (100k vertices) and 2 % slower on a
@@ -2484,7 +2489,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   // C4 serial cc_step 207.6 -> 155.1 ms, query 343 -> 286 ms.
 #define RGPU_PK_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr
+    cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr, cbf ? cb.prev : nullptr
   const unsigned gridp = grid_for(g.nv, 256, cap);
   if (work) k_cc_step_pk<false, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
   else k_cc_step_pk<false, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);

@@ -224,7 +224,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     unsigned long long* work, unsigned long long* lanechg,
                     int32_t* hbest = nullptr, const int32_t* uw_cur = nullptr, int32_t* uw_next = nullptr,
                     const ChgBits& cb = ChgBits(), int32_t* ccount = nullptr, int dense_div = 0,
-                    const int32_t* mneg = nullptr);
+                    const int32_t* mneg = nullptr, bool cbf = false);
 constexpr int kIsoWords = 64 * 64;  // isolated-member counts [64 shards][64 views]
 // DegreeRanking top-20 per view (kernels.hip k_deg_top_merge): key = in-degree << 32 | ~label
 constexpr int kTop = 20;

@@ -259,6 +259,7 @@ struct rgpu_ctx {
   hipEvent_t k1_ev = nullptr;
   int64_t k1_last = INT64_MIN;          // INT64_MIN: no carry to read
   bool k1_carry = true;
+  bool cbf = false;                     // RGPU_CBF: the superstep probes a neighbour's changed bit first (A/B)
   int grp_last[kMaxPlanes] = {};        // supersteps of the last batch of each window group
   // last run: views (hop, win) -> batch (hop/K)*G + win/gsize, lane (win%gsize)*K + hop%K
   int algo = -1, K = 0, W = 0, G = 1, gsize = 1;
@@ -694,7 +695,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
                      s.act[(r + 2) % 3], s.stepcnt, s.d_hostflag,
                      work_buf(c, s), s.stats + kLaneOff,
                      hv ? s.hv.best : nullptr, s.uw[(r - 1) & 1], s.uw[r & 1],
-                     chg_bits(c, s, r), s.ccount, dense_div(c), min_labels(c, s));
+                     chg_bits(c, s, r), s.ccount, dense_div(c), min_labels(c, s), c->cbf);
     }, r, per_launch);
     if (hv)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
@@ -1678,7 +1679,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
                    s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
                    work_buf(c, s), s.stats + kLaneOff, hv ? s.hv.best : nullptr,
                    s.uw[r & 1], s.uw[n & 1], chg_bits(c, s, n), s.ccount,
-                   dense_div(c), min_labels(c, s));
+                   dense_div(c), min_labels(c, s), c->cbf);
   }, n);
   part_post_step(c, si, rc, n);
 }
@@ -3052,6 +3053,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   }
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   c->k1_carry = env_int("RGPU_K1_CARRY", 1) != 0;
+  c->cbf = env_int("RGPU_CBF", 0) != 0;
   try {
     HIPCHK(hipSetDevice(c->device));
     apply_pending(c);  // a run sees every seal that finished before it started
