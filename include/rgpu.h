@@ -302,6 +302,31 @@ int rgpu_vp_result(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, int64_t*
 /* supersteps the reference's job for that hop runs (as rgpu_cc_summary_t.supersteps) */
 int rgpu_vp_supersteps(rgpu_ctx* ctx, size_t hop, int64_t* supersteps);
 
+/* Float vertex programs (ABI 10): VertexMessageFloat (raphtoryMessages.scala:117; messageNeighbour /
+ * messageAllOutgoingNeighbors(Float) / messageAllIngoingNeighbors(Float), VertexVisitor.scala:
+ * 137-147) folded by summation — the message shape of the reference's float analyser
+ * (examples/random/depricated/PageRank.scala:20-37, whose queue loop is commented out there).
+ *   setup (superstep 0, maxSteps > 1): every member's state = (float) its id (RGPU_VP_INIT_ID) or
+ *     init_value (seed_value at seed_id); the senders (every member, or the seed) message their
+ *     neighbours in `direction` (OUT or IN) the value state, or with per_degree (float)(state /
+ *     max(deg, 1)) — deg = its message targets over edges alive in the view (getOutgoingNeighbors.size
+ *     for OUT, self-loop included; in-edges without the self-loop for IN);
+ *   superstep r >= 1: a member holding messages sets state = (float)(bias + mult * sum), the sum in
+ *     double precision, and messages again (it never votes to halt); the others keep their state;
+ *   the job halts when no member received a message in some superstep, or at maxSteps.
+ * Floats are IEEE binary32 values carried as doubles.  The reference sums its Float queue in
+ * message-arrival order (nondeterministic across actors), so parity is stated within float32
+ * rounding: per member |gpu - oracle| <= 1e-6 * max(1, |oracle|) (oracle.h orc_vertex_program_f).
+ * One partition; RGPU_ALGO_VP runs it; rgpu_vp_result_f reads the states (rgpu_vp_result returns
+ * their double bit patterns). */
+typedef struct {
+  int32_t direction, init, senders, per_degree;
+  int64_t seed_id;
+  double init_value, seed_value, bias, mult;
+} rgpu_vertex_program_f_t;
+int rgpu_set_vertex_program_f(rgpu_ctx* ctx, const rgpu_vertex_program_f_t* program);
+int rgpu_vp_result_f(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, double* values, size_t cap, size_t* n);
+
 int rgpu_stats(rgpu_ctx* ctx, rgpu_stats_t* out);
 const char* rgpu_last_error(rgpu_ctx* ctx);
 void rgpu_close(rgpu_ctx* ctx);

@@ -59,6 +59,10 @@ def lib() -> C.CDLL:
         L.orc_vertex_program.argtypes = [C.c_void_p, C.c_int64, _P64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_int64, _P64, _P64, _SZ,
                                          C.POINTER(_SZ), C.POINTER(C.c_int)]
+        L.orc_vertex_program_f.restype = C.c_int
+        L.orc_vertex_program_f.argtypes = [C.c_void_p, C.c_int64, _P64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, _P64,
+                                           _PD, _SZ, C.POINTER(_SZ), C.POINTER(C.c_int)]
         L.orc_diffusion.restype = C.c_int
         L.orc_diffusion.argtypes = [C.c_void_p, C.c_int64, _P64, C.c_int, C.c_int, C.c_int64, C.c_uint64,
                                     C.c_int, _P64, _P32, _SZ, C.POINTER(_SZ), C.POINTER(C.c_int)]
@@ -194,6 +198,25 @@ class Oracle:
                                       _p(ids, C.c_int64), _p(vals, C.c_int64), cap, n, C.byref(steps))
         if rc != 0:
             raise RuntimeError("orc_vertex_program failed")
+        return [(ids[i * cap:i * cap + n[i]].copy(), vals[i * cap:i * cap + n[i]].copy()) for i in range(nw)], steps.value
+
+    def vertex_program_f(self, t: int, windows: Sequence[int] = (), max_steps: int = 100, direction: str = "out",
+                         init: str = "id", senders: str = "all", per_degree: bool = False, seed_id: int = -1,
+                         init_value: float = 0.0, seed_value: float = 0.0, bias: float = 0.0, mult: float = 1.0):
+        """float vertex program, VertexMessageFloat summed (oracle.h orc_vertex_program_f) ->
+        ([(ids, float states as float64)] per window, supersteps)"""
+        w, nw = self._win(windows)
+        cap = max(1, self.nv)
+        ids = np.empty(nw * cap, np.int64)
+        vals = np.empty(nw * cap, np.float64)
+        n = (C.c_size_t * nw)()
+        steps = C.c_int()
+        rc = lib().orc_vertex_program_f(self._g, t, _p(w, C.c_int64) if len(w) else None, len(w), max_steps,
+                                        self.VP_DIRS[direction], 0 if init == "id" else 1, 0 if senders == "all" else 1,
+                                        int(per_degree), seed_id, init_value, seed_value, bias, mult,
+                                        _p(ids, C.c_int64), _p(vals, C.c_double), cap, n, C.byref(steps))
+        if rc != 0:
+            raise RuntimeError("orc_vertex_program_f failed")
         return [(ids[i * cap:i * cap + n[i]].copy(), vals[i * cap:i * cap + n[i]].copy()) for i in range(nw)], steps.value
 
     def diffusion(self, t: int, windows: Sequence[int] = (), max_steps: int = 100, seed_id: int = 31,

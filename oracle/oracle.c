@@ -1018,6 +1018,103 @@ done:
   return rc;
 }
 
+/* Float vertex programs (include/rgpu.h rgpu_vertex_program_f_t): VertexMessageFloat messages
+ * (raphtoryMessages.scala:117, VertexVisitor.scala:137-147) summed.  The reference's BSP as
+ * orc_vertex_program: Setup sends, then every member holding messages takes (float)(bias + mult *
+ * sum) and sends again (no vote to halt); the job halts when no member held a message, or at
+ * maxSteps.  A message is the sender's state, or with per_degree (float)(state / max(deg, 1)), deg
+ * = its message targets alive in the view (vp_neighbours: distinct, members or not).  The queue sums
+ * in double in arrival order (the reference sums Floats in nondeterministic arrival order). */
+int orc_vertex_program_f(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int max_steps, int dir,
+                         int init, int senders, int per_degree, int64_t seed_id, double init_value, double seed_value,
+                         double bias, double mult, int64_t* ids, double* values, size_t cap, size_t* n_out,
+                         int* steps) {
+  WinSet ws;
+  if (winset_init(&ws, windows, nw) != 0 || dir < 0 || dir > 2) return -1;
+  size_t nv = g->nv, nvs = nv ? nv : 1;
+  int nwin = ws.nwin;
+  uint8_t* mem = (uint8_t*)calloc((size_t)nwin * nvs, 1);
+  uint8_t* sset = (uint8_t*)calloc((size_t)nwin * nvs, 1);
+  double* st = (double*)malloc(sizeof(double) * nwin * nvs);
+  double* qs = (double*)calloc((size_t)2 * nwin * nvs, sizeof(double)); /* queue sums, even/odd parity */
+  uint32_t* qc = (uint32_t*)calloc((size_t)2 * nwin * nvs, sizeof(uint32_t));
+  int* nb = (int*)malloc(sizeof(int) * nvs);
+  int* list = (int*)malloc(sizeof(int) * nvs);
+  uint8_t* mark = (uint8_t*)calloc(nvs, 1);
+  int rc = -1;
+  int32_t sv = (seed_id >= 0 && seed_id < ((int64_t)1 << 31)) ? hm_get(&g->vmap, (uint64_t)seed_id) : -1;
+  if (!mem || !sset || !st || !qs || !qc || !nb || !list || !mark) goto done;
+  *steps = 0;
+  build_keysets(g, t, &ws, mem);
+#define FSEND(i, s, val, v)                                                        \
+  do {                                                                             \
+    int nn_ = vp_neighbours(g, (v), t, ws.w[i], dir, nb, mark);                    \
+    const double x_ = per_degree ? (double)(float)((val) / (double)(nn_ > 1 ? nn_ : 1)) : (val); \
+    size_t qb_ = ((size_t)(((s) + 1) % 2) * nwin + ws.canon[i]) * nv;              \
+    for (int q_ = 0; q_ < nn_; q_++) {                                             \
+      qs[qb_ + nb[q_]] += x_;                                                      \
+      qc[qb_ + nb[q_]]++;                                                          \
+    }                                                                              \
+  } while (0)
+  if (max_steps > 1) { /* AnalysisTask.timeResponse :169 */
+    for (int i = 0; i < nwin; i++) {
+      int c = ws.canon[i];
+      for (size_t v = 0; v < nv; v++) {
+        if (!mem[(size_t)i * nv + v]) continue;
+        size_t li = (size_t)c * nv + v;
+        if (!sset[li]) {
+          sset[li] = 1;
+          st[li] = (double)(float)(init == 0 ? (double)g->vs[v].id : ((int32_t)v == sv ? seed_value : init_value));
+        }
+        if (senders == 0 || (int32_t)v == sv) FSEND(i, 0, st[li], (int)v);
+      }
+    }
+    for (int s = 1;; s++) {
+      long totalKeys = 0;
+      for (int i = 0; i < nwin; i++) {
+        int c = ws.canon[i];
+        size_t qb = ((size_t)(s % 2) * nwin + c) * nv;
+        int nl = 0;
+        for (size_t v = 0; v < nv; v++)
+          if (mem[(size_t)i * nv + v] && qc[qb + v] > 0) list[nl++] = (int)v;
+        totalKeys += nl;
+        for (int a = 0; a < nl; a++) { /* every message holder updates and sends (it never votes) */
+          int v = list[a];
+          size_t li = (size_t)c * nv + v;
+          st[li] = (double)(float)(bias + mult * qs[qb + v]);
+          qs[qb + v] = 0.0;
+          qc[qb + v] = 0;
+          FSEND(i, s, st[li], v);
+        }
+        for (size_t v = 0; v < nv; v++) { qs[qb + v] = 0.0; qc[qb + v] = 0; } /* non-members' drops */
+      }
+      *steps = s;
+      if (s == max_steps || totalKeys == 0) break;
+    }
+  }
+#undef FSEND
+  for (int i = 0; i < nwin; i++) {
+    int c = ws.canon[i];
+    size_t k = 0;
+    for (size_t r = 0; r < nv; r++) {
+      int v = g->order[r];
+      if (!mem[(size_t)i * nv + v]) continue;
+      if (k >= cap) goto done;
+      size_t li = (size_t)c * nv + v;
+      ids[(size_t)i * cap + k] = g->vs[v].id;
+      values[(size_t)i * cap + k] = sset[li] ? st[li]
+                                             : (double)(float)(init == 0 ? (double)g->vs[v].id
+                                                                         : ((int32_t)v == sv ? seed_value : init_value));
+      k++;
+    }
+    n_out[i] = k;
+  }
+  rc = 0;
+done:
+  free(mem); free(sset); free(st); free(qs); free(qc); free(nb); free(list); free(mark);
+  return rc;
+}
+
 /* ============================================================ add-only streams (C4 / GAB)
  * A memory-compact restatement for streams of VertexAdds and EdgeAdds only, in time order
  * (GabUserGraphRouter.scala:31-33 emits nothing else).  Every history point is then an add, and

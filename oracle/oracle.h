@@ -93,6 +93,12 @@ int orc_vertex_program(const orc_graph* g, int64_t t, const int64_t* windows, in
                        size_t* n_out, int* steps);
 int orc_pagerank(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int iters,
                  int64_t* ids, double* pr, size_t cap, size_t* n_out);
+/* Float vertex program (include/rgpu.h rgpu_vertex_program_f_t): VertexMessageFloat summed; per
+ * window every member's float state (as a double), ascending id. */
+int orc_vertex_program_f(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int max_steps, int dir,
+                         int init, int senders, int per_degree, int64_t seed_id, double init_value, double seed_value,
+                         double bias, double mult, int64_t* ids, double* values, size_t cap, size_t* n_out,
+                         int* steps);
 
 /* Add-only streams (VertexAdds and EdgeAdds in time order — the GAB / C4 shape): a
  * memory-compact restatement that reads each view off the time-sorted stream (oracle.c, "add-only

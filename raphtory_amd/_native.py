@@ -40,6 +40,7 @@ EXPORTS = [
     "rgpu_rgev_encode", "rgpu_rgev_decode", "rgpu_rgev_last_error", "rgpu_ingest_rgev",
     "rgpu_set_diffusion", "rgpu_diffusion_result", "rgpu_diffusion_vertex", "rgpu_set_vertex_order",
     "rgpu_set_vertex_program", "rgpu_vp_result", "rgpu_vp_supersteps", "rgpu_exchange_probe",
+    "rgpu_set_vertex_program_f", "rgpu_vp_result_f",
 ]
 
 
@@ -51,6 +52,12 @@ class CCSummary(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "biggest", "total", "total_without_islands", "total_islands", "clusters_gt2",
         "sum_all", "sum_without_islands", "supersteps", "alive_edges")]
+
+
+class VertexProgramF(C.Structure):
+    _fields_ = [("direction", C.c_int32), ("init", C.c_int32), ("senders", C.c_int32), ("per_degree", C.c_int32),
+                ("seed_id", C.c_int64), ("init_value", C.c_double), ("seed_value", C.c_double), ("bias", C.c_double),
+                ("mult", C.c_double)]
 
 
 class VertexProgram(C.Structure):
@@ -99,6 +106,8 @@ _SIGS = {
     "rgpu_set_vertex_program": (C.c_int, [_CTX, C.POINTER(VertexProgram)]),
     "rgpu_vp_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P64, _SZ, C.POINTER(_SZ)]),
     "rgpu_vp_supersteps": (C.c_int, [_CTX, _SZ, _P64]),
+    "rgpu_set_vertex_program_f": (C.c_int, [_CTX, C.POINTER(VertexProgramF)]),
+    "rgpu_vp_result_f": (C.c_int, [_CTX, _SZ, _SZ, _P64, _PD, _SZ, C.POINTER(_SZ)]),
     "rgpu_diffusion_result": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P64]),
     "rgpu_diffusion_vertex": (C.c_int, [_CTX, _SZ, _SZ, _P64, _P32, _SZ, C.POINTER(_SZ)]),
     "rgpu_stats": (C.c_int, [_CTX, C.POINTER(Stats)]),

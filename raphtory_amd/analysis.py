@@ -341,6 +341,69 @@ class HopDistance(VertexProgram):
                          init_value=2**63 - 1, seed_id=seed_id, seed_value=0, step_add=1, max_steps=max_steps)
 
 
+class FloatVertexProgram(Analyser):
+    """A user Analyser that sends Float messages (VertexMessageFloat, VertexVisitor.scala:137-147)
+    and sums its queue — run on the GPU as a float vertex program (include/rgpu.h
+    rgpu_set_vertex_program_f):
+
+        setup():   setCompValue(key, init); if sender: messageAll<direction>(state [/ degree])
+        analyse(): if moreMessages: state = bias + mult * sum(queue); setCompValue(key, state);
+                   messageAll<direction>(state [/ degree])
+
+    ``returnResults`` gives {id: state}; the lines print the top five states per view as the
+    reference's float analyser's processResults does (examples/random/depricated/PageRank.scala:
+    45-50), with Float.toString."""
+    algo = "vp"
+
+    def __init__(self, args: Sequence[str] = (), direction: str = "out", init: str = "id", senders: str = "all",
+                 per_degree: bool = False, seed_id: int = -1, init_value: float = 0.0, seed_value: float = 0.0,
+                 bias: float = 0.0, mult: float = 1.0, max_steps: int = 100):
+        super().__init__(args)
+        self.program = dict(direction=direction, init=init, senders=senders, per_degree=per_degree, seed_id=seed_id,
+                            init_value=init_value, seed_value=seed_value, bias=bias, mult=mult)
+        self.max_steps = max_steps
+
+    def defineMaxSteps(self) -> int:  # noqa: N802
+        return self.max_steps
+
+    def prepare(self, graph) -> None:
+        graph.set_vertex_program_f(**self.program)
+
+    def returnResults(self, graph, hop, win):  # noqa: N802
+        ids, vals = graph.vp_result_f(hop, win)
+        return dict(zip(ids.tolist(), vals.tolist()))
+
+    def _line(self, results, timestamp, window=None) -> str:
+        merged: Dict[int, float] = {}
+        for part in results:
+            merged.update(part)
+        top = sorted(merged.items(), key=lambda kv: (-kv[1], kv[0]))[:5]
+        d = "{" + f'"time":{timestamp},' + (f'"windowsize":{window},' if window is not None else "")
+        return d + '"top5":[' + ",".join(f"[{k},{java_float_str(v)}]" for k, v in top) + "]}"
+
+    def processResults(self, results, timestamp, viewCompleteTime):  # noqa: N802
+        self.lines.append(self._line(results, timestamp))
+
+    def processWindowResults(self, results, timestamp, windowSize, viewCompleteTime):  # noqa: N802
+        self.lines.append(self._line(results, timestamp, windowSize))
+
+    def processBatchWindowResults(self, results, timestamp, windowSet, viewCompleteTime):  # noqa: N802
+        for i, window in enumerate(results):
+            self.lines.append(self._line(window, timestamp, windowSet[i]))
+
+
+class FloatPageRank(FloatVertexProgram):
+    """The PageRank its fields declare (examples/random/depricated/PageRank.scala:11-14: defaultPR 1f,
+    dumplingFactor 0.85f, defineMaxSteps 10) as a float vertex program: a sender sends PR / its
+    out-degree in the view, a receiver takes 0.15 + 0.85 * sum.  The reference's own analyse() is a
+    stub (its queue loop is commented out, so every PR becomes 0 / outdegree), which this does not
+    reproduce; the fp64 PageRank of SURVEY App. A.5 is RGPU_ALGO_PR."""
+
+    def __init__(self, args: Sequence[str] = (), max_steps: int = 10):
+        super().__init__(args, direction="out", init="value", per_degree=True, init_value=1.0, bias=0.15, mult=0.85,
+                         max_steps=max_steps)
+
+
 # ---------------------------------------------------------------- tasks
 class TimeNotIngested(RuntimeError):
     """TimeCheck failed (ReaderWorker.processTimeCheckRequest :259-274); the reference retries in 10 s."""

@@ -253,14 +253,21 @@ void launch_pr_step(hipStream_t s, const DevGraph& g, const uint64_t* vm, const 
 struct VpParams {
   int32_t dir = 2, reduce = 0, init = 0, senders = 0;
   int64_t init_value = 0, seed_rank = -1, seed_value = 0, step_add = 0;
+  // float programs (rgpu_set_vertex_program_f, ABI 10): VertexMessageFloat summed.  State rows
+  // hold the double bit pattern of a float32 value; a sender sends state (/ max(deg, 1) with
+  // per_degree: deg = its message targets alive in the view, rows deg[v][64]); a member holding
+  // messages takes (float)(f_bias + f_mult * sum) (the sum in double) and sends again
+  int32_t fsum = 0, per_degree = 0;
+  double f_init = 0, f_seed = 0, f_bias = 0, f_mult = 1;
 };
 void launch_vp_setup(hipStream_t s, const DevGraph& g, const VpParams& p, const int64_t* vid, const uint64_t* vm,
-                     const uint64_t* em, int32_t* cnt, int32_t* snbr, uint64_t* smask, int64_t* st0, uint64_t* chg0);
+                     const uint64_t* em, int32_t* cnt, int32_t* snbr, uint64_t* smask, int64_t* st0, uint64_t* chg0,
+                     int32_t* deg = nullptr);
 void launch_vp_go(hipStream_t s, int32_t* stepflag);
 void launch_vp_step(hipStream_t s, int step, const DevGraph& g, const VpParams& p, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, const int64_t* st_cur,
                     int64_t* st_next, const uint64_t* chg_prev, uint64_t* chg_next, int32_t* stepflag,
-                    int32_t* hostflag, unsigned long long* lanechg);
+                    int32_t* hostflag, unsigned long long* lanechg, const int32_t* deg = nullptr);
 
 // BinaryDefusion (diffusion.hip): per-lane coin salts of a batch (view j -> (hop, window))
 struct DiffSalts {

@@ -66,6 +66,7 @@ struct Slot {
   // buffers allocated for this slot (slots are allocated lazily: a run uses min(slots, batches))
   bool a_cc = false, a_deg = false, a_pr = false, h_cc = false, h_pr = false, a_diff = false, a_vp = false;
   int64_t* vst[2] = {nullptr, nullptr};  // vertex program state rows [nv][64] (int64), Jacobi
+  int32_t* vdeg = nullptr;                // float programs with per_degree: message targets [nv][64]
   hipStream_t stream = nullptr;
   hipEvent_t ev = nullptr;
   uint64_t *vm = nullptr, *em = nullptr;          // masks of the batch in flight
@@ -569,6 +570,7 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
         s.vst[b] = dalloc<int64_t>(L, rows);
       }
     }
+    if (algo == RGPU_ALGO_VP && c->vp.fsum && c->vp.per_degree && !s.vdeg) s.vdeg = dalloc<int32_t>(L, rows);
     if (algo == RGPU_ALGO_DIFFUSION && !s.a_diff) {
       s.dinf = dalloc<uint64_t>(L, nv + kPad);
       s.dfront[0] = dalloc<uint64_t>(L, nv + kPad);
@@ -670,7 +672,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
       timed_launch(c, si, KID_VP, 0.0, [&] {
         launch_vp_step(s.stream, r, g, c->vp, s.vm, s.cnt, s.snbr, s.smask, s.vst[(r - 1) & 1], s.vst[r & 1],
                        s.chg[(r - 1) & 1], s.chg[r & 1], s.stepcnt, s.d_hostflag,
-                       s.stats + kLaneOff);
+                       s.stats + kLaneOff, s.vdeg);
       }, r, false);
       continue;
     }
@@ -953,7 +955,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     HIPCHK(hipGetLastError());
   }
   if (rc.algo == RGPU_ALGO_VP) {  // setup (superstep 0), only when maxSteps > 1 (AnalysisTask.timeResponse :169)
-    launch_vp_setup(s.stream, g, c->vp, c->d_vid, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vst[0], s.chg[0]);
+    launch_vp_setup(s.stream, g, c->vp, c->d_vid, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vst[0], s.chg[0], s.vdeg);
     HIPCHK(hipGetLastError());
     s.r_launched = 0;
     if (rc.max_steps <= 1) {
@@ -3397,6 +3399,7 @@ int rgpu_set_vertex_program(rgpu_ctx* c, const rgpu_vertex_program_t* p) {
       p->init < RGPU_VP_INIT_ID || p->init > RGPU_VP_INIT_VALUE || p->senders < RGPU_VP_SEND_ALL ||
       p->senders > RGPU_VP_SEND_SEED)
     return fail(c, RGPU_EINVAL, "bad vertex program");
+  c->vp = VpParams();
   c->vp.dir = p->direction;
   c->vp.reduce = p->reduce;
   c->vp.init = p->init;
@@ -3427,6 +3430,38 @@ int rgpu_vp_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int64_t* v
   }
   *n = k;
   return RGPU_OK;
+}
+
+int rgpu_set_vertex_program_f(rgpu_ctx* c, const rgpu_vertex_program_f_t* p) {
+  if (!c || !p) return RGPU_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((p->direction != RGPU_VP_OUT && p->direction != RGPU_VP_IN) || p->init < RGPU_VP_INIT_ID ||
+      p->init > RGPU_VP_INIT_VALUE || p->senders < RGPU_VP_SEND_ALL || p->senders > RGPU_VP_SEND_SEED ||
+      (p->per_degree != 0 && p->per_degree != 1))
+    return fail(c, RGPU_EINVAL, "bad float vertex program (direction OUT or IN)");
+  c->vp = VpParams();
+  c->vp.dir = p->direction;
+  c->vp.init = p->init;
+  c->vp.senders = p->senders;
+  c->vp.fsum = 1;
+  c->vp.per_degree = p->per_degree;
+  c->vp.f_init = p->init_value;
+  c->vp.f_seed = p->seed_value;
+  c->vp.f_bias = p->bias;
+  c->vp.f_mult = p->mult;
+  c->vp_seed_id = p->seed_id;
+  c->vp_set = true;
+  return RGPU_OK;
+}
+
+int rgpu_vp_result_f(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, double* values, size_t cap, size_t* n) {
+  if (!c || !n) return RGPU_EINVAL;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->vp.fsum) return fail(c, RGPU_ESTATE, "the vertex program is not a float program");
+  }
+  static_assert(sizeof(double) == sizeof(int64_t), "state rows hold double bits");
+  return rgpu_vp_result(c, hop, win, ids, reinterpret_cast<int64_t*>(values), cap, n);
 }
 
 int rgpu_vp_supersteps(rgpu_ctx* c, size_t hop, int64_t* supersteps) {

@@ -12,6 +12,13 @@
 //   k_vp_step   superstep r: per member, the fold (min / max) of sender state + step_add over the
 //               kept slots whose sender changed in r-1 (those sent it a message); a member whose
 //               state the fold changes keeps it and sends next step, the others vote to halt
+//   float programs (ABI 10, VertexMessageFloat summed — the message shape of the reference's float
+//   analyser, examples/random/depricated/PageRank.scala:20-37, with its commented-out queue loop
+//   done):
+//   k_vp_deg    per member and view, its message targets alive in the view (the divisor of
+//               per_degree programs: getOutgoingNeighbors.size for OUT)
+//   k_vp_step_f superstep r: per member, the sum (double) of the senders' float messages, state =
+//               (float)(bias + mult * sum) when a message arrived (it sends again), else unchanged
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -102,6 +109,9 @@ __global__ __launch_bounds__(256) void k_vp_slots(int64_t nv, int dir, const int
   }
 }
 
+__device__ __forceinline__ int64_t f_bits(double x) { return __double_as_longlong(x); }
+__device__ __forceinline__ double f_val(int64_t b) { return __longlong_as_double(b); }
+
 __global__ __launch_bounds__(256) void k_vp_init(int64_t nv, VpParams p, const int32_t* __restrict__ grank,
                                                  const int64_t* __restrict__ vid, const uint64_t* __restrict__ vm,
                                                  int64_t* __restrict__ st, uint64_t* __restrict__ chg) {
@@ -110,7 +120,8 @@ __global__ __launch_bounds__(256) void k_vp_init(int64_t nv, VpParams p, const i
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t v = wave; v < nv; v += nwaves) {
     const uint64_t mv = vm[v];
-    const int64_t x = p.init == 0 ? vid[v] : (v == p.seed_rank ? p.seed_value : p.init_value);
+    const int64_t x = p.fsum ? f_bits((double)(float)(p.init == 0 ? (double)vid[v] : (v == p.seed_rank ? p.f_seed : p.f_init)))
+                             : (p.init == 0 ? vid[v] : (v == p.seed_rank ? p.seed_value : p.init_value));
     st[v * 64 + lane] = x;
     if (lane == 0) chg[v] = (p.senders == 0 || v == p.seed_rank) ? mv : 0ull;  // the setup's senders
   }
@@ -179,6 +190,97 @@ __global__ __launch_bounds__(256) void k_vp_step(int step, int64_t nv, int64_t s
   }
 }
 
+// message targets of member v alive in each view (lane = view): OUT its out-edges (a self-loop
+// included, outgoingProcessing), IN its in-edges (a self-loop never enters incomingEdges)
+__global__ __launch_bounds__(256) void k_vp_deg(int64_t nv, int dir, const int64_t* __restrict__ out_off,
+                                                const int64_t* __restrict__ in_off, const int32_t* __restrict__ in_eid,
+                                                const int32_t* __restrict__ esrc, const uint64_t* __restrict__ vm,
+                                                const uint64_t* __restrict__ em, int32_t* __restrict__ deg) {
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    const uint64_t mv = vm[v];
+    int32_t d = 0;
+    if (mv) {
+      const int64_t a0 = dir == 0 ? out_off[v] : in_off[v], n = (dir == 0 ? out_off[v + 1] : in_off[v + 1]) - a0;
+      for (int64_t c = 0; c < n; c++) {  // (a few edges per vertex: the wave walks them, lane = view)
+        const int32_t e = dir == 0 ? (int32_t)(a0 + c) : in_eid[a0 + c];
+        if (dir == 1 && esrc[e] == (int32_t)v) continue;
+        d += (int32_t)((em[e] & mv) >> lane) & 1;
+      }
+    }
+    deg[v * 64 + lane] = d;
+  }
+}
+
+// float programs: superstep r (see k_vp_step); the messages of a sender q are (float)(state_q /
+// max(deg_q, 1)) with per_degree, else its state; summed in double in slot order
+__global__ __launch_bounds__(256) void k_vp_step_f(int step, int64_t nv, VpParams p, const int64_t* __restrict__ adj_off,
+                                                   const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
+                                                   const int32_t* __restrict__ snbr, const uint64_t* __restrict__ smask,
+                                                   const int64_t* __restrict__ st_cur, int64_t* __restrict__ st_next,
+                                                   const uint64_t* __restrict__ chg_prev, uint64_t* __restrict__ chg_next,
+                                                   int32_t* __restrict__ stepflag, int32_t* __restrict__ hostflag,
+                                                   unsigned long long* __restrict__ lanechg,
+                                                   const int32_t* __restrict__ deg) {
+  if (stepflag[step - 1] == 0) return;
+  __shared__ unsigned long long lanes_s;
+  if (threadIdx.x == 0) lanes_s = 0;
+  __syncthreads();
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  uint64_t lanes = 0;
+  for (int64_t v = wave; v < nv; v += nwaves) {
+    const uint64_t mv = vm[v];
+    if (mv == 0) continue;
+    const int32_t n = cnt[v];
+    const int64_t base = adj_off[v];
+    const int64_t cur = st_cur[v * 64 + lane];
+    double sum = 0.0;
+    bool got = false;
+    for (int32_t c = 0; c < n; c += 64) {
+      const int32_t j = c + lane;
+      int32_t nb = 0;
+      uint64_t a = 0;
+      if (j < n) {
+        nb = snbr[base + j];
+        a = smask[base + j] & chg_prev[nb];
+      }
+      for (uint64_t bal = __ballot(a != 0); bal; bal &= bal - 1) {  // slot order
+        const int L = __builtin_ctzll(bal);
+        const int32_t q = __builtin_amdgcn_readlane(nb, L);
+        if ((rl64(a, L) >> lane) & 1) {
+          double x = f_val(st_cur[(int64_t)q * 64 + lane]);
+          if (p.per_degree) {
+            const int32_t dq = deg[(int64_t)q * 64 + lane];
+            x = (double)(float)(x / (double)(dq > 1 ? dq : 1));
+          }
+          sum += x;
+          got = true;
+        }
+      }
+    }
+    const bool member = (mv >> lane) & 1;
+    const bool upd = member && got;
+    const int64_t nx = upd ? f_bits((double)(float)(p.f_bias + p.f_mult * sum)) : cur;
+    const uint64_t ch = __ballot(upd);  // a member that received messages sends again
+    st_next[v * 64 + lane] = nx;
+    if (lane == 0) chg_next[v] = ch;
+    lanes |= ch;
+  }
+  if (lane == 0 && lanes) atomicOr(&lanes_s, (unsigned long long)lanes);
+  __syncthreads();
+  if (threadIdx.x == 0 && lanes_s) {
+    atomicOr(&lanechg[step * kLaneShards + (blockIdx.x & (kLaneShards - 1))], lanes_s);
+    if (stepflag[step] == 0) {
+      stepflag[step] = 1;
+      if (hostflag) hostflag[step] = 1;
+    }
+  }
+}
+
 unsigned vgrid(int64_t items, int per_block, unsigned cap) {
   int64_t g = (items + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -188,20 +290,26 @@ unsigned vgrid(int64_t items, int per_block, unsigned cap) {
 }  // namespace
 
 void launch_vp_setup(hipStream_t s, const DevGraph& g, const VpParams& p, const int64_t* vid, const uint64_t* vm,
-                     const uint64_t* em, int32_t* cnt, int32_t* snbr, uint64_t* smask, int64_t* st0, uint64_t* chg0) {
+                     const uint64_t* em, int32_t* cnt, int32_t* snbr, uint64_t* smask, int64_t* st0, uint64_t* chg0,
+                     int32_t* deg) {
   const unsigned grid = vgrid(g.nv, 4, 8192);
   k_vp_slots<<<grid, 256, 0, s>>>(g.nv, p.dir, g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em, cnt,
                                   snbr, smask);
   k_vp_init<<<grid, 256, 0, s>>>(g.nv, p, g.grank, vid, vm, st0, chg0);
+  if (p.fsum && p.per_degree && deg)
+    k_vp_deg<<<grid, 256, 0, s>>>(g.nv, p.dir, g.out_off, g.in_off, g.in_eid, g.esrc, vm, em, deg);
 }
 void launch_vp_go(hipStream_t s, int32_t* stepflag) { k_vp_go<<<1, 1, 0, s>>>(stepflag); }
 
 void launch_vp_step(hipStream_t s, int step, const DevGraph& g, const VpParams& p, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, const int64_t* st_cur,
                     int64_t* st_next, const uint64_t* chg_prev, uint64_t* chg_next, int32_t* stepflag,
-                    int32_t* hostflag, unsigned long long* lanechg) {
+                    int32_t* hostflag, unsigned long long* lanechg, const int32_t* deg) {
   const unsigned grid = vgrid(g.nv, 4, 8192);
-  if (p.reduce == 0)
+  if (p.fsum)
+    k_vp_step_f<<<grid, 256, 0, s>>>(step, g.nv, p, g.adj_off, vm, cnt, snbr, smask, st_cur, st_next, chg_prev, chg_next,
+                                     stepflag, hostflag, lanechg, deg);
+  else if (p.reduce == 0)
     k_vp_step<0><<<grid, 256, 0, s>>>(step, g.nv, p.step_add, g.adj_off, vm, cnt, snbr, smask, st_cur, st_next,
                                       chg_prev, chg_next, stepflag, hostflag, lanechg);
   else

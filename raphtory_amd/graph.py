@@ -229,6 +229,22 @@ class TemporalGraph:
         return self._sized(self._lib.rgpu_vp_result, hop, win,
                            lambda n: ([(np.empty(n, np.int64), C.c_int64), (np.empty(n, np.int64), C.c_int64)], 2))
 
+    def set_vertex_program_f(self, direction: str = "out", init: str = "id", senders: str = "all",
+                             per_degree: bool = False, seed_id: int = -1, init_value: float = 0.0,
+                             seed_value: float = 0.0, bias: float = 0.0, mult: float = 1.0) -> None:
+        """A float vertex program (VertexMessageFloat summed; rgpu_set_vertex_program_f) for later
+        run("vp", ...) calls; read the states with vp_result_f"""
+        if direction not in ("out", "in"):
+            raise ValueError("float vertex programs message out- or in-neighbours")
+        p = N.VertexProgramF(VP_DIRS[direction], 0 if init == "id" else 1, 0 if senders == "all" else 1,
+                             int(bool(per_degree)), seed_id, init_value, seed_value, bias, mult)
+        self._check(self._lib.rgpu_set_vertex_program_f(self._ctx, C.byref(p)))
+
+    def vp_result_f(self, hop: int, win: int) -> Tuple[np.ndarray, np.ndarray]:
+        """(ids, float states as float64) of the view's members, ascending id (needs retain)"""
+        return self._sized(self._lib.rgpu_vp_result_f, hop, win,
+                           lambda n: ([(np.empty(n, np.int64), C.c_int64), (np.empty(n, np.float64), C.c_double)], 2))
+
     def vp_supersteps(self, hop: int) -> int:
         out = C.c_int64()
         self._check(self._lib.rgpu_vp_supersteps(self._ctx, hop, C.byref(out)))

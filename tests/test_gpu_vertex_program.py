@@ -118,3 +118,49 @@ def test_hop_distance_analyser_task_lines():
                 assert lines[k]["time"] == t and lines[k]["windowsize"] == w
                 assert [tuple(x) for x in lines[k]["states"]] == exp
                 k += 1
+
+
+FLOAT_PROGRAMS = {
+    "pagerank_shape": dict(direction="out", per_degree=True, bias=0.15, mult=0.85, init="const", init_value=1.0),
+    "in_sum": dict(direction="in", per_degree=False, bias=0.0, mult=0.5),
+    "seed_out": dict(direction="out", per_degree=True, bias=0.0, mult=1.0, senders="seed", init="const",
+                     init_value=0.0, seed_value=1000.0),
+}
+
+
+@pytest.mark.parametrize("name", sorted(FLOAT_PROGRAMS))
+@pytest.mark.parametrize("stream", ["uniform", "gab"])
+def test_float_vertex_programs(name, stream):
+    """VertexMessageFloat summed (rgpu_set_vertex_program_f, ABI 10) against the oracle's
+    orc_vertex_program_f: every member's float state within float32 rounding (rgpu.h: the sum is
+    double in both, in slot order on the GPU and arrival order in the oracle), float32 values, and
+    the hop's superstep count exactly; power-law hubs (segments do not apply: the program walks its
+    own slots) and window-major batches of many hops."""
+    if stream == "uniform":
+        s = gen_uniform(23, 500, 15_000, t0=T0_README, dt=2_102_400)
+        hops = range_hops(T0_README + 30 * DAY, T0_README + 365 * DAY, 4 * DAY)
+    else:
+        s = gen_gab(8, 4000, 12_000)
+        end = int(s.t[-1])
+        hops = range_hops(end - 90 * DAY, end, 2 * DAY)
+    o = Oracle.from_stream(s)
+    prog = dict(FLOAT_PROGRAMS[name])
+    if prog.get("senders") == "seed":
+        prog["seed_id"] = int(s.src[len(s) // 2])
+    with TemporalGraph() as g:
+        g.ingest_stream(s)
+        g.seal()
+        g.set_vertex_program_f(**prog)
+        g.run("vp", hops, BATCH_WINDOWS, max_steps=12, retain=True)
+        okw = dict(prog)
+        okw["init"] = "id" if okw.get("init", "id") == "id" else "const"
+        for h, t in enumerate(np.asarray(hops).tolist()[::3]):
+            res, steps = o.vertex_program_f(t, BATCH_WINDOWS, max_steps=12, **okw)
+            assert g.vp_supersteps(h * 3) == steps, (t, g.vp_supersteps(h * 3), steps)
+            for w in range(5):
+                ids, vals = res[w]
+                gids, gvals = g.vp_result_f(h * 3, w)
+                assert np.array_equal(gids, ids), (t, w)
+                assert np.all(gvals == gvals.astype(np.float32).astype(np.float64))
+                bad = np.abs(gvals - vals) > 1e-6 * np.maximum(1.0, np.abs(vals))
+                assert not bad.any(), (t, w, int(bad.sum()), gvals[bad][:4], vals[bad][:4])
