@@ -264,6 +264,16 @@ void launch_vp_setup(hipStream_t s, const DevGraph& g, const VpParams& p, const 
                      const uint64_t* em, int32_t* cnt, int32_t* snbr, uint64_t* smask, int64_t* st0, uint64_t* chg0,
                      int32_t* deg = nullptr);
 void launch_vp_go(hipStream_t s, int32_t* stepflag);
+// partitioned vertex programs (rgpu.cpp run_partitioned_vp): boundary records of kVpRec words
+constexpr int kVpRec = 65;  // 64 state words + the change word
+void launch_vp_xgather(hipStream_t s, int64_t n, const int32_t* xv, const int64_t* st, const uint64_t* chg,
+                       int64_t* buf);
+void launch_vp_xscatter(hipStream_t s, int64_t n, const int32_t* xv, const int64_t* buf, int64_t* st, uint64_t* chg);
+void launch_vp_xgather_deg(hipStream_t s, int64_t n, const int32_t* xv, const int32_t* deg, int32_t* buf);
+void launch_vp_xscatter_deg(hipStream_t s, int64_t n, const int32_t* xv, const int32_t* buf, int32_t* deg);
+void launch_vp_lanes(hipStream_t s, const unsigned long long* lanechg, int step, unsigned long long* w);
+void launch_vp_vote(hipStream_t s, const unsigned long long* w, int step, int32_t* stepflag,
+                    unsigned long long* lanechg);
 void launch_vp_step(hipStream_t s, int step, const DevGraph& g, const VpParams& p, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask, const int64_t* st_cur,
                     int64_t* st_next, const uint64_t* chg_prev, uint64_t* chg_next, int32_t* stepflag,

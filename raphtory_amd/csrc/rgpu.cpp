@@ -1922,6 +1922,121 @@ int run_partitioned_dp(rgpu_ctx* c, RunCfg& rc) {
   return 0;
 }
 
+// Generic vertex programs across partitions (VertexVisitor messages cross
+// Partition Managers through the mediator, VertexVisitor.scala:99-147), one hop-major batch at a
+// time on slot 0.  Setup on every local rank; then, after the setup and after every superstep over
+// the owned vertices, each owned boundary vertex's record (its state row and change word) goes to
+// the peers that hold it as a ghost — the exchange plan's lists, fixed sizes, so no counts round —
+// and the global vote: an all-reduce of the step's per-view change flags, the next superstep
+// running everywhere while any partition changed a state (AnalysisTask.endStep :208-225).  A
+// per_degree float program's degree rows go to the ghosts once per batch (a ghost's message
+// targets live on its owner).
+int run_partitioned_vp(rgpu_ctx* c, RunCfg& rc) {
+  const size_t nb = rc.nb;  // hop-major (G = 1)
+  c->st.views += (int64_t)(rc.n_hops * rc.W);
+  c->st.batches += (int64_t)nb;
+  Slot& s = c->slot[0];
+  const DevGraph go = owned_view(c);
+  const DevGraph& g = c->g;
+  Part& X = c->pt;
+  Exchange* x = X.xs[0].x;
+  const int P = c->nparts, me = c->part;
+  std::vector<void*> T;
+  try {
+    int64_t* sbuf = dalloc<int64_t>(T, (size_t)std::max<int64_t>(X.nxs, 1) * kVpRec);
+    int64_t* rbuf = dalloc<int64_t>(T, (size_t)std::max<int64_t>(X.nxr, 1) * kVpRec);
+    const bool degx = c->vp.fsum && c->vp.per_degree;
+    int32_t* sdeg = degx ? dalloc<int32_t>(T, (size_t)std::max<int64_t>(X.nxs, 1) * kViews) : nullptr;
+    int32_t* rdeg = degx ? dalloc<int32_t>(T, (size_t)std::max<int64_t>(X.nxr, 1) * kViews) : nullptr;
+    unsigned long long* vw = dalloc<unsigned long long>(T, kViews);
+    int32_t flag = 0;
+    auto sendrecv = [&](void* sb0, void* rb0, size_t bytes_per_entry, int kind) {
+      std::vector<void*> sp(P), rp(P);
+      std::vector<size_t> sb(P), rb(P);
+      for (int q = 0; q < P; q++) {
+        sp[q] = (char*)sb0 + bytes_per_entry * X.xs_off[q];
+        rp[q] = (char*)rb0 + bytes_per_entry * X.xr_off[q];
+        sb[q] = q == me ? 0 : bytes_per_entry * (size_t)(X.xs_off[q + 1] - X.xs_off[q]);
+        rb[q] = q == me ? 0 : bytes_per_entry * (size_t)(X.xr_off[q + 1] - X.xr_off[q]);
+        X.xs[0].bytes[kind] += (double)sb[q];
+      }
+      x->sendrecv(sp.data(), sb.data(), rp.data(), rb.data(), s.stream);
+    };
+    auto records = [&](int par) {  // owned boundary rows of buffer par -> the peers' ghost rows
+      timed_launch(c, 0, KID_XCHG, 0.0, [&] { launch_vp_xgather(s.stream, X.nxs, X.xs_v, s.vst[par], s.chg[par], sbuf); });
+      sendrecv(sbuf, rbuf, sizeof(int64_t) * kVpRec, 1);
+      timed_launch(c, 0, KID_XCHG, 0.0, [&] { launch_vp_xscatter(s.stream, X.nxr, X.xr_v, rbuf, s.vst[par], s.chg[par]); });
+    };
+    for (size_t b = 0; b < nb; b++) {
+      BatchParams bp;
+      std::memset(&bp, 0, sizeof(bp));
+      const size_t h0 = b * rc.K;
+      bp.K = (int)std::min<size_t>(rc.K, rc.n_hops - h0);
+      bp.W = rc.W;
+      bp.KS = rc.K;
+      bp.sorted = 1;
+      bp.iv_max = c->iv_max;
+      for (int k = 0; k < bp.K; k++) {
+        bp.hop[k] = rc.hops[h0 + k];
+        if (k > 0 && bp.hop[k] < bp.hop[k - 1]) bp.sorted = 0;
+      }
+      bp.jump = even_jump(bp);
+      for (int w = 0; w < rc.W; w++) { bp.thr_v[w] = rc.thr_v[w]; bp.thr_e[w] = rc.thr_e[w]; }
+      s.batch = (int)b;
+      s.kb = bp.K;
+      s.r_final = 0;
+      BatchClear clr;
+      clr.stats = s.stats;
+      clr.n_stats = kStatCopy;
+      clr.flags = s.stepcnt;
+      clr.n_flags = kMaxSteps;
+      s.vm = s.vm_own;
+      s.em = s.em_own;
+      timed_launch(c, 0, KID_MASK, 8.0 * (go.nv + 1) + 16.0 * go.nv + 8.0 * go.nv,
+                   [&] { launch_vertex_mask(s.stream, go, bp, s.vm, 0, false, clr); });
+      timed_launch(c, 0, KID_EMASK, bytes_emask(c, 1, false),
+                   [&] { launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0); });
+      part_vm_exchange(c, 0, s.vm, 0, 1, false);
+      launch_vp_setup(s.stream, g, c->vp, c->d_vid, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vst[0], s.chg[0], s.vdeg);
+      HIPCHK(hipGetLastError());
+      records(0);  // a ghost's setup state and sender flag are its owner's (a seed owned elsewhere)
+      if (degx) {
+        launch_vp_xgather_deg(s.stream, X.nxs, X.xs_v, s.vdeg, sdeg);
+        sendrecv(sdeg, rdeg, sizeof(int32_t) * kViews, 1);
+        launch_vp_xscatter_deg(s.stream, X.nxr, X.xr_v, rdeg, s.vdeg);
+      }
+      if (rc.max_steps > 1) {
+        launch_vp_go(s.stream, s.stepcnt);
+        for (int r = 1; r <= rc.max_steps; r++) {
+          timed_launch(c, 0, KID_VP, 0.0, [&] {
+            launch_vp_step(s.stream, r, go, c->vp, s.vm, s.cnt, s.snbr, s.smask, s.vst[(r - 1) & 1], s.vst[r & 1],
+                           s.chg[(r - 1) & 1], s.chg[r & 1], s.stepcnt, nullptr, s.stats + kLaneOff, s.vdeg);
+          });
+          records(r & 1);
+          launch_vp_lanes(s.stream, s.stats + kLaneOff, r, vw);
+          x->allreduce_u64(vw, kViews, true, s.stream);
+          launch_vp_vote(s.stream, vw, r, s.stepcnt, s.stats + kLaneOff);
+          HIPCHK(hipGetLastError());
+          HIPCHK(hipMemcpyAsync(&flag, s.stepcnt + r, sizeof(int32_t), hipMemcpyDeviceToHost, s.stream));
+          HIPCHK(hipStreamSynchronize(s.stream));
+          s.r_final = r;
+          if (!flag) break;  // no partition changed a state in superstep r
+        }
+      }
+      c->st.supersteps += s.r_final;
+      finish_tail(c, 0, rc);
+      HIPCHK(hipStreamSynchronize(s.stream));
+      harvest(c, 0, rc);
+    }
+  } catch (...) {
+    (void)hipStreamSynchronize(s.stream);
+    for (void* p : T) (void)hipFree(p);
+    throw;
+  }
+  for (void* p : T) (void)hipFree(p);
+  return 0;
+}
+
 // The reference runs one job per hop for all its windows (BWindowedRangeAnalysisTask); it halts
 // at the first superstep in which no label of any window improved, or at maxSteps
 // (AnalysisTask.endStep :208-225), so every view of hop h reports min(maxSteps, 1 + the last
@@ -2999,8 +3114,8 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   if (c->partitioned && !c->pt.xchg)
     return fail(c, RGPU_ESTATE, "partitioned context: call rgpu_exchange_init before running");
   if (algo < RGPU_ALGO_CC || algo > RGPU_ALGO_VP) return fail(c, RGPU_EINVAL, "unknown algo");
-  if ((algo == RGPU_ALGO_DIFFUSION || algo == RGPU_ALGO_VP) && c->partitioned)
-    return fail(c, RGPU_EINVAL, "diffusion and vertex-program runs need one partition");
+  if (algo == RGPU_ALGO_DIFFUSION && c->partitioned)
+    return fail(c, RGPU_EINVAL, "diffusion runs need one partition");
   if (algo == RGPU_ALGO_VP && !c->vp_set) return fail(c, RGPU_ESTATE, "rgpu_set_vertex_program before a vertex-program run");
   if (!hops || n_hops == 0) return fail(c, RGPU_EINVAL, "no hops");
   if (n_w > (size_t)kViews) return fail(c, RGPU_EINVAL, "more than 64 windows in one batch");
@@ -3120,6 +3235,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     c->pt.bytes_sent = 0;
     for (XSlot& xs : c->pt.xs) xs.bytes[0] = xs.bytes[1] = xs.bytes[2] = 0;
     if (c->partitioned && algo == RGPU_ALGO_CC) run_partitioned_cc(c, rc);
+    else if (c->partitioned && algo == RGPU_ALGO_VP) run_partitioned_vp(c, rc);
     else if (c->partitioned) run_partitioned_dp(c, rc);
     else run_impl(c, rc);
     for (int si = 0; si < kMaxSlots; si++)

@@ -281,6 +281,71 @@ __global__ __launch_bounds__(256) void k_vp_step_f(int step, int64_t nv, VpParam
   }
 }
 
+// Partitioned vertex programs: a boundary vertex's record for a peer = its 64 state words and its
+// change word (kVpRec words; one wave per entry, lane = view), gathered in the plan's send order
+// and scattered into the receiver's ghost rows (xv: send / receive entries -> local ranks)
+__global__ __launch_bounds__(256) void k_vp_xgather(int64_t n, const int32_t* __restrict__ xv,
+                                                    const int64_t* __restrict__ st, const uint64_t* __restrict__ chg,
+                                                    int64_t* __restrict__ buf) {
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t k = wave; k < n; k += nwaves) {
+    const int64_t v = xv[k];
+    buf[k * kVpRec + lane] = st[v * 64 + lane];
+    if (lane == 0) buf[k * kVpRec + 64] = (int64_t)chg[v];
+  }
+}
+__global__ __launch_bounds__(256) void k_vp_xscatter(int64_t n, const int32_t* __restrict__ xv,
+                                                     const int64_t* __restrict__ buf, int64_t* __restrict__ st,
+                                                     uint64_t* __restrict__ chg) {
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t k = wave; k < n; k += nwaves) {
+    const int64_t v = xv[k];
+    st[v * 64 + lane] = buf[k * kVpRec + lane];
+    if (lane == 0) chg[v] = (uint64_t)buf[k * kVpRec + 64];
+  }
+}
+// the degree rows of per_degree float programs (a ghost's targets live on its owner), once per batch
+__global__ __launch_bounds__(256) void k_vp_xgather_deg(int64_t n, const int32_t* __restrict__ xv,
+                                                        const int32_t* __restrict__ deg, int32_t* __restrict__ buf) {
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t k = wave; k < n; k += nwaves) buf[k * 64 + lane] = deg[(int64_t)xv[k] * 64 + lane];
+}
+__global__ __launch_bounds__(256) void k_vp_xscatter_deg(int64_t n, const int32_t* __restrict__ xv,
+                                                         const int32_t* __restrict__ buf, int32_t* __restrict__ deg) {
+  const int lane = lane_of();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t k = wave; k < n; k += nwaves) deg[(int64_t)xv[k] * 64 + lane] = buf[k * 64 + lane];
+}
+// the step's views with a change, folded from the lane shards (the global vote is their all-reduce)
+__global__ void k_vp_lanes(const unsigned long long* __restrict__ lanechg, int step, unsigned long long* __restrict__ w) {
+  const int j = threadIdx.x;
+  if (j >= 64) return;
+  unsigned long long x = 0;
+  for (int sh = 0; sh < kLaneShards; sh++) x |= lanechg[step * kLaneShards + sh];
+  w[j] = (x >> j) & 1;
+}
+// after the all-reduce (max) of the per-view change flags: the step's flag, as if this partition
+// had changed a state itself (the next superstep runs on every partition while any changed)
+__global__ void k_vp_vote(const unsigned long long* __restrict__ w, int step, int32_t* __restrict__ stepflag,
+                          unsigned long long* __restrict__ lanechg) {
+  const int j = threadIdx.x;
+  if (j >= 64) return;
+  const bool any = __ballot(w[j] != 0) != 0;
+  if (j == 0) {
+    stepflag[step] = any ? 1 : 0;
+    unsigned long long m = 0;
+    for (int k = 0; k < 64; k++) m |= (w[k] ? 1ull : 0ull) << k;
+    lanechg[step * kLaneShards] |= m;  // (the views' last changing step: global, as the reference's job)
+  }
+}
+
 unsigned vgrid(int64_t items, int per_block, unsigned cap) {
   int64_t g = (items + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -317,4 +382,27 @@ void launch_vp_step(hipStream_t s, int step, const DevGraph& g, const VpParams& 
                                       chg_prev, chg_next, stepflag, hostflag, lanechg);
 }
 
+}  // namespace rgpu
+
+namespace rgpu {
+void launch_vp_xgather(hipStream_t s, int64_t n, const int32_t* xv, const int64_t* st, const uint64_t* chg,
+                       int64_t* buf) {
+  if (n > 0) k_vp_xgather<<<vgrid(n, 4, 4096), 256, 0, s>>>(n, xv, st, chg, buf);
+}
+void launch_vp_xscatter(hipStream_t s, int64_t n, const int32_t* xv, const int64_t* buf, int64_t* st, uint64_t* chg) {
+  if (n > 0) k_vp_xscatter<<<vgrid(n, 4, 4096), 256, 0, s>>>(n, xv, buf, st, chg);
+}
+void launch_vp_xgather_deg(hipStream_t s, int64_t n, const int32_t* xv, const int32_t* deg, int32_t* buf) {
+  if (n > 0) k_vp_xgather_deg<<<vgrid(n, 4, 4096), 256, 0, s>>>(n, xv, deg, buf);
+}
+void launch_vp_xscatter_deg(hipStream_t s, int64_t n, const int32_t* xv, const int32_t* buf, int32_t* deg) {
+  if (n > 0) k_vp_xscatter_deg<<<vgrid(n, 4, 4096), 256, 0, s>>>(n, xv, buf, deg);
+}
+void launch_vp_lanes(hipStream_t s, const unsigned long long* lanechg, int step, unsigned long long* w) {
+  k_vp_lanes<<<1, 64, 0, s>>>(lanechg, step, w);
+}
+void launch_vp_vote(hipStream_t s, const unsigned long long* w, int step, int32_t* stepflag,
+                    unsigned long long* lanechg) {
+  k_vp_vote<<<1, 64, 0, s>>>(w, step, stepflag, lanechg);
+}
 }  // namespace rgpu

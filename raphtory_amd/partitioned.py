@@ -118,6 +118,32 @@ class LoopbackPartitions:
         o = np.argsort(ids, kind="stable")
         return ids[o], pr[o]
 
+    # vertex programs (VertexVisitor messaging across partitions) ---------------------
+    def set_vertex_program(self, **kw) -> None:
+        for g in self.parts:
+            g.set_vertex_program(**kw)
+
+    def set_vertex_program_f(self, **kw) -> None:
+        for g in self.parts:
+            g.set_vertex_program_f(**kw)
+
+    def _merged(self, fn, hop, win):
+        ids, val = zip(*[fn(g, hop, win) for g in self.parts])
+        ids, val = np.concatenate(ids), np.concatenate(val)
+        o = np.argsort(ids, kind="stable")
+        return ids[o], val[o]
+
+    def vp_result(self, hop: int, win: int):
+        return self._merged(lambda g, h, w: g.vp_result(h, w), hop, win)
+
+    def vp_result_f(self, hop: int, win: int):
+        return self._merged(lambda g, h, w: g.vp_result_f(h, w), hop, win)
+
+    def vp_supersteps(self, hop: int) -> int:
+        steps = {g.vp_supersteps(hop) for g in self.parts}
+        assert len(steps) == 1, steps  # the job's superstep count is global
+        return steps.pop()
+
     def close(self) -> None:
         for g in self.parts:
             g.close()

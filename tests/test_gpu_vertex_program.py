@@ -164,3 +164,46 @@ def test_float_vertex_programs(name, stream):
                 assert np.all(gvals == gvals.astype(np.float32).astype(np.float64))
                 bad = np.abs(gvals - vals) > 1e-6 * np.maximum(1.0, np.abs(vals))
                 assert not bad.any(), (t, w, int(bad.sum()), gvals[bad][:4], vals[bad][:4])
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_vertex_programs_partitioned(P):
+    """Vertex programs across loopback partitions (run_partitioned_vp: boundary records of state rows
+    and change words after setup and every superstep, the global vote by all-reduce): the min / max
+    int64 programs bit-exact against the oracle (states and the hop's superstep count), a seeded
+    program whose seed is owned by one partition only, and a per_degree float program (degree rows
+    of ghosts from their owners) within the float32 bound."""
+    from raphtory_amd.partitioned import LoopbackPartitions
+    s = gen_uniform(29, 500, 14_000, t0=T0_README, dt=2_252_571)
+    o = Oracle.from_stream(s)
+    hops = range_hops(T0_README + 40 * DAY, T0_README + 360 * DAY, 9 * DAY)
+    lp = LoopbackPartitions(P)
+    lp.ingest_stream(s)
+    lp.seal()
+    seed = int(s.src[len(s) // 3])
+    for name in ("cc", "max_id_out", "hops_in", "hops_all_capped"):
+        prog = dict(PROGRAMS[name])
+        if prog.get("senders") == "seed":
+            prog["seed_id"] = seed
+        cap = 4 if name == "hops_all_capped" else 100
+        lp.set_vertex_program(**prog)
+        lp.run("vp", hops, BATCH_WINDOWS, max_steps=cap, retain=True)
+        for h, t in enumerate(np.asarray(hops).tolist()[::4]):
+            res, steps = o.vertex_program(t, BATCH_WINDOWS, max_steps=cap, **_oracle_kw(prog))
+            assert lp.vp_supersteps(h * 4) == steps, (name, t)
+            for w in range(5):
+                gids, gvals = lp.vp_result(h * 4, w)
+                assert np.array_equal(gids, res[w][0]) and np.array_equal(gvals, res[w][1]), (name, t, w)
+    prog = dict(FLOAT_PROGRAMS["pagerank_shape"])
+    lp.set_vertex_program_f(**prog)
+    lp.run("vp", hops, BATCH_WINDOWS, max_steps=8, retain=True)
+    okw = dict(prog)
+    okw["init"] = "const"
+    for h, t in enumerate(np.asarray(hops).tolist()[::5]):
+        res, steps = o.vertex_program_f(t, BATCH_WINDOWS, max_steps=8, **okw)
+        assert lp.vp_supersteps(h * 5) == steps
+        for w in range(5):
+            gids, gvals = lp.vp_result_f(h * 5, w)
+            assert np.array_equal(gids, res[w][0])
+            assert np.all(np.abs(gvals - res[w][1]) <= 1e-6 * np.maximum(1.0, np.abs(res[w][1]))), (t, w)
+    lp.close()
