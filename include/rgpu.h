@@ -281,8 +281,11 @@ int rgpu_diffusion_vertex(rgpu_ctx* ctx, size_t hop, size_t win, int64_t* ids, i
  *   the job halts at the first superstep in which no state changed in any window of the hop, or
  *     at maxSteps.
  * CC = {ALL, MIN, INIT_ID, SEND_ALL, step_add 0}; hop distance from a seed over out-edges = {OUT,
- * MIN, INIT_VALUE init_value INT64_MAX seed_value 0, SEND_SEED, step_add 1}.  One partition;
- * max_steps <= 127.  Oracle: oracle.h orc_vertex_program. */
+ * MIN, INIT_VALUE init_value INT64_MAX seed_value 0, SEND_SEED, step_add 1}.  max_steps <= 127.
+ * Partitioned contexts (ABI 10) run it too: after setup and every superstep each partition sends
+ * its peers the states of its changed boundary vertices (the messages that cross partitions, as
+ * the mediator carries VertexMessage between PMs), and the halt vote is global (an all-reduce).
+ * Oracle: oracle.h orc_vertex_program. */
 #define RGPU_VP_OUT 0
 #define RGPU_VP_IN 1
 #define RGPU_VP_ALL 2
@@ -317,8 +320,9 @@ int rgpu_vp_supersteps(rgpu_ctx* ctx, size_t hop, int64_t* supersteps);
  * Floats are IEEE binary32 values carried as doubles.  The reference sums its Float queue in
  * message-arrival order (nondeterministic across actors), so parity is stated within float32
  * rounding: per member |gpu - oracle| <= 1e-6 * max(1, |oracle|) (oracle.h orc_vertex_program_f).
- * One partition; RGPU_ALGO_VP runs it; rgpu_vp_result_f reads the states (rgpu_vp_result returns
- * their double bit patterns). */
+ * RGPU_ALGO_VP runs it, on one partition or partitioned (as above; with per_degree the ghosts'
+ * out/in degrees in the view are exchanged once per batch); rgpu_vp_result_f reads the states
+ * (rgpu_vp_result returns their double bit patterns). */
 typedef struct {
   int32_t direction, init, senders, per_degree;
   int64_t seed_id;

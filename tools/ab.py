@@ -5,6 +5,8 @@ one JSON line per (round, setting): wall ms of the query and, with --profile, th
 per-kernel ms of a lean profile pass (RGPU_PROF_LEAN).
 
 usage: python tools/ab.py --var RGPU_AB --values 0,1 [--interactions N] [--rounds 2] [--profile]
+       python tools/ab.py --settings "base,RGPU_A=1,RGPU_A=2+RGPU_B=1" ...  (several variables: each
+       setting sets its K=V pairs and unsets the others' keys; "base" sets nothing)
 """
 import argparse
 import json
@@ -21,8 +23,9 @@ from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops  #
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--var", required=True)
-    ap.add_argument("--values", required=True)
+    ap.add_argument("--var", default="")
+    ap.add_argument("--values", default="")
+    ap.add_argument("--settings", default="")
     ap.add_argument("--interactions", type=int, default=333_333_334)
     ap.add_argument("--users", type=int, default=20_000_000)
     ap.add_argument("--rounds", type=int, default=2)
@@ -44,10 +47,18 @@ def main():
         hops = range_hops(end - 167 * HOUR, end, HOUR)
     g.seal()
     print(f"sealed in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    if a.settings:
+        settings = [dict(kv.split("=", 1) for kv in st.split("+") if kv != "base") for st in a.settings.split(",")]
+    else:
+        settings = [{a.var: v} for v in a.values.split(",")]
+    keys = sorted({k for st in settings for k in st})
     ref = None
     for rnd in range(a.rounds):
-        for val in a.values.split(","):
-            os.environ[a.var] = val
+        for st in settings:
+            for k in keys:
+                os.environ.pop(k, None)
+            os.environ.update(st)
+            val = "+".join(f"{k}={v}" for k, v in st.items()) or "base"
             g.run("cc", hops, BATCH_WINDOWS)  # warm
             t = time.perf_counter()
             g.run("cc", hops, BATCH_WINDOWS)
@@ -55,7 +66,8 @@ def main():
             summ = g.cc_summaries()[..., :8]
             same = ref is None or bool((summ == ref).all())
             ref = summ if ref is None else ref
-            out = {"round": rnd, a.var: val, "query_ms": round(ms, 2), "summaries_equal": same}
+            out = {"round": rnd, (a.var or "setting"): (st.get(a.var) if a.var else val), "query_ms": round(ms, 2),
+                   "summaries_equal": same}
             if a.profile:
                 os.environ["RGPU_PROF_LEAN"] = "1"
                 g.run("cc", hops, BATCH_WINDOWS, profile=True, serial=True)

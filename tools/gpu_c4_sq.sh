@@ -1,0 +1,28 @@
+#!/bin/bash
+# Instruction-mix / wait counters (SQ_*, one group per pass, no tracing) of the C4 1B headline's
+# serial lean pass (bench.py --profile-only --lean-pass-only), for the kernels in $KREGEX.
+# Summary -> gpurun_out/c4sq/summary.txt (per kernel: counter totals and per-dispatch means).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/c4sq; mkdir -p $O
+K=${KREGEX:-k_cc_step_pk|k_heavy_gather|k_cc_slots}
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU" \
+           "TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  echo "=== pass $i: $grp"
+  timeout -k 10 540 rocprofv3 --pmc $grp --kernel-include-regex "$K" -d $O/p$i -o run --output-format csv -- \
+    python3 bench.py --profile-only --lean-pass-only --no-cpu-baseline --no-secondary > $O/p$i.log 2>&1
+  rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/p$i.log; exit $rc; }
+done
+python3 - <<'PY' | tee gpurun_out/c4sq/summary.txt
+import csv, glob, collections
+tot = collections.defaultdict(float); n = collections.Counter()
+for f in glob.glob("gpurun_out/c4sq/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = (r["Kernel_Name"].split("(")[0], r["Counter_Name"])
+        tot[k] += float(r["Counter_Value"]); n[k] += 1
+for k in sorted(tot):
+    print(f"{k[0][:48]:48s} {k[1]:28s} total {tot[k]:.4g}  per-dispatch {tot[k]/n[k]:.4g}  dispatches {n[k]}")
+PY
