@@ -560,8 +560,8 @@ __device__ __forceinline__ uint64_t slot_bits(const HopLDS& L, const BatchParams
 
 // PROF = false: the work counters compile away (launch_cc_slots: work == null).  IEM: inline edge
 // bits (slot_bits; time-ordered slots required), em unused
-template <bool PROF, bool IEM, bool PART>
-__global__ __launch_bounds__(256) void k_cc_slots(int64_t nv, int64_t n_own,
+template <bool PROF, bool IEM, bool PART, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_cc_slots(int64_t nv, int64_t n_own,
                                                   const int64_t* __restrict__ out_off,
                                                   const int64_t* __restrict__ in_off,
                                                   const int32_t* __restrict__ in_eid,
@@ -1608,7 +1608,8 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
 
 // Superstep r, before the full-grid kernel: minimum over each segment of a flagged heavy
 // vertex of the labels of its neighbours that changed in r-1 (views where they did).
-__global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, const int32_t* __restrict__ seg_v,
+template <int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_heavy_gather(int step, int64_t nseg, const int32_t* __restrict__ seg_v,
                                                       const int32_t* __restrict__ seg_h,
                                                       const int64_t* __restrict__ seg_lo,
                                                       const int32_t* __restrict__ segcnt,
@@ -1624,7 +1625,7 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
                                                       const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
                                                       unsigned long long* __restrict__ work,
                                                       const uint64_t* __restrict__ vm,
-                                                      const int32_t* __restrict__ mneg) {
+                                                      const int32_t* __restrict__ mneg, int pro) {
   if (stepflag[step - 1] == 0) return;
   const bool use_fin = vm && uw_cur && mneg;
   const int32_t mfin = use_fin ? final_label(mneg, threadIdx.x & 63) : INT32_MIN;
@@ -1633,79 +1634,94 @@ __global__ __launch_bounds__(256) void k_heavy_gather(int step, int64_t nseg, co
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   unsigned long long w_seg = 0, w_slots = 0, w_hot = 0, w_mixed = 0, w_lanes = 0;
-  for (int64_t sg = wave; sg < nseg; sg += nwaves) {
-    const int32_t v = seg_v[sg];
-    if (v >= n_own || (!visit_all && !act_cur[v])) continue;  // ghosts are not visited (their owner computes them)
-    const int32_t n = segcnt[sg];
-    if (n == 0) continue;
-    if (use_fin && holds_final(uw_cur[v], vm[v], mfin, lane)) continue;  // its label is final (wave-uniform)
-    if (work) { w_seg++; w_slots += (unsigned long long)n; }
-    const int64_t base = seg_lo[sg];
-    int32_t best = INT32_MAX;  // lane = view
-    if (cb_prev && uw_cur && n <= kSegSlots) {
-      // Loads first over the segment's (at most 8) chunks: neighbours, their changed-bit words,
-      // then the hot slots' masks and words, then the folds — three dependent trips per segment
-      // instead of three per chunk.
-      constexpr int NC = kSegSlots / 64;
-      int32_t q[NC];
-      uint64_t cbw[NC], m[NC];
-      int32_t u[NC];
-#pragma unroll
-      for (int k = 0; k < NC; k++) q[k] = k * 64 < n ? snbr[base + (k * 64 + lane < n ? k * 64 + lane : k * 64)] : 0;
-#pragma unroll
-      for (int k = 0; k < NC; k++) cbw[k] = k * 64 < n ? cb_prev[q[k] >> 6] : 0;
-#pragma unroll
-      for (int k = 0; k < NC; k++) {
-        const bool hot = k * 64 + lane < n && ((cbw[k] >> (q[k] & 63)) & 1);
-        m[k] = hot ? smask[base + k * 64 + lane] : 0;
-        u[k] = hot ? uw_label(uw_cur[q[k]]) : kMixed;
+  // pro (kHubPro) segments per wave and round, strided over the waves as one segment per wave was: their
+  // vertex, flag and kept count load lane-parallel (lane l < pro: segment wave + (r + l)·nwaves),
+  // so a late step's idle segments cost one round of loads per pro of them instead of a
+  // dependent chain each (the launch is pro times smaller, launch_heavy_gather)
+  for (int64_t r0 = 0; wave + r0 * nwaves < nseg; r0 += pro) {
+    const int64_t sl = wave + (r0 + lane) * nwaves;
+    const bool in = lane < pro && sl < nseg;
+    const int32_t vl = in ? seg_v[sl] : 0;
+    const int32_t nl = in ? segcnt[sl] : 0;
+    // ghosts are not visited (their owner computes them)
+    const bool on = in && vl < n_own && nl > 0 && (visit_all || act_cur[vl] != 0);
+    // (the final-label test's word and mask, loaded with the segments')
+    const int32_t ul = (use_fin && on) ? uw_cur[vl] : kMixed;
+    const uint64_t ml = (use_fin && on) ? vm[vl] : 0;
+    for (uint64_t todo = __ballot(on); todo; todo &= todo - 1) {
+      const int L = __builtin_ctzll(todo);
+      const int64_t sg = wave + (r0 + L) * nwaves;
+      const int32_t n = __builtin_amdgcn_readlane(nl, L);
+      // its label is final (wave-uniform)
+      if (use_fin && holds_final(__builtin_amdgcn_readlane(ul, L), readlane64(ml, L), mfin, lane)) continue;
+      if (work) { w_seg++; w_slots += (unsigned long long)n; }
+      const int64_t base = seg_lo[sg];
+      int32_t best = INT32_MAX;  // lane = view
+      if (cb_prev && uw_cur && n <= kSegSlots) {
+        // Loads first over the segment's (at most 8) chunks: neighbours, their changed-bit words,
+        // then the hot slots' masks and words, then the folds — three dependent trips per segment
+        // instead of three per chunk.
+        constexpr int NC = kSegSlots / 64;
+        int32_t q[NC];
+        uint64_t cbw[NC], m[NC];
+        int32_t u[NC];
+  #pragma unroll
+        for (int k = 0; k < NC; k++) q[k] = k * 64 < n ? snbr[base + (k * 64 + lane < n ? k * 64 + lane : k * 64)] : 0;
+  #pragma unroll
+        for (int k = 0; k < NC; k++) cbw[k] = k * 64 < n ? cb_prev[q[k] >> 6] : 0;
+  #pragma unroll
+        for (int k = 0; k < NC; k++) {
+          const bool hot = k * 64 + lane < n && ((cbw[k] >> (q[k] & 63)) & 1);
+          m[k] = hot ? smask[base + k * 64 + lane] : 0;
+          u[k] = hot ? uw_label(uw_cur[q[k]]) : kMixed;
+        }
+  #pragma unroll
+        for (int k = 0; k < NC; k++) {
+          if (k * 64 >= n) break;
+          const uint64_t a = (m[k] && u[k] == kMixed) ? (m[k] & chg_prev[q[k]]) : m[k];
+          if (work) {
+            w_hot += __popcll(__ballot(a != 0));
+            w_mixed += __popcll(__ballot(a != 0 && u[k] == kMixed));
+            unsigned long long g = u[k] == kMixed ? (unsigned long long)__popcll(a) : 0ull;
+            for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o);
+            w_lanes += g;
+          }
+          best = gather_min<false>(u[k] == kMixed ? a : 0, q[k], best, lab_cur, lane);
+          best = fold_uniform_by_label(__ballot(u[k] != kMixed), a, u[k], best, lane);
+        }
+        if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
+        continue;
       }
-#pragma unroll
-      for (int k = 0; k < NC; k++) {
-        if (k * 64 >= n) break;
-        const uint64_t a = (m[k] && u[k] == kMixed) ? (m[k] & chg_prev[q[k]]) : m[k];
+      for (int32_t c = 0; c < n; c += 64) {
+        const int32_t jj = c + lane;
+        const int64_t idx = base + (jj < n ? jj : c);
+        const int32_t q = snbr[idx];
+        uint64_t a;
+        int32_t u;
+        if (cb_prev) {  // changed bits: uniform changed neighbours on every kept view (exact);
+                        // the slot's mask word is read only for a changed neighbour (the walk streams
+                        // the hub's slot list: 4 B instead of 12 B per unchanged neighbour)
+          const bool hot = jj < n && ((cb_prev[q >> 6] >> (q & 63)) & 1);
+          const uint64_t m = hot ? smask[idx] : 0;
+          u = hot ? uw_label(uw_cur[q]) : kMixed;
+          a = hot ? (u == kMixed ? m & chg_prev[q] : m) : 0;
+        } else {
+          a = jj < n ? (smask[idx] & chg_prev[q]) : 0;
+          u = (uw_cur && a) ? uw_label(uw_cur[q]) : kMixed;
+        }
+        // lane = view: the changed mixed rows (4 in flight), then the uniform neighbours' words
         if (work) {
           w_hot += __popcll(__ballot(a != 0));
-          w_mixed += __popcll(__ballot(a != 0 && u[k] == kMixed));
-          unsigned long long g = u[k] == kMixed ? (unsigned long long)__popcll(a) : 0ull;
+          w_mixed += __popcll(__ballot(a != 0 && u == kMixed));
+          unsigned long long g = u == kMixed ? (unsigned long long)__popcll(a) : 0ull;
           for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o);
           w_lanes += g;
         }
-        best = gather_min<false>(u[k] == kMixed ? a : 0, q[k], best, lab_cur, lane);
-        best = fold_uniform_by_label(__ballot(u[k] != kMixed), a, u[k], best, lane);
+        best = gather_min<false>(u == kMixed ? a : 0, q, best, lab_cur, lane);
+        if (uw_cur) best = fold_uniform_by_label(__ballot(u != kMixed), a, u, best, lane);
       }
       if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
-      continue;
     }
-    for (int32_t c = 0; c < n; c += 64) {
-      const int32_t jj = c + lane;
-      const int64_t idx = base + (jj < n ? jj : c);
-      const int32_t q = snbr[idx];
-      uint64_t a;
-      int32_t u;
-      if (cb_prev) {  // changed bits: uniform changed neighbours on every kept view (exact);
-                      // the slot's mask word is read only for a changed neighbour (the walk streams
-                      // the hub's slot list: 4 B instead of 12 B per unchanged neighbour)
-        const bool hot = jj < n && ((cb_prev[q >> 6] >> (q & 63)) & 1);
-        const uint64_t m = hot ? smask[idx] : 0;
-        u = hot ? uw_label(uw_cur[q]) : kMixed;
-        a = hot ? (u == kMixed ? m & chg_prev[q] : m) : 0;
-      } else {
-        a = jj < n ? (smask[idx] & chg_prev[q]) : 0;
-        u = (uw_cur && a) ? uw_label(uw_cur[q]) : kMixed;
-      }
-      // lane = view: the changed mixed rows (4 in flight), then the uniform neighbours' words
-      if (work) {
-        w_hot += __popcll(__ballot(a != 0));
-        w_mixed += __popcll(__ballot(a != 0 && u == kMixed));
-        unsigned long long g = u == kMixed ? (unsigned long long)__popcll(a) : 0ull;
-        for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o);
-        w_lanes += g;
-      }
-      best = gather_min<false>(u == kMixed ? a : 0, q, best, lab_cur, lane);
-      if (uw_cur) best = fold_uniform_by_label(__ballot(u != kMixed), a, u, best, lane);
-    }
-    if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
   }
   heavy_work(work, 0, w_seg);
   heavy_work(work, 1, w_slots);
@@ -1740,7 +1756,7 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
                                                     const int64_t* __restrict__ ts_t, int64_t tcut,
                                                     const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
                                                     unsigned long long* __restrict__ work,
-                                                    const int32_t* __restrict__ uw_ghost) {
+                                                    const int32_t* __restrict__ uw_ghost, int pro) {
   if (stepflag[step] == 0) return;
   if (dense_rule(ccount, step, nv_all, dense_div)) return;  // dense step: the next one visits every member
   if (dense_rule(ccount, step - 1, nv_all, dense_div)) act_cur = nullptr;  // this step visited every member
@@ -1748,19 +1764,28 @@ __global__ __launch_bounds__(256) void k_heavy_mark(int step, int64_t nseg, cons
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   unsigned long long w_walk = 0;
-  for (int64_t sg = wave; sg < nseg; sg += nwaves) {
-    const int32_t v = seg_v[sg];
-    if (act_cur && v < n_own && !act_cur[v]) continue;  // a ghost's word is current (set by its records)
+  for (int64_t r0 = 0; wave + r0 * nwaves < nseg; r0 += pro) {  // (the gather's rounds)
+    const int64_t sl = wave + (r0 + lane) * nwaves;
+    const bool in = lane < pro && sl < nseg;
+    const int32_t vl = in ? seg_v[sl] : 0;
+    // a ghost's word is current (set by its records)
+    bool on = in && !(act_cur && vl < n_own && !act_cur[vl]);
     // a ghost hub's U record sets its uniform word (changed: every view) and no change word
-    const int32_t wg = (uw_ghost && v >= n_own) ? uw_ghost[v] : kMixed;
-    const uint64_t ch = (wg != kMixed && wg < 0) ? ~0ull : chg_now[v];
-    if (!ch) continue;
-    const int32_t n = segcnt[sg];
-    const int64_t base = seg_lo[sg];
-    w_walk += (unsigned long long)n;
-    for (int32_t c = 0; c < n; c += 64) {
-      const int32_t jj = c + lane;
-      if (jj < n && (smask[base + jj] & ch)) act_next[snbr[base + jj]] = 1;
+    const int32_t wg = (on && uw_ghost && vl >= n_own) ? uw_ghost[vl] : kMixed;
+    const uint64_t chl = on ? ((wg != kMixed && wg < 0) ? ~0ull : chg_now[vl]) : 0ull;
+    const int32_t nl = (on && chl) ? segcnt[sl] : 0;
+    on = on && chl != 0 && nl > 0;
+    for (uint64_t todo = __ballot(on); todo; todo &= todo - 1) {
+      const int L = __builtin_ctzll(todo);
+      const int64_t sg = wave + (r0 + L) * nwaves;
+      const uint64_t ch = readlane64(chl, L);
+      const int32_t n = __builtin_amdgcn_readlane(nl, L);
+      const int64_t base = seg_lo[sg];
+      w_walk += (unsigned long long)n;
+      for (int32_t c = 0; c < n; c += 64) {
+        const int32_t jj = c + lane;
+        if (jj < n && (smask[base + jj] & ch)) act_next[snbr[base + jj]] = 1;
+      }
     }
   }
   heavy_work(work, 5, w_walk);
@@ -2445,6 +2470,9 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                            : (iem ? k_cc_slots<false, true, true> : k_cc_slots<false, false, true>))
                    : (work ? (iem ? k_cc_slots<true, true, false> : k_cc_slots<true, false, false>)
                            : (iem ? k_cc_slots<false, true, false> : k_cc_slots<false, false, false>));
+  // the lean one-partition form held to 7 waves per SIMD (<= 72 VGPRs, a few spilled): C4 cc_slots
+  // 54.7 -> 53.4 ms serial (profiles/r05/ab_occ_c4.jsonl)
+  if (!work && iem && !(gpeer && pmask)) kern = k_cc_slots<false, true, false, 7>;
   BatchParams bp0;
   if (!iem) std::memset(&bp0, 0, sizeof(bp0));
   kern<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
@@ -2507,16 +2535,25 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
       snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own, g.ts_e, g.ts_nb, g.ts_t, tcut, ends ? 1 : 0, work,
       iem ? *ebp : bp0, g.ts_g);
 }
+// segments per wave and round of the hub kernels' prologue (kernels.hpp kHubPro; RGPU_HUB_PRO)
+// (read per launch, as tools/ab.py flips it in-process)
+static int hub_pro() {
+  const char* e = getenv("RGPU_HUB_PRO");
+  const int v = e ? atoi(e) : kHubPro;
+  return v < 1 ? 1 : (v > 64 ? 64 : v);
+}
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur,
                          const uint64_t* cb_prev, const int32_t* ccount, int dense_div, unsigned long long* work,
                          const uint64_t* vm, const int32_t* mneg) {
   if (g.n_seg <= 0) return;
-  k_heavy_gather<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
+  // held to 6 waves per SIMD (<= 80 VGPRs; unconstrained it takes 103, 4 waves): C4 heavy 48.6 ->
+  // 47.7 ms serial (profiles/r05/ab_occ_c4.jsonl)
+  k_heavy_gather<6><<<grid_for(g.n_seg, 4 * hub_pro(), 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
                                                              hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
-                                                             g.n_own, work, vm, mneg);
+                                                             g.n_own, work, vm, mneg, hub_pro());
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
@@ -2524,11 +2561,11 @@ void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, co
                        int64_t tcut, const int32_t* ccount, int dense_div, unsigned long long* work,
                        const int32_t* uw_ghost) {
   if (g.n_seg <= 0) return;
-  k_heavy_mark<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
+  k_heavy_mark<<<grid_for(g.n_seg, 4 * hub_pro(), 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
                                                            chg_now, act_cur, act_next, stepflag, g.n_own, g.seg_n,
                                                            g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst,
                                                            vm, em, g.ts_e, g.ts_nb, g.ts_t, tcut, ccount, dense_div,
-                                                           g.n_own, work, uw_ghost);
+                                                           g.n_own, work, uw_ghost, hub_pro());
 }
 int64_t deg_top_waves(int64_t nv) { return (int64_t)grid_for(nv, 4, 2048) * 4; }
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,

@@ -91,6 +91,11 @@ bool build_time_slots(hipStream_t s, const DevGraph& g, int32_t* ts_e, int32_t* 
                       std::vector<void*>& temps);
 void build_slot_labels(hipStream_t s, int64_t n, const int32_t* ts_nb, const int32_t* grank, int32_t* ts_g);
 constexpr int kSegSlots = 512;
+// hub segments per wave and round in the per-superstep hub kernels (k_heavy_gather / k_heavy_mark):
+// their prologue loads that many segments' vertex, flag and count at once (lane = segment); the
+// launchers read RGPU_HUB_PRO (1..64, default kHubPro) per launch, for A/B runs (C4, profiles/r05/
+// ab_hubpro_c4.jsonl + ab_occ_c4.jsonl: heavy 64.7 ms serial at 1, 49.9 at 8, 48.3 at 16, 47.9 at 32)
+constexpr int kHubPro = 32;
 
 // Per-batch state of the heavy-vertex path (one per batch slot).
 struct HeavyBuf {

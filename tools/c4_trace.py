@@ -71,7 +71,8 @@ def digest(path):
         pg = sum(x[4] for x in st)
         print(f"batch {b:3d}: steps {len(st):3d} step_ms {ms[(b, 'cc_step')]:8.2f} slots_ms {ms[(b, 'cc_slots')]:7.2f}"
               f" visited {pv / 1e6:8.2f}M slots {ps / 1e6:9.2f}M gathers {pg / 1e6:9.2f}M "
-              f"per-step visited(M) {[round(x[1] / 1e6, 2) for x in st[:12]]}")
+              f"per-step visited(M) {[round(x[1] / 1e6, 2) for x in st[:12]]} "
+              f"slots(M) {[round(x[2] / 1e6, 1) for x in st[:12]]}")
 
 
 if __name__ == "__main__":
