@@ -1012,6 +1012,27 @@ __device__ __forceinline__ void mark(bool want, int32_t v, uint8_t* act_next) {
   if (want) act_next[v] = 1;
 }
 
+// superstep kernel options (k_cc_step_pk opts): members holding the final label finished lane-
+// parallel; full uniform slots folded by a segmented min over the pack (and over a hub segment or a
+// big member's chunks); simple members (every fold full) visited lane-parallel
+constexpr int kStepFinLanes = 1, kStepSegMin = 2, kStepSimple = 4;
+// Per lane: the views whose final label (mfin, lane = view: final_label) equals this lane's label
+// x.  The loop runs once per distinct final label of the batch (one for a long window: its views
+// share their smallest member), so a wave tests 64 members at once instead of one per ballot.
+// Call it with every lane of the wave active (its loop takes one view's label per round from
+// the ballot of all lanes; the view itself is always retired, so the loop ends regardless).
+__device__ __forceinline__ uint64_t views_with_final(int32_t x, int32_t mfin) {
+  uint64_t eq = 0;
+  for (uint64_t rest = ~0ull; rest;) {
+    const int L = __builtin_ctzll(rest);
+    const int32_t d = __builtin_amdgcn_readlane(mfin, L);
+    const uint64_t m = __ballot(mfin == d) | (1ull << L);
+    rest &= ~m;
+    if (x == d) eq |= m;
+  }
+  return eq;
+}
+
 // One CH-vertex chunk of a superstep.  Vertex i (< CH) of the chunk is readlane(vl, i) and
 // is taken iff bit i of `bits` is set; every lane holds a valid (padded) vertex for the
 // unconditional loads.  The chunk runs loads-first: metadata + own change words + own label
@@ -1036,7 +1057,7 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
                                          const int32_t* __restrict__ uw_cur = nullptr,
                                          int32_t* __restrict__ uw_next = nullptr,
                                          uint64_t* __restrict__ cb_next = nullptr, bool skip_marks = false,
-                                         int32_t mfin = INT32_MIN, bool use_fin = false) {
+                                         int32_t mfin = INT32_MIN, bool use_fin = false, bool segmin = false) {
   {
     // stage 1: metadata (lane i -> vertex i of the chunk), own change words, own label rows
     const bool okl = lane < CH && ((bits >> lane) & 1);
@@ -1135,10 +1156,19 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
     }
 #pragma unroll
     for (int i = 0; i < CH; i++) best[i] = gather_min<BUF>(actr[i], nb[i], best[i], lab_cur, lane);
+    // full slots (a changed uniform neighbour folded on every view of the vertex): a wave min
+    // (lane = slot) over all its chunks, applied once below, instead of a fold lane by lane
+    int32_t fmv[CH];
+#pragma unroll
+    for (int i = 0; i < CH; i++) fmv[i] = INT32_MAX;
     if (uw_cur) {
 #pragma unroll
-      for (int i = 0; i < CH; i++)
-        best[i] = fold_uniform(__ballot(un[i] != kMixed && act[i] != 0), act[i], un[i], best[i], lane);
+      for (int i = 0; i < CH; i++) {
+        const uint64_t mvi = readlane64(mv_l, i);
+        const bool full = segmin && un[i] != kMixed && act[i] != 0 && (act[i] & mvi) == mvi;
+        if (full) fmv[i] = un[i];
+        best[i] = fold_uniform(__ballot(un[i] != kMixed && act[i] != 0 && !full), act[i], un[i], best[i], lane);
+      }
     }
 #pragma unroll
     for (int i = 0; i < CH; i++) {
@@ -1168,8 +1198,21 @@ __device__ __forceinline__ void cc_chunk(int64_t vl, uint32_t bits, const int64_
           }
           wk.g += u2 == kMixed ? __popcll(a2) : 0;
           best[i] = gather_min<BUF>(u2 == kMixed ? a2 : 0, q, best[i], lab_cur, lane);
-          if (uw_cur) best[i] = fold_uniform(__ballot(u2 != kMixed && a2 != 0), a2, u2, best[i], lane);
+          if (uw_cur) {
+            const uint64_t mvi = readlane64(mv_l, i);
+            const bool full = segmin && u2 != kMixed && a2 != 0 && (a2 & mvi) == mvi;
+            if (full) fmv[i] = min(fmv[i], u2);
+            best[i] = fold_uniform(__ballot(u2 != kMixed && a2 != 0 && !full), a2, u2, best[i], lane);
+          }
         }
+      }
+    }
+    if (segmin) {
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        int32_t f = fmv[i];
+        for (int o = 32; o > 0; o >>= 1) f = min(f, __shfl_xor(f, o));
+        if ((readlane64(mv_l, i) >> lane) & 1) best[i] = min(best[i], f);
       }
     }
     // heavy vertices: the step's minima over their segments (k_heavy_gather); reset for the
@@ -1264,8 +1307,10 @@ __global__ __launch_bounds__(256) void k_uw_rows(int64_t nv, const uint64_t* __r
 // uniform word, change word and own frontier flag are stored lane-parallel at the end of the round.
 // Members with more than 64 kept slots take the chunk path (cc_chunk) one at a time, before the
 // packs (so its registers do not add to the round's).
-template <bool BUF, bool PROF>
-__global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const int64_t* __restrict__ adj_off,
+// (the lean form is held to 6 waves per SIMD, <= 80 VGPRs: at 5 waves the kernel measured 13 %
+// slower on C4, profiles/r05/ab_occ_c4.jsonl)
+template <bool BUF, bool PROF, int WPE = PROF ? 1 : 6>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_cc_step_pk(int step, int64_t nv, const int64_t* __restrict__ adj_off,
                                                     const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
                                                     const int32_t* __restrict__ snbr, const uint64_t* __restrict__ smask,
                                                     const int32_t* __restrict__ lab_cur, int32_t* __restrict__ lab_next,
@@ -1278,7 +1323,8 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
                                                     const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
                                                     uint64_t* __restrict__ cb_next, uint64_t* __restrict__ cb_clear,
                                                     int64_t cb_words, int32_t* __restrict__ ccount, int dense_div, int gmax,
-                                                    const int32_t* __restrict__ mneg, const uint64_t* __restrict__ cb_prev) {
+                                                    const int32_t* __restrict__ mneg, const uint64_t* __restrict__ cb_prev,
+                                                    int opts) {
   if (stepflag[step - 1] == 0) return;
   const int lane = lane_id();
   const bool use_fin = mneg != nullptr && uw_cur != nullptr;
@@ -1317,20 +1363,13 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
     }
     uint64_t todo = __ballot(flag);
     if (!todo) continue;
-    int32_t n = flag ? cnt[vl] : 0;  // 0 for a heavy vertex (its slots are in segments)
-    // members with more than 64 kept slots: the chunk path, one vertex at a time
-    for (uint64_t big = __ballot(flag && n > 64); big; big &= big - 1) {
-      const int L = __builtin_ctzll(big);
-      cc_chunk<2, BUF>((int64_t)readlane64((uint64_t)vl, L), 1u, adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
-                       chg_prev, chg_next, act_next, lane, changed, &wred[7], wk, hv_of, hbest, uw_cur, uw_next, cb_next,
-                       skip_marks, mfin, use_fin);
-    }
-    bool mine = flag && n <= 64;  // this lane's member is handled below
-    if (!__ballot(mine)) continue;
+    // the flagged members' metadata in one trip: kept-slot count (0 for a hub: its slots are in
+    // segments), view mask, slot offset, change word, uniform words, hub index
+    int32_t n = 0, u = kMixed, un = kMixed, hh = -1;
     int64_t base = 0;
     uint64_t cp = 0;
-    int32_t u = kMixed, un = kMixed, hh = -1;
-    if (mine) {
+    if (flag) {
+      n = cnt[vl];
       if (!visit_all) mv = vm[vl];
       base = adj_off[vl];
       cp = chg_prev[vl];
@@ -1338,10 +1377,38 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
       if (uw_next) un = uw_next[vl];
       if (hv_of) hh = hv_of[vl];
     }
-    mine = mine && mv != 0;  // (a flagged non-member has nothing to do)
+    flag = flag && mv != 0;  // (a flagged non-member has nothing to do)
+    if (use_fin && uw_next && (opts & kStepFinLanes)) {
+      // A member that holds its views' final label (uniform, and equal to every member view's
+      // final label: views_with_final, lane-parallel) gathers nothing and cannot change.  The
+      // non-hubs among them are finished here, lane = member, as the member loop below would
+      // finish them: the word rewritten (without the changed flag) if it changed in step r-1 —
+      // both label buffers then differ — else a stale changed flag cleared; no change word.
+      // (Hubs keep their slot-less visit below: it resets their minima row.)
+      const uint64_t eqf = views_with_final(u & 0x7fffffff, mfin);  // (every lane: see its note)
+      const bool fin = flag && u != kMixed && hh < 0 && (mv & ~eqf) == 0;
+      const uint64_t fz = __ballot(fin);
+      if (fz) {
+        if (fin) {
+          if (cp) uw_next[vl] = u & 0x7fffffff;
+          else if (un != kMixed && un < 0) uw_next[vl] = un & 0x7fffffff;
+          chg_next[vl] = 0;
+        }
+        wk.v += __popcll(fz);
+        flag = flag && !fin;
+      }
+    }
+    // members with more than 64 kept slots: the chunk path, one vertex at a time
+    for (uint64_t big = __ballot(flag && n > 64); big; big &= big - 1) {
+      const int L = __builtin_ctzll(big);
+      cc_chunk<2, BUF>((int64_t)readlane64((uint64_t)vl, L), 1u, adj_off, vm, cnt, snbr, smask, lab_cur, lab_next,
+                       chg_prev, chg_next, act_next, lane, changed, &wred[7], wk, hv_of, hbest, uw_cur, uw_next, cb_next,
+                       skip_marks, mfin, use_fin, (opts & kStepSegMin) != 0);
+    }
+    bool mine = flag && n <= 64;  // this lane's member is handled below
     todo = __ballot(mine);
     if (!todo) continue;
-    if (use_fin) {  // a member that holds its views' final label gathers nothing
+    if (use_fin && !(uw_next && (opts & kStepFinLanes))) {  // (the members' own test, one at a time)
       for (uint64_t t = todo; t; t &= t - 1) {
         const int L = __builtin_ctzll(t);
         const bool fin = holds_final(__builtin_amdgcn_readlane(u, L), readlane64(mv, L), mfin, lane);
@@ -1397,13 +1464,98 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
         act = sma & chg_prev[nbp];
       }
       wk.g += unp == kMixed ? __popcll(act) : 0;
+      // Full slots: a changed uniform neighbour whose fold covers every view of its member (the
+      // usual slot of a long window) adds the same label to all of them, so the pack folds those
+      // at once, lane = slot: a min over each member's span of lanes (a segmented scan, 6 shuffle
+      // rounds), read by the member below from its span's last lane.  The other uniform slots
+      // fold view by view (fold_uniform_by_label), the mixed ones from their rows (gather_min).
+      bool full = false;
+      int32_t fmin = INT32_MAX;
+      if (uw_cur && (opts & kStepSegMin)) {
+        const uint64_t mvs = ((uint64_t)(uint32_t)__shfl((int)(mv >> 32), myL) << 32) | (uint32_t)__shfl((int)mv, myL);
+        full = on && unp != kMixed && act != 0 && (act & mvs) == mvs;
+        fmin = full ? unp : INT32_MAX;
+        if (__ballot(full)) {
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const int32_t y = __shfl_up(fmin, d);
+            if (myj >= d) fmin = min(fmin, y);
+          }
+        }
+      }
       uint64_t markp = 0;  // lane = slot: its neighbour joins the next frontier
-      int pre = 0;
-      for (uint64_t pk = pack; pk; pk &= pk - 1) {
+      // lane = member of the pack: the first slot lane of its span (exclusive prefix of the counts)
+      const bool inpk = (pack >> lane) & 1;
+      const int32_t kin = inpk ? n : 0;
+      int32_t prem = kin;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t y = __shfl_up(prem, d);
+        if (lane >= d) prem += y;
+      }
+      prem -= kin;
+      // Simple members (lane = member): uniform, no hub, and every fold in their span full.  Their
+      // new label is min(own, span minimum) on all their views, so their whole visit is lane-
+      // parallel: the span's minimum and its "any other fold" flag are read from the span's last
+      // lane, then the word, change word, changed views and the neighbours' frontier marks follow
+      // exactly as the member loop below writes them for any member.
+      uint64_t simple = 0;
+      if (uw_cur && uw_next && (opts & kStepSegMin) && (opts & kStepSimple)) {
+        int32_t bad = (on && act != 0 && !full) ? 1 : 0;  // a fold that is not full
+        if (__ballot(bad)) {
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const int32_t y = __shfl_up(bad, d);
+            if (myj >= d) bad |= y;
+          }
+        }
+        const int lastl = kin > 0 ? prem + kin - 1 : 0;
+        const int32_t fm = __shfl(fmin, lastl), bd = __shfl(bad, lastl);
+        const bool sl = inpk && u != kMixed && hh < 0 && (kin == 0 || bd == 0);
+        simple = __ballot(sl);
+        if (simple) {
+          uint64_t sch = 0;
+          if (sl) {
+            const int32_t X = u & 0x7fffffff;
+            const int32_t nbl = kin > 0 ? min(X, fm) : X;
+            if (nbl < X) {
+              sch = mv;
+              my_w = uw_word(nbl, true);
+              has_w = true;
+            } else if (cp) {  // both label buffers differ: rewrite the word
+              my_w = X;
+              has_w = true;
+            } else if (un != kMixed && un < 0) {  // stale flag
+              my_w = un & 0x7fffffff;
+              has_w = true;
+            }
+            my_ch = sch;
+          }
+          const uint64_t chb = __ballot(sch != 0);
+          if (chb) {
+            changed += __popcll(chb);
+            uint64_t o = sch;
+            for (int d = 32; d > 0; d >>= 1) o |= shfl_xor64(o, d);
+            lanes_or |= o;
+            const uint64_t chm = ((uint64_t)(uint32_t)__shfl((int)(sch >> 32), myL) << 32) |
+                                 (uint32_t)__shfl((int)sch, myL);
+            if (on && (smp & chm)) markp = 1;
+          }
+          wk.v += __popcll(simple);
+          if constexpr (PROF) {
+            unsigned long long ks = sl ? (unsigned long long)kin : 0ull;
+            for (int d = 32; d > 0; d >>= 1) ks += __shfl_xor(ks, d);
+            wk.s += ks;
+            wk.uw += __popcll(__ballot(sl && (sch != 0 || cp != 0)));
+          }
+        }
+      }
+      for (uint64_t pk = pack & ~simple; pk; pk &= pk - 1) {
         const int L = __builtin_ctzll(pk);
         const int k = __builtin_amdgcn_readlane(n, L);
+        const int pre = __builtin_amdgcn_readlane(prem, L);
         const uint64_t span = k == 0 ? 0ull : ((k >= 64 ? ~0ull : ((1ull << k) - 1)) << pre);
-        pre += k;
+        const int32_t fL = k == 0 ? INT32_MAX : __builtin_amdgcn_readlane(fmin, pre + k - 1);
         const uint64_t mvL = readlane64(mv, L);
         const int64_t v = (int64_t)readlane64((uint64_t)vl, L);
         const int32_t uL = __builtin_amdgcn_readlane(u, L);
@@ -1418,7 +1570,10 @@ __global__ __launch_bounds__(256) void k_cc_step_pk(int step, int64_t nv, const 
         cur = mem ? cur : INT32_MAX;
         const bool inspan = (span >> lane) & 1;
         int32_t best = gather_min<BUF>(inspan && unp == kMixed ? act : 0, nbp, cur, lab_cur, lane);
-        if (uw_cur) best = fold_uniform_by_label(__ballot(inspan && unp != kMixed && act != 0), act, unp, best, lane);
+        if (uw_cur) {
+          if (mem) best = min(best, fL);
+          best = fold_uniform_by_label(__ballot(inspan && unp != kMixed && act != 0 && !full), act, unp, best, lane);
+        }
         const int32_t hL = __builtin_amdgcn_readlane(hh, L);
         if (hL >= 0) {  // a hub: the step's minima over its segments (k_heavy_gather), reset for the next step
           const int32_t x = hbest[(int64_t)hL * 64 + lane];
@@ -1625,7 +1780,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                                       const int32_t* __restrict__ ccount, int dense_div, int64_t nv_all,
                                                       unsigned long long* __restrict__ work,
                                                       const uint64_t* __restrict__ vm,
-                                                      const int32_t* __restrict__ mneg, int pro) {
+                                                      const int32_t* __restrict__ mneg, int pro, int pro_opts) {
   if (stepflag[step - 1] == 0) return;
   const bool use_fin = vm && uw_cur && mneg;
   const int32_t mfin = use_fin ? final_label(mneg, threadIdx.x & 63) : INT32_MIN;
@@ -1645,9 +1800,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int32_t nl = in ? segcnt[sl] : 0;
     // ghosts are not visited (their owner computes them)
     const bool on = in && vl < n_own && nl > 0 && (visit_all || act_cur[vl] != 0);
-    // (the final-label test's word and mask, loaded with the segments')
+    // (the final-label test's word and the hub's view mask, loaded with the segments')
     const int32_t ul = (use_fin && on) ? uw_cur[vl] : kMixed;
-    const uint64_t ml = (use_fin && on) ? vm[vl] : 0;
+    const uint64_t ml = on ? vm[vl] : 0;
     for (uint64_t todo = __ballot(on); todo; todo &= todo - 1) {
       const int L = __builtin_ctzll(todo);
       const int64_t sg = wave + (r0 + L) * nwaves;
@@ -1675,6 +1830,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           m[k] = hot ? smask[base + k * 64 + lane] : 0;
           u[k] = hot ? uw_label(uw_cur[q[k]]) : kMixed;
         }
+        // full slots (a changed uniform neighbour folded on every view of the hub): one wave min
+        // over the segment (lane = slot) instead of a fold per distinct label (as k_cc_step_pk)
+        const uint64_t mvv = readlane64(ml, L);
+        const bool segmin = (pro_opts & kStepSegMin) != 0;
+        int32_t fm = INT32_MAX;
   #pragma unroll
         for (int k = 0; k < NC; k++) {
           if (k * 64 >= n) break;
@@ -1686,8 +1846,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             for (int o = 32; o > 0; o >>= 1) g += __shfl_xor(g, o);
             w_lanes += g;
           }
+          const bool fullk = segmin && u[k] != kMixed && a != 0 && (a & mvv) == mvv;
+          if (fullk) fm = min(fm, u[k]);
           best = gather_min<false>(u[k] == kMixed ? a : 0, q[k], best, lab_cur, lane);
-          best = fold_uniform_by_label(__ballot(u[k] != kMixed), a, u[k], best, lane);
+          best = fold_uniform_by_label(__ballot(u[k] != kMixed && !fullk), a, u[k], best, lane);
+        }
+        if (segmin) {
+          for (int o = 32; o > 0; o >>= 1) fm = min(fm, __shfl_xor(fm, o));
+          if ((mvv >> lane) & 1) best = min(best, fm);
         }
         if (best != INT32_MAX) atomicMin(&hbest[(int64_t)seg_h[sg] * 64 + lane], best);
         continue;
@@ -2498,6 +2664,13 @@ void launch_cc_roots(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, 
   k_cc_roots<<<grid_for(nv, 256, 4096), 256, 0, s>>>(nv, vmask, vm, vadj, uw, lab, counts, stats, iso,
                                                      scan_all ? 1 : 0, grank, rows_by_rank ? 1 : 0);
 }
+// superstep kernel options (k_cc_step_pk, k_heavy_gather): RGPU_STEP_OPTS (A/B; default all) bit 0
+// kStepFinLanes, bit 1 kStepSegMin, bit 2 kStepSimple; 0 is the round-4 form.  Read per launch
+// (tools/ab.py).
+static int step_opts() {
+  const char* ov = getenv("RGPU_STEP_OPTS");
+  return ov ? atoi(ov) : (kStepFinLanes | kStepSegMin | kStepSimple);
+}
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
@@ -2517,7 +2690,9 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   // C4 serial cc_step 207.6 -> 155.1 ms, query 343 -> 286 ms.
 #define RGPU_PK_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr, cbf ? cb.prev : nullptr
+    cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr, cbf ? cb.prev : nullptr, \
+    opts
+  const int opts = step_opts();
   const unsigned gridp = grid_for(g.nv, 256, cap);
   if (work) k_cc_step_pk<false, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
   else k_cc_step_pk<false, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
@@ -2553,7 +2728,7 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
   k_heavy_gather<6><<<grid_for(g.n_seg, 4 * hub_pro(), 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
                                                              hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
-                                                             g.n_own, work, vm, mneg, hub_pro());
+                                                             g.n_own, work, vm, mneg, hub_pro(), step_opts());
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
