@@ -363,6 +363,27 @@ void launch_count_simple(hipStream_t s, const DevGraph& g, unsigned long long* o
   if (g.ne > 0)
     k_count_simple<<<1024, 256, 0, s>>>(g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dbits, out);
 }
+// lane = edge, one bitmap word per wave (64 consecutive edges)
+__global__ __launch_bounds__(256) void k_edge_simple_bits(int64_t ne, const int32_t* __restrict__ esrc,
+                                                          const int32_t* __restrict__ edst,
+                                                          const int64_t* __restrict__ eoff,
+                                                          const int64_t* __restrict__ ekey,
+                                                          const int64_t* __restrict__ doff,
+                                                          const uint64_t* __restrict__ dbits,
+                                                          uint64_t* __restrict__ out) {
+  const int lane = lane_id();
+  for (int64_t e0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63ll; e0 < ne;
+       e0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = e0 + lane;
+    const uint64_t w = __ballot(e < ne && edge_simple(eoff[e], eoff[e + 1], ekey, esrc[e], edst[e], doff, dbits));
+    if (lane == 0) out[e0 >> 6] = w;
+  }
+}
+void launch_edge_simple_bits(hipStream_t s, const DevGraph& g, uint64_t* out) {
+  if (g.ne > 0)
+    k_edge_simple_bits<<<(unsigned)std::min<int64_t>((g.ne + 255) / 256, 16384), 256, 0, s>>>(
+        g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dbits, out);
+}
 
 // The loop runs wave-uniform (lane = edge within a 64-edge group) so that profile runs can
 // count alive edges per view: the wave's 64 mask words are bit-transposed (lane j <- view j)
@@ -380,7 +401,7 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
                                                    unsigned long long* __restrict__ ecnt, int64_t h0,
                                                    int64_t own_lim, const uint64_t* __restrict__ vm_ends,
                                                    int64_t vstride, const uint64_t* __restrict__ dbits,
-                                                   int32_t* __restrict__ fc) {
+                                                   int32_t* __restrict__ fc, const uint64_t* __restrict__ esimple) {
   __shared__ HopLDS L;
   __shared__ unsigned int cnt_s[PLANAR ? kMaxPlanes : 1][64];
   hop_lds_init(L, bp, bp.thr_e);
@@ -394,7 +415,12 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
     const int64_t e = e0 + lane;
     uint64_t m[NP] = {};
     uint64_t mo[NP];  // the edge's own aliveness (the |E_w| counts)
-    if (SKIP && e < ne && edge_simple(eoff[e], eoff[e + 1], ekey, esrc[e], edst[e], doff, dbits)) continue;
+    if (SKIP && esimple) {  // the group's simple bits (a wave of simple edges costs one 8-B load)
+      const uint64_t sw = esimple[e0 >> 6];
+      if (sw == ~0ull || (e < ne && ((sw >> lane) & 1))) continue;
+    } else if (SKIP && e < ne && edge_simple(eoff[e], eoff[e + 1], ekey, esrc[e], edst[e], doff, dbits)) {
+      continue;
+    }
     if (e < ne) {
       edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime, dbits, fc);
 #pragma unroll
@@ -592,7 +618,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                                   int32_t* __restrict__ ccount, int gmax, BatchParams ebp,
                                                   int dense1, const int32_t* __restrict__ ts_g,
                                                   int32_t* __restrict__ mneg, const uint8_t* __restrict__ gpeer,
-                                                  uint8_t* __restrict__ pmask) {
+                                                  uint8_t* __restrict__ pmask, int kopts) {
   __shared__ unsigned long long red[4];
   int32_t wmin = INT32_MAX;  // lane = view: the minimum label of this wave's owned members
   __shared__ HopLDS L;
@@ -662,7 +688,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int64_t p = bmy + myj;
         const int64_t tsw = ts_t[p];
         nb = ts_nb[p];
-        const int32_t e = ts_e[p];
+        const int32_t e = (IEM && ts_simple(tsw)) ? 0 : ts_e[p];  // (a simple slot's bits need no edge index)
         if (nb != (int32_t)vmy && ts_time(tsw) >= tcut) {
           if constexpr (IEM) {
             m = slot_bits(L, ebp, tsw, em, e, vm, nb) & mvmy;
@@ -681,6 +707,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const int64_t pos = bmy + __popcll(bal & below);
         snbr[pos] = nb;
         smask[pos] = m;
+      }
+      // Full kept slots (kept on every view of their member: the usual slot of a long window) fold
+      // the same label into all of the member's views: a segmented min over the pack (lane = slot,
+      // spans of consecutive lanes), read from the span's last lane; the member loop below folds
+      // only the other kept slots one by one (as k_cc_step_pk).  Partitioned: the peer bits OR-ed
+      // the same way.
+      const bool fullk = (kopts & kStepSegMin) && m != 0 && m == mvmy;
+      const uint64_t fullb = __ballot(fullk);
+      int32_t fmin = fullk ? lb : INT32_MAX;
+      if (fullb) {
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int32_t y = __shfl_up(fmin, d);
+          if (myj >= d) fmin = min(fmin, y);
+        }
+      }
+      if constexpr (PART) {
+        if (__ballot(pbit != 0)) {
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)pbit, d);
+            if (myj >= d) pbit |= y;
+          }
+        }
       }
       // per member of the pack: superstep 1 (lane = view) and its words
       int pre = 0;
@@ -707,11 +757,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         uint64_t any = 0;
         uint32_t pm = 0;
         if (own) {
-          for (uint64_t b = kept; b; b &= b - 1) {
+          const int32_t fL = n == 0 ? INT32_MAX : __builtin_amdgcn_readlane(fmin, pre - 1);
+          if (fL != INT32_MAX) {  // (a full slot: labels are never INT32_MAX)
+            any = mv;
+            if (((mv >> lane) & 1) && fL < best) best = fL;
+          }
+          if constexpr (PART) pm = n == 0 ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)pbit, pre - 1);
+          for (uint64_t b = kept & ~fullb; b; b &= b - 1) {
             const int K = __builtin_ctzll(b);
             const int32_t q = __builtin_amdgcn_readlane(lb, K);
             const uint64_t mK = readlane64(m, K);
-            if constexpr (PART) pm |= (uint32_t)__builtin_amdgcn_readlane((int)pbit, K);
             any |= mK;
             if (((mK >> lane) & 1) && q < best) best = q;
           }
@@ -832,8 +887,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       int32_t nb = 0, lb = 0;
       if (j < ntot) {
         int64_t e;
+        const int64_t tsw = ts_t ? ts_t[base + j] : 0;
         if (ts_e) {
-          e = ts_e[base + j];
+          e = (IEM && ts_simple(tsw)) ? 0 : ts_e[base + j];  // (a simple slot's bits need no edge index)
           nb = ts_nb[base + j];
         } else if (j < nout) {
           e = o0 + j;
@@ -842,7 +898,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           e = in_eid[i0 + (j - nout)];
           nb = esrc[e];
         }
-        const int64_t tsw = ts_t ? ts_t[base + j] : 0;
         if (nb != (int32_t)v && (!ts_t || ts_time(tsw) >= tcut)) {
           if constexpr (IEM) {
             m = slot_bits(L, ebp, tsw, em, e, vm, nb) & mv;
@@ -1012,10 +1067,6 @@ __device__ __forceinline__ void mark(bool want, int32_t v, uint8_t* act_next) {
   if (want) act_next[v] = 1;
 }
 
-// superstep kernel options (k_cc_step_pk opts): members holding the final label finished lane-
-// parallel; full uniform slots folded by a segmented min over the pack (and over a hub segment or a
-// big member's chunks); simple members (every fold full) visited lane-parallel
-constexpr int kStepFinLanes = 1, kStepSegMin = 2, kStepSimple = 4;
 // Per lane: the views whose final label (mfin, lane = view: final_label) equals this lane's label
 // x.  The loop runs once per distinct final label of the batch (one for a long window: its views
 // share their smallest member), so a wave tests 64 members at once instead of one per ballot.
@@ -1309,7 +1360,7 @@ __global__ __launch_bounds__(256) void k_uw_rows(int64_t nv, const uint64_t* __r
 // packs (so its registers do not add to the round's).
 // (the lean form is held to 6 waves per SIMD, <= 80 VGPRs: at 5 waves the kernel measured 13 %
 // slower on C4, profiles/r05/ab_occ_c4.jsonl)
-template <bool BUF, bool PROF, int WPE = PROF ? 1 : 6>
+template <bool BUF, bool PROF, bool LONG, int WPE = (PROF || !LONG) ? 1 : 6>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_cc_step_pk(int step, int64_t nv, const int64_t* __restrict__ adj_off,
                                                     const uint64_t* __restrict__ vm, const int32_t* __restrict__ cnt,
                                                     const int32_t* __restrict__ snbr, const uint64_t* __restrict__ smask,
@@ -1324,8 +1375,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                                     uint64_t* __restrict__ cb_next, uint64_t* __restrict__ cb_clear,
                                                     int64_t cb_words, int32_t* __restrict__ ccount, int dense_div, int gmax,
                                                     const int32_t* __restrict__ mneg, const uint64_t* __restrict__ cb_prev,
-                                                    int opts) {
+                                                    int opts_in) {
   if (stepflag[step - 1] == 0) return;
+  // LONG (a batch of long windows, launch_cc_step): the lane-parallel forms (RGPU_STEP_OPTS) are
+  // compiled in; the short-window form is the round-4 kernel (its registers stay at 77, no spills)
+  const int opts = LONG ? opts_in : 0;
   const int lane = lane_id();
   const bool use_fin = mneg != nullptr && uw_cur != nullptr;
   const int32_t mfin = final_label(mneg, lane);
@@ -1488,10 +1542,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const bool inpk = (pack >> lane) & 1;
       const int32_t kin = inpk ? n : 0;
       int32_t prem = kin;
+      if (LONG) {
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int32_t y = __shfl_up(prem, d);
-        if (lane >= d) prem += y;
+        for (int d = 1; d < 64; d <<= 1) {
+          const int32_t y = __shfl_up(prem, d);
+          if (lane >= d) prem += y;
+        }
       }
       prem -= kin;
       // Simple members (lane = member): uniform, no hub, and every fold in their span full.  Their
@@ -1550,10 +1606,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
         }
       }
+      int pre_run = 0;  // (the short-window form: the running prefix, every pack member in order)
       for (uint64_t pk = pack & ~simple; pk; pk &= pk - 1) {
         const int L = __builtin_ctzll(pk);
         const int k = __builtin_amdgcn_readlane(n, L);
-        const int pre = __builtin_amdgcn_readlane(prem, L);
+        const int pre = LONG ? __builtin_amdgcn_readlane(prem, L) : pre_run;
+        pre_run += k;
         const uint64_t span = k == 0 ? 0ull : ((k >= 64 ? ~0ull : ((1ull << k) - 1)) << pre);
         const int32_t fL = k == 0 ? INT32_MAX : __builtin_amdgcn_readlane(fmin, pre + k - 1);
         const uint64_t mvL = readlane64(mv, L);
@@ -1684,7 +1742,7 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
                                                      const int32_t* __restrict__ ts_nb,
                                                      const int64_t* __restrict__ ts_t, int64_t tcut, int ends,
                                                      unsigned long long* __restrict__ work, BatchParams ebp,
-                                                     const int32_t* __restrict__ ts_g) {
+                                                     const int32_t* __restrict__ ts_g, int kopts) {
   __shared__ HopLDS L;
   if constexpr (IEM) hop_lds_init(L, ebp, ebp.thr_e);
   const int lane = lane_id();
@@ -1706,6 +1764,8 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
     const int64_t nout = out_off[v + 1] - o0;
     const int32_t ns = seg_n[sg];
     int32_t best = INT32_MAX;  // lane = view
+    int32_t fmin = INT32_MAX;  // lane = slot: the full slots' minimum label
+    const bool segmin = (kopts & kStepSegMin) != 0;
     int32_t count = 0;
     uint64_t any = 0;
     for (int32_t c = 0; c < ns; c += 64) {
@@ -1717,8 +1777,9 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
       if (jj < ns) {
         const int64_t rel = rel0 + jj;
         int64_t e;
+        const int64_t tsw = ts_t ? ts_t[lo + jj] : 0;
         if (ts_e) {
-          e = ts_e[lo + jj];
+          e = (IEM && ts_simple(tsw)) ? 0 : ts_e[lo + jj];  // (as K2)
           nb = ts_nb[lo + jj];
         } else if (rel < nout) {
           e = o0 + rel;
@@ -1727,7 +1788,6 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
           e = in_eid[i0 + (rel - nout)];
           nb = esrc[e];
         }
-        const int64_t tsw = ts_t ? ts_t[lo + jj] : 0;
         if (nb != v && (!ts_t || ts_time(tsw) >= tcut)) {
           if constexpr (IEM) {
             m = slot_bits(L, ebp, tsw, em, e, vm, nb) & mv;
@@ -1745,11 +1805,18 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
       count += __popcll(bal);
       any |= m;
       const int32_t lb = (grank && m) ? (ts_g ? ts_g[lo + jj] : grank[nb]) : nb;  // setup sends the neighbour's label (id)
-      for (uint64_t b = bal; b; b &= b - 1) {  // lane = view from here: the kept slots one by one
+      // full slots (kept on every view of the hub): their labels' wave min, folded once below
+      const bool fullk = segmin && m != 0 && m == mv;
+      if (fullk) fmin = min(fmin, lb);
+      for (uint64_t b = bal & ~__ballot(fullk); b; b &= b - 1) {  // lane = view from here: the other kept slots one by one
         const int L = __builtin_ctzll(b);
         const int32_t q = __builtin_amdgcn_readlane(lb, L);
         if ((readlane64(m, L) >> lane) & 1) best = min(best, q);
       }
+    }
+    if (segmin) {
+      for (int o = 32; o > 0; o >>= 1) fmin = min(fmin, __shfl_xor(fmin, o));
+      if ((mv >> lane) & 1) best = min(best, fmin);
     }
     for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
     if (lane == 0) { segcnt[sg] = count; segor[sg] = any; }
@@ -2611,7 +2678,7 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
   BatchParams b = bp;
   if (!fc || !bp.sorted) b.carry = 0;
 #define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, b, em, g.ne, ecnt, h0, g.n_own, vm_ends, \
-    vstride, g.dbits, fc
+    vstride, g.dbits, fc, g.esimple
   const unsigned grid = grid_for(g.ne, 256);
   if (planar && ecnt) k_edge_mask<true, true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
   else if (planar && skip_simple) k_edge_mask<true, false, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
@@ -2620,6 +2687,13 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
   else if (skip_simple) k_edge_mask<false, false, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
   else k_edge_mask<false, false, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
 #undef RGPU_EM_ARGS
+}
+// superstep kernel options (k_cc_step_pk, k_heavy_gather): RGPU_STEP_OPTS (A/B; default all) bit 0
+// kStepFinLanes, bit 1 kStepSegMin, bit 2 kStepSimple; 0 is the round-4 form.  Read per launch
+// (tools/ab.py).
+static int step_opts() {
+  const char* ov = getenv("RGPU_STEP_OPTS");
+  return ov ? atoi(ov) : (kStepFinLanes | kStepSegMin | kStepSimple);
 }
 void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
@@ -2636,9 +2710,11 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                            : (iem ? k_cc_slots<false, true, true> : k_cc_slots<false, false, true>))
                    : (work ? (iem ? k_cc_slots<true, true, false> : k_cc_slots<true, false, false>)
                            : (iem ? k_cc_slots<false, true, false> : k_cc_slots<false, false, false>));
-  // the lean one-partition form held to 7 waves per SIMD (<= 72 VGPRs, a few spilled): C4 cc_slots
-  // 54.7 -> 53.4 ms serial (profiles/r05/ab_occ_c4.jsonl)
-  if (!work && iem && !(gpeer && pmask)) kern = k_cc_slots<false, true, false, 7>;
+  // the lean one-partition form held to 6 waves per SIMD (<= 80 VGPRs): C4 cc_slots 54.7 -> 53.4 ms
+  // serial at 7 waves before the full-slot fold, 50.8 (7) -> 49.2 ms (6) with it
+  // (profiles/r05/ab_occ_c4.jsonl, ab_k2_c4.jsonl)
+  if (!work && iem && !(gpeer && pmask)) kern = k_cc_slots<false, true, false, 6>;
+  if (!work && iem && gpeer && pmask) kern = k_cc_slots<false, true, true, 6>;  // (86 VGPRs unheld)
   BatchParams bp0;
   if (!iem) std::memset(&bp0, 0, sizeof(bp0));
   kern<<<grid_for(g.nv, 4), 256, 0, s>>>(g.nv, g.n_own, g.out_off, g.in_off, g.in_eid, g.esrc,
@@ -2647,7 +2723,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
                                                 uw0, uw1, cb1, ends ? 1 : 0, ccount, kDealSlots, iem ? *ebp : bp0,
                                                 dense_div > 0 && (dense_div & kDense1) && ccount ? 1 : 0,
-                                                g.ts_g, mneg, gpeer, pmask);
+                                                g.ts_g, mneg, gpeer, pmask, step_opts());
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
@@ -2664,20 +2740,14 @@ void launch_cc_roots(hipStream_t s, int64_t nv, int nviews, const uint64_t* vm, 
   k_cc_roots<<<grid_for(nv, 256, 4096), 256, 0, s>>>(nv, vmask, vm, vadj, uw, lab, counts, stats, iso,
                                                      scan_all ? 1 : 0, grank, rows_by_rank ? 1 : 0);
 }
-// superstep kernel options (k_cc_step_pk, k_heavy_gather): RGPU_STEP_OPTS (A/B; default all) bit 0
-// kStepFinLanes, bit 1 kStepSegMin, bit 2 kStepSimple; 0 is the round-4 form.  Read per launch
-// (tools/ab.py).
-static int step_opts() {
-  const char* ov = getenv("RGPU_STEP_OPTS");
-  return ov ? atoi(ov) : (kStepFinLanes | kStepSegMin | kStepSimple);
-}
 void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* vm,
                     const int32_t* cnt, const int32_t* snbr, const uint64_t* smask,
                     const int32_t* lab_cur, int32_t* lab_next, const uint64_t* chg_prev,
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next,
-                    const ChgBits& cb, int32_t* ccount, int dense_div, const int32_t* mneg, bool cbf) {
+                    const ChgBits& cb, int32_t* ccount, int dense_div, const int32_t* mneg, bool cbf,
+                    bool long_views) {
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
   // A small graph's dense supersteps are latency-bound and share the GPU with the other batch
   // slots too: a 1,024-block cap measured 4 % faster on C2 (100k vertices) and 2 % slower on a
@@ -2694,8 +2764,19 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
     opts
   const int opts = step_opts();
   const unsigned gridp = grid_for(g.nv, 256, cap);
-  if (work) k_cc_step_pk<false, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
-  else k_cc_step_pk<false, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
+  // The long-window form (lane-parallel members, full folds) pays in the busy early supersteps; it
+  // spills a few registers, and a kernel with scratch launches its waves more slowly, which the
+  // late, sparse supersteps (mostly idle waves) feel: from kLongSteps on, the short form runs.
+  const char* ls = getenv("RGPU_LONG_STEPS");
+  const bool lf = long_views && step < (ls ? atoi(ls) : kLongSteps);
+  if (work) {
+    if (lf) k_cc_step_pk<false, true, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
+    else k_cc_step_pk<false, true, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
+  } else if (lf) {
+    k_cc_step_pk<false, false, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
+  } else {
+    k_cc_step_pk<false, false, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
+  }
 #undef RGPU_PK_ARGS
 }
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
@@ -2708,7 +2789,7 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
   (iem ? k_heavy_slots<true> : k_heavy_slots<false>)<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(
       g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
       snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own, g.ts_e, g.ts_nb, g.ts_t, tcut, ends ? 1 : 0, work,
-      iem ? *ebp : bp0, g.ts_g);
+      iem ? *ebp : bp0, g.ts_g, step_opts());
 }
 // segments per wave and round of the hub kernels' prologue (kernels.hpp kHubPro; RGPU_HUB_PRO)
 // (read per launch, as tools/ab.py flips it in-process)

@@ -54,6 +54,8 @@ struct DevGraph {
   const int64_t *voff = nullptr, *vkey = nullptr;    // vertex histories
   const int64_t *doff = nullptr, *dtime = nullptr;   // vertex death lists
   const uint64_t* dbits = nullptr;                   // bit v: vertex v has a death (null: read doff)
+  const uint64_t* esimple = nullptr;                 // bit e: edge e is simple (edge_simple; built with
+                                                     // the time-ordered slots; null: test per edge)
   const int32_t *esrc = nullptr, *edst = nullptr;    // edges sorted by (src, dst)
   const int64_t *eoff = nullptr, *ekey = nullptr;    // edge own histories
   const int64_t *out_off = nullptr, *in_off = nullptr;
@@ -96,6 +98,14 @@ constexpr int kSegSlots = 512;
 // launchers read RGPU_HUB_PRO (1..64, default kHubPro) per launch, for A/B runs (C4, profiles/r05/
 // ab_hubpro_c4.jsonl + ab_occ_c4.jsonl: heavy 64.7 ms serial at 1, 49.9 at 8, 48.3 at 16, 47.9 at 32)
 constexpr int kHubPro = 32;
+// superstep options (k_cc_step_pk, k_heavy_gather, k_cc_slots; RGPU_STEP_OPTS, all by default):
+// members holding the final label finished lane-parallel; full folds (one label on every view of
+// the member) as a segmented min over the pack (a wave min over a hub segment or a big member's
+// chunks, and K2's superstep-1 fold); simple members (every fold full) visited lane-parallel
+constexpr int kStepFinLanes = 1, kStepSegMin = 2, kStepSimple = 4;
+// supersteps >= kLongSteps of a long-window batch run the short-window superstep form
+// (launch_cc_step; RGPU_LONG_STEPS overrides it per launch, A/B)
+constexpr int kLongSteps = 8;
 
 // Per-batch state of the heavy-vertex path (one per batch slot).
 struct HeavyBuf {
@@ -163,6 +173,8 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
 // and reads em only for the others (K1 then runs with skip_simple)
 // edges whose bits K2 computes itself (kernels.hip edge_simple), added into *out
 void launch_count_simple(hipStream_t s, const DevGraph& g, unsigned long long* out);
+// bit e of out ((ne + 63) / 64 words): edge e is simple (edge_simple) — DevGraph.esimple
+void launch_edge_simple_bits(hipStream_t s, const DevGraph& g, uint64_t* out);
 void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
@@ -229,7 +241,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     unsigned long long* work, unsigned long long* lanechg,
                     int32_t* hbest = nullptr, const int32_t* uw_cur = nullptr, int32_t* uw_next = nullptr,
                     const ChgBits& cb = ChgBits(), int32_t* ccount = nullptr, int dense_div = 0,
-                    const int32_t* mneg = nullptr, bool cbf = false);
+                    const int32_t* mneg = nullptr, bool cbf = false, bool long_views = false);
 constexpr int kIsoWords = 64 * 64;  // isolated-member counts [64 shards][64 views]
 // DegreeRanking top-20 per view (kernels.hip k_deg_top_merge): key = in-degree << 32 | ~label
 constexpr int kTop = 20;

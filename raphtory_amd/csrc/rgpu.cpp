@@ -106,6 +106,7 @@ struct Slot {
   // state of the batch in flight
   int batch = -1, phase = 0, r_launched = 0, r_final = 0, kb = 0;
   int64_t tcut = INT64_MIN;  // the batch's window cut for time-ordered slots (start_batch)
+  bool long_views = false;  // every window of the batch >= long_ratio x its hop span (launch_cc_step)
   uint64_t evseq = 0;  // order in which slot events were recorded (wait on the oldest)
 };
 
@@ -261,6 +262,9 @@ struct rgpu_ctx {
   int64_t k1_last = INT64_MIN;          // INT64_MIN: no carry to read
   bool k1_carry = true;
   bool cbf = false;                     // RGPU_CBF: the superstep probes a neighbour's changed bit first (A/B)
+  // RGPU_LONG_RATIO (read per run; default 4, < 0: never): a batch whose every window is at least
+  // this many times its hop span runs the long-window superstep form (Slot::long_views)
+  int long_ratio = 4;
   int grp_last[kMaxPlanes] = {};        // supersteps of the last batch of each window group
   // last run: views (hop, win) -> batch (hop/K)*G + win/gsize, lane (win%gsize)*K + hop%K
   int algo = -1, K = 0, W = 0, G = 1, gsize = 1;
@@ -697,7 +701,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
                      s.act[(r + 2) % 3], s.stepcnt, s.d_hostflag,
                      work_buf(c, s), s.stats + kLaneOff,
                      hv ? s.hv.best : nullptr, s.uw[(r - 1) & 1], s.uw[r & 1],
-                     chg_bits(c, s, r), s.ccount, dense_div(c), min_labels(c, s), c->cbf);
+                     chg_bits(c, s, r), s.ccount, dense_div(c), min_labels(c, s), c->cbf, s.long_views);
     }, r, per_launch);
     if (hv)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
@@ -854,6 +858,17 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     if (thr < INT64_MAX / 4 && hmin > INT64_MIN / 4) tcut = hmin - thr;
   }
   s.tcut = tcut;
+  {  // long views: the batch's views nearly coincide (the lane-parallel superstep forms pay)
+    const int w0 = rc.G == 1 ? 0 : grp * rc.gsize, w1 = rc.G == 1 ? rc.W : w0 + rc.gsize;
+    int64_t wmin = INT64_MAX, hmin = INT64_MAX, hmax = INT64_MIN;
+    for (int w = w0; w < w1; w++) wmin = std::min(wmin, rc.thr_e[w]);
+    for (int k = 0; k < bp.K; k++) {
+      hmin = std::min(hmin, bp.hop[k]);
+      hmax = std::max(hmax, bp.hop[k]);
+    }
+    const int64_t span = std::max<int64_t>(hmax - hmin, 1);
+    s.long_views = c->long_ratio >= 0 && wmin / span >= c->long_ratio;
+  }
   s.batch = b;
   s.kb = bp.K;
   s.r_launched = 0;
@@ -1127,8 +1142,9 @@ void harvest(rgpu_ctx* c, int si, const RunCfg& rc) {
         const double mem = (double)wsum(1, 0);
         c->st.kernel_bytes[KID_SLOTS] += 12.0 * ((double)c->g.nv - mem) + 52.0 * mem +
                                          // per static slot: slot words (ts_e 4 + ts_nb 4 + ts_t 8, or the
-                                         // CSR's 8), em[e] 8 unless inline (slot_bits), vm[nb] 8
-                                         ((c->g.ts_e ? 32.0 : 24.0) - (s.iem ? 8.0 : 0.0)) * (double)wsum(1, 4) +
+                                         // CSR's 8), em[e] 8 unless inline (slot_bits: then neither em[e]
+                                         // nor ts_e is read for a simple slot), vm[nb] 8
+                                         ((c->g.ts_e ? 32.0 : 24.0) - (s.iem ? 12.0 : 0.0)) * (double)wsum(1, 4) +
                                          12.0 * (double)wsum(1, 1) +
                                          4.0 * (double)wsum(1, 7) + 64.0 * (double)wsum(1, 6);
       }
@@ -1681,7 +1697,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
                    s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
                    work_buf(c, s), s.stats + kLaneOff, hv ? s.hv.best : nullptr,
                    s.uw[r & 1], s.uw[n & 1], chg_bits(c, s, n), s.ccount,
-                   dense_div(c), min_labels(c, s), c->cbf);
+                   dense_div(c), min_labels(c, s), c->cbf, s.long_views);
   }, n);
   part_post_step(c, si, rc, n);
 }
@@ -2317,6 +2333,13 @@ void build_tslots(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L) {
     g.ts_e = e;
     g.ts_nb = nb;
     g.ts_t = t;
+    // the simple-edge bitmap (K1's SKIP form reads one word per 64 edges instead of testing each
+    // edge's history and endpoints every batch)
+    uint64_t* es = dalloc<uint64_t>(L, (g.ne + 63) / 64 + 1);
+    launch_edge_simple_bits(nullptr, g, es);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    g.esimple = es;
   }
 }
 
@@ -3171,6 +3194,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   c->k1_carry = env_int("RGPU_K1_CARRY", 1) != 0;
   c->cbf = env_int("RGPU_CBF", 0) != 0;
+  c->long_ratio = env_int("RGPU_LONG_RATIO", 4);
   try {
     HIPCHK(hipSetDevice(c->device));
     apply_pending(c);  // a run sees every seal that finished before it started

@@ -121,7 +121,8 @@ __device__ __forceinline__ int hop_lb_search(const HopLDS& L, int64_t x) {
 __device__ __forceinline__ uint64_t simple_bits(const HopLDS& L, int sorted, int64_t tf) {
   uint64_t m[1] = {0};
   if (sorted) {  // hops [first >= tf, first > tf + w) of each window
-    const int a = hop_lb_search(L, tf);
+    // (a point before the block's first hop — most slots of a long window — needs no search)
+    const int a = tf <= L.hop[0] ? 0 : hop_lb_search(L, tf);
     const int64_t tlast = L.hop[L.K - 1];
     for (int w = 0; w < L.W; w++) {  // (a window reaching past the last hop: no search, no overflow)
       const int u = L.thr[w] >= tlast - tf ? L.K : hop_lb_search(L, tf + L.thr[w] + 1);
