@@ -732,13 +732,78 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
         }
       }
+      // lane = member of the pack: the first slot lane of its span (exclusive prefix of the counts)
+      const bool inpk = (pack >> lane) & 1;
+      const int32_t nin = inpk ? neff : 0;
+      int32_t prel = nin;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t y = __shfl_up(prel, d);
+        if (lane >= d) prel += y;
+      }
+      prel -= nin;
+      // Simple members (lane = member; one partition, uniform words): every kept slot full.  Their
+      // superstep-1 label is min(own id, span minimum) on all their views, so the words, counts,
+      // change word and the step-2 frontier marks are written lane = member, exactly as the member
+      // loop below writes them; only the view minima (wmin) take a short loop.
+      uint64_t simple = 0;
+      if (!PART && uw0 && uw1 && (kopts & kStepSegMin) && (kopts & kStepSimple)) {
+        const uint64_t spanl = nin == 0 ? 0ull : ((nin >= 64 ? ~0ull : ((1ull << nin) - 1)) << prel);
+        const uint64_t keptl = bal & spanl;
+        const int32_t fml = __shfl(fmin, nin > 0 ? prel + nin - 1 : 0);
+        const int32_t fL = nin > 0 ? fml : INT32_MAX;
+        const int64_t vme = dealt_item(wave, nwaves, r, G, lane);
+        const bool sl = inpk && vme < n_own && mel != INT32_MAX && (keptl & ~fullb) == 0;
+        simple = __ballot(sl);
+        if (simple) {
+          uint64_t chl = 0;
+          if (sl) {
+            const int32_t best1 = min(mel, fL);
+            chl = best1 < mel ? mvl : 0;
+            uw0[vme] = mel;
+            uw1[vme] = uw_word(best1, chl != 0);
+            cnt[vme] = __popcll(keptl);
+            vadj[vme] = fL != INT32_MAX ? mvl : 0;
+            chg1[vme] = chl;
+            if (chl && cb1) atomicOr((unsigned long long*)&cb1[vme >> 6], 1ull << (vme & 63));
+            if (chl && !dense1) act2[vme] = 1;
+          }
+          const uint64_t chb = __ballot(chl != 0);
+          if (chb) {
+            changed += __popcll(chb);
+            uint64_t o = chl;
+            for (int d = 32; d > 0; d >>= 1) o |= shfl_xor64(o, d);
+            lanes |= o;
+            if (!dense1) {  // neighbours across a kept slot of a changed simple member
+              const uint64_t chm = ((uint64_t)(uint32_t)__shfl((int)(chl >> 32), myL) << 32) |
+                                   (uint32_t)__shfl((int)chl, myL);
+              if (on && (m & chm)) act2[nb] = 1;
+            }
+          }
+          for (uint64_t t = simple; t; t &= t - 1) {  // the views' minimum own label (lane = view)
+            const int Ls = __builtin_ctzll(t);
+            if ((readlane64(mvl, Ls) >> lane) & 1) wmin = min(wmin, __builtin_amdgcn_readlane(mel, Ls));
+          }
+          if constexpr (PROF) {
+            unsigned long long a2 = sl ? (unsigned long long)__popcll(keptl) : 0ull, s2 = sl ? (unsigned long long)nin : 0ull;
+            for (int d = 32; d > 0; d >>= 1) {
+              a2 += __shfl_xor(a2, d);
+              s2 += __shfl_xor(s2, d);
+            }
+            members += (unsigned long long)__popcll(simple);
+            alive += a2;
+            scanned += s2;
+            uwn += 2ull * __popcll(simple);
+          }
+        }
+      }
       // per member of the pack: superstep 1 (lane = view) and its words
-      int pre = 0;
-      for (uint64_t pk = pack; pk; pk &= pk - 1) {
+      for (uint64_t pk = pack & ~simple; pk; pk &= pk - 1) {
         const int Lp = __builtin_ctzll(pk);
         const int n = __builtin_amdgcn_readlane(neff, Lp);
-        const uint64_t span = n == 0 ? 0ull : ((n >= 64 ? ~0ull : ((1ull << n) - 1)) << pre);
-        pre += n;
+        const int pre0 = __builtin_amdgcn_readlane(prel, Lp);
+        const uint64_t span = n == 0 ? 0ull : ((n >= 64 ? ~0ull : ((1ull << n) - 1)) << pre0);
+        const int pre = pre0 + n;  // (the span's end)
         const int64_t v = dealt_item(wave, nwaves, r, G, Lp);
         const uint64_t mv = readlane64(mvl, Lp);
         const bool own = v < n_own;
@@ -2678,7 +2743,9 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
   BatchParams b = bp;
   if (!fc || !bp.sorted) b.carry = 0;
 #define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, b, em, g.ne, ecnt, h0, g.n_own, vm_ends, \
-    vstride, g.dbits, fc, g.esimple
+    vstride, g.dbits, fc, esimple
+  const char* es = getenv("RGPU_ESIMPLE");  // (A/B: 0 tests each edge's history as before)
+  const uint64_t* esimple = (es && atoi(es) == 0) ? nullptr : g.esimple;
   const unsigned grid = grid_for(g.ne, 256);
   if (planar && ecnt) k_edge_mask<true, true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
   else if (planar && skip_simple) k_edge_mask<true, false, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
@@ -2713,7 +2780,12 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
   // the lean one-partition form held to 6 waves per SIMD (<= 80 VGPRs): C4 cc_slots 54.7 -> 53.4 ms
   // serial at 7 waves before the full-slot fold, 50.8 (7) -> 49.2 ms (6) with it
   // (profiles/r05/ab_occ_c4.jsonl, ab_k2_c4.jsonl)
-  if (!work && iem && !(gpeer && pmask)) kern = k_cc_slots<false, true, false, 6>;
+  if (!work && iem && !(gpeer && pmask)) {
+    const char* w = getenv("RGPU_SLOTS_WPE");  // (A/B)
+    const int wp = w ? atoi(w) : 6;
+    kern = wp == 4 ? k_cc_slots<false, true, false, 1>
+                   : (wp == 5 ? k_cc_slots<false, true, false, 5> : k_cc_slots<false, true, false, 6>);
+  }
   if (!work && iem && gpeer && pmask) kern = k_cc_slots<false, true, true, 6>;  // (86 VGPRs unheld)
   BatchParams bp0;
   if (!iem) std::memset(&bp0, 0, sizeof(bp0));
