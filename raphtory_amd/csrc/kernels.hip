@@ -732,78 +732,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
         }
       }
-      // lane = member of the pack: the first slot lane of its span (exclusive prefix of the counts)
-      const bool inpk = (pack >> lane) & 1;
-      const int32_t nin = inpk ? neff : 0;
-      int32_t prel = nin;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int32_t y = __shfl_up(prel, d);
-        if (lane >= d) prel += y;
-      }
-      prel -= nin;
-      // Simple members (lane = member; one partition, uniform words): every kept slot full.  Their
-      // superstep-1 label is min(own id, span minimum) on all their views, so the words, counts,
-      // change word and the step-2 frontier marks are written lane = member, exactly as the member
-      // loop below writes them; only the view minima (wmin) take a short loop.
-      uint64_t simple = 0;
-      if (!PART && uw0 && uw1 && (kopts & kStepSegMin) && (kopts & kStepSimple)) {
-        const uint64_t spanl = nin == 0 ? 0ull : ((nin >= 64 ? ~0ull : ((1ull << nin) - 1)) << prel);
-        const uint64_t keptl = bal & spanl;
-        const int32_t fml = __shfl(fmin, nin > 0 ? prel + nin - 1 : 0);
-        const int32_t fL = nin > 0 ? fml : INT32_MAX;
-        const int64_t vme = dealt_item(wave, nwaves, r, G, lane);
-        const bool sl = inpk && vme < n_own && mel != INT32_MAX && (keptl & ~fullb) == 0;
-        simple = __ballot(sl);
-        if (simple) {
-          uint64_t chl = 0;
-          if (sl) {
-            const int32_t best1 = min(mel, fL);
-            chl = best1 < mel ? mvl : 0;
-            uw0[vme] = mel;
-            uw1[vme] = uw_word(best1, chl != 0);
-            cnt[vme] = __popcll(keptl);
-            vadj[vme] = fL != INT32_MAX ? mvl : 0;
-            chg1[vme] = chl;
-            if (chl && cb1) atomicOr((unsigned long long*)&cb1[vme >> 6], 1ull << (vme & 63));
-            if (chl && !dense1) act2[vme] = 1;
-          }
-          const uint64_t chb = __ballot(chl != 0);
-          if (chb) {
-            changed += __popcll(chb);
-            uint64_t o = chl;
-            for (int d = 32; d > 0; d >>= 1) o |= shfl_xor64(o, d);
-            lanes |= o;
-            if (!dense1) {  // neighbours across a kept slot of a changed simple member
-              const uint64_t chm = ((uint64_t)(uint32_t)__shfl((int)(chl >> 32), myL) << 32) |
-                                   (uint32_t)__shfl((int)chl, myL);
-              if (on && (m & chm)) act2[nb] = 1;
-            }
-          }
-          for (uint64_t t = simple; t; t &= t - 1) {  // the views' minimum own label (lane = view)
-            const int Ls = __builtin_ctzll(t);
-            if ((readlane64(mvl, Ls) >> lane) & 1) wmin = min(wmin, __builtin_amdgcn_readlane(mel, Ls));
-          }
-          if constexpr (PROF) {
-            unsigned long long a2 = sl ? (unsigned long long)__popcll(keptl) : 0ull, s2 = sl ? (unsigned long long)nin : 0ull;
-            for (int d = 32; d > 0; d >>= 1) {
-              a2 += __shfl_xor(a2, d);
-              s2 += __shfl_xor(s2, d);
-            }
-            members += (unsigned long long)__popcll(simple);
-            alive += a2;
-            scanned += s2;
-            uwn += 2ull * __popcll(simple);
-          }
-        }
-      }
       // per member of the pack: superstep 1 (lane = view) and its words
-      for (uint64_t pk = pack & ~simple; pk; pk &= pk - 1) {
+      int pre = 0;
+      for (uint64_t pk = pack; pk; pk &= pk - 1) {
         const int Lp = __builtin_ctzll(pk);
         const int n = __builtin_amdgcn_readlane(neff, Lp);
-        const int pre0 = __builtin_amdgcn_readlane(prel, Lp);
-        const uint64_t span = n == 0 ? 0ull : ((n >= 64 ? ~0ull : ((1ull << n) - 1)) << pre0);
-        const int pre = pre0 + n;  // (the span's end)
+        const uint64_t span = n == 0 ? 0ull : ((n >= 64 ? ~0ull : ((1ull << n) - 1)) << pre);
+        pre += n;
         const int64_t v = dealt_item(wave, nwaves, r, G, Lp);
         const uint64_t mv = readlane64(mvl, Lp);
         const bool own = v < n_own;
@@ -2768,7 +2703,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
                      unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends,
                      int32_t* ccount, const BatchParams* ebp, int dense_div, int32_t* mneg,
-                     const uint8_t* gpeer, uint8_t* pmask) {
+                     const uint8_t* gpeer, uint8_t* pmask, bool long_views) {
   const bool hv = g.n_seg > 0;
   const bool iem = ebp != nullptr && g.ts_t != nullptr;
   // (partitioned: the peer masks; gpeer and pmask both set)
@@ -2780,12 +2715,8 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
   // the lean one-partition form held to 6 waves per SIMD (<= 80 VGPRs): C4 cc_slots 54.7 -> 53.4 ms
   // serial at 7 waves before the full-slot fold, 50.8 (7) -> 49.2 ms (6) with it
   // (profiles/r05/ab_occ_c4.jsonl, ab_k2_c4.jsonl)
-  if (!work && iem && !(gpeer && pmask)) {
-    const char* w = getenv("RGPU_SLOTS_WPE");  // (A/B)
-    const int wp = w ? atoi(w) : 6;
-    kern = wp == 4 ? k_cc_slots<false, true, false, 1>
-                   : (wp == 5 ? k_cc_slots<false, true, false, 5> : k_cc_slots<false, true, false, 6>);
-  }
+  if (!work && iem && !(gpeer && pmask)) kern = k_cc_slots<false, true, false, 6>;
+  (void)long_views;  // (a lane-parallel K2 for long windows measured no gain: DESIGN.md §4h)
   if (!work && iem && gpeer && pmask) kern = k_cc_slots<false, true, true, 6>;  // (86 VGPRs unheld)
   BatchParams bp0;
   if (!iem) std::memset(&bp0, 0, sizeof(bp0));
@@ -2865,8 +2796,10 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
 }
 // segments per wave and round of the hub kernels' prologue (kernels.hpp kHubPro; RGPU_HUB_PRO)
 // (read per launch, as tools/ab.py flips it in-process)
-static int hub_pro() {
-  const char* e = getenv("RGPU_HUB_PRO");
+static int hub_pro(bool early = false) {
+  // (early: a busy superstep of a long-window batch, where the segments are mostly active and
+  // fewer per wave means more of them in flight; RGPU_HUB_PRO_EARLY, A/B)
+  const char* e = getenv(early ? "RGPU_HUB_PRO_EARLY" : "RGPU_HUB_PRO");
   const int v = e ? atoi(e) : kHubPro;
   return v < 1 ? 1 : (v > 64 ? 64 : v);
 }
@@ -2874,14 +2807,15 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur,
                          const uint64_t* cb_prev, const int32_t* ccount, int dense_div, unsigned long long* work,
-                         const uint64_t* vm, const int32_t* mneg) {
+                         const uint64_t* vm, const int32_t* mneg, bool early) {
   if (g.n_seg <= 0) return;
   // held to 6 waves per SIMD (<= 80 VGPRs; unconstrained it takes 103, 4 waves): C4 heavy 48.6 ->
   // 47.7 ms serial (profiles/r05/ab_occ_c4.jsonl)
-  k_heavy_gather<6><<<grid_for(g.n_seg, 4 * hub_pro(), 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
+  const int pro = hub_pro(early);
+  k_heavy_gather<6><<<grid_for(g.n_seg, 4 * pro, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
                                                              hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
-                                                             g.n_own, work, vm, mneg, hub_pro(), step_opts());
+                                                             g.n_own, work, vm, mneg, pro, step_opts());
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,

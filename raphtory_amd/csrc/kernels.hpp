@@ -182,7 +182,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      unsigned long long* lanechg, int32_t* uw0 = nullptr, int32_t* uw1 = nullptr,
                      uint64_t* cb1 = nullptr, bool ends = false, int32_t* ccount = nullptr,
                      const BatchParams* ebp = nullptr, int dense_div = 0, int32_t* mneg = nullptr,
-                     const uint8_t* gpeer = nullptr, uint8_t* pmask = nullptr);
+                     const uint8_t* gpeer = nullptr, uint8_t* pmask = nullptr, bool long_views = false);
 // (partitioned: gpeer[g - n_own] = the partition owning ghost g; pmask[v] = the peers owning a ghost
 // neighbour of owned v across a kept slot of the batch, every peer for a hub)
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
@@ -197,7 +197,7 @@ void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, 
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr,
                          const uint64_t* cb_prev = nullptr, const int32_t* ccount = nullptr, int dense_div = 0,
                          unsigned long long* work = nullptr, const uint64_t* vm = nullptr,
-                         const int32_t* mneg = nullptr);
+                         const int32_t* mneg = nullptr, bool early = false);
 // vm/em (partitioned mode): heavy ghosts (ranks >= n_own) have no compacted slots; their kept
 // slots are recomputed from the static adjacency (em & vm[nb] & vm[v]) while marking
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,

@@ -693,7 +693,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[(r - 1) & 1], s.chg[(r - 1) & 1], s.act[r % 3],
                             s.stepcnt, r, s.hv, s.uw[(r - 1) & 1], chg_bits(c, s, r).prev, s.ccount,
-                            dense_div(c), work_buf(c, s), s.vm, min_labels(c, s));
+                            dense_div(c), work_buf(c, s), s.vm, min_labels(c, s), s.long_views && r < kLongSteps);
       }, r, per_launch);
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
@@ -1025,7 +1025,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
                       work_buf(c, s), s.hv, s.stats + kLaneOff, s.uw[0],
                       s.uw[1], chg_bits(c, s, 1).next, ends, s.ccount, iem ? &ebp : nullptr,
                       dense_div(c), min_labels(c, s), c->partitioned ? c->pt.gpeer : nullptr,
-                      c->partitioned ? c->pt.xs[si].pmask : nullptr);
+                      c->partitioned ? c->pt.xs[si].pmask : nullptr, s.long_views);
     });
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
@@ -1690,7 +1690,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[n % 3], s.stepcnt, n, s.hv,
                           s.uw[r & 1], chg_bits(c, s, n).prev, s.ccount, dense_div(c), work_buf(c, s), s.vm,
-                          min_labels(c, s));
+                          min_labels(c, s), s.long_views && n < kLongSteps);
     });
   timed_launch(c, si, KID_STEP, 0.0, [&] {
     launch_cc_step(s.stream, n, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[r & 1], s.lab[n & 1], s.chg[r & 1],
