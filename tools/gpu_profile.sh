@@ -13,12 +13,15 @@ run() { local name=$1 secs=$2; shift 2; echo "=== $name"; timeout -k 10 "$secs" 
 if [ -z "${SKIP_BENCH:-}" ]; then
   run bench 600 python bench.py ${BENCH_ARGS:-}
   grep '^{' $O/bench.log > $O/bench.json || true
-  run prof_only 300 python bench.py --profile-only ${BENCH_ARGS:-}
-  grep '^{' $O/prof_only.log > $O/prof_only.json || true
+  if [ -z "${SKIP_PROF_ONLY:-}" ]; then
+    run prof_only 300 python bench.py --profile-only ${BENCH_ARGS:-}
+    grep '^{' $O/prof_only.log > $O/prof_only.json || true
+  fi
 fi
-run kt ${STEP_SECS:-600} rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
-run fetch ${STEP_SECS:-600} rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $O/fetch -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
-run write ${STEP_SECS:-600} rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O/write -o run --output-format csv -- python3 bench.py --profile-only ${BENCH_ARGS:-}
+[ -z "${SKIP_KT:-}" ] && run kt ${STEP_SECS:-600} rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py --profile-only ${PROF_ARGS---lean-pass-only} ${BENCH_ARGS:-}
+[ -n "${SKIP_PMC:-}" ] && exit 0
+run fetch ${STEP_SECS:-600} rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $O/fetch -o run --output-format csv -- python3 bench.py --profile-only ${PROF_ARGS---lean-pass-only} ${BENCH_ARGS:-}
+run write ${STEP_SECS:-600} rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O/write -o run --output-format csv -- python3 bench.py --profile-only ${PROF_ARGS---lean-pass-only} ${BENCH_ARGS:-}
 python3 - "$K" <<'PY'
 import csv, glob, json, sys
 k = sys.argv[1]
