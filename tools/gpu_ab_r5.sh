@@ -1,4 +1,2 @@
-# round-5 GPU check: parity suites, then a same-box A/B (hub prologue width in early long-window steps)
-mkdir -p gpurun_out && timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_batch_modes.py tests/test_gpu_heavy.py tests/test_gpu_parity.py tests/test_gpu_partitioned.py tests/test_gpu_live.py tests/test_gpu_configs.py::test_c5_live_at_size_vs_oracle > gpurun_out/pytest_r5l.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_r5l.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 500 python -u tools/ab.py --settings "base,RGPU_HUB_PRO_EARLY=8,RGPU_HUB_PRO_EARLY=4" --rounds 2 --profile > gpurun_out/ab_hubearly_c4.jsonl 2> gpurun_out/ab_hubearly_c4.err; rc=$?; cat gpurun_out/ab_hubearly_c4.jsonl; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 400 python -u tools/c4_trace.py --lean --out gpurun_out/c4_trace_lean3.csv > gpurun_out/c4_trace_lean3.txt 2>&1; rc=$?; head -8 gpurun_out/c4_trace_lean3.txt | cut -c1-300; exit $rc
+# round-5 GPU: same-box A/B of the changed-bit probe (RGPU_CBF) on the round-5 superstep kernel
+mkdir -p gpurun_out && timeout -k 10 500 python -u tools/ab.py --settings "base,RGPU_CBF=1" --rounds 2 --profile > gpurun_out/ab_cbf2_c4.jsonl 2> gpurun_out/ab_cbf2_c4.err; rc=$?; cat gpurun_out/ab_cbf2_c4.jsonl; exit $rc
