@@ -2776,9 +2776,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
     if (lf) k_cc_step_pk<false, true, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
     else k_cc_step_pk<false, true, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
   } else if (lf) {
-    const char* lw = getenv("RGPU_LONG_WPE");  // (A/B: 5 waves per SIMD, fewer spills)
-    if (lw && atoi(lw) == 5) k_cc_step_pk<false, false, true, 5><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
-    else k_cc_step_pk<false, false, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
+    k_cc_step_pk<false, false, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
   } else {
     k_cc_step_pk<false, false, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
   }
