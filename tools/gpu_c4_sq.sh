@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/c4sq; mkdir -p $O
+O=gpurun_out/c4sq${SQ_TAG:-}; mkdir -p $O
 K=${KREGEX:-k_cc_step_pk}
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU" \
@@ -16,19 +16,20 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_IN
     python3 bench.py --profile-only --lean-pass-only --no-cpu-baseline --no-secondary > $O/p$i.log 2>&1
   rc=$?; echo "rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/p$i.log; exit $rc; }
 done
-python3 - <<'PY' | tee gpurun_out/c4sq/summary.txt
-import csv, glob, collections, json
+python3 - "$O" <<'PY' | tee $O/summary.txt
+import csv, glob, collections, json, sys
+O = sys.argv[1]
 tot = collections.defaultdict(float); n = collections.Counter()
 per = collections.defaultdict(dict)  # (pass, dispatch order) -> counter values
-for f in sorted(glob.glob("gpurun_out/c4sq/p*/**/*counter_collection.csv", recursive=True)):
-    pas = f.split("/")[2]
+for f in sorted(glob.glob(O + "/p*/**/*counter_collection.csv", recursive=True)):
+    pas = f[len(O) + 1:].split("/")[0]
     for r in csv.DictReader(open(f)):
-        k = (r["Kernel_Name"].split("(")[0], r["Counter_Name"])
+        k = (r["Kernel_Name"].split("(")[0].replace("void ", ""), r["Counter_Name"])
         tot[k] += float(r["Counter_Value"]); n[k] += 1
-        per[(pas, k[0][:40], int(r.get("Dispatch_Id", 0) or 0))][r["Counter_Name"]] = float(r["Counter_Value"])
+        per[(pas, k[0], int(r.get("Dispatch_Id", 0) or 0))][r["Counter_Name"]] = float(r["Counter_Value"])
 for k in sorted(tot):
-    print(f"{k[0][:48]:48s} {k[1]:28s} total {tot[k]:.4g}  per-dispatch {tot[k]/n[k]:.4g}  dispatches {n[k]}")
-with open("gpurun_out/c4sq/per_dispatch.jsonl", "w") as o:
+    print(f"{k[0][:56]:56s} {k[1]:28s} total {tot[k]:.4g}  per-dispatch {tot[k]/n[k]:.4g}  dispatches {n[k]}")
+with open(O + "/per_dispatch.jsonl", "w") as o:
     for key in sorted(per):
         o.write(json.dumps({"pass": key[0], "kernel": key[1], "dispatch": key[2], **per[key]}) + "\n")
 PY
