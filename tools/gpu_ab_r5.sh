@@ -1,3 +1,2 @@
-# round-5 GPU: K2 deferred member stores (RGPU_STEP_OPTS bit 8) and K2 occupancy: parity, then A/B
-mkdir -p gpurun_out && RGPU_STEP_OPTS=15 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_step_forms.py tests/test_gpu_heavy.py tests/test_gpu_parity.py tests/test_gpu_batch_modes.py tests/test_gpu_live.py > gpurun_out/pytest_k2d.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_k2d.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 500 python -u tools/ab.py --settings "base,RGPU_STEP_OPTS=15,RGPU_STEP_OPTS=15+RGPU_SLOTS_WPE=5,RGPU_SLOTS_WPE=5" --rounds 2 --profile > gpurun_out/ab_k2d_c4.jsonl 2> gpurun_out/ab_k2d_c4.err; rc=$?; cat gpurun_out/ab_k2d_c4.jsonl; exit $rc
+# round-5 GPU: a quick parity check of the final library
+mkdir -p gpurun_out && timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_step_forms.py tests/test_gpu_parity.py tests/test_gpu_heavy.py tests/test_gpu_batch_modes.py > gpurun_out/pytest_final_quick.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_final_quick.log; exit $rc
