@@ -1,2 +1,2 @@
-# round-5 GPU: a quick parity check of the final library
-mkdir -p gpurun_out && timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_step_forms.py tests/test_gpu_parity.py tests/test_gpu_heavy.py tests/test_gpu_batch_modes.py > gpurun_out/pytest_final_quick.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_final_quick.log; exit $rc
+# round-5 GPU: the dense-superstep divisor on the round-5 kernels (RGPU_DENSE; default 4)
+mkdir -p gpurun_out && timeout -k 10 600 python -u tools/ab.py --settings "base,RGPU_DENSE=2,RGPU_DENSE=8,RGPU_DENSE=16" --rounds 2 --profile > gpurun_out/ab_dense_r5.jsonl 2> gpurun_out/ab_dense_r5.err; rc=$?; cat gpurun_out/ab_dense_r5.jsonl; exit $rc
