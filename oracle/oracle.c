@@ -525,7 +525,7 @@ int orc_alive(const orc_graph* g, int is_edge, int64_t src, int64_t dst, int64_t
 typedef struct {
   int nwin;
   int64_t w[64];
-  int canon[64]; /* comp keys / job ids are name+t+w (VertexVisitor.scala:81-96, WindowLens.scala:160):
+  int canon[64]; /* comp keys / job ids are name+t+w (VertexVisitor.scala:81-96, WindowLens.scala:52):
                     equal window values share state */
 } WinSet;
 
@@ -541,8 +541,8 @@ static int winset_init(WinSet* ws, const int64_t* windows, int nw) {
   return 0;
 }
 
-/* Lens key sets: new WindowLens(t, w0) filters every vertex (WindowLens.scala:131-132), then
- * shrinkWindow(w_i) filters the running key set (:167-173).  mem[i*nv + v]. */
+/* Lens key sets: new WindowLens(t, w0) filters every vertex (WindowLens.scala:23-24), then
+ * shrinkWindow(w_i) filters the running key set (WindowLens.scala:59-65).  mem[i*nv + v]. */
 static void build_keysets(const orc_graph* g, int64_t t, const WinSet* ws, uint8_t* mem) {
   size_t nv = g->nv;
   for (size_t v = 0; v < nv; v++) mem[v] = (uint8_t)ent_alive(&g->vs[v].e, t, ws->w[0]);
@@ -647,7 +647,7 @@ int orc_cc(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int ma
       for (int i = 0; i < nwin; i++) {
         int c = ws.canon[i];
         size_t qb = ((size_t)(s % 2) * nwin + c) * nv;
-        /* getVerticesWithMessages, WindowLens.scala:149-158 */
+        /* getVerticesWithMessages, WindowLens.scala:41-50 */
         int nl = 0;
         for (size_t v = 0; v < nv; v++)
           if (mem[(size_t)i * nv + v] && qcnt[qb + v] > 0) list[nl++] = (int)v;
@@ -665,7 +665,7 @@ int orc_cc(const orc_graph* g, int64_t t, const int64_t* windows, int nw, int ma
         }
       }
       *steps = s;
-      /* AnalysisTask.endStep :208-225, WindowLens.checkVotes :175-176 */
+      /* AnalysisTask.endStep :208-225, WindowLens.checkVotes WindowLens.scala:67-68 */
       if (s == max_steps || totalKeys == votes) break;
     }
   }
@@ -802,7 +802,7 @@ done:
 /* ------------------------------------------------------------ diffusion */
 /* BinaryDefusion.scala:9-51 run through the reference's BSP: Setup (superstep 0, only when
  * maxSteps > 1, AnalysisTask.scala:169), then per superstep s the vertices with messages
- * (getVerticesWithMessages, WindowLens.scala:149-158) clear their queue; an infected one
+ * (getVerticesWithMessages, WindowLens.scala:41-50) clear their queue; an infected one
  * votes to halt (:27-28), a new one records infected = s and messages every out-neighbour
  * (outgoingProcessing after viewAtWithWindow, VertexVisitor.scala:32) on a coin flip (:31-33);
  * halt at s == maxSteps or when every message holder voted (AnalysisTask.endStep :208-225).
@@ -979,7 +979,7 @@ int orc_vertex_program(const orc_graph* g, int64_t t, const int64_t* windows, in
         int c = ws.canon[i];
         size_t qb = ((size_t)(s % 2) * nwin + c) * nv;
         int nl = 0;
-        for (size_t v = 0; v < nv; v++) /* getVerticesWithMessages, WindowLens.scala:149-158 */
+        for (size_t v = 0; v < nv; v++) /* getVerticesWithMessages, WindowLens.scala:41-50 */
           if (mem[(size_t)i * nv + v] && qc[qb + v] > 0) list[nl++] = (int)v;
         totalKeys += nl;
         for (int a = 0; a < nl; a++) {

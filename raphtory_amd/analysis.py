@@ -490,7 +490,7 @@ class BWindowedViewAnalysisTask(ViewAnalysisTask):
 
 
 class RangeAnalysisTask(AnalysisTask):
-    """RangeTasks/RangeAnalysisTask.scala:51-78"""
+    """RangeTasks/RangeAnalysisTask.scala:12-39 (restart :18-35)"""
 
     def __init__(self, graphs, analyser, start: int, end: int, jump: int, **kw):
         super().__init__(graphs, analyser, **kw)

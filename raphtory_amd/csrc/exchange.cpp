@@ -51,7 +51,8 @@ void check_dev_range(const void* p, size_t bytes, const char* what, int rank, in
 }
 
 const char kLoopMagic[8] = {'R', 'G', 'P', 'U', 'L', 'O', 'O', 'P'};
-const char kShmMagic[8] = {'R', 'G', 'P', 'U', 'S', 'H', 'M', '1'};
+// (version 2: ShmCtl gained `broken` in front of size[]; a process of another layout cannot attach)
+const char kShmMagic[8] = {'R', 'G', 'P', 'U', 'S', 'H', 'M', '2'};
 
 // ------------------------------------------------------------------ RCCL
 class RcclExchange : public Exchange {

@@ -5,7 +5,7 @@
 // one pass over the adjacency serves every view of every hop in the batch.
 //
 //   k_vertex_mask  K1  Entity.aliveAtWithWindow for every vertex x hop x window, with the
-//                      batched running-min window (WindowLens.shrinkWindow, WindowLens.scala:167-173)
+//                      batched running-min window (WindowLens.shrinkWindow, WindowLens.scala:59-65)
 //   k_edge_mask    K1  the same for edges: own history + endpoint death lists (killList)
 //   k_cc_slots     K2  per-view adjacency filter (Vertex.viewAtWithWindow, Vertex.scala:70-74)
 //                      compacted into a batch CSR with a 64-bit view mask per slot
@@ -565,7 +565,7 @@ struct NoWork {
 //   em[e] & vm[nbr] & vm[v]  != 0
 // i.e. the edge is alive in the view's own window AND both endpoints are in the view's
 // (running-min) vertex set — messages to vertices outside the lens are never read
-// (WindowLens.getVerticesWithMessages, WindowLens.scala:149-158).  Self-loops only
+// (WindowLens.getVerticesWithMessages, WindowLens.scala:41-50).  Self-loops only
 // message the vertex itself and never change a label: dropped.
 //
 // Setup (ConnectedComponents.setup :10-17) sends every member's own id, so superstep 1 needs
@@ -1374,8 +1374,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                                     const int32_t* __restrict__ uw_cur, int32_t* __restrict__ uw_next,
                                                     uint64_t* __restrict__ cb_next, uint64_t* __restrict__ cb_clear,
                                                     int64_t cb_words, int32_t* __restrict__ ccount, int dense_div, int gmax,
-                                                    const int32_t* __restrict__ mneg, const uint64_t* __restrict__ cb_prev,
-                                                    int opts_in) {
+                                                    const int32_t* __restrict__ mneg, int opts_in) {
   if (stepflag[step - 1] == 0) return;
   // LONG (a batch of long windows, launch_cc_step): the lane-parallel forms (RGPU_STEP_OPTS) are
   // compiled in; the short-window form is the round-4 kernel (its registers stay at 77, no spills)
@@ -1496,15 +1495,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const uint64_t m = smask[idx];
       const int32_t nbp = on ? q : 0;
       const uint64_t smp = on ? m : 0;
-      // cb_prev (RGPU_CBF): the neighbour's changed bit (one bit per vertex: an L2-resident
-      // bitmap) first; a neighbour that did not change in step r-1 contributes nothing to the
-      // fold (it still joins the next frontier below, through smp), so its word / change word (a
-      // random line each, most of them Infinity-Cache reads) is not loaded
-      const uint64_t sma = (cb_prev && smp && !((cb_prev[nbp >> 6] >> (nbp & 63)) & 1)) ? 0 : smp;
+      // (probing the neighbour's changed bit before its word measured slower twice: DESIGN.md §4c, §4h)
+      const uint64_t sma = smp;
       uint64_t act = 0;
       int32_t unp = kMixed;
       if (uw_cur) {
-        const int32_t w = (cb_prev && !sma) ? 0 : uw_cur[nbp];
+        const int32_t w = uw_cur[nbp];
         act = (w != kMixed && w < 0) ? sma : 0;
         unp = w == kMixed ? kMixed : (w & 0x7fffffff);
         const bool mx = w == kMixed && sma != 0;
@@ -2679,8 +2675,7 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
   if (!fc || !bp.sorted) b.carry = 0;
 #define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, b, em, g.ne, ecnt, h0, g.n_own, vm_ends, \
     vstride, g.dbits, fc, esimple
-  const char* es = getenv("RGPU_ESIMPLE");  // (A/B: 0 tests each edge's history as before)
-  const uint64_t* esimple = (es && atoi(es) == 0) ? nullptr : g.esimple;
+  const uint64_t* esimple = g.esimple;
   const unsigned grid = grid_for(g.ne, 256);
   if (planar && ecnt) k_edge_mask<true, true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
   else if (planar && skip_simple) k_edge_mask<true, false, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
@@ -2690,20 +2685,13 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
   else k_edge_mask<false, false, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
 #undef RGPU_EM_ARGS
 }
-// superstep kernel options (k_cc_step_pk, k_heavy_gather): RGPU_STEP_OPTS (A/B; default all) bit 0
-// kStepFinLanes, bit 1 kStepSegMin, bit 2 kStepSimple; 0 is the round-4 form.  Read per launch
-// (tools/ab.py).
-static int step_opts() {
-  const char* ov = getenv("RGPU_STEP_OPTS");
-  return ov ? atoi(ov) : (kStepFinLanes | kStepSegMin | kStepSimple);
-}
 void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,
                      int32_t* hostflag, unsigned long long* work, const HeavyBuf& hb,
                      unsigned long long* lanechg, int32_t* uw0, int32_t* uw1, uint64_t* cb1, bool ends,
                      int32_t* ccount, const BatchParams* ebp, int dense_div, int32_t* mneg,
-                     const uint8_t* gpeer, uint8_t* pmask, bool long_views) {
+                     const uint8_t* gpeer, uint8_t* pmask, const KernOpts& ko) {
   const bool hv = g.n_seg > 0;
   const bool iem = ebp != nullptr && g.ts_t != nullptr;
   // (partitioned: the peer masks; gpeer and pmask both set)
@@ -2716,7 +2704,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
   // serial at 7 waves before the full-slot fold, 50.8 (7) -> 49.2 ms (6) with it
   // (profiles/r05/ab_occ_c4.jsonl, ab_k2_c4.jsonl)
   if (!work && iem && !(gpeer && pmask)) kern = k_cc_slots<false, true, false, 6>;
-  (void)long_views;  // (a lane-parallel K2 for long windows measured no gain: DESIGN.md §4h)
+  // (a lane-parallel K2 for long windows measured no gain: DESIGN.md §4h)
   if (!work && iem && gpeer && pmask) kern = k_cc_slots<false, true, true, 6>;  // (86 VGPRs unheld)
   BatchParams bp0;
   if (!iem) std::memset(&bp0, 0, sizeof(bp0));
@@ -2726,7 +2714,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                                                 hb.segcnt, hb.segor, hb.best, lanechg, g.ts_e, g.ts_nb, g.ts_t, tcut,
                                                 uw0, uw1, cb1, ends ? 1 : 0, ccount, kDealSlots, iem ? *ebp : bp0,
                                                 dense_div > 0 && (dense_div & kDense1) && ccount ? 1 : 0,
-                                                g.ts_g, mneg, gpeer, pmask, step_opts());
+                                                g.ts_g, mneg, gpeer, pmask, ko.step);
 }
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab) {
   k_uw_rows<<<grid_for(nv, 256), 256, 0, s>>>(nv, vm, uw, lab);
@@ -2749,8 +2737,8 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     uint64_t* chg_next, const uint8_t* act_cur, uint8_t* act_next,
                     uint8_t* act_clear, int32_t* stepflag, int32_t* hostflag,
                     unsigned long long* work, unsigned long long* lanechg, int32_t* hbest, const int32_t* uw_cur, int32_t* uw_next,
-                    const ChgBits& cb, int32_t* ccount, int dense_div, const int32_t* mneg, bool cbf,
-                    bool long_views) {
+                    const ChgBits& cb, int32_t* ccount, int dense_div, const int32_t* mneg, bool long_views,
+                    const KernOpts& ko) {
   // late supersteps have small frontiers: a smaller grid leaves the GPU to the other batches.
   // A small graph's dense supersteps are latency-bound and share the GPU with the other batch
   // slots too: a 1,024-block cap measured 4 % faster on C2 (100k vertices) and 2 % slower on a
@@ -2763,15 +2751,13 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
   // C4 serial cc_step 207.6 -> 155.1 ms, query 343 -> 286 ms.
 #define RGPU_PK_ARGS step, g.nv, g.adj_off, vm, cnt, snbr, smask, lab_cur, lab_next, chg_prev, chg_next, \
     act_cur, act_next, act_clear, stepflag, hostflag, work, hv_of, hbest, lanechg, uw_cur, uw_next, \
-    cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr, cbf ? cb.prev : nullptr, \
-    opts
-  const int opts = step_opts();
+    cb.next, cb.clear, cb.words, ccount, dense_div, kDealSlots, uw_cur ? mneg : nullptr, opts
+  const int opts = ko.step;
   const unsigned gridp = grid_for(g.nv, 256, cap);
   // The long-window form (lane-parallel members, full folds) pays in the busy early supersteps; it
   // spills a few registers, and a kernel with scratch launches its waves more slowly, which the
   // late, sparse supersteps (mostly idle waves) feel: from kLongSteps on, the short form runs.
-  const char* ls = getenv("RGPU_LONG_STEPS");
-  const bool lf = long_views && step < (ls ? atoi(ls) : kLongSteps);
+  const bool lf = long_views && step < ko.long_steps;
   if (work) {
     if (lf) k_cc_step_pk<false, true, true><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
     else k_cc_step_pk<false, true, false><<<gridp, 256, 0, s>>>(RGPU_PK_ARGS);
@@ -2784,7 +2770,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
 }
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                         int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends, unsigned long long* work,
-                        const BatchParams* ebp) {
+                        const BatchParams* ebp, const KernOpts& ko) {
   if (g.n_seg <= 0) return;
   const bool iem = ebp != nullptr && g.ts_t != nullptr;
   BatchParams bp0;
@@ -2792,42 +2778,35 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
   (iem ? k_heavy_slots<true> : k_heavy_slots<false>)<<<grid_for(g.n_seg, 4, 16384), 256, 0, s>>>(
       g.n_seg, g.seg_v, g.seg_h, g.seg_lo, g.seg_n, g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst, vm, em,
       snbr, smask, hb.segcnt, hb.segor, hb.best, g.grank, g.n_own, g.ts_e, g.ts_nb, g.ts_t, tcut, ends ? 1 : 0, work,
-      iem ? *ebp : bp0, g.ts_g, step_opts());
+      iem ? *ebp : bp0, g.ts_g, ko.step);
 }
-// segments per wave and round of the hub kernels' prologue (kernels.hpp kHubPro; RGPU_HUB_PRO)
-// (read per launch, as tools/ab.py flips it in-process)
-static int hub_pro(bool early = false) {
-  // (early: a busy superstep of a long-window batch, where the segments are mostly active and
-  // fewer per wave means more of them in flight; RGPU_HUB_PRO_EARLY, A/B)
-  const char* e = getenv(early ? "RGPU_HUB_PRO_EARLY" : "RGPU_HUB_PRO");
-  const int v = e ? atoi(e) : kHubPro;
-  return v < 1 ? 1 : (v > 64 ? 64 : v);
-}
+// segments per wave and round of the hub kernels' prologue (kernels.hpp kHubPro, KernOpts.hub_pro)
+static int hub_pro(const KernOpts& ko) { return ko.hub_pro < 1 ? 1 : (ko.hub_pro > 64 ? 64 : ko.hub_pro); }
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur,
                          const uint64_t* cb_prev, const int32_t* ccount, int dense_div, unsigned long long* work,
-                         const uint64_t* vm, const int32_t* mneg, bool early) {
+                         const uint64_t* vm, const int32_t* mneg, const KernOpts& ko) {
   if (g.n_seg <= 0) return;
   // held to 6 waves per SIMD (<= 80 VGPRs; unconstrained it takes 103, 4 waves): C4 heavy 48.6 ->
   // 47.7 ms serial (profiles/r05/ab_occ_c4.jsonl)
-  const int pro = hub_pro(early);
+  const int pro = hub_pro(ko);
   k_heavy_gather<6><<<grid_for(g.n_seg, 4 * pro, 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_h, g.seg_lo, hb.segcnt,
                                                              snbr, smask, lab_cur, chg_prev, act_cur, stepflag,
                                                              hb.best, g.n_own, uw_cur, cb_prev, ccount, dense_div,
-                                                             g.n_own, work, vm, mneg, pro, step_opts());
+                                                             g.n_own, work, vm, mneg, pro, ko.step);
 }
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
                        const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm, const uint64_t* em,
                        int64_t tcut, const int32_t* ccount, int dense_div, unsigned long long* work,
-                       const int32_t* uw_ghost) {
+                       const int32_t* uw_ghost, const KernOpts& ko) {
   if (g.n_seg <= 0) return;
-  k_heavy_mark<<<grid_for(g.n_seg, 4 * hub_pro(), 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
+  k_heavy_mark<<<grid_for(g.n_seg, 4 * hub_pro(ko), 16384), 256, 0, s>>>(step, g.n_seg, g.seg_v, g.seg_lo, hb.segcnt, snbr, smask,
                                                            chg_now, act_cur, act_next, stepflag, g.n_own, g.seg_n,
                                                            g.out_off, g.in_off, g.adj_off, g.in_eid, g.esrc, g.edst,
                                                            vm, em, g.ts_e, g.ts_nb, g.ts_t, tcut, ccount, dense_div,
-                                                           g.n_own, work, uw_ghost, hub_pro());
+                                                           g.n_own, work, uw_ghost, hub_pro(ko));
 }
 int64_t deg_top_waves(int64_t nv) { return (int64_t)grid_for(nv, 4, 2048) * 4; }
 void launch_degree(hipStream_t s, const DevGraph& g, const uint64_t* vm, const uint64_t* em,

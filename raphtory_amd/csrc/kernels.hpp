@@ -95,17 +95,25 @@ void build_slot_labels(hipStream_t s, int64_t n, const int32_t* ts_nb, const int
 constexpr int kSegSlots = 512;
 // hub segments per wave and round in the per-superstep hub kernels (k_heavy_gather / k_heavy_mark):
 // their prologue loads that many segments' vertex, flag and count at once (lane = segment); the
-// launchers read RGPU_HUB_PRO (1..64, default kHubPro) per launch, for A/B runs (C4, profiles/r05/
-// ab_hubpro_c4.jsonl + ab_occ_c4.jsonl: heavy 64.7 ms serial at 1, 49.9 at 8, 48.3 at 16, 47.9 at 32)
+// value comes from KernOpts.hub_pro (C4, profiles/r05/ab_hubpro_c4.jsonl + ab_occ_c4.jsonl: heavy
+// 64.7 ms serial at 1, 49.9 at 8, 48.3 at 16, 47.9 at 32)
 constexpr int kHubPro = 32;
 // superstep options (k_cc_step_pk, k_heavy_gather, k_cc_slots; RGPU_STEP_OPTS, all by default):
 // members holding the final label finished lane-parallel; full folds (one label on every view of
 // the member) as a segmented min over the pack (a wave min over a hub segment or a big member's
 // chunks, and K2's superstep-1 fold); simple members (every fold full) visited lane-parallel
 constexpr int kStepFinLanes = 1, kStepSegMin = 2, kStepSimple = 4;
-// supersteps >= kLongSteps of a long-window batch run the short-window superstep form
-// (launch_cc_step; RGPU_LONG_STEPS overrides it per launch, A/B)
+// supersteps >= kLongSteps of a long-window batch run the short-window superstep form (launch_cc_step)
 constexpr int kLongSteps = 8;
+// The kernel options of one run.  rgpu_run_view_batch fills them once per run (the parity tests
+// of tests/test_gpu_step_forms.py set RGPU_STEP_OPTS / RGPU_HUB_PRO / RGPU_LONG_STEPS to run every
+// superstep form; the defaults are the measured best) and hands them to every launcher, so that a
+// run never reads the environment while it launches (loopback partitions are threads of one process).
+struct KernOpts {
+  int step = kStepFinLanes | kStepSegMin | kStepSimple;  // superstep options above
+  int hub_pro = kHubPro;                                  // hub segments per wave and round, 1..64
+  int long_steps = kLongSteps;                            // first superstep of the short form in a long batch
+};
 
 // Per-batch state of the heavy-vertex path (one per batch slot).
 struct HeavyBuf {
@@ -182,7 +190,7 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
                      unsigned long long* lanechg, int32_t* uw0 = nullptr, int32_t* uw1 = nullptr,
                      uint64_t* cb1 = nullptr, bool ends = false, int32_t* ccount = nullptr,
                      const BatchParams* ebp = nullptr, int dense_div = 0, int32_t* mneg = nullptr,
-                     const uint8_t* gpeer = nullptr, uint8_t* pmask = nullptr, bool long_views = false);
+                     const uint8_t* gpeer = nullptr, uint8_t* pmask = nullptr, const KernOpts& ko = KernOpts());
 // (partitioned: gpeer[g - n_own] = the partition owning ghost g; pmask[v] = the peers owning a ghost
 // neighbour of owned v across a kept slot of the batch, every peer for a hub)
 // heavy-vertex phases (g.n_seg > 0): K2 segment compaction + superstep-1 partial minima
@@ -191,20 +199,22 @@ void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint6
 // work (profile runs, else null): the hub kernels' work counters (kernels.hip heavy_work)
 void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                         int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends = false,
-                        unsigned long long* work = nullptr, const BatchParams* ebp = nullptr);
+                        unsigned long long* work = nullptr, const BatchParams* ebp = nullptr,
+                        const KernOpts& ko = KernOpts());
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr,
                          const uint64_t* cb_prev = nullptr, const int32_t* ccount = nullptr, int dense_div = 0,
                          unsigned long long* work = nullptr, const uint64_t* vm = nullptr,
-                         const int32_t* mneg = nullptr, bool early = false);
+                         const int32_t* mneg = nullptr, const KernOpts& ko = KernOpts());
 // vm/em (partitioned mode): heavy ghosts (ranks >= n_own) have no compacted slots; their kept
 // slots are recomputed from the static adjacency (em & vm[nb] & vm[v]) while marking
 void launch_heavy_mark(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                        const uint64_t* chg_now, uint8_t* act_next, const int32_t* stepflag, int step,
                        const HeavyBuf& hb, const uint8_t* act_cur, const uint64_t* vm = nullptr,
                        const uint64_t* em = nullptr, int64_t tcut = INT64_MIN, const int32_t* ccount = nullptr,
-                       int dense_div = 0, unsigned long long* work = nullptr, const int32_t* uw_ghost = nullptr);
+                       int dense_div = 0, unsigned long long* work = nullptr, const int32_t* uw_ghost = nullptr,
+                       const KernOpts& ko = KernOpts());
 // uniform label words (kernels.hip, kMixed): rows of the uniform vertices written into lab
 void launch_uw_rows(hipStream_t s, int64_t nv, const uint64_t* vm, const int32_t* uw, int32_t* lab);
 // component counts from the uniform words (one partition): counts = zeroed [nv][64] rows, kept
@@ -241,7 +251,7 @@ void launch_cc_step(hipStream_t s, int step, const DevGraph& g, const uint64_t* 
                     unsigned long long* work, unsigned long long* lanechg,
                     int32_t* hbest = nullptr, const int32_t* uw_cur = nullptr, int32_t* uw_next = nullptr,
                     const ChgBits& cb = ChgBits(), int32_t* ccount = nullptr, int dense_div = 0,
-                    const int32_t* mneg = nullptr, bool cbf = false, bool long_views = false);
+                    const int32_t* mneg = nullptr, bool long_views = false, const KernOpts& ko = KernOpts());
 constexpr int kIsoWords = 64 * 64;  // isolated-member counts [64 shards][64 views]
 // DegreeRanking top-20 per view (kernels.hip k_deg_top_merge): key = in-degree << 32 | ~label
 constexpr int kTop = 20;

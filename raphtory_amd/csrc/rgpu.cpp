@@ -260,8 +260,10 @@ struct rgpu_ctx {
   int32_t *k1c_v = nullptr, *k1c_e = nullptr;
   hipEvent_t k1_ev = nullptr;
   int64_t k1_last = INT64_MIN;          // INT64_MIN: no carry to read
+  bool k1_ev_live = false;              // k1_ev recorded this run: a carry K1 (read or write) waits on it
   bool k1_carry = true;
-  bool cbf = false;                     // RGPU_CBF: the superstep probes a neighbour's changed bit first (A/B)
+  bool vp_run_fsum = false;             // the last vertex-program run ran a float program
+  KernOpts ko;                          // kernel options of the run (RGPU_STEP_OPTS / _HUB_PRO / _LONG_STEPS)
   // RGPU_LONG_RATIO (read per run; default 4, < 0: never): a batch whose every window is at least
   // this many times its hop span runs the long-window superstep form (Slot::long_views)
   int long_ratio = 4;
@@ -469,6 +471,7 @@ void ensure_masks(rgpu_ctx* c, int G, int nuse) {
     HIPCHK(hipEventCreateWithFlags(&c->k1_ev, hipEventDisableTiming));
   }
   c->k1_last = INT64_MIN;  // (called once per run, before its first block)
+  c->k1_ev_live = false;
   if (G == 1) {
     for (int i = 0; i < nuse; i++) {
       Slot& s = c->slot[i];
@@ -693,7 +696,7 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[(r - 1) & 1], s.chg[(r - 1) & 1], s.act[r % 3],
                             s.stepcnt, r, s.hv, s.uw[(r - 1) & 1], chg_bits(c, s, r).prev, s.ccount,
-                            dense_div(c), work_buf(c, s), s.vm, min_labels(c, s), s.long_views && r < kLongSteps);
+                            dense_div(c), work_buf(c, s), s.vm, min_labels(c, s), c->ko);
       }, r, per_launch);
     timed_launch(c, si, KID_STEP, 0.0, [&] {
       launch_cc_step(s.stream, r, g, s.vm, s.cnt, s.snbr, s.smask, s.lab[(r - 1) & 1], s.lab[r & 1],
@@ -701,12 +704,13 @@ void launch_chunk(rgpu_ctx* c, int si, const RunCfg& rc, int n) {
                      s.act[(r + 2) % 3], s.stepcnt, s.d_hostflag,
                      work_buf(c, s), s.stats + kLaneOff,
                      hv ? s.hv.best : nullptr, s.uw[(r - 1) & 1], s.uw[r & 1],
-                     chg_bits(c, s, r), s.ccount, dense_div(c), min_labels(c, s), c->cbf, s.long_views);
+                     chg_bits(c, s, r), s.ccount, dense_div(c), min_labels(c, s), s.long_views, c->ko);
     }, r, per_launch);
     if (hv)
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[r & 1], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
-                          s.act[r % 3], nullptr, nullptr, INT64_MIN, s.ccount, dense_div(c), work_buf(c, s));
+                          s.act[r % 3], nullptr, nullptr, INT64_MIN, s.ccount, dense_div(c), work_buf(c, s),
+                          nullptr, c->ko);
       }, r, per_launch);
   }
   if (ea) {
@@ -928,7 +932,10 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
   const bool k1_runs = rc.G == 1 || grp == 0;
   if (k1_runs && c->k1_carry && c->k1c_v && bp.sorted) {
     bp.carry = c->k1_last != INT64_MIN && c->k1_last <= bp.hop[0] ? 2 : 1;
-    if (bp.carry == 2) HIPCHK(hipStreamWaitEvent(s.stream, c->k1_ev, 0));
+    // every K1 that writes the carry arrays (carry 1 or 2) is ordered after the previous carry K1
+    // of the run, which ran on another slot's stream: a write-only block after a backward hop must
+    // not overwrite floors that block is still reading or writing
+    if (c->k1_ev_live) HIPCHK(hipStreamWaitEvent(s.stream, c->k1_ev, 0));
     c->k1_last = bp.hop[bp.K - 1];
   } else if (k1_runs) {
     c->k1_last = INT64_MIN;
@@ -943,7 +950,10 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       launch_edge_mask(s.stream, g, bp, s.em, false, c->d_ecnt, (int64_t)h0, ends ? s.vm : nullptr, 0, skip_simple,
                        fce);
     });
-    if (bp.carry) HIPCHK(hipEventRecord(c->k1_ev, s.stream));
+    if (bp.carry) {
+      HIPCHK(hipEventRecord(c->k1_ev, s.stream));
+      c->k1_ev_live = true;
+    }
     if (c->partitioned) part_vm_exchange(c, si, s.vm, 0, 1, ghost_vm_free(c, rc));
   } else {
     MaskSet& M = c->mset[hb % kMaskSets];
@@ -957,7 +967,10 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
         launch_edge_mask(s.stream, g, bp, M.em, true, c->d_ecnt, (int64_t)h0, ends ? M.vm : nullptr, g.nv + kPad,
                          skip_simple, fce);
       });
-      if (bp.carry) HIPCHK(hipEventRecord(c->k1_ev, s.stream));
+      if (bp.carry) {
+        HIPCHK(hipEventRecord(c->k1_ev, s.stream));
+        c->k1_ev_live = true;
+      }
       if (c->partitioned) part_vm_exchange(c, si, M.vm, g.nv + kPad, rc.G, ghost_vm_free(c, rc));
       HIPCHK(hipEventRecord(M.k1, s.stream));
       M.pending = rc.G;
@@ -1017,7 +1030,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
       timed_launch(c, si, KID_HEAVY, 0.0,
                    [&] {
                      launch_heavy_slots(s.stream, g, tcut, s.vm, s.em, s.snbr, s.smask, s.hv, ends, work_buf(c, s),
-                                        iem ? &ebp : nullptr);
+                                        iem ? &ebp : nullptr, c->ko);
                    });
     timed_launch(c, si, KID_SLOTS, b2, [&] {  // (partitioned: owned vertices only, gk)
       launch_cc_slots(s.stream, gk, tcut, s.vm, s.em, s.cnt, s.snbr, s.smask, s.vadj, s.lab[0], s.lab[1],
@@ -1025,7 +1038,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
                       work_buf(c, s), s.hv, s.stats + kLaneOff, s.uw[0],
                       s.uw[1], chg_bits(c, s, 1).next, ends, s.ccount, iem ? &ebp : nullptr,
                       dense_div(c), min_labels(c, s), c->partitioned ? c->pt.gpeer : nullptr,
-                      c->partitioned ? c->pt.xs[si].pmask : nullptr, s.long_views);
+                      c->partitioned ? c->pt.xs[si].pmask : nullptr, c->ko);
     });
     if (c->check)
       run_check(s.stream, "after K2", [&](unsigned long long* bad) {
@@ -1035,7 +1048,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     if (g.n_seg > 0 && !c->partitioned)  // partitioned: after the step's records are in
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[1], s.act[2], s.stepcnt, 1, s.hv, nullptr, nullptr,
-                          nullptr, INT64_MIN, s.ccount, dense_div(c), work_buf(c, s));
+                          nullptr, INT64_MIN, s.ccount, dense_div(c), work_buf(c, s), nullptr, c->ko);
       });
     s.r_launched = 1;  // superstep 1 ran inside the slot kernel
     if (c->partitioned) {
@@ -1680,7 +1693,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[par], s.act[(r + 1) % 3], s.stepcnt, r, s.hv,
                         r == 1 ? nullptr : s.act[r % 3], s.vm, s.em, s.tcut, s.ccount, dense_div(c), work_buf(c, s),
-                        s.uw[par]);
+                        s.uw[par], c->ko);
     });
   HIPCHK(hipGetLastError());
   // superstep r+1 over the owned vertices
@@ -1690,14 +1703,14 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
     timed_launch(c, si, KID_HEAVY, 0.0, [&] {
       launch_heavy_gather(s.stream, g, s.snbr, s.smask, s.lab[r & 1], s.chg[r & 1], s.act[n % 3], s.stepcnt, n, s.hv,
                           s.uw[r & 1], chg_bits(c, s, n).prev, s.ccount, dense_div(c), work_buf(c, s), s.vm,
-                          min_labels(c, s), s.long_views && n < kLongSteps);
+                          min_labels(c, s), c->ko);
     });
   timed_launch(c, si, KID_STEP, 0.0, [&] {
     launch_cc_step(s.stream, n, go, s.vm, s.cnt, s.snbr, s.smask, s.lab[r & 1], s.lab[n & 1], s.chg[r & 1],
                    s.chg[n & 1], s.act[n % 3], s.act[(n + 1) % 3], s.act[(n + 2) % 3], s.stepcnt, nullptr,
                    work_buf(c, s), s.stats + kLaneOff, hv ? s.hv.best : nullptr,
                    s.uw[r & 1], s.uw[n & 1], chg_bits(c, s, n), s.ccount,
-                   dense_div(c), min_labels(c, s), c->cbf, s.long_views);
+                   dense_div(c), min_labels(c, s), s.long_views, c->ko);
   }, n);
   part_post_step(c, si, rc, n);
 }
@@ -3193,7 +3206,10 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   }
   c->dense = env_int("RGPU_DENSE", -1);  // < 0: by graph size (dense_div)
   c->k1_carry = env_int("RGPU_K1_CARRY", 1) != 0;
-  c->cbf = env_int("RGPU_CBF", 0) != 0;
+  c->ko = KernOpts();
+  c->ko.step = env_int("RGPU_STEP_OPTS", c->ko.step);
+  c->ko.hub_pro = env_int("RGPU_HUB_PRO", c->ko.hub_pro);
+  c->ko.long_steps = env_int("RGPU_LONG_STEPS", c->ko.long_steps);
   c->long_ratio = env_int("RGPU_LONG_RATIO", 4);
   try {
     HIPCHK(hipSetDevice(c->device));
@@ -3211,6 +3227,7 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
     }
     const size_t nb = rc.nb;
     c->algo = algo;
+    c->vp_run_fsum = algo == RGPU_ALGO_VP && c->vp.fsum;  // the retained states' kind (rgpu_vp_result[_f])
     c->K = rc.K;
     c->W = rc.W;
     c->G = rc.G;
@@ -3552,10 +3569,19 @@ int rgpu_set_vertex_program(rgpu_ctx* c, const rgpu_vertex_program_t* p) {
   return RGPU_OK;
 }
 
+static int vp_result_rows(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int64_t* values, size_t cap, size_t* n);
+
 int rgpu_vp_result(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int64_t* values, size_t cap, size_t* n) {
   if (!c || !n) return RGPU_EINVAL;
   std::lock_guard<std::mutex> lk(c->mu);
   if (c->algo != RGPU_ALGO_VP || !c->retained) return fail(c, RGPU_ESTATE, "needs a vertex-program run with RGPU_RUN_RETAIN");
+  // the kind of the program the retained run ran (not the one set since): int64 states here
+  if (c->vp_run_fsum) return fail(c, RGPU_ESTATE, "the last vertex-program run was a float program (rgpu_vp_result_f)");
+  return vp_result_rows(c, hop, win, ids, values, cap, n);
+}
+
+// (caller holds mu; the run's program kind checked)
+static int vp_result_rows(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, int64_t* values, size_t cap, size_t* n) {
   size_t b;
   int j;
   if (int e = view_index(c, hop, win, &b, &j)) return e;
@@ -3596,12 +3622,11 @@ int rgpu_set_vertex_program_f(rgpu_ctx* c, const rgpu_vertex_program_f_t* p) {
 
 int rgpu_vp_result_f(rgpu_ctx* c, size_t hop, size_t win, int64_t* ids, double* values, size_t cap, size_t* n) {
   if (!c || !n) return RGPU_EINVAL;
-  {
-    std::lock_guard<std::mutex> lk(c->mu);
-    if (!c->vp.fsum) return fail(c, RGPU_ESTATE, "the vertex program is not a float program");
-  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->algo != RGPU_ALGO_VP || !c->retained) return fail(c, RGPU_ESTATE, "needs a vertex-program run with RGPU_RUN_RETAIN");
+  if (!c->vp_run_fsum) return fail(c, RGPU_ESTATE, "the last vertex-program run was not a float program");
   static_assert(sizeof(double) == sizeof(int64_t), "state rows hold double bits");
-  return rgpu_vp_result(c, hop, win, ids, reinterpret_cast<int64_t*>(values), cap, n);
+  return vp_result_rows(c, hop, win, ids, reinterpret_cast<int64_t*>(values), cap, n);
 }
 
 int rgpu_vp_supersteps(rgpu_ctx* c, size_t hop, int64_t* supersteps) {

@@ -142,7 +142,7 @@ def _dtoa(bin_exp: int, fract_bits: int, n_sig: int):
             else:  # m overflowed: it is certainly > b, and b + m > tens
                 low = high = True
             digits.append(q)
-        low_diff = w(b << 1) - tens
+        low_diff = w(w(b << 1) - tens)  # (b << 1) - tens in int / long arithmetic: wraps before widening
     else:  # FDBigInteger
         S = 5 ** S5 << S2
         B = fract_bits * 5 ** B5 << B2

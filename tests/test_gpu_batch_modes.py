@@ -222,3 +222,26 @@ def test_k1_floor_carry_equals_from_scratch(wmajor):
                 for w in range(5):
                     gi, gl = a[1][k * 5 + w]
                     assert np.array_equal(gi, r[w][0]) and np.array_equal(gl, r[w][1]), (h, w)
+
+
+def test_k1_floor_carry_backward_blocks_overlap():
+    """a K1 that only writes the floor carry (its first hop is before the previous
+    block's last) runs on another slot's stream than the previous carry K1, and must still be
+    ordered after it (rgpu.cpp k1_ev_live), or a later block reads floors left at a later hop.
+    A 4M-update power-law graph makes each K1 last long enough for the blocks to overlap; the hop
+    list alternates late and early 64-hop blocks.  Carry on and off must agree on every summary."""
+    from raphtory_amd.synth import gen_powerlaw
+    s = gen_powerlaw(5, 200_000, 4_000_000, t0=0, t1=YEAR)
+    hops = range_hops(YEAR - 60 * DAY, YEAR, HOUR)
+    blocks = []
+    for i in range(3):
+        blocks += [hops[800 + 64 * i:864 + 64 * i], hops[64 * i:64 * i + 64]]
+    hs = np.concatenate(blocks)
+    out = {}
+    for carry in ("1", "0"):
+        with envset({"RGPU_K1_CARRY": carry}):
+            g = graph_env(s, {})
+            g.run("cc", hs, BATCH_WINDOWS)
+            out[carry] = g.cc_summaries().copy()
+            g.close()
+    assert np.array_equal(out["1"], out["0"])

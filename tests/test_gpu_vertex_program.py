@@ -164,6 +164,14 @@ def test_float_vertex_programs(name, stream):
                 assert np.all(gvals == gvals.astype(np.float32).astype(np.float64))
                 bad = np.abs(gvals - vals) > 1e-6 * np.maximum(1.0, np.abs(vals))
                 assert not bad.any(), (t, w, int(bad.sum()), gvals[bad][:4], vals[bad][:4])
+        # the result calls follow the kind of the program the retained run ran, not the one set
+        # since: an int program set after the float run changes neither
+        keep = g.vp_result_f(0, 0)
+        g.set_vertex_program(reduce="min")
+        again = g.vp_result_f(0, 0)
+        assert np.array_equal(keep[0], again[0]) and np.array_equal(keep[1], again[1])
+        with pytest.raises(Exception):
+            g.vp_result(0, 0)
 
 
 @pytest.mark.parametrize("P", [2, 3])
