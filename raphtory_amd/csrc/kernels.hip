@@ -160,16 +160,6 @@ __device__ __forceinline__ int64_t first_after(const int64_t* dt, int64_t p, int
   }
   return a;
 }
-// cursor p = first death after the previous hop; advance to the first death after t (a few
-// linear steps, then a binary search: a power-law hub can die thousands of times per day)
-__device__ __forceinline__ int64_t death_advance(const int64_t* dt, int64_t p, int64_t hi, int64_t t) {
-  for (int s = 0; s < 4; s++) {
-    if (p >= hi || dt[p] > t) return p;
-    p++;
-  }
-  return first_after(dt, p, hi, t);
-}
-
 // A batch's small state (stats words, superstep flags, frontier flags) is cleared by its
 // first kernel: the vertex-mask kernel when the batch has its own masks, else k_batch_clear.
 __device__ __forceinline__ void batch_clear(const BatchClear& clr) {
@@ -225,6 +215,38 @@ __device__ __forceinline__ void store_carry(int32_t* __restrict__ fc, const Batc
   if (bp.carry) fc[i] = f1 < 0 ? -1 : (int32_t)(f1 - lo);
 }
 
+// An entity with more than bp.iv_max points between a sorted block's first and last hop (a
+// power-law hub: a vertex has a point per EADD touching it, thousands per hour) took the per-hop
+// form in its own thread: 64 dependent floor advances, each up to 8 steps and a binary search —
+// ~1,800 dependent loads, so that thread alone set the launch's length (a K1 launch over a 2.2M-
+// vertex partition lasted 0.5 ms).  The wave now takes such entities one at a time, lane = hop: each
+// lane searches its own hop's floor in [f0, f1] (the block's first and last floors bound every hop's),
+// all in flight together, and the window bits are ballots (lane k is bit k of a plane).
+// (f0 < 0: no point at or before the first hop; the points from lo on count)
+__device__ __forceinline__ int64_t block_points(int64_t lo, int64_t f0, int64_t f1) { return f1 - (f0 < 0 ? lo - 1 : f0); }
+// floor of lane k's hop within [a, f1] (f1 = the floor at the block's last hop), or -1
+__device__ __forceinline__ int64_t floor_in(const int64_t* __restrict__ key, int64_t a, int64_t f1, int64_t t) {
+  const int64_t probe = 2 * t + 1;
+  int64_t lo = a, hi = f1 + 1;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (key[m] <= probe) lo = m + 1; else hi = m;
+  }
+  return lo - 1 >= a ? lo - 1 : -1;
+}
+// lane = hop: the window planes of one entity from each lane's (alive, age), as ballots
+template <bool PLANAR>
+__device__ __forceinline__ void lane_hop_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const HopLDS& L, bool alive,
+                                              int64_t age) {
+  if constexpr (PLANAR) {
+#pragma unroll
+    for (int w = 0; w < kMaxPlanes; w++) m[w] = w < L.W ? __ballot(alive && age <= L.thr[w]) : 0ull;
+  } else {
+    m[0] = 0;
+    for (int w = 0; w < L.W; w++) m[0] |= __ballot(alive && age <= L.thr[w]) << (w * L.KS);
+  }
+}
+
 template <bool PLANAR>
 __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* __restrict__ voff,
                                                      const int64_t* __restrict__ vkey, BatchParams bp,
@@ -234,49 +256,79 @@ __global__ __launch_bounds__(256) void k_vertex_mask(int64_t nv, const int64_t* 
   hop_lds_init(L, bp, bp.thr_v);
   batch_clear(clr);
   const int K = L.K;
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv;
-       v += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t lo = voff[v], hi = voff[v + 1];
-    uint64_t m[PLANAR ? kMaxPlanes : 1] = {};
-    int64_t f = -1;
-    if (bp.sorted) {
-      int64_t f0, f1;
-      block_floors(vkey, lo, hi, bp, L, fc, v, f0, f1);
-      store_carry(fc, bp, v, f1, lo);
-      if (bp.iv_max >= 0 && f1 - f0 <= bp.iv_max) {  // f1 < 0: dead at every hop
-        for (int64_t i = f0 < 0 ? lo : f0; i <= f1; i++) {
-          const int64_t key = vkey[i];
-          if (!(key & 1)) continue;  // a deletion: dead over its interval
-          const int64_t tf = key >> 1;
-          const int b = i + 1 < hi ? hop_lb(L, vkey[i + 1] >> 1) : K;
-          interval_bits<PLANAR>(m, L, tf, hop_lb(L, tf), b);
+  const int lane = lane_id();
+  // wave-uniform loop (lane = vertex): the wave's hubs are then done together, lane = hop
+  for (int64_t v0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); v0 < nv;
+       v0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = v0 + lane;
+    bool hub = false;
+    int64_t lo = 0, f0 = -1, f1 = -1;
+    if (v < nv) {
+      lo = voff[v];
+      const int64_t hi = voff[v + 1];
+      uint64_t m[PLANAR ? kMaxPlanes : 1] = {};
+      if (bp.sorted) {
+        block_floors(vkey, lo, hi, bp, L, fc, v, f0, f1);
+        store_carry(fc, bp, v, f1, lo);
+        if (bp.iv_max >= 0 && block_points(lo, f0, f1) <= bp.iv_max) {  // f1 < 0: dead at every hop
+          for (int64_t i = f0 < 0 ? lo : f0; i <= f1; i++) {
+            const int64_t key = vkey[i];
+            if (!(key & 1)) continue;  // a deletion: dead over its interval
+            const int64_t tf = key >> 1;
+            const int b = i + 1 < hi ? hop_lb(L, vkey[i + 1] >> 1) : K;
+            interval_bits<PLANAR>(m, L, tf, hop_lb(L, tf), b);
+          }
+          store_bits<PLANAR>(m, bp, vm, vstride, v);
+        } else {
+          hub = true;
+        }
+      } else {  // hops not ascending: the per-hop search in this thread
+        for (int k = 0; k < K; k++) {
+          const int64_t t = L.hop[k];
+          const int64_t f = floor_idx(vkey, lo, hi, t);
+          if (f < 0) continue;
+          const int64_t key = vkey[f];
+          if (!(key & 1)) continue;  // floor is a deletion
+          hop_bits<PLANAR>(m, L, t - (key >> 1), k);
         }
         store_bits<PLANAR>(m, bp, vm, vstride, v);
-        continue;
       }
-      f = f0;
     }
-    for (int k = 0; k < K; k++) {
-      const int64_t t = L.hop[k];
-      if (k > 0 || !bp.sorted) f = bp.sorted ? floor_advance(vkey, f, lo, hi, t) : floor_idx(vkey, lo, hi, t);
-      if (f < 0) continue;
-      const int64_t key = vkey[f];
-      if (!(key & 1)) continue;  // floor is a deletion
-      const int64_t age = t - (key >> 1);
-      hop_bits<PLANAR>(m, L, age, k);
+    for (uint64_t hb = __ballot(hub); hb; hb &= hb - 1) {
+      const int H = __builtin_ctzll(hb);
+      const int64_t loH = (int64_t)readlane64((uint64_t)lo, H), f0H = (int64_t)readlane64((uint64_t)f0, H);
+      const int64_t f1H = (int64_t)readlane64((uint64_t)f1, H);
+      bool alive = false;
+      int64_t age = 0;
+      if (lane < K && f1H >= 0) {
+        const int64_t t = L.hop[lane];
+        const int64_t f = floor_in(vkey, f0H < 0 ? loH : f0H, f1H, t);
+        if (f >= 0) {
+          const int64_t key = vkey[f];
+          alive = (key & 1) != 0;
+          age = t - (key >> 1);
+        }
+      }
+      uint64_t m[PLANAR ? kMaxPlanes : 1];
+      lane_hop_bits<PLANAR>(m, L, alive, age);
+      if (lane == H) store_bits<PLANAR>(m, bp, vm, vstride, v);
     }
-    store_bits<PLANAR>(m, bp, vm, vstride, v);
   }
 }
 
-// Window bits of edge e (own history + endpoint death lists), interval or per-hop form.
+// Window bits of edge e (own history + endpoint death lists), interval or per-hop form.  A sorted
+// block's edge with more than bp.iv_max points in the block is not done here: the function returns
+// true with its floors (f0, f1) and death-list ranges, and the wave does it lane = hop (edge_hub_bits).
+struct EdgeHub {
+  int64_t lo = 0, f0 = -1, f1 = -1, s0 = 0, s1 = 0, d0 = 0, d1 = 0;
+};
 template <bool PLANAR>
-__device__ __forceinline__ void edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const HopLDS& L,
+__device__ __forceinline__ bool edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const HopLDS& L,
                                           const BatchParams& bp, int64_t e, const int32_t* __restrict__ esrc,
                                           const int32_t* __restrict__ edst, const int64_t* __restrict__ eoff,
                                           const int64_t* __restrict__ ekey, const int64_t* __restrict__ doff,
                                           const int64_t* __restrict__ dtime, const uint64_t* __restrict__ dbits,
-                                          int32_t* __restrict__ fc) {
+                                          int32_t* __restrict__ fc, EdgeHub& hb) {
   const int K = L.K;
   const int64_t lo = eoff[e], hi = eoff[e + 1];
   const int32_t s = esrc[e], d = edst[e];
@@ -284,13 +336,11 @@ __device__ __forceinline__ void edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1]
   // list [0, 0) reads as "no death" everywhere below
   const bool ds = !dbits || ((dbits[s >> 6] >> (s & 63)) & 1), dd = !dbits || ((dbits[d >> 6] >> (d & 63)) & 1);
   const int64_t s0 = ds ? doff[s] : 0, s1 = ds ? doff[s + 1] : 0, d0 = dd ? doff[d] : 0, d1 = dd ? doff[d + 1] : 0;
-  int64_t fb0 = -1;
   if (bp.sorted) {
     int64_t f0, f1;
     block_floors(ekey, lo, hi, bp, L, fc, e, f0, f1);
     store_carry(fc, bp, e, f1, lo);
-    fb0 = f0;
-    if (bp.iv_max >= 0 && f1 - f0 <= bp.iv_max) {
+    if (bp.iv_max >= 0 && block_points(lo, f0, f1) <= bp.iv_max) {
       for (int64_t i = f0 < 0 ? lo : f0; i <= f1; i++) {
         const int64_t key = ekey[i];
         if (!(key & 1)) continue;
@@ -302,37 +352,47 @@ __device__ __forceinline__ void edge_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1]
         if (dn != INT64_MAX) b = min(b, hop_lb(L, dn));
         interval_bits<PLANAR>(m, L, tf, hop_lb(L, tf), b);
       }
-      return;
+      return false;
     }
+    hb.lo = lo; hb.f0 = f0; hb.f1 = f1; hb.s0 = s0; hb.s1 = s1; hb.d0 = d0; hb.d1 = d1;
+    return true;
   }
-  int64_t f = -1, ps = s0, pd = d0;
-  for (int k = 0; k < K; k++) {
+  for (int k = 0; k < K; k++) {  // hops not ascending: the per-hop search in this thread
     const int64_t t = L.hop[k];
-    int64_t lds, ldd;  // last death time <= t of src / dst (-1: none)
-    if (bp.sorted && k > 0) {
-      f = floor_advance(ekey, f, lo, hi, t);
-      ps = death_advance(dtime, ps, s1, t);
-      pd = death_advance(dtime, pd, d1, t);
-      lds = ps > s0 ? dtime[ps - 1] : -1;
-      ldd = pd > d0 ? dtime[pd - 1] : -1;
-    } else {
-      f = bp.sorted ? fb0 : floor_idx(ekey, lo, hi, t);  // (k == 0 of a sorted block: block_floors)
-      lds = s1 > s0 ? last_death(dtime, s0, s1, t) : -1;
-      ldd = d1 > d0 ? last_death(dtime, d0, d1, t) : -1;
-      if (bp.sorted) {  // k == 0: position the death cursors
-        ps = first_after(dtime, s0, s1, t);
-        pd = first_after(dtime, d0, d1, t);
-      }
-    }
+    const int64_t f = floor_idx(ekey, lo, hi, t);
     if (f < 0) continue;
     const int64_t key = ekey[f];
     if (!(key & 1)) continue;
     const int64_t ft = key >> 1;
     // an endpoint death in (ft, t] is a later kill point (killList / vertexRemoval)
+    const int64_t lds = s1 > s0 ? last_death(dtime, s0, s1, t) : -1;
+    const int64_t ldd = d1 > d0 ? last_death(dtime, d0, d1, t) : -1;
     if (lds > ft || ldd > ft) continue;
-    const int64_t age = t - ft;
-    hop_bits<PLANAR>(m, L, age, k);
+    hop_bits<PLANAR>(m, L, t - ft, k);
   }
+  return false;
+}
+// lane = hop: the window bits of a hub edge (edge_bits returned true), every lane's floor and
+// endpoint death searches in flight together; call from the whole wave
+template <bool PLANAR>
+__device__ __forceinline__ void edge_hub_bits(uint64_t (&m)[PLANAR ? kMaxPlanes : 1], const HopLDS& L,
+                                              const EdgeHub& h, const int64_t* __restrict__ ekey,
+                                              const int64_t* __restrict__ dtime, int lane) {
+  bool alive = false;
+  int64_t age = 0;
+  if (lane < L.K && h.f1 >= 0) {
+    const int64_t t = L.hop[lane];
+    const int64_t f = floor_in(ekey, h.f0 < 0 ? h.lo : h.f0, h.f1, t);
+    if (f >= 0) {
+      const int64_t key = ekey[f];
+      const int64_t ft = key >> 1;
+      const int64_t lds = h.s1 > h.s0 ? last_death(dtime, h.s0, h.s1, t) : -1;
+      const int64_t ldd = h.d1 > h.d0 ? last_death(dtime, h.d0, h.d1, t) : -1;
+      alive = (key & 1) && !(lds > ft || ldd > ft);
+      age = t - ft;
+    }
+  }
+  lane_hop_bits<PLANAR>(m, L, alive, age);
 }
 
 // an edge whose bits K2 computes itself (the same test as tslots.hip k_slot_keys)
@@ -415,14 +475,33 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
     const int64_t e = e0 + lane;
     uint64_t m[NP] = {};
     uint64_t mo[NP];  // the edge's own aliveness (the |E_w| counts)
+    bool skip = e >= ne;
     if (SKIP && esimple) {  // the group's simple bits (a wave of simple edges costs one 8-B load)
       const uint64_t sw = esimple[e0 >> 6];
-      if (sw == ~0ull || (e < ne && ((sw >> lane) & 1))) continue;
-    } else if (SKIP && e < ne && edge_simple(eoff[e], eoff[e + 1], ekey, esrc[e], edst[e], doff, dbits)) {
-      continue;
+      if (sw == ~0ull) continue;
+      skip = skip || ((sw >> lane) & 1);
+    } else if (SKIP && !skip && edge_simple(eoff[e], eoff[e + 1], ekey, esrc[e], edst[e], doff, dbits)) {
+      skip = true;
     }
-    if (e < ne) {
-      edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime, dbits, fc);
+    EdgeHub hb;
+    const bool hub = !skip && edge_bits<PLANAR>(m, L, bp, e, esrc, edst, eoff, ekey, doff, dtime, dbits, fc, hb);
+    for (uint64_t hw = __ballot(hub); hw; hw &= hw - 1) {  // hub edges: the whole wave, lane = hop
+      const int H = __builtin_ctzll(hw);
+      EdgeHub h;
+      h.lo = (int64_t)readlane64((uint64_t)hb.lo, H);
+      h.f0 = (int64_t)readlane64((uint64_t)hb.f0, H);
+      h.f1 = (int64_t)readlane64((uint64_t)hb.f1, H);
+      h.s0 = (int64_t)readlane64((uint64_t)hb.s0, H);
+      h.s1 = (int64_t)readlane64((uint64_t)hb.s1, H);
+      h.d0 = (int64_t)readlane64((uint64_t)hb.d0, H);
+      h.d1 = (int64_t)readlane64((uint64_t)hb.d1, H);
+      uint64_t mh[NP];
+      edge_hub_bits<PLANAR>(mh, L, h, ekey, dtime, lane);
+      if (lane == H)
+#pragma unroll
+        for (int w = 0; w < NP; w++) m[w] = mh[w];
+    }
+    if (!skip) {
 #pragma unroll
       for (int w = 0; w < NP; w++) mo[w] = m[w];
       if (vm_ends) {  // CC: both endpoints' memberships folded in (K2 then skips vm[nb])

@@ -236,6 +236,7 @@ struct rgpu_ctx {
   // still fits keeps them: reallocating tens of GB per merge would dominate the tick)
   std::vector<void*> slot_allocs;
   int64_t cap_nv = 0, cap_ne = 0, cap_nin = 0;
+  int64_t cap_nown = 0;                 // count rows (partitioned: owned ranks only, else every rank)
   Slot slot[kMaxSlots];
   int nslots = 3;                       // batches in flight (2 / 4 measured slower on C4)
   bool prof_lean = false;               // RGPU_PROF_LEAN (work_buf)
@@ -254,6 +255,7 @@ struct rgpu_ctx {
   int heavy_t = 2048;                   // static slots above which a vertex is split (hub_threshold)
   int heavy_env = -1;                   // RGPU_HEAVY (0: off), or -1: hub_threshold's rule
   MaskSet mset[kMaskSets];
+  int nsets = kMaskSets;                // mask sets in rotation this run (one with one batch slot)
   // K1 floor carry across a run's hop blocks (BatchParams::carry; RGPU_K1_CARRY=0 turns it off):
   // per-entity floor index at the last K1'd block's last hop, that hop, and an event after that
   // K1 (the next block's K1, on another slot's stream, waits for it)
@@ -351,7 +353,7 @@ void free_graph(rgpu_ctx* c) {
 void release_slots(rgpu_ctx* c) {
   for (void* p : c->slot_allocs) (void)hipFree(p);
   c->slot_allocs.clear();
-  c->cap_nv = c->cap_ne = c->cap_nin = 0;
+  c->cap_nv = c->cap_ne = c->cap_nin = c->cap_nown = 0;
   c->d_vid = nullptr;
   for (Slot& s : c->slot) {
     if (s.h_stepcnt) (void)hipHostFree(s.h_stepcnt);
@@ -482,7 +484,11 @@ void ensure_masks(rgpu_ctx* c, int G, int nuse) {
     }
     return;
   }
-  for (MaskSet& m : c->mset) {
+  // one batch slot runs the blocks one after another: one mask set serves (a 1B loopback rehearsal of
+  // eight partitions on one GPU needs the memory)
+  c->nsets = nuse == 1 ? 1 : kMaskSets;
+  for (int si = 0; si < c->nsets; si++) {
+    MaskSet& m = c->mset[si];
     if (m.planes < G) {  // (a smaller earlier allocation stays in slot_allocs until re-seal)
       m.vm = dalloc<uint64_t>(L, (size_t)G * (nv + kPad));
       m.em = dalloc<uint64_t>(L, (size_t)G * ne);
@@ -497,11 +503,13 @@ void ensure_masks(rgpu_ctx* c, int G, int nuse) {
 }
 
 void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
-  if (c->cap_nv < c->g.nv || c->cap_ne < c->g.ne || c->cap_nin < c->g.n_in) {
+  const int64_t nrow_need = c->partitioned ? c->pk.n_own : c->g.nv;
+  if (c->cap_nv < c->g.nv || c->cap_ne < c->g.ne || c->cap_nin < c->g.n_in || c->cap_nown < nrow_need) {
     release_slots(c);
     c->cap_nv = c->g.nv;
     c->cap_ne = c->g.ne;
     c->cap_nin = c->g.n_in;
+    c->cap_nown = nrow_need;
   }
   auto& L = c->slot_allocs;
   auto& LG = c->graph_allocs;  // heavy-vertex buffers: sized by the graph's segments
@@ -530,9 +538,12 @@ void ensure_slots(rgpu_ctx* c, int algo, int nuse) {
       s.lab[1] = dalloc<int32_t>(L, rows + kPad * kViews);
       s.uw[0] = dalloc<int32_t>(L, nv + kPad);
       s.uw[1] = dalloc<int32_t>(L, nv + kPad);
-      // component counts at the root's row (zero between batches)
-      s.counts = dalloc<int32_t>(L, rows + kPad * kViews);
-      HIPCHK(hipMemset(s.counts, 0, sizeof(int32_t) * (rows + kPad * kViews)));
+      // component counts at the root's row (zero between batches).  Partitioned: a label is counted
+      // at its owner, at the label vertex's owned rank (xchg.hip label_row), so only owned rows exist
+      // — ghosts are most of a partition's ranks at P = 8 (1B graph: ~15M of ~17M)
+      const size_t crows = (size_t)c->cap_nown * kViews + kPad * kViews;
+      s.counts = dalloc<int32_t>(L, crows);
+      HIPCHK(hipMemset(s.counts, 0, sizeof(int32_t) * crows));
       s.chg[0] = dalloc<uint64_t>(L, nv + kPad);
       s.chg[1] = dalloc<uint64_t>(L, nv + kPad);
       HIPCHK(hipMemset(s.chg[0], 0, sizeof(uint64_t) * (nv + kPad)));
@@ -772,7 +783,7 @@ void finish_tail(rgpu_ctx* c, int si, const RunCfg& rc) {
     }
   }
   if (rc.G > 1) {  // the batch no longer reads its mask set
-    MaskSet& M = c->mset[(s.batch / rc.G) % kMaskSets];
+    MaskSet& M = c->mset[(s.batch / rc.G) % c->nsets];
     HIPCHK(hipEventRecord(M.done[s.batch % rc.G], s.stream));
     M.pending--;
   }
@@ -815,7 +826,7 @@ bool ghost_vm_free(const rgpu_ctx* c, const RunCfg& rc);
 // every window, on the stream of the block's first batch, into a shared mask set.
 bool can_start(const rgpu_ctx* c, size_t b, const RunCfg& rc) {
   if (rc.G == 1 || b % rc.G != 0) return true;
-  return c->mset[(b / rc.G) % kMaskSets].pending == 0;  // set still read by an older block
+  return c->mset[(b / rc.G) % c->nsets].pending == 0;  // set still read by an older block
 }
 
 // the hops' common step when a block's hops are evenly spaced (K1 then finds hop indices
@@ -956,7 +967,7 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     }
     if (c->partitioned) part_vm_exchange(c, si, s.vm, 0, 1, ghost_vm_free(c, rc));
   } else {
-    MaskSet& M = c->mset[hb % kMaskSets];
+    MaskSet& M = c->mset[hb % c->nsets];
     if (grp == 0) {
       // the set's previous block is finished-enqueued (can_start); wait for it on the device
       for (int w = 0; w < rc.G; w++) HIPCHK(hipStreamWaitEvent(s.stream, M.done[w], 0));
@@ -2190,6 +2201,9 @@ int rgpu_open(int partition_id, int num_partitions, int device, rgpu_ctx** out) 
   c->wmajor = env_int("RGPU_WMAJOR", 1) != 0;
   c->hostprof = env_int("RGPU_HOSTPROF", 0) != 0;
   c->iv_max = env_int("RGPU_IVMAX", 32);
+  // batches in flight (default 3; 2 / 4 measured slower on C4).  RGPU_SLOTS=1 for the
+  // 1B loopback rehearsal: eight partitions' slots do not fit one GPU three times over
+  c->nslots = std::max(1, std::min(kMaxSlots, env_int("RGPU_SLOTS", 3)));
   c->heavy_env = env_int("RGPU_HEAVY", -1);
   c->heavy_t = c->heavy_env >= 0 ? c->heavy_env : 2048;
   c->delta_on = env_int("RGPU_DELTA", 1) != 0;
@@ -2526,11 +2540,13 @@ void apply_merged(rgpu_ctx* c, Merged& M) {
   c->pt.tab_ready = false;
   for (void* p : old) (void)hipFree(p);  // (the slots' kernels have finished: runs hold mu)
   // slot state that K2 does not rewrite, for the new graph
-  if (g.nv > c->cap_nv || g.ne > c->cap_ne || g.n_in > c->cap_nin) {
+  if (g.nv > c->cap_nv || g.ne > c->cap_ne || g.n_in > c->cap_nin ||
+      (c->partitioned ? c->pk.n_own : g.nv) > c->cap_nown) {
     release_slots(c);
     c->cap_nv = 2 * g.nv;  // doubling: a growing live graph re-allocates O(log) times
     c->cap_ne = 2 * g.ne;
     c->cap_nin = 2 * g.n_in;
+    c->cap_nown = 2 * (c->partitioned ? c->pk.n_own : g.nv);
   } else {
     try {
       for (int i = 0; i < c->nslots; i++) {
