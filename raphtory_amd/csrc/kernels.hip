@@ -1467,7 +1467,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __shared__ unsigned long long wred[8];  // [0..6] work fields (StepWork), [7] changed views (LDS OR)
   if (threadIdx.x < 8) wred[threadIdx.x] = 0;
   if (threadIdx.x == 0) red = 0;
-  const int64_t nwords = (nv + 7) >> 3;
+  // act_clear (the flags step r+2 will write) was last written by step r-2 — by the superstep, the hub
+  // mark and the partitioned record apply, all of which write nothing in a dense step (dense_rule) —
+  // and cleared by step r-3 before that (step 2: by the batch's first kernel).  So the nv-byte sweep
+  // runs only after a step that wrote flags (every launch swept it, 20 MB on C4)
+  const bool clear_act = step >= 3 && !dense_rule(ccount, step - 2, nv, dense_div);
+  const int64_t nwords = clear_act ? (nv + 7) >> 3 : 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords; i += (int64_t)gridDim.x * blockDim.x)
     reinterpret_cast<uint64_t*>(act_clear)[i] = 0;
   if (cb_clear)

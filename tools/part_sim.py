@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--profile-rounds", type=int, default=2,
                     help="profile passes; the one with the smallest slowest-partition time is reported")
     ap.add_argument("--probe-rounds", type=int, default=500, help="rgpu_exchange_probe rounds (0: skip)")
+    ap.add_argument("--ab", default="",
+                    help="per-run knob settings to profile on the same sealed partitions after the main pass, "
+                         "';'-separated, each 'K=V[,K=V]' (read per run by the library): one extra JSON line each")
     a = ap.parse_args()
     probe = None
     if a.probe_rounds > 0:  # one RCCL rank: the fixed cost of a round without peer latency
@@ -132,6 +135,32 @@ def main():
                "vertices_here": [g.stats()["vertices"] for g in parts], "edges_here": [g.stats()["edges"] for g in parts],
                "check": [int(summ[..., 0].sum()), int(summ[..., 1].sum()), int(summ[..., 5].sum())]}
         print(json.dumps(out), flush=True)
+        for setting in [x for x in a.ab.split(";") if x.strip()]:  # same-process A/B on these partitions
+            kv = dict(x.split("=", 1) for x in setting.split(","))
+            old = {k: os.environ.get(k) for k in kv}
+            os.environ.update(kv)
+            try:
+                run(profile=True, serial=True)
+            finally:
+                for k, v in old.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+            per, ks = [], {}
+            for g in parts:
+                mine = 0.0
+                for k, v in g.stats()["kernels"].items():
+                    if v["launches"]:
+                        ks[k] = ks.get(k, 0.0) + v["ms"]
+                        mine += v["ms"]
+                per.append(round(mine, 1))
+            summ = parts[0].cc_summaries()
+            print(json.dumps({"P": P, "ab": setting, "kernel_ms_per_partition": per, "kernel_ms_max": max(per),
+                              "kernel_ms_total": round(sum(per), 1),
+                              "kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in ks.items()},
+                              "check": [int(summ[..., 0].sum()), int(summ[..., 1].sum()), int(summ[..., 5].sum())]}),
+                  flush=True)
         for g in parts:
             g.close()
 
