@@ -98,6 +98,7 @@ constexpr int kSegSlots = 512;
 // value comes from KernOpts.hub_pro (C4, profiles/r05/ab_hubpro_c4.jsonl + ab_occ_c4.jsonl: heavy
 // 64.7 ms serial at 1, 49.9 at 8, 48.3 at 16, 47.9 at 32)
 constexpr int kHubPro = 32;
+constexpr int kHubProPart = 4;  // partitioned contexts (rgpu_run_view_batch)
 // superstep options (k_cc_step_pk, k_heavy_gather, k_cc_slots; RGPU_STEP_OPTS, all by default):
 // members holding the final label finished lane-parallel; full folds (one label on every view of
 // the member) as a segmented min over the pack (a wave min over a hub segment or a big member's
@@ -400,7 +401,10 @@ void launch_xbc_clear(hipStream_t s, const XBcIn& I, uint64_t* chg, int32_t* uw)
 // is marked when superstep `step` is dense
 void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg, int32_t* uw, uint64_t* cb,
                       const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next, int64_t tcut,
-                      const BatchParams* ebp, const int32_t* ccount, int dense_div, int step);
+                      const BatchParams* ebp, const int32_t* ccount, int dense_div, int step,
+                      const int32_t* gcut = nullptr);
+// per batch, ghost g: its time-ordered static slots at or after the cut (gcut[g], g >= n_own)
+void launch_ghost_cut(hipStream_t s, const DevGraph& g, int64_t tcut, int32_t* gcut);
 // owned id -> owned rank: ids ascend with rank; bucket b = id >> shift covers ranks
 // [boff[b], boff[b+1]) (about one id per bucket)
 // Work units of the record pack and the partitioned counts (xchg.hip): chunks of 64 consecutive owned

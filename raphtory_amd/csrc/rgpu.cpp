@@ -130,6 +130,7 @@ struct XSlot {
   XRec* sm = nullptr;                     // M records to send, peer q's at q * smcap (grown on demand)
   int64_t smcap = 0;
   uint8_t* pmask = nullptr;               // [nv] peers that read an owned vertex in the batch (K2)
+  int32_t* gcut = nullptr;                // [nv] ghost g: its time-ordered slots at or after the batch's cut
   unsigned long long* ru[2] = {nullptr, nullptr};  // received U records per superstep parity, region q
                                                    // = peer q's boundary count (never grows)
   XRec* rm[2] = {nullptr, nullptr};       // received M records per parity
@@ -1064,6 +1065,8 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
     s.r_launched = 1;  // superstep 1 ran inside the slot kernel
     if (c->partitioned) {
       s.r_final = 0;
+      // the ghosts' slots at or after the batch's cut (the record apply walks only those)
+      timed_launch(c, si, KID_XCHG, 0.0, [&] { launch_ghost_cut(s.stream, g, tcut, c->pt.xs[si].gcut); });
       part_min_labels(c, si);  // (also the count pass's minimum-label counts, part_finish_begin)
       if (rc.max_steps <= 1) part_finish_begin(c, si, rc);
       else part_post_step(c, si, rc, 1);
@@ -1331,7 +1334,8 @@ XPeers peers_layout(const rgpu_ctx* c, const int64_t* cap, const std::vector<int
 void free_part_slots(rgpu_ctx* c, bool keep_channels) {
   for (XSlot& xs : c->pt.xs) {
     for (void* p : {(void*)xs.su, (void*)xs.sm, (void*)xs.ru[0], (void*)xs.ru[1], (void*)xs.rm[0], (void*)xs.rm[1],
-                    (void*)xs.hsbuf, (void*)xs.hrbuf, (void*)xs.ccnt, (void*)xs.coff, xs.scan_tmp, (void*)xs.pmask})
+                    (void*)xs.hsbuf, (void*)xs.hrbuf, (void*)xs.ccnt, (void*)xs.coff, xs.scan_tmp, (void*)xs.pmask,
+                    (void*)xs.gcut})
       if (p) (void)hipFree(p);
     if (xs.h_xab) (void)hipHostFree(xs.h_xab);
     Exchange* x = xs.x;
@@ -1455,7 +1459,7 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
       // U records: worst case one per boundary vertex and peer, sent and received (sized by the
       // plan: no growth during a run, no host sizing)
       for (void* p : {(void*)xs.su, (void*)xs.ru[0], (void*)xs.ru[1], (void*)xs.ccnt, (void*)xs.coff, xs.scan_tmp,
-                      (void*)xs.pmask})
+                      (void*)xs.pmask, (void*)xs.gcut})
         if (p) HIPCHK(hipFree(p));
       xs.su_cap = std::max<int64_t>(X.xsend.nb, 1);
       xs.ru_cap = std::max<int64_t>(X.tab.toff[P], 1);
@@ -1471,6 +1475,7 @@ void ensure_part(rgpu_ctx* c, int nuse, int planes) {
       xs.scan_bytes = std::max<size_t>(xbc_scan_bytes(no, P), 16);
       HIPCHK(hipMalloc(&xs.scan_tmp, xs.scan_bytes));
       HIPCHK(hipMalloc((void**)&xs.pmask, (size_t)std::max<int64_t>(c->g.nv, 1)));
+      HIPCHK(hipMalloc((void**)&xs.gcut, sizeof(int32_t) * (size_t)std::max<int64_t>(c->g.nv, 1)));
     }
     if (!xs.sm) {
       // M records: a first guess, grown on demand (both receive parities share one layout, xs.rmcap)
@@ -1695,7 +1700,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
       }
   timed_launch(c, si, KID_XMARK, 0.0, [&] {
     launch_xbc_apply(s.stream, in, s.lab[par], s.chg[par], s.uw[par], chg_bits(c, s, r).next, g, s.vm, s.em,
-                     s.act[(r + 1) % 3], s.tcut, s.iem ? &s.ebp : nullptr, s.ccount, dense_div(c), r);
+                     s.act[(r + 1) % 3], s.tcut, s.iem ? &s.ebp : nullptr, s.ccount, dense_div(c), r, xs.gcut);
   });
   // the vote is global: superstep r+1 runs here even if nothing changed here
   HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(s.stepcnt + r), 1, 1, s.stream));
@@ -3224,7 +3229,10 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   c->k1_carry = env_int("RGPU_K1_CARRY", 1) != 0;
   c->ko = KernOpts();
   c->ko.step = env_int("RGPU_STEP_OPTS", c->ko.step);
-  c->ko.hub_pro = env_int("RGPU_HUB_PRO", c->ko.hub_pro);
+  // (partitioned: 4 segments per wave and round — at P = 8 the hub threshold is low and most segments
+  // are active in every superstep, so a wave walking 32 of them in turn was the launch: summed hub
+  // kernels 138 -> 101 ms, slowest partition 79.4 -> 74.5 ms, profiles/r06/part_sim_hubpro_p8.jsonl)
+  c->ko.hub_pro = env_int("RGPU_HUB_PRO", c->partitioned ? kHubProPart : c->ko.hub_pro);
   c->ko.long_steps = env_int("RGPU_LONG_STEPS", c->ko.long_steps);
   c->long_ratio = env_int("RGPU_LONG_RATIO", 4);
   try {

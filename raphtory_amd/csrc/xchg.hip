@@ -372,6 +372,25 @@ __device__ __forceinline__ void mark_slot(int64_t p, int32_t g, uint64_t ch, con
   const uint64_t bits = (iem && ts_simple(tsw)) ? simple_bits(L, ebp.sorted, ts_time(tsw)) : em[ts_e[p]];
   if (bits & ch & ((iem && ebp.simple_ends && ts_nodeath(tsw)) ? ~0ull : vm[nb])) act_next[nb] = 1;
 }
+// Per batch: the number of each ghost's time-ordered static slots at or after the batch's cut (the
+// slots are newest first, so the ones older than the cut are a suffix, dead in every view of the
+// batch).  A ghost's records then walk only that prefix: in a short window most ghosts with more than
+// 64 static slots keep a few, so they pack into the lane = slot passes with the others instead of
+// taking the wave one at a time (P = 8, hour batches: ~280 us per record apply before).
+__global__ __launch_bounds__(256) void k_ghost_cut(int64_t n_own, int64_t nv, const int64_t* __restrict__ adj_off,
+                                                   const int64_t* __restrict__ ts_t, int64_t tcut,
+                                                   int32_t* __restrict__ gcut) {
+  for (int64_t g = n_own + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < nv; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t lo = adj_off[g];
+    int64_t a = lo, b = adj_off[g + 1];
+    while (a < b) {  // first slot older than the cut
+      const int64_t m = (a + b) >> 1;
+      if (ts_time(ts_t[m]) >= tcut) a = m + 1; else b = m;
+    }
+    gcut[g] = (int32_t)(a - lo);
+  }
+}
+
 template <bool TS>
 __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict__ lab, uint64_t* __restrict__ chg,
                                                    int32_t* __restrict__ uw, uint64_t* __restrict__ cb,
@@ -384,7 +403,8 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
                                                    const int64_t* __restrict__ adj_off, const int32_t* __restrict__ ts_e,
                                                    const int32_t* __restrict__ ts_nb, const int64_t* __restrict__ ts_t,
                                                    int64_t tcut, BatchParams ebp, int iem,
-                                                   const int32_t* __restrict__ ccount, int dense_div, int step) {
+                                                   const int32_t* __restrict__ ccount, int dense_div, int step,
+                                                   const int32_t* __restrict__ gcut) {
   const bool do_mark = !dense_after(ccount, step + 1, I.n_own, dense_div);  // step r dense: r+1 visits every member
   __shared__ HopLDS L;
   if (TS && iem) hop_lds_init(L, ebp, ebp.thr_e);
@@ -441,7 +461,7 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
       ch = views & vm[g];
       if (TS) {
         a = adj_off[g];
-        k = (int32_t)(adj_off[g + 1] - a);
+        k = gcut ? gcut[g] : (int32_t)(adj_off[g + 1] - a);  // (the slots at or after the cut, k_ghost_cut)
       } else {
         a = out_off[g];
         k = (int32_t)((out_off[g + 1] - a) + (in_off[g + 1] - in_off[g]));
@@ -929,7 +949,7 @@ void launch_xbc_clear(hipStream_t s, const XBcIn& I, uint64_t* chg, int32_t* uw)
 }
 void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg, int32_t* uw, uint64_t* cb,
                       const DevGraph& g, const uint64_t* vm, const uint64_t* em, uint8_t* act_next, int64_t tcut,
-                      const BatchParams* ebp, const int32_t* ccount, int dense_div, int step) {
+                      const BatchParams* ebp, const int32_t* ccount, int dense_div, int step, const int32_t* gcut) {
   const int64_t n = I.U.pre[I.U.np] + I.M.pre[I.M.np];
   if (n <= 0) return;
   BatchParams bp0;
@@ -937,7 +957,11 @@ void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg
   auto* kern = g.ts_t ? k_xbc_apply<true> : k_xbc_apply<false>;
   kern<<<xgrid(n, 256), 256, 0, s>>>(I, lab, chg, uw, cb, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
                                    g.n_seg > 0 ? g.hv_of : nullptr, act_next, g.adj_off, g.ts_e, g.ts_nb, g.ts_t, tcut,
-                                   ebp ? *ebp : bp0, ebp ? 1 : 0, ccount, dense_div, step);
+                                   ebp ? *ebp : bp0, ebp ? 1 : 0, ccount, dense_div, step, g.ts_t ? gcut : nullptr);
+}
+void launch_ghost_cut(hipStream_t s, const DevGraph& g, int64_t tcut, int32_t* gcut) {
+  if (g.ts_t && g.nv > g.n_own)
+    k_ghost_cut<<<xgrid(g.nv - g.n_own, 256), 256, 0, s>>>(g.n_own, g.nv, g.adj_off, g.ts_t, tcut, gcut);
 }
 void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,
