@@ -22,6 +22,11 @@
 #include <cstring>
 #include <cstdlib>
 
+#include <algorithm>
+#include <stdexcept>
+
+#include <hipcub/device/device_scan.hpp>
+
 #include "kernels.hpp"
 #include "window_bits.hpp"
 
@@ -445,11 +450,73 @@ void launch_edge_simple_bits(hipStream_t s, const DevGraph& g, uint64_t* out) {
         g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dbits, out);
 }
 
+// the non-simple edge list (DevGraph.ens): per 64-edge word its count, scanned, then each written
+__global__ __launch_bounds__(256) void k_ns_count(int64_t ne, const uint64_t* __restrict__ es, int32_t* __restrict__ cnt) {
+  const int64_t nw = (ne + 63) >> 6;
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t left = ne - w * 64;
+    const uint64_t valid = left >= 64 ? ~0ull : ((1ull << left) - 1);
+    cnt[w] = __popcll(~es[w] & valid);
+  }
+}
+__global__ __launch_bounds__(256) void k_ns_write(int64_t ne, const uint64_t* __restrict__ es, const int64_t* __restrict__ off,
+                                                  int32_t* __restrict__ out) {
+  const int64_t nw = (ne + 63) >> 6;
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t left = ne - w * 64;
+    uint64_t m = ~es[w] & (left >= 64 ? ~0ull : ((1ull << left) - 1));
+    int64_t o = off[w];
+    for (; m; m &= m - 1) out[o++] = (int32_t)(w * 64 + __builtin_ctzll(m));
+  }
+}
+int64_t build_nonsimple_list(const DevGraph& g, const uint64_t* es, int32_t* out) {
+  const int64_t nw = (g.ne + 63) / 64;
+  if (nw == 0) return 0;
+  int32_t* cnt = nullptr;
+  int64_t* off = nullptr;
+  void* tmp = nullptr;
+  size_t tb = 0;
+  int64_t total = 0;
+  auto chk = [](hipError_t e) { if (e != hipSuccess) throw std::runtime_error(hipGetErrorString(e)); };
+  try {
+    chk(hipMalloc((void**)&cnt, sizeof(int32_t) * nw));
+    chk(hipMalloc((void**)&off, sizeof(int64_t) * (nw + 1)));
+    const unsigned grid = (unsigned)std::min<int64_t>((nw + 255) / 256, 16384);
+    k_ns_count<<<grid, 256>>>(g.ne, es, cnt);
+    chk(hipGetLastError());
+    chk(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, (int)nw));
+    chk(hipMalloc(&tmp, tb));
+    chk(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, off, (int)nw));  // (the total: last offset + count)
+    int64_t last_off = 0;
+    int32_t last_cnt = 0;
+    chk(hipMemcpy(&last_off, off + nw - 1, sizeof(int64_t), hipMemcpyDeviceToHost));
+    chk(hipMemcpy(&last_cnt, cnt + nw - 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+    total = last_off + last_cnt;
+    if (out && total > 0) {
+      k_ns_write<<<grid, 256>>>(g.ne, es, off, out);
+      chk(hipGetLastError());
+    }
+    chk(hipDeviceSynchronize());
+  } catch (...) {
+    (void)hipFree(cnt);
+    (void)hipFree(off);
+    (void)hipFree(tmp);
+    throw;
+  }
+  (void)hipFree(cnt);
+  (void)hipFree(off);
+  (void)hipFree(tmp);
+  return total;
+}
+
 // The loop runs wave-uniform (lane = edge within a 64-edge group) so that profile runs can
 // count alive edges per view: the wave's 64 mask words are bit-transposed (lane j <- view j)
 // and popcounted; the block sums them in LDS, one atomicAdd per (plane, view) per block.
 __device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane);
-// SKIP: simple edges (edge_simple) are left unwritten: every reader computes their bits itself
+// SKIP: simple edges (edge_simple) are left unwritten: every reader computes their bits itself.  With
+// the non-simple edge list (ens) the lanes walk only those edges: on C4 ~15 % of the edges are not
+// simple and spread evenly, so almost every 64-edge group held one and the bitmap skip left most lanes
+// idle (edge masks 2.77 ms per launch over 290M edges)
 template <bool PLANAR, bool COUNT, bool SKIP>
 __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __restrict__ esrc,
                                                    const int32_t* __restrict__ edst,
@@ -461,7 +528,8 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
                                                    unsigned long long* __restrict__ ecnt, int64_t h0,
                                                    int64_t own_lim, const uint64_t* __restrict__ vm_ends,
                                                    int64_t vstride, const uint64_t* __restrict__ dbits,
-                                                   int32_t* __restrict__ fc, const uint64_t* __restrict__ esimple) {
+                                                   int32_t* __restrict__ fc, const uint64_t* __restrict__ esimple,
+                                                   const int32_t* __restrict__ ens, int64_t n_ens) {
   __shared__ HopLDS L;
   __shared__ unsigned int cnt_s[PLANAR ? kMaxPlanes : 1][64];
   hop_lds_init(L, bp, bp.thr_e);
@@ -471,12 +539,17 @@ __global__ __launch_bounds__(256) void k_edge_mask(int64_t ne, const int32_t* __
   const int lane = lane_id();
   uint32_t acc[COUNT ? NP : 1] = {};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t e0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); e0 < ne; e0 += stride) {
-    const int64_t e = e0 + lane;
+  const bool list = SKIP && ens != nullptr;
+  const int64_t nitems = list ? n_ens : ne;
+  for (int64_t e0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); e0 < nitems; e0 += stride) {
+    const int64_t ii = e0 + lane;
+    const int64_t e = list ? (ii < n_ens ? (int64_t)ens[ii] : ne) : ii;
     uint64_t m[NP] = {};
     uint64_t mo[NP];  // the edge's own aliveness (the |E_w| counts)
     bool skip = e >= ne;
-    if (SKIP && esimple) {  // the group's simple bits (a wave of simple edges costs one 8-B load)
+    if (list) {
+      // (every listed edge is non-simple)
+    } else if (SKIP && esimple) {  // the group's simple bits (a wave of simple edges costs one 8-B load)
       const uint64_t sw = esimple[e0 >> 6];
       if (sw == ~0ull) continue;
       skip = skip || ((sw >> lane) & 1);
@@ -2758,9 +2831,11 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
   BatchParams b = bp;
   if (!fc || !bp.sorted) b.carry = 0;
 #define RGPU_EM_ARGS g.ne, g.esrc, g.edst, g.eoff, g.ekey, g.doff, g.dtime, b, em, g.ne, ecnt, h0, g.n_own, vm_ends, \
-    vstride, g.dbits, fc, esimple
+    vstride, g.dbits, fc, esimple, ens, g.n_ens
   const uint64_t* esimple = g.esimple;
-  const unsigned grid = grid_for(g.ne, 256);
+  const int32_t* ens = (skip_simple && g.ens) ? g.ens : nullptr;
+  if (skip_simple && g.ens && g.n_ens == 0) return;  // every edge simple: nothing to write
+  const unsigned grid = grid_for(ens ? g.n_ens : g.ne, 256);
   if (planar && ecnt) k_edge_mask<true, true, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
   else if (planar && skip_simple) k_edge_mask<true, false, true><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);
   else if (planar) k_edge_mask<true, false, false><<<grid, 256, 0, s>>>(RGPU_EM_ARGS);

@@ -56,6 +56,8 @@ struct DevGraph {
   const uint64_t* dbits = nullptr;                   // bit v: vertex v has a death (null: read doff)
   const uint64_t* esimple = nullptr;                 // bit e: edge e is simple (edge_simple; built with
                                                      // the time-ordered slots; null: test per edge)
+  const int32_t* ens = nullptr;                      // the other edges' ids, ascending (K1's SKIP form
+  int64_t n_ens = 0;                                 // walks only these; built with esimple)
   const int32_t *esrc = nullptr, *edst = nullptr;    // edges sorted by (src, dst)
   const int64_t *eoff = nullptr, *ekey = nullptr;    // edge own histories
   const int64_t *out_off = nullptr, *in_off = nullptr;
@@ -184,6 +186,9 @@ void launch_edge_mask(hipStream_t s, const DevGraph& g, const BatchParams& bp, u
 void launch_count_simple(hipStream_t s, const DevGraph& g, unsigned long long* out);
 // bit e of out ((ne + 63) / 64 words): edge e is simple (edge_simple) — DevGraph.esimple
 void launch_edge_simple_bits(hipStream_t s, const DevGraph& g, uint64_t* out);
+// the non-simple edges (zero bits of es, e < ne) as an ascending id list: returns the count; out null
+// = count only.  Synchronous (one device scan; temporaries freed before it returns)
+int64_t build_nonsimple_list(const DevGraph& g, const uint64_t* es, int32_t* out);
 void launch_cc_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const uint64_t* vm, const uint64_t* em,
                      int32_t* cnt, int32_t* snbr, uint64_t* smask, uint64_t* vadj, int32_t* lab0,
                      int32_t* lab1, uint64_t* chg1, uint8_t* act2, int32_t* stepflag,

@@ -2372,6 +2372,11 @@ void build_tslots(rgpu_ctx* c, DevGraph& g, std::vector<void*>& L) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipDeviceSynchronize());
     g.esimple = es;
+    // and the other edges' ids: K1's SKIP form walks only those (kernels.hip k_edge_mask)
+    const int64_t nns = build_nonsimple_list(g, es, nullptr);
+    int32_t* ens = dalloc<int32_t>(L, nns + 1);
+    g.n_ens = build_nonsimple_list(g, es, ens);
+    g.ens = ens;
   }
 }
 
