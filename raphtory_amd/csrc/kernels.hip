@@ -817,18 +817,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
      const int32_t mel = mvl ? (grank ? grank[vlane] : (int32_t)vlane) : 0;
      uint64_t light = todo & ~heavyl & __ballot(ntotl <= 64);
      todo &= ~light;
-     while (light) {
-      uint64_t pack = 0;
-      int sum = 0, myL = 0, myj = 0;
-      while (light) {
-        const int Lp = __builtin_ctzll(light);
-        const int n = __builtin_amdgcn_readlane(neff, Lp);
-        if (pack && sum + n > 64) break;
-        if (lane >= sum && lane < sum + n) { myL = Lp; myj = lane - sum; }
-        pack |= 1ull << Lp;
-        sum += n;
-        light &= light - 1;
-      }
+     // (kK2Pipe) the next pack is built and its slot words loaded before this pack's bits, stores and
+     // member loop, so that its loads are in flight behind them (one exposed trip per pack less)
+     const bool pipe = (kopts & kK2Pipe) != 0;
+     uint64_t pack_n = 0;
+     int sum_n = 0, myL_n = 0, myj_n = 0;
+     int64_t tsw_n = 0;
+     int32_t nb_n = 0, lb_n = 0;
+     auto next_pack = [&]() {
+       pack_n = 0;
+       sum_n = 0;
+       myL_n = 0;
+       myj_n = 0;
+       while (light) {
+         const int Lp = __builtin_ctzll(light);
+         const int n = __builtin_amdgcn_readlane(neff, Lp);
+         if (pack_n && sum_n + n > 64) break;
+         if (lane >= sum_n && lane < sum_n + n) { myL_n = Lp; myj_n = lane - sum_n; }
+         pack_n |= 1ull << Lp;
+         sum_n += n;
+         light &= light - 1;
+       }
+       if (pipe && lane < sum_n) {
+         const int64_t p = (int64_t)__shfl(o0l + i0l, myL_n) + myj_n;
+         tsw_n = ts_t[p];
+         nb_n = ts_nb[p];
+         lb_n = ts_g ? ts_g[p] : 0;
+       }
+     };
+     if (pipe) next_pack();
+     while (pipe ? pack_n != 0 : light != 0) {
+      if (!pipe) next_pack();
+      const uint64_t pack = pack_n;
+      const int sum = sum_n, myL = myL_n, myj = myj_n;
+      const int64_t tsw_c = tsw_n;
+      const int32_t nb_c = nb_n, lb_c = lb_n;
+      if (pipe) next_pack();  // (the next pack's slot words, behind this pack's work)
       // every lane of the pack: its member, slot and kept views
       const bool on = lane < sum;
       const int64_t vmy = dealt_item(wave, nwaves, r, G, myL);
@@ -838,8 +862,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       int32_t nb = 0, lb = 0;
       if (on) {
         const int64_t p = bmy + myj;
-        const int64_t tsw = ts_t[p];
-        nb = ts_nb[p];
+        const int64_t tsw = pipe ? tsw_c : ts_t[p];
+        nb = pipe ? nb_c : ts_nb[p];
         const int32_t e = (IEM && ts_simple(tsw)) ? 0 : ts_e[p];  // (a simple slot's bits need no edge index)
         if (nb != (int32_t)vmy && ts_time(tsw) >= tcut) {
           if constexpr (IEM) {
@@ -848,7 +872,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             m = em[e] & (ends ? mvmy : vm[nb]) & mvmy;
           }
         }
-        lb = ts_g ? ts_g[p] : (grank ? grank[nb] : nb);
+        lb = ts_g ? (pipe ? lb_c : ts_g[p]) : (grank ? grank[nb] : nb);
       }
       // partitioned: the peer owning a ghost neighbour across a kept slot (pmask, k_xbc_pack)
       uint32_t pbit = 0u;
@@ -1630,6 +1654,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     int32_t my_w = 0;
     bool has_w = false;
     uint64_t pend = todo;
+    // (software-pipelining the packs — the next pack's slot loads issued behind this pack's gather —
+    // measured 1.5 % faster than the same build without it, but its registers spilled 32 B more and
+    // the build with it was 5 % slower than without the code: profiles/r06/ab_step_pipe_c4_rejected.jsonl)
     while (pend) {
       // the next pack: members in lane order while their slots fit 64 lanes
       uint64_t pack = 0;
