@@ -838,8 +838,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
          sum_n += n;
          light &= light - 1;
        }
+       // (the shuffle with every lane active: a shuffle from an inactive lane reads 0)
+       const int64_t bq = pipe ? (int64_t)__shfl(o0l + i0l, myL_n) : 0;
        if (pipe && lane < sum_n) {
-         const int64_t p = (int64_t)__shfl(o0l + i0l, myL_n) + myj_n;
+         const int64_t p = bq + myj_n;
          tsw_n = ts_t[p];
          nb_n = ts_nb[p];
          lb_n = ts_g ? ts_g[p] : 0;
