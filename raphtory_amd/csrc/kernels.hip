@@ -817,44 +817,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
      const int32_t mel = mvl ? (grank ? grank[vlane] : (int32_t)vlane) : 0;
      uint64_t light = todo & ~heavyl & __ballot(ntotl <= 64);
      todo &= ~light;
-     // (kK2Pipe) the next pack is built and its slot words loaded before this pack's bits, stores and
-     // member loop, so that its loads are in flight behind them (one exposed trip per pack less)
-     const bool pipe = (kopts & kK2Pipe) != 0;
-     uint64_t pack_n = 0;
-     int sum_n = 0, myL_n = 0, myj_n = 0;
-     int64_t tsw_n = 0;
-     int32_t nb_n = 0, lb_n = 0;
-     auto next_pack = [&]() {
-       pack_n = 0;
-       sum_n = 0;
-       myL_n = 0;
-       myj_n = 0;
-       while (light) {
-         const int Lp = __builtin_ctzll(light);
-         const int n = __builtin_amdgcn_readlane(neff, Lp);
-         if (pack_n && sum_n + n > 64) break;
-         if (lane >= sum_n && lane < sum_n + n) { myL_n = Lp; myj_n = lane - sum_n; }
-         pack_n |= 1ull << Lp;
-         sum_n += n;
-         light &= light - 1;
-       }
-       // (the shuffle with every lane active: a shuffle from an inactive lane reads 0)
-       const int64_t bq = pipe ? (int64_t)__shfl(o0l + i0l, myL_n) : 0;
-       if (pipe && lane < sum_n) {
-         const int64_t p = bq + myj_n;
-         tsw_n = ts_t[p];
-         nb_n = ts_nb[p];
-         lb_n = ts_g ? ts_g[p] : 0;
-       }
-     };
-     if (pipe) next_pack();
-     while (pipe ? pack_n != 0 : light != 0) {
-      if (!pipe) next_pack();
-      const uint64_t pack = pack_n;
-      const int sum = sum_n, myL = myL_n, myj = myj_n;
-      const int64_t tsw_c = tsw_n;
-      const int32_t nb_c = nb_n, lb_c = lb_n;
-      if (pipe) next_pack();  // (the next pack's slot words, behind this pack's work)
+     // (software-pipelining the packs — the next pack's slot words loaded before this pack's bits,
+     // stores and member loop — measured 2.5 % faster than the same build without it, but its
+     // registers doubled the spills of the 6-wave hold and that build's K2 was ~10 % slower than
+     // without the code: profiles/r06/ab_k2_pipe_c4_rejected.jsonl)
+     while (light) {
+      uint64_t pack = 0;
+      int sum = 0, myL = 0, myj = 0;
+      while (light) {
+        const int Lp = __builtin_ctzll(light);
+        const int n = __builtin_amdgcn_readlane(neff, Lp);
+        if (pack && sum + n > 64) break;
+        if (lane >= sum && lane < sum + n) { myL = Lp; myj = lane - sum; }
+        pack |= 1ull << Lp;
+        sum += n;
+        light &= light - 1;
+      }
       // every lane of the pack: its member, slot and kept views
       const bool on = lane < sum;
       const int64_t vmy = dealt_item(wave, nwaves, r, G, myL);
@@ -864,8 +842,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       int32_t nb = 0, lb = 0;
       if (on) {
         const int64_t p = bmy + myj;
-        const int64_t tsw = pipe ? tsw_c : ts_t[p];
-        nb = pipe ? nb_c : ts_nb[p];
+        const int64_t tsw = ts_t[p];
+        nb = ts_nb[p];
         const int32_t e = (IEM && ts_simple(tsw)) ? 0 : ts_e[p];  // (a simple slot's bits need no edge index)
         if (nb != (int32_t)vmy && ts_time(tsw) >= tcut) {
           if constexpr (IEM) {
@@ -874,7 +852,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             m = em[e] & (ends ? mvmy : vm[nb]) & mvmy;
           }
         }
-        lb = ts_g ? (pipe ? lb_c : ts_g[p]) : (grank ? grank[nb] : nb);
+        lb = ts_g ? ts_g[p] : (grank ? grank[nb] : nb);
       }
       // partitioned: the peer owning a ghost neighbour across a kept slot (pmask, k_xbc_pack)
       uint32_t pbit = 0u;

@@ -106,8 +106,6 @@ constexpr int kHubProPart = 4;  // partitioned contexts (rgpu_run_view_batch)
 // the member) as a segmented min over the pack (a wave min over a hub segment or a big member's
 // chunks, and K2's superstep-1 fold); simple members (every fold full) visited lane-parallel
 constexpr int kStepFinLanes = 1, kStepSegMin = 2, kStepSimple = 4;
-// (K2) the next light pack's slot words loaded behind the current pack's work (k_cc_slots)
-constexpr int kK2Pipe = 16;
 // supersteps >= kLongSteps of a long-window batch run the short-window superstep form (launch_cc_step)
 constexpr int kLongSteps = 8;
 // The kernel options of one run.  rgpu_run_view_batch fills them once per run (the parity tests
@@ -115,7 +113,7 @@ constexpr int kLongSteps = 8;
 // superstep form; the defaults are the measured best) and hands them to every launcher, so that a
 // run never reads the environment while it launches (loopback partitions are threads of one process).
 struct KernOpts {
-  int step = kStepFinLanes | kStepSegMin | kStepSimple | kK2Pipe;  // superstep options above
+  int step = kStepFinLanes | kStepSegMin | kStepSimple;  // superstep options above
   int hub_pro = kHubPro;                                  // hub segments per wave and round, 1..64
   int long_steps = kLongSteps;                            // first superstep of the short form in a long batch
 };

@@ -1663,6 +1663,11 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   }
   std::copy(recv_u, recv_u + kMaxParts, xs.rucnt[par]);
   std::copy(recv_m, recv_m + kMaxParts, xs.rmcnt[par]);
+  if (!c->trace_path.empty()) {  // trace: step 1000 + r = the label records received after superstep r (U, M)
+    unsigned long long tu = 0, tm = 0;
+    for (int q = 0; q < P; q++) tu += recv_u[q], tm += recv_m[q];
+    c->steprec.push_back({s.batch, 1000 + r, tu, tm, 0, 0});
+  }
   const XBcIn in = bc_in(c, xs, par);
   {
     int64_t rm_alloc = 0;

@@ -404,8 +404,14 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
                                                    const int32_t* __restrict__ ts_nb, const int64_t* __restrict__ ts_t,
                                                    int64_t tcut, BatchParams ebp, int iem,
                                                    const int32_t* __restrict__ ccount, int dense_div, int step,
-                                                   const int32_t* __restrict__ gcut) {
+                                                   const int32_t* __restrict__ gcut, int phase) {
+  // phase 0: apply every record, mark the U records' ghosts; phase 1 (a second launch, only when M
+  // records arrived): mark the M records' ghosts, whose changed views are then complete in their
+  // change word (every M record ORs its views into it in phase 0; the parity's clear left only this
+  // step's) — instead of one lane walking its sender's further records one dependent load at a time
+  // (a mixed sender in a short window has dozens: ~300 us per apply in the P = 8 hour batches)
   const bool do_mark = !dense_after(ccount, step + 1, I.n_own, dense_div);  // step r dense: r+1 visits every member
+  if (phase == 1 && !do_mark) return;
   __shared__ HopLDS L;
   if (TS && iem) hop_lds_init(L, ebp, ebp.thr_e);
   const int64_t n = bc_total(I);
@@ -425,39 +431,40 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
     bool isu = false, first = false;
     int64_t mj = -1, mend = -1;
     if (i < n) g = bc_rec(I, i, b, val, mask, isu, first, &mj, &mend);
-    // apply
-    if (g >= 0 && isu) {
-      uw[g] = uw_word(val, true);
-      if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // (ChgBits)
-    }
-    // M records: a record with few views writes its row lanes itself; one with many, the wave
-    // (lane = view), one record at a time
-    const bool mrec = g >= 0 && !isu;
-    const bool wide = mrec && __popcll(mask) > 8;
-    if (mrec) {
-      uw[g] = kMixed;
-      atomicOr((unsigned long long*)&chg[g], (unsigned long long)mask);
-      if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));
-      if (!wide)
-        for (uint64_t mm = mask; mm; mm &= mm - 1) lab[(int64_t)g * 64 + __builtin_ctzll(mm)] = val;
-    }
-    for (uint64_t bb = __ballot(wide); bb; bb &= bb - 1) {
-      const int L = __builtin_ctzll(bb);
-      const int32_t gL = __builtin_amdgcn_readlane(g, L);
-      const int32_t vL = __builtin_amdgcn_readlane(val, L);
-      const uint64_t mL = rl64(mask, L);
-      if ((mL >> lane) & 1) lab[(int64_t)gL * 64 + lane] = vL;
+    if (phase == 0) {  // (wave-uniform) apply
+      // apply
+      if (g >= 0 && isu) {
+        uw[g] = uw_word(val, true);
+        if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // (ChgBits)
+      }
+      // M records: a record with few views writes its row lanes itself; one with many, the wave
+      // (lane = view), one record at a time
+      const bool mrec = g >= 0 && !isu;
+      const bool wide = mrec && __popcll(mask) > 8;
+      if (mrec) {
+        uw[g] = kMixed;
+        atomicOr((unsigned long long*)&chg[g], (unsigned long long)mask);
+        if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));
+        if (!wide)
+          for (uint64_t mm = mask; mm; mm &= mm - 1) lab[(int64_t)g * 64 + __builtin_ctzll(mm)] = val;
+      }
+      for (uint64_t bb = __ballot(wide); bb; bb &= bb - 1) {
+        const int L = __builtin_ctzll(bb);
+        const int32_t gL = __builtin_amdgcn_readlane(g, L);
+        const int32_t vL = __builtin_amdgcn_readlane(val, L);
+        const uint64_t mL = rl64(mask, L);
+        if ((mL >> lane) & 1) lab[(int64_t)gL * 64 + lane] = vL;
+      }
     }
     if (!do_mark) continue;
-    // mark: lane = record, its ghost when it is the ghost's first record and the ghost is no hub
-    const bool go = g >= 0 && first && !(hv_of && hv_of[g] >= 0);
+    // mark: lane = record, its ghost when it is the ghost's first record and the ghost is no hub (U
+    // records in phase 0, M records in phase 1)
+    const bool go = g >= 0 && first && isu == (phase == 0) && !(hv_of && hv_of[g] >= 0);
     uint64_t ch = 0;
     int64_t a = 0;
     int32_t k = 0;
     if (go) {
-      uint64_t views = mask;  // U: every view; M: the union of the sender's records of this step
-      if (!isu)
-        for (int64_t j = mj + 1; j < mend && I.rm[j].e == b; j++) views |= I.rm[j].mask;
+      const uint64_t views = isu ? mask : chg[g];  // U: every view; M: this step's views (phase 0's ORs)
       ch = views & vm[g];
       if (TS) {
         a = adj_off[g];
@@ -955,9 +962,11 @@ void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg
   BatchParams bp0;
   if (!ebp) std::memset(&bp0, 0, sizeof(bp0));
   auto* kern = g.ts_t ? k_xbc_apply<true> : k_xbc_apply<false>;
-  kern<<<xgrid(n, 256), 256, 0, s>>>(I, lab, chg, uw, cb, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
-                                   g.n_seg > 0 ? g.hv_of : nullptr, act_next, g.adj_off, g.ts_e, g.ts_nb, g.ts_t, tcut,
-                                   ebp ? *ebp : bp0, ebp ? 1 : 0, ccount, dense_div, step, g.ts_t ? gcut : nullptr);
+  for (int phase = 0; phase < (I.M.pre[I.M.np] > 0 ? 2 : 1); phase++)
+    kern<<<xgrid(n, 256), 256, 0, s>>>(I, lab, chg, uw, cb, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
+                                     g.n_seg > 0 ? g.hv_of : nullptr, act_next, g.adj_off, g.ts_e, g.ts_nb, g.ts_t, tcut,
+                                     ebp ? *ebp : bp0, ebp ? 1 : 0, ccount, dense_div, step, g.ts_t ? gcut : nullptr,
+                                     phase);
 }
 void launch_ghost_cut(hipStream_t s, const DevGraph& g, int64_t tcut, int32_t* gcut) {
   if (g.ts_t && g.nv > g.n_own)
