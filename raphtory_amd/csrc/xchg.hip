@@ -282,6 +282,9 @@ __global__ void k_xcounts(int np, int me, unsigned long long* __restrict__ scnt,
   scnt[q] = 0;
 }
 
+// lanes (views) of the 64-B lines of a row (16 lanes each) that hold at least one view of m
+__device__ __forceinline__ bool line_of(uint64_t m, int lane) { return ((m >> (lane & 48)) & 0xffffull) != 0; }
+
 // record i of a received broadcast (U records of every peer, then M records of every peer, XBcIn)
 // -> the ghost it names (-1: none here; out-of-plan records are counted into err and skipped — a
 // bug upstream, reported by the run instead of faulting the device)
@@ -405,16 +408,20 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
                                                    int64_t tcut, BatchParams ebp, int iem,
                                                    const int32_t* __restrict__ ccount, int dense_div, int step,
                                                    const int32_t* __restrict__ gcut, int phase) {
-  // phase 0: apply every record, mark the U records' ghosts; phase 1 (a second launch, only when M
-  // records arrived): mark the M records' ghosts, whose changed views are then complete in their
-  // change word (every M record ORs its views into it in phase 0; the parity's clear left only this
-  // step's) — instead of one lane walking its sender's further records one dependent load at a time
-  // (a mixed sender in a short window has dozens: ~300 us per apply in the P = 8 hour batches)
+  // phase 0: the U records (apply + mark); phase 1 (a second launch, only when M records arrived): the
+  // M records, one ghost at a time per wave.  A ghost has one owner, so one sender, whose records for
+  // it are consecutive and at most 64 (one per distinct label of its views): the wave loads them lane
+  // = record, forms the ghost's new row lane = view and stores it in whole 64-B lines over the old
+  // row, sets its words once (no atomics on its change word), and its marking uses the union of the
+  // views.  Before, every M record wrote its row lanes as single 4-B stores (each a partial-line fill)
+  // and ORed its views with atomics, and the marking lane walked the sender's further records one
+  // dependent load at a time: ~300 us per apply in the P = 8 hour batches (297k M records a step).
   const bool do_mark = !dense_after(ccount, step + 1, I.n_own, dense_div);  // step r dense: r+1 visits every member
-  if (phase == 1 && !do_mark) return;
   __shared__ HopLDS L;
   if (TS && iem) hop_lds_init(L, ebp, ebp.thr_e);
-  const int64_t n = bc_total(I);
+  // phase 0 walks the U records, phase 1 the M records (bc_rec: U records first, then M)
+  const int64_t nu = I.U.pre[I.U.np];
+  const int64_t i0 = phase == 0 ? 0 : nu, n = phase == 0 ? nu : I.M.pre[I.M.np];
   const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -430,30 +437,40 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
     uint64_t mask = 0;
     bool isu = false, first = false;
     int64_t mj = -1, mend = -1;
-    if (i < n) g = bc_rec(I, i, b, val, mask, isu, first, &mj, &mend);
-    if (phase == 0) {  // (wave-uniform) apply
-      // apply
+    if (i < n) g = bc_rec(I, i0 + i, b, val, mask, isu, first, &mj, &mend);
+    uint64_t chv = 0;  // phase 1, a ghost's first M record: the views its records changed
+    if (phase == 0) {  // (wave-uniform) U records
       if (g >= 0 && isu) {
         uw[g] = uw_word(val, true);
         if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // (ChgBits)
       }
-      // M records: a record with few views writes its row lanes itself; one with many, the wave
-      // (lane = view), one record at a time
-      const bool mrec = g >= 0 && !isu;
-      const bool wide = mrec && __popcll(mask) > 8;
-      if (mrec) {
-        uw[g] = kMixed;
-        atomicOr((unsigned long long*)&chg[g], (unsigned long long)mask);
-        if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));
-        if (!wide)
-          for (uint64_t mm = mask; mm; mm &= mm - 1) lab[(int64_t)g * 64 + __builtin_ctzll(mm)] = val;
-      }
-      for (uint64_t bb = __ballot(wide); bb; bb &= bb - 1) {
-        const int L = __builtin_ctzll(bb);
-        const int32_t gL = __builtin_amdgcn_readlane(g, L);
-        const int32_t vL = __builtin_amdgcn_readlane(val, L);
-        const uint64_t mL = rl64(mask, L);
-        if ((mL >> lane) & 1) lab[(int64_t)gL * 64 + lane] = vL;
+    } else {  // M records: per ghost (its sender's run of records), lane = record, then lane = view
+      for (uint64_t t = __ballot(g >= 0 && !isu && first); t; t &= t - 1) {
+        const int L = __builtin_ctzll(t);
+        const int32_t gL = __builtin_amdgcn_readlane(g, L), bL = __builtin_amdgcn_readlane(b, L);
+        const int64_t j0 = (int64_t)rl64((uint64_t)mj, L), je = (int64_t)rl64((uint64_t)mend, L);
+        const int64_t jj = j0 + lane;
+        XRec rr{-1, 0, 0};
+        if (jj < je) rr = I.rm[jj];
+        const uint64_t run = __ballot(jj < je && rr.e == bL);  // (a prefix: the sender's records are consecutive)
+        const uint64_t sel = run == ~0ull ? ~0ull : ((1ull << __builtin_ctzll(~run)) - 1);
+        int32_t nv_ = 0;
+        uint64_t uni = 0;
+        for (uint64_t rs = sel; rs; rs &= rs - 1) {
+          const int R = __builtin_ctzll(rs);
+          const uint64_t mR = rl64(rr.mask, R);
+          uni |= mR;
+          if ((mR >> lane) & 1) nv_ = __builtin_amdgcn_readlane(rr.val, R);
+        }
+        int32_t* row = lab + (int64_t)gL * 64;
+        const int32_t old = row[lane];
+        if (line_of(uni, lane)) row[lane] = ((uni >> lane) & 1) ? nv_ : old;
+        if (lane == 0) {
+          uw[gL] = kMixed;
+          chg[gL] = uni;  // (the parity's clear left it 0: this step's views only)
+          if (cb) atomicOr((unsigned long long*)&cb[gL >> 6], 1ull << (gL & 63));
+        }
+        if (lane == L) chv = uni;
       }
     }
     if (!do_mark) continue;
@@ -464,7 +481,7 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
     int64_t a = 0;
     int32_t k = 0;
     if (go) {
-      const uint64_t views = isu ? mask : chg[g];  // U: every view; M: this step's views (phase 0's ORs)
+      const uint64_t views = isu ? mask : chv;  // U: every view; M: the union of its records
       ch = views & vm[g];
       if (TS) {
         a = adj_off[g];
@@ -962,11 +979,14 @@ void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg
   BatchParams bp0;
   if (!ebp) std::memset(&bp0, 0, sizeof(bp0));
   auto* kern = g.ts_t ? k_xbc_apply<true> : k_xbc_apply<false>;
-  for (int phase = 0; phase < (I.M.pre[I.M.np] > 0 ? 2 : 1); phase++)
-    kern<<<xgrid(n, 256), 256, 0, s>>>(I, lab, chg, uw, cb, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
+  for (int phase = 0; phase < 2; phase++) {
+    const int64_t np = phase == 0 ? I.U.pre[I.U.np] : I.M.pre[I.M.np];
+    if (np > 0)
+    kern<<<xgrid(np, 256), 256, 0, s>>>(I, lab, chg, uw, cb, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
                                      g.n_seg > 0 ? g.hv_of : nullptr, act_next, g.adj_off, g.ts_e, g.ts_nb, g.ts_t, tcut,
                                      ebp ? *ebp : bp0, ebp ? 1 : 0, ccount, dense_div, step, g.ts_t ? gcut : nullptr,
                                      phase);
+  }
 }
 void launch_ghost_cut(hipStream_t s, const DevGraph& g, int64_t tcut, int32_t* gcut) {
   if (g.ts_t && g.nv > g.n_own)
