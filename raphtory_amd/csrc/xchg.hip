@@ -282,6 +282,8 @@ __global__ void k_xcounts(int np, int me, unsigned long long* __restrict__ scnt,
   scnt[q] = 0;
 }
 
+// M records received in a superstep from which the record apply goes per ghost (k_xbc_apply phase 1)
+constexpr int64_t kMGhostMin = 32768;
 // lanes (views) of the 64-B lines of a row (16 lanes each) that hold at least one view of m
 __device__ __forceinline__ bool line_of(uint64_t m, int lane) { return ((m >> (lane & 48)) & 0xffffull) != 0; }
 
@@ -419,9 +421,10 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
   const bool do_mark = !dense_after(ccount, step + 1, I.n_own, dense_div);  // step r dense: r+1 visits every member
   __shared__ HopLDS L;
   if (TS && iem) hop_lds_init(L, ebp, ebp.thr_e);
-  // phase 0 walks the U records, phase 1 the M records (bc_rec: U records first, then M)
+  // phase 0 walks the U records, phase 1 the M records (bc_rec: U records first, then M); phase 2 (few
+  // M records: the per-ghost loop would serialise a wave's ghosts) walks all of them per lane
   const int64_t nu = I.U.pre[I.U.np];
-  const int64_t i0 = phase == 0 ? 0 : nu, n = phase == 0 ? nu : I.M.pre[I.M.np];
+  const int64_t i0 = phase == 1 ? nu : 0, n = phase == 0 ? nu : phase == 1 ? I.M.pre[I.M.np] : nu + I.M.pre[I.M.np];
   const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -439,12 +442,35 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
     int64_t mj = -1, mend = -1;
     if (i < n) g = bc_rec(I, i0 + i, b, val, mask, isu, first, &mj, &mend);
     uint64_t chv = 0;  // phase 1, a ghost's first M record: the views its records changed
-    if (phase == 0) {  // (wave-uniform) U records
+    if (phase != 1) {  // (wave-uniform) U records
       if (g >= 0 && isu) {
         uw[g] = uw_word(val, true);
         if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));  // (ChgBits)
       }
-    } else {  // M records: per ghost (its sender's run of records), lane = record, then lane = view
+    }
+    if (phase == 2) {  // M records per lane: row lanes as single stores, views ORed with atomics
+      const bool mrec = g >= 0 && !isu;
+      const bool wide = mrec && __popcll(mask) > 8;
+      if (mrec) {
+        uw[g] = kMixed;
+        atomicOr((unsigned long long*)&chg[g], (unsigned long long)mask);
+        if (cb) atomicOr((unsigned long long*)&cb[g >> 6], 1ull << (g & 63));
+        if (!wide)
+          for (uint64_t mm = mask; mm; mm &= mm - 1) lab[(int64_t)g * 64 + __builtin_ctzll(mm)] = val;
+      }
+      for (uint64_t bb = __ballot(wide); bb; bb &= bb - 1) {
+        const int L = __builtin_ctzll(bb);
+        const int32_t gL = __builtin_amdgcn_readlane(g, L);
+        const int32_t vL = __builtin_amdgcn_readlane(val, L);
+        const uint64_t mL = rl64(mask, L);
+        if ((mL >> lane) & 1) lab[(int64_t)gL * 64 + lane] = vL;
+      }
+      if (g >= 0 && !isu && first) {  // the marking lane: the union of its sender's records
+        chv = mask;
+        for (int64_t j = mj + 1; j < mend && I.rm[j].e == b; j++) chv |= I.rm[j].mask;
+      }
+    }
+    if (phase == 1) {  // M records: per ghost (its sender's run of records), lane = record, then lane = view
       for (uint64_t t = __ballot(g >= 0 && !isu && first); t; t &= t - 1) {
         const int L = __builtin_ctzll(t);
         const int32_t gL = __builtin_amdgcn_readlane(g, L), bL = __builtin_amdgcn_readlane(b, L);
@@ -476,7 +502,7 @@ __global__ __launch_bounds__(256) void k_xbc_apply(XBcIn I, int32_t* __restrict_
     if (!do_mark) continue;
     // mark: lane = record, its ghost when it is the ghost's first record and the ghost is no hub (U
     // records in phase 0, M records in phase 1)
-    const bool go = g >= 0 && first && isu == (phase == 0) && !(hv_of && hv_of[g] >= 0);
+    const bool go = g >= 0 && first && (phase == 2 || isu == (phase == 0)) && !(hv_of && hv_of[g] >= 0);
     uint64_t ch = 0;
     int64_t a = 0;
     int32_t k = 0;
@@ -979,8 +1005,12 @@ void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg
   BatchParams bp0;
   if (!ebp) std::memset(&bp0, 0, sizeof(bp0));
   auto* kern = g.ts_t ? k_xbc_apply<true> : k_xbc_apply<false>;
-  for (int phase = 0; phase < 2; phase++) {
-    const int64_t np = phase == 0 ? I.U.pre[I.U.np] : I.M.pre[I.M.np];
+  // many M records (short windows' early supersteps): U records, then M records per ghost; else one
+  // pass over every record (the per-ghost loop serialises a wave's ghosts: late supersteps with a few
+  // thousand M records took ~100 us that way, profiles/r06/part_sim_*_mrow*)
+  const bool split = I.M.pre[I.M.np] >= kMGhostMin;
+  for (int phase = split ? 0 : 2; phase < (split ? 2 : 3); phase++) {
+    const int64_t np = phase == 0 ? I.U.pre[I.U.np] : phase == 1 ? I.M.pre[I.M.np] : n;
     if (np > 0)
     kern<<<xgrid(np, 256), 256, 0, s>>>(I, lab, chg, uw, cb, g.out_off, g.in_off, g.in_eid, g.esrc, g.edst, vm, em,
                                      g.n_seg > 0 ? g.hv_of : nullptr, act_next, g.adj_off, g.ts_e, g.ts_nb, g.ts_t, tcut,
