@@ -1008,7 +1008,10 @@ void launch_xbc_apply(hipStream_t s, const XBcIn& I, int32_t* lab, uint64_t* chg
   // many M records (short windows' early supersteps): U records, then M records per ghost; else one
   // pass over every record (the per-ghost loop serialises a wave's ghosts: late supersteps with a few
   // thousand M records took ~100 us that way, profiles/r06/part_sim_*_mrow*)
-  const bool split = I.M.pre[I.M.np] >= kMGhostMin;
+  // (per ghost pays where a mixed sender has many labels — short windows, M records ~5x the U records —
+  // and loses where it has two or three: month views' M records are 0.2-0.5x the U records, and a
+  // wave then walks dozens of ghosts in turn)
+  const bool split = I.M.pre[I.M.np] >= kMGhostMin && I.M.pre[I.M.np] > 2 * I.U.pre[I.U.np];
   for (int phase = split ? 0 : 2; phase < (split ? 2 : 3); phase++) {
     const int64_t np = phase == 0 ? I.U.pre[I.U.np] : phase == 1 ? I.M.pre[I.M.np] : n;
     if (np > 0)

@@ -15,10 +15,13 @@ serialised (no overlap with the other batch slots: an upper bound on what they c
 ms alone is the lower bound).  RCCL at P = 8 adds peer latency that one rank does not have; the
 line reports the ratio at the measured cost and with an extra 25 / 50 us per round."""
 import argparse
+import hashlib
 import json
 import os
 import sys
 import time
+
+import numpy as np
 
 os.environ.setdefault("RGPU_LOOPBACK_ISOLATE", "1")
 
@@ -133,7 +136,9 @@ def main():
                # timers above leave out too (exchange pack / unpack / mark kernels, host turns)
                "serial_wall_ms_per_partition": round(t_prof * 1e3 / P, 1),
                "vertices_here": [g.stats()["vertices"] for g in parts], "edges_here": [g.stats()["edges"] for g in parts],
-               "check": [int(summ[..., 0].sum()), int(summ[..., 1].sum()), int(summ[..., 5].sum())]}
+               "check": [int(summ[..., 0].sum()), int(summ[..., 1].sum()), int(summ[..., 5].sum())],
+               # every view's summary fields (biggest .. supersteps), hashed: equal at every P
+               "summaries_sha256": hashlib.sha256(np.ascontiguousarray(summ[..., :8]).tobytes()).hexdigest()[:16]}
         print(json.dumps(out), flush=True)
         for setting in [x for x in a.ab.split(";") if x.strip()]:  # same-process A/B on these partitions
             kv = dict(x.split("=", 1) for x in setting.split(","))
