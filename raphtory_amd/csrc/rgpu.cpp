@@ -664,6 +664,11 @@ double bytes_emask(const rgpu_ctx* c, int planes, bool skip_simple) {
   const DevGraph& g = c->g;
   const double ne = (double)g.ne, simple = skip_simple ? (double)std::max<int64_t>(c->n_simple, 0) : 0.0;
   const double keys = (double)c->pk.n_ekey;
+  if (skip_simple && g.ens) {  // the non-simple list (kernels.hip k_edge_mask): per listed edge its id, its
+                               // two offsets, both endpoints, its keys, the death offsets and the plane stores
+    const double ns = (double)g.n_ens;
+    return 4.0 * ns + 16.0 * ns + 8.0 * ns + 8.0 * (keys - simple) + (16.0 + 8.0 * planes) * ns;
+  }
   return 8.0 * (ne + 1) + 8.0 * ne + (skip_simple ? 8.0 * simple : 0.0) + 8.0 * (keys - simple) +
          (16.0 + 8.0 * planes) * (ne - simple);
 }
