@@ -1988,6 +1988,59 @@ __global__ __launch_bounds__(256) void k_heavy_slots(int64_t nseg, const int32_t
   heavy_work(work, 7, w_kept);
 }
 
+// Hub demotion (kHubDemote; after K2, before the step-1 hub mark): an owned hub whose kept slots in
+// this batch fit one pass (<= 64) and sit in one segment (the slots are time-ordered, so usually the
+// first) takes the light path for the batch: its kept slots move to its static offset, cnt = their
+// count, its segment reports 0 — the hub gather and mark skip it, the superstep packs it with the
+// other members and marks its neighbours itself (its `hbest` row stays INT32_MAX: nothing gathers into
+// it).  K2 flagged no neighbour of a hub (k_heavy_mark did that after step 1), so a demoted hub that
+// changed in step 1 flags its own here when step 1 was not dense.  In short windows most hubs keep a
+// few slots, and a hub segment costs a dependent chain per superstep (P = 8 hour batches: ~170 us of
+// hub kernels a superstep).  One wave per hub; a separate kernel so that K2's registers stay as they are.
+__global__ __launch_bounds__(256) void k_hub_demote(int64_t n_heavy, int64_t n_own, const int32_t* __restrict__ hv_seg,
+                                                    const int32_t* __restrict__ seg_v,
+                                                    const int64_t* __restrict__ seg_lo,
+                                                    const int64_t* __restrict__ adj_off,
+                                                    int32_t* __restrict__ segcnt, int32_t* __restrict__ cnt,
+                                                    int32_t* __restrict__ snbr, uint64_t* __restrict__ smask,
+                                                    const uint64_t* __restrict__ chg1, uint8_t* __restrict__ act2,
+                                                    int dense1) {
+  const int lane = lane_id();
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t h = wave; h < n_heavy; h += nwaves) {
+    const int32_t s0 = hv_seg[h], s1 = hv_seg[h + 1];
+    const int32_t v = seg_v[s0];
+    if (v >= n_own) continue;  // (a ghost hub's marks come from k_heavy_mark)
+    int32_t kept = 0, nzc = 0, nzk = -1;
+    for (int32_t k = s0 + lane; k < s1; k += 64) {
+      const int32_t c = segcnt[k];
+      kept += c;
+      if (c > 0) { nzc++; nzk = k; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      kept += __shfl_xor(kept, o);
+      nzc += __shfl_xor(nzc, o);
+      nzk = max(nzk, __shfl_xor(nzk, o));
+    }
+    if (kept == 0 || kept > 64 || nzc != 1) continue;
+    const int64_t from = seg_lo[nzk], to = adj_off[v];
+    const bool in = lane < kept;
+    const int32_t q = in ? snbr[from + lane] : 0;
+    const uint64_t m = in ? smask[from + lane] : 0;
+    if (in && from != to) {
+      snbr[to + lane] = q;
+      smask[to + lane] = m;
+    }
+    const uint64_t ch = dense1 ? 0ull : chg1[v];
+    if (in && (m & ch)) act2[q] = 1;
+    if (lane == 0) {
+      cnt[v] = kept;
+      segcnt[nzk] = 0;
+    }
+  }
+}
+
 // Superstep r, before the full-grid kernel: minimum over each segment of a flagged heavy
 // vertex of the labels of its neighbours that changed in r-1 (views where they did).
 template <int WPE>
@@ -2948,6 +3001,12 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
 }
 // segments per wave and round of the hub kernels' prologue (kernels.hpp kHubPro, KernOpts.hub_pro)
 static int hub_pro(const KernOpts& ko) { return ko.hub_pro < 1 ? 1 : (ko.hub_pro > 64 ? 64 : ko.hub_pro); }
+void launch_hub_demote(hipStream_t s, const DevGraph& g, const HeavyBuf& hb, int32_t* cnt, int32_t* snbr,
+                       uint64_t* smask, const uint64_t* chg1, uint8_t* act2, bool dense1) {
+  if (g.n_heavy <= 0) return;
+  k_hub_demote<<<grid_for(g.n_heavy, 4, 16384), 256, 0, s>>>(g.n_heavy, g.n_own, g.hv_seg, g.seg_v, g.seg_lo, g.adj_off,
+                                                             hb.segcnt, cnt, snbr, smask, chg1, act2, dense1 ? 1 : 0);
+}
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur,

@@ -106,6 +106,9 @@ constexpr int kHubProPart = 4;  // partitioned contexts (rgpu_run_view_batch)
 // the member) as a segmented min over the pack (a wave min over a hub segment or a big member's
 // chunks, and K2's superstep-1 fold); simple members (every fold full) visited lane-parallel
 constexpr int kStepFinLanes = 1, kStepSegMin = 2, kStepSimple = 4;
+// (after K2, k_hub_demote) an owned hub keeping at most 64 slots, all in one segment, takes the light path
+// for the batch
+constexpr int kHubDemote = 8;
 // supersteps >= kLongSteps of a long-window batch run the short-window superstep form (launch_cc_step)
 constexpr int kLongSteps = 8;
 // The kernel options of one run.  rgpu_run_view_batch fills them once per run (the parity tests
@@ -113,7 +116,7 @@ constexpr int kLongSteps = 8;
 // superstep form; the defaults are the measured best) and hands them to every launcher, so that a
 // run never reads the environment while it launches (loopback partitions are threads of one process).
 struct KernOpts {
-  int step = kStepFinLanes | kStepSegMin | kStepSimple;  // superstep options above
+  int step = kStepFinLanes | kStepSegMin | kStepSimple | kHubDemote;  // superstep options above
   int hub_pro = kHubPro;                                  // hub segments per wave and round, 1..64
   int long_steps = kLongSteps;                            // first superstep of the short form in a long batch
 };
@@ -207,6 +210,9 @@ void launch_heavy_slots(hipStream_t s, const DevGraph& g, int64_t tcut, const ui
                         int32_t* snbr, uint64_t* smask, const HeavyBuf& hb, bool ends = false,
                         unsigned long long* work = nullptr, const BatchParams* ebp = nullptr,
                         const KernOpts& ko = KernOpts());
+// (kHubDemote) after K2: owned hubs keeping <= 64 slots in one segment take the light path for the batch
+void launch_hub_demote(hipStream_t s, const DevGraph& g, const HeavyBuf& hb, int32_t* cnt, int32_t* snbr,
+                       uint64_t* smask, const uint64_t* chg1, uint8_t* act2, bool dense1);
 void launch_heavy_gather(hipStream_t s, const DevGraph& g, const int32_t* snbr, const uint64_t* smask,
                          const int32_t* lab_cur, const uint64_t* chg_prev, const uint8_t* act_cur,
                          const int32_t* stepflag, int step, const HeavyBuf& hb, const int32_t* uw_cur = nullptr,

@@ -1062,6 +1062,12 @@ void start_batch(rgpu_ctx* c, int si, int b, const RunCfg& rc) {
         launch_check_slots(s.stream, gk.nv, g.nv, g.adj_off, s.vm, s.cnt, s.snbr, s.uw[0],
                            s.uw[1], bad, g.grank);
       });
+    if (g.n_seg > 0 && (c->ko.step & kHubDemote)) {  // owned hubs keeping few slots: the light path (§4i)
+      const int dd = dense_div(c);
+      timed_launch(c, si, KID_HEAVY, 0.0, [&] {
+        launch_hub_demote(s.stream, g, s.hv, s.cnt, s.snbr, s.smask, s.chg[1], s.act[2], dd > 0 && (dd & kDense1));
+      });
+    }
     if (g.n_seg > 0 && !c->partitioned)  // partitioned: after the step's records are in
       timed_launch(c, si, KID_HEAVY, 0.0, [&] {
         launch_heavy_mark(s.stream, g, s.snbr, s.smask, s.chg[1], s.act[2], s.stepcnt, 1, s.hv, nullptr, nullptr,
