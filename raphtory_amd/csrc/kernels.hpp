@@ -381,11 +381,7 @@ void launch_xtab_fill(hipStream_t s, int64_t n, const int32_t* xr_v, const int32
 // regions su + q * ucap, sm + q * mcap.  write_only: coff is current (a repack into larger M
 // regions).  ccnt / coff hold nch * np + 1 words, scan_tmp xbc_scan_bytes(n_own, np).
 size_t xbc_scan_bytes(int64_t n_own, int np);
-void launch_xbc_pack(hipStream_t s, int64_t n_own, int np, const XSend& X, const uint64_t* cb_now,
-                     const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab, const int32_t* uw,
-                     const uint8_t* pmask, unsigned long long* su, int64_t ucap, XRec* sm, int64_t mcap,
-                     unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp, size_t scan_bytes,
-                     bool write_only);
+
 // counts words (4 per peer): U records, M records (coff / nch: the pack's scan), the halting vote
 void launch_xbc_counts(hipStream_t s, int np, int me, const unsigned long long* coff, int64_t nch,
                        const int32_t* stepflag, int64_t* xa);
@@ -405,6 +401,13 @@ struct XBcIn {
   int64_t n_own = 0, nv = 0;
   unsigned long long* err = nullptr;
 };
+// (clr: the ghosts of step r-2's records cleared by the count pass, k_xbc_clear folded in)
+void launch_xbc_pack(hipStream_t s, int64_t n_own, int np, const XSend& X, const uint64_t* cb_now,
+                     const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab, const int32_t* uw,
+                     const uint8_t* pmask, unsigned long long* su, int64_t ucap, XRec* sm, int64_t mcap,
+                     unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp, size_t scan_bytes,
+                     bool write_only, const struct XBcIn* clr = nullptr, uint64_t* cchg = nullptr,
+                     int32_t* cuw = nullptr);
 void launch_xbc_clear(hipStream_t s, const XBcIn& I, uint64_t* chg, int32_t* uw);
 // a superstep's received records applied to the ghost words / rows / change words (cb: changed
 // bits) and the ghosts' owned neighbours marked in act_next.  tcut / ebp: the batch's slot cut and

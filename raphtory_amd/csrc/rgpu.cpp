@@ -1558,14 +1558,19 @@ void part_min_labels(rgpu_ctx* c, int si) {
 // the label records of superstep r for every peer (U into xs.su, M into xs.sm, peer q's regions),
 // from the step's changed bits and K2's peer masks.  write_only: the offsets of the last pack are
 // current (a repack into larger M regions)
+XBcIn bc_in(const rgpu_ctx* c, const XSlot& xs, int par);
+// (clear: the count pass also clears the ghosts that step r-2's records set in parity r & 1 — the
+// k_xbc_clear launch folded in; step r-1 has read those words, step r's apply comes after)
 void part_pack(rgpu_ctx* c, int si, int r, bool write_only = false) {
   Slot& s = c->slot[si];
   Part& X = c->pt;
   XSlot& xs = X.xs[si];
+  const int par = r & 1;
+  const XBcIn clr = bc_in(c, xs, par);
   timed_launch(c, si, KID_XPACK, 0.0, [&] {
     launch_xbc_pack(s.stream, c->pk.n_own, c->nparts, X.xsend, chg_bits(c, s, r).next, s.chg[r & 1], s.vadj,
                     s.lab[r & 1], s.uw[r & 1], xs.pmask, xs.su, xs.su_cap, xs.sm, xs.smcap, xs.ccnt, xs.coff,
-                    xs.scan_tmp, xs.scan_bytes, write_only);
+                    xs.scan_tmp, xs.scan_bytes, write_only, write_only ? nullptr : &clr, s.chg[par], s.uw[par]);
   });
 }
 
@@ -1651,7 +1656,7 @@ void part_after_counts(rgpu_ctx* c, int si, const RunCfg& rc) {
   // words go quiet and the M records' change words are cleared, so that this parity holds only
   // step r's news (an M record ORs its views into the change word; hub marking reads a ghost hub's
   // word and change word as this step's).
-  timed_launch(c, si, KID_XUNPACK, 0.0, [&] { launch_xbc_clear(s.stream, bc_in(c, xs, par), s.chg[par], s.uw[par]); });
+  // (the ghosts of step r-2's records, in this parity, were cleared by this step's pack: part_pack)
   bool rover = false;
   for (int q = 0; q < P; q++) rover |= recv_m[q] > xs.rmcap[q];
   if (rover) {  // a larger M layout for both parities; the other parity's records of step r-1 are

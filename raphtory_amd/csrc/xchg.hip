@@ -131,6 +131,9 @@ __device__ __forceinline__ int distinct_labels(int32_t x, uint64_t mm, int lane)
   }
   return k;
 }
+__device__ __forceinline__ int64_t bc_total(const XBcIn& I);
+__device__ __forceinline__ int32_t bc_rec(const XBcIn& I, int64_t i, int32_t& b, int32_t& val, uint64_t& mask, bool& isu,
+                                          bool& first, int64_t* mj, int64_t* mend);
 template <bool WRITE>
 __global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, int np, const int32_t* __restrict__ bidx,
                                                   const uint64_t* __restrict__ cb_now,
@@ -140,7 +143,22 @@ __global__ __launch_bounds__(256) void k_xbc_pack(int64_t n_own, int np, const i
                                                   unsigned long long* __restrict__ su, int64_t ucap,
                                                   XRec* __restrict__ sm, int64_t mcap,
                                                   unsigned long long* __restrict__ ccnt,
-                                                  const unsigned long long* __restrict__ coff) {
+                                                  const unsigned long long* __restrict__ coff, XBcIn CI, int do_clear,
+                                                  uint64_t* __restrict__ cchg, int32_t* __restrict__ cuw) {
+  // (the count pass also clears the ghosts that step r-2's records set: k_xbc_clear folded in, one
+  // launch less per superstep — the pack runs after step r-1 read those words, before step r's apply)
+  if (!WRITE && do_clear) {
+    const int64_t nc = bc_total(CI);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nc; i += (int64_t)gridDim.x * blockDim.x) {
+      int32_t b, val;
+      uint64_t mask;
+      bool isu, first;
+      const int32_t g = bc_rec(CI, i, b, val, mask, isu, first, nullptr, nullptr);
+      if (g < 0) continue;
+      if (!isu) cchg[g] = 0;
+      cuw[g] = kGhostQuiet;
+    }
+  }
   const int lane = lane_of();
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -294,7 +312,7 @@ __device__ __forceinline__ int64_t bc_total(const XBcIn& I) { return I.U.pre[I.U
 // (b, label, views, is_u) of record i and the ghost it names; for an M record also its index in rm
 // and the end of its sender's region (mj, mend; -1 for a U record)
 __device__ __forceinline__ int32_t bc_rec(const XBcIn& I, int64_t i, int32_t& b, int32_t& val, uint64_t& mask, bool& isu,
-                                          bool& first, int64_t* mj = nullptr, int64_t* mend = nullptr) {
+                                          bool& first, int64_t* mj, int64_t* mend) {
   const int64_t nu = I.U.pre[I.U.np];
   int q;
   first = true;
@@ -341,7 +359,7 @@ __global__ __launch_bounds__(256) void k_xbc_clear(XBcIn I, uint64_t* __restrict
     int32_t b, val;
     uint64_t mask;
     bool isu, first;
-    const int32_t g = bc_rec(I, i, b, val, mask, isu, first);
+    const int32_t g = bc_rec(I, i, b, val, mask, isu, first, nullptr, nullptr);
     if (g < 0) continue;
     if (!isu) chg[g] = 0;
     uw[g] = kGhostQuiet;
@@ -930,19 +948,24 @@ void launch_xbc_pack(hipStream_t s, int64_t n_own, int np, const XSend& X, const
                      const uint64_t* chg_now, const uint64_t* vadj, const int32_t* lab, const int32_t* uw,
                      const uint8_t* pmask, unsigned long long* su, int64_t ucap, XRec* sm, int64_t mcap,
                      unsigned long long* ccnt, unsigned long long* coff, void* scan_tmp, size_t scan_bytes,
-                     bool write_only) {
-  if (X.nb <= 0 || n_own <= 0) return;
+                     bool write_only, const XBcIn* clr, uint64_t* cchg, int32_t* cuw) {
+  if (X.nb <= 0 || n_own <= 0) {
+    if (clr) launch_xbc_clear(s, *clr, cchg, cuw);
+    return;
+  }
   const int64_t nun = xbc_units(n_own);
   const unsigned grid = xgrid(nun, 4, 4096);
+  XBcIn none;
+  std::memset(&none, 0, sizeof(none));
   if (!write_only) {
     k_xbc_pack<false><<<grid, 256, 0, s>>>(n_own, np, X.bidx, cb_now, chg_now, vadj, lab, uw, pmask, su, ucap, sm, mcap,
-                                           ccnt, coff);
+                                           ccnt, coff, clr ? *clr : none, clr ? 1 : 0, cchg, cuw);
     // ccnt[np * nun] stays 0: coff[q * nun] .. coff[(q + 1) * nun] = peer q's records
     if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, ccnt, coff, (int)(nun * np + 1), s) != hipSuccess)
       throw std::runtime_error("xbc pack: scan");
   }
   k_xbc_pack<true><<<grid, 256, 0, s>>>(n_own, np, X.bidx, cb_now, chg_now, vadj, lab, uw, pmask, su, ucap, sm, mcap,
-                                        ccnt, coff);
+                                        ccnt, coff, none, 0, nullptr, nullptr);
 }
 XSend build_xsend(hipStream_t s, int64_t n_own, int64_t nx, const int32_t* xv, std::vector<void*>& T,
                   std::vector<void*>& L) {
