@@ -479,7 +479,7 @@ inline int own_bucket_shift(int64_t n_own, int64_t id_max) {
 void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,
                        unsigned int* iso, unsigned long long* gcnt, XRec* hsbuf, const int32_t* mneg = nullptr,
-                       unsigned int* fin_g = nullptr, bool long_views = true);
+                       unsigned int* fin_g = nullptr);
 // members carrying the view's global minimum label (mneg) are counted into fin_g (64 shards x 64
 // views) instead of records; fold them into w (zeroing the shards), all-reduce w, and the label's
 // owner adds w at the label's count row

@@ -1773,7 +1773,7 @@ void part_finish_begin(rgpu_ctx* c, int si, const RunCfg& rc) {
   const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);
   timed_launch(c, si, KID_HIST, 28.0 * no, [&] {
     launch_part_count(s.stream, false, L, X.own, nviews, s.vm, s.vadj, uw, s.lab[s.r_final & 1], s.counts, s.iso,
-                      xs.htot, xs.hsbuf, min_labels(c, s), xs.fin_g, s.long_views);
+                      xs.htot, xs.hsbuf, min_labels(c, s), xs.fin_g);
   });
   launch_xcounts(s.stream, P, c->part, xs.htot, xs.xab);
   HIPCHK(hipGetLastError());
@@ -1804,7 +1804,7 @@ void part_finish_end(rgpu_ctx* c, int si, const RunCfg& rc) {
     grow_regions(&xs.hsbuf, xs.hscap, sent, P, s.stream);
     const XPeers L = peers_layout(c, xs.hscap, X.xs_off, nullptr);
     launch_part_count(s.stream, true, L, X.own, nviews, s.vm, s.vadj, uw, s.lab[s.r_final & 1], s.counts, s.iso,
-                      xs.htot, xs.hsbuf, min_labels(c, s), xs.fin_g, s.long_views);
+                      xs.htot, xs.hsbuf, min_labels(c, s), xs.fin_g);
     HIPCHK(hipMemcpyAsync(xs.h_xab, xs.htot, sizeof(int64_t) * P, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipStreamSynchronize(s.stream));
     for (int q = 0; q < P; q++)

@@ -1051,15 +1051,14 @@ void launch_ghost_cut(hipStream_t s, const DevGraph& g, int64_t tcut, int32_t* g
 void launch_part_count(hipStream_t s, bool remote_only, const XPeers& P, const OwnIdx& I, int nviews,
                        const uint64_t* vm, const uint64_t* vadj, const int32_t* uw, const int32_t* lab, int32_t* counts,
                        unsigned int* iso, unsigned long long* gcnt, XRec* hsbuf, const int32_t* mneg,
-                       unsigned int* fin_g, bool long_views) {
+                       unsigned int* fin_g) {
   const uint64_t vmask = nviews >= 64 ? ~0ull : ((1ull << nviews) - 1);
-  // Long windows: 16 chunks of 64 members per wave — a wave flushes its label cache once, as records,
-  // so fewer waves emit fewer records (one per cached label and count group) and flush less (grid 2048
-  // -> 512 at 2.2M members: 7.3 -> 5.0 ms per partition and query, profiles/r04/ab_part_count_grid.jsonl).
-  // Short windows: 2 chunks per wave — their members are mostly mixed (a label per hop), the cache
-  // rarely hits, and a wave walking 16 chunks of mixed rows in turn was the launch (~330 us per hour
-  // batch at P = 8, the same as the whole graph's count at P = 1)
-  const unsigned grid = xgrid(xbc_units(I.n_own), 4 * (long_views ? 16 : 2), 8192);
+  // 16 chunks of 64 members per wave: a wave flushes its label cache once, as records, so fewer
+  // waves emit fewer records (one per cached label and count group) and flush less (grid 2048 ->
+  // 512 at 2.2M members: 7.3 -> 5.0 ms per partition and query, profiles/r04/ab_part_count_grid.jsonl).
+  // (Round 6: 2 chunks per wave for short windows, whose members are mostly mixed, doubled the hour
+  // batches' count time at P = 8 — 324 -> 708 us, more flushes — profiles/r06/part_sim_p8_300m_count_grid_rejected.jsonl)
+  const unsigned grid = xgrid(xbc_units(I.n_own), 4 * 16, 2048);
   if (remote_only)
     k_part_count<true><<<grid, 256, 0, s>>>(P, I, vmask, vm, vadj, uw, lab, counts, iso, gcnt, hsbuf, mneg, fin_g);
   else

@@ -217,8 +217,39 @@ def add_year(threads: int):
     print(f"-> {OUT}", flush=True)
 
 
+def extend(k: int, threads: int):
+    """Round 6 (40 of the 840 views were oracle-checked): k more hops, the ones of
+    picks(168, k) not in the file yet.  Their month..hour records come from the literal replay over the
+    37-day slice and their year record and superstep count from the add-only restatement over the year
+    slice; the add-only month..hour records must equal the literal replay's (the run stops otherwise), as
+    for the first eight."""
+    data = json.load(open(OUT))
+    assert data["windows"] == list(BATCH_WINDOWS)
+    have = {int(h) for h in data["hops"]}
+    sel = [h for h in picks(168, k) if h not in have]
+    log = lambda m: print(m, flush=True)  # noqa: E731
+    log(f"extending {sorted(have)} by {sel}")
+    _, lit = sliced_views(INTER, BATCH_WINDOWS[1:], sel, threads, log=log)
+    _, yv = year_views(INTER, sel, threads, log=log)
+    for h in sel:
+        new, old = yv[str(h)], lit[str(h)]
+        assert new["t"] == old["t"], h
+        for j in range(4):
+            if new["windows"][1 + j] != old["windows"][j]:
+                raise SystemExit(f"hop {h} window {BATCH_WINDOWS[1 + j]}: add-only {new['windows'][1 + j]} != "
+                                 f"literal {old['windows'][j]}")
+        log(f"hop {h}: month..hour == literal replay; year members {new['windows'][0]['members']}, "
+            f"{new['supersteps']} supersteps")
+        data["hops"][str(h)] = {"t": new["t"], "supersteps": new["supersteps"], "windows": new["windows"]}
+    with open(OUT, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
+    log(f"-> {OUT} ({len(data['hops'])} hops)")
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--extend", type=int, default=0,
+                    help="add the hops of picks(168, N) not in the file yet (all five windows, both oracles)")
     ap.add_argument("--hops", type=int, default=8, help="hops sampled over the 168")
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--verify-prefix", action="store_true",
@@ -226,6 +257,8 @@ def main():
     ap.add_argument("--year", action="store_true",
                     help="add the year views and superstep counts (add-only oracle over the year slice)")
     a = ap.parse_args()
+    if a.extend:
+        return extend(a.extend, a.threads)
     if a.year:
         return add_year(a.threads)
     if a.verify_prefix:
