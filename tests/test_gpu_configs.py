@@ -226,8 +226,8 @@ def _check_view(full_row, ids, lab, exp, where):
 
 def test_c4_full_1b_vs_sliced_oracle_goldens():
     """The headline query itself: the whole 1B-update C4 stream, 168 hourly hops x {y,m,w,d,h}.
-    Summary invariants on all 840 views; at the 8 hops of tests/golden/c4_sliced_goldens.json
-    (spread over the 168), the month, week, day and hour views against the oracle — summary
+    Summary invariants on all 840 views; at the 30 hops of tests/golden/c4_sliced_goldens.json
+    (spread over the 168; 8 in round 5, 22 more in round 6), the month, week, day and hour views against the oracle — summary
     fields, member count and the checksum of every member's (id, label).  The oracle replays the
     stream's last 37 days, which is exact for these windows on an add-only stream
     (tools/make_c4_sliced_goldens.py; tests/test_c4_slice.py checks it on the 100M prefix).
@@ -261,8 +261,9 @@ def test_c4_full_1b_vs_sliced_oracle_goldens():
         for k, h in enumerate(pick):
             rec = _SLICED["hops"][str(h)]
             assert int(hops[h]) == rec["t"]
-            if "supersteps" in rec:  # (the year views are in: the hop's count is the oracle's)
-                assert full[h, 0, 7] == rec["supersteps"], (h, full[h, 0, 7], rec["supersteps"])
+            if "supersteps" in rec:  # (the year views are in: the hop's count, over its five views, is the oracle's)
+                got = int(full[h, :, 7].max())
+                assert got == rec["supersteps"], (h, full[h, :, 7].tolist(), rec["supersteps"])
             for j, w in enumerate(_SLICED["window_index_in_query"]):
                 ids, lab = g.cc_vertex_labels(k, w)
                 _check_view(full[h, w], ids, lab, rec["windows"][j], ("1B", h, w))
