@@ -75,6 +75,10 @@ def parse():
     p.add_argument("--c4-users", type=int, default=20_000_000)
     p.add_argument("--c4-interactions", type=int, default=333_333_334, help="x3 updates (1B at the default)")
     p.add_argument("--c4-hops", type=int, default=168)
+    p.add_argument("--exchange", default="rccl", choices=["rccl", "shm"],
+                   help="N > 1, C4 / C5: the label-record channel.  shm = the library's shared-memory group of "
+                        "processes on one host, rank r on GPU r mod the visible GPUs: a rehearsal of the N > 1 "
+                        "bench path on a one-GPU box (never a scaling number)")
     p.add_argument("--vertex-order", default="locality", choices=["locality", "id"],
                    help="local vertex order of the sealed graph (rgpu_set_vertex_order; A/B runs)")
     return p.parse_args()
@@ -460,7 +464,7 @@ def run_c4(a, rank, world, local):
         dist.init_process_group("gloo")  # control plane; the data path is the library's RCCL
     if dist is not None:
         from raphtory_amd.partitioned import open_rccl_partition
-        g = open_rccl_partition(local, dist)
+        g = open_rccl_partition(local, dist, kind=a.exchange)
     elif a.partitioned:
         os.environ["RGPU_PARTITIONED"] = "1"
         g = TemporalGraph(device=local)
@@ -601,7 +605,9 @@ def run_c4(a, rank, world, local):
                        "windows": len(windows),
                        "parallelism": ("one GPU, partitioned path (P = 1)" if a.partitioned else "one GPU")
                                       if world == 1 else
-                                      f"vertex-partitioned x{world} (Utils.getPartition), RCCL label records",
+                                      f"vertex-partitioned x{world} (Utils.getPartition), "
+                                      + ("RCCL label records" if a.exchange == "rccl" else
+                                         "shared-memory label records on one host (rehearsal, not a scaling number)"),
                        "gen_ingest_s": round(gen_s, 1), "seal_s": round(seal_s, 1),
                        "supersteps_per_view_mean": round(float(summ[..., 7].mean()), 2),
                        "alive_edge_windows": s8d["alive_edge_windows"] if s8d else None,
@@ -649,7 +655,7 @@ def run_c5(a, rank, world, local):
         import torch.distributed as dist
         dist.init_process_group("gloo")  # control plane; the data path is the library's RCCL
         from raphtory_amd.partitioned import open_rccl_partition
-        g = open_rccl_partition(local, dist, vertex_order="id")  # live: later seals merge
+        g = open_rccl_partition(local, dist, vertex_order="id", kind=a.exchange)  # live: later seals merge
     elif a.partitioned:
         os.environ["RGPU_PARTITIONED"] = "1"
         g = TemporalGraph(device=local, vertex_order="id")
@@ -937,6 +943,8 @@ def main():
     heartbeat()
     rank, world, local = dist_env()
     import torch
+    if a.exchange == "shm":  # one-host rehearsal: ranks share the visible GPUs (device_count: no HIP init)
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     run = {"c2": run_c2, "c3": run_c3, "c4": run_c4, "c5": run_c5, "diffusion": run_diffusion}[a.config]
     run(a, rank, world, local)
