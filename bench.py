@@ -79,6 +79,12 @@ def parse():
                    help="N > 1, C4 / C5: the label-record channel.  shm = the library's shared-memory group of "
                         "processes on one host, rank r on GPU r mod the visible GPUs: a rehearsal of the N > 1 "
                         "bench path on a one-GPU box (never a scaling number)")
+    p.add_argument("--hybrid", default="dh",
+                   help="N > 1, C4: these windows (letters of 'ymwdh') are answered hop-sharded instead of "
+                        "vertex-partitioned: rank r runs them for its contiguous block of the hops on a replica of "
+                        "the stream's time slice [hop0 - the longest of them, end] (exact on the add-only C4 stream: a "
+                        "view (t, w) reads only the updates in [t - w, t]); the partitions answer the other windows. "
+                        "'' = every window partitioned")
     p.add_argument("--vertex-order", default="locality", choices=["locality", "id"],
                    help="local vertex order of the sealed graph (rgpu_set_vertex_order; A/B runs)")
     return p.parse_args()
@@ -457,7 +463,8 @@ def run_c4(a, rank, world, local):
     GPU when N > 1)."""
     import torch
     from raphtory_amd import TemporalGraph
-    from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops
+    from raphtory_amd.partitioned import combine_window_groups, hop_blocks
+    from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gab_first_at, gen_gab_range, range_hops
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -503,6 +510,36 @@ def run_c4(a, rank, world, local):
         f"graph {n_vert} vertices, {n_edges} edge entities")
     hops = range_hops(end - (a.c4_hops - 1) * HOUR, end, HOUR)
     windows = BATCH_WINDOWS
+    # N > 1 (--hybrid): the short windows hop-sharded on a time-slice replica, the others partitioned
+    short_i = [i for i, c in enumerate("ymwdh") if c in a.hybrid] if dist is not None else []
+    long_w = [w for i, w in enumerate(windows) if i not in short_i]
+    short_w = [windows[i] for i in short_i]
+    blocks = hop_blocks(len(hops), world)
+    gs = None
+    if short_i:
+        t1 = time.perf_counter()
+        f0 = gab_first_at(4, users, inter, int(hops[0]) - max(short_w))
+        gs = TemporalGraph(device=local)
+        for first in range(f0, inter, chunk):
+            gs.ingest_stream(gen_gab_range(4, users, inter, first, min(chunk, inter - first)))
+        gs.seal()
+        log(f"rank {rank}: windows {a.hybrid} hop-sharded: slice replica of {3 * (inter - f0)} updates, hops "
+            f"[{blocks[rank][0]}, {blocks[rank][1]}), built in {time.perf_counter() - t1:.1f} s")
+    my_hops = hops[blocks[rank][0]:blocks[rank][1]]
+
+    def query():
+        g.run("cc", hops, long_w)  # collective over the partitions
+        if gs is not None and len(my_hops):
+            gs.run("cc", my_hops, short_w)  # this rank's block, no exchange
+
+    def summaries():
+        sl = g.cc_summaries()
+        if gs is None:
+            return sl
+        got = [None] * world
+        dist.all_gather_object(got, gs.cc_summaries() if len(my_hops) else None)
+        return combine_window_groups(len(windows), [i for i in range(len(windows)) if i not in short_i], sl, short_i,
+                                     [(lo, hi, x) for (lo, hi), x in zip(blocks, got)])
 
     def barrier():
         if dist is not None:
@@ -514,11 +551,11 @@ def run_c4(a, rank, world, local):
     if a.lean_pass_only:  # a rocprofv3 trace of this command holds the serial lean pass alone
         a.no_edge_counts = True
     for _ in range(a.warmup):
-        g.run("cc", hops, windows)
+        query()
     barrier()
     t0 = time.perf_counter()
     for _ in range(0 if a.profile_only else a.steps):
-        g.run("cc", hops, windows)
+        query()
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -529,14 +566,18 @@ def run_c4(a, rank, world, local):
     if a.profile_only:
         ms_per_step = value = None
     log(f"rank {rank}: query {ms_per_step} ms")
-    summ = None if a.profile_only else g.cc_summaries()  # (profile-only: after the profile pass)
+    summ = None if a.profile_only or gs is not None else g.cc_summaries()  # (profile-only: after the profile pass)
+    if gs is not None and not a.profile_only:
+        summ = summaries()  # (collective) before the profile passes overwrite the partitions' results
     roofline, ks, s8d = None, {}, None
     if not a.no_profile_pass:
         log("profile passes")
-        kraw = profile_passes(g, hops, windows, lean_only=a.lean_pass_only)  # collective at N > 1
+        if a.profile_only and gs is not None and len(my_hops):
+            gs.run("cc", my_hops, short_w)  # (its summaries for the check; not profiled)
+        kraw = profile_passes(g, hops, long_w, lean_only=a.lean_pass_only)  # collective at N > 1
         ks = kernel_table({"kernels": kraw})
         if summ is None:
-            summ = g.cc_summaries()
+            summ = summaries()
         d = kraw["cc_step"]
         gbs = d["bytes"] / (d["ms"] / 1e3) / 1e9
         traffic, tsrc = pmc_traffic("k_cc_step_pk", config="C4")
@@ -556,7 +597,7 @@ def run_c4(a, rank, world, local):
             roofline["aggregate"] = aggregate_roofline(kraw, "C4")
         if not a.no_edge_counts and world == 1:
             g.run("cc", hops, windows, edge_counts=True)
-            summ = g.cc_summaries()
+            summ = summaries()
             s8d = survey_bytes(summ, len(hops), windows, st["vertices"], st["edges"],
                                st["vertex_events"] + st["edge_events"] + st["deaths"], ks, d["launches"])
             roofline["survey_8d"] = {"achieved": round(s8d["cc_step"]["achieved_GBps"], 1),
@@ -607,7 +648,9 @@ def run_c4(a, rank, world, local):
                                       if world == 1 else
                                       f"vertex-partitioned x{world} (Utils.getPartition), "
                                       + ("RCCL label records" if a.exchange == "rccl" else
-                                         "shared-memory label records on one host (rehearsal, not a scaling number)"),
+                                         "shared-memory label records on one host (rehearsal, not a scaling number)")
+                                      + (f"; windows {a.hybrid} hop-sharded over the ranks on a time-slice replica"
+                                         if short_i else ""),
                        "gen_ingest_s": round(gen_s, 1), "seal_s": round(seal_s, 1),
                        "supersteps_per_view_mean": round(float(summ[..., 7].mean()), 2),
                        "alive_edge_windows": s8d["alive_edge_windows"] if s8d else None,
@@ -623,6 +666,8 @@ def run_c4(a, rank, world, local):
         }
         print(json.dumps(out), flush=True)
     g.close()
+    if gs is not None:
+        gs.close()
     if dist is not None:
         dist.destroy_process_group()
 

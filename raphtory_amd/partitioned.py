@@ -147,3 +147,35 @@ class LoopbackPartitions:
     def close(self) -> None:
         for g in self.parts:
             g.close()
+
+
+# ---------------------------------------------------------------- window-class hybrid (N > 1, C4)
+# The short windows of a batched-window range query read only a recent time slice of the stream: on
+# an add-only stream a view (t, w) depends only on the updates in [t - w, t] (aliveAtWithWindow,
+# Entity.scala:173-201; tools/make_c4_sliced_goldens.py states the argument, tests/test_c4_slice.py
+# checks it).  Partitioned, those windows do not scale (their batches are a few milliseconds of
+# per-superstep floors on every partition), so with N ranks each rank answers them for
+# its own contiguous block of the hops on a replica of that slice — no exchange — while the
+# partitions answer the long windows.  Descending windows keep the batched lens exact under the split
+# (each window's vertex set is the running minimum of the windows before it, i.e. its own, as
+# WindowLens.shrinkWindow gives for {y, m, w, d, h}); the hop's superstep count is recombined below.
+
+def hop_blocks(n_hops: int, world: int) -> list:
+    """Rank r's contiguous block [lo, hi) of the hops."""
+    return [(r * n_hops // world, (r + 1) * n_hops // world) for r in range(world)]
+
+
+def combine_window_groups(n_windows: int, long_idx, long_summ: np.ndarray, short_idx, short_blocks) -> np.ndarray:
+    """The query's [n_hops, n_windows, 9] cc_summaries from the partitions' long-window summaries
+    and each rank's short-window block ((lo, hi, summaries) per rank).  Field 7 (supersteps) is the
+    hop's job count over the windows of one run — min(maxSteps, 1 + the last changing step over
+    them), rgpu.cpp finish_supersteps — so the hop's count over all its windows is the maximum of
+    the two runs' counts (min and max commute with the monotone 1 + x)."""
+    short_idx = list(short_idx)
+    full = np.zeros((long_summ.shape[0], n_windows) + long_summ.shape[2:], long_summ.dtype)
+    full[:, list(long_idx)] = long_summ
+    for lo, hi, x in short_blocks:
+        if hi > lo:
+            full[lo:hi, short_idx] = x
+    full[..., 7] = full[..., 7].max(axis=1, keepdims=True)
+    return full

@@ -88,6 +88,19 @@ def gen_gab_range(seed: int, users: int, interactions: int, first: int, count: i
     return Stream(t[:n], k[:n], s[:n], d[:n])
 
 
+def gab_first_at(seed: int, users: int, interactions: int, t_from: int) -> int:
+    """The first interaction index of the gen_gab stream with time >= t_from (`interactions` if
+    none): bisection on the generator itself, whose times are monotone in the index."""
+    lo, hi = 0, interactions
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if int(gen_gab_range(seed, users, interactions, mid, 1).t[0]) >= t_from:
+            hi = mid
+        else:
+            lo = mid + 1
+    return lo
+
+
 def range_hops(start: int, end: int, jump: int) -> np.ndarray:
     """Hop timestamps of a Range job: RangeAnalysisTask.restart (RangeAnalysisTask.scala:18-35)
     starts at `start`, adds `jump`, clamps to `end`, and stops once it has run `end`."""

@@ -192,3 +192,48 @@ def test_partitioned_partition_without_edges(P):
     end = int(s.t[-1])
     check_cc(lp, o, range_hops(end - 30 * DAY, end, 2 * DAY), BATCH_WINDOWS)
     lp.close()
+
+
+@pytest.mark.parametrize("P,letters", [(2, "dh"), (3, "wdh")])
+def test_window_hybrid_equals_one_graph(P, letters):
+    """bench.py's N > 1 window-class hybrid (raphtory_amd/partitioned.py): the partitions answer the
+    long windows, each rank its block of the hops for the short windows on a replica of the stream's
+    time slice [hop0 - the longest short window, end].  On the add-only GAB stream every view's
+    summary — the hop's superstep count included — equals the one-graph batched query's (itself
+    oracle-checked on the C4 goldens), and a sampled view's labels equal the oracle's."""
+    from raphtory_amd import TemporalGraph
+    from raphtory_amd.partitioned import combine_window_groups, hop_blocks
+    from raphtory_amd.synth import Stream
+    s = gen_gab(4, 30_000, 1_000_000)
+    end = int(s.t[-1])
+    hops = range_hops(end - 99 * HOUR, end, HOUR)  # 100 hops: two batches per window
+    g = TemporalGraph()
+    g.ingest_stream(s)
+    g.seal()
+    g.run("cc", hops, BATCH_WINDOWS)
+    ref = g.cc_summaries()
+    g.close()
+    short_i = [i for i, c in enumerate("ymwdh") if c in letters]
+    long_i = [i for i in range(len(BATCH_WINDOWS)) if i not in short_i]
+    sw = [BATCH_WINDOWS[i] for i in short_i]
+    lp = _parts(s, P)
+    lp.run("cc", hops, [BATCH_WINDOWS[i] for i in long_i])
+    ls = lp.parts[0].cc_summaries()
+    lp.close()
+    keep = s.t >= int(hops[0]) - max(sw)
+    assert 0 < keep.sum() < len(s) // 10  # a real slice
+    sl = Stream(s.t[keep], s.kind[keep], s.src[keep], s.dst[keep])
+    rep = TemporalGraph()
+    rep.ingest_stream(sl)
+    rep.seal()
+    blocks = []
+    for lo, hi in hop_blocks(len(hops), P):
+        rep.run("cc", hops[lo:hi], sw, retain=lo == 0)
+        blocks.append((lo, hi, rep.cc_summaries()))
+        if lo == 0:  # the first hop of rank 0's block, the shortest window: labels vs the oracle on the slice
+            res, _ = Oracle.from_stream(sl).cc(int(hops[0]), [sw[-1]], mode=1)
+            gids, glab = rep.cc_vertex_labels(0, len(sw) - 1)
+            assert np.array_equal(gids, res[0][0]) and np.array_equal(glab, res[0][1])
+    rep.close()
+    got = combine_window_groups(len(BATCH_WINDOWS), long_i, ls, short_i, blocks)
+    assert np.array_equal(got, ref)

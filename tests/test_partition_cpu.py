@@ -172,3 +172,29 @@ def test_locality_order_partitions(ph, P):
                 assert np.array_equal(plist(ph, hl[p], 2, q), plist(ph, hl[q], 3, p))
     for h in hl + hi:
         ph.ph_free(h)
+
+
+def test_window_hybrid_blocks_and_superstep_recombination():
+    """bench.py's N > 1 window-class hybrid (raphtory_amd/partitioned.py): the hop blocks tile the
+    range, and the combined summaries carry each hop's job superstep count over all its windows —
+    the maximum of the two runs' counts (rgpu.cpp finish_supersteps reports min(maxSteps, 1 + the
+    last changing step over the run's windows) on every view of the hop)."""
+    from raphtory_amd.partitioned import combine_window_groups, hop_blocks
+    for n, world in ((168, 8), (168, 3), (5, 8), (1, 2)):
+        b = hop_blocks(n, world)
+        assert len(b) == world and b[0][0] == 0 and b[-1][1] == n
+        assert all(b[i][1] == b[i + 1][0] and b[i][0] <= b[i][1] for i in range(world - 1))
+        assert max(hi - lo for lo, hi in b) - min(hi - lo for lo, hi in b) <= 1
+    rng = np.random.default_rng(0)
+    H, W, long_i, short_i = 10, 5, [0, 1, 2], [3, 4]
+    full = rng.integers(0, 1000, (H, W, 9))
+    last = rng.integers(0, 120, (H, W))  # a view's last changing step
+    cap = 100
+    run_steps = lambda idx: np.minimum(cap, 1 + last[:, idx].max(axis=1))  # noqa: E731  (finish_supersteps)
+    full[..., 7] = run_steps(list(range(W)))[:, None]
+    ls = full[:, long_i].copy()
+    ls[..., 7] = run_steps(long_i)[:, None]
+    ss = full[:, short_i].copy()
+    ss[..., 7] = run_steps(short_i)[:, None]
+    blocks = [(lo, hi, ss[lo:hi]) for lo, hi in hop_blocks(H, 3)]
+    assert np.array_equal(combine_window_groups(W, long_i, ls, short_i, blocks), full)

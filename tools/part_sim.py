@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from raphtory_amd import TemporalGraph  # noqa: E402
-from raphtory_amd.partitioned import LoopbackPartitions  # noqa: E402
+from raphtory_amd.partitioned import LoopbackPartitions, combine_window_groups, hop_blocks  # noqa: E402
 from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops  # noqa: E402
 
 
@@ -45,6 +45,11 @@ def main():
     ap.add_argument("--ab", default="",
                     help="per-run knob settings to profile on the same sealed partitions after the main pass, "
                          "';'-separated, each 'K=V[,K=V]' (read per run by the library): one extra JSON line each")
+    ap.add_argument("--hybrid", default="",
+                    help="P > 1: these windows (letters of 'ymwdh', e.g. 'dh') run hop-sharded instead of partitioned: "
+                         "rank r answers them for its block of the hops on a replica of the stream's time slice "
+                         "[hop0 - the longest of them, end] (exact: a view (t, w) reads only updates in (t - w, t]); "
+                         "the partitions run the other windows.  Per rank: its partition's kernel ms + its block's")
     a = ap.parse_args()
     probe = None
     if a.probe_rounds > 0:  # one RCCL rank: the fixed cost of a round without peer latency
@@ -59,6 +64,9 @@ def main():
     s = gen_gab_range(4, a.users, inter_full, 0, a.interactions)
     end = int(s.t[-1])
     hops = range_hops(end - 167 * HOUR, end, HOUR)
+    short_i = [i for i, c in enumerate("ymwdh") if c in a.hybrid]
+    long_i = [i for i in range(len(BATCH_WINDOWS)) if i not in short_i]
+    replica, replica_n = None, 0  # the time-slice replica (--hybrid), built at the first P > 1
     for P in [int(x) for x in a.parts.split(",")]:
         t0 = time.time()
         if a.trace:  # read when a context opens; a partition's file gets ".p<partition>"
@@ -76,7 +84,17 @@ def main():
             lp.ingest_stream(s)
             lp.seal()
             parts = lp.parts
-            run = lambda **kw: lp.run("cc", hops, BATCH_WINDOWS, **kw)  # noqa: E731
+            pw = [BATCH_WINDOWS[i] for i in long_i] if short_i else BATCH_WINDOWS
+            run = lambda **kw: lp.run("cc", hops, pw, **kw)  # noqa: E731
+            if short_i and replica is None:
+                cut = int(hops[0]) - max(BATCH_WINDOWS[i] for i in short_i)
+                keep = s.t >= cut
+                replica = TemporalGraph()
+                replica.ingest_stream(type(s)(s.t[keep], s.kind[keep], s.src[keep], s.dst[keep]))
+                replica.seal()
+                replica_n = int(keep.sum())
+                print(f"hybrid: slice replica of {int(keep.sum())} updates (t >= hop0 - {max(BATCH_WINDOWS[i] for i in short_i)} ms)",
+                      file=sys.stderr, flush=True)
         print(f"P={P}: sealed in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
         run()
         print(f"P={P}: warm run done", file=sys.stderr, flush=True)
@@ -98,11 +116,38 @@ def main():
             if best is None or max(per) < max(best[0]):
                 best = (per, ks, p0, t_prof)
         per, ks, p0, t_prof = best
+        hyb = None
+        summ = parts[0].cc_summaries()
+        if short_i and P > 1:
+            # rank r's block of the hops, short windows, on the slice replica: profile each block (best of
+            # the profile rounds) and assemble the whole query's summaries for the check
+            sw = [BATCH_WINDOWS[i] for i in short_i]
+            blk_ms, blk_ks, got = [], {}, []
+            for r, (lo, hi) in enumerate(hop_blocks(len(hops), P)):
+                blk = hops[lo:hi]
+                replica.run("cc", blk, sw)
+                bm, bk = None, None
+                for _ in range(max(1, a.profile_rounds)):
+                    replica.run("cc", blk, sw, profile=True, serial=True)
+                    kk = {k: v["ms"] for k, v in replica.stats()["kernels"].items() if v["launches"]}
+                    if bm is None or sum(kk.values()) < bm:
+                        bm, bk = sum(kk.values()), kk
+                blk_ms.append(round(bm, 1))
+                for k, v in bk.items():
+                    blk_ks[k] = blk_ks.get(k, 0.0) + v
+                got.append((lo, hi, replica.cc_summaries()))
+            summ = combine_window_groups(len(BATCH_WINDOWS), long_i, summ, short_i, got)
+            hyb = {"windows_replicated": "".join("ymwdh"[i] for i in short_i),
+                   "replica_updates": replica_n,
+                   "partition_kernel_ms": per, "replica_block_kernel_ms": blk_ms,
+                   "replica_kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in blk_ks.items()}}
+            per = [round(x + y, 1) for x, y in zip(per, blk_ms)]
+            for k, v in blk_ks.items():
+                ks[k] = ks.get(k, 0.0) + v
         by = {}
         for g in parts:
             for k, v in g.stats()["xchg_bytes_by"].items():
                 by[k] = by.get(k, 0.0) + v / 1e6
-        summ = parts[0].cc_summaries()
         # modelled exchange time per partition: the bytes it sends, spread over its P-1 xGMI links
         # (point-to-point, ~153 GB/s each per the MI355X platform figures in the task brief) — a
         # bandwidth term only; the number of exchange rounds (one per superstep per batch, plus one
@@ -139,6 +184,8 @@ def main():
                "check": [int(summ[..., 0].sum()), int(summ[..., 1].sum()), int(summ[..., 5].sum())],
                # every view's summary fields (biggest .. supersteps), hashed: equal at every P
                "summaries_sha256": hashlib.sha256(np.ascontiguousarray(summ[..., :8]).tobytes()).hexdigest()[:16]}
+        if hyb:
+            out["hybrid"] = hyb
         print(json.dumps(out), flush=True)
         for setting in [x for x in a.ab.split(";") if x.strip()]:  # same-process A/B on these partitions
             kv = dict(x.split("=", 1) for x in setting.split(","))
@@ -168,6 +215,8 @@ def main():
                   flush=True)
         for g in parts:
             g.close()
+    if replica is not None:
+        replica.close()
 
 
 if __name__ == "__main__":
