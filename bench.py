@@ -661,7 +661,8 @@ def run_c4(a, rank, world, local):
             "cpu_baseline": cpu,
             "kernels": ks,
             "check": {"views": int(summ.shape[0] * summ.shape[1]), "sum_biggest": int(summ[..., 0].sum()),
-                      "sum_total": int(summ[..., 1].sum()), "sum_members": int(summ[..., 5].sum())},
+                      "sum_total": int(summ[..., 1].sum()), "sum_members": int(summ[..., 5].sum()),
+                      "sum_supersteps": int(summ[..., 7].sum())},
             "secondary": secondary,
         }
         print(json.dumps(out), flush=True)
