@@ -50,6 +50,8 @@ def main():
                          "rank r answers them for its block of the hops on a replica of the stream's time slice "
                          "[hop0 - the longest of them, end] (exact: a view (t, w) reads only updates in (t - w, t]); "
                          "the partitions run the other windows.  Per rank: its partition's kernel ms + its block's")
+    ap.add_argument("--replica-env", default="",
+                    help="--hybrid: 'K=V[,K=V]' library knobs set while the slice replica opens (A/B of its options)")
     a = ap.parse_args()
     probe = None
     if a.probe_rounds > 0:  # one RCCL rank: the fixed cost of a round without peer latency
@@ -89,7 +91,17 @@ def main():
             if short_i and replica is None:
                 cut = int(hops[0]) - max(BATCH_WINDOWS[i] for i in short_i)
                 keep = s.t >= cut
-                replica = TemporalGraph()
+                kv = dict(x.split("=", 1) for x in a.replica_env.split(",") if x.strip())
+                old = {k: os.environ.get(k) for k in kv}
+                os.environ.update(kv)
+                try:
+                    replica = TemporalGraph()  # (rgpu_open reads the knobs)
+                finally:
+                    for k, v in old.items():
+                        if v is None:
+                            os.environ.pop(k, None)
+                        else:
+                            os.environ[k] = v
                 replica.ingest_stream(type(s)(s.t[keep], s.kind[keep], s.src[keep], s.dst[keep]))
                 replica.seal()
                 replica_n = int(keep.sum())
@@ -137,7 +149,7 @@ def main():
                     blk_ks[k] = blk_ks.get(k, 0.0) + v
                 got.append((lo, hi, replica.cc_summaries()))
             summ = combine_window_groups(len(BATCH_WINDOWS), long_i, summ, short_i, got)
-            hyb = {"windows_replicated": "".join("ymwdh"[i] for i in short_i),
+            hyb = {"windows_replicated": "".join("ymwdh"[i] for i in short_i), "replica_env": a.replica_env,
                    "replica_updates": replica_n,
                    "partition_kernel_ms": per, "replica_block_kernel_ms": blk_ms,
                    "replica_kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in blk_ks.items()}}
