@@ -79,7 +79,7 @@ def parse():
                    help="N > 1, C4 / C5: the label-record channel.  shm = the library's shared-memory group of "
                         "processes on one host, rank r on GPU r mod the visible GPUs: a rehearsal of the N > 1 "
                         "bench path on a one-GPU box (never a scaling number)")
-    p.add_argument("--hybrid", default="dh",
+    p.add_argument("--hybrid", default="wdh",
                    help="N > 1, C4: these windows (letters of 'ymwdh') are answered hop-sharded instead of "
                         "vertex-partitioned: rank r runs them for its contiguous block of the hops on a replica of "
                         "the stream's time slice [hop0 - the longest of them, end] (exact on the add-only C4 stream: a "
