@@ -11,5 +11,5 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_partitioned.py -k hybrid -x
 tail -2 gpurun_out/pytest_$T.log
 [ -n "${SKIP_NRANK:-}" ] || TAG=$T N=2 SECS=300 bash tools/gpu_nrank_rehearsal_r6.sh || exit 1
 RGPU_SLOTS=1 timeout -k 10 ${SECS:-800} python -u tools/part_sim.py --interactions ${INTER:-333333334} --parts ${PARTS:-1,8} \
-  --probe-rounds 300 --profile-rounds 1 --hybrid ${HYB:-dh} ${REPENV:+--replica-env $REPENV} > gpurun_out/part_$T.jsonl 2> gpurun_out/part_$T.err; rc=$?
+  --probe-rounds 300 --profile-rounds 1 --hybrid ${HYB:-dh} ${REPENV:+--replica-env $REPENV} ${EXTRA:-} > gpurun_out/part_$T.jsonl 2> gpurun_out/part_$T.err; rc=$?
 tail -c 1200 gpurun_out/part_$T.jsonl; tail -3 gpurun_out/part_$T.err; exit $rc

@@ -33,6 +33,55 @@ from raphtory_amd.partitioned import LoopbackPartitions, combine_window_groups, 
 from raphtory_amd.synth import BATCH_WINDOWS, HOUR, gen_gab_range, range_hops  # noqa: E402
 
 
+class _Env:
+    """library knobs set for a block of calls ('K=V[,K=V]'): rgpu_open and each run read them"""
+
+    def __init__(self, spec: str):
+        self.kv = dict(x.split("=", 1) for x in spec.split(",") if x.strip())
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def open_replica(s, cut, env=""):
+    """the --hybrid time-slice replica: the updates with t >= cut, one graph"""
+    keep = s.t >= cut
+    with _Env(env):
+        replica = TemporalGraph()  # (rgpu_open reads the knobs)
+    replica.ingest_stream(type(s)(s.t[keep], s.kind[keep], s.src[keep], s.dst[keep]))
+    replica.seal()
+    return replica, int(keep.sum())
+
+
+def profile_blocks(replica, hops, sw, P, rounds, env=""):
+    """rank r's block of the hops (hop_blocks), short windows, on the replica: serial kernel ms per
+    block (best of `rounds` profile passes), kernel ms by group summed, and (lo, hi, summaries)"""
+    blk_ms, blk_ks, got = [], {}, []
+    with _Env(env):
+        for lo, hi in hop_blocks(len(hops), P):
+            blk = hops[lo:hi]
+            replica.run("cc", blk, sw)
+            bm, bk = None, None
+            for _ in range(max(1, rounds)):
+                replica.run("cc", blk, sw, profile=True, serial=True)
+                kk = {k: v["ms"] for k, v in replica.stats()["kernels"].items() if v["launches"]}
+                if bm is None or sum(kk.values()) < bm:
+                    bm, bk = sum(kk.values()), kk
+            blk_ms.append(round(bm, 1))
+            for k, v in bk.items():
+                blk_ks[k] = blk_ks.get(k, 0.0) + v
+            got.append((lo, hi, replica.cc_summaries()))
+    return blk_ms, blk_ks, got
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--users", type=int, default=20_000_000)
@@ -52,6 +101,11 @@ def main():
                          "the partitions run the other windows.  Per rank: its partition's kernel ms + its block's")
     ap.add_argument("--replica-env", default="",
                     help="--hybrid: 'K=V[,K=V]' library knobs set while the slice replica opens (A/B of its options)")
+    ap.add_argument("--replica-ab", default="",
+                    help="--hybrid: replica knob settings to compare (';'-separated 'K=V[,K=V]'): per P a fresh "
+                         "replica per setting, its blocks profiled, one JSON line each")
+    ap.add_argument("--replica-only", action="store_true",
+                    help="--hybrid: profile only the replica's blocks per P (no partitions): quick replica A/B")
     a = ap.parse_args()
     probe = None
     if a.probe_rounds > 0:  # one RCCL rank: the fixed cost of a round without peer latency
@@ -69,6 +123,20 @@ def main():
     short_i = [i for i, c in enumerate("ymwdh") if c in a.hybrid]
     long_i = [i for i in range(len(BATCH_WINDOWS)) if i not in short_i]
     replica, replica_n = None, 0  # the time-slice replica (--hybrid), built at the first P > 1
+    sw = [BATCH_WINDOWS[i] for i in short_i]
+    cut = int(hops[0]) - max(sw) if short_i else 0
+    if short_i and a.replica_only:
+        for P in [int(x) for x in a.parts.split(",")]:
+            for setting in [a.replica_env] + [x for x in a.replica_ab.split(";") if x.strip()]:
+                rep, n = open_replica(s, cut, setting)
+                blk_ms, blk_ks, _ = profile_blocks(rep, hops, sw, P, a.profile_rounds, setting)
+                rep.close()
+                print(json.dumps({"P": P, "replica_only": "".join("ymwdh"[i] for i in short_i), "replica_env": setting,
+                                  "replica_updates": n, "replica_block_kernel_ms": blk_ms,
+                                  "replica_block_kernel_ms_max": max(blk_ms),
+                                  "replica_kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in blk_ks.items()}}),
+                      flush=True)
+        return
     for P in [int(x) for x in a.parts.split(",")]:
         t0 = time.time()
         if a.trace:  # read when a context opens; a partition's file gets ".p<partition>"
@@ -89,24 +157,9 @@ def main():
             pw = [BATCH_WINDOWS[i] for i in long_i] if short_i else BATCH_WINDOWS
             run = lambda **kw: lp.run("cc", hops, pw, **kw)  # noqa: E731
             if short_i and replica is None:
-                cut = int(hops[0]) - max(BATCH_WINDOWS[i] for i in short_i)
-                keep = s.t >= cut
-                kv = dict(x.split("=", 1) for x in a.replica_env.split(",") if x.strip())
-                old = {k: os.environ.get(k) for k in kv}
-                os.environ.update(kv)
-                try:
-                    replica = TemporalGraph()  # (rgpu_open reads the knobs)
-                finally:
-                    for k, v in old.items():
-                        if v is None:
-                            os.environ.pop(k, None)
-                        else:
-                            os.environ[k] = v
-                replica.ingest_stream(type(s)(s.t[keep], s.kind[keep], s.src[keep], s.dst[keep]))
-                replica.seal()
-                replica_n = int(keep.sum())
-                print(f"hybrid: slice replica of {int(keep.sum())} updates (t >= hop0 - {max(BATCH_WINDOWS[i] for i in short_i)} ms)",
-                      file=sys.stderr, flush=True)
+                replica, replica_n = open_replica(s, cut, a.replica_env)
+                print(f"hybrid: slice replica of {replica_n} updates (t >= hop0 - {max(sw)} ms)", file=sys.stderr,
+                      flush=True)
         print(f"P={P}: sealed in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
         run()
         print(f"P={P}: warm run done", file=sys.stderr, flush=True)
@@ -133,22 +186,18 @@ def main():
         if short_i and P > 1:
             # rank r's block of the hops, short windows, on the slice replica: profile each block (best of
             # the profile rounds) and assemble the whole query's summaries for the check
-            sw = [BATCH_WINDOWS[i] for i in short_i]
-            blk_ms, blk_ks, got = [], {}, []
-            for r, (lo, hi) in enumerate(hop_blocks(len(hops), P)):
-                blk = hops[lo:hi]
-                replica.run("cc", blk, sw)
-                bm, bk = None, None
-                for _ in range(max(1, a.profile_rounds)):
-                    replica.run("cc", blk, sw, profile=True, serial=True)
-                    kk = {k: v["ms"] for k, v in replica.stats()["kernels"].items() if v["launches"]}
-                    if bm is None or sum(kk.values()) < bm:
-                        bm, bk = sum(kk.values()), kk
-                blk_ms.append(round(bm, 1))
-                for k, v in bk.items():
-                    blk_ks[k] = blk_ks.get(k, 0.0) + v
-                got.append((lo, hi, replica.cc_summaries()))
+            blk_ms, blk_ks, got = profile_blocks(replica, hops, sw, P, a.profile_rounds, a.replica_env)
+            long_summ = summ
             summ = combine_window_groups(len(BATCH_WINDOWS), long_i, summ, short_i, got)
+            for setting in [x for x in a.replica_ab.split(";") if x.strip()]:  # same partitions, other replicas
+                rep, _ = open_replica(s, cut, setting)
+                bms, bks, bgot = profile_blocks(rep, hops, sw, P, a.profile_rounds, setting)
+                rep.close()
+                same = np.array_equal(combine_window_groups(len(BATCH_WINDOWS), long_i, long_summ, short_i, bgot), summ)
+                print(json.dumps({"P": P, "replica_ab": setting, "replica_block_kernel_ms": bms,
+                                  "slowest_rank_ms": max(x + y for x, y in zip(per, bms)), "summaries_equal": bool(same),
+                                  "replica_kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in bks.items()}}),
+                      flush=True)
             hyb = {"windows_replicated": "".join("ymwdh"[i] for i in short_i), "replica_env": a.replica_env,
                    "replica_updates": replica_n,
                    "partition_kernel_ms": per, "replica_block_kernel_ms": blk_ms,
