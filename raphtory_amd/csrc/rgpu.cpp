@@ -2336,16 +2336,18 @@ void build_heavy_list(DevGraph& g, std::vector<void*>& L, const std::vector<int3
   g.seg_lo = dupload(L, seg_lo);
   g.seg_n = dupload(L, seg_n);
 }
-// The hub threshold (static slots): RGPU_HEAVY when set; else 2048 for one partition and, for a
-// partition of a vertex-partitioned graph, scaled with its owned vertices (2048 at 16M, at least
-// 256).  A superstep or K2 launch lasts as long as its slowest wave, and a wave walks a non-hub
+// The hub threshold (static slots): RGPU_HEAVY when set; else scaled with the graph's (a partition's:
+// its owned) vertices, 2048 at 16M and above, at least 256.  A superstep or K2 launch lasts as long as its slowest wave, and a wave walks a non-hub
 // member's slots one chunk after another: with a few owned vertices per wave (8 partitions) that
 // tail is the launch.  Measured on the 300M-update prefix at P = 8, slowest partition: 2048 ->
 // 118 ms, 512 -> 102, 256 -> 98, 128 -> 99, 64 -> 107 (profiles/r04/part_sim_heavy*.jsonl); the
-// 1B graph in one partition: 2048 273 ms, 512 286, 256 296 (hub passes grow).
+// 1B graph in one partition: 2048 273 ms, 512 286, 256 296 (hub passes grow).  Round 6: the rule holds
+// for a graph that is not partitioned too (it was 2048 whatever the size): the week slice of the 1B
+// stream (21M updates, the N > 1 hybrid's replica) answering 21 hops x {w, d, h}: 2048 ->
+// 26.3 ms per block, 1024 -> 20.2, 4096 -> 37.6 (profiles/r06/part_sim_replica_ab_1b.jsonl); the
+// 1B graph itself (19.9M vertices) keeps 2048.
 int hub_threshold(const rgpu_ctx* c, int64_t n_own) {
   if (c->heavy_env >= 0) return c->heavy_env;
-  if (!c->partitioned) return 2048;
   const int64_t t = (int64_t)2048 * n_own / ((int64_t)1 << 24);
   return (int)std::max<int64_t>(256, std::min<int64_t>(2048, t));
 }
@@ -3258,7 +3260,11 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   // (partitioned: 4 segments per wave and round — at P = 8 the hub threshold is low and most segments
   // are active in every superstep, so a wave walking 32 of them in turn was the launch: summed hub
   // kernels 138 -> 101 ms, slowest partition 79.4 -> 74.5 ms, profiles/r06/part_sim_hubpro_p8.jsonl)
-  c->ko.hub_pro = env_int("RGPU_HUB_PRO", c->partitioned ? kHubProPart : c->ko.hub_pro);
+  // The same holds for a small graph (below 2^23 vertices: a low hub threshold, short windows): the
+  // 1B stream's week slice, 21 hops x {w, d, h}, hub kernels 57.3 -> 15.0 ms over eight blocks with 4
+  // (22.4 with 8; profiles/r06/part_sim_replica_ab_1b.jsonl).  The 1B graph keeps 32.
+  c->ko.hub_pro = env_int("RGPU_HUB_PRO", (c->partitioned || c->g.nv < ((int64_t)1 << 23)) ? kHubProPart
+                                                                                         : c->ko.hub_pro);
   c->ko.long_steps = env_int("RGPU_LONG_STEPS", c->ko.long_steps);
   c->long_ratio = env_int("RGPU_LONG_RATIO", 4);
   try {

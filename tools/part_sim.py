@@ -130,9 +130,10 @@ def main():
             for setting in [a.replica_env] + [x for x in a.replica_ab.split(";") if x.strip()]:
                 rep, n = open_replica(s, cut, setting)
                 blk_ms, blk_ks, _ = profile_blocks(rep, hops, sw, P, a.profile_rounds, setting)
+                nv = rep.stats()["vertices"]
                 rep.close()
                 print(json.dumps({"P": P, "replica_only": "".join("ymwdh"[i] for i in short_i), "replica_env": setting,
-                                  "replica_updates": n, "replica_block_kernel_ms": blk_ms,
+                                  "replica_updates": n, "replica_vertices": nv, "replica_block_kernel_ms": blk_ms,
                                   "replica_block_kernel_ms_max": max(blk_ms),
                                   "replica_kernel_ms_sum_by_kernel": {k: round(v, 1) for k, v in blk_ks.items()}}),
                       flush=True)
