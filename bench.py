@@ -85,6 +85,8 @@ def parse():
                         "the stream's time slice [hop0 - the longest of them, end] (exact on the add-only C4 stream: a "
                         "view (t, w) reads only the updates in [t - w, t]); the partitions answer the other windows. "
                         "'' = every window partitioned")
+    p.add_argument("--hybrid-n1", action="store_true",
+                   help="N = 1 too: the --hybrid windows on the time-slice replica (every hop), the others on the graph")
     p.add_argument("--vertex-order", default="locality", choices=["locality", "id"],
                    help="local vertex order of the sealed graph (rgpu_set_vertex_order; A/B runs)")
     return p.parse_args()
@@ -511,7 +513,7 @@ def run_c4(a, rank, world, local):
     hops = range_hops(end - (a.c4_hops - 1) * HOUR, end, HOUR)
     windows = BATCH_WINDOWS
     # N > 1 (--hybrid): the short windows hop-sharded on a time-slice replica, the others partitioned
-    short_i = [i for i, c in enumerate("ymwdh") if c in a.hybrid] if dist is not None else []
+    short_i = [i for i, c in enumerate("ymwdh") if c in a.hybrid] if (dist is not None or a.hybrid_n1) else []
     long_w = [w for i, w in enumerate(windows) if i not in short_i]
     short_w = [windows[i] for i in short_i]
     blocks = hop_blocks(len(hops), world)
@@ -537,7 +539,10 @@ def run_c4(a, rank, world, local):
         if gs is None:
             return sl
         got = [None] * world
-        dist.all_gather_object(got, gs.cc_summaries() if len(my_hops) else None)
+        if dist is None:
+            got = [gs.cc_summaries()]
+        else:
+            dist.all_gather_object(got, gs.cc_summaries() if len(my_hops) else None)
         return combine_window_groups(len(windows), [i for i in range(len(windows)) if i not in short_i], sl, short_i,
                                      [(lo, hi, x) for (lo, hi), x in zip(blocks, got)])
 
@@ -597,7 +602,7 @@ def run_c4(a, rank, world, local):
             roofline["aggregate"] = aggregate_roofline(kraw, "C4")
         if not a.no_edge_counts and world == 1:
             g.run("cc", hops, windows, edge_counts=True)
-            summ = summaries()
+            summ = g.cc_summaries()  # (every window on the graph here)
             s8d = survey_bytes(summ, len(hops), windows, st["vertices"], st["edges"],
                                st["vertex_events"] + st["edge_events"] + st["deaths"], ks, d["launches"])
             roofline["survey_8d"] = {"achieved": round(s8d["cc_step"]["achieved_GBps"], 1),
@@ -644,7 +649,8 @@ def run_c4(a, rank, world, local):
                                    "168 hourly hops x 5 batched windows {y,m,w,d,h}, ConnectedComponents",
                        "updates": 3 * inter, "vertices": n_vert, "edge_entities": n_edges, "hops": int(len(hops)),
                        "windows": len(windows),
-                       "parallelism": ("one GPU, partitioned path (P = 1)" if a.partitioned else "one GPU")
+                       "parallelism": ("one GPU, partitioned path (P = 1)" if a.partitioned else
+                                       f"one GPU; windows {a.hybrid} on a time-slice replica" if short_i else "one GPU")
                                       if world == 1 else
                                       f"vertex-partitioned x{world} (Utils.getPartition), "
                                       + ("RCCL label records" if a.exchange == "rccl" else
