@@ -577,9 +577,12 @@ def run_c4(a, rank, world, local):
     roofline, ks, s8d = None, {}, None
     if not a.no_profile_pass:
         log("profile passes")
-        if a.profile_only and gs is not None and len(my_hops):
-            gs.run("cc", my_hops, short_w)  # (its summaries for the check; not profiled)
         kraw = profile_passes(g, hops, long_w, lean_only=a.lean_pass_only)  # collective at N > 1
+        if gs is not None and len(my_hops):  # the replica's share of the query, pooled per kernel
+            for k, v in profile_passes(gs, my_hops, short_w, lean_only=a.lean_pass_only).items():
+                d = kraw.setdefault(k, {"launches": 0, "ms": 0.0, "bytes": 0.0, "ms_counting_pass": 0.0})
+                for f in ("launches", "ms", "bytes", "ms_counting_pass"):
+                    d[f] += v[f]
         ks = kernel_table({"kernels": kraw})
         if summ is None:
             summ = summaries()
