@@ -79,14 +79,12 @@ def parse():
                    help="N > 1, C4 / C5: the label-record channel.  shm = the library's shared-memory group of "
                         "processes on one host, rank r on GPU r mod the visible GPUs: a rehearsal of the N > 1 "
                         "bench path on a one-GPU box (never a scaling number)")
-    p.add_argument("--hybrid", default="wdh",
-                   help="N > 1, C4: these windows (letters of 'ymwdh') are answered hop-sharded instead of "
-                        "vertex-partitioned: rank r runs them for its contiguous block of the hops on a replica of "
-                        "the stream's time slice [hop0 - the longest of them, end] (exact on the add-only C4 stream: a "
-                        "view (t, w) reads only the updates in [t - w, t]); the partitions answer the other windows. "
-                        "'' = every window partitioned")
-    p.add_argument("--hybrid-n1", action="store_true",
-                   help="N = 1 too: the --hybrid windows on the time-slice replica (every hop), the others on the graph")
+    p.add_argument("--hybrid", default="auto",
+                   help="C4: these windows (letters of 'ymwdh') are answered on a replica of the stream's time slice "
+                        "[hop0 - the longest of them, end] (exact on the add-only C4 stream: a view (t, w) reads only "
+                        "the updates in [t - w, t]), the others on the graph.  N > 1: hop-sharded, rank r runs its "
+                        "contiguous block of the hops on its replica, the partitions answer the other windows.  "
+                        "auto = 'mwdh' at N = 1, 'wdh' at N > 1 (measured, DESIGN.md §7); '' = off")
     p.add_argument("--vertex-order", default="locality", choices=["locality", "id"],
                    help="local vertex order of the sealed graph (rgpu_set_vertex_order; A/B runs)")
     return p.parse_args()
@@ -513,7 +511,9 @@ def run_c4(a, rank, world, local):
     hops = range_hops(end - (a.c4_hops - 1) * HOUR, end, HOUR)
     windows = BATCH_WINDOWS
     # N > 1 (--hybrid): the short windows hop-sharded on a time-slice replica, the others partitioned
-    short_i = [i for i, c in enumerate("ymwdh") if c in a.hybrid] if (dist is not None or a.hybrid_n1) else []
+    if a.hybrid == "auto":
+        a.hybrid = "wdh" if world > 1 else "mwdh"
+    short_i = [i for i, c in enumerate("ymwdh") if c in a.hybrid]
     long_w = [w for i, w in enumerate(windows) if i not in short_i]
     short_w = [windows[i] for i in short_i]
     blocks = hop_blocks(len(hops), world)

@@ -249,6 +249,20 @@ def main():
         if hyb:
             out["hybrid"] = hyb
         print(json.dumps(out), flush=True)
+        if short_i and P == 1:  # the hybrid on one GPU: long windows on the graph + every hop on the replica
+            if replica is None:
+                replica, replica_n = open_replica(s, cut, a.replica_env)
+            lw = [BATCH_WINDOWS[i] for i in long_i]
+            g.run("cc", hops, lw)
+            g.run("cc", hops, lw, profile=True, serial=True)
+            lks = {k: v["ms"] for k, v in g.stats()["kernels"].items() if v["launches"]}
+            bms, bks, bgot = profile_blocks(replica, hops, sw, 1, a.profile_rounds, a.replica_env)
+            same = np.array_equal(combine_window_groups(len(BATCH_WINDOWS), long_i, g.cc_summaries(), short_i, bgot), summ)
+            print(json.dumps({"P": 1, "hybrid_p1": "".join("ymwdh"[i] for i in short_i),
+                              "kernel_ms": round(sum(lks.values()) + bms[0], 1), "graph_kernel_ms": round(sum(lks.values()), 1),
+                              "replica_kernel_ms": bms[0], "summaries_equal": bool(same),
+                              "graph_kernel_ms_by_kernel": {k: round(v, 1) for k, v in lks.items()},
+                              "replica_kernel_ms_by_kernel": {k: round(v, 1) for k, v in bks.items()}}), flush=True)
         for setting in [x for x in a.ab.split(";") if x.strip()]:  # same-process A/B on these partitions
             kv = dict(x.split("=", 1) for x in setting.split(","))
             old = {k: os.environ.get(k) for k in kv}
