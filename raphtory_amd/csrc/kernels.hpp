@@ -100,7 +100,7 @@ constexpr int kSegSlots = 512;
 // value comes from KernOpts.hub_pro (C4, profiles/r05/ab_hubpro_c4.jsonl + ab_occ_c4.jsonl: heavy
 // 64.7 ms serial at 1, 49.9 at 8, 48.3 at 16, 47.9 at 32)
 constexpr int kHubPro = 32;
-constexpr int kHubProPart = 4;  // partitioned contexts and graphs below 2^23 vertices (rgpu_run_view_batch)
+constexpr int kHubProPart = 4;  // partitioned contexts and graphs below 2^24 vertices (rgpu_run_view_batch)
 // superstep options (k_cc_step_pk, k_heavy_gather, k_cc_slots; RGPU_STEP_OPTS, all by default):
 // members holding the final label finished lane-parallel; full folds (one label on every view of
 // the member) as a segmented min over the pack (a wave min over a hub segment or a big member's

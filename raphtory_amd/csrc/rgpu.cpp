@@ -3260,10 +3260,11 @@ int rgpu_run_view_batch(rgpu_ctx* c, int algo, const int64_t* hops, size_t n_hop
   // (partitioned: 4 segments per wave and round — at P = 8 the hub threshold is low and most segments
   // are active in every superstep, so a wave walking 32 of them in turn was the launch: summed hub
   // kernels 138 -> 101 ms, slowest partition 79.4 -> 74.5 ms, profiles/r06/part_sim_hubpro_p8.jsonl)
-  // The same holds for a small graph (below 2^23 vertices: a low hub threshold, short windows): the
-  // 1B stream's week slice, 21 hops x {w, d, h}, hub kernels 57.3 -> 15.0 ms over eight blocks with 4
-  // (22.4 with 8; profiles/r06/part_sim_replica_ab_1b.jsonl).  The 1B graph keeps 32.
-  c->ko.hub_pro = env_int("RGPU_HUB_PRO", (c->partitioned || c->g.nv < ((int64_t)1 << 23)) ? kHubProPart
+  // The same holds for a smaller graph (below 2^24 vertices: a lower hub threshold, shorter windows):
+  // the 1B stream's week slice, 21 hops x {w, d, h}, hub kernels 57.3 -> 15.0 ms over eight blocks with 4
+  // (22.4 with 8; profiles/r06/part_sim_replica_ab_1b.jsonl); its month slice (8.49M vertices), 168 hops
+  // x {m, w, d, h}, 43.5 -> 17.0 ms (part_sim_replica_month_ab_1b.jsonl).  The 1B graph (19.9M) keeps 32.
+  c->ko.hub_pro = env_int("RGPU_HUB_PRO", (c->partitioned || c->g.nv < ((int64_t)1 << 24)) ? kHubProPart
                                                                                          : c->ko.hub_pro);
   c->ko.long_steps = env_int("RGPU_LONG_STEPS", c->ko.long_steps);
   c->long_ratio = env_int("RGPU_LONG_RATIO", 4);
