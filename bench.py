@@ -30,6 +30,7 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -85,6 +86,8 @@ def parse():
                         "the updates in [t - w, t]), the others on the graph.  N > 1: hop-sharded, rank r runs its "
                         "contiguous block of the hops on its replica, the partitions answer the other windows.  "
                         "auto = 'mwdh' at N = 1, 'wdh' at N > 1 (measured, DESIGN.md §7); '' = off")
+    p.add_argument("--hybrid-serial", action="store_true",
+                   help="N = 1: run the graph's and the replica's parts one after the other (default: on two threads)")
     p.add_argument("--vertex-order", default="locality", choices=["locality", "id"],
                    help="local vertex order of the sealed graph (rgpu_set_vertex_order; A/B runs)")
     return p.parse_args()
@@ -530,6 +533,25 @@ def run_c4(a, rank, world, local):
     my_hops = hops[blocks[rank][0]:blocks[rank][1]]
 
     def query():
+        if gs is not None and len(my_hops) and dist is None and not a.hybrid_serial:
+            # N = 1: the two runs on two host threads (the library call drops the GIL), so that each run's
+            # sparse late supersteps overlap the other's work on the GPU
+            err = []
+
+            def short():
+                try:
+                    gs.run("cc", my_hops, short_w)
+                except BaseException as e:  # noqa: BLE001  (re-raised below)
+                    err.append(e)
+            th = threading.Thread(target=short)
+            th.start()
+            try:
+                g.run("cc", hops, long_w)
+            finally:
+                th.join()
+            if err:
+                raise err[0]
+            return
         g.run("cc", hops, long_w)  # collective over the partitions
         if gs is not None and len(my_hops):
             gs.run("cc", my_hops, short_w)  # this rank's block, no exchange
